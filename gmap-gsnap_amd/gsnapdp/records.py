@@ -1,0 +1,58 @@
+"""numpy views of the C-ABI records of include/gsnapdp.h (byte-for-byte)."""
+from __future__ import annotations
+
+import numpy as np
+
+WINDOW = np.dtype([
+    ("kind", "<i4"), ("length1", "<i4"), ("length2", "<i4"), ("offset1", "<i4"), ("offset2", "<i4"),
+    ("chroffset", "<u4"), ("chrhigh", "<u4"), ("chrpos", "<u4"), ("genomiclength", "<u4"), ("qpos", "<u4"),
+    ("cdna_direction", "<i4"), ("extraband", "<i4"), ("dynprogindex", "<i4"),
+    ("maxlength1", "<i4"), ("maxlength2", "<i4"), ("defect_rate", "<f4"),
+    ("watsonp", "u1"), ("jump_late_p", "u1"), ("widebandp", "u1"), ("endalign", "u1"),
+])
+assert WINDOW.itemsize == 68
+
+RESULT = np.dtype([
+    ("finalscore", "<i4"), ("nmatches", "<i4"), ("nmismatches", "<i4"), ("nopens", "<i4"),
+    ("nindels", "<i4"), ("bestr", "<i4"), ("bestc", "<i4"), ("nops", "<i4"), ("status", "<i4"),
+    ("length1", "<i4"), ("length2", "<i4"), ("reserved", "<i4"),
+])
+assert RESULT.itemsize == 48
+
+PAIR = np.dtype([
+    ("querypos", "<i4"), ("genomepos", "<i4"), ("queryjump", "<i4"), ("genomejump", "<i4"),
+    ("dynprogindex", "<i4"), ("cdna", "S1"), ("comp", "S1"), ("genome", "S1"), ("gapp", "u1"),
+])
+assert PAIR.itemsize == 24
+
+GGAP_WINDOW = np.dtype([
+    ("length1", "<i4"), ("length2L", "<i4"), ("length2R", "<i4"),
+    ("offset1", "<i4"), ("offset2L", "<i4"), ("revoffset2R", "<i4"),
+    ("chroffset", "<u4"), ("chrhigh", "<u4"), ("chrpos", "<u4"), ("genomiclength", "<u4"), ("qpos", "<u4"),
+    ("cdna_direction", "<i4"), ("extraband_paired", "<i4"), ("maxpeelback", "<i4"),
+    ("score_threshold", "<i4"), ("dynprogindex", "<i4"), ("maxlength1", "<i4"), ("maxlength2", "<i4"),
+    ("defect_rate", "<f4"),
+    ("watsonp", "u1"), ("jump_late_p", "u1"), ("halfp", "u1"), ("finalp", "u1"),
+    ("use_probabilities_p", "u1"), ("splicingp", "u1"), ("pad0", "u1"), ("pad1", "u1"),
+])
+assert GGAP_WINDOW.itemsize == 84
+
+GGAP_RESULT = np.dtype([
+    ("finalscore", "<i4"), ("new_leftgenomepos", "<i4"), ("new_rightgenomepos", "<i4"),
+    ("nmatches", "<i4"), ("nmismatches", "<i4"), ("nopens", "<i4"), ("nindels", "<i4"),
+    ("exonhead", "<i4"), ("introntype", "<i4"), ("dynprogindex", "<i4"),
+    ("returned_null", "<i4"), ("bridge_ok", "<i4"), ("left_prob", "<f8"), ("right_prob", "<f8"),
+])
+assert GGAP_RESULT.itemsize == 64
+
+MAXENT_IN = np.dtype([("model", "<u4"), ("splice_pos", "<u4"), ("chroffset", "<u4"), ("pad", "<u4")])
+
+# enums (include/gsnapdp.h)
+SINGLE_GAP, END5_GAP, END3_GAP = 0, 1, 2
+QUERYEND_GAP, QUERYEND_INDELS, QUERYEND_NOGAPS, BEST_LOCAL = 0, 1, 2, 3
+DONOR, ACCEPTOR, ANTIDONOR, ANTIACCEPTOR = 0, 1, 2, 3
+OP_DIAG, OP_HDASH, OP_HGAP, OP_VSKIP = 0, 1, 2, 3
+
+# Dynprog_new(600, 10, 11, 10, 8) as called by gmap.c:2270 -> 611 x 2000 (dynprog.c:831-852)
+MAXLENGTH1 = 611
+MAXLENGTH2 = 2000

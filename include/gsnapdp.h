@@ -1,0 +1,238 @@
+/*
+ * gsnapdp.h -- batched C-ABI of the MI355X stage-3 gap-filling DP engine.
+ *
+ * This is the throughput boundary of the drop-in (the per-call reference
+ * entry points Dynprog_* / Maxent_hr_* are declared in gsnapdp_dropin.h and
+ * are thin wrappers over this API).  Every entry point is extern "C", takes
+ * plain pointers and sizes, and carries no torch / HIP types.
+ *
+ * Reference interfaces replaced (GMAP/GSNAP 2012-07-03, src/):
+ *   - Dynprog_single_gap   dynprog.c:4450-4572   (kind GSNAPDP_SINGLE_GAP)
+ *   - Dynprog_end5_gap     dynprog.c:5094-5284   (kind GSNAPDP_END5_GAP)
+ *   - Dynprog_end3_gap     dynprog.c:5556-5741   (kind GSNAPDP_END3_GAP)
+ *   - Maxent_hr_*_prob     maxent_hr.c:27217-27390 (gsnapdp_maxent_batch)
+ *   - Genome_user_setup / Maxent_hr_setup (genome.c:9989, maxent_hr.c:27195):
+ *     the packed genome blocks are uploaded once per context.
+ *
+ * Semantics of every window field follow the argument of the same name in
+ * the reference entry point (dynprog.h:74-160).  A window never aliases
+ * reference memory: query bytes live in a batch buffer addressed by `qpos`.
+ */
+#ifndef GSNAPDP_H
+#define GSNAPDP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSNAPDP_ABI_VERSION 1
+
+/* Window kinds (one reference entry point each). */
+enum {
+  GSNAPDP_SINGLE_GAP = 0, /* Dynprog_single_gap, fwd fill, endpoint (L1,L2) */
+  GSNAPDP_END5_GAP = 1,   /* Dynprog_end5_gap, rev fill + endpoint search   */
+  GSNAPDP_END3_GAP = 2    /* Dynprog_end3_gap, fwd fill + endpoint search   */
+};
+
+/* Endalign_T, same order as dynprog.h:8. */
+enum {
+  GSNAPDP_QUERYEND_GAP = 0,
+  GSNAPDP_QUERYEND_INDELS = 1,
+  GSNAPDP_QUERYEND_NOGAPS = 2,
+  GSNAPDP_BEST_LOCAL = 3
+};
+
+/* Mode_T, same order as mode.h. */
+enum {
+  GSNAPDP_MODE_STANDARD = 0,
+  GSNAPDP_MODE_CMET_STRANDED = 1,
+  GSNAPDP_MODE_CMET_NONSTRANDED = 2,
+  GSNAPDP_MODE_ATOI_STRANDED = 3,
+  GSNAPDP_MODE_ATOI_NONSTRANDED = 4
+};
+
+/* Comp characters written into pairs (comp.h:5-30). */
+#define GSNAPDP_DYNPROG_MATCH_COMP '*'
+#define GSNAPDP_AMBIGUOUS_COMP ':'
+#define GSNAPDP_MISMATCH_COMP ' '
+#define GSNAPDP_INDEL_COMP '-'
+#define GSNAPDP_UNKNOWNJUMP (-1000000) /* dynprog.h:30 */
+#define GSNAPDP_NEG_INFINITY (-1000000) /* dynprog.c:119 */
+
+/* One DP window.  Field meaning = the reference argument of the same name.
+ * For GSNAPDP_END5_GAP, offset1/offset2 are revoffset1/revoffset2 and the
+ * query is read backwards from qpos (qpos = index of revsequence1[0], the
+ * LAST query base, exactly like the reference's rev pointers). */
+typedef struct gsnapdp_window {
+  int32_t kind;
+  int32_t length1;        /* query rows   */
+  int32_t length2;        /* genome cols  */
+  int32_t offset1;        /* query offset (or revoffset1)  */
+  int32_t offset2;        /* genome offset (or revoffset2) */
+  uint32_t chroffset;
+  uint32_t chrhigh;
+  uint32_t chrpos;
+  uint32_t genomiclength;
+  uint32_t qpos;          /* index of sequence1[0] in the batch query buffers */
+  int32_t cdna_direction;
+  int32_t extraband;      /* extraband_single / extraband_end */
+  int32_t dynprogindex;   /* value of *dynprogindex at the call */
+  int32_t maxlength1;     /* dynprog->maxlength1 of the Dynprog_T passed (dynprog.c:831-852) */
+  int32_t maxlength2;     /* dynprog->maxlength2 */
+  float defect_rate;      /* only its bin matters: <0.003 HIGHQ, <0.014 MEDQ, else LOWQ */
+  uint8_t watsonp;
+  uint8_t jump_late_p;
+  uint8_t widebandp;      /* single gap only; end gaps always widen (dynprog.c:5189) */
+  uint8_t endalign;       /* end gaps only */
+} gsnapdp_window;
+
+/* Per-window result.  finalscore/counts are the values the reference entry
+ * point leaves in its out-parameters (all post-rules applied: end-gap
+ * zeroing dynprog.c:5259/5715, NOGAPS rescoring :5243/:5700, too-long
+ * sentinels :4511).  The traceback itself is returned as a compact op stream
+ * (see below) that gsnapdp_expand turns into the reference's pair list,
+ * push for push. */
+typedef struct gsnapdp_result {
+  int32_t finalscore;
+  int32_t nmatches;
+  int32_t nmismatches;
+  int32_t nopens;
+  int32_t nindels;
+  int32_t bestr;          /* traceback start row */
+  int32_t bestc;          /* traceback start column */
+  int32_t nops;           /* ops written (<= capacity) */
+  int32_t status;         /* 0 ok, 1 early return (NULL list), 2 op overflow, 3 zeroed end */
+  int32_t length1;        /* effective lengths after end-gap chopping */
+  int32_t length2;
+  int32_t reserved;
+} gsnapdp_result;
+
+/* Op stream: one uint32 per op, in traceback order (from the endpoint back
+ * towards (0,0)).  Low 2 bits = type, high 30 bits = count. */
+enum {
+  GSNAPDP_OP_DIAG = 0,     /* `count` consecutive diagonal steps (pairs pushed unless genome '*') */
+  GSNAPDP_OP_HDASH = 1,    /* genome skip of `count`, pushed as INDEL pairs (add_genomeskip dashes) */
+  GSNAPDP_OP_HGAP = 2,     /* genome skip of `count` replaced by one gapholder (intron-like) */
+  GSNAPDP_OP_VSKIP = 3     /* query skip of `count` (add_queryskip) */
+};
+#define GSNAPDP_OP(type, count) ((uint32_t)(type) | ((uint32_t)(count) << 2))
+#define GSNAPDP_OP_TYPE(op) ((op) & 3u)
+#define GSNAPDP_OP_COUNT(op) ((op) >> 2)
+
+/* One pair of the output list (the DP-set fields of Pair_T, pairdef.h:9-49,
+ * as written by Pairpool_push / Pairpool_push_gapholder, pairpool.c:169,352). */
+typedef struct gsnapdp_pair {
+  int32_t querypos;
+  int32_t genomepos;
+  int32_t queryjump;      /* gapholder only */
+  int32_t genomejump;     /* gapholder only */
+  int32_t dynprogindex;
+  char cdna;
+  char comp;
+  char genome;
+  uint8_t gapp;           /* 1 for a gapholder */
+} gsnapdp_pair;
+
+/* One intron window (Dynprog_genome_gap, dynprog.c:4798-5061), run with
+ * splicing_iit == NULL (no known-site rewards, Dynprog_setup :350).  The query
+ * is sequence1[0..length1) at qpos; genome flanks are addressed through
+ * offset2L (left, fwd) and revoffset2R (right, rev) like the reference. */
+typedef struct gsnapdp_ggap_window {
+  int32_t length1, length2L, length2R;
+  int32_t offset1, offset2L, revoffset2R;
+  uint32_t chroffset, chrhigh, chrpos, genomiclength;
+  uint32_t qpos;
+  int32_t cdna_direction, extraband_paired, maxpeelback, score_threshold, dynprogindex;
+  int32_t maxlength1, maxlength2;
+  float defect_rate;
+  uint8_t watsonp, jump_late_p, halfp, finalp;
+  uint8_t use_probabilities_p, splicingp, pad0, pad1;
+} gsnapdp_ggap_window;
+
+/* Out-parameters of Dynprog_genome_gap for one window. */
+typedef struct gsnapdp_ggap_result {
+  int32_t finalscore, new_leftgenomepos, new_rightgenomepos;
+  int32_t nmatches, nmismatches, nopens, nindels, exonhead, introntype;
+  int32_t dynprogindex;   /* *dynprogindex after the call */
+  int32_t returned_null;  /* 1 if the reference returns NULL */
+  int32_t bridge_ok;      /* 0: probability mode found no candidate (reference UB, excluded) */
+  double left_prob, right_prob;
+} gsnapdp_ggap_result;
+
+/* ---------------------------------------------------------------- context */
+
+typedef struct gsnapdp_ctx gsnapdp_ctx;
+
+/* Create a context on HIP device `device`.  `blocks` are the reference's
+ * packed genome blocks (3 x uint32 per 32 nt: high, low, flags; genome.c:9325)
+ * of `nblocks_u32` words; they are copied to HBM once.  The host pointer is
+ * borrowed (kept for gsnapdp_expand) and must outlive the context.
+ * `mode` is the Mode_T given to Dynprog_init (dynprog.c:1339).
+ * Returns NULL on failure (message via gsnapdp_last_error). */
+gsnapdp_ctx *gsnapdp_create(int device, const uint32_t *blocks, size_t nblocks_u32, int mode);
+void gsnapdp_destroy(gsnapdp_ctx *ctx);
+const char *gsnapdp_last_error(void);
+
+/* Device id the library was built for / found ("gfx950"). */
+const char *gsnapdp_device_arch(gsnapdp_ctx *ctx);
+
+/* ------------------------------------------------------------ host batches
+ * Fill + endpoint + traceback for `n` windows.  Inputs are host buffers;
+ * this call copies them to HBM, runs the kernels on the context stream and
+ * copies results back (synchronous).  `op_offsets[i]` is where window i's
+ * op stream starts in `ops`; window i may write at most
+ * op_offsets[i+1]-op_offsets[i] ops (op_offsets has n+1 entries).
+ * Returns 0 on success. */
+int gsnapdp_run_host(gsnapdp_ctx *ctx, const gsnapdp_window *windows, int n,
+                     const char *query, const char *query_uc, size_t query_bytes,
+                     gsnapdp_result *results, uint32_t *ops, const int64_t *op_offsets);
+
+/* ---------------------------------------------------------- device batches
+ * Same computation with every buffer already resident in HBM (device
+ * pointers); asynchronous on `stream` (a hipStream_t, NULL = context stream).
+ * This is the path the benchmark times. */
+int gsnapdp_run_device(gsnapdp_ctx *ctx, const gsnapdp_window *d_windows, int n,
+                       const char *d_query, const char *d_query_uc,
+                       gsnapdp_result *d_results, uint32_t *d_ops, const int64_t *d_op_offsets,
+                       void *stream);
+
+/* Device scratch needed by gsnapdp_run_device for n windows whose largest
+ * dimensions are max_length1 x max_length2 (bytes).  Scratch is owned by
+ * the context and grown on demand; this is informational. */
+size_t gsnapdp_scratch_bytes(gsnapdp_ctx *ctx, int n, int max_length1, int max_length2);
+
+/* Synchronise the context stream. */
+int gsnapdp_sync(gsnapdp_ctx *ctx);
+
+/* ------------------------------------------------------------ maxent_hr
+ * Batched Maxent_hr_{donor,acceptor,antidonor,antiacceptor}_prob
+ * (maxent_hr.c:27217-27390) on the context genome.  model[i] in 0..3 =
+ * donor, acceptor, antidonor, antiacceptor.  Host buffers, synchronous. */
+enum { GSNAPDP_DONOR = 0, GSNAPDP_ACCEPTOR = 1, GSNAPDP_ANTIDONOR = 2, GSNAPDP_ANTIACCEPTOR = 3 };
+int gsnapdp_maxent_host(gsnapdp_ctx *ctx, const uint8_t *model, const uint32_t *splice_pos,
+                        const uint32_t *chroffset, double *out, int n);
+int gsnapdp_maxent_device(gsnapdp_ctx *ctx, const uint8_t *d_model, const uint32_t *d_splice_pos,
+                          const uint32_t *d_chroffset, double *d_out, int n, void *stream);
+
+/* Load the MaxEnt parameter tables (12 x 16384 + 4 x 16 doubles, order in
+ * DESIGN.md) into the context.  Must be called before gsnapdp_maxent_*. */
+int gsnapdp_load_maxent_tables(gsnapdp_ctx *ctx, const double *tables, size_t ndoubles);
+
+/* -------------------------------------------------------------- expansion
+ * Replay window i's op stream into the reference's pair list, in final list
+ * order (after the entry point's List_reverse / INDEL stripping / zeroing
+ * rules).  Host only.  `query`/`query_uc` are the same host buffers given to
+ * the run.  Writes at most `cap` pairs; returns the number of pairs in the
+ * list (may exceed cap), or -1 on error.  `*finalscore` receives the
+ * entry point's final score after its post-rules (end-gap zeroing). */
+int gsnapdp_expand(gsnapdp_ctx *ctx, const gsnapdp_window *w, const gsnapdp_result *res,
+                   const uint32_t *ops, const char *query, const char *query_uc,
+                   gsnapdp_pair *pairs, int cap, int *finalscore);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSNAPDP_H */

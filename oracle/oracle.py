@@ -1,0 +1,127 @@
+"""ctypes binding of the CPU restatement (oracle/_build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker / CPU baseline.  The product
+library (gmap-gsnap_amd/) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
+from gsnapdp.records import GGAP_RESULT, GGAP_WINDOW, PAIR, RESULT, WINDOW  # noqa: E402
+
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+TABLES_PATH = os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin")
+
+_lib = None
+_keep = {}
+
+
+def build() -> str:
+    subprocess.check_call(["make", "-s", "-C", HERE], stdout=subprocess.DEVNULL)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        srcs = [os.path.join(HERE, f) for f in ("dp_oracle.c", "maxent_oracle.c", "dp_oracle.h")]
+        if not os.path.exists(LIB_PATH) or any(os.path.getmtime(s) > os.path.getmtime(LIB_PATH) for s in srcs):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32 = ctypes.c_void_p, ctypes.c_int
+        L.orc_init.argtypes = [i32]
+        L.orc_set_genome.argtypes = [vp]
+        L.orc_maxent_load.argtypes = [vp, ctypes.c_size_t]
+        L.orc_maxent_load.restype = i32
+        L.orc_run_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i32]
+        L.orc_run_ggap_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
+        L.orc_maxent_batch.argtypes = [vp, vp, vp, vp, i32]
+        L.orc_pairdistance.argtypes = [i32, i32, i32]
+        L.orc_pairdistance.restype = i32
+        L.orc_consistent.argtypes = [i32, i32]
+        L.orc_consistent.restype = i32
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def setup(blocks: np.ndarray, mode: int = 0, tables: np.ndarray | None = None) -> None:
+    """Dynprog_init(mode) + Genome_user_setup/Maxent_hr_setup(blocks)."""
+    L = lib()
+    L.orc_init(mode)
+    b = np.ascontiguousarray(blocks, dtype=np.uint32)
+    _keep["blocks"] = b
+    L.orc_set_genome(_p(b))
+    if tables is None and os.path.exists(TABLES_PATH):
+        tables = np.fromfile(TABLES_PATH, dtype="<f8")
+    if tables is not None:
+        t = np.ascontiguousarray(tables, dtype="<f8")
+        _keep["tables"] = t
+        if L.orc_maxent_load(_p(t), t.size) != 0:
+            raise RuntimeError("maxent table size mismatch")
+
+
+def pair_offsets_for(windows: np.ndarray, slack: int = 8) -> np.ndarray:
+    """Worst-case list length per window: every pair of the window rectangle
+    (a diagonal pair per row + a dash per column) + 2 gapholders."""
+    l1 = windows["length1"].astype(np.int64) if "length1" in windows.dtype.names else None
+    if "length2L" in windows.dtype.names:
+        cap = 2 * l1 + windows["length2L"] + windows["length2R"] + slack
+    else:
+        cap = l1 + windows["length2"].astype(np.int64) + slack
+    off = np.zeros(len(windows) + 1, dtype=np.int64)
+    np.cumsum(cap, out=off[1:])
+    return off
+
+
+def run_batch(windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray, nthreads: int = 1):
+    """Returns (results[RESULT], pairs[PAIR], pair_offsets[int64], npairs[int32])."""
+    L = lib()
+    w = np.ascontiguousarray(windows, dtype=WINDOW)
+    q = np.ascontiguousarray(query, dtype=np.uint8)
+    u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+    res = np.zeros(len(w), dtype=RESULT)
+    off = pair_offsets_for(w)
+    pairs = np.zeros(int(off[-1]), dtype=PAIR)
+    npairs = np.zeros(len(w), dtype=np.int32)
+    L.orc_run_batch(_p(w), len(w), _p(q), _p(u), _p(res), _p(pairs), _p(off), _p(npairs), nthreads)
+    return res, pairs, off, npairs
+
+
+def run_ggap_batch(windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray):
+    L = lib()
+    w = np.ascontiguousarray(windows, dtype=GGAP_WINDOW)
+    q = np.ascontiguousarray(query, dtype=np.uint8)
+    u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+    res = np.zeros(len(w), dtype=GGAP_RESULT)
+    off = pair_offsets_for(w)
+    pairs = np.zeros(int(off[-1]), dtype=PAIR)
+    npairs = np.zeros(len(w), dtype=np.int32)
+    L.orc_run_ggap_batch(_p(w), len(w), _p(q), _p(u), _p(res), _p(pairs), _p(off), _p(npairs))
+    return res, pairs, off, npairs
+
+
+def maxent(model: np.ndarray, pos: np.ndarray, chroffset: np.ndarray) -> np.ndarray:
+    L = lib()
+    m = np.ascontiguousarray(model, dtype=np.uint8)
+    p = np.ascontiguousarray(pos, dtype=np.uint32)
+    c = np.ascontiguousarray(chroffset, dtype=np.uint32)
+    out = np.zeros(len(m), dtype=np.float64)
+    L.orc_maxent_batch(_p(m), _p(p), _p(c), _p(out), len(m))
+    return out
+
+
+def pairs_of(pairs: np.ndarray, off: np.ndarray, npairs: np.ndarray, i: int) -> np.ndarray:
+    return pairs[off[i]:off[i] + npairs[i]]

@@ -1,0 +1,270 @@
+/*
+ * ref_driver.c -- TEST INFRASTRUCTURE ONLY.  Built only in the survey/dev
+ * container, against the reference's own sources under /root/reference/src
+ * (see oracle/Makefile).  Output goes to oracle/_ref/ (git-ignored) and is used
+ * to generate the golden fixtures in tests/golden/.  Never shipped, never
+ * loaded by the product library.
+ *
+ * Usage:
+ *   ref_driver dp     <dir>   windows.bin query.bin query_uc.bin genome.u32 -> results.bin pairs.bin npairs.i32
+ *   ref_driver ggap   <dir>   ggap_windows.bin query.bin query_uc.bin genome.u32 -> ggap_results.bin pairs.bin npairs.i32
+ *   ref_driver maxent <dir>   maxent_in.bin genome.u32 -> maxent_out.f64
+ *   ref_driver pdist  <dir>   -> pdist.i32 (4 x 128 x 128 via Dynprog_pairdistance for HIGHQ only) + consistent probe
+ * All inputs use the record layouts of include/gsnapdp.h.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* reference headers (from -I/root/reference/src) */
+#include "bool.h"
+#include "dynprog.h"
+#include "genome.h"
+#include "list.h"
+#include "listdef.h"
+#include "maxent_hr.h"
+#include "pairdef.h"
+#include "pairpool.h"
+
+/* our record layouts */
+#include "../include/gsnapdp.h"
+
+static void *slurp(const char *dir, const char *name, size_t *n) {
+  char path[4096];
+  FILE *f;
+  void *buf;
+  long sz;
+  snprintf(path, sizeof(path), "%s/%s", dir, name);
+  f = fopen(path, "rb");
+  if (!f) {
+    fprintf(stderr, "cannot open %s\n", path);
+    exit(2);
+  }
+  fseek(f, 0, SEEK_END);
+  sz = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  buf = malloc((size_t)sz + 64);
+  memset(buf, 0, (size_t)sz + 64);
+  if (sz > 0 && fread(buf, 1, (size_t)sz, f) != (size_t)sz) exit(3);
+  fclose(f);
+  *n = (size_t)sz;
+  return buf;
+}
+
+static void spit(const char *dir, const char *name, const void *buf, size_t n) {
+  char path[4096];
+  FILE *f;
+  snprintf(path, sizeof(path), "%s/%s", dir, name);
+  f = fopen(path, "wb");
+  if (!f) exit(4);
+  if (n) fwrite(buf, 1, n, f);
+  fclose(f);
+}
+
+/* Walk a reference List_T of Pair_T into flat records. */
+static int flatten(List_T pairs, gsnapdp_pair *out, int cap) {
+  int n = 0;
+  List_T p;
+  for (p = pairs; p != NULL; p = p->rest) {
+    Pair_T pair = (Pair_T)p->first;
+    if (n < cap) {
+      gsnapdp_pair *o = &out[n];
+      memset(o, 0, sizeof(*o));
+      o->querypos = pair->querypos;
+      o->genomepos = (int32_t)pair->genomepos;
+      o->queryjump = pair->gapp ? pair->queryjump : 0;
+      o->genomejump = pair->gapp ? pair->genomejump : 0;
+      o->dynprogindex = pair->dynprogindex;
+      o->cdna = pair->cdna;
+      o->comp = pair->comp;
+      o->genome = pair->genome;
+      o->gapp = pair->gapp ? 1 : 0;
+    }
+    n++;
+  }
+  return n;
+}
+
+#define PAIRCAP 8192
+
+static int run_dp(const char *dir) {
+  size_t nw, nq, nu, ng;
+  gsnapdp_window *w = (gsnapdp_window *)slurp(dir, "windows.bin", &nw);
+  char *q = (char *)slurp(dir, "query.bin", &nq);
+  char *qu = (char *)slurp(dir, "query_uc.bin", &nu);
+  UINT4 *g = (UINT4 *)slurp(dir, "genome.u32", &ng);
+  int n = (int)(nw / sizeof(gsnapdp_window)), i;
+  gsnapdp_result *res = (gsnapdp_result *)calloc((size_t)n + 1, sizeof(gsnapdp_result));
+  int32_t *npairs = (int32_t *)calloc((size_t)n + 1, sizeof(int32_t));
+  gsnapdp_pair *tmp = (gsnapdp_pair *)malloc(sizeof(gsnapdp_pair) * PAIRCAP);
+  FILE *fp;
+  char path[4096];
+  Dynprog_T dp = Dynprog_new(600, 10, 11, 10, 8);
+  Pairpool_T pool = Pairpool_new();
+
+  Genome_user_setup(g);
+  Maxent_hr_setup(g);
+  snprintf(path, sizeof(path), "%s/pairs.bin", dir);
+  fp = fopen(path, "wb");
+  for (i = 0; i < n; i++) {
+    gsnapdp_window *x = &w[i];
+    int dpi = x->dynprogindex, fs = 0, nm = 0, nmm = 0, no = 0, ni = 0, k;
+    List_T pairs = NULL;
+    if (x->maxlength1 != 611 || x->maxlength2 != 2000) {
+      fprintf(stderr, "window %d: ref driver only supports maxlength 611x2000\n", i);
+      return 5;
+    }
+    Pairpool_reset(pool);
+    if (getenv("REF_TRACE")) {
+      fprintf(stderr, "w %d kind %d L1 %d L2 %d off2 %d glen %u chrpos %u chrhigh %u chroff %u watson %d band %d end %d\n",
+              i, x->kind, x->length1, x->length2, x->offset2, x->genomiclength, x->chrpos, x->chrhigh,
+              x->chroffset, x->watsonp, x->extraband, x->endalign);
+      fflush(stderr);
+    }
+    if (x->kind == GSNAPDP_SINGLE_GAP) {
+      pairs = Dynprog_single_gap(&dpi, &fs, &nm, &nmm, &no, &ni, dp, q + x->qpos, qu + x->qpos,
+                                 NULL, NULL, x->length1, x->length2, x->offset1, x->offset2,
+                                 x->chroffset, x->chrhigh, x->chrpos, x->genomiclength,
+                                 x->cdna_direction, x->watsonp, x->jump_late_p, pool, x->extraband,
+                                 (double)x->defect_rate, 0, x->widebandp);
+    } else if (x->kind == GSNAPDP_END5_GAP) {
+      pairs = Dynprog_end5_gap(&dpi, &fs, &nm, &nmm, &no, &ni, dp, q + x->qpos, qu + x->qpos, NULL,
+                               NULL, x->length1, x->length2, x->offset1, x->offset2, x->chroffset,
+                               x->chrhigh, x->chrpos, x->genomiclength, x->cdna_direction,
+                               x->watsonp, x->jump_late_p, pool, x->extraband,
+                               (double)x->defect_rate, (Endalign_T)x->endalign,
+                               /*use_genomicseg_p*/ false);
+    } else {
+      pairs = Dynprog_end3_gap(&dpi, &fs, &nm, &nmm, &no, &ni, dp, q + x->qpos, qu + x->qpos, NULL,
+                               NULL, x->length1, x->length2, x->offset1, x->offset2, x->chroffset,
+                               x->chrhigh, x->chrpos, x->genomiclength, x->cdna_direction,
+                               x->watsonp, x->jump_late_p, pool, x->extraband,
+                               (double)x->defect_rate, (Endalign_T)x->endalign, false);
+    }
+    res[i].finalscore = fs;
+    res[i].nmatches = nm;
+    res[i].nmismatches = nmm;
+    res[i].nopens = no;
+    res[i].nindels = ni;
+    res[i].reserved = dpi;
+    k = flatten(pairs, tmp, PAIRCAP);
+    npairs[i] = k;
+    fwrite(tmp, sizeof(gsnapdp_pair), (size_t)(k < PAIRCAP ? k : PAIRCAP), fp);
+  }
+  fclose(fp);
+  spit(dir, "results.bin", res, sizeof(gsnapdp_result) * (size_t)n);
+  spit(dir, "npairs.i32", npairs, sizeof(int32_t) * (size_t)n);
+  return 0;
+}
+
+static int run_ggap(const char *dir) {
+  size_t nw, nq, nu, ng;
+  gsnapdp_ggap_window *w = (gsnapdp_ggap_window *)slurp(dir, "ggap_windows.bin", &nw);
+  char *q = (char *)slurp(dir, "query.bin", &nq);
+  char *qu = (char *)slurp(dir, "query_uc.bin", &nu);
+  UINT4 *g = (UINT4 *)slurp(dir, "genome.u32", &ng);
+  int n = (int)(nw / sizeof(gsnapdp_ggap_window)), i;
+  gsnapdp_ggap_result *res = (gsnapdp_ggap_result *)calloc((size_t)n + 1, sizeof(*res));
+  int32_t *npairs = (int32_t *)calloc((size_t)n + 1, sizeof(int32_t));
+  gsnapdp_pair *tmp = (gsnapdp_pair *)malloc(sizeof(gsnapdp_pair) * PAIRCAP);
+  FILE *fp;
+  char path[4096];
+  Dynprog_T dpL = Dynprog_new(600, 10, 11, 10, 8), dpR = Dynprog_new(600, 10, 11, 10, 8);
+  Pairpool_T pool = Pairpool_new();
+
+  Genome_user_setup(g);
+  Maxent_hr_setup(g);
+  snprintf(path, sizeof(path), "%s/pairs.bin", dir);
+  fp = fopen(path, "wb");
+  for (i = 0; i < n; i++) {
+    gsnapdp_ggap_window *x = &w[i];
+    gsnapdp_ggap_result *o = &res[i];
+    int dpi = x->dynprogindex, k;
+    int fs = 0, nl = 0, nr = 0, nm = 0, nmm = 0, no = 0, ni = 0, eh = 0, it = 0;
+    double lp = 0, rp = 0;
+    List_T pairs;
+    const char *s1 = q + x->qpos, *s1u = qu + x->qpos;
+    Pairpool_reset(pool);
+    pairs = Dynprog_genome_gap(&dpi, &fs, &nl, &nr, &lp, &rp, &nm, &nmm, &no, &ni, &eh, &it, dpL,
+                               dpR, (char *)s1, (char *)s1u, NULL, NULL, NULL, NULL, x->length1,
+                               x->length2L, x->length2R, x->offset1, x->offset2L, x->revoffset2R,
+                               /*chrnum*/ 1, x->chroffset, x->chrhigh, x->chrpos, x->genomiclength,
+                               NULL, false, x->cdna_direction, x->watsonp, x->jump_late_p, pool,
+                               x->extraband_paired, (double)x->defect_rate, x->maxpeelback,
+                               x->halfp, x->finalp, x->use_probabilities_p, x->score_threshold,
+                               x->splicingp);
+    o->finalscore = fs;
+    o->new_leftgenomepos = nl;
+    o->new_rightgenomepos = nr;
+    o->nmatches = nm;
+    o->nmismatches = nmm;
+    o->nopens = no;
+    o->nindels = ni;
+    o->exonhead = eh;
+    o->introntype = it;
+    o->dynprogindex = dpi;
+    o->returned_null = pairs == NULL;
+    o->bridge_ok = 1;
+    o->left_prob = lp;
+    o->right_prob = rp;
+    k = flatten(pairs, tmp, PAIRCAP);
+    npairs[i] = k;
+    fwrite(tmp, sizeof(gsnapdp_pair), (size_t)(k < PAIRCAP ? k : PAIRCAP), fp);
+  }
+  fclose(fp);
+  spit(dir, "ggap_results.bin", res, sizeof(*res) * (size_t)n);
+  spit(dir, "npairs.i32", npairs, sizeof(int32_t) * (size_t)n);
+  return 0;
+}
+
+typedef struct maxent_in {
+  uint32_t model, splice_pos, chroffset, pad;
+} maxent_in;
+
+static int run_maxent(const char *dir) {
+  size_t ni, ng;
+  maxent_in *in = (maxent_in *)slurp(dir, "maxent_in.bin", &ni);
+  UINT4 *g = (UINT4 *)slurp(dir, "genome.u32", &ng);
+  int n = (int)(ni / sizeof(maxent_in)), i;
+  double *out = (double *)calloc((size_t)n + 1, sizeof(double));
+  Genome_user_setup(g);
+  Maxent_hr_setup(g);
+  for (i = 0; i < n; i++) {
+    switch (in[i].model) {
+      case 0: out[i] = Maxent_hr_donor_prob(in[i].splice_pos, in[i].chroffset); break;
+      case 1: out[i] = Maxent_hr_acceptor_prob(in[i].splice_pos, in[i].chroffset); break;
+      case 2: out[i] = Maxent_hr_antidonor_prob(in[i].splice_pos, in[i].chroffset); break;
+      default: out[i] = Maxent_hr_antiacceptor_prob(in[i].splice_pos, in[i].chroffset); break;
+    }
+  }
+  spit(dir, "maxent_out.f64", out, sizeof(double) * (size_t)n);
+  return 0;
+}
+
+static int run_pdist(const char *dir) {
+  /* Only HIGHQ is exported by the reference (Dynprog_pairdistance :1048). */
+  int32_t *t = (int32_t *)malloc(sizeof(int32_t) * 128 * 128);
+  int a, b;
+  for (a = 0; a < 128; a++)
+    for (b = 0; b < 128; b++) t[a * 128 + b] = Dynprog_pairdistance(a, b);
+  spit(dir, "pdist_highq.i32", t, sizeof(int32_t) * 128 * 128);
+  return 0;
+}
+
+int main(int argc, char **argv) {
+  int mode = 0; /* STANDARD */
+  if (argc < 3) {
+    fprintf(stderr, "usage: ref_driver dp|ggap|maxent|pdist <dir> [mode]\n");
+    return 1;
+  }
+  if (argc > 3) mode = atoi(argv[3]);
+  Dynprog_init(600, 10, 11, 10, 8, (Mode_T)mode);
+  Dynprog_setup(/*novelsplicingp*/ false, NULL, NULL, -1, -1, NULL, NULL, NULL, 0, NULL, NULL,
+                NULL, NULL, /*genome*/ NULL);
+  if (!strcmp(argv[1], "dp")) return run_dp(argv[2]);
+  if (!strcmp(argv[1], "ggap")) return run_ggap(argv[2]);
+  if (!strcmp(argv[1], "maxent")) return run_maxent(argv[2]);
+  if (!strcmp(argv[1], "pdist")) return run_pdist(argv[2]);
+  return 1;
+}

@@ -1,0 +1,88 @@
+"""Pin the CPU restatement (oracle/) to the reference's own outputs.
+
+The fixtures in tests/golden/ were produced by the reference compiled from
+its own sources (oracle/gen_golden.py, oracle/_ref/ref_driver).  Every field
+of every pair, every score / count and every maxent probability must match
+bit for bit.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from gsnapdp.records import PAIR
+
+DP_CASES = ["dp_chr17_mix", "dp_synth_mix", "dp_synth_cmet", "dp_chr17_c2", "dp_synth_long"]
+
+
+def load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+
+
+def split_pairs(pairs, npairs):
+    off = np.zeros(len(npairs) + 1, dtype=np.int64)
+    np.cumsum(npairs, out=off[1:])
+    return off
+
+
+@pytest.mark.parametrize("name", DP_CASES)
+def test_dp_oracle_matches_reference(golden_dir, name):
+    z = load(golden_dir, name)
+    O.setup(z["blocks"], mode=int(z["mode"]))
+    res, pairs, off, npairs = O.run_batch(z["windows"], z["query"], z["query_uc"], nthreads=4)
+    for f in ("finalscore", "nmatches", "nmismatches", "nopens", "nindels"):
+        bad = np.nonzero(res[f] != z[f])[0]
+        assert bad.size == 0, "%s differs at windows %s" % (f, bad[:10])
+    assert np.array_equal(res["reserved"], z["dynprogindex"])
+    assert np.array_equal(npairs, z["npairs"])
+    goff = split_pairs(z["pairs"], z["npairs"])
+    got = np.concatenate([pairs[off[i]:off[i] + npairs[i]] for i in range(len(npairs))])
+    assert got.dtype == PAIR
+    for f in PAIR.names:
+        bad = np.nonzero(got[f] != z["pairs"][f])[0]
+        assert bad.size == 0, "pair field %s differs (first pair %s)" % (f, bad[:5])
+    assert goff[-1] == got.size
+
+
+def test_ggap_oracle_matches_reference(golden_dir):
+    z = load(golden_dir, "ggap_chr17")
+    O.setup(z["blocks"])
+    res, pairs, off, npairs = O.run_ggap_batch(z["windows"], z["query"], z["query_uc"])
+    ref = z["results"]
+    assert np.all(res["bridge_ok"] == 1)
+    nn = ref["returned_null"] == 0
+    # out-parameters the reference always writes
+    for f in ("finalscore", "nmatches", "nmismatches", "nopens", "nindels", "dynprogindex",
+              "returned_null"):
+        bad = np.nonzero(res[f] != ref[f])[0]
+        assert bad.size == 0, "%s differs at %s" % (f, bad[:10])
+    # written only when a list is returned
+    for f in ("new_leftgenomepos", "new_rightgenomepos", "exonhead", "introntype"):
+        bad = np.nonzero((res[f] != ref[f]) & nn)[0]
+        assert bad.size == 0, "%s differs at %s" % (f, bad[:10])
+    for f in ("left_prob", "right_prob"):
+        assert np.array_equal(res[f].view(np.uint64), ref[f].view(np.uint64)), f
+    assert np.array_equal(npairs, z["npairs"])
+    got = np.concatenate([pairs[off[i]:off[i] + npairs[i]] for i in range(len(npairs))])
+    for f in PAIR.names:
+        assert np.array_equal(got[f], z["pairs"][f]), f
+
+
+@pytest.mark.parametrize("name", ["maxent_chr17", "maxent_synth"])
+def test_maxent_oracle_matches_reference(golden_dir, name):
+    z = load(golden_dir, name)
+    O.setup(z["blocks"])
+    got = O.maxent(z["model"], z["splice_pos"], z["chroffset"])
+    ref = z["prob"]
+    bad = np.nonzero(got.view(np.uint64) != ref.view(np.uint64))[0]
+    assert bad.size == 0, "maxent differs at %s (model %s shift %s)" % (
+        bad[:10], z["model"][bad[:10]], z["splice_pos"][bad[:10]] % 32)
+
+
+def test_pairdistance_matches_reference(golden_dir):
+    z = load(golden_dir, "pairdistance_highq")
+    O.setup(np.zeros(16, np.uint32))
+    L = O.lib()
+    got = np.array([[L.orc_pairdistance(0, a, b) for b in range(128)] for a in range(128)])
+    assert np.array_equal(got, z["table"])
