@@ -1,0 +1,231 @@
+// gsnapdp_host.cpp -- host half of the product library: substitution tables
+// (the profile words the kernels read) and the op-stream -> pair-list
+// expansion that reproduces the reference's Pairpool_push sequence.
+#include <ctype.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "gsnapdp_internal.h"
+
+extern "C" const uint32_t* gsnapdp__host_blocks(gsnapdp_ctx* ctx);
+extern "C" size_t gsnapdp__host_nwords(gsnapdp_ctx* ctx);
+extern "C" const uint32_t* gsnapdp__host_prof(gsnapdp_ctx* ctx);
+
+namespace gsnapdp {
+
+namespace {
+int pd_tab[4][128][128];
+unsigned char cons_tab[128][128];
+int tab_mode = -1;
+
+void set_all_cases(int a, int b, int score, bool symmetric) {
+  // every upper/lower-case combination (permute_cases / _oneway, dynprog.c:1053-1124)
+  const int as[2] = {a, tolower(a)}, bs[2] = {b, tolower(b)};
+  for (int i = 0; i < 2; i++)
+    for (int j = 0; j < 2; j++) {
+      cons_tab[as[i]][bs[j]] = 1;
+      for (int t = 0; t < 4; t++) pd_tab[t][as[i]][bs[j]] = score;
+      if (symmetric) {
+        cons_tab[bs[j]][as[i]] = 1;
+        for (int t = 0; t < 4; t++) pd_tab[t][bs[j]][as[i]] = score;
+      }
+    }
+}
+
+void init_tables(int mode) {
+  // pairdistance_init (dynprog.c:1127-1226)
+  static const int mism[4] = {-3, -2, -1, -5};
+  memset(pd_tab, 0, sizeof(pd_tab));
+  memset(cons_tab, 0, sizeof(cons_tab));
+  for (int c1 = 'A'; c1 <= 'z'; c1++)
+    for (int c2 = 'A'; c2 < 'z'; c2++)
+      for (int t = 0; t < 4; t++) pd_tab[t][c1][c2] = mism[t];
+  set_all_cases('U', 'T', 3, true);
+  struct Amb { char code; const char* bases; int score; };
+  static const Amb amb[] = {{'R', "AG", 1},  {'Y', "TC", 1},  {'W', "AT", 1},  {'S', "GC", 1},
+                            {'M', "AC", 1},  {'K', "GT", 1},  {'H', "ATC", -1}, {'B', "GCT", -1},
+                            {'V', "GAC", -1}, {'D', "GAT", -1}, {'N', "TCAG", -1}, {'X', "TCAG", -1}};
+  for (const Amb& a : amb)
+    for (const char* p = a.bases; *p; p++) set_all_cases(a.code, *p, a.score, true);
+  if (mode == GSNAPDP_MODE_CMET_STRANDED || mode == GSNAPDP_MODE_CMET_NONSTRANDED) {
+    set_all_cases('T', 'C', 3, false);
+    set_all_cases('A', 'G', 3, false);
+  }
+  for (int c = 'A'; c < 'Z'; c++) set_all_cases(c, c, 3, true);
+  tab_mode = mode;
+}
+}  // namespace
+
+void build_profile_table(int mode, uint32_t prof[4 * 128]) {
+  init_tables(mode);
+  static const char cls[6] = {'A', 'C', 'G', 'T', 'N', '*'};
+  for (int t = 0; t < 4; t++)
+    for (int c = 0; c < 128; c++) {
+      uint32_t w = 0;
+      for (int g = 0; g < 6; g++) w |= ((uint32_t)pd_tab[t][c][(int)cls[g]] & 0xFu) << (4 * g);
+      for (int g = 0; g < 5; g++) w |= (uint32_t)cons_tab[c][(int)cls[g]] << (24 + g);
+      prof[t * 128 + c] = w;
+    }
+}
+
+int host_pairdistance(int mt, int c1, int c2) { return pd_tab[mt][c1 & 127][c2 & 127]; }
+int host_consistent(int c1, int c2) { return cons_tab[c1 & 127][c2 & 127]; }
+
+}  // namespace gsnapdp
+
+using namespace gsnapdp;
+
+namespace {
+
+struct HostGenome {
+  const uint32_t* blocks;
+  size_t nwords;
+  uint32_t chroffset, chrhigh, chrpos;
+  int glen, watson;
+  // get_genomic_nt (dynprog.c:403-441)
+  char nt(int gpos) const {
+    if (gpos < 0 || gpos >= glen) return '*';
+    const uint32_t base = chroffset + chrpos;
+    if (base < chroffset || base >= chrhigh) return '*';
+    const uint32_t pos = watson ? base + (uint32_t)gpos : base + (uint32_t)(glen - 1) - (uint32_t)gpos;
+    const size_t ptr = (size_t)(pos >> 5) * 3;
+    if (ptr + 2 >= nwords) return 'N';
+    const uint32_t bit = pos & 31u;
+    char c;
+    if ((blocks[ptr + 2] >> bit) & 1u) c = 'N';
+    else c = "ACGT"[((bit < 16 ? blocks[ptr + 1] : blocks[ptr]) >> ((bit & 15u) * 2u)) & 3u];
+    if (watson) return c;
+    switch (c) {
+      case 'A': return 'T';
+      case 'C': return 'G';
+      case 'G': return 'C';
+      case 'T': return 'A';
+      default: return 'N';
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" int gsnapdp_expand(gsnapdp_ctx* ctx, const gsnapdp_window* w, const gsnapdp_result* res,
+                              const uint32_t* ops, const char* query, const char* query_uc,
+                              gsnapdp_pair* pairs, int cap, int* finalscore) {
+  if (!ctx || !w || !res) return -1;
+  if (finalscore) *finalscore = res->finalscore;
+  if (res->status == ST_EARLY || res->status == ST_ZEROED || res->status == ST_UNSUPPORTED) return 0;
+  if (res->status == ST_OPS_OVERFLOW) return -1;
+  const uint32_t* prof = gsnapdp__host_prof(ctx);
+  HostGenome G = {gsnapdp__host_blocks(ctx), gsnapdp__host_nwords(ctx), w->chroffset, w->chrhigh,
+                  w->chrpos, (int)w->genomiclength, w->watsonp ? 1 : 0};
+  const bool rev = w->kind == GSNAPDP_END5_GAP;
+  const char* q = query + w->qpos;
+  const char* qu = query_uc + w->qpos;
+  const int qoff = w->offset1, goff = w->offset2, dpi = w->dynprogindex;
+  int r = res->bestr, c = res->bestc;
+  std::vector<gsnapdp_pair> p;  // push order
+  p.reserve(256);
+  auto push = [&](int qpos, int gpos, char cdna, char comp, char g) {
+    gsnapdp_pair x;
+    memset(&x, 0, sizeof(x));
+    x.querypos = qpos;
+    x.genomepos = gpos;
+    x.dynprogindex = dpi;
+    x.cdna = cdna;
+    x.comp = comp;
+    x.genome = g;
+    p.push_back(x);
+  };
+  auto consistent = [&](unsigned char c1, char g) -> bool {
+    int gi = g == 'A' ? 0 : g == 'C' ? 1 : g == 'G' ? 2 : g == 'T' ? 3 : 4;
+    return (prof[c1 & 127] >> (24 + gi)) & 1u;  // consistent_array is mode-independent per mt
+  };
+  for (int k = 0; k < res->nops; k++) {
+    const uint32_t op = ops[k];
+    const int cnt = (int)GSNAPDP_OP_COUNT(op);
+    switch (GSNAPDP_OP_TYPE(op)) {
+      case GSNAPDP_OP_DIAG:
+        for (int j = 0; j < cnt; j++, r--, c--) {
+          int qc = r - 1, gc = c - 1;
+          if (rev) {
+            qc = -qc;
+            gc = -gc;
+          }
+          const char c1 = q[qc];
+          const char c2 = G.nt(goff + gc);
+          if (c2 == '*') continue;  // dynprog.c:2644
+          char comp;
+          if (qu[qc] == c2) comp = GSNAPDP_DYNPROG_MATCH_COMP;
+          else if (consistent((unsigned char)c1, c2)) comp = GSNAPDP_AMBIGUOUS_COMP;
+          else comp = GSNAPDP_MISMATCH_COMP;
+          push(qoff + qc, goff + gc, c1, comp, c2);
+        }
+        break;
+      case GSNAPDP_OP_HDASH: {  // add_genomeskip dashes (dynprog.c:2478-2499)
+        int qc = r - 1, left = c - cnt, right = c - 1, step;
+        if (rev) {
+          const int t = left;
+          qc = -qc;
+          left = -right;
+          right = -t;
+          step = +1;
+        } else {
+          qc++;
+          step = -1;
+        }
+        int gc = rev ? left : right;
+        for (int j = 0; j < cnt; j++, gc += step) push(qoff + qc, goff + gc, ' ', '-', G.nt(goff + gc));
+        c -= cnt;
+        break;
+      }
+      case GSNAPDP_OP_HGAP: {  // gapholder (dynprog.c:2507)
+        gsnapdp_pair x;
+        memset(&x, 0, sizeof(x));
+        x.querypos = -1;
+        x.genomepos = -1;
+        x.queryjump = GSNAPDP_UNKNOWNJUMP;
+        x.genomejump = GSNAPDP_UNKNOWNJUMP;
+        x.cdna = ' ';
+        x.comp = ' ';
+        x.genome = ' ';
+        x.gapp = 1;
+        p.push_back(x);
+        c -= cnt;
+        break;
+      }
+      default: {  // GSNAPDP_OP_VSKIP, add_queryskip (dynprog.c:2372-2413)
+        int qc = r - 1, gc = c - 1, step;
+        if (rev) {
+          qc = -qc;
+          gc = -gc;
+          step = +1;
+        } else {
+          gc++;
+          step = -1;
+        }
+        for (int j = 0; j < cnt; j++, qc += step) push(qoff + qc, goff + gc, q[qc], '-', ' ');
+        r -= cnt;
+        break;
+      }
+    }
+  }
+  // final list orientation (dynprog.c:4571, 5264-5283, 5721-5740)
+  const int m = (int)p.size();
+  int n = 0;
+  if (w->kind == GSNAPDP_SINGLE_GAP) {
+    for (int i = 0; i < m; i++, n++)
+      if (n < cap) pairs[n] = p[i];
+  } else {
+    int j = 0;
+    while (j < m && p[j].comp == '-') j++;
+    if (w->kind == GSNAPDP_END3_GAP) {
+      for (int i = j; i < m; i++, n++)
+        if (n < cap) pairs[n] = p[i];
+    } else {
+      for (int i = m - 1; i >= j; i--, n++)
+        if (n < cap) pairs[n] = p[i];
+    }
+  }
+  return n;
+}

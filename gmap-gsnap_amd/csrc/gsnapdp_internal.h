@@ -1,0 +1,142 @@
+// gsnapdp_internal.h -- shared between the HIP kernels (gsnapdp_kernels.hip)
+// and the host-side code (gsnapdp_host.cpp).  Not part of the public ABI.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/gsnapdp.h"
+
+namespace gsnapdp {
+
+constexpr int NEG = -1000000;          // NEG_INFINITY, dynprog.c:119
+constexpr int MICROINTRON_LENGTH = 9;  // dynprog.c:139
+constexpr int FAST_L2MAX = 640;        // longest genome span handled by the register-band kernel
+// band-width groups, one k_fill launch each: W in (CLASS_W[c-1], CLASS_W[c]]
+constexpr int NCLASS = 9;
+constexpr int CLASS_W[NCLASS] = {8, 16, 24, 28, 32, 36, 40, 44, 48};
+constexpr int FAST_WMAX = 48;
+// bucket key = ((W * (FAST_WMAX+1) + lband) * 6 + jl*3 + mode), W <= 48, lband <= 47
+constexpr int NKEYS = (FAST_WMAX + 1) * (FAST_WMAX + 1) * 6;
+constexpr int BIG_LANES = 256;         // lanes of the generic (global-memory band) kernel
+constexpr int BIG_WMAX = 2048;
+constexpr int BIG_L2MAX = 2048;
+constexpr int BIG_L1MAX = 2048;
+
+// Mismatch types (dynprog.c:150)
+enum { MT_HIGHQ = 0, MT_MEDQ = 1, MT_LOWQ = 2, MT_ENDQ = 3 };
+
+// Window status (gsnapdp_result.status)
+enum { ST_OK = 0, ST_EARLY = 1, ST_OPS_OVERFLOW = 2, ST_ZEROED = 3, ST_UNSUPPORTED = 4 };
+
+// Derived per-window parameters (device + host), restating the parameter
+// selection of Dynprog_single_gap (dynprog.c:4471-4519) and
+// Dynprog_end5/3_gap (:5127-5163, 5589-5623).
+struct Derived {
+  int L1, L2;          // effective lengths (after end-gap chopping)
+  int lband, rband;    // fill band (dynprog.c:1442-1454)
+  int W;               // lband + rband + 1
+  int mode;            // 0 endpoint (L1,L2); 1 best local; 2 queryend indels; 3 nogaps
+  int eb;              // extraband
+  int open, ext, mt, jl, rev;
+  int status;          // ST_OK or an early-return / unsupported status
+  int early_score;     // finalscore for early returns
+  int early_dpi_step;  // 1 if *dynprogindex is stepped on the early return
+};
+
+#if defined(__HIPCC__)
+#define GSNAPDP_HD __host__ __device__
+#else
+#define GSNAPDP_HD
+#endif
+
+GSNAPDP_HD inline Derived derive(const gsnapdp_window& w) {
+  Derived d;
+  d.L1 = w.length1;
+  d.L2 = w.length2;
+  d.eb = w.extraband;
+  d.status = ST_OK;
+  d.early_score = 0;
+  d.early_dpi_step = 0;
+  d.rev = (w.kind == GSNAPDP_END5_GAP) ? 1 : 0;
+  int wide = 1;
+  if (w.kind == GSNAPDP_SINGLE_GAP) {
+    const double dr = (double)w.defect_rate;  // DEFECT_HIGHQ/MEDQ, dynprog.h:27-28
+    d.mt = dr < 0.003 ? MT_HIGHQ : (dr < 0.014 ? MT_MEDQ : MT_LOWQ);
+    d.open = -10;
+    d.ext = -3;
+    d.jl = w.jump_late_p ? 1 : 0;
+    d.mode = 0;
+    wide = w.widebandp ? 1 : 0;
+    if (d.L1 > w.maxlength1 || d.L2 > w.maxlength2) {
+      d.status = ST_EARLY;
+      d.early_score = -10000;
+      d.early_dpi_step = 1;
+    } else if (d.L1 <= 0 || d.L2 <= 0) {
+      d.status = ST_UNSUPPORTED;  // reference aborts (Matrix3_alloc, dynprog.c:495-498)
+    } else if (!wide && (d.L2 - d.L1 > d.eb || d.L1 - d.L2 > d.eb)) {
+      d.status = ST_UNSUPPORTED;  // reference writes past the matrix (dynprog.c:1504)
+    }
+  } else {
+    d.mt = MT_ENDQ;
+    d.open = -12;
+    d.ext = -1;
+    d.jl = (d.rev ? !w.jump_late_p : w.jump_late_p) ? 1 : 0;
+    if (w.endalign == GSNAPDP_QUERYEND_NOGAPS) d.mode = 3;
+    else if (w.endalign == GSNAPDP_QUERYEND_INDELS) d.mode = 2;
+    else if (w.endalign == GSNAPDP_QUERYEND_GAP || w.endalign == GSNAPDP_BEST_LOCAL) d.mode = 1;
+    else d.status = ST_UNSUPPORTED;  // reference aborts (dynprog.c:5215)
+    if (d.L1 <= 0 || d.L2 <= 0) {
+      d.status = ST_EARLY;
+      d.early_score = 0;
+      d.early_dpi_step = 0;
+    } else if (d.mode != 3) {
+      if (d.L1 > w.maxlength1) d.L1 = w.maxlength1;
+      if (d.L2 > w.maxlength2) d.L2 = w.maxlength2;
+    }
+  }
+  if (!wide) {
+    d.lband = d.eb;
+    d.rband = d.eb;
+  } else if (d.L2 >= d.L1) {
+    d.rband = d.L2 - d.L1 + d.eb;
+    d.lband = d.eb;
+  } else {
+    d.lband = d.L1 - d.L2 + d.eb;
+    d.rband = d.eb;
+  }
+  if (d.eb < 0) d.status = ST_UNSUPPORTED;
+  d.W = d.lband + d.rband + 1;
+  return d;
+}
+
+GSNAPDP_HD inline int step_dpi(int dpi) { return dpi + (dpi > 0 ? 1 : -1); }
+
+// Intron_type (intron.c:18-180, non-PMAP) on genome class codes
+// 0..5 = A C G T N *
+GSNAPDP_HD inline int intron_type_codes(int l1, int l2, int r2, int r1, int cdna_direction) {
+  int leftdi, rightdi, t;
+  if (l1 == 2 && l2 == 3) leftdi = 0x21;       // GT
+  else if (l1 == 2 && l2 == 1) leftdi = 0x10;  // GC
+  else if (l1 == 0 && l2 == 3) leftdi = 0x08;  // AT
+  else if (l1 == 1 && l2 == 3) leftdi = 0x06;  // CT
+  else return 0;
+  if (r2 == 0 && r1 == 2) rightdi = 0x30;       // AG
+  else if (r2 == 0 && r1 == 1) rightdi = 0x0C;  // AC
+  else if (r2 == 2 && r1 == 1) rightdi = 0x02;  // GC
+  else if (r2 == 0 && r1 == 3) rightdi = 0x01;  // AT
+  else return 0;
+  if ((t = leftdi & rightdi) == 0) return 0;
+  if (cdna_direction > 0) return t < 0x08 ? 0 : t;
+  if (cdna_direction < 0) return t > 0x04 ? 0 : t;
+  return 0;
+}
+
+}  // namespace gsnapdp
+
+// Host-side helpers implemented in gsnapdp_host.cpp
+namespace gsnapdp {
+// Profile words prof[mt*128 + c]: bits 4g..4g+3 = pairdistance[mt][c][class g] as a
+// signed 4-bit field (g = A C G T N *), bits 24..28 = consistent_array[c][class g].
+void build_profile_table(int mode, uint32_t prof[4 * 128]);
+int host_pairdistance(int mt, int c1, int c2);
+int host_consistent(int c1, int c2);
+}  // namespace gsnapdp

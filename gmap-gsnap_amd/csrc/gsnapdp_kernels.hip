@@ -1,0 +1,1017 @@
+// gsnapdp_kernels.hip -- MI355X (gfx950) kernels for GMAP/GSNAP's stage-3
+// gap-filling DP (reference src/dynprog.c, 2012-07-03).
+//
+// Design (DESIGN.md has the long form):
+//   * one LANE per DP window (inter-window parallelism; 64 windows per wave);
+//   * the window's band lives in registers as WMAX "slots", one per diagonal
+//     d = r - c + rband, bottom-aligned so slot WMAX-1 is the lowest diagonal
+//     and the sentinel below it (dynprog.c:1508-1513) is a compile-time NEG;
+//   * column-major sweep (the reference's own order, dynprog.c:1491-1563):
+//     per column every slot does gap1 (from slot+1), gap2 (chained from slot-1)
+//     and nogap (same slot) with the sequential tie rule;
+//   * waves are made uniform in (band, tie rule, endpoint mode) by an on-device
+//     counting sort (k_plan / k_scan / k_scatter), so band edges are scalar;
+//   * 4-bit direction nibbles stream to HBM scratch; each lane then walks its
+//     own traceback and emits a compact op stream (include/gsnapdp.h).
+//   Windows too wide (W > 48) or too long (L2 > 640) for registers run the same
+//   recurrences with the band in global memory (k_big).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gsnapdp_internal.h"
+
+using namespace gsnapdp;
+
+namespace {
+
+// ------------------------------------------------------------ per-lane view
+struct Lane {
+  Derived d;
+  int qbase, qstep;   // query index of row r: qbase + qstep*(r-1)
+  int g0, gstep;      // genomicpos of column c: g0 + gstep*(c-1)
+  uint32_t base;      // chroffset + chrpos (uint32 wrap, like the reference)
+  int glen;
+  int watson;
+  int allstar;        // chroffset+chrpos overflow or >= chrhigh (dynprog.c:415-419)
+  int off1, off2;     // pair coordinate offsets
+  int cdna_direction;
+};
+
+__device__ inline Lane make_lane(const gsnapdp_window& w) {
+  Lane L;
+  L.d = derive(w);
+  L.qbase = (int)w.qpos;
+  L.qstep = L.d.rev ? -1 : 1;
+  L.g0 = w.offset2;
+  L.gstep = L.d.rev ? -1 : 1;
+  L.base = w.chroffset + w.chrpos;
+  L.glen = (int)w.genomiclength;
+  L.watson = w.watsonp ? 1 : 0;
+  L.allstar = (L.base < w.chroffset) || (L.base >= w.chrhigh);
+  L.off1 = w.offset1;
+  L.off2 = w.offset2;
+  L.cdna_direction = w.cdna_direction;
+  return L;
+}
+
+// get_genomic_nt (dynprog.c:403-441) on the packed blocks (uncompress_one_char,
+// genome.c:9325): class code 0..5 = A C G T N '*'.
+__device__ inline int gclass(const uint32_t* __restrict__ blocks, uint64_t nwords, const Lane& L,
+                             int gpos) {
+  if (gpos < 0 || gpos >= L.glen || L.allstar) return 5;
+  const uint32_t pos = L.watson ? (L.base + (uint32_t)gpos)
+                                : (L.base + (uint32_t)(L.glen - 1) - (uint32_t)gpos);
+  const uint64_t ptr = (uint64_t)(pos >> 5) * 3u;
+  if (ptr + 2 >= nwords) return 4;  // outside the genome (outside the reference's domain)
+  const uint32_t bit = pos & 31u;
+  const uint32_t fl = blocks[ptr + 2];
+  if ((fl >> bit) & 1u) return 4;
+  const uint32_t word = bit < 16 ? blocks[ptr + 1] : blocks[ptr];
+  const int code = (int)((word >> ((bit & 15u) * 2u)) & 3u);
+  return L.watson ? code : 3 - code;
+}
+
+__device__ inline int wave_max(int x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o));
+  return x;
+}
+
+__device__ inline unsigned char qchar(const char* __restrict__ q, int idx) {
+  return (unsigned char)q[idx] & 127u;
+}
+
+// --------------------------------------------------------------- op writer
+struct OpWriter {
+  uint32_t* out;
+  int cap, n;
+  int run;  // pending DIAG steps
+  __device__ inline void put(uint32_t op) {
+    if (n < cap) out[n] = op;
+    n++;
+  }
+  __device__ inline void flush() {
+    if (run > 0) put(GSNAPDP_OP(GSNAPDP_OP_DIAG, run));
+    run = 0;
+  }
+};
+
+// Counts of one traceback
+struct Tally {
+  int nmatches, nmismatches, nopens, nindels;
+};
+
+// Direction nibble: bit0 gap1==HORIZ, bit1 gap2==VERT, bit2 nogap HORIZ, bit3 nogap VERT.
+// `dirs(r, c)` returns the nibble of an in-band cell with r >= 1, c >= 1.
+//
+// traceback (dynprog.c:2611-2712) with the reference's memset semantics for
+// cells outside the band and the row-0 / column-0 initialisation
+// (dynprog.c:1460-1488).
+template <class Dirs>
+__device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c,
+                                 const char* __restrict__ q, const char* __restrict__ qu,
+                                 const uint32_t* __restrict__ blocks, uint64_t nwords,
+                                 const uint32_t* __restrict__ prof, Tally& t, OpWriter& ow) {
+  const int lband = L.d.lband, rband = L.d.rband;
+  auto inband = [&](int rr, int cc) {
+    const int d = rr - cc + rband;
+    return rr >= 1 && cc >= 1 && d >= 0 && d <= lband + rband;
+  };
+  auto gap1_horiz = [&](int rr, int cc) -> bool {
+    if (rr == 0) return cc >= 2 && cc <= rband && cc <= L.d.L2;
+    if (!inband(rr, cc)) return false;
+    return dirs(rr, cc) & 1u;
+  };
+  auto gap2_vert = [&](int rr, int cc) -> bool {
+    if (cc == 0) return rr >= 2 && rr <= lband && rr <= L.d.L1;
+    if (!inband(rr, cc)) return false;
+    return (dirs(rr, cc) >> 1) & 1u;
+  };
+  const uint32_t* ptab = prof + L.d.mt * 128;
+  while (inband(r, c)) {
+    const uint32_t nib = dirs(r, c);
+    // the nogap cell (r,c) itself: one pair unless the genome is '*'
+    const int g = gclass(blocks, nwords, L, L.g0 + L.gstep * (c - 1));
+    if (g != 5) {
+      const int qi = L.qbase + L.qstep * (r - 1);
+      const unsigned char c1 = qchar(q, qi);
+      const unsigned char u1 = (unsigned char)qu[qi];
+      const unsigned char gch = (unsigned char)("ACGTN"[g]);
+      if (u1 == gch || ((ptab[c1] >> (24 + g)) & 1u)) t.nmatches++;
+      else t.nmismatches++;
+    }
+    ow.run++;
+    if (nib & 8u) {  // VERT: query skip (add_queryskip, dynprog.c:2372)
+      int dist = 1;
+      r--;
+      c--;
+      while (gap2_vert(r, c)) {
+        dist++;
+        r--;
+      }
+      r--;
+      ow.flush();
+      ow.put(GSNAPDP_OP(GSNAPDP_OP_VSKIP, dist));
+      t.nopens++;
+      t.nindels += dist;
+    } else if (nib & 4u) {  // HORIZ: genome skip (add_genomeskip, dynprog.c:2416)
+      int dist = 1;
+      r--;
+      c--;
+      while (gap1_horiz(r, c)) {
+        dist++;
+        c--;
+      }
+      c--;
+      bool dashes = true;
+      if (dist >= MICROINTRON_LENGTH) {
+        // columns c+1 .. c+dist are skipped; left = column c+1, right = column c+dist
+        const int cl = c + 1, cr = c + dist;
+        const int gl = L.g0 + L.gstep * (cl - 1), gr = L.g0 + L.gstep * (cr - 1);
+        // in window-coordinate order (leftgenomecoord < rightgenomecoord)
+        const int lo = L.d.rev ? gr : gl, hi = L.d.rev ? gl : gr;
+        const int l1 = gclass(blocks, nwords, L, lo), l2 = gclass(blocks, nwords, L, lo + 1);
+        const int r2 = gclass(blocks, nwords, L, hi - 1), r1 = gclass(blocks, nwords, L, hi);
+        dashes = intron_type_codes(l1, l2, r2, r1, L.cdna_direction) == 0;
+      }
+      ow.flush();
+      ow.put(GSNAPDP_OP(dashes ? GSNAPDP_OP_HDASH : GSNAPDP_OP_HGAP, dist));
+      if (dashes) {
+        t.nopens++;
+        t.nindels += dist;
+      }
+    } else {
+      r--;
+      c--;
+    }
+  }
+  ow.flush();
+}
+
+// Final bookkeeping shared by all paths.
+__device__ inline void write_result(gsnapdp_result* res, const gsnapdp_window& w, const Lane& L,
+                                    int score, int bestr, int bestc, const Tally& t,
+                                    const OpWriter& ow) {
+  gsnapdp_result R;
+  R.finalscore = score;
+  R.nmatches = t.nmatches;
+  R.nmismatches = t.nmismatches;
+  R.nopens = t.nopens;
+  R.nindels = t.nindels;
+  R.bestr = bestr;
+  R.bestc = bestc;
+  R.nops = ow.n < ow.cap ? ow.n : ow.cap;
+  R.status = ow.n > ow.cap ? ST_OPS_OVERFLOW : ST_OK;
+  R.length1 = L.d.L1;
+  R.length2 = L.d.L2;
+  R.reserved = step_dpi(w.dynprogindex);
+  // end gaps, QUERYEND_GAP / BEST_LOCAL: dynprog.c:5259-5262 / 5715-5718
+  if (L.d.mode == 1 && t.nmatches + 1 < t.nmismatches) {
+    R.finalscore = 0;
+    if (R.status == ST_OK) R.status = ST_ZEROED;
+  }
+  // QUERYEND_NOGAPS rescoring: dynprog.c:5243 / 5700
+  if (L.d.mode == 3) R.finalscore = t.nmatches * 3 + t.nmismatches * (-5);
+  *res = R;
+}
+
+// ------------------------------------------------------------------ k_plan
+// Early returns, QUERYEND_NOGAPS windows (no fill at all) and bucketing.
+__global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* __restrict__ q,
+                       const char* __restrict__ qu, const uint32_t* __restrict__ blocks,
+                       uint64_t nwords, const uint32_t* __restrict__ prof,
+                       gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
+                       const int64_t* __restrict__ op_off, int* __restrict__ keys,
+                       int* __restrict__ hist, int* __restrict__ big_list,
+                       int* __restrict__ big_count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const gsnapdp_window w = W[i];
+  const Lane L = make_lane(w);
+  keys[i] = -1;
+  if (L.d.status != ST_OK) {
+    gsnapdp_result R = {};
+    R.finalscore = L.d.early_score;
+    R.status = L.d.status;
+    R.length1 = L.d.L1;
+    R.length2 = L.d.L2;
+    R.reserved = L.d.early_dpi_step ? step_dpi(w.dynprogindex) : w.dynprogindex;
+    res[i] = R;
+    return;
+  }
+  if (L.d.mode == 3) {  // traceback_nogaps (dynprog.c:2815-2872) from (min,min)
+    Tally t = {0, 0, 0, 0};
+    OpWriter ow = {ops + op_off[i], (int)(op_off[i + 1] - op_off[i]), 0, 0};
+    const int m = min(L.d.L1, L.d.L2);
+    const uint32_t* ptab = prof + L.d.mt * 128;
+    for (int r = m, c = m; r > 0 && c > 0; r--, c--) {
+      const int g = gclass(blocks, nwords, L, L.g0 + L.gstep * (c - 1));
+      if (g != 5) {
+        const int qi = L.qbase + L.qstep * (r - 1);
+        const unsigned char c1 = qchar(q, qi);
+        const unsigned char u1 = (unsigned char)qu[qi];
+        if (u1 == (unsigned char)("ACGTN"[g]) || ((ptab[c1] >> (24 + g)) & 1u)) t.nmatches++;
+        else t.nmismatches++;
+      }
+      ow.run++;
+    }
+    ow.flush();
+    write_result(&res[i], w, L, 0, m, m, t, ow);
+    return;
+  }
+  if (L.d.mode == 0 && L.d.W <= FAST_WMAX && L.d.L2 <= FAST_L2MAX) {
+    const int key = ((L.d.W * (FAST_WMAX + 1) + L.d.lband) * 6) + L.d.jl * 3 + L.d.mode;
+    keys[i] = key;
+    atomicAdd(&hist[key], 1);
+  } else {
+    const int slot = atomicAdd(big_count, 1);
+    big_list[slot] = i;
+  }
+}
+
+// Exclusive scan of bucket sizes padded to whole waves; class wave ranges.
+// cursor[k] = first perm entry of bucket k; class_range[c] = first wave of class c.
+__global__ void k_scan(const int* __restrict__ hist, int* __restrict__ cursor,
+                       int* __restrict__ class_range) {
+  __shared__ int part[1024];
+  const int tid = threadIdx.x;
+  const int per = (NKEYS + 1023) / 1024;
+  const int lo = tid * per, hi = min(NKEYS, lo + per);
+  int s = 0;
+  for (int k = lo; k < hi; k++) s += (hist[k] + 63) & ~63;
+  part[tid] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    int v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int run = part[tid] - s;
+  for (int k = lo; k < hi; k++) {
+    cursor[k] = run;
+    run += (hist[k] + 63) & ~63;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // class c covers W in (CLASS_W[c-1], CLASS_W[c]]; keys are W-major
+    int wlo = 0;
+    for (int c = 0; c < NCLASS; c++) {
+      const int kfirst = (wlo + 1) * (FAST_WMAX + 1) * 6;
+      class_range[c] = (kfirst < NKEYS ? cursor[kfirst] : part[1023]) / 64;
+      wlo = CLASS_W[c];
+    }
+    class_range[NCLASS] = part[1023] / 64;
+  }
+}
+
+__global__ void k_scatter(const int* __restrict__ keys, int n, int* __restrict__ cursor,
+                          int* __restrict__ perm) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int k = keys[i];
+  if (k < 0) return;
+  perm[atomicAdd(&cursor[k], 1)] = i;
+}
+
+// ------------------------------------------------------------------ k_fill
+// Per-lane column genome stream: class of column c for the window, branch
+// free.  pos(c) = P0 + PS*c in reference uint32 arithmetic (get_genomic_nt).
+struct ColStream {
+  uint32_t P0;
+  int PS;        // +1 / -1
+  int cvlo, cvhi;  // columns whose genomicpos is inside [0, genomiclength)
+  int xorc;      // 0 watson, 3 crick (complement of the 2-bit code)
+  __device__ inline void init(const Lane& L) {
+    const int gstep = L.gstep;
+    if (L.watson) {
+      P0 = L.base + (uint32_t)(L.g0 - gstep);
+      PS = gstep;
+    } else {
+      P0 = L.base + (uint32_t)(L.glen - 1) - (uint32_t)(L.g0 - gstep);
+      PS = -gstep;
+    }
+    if (gstep > 0) {
+      cvlo = 1 - L.g0;
+      cvhi = L.glen - L.g0;
+    } else {
+      cvlo = L.g0 + 2 - L.glen;
+      cvhi = L.g0 + 1;
+    }
+    if (L.allstar) {
+      cvlo = 1 << 30;
+      cvhi = -(1 << 30);
+    }
+    xorc = L.watson ? 0 : 3;
+  }
+  __device__ inline int cls(const uint32_t* __restrict__ blocks, uint64_t nwords, int c) const {
+    const uint32_t pos = P0 + (uint32_t)(PS * c);
+    const uint64_t ptr = (uint64_t)(pos >> 5) * 3u;
+    const bool inr = c >= cvlo && c <= cvhi;
+    const bool ing = ptr + 2 < nwords;
+    const uint64_t p = (inr && ing) ? ptr : 0;
+    const uint32_t bit = pos & 31u;
+    const uint32_t fl = blocks[p + 2];
+    const uint32_t word = blocks[p + (bit < 16 ? 1 : 0)];
+    const int code = (int)((word >> ((bit & 15u) * 2u)) & 3u) ^ xorc;
+    const bool isn = !ing || ((fl >> bit) & 1u);
+    return !inr ? 5 : (isn ? 4 : code);
+  }
+};
+
+// Register-band fill + endpoint + traceback for one wave of 64 single-gap
+// windows sharing (lband, rband, jl).  The band is bottom-aligned in WMAX
+// register slots: slot s holds diagonal d = s - stop, stop = WMAX - W.
+//
+// Slots above the band (s < stop) are computed like every other slot, which
+// keeps the column body free of control flow, but their nogap score gets a
+// -2^29 bias so nothing they hold can reach the band: the only edge from
+// them into the band is the gap2 chain of the top slot, which then sees a
+// NEG-like value exactly where the reference reads its NEG_INFINITY sentinel
+// (dynprog.c:1501-1506).  Rows <= 0 inside the band need no special case:
+// they start from the column-0 initialisation and only ever read rows above
+// them, so they stay NEG-like, while row 0's gap1 chain reproduces the
+// reference's open + c*extend initialisation exactly (dynprog.c:1464-1475).
+// NEG-like values never compete with reachable ones (SURVEY.md 8(a) a5,
+// "only band cells, sentinels and inits are ever read"); see DESIGN.md.
+template <int WMAX>
+struct RegDirs {
+  const uint32_t* D;
+  int lane, stop, rband;
+  __device__ inline uint32_t operator()(int r, int c) const {
+    const int s = stop + r - c + rband;
+    return (D[((size_t)c * ((WMAX + 7) / 8) + (s >> 3)) * 64 + lane] >> ((s & 7) * 4)) & 0xFu;
+  }
+};
+
+constexpr int ABOVE_BIAS = -(1 << 29);
+
+template <int WMAX, int LOW, int JL>
+__device__ void fill_wave(const gsnapdp_window* __restrict__ Wn, int wi, bool active, int lane,
+                          uint32_t* __restrict__ D, const char* __restrict__ q,
+                          const char* __restrict__ qu, const uint32_t* __restrict__ blocks,
+                          uint64_t nwords, const uint32_t* __restrict__ prof,
+                          gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
+                          const int64_t* __restrict__ op_off) {
+  constexpr int NK = (WMAX + 7) / 8;
+  constexpr int NABOVE = WMAX - LOW;  // slots that can lie above the band in this class
+  int lband, rband, open, ext, L1, L2, qnext, qstep, ptab_off;
+  ColStream cs;
+  {
+    const Lane L = make_lane(Wn[wi]);
+    lband = __builtin_amdgcn_readfirstlane(L.d.lband);  // wave-uniform (bucket key)
+    rband = __builtin_amdgcn_readfirstlane(L.d.rband);
+    open = __builtin_amdgcn_readfirstlane(L.d.open);
+    ext = __builtin_amdgcn_readfirstlane(L.d.ext);
+    L1 = active ? L.d.L1 : 0;
+    L2 = active ? L.d.L2 : 0;
+    qstep = L.qstep;
+    qnext = L.qbase + L.qstep * lband;  // query index of row lband+1 (enters at column 1)
+    ptab_off = L.d.mt * 128;
+    cs.init(L);
+  }
+  const int stop = WMAX - (lband + rband + 1);
+  const int maxL2 = __builtin_amdgcn_readfirstlane(wave_max(L2));
+  const uint32_t* ptab = prof + ptab_off;
+  const int qbase0 = qnext - qstep * lband;
+  int bias[NABOVE > 0 ? NABOVE : 1];
+#pragma unroll
+  for (int s = 0; s < NABOVE; s++) bias[s] = __builtin_amdgcn_readfirstlane(s < stop ? ABOVE_BIAS : 0);
+
+  int H[WMAX], E[WMAX], F[WMAX];
+  uint32_t P[WMAX];
+  // column 0 (dynprog.c:1460-1488): slot s holds row r = s - stop - rband
+#pragma unroll
+  for (int s = 0; s < WMAX; s++) {
+    const int r = s - stop - rband;
+    H[s] = (r == 0) ? 0 : NEG;
+    E[s] = NEG;
+    F[s] = (r >= 1) ? open + r * ext : NEG;
+    const bool ld = r >= 1 && r <= L1;
+    P[s] = ptab[ld ? qchar(q, qbase0 + qstep * (r - 1)) : 0];
+  }
+  int fin = NEG;
+  const int se = stop + (L1 - L2 + rband);  // slot of the endpoint (L1,L2)
+
+  for (int c = 1; c <= maxL2; c++) {
+    const uint32_t gsh = 4u * (uint32_t)cs.cls(blocks, nwords, c);
+    // slide the row profiles down one diagonal; row c+lband enters at the bottom
+#pragma unroll
+    for (int s = 0; s < WMAX - 1; s++) P[s] = P[s + 1];
+    P[WMAX - 1] = ptab[(c + lband <= L1) ? qchar(q, qnext) : 0];
+    qnext += qstep;
+    int hp = NEG, fp = NEG;  // new (nogap, gap2) above slot 0: the top sentinel
+    uint32_t acc[NK];
+#pragma unroll
+    for (int k = 0; k < NK; k++) acc[k] = 0u;
+#pragma unroll
+    for (int s = 0; s < WMAX; s++) {
+      const int Hd = H[s], Ed = E[s], Fd = F[s];
+      const int Hr = (s + 1 < WMAX) ? H[(s + 1) % WMAX] : NEG;  // sentinel below the band
+      const int Er = (s + 1 < WMAX) ? E[(s + 1) % WMAX] : NEG;
+      const int a = Hr + open;  // gap1 (dynprog.c:1519-1529)
+      const bool dE = JL ? (Er >= a) : (Er > a);
+      const int e = max(a, Er) + ext;
+      const int b = hp + open;  // gap2 (:1532-1542)
+      const bool dF = JL ? (fp >= b) : (fp > b);
+      const int f = max(b, fp) + ext;
+      const bool h1 = JL ? (Ed >= Hd) : (Ed > Hd);  // nogap (:1545-1561)
+      const int m1 = max(Hd, Ed);
+      const bool v1 = JL ? (Fd >= m1) : (Fd > m1);
+      const int sc = __builtin_amdgcn_sbfe((int)P[s], gsh, 4);
+      const int hn = max(m1, Fd) + sc + (s < NABOVE ? bias[s < NABOVE ? s : 0] : 0);
+      const uint32_t nib = (dE ? 1u : 0u) | (dF ? 2u : 0u) | (v1 ? 8u : (h1 ? 4u : 0u));
+      acc[s / 8] |= nib << (4 * (s % 8));
+      E[s] = e;
+      F[s] = f;
+      H[s] = hn;
+      hp = hn;
+      fp = f;
+    }
+    uint32_t* Dc = D + (size_t)c * NK * 64;
+#pragma unroll
+    for (int k = 0; k < NK; k++) Dc[k * 64 + lane] = acc[k];
+    // endpoint (L1,L2): captured in the column the lane ends (dynprog.c:4545)
+    if (__builtin_amdgcn_ballot_w64(c == L2) != 0) {
+#pragma unroll
+      for (int s = 0; s < WMAX; s++)
+        if (c == L2 && s == se) fin = H[s];
+    }
+  }
+
+  if (!active) return;
+  const gsnapdp_window w = Wn[wi];
+  const Lane L = make_lane(w);
+  RegDirs<WMAX> dirs = {D, lane, stop, rband};
+  Tally t = {0, 0, 0, 0};
+  OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
+  traceback(dirs, L, L1, L2, q, qu, blocks, nwords, prof, t, ow);
+  write_result(res + wi, w, L, fin, L1, L2, t, ow);
+}
+
+// One launch per register class: waves whose band width W is in [LOW, WMAX].
+template <int WMAX, int LOW>
+__global__ __launch_bounds__(256) void k_fill(
+    const gsnapdp_window* __restrict__ Wn, const int* __restrict__ perm,
+    const int* __restrict__ class_range, int cls, const char* __restrict__ q,
+    const char* __restrict__ qu, const uint32_t* __restrict__ blocks, uint64_t nwords,
+    const uint32_t* __restrict__ prof, uint32_t* __restrict__ dirpool, size_t wave_stride,
+    gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
+    const int64_t* __restrict__ op_off) {
+  const int lane = threadIdx.x & 63;
+  const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  const int t0 = class_range[cls], t1 = class_range[cls + 1];
+  uint32_t* D = dirpool + (size_t)gw * wave_stride;
+  for (int t = t0 + gw; t < t1; t += nw) {
+    const int wi0 = perm[(size_t)t * 64 + lane];
+    const int w0 = __builtin_amdgcn_readfirstlane(perm[(size_t)t * 64]);  // lane 0: real window
+    const bool active = wi0 >= 0;
+    const int wi = active ? wi0 : w0;  // idle lanes shadow lane 0 (reads only)
+    const int jl = __builtin_amdgcn_readfirstlane((int)Wn[w0].jump_late_p);
+    if (jl)
+      fill_wave<WMAX, LOW, 1>(Wn, wi, active, lane, D, q, qu, blocks, nwords, prof, res, ops, op_off);
+    else
+      fill_wave<WMAX, LOW, 0>(Wn, wi, active, lane, D, q, qu, blocks, nwords, prof, res, ops, op_off);
+  }
+}
+
+// ------------------------------------------------------------------- k_big
+// Same recurrences, band in per-lane global scratch (any width / length).
+struct BigDirs {
+  const uint32_t* D;
+  int NKd, rband;
+  __device__ inline uint32_t operator()(int r, int c) const {
+    const int d = r - c + rband;
+    return (D[(size_t)c * NKd + (d >> 3)] >> ((d & 7) * 4)) & 0xFu;
+  }
+};
+
+__global__ __launch_bounds__(64) void k_big(
+    const gsnapdp_window* __restrict__ Wn, const int* __restrict__ big_list,
+    const int* __restrict__ big_count, const char* __restrict__ q, const char* __restrict__ qu,
+    const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
+    uint32_t* __restrict__ pool, size_t lane_stride, gsnapdp_result* __restrict__ res,
+    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
+  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nl = gridDim.x * blockDim.x;
+  const int nbig = *big_count;
+  int* S = (int*)(pool + (size_t)gl * lane_stride);
+  for (int j = gl; j < nbig; j += nl) {
+    const int wi = big_list[j];
+    const gsnapdp_window w = Wn[wi];
+    const Lane L = make_lane(w);
+    const int lband = L.d.lband, rband = L.d.rband, Wd = L.d.W;
+    const int L1 = L.d.L1, L2 = L.d.L2;
+    const int NKd = (Wd + 7) / 8;
+    if (Wd > BIG_WMAX || L2 > BIG_L2MAX || L1 > BIG_L1MAX) {
+      gsnapdp_result R = {};
+      R.status = ST_UNSUPPORTED;
+      res[wi] = R;
+      continue;
+    }
+    int* Hs = S;
+    int* Es = Hs + BIG_WMAX;
+    int* Fs = Es + BIG_WMAX;
+    uint32_t* Pr = (uint32_t*)(Fs + BIG_WMAX);           // per row, rows 0..L1
+    uint32_t* D = Pr + (BIG_L1MAX + 1);                  // (L2+1) x NKd
+    const uint32_t* ptab = prof + L.d.mt * 128;
+    const int open = L.d.open, ext = L.d.ext, jl = L.d.jl, mode = L.d.mode, eb = L.d.eb;
+    for (int r = 1; r <= L1; r++) Pr[r] = ptab[qchar(q, L.qbase + L.qstep * (r - 1))];
+    // slot d (0..Wd-1) holds diagonal d: row r = c - rband + d
+    for (int d = 0; d < Wd; d++) {
+      const int r = d - rband;
+      Hs[d] = (r == 0) ? 0 : NEG;
+      Es[d] = NEG;
+      Fs[d] = (r >= 1) ? open + r * ext : NEG;
+    }
+    int fin = NEG, best = (mode == 1) ? 0 : NEG, bkey = 0, bestc2 = 0;
+    for (int c = 1; c <= L2; c++) {
+      const int g = gclass(blocks, nwords, L, L.g0 + L.gstep * (c - 1));
+      const int start = max(0, rband - c);
+      int hp = NEG, fp = NEG;
+      uint32_t acc = 0u;
+      for (int d = start; d < Wd; d++) {
+        const int r = c - rband + d;
+        const int Hd = Hs[d], Ed = Es[d], Fd = Fs[d];
+        const int Hr = (d + 1 < Wd) ? Hs[d + 1] : NEG;
+        const int Er = (d + 1 < Wd) ? Es[d + 1] : NEG;
+        const int a = Hr + open;
+        const bool dE = jl ? (Er >= a) : (Er > a);
+        const int e = max(a, Er) + ext;
+        const int b = hp + open;
+        const bool dF = jl ? (fp >= b) : (fp > b);
+        const int f = max(b, fp) + ext;
+        const bool h1 = jl ? (Ed >= Hd) : (Ed > Hd);
+        const int m1 = max(Hd, Ed);
+        const bool v1 = jl ? (Fd >= m1) : (Fd > m1);
+        const uint32_t pw = (r >= 1 && r <= L1) ? Pr[r] : 0u;
+        const int hn = max(m1, Fd) + __builtin_amdgcn_sbfe((int)pw, 4u * (uint32_t)g, 4);
+        const uint32_t nib = (dE ? 1u : 0u) | (dF ? 2u : 0u) | (v1 ? 8u : (h1 ? 4u : 0u));
+        acc |= nib << (4 * (d & 7));
+        if ((d & 7) == 7 || d == Wd - 1) {
+          D[(size_t)c * NKd + (d >> 3)] = acc;
+          acc = 0u;
+        }
+        Es[d] = e;
+        Fs[d] = f;
+        Hs[d] = hn;
+        hp = hn;
+        fp = f;
+        if (mode == 1 && r >= 1 && r <= L1 && r - c <= eb && c - r <= eb) {
+          const int key = (r << 12) | c;
+          if (hn > best || (hn == best && (jl ? key > bkey : key < bkey))) {
+            best = hn;
+            bkey = key;
+          }
+        }
+        if (mode == 2 && r == L1) {
+          if (hn > best || (jl && hn == best)) {
+            best = hn;
+            bestc2 = c;
+          }
+        }
+        if (mode == 0 && r == L1 && c == L2) fin = hn;
+      }
+    }
+    int r0, c0, score;
+    if (mode == 0) {
+      r0 = L1;
+      c0 = L2;
+      score = fin;
+    } else if (mode == 1) {
+      r0 = bkey >> 12;
+      c0 = bkey & 4095;
+      score = best;
+    } else {
+      r0 = L1;
+      c0 = bestc2;
+      score = best;
+    }
+    BigDirs dirs = {D, NKd, rband};
+    Tally t = {0, 0, 0, 0};
+    OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
+    traceback(dirs, L, r0, c0, q, qu, blocks, nwords, prof, t, ow);
+    write_result(&res[wi], w, L, score, r0, c0, t, ow);
+  }
+}
+
+// --------------------------------------------------------------- k_maxent
+// Maxent_hr_{donor,acceptor,antidonor,antiacceptor}_prob (maxent_hr.c:27217-27390).
+// The reference's 32 shift-specialised handlers all read a k-mer `off` nt past
+// startpos from the 128-bit window (low, high, nextlow, nexthigh).
+__device__ inline uint32_t kmer_at(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int bit) {
+  // bits [bit, bit+32) of the little-endian 128-bit value w0 | w1<<32 | w2<<64 | w3<<96
+  const uint32_t w[5] = {w0, w1, w2, w3, 0u};
+  const int i = bit >> 5, sh = bit & 31;
+  return sh == 0 ? w[i] : ((w[i] >> sh) | (w[i + 1] << (32 - sh)));
+}
+
+__global__ void k_maxent(const uint8_t* __restrict__ model, const uint32_t* __restrict__ pos,
+                         const uint32_t* __restrict__ chroff, double* __restrict__ out, int n,
+                         const uint32_t* __restrict__ blocks, uint64_t nwords,
+                         const double* __restrict__ T) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int m = model[i];
+  const uint32_t sp = pos[i], co = chroff[i];
+  // table offsets (declaration order of maxent_hr.c:25-22606)
+  const double* donor_p = T;
+  const double* donor_di_p = donor_p + 16384;
+  const double* acc1_p = donor_di_p + 16;
+  const double* acc2_p = acc1_p + 16384;
+  const double* acc3_p = acc2_p + 16384;
+  const double* accdi_p = acc3_p + 16384;
+  const double* acc467_p = accdi_p + 16;
+  const double* acc589_p = acc467_p + 16384;
+  const double* donor_m = acc589_p + 16384;
+  const double* donor_di_m = donor_m + 16384;
+  const double* acc1_m = donor_di_m + 16;
+  const double* acc2_m = acc1_m + 16384;
+  const double* acc3_m = acc2_m + 16384;
+  const double* accdi_m = acc3_m + 16384;
+  const double* acc467_m = accdi_m + 16;
+  const double* acc589_m = acc467_m + 16384;
+  const uint32_t margin = (m == 0) ? 3u : (m == 1) ? 20u : (m == 2) ? 6u : 3u;
+  if (sp < co + margin) {
+    out[i] = 0.0;
+    return;
+  }
+  const uint32_t start = sp - margin;
+  const uint64_t ptr = (uint64_t)(start >> 5) * 3u;
+  if (ptr + 4 >= nwords) {  // outside the genome: outside the reference's domain
+    out[i] = 0.0;
+    return;
+  }
+  const uint32_t high = blocks[ptr], low = blocks[ptr + 1];
+  const uint32_t nexthigh = blocks[ptr + 3], nextlow = blocks[ptr + 4];
+  const int b0 = 2 * (int)(start & 31u);
+  auto seq = [&](int off) { return kmer_at(low, high, nextlow, nexthigh, b0 + 2 * off); };
+  double odds;
+  if (m == 0) {
+    const uint32_t s = seq(0);
+    odds = donor_p[(s & 0x3Fu) | ((s >> 4) & 0x3FC0u)] * donor_di_p[(s >> 6) & 0xFu];
+  } else if (m == 2) {
+    const uint32_t s = seq(0);
+    odds = donor_m[(s & 0xFFu) | ((s >> 4) & 0x3F00u)] * donor_di_m[(s >> 8) & 0xFu];
+  } else if (m == 1) {
+    odds = acc1_p[seq(0) & 0x3FFFu];
+    odds = __dmul_rn(odds, acc2_p[seq(7) & 0x3FFFu]);
+    const uint32_t s = seq(14);
+    odds = __dmul_rn(odds, acc3_p[(s & 0xFFu) | ((s >> 4) & 0x3F00u)]);
+    odds = __dmul_rn(odds, accdi_p[(s >> 8) & 0xFu]);
+    odds = __dmul_rn(odds, acc467_p[seq(4) & 0x3FFFu]);
+    odds = __dmul_rn(odds, acc589_p[seq(11) & 0x3FFFu]);
+  } else {
+    odds = acc1_m[seq(16) & 0x3FFFu];
+    odds = __dmul_rn(odds, acc2_m[seq(9) & 0x3FFFu]);
+    const uint32_t s = seq(0);
+    odds = __dmul_rn(odds, acc3_m[(s & 0x3Fu) | ((s >> 4) & 0x3FC0u)]);
+    odds = __dmul_rn(odds, accdi_m[(s >> 6) & 0xFu]);
+    odds = __dmul_rn(odds, acc467_m[seq(12) & 0x3FFFu]);
+    odds = __dmul_rn(odds, acc589_m[seq(5) & 0x3FFFu]);
+  }
+  out[i] = __ddiv_rn(odds, __dadd_rn(1.0, odds));
+}
+
+}  // namespace
+
+// ======================================================================
+// Host side: context and the C-ABI of include/gsnapdp.h
+// ======================================================================
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+static thread_local std::string g_err;
+static void set_err(const std::string& s) { g_err = s; }
+
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      set_err(std::string(#x) + ": " + hipGetErrorString(e_));                           \
+      return -1;                                                                         \
+    }                                                                                    \
+  } while (0)
+
+struct gsnapdp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  const uint32_t* h_blocks = nullptr;
+  size_t nwords = 0;
+  uint32_t* d_blocks = nullptr;
+  int mode = 0;
+  uint32_t h_prof[4 * 128];
+  uint32_t* d_prof = nullptr;
+  double* d_tables = nullptr;
+  size_t ntables = 0;
+  // per-run scratch
+  int cap_n = 0;
+  int* d_keys = nullptr;
+  int* d_perm = nullptr;
+  int* d_big_list = nullptr;
+  int* d_small = nullptr;  // hist[NKEYS] | cursor[NKEYS] | class_range[NCLASS+1] | big_count
+  size_t perm_cap = 0;
+  uint32_t* d_dirpool = nullptr;
+  size_t dirpool_waves = 0;
+  uint32_t* d_bigpool = nullptr;
+  // host-run staging
+  size_t stage_cap = 0;
+  void* d_stage = nullptr;
+  std::string arch;
+  std::mutex mu;
+  int fill_waves = 0;  // waves launched per k_fill class kernel
+};
+
+static const size_t WAVE_STRIDE_DW = (size_t)(FAST_L2MAX + 1) * (FAST_WMAX / 8) * 64;
+static const size_t BIG_LANE_STRIDE_DW =
+    (size_t)3 * BIG_WMAX + (BIG_L1MAX + 1) + (size_t)(BIG_L2MAX + 1) * (BIG_WMAX / 8) + 64;
+
+extern "C" const char* gsnapdp_last_error(void) { return g_err.c_str(); }
+
+extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_t nwords,
+                                        int mode) {
+  gsnapdp_ctx* ctx = new gsnapdp_ctx();
+  ctx->device = device;
+  ctx->h_blocks = blocks;
+  ctx->nwords = nwords;
+  ctx->mode = mode;
+  auto fail = [&](const char* what, hipError_t e) -> gsnapdp_ctx* {
+    set_err(std::string(what) + ": " + hipGetErrorString(e));
+    delete ctx;
+    return nullptr;
+  };
+  hipError_t e;
+  if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
+  hipDeviceProp_t prop;
+  if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return fail("props", e);
+  ctx->arch = prop.gcnArchName;
+  if (ctx->arch.find("gfx950") == std::string::npos) {
+    set_err("gsnapdp is built for gfx950 only; device is " + ctx->arch);
+    delete ctx;
+    return nullptr;
+  }
+  ctx->fill_waves = prop.multiProcessorCount * 8;
+  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
+    return fail("stream", e);
+  if ((e = hipMalloc(&ctx->d_blocks, (nwords + 8) * 4)) != hipSuccess) return fail("malloc blocks", e);
+  if ((e = hipMemset(ctx->d_blocks, 0xFF, (nwords + 8) * 4)) != hipSuccess) return fail("memset", e);
+  if ((e = hipMemcpy(ctx->d_blocks, blocks, nwords * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    return fail("copy blocks", e);
+  build_profile_table(mode, ctx->h_prof);
+  if ((e = hipMalloc(&ctx->d_prof, sizeof(ctx->h_prof))) != hipSuccess) return fail("malloc prof", e);
+  if ((e = hipMemcpy(ctx->d_prof, ctx->h_prof, sizeof(ctx->h_prof), hipMemcpyHostToDevice)) !=
+      hipSuccess)
+    return fail("copy prof", e);
+  const size_t small = (size_t)2 * NKEYS + NCLASS + 1 + 1 + 64;
+  if ((e = hipMalloc(&ctx->d_small, small * 4)) != hipSuccess) return fail("malloc small", e);
+  ctx->dirpool_waves = (size_t)ctx->fill_waves;
+  if ((e = hipMalloc(&ctx->d_dirpool, ctx->dirpool_waves * WAVE_STRIDE_DW * 4)) != hipSuccess)
+    return fail("malloc dirpool", e);
+  if ((e = hipMalloc(&ctx->d_bigpool, (size_t)BIG_LANES * BIG_LANE_STRIDE_DW * 4)) != hipSuccess)
+    return fail("malloc bigpool", e);
+  return ctx;
+}
+
+extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipFree(ctx->d_blocks);
+  hipFree(ctx->d_prof);
+  hipFree(ctx->d_tables);
+  hipFree(ctx->d_keys);
+  hipFree(ctx->d_perm);
+  hipFree(ctx->d_big_list);
+  hipFree(ctx->d_small);
+  hipFree(ctx->d_dirpool);
+  hipFree(ctx->d_bigpool);
+  hipFree(ctx->d_stage);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+extern "C" const char* gsnapdp_device_arch(gsnapdp_ctx* ctx) { return ctx ? ctx->arch.c_str() : ""; }
+
+extern "C" int gsnapdp_sync(gsnapdp_ctx* ctx) {
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+extern "C" size_t gsnapdp_scratch_bytes(gsnapdp_ctx* ctx, int n, int max_length1, int max_length2) {
+  (void)max_length1;
+  (void)max_length2;
+  const size_t waves = (size_t)n / 64 + NKEYS;
+  return (size_t)n * 8 + waves * 64 * 4 + (ctx ? ctx->dirpool_waves : 0) * WAVE_STRIDE_DW * 4 +
+         (size_t)BIG_LANES * BIG_LANE_STRIDE_DW * 4;
+}
+
+static int ensure_capacity(gsnapdp_ctx* ctx, int n) {
+  if (n <= ctx->cap_n) return 0;
+  int cap = n + n / 4 + 1024;
+  hipFree(ctx->d_keys);
+  hipFree(ctx->d_perm);
+  hipFree(ctx->d_big_list);
+  HIPCHK(hipMalloc(&ctx->d_keys, (size_t)cap * 4));
+  HIPCHK(hipMalloc(&ctx->d_big_list, (size_t)cap * 4));
+  // perm: every bucket padded to a whole wave
+  ctx->perm_cap = ((size_t)cap + (size_t)NKEYS * 64 + 63) & ~(size_t)63;
+  HIPCHK(hipMalloc(&ctx->d_perm, ctx->perm_cap * 4));
+  ctx->cap_n = cap;
+  return 0;
+}
+
+extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_windows, int n,
+                                  const char* d_query, const char* d_query_uc,
+                                  gsnapdp_result* d_results, uint32_t* d_ops,
+                                  const int64_t* d_op_offsets, void* stream_v) {
+  if (!ctx) return -1;
+  if (n <= 0) return 0;
+  hipStream_t st = stream_v ? (hipStream_t)stream_v : ctx->stream;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  if (ensure_capacity(ctx, n)) return -1;
+  int* hist = ctx->d_small;
+  int* cursor = hist + NKEYS;
+  int* class_range = cursor + NKEYS;
+  int* big_count = class_range + NCLASS + 1;
+  HIPCHK(hipMemsetAsync(hist, 0, (size_t)NKEYS * 4, st));
+  HIPCHK(hipMemsetAsync(big_count, 0, 4, st));
+  // perm padding entries must read -1; only the used prefix matters
+  const size_t used = ((size_t)n + (size_t)NKEYS * 64 + 63) & ~(size_t)63;
+  HIPCHK(hipMemsetAsync(ctx->d_perm, 0xFF, (used < ctx->perm_cap ? used : ctx->perm_cap) * 4, st));
+  const int tb = 256, nb = (n + tb - 1) / tb;
+  hipLaunchKernelGGL(k_plan, dim3(nb), dim3(tb), 0, st, d_windows, n, d_query, d_query_uc,
+                     ctx->d_blocks, (uint64_t)ctx->nwords, ctx->d_prof, d_results, d_ops,
+                     d_op_offsets, ctx->d_keys, hist, ctx->d_big_list, big_count);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, hist, cursor, class_range);
+  hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(tb), 0, st, ctx->d_keys, n, cursor, ctx->d_perm);
+  const int blocks = (int)(ctx->dirpool_waves / 4);
+  const uint64_t nw = (uint64_t)ctx->nwords;
+#define LAUNCH_FILL(WM, LO, CLS)                                                                \
+  hipLaunchKernelGGL((k_fill<WM, LO>), dim3(blocks), dim3(256), 0, st, d_windows, ctx->d_perm, \
+                     class_range, CLS, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,    \
+                     ctx->d_dirpool, WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets)
+  LAUNCH_FILL(8, 1, 0);
+  LAUNCH_FILL(16, 9, 1);
+  LAUNCH_FILL(24, 17, 2);
+  LAUNCH_FILL(28, 25, 3);
+  LAUNCH_FILL(32, 29, 4);
+  LAUNCH_FILL(36, 33, 5);
+  LAUNCH_FILL(40, 37, 6);
+  LAUNCH_FILL(44, 41, 7);
+  LAUNCH_FILL(48, 45, 8);
+#undef LAUNCH_FILL
+  hipLaunchKernelGGL(k_big, dim3(BIG_LANES / 64), dim3(64), 0, st, d_windows, ctx->d_big_list,
+                     big_count, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
+                     ctx->d_bigpool, BIG_LANE_STRIDE_DW, d_results, d_ops, d_op_offsets);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows, int n,
+                                const char* query, const char* query_uc, size_t query_bytes,
+                                gsnapdp_result* results, uint32_t* ops,
+                                const int64_t* op_offsets) {
+  if (!ctx) return -1;
+  if (n <= 0) return 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t nops = (size_t)op_offsets[n];
+  const size_t szw = (size_t)n * sizeof(gsnapdp_window);
+  const size_t szq = (query_bytes + 255) & ~(size_t)255;
+  const size_t szr = (size_t)n * sizeof(gsnapdp_result);
+  const size_t szo = (nops + 1) * 4;
+  const size_t szoff = (size_t)(n + 1) * 8;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t total = al(szw) + 2 * al(szq) + al(szr) + al(szo) + al(szoff);
+  {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (total > ctx->stage_cap) {
+      hipFree(ctx->d_stage);
+      ctx->d_stage = nullptr;
+      HIPCHK(hipMalloc(&ctx->d_stage, total));
+      ctx->stage_cap = total;
+    }
+  }
+  char* base = (char*)ctx->d_stage;
+  gsnapdp_window* dw = (gsnapdp_window*)base;
+  char* dq = base + al(szw);
+  char* du = dq + al(szq);
+  gsnapdp_result* dr = (gsnapdp_result*)(du + al(szq));
+  uint32_t* dops = (uint32_t*)((char*)dr + al(szr));
+  int64_t* doff = (int64_t*)((char*)dops + al(szo));
+  hipStream_t st = ctx->stream;
+  HIPCHK(hipMemcpyAsync(dw, windows, szw, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(dq, query, query_bytes, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(doff, op_offsets, szoff, hipMemcpyHostToDevice, st));
+  if (gsnapdp_run_device(ctx, dw, n, dq, du, dr, dops, doff, st)) return -1;
+  HIPCHK(hipMemcpyAsync(results, dr, szr, hipMemcpyDeviceToHost, st));
+  if (nops) HIPCHK(hipMemcpyAsync(ops, dops, nops * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
+extern "C" int gsnapdp_load_maxent_tables(gsnapdp_ctx* ctx, const double* tables, size_t nd) {
+  if (!ctx) return -1;
+  if (nd != (size_t)12 * 16384 + 4 * 16) {
+    set_err("maxent tables: expected 196672 doubles");
+    return -1;
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  if (!ctx->d_tables) HIPCHK(hipMalloc(&ctx->d_tables, nd * 8));
+  HIPCHK(hipMemcpy(ctx->d_tables, tables, nd * 8, hipMemcpyHostToDevice));
+  ctx->ntables = nd;
+  return 0;
+}
+
+extern "C" int gsnapdp_maxent_device(gsnapdp_ctx* ctx, const uint8_t* d_model,
+                                     const uint32_t* d_pos, const uint32_t* d_chroff,
+                                     double* d_out, int n, void* stream_v) {
+  if (!ctx || !ctx->d_tables) {
+    set_err("maxent tables not loaded");
+    return -1;
+  }
+  if (n <= 0) return 0;
+  hipStream_t st = stream_v ? (hipStream_t)stream_v : ctx->stream;
+  hipLaunchKernelGGL(k_maxent, dim3((n + 255) / 256), dim3(256), 0, st, d_model, d_pos, d_chroff,
+                     d_out, n, ctx->d_blocks, (uint64_t)ctx->nwords, ctx->d_tables);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int gsnapdp_maxent_host(gsnapdp_ctx* ctx, const uint8_t* model, const uint32_t* pos,
+                                   const uint32_t* chroff, double* out, int n) {
+  if (!ctx) return -1;
+  if (n <= 0) return 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  uint8_t* dm;
+  uint32_t *dp, *dc;
+  double* dout;
+  HIPCHK(hipMalloc(&dm, (size_t)n));
+  HIPCHK(hipMalloc(&dp, (size_t)n * 4));
+  HIPCHK(hipMalloc(&dc, (size_t)n * 4));
+  HIPCHK(hipMalloc(&dout, (size_t)n * 8));
+  HIPCHK(hipMemcpy(dm, model, (size_t)n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dp, pos, (size_t)n * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dc, chroff, (size_t)n * 4, hipMemcpyHostToDevice));
+  int rc = gsnapdp_maxent_device(ctx, dm, dp, dc, dout, n, ctx->stream);
+  if (rc == 0) {
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost));
+  }
+  hipFree(dm);
+  hipFree(dp);
+  hipFree(dc);
+  hipFree(dout);
+  return rc;
+}
+
+// exposed for gsnapdp_host.cpp (expansion needs the host genome and tables)
+extern "C" const uint32_t* gsnapdp__host_blocks(gsnapdp_ctx* ctx) { return ctx->h_blocks; }
+extern "C" size_t gsnapdp__host_nwords(gsnapdp_ctx* ctx) { return ctx->nwords; }
+extern "C" const uint32_t* gsnapdp__host_prof(gsnapdp_ctx* ctx) { return ctx->h_prof; }

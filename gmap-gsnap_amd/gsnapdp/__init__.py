@@ -1,0 +1,180 @@
+"""Host-side mirror of GMAP/GSNAP's stage-3 DP interface over the MI355X C-ABI.
+
+The native library ``gmap-gsnap_amd/lib/libgsnapdp.so`` (HIP kernels for
+gfx950 + the C-ABI of include/gsnapdp.h) is the product; this module is a thin
+ctypes binding used by tests and bench.py.  There is no CPU fallback: if the
+library or a gfx950 device is missing, ``Context`` raises.
+
+Entry-point mapping (reference src/dynprog.c):
+    Context.run(batch)           Dynprog_single_gap / Dynprog_end5_gap / Dynprog_end3_gap
+                                 (batched; one gsnapdp_window per call)
+    Context.pairs(batch, i, ...) the List_T of Pair_T the call returns
+    Context.maxent(...)          Maxent_hr_{donor,acceptor,antidonor,antiacceptor}_prob
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .records import MAXENT_IN, PAIR, RESULT, WINDOW  # noqa: F401
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG, "lib", "libgsnapdp.so")
+TABLES_PATH = os.path.join(PKG, "data", "maxent_hr_tables.bin")
+
+_lib = None
+
+
+class GsnapdpError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the native library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise GsnapdpError("native library missing: %s (run `make -C gmap-gsnap_amd`)" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        L.gsnapdp_create.argtypes = [i32, vp, sz, i32]
+        L.gsnapdp_create.restype = vp
+        L.gsnapdp_destroy.argtypes = [vp]
+        L.gsnapdp_last_error.restype = ctypes.c_char_p
+        L.gsnapdp_device_arch.argtypes = [vp]
+        L.gsnapdp_device_arch.restype = ctypes.c_char_p
+        L.gsnapdp_run_host.argtypes = [vp, vp, i32, vp, vp, sz, vp, vp, vp]
+        L.gsnapdp_run_host.restype = i32
+        L.gsnapdp_run_device.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp]
+        L.gsnapdp_run_device.restype = i32
+        L.gsnapdp_sync.argtypes = [vp]
+        L.gsnapdp_sync.restype = i32
+        L.gsnapdp_expand.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, vp]
+        L.gsnapdp_expand.restype = i32
+        L.gsnapdp_load_maxent_tables.argtypes = [vp, vp, sz]
+        L.gsnapdp_load_maxent_tables.restype = i32
+        L.gsnapdp_maxent_host.argtypes = [vp, vp, vp, vp, vp, i32]
+        L.gsnapdp_maxent_host.restype = i32
+        L.gsnapdp_maxent_device.argtypes = [vp, vp, vp, vp, vp, i32, vp]
+        L.gsnapdp_maxent_device.restype = i32
+        L.gsnapdp_scratch_bytes.argtypes = [vp, i32, i32, i32]
+        L.gsnapdp_scratch_bytes.restype = sz
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def op_offsets(windows: np.ndarray) -> np.ndarray:
+    """Per-window op capacity: a traceback takes at most L1 + L2 steps and
+    every op consumes at least one step."""
+    cap = windows["length1"].astype(np.int64).clip(0) + windows["length2"].astype(np.int64).clip(0) + 2
+    off = np.zeros(len(windows) + 1, dtype=np.int64)
+    np.cumsum(cap, out=off[1:])
+    return off
+
+
+class Context:
+    """A device context: packed genome resident in HBM (Genome_user_setup +
+    Maxent_hr_setup) and the substitution tables of Dynprog_init(mode)."""
+
+    def __init__(self, blocks: np.ndarray, mode: int = 0, device: int = 0, maxent_tables=None):
+        L = lib()
+        self._blocks = np.ascontiguousarray(blocks, dtype=np.uint32)
+        h = L.gsnapdp_create(device, _p(self._blocks), self._blocks.size, mode)
+        if not h:
+            raise GsnapdpError("gsnapdp_create failed: %s" % L.gsnapdp_last_error().decode())
+        self.h = ctypes.c_void_p(h)
+        self.mode = mode
+        if maxent_tables is None and os.path.exists(TABLES_PATH):
+            maxent_tables = np.fromfile(TABLES_PATH, dtype="<f8")
+        if maxent_tables is not None:
+            t = np.ascontiguousarray(maxent_tables, dtype="<f8")
+            if L.gsnapdp_load_maxent_tables(self.h, _p(t), t.size) != 0:
+                raise GsnapdpError(L.gsnapdp_last_error().decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().gsnapdp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def arch(self) -> str:
+        return lib().gsnapdp_device_arch(self.h).decode()
+
+    def run(self, windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray):
+        """Fill + endpoint + traceback on the GPU.  Returns (results, ops, op_offsets)."""
+        w = np.ascontiguousarray(windows, dtype=WINDOW)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        off = op_offsets(w)
+        res = np.zeros(len(w), dtype=RESULT)
+        ops = np.zeros(max(1, int(off[-1])), dtype=np.uint32)
+        rc = lib().gsnapdp_run_host(self.h, _p(w), len(w), _p(q), _p(u), q.size, _p(res), _p(ops), _p(off))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_run_host: %s" % lib().gsnapdp_last_error().decode())
+        return res, ops, off
+
+    def pairs(self, windows, query, query_uc, results, ops, off, i: int) -> tuple[np.ndarray, int]:
+        """The pair list window i's reference call returns (gsnapdp_expand)."""
+        w = np.ascontiguousarray(windows[i:i + 1], dtype=WINDOW)
+        r = np.ascontiguousarray(results[i:i + 1], dtype=RESULT)
+        cap = int(w["length1"][0]) + int(w["length2"][0]) + 8
+        out = np.zeros(cap, dtype=PAIR)
+        fs = np.zeros(1, dtype=np.int32)
+        o = ops[off[i]:]
+        n = lib().gsnapdp_expand(self.h, _p(w), _p(r), _p(o), _p(query), _p(query_uc), _p(out), cap, _p(fs))
+        if n < 0:
+            raise GsnapdpError("gsnapdp_expand failed for window %d" % i)
+        return out[:n], int(fs[0])
+
+    def all_pairs(self, windows, query, query_uc, results, ops, off):
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        outs, counts = [], np.zeros(len(windows), dtype=np.int32)
+        for i in range(len(windows)):
+            p, _ = self.pairs(windows, q, u, results, ops, off, i)
+            outs.append(p)
+            counts[i] = p.size
+        return (np.concatenate(outs) if outs else np.zeros(0, PAIR)), counts
+
+    def run_device(self, d_windows: int, n: int, d_query: int, d_query_uc: int, d_results: int,
+                   d_ops: int, d_op_offsets: int, stream: int = 0) -> None:
+        """Device-resident batch (raw device pointers, e.g. torch tensor.data_ptr())."""
+        rc = lib().gsnapdp_run_device(self.h, ctypes.c_void_p(d_windows), n, ctypes.c_void_p(d_query),
+                                      ctypes.c_void_p(d_query_uc), ctypes.c_void_p(d_results),
+                                      ctypes.c_void_p(d_ops), ctypes.c_void_p(d_op_offsets),
+                                      ctypes.c_void_p(stream) if stream else None)
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_run_device: %s" % lib().gsnapdp_last_error().decode())
+
+    def sync(self):
+        if lib().gsnapdp_sync(self.h) != 0:
+            raise GsnapdpError(lib().gsnapdp_last_error().decode())
+
+    def maxent(self, model: np.ndarray, pos: np.ndarray, chroffset: np.ndarray) -> np.ndarray:
+        m = np.ascontiguousarray(model, dtype=np.uint8)
+        p = np.ascontiguousarray(pos, dtype=np.uint32)
+        c = np.ascontiguousarray(chroffset, dtype=np.uint32)
+        out = np.zeros(m.size, dtype=np.float64)
+        if lib().gsnapdp_maxent_host(self.h, _p(m), _p(p), _p(c), _p(out), m.size) != 0:
+            raise GsnapdpError("maxent: %s" % lib().gsnapdp_last_error().decode())
+        return out
+
+    def maxent_device(self, d_model: int, d_pos: int, d_chroff: int, d_out: int, n: int, stream: int = 0):
+        rc = lib().gsnapdp_maxent_device(self.h, ctypes.c_void_p(d_model), ctypes.c_void_p(d_pos),
+                                         ctypes.c_void_p(d_chroff), ctypes.c_void_p(d_out), n,
+                                         ctypes.c_void_p(stream) if stream else None)
+        if rc != 0:
+            raise GsnapdpError("maxent_device: %s" % lib().gsnapdp_last_error().decode())

@@ -73,7 +73,7 @@ def c2_windows(gseq: np.ndarray, n: int = 100_000, seed: int = 2, read_len: int 
     rng = np.random.default_rng(seed)
     G = gseq.size
     w = np.zeros(n, dtype=WINDOW)
-    qbuf = np.empty(n * (read_len + 8), dtype=np.uint8)
+    qbuf = np.full(n * (read_len + 8), ord("#"), dtype=np.uint8)
     qpos = 0
     has_indel = rng.random(n) < indel_frac
     indel_len = rng.integers(1, 4, size=n)

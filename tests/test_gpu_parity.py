@@ -1,0 +1,94 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden
+vectors and against the CPU restatement (which the golden vectors pin)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from gsnapdp import Context
+from gsnapdp import workload as W
+from gsnapdp.records import PAIR
+
+pytestmark = pytest.mark.gpu
+
+DP_CASES = ["dp_chr17_mix", "dp_synth_mix", "dp_synth_cmet", "dp_chr17_c2", "dp_synth_long"]
+
+
+def load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+
+
+def compare(res, gpu_pairs, gpu_np, ref_scores, ref_pairs, ref_np, what):
+    for f in ("finalscore", "nmatches", "nmismatches", "nopens", "nindels"):
+        bad = np.nonzero(res[f] != ref_scores[f])[0]
+        assert bad.size == 0, "%s: %s differs at windows %s (gpu %s ref %s)" % (
+            what, f, bad[:8], res[f][bad[:8]], ref_scores[f][bad[:8]])
+    bad = np.nonzero(res["reserved"] != ref_scores["dynprogindex"])[0]
+    assert bad.size == 0, "%s: dynprogindex differs at %s" % (what, bad[:8])
+    bad = np.nonzero(gpu_np != ref_np)[0]
+    assert bad.size == 0, "%s: list length differs at windows %s (gpu %s ref %s)" % (
+        what, bad[:8], gpu_np[bad[:8]], ref_np[bad[:8]])
+    for f in PAIR.names:
+        bad = np.nonzero(gpu_pairs[f] != ref_pairs[f])[0]
+        assert bad.size == 0, "%s: pair field %s differs at pair %s" % (what, f, bad[:8])
+
+
+@pytest.mark.parametrize("name", DP_CASES)
+def test_gpu_matches_reference_golden(golden_dir, name):
+    z = load(golden_dir, name)
+    ctx = Context(z["blocks"], mode=int(z["mode"]))
+    assert "gfx950" in ctx.arch
+    res, ops, off = ctx.run(z["windows"], z["query"], z["query_uc"])
+    assert np.all(res["status"] != 2), "op stream overflow"
+    pairs, npairs = ctx.all_pairs(z["windows"], z["query"], z["query_uc"], res, ops, off)
+    ref = {f: z[f] for f in ("finalscore", "nmatches", "nmismatches", "nopens", "nindels", "dynprogindex")}
+    compare(res, pairs, npairs, ref, z["pairs"], z["npairs"], name)
+
+
+def run_both(blocks, batch, mode=0, threads=16):
+    ctx = Context(blocks, mode=mode)
+    res, ops, off = ctx.run(batch.windows, batch.query, batch.query_uc)
+    pairs, npairs = ctx.all_pairs(batch.windows, batch.query, batch.query_uc, res, ops, off)
+    O.setup(blocks, mode=mode)
+    ores, opairs, ooff, onp = O.run_batch(batch.windows, batch.query, batch.query_uc, nthreads=threads)
+    oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
+    ref = {f: ores[f] for f in ("finalscore", "nmatches", "nmismatches", "nopens", "nindels")}
+    ref["dynprogindex"] = ores["reserved"]
+    return res, pairs, npairs, ref, oflat, onp
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_gpu_matches_oracle_random(seed):
+    g = W.synthetic_genome(2_000_000, seed=100 + seed, n_rate=0.002)
+    blocks = W.pack_genome(g)
+    batch = W.random_windows(g, 6000, seed=seed, max_len1=120, max_len2=140, max_band=20)
+    res, pairs, npairs, ref, oflat, onp = run_both(blocks, batch)
+    compare(res, pairs, npairs, ref, oflat, onp, "random seed %d" % seed)
+
+
+def test_gpu_matches_oracle_wide_and_long():
+    g = W.synthetic_genome(1_000_000, seed=7, n_rate=0.002)
+    blocks = W.pack_genome(g)
+    batch = W.random_windows(g, 400, seed=9, max_len1=700, max_len2=900, max_band=60)
+    res, pairs, npairs, ref, oflat, onp = run_both(blocks, batch)
+    compare(res, pairs, npairs, ref, oflat, onp, "wide/long")
+
+
+def test_gpu_c2_full_size_parity():
+    """BASELINE config 2 at full size: 100k x 150 bp, band 31, bit-exact."""
+    g = W.synthetic_genome(64_000_000, seed=1)
+    blocks = W.pack_genome(g)
+    batch = W.c2_windows(g, n=100_000, seed=2)
+    res, pairs, npairs, ref, oflat, onp = run_both(blocks, batch, threads=32)
+    compare(res, pairs, npairs, ref, oflat, onp, "C2 100k")
+
+
+@pytest.mark.parametrize("name", ["maxent_chr17", "maxent_synth"])
+def test_gpu_maxent_matches_reference(golden_dir, name):
+    z = load(golden_dir, name)
+    ctx = Context(z["blocks"])
+    got = ctx.maxent(z["model"], z["splice_pos"], z["chroffset"])
+    ref = z["prob"]
+    bad = np.nonzero(got.view(np.uint64) != ref.view(np.uint64))[0]
+    assert bad.size == 0, "maxent differs at %s" % bad[:10]
