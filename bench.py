@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Benchmark: GMAP/GSNAP stage-3 single-gap DP on MI355X (BASELINE config 2).
+
+One step = one pass of the hot path (Dynprog_single_gap fill + endpoint +
+traceback, batched through gsnapdp_run_device) over one batch of 100k
+synthetic 150 bp reads (band 31, 2 % substitutions, 30 % with a 1-3 bp indel)
+already resident in HBM.  N GPUs: one process per GPU, each aligning its own
+100k-read shard against a replicated genome (weak scaling, no data-path
+collective: windows are independent).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1 under torch.distributed.run, see the task contract)
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
+
+import torch  # noqa: E402
+
+from gsnapdp import Context, op_offsets  # noqa: E402
+from gsnapdp import workload as W  # noqa: E402
+from gsnapdp.records import RESULT  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+VALU_INT32_PEAK = 256 * 64 * 2.4e9  # 256 CU x 64 int32 lane-ops/clk x 2.4 GHz
+OPS_PER_CELL = 14             # gap1 4 + gap2 4 + nogap 6 int32 ops
+READS_PER_GPU = 100_000
+GENOME_NT = 64_000_000
+DOMINANT = "k_fill<32,29>"    # band width 31..32: 70 % of C2 windows
+
+
+def window_bytes(w: np.ndarray, nops: np.ndarray) -> np.ndarray:
+    """Algorithmic HBM bytes of one window (DESIGN.md "Roofline"): query and
+    uppercase query (L1 each), the packed genome blocks its columns touch
+    (12 B per 32 nt), the 68 B descriptor, the 48 B result and 4 B per op."""
+    span_blocks = (w["length2"].astype(np.int64) + 31) // 32 + 1
+    return (2 * w["length1"].astype(np.int64) + 12 * span_blocks + 68 + 48 + 4 * nops.astype(np.int64))
+
+
+def band_cells(w: np.ndarray) -> int:
+    """Exact in-band cell count of the widened band (dynprog.c:1442-1516)."""
+    L1 = w["length1"].astype(np.int64)
+    L2 = w["length2"].astype(np.int64)
+    eb = w["extraband"].astype(np.int64)
+    rband = np.where(L2 >= L1, L2 - L1 + eb, eb)
+    lband = np.where(L2 >= L1, eb, L1 - L2 + eb)
+    total = 0
+    for c in range(1, int(L2.max()) + 1):
+        lo = np.maximum(1, c - rband)
+        hi = np.minimum(L1, c + lband)
+        total += int(np.where(c <= L2, np.clip(hi - lo + 1, 0, None), 0).sum())
+    return total
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--reads", type=int, default=READS_PER_GPU)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    # ---- workload (identical genome on every rank, a disjoint read shard per rank)
+    genome = W.synthetic_genome(GENOME_NT, seed=1)
+    blocks = W.pack_genome(genome)
+    batch = W.c2_windows(genome, n=args.reads, seed=2 + rank)
+    n = len(batch)
+    off = op_offsets(batch.windows)
+    ctx = Context(blocks, mode=0, device=local)
+
+    d_w = torch.from_numpy(batch.windows.view(np.uint8).copy()).to(dev)
+    d_q = torch.from_numpy(batch.query.copy()).to(dev)
+    d_u = torch.from_numpy(batch.query_uc.copy()).to(dev)
+    d_off = torch.from_numpy(off.copy()).to(dev)
+    d_res = torch.zeros(n * RESULT.itemsize, dtype=torch.uint8, device=dev)
+    d_ops = torch.zeros(int(off[-1]) + 1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        ctx.run_device(d_w.data_ptr(), n, d_q.data_ptr(), d_u.data_ptr(), d_res.data_ptr(),
+                       d_ops.data_ptr(), d_off.data_ptr())
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+
+    # ---- timed region: exactly K steps, barrier + sync on both sides
+    barrier()
+    ctx.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = world * n * args.steps / elapsed
+
+    # ---- per-kernel durations (HIP events on the launch stream), same K steps
+    names = ctx.profile(True)
+    acc = np.zeros(len(names), dtype=np.float64)
+    for _ in range(args.steps):
+        step()
+        ctx.profile_read(acc)
+    ctx.profile(False)
+    kernel_ms = {nm: acc[i] / args.steps for i, nm in enumerate(names) if acc[i] > 0}
+
+    # ---- results of the last step: sanity + algorithmic bytes
+    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=RESULT)
+    Wd = (batch.windows["extraband"].astype(np.int64) * 2 + 1
+          + np.abs(batch.windows["length2"].astype(np.int64) - batch.windows["length1"]))
+    dom = (Wd >= 29) & (Wd <= 32)
+    dom_bytes = float(window_bytes(batch.windows[dom], res["nops"][dom]).sum())
+    dom_ms = kernel_ms.get(DOMINANT, float("nan"))
+    achieved_gbs = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms == dom_ms else None
+    cells = band_cells(batch.windows)
+    fill_ms = sum(v for k, v in kernel_ms.items() if k.startswith("k_fill"))
+
+    out = None
+    if rank == 0:
+        cpu = None
+        parity = None
+        if not args.no_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O  # CPU restatement: baseline + checker only
+            O.setup(blocks)
+            cores = 16
+            sample = min(n, 100_000)
+            ws = batch.windows[:sample]
+            t1 = time.perf_counter()
+            reps = 0
+            while True:
+                ores, _, _, _ = O.run_batch(ws, batch.query, batch.query_uc, nthreads=cores)
+                reps += 1
+                if time.perf_counter() - t1 > 3.0:
+                    break
+            cpu_rate = reps * sample / (time.perf_counter() - t1)
+            t2 = time.perf_counter()
+            O.run_batch(ws[:10_000], batch.query, batch.query_uc, nthreads=1)
+            cpu1 = 10_000 / (time.perf_counter() - t2)
+            same = all(np.array_equal(res[f][:sample], ores[f]) for f in
+                       ("finalscore", "nmatches", "nmismatches", "nopens", "nindels"))
+            parity = {"windows_checked": sample, "scores_and_counts_bit_exact": bool(same)}
+            cpu = {"value": round(cpu_rate, 1), "unit": "reads/s", "cores": cores, "kind": "port",
+                   "sample": "%d C2 windows x %d passes (oracle/ restatement, pthreads); 1 core: %.0f reads/s"
+                             % (sample, reps, cpu1)}
+        out = {
+            "metric": "aligned reads/sec (whole node), 150 bp vs GRCh38; bit-exact vs CPU dynprog",
+            "value": round(value, 1),
+            "unit": "reads/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (64 Mbp uniform genome with N runs; 150 bp reads, 2% subs, 30% 1-3 bp indels)",
+            "config": {"workload": "C2: Dynprog_single_gap, %d x 150 bp reads per GPU, extraband 15 (band 31), "
+                                   "widebandp, HIGHQ, both strands" % n,
+                       "reads_per_gpu": n, "genome_nt": GENOME_NT, "parallelism": "dp%d" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2) if achieved_gbs else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 5) if achieved_gbs else None,
+                         "traffic": None, "kernel": DOMINANT,
+                         "kernel_ms": round(dom_ms, 4), "windows_in_kernel": int(dom.sum())},
+            "roofline_valu": {"bound": "valu-int32", "unit": "int32 ops/s",
+                              "achieved": round(cells * OPS_PER_CELL / (fill_ms * 1e-3), 1) if fill_ms else None,
+                              "peak": VALU_INT32_PEAK,
+                              "frac": round(cells * OPS_PER_CELL / (fill_ms * 1e-3) / VALU_INT32_PEAK, 4)
+                              if fill_ms else None,
+                              "note": "14 ops per in-band cell over all k_fill launches (SURVEY.md 8(d))"},
+            "kernel_ms_per_step": {k: round(v, 4) for k, v in kernel_ms.items()},
+            "gcups": round(cells * args.steps * world / elapsed / 1e9, 2),
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

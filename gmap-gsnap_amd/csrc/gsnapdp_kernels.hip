@@ -215,6 +215,26 @@ __device__ inline void write_result(gsnapdp_result* res, const gsnapdp_window& w
   *res = R;
 }
 
+// Wave-aggregated "pos = atomicAdd(&counter[key], 1)" for lanes with key >= 0
+// (most lanes of a wave share a key, so one atomic per distinct key per wave).
+// Every lane of the wave must call it.
+__device__ inline int agg_atomic_inc(int* counter, int key) {
+  const int lane = threadIdx.x & 63;
+  int pos = -1;
+  uint64_t todo = __ballot(key >= 0);
+  while (todo) {
+    const int leader = __ffsll((unsigned long long)todo) - 1;
+    const int lkey = __shfl(key, leader);
+    const uint64_t m = __ballot(key == lkey) & todo;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&counter[lkey], __popcll(m));
+    base = __shfl(base, leader);
+    if (key == lkey) pos = base + __popcll(m & ((1ull << lane) - 1ull));
+    todo &= ~m;
+  }
+  return pos;
+}
+
 // ------------------------------------------------------------------ k_plan
 // Early returns, QUERYEND_NOGAPS windows (no fill at all) and bucketing.
 __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* __restrict__ q,
@@ -225,48 +245,46 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
                        int* __restrict__ hist, int* __restrict__ big_list,
                        int* __restrict__ big_count) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const gsnapdp_window w = W[i];
-  const Lane L = make_lane(w);
-  keys[i] = -1;
-  if (L.d.status != ST_OK) {
-    gsnapdp_result R = {};
-    R.finalscore = L.d.early_score;
-    R.status = L.d.status;
-    R.length1 = L.d.L1;
-    R.length2 = L.d.L2;
-    R.reserved = L.d.early_dpi_step ? step_dpi(w.dynprogindex) : w.dynprogindex;
-    res[i] = R;
-    return;
-  }
-  if (L.d.mode == 3) {  // traceback_nogaps (dynprog.c:2815-2872) from (min,min)
-    Tally t = {0, 0, 0, 0};
-    OpWriter ow = {ops + op_off[i], (int)(op_off[i + 1] - op_off[i]), 0, 0};
-    const int m = min(L.d.L1, L.d.L2);
-    const uint32_t* ptab = prof + L.d.mt * 128;
-    for (int r = m, c = m; r > 0 && c > 0; r--, c--) {
-      const int g = gclass(blocks, nwords, L, L.g0 + L.gstep * (c - 1));
-      if (g != 5) {
-        const int qi = L.qbase + L.qstep * (r - 1);
-        const unsigned char c1 = qchar(q, qi);
-        const unsigned char u1 = (unsigned char)qu[qi];
-        if (u1 == (unsigned char)("ACGTN"[g]) || ((ptab[c1] >> (24 + g)) & 1u)) t.nmatches++;
-        else t.nmismatches++;
+  int key = -1, big = -1;
+  if (i < n) {
+    const gsnapdp_window w = W[i];
+    const Lane L = make_lane(w);
+    if (L.d.status != ST_OK) {
+      gsnapdp_result R = {};
+      R.finalscore = L.d.early_score;
+      R.status = L.d.status;
+      R.length1 = L.d.L1;
+      R.length2 = L.d.L2;
+      R.reserved = L.d.early_dpi_step ? step_dpi(w.dynprogindex) : w.dynprogindex;
+      res[i] = R;
+    } else if (L.d.mode == 3) {  // traceback_nogaps (dynprog.c:2815-2872) from (min,min)
+      Tally t = {0, 0, 0, 0};
+      OpWriter ow = {ops + op_off[i], (int)(op_off[i + 1] - op_off[i]), 0, 0};
+      const int m = min(L.d.L1, L.d.L2);
+      const uint32_t* ptab = prof + L.d.mt * 128;
+      for (int r = m, c = m; r > 0 && c > 0; r--, c--) {
+        const int g = gclass(blocks, nwords, L, L.g0 + L.gstep * (c - 1));
+        if (g != 5) {
+          const int qi = L.qbase + L.qstep * (r - 1);
+          const unsigned char c1 = qchar(q, qi);
+          const unsigned char u1 = (unsigned char)qu[qi];
+          if (u1 == (unsigned char)("ACGTN"[g]) || ((ptab[c1] >> (24 + g)) & 1u)) t.nmatches++;
+          else t.nmismatches++;
+        }
+        ow.run++;
       }
-      ow.run++;
+      ow.flush();
+      write_result(&res[i], w, L, 0, m, m, t, ow);
+    } else if (L.d.mode == 0 && L.d.W <= FAST_WMAX && L.d.L2 <= FAST_L2MAX) {
+      key = ((L.d.W * (FAST_WMAX + 1) + L.d.lband) * 6) + L.d.jl * 3 + L.d.mode;
+    } else {
+      big = 0;
     }
-    ow.flush();
-    write_result(&res[i], w, L, 0, m, m, t, ow);
-    return;
-  }
-  if (L.d.mode == 0 && L.d.W <= FAST_WMAX && L.d.L2 <= FAST_L2MAX) {
-    const int key = ((L.d.W * (FAST_WMAX + 1) + L.d.lband) * 6) + L.d.jl * 3 + L.d.mode;
     keys[i] = key;
-    atomicAdd(&hist[key], 1);
-  } else {
-    const int slot = atomicAdd(big_count, 1);
-    big_list[slot] = i;
   }
+  agg_atomic_inc(hist, key);
+  const int slot = agg_atomic_inc(big_count, big);
+  if (big == 0) big_list[slot] = i;
 }
 
 // Exclusive scan of bucket sizes padded to whole waves; class wave ranges.
@@ -308,10 +326,9 @@ __global__ void k_scan(const int* __restrict__ hist, int* __restrict__ cursor,
 __global__ void k_scatter(const int* __restrict__ keys, int n, int* __restrict__ cursor,
                           int* __restrict__ perm) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int k = keys[i];
-  if (k < 0) return;
-  perm[atomicAdd(&cursor[k], 1)] = i;
+  const int k = i < n ? keys[i] : -1;
+  const int pos = agg_atomic_inc(cursor, k);
+  if (k >= 0) perm[pos] = i;
 }
 
 // ------------------------------------------------------------------ k_fill
@@ -766,6 +783,10 @@ struct gsnapdp_ctx {
   std::string arch;
   std::mutex mu;
   int fill_waves = 0;  // waves launched per k_fill class kernel
+  // per-stage event timing (gsnapdp_profile)
+  int prof_on = 0;
+  hipEvent_t ev[2 * 16] = {};
+  int ev_used[16] = {};
 };
 
 static const size_t WAVE_STRIDE_DW = (size_t)(FAST_L2MAX + 1) * (FAST_WMAX / 8) * 64;
@@ -885,17 +906,31 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   const size_t used = ((size_t)n + (size_t)NKEYS * 64 + 63) & ~(size_t)63;
   HIPCHK(hipMemsetAsync(ctx->d_perm, 0xFF, (used < ctx->perm_cap ? used : ctx->perm_cap) * 4, st));
   const int tb = 256, nb = (n + tb - 1) / tb;
+  // stage timing: events on the launch stream around each kernel
+  auto mark = [&](int stage, int end) {
+    if (!ctx->prof_on) return;
+    hipEvent_t& e = ctx->ev[2 * stage + end];
+    if (!e) (void)hipEventCreate(&e);
+    (void)hipEventRecord(e, st);
+    ctx->ev_used[stage] = 1;
+  };
+  mark(0, 0);
   hipLaunchKernelGGL(k_plan, dim3(nb), dim3(tb), 0, st, d_windows, n, d_query, d_query_uc,
                      ctx->d_blocks, (uint64_t)ctx->nwords, ctx->d_prof, d_results, d_ops,
                      d_op_offsets, ctx->d_keys, hist, ctx->d_big_list, big_count);
+  mark(0, 1);
+  mark(1, 0);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, hist, cursor, class_range);
   hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(tb), 0, st, ctx->d_keys, n, cursor, ctx->d_perm);
+  mark(1, 1);
   const int blocks = (int)(ctx->dirpool_waves / 4);
   const uint64_t nw = (uint64_t)ctx->nwords;
 #define LAUNCH_FILL(WM, LO, CLS)                                                                \
+  mark(2 + CLS, 0);                                                                             \
   hipLaunchKernelGGL((k_fill<WM, LO>), dim3(blocks), dim3(256), 0, st, d_windows, ctx->d_perm, \
                      class_range, CLS, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,    \
-                     ctx->d_dirpool, WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets)
+                     ctx->d_dirpool, WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets);          \
+  mark(2 + CLS, 1)
   LAUNCH_FILL(8, 1, 0);
   LAUNCH_FILL(16, 9, 1);
   LAUNCH_FILL(24, 17, 2);
@@ -906,9 +941,11 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   LAUNCH_FILL(44, 41, 7);
   LAUNCH_FILL(48, 45, 8);
 #undef LAUNCH_FILL
+  mark(2 + NCLASS, 0);
   hipLaunchKernelGGL(k_big, dim3(BIG_LANES / 64), dim3(64), 0, st, d_windows, ctx->d_big_list,
                      big_count, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
                      ctx->d_bigpool, BIG_LANE_STRIDE_DW, d_results, d_ops, d_op_offsets);
+  mark(2 + NCLASS, 1);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -954,6 +991,35 @@ extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows,
   if (nops) HIPCHK(hipMemcpyAsync(ops, dops, nops * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   return 0;
+}
+
+static const char* const kStageNames[] = {
+    "k_plan",         "k_scan+k_scatter", "k_fill<8,1>",    "k_fill<16,9>",  "k_fill<24,17>",
+    "k_fill<28,25>",  "k_fill<32,29>",    "k_fill<36,33>",  "k_fill<40,37>", "k_fill<44,41>",
+    "k_fill<48,45>",  "k_big"};
+static const int kNStages = (int)(sizeof(kStageNames) / sizeof(kStageNames[0]));
+
+extern "C" const char* gsnapdp_stage_name(int stage) {
+  return (stage >= 0 && stage < kNStages) ? kStageNames[stage] : "";
+}
+
+extern "C" int gsnapdp_profile(gsnapdp_ctx* ctx, int enable) {
+  if (!ctx) return -1;
+  ctx->prof_on = enable ? 1 : 0;
+  return kNStages;
+}
+
+extern "C" int gsnapdp_profile_read(gsnapdp_ctx* ctx, double* ms, int nstages) {
+  if (!ctx) return -1;
+  HIPCHK(hipSetDevice(ctx->device));
+  for (int i = 0; i < kNStages && i < nstages; i++) {
+    if (!ctx->ev_used[i]) continue;
+    HIPCHK(hipEventSynchronize(ctx->ev[2 * i + 1]));
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, ctx->ev[2 * i], ctx->ev[2 * i + 1]));
+    ms[i] += (double)t;
+  }
+  return kNStages;
 }
 
 extern "C" int gsnapdp_load_maxent_tables(gsnapdp_ctx* ctx, const double* tables, size_t nd) {

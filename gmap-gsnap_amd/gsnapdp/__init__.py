@@ -62,6 +62,12 @@ def lib():
         L.gsnapdp_maxent_device.restype = i32
         L.gsnapdp_scratch_bytes.argtypes = [vp, i32, i32, i32]
         L.gsnapdp_scratch_bytes.restype = sz
+        L.gsnapdp_profile.argtypes = [vp, i32]
+        L.gsnapdp_profile.restype = i32
+        L.gsnapdp_profile_read.argtypes = [vp, vp, i32]
+        L.gsnapdp_profile_read.restype = i32
+        L.gsnapdp_stage_name.argtypes = [i32]
+        L.gsnapdp_stage_name.restype = ctypes.c_char_p
         _lib = L
     return _lib
 
@@ -158,6 +164,16 @@ class Context:
                                       ctypes.c_void_p(stream) if stream else None)
         if rc != 0:
             raise GsnapdpError("gsnapdp_run_device: %s" % lib().gsnapdp_last_error().decode())
+
+    def profile(self, enable: bool) -> list:
+        """Enable per-kernel HIP-event timing; returns the stage names."""
+        n = lib().gsnapdp_profile(self.h, 1 if enable else 0)
+        return [lib().gsnapdp_stage_name(i).decode() for i in range(n)]
+
+    def profile_read(self, acc: np.ndarray) -> None:
+        """Add the last run's per-stage milliseconds into acc (float64)."""
+        if lib().gsnapdp_profile_read(self.h, _p(acc), acc.size) < 0:
+            raise GsnapdpError(lib().gsnapdp_last_error().decode())
 
     def sync(self):
         if lib().gsnapdp_sync(self.h) != 0:

@@ -207,6 +207,15 @@ size_t gsnapdp_scratch_bytes(gsnapdp_ctx *ctx, int n, int max_length1, int max_l
 /* Synchronise the context stream. */
 int gsnapdp_sync(gsnapdp_ctx *ctx);
 
+/* Per-kernel timing with HIP events recorded on the stream each kernel is
+ * launched on.  After gsnapdp_profile(ctx, 1), every run_device records an
+ * event pair around each of its launches; gsnapdp_profile_read synchronises
+ * and ADDS the last run's per-stage milliseconds into ms[0..nstages).
+ * Returns the number of stages (see gsnapdp_stage_name), or -1. */
+int gsnapdp_profile(gsnapdp_ctx *ctx, int enable);
+int gsnapdp_profile_read(gsnapdp_ctx *ctx, double *ms, int nstages);
+const char *gsnapdp_stage_name(int stage);
+
 /* ------------------------------------------------------------ maxent_hr
  * Batched Maxent_hr_{donor,acceptor,antidonor,antiacceptor}_prob
  * (maxent_hr.c:27217-27390) on the context genome.  model[i] in 0..3 =
