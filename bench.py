@@ -32,11 +32,11 @@ from gsnapdp import workload as W  # noqa: E402
 from gsnapdp.records import RESULT  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-VALU_INT32_PEAK = 256 * 64 * 2.4e9  # 256 CU x 64 int32 lane-ops/clk x 2.4 GHz
+VALU_INT32_PEAK = 256 * 128 * 2.4e9  # 256 CU x 4 SIMD x 32 lanes/clk (MI355X_MICROARCH.md) x 2.4 GHz
 OPS_PER_CELL = 14             # gap1 4 + gap2 4 + nogap 6 int32 ops
 READS_PER_GPU = 100_000
 GENOME_NT = 64_000_000
-DOMINANT = "k_fill<32,29>"    # band width 31..32: 70 % of C2 windows
+DOMINANT = "k_fill[W29-32]"   # band width 31..32: 70 % of C2 windows
 
 
 def window_bytes(w: np.ndarray, nops: np.ndarray) -> np.ndarray:

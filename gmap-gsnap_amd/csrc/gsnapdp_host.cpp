@@ -58,7 +58,7 @@ void init_tables(int mode) {
 }
 }  // namespace
 
-void build_profile_table(int mode, uint32_t prof[4 * 128]) {
+void build_profile_table(int mode, uint32_t prof[PROF_WORDS]) {
   init_tables(mode);
   static const char cls[6] = {'A', 'C', 'G', 'T', 'N', '*'};
   for (int t = 0; t < 4; t++)
@@ -68,6 +68,12 @@ void build_profile_table(int mode, uint32_t prof[4 * 128]) {
       for (int g = 0; g < 5; g++) w |= (uint32_t)cons_tab[c][(int)cls[g]] << (24 + g);
       prof[t * 128 + c] = w;
     }
+  for (int u = 0; u < 128; u++) {
+    uint32_t w = 0;
+    for (int g = 0; g < 5; g++)
+      if (u == cls[g]) w |= 1u << (24 + g);
+    prof[4 * 128 + u] = w;
+  }
 }
 
 int host_pairdistance(int mt, int c1, int c2) { return pd_tab[mt][c1 & 127][c2 & 127]; }

@@ -5,15 +5,30 @@
 
 #include "../../include/gsnapdp.h"
 
+#if defined(__HIPCC__)
+#define GSNAPDP_HD_CONST __host__ __device__ constexpr
+#else
+#define GSNAPDP_HD_CONST constexpr
+#endif
+
 namespace gsnapdp {
 
 constexpr int NEG = -1000000;          // NEG_INFINITY, dynprog.c:119
 constexpr int MICROINTRON_LENGTH = 9;  // dynprog.c:139
 constexpr int FAST_L2MAX = 640;        // longest genome span handled by the register-band kernel
-// band-width groups, one k_fill launch each: W in (CLASS_W[c-1], CLASS_W[c]]
-constexpr int NCLASS = 9;
-constexpr int CLASS_W[NCLASS] = {8, 16, 24, 28, 32, 36, 40, 44, 48};
+// band-width classes, one k_fill launch each: W in (CLASS_W[c-1], CLASS_W[c]].
+// A window of class c is spread over CLASS_LPW[c] lanes of CLASS_S[c] diagonals
+// each (CLASS_S * CLASS_LPW = CLASS_W), so a wave carries 64 / LPW windows.
+constexpr int NCLASS = 7;
+constexpr int CLASS_W[NCLASS] = {8, 16, 24, 28, 32, 40, 48};
+constexpr int CLASS_S[NCLASS] = {8, 8, 6, 7, 8, 5, 6};
+constexpr int CLASS_LPW[NCLASS] = {1, 2, 4, 4, 4, 8, 8};
 constexpr int FAST_WMAX = 48;
+GSNAPDP_HD_CONST inline int class_of_w(int W) {
+  int c = 0;
+  while (c < NCLASS - 1 && W > CLASS_W[c]) c++;
+  return c;
+}
 // bucket key = ((W * (FAST_WMAX+1) + lband) * 6 + jl*3 + mode), W <= 48, lband <= 47
 constexpr int NKEYS = (FAST_WMAX + 1) * (FAST_WMAX + 1) * 6;
 constexpr int BIG_LANES = 256;         // lanes of the generic (global-memory band) kernel
@@ -136,7 +151,10 @@ GSNAPDP_HD inline int intron_type_codes(int l1, int l2, int r2, int r1, int cdna
 namespace gsnapdp {
 // Profile words prof[mt*128 + c]: bits 4g..4g+3 = pairdistance[mt][c][class g] as a
 // signed 4-bit field (g = A C G T N *), bits 24..28 = consistent_array[c][class g].
-void build_profile_table(int mode, uint32_t prof[4 * 128]);
+// prof[4*128 + u]: bit 24+g set when the uppercase query byte u equals "ACGTN"[g]
+// (the `rsequenceuc[r] == c2` half of the match test, dynprog.c:2650).
+constexpr int PROF_WORDS = 5 * 128;
+void build_profile_table(int mode, uint32_t prof[PROF_WORDS]);
 int host_pairdistance(int mt, int c1, int c2);
 int host_consistent(int c1, int c2);
 }  // namespace gsnapdp

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "gsnapdp_internal.h"
 
 using namespace gsnapdp;
@@ -287,16 +289,23 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
   if (big == 0) big_list[slot] = i;
 }
 
-// Exclusive scan of bucket sizes padded to whole waves; class wave ranges.
-// cursor[k] = first perm entry of bucket k; class_range[c] = first wave of class c.
+// Exclusive scan of bucket sizes, each padded to whole waves of its class
+// (64 / CLASS_LPW windows).  cursor[k] = first perm entry of bucket k;
+// class_start[c] = first perm entry of class c (a multiple of its wave size,
+// since wave sizes shrink as W grows and are powers of two).
+__device__ inline int padded_bucket(int k, int h) {
+  const int ng = 64 / CLASS_LPW[class_of_w(k / ((FAST_WMAX + 1) * 6))];
+  return (h + ng - 1) / ng * ng;
+}
+
 __global__ void k_scan(const int* __restrict__ hist, int* __restrict__ cursor,
-                       int* __restrict__ class_range) {
+                       int* __restrict__ class_start) {
   __shared__ int part[1024];
   const int tid = threadIdx.x;
   const int per = (NKEYS + 1023) / 1024;
   const int lo = tid * per, hi = min(NKEYS, lo + per);
   int s = 0;
-  for (int k = lo; k < hi; k++) s += (hist[k] + 63) & ~63;
+  for (int k = lo; k < hi; k++) s += padded_bucket(k, hist[k]);
   part[tid] = s;
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
@@ -308,7 +317,7 @@ __global__ void k_scan(const int* __restrict__ hist, int* __restrict__ cursor,
   int run = part[tid] - s;
   for (int k = lo; k < hi; k++) {
     cursor[k] = run;
-    run += (hist[k] + 63) & ~63;
+    run += padded_bucket(k, hist[k]);
   }
   __syncthreads();
   if (tid == 0) {
@@ -316,10 +325,10 @@ __global__ void k_scan(const int* __restrict__ hist, int* __restrict__ cursor,
     int wlo = 0;
     for (int c = 0; c < NCLASS; c++) {
       const int kfirst = (wlo + 1) * (FAST_WMAX + 1) * 6;
-      class_range[c] = (kfirst < NKEYS ? cursor[kfirst] : part[1023]) / 64;
+      class_start[c] = kfirst < NKEYS ? cursor[kfirst] : part[1023];
       wlo = CLASS_W[c];
     }
-    class_range[NCLASS] = part[1023] / 64;
+    class_start[NCLASS] = part[1023];
   }
 }
 
@@ -376,44 +385,74 @@ struct ColStream {
   }
 };
 
-// Register-band fill + endpoint + traceback for one wave of 64 single-gap
-// windows sharing (lband, rband, jl).  The band is bottom-aligned in WMAX
-// register slots: slot s holds diagonal d = s - stop, stop = WMAX - W.
+// ------------------------------------------------------------------ k_fill
+// Register-band fill, endpoint and traceback for one wave of 64/LPW single-gap
+// windows sharing (lband, rband, jl) (Dynprog_single_gap, dynprog.c:4471-4575).
 //
-// Slots above the band (s < stop) are computed like every other slot, which
-// keeps the column body free of control flow, but their nogap score gets a
-// -2^29 bias so nothing they hold can reach the band: the only edge from
-// them into the band is the gap2 chain of the top slot, which then sees a
+// Band layout.  A window's band is bottom-aligned in WMAX = S*LPW diagonal
+// slots: global slot gs holds diagonal gs - stop (stop = WMAX - W), i.e. row
+// r = c - rband + gs - stop of column c.  Lane j of the window's lane group
+// owns slots j*S .. j*S+S-1 in registers.  The group runs a skewed wavefront:
+// at step t lane j computes column t - j, so the gap2 chain (top to bottom of
+// a column, dynprog.c:1532-1542) arrives from lane j-1's previous step and the
+// gap1 input of the lowest slot (dynprog.c:1519-1529) from lane j+1's slot 0
+// of this step; both move by DPP row shifts.
+//
+// Offset scores.  Registers hold X(r,c) - (r+c)*ext for X in {H, E, F}.  This
+// is an exact change of variables of the recurrences of dynprog.c:1519-1561:
+// gap1 and gap2 lose their "+ extend", the nogap step gains a constant
+// -2*ext, and every comparison is between two values of the same cell, so
+// each tie decision is the reference's.  The endpoint score is converted back.
+//
+// Slots above the band (gs < stop) run the same code with a -2^29 bias on
+// their nogap score, and rows <= 0 need no special case: the only edge from
+// them into the band is the top slot's gap2 input, which then holds a
 // NEG-like value exactly where the reference reads its NEG_INFINITY sentinel
-// (dynprog.c:1501-1506).  Rows <= 0 inside the band need no special case:
-// they start from the column-0 initialisation and only ever read rows above
-// them, so they stay NEG-like, while row 0's gap1 chain reproduces the
-// reference's open + c*extend initialisation exactly (dynprog.c:1464-1475).
-// NEG-like values never compete with reachable ones (SURVEY.md 8(a) a5,
-// "only band cells, sentinels and inits are ever read"); see DESIGN.md.
-template <int WMAX>
-struct RegDirs {
-  const uint32_t* D;
-  int lane, stop, rband;
-  __device__ inline uint32_t operator()(int r, int c) const {
-    const int s = stop + r - c + rband;
-    return (D[((size_t)c * ((WMAX + 7) / 8) + (s >> 3)) * 64 + lane] >> ((s & 7) * 4)) & 0xFu;
-  }
-};
-
+// (dynprog.c:1501-1506), and row 0's gap1 chain reproduces the open + c*ext
+// initialisation (dynprog.c:1464-1475).  NEG-like values never compete with
+// reachable ones ("Band edges").
+//
+// Per cell the fill streams 4 direction bits (the sign bits of differences,
+// pushed with alignbit: v1 h1 dF dE -> nibble bits 3..0; a jump-late fill
+// stores their complements) and a match bit (consistent_array or uppercase
+// equality, dynprog.c:2650-2656) to per-wave scratch.  The traceback is then
+// a backward column sweep over that scratch: every lane reloads the words it
+// wrote (coalesced, prefetched two columns ahead) and the group's traceback
+// lane walks the reference's traceback (dynprog.c:2611-2712) one column per
+// step, so no step waits on a dependent global load.
 constexpr int ABOVE_BIAS = -(1 << 29);
+constexpr int UTAB = 4 * 128;  // LDS profile: 4 x 128 pairdistance words, then 256 uppercase words
+constexpr int SPROF_WORDS = 4 * 128 + 256;
 
-template <int WMAX, int LOW, int JL>
-__device__ void fill_wave(const gsnapdp_window* __restrict__ Wn, int wi, bool active, int lane,
-                          uint32_t* __restrict__ D, const char* __restrict__ q,
-                          const char* __restrict__ qu, const uint32_t* __restrict__ blocks,
-                          uint64_t nwords, const uint32_t* __restrict__ prof,
-                          gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
-                          const int64_t* __restrict__ op_off) {
-  constexpr int NK = (WMAX + 7) / 8;
-  constexpr int NABOVE = WMAX - LOW;  // slots that can lie above the band in this class
-  int lband, rband, open, ext, L1, L2, qnext, qstep, ptab_off;
-  ColStream cs;
+__device__ inline uint32_t push_sign(uint32_t acc, int d) {
+  return __builtin_amdgcn_alignbit(acc, (uint32_t)d, 31u);  // (acc << 1) | (d < 0)
+}
+// the same register of lane-1 / lane+1 (rows of 16 lanes; groups never straddle rows)
+__device__ inline int from_lane_above(int v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x111, 0xF, 0xF, true);  // row_shr:1
+}
+__device__ inline int from_lane_below(int v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x101, 0xF, 0xF, true);  // row_shl:1
+}
+
+template <int S, int LPW, int LOW, int JL>
+__device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool active, int lane,
+                           uint32_t* __restrict__ D, uint8_t* __restrict__ M,
+                           const char* __restrict__ q, const char* __restrict__ qu,
+                           const uint32_t* __restrict__ blocks, uint64_t nwords,
+                           const uint32_t* sprof, gsnapdp_result* __restrict__ res,
+                           uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
+  static_assert(S >= 2 && S <= 8 && LPW <= 16 && 64 % LPW == 0, "class shape");
+  constexpr int WMAX = S * LPW;
+  constexpr int NG = 64 / LPW;
+  constexpr int NAB = (WMAX - LOW) < S ? (WMAX - LOW) : S;  // local slots that may lie above the band
+  const int j = lane % LPW;
+  const int gbase = lane - j;
+  const int g = lane / LPW;
+  int lband, rband, open, ext, L1, L2, stop, maxL2, mtoff, cvlo, cvhi;
+  int qrow0, qstep, dlo, dhi, xorc;  // query byte of the bottom row at column c: qrow0 + qstep*c
+  uint32_t gp0;                      // genome position of column c: gp0 + gps*c
+  int gps;
   {
     const Lane L = make_lane(Wn[wi]);
     lband = __builtin_amdgcn_readfirstlane(L.d.lband);  // wave-uniform (bucket key)
@@ -422,114 +461,381 @@ __device__ void fill_wave(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
     ext = __builtin_amdgcn_readfirstlane(L.d.ext);
     L1 = active ? L.d.L1 : 0;
     L2 = active ? L.d.L2 : 0;
-    qstep = L.qstep;
-    qnext = L.qbase + L.qstep * lband;  // query index of row lband+1 (enters at column 1)
-    ptab_off = L.d.mt * 128;
+    stop = WMAX - (lband + rband + 1);
+    mtoff = L.d.mt * 128;
+    ColStream cs;
     cs.init(L);
+    cvlo = cs.cvlo;
+    cvhi = cs.cvhi;
+    gp0 = cs.P0;
+    gps = cs.PS;
+    xorc = cs.xorc;
+    // bottom slot of this lane holds row j*S - stop - rband + S - 1 + c at column c
+    const int rbot0 = j * S - stop - rband + S - 1;
+    qstep = L.qstep;
+    qrow0 = L.qbase + L.qstep * (rbot0 - 1);
+    const int L1v = L.d.L1;  // the window's query bytes (rows 1..L1) bound every read
+    dlo = (L.qstep > 0 ? L.qbase : L.qbase - (L1v - 1)) >> 2;
+    dhi = (L.qstep > 0 ? L.qbase + (L1v - 1) : L.qbase) >> 2;
   }
-  const int stop = WMAX - (lband + rband + 1);
-  const int maxL2 = __builtin_amdgcn_readfirstlane(wave_max(L2));
-  const uint32_t* ptab = prof + ptab_off;
-  const int qbase0 = qnext - qstep * lband;
-  int bias[NABOVE > 0 ? NABOVE : 1];
+  maxL2 = __builtin_amdgcn_readfirstlane(wave_max(L2));
+  const int K = -2 * ext;
+  int Kab[NAB > 0 ? NAB : 1];
 #pragma unroll
-  for (int s = 0; s < NABOVE; s++) bias[s] = __builtin_amdgcn_readfirstlane(s < stop ? ABOVE_BIAS : 0);
+  for (int s = 0; s < NAB; s++) Kab[s] = K + ((j * S + s < stop) ? ABOVE_BIAS : 0);
+  const int row0 = j * S - stop - rband;  // row of local slot 0 at column 0
 
-  int H[WMAX], E[WMAX], F[WMAX];
-  uint32_t P[WMAX];
-  // column 0 (dynprog.c:1460-1488): slot s holds row r = s - stop - rband
+  // profile word of row r from LDS; rows outside 1..L1 get a neutral word
+  // (their cells never feed a reachable in-band cell)
+  auto profw = [&](int r, uint32_t qb, uint32_t ub) -> uint32_t {
+    const bool ok = r >= 1 && r <= L1;
+    return sprof[mtoff + (ok ? (qb & 127u) : 0u)] | sprof[UTAB + (ok ? ub : 255u)];
+  };
+
+  int H[S], E[S], F[S];
+  uint32_t P[S];
+  // column 0 (dynprog.c:1460-1488) in offset coordinates; rows come from global
+  // memory once here, then only the bottom row enters per column
+  {
+    const Lane L = make_lane(Wn[wi]);
 #pragma unroll
-  for (int s = 0; s < WMAX; s++) {
-    const int r = s - stop - rband;
-    H[s] = (r == 0) ? 0 : NEG;
-    E[s] = NEG;
-    F[s] = (r >= 1) ? open + r * ext : NEG;
-    const bool ld = r >= 1 && r <= L1;
-    P[s] = ptab[ld ? qchar(q, qbase0 + qstep * (r - 1)) : 0];
+    for (int s = 0; s < S; s++) {
+      const int r = row0 + s;
+      H[s] = (r == 0) ? 0 : NEG;
+      E[s] = NEG;
+      F[s] = (r >= 1) ? open : NEG;  // open + r*ext - r*ext
+      uint32_t qb = 0u, ub = 255u;
+      if (r >= 1 && r <= L1) {
+        const int qi = L.qbase + L.qstep * (r - 1);
+        qb = (unsigned char)q[qi];
+        ub = (unsigned char)qu[qi];
+      }
+      P[s] = profw(r, qb, ub);
+    }
   }
+  // Per-column inputs of a lane: the dwords holding its bottom row's query
+  // bytes and the 32-nt genome block of its column.  In the steady state they
+  // are loaded two columns ahead into alternating buffers (no register copy
+  // of a load in flight), and turned into the profile word / genome class one
+  // column ahead.
+  const uint32_t* q4 = (const uint32_t*)q;
+  const uint32_t* u4 = (const uint32_t*)qu;
+  const uint64_t gmax = nwords >= 3 ? (nwords - 3) / 3 : 0;  // last whole block
+  struct ColIn {
+    uint32_t qw, uw, gh, gl, gf;
+  };
+  auto fetch = [&](int c, ColIn& x) {
+    const int qi = qrow0 + qstep * c;
+    const int d = min(max(qi >> 2, dlo), dhi);
+    x.qw = q4[d];
+    x.uw = u4[d];
+    const uint64_t b = (uint64_t)((gp0 + (uint32_t)(gps * c)) >> 5);
+    const uint64_t ptr = (b <= gmax ? b : gmax) * 3u;
+    x.gh = blocks[ptr];
+    x.gl = blocks[ptr + 1];
+    x.gf = blocks[ptr + 2];
+  };
+  auto prof_of = [&](int c, const ColIn& x) -> uint32_t {
+    const int qi = qrow0 + qstep * c;
+    const uint32_t sh = (uint32_t)(qi & 3) * 8u;
+    return profw(row0 + S - 1 + c, (x.qw >> sh) & 0xFFu, (x.uw >> sh) & 0xFFu);
+  };
+  auto class_of = [&](int c, const ColIn& x) -> int {
+    const uint32_t pos = gp0 + (uint32_t)(gps * c);
+    const uint32_t bit = pos & 31u;
+    const bool ing = (uint64_t)(pos >> 5) <= gmax;  // outside the genome: N
+    const uint32_t word = bit < 16 ? x.gl : x.gh;
+    const int code = (int)((word >> ((bit & 15u) * 2u)) & 3u) ^ xorc;
+    const bool inr = c >= cvlo && c <= cvhi;
+    return !inr ? 5 : ((!ing || ((x.gf >> bit) & 1u)) ? 4 : code);
+  };
+  ColIn xa, xb;
+  uint32_t pnext;
+  int gnext;
+  fetch(1, xa);
+  pnext = prof_of(1, xa);
+  gnext = class_of(1, xa);
   int fin = NEG;
-  const int se = stop + (L1 - L2 + rband);  // slot of the endpoint (L1,L2)
+  const int se = stop + L1 - L2 + rband;  // global slot of the endpoint (L1,L2)
+  const int je = se / S, sle = se - je * S;
+  // scratch layout: column c's words are D[c*64 + (j*NG + g)], one 256-byte
+  // row per column (coalesced stores); the match bytes likewise in M
+  uint32_t* Dl = D + j * NG + g;
+  uint8_t* Ml = M + j * NG + g;
 
-  for (int c = 1; c <= maxL2; c++) {
-    const uint32_t gsh = 4u * (uint32_t)cs.cls(blocks, nwords, c);
-    // slide the row profiles down one diagonal; row c+lband enters at the bottom
-#pragma unroll
-    for (int s = 0; s < WMAX - 1; s++) P[s] = P[s + 1];
-    P[WMAX - 1] = ptab[(c + lband <= L1) ? qchar(q, qnext) : 0];
-    qnext += qstep;
-    int hp = NEG, fp = NEG;  // new (nogap, gap2) above slot 0: the top sentinel
-    uint32_t acc[NK];
-#pragma unroll
-    for (int k = 0; k < NK; k++) acc[k] = 0u;
-#pragma unroll
-    for (int s = 0; s < WMAX; s++) {
+  // One skewed step.  MASKED steps (the first and last LPW-1) leave lanes
+  // whose column is outside 1..maxL2 untouched.
+  // PIPE 0: inputs of column c+1 loaded and used at the end of the step;
+  // PIPE 1 / 2: xa / xb receives column c+2 while the other buffer (column
+  // c+1, loaded one step earlier) yields the next profile word and class.
+  auto step = [&](auto masked, auto pipe, int t) {
+    constexpr bool MASKED = decltype(masked)::value;
+    constexpr int PIPE = decltype(pipe)::value;
+    const int c = t - j;
+    const bool act = !MASKED || (c >= 1 && c <= maxL2);
+    int hp = NEG, fp = NEG;  // new (nogap, gap2) just above local slot 0
+    if (LPW > 1) {
+      const int h = from_lane_above(H[S - 1]), f = from_lane_above(F[S - 1]);
+      if (j != 0) {
+        hp = h;
+        fp = f;
+      }
+    }
+    uint32_t acc = 0u, macc = 0u, gsh = 0u, msh = 0u;
+    auto cell = [&](int s, int Hr, int Er) {
       const int Hd = H[s], Ed = E[s], Fd = F[s];
-      const int Hr = (s + 1 < WMAX) ? H[(s + 1) % WMAX] : NEG;  // sentinel below the band
-      const int Er = (s + 1 < WMAX) ? E[(s + 1) % WMAX] : NEG;
-      const int a = Hr + open;  // gap1 (dynprog.c:1519-1529)
-      const bool dE = JL ? (Er >= a) : (Er > a);
-      const int e = max(a, Er) + ext;
-      const int b = hp + open;  // gap2 (:1532-1542)
-      const bool dF = JL ? (fp >= b) : (fp > b);
-      const int f = max(b, fp) + ext;
-      const bool h1 = JL ? (Ed >= Hd) : (Ed > Hd);  // nogap (:1545-1561)
+      const uint32_t pw = P[s];
+      const int a = Hr + open;
+      const int b = hp + open;
       const int m1 = max(Hd, Ed);
-      const bool v1 = JL ? (Fd >= m1) : (Fd > m1);
-      const int sc = __builtin_amdgcn_sbfe((int)P[s], gsh, 4);
-      const int hn = max(m1, Fd) + sc + (s < NABOVE ? bias[s < NABOVE ? s : 0] : 0);
-      const uint32_t nib = (dE ? 1u : 0u) | (dF ? 2u : 0u) | (v1 ? 8u : (h1 ? 4u : 0u));
-      acc[s / 8] |= nib << (4 * (s % 8));
-      E[s] = e;
+      const int kk = (s < NAB) ? Kab[s < NAB ? s : 0] : K;
+      const int hn = max(m1, Fd) + __builtin_amdgcn_sbfe((int)pw, gsh, 4) + kk;
+      acc = push_sign(acc, JL ? (Fd - m1) : (m1 - Fd));  // v1: nogap from gap2
+      acc = push_sign(acc, JL ? (Ed - Hd) : (Hd - Ed));  // h1: nogap from gap1
+      acc = push_sign(acc, JL ? (fp - b) : (b - fp));    // dF: gap2 extends
+      acc = push_sign(acc, JL ? (Er - a) : (a - Er));    // dE: gap1 extends
+      macc = (macc << 1) | __builtin_amdgcn_ubfe(pw, msh, 1);
+      E[s] = max(a, Er);
+      const int f = max(b, fp);
       F[s] = f;
       H[s] = hn;
       hp = hn;
       fp = f;
+    };
+    if (act) {
+#pragma unroll
+      for (int s = 0; s < S - 1; s++) P[s] = P[s + 1];
+      P[S - 1] = pnext;
+      gsh = 4u * (uint32_t)gnext;
+      msh = 24u + (uint32_t)gnext;
+      cell(0, H[1], E[1]);
     }
-    uint32_t* Dc = D + (size_t)c * NK * 64;
+    int hb = NEG, eb = NEG;  // old (nogap, gap1) just below the lowest local slot
+    if (LPW > 1) {
+      const int h = from_lane_below(H[0]), e = from_lane_below(E[0]);
+      if (j != LPW - 1) {
+        hb = h;
+        eb = e;
+      }
+    }
+    if (act) {
 #pragma unroll
-    for (int k = 0; k < NK; k++) Dc[k * 64 + lane] = acc[k];
-    // endpoint (L1,L2): captured in the column the lane ends (dynprog.c:4545)
-    if (__builtin_amdgcn_ballot_w64(c == L2) != 0) {
+      for (int s = 1; s < S - 1; s++) cell(s, H[s + 1], E[s + 1]);
+      cell(S - 1, hb, eb);
+      Dl[(size_t)c * 64] = acc;
+      Ml[(size_t)c * 64] = (uint8_t)macc;
+      // endpoint (L1,L2), captured in the column the window ends (dynprog.c:4545)
+      if (__builtin_amdgcn_ballot_w64(c == L2 && j == je) != 0) {
 #pragma unroll
-      for (int s = 0; s < WMAX; s++)
-        if (c == L2 && s == se) fin = H[s];
+        for (int s = 0; s < S; s++)
+          if (c == L2 && j == je && s == sle) fin = H[s];
+      }
+      if (PIPE == 0) {
+        ColIn x;
+        fetch(c + 1, x);
+        pnext = prof_of(c + 1, x);
+        gnext = class_of(c + 1, x);
+      } else {
+        ColIn& mine = PIPE == 1 ? xa : xb;
+        ColIn& other = PIPE == 1 ? xb : xa;
+        pnext = prof_of(c + 1, other);
+        gnext = class_of(c + 1, other);
+        fetch(c + 2, mine);
+      }
+    }
+  };
+  using Masked = std::integral_constant<bool, true>;
+  using Full = std::integral_constant<bool, false>;
+  using Direct = std::integral_constant<int, 0>;
+  using PipeA = std::integral_constant<int, 1>;
+  using PipeB = std::integral_constant<int, 2>;
+  int t = 1;
+  for (; t < LPW && t < maxL2 + LPW; t++) step(Masked(), Direct(), t);
+  if (t + 1 <= maxL2) {
+    fetch(t - j + 1, xb);  // column c+1 of the first pipelined step
+    for (; t + 1 <= maxL2; t += 2) {
+      step(Full(), PipeA(), t);
+      step(Full(), PipeB(), t + 1);
     }
   }
+  for (; t <= maxL2; t++) step(Full(), Direct(), t);
+  for (; t < maxL2 + LPW; t++) step(Masked(), Direct(), t);
+  fin = __shfl(fin, gbase + je);
+  const int finalscore = fin + (L1 + L2) * ext;
+#ifdef EXP_NOTRACE
+  if (active && j == 0) res[wi].finalscore = finalscore;
+  return;
+#endif
+  if (!active || j != 0) return;
 
-  if (!active) return;
+  // ---- traceback (dynprog.c:2611-2712), one column per step on the group's
+  // lane 0.  The direction words of the lane that holds the path's current
+  // diagonal arrive four columns per load, two groups ahead; a gap that moves
+  // the path to another lane's slots costs one dependent load.
   const gsnapdp_window w = Wn[wi];
   const Lane L = make_lane(w);
-  RegDirs<WMAX> dirs = {D, lane, stop, rband};
-  Tally t = {0, 0, 0, 0};
+  enum { T_DIAG = 0, T_VERT = 1, T_HORIZ = 2, T_DONE = 3 };
+  int st = T_DIAG;
+  int r = L1, dist = 0;
+  Tally tal = {0, 0, 0, 0};
   OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
-  traceback(dirs, L, L1, L2, q, qu, blocks, nwords, prof, t, ow);
-  write_result(res + wi, w, L, fin, L1, L2, t, ow);
+  const uint32_t inv = JL ? 0xFu : 0u;
+  const int wband = lband + rband;
+  const uint32_t* Dg = D + g;
+  const uint8_t* Mg = M + g;
+  auto jj_of = [&](int rr, int cc) {
+    const int sg = stop + rr - cc + rband;
+    return sg < 0 ? 0 : (sg >= WMAX ? LPW - 1 : sg / S);
+  };
+  auto ldw = [&](int cc, int jj) -> uint32_t { return Dg[(size_t)cc * 64 + jj * NG]; };
+  auto ldm = [&](int cc, int jj) -> uint32_t { return Mg[(size_t)cc * 64 + jj * NG]; };
+  auto column = [&](int c, uint32_t wv, uint32_t mv, int jw) {
+    auto inb = [&](int rr) {
+      const int d = rr - c + rband;
+      return rr >= 1 && c >= 1 && d >= 0 && d <= wband;
+    };
+    auto nib = [&](int rr) -> uint32_t {
+      const int sg = stop + rr - c + rband;
+      const int jj = sg / S, sl = sg - jj * S;
+      const uint32_t x = (jj == jw) ? wv : ldw(c, jj);
+      return ((x >> (4 * (S - 1 - sl))) & 0xFu) ^ inv;
+    };
+    auto mbit = [&](int rr) -> uint32_t {
+      const int sg = stop + rr - c + rband;
+      const int jj = sg / S, sl = sg - jj * S;
+      const uint32_t x = (jj == jw) ? mv : ldm(c, jj);
+      return (x >> (S - 1 - sl)) & 1u;
+    };
+    if (st == T_VERT) {  // gap2 chain in this column (add_queryskip, dynprog.c:2372)
+      while (c == 0 ? (r >= 2 && r <= lband && r <= L1) : (inb(r) && (nib(r) & 2u))) {
+        dist++;
+        r--;
+      }
+      r--;
+      ow.flush();
+      ow.put(GSNAPDP_OP(GSNAPDP_OP_VSKIP, dist));
+      tal.nopens++;
+      tal.nindels += dist;
+      st = T_DIAG;
+    }
+    if (st == T_HORIZ) {  // gap1 chain, one column per step (add_genomeskip, dynprog.c:2416)
+      const bool more = (r == 0) ? (c >= 2 && c <= rband && c <= L2) : (inb(r) && (nib(r) & 1u));
+      if (more) {
+        dist++;
+      } else {
+        // skipped columns c .. c+dist-1; the path lands in column c-1
+        bool dashes = true;
+        if (dist >= MICROINTRON_LENGTH) {
+          const int cl = c, cr = c + dist - 1;
+          const int gl = L.g0 + L.gstep * (cl - 1), gr = L.g0 + L.gstep * (cr - 1);
+          const int lo = L.d.rev ? gr : gl, hi = L.d.rev ? gl : gr;
+          const int l1 = gclass(blocks, nwords, L, lo), l2 = gclass(blocks, nwords, L, lo + 1);
+          const int r2 = gclass(blocks, nwords, L, hi - 1), r1 = gclass(blocks, nwords, L, hi);
+          dashes = intron_type_codes(l1, l2, r2, r1, L.cdna_direction) == 0;
+        }
+        ow.flush();
+        ow.put(GSNAPDP_OP(dashes ? GSNAPDP_OP_HDASH : GSNAPDP_OP_HGAP, dist));
+        if (dashes) {
+          tal.nopens++;
+          tal.nindels += dist;
+        }
+        st = T_DIAG;
+      }
+    } else if (st == T_DIAG) {
+      if (!inb(r)) {
+        st = T_DONE;
+      } else {
+        const uint32_t nb = nib(r);
+        if (c >= cvlo && c <= cvhi) {  // not a '*' column (dynprog.c:2644)
+          if (mbit(r)) tal.nmatches++;
+          else tal.nmismatches++;
+        }
+        ow.run++;
+        if (nb & 8u) {
+          st = T_VERT;
+          dist = 1;
+        } else if (nb & 4u) {
+          st = T_HORIZ;
+          dist = 1;
+        }
+        r--;
+      }
+    }
+  };
+  // groups of four columns (4G .. 4G+3), two groups in flight
+  struct Grp {
+    uint32_t w[4], m[4];
+    int jw;
+  };
+  auto fetch_group = [&](Grp& x, int G, int jj) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int cc = 4 * G + k;
+      x.w[k] = ldw(cc, jj);
+      x.m[k] = ldm(cc, jj);
+    }
+    x.jw = jj;
+  };
+  // ga holds the current group, gb the next one (loaded a group ahead)
+  int c = L2;
+  int G = c >> 2;
+  int jp = jj_of(r, L2);
+  Grp ga, gb;
+  fetch_group(ga, G, jp);
+  fetch_group(gb, G >= 1 ? G - 1 : 0, jp);
+  for (; c >= 0 && st != T_DONE; c--) {
+    const int k = c & 3;
+    uint32_t wv = ga.w[0], mv = ga.m[0];
+#pragma unroll
+    for (int kk = 1; kk < 4; kk++) {
+      wv = (k == kk) ? ga.w[kk] : wv;
+      mv = (k == kk) ? ga.m[kk] : mv;
+    }
+    column(c, wv, mv, ga.jw);
+    if (k == 0) {  // leaving group G
+      ga = gb;
+      G--;
+      if (G >= 1) fetch_group(gb, G - 1, jj_of(r, c - 1));  // the path's diagonal, predicted unchanged
+    }
+  }
+  if (st != T_DONE) column(-1, 0u, 0u, -1);
+  ow.flush();
+  write_result(res + wi, w, L, finalscore, L1, L2, tal, ow);
 }
 
-// One launch per register class: waves whose band width W is in [LOW, WMAX].
-template <int WMAX, int LOW>
+// One launch per band-width class; a task is one wave of 64/LPW windows.
+template <int S, int LPW, int LOW>
 __global__ __launch_bounds__(256) void k_fill(
     const gsnapdp_window* __restrict__ Wn, const int* __restrict__ perm,
-    const int* __restrict__ class_range, int cls, const char* __restrict__ q,
+    const int* __restrict__ class_start, int cls, const char* __restrict__ q,
     const char* __restrict__ qu, const uint32_t* __restrict__ blocks, uint64_t nwords,
     const uint32_t* __restrict__ prof, uint32_t* __restrict__ dirpool, size_t wave_stride,
     gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
     const int64_t* __restrict__ op_off) {
+  constexpr int NG = 64 / LPW;
+  __shared__ uint32_t sprof[SPROF_WORDS];
+  for (int i = threadIdx.x; i < SPROF_WORDS; i += blockDim.x)
+    sprof[i] = i < UTAB ? prof[i] : (i - UTAB < 128 ? prof[i] : 0u);
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nw = (gridDim.x * blockDim.x) >> 6;
-  const int t0 = class_range[cls], t1 = class_range[cls + 1];
+  const int t0 = class_start[cls] / NG, t1 = class_start[cls + 1] / NG;
   uint32_t* D = dirpool + (size_t)gw * wave_stride;
+  uint8_t* M = (uint8_t*)(D + (size_t)(FAST_L2MAX + 4) * 64);
+  const int g = lane / LPW;
   for (int t = t0 + gw; t < t1; t += nw) {
-    const int wi0 = perm[(size_t)t * 64 + lane];
-    const int w0 = __builtin_amdgcn_readfirstlane(perm[(size_t)t * 64]);  // lane 0: real window
+    const int wi0 = perm[(size_t)t * NG + g];
+    const int w0 = __builtin_amdgcn_readfirstlane(perm[(size_t)t * NG]);  // group 0: a real window
     const bool active = wi0 >= 0;
-    const int wi = active ? wi0 : w0;  // idle lanes shadow lane 0 (reads only)
+    const int wi = active ? wi0 : w0;  // idle groups shadow group 0 (reads only)
     const int jl = __builtin_amdgcn_readfirstlane((int)Wn[w0].jump_late_p);
     if (jl)
-      fill_wave<WMAX, LOW, 1>(Wn, wi, active, lane, D, q, qu, blocks, nwords, prof, res, ops, op_off);
+      fill_group<S, LPW, LOW, 1>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, res, ops,
+                                 op_off);
     else
-      fill_wave<WMAX, LOW, 0>(Wn, wi, active, lane, D, q, qu, blocks, nwords, prof, res, ops, op_off);
+      fill_group<S, LPW, LOW, 0>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, res, ops,
+                                 op_off);
   }
 }
 
@@ -558,7 +864,7 @@ __global__ __launch_bounds__(64) void k_big(
     const int wi = big_list[j];
     const gsnapdp_window w = Wn[wi];
     const Lane L = make_lane(w);
-    const int lband = L.d.lband, rband = L.d.rband, Wd = L.d.W;
+    const int rband = L.d.rband, Wd = L.d.W;
     const int L1 = L.d.L1, L2 = L.d.L2;
     const int NKd = (Wd + 7) / 8;
     if (Wd > BIG_WMAX || L2 > BIG_L2MAX || L1 > BIG_L1MAX) {
@@ -763,7 +1069,7 @@ struct gsnapdp_ctx {
   size_t nwords = 0;
   uint32_t* d_blocks = nullptr;
   int mode = 0;
-  uint32_t h_prof[4 * 128];
+  uint32_t h_prof[PROF_WORDS];
   uint32_t* d_prof = nullptr;
   double* d_tables = nullptr;
   size_t ntables = 0;
@@ -772,7 +1078,7 @@ struct gsnapdp_ctx {
   int* d_keys = nullptr;
   int* d_perm = nullptr;
   int* d_big_list = nullptr;
-  int* d_small = nullptr;  // hist[NKEYS] | cursor[NKEYS] | class_range[NCLASS+1] | big_count
+  int* d_small = nullptr;  // hist[NKEYS] | cursor[NKEYS] | class_start[NCLASS+1] | big_count
   size_t perm_cap = 0;
   uint32_t* d_dirpool = nullptr;
   size_t dirpool_waves = 0;
@@ -789,7 +1095,11 @@ struct gsnapdp_ctx {
   int ev_used[16] = {};
 };
 
-static const size_t WAVE_STRIDE_DW = (size_t)(FAST_L2MAX + 1) * (FAST_WMAX / 8) * 64;
+// per-wave k_fill scratch: direction words (u32) then match bytes, one
+// 64-lane row per column 0 .. FAST_L2MAX + 3 (the traceback reads whole
+// 4-column groups)
+static const size_t FILL_COLS = (size_t)FAST_L2MAX + 4;
+static const size_t WAVE_STRIDE_DW = FILL_COLS * 64 + FILL_COLS * 16;
 static const size_t BIG_LANE_STRIDE_DW =
     (size_t)3 * BIG_WMAX + (BIG_L1MAX + 1) + (size_t)(BIG_L2MAX + 1) * (BIG_WMAX / 8) + 64;
 
@@ -817,7 +1127,7 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
     delete ctx;
     return nullptr;
   }
-  ctx->fill_waves = prop.multiProcessorCount * 8;
+  ctx->fill_waves = prop.multiProcessorCount * 16;
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     return fail("stream", e);
   if ((e = hipMalloc(&ctx->d_blocks, (nwords + 8) * 4)) != hipSuccess) return fail("malloc blocks", e);
@@ -841,18 +1151,18 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
 
 extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   if (!ctx) return;
-  hipSetDevice(ctx->device);
-  hipFree(ctx->d_blocks);
-  hipFree(ctx->d_prof);
-  hipFree(ctx->d_tables);
-  hipFree(ctx->d_keys);
-  hipFree(ctx->d_perm);
-  hipFree(ctx->d_big_list);
-  hipFree(ctx->d_small);
-  hipFree(ctx->d_dirpool);
-  hipFree(ctx->d_bigpool);
-  hipFree(ctx->d_stage);
-  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  (void)hipSetDevice(ctx->device);
+  (void)hipFree(ctx->d_blocks);
+  (void)hipFree(ctx->d_prof);
+  (void)hipFree(ctx->d_tables);
+  (void)hipFree(ctx->d_keys);
+  (void)hipFree(ctx->d_perm);
+  (void)hipFree(ctx->d_big_list);
+  (void)hipFree(ctx->d_small);
+  (void)hipFree(ctx->d_dirpool);
+  (void)hipFree(ctx->d_bigpool);
+  (void)hipFree(ctx->d_stage);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
 
@@ -874,9 +1184,9 @@ extern "C" size_t gsnapdp_scratch_bytes(gsnapdp_ctx* ctx, int n, int max_length1
 static int ensure_capacity(gsnapdp_ctx* ctx, int n) {
   if (n <= ctx->cap_n) return 0;
   int cap = n + n / 4 + 1024;
-  hipFree(ctx->d_keys);
-  hipFree(ctx->d_perm);
-  hipFree(ctx->d_big_list);
+  (void)hipFree(ctx->d_keys);
+  (void)hipFree(ctx->d_perm);
+  (void)hipFree(ctx->d_big_list);
   HIPCHK(hipMalloc(&ctx->d_keys, (size_t)cap * 4));
   HIPCHK(hipMalloc(&ctx->d_big_list, (size_t)cap * 4));
   // perm: every bucket padded to a whole wave
@@ -898,8 +1208,8 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   if (ensure_capacity(ctx, n)) return -1;
   int* hist = ctx->d_small;
   int* cursor = hist + NKEYS;
-  int* class_range = cursor + NKEYS;
-  int* big_count = class_range + NCLASS + 1;
+  int* class_start = cursor + NKEYS;
+  int* big_count = class_start + NCLASS + 1;
   HIPCHK(hipMemsetAsync(hist, 0, (size_t)NKEYS * 4, st));
   HIPCHK(hipMemsetAsync(big_count, 0, 4, st));
   // perm padding entries must read -1; only the used prefix matters
@@ -920,26 +1230,25 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
                      d_op_offsets, ctx->d_keys, hist, ctx->d_big_list, big_count);
   mark(0, 1);
   mark(1, 0);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, hist, cursor, class_range);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, hist, cursor, class_start);
   hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(tb), 0, st, ctx->d_keys, n, cursor, ctx->d_perm);
   mark(1, 1);
   const int blocks = (int)(ctx->dirpool_waves / 4);
   const uint64_t nw = (uint64_t)ctx->nwords;
-#define LAUNCH_FILL(WM, LO, CLS)                                                                \
+#define LAUNCH_FILL(S_, LPW_, LO, CLS)                                                          \
   mark(2 + CLS, 0);                                                                             \
-  hipLaunchKernelGGL((k_fill<WM, LO>), dim3(blocks), dim3(256), 0, st, d_windows, ctx->d_perm, \
-                     class_range, CLS, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,    \
-                     ctx->d_dirpool, WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets);          \
+  hipLaunchKernelGGL((k_fill<S_, LPW_, LO>), dim3(blocks), dim3(256), 0, st, d_windows,         \
+                     ctx->d_perm, class_start, CLS, d_query, d_query_uc, ctx->d_blocks, nw,     \
+                     ctx->d_prof, ctx->d_dirpool, WAVE_STRIDE_DW, d_results, d_ops,             \
+                     d_op_offsets);                                                             \
   mark(2 + CLS, 1)
-  LAUNCH_FILL(8, 1, 0);
-  LAUNCH_FILL(16, 9, 1);
-  LAUNCH_FILL(24, 17, 2);
-  LAUNCH_FILL(28, 25, 3);
-  LAUNCH_FILL(32, 29, 4);
-  LAUNCH_FILL(36, 33, 5);
-  LAUNCH_FILL(40, 37, 6);
-  LAUNCH_FILL(44, 41, 7);
-  LAUNCH_FILL(48, 45, 8);
+  LAUNCH_FILL(8, 1, 1, 0);
+  LAUNCH_FILL(8, 2, 9, 1);
+  LAUNCH_FILL(6, 4, 17, 2);
+  LAUNCH_FILL(7, 4, 25, 3);
+  LAUNCH_FILL(8, 4, 29, 4);
+  LAUNCH_FILL(5, 8, 33, 5);
+  LAUNCH_FILL(6, 8, 41, 6);
 #undef LAUNCH_FILL
   mark(2 + NCLASS, 0);
   hipLaunchKernelGGL(k_big, dim3(BIG_LANES / 64), dim3(64), 0, st, d_windows, ctx->d_big_list,
@@ -968,7 +1277,7 @@ extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows,
   {
     std::lock_guard<std::mutex> lock(ctx->mu);
     if (total > ctx->stage_cap) {
-      hipFree(ctx->d_stage);
+      (void)hipFree(ctx->d_stage);
       ctx->d_stage = nullptr;
       HIPCHK(hipMalloc(&ctx->d_stage, total));
       ctx->stage_cap = total;
@@ -994,9 +1303,8 @@ extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows,
 }
 
 static const char* const kStageNames[] = {
-    "k_plan",         "k_scan+k_scatter", "k_fill<8,1>",    "k_fill<16,9>",  "k_fill<24,17>",
-    "k_fill<28,25>",  "k_fill<32,29>",    "k_fill<36,33>",  "k_fill<40,37>", "k_fill<44,41>",
-    "k_fill<48,45>",  "k_big"};
+    "k_plan",          "k_scan+k_scatter", "k_fill[W1-8]",   "k_fill[W9-16]", "k_fill[W17-24]",
+    "k_fill[W25-28]",  "k_fill[W29-32]",   "k_fill[W33-40]", "k_fill[W41-48]", "k_big"};
 static const int kNStages = (int)(sizeof(kStageNames) / sizeof(kStageNames[0]));
 
 extern "C" const char* gsnapdp_stage_name(int stage) {
@@ -1070,10 +1378,10 @@ extern "C" int gsnapdp_maxent_host(gsnapdp_ctx* ctx, const uint8_t* model, const
     HIPCHK(hipStreamSynchronize(ctx->stream));
     HIPCHK(hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost));
   }
-  hipFree(dm);
-  hipFree(dp);
-  hipFree(dc);
-  hipFree(dout);
+  (void)hipFree(dm);
+  (void)hipFree(dp);
+  (void)hipFree(dc);
+  (void)hipFree(dout);
   return rc;
 }
 

@@ -22,7 +22,7 @@ from .records import MAXENT_IN, PAIR, RESULT, WINDOW  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG, "lib", "libgsnapdp.so")
+LIB_PATH = os.environ.get("GSNAPDP_LIB") or os.path.join(PKG, "lib", "libgsnapdp.so")
 TABLES_PATH = os.path.join(PKG, "data", "maxent_hr_tables.bin")
 
 _lib = None
