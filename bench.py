@@ -32,11 +32,14 @@ from gsnapdp import workload as W  # noqa: E402
 from gsnapdp.records import RESULT  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-VALU_INT32_PEAK = 256 * 128 * 2.4e9  # 256 CU x 4 SIMD x 32 lanes/clk (MI355X_MICROARCH.md) x 2.4 GHz
+# int32 VALU: measured 4 cycles per wave64 instruction on gfx950 (v_max_i32,
+# v_add_u32, v_alignbit_b32; tools/ubench/valu_rate.hip), i.e. 16 lanes/clk per
+# SIMD (fp32 FMA issues at 2 cycles): 256 CU x 4 SIMD x 16 lanes x 2.4 GHz
+VALU_INT32_PEAK = 256 * 4 * 16 * 2.4e9
 OPS_PER_CELL = 14             # gap1 4 + gap2 4 + nogap 6 int32 ops
 READS_PER_GPU = 100_000
 GENOME_NT = 64_000_000
-DOMINANT = "k_fill[W29-32]"   # band width 31..32: 70 % of C2 windows
+DOMINANT = "k_fill"           # every C2 window is a register-band (k_fill) window
 
 
 def window_bytes(w: np.ndarray, nops: np.ndarray) -> np.ndarray:
@@ -142,7 +145,7 @@ def main() -> None:
     res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=RESULT)
     Wd = (batch.windows["extraband"].astype(np.int64) * 2 + 1
           + np.abs(batch.windows["length2"].astype(np.int64) - batch.windows["length1"]))
-    dom = (Wd >= 29) & (Wd <= 32)
+    dom = (Wd <= 48) & (batch.windows["length2"] <= 640)  # k_fill's windows (FAST_WMAX, FAST_L2MAX)
     dom_bytes = float(window_bytes(batch.windows[dom], res["nops"][dom]).sum())
     dom_ms = kernel_ms.get(DOMINANT, float("nan"))
     achieved_gbs = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms == dom_ms else None

@@ -413,8 +413,8 @@ struct ColStream {
 // reachable ones ("Band edges").
 //
 // Per cell the fill streams 4 direction bits (the sign bits of differences,
-// pushed with alignbit: v1 h1 dF dE -> nibble bits 3..0; a jump-late fill
-// stores their complements) and a match bit (consistent_array or uppercase
+// pushed with alignbit into four bit planes v1 | h1 | dF | dE of S bits each;
+// a jump-late fill stores their complements) and a match bit (consistent_array or uppercase
 // equality, dynprog.c:2650-2656) to per-wave scratch.  The traceback is then
 // a backward column sweep over that scratch: every lane reloads the words it
 // wrote (coalesced, prefetched two columns ahead) and the group's traceback
@@ -525,6 +525,10 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
     uint32_t qw, uw, gh, gl, gf;
   };
   auto fetch = [&](int c, ColIn& x) {
+#ifdef EXP_NOLOAD
+    x.qw = 0x41434754u + (uint32_t)c; x.uw = x.qw; x.gh = 0x1234567u * (uint32_t)c; x.gl = x.gh ^ 0x55u; x.gf = 0u;
+    return;
+#endif
     const int qi = qrow0 + qstep * c;
     const int d = min(max(qi >> 2, dlo), dhi);
     x.qw = q4[d];
@@ -581,7 +585,8 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
         fp = f;
       }
     }
-    uint32_t acc = 0u, macc = 0u, gsh = 0u, msh = 0u;
+    // four bit planes (v1, h1, dF, dE), each a short independent chain
+    uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u, macc = 0u, gsh = 0u, msh = 0u;
     auto cell = [&](int s, int Hr, int Er) {
       const int Hd = H[s], Ed = E[s], Fd = F[s];
       const uint32_t pw = P[s];
@@ -590,10 +595,10 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       const int m1 = max(Hd, Ed);
       const int kk = (s < NAB) ? Kab[s < NAB ? s : 0] : K;
       const int hn = max(m1, Fd) + __builtin_amdgcn_sbfe((int)pw, gsh, 4) + kk;
-      acc = push_sign(acc, JL ? (Fd - m1) : (m1 - Fd));  // v1: nogap from gap2
-      acc = push_sign(acc, JL ? (Ed - Hd) : (Hd - Ed));  // h1: nogap from gap1
-      acc = push_sign(acc, JL ? (fp - b) : (b - fp));    // dF: gap2 extends
-      acc = push_sign(acc, JL ? (Er - a) : (a - Er));    // dE: gap1 extends
+      av = push_sign(av, JL ? (Fd - m1) : (m1 - Fd));  // v1: nogap from gap2
+      ah = push_sign(ah, JL ? (Ed - Hd) : (Hd - Ed));  // h1: nogap from gap1
+      af = push_sign(af, JL ? (fp - b) : (b - fp));    // dF: gap2 extends
+      ae = push_sign(ae, JL ? (Er - a) : (a - Er));    // dE: gap1 extends
       macc = (macc << 1) | __builtin_amdgcn_ubfe(pw, msh, 1);
       E[s] = max(a, Er);
       const int f = max(b, fp);
@@ -622,8 +627,13 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
 #pragma unroll
       for (int s = 1; s < S - 1; s++) cell(s, H[s + 1], E[s + 1]);
       cell(S - 1, hb, eb);
+      const uint32_t acc = (((((av << S) | ah) << S) | af) << S) | ae;
+#ifndef EXP_NOSTORE
       Dl[(size_t)c * 64] = acc;
       Ml[(size_t)c * 64] = (uint8_t)macc;
+#else
+      if (acc == 0x12345678u && macc == 77u) Dl[0] = 1u;
+#endif
       // endpoint (L1,L2), captured in the column the window ends (dynprog.c:4545)
       if (__builtin_amdgcn_ballot_w64(c == L2 && j == je) != 0) {
 #pragma unroll
@@ -694,11 +704,13 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       const int d = rr - c + rband;
       return rr >= 1 && c >= 1 && d >= 0 && d <= wband;
     };
-    auto nib = [&](int rr) -> uint32_t {
+    auto nib = [&](int rr) -> uint32_t {  // planes v1 | h1 | dF | dE, S bits each
       const int sg = stop + rr - c + rband;
       const int jj = sg / S, sl = sg - jj * S;
-      const uint32_t x = (jj == jw) ? wv : ldw(c, jj);
-      return ((x >> (4 * (S - 1 - sl))) & 0xFu) ^ inv;
+      const uint32_t x = ((jj == jw) ? wv : ldw(c, jj)) >> (S - 1 - sl);
+      const uint32_t n = (x & 1u) | ((x >> (S - 1)) & 2u) | ((x >> (2 * S - 2)) & 4u) |
+                         ((x >> (3 * S - 3)) & 8u);
+      return n ^ inv;
     };
     auto mbit = [&](int rr) -> uint32_t {
       const int sg = stop + rr - c + rband;
@@ -803,39 +815,94 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   write_result(res + wi, w, L, finalscore, L1, L2, tal, ow);
 }
 
-// One launch per band-width class; a task is one wave of 64/LPW windows.
+// One wave-task of class (S, LPW, LOW): the 64/LPW windows perm[t*NG ..].
+// Not inlined, so each class gets its own register allocation; its pointers
+// carry their address spaces (global / LDS) so that the body still compiles
+// to global_* and ds_* accesses rather than flat ones.
+#define AS_GLOBAL __attribute__((address_space(1)))
+#define AS_LDS __attribute__((address_space(3)))
 template <int S, int LPW, int LOW>
-__global__ __launch_bounds__(256) void k_fill(
-    const gsnapdp_window* __restrict__ Wn, const int* __restrict__ perm,
-    const int* __restrict__ class_start, int cls, const char* __restrict__ q,
-    const char* __restrict__ qu, const uint32_t* __restrict__ blocks, uint64_t nwords,
-    const uint32_t* __restrict__ prof, uint32_t* __restrict__ dirpool, size_t wave_stride,
-    gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
-    const int64_t* __restrict__ op_off) {
+__device__ __noinline__ void fill_task(int t, const AS_GLOBAL gsnapdp_window* Wn1,
+                                       const AS_GLOBAL int* perm1, const AS_GLOBAL char* q1,
+                                       const AS_GLOBAL char* qu1, const AS_GLOBAL uint32_t* blocks1,
+                                       uint64_t nwords, const AS_LDS uint32_t* sprof3,
+                                       AS_GLOBAL uint32_t* D1, AS_GLOBAL gsnapdp_result* res1,
+                                       AS_GLOBAL uint32_t* ops1, const AS_GLOBAL int64_t* op_off1) {
+  const gsnapdp_window* __restrict__ Wn = (const gsnapdp_window*)Wn1;
+  const int* __restrict__ perm = (const int*)perm1;
+  const char* __restrict__ q = (const char*)q1;
+  const char* __restrict__ qu = (const char*)qu1;
+  const uint32_t* __restrict__ blocks = (const uint32_t*)blocks1;
+  const uint32_t* sprof = (const uint32_t*)sprof3;
+  uint32_t* __restrict__ D = (uint32_t*)D1;
+  gsnapdp_result* __restrict__ res = (gsnapdp_result*)res1;
+  uint32_t* __restrict__ ops = (uint32_t*)ops1;
+  const int64_t* __restrict__ op_off = (const int64_t*)op_off1;
   constexpr int NG = 64 / LPW;
+  const int lane = threadIdx.x & 63;
+  uint8_t* M = (uint8_t*)(D + (size_t)(FAST_L2MAX + 4) * 64);
+  const int g = lane / LPW;
+  const int wi0 = perm[(size_t)t * NG + g];
+  const int w0 = __builtin_amdgcn_readfirstlane(perm[(size_t)t * NG]);  // group 0: a real window
+  const bool active = wi0 >= 0;
+  const int wi = active ? wi0 : w0;  // idle groups shadow group 0 (reads only)
+  const int jl = __builtin_amdgcn_readfirstlane((int)Wn[w0].jump_late_p);
+  if (jl)
+    fill_group<S, LPW, LOW, 1>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, res, ops,
+                               op_off);
+  else
+    fill_group<S, LPW, LOW, 0>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, res, ops,
+                               op_off);
+}
+
+// All register-band classes in one persistent launch: the wave-tasks of the
+// classes form one index space (class by class), so one class's tail overlaps
+// the next class's work and empty classes cost nothing.  Register budget:
+// 128 VGPRs (4 waves per SIMD); the few spills this forces sit in the task
+// call's prologue/epilogue and loop preheaders, not in the column loops.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_fill(
+    const gsnapdp_window* __restrict__ Wn, const int* __restrict__ perm,
+    const int* __restrict__ class_start, const char* __restrict__ q, const char* __restrict__ qu,
+    const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
+    uint32_t* __restrict__ dirpool, size_t wave_stride, gsnapdp_result* __restrict__ res,
+    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
   __shared__ uint32_t sprof[SPROF_WORDS];
   for (int i = threadIdx.x; i < SPROF_WORDS; i += blockDim.x)
     sprof[i] = i < UTAB ? prof[i] : (i - UTAB < 128 ? prof[i] : 0u);
   __syncthreads();
-  const int lane = threadIdx.x & 63;
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nw = (gridDim.x * blockDim.x) >> 6;
-  const int t0 = class_start[cls] / NG, t1 = class_start[cls + 1] / NG;
   uint32_t* D = dirpool + (size_t)gw * wave_stride;
-  uint8_t* M = (uint8_t*)(D + (size_t)(FAST_L2MAX + 4) * 64);
-  const int g = lane / LPW;
-  for (int t = t0 + gw; t < t1; t += nw) {
-    const int wi0 = perm[(size_t)t * NG + g];
-    const int w0 = __builtin_amdgcn_readfirstlane(perm[(size_t)t * NG]);  // group 0: a real window
-    const bool active = wi0 >= 0;
-    const int wi = active ? wi0 : w0;  // idle groups shadow group 0 (reads only)
-    const int jl = __builtin_amdgcn_readfirstlane((int)Wn[w0].jump_late_p);
-    if (jl)
-      fill_group<S, LPW, LOW, 1>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, res, ops,
-                                 op_off);
-    else
-      fill_group<S, LPW, LOW, 0>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, res, ops,
-                                 op_off);
+  int tfirst[NCLASS + 1];  // first task index of each class, then the total
+  tfirst[0] = 0;
+#pragma unroll
+  for (int c = 0; c < NCLASS; c++)
+    tfirst[c + 1] = tfirst[c] + (class_start[c + 1] - class_start[c]) / (64 / CLASS_LPW[c]);
+  for (int tau = gw; tau < tfirst[NCLASS]; tau += nw) {
+    int c = 0;
+#pragma unroll
+    for (int k = 1; k < NCLASS; k++) c += tau >= tfirst[k] ? 1 : 0;
+    const int t = class_start[c] / (64 / CLASS_LPW[c]) + (tau - tfirst[c]);
+    switch (c) {
+#define FILL_CASE(C, S_, LPW_, LO)                                                              \
+  case C:                                                                                       \
+    static_assert(CLASS_S[C] == S_ && CLASS_LPW[C] == LPW_ && CLASS_W[C] == S_ * LPW_, "class"); \
+    fill_task<S_, LPW_, LO>(t, (const AS_GLOBAL gsnapdp_window*)Wn, (const AS_GLOBAL int*)perm, \
+                            (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu,                 \
+                            (const AS_GLOBAL uint32_t*)blocks, nwords,                           \
+                            (const AS_LDS uint32_t*)sprof, (AS_GLOBAL uint32_t*)D,               \
+                            (AS_GLOBAL gsnapdp_result*)res, (AS_GLOBAL uint32_t*)ops,            \
+                            (const AS_GLOBAL int64_t*)op_off);                                   \
+    break;
+      FILL_CASE(0, 8, 1, 1)
+      FILL_CASE(1, 8, 2, 9)
+      FILL_CASE(2, 6, 4, 17)
+      FILL_CASE(3, 7, 4, 25)
+      FILL_CASE(4, 8, 4, 29)
+      FILL_CASE(5, 5, 8, 33)
+      FILL_CASE(6, 6, 8, 41)
+#undef FILL_CASE
+    }
   }
 }
 
@@ -1127,7 +1194,7 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
     delete ctx;
     return nullptr;
   }
-  ctx->fill_waves = prop.multiProcessorCount * 16;
+  ctx->fill_waves = prop.multiProcessorCount * 16;  // 4 waves per SIMD (k_fill's register budget)
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     return fail("stream", e);
   if ((e = hipMalloc(&ctx->d_blocks, (nwords + 8) * 4)) != hipSuccess) return fail("malloc blocks", e);
@@ -1235,26 +1302,16 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   mark(1, 1);
   const int blocks = (int)(ctx->dirpool_waves / 4);
   const uint64_t nw = (uint64_t)ctx->nwords;
-#define LAUNCH_FILL(S_, LPW_, LO, CLS)                                                          \
-  mark(2 + CLS, 0);                                                                             \
-  hipLaunchKernelGGL((k_fill<S_, LPW_, LO>), dim3(blocks), dim3(256), 0, st, d_windows,         \
-                     ctx->d_perm, class_start, CLS, d_query, d_query_uc, ctx->d_blocks, nw,     \
-                     ctx->d_prof, ctx->d_dirpool, WAVE_STRIDE_DW, d_results, d_ops,             \
-                     d_op_offsets);                                                             \
-  mark(2 + CLS, 1)
-  LAUNCH_FILL(8, 1, 1, 0);
-  LAUNCH_FILL(8, 2, 9, 1);
-  LAUNCH_FILL(6, 4, 17, 2);
-  LAUNCH_FILL(7, 4, 25, 3);
-  LAUNCH_FILL(8, 4, 29, 4);
-  LAUNCH_FILL(5, 8, 33, 5);
-  LAUNCH_FILL(6, 8, 41, 6);
-#undef LAUNCH_FILL
-  mark(2 + NCLASS, 0);
+  mark(2, 0);
+  hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, st, d_windows, ctx->d_perm, class_start,
+                     d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_dirpool,
+                     WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets);
+  mark(2, 1);
+  mark(3, 0);
   hipLaunchKernelGGL(k_big, dim3(BIG_LANES / 64), dim3(64), 0, st, d_windows, ctx->d_big_list,
                      big_count, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
                      ctx->d_bigpool, BIG_LANE_STRIDE_DW, d_results, d_ops, d_op_offsets);
-  mark(2 + NCLASS, 1);
+  mark(3, 1);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1302,9 +1359,7 @@ extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows,
   return 0;
 }
 
-static const char* const kStageNames[] = {
-    "k_plan",          "k_scan+k_scatter", "k_fill[W1-8]",   "k_fill[W9-16]", "k_fill[W17-24]",
-    "k_fill[W25-28]",  "k_fill[W29-32]",   "k_fill[W33-40]", "k_fill[W41-48]", "k_big"};
+static const char* const kStageNames[] = {"k_plan", "k_scan+k_scatter", "k_fill", "k_big"};
 static const int kNStages = (int)(sizeof(kStageNames) / sizeof(kStageNames[0]));
 
 extern "C" const char* gsnapdp_stage_name(int stage) {
