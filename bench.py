@@ -65,6 +65,21 @@ def band_cells(w: np.ndarray) -> int:
     return total
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/*_traffic.json, written by tools/pmc_traffic.py), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel") == kernel:
+            best = (d["traffic_bytes"], os.path.basename(f))
+    return best
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -152,6 +167,7 @@ def main() -> None:
     cells = band_cells(batch.windows)
     fill_ms = sum(v for k, v in kernel_ms.items() if k.startswith("k_fill"))
 
+    traffic = pmc_traffic(DOMINANT)
     out = None
     if rank == 0:
         cpu = None
@@ -199,7 +215,9 @@ def main() -> None:
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2) if achieved_gbs else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 5) if achieved_gbs else None,
-                         "traffic": None, "kernel": DOMINANT,
+                         "traffic": traffic[0] if traffic else None,
+                         "traffic_source": traffic[1] if traffic else None,
+                         "algorithmic_bytes": round(dom_bytes), "kernel": DOMINANT,
                          "kernel_ms": round(dom_ms, 4), "windows_in_kernel": int(dom.sum())},
             "roofline_valu": {"bound": "valu-int32", "unit": "int32 ops/s",
                               "achieved": round(cells * OPS_PER_CELL / (fill_ms * 1e-3), 1) if fill_ms else None,

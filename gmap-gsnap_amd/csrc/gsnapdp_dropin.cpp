@@ -1,0 +1,318 @@
+// gsnapdp_dropin.cpp -- the reference's per-call entry points (include/
+// gsnapdp_dropin.h) over the batched C-ABI of include/gsnapdp.h.
+//
+// Each gap-filler call becomes a batch of one window: the query bytes the
+// reference would read are staged, the GPU runs fill + endpoint + traceback,
+// and the op stream is expanded into pairs that are pushed into the caller's
+// Pairpool so that the returned List_T is the reference's, cell for cell.
+// There is no CPU fallback: without a gfx950 device the first call aborts,
+// as the reference aborts on its own fatal conditions.
+#include <dlfcn.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gsnapdp.h"
+#include "../../include/gsnapdp_dropin.h"
+#include "gsnapdp_internal.h"
+
+namespace {
+
+struct Dynprog {  // the Dynprog_T workspace: only its length limits matter here
+  int maxlength1, maxlength2;
+};
+
+struct State {
+  std::mutex mu;
+  int mode = 0;
+  const unsigned int* blocks = nullptr;
+  size_t nwords = 0;
+  int device = 0;
+  gsnapdp_ctx* ctx = nullptr;
+  bool tables = false;
+  std::vector<char> q, qu;
+  std::vector<uint32_t> ops;
+  std::vector<gsnapdp_pair> pairs;
+};
+State g;
+
+[[noreturn]] void fatal(const std::string& msg) {
+  fprintf(stderr, "gsnapdp drop-in: %s\n", msg.c_str());
+  abort();
+}
+
+// Context on first use (after Dynprog_init and Gsnapdp_dropin_genome).
+gsnapdp_ctx* ctx() {
+  if (g.ctx) return g.ctx;
+  if (!g.blocks) fatal("no genome: call Gsnapdp_dropin_genome(blocks, nwords, device) after Genome_new");
+  g.ctx = gsnapdp_create(g.device, g.blocks, g.nwords, g.mode);
+  if (!g.ctx) fatal(std::string("gsnapdp_create: ") + gsnapdp_last_error());
+  return g.ctx;
+}
+
+// MaxEnt tables: $GSNAPDP_MAXENT_TABLES, else <libdir>/../data/maxent_hr_tables.bin
+void ensure_tables() {
+  if (g.tables) return;
+  std::string path;
+  if (const char* e = getenv("GSNAPDP_MAXENT_TABLES")) {
+    path = e;
+  } else {
+    Dl_info info;
+    if (dladdr((void*)&ensure_tables, &info) && info.dli_fname) {
+      path = info.dli_fname;
+      path = path.substr(0, path.rfind('/')) + "/../data/maxent_hr_tables.bin";
+    }
+  }
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) fatal("cannot open MaxEnt tables " + path);
+  std::vector<double> t(12 * 16384 + 4 * 16);
+  const size_t n = fread(t.data(), sizeof(double), t.size(), f);
+  fclose(f);
+  if (n != t.size()) fatal("short MaxEnt table file " + path);
+  if (gsnapdp_load_maxent_tables(ctx(), t.data(), t.size()))
+    fatal(std::string("load tables: ") + gsnapdp_last_error());
+  g.tables = true;
+}
+
+// One window through the GPU; pushes its pairs (final list order) into the
+// pool, last pair first, so the list head is the first pair.
+gsnapdp_List_T run_one(gsnapdp_window& w, const char* seq, const char* sequc, bool rev,
+                       gsnapdp_Pairpool_T pool, int* dynprogindex, int* finalscore,
+                       int* nmatches, int* nmismatches, int* nopens, int* nindels) {
+  std::lock_guard<std::mutex> lock(g.mu);
+  gsnapdp_ctx* c = ctx();
+  const int L1 = w.length1 > 0 ? w.length1 : 0;
+  // query bytes the reference may read: sequence1[0..L1) or revsequence1[-(L1-1)..0]
+  g.q.assign((size_t)L1 + 8, 0);
+  g.qu.assign((size_t)L1 + 8, 0);
+  if (L1 > 0) {
+    const char* s = rev ? seq - (L1 - 1) : seq;
+    const char* u = rev ? sequc - (L1 - 1) : sequc;
+    memcpy(g.q.data(), s, (size_t)L1);
+    memcpy(g.qu.data(), u, (size_t)L1);
+  }
+  w.qpos = rev ? (uint32_t)(L1 > 0 ? L1 - 1 : 0) : 0u;
+  const int64_t cap = (int64_t)L1 + (w.length2 > 0 ? w.length2 : 0) + 2;
+  const int64_t off[2] = {0, cap};
+  g.ops.assign((size_t)cap + 1, 0u);
+  gsnapdp_result r;
+  if (gsnapdp_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, g.ops.data(), off))
+    fatal(std::string("gsnapdp_run_host: ") + gsnapdp_last_error());
+  if (r.status == gsnapdp::ST_UNSUPPORTED)
+    fatal("window outside the reference's domain (the reference aborts here)");
+  if (r.status == gsnapdp::ST_OPS_OVERFLOW) fatal("op stream overflow");
+  g.pairs.resize((size_t)cap + 8);
+  int fs = 0;
+  const int n = gsnapdp_expand(c, &w, &r, g.ops.data(), g.q.data(), g.qu.data(), g.pairs.data(),
+                               (int)g.pairs.size(), &fs);
+  if (n < 0 || n > (int)g.pairs.size()) fatal("gsnapdp_expand failed");
+  *dynprogindex = r.reserved;  // the stepped *dynprogindex
+  *finalscore = r.finalscore;
+  *nmatches = r.nmatches;
+  *nmismatches = r.nmismatches;
+  *nopens = r.nopens;
+  *nindels = r.nindels;
+  gsnapdp_List_T list = nullptr;
+  for (int i = n - 1; i >= 0; i--) {
+    const gsnapdp_pair& p = g.pairs[(size_t)i];
+    if (p.gapp)
+      list = Pairpool_push_gapholder(list, pool, p.queryjump, p.genomejump, /*knownp*/ 0);
+    else
+      list = Pairpool_push(list, pool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome,
+                           p.dynprogindex);
+  }
+  return list;
+}
+
+gsnapdp_window base_window(int kind, int length1, int length2, int offset1, int offset2,
+                           unsigned chroffset, unsigned chrhigh, unsigned chrpos,
+                           unsigned genomiclength, int cdna_direction, int watsonp,
+                           int jump_late_p, int extraband, double defect_rate,
+                           const Dynprog* dp, int dynprogindex) {
+  gsnapdp_window w;
+  memset(&w, 0, sizeof(w));
+  w.kind = kind;
+  w.length1 = length1;
+  w.length2 = length2;
+  w.offset1 = offset1;
+  w.offset2 = offset2;
+  w.chroffset = chroffset;
+  w.chrhigh = chrhigh;
+  w.chrpos = chrpos;
+  w.genomiclength = genomiclength;
+  w.cdna_direction = cdna_direction;
+  w.extraband = extraband;
+  w.dynprogindex = dynprogindex;
+  w.maxlength1 = dp->maxlength1;
+  w.maxlength2 = dp->maxlength2;
+  // only the bin matters (dynprog.c:4471-4486): keep the double comparison exact
+  w.defect_rate = defect_rate < 0.003 ? 0.001f : (defect_rate < 0.014 ? 0.01f : 0.5f);
+  w.watsonp = watsonp ? 1 : 0;
+  w.jump_late_p = jump_late_p ? 1 : 0;
+  return w;
+}
+
+double maxent_one(int model, unsigned splice_pos, unsigned chroffset) {
+  std::lock_guard<std::mutex> lock(g.mu);
+  ensure_tables();
+  const uint8_t m = (uint8_t)model;
+  double out = 0.0;
+  if (gsnapdp_maxent_host(ctx(), &m, &splice_pos, &chroffset, &out, 1))
+    fatal(std::string("maxent: ") + gsnapdp_last_error());
+  return out;
+}
+
+}  // namespace
+
+extern "C" {
+
+int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device) {
+  std::lock_guard<std::mutex> lock(g.mu);
+  if (g.ctx && (blocks != g.blocks || nwords != g.nwords)) fatal("genome changed after first use");
+  g.blocks = blocks;
+  g.nwords = nwords;
+  g.device = device;
+  return 0;
+}
+
+char* Dynprog_endalign_string(gsnapdp_Endalign_T endalign) {  // dynprog.c:335-345
+  switch (endalign) {
+    case GSNAPDP_QUERYEND_GAP: return (char*)"queryend_gap";
+    case GSNAPDP_QUERYEND_INDELS: return (char*)"queryend_indels";
+    case GSNAPDP_QUERYEND_NOGAPS: return (char*)"queryend_nogaps";
+    case GSNAPDP_BEST_LOCAL: return (char*)"best_local";
+    default:
+      printf("endalign %d not recognized\n", endalign);
+      return (char*)"";
+  }
+}
+
+// Known-site data only feeds Dynprog_genome_gap / splicejunction paths, which
+// this library does not serve yet; the genome arrives through
+// Gsnapdp_dropin_genome.
+void Dynprog_setup(gsnapdp_bool, gsnapdp_IIT_T, int*, int, int, gsnapdp_Genomicpos_T*,
+                   gsnapdp_Splicetype_T*, gsnapdp_Genomicpos_T*, int, unsigned int*,
+                   unsigned int*, unsigned int*, unsigned int*, gsnapdp_Genome_T) {}
+
+int Dynprog_score(int matches, int mismatches, int qopens, int qindels, int topens, int tindels,
+                  double defect_rate) {  // dynprog.c:381-394 (open -10, extend -3 in every bin)
+  const int mism = defect_rate < 0.003 ? -3 : (defect_rate < 0.014 ? -2 : -1);
+  return 3 * matches + mism * mismatches - 10 * qopens - 3 * qindels - 10 * topens - 3 * tindels;
+}
+
+gsnapdp_Dynprog_T Dynprog_new(int maxlookback, int extraquerygap, int maxpeelback,
+                              int extramaterial_end, int extramaterial_paired) {
+  // compute_maxlengths, dynprog.c:831-852 (QUERY_MAXLENGTH 500, GENOMIC_MAXLENGTH 2000)
+  int m1 = maxlookback + maxpeelback;
+  if (m1 < 500) m1 = 500;
+  int m2 = m1 + extraquerygap + (extramaterial_end > extramaterial_paired ? extramaterial_end
+                                                                           : extramaterial_paired);
+  if (m2 < 2000) m2 = 2000;
+  Dynprog* d = new Dynprog{m1, m2};
+  return (gsnapdp_Dynprog_T)d;
+}
+
+void Dynprog_free(gsnapdp_Dynprog_T* old) {
+  if (old && *old) {
+    delete (Dynprog*)*old;
+    *old = nullptr;
+  }
+}
+
+int Dynprog_pairdistance(int c1, int c2) {  // dynprog.c:1048 (HIGHQ table)
+  return gsnapdp::host_pairdistance(0, c1, c2);
+}
+
+void Dynprog_term(void) {
+  std::lock_guard<std::mutex> lock(g.mu);
+  if (g.ctx) gsnapdp_destroy(g.ctx);
+  g.ctx = nullptr;
+  g.tables = false;
+}
+
+void Dynprog_init(int, int, int, int, int, gsnapdp_Mode_T mode) {  // dynprog.c:1339
+  std::lock_guard<std::mutex> lock(g.mu);
+  g.mode = mode;
+  uint32_t prof[gsnapdp::PROF_WORDS];
+  gsnapdp::build_profile_table(mode, prof);  // pairdistance_init for Dynprog_pairdistance
+}
+
+gsnapdp_List_T Dynprog_single_gap(
+    int* dynprogindex, int* finalscore, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* sequence1, char* sequenceuc1, char*, char*,
+    int length1, int length2, int offset1, int offset2, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_single,
+    double defect_rate, int /*close_indels_mode: no effect, SURVEY A.14*/,
+    gsnapdp_bool widebandp) {
+  gsnapdp_window w = base_window(GSNAPDP_SINGLE_GAP, length1, length2, offset1, offset2,
+                                 chroffset, chrhigh, chrpos, genomiclength, cdna_direction,
+                                 watsonp, jump_late_p, extraband_single, defect_rate,
+                                 (const Dynprog*)dynprog, *dynprogindex);
+  w.widebandp = widebandp ? 1 : 0;
+  return run_one(w, sequence1, sequenceuc1, false, pairpool, dynprogindex, finalscore, nmatches,
+                 nmismatches, nopens, nindels);
+}
+
+gsnapdp_List_T Dynprog_end5_gap(
+    int* dynprogindex, int* finalscore, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* revsequence1, char* revsequenceuc1, char*,
+    char*, int length1, int length2, int revoffset1, int revoffset2,
+    gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_end,
+    double defect_rate, gsnapdp_Endalign_T endalign, gsnapdp_bool /*use_genomicseg_p*/) {
+  gsnapdp_window w = base_window(GSNAPDP_END5_GAP, length1, length2, revoffset1, revoffset2,
+                                 chroffset, chrhigh, chrpos, genomiclength, cdna_direction,
+                                 watsonp, jump_late_p, extraband_end, defect_rate,
+                                 (const Dynprog*)dynprog, *dynprogindex);
+  w.widebandp = 1;
+  w.endalign = (uint8_t)endalign;
+  return run_one(w, revsequence1, revsequenceuc1, true, pairpool, dynprogindex, finalscore,
+                 nmatches, nmismatches, nopens, nindels);
+}
+
+gsnapdp_List_T Dynprog_end3_gap(
+    int* dynprogindex, int* finalscore, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* sequence1, char* sequenceuc1, char*, char*,
+    int length1, int length2, int offset1, int offset2, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_end,
+    double defect_rate, gsnapdp_Endalign_T endalign, gsnapdp_bool /*use_genomicseg_p*/) {
+  gsnapdp_window w = base_window(GSNAPDP_END3_GAP, length1, length2, offset1, offset2, chroffset,
+                                 chrhigh, chrpos, genomiclength, cdna_direction, watsonp,
+                                 jump_late_p, extraband_end, defect_rate,
+                                 (const Dynprog*)dynprog, *dynprogindex);
+  w.widebandp = 1;
+  w.endalign = (uint8_t)endalign;
+  return run_one(w, sequence1, sequenceuc1, false, pairpool, dynprogindex, finalscore, nmatches,
+                 nmismatches, nopens, nindels);
+}
+
+void Maxent_hr_setup(unsigned int* ref_blocks) {  // maxent_hr.c:27195
+  std::lock_guard<std::mutex> lock(g.mu);
+  if (g.blocks && ref_blocks != g.blocks) fatal("Maxent_hr_setup blocks differ from the genome");
+  if (!g.blocks) g.blocks = ref_blocks;  // length still needed: Gsnapdp_dropin_genome
+}
+
+double Maxent_hr_donor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomicpos_T chroffset) {
+  return maxent_one(GSNAPDP_DONOR, splice_pos, chroffset);
+}
+double Maxent_hr_acceptor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomicpos_T chroffset) {
+  return maxent_one(GSNAPDP_ACCEPTOR, splice_pos, chroffset);
+}
+double Maxent_hr_antidonor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomicpos_T chroffset) {
+  return maxent_one(GSNAPDP_ANTIDONOR, splice_pos, chroffset);
+}
+double Maxent_hr_antiacceptor_prob(gsnapdp_Genomicpos_T splice_pos,
+                                   gsnapdp_Genomicpos_T chroffset) {
+  return maxent_one(GSNAPDP_ANTIACCEPTOR, splice_pos, chroffset);
+}
+
+}  // extern "C"

@@ -1,0 +1,118 @@
+/*
+ * gsnapdp_dropin.h -- the reference's own per-call entry points, served by
+ * the MI355X engine (libgsnapdp_dropin.so replaces dynprog.o + maxent_hr.o in
+ * the gmap / gsnap link).
+ *
+ * Every prototype below is ABI-identical to the reference declaration it
+ * cites (GMAP/GSNAP 2012-07-03, non-PMAP build): `bool` is the reference's
+ * `typedef unsigned char bool` (bool.h:7), Genomicpos_T / UINT4 are
+ * `unsigned int` (types.h:12, genomicpos.h:9), the enums are int-sized, and
+ * Dynprog_T / List_T / Pairpool_T / IIT_T / Genome_T are opaque pointers.
+ * When compiled inside the reference tree, include the reference headers
+ * instead of this one; the symbols are the same.
+ *
+ * Output pairs are materialised with the host program's own
+ * Pairpool_push / Pairpool_push_gapholder (pairpool.c:169, 352), in the
+ * reference's list order, so callers cannot tell the difference.
+ *
+ * Per call these run a batch of one window on the GPU (a few tens of
+ * microseconds of launch latency); the throughput path is the batched
+ * C-ABI of gsnapdp.h.
+ */
+#ifndef GSNAPDP_DROPIN_H
+#define GSNAPDP_DROPIN_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef unsigned char gsnapdp_bool;                 /* bool.h:7 */
+typedef unsigned int gsnapdp_Genomicpos_T;          /* genomicpos.h:9 */
+typedef int gsnapdp_Endalign_T;                     /* dynprog.h:8 */
+typedef int gsnapdp_Mode_T;                         /* mode.h */
+typedef int gsnapdp_Splicetype_T;                   /* splicetrie_build.h */
+typedef struct Dynprog_T *gsnapdp_Dynprog_T;        /* dynprog.h:9 (opaque) */
+typedef struct List_T *gsnapdp_List_T;              /* list.h:6 */
+typedef struct Pairpool_T *gsnapdp_Pairpool_T;      /* pairpool.h */
+typedef struct IIT_T *gsnapdp_IIT_T;                /* iit-read.h */
+typedef struct Genome_T *gsnapdp_Genome_T;          /* genome.h */
+
+/* --- provided by the host program (reference pairpool.c), used by the shim --- */
+gsnapdp_List_T Pairpool_push(gsnapdp_List_T list, gsnapdp_Pairpool_T pool, int querypos,
+                             int genomepos, char cdna, char comp, char genome,
+                             int dynprogindex);                     /* pairpool.h:24 */
+gsnapdp_List_T Pairpool_push_gapholder(gsnapdp_List_T list, gsnapdp_Pairpool_T pool,
+                                       int queryjump, int genomejump,
+                                       gsnapdp_bool knownp);        /* pairpool.h:28 */
+
+/* --- setup / workspace (dynprog.h:34-72) --- */
+char* Dynprog_endalign_string(gsnapdp_Endalign_T endalign);                    /* dynprog.c:335 */
+void Dynprog_setup(gsnapdp_bool novelsplicingp, gsnapdp_IIT_T splicesites_iit,
+                   int* splicesites_divint_crosstable, int donor_typeint, int acceptor_typeint,
+                   gsnapdp_Genomicpos_T* splicesites, gsnapdp_Splicetype_T* splicetypes,
+                   gsnapdp_Genomicpos_T* splicedists, int nsplicesites,
+                   unsigned int* trieoffsets_obs, unsigned int* triecontents_obs,
+                   unsigned int* trieoffsets_max, unsigned int* triecontents_max,
+                   gsnapdp_Genome_T genome);                                   /* dynprog.c:350 */
+int Dynprog_score(int matches, int mismatches, int qopens, int qindels, int topens, int tindels,
+                  double defect_rate);                                         /* dynprog.c:381 */
+gsnapdp_Dynprog_T Dynprog_new(int maxlookback, int extraquerygap, int maxpeelback,
+                              int extramaterial_end, int extramaterial_paired); /* dynprog.c:856 */
+void Dynprog_free(gsnapdp_Dynprog_T* old);                                     /* dynprog.c:877 */
+int Dynprog_pairdistance(int c1, int c2);                                      /* dynprog.c:1049 */
+void Dynprog_term(void);                                                       /* dynprog.c:1348 */
+void Dynprog_init(int maxlookback, int extraquerygap, int maxpeelback, int extramaterial_end,
+                  int extramaterial_paired, gsnapdp_Mode_T mode);              /* dynprog.c:1339 */
+
+/* --- the gap fillers served by the GPU (dynprog.h:74-160) --- */
+gsnapdp_List_T Dynprog_single_gap(
+    int* dynprogindex, int* finalscore, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* sequence1, char* sequenceuc1,
+    char* sequence2, char* sequenceuc2, int length1, int length2, int offset1, int offset2,
+    gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_single,
+    double defect_rate, int close_indels_mode, gsnapdp_bool widebandp); /* dynprog.c:4450 */
+
+gsnapdp_List_T Dynprog_end5_gap(
+    int* dynprogindex, int* finalscore, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* revsequence1, char* revsequenceuc1,
+    char* revsequence2, char* revsequenceuc2, int length1, int length2, int revoffset1,
+    int revoffset2, gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh,
+    gsnapdp_Genomicpos_T chrpos, gsnapdp_Genomicpos_T genomiclength, int cdna_direction,
+    gsnapdp_bool watsonp, gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool,
+    int extraband_end, double defect_rate, gsnapdp_Endalign_T endalign,
+    gsnapdp_bool use_genomicseg_p);                                     /* dynprog.c:5094 */
+
+gsnapdp_List_T Dynprog_end3_gap(
+    int* dynprogindex, int* finalscore, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* sequence1, char* sequenceuc1,
+    char* sequence2, char* sequenceuc2, int length1, int length2, int offset1, int offset2,
+    gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_end,
+    double defect_rate, gsnapdp_Endalign_T endalign,
+    gsnapdp_bool use_genomicseg_p);                                     /* dynprog.c:5556 */
+
+/* --- MaxEnt splice-site probabilities (maxent_hr.h:6-19) --- */
+void Maxent_hr_setup(unsigned int* ref_blocks);                                 /* maxent_hr.c:27195 */
+double Maxent_hr_donor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomicpos_T chroffset);
+double Maxent_hr_acceptor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomicpos_T chroffset);
+double Maxent_hr_antidonor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomicpos_T chroffset);
+double Maxent_hr_antiacceptor_prob(gsnapdp_Genomicpos_T splice_pos,
+                                   gsnapdp_Genomicpos_T chroffset);
+
+/* --- one addition: the reference hands the packed genome to Genome_T /
+ * Maxent_hr_setup without its length; the host calls this once after
+ * Genome_new (gmap.c:3801 / gsnap.c:1064), before the first DP call. ---
+ * `blocks` = Genome_blocks(genome), `nwords` = its length in UINT4 words
+ * (3 per 32 nt plus the reference's padding).  `device` = HIP device index. */
+int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSNAPDP_DROPIN_H */

@@ -1,0 +1,162 @@
+"""The reference-ABI drop-in (libgsnapdp_dropin.so, include/gsnapdp_dropin.h):
+the per-call Dynprog_* / Maxent_hr_* entry points a gmap/gsnap link would
+resolve, driven exactly like the reference's callers do (stage3.c), with the
+host program's Pairpool replaced by a test double (tests/dropin/)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from gsnapdp.records import END3_GAP, END5_GAP, PAIR, SINGLE_GAP
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DROPIN = os.path.join(ROOT, "gmap-gsnap_amd", "lib", "libgsnapdp_dropin.so")
+HEADER = os.path.join(ROOT, "include", "gsnapdp_dropin.h")
+DOUBLE_SRC = os.path.join(ROOT, "tests", "dropin", "pairpool_double.c")
+
+REC = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("queryjump", "<i4"), ("genomejump", "<i4"),
+                ("dynprogindex", "<i4"), ("cdna", "S1"), ("comp", "S1"), ("genome", "S1"), ("gapp", "u1")])
+assert REC.itemsize == PAIR.itemsize
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    names = re.findall(r"\b((?:Dynprog|Maxent_hr|Gsnapdp_dropin)_\w+)\s*\(", text)
+    return sorted(set(names))
+
+
+def test_dropin_exports_every_declared_entry_point():
+    assert os.path.exists(DROPIN), "build with `make -C gmap-gsnap_amd`"
+    out = subprocess.run(["nm", "-D", "--defined-only", DROPIN], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r" T (\w+)", out))
+    missing = [f for f in declared_functions() if f not in exported]
+    assert not missing, missing
+    # the pair pool comes from the host program, never from the shim
+    undef = subprocess.run(["nm", "-D", "--undefined-only", DROPIN], capture_output=True, text=True,
+                           check=True).stdout
+    assert "Pairpool_push" in undef and "Pairpool_push_gapholder" in undef
+
+
+def test_dropin_host_helpers_match_reference(tmp_path):
+    """Dynprog_new's length limits (dynprog.c:831-852), Dynprog_score (:381) and
+    Dynprog_pairdistance (:1049) need no GPU."""
+    dbl = load_double(tmp_path)
+    L = ctypes.CDLL(DROPIN)
+    L.Dynprog_new.restype = ctypes.c_void_p
+    L.Dynprog_new.argtypes = [ctypes.c_int] * 5
+    d = L.Dynprog_new(600, 10, 11, 10, 8)
+    lens = (ctypes.c_int * 2).from_address(d)
+    assert (lens[0], lens[1]) == (611, 2000)
+    L.Dynprog_free(ctypes.byref(ctypes.c_void_p(d)))
+    L.Dynprog_score.argtypes = [ctypes.c_int] * 6 + [ctypes.c_double]
+    assert L.Dynprog_score(100, 2, 1, 3, 0, 0, 0.001) == 300 - 6 - 10 - 9
+    assert L.Dynprog_score(100, 2, 1, 3, 0, 0, 0.01) == 300 - 4 - 10 - 9
+    assert L.Dynprog_score(100, 2, 1, 3, 1, 1, 0.5) == 300 - 2 - 10 - 9 - 10 - 3
+    L.Dynprog_init(600, 10, 11, 10, 8, 0)
+    assert L.Dynprog_pairdistance(ord("A"), ord("A")) == 3
+    assert L.Dynprog_pairdistance(ord("A"), ord("C")) == -3
+    assert L.Dynprog_pairdistance(ord("N"), ord("A")) == -1
+    assert L.Dynprog_pairdistance(ord("z"), ord("z")) == 0  # c2 < 'z' quirk (dynprog.c:1151)
+    L.Dynprog_endalign_string.restype = ctypes.c_char_p
+    assert L.Dynprog_endalign_string(3) == b"best_local"
+    del dbl
+
+
+def load_double(tmp_path):
+    so = os.path.join(str(tmp_path), "libpairpool_double.so")
+    subprocess.check_call(["gcc", "-O1", "-shared", "-fPIC", "-o", so, DOUBLE_SRC])
+    lib = ctypes.CDLL(so, mode=ctypes.RTLD_GLOBAL)  # resolves the shim's Pairpool_push*
+    lib.dbl_list_read.restype = ctypes.c_int
+    lib.dbl_list_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    lib.dbl_list_free.argtypes = [ctypes.c_void_p]
+    return lib
+
+
+GAP_ARGS = ([ctypes.c_void_p] * 7 + [ctypes.c_char_p] * 4 + [ctypes.c_int] * 4 + [ctypes.c_uint] * 4
+            + [ctypes.c_int, ctypes.c_ubyte, ctypes.c_ubyte, ctypes.c_void_p, ctypes.c_int, ctypes.c_double])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,limit", [("dp_chr17_mix", 400), ("dp_synth_cmet", 150)])
+def test_dropin_gap_fillers_match_reference_golden(golden_dir, tmp_path, name, limit):
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    dbl = load_double(tmp_path)
+    L = ctypes.CDLL(DROPIN)
+    L.Dynprog_new.restype = ctypes.c_void_p
+    L.Dynprog_new.argtypes = [ctypes.c_int] * 5
+    L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    for f in ("Dynprog_single_gap", "Dynprog_end5_gap", "Dynprog_end3_gap"):
+        getattr(L, f).restype = ctypes.c_void_p
+    L.Dynprog_single_gap.argtypes = GAP_ARGS + [ctypes.c_int, ctypes.c_ubyte]
+    L.Dynprog_end5_gap.argtypes = GAP_ARGS + [ctypes.c_int, ctypes.c_ubyte]
+    L.Dynprog_end3_gap.argtypes = GAP_ARGS + [ctypes.c_int, ctypes.c_ubyte]
+    blocks = np.ascontiguousarray(z["blocks"])
+    L.Dynprog_init(600, 10, 11, 10, 8, int(z["mode"]))
+    L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
+    dp = L.Dynprog_new(600, 10, 11, 10, 8)
+    q = np.ascontiguousarray(z["query"])
+    qu = np.ascontiguousarray(z["query_uc"])
+    qaddr, uaddr = q.ctypes.data, qu.ctypes.data
+    offs = np.zeros(len(z["npairs"]) + 1, dtype=np.int64)
+    np.cumsum(z["npairs"], out=offs[1:])
+    out = np.zeros(8192, dtype=REC)
+    W = z["windows"]
+    n = min(limit, len(W))
+    for i in range(n):
+        w = W[i]
+        ints = [ctypes.c_int(int(w["dynprogindex"]))] + [ctypes.c_int(0) for _ in range(5)]
+        seq = ctypes.c_char_p(qaddr + int(w["qpos"]))
+        sequc = ctypes.c_char_p(uaddr + int(w["qpos"]))
+        common = [ctypes.byref(x) for x in ints] + [dp, seq, sequc, None, None,
+                                                    int(w["length1"]), int(w["length2"]),
+                                                    int(w["offset1"]), int(w["offset2"]),
+                                                    int(w["chroffset"]), int(w["chrhigh"]),
+                                                    int(w["chrpos"]), int(w["genomiclength"]),
+                                                    int(w["cdna_direction"]), int(w["watsonp"]),
+                                                    int(w["jump_late_p"]), None, int(w["extraband"]),
+                                                    float(w["defect_rate"])]
+        kind = int(w["kind"])
+        if kind == SINGLE_GAP:
+            lst = L.Dynprog_single_gap(*common, 0, int(w["widebandp"]))
+        elif kind == END5_GAP:
+            lst = L.Dynprog_end5_gap(*common, int(w["endalign"]), 0)
+        else:
+            assert kind == END3_GAP
+            lst = L.Dynprog_end3_gap(*common, int(w["endalign"]), 0)
+        got = [x.value for x in ints]
+        want = [int(z[f][i]) for f in ("dynprogindex", "finalscore", "nmatches", "nmismatches", "nopens",
+                                       "nindels")]
+        assert got == want, (name, i, got, want)
+        k = dbl.dbl_list_read(lst, out.ctypes.data, out.size)
+        ref = z["pairs"][offs[i]:offs[i + 1]]
+        assert k == ref.size, (name, i, k, ref.size)
+        assert out[:k].tobytes() == ref.tobytes(), (name, i)
+        dbl.dbl_list_free(lst)
+    L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dp)))
+    L.Dynprog_term()  # releases the device context (the genome array dies with this test)
+
+
+@pytest.mark.gpu
+def test_dropin_maxent_matches_reference_golden(golden_dir, tmp_path):
+    z = np.load(os.path.join(golden_dir, "maxent_chr17.npz"), allow_pickle=False)
+    load_double(tmp_path)
+    L = ctypes.CDLL(DROPIN)
+    blocks = np.ascontiguousarray(z["blocks"])
+    L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
+    L.Maxent_hr_setup.argtypes = [ctypes.c_void_p]
+    L.Maxent_hr_setup(blocks.ctypes.data)
+    fns = [L.Maxent_hr_donor_prob, L.Maxent_hr_acceptor_prob, L.Maxent_hr_antidonor_prob,
+           L.Maxent_hr_antiacceptor_prob]
+    for f in fns:
+        f.restype = ctypes.c_double
+        f.argtypes = [ctypes.c_uint, ctypes.c_uint]
+    idx = np.linspace(0, z["model"].size - 1, 200).astype(int)
+    for i in idx:
+        got = fns[int(z["model"][i])](int(z["splice_pos"][i]), int(z["chroffset"][i]))
+        assert np.float64(got).tobytes() == np.float64(z["prob"][i]).tobytes(), i
+    L.Dynprog_term()

@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of one kernel from two rocprofv3 --pmc passes.
+
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR OUT_JSON
+
+FETCH_SIZE / WRITE_SIZE are in KB per dispatch.  On gfx950 FETCH_SIZE counts
+half the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM), so the read
+side is doubled; WRITE_SIZE is taken as is.  Both are uncalibrated for this
+kernel's dword-wide accesses (Measurement).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_dispatch(d, counter, ksub):
+    vals = {}
+    for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter and ksub in r["Kernel_Name"]:
+                key = r.get("Dispatch_Id") or r.get("Correlation_Id") or str(len(vals))
+                vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
+    if not vals:
+        raise SystemExit("no %s rows for %s in %s" % (counter, ksub, d))
+    return sum(vals.values()) / len(vals), len(vals)
+
+
+def main():
+    fdir, wdir, ksub, out = sys.argv[1:5]
+    fetch_kb, nf = per_dispatch(fdir, "FETCH_SIZE", ksub)
+    write_kb, nw = per_dispatch(wdir, "WRITE_SIZE", ksub)
+    res = {"kernel": ksub, "dispatches": [nf, nw], "fetch_size_kb": round(fetch_kb, 1),
+           "write_size_kb": round(write_kb, 1),
+           "traffic_bytes": round((2.0 * fetch_kb + write_kb) * 1024.0),
+           "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halving)"}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
