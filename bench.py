@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
 
 import torch  # noqa: E402
 
-from gsnapdp import Context, op_offsets  # noqa: E402
+from gsnapdp import Context, op_offsets, shard  # noqa: E402
 from gsnapdp import workload as W  # noqa: E402
 from gsnapdp.records import RESULT  # noqa: E402
 
@@ -89,21 +89,15 @@ def main() -> None:
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    ranks = shard.init_from_env("nccl")
+    world, rank, local = ranks.world, ranks.rank, ranks.local
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
     # ---- workload (identical genome on every rank, a disjoint read shard per rank)
     genome = W.synthetic_genome(GENOME_NT, seed=1)
     blocks = W.pack_genome(genome)
-    batch = W.c2_windows(genome, n=args.reads, seed=2 + rank)
+    batch = W.c2_windows(genome, n=args.reads, seed=shard.shard_seed(2, rank))
     n = len(batch)
     off = op_offsets(batch.windows)
     ctx = Context(blocks, mode=0, device=local)
@@ -120,32 +114,18 @@ def main() -> None:
         ctx.run_device(d_w.data_ptr(), n, d_q.data_ptr(), d_u.data_ptr(), d_res.data_ptr(),
                        d_ops.data_ptr(), d_off.data_ptr())
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
+    def sync():
+        ctx.sync()
+        torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step()
-    ctx.sync()
-    torch.cuda.synchronize()
+    sync()
 
-    # ---- timed region: exactly K steps, barrier + sync on both sides
-    barrier()
-    ctx.sync()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    ctx.sync()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    # ---- timed region: exactly K steps, barrier + sync on both sides, max over ranks
+    elapsed = shard.timed_steps(ranks, step, args.steps, sync)
     ms_per_step = 1000.0 * elapsed / args.steps
-    value = world * n * args.steps / elapsed
+    value = shard.aggregate_rate(n, ranks, args.steps, elapsed)
 
     # ---- per-kernel durations (HIP events on the launch stream), same K steps
     names = ctx.profile(True)
@@ -231,9 +211,7 @@ def main() -> None:
             "parity": parity,
         }
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    shard.finish(ranks)
     ctx.close()
 
 
