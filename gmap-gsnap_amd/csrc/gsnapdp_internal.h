@@ -16,7 +16,7 @@ namespace gsnapdp {
 constexpr int NEG = -1000000;          // NEG_INFINITY, dynprog.c:119
 constexpr int MICROINTRON_LENGTH = 9;  // dynprog.c:139
 constexpr int FAST_L2MAX = 640;        // longest genome span handled by the register-band kernel
-// band-width classes, one k_fill launch each: W in (CLASS_W[c-1], CLASS_W[c]].
+// band-width classes of k_fill: W in (CLASS_W[c-1], CLASS_W[c]].
 // A window of class c is spread over CLASS_LPW[c] lanes of CLASS_S[c] diagonals
 // each (CLASS_S * CLASS_LPW = CLASS_W), so a wave carries 64 / LPW windows.
 constexpr int NCLASS = 7;
@@ -29,8 +29,9 @@ GSNAPDP_HD_CONST inline int class_of_w(int W) {
   while (c < NCLASS - 1 && W > CLASS_W[c]) c++;
   return c;
 }
-// bucket key = ((W * (FAST_WMAX+1) + lband) * 6 + jl*3 + mode), W <= 48, lband <= 47
-constexpr int NKEYS = (FAST_WMAX + 1) * (FAST_WMAX + 1) * 6;
+// k_fill bucket key = (W * (FAST_WMAX+1) + lband) * 2 + jump_late (W <= 48, lband <= 48)
+constexpr int NKEYS = (FAST_WMAX + 1) * (FAST_WMAX + 1) * 2;
+constexpr int KEYS_PER_W = (FAST_WMAX + 1) * 2;
 constexpr int BIG_LANES = 256;         // lanes of the generic (global-memory band) kernel
 constexpr int BIG_WMAX = 2048;
 constexpr int BIG_L2MAX = 2048;

@@ -246,6 +246,9 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
                        const int64_t* __restrict__ op_off, int* __restrict__ keys,
                        int* __restrict__ hist, int* __restrict__ big_list,
                        int* __restrict__ big_count) {
+  __shared__ int lh[NKEYS];  // block-local histogram: one global atomic per key per block
+  for (int k = threadIdx.x; k < NKEYS; k += blockDim.x) lh[k] = 0;
+  __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   int key = -1, big = -1;
   if (i < n) {
@@ -278,15 +281,18 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
       ow.flush();
       write_result(&res[i], w, L, 0, m, m, t, ow);
     } else if (L.d.mode == 0 && L.d.W <= FAST_WMAX && L.d.L2 <= FAST_L2MAX) {
-      key = ((L.d.W * (FAST_WMAX + 1) + L.d.lband) * 6) + L.d.jl * 3 + L.d.mode;
+      key = (L.d.W * (FAST_WMAX + 1) + L.d.lband) * 2 + L.d.jl;
     } else {
       big = 0;
     }
     keys[i] = key;
   }
-  agg_atomic_inc(hist, key);
+  if (key >= 0) atomicAdd(&lh[key], 1);
   const int slot = agg_atomic_inc(big_count, big);
   if (big == 0) big_list[slot] = i;
+  __syncthreads();
+  for (int k = threadIdx.x; k < NKEYS; k += blockDim.x)
+    if (lh[k] > 0) atomicAdd(&hist[k], lh[k]);
 }
 
 // Exclusive scan of bucket sizes, each padded to whole waves of its class
@@ -294,12 +300,14 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
 // class_start[c] = first perm entry of class c (a multiple of its wave size,
 // since wave sizes shrink as W grows and are powers of two).
 __device__ inline int padded_bucket(int k, int h) {
-  const int ng = 64 / CLASS_LPW[class_of_w(k / ((FAST_WMAX + 1) * 6))];
+  const int ng = 64 / CLASS_LPW[class_of_w(k / KEYS_PER_W)];
   return (h + ng - 1) / ng * ng;
 }
 
+// Also writes -1 into every bucket's padding entries of perm, so perm needs
+// no clearing.
 __global__ void k_scan(const int* __restrict__ hist, int* __restrict__ cursor,
-                       int* __restrict__ class_start) {
+                       int* __restrict__ class_start, int* __restrict__ perm) {
   __shared__ int part[1024];
   const int tid = threadIdx.x;
   const int per = (NKEYS + 1023) / 1024;
@@ -316,15 +324,17 @@ __global__ void k_scan(const int* __restrict__ hist, int* __restrict__ cursor,
   }
   int run = part[tid] - s;
   for (int k = lo; k < hi; k++) {
+    const int h = hist[k], p = padded_bucket(k, h);
     cursor[k] = run;
-    run += padded_bucket(k, hist[k]);
+    for (int e = run + h; e < run + p; e++) perm[e] = -1;
+    run += p;
   }
   __syncthreads();
   if (tid == 0) {
     // class c covers W in (CLASS_W[c-1], CLASS_W[c]]; keys are W-major
     int wlo = 0;
     for (int c = 0; c < NCLASS; c++) {
-      const int kfirst = (wlo + 1) * (FAST_WMAX + 1) * 6;
+      const int kfirst = (wlo + 1) * KEYS_PER_W;
       class_start[c] = kfirst < NKEYS ? cursor[kfirst] : part[1023];
       wlo = CLASS_W[c];
     }
@@ -332,12 +342,20 @@ __global__ void k_scan(const int* __restrict__ hist, int* __restrict__ cursor,
   }
 }
 
+// Block-local ranks (LDS atomics), one global reservation per key per block.
 __global__ void k_scatter(const int* __restrict__ keys, int n, int* __restrict__ cursor,
                           int* __restrict__ perm) {
+  __shared__ int lh[NKEYS];
+  for (int k = threadIdx.x; k < NKEYS; k += blockDim.x) lh[k] = 0;
+  __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int k = i < n ? keys[i] : -1;
-  const int pos = agg_atomic_inc(cursor, k);
-  if (k >= 0) perm[pos] = i;
+  const int key = i < n ? keys[i] : -1;
+  const int rank = key >= 0 ? atomicAdd(&lh[key], 1) : 0;
+  __syncthreads();
+  for (int k = threadIdx.x; k < NKEYS; k += blockDim.x)
+    if (lh[k] > 0) lh[k] = atomicAdd(&cursor[k], lh[k]);  // the block's base in bucket k
+  __syncthreads();
+  if (key >= 0) perm[lh[key] + rank] = i;
 }
 
 // ------------------------------------------------------------------ k_fill
@@ -421,6 +439,20 @@ struct ColStream {
 // lane walks the reference's traceback (dynprog.c:2611-2712) one column per
 // step, so no step waits on a dependent global load.
 constexpr int ABOVE_BIAS = -(1 << 29);
+constexpr int FILL_SC_BIAS = 6;  // -2 * SINGLE_EXTEND (dynprog.c:222)
+
+// k_fill's LDS profile word: each signed 4-bit pairdistance nibble s becomes
+// the unsigned nibble s + 6 (s in -5..3, so 1..9); match bits unchanged.
+__device__ inline uint32_t fill_profile_word(uint32_t w) {
+  uint32_t o = w & 0xFF000000u;
+#pragma unroll
+  for (int g = 0; g < 6; g++) {
+    const int n = (int)((w >> (4 * g)) & 0xFu);
+    const int sn = n >= 8 ? n - 16 : n;
+    o |= (uint32_t)((sn + FILL_SC_BIAS) & 0xF) << (4 * g);
+  }
+  return o;
+}
 constexpr int UTAB = 4 * 128;  // LDS profile: 4 x 128 pairdistance words, then 256 uppercase words
 constexpr int SPROF_WORDS = 4 * 128 + 256;
 
@@ -479,10 +511,11 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
     dhi = (L.qstep > 0 ? L.qbase + (L1v - 1) : L.qbase) >> 2;
   }
   maxL2 = __builtin_amdgcn_readfirstlane(wave_max(L2));
-  const int K = -2 * ext;
+  // the nogap step's constant -2*extend (= +6: k_fill serves single gaps, extend -3)
+  // is folded into the LDS profile nibbles (FILL_SC_BIAS); above-band slots add a bias
   int Kab[NAB > 0 ? NAB : 1];
 #pragma unroll
-  for (int s = 0; s < NAB; s++) Kab[s] = K + ((j * S + s < stop) ? ABOVE_BIAS : 0);
+  for (int s = 0; s < NAB; s++) Kab[s] = (j * S + s < stop) ? ABOVE_BIAS : 0;
   const int row0 = j * S - stop - rband;  // row of local slot 0 at column 0
 
   // profile word of row r from LDS; rows outside 1..L1 get a neutral word
@@ -563,9 +596,10 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   const int se = stop + L1 - L2 + rband;  // global slot of the endpoint (L1,L2)
   const int je = se / S, sle = se - je * S;
   // scratch layout: column c's words are D[c*64 + (j*NG + g)], one 256-byte
-  // row per column (coalesced stores); the match bytes likewise in M
-  uint32_t* Dl = D + j * NG + g;
-  uint8_t* Ml = M + j * NG + g;
+  // row per column (coalesced stores); the match bytes likewise in M.  Lane
+  // (j, g) stores column c = t - j at the wave-uniform row t-(LPW-1) plus a
+  // non-negative lane offset.
+  const int lane_off = (LPW - 1 - j) * 64 + j * NG + g;
 
   // One skewed step.  MASKED steps (the first and last LPW-1) leave lanes
   // whose column is outside 1..maxL2 untouched.
@@ -593,8 +627,8 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       const int a = Hr + open;
       const int b = hp + open;
       const int m1 = max(Hd, Ed);
-      const int kk = (s < NAB) ? Kab[s < NAB ? s : 0] : K;
-      const int hn = max(m1, Fd) + __builtin_amdgcn_sbfe((int)pw, gsh, 4) + kk;
+      const int sc = (int)__builtin_amdgcn_ubfe(pw, gsh, 4);  // pairdistance - 2*extend
+      const int hn = (s < NAB) ? max(m1, Fd) + sc + Kab[s < NAB ? s : 0] : max(m1, Fd) + sc;
       av = push_sign(av, JL ? (Fd - m1) : (m1 - Fd));  // v1: nogap from gap2
       ah = push_sign(ah, JL ? (Ed - Hd) : (Hd - Ed));  // h1: nogap from gap1
       af = push_sign(af, JL ? (fp - b) : (b - fp));    // dF: gap2 extends
@@ -629,10 +663,10 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       cell(S - 1, hb, eb);
       const uint32_t acc = (((((av << S) | ah) << S) | af) << S) | ae;
 #ifndef EXP_NOSTORE
-      Dl[(size_t)c * 64] = acc;
-      Ml[(size_t)c * 64] = (uint8_t)macc;
+      D[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = acc;
+      M[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = (uint8_t)macc;
 #else
-      if (acc == 0x12345678u && macc == 77u) Dl[0] = 1u;
+      if (acc == 0x12345678u && macc == 77u) D[0] = 1u;
 #endif
       // endpoint (L1,L2), captured in the column the window ends (dynprog.c:4545)
       if (__builtin_amdgcn_ballot_w64(c == L2 && j == je) != 0) {
@@ -868,7 +902,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
   __shared__ uint32_t sprof[SPROF_WORDS];
   for (int i = threadIdx.x; i < SPROF_WORDS; i += blockDim.x)
-    sprof[i] = i < UTAB ? prof[i] : (i - UTAB < 128 ? prof[i] : 0u);
+    sprof[i] = i < UTAB ? fill_profile_word(prof[i]) : (i - UTAB < 128 ? prof[i] : 0u);
   __syncthreads();
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nw = (gridDim.x * blockDim.x) >> 6;
@@ -1279,10 +1313,7 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   int* big_count = class_start + NCLASS + 1;
   HIPCHK(hipMemsetAsync(hist, 0, (size_t)NKEYS * 4, st));
   HIPCHK(hipMemsetAsync(big_count, 0, 4, st));
-  // perm padding entries must read -1; only the used prefix matters
-  const size_t used = ((size_t)n + (size_t)NKEYS * 64 + 63) & ~(size_t)63;
-  HIPCHK(hipMemsetAsync(ctx->d_perm, 0xFF, (used < ctx->perm_cap ? used : ctx->perm_cap) * 4, st));
-  const int tb = 256, nb = (n + tb - 1) / tb;
+  const int tb = 1024, nb = (n + tb - 1) / tb;
   // stage timing: events on the launch stream around each kernel
   auto mark = [&](int stage, int end) {
     if (!ctx->prof_on) return;
@@ -1297,7 +1328,7 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
                      d_op_offsets, ctx->d_keys, hist, ctx->d_big_list, big_count);
   mark(0, 1);
   mark(1, 0);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, hist, cursor, class_start);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, hist, cursor, class_start, ctx->d_perm);
   hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(tb), 0, st, ctx->d_keys, n, cursor, ctx->d_perm);
   mark(1, 1);
   const int blocks = (int)(ctx->dirpool_waves / 4);
