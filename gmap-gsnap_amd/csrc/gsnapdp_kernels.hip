@@ -712,48 +712,64 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
 #endif
   if (!active || j != 0) return;
 
-  // ---- traceback (dynprog.c:2611-2712), one column per step on the group's
-  // lane 0.  The direction words of the lane that holds the path's current
-  // diagonal arrive four columns per load, two groups ahead; a gap that moves
-  // the path to another lane's slots costs one dependent load.
+  // ---- traceback (dynprog.c:2611-2712) on the group's lane 0, as a backward
+  // sweep in which every lane visits the same column at the same time (a
+  // window waits until the sweep reaches its own L2).  The path's current
+  // diagonal (slot, owning lane, bit position) stays in registers, so a
+  // diagonal step costs a few ALU ops; the direction and match words of that
+  // lane arrive four columns per group, one group ahead.  VERT / HORIZ runs
+  // take the general path; a gap that moves the path to another lane's slots
+  // costs one dependent load.
   const gsnapdp_window w = Wn[wi];
   const Lane L = make_lane(w);
-  enum { T_DIAG = 0, T_VERT = 1, T_HORIZ = 2, T_DONE = 3 };
-  int st = T_DIAG;
+  enum { T_WAIT = 0, T_DIAG = 1, T_VERT = 2, T_HORIZ = 3, T_DONE = 4 };
+  int st = T_WAIT;
   int r = L1, dist = 0;
+  int jj = 0, pb = 0;  // DIAG: lane holding the path's diagonal, bit of its slot in each plane
   Tally tal = {0, 0, 0, 0};
   OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
-  const uint32_t inv = JL ? 0xFu : 0u;
+  const uint32_t jlbit = JL ? 1u : 0u;
   const int wband = lband + rband;
   const uint32_t* Dg = D + g;
   const uint8_t* Mg = M + g;
-  auto jj_of = [&](int rr, int cc) {
+  auto set_diag = [&](int rr, int cc) {
     const int sg = stop + rr - cc + rband;
-    return sg < 0 ? 0 : (sg >= WMAX ? LPW - 1 : sg / S);
+    const int sgc = sg < 0 ? 0 : (sg >= WMAX ? WMAX - 1 : sg);  // out of band: DONE next
+    jj = sgc / S;
+    pb = S - 1 - (sgc - jj * S);
   };
-  auto ldw = [&](int cc, int jj) -> uint32_t { return Dg[(size_t)cc * 64 + jj * NG]; };
-  auto ldm = [&](int cc, int jj) -> uint32_t { return Mg[(size_t)cc * 64 + jj * NG]; };
-  auto column = [&](int c, uint32_t wv, uint32_t mv, int jw) {
+  auto ldw = [&](int cc, int jw) -> uint32_t { return Dg[(size_t)cc * 64 + jw * NG]; };
+  auto ldm = [&](int cc, int jw) -> uint32_t { return Mg[(size_t)cc * 64 + jw * NG]; };
+  struct Grp {
+    uint32_t w[4], m[4];
+    int jw;
+  };
+  auto fetch_group = [&](Grp& x, int G, int jw) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int cc = 4 * G + k;
+      x.w[k] = ldw(cc, jw);
+      x.m[k] = ldm(cc, jw);
+    }
+    x.jw = jw;
+  };
+  auto column = [&](int c, uint32_t wk, uint32_t mk, int jw) {
     auto inb = [&](int rr) {
       const int d = rr - c + rband;
       return rr >= 1 && c >= 1 && d >= 0 && d <= wband;
     };
-    auto nib = [&](int rr) -> uint32_t {  // planes v1 | h1 | dF | dE, S bits each
+    auto plane_bit = [&](int rr, int plane) -> uint32_t {  // planes dE | dF | h1 | v1 from bit 0
       const int sg = stop + rr - c + rband;
-      const int jj = sg / S, sl = sg - jj * S;
-      const uint32_t x = ((jj == jw) ? wv : ldw(c, jj)) >> (S - 1 - sl);
-      const uint32_t n = (x & 1u) | ((x >> (S - 1)) & 2u) | ((x >> (2 * S - 2)) & 4u) |
-                         ((x >> (3 * S - 3)) & 8u);
-      return n ^ inv;
+      const int jr = sg / S, sl = sg - jr * S;
+      const uint32_t x = (jr == jw) ? wk : ldw(c, jr);
+      return ((x >> (plane * S + S - 1 - sl)) & 1u) ^ jlbit;
     };
-    auto mbit = [&](int rr) -> uint32_t {
-      const int sg = stop + rr - c + rband;
-      const int jj = sg / S, sl = sg - jj * S;
-      const uint32_t x = (jj == jw) ? mv : ldm(c, jj);
-      return (x >> (S - 1 - sl)) & 1u;
-    };
+    if (st == T_WAIT && c == L2) {
+      st = T_DIAG;
+      set_diag(r, c);
+    }
     if (st == T_VERT) {  // gap2 chain in this column (add_queryskip, dynprog.c:2372)
-      while (c == 0 ? (r >= 2 && r <= lband && r <= L1) : (inb(r) && (nib(r) & 2u))) {
+      while (c == 0 ? (r >= 2 && r <= lband && r <= L1) : (inb(r) && plane_bit(r, 1))) {
         dist++;
         r--;
       }
@@ -763,9 +779,10 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       tal.nopens++;
       tal.nindels += dist;
       st = T_DIAG;
+      set_diag(r, c);
     }
     if (st == T_HORIZ) {  // gap1 chain, one column per step (add_genomeskip, dynprog.c:2416)
-      const bool more = (r == 0) ? (c >= 2 && c <= rband && c <= L2) : (inb(r) && (nib(r) & 1u));
+      const bool more = (r == 0) ? (c >= 2 && c <= rband && c <= L2) : (inb(r) && plane_bit(r, 0));
       if (more) {
         dist++;
       } else {
@@ -786,21 +803,23 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
           tal.nindels += dist;
         }
         st = T_DIAG;
+        set_diag(r, c - 1);
       }
     } else if (st == T_DIAG) {
       if (!inb(r)) {
         st = T_DONE;
       } else {
-        const uint32_t nb = nib(r);
+        const uint32_t x = ((jj == jw) ? wk : ldw(c, jj)) >> pb;
         if (c >= cvlo && c <= cvhi) {  // not a '*' column (dynprog.c:2644)
-          if (mbit(r)) tal.nmatches++;
-          else tal.nmismatches++;
+          const uint32_t mb = (((jj == jw) ? mk : ldm(c, jj)) >> pb) & 1u;
+          tal.nmatches += (int)mb;
+          tal.nmismatches += 1 - (int)mb;
         }
         ow.run++;
-        if (nb & 8u) {
+        if (((x >> (3 * S)) & 1u) ^ jlbit) {  // v1: VERT
           st = T_VERT;
           dist = 1;
-        } else if (nb & 4u) {
+        } else if (((x >> (2 * S)) & 1u) ^ jlbit) {  // h1: HORIZ
           st = T_HORIZ;
           dist = 1;
         }
@@ -808,43 +827,55 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       }
     }
   };
-  // groups of four columns (4G .. 4G+3), two groups in flight
-  struct Grp {
-    uint32_t w[4], m[4];
-    int jw;
-  };
-  auto fetch_group = [&](Grp& x, int G, int jj) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int cc = 4 * G + k;
-      x.w[k] = ldw(cc, jj);
-      x.m[k] = ldm(cc, jj);
-    }
-    x.jw = jj;
-  };
-  // ga holds the current group, gb the next one (loaded a group ahead)
-  int c = L2;
-  int G = c >> 2;
-  int jp = jj_of(r, L2);
+  // wave-uniform sweep from the wave's longest window down to column -1
+  int G = maxL2 >> 2;
+  set_diag(L1, L2);
   Grp ga, gb;
-  fetch_group(ga, G, jp);
-  fetch_group(gb, G >= 1 ? G - 1 : 0, jp);
-  for (; c >= 0 && st != T_DONE; c--) {
+  fetch_group(ga, G, jj);
+  fetch_group(gb, G >= 1 ? G - 1 : 0, jj);
+  const uint32_t invall = JL ? 0xFFFFFFFFu : 0u;
+  bool fast4 = false;
+  for (int c = maxL2; c >= 0; c--) {
     const int k = c & 3;
-    uint32_t wv = ga.w[0], mv = ga.m[0];
-#pragma unroll
-    for (int kk = 1; kk < 4; kk++) {
-      wv = (k == kk) ? ga.w[kk] : wv;
-      mv = (k == kk) ? ga.m[kk] : mv;
+    if (k == 3) {
+      // Four diagonal steps at once: the path stays on its diagonal through
+      // columns c .. c-3 (no v1/h1 there), inside the band and the query, and
+      // the four columns are all inside or all outside the window's genome.
+      const int dd = (S - 1 - pb) + jj * S - stop;  // the diagonal's offset in the band
+      fast4 = st == T_DIAG && jj == ga.jw && r >= 4 && c >= 4 && dd >= 0 && dd <= wband;
+      if (fast4) {
+        const uint32_t x0 = (ga.w[0] ^ invall) >> pb, x1 = (ga.w[1] ^ invall) >> pb;
+        const uint32_t x2 = (ga.w[2] ^ invall) >> pb, x3 = (ga.w[3] ^ invall) >> pb;
+        const bool inside = c - 3 >= cvlo && c <= cvhi;
+        const bool outside = c < cvlo || c - 3 > cvhi;
+        const uint32_t vh = (1u << (2 * S)) | (1u << (3 * S));  // h1 and v1 of this slot
+        fast4 = ((x0 | x1 | x2 | x3) & vh) == 0u && (inside || outside);
+        if (fast4) {
+          if (inside) {
+            const int mcount = (int)(((ga.m[0] >> pb) & 1u) + ((ga.m[1] >> pb) & 1u) +
+                                     ((ga.m[2] >> pb) & 1u) + ((ga.m[3] >> pb) & 1u));
+            tal.nmatches += mcount;
+            tal.nmismatches += 4 - mcount;
+          }
+          ow.run += 4;
+          r -= 4;
+        }
+      }
     }
-    column(c, wv, mv, ga.jw);
+    if (!fast4 && st != T_DONE && (st != T_WAIT || c == L2)) {
+      const uint32_t wk = k == 0 ? ga.w[0] : k == 1 ? ga.w[1] : k == 2 ? ga.w[2] : ga.w[3];
+      const uint32_t mk = k == 0 ? ga.m[0] : k == 1 ? ga.m[1] : k == 2 ? ga.m[2] : ga.m[3];
+      column(c, wk, mk, ga.jw);
+    }
     if (k == 0) {  // leaving group G
+      if (__builtin_amdgcn_ballot_w64(st != T_DONE) == 0) break;
       ga = gb;
       G--;
-      if (G >= 1) fetch_group(gb, G - 1, jj_of(r, c - 1));  // the path's diagonal, predicted unchanged
+      if (G >= 1) fetch_group(gb, G - 1, jj);  // the path's diagonal, predicted unchanged
+      fast4 = false;
     }
   }
-  if (st != T_DONE) column(-1, 0u, 0u, -1);
+  if (st != T_DONE && st != T_WAIT) column(-1, 0u, 0u, -1);
   ow.flush();
   write_result(res + wi, w, L, finalscore, L1, L2, tal, ow);
 }
