@@ -467,24 +467,44 @@ __device__ inline int from_lane_below(int v) {
   return __builtin_amdgcn_mov_dpp(v, 0x101, 0xF, 0xF, true);  // row_shl:1
 }
 
+// Per-wave LDS rings of k_fill (sizes per band class): for each window of the
+// wave, the profile words of the rows its lanes' bottom slots will need and the
+// genome classes of the columns they will need, staged RING_K columns at a time.
+constexpr int RING_K = 16;
+constexpr int pow2ceil(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+template <int S, int LPW>
+struct Rings {
+  static constexpr int NG = 64 / LPW;
+  static constexpr int SPAN = (LPW - 1) * (S - 1);  // rows between the group's bottom slots
+  static constexpr int RR = pow2ceil(RING_K + SPAN);
+  static constexpr int CR = pow2ceil(RING_K + LPW - 1);
+  static constexpr int WORDS = NG * RR + (NG * CR + 3) / 4;
+};
+constexpr int RING_WORDS_MAX = 1280;  // max Rings<S,LPW>::WORDS over the classes (checked below)
+
 template <int S, int LPW, int LOW, int JL>
 __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool active, int lane,
                            uint32_t* __restrict__ D, uint8_t* __restrict__ M,
                            const char* __restrict__ q, const char* __restrict__ qu,
                            const uint32_t* __restrict__ blocks, uint64_t nwords,
-                           const uint32_t* sprof, gsnapdp_result* __restrict__ res,
-                           uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
+                           const uint32_t* sprof, uint32_t* ring,
+                           gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
+                           const int64_t* __restrict__ op_off) {
   static_assert(S >= 2 && S <= 8 && LPW <= 16 && 64 % LPW == 0, "class shape");
+  using RG = Rings<S, LPW>;
+  static_assert(RG::WORDS <= RING_WORDS_MAX, "LDS ring budget");
   constexpr int WMAX = S * LPW;
   constexpr int NG = 64 / LPW;
   constexpr int NAB = (WMAX - LOW) < S ? (WMAX - LOW) : S;  // local slots that may lie above the band
   const int j = lane % LPW;
   const int gbase = lane - j;
   const int g = lane / LPW;
-  int lband, rband, open, ext, L1, L2, stop, maxL2, mtoff, cvlo, cvhi;
-  int qrow0, qstep, dlo, dhi, xorc;  // query byte of the bottom row at column c: qrow0 + qstep*c
-  uint32_t gp0;                      // genome position of column c: gp0 + gps*c
-  int gps;
+  int lband, rband, open, ext, L1, L2, stop, maxL2, mtoff, cvlo, cvhi, qbase, qstep, xorc, gps;
+  uint32_t gp0;  // genome position of column c: gp0 + gps*c
   {
     const Lane L = make_lane(Wn[wi]);
     lband = __builtin_amdgcn_readfirstlane(L.d.lband);  // wave-uniform (bucket key)
@@ -502,13 +522,8 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
     gp0 = cs.P0;
     gps = cs.PS;
     xorc = cs.xorc;
-    // bottom slot of this lane holds row j*S - stop - rband + S - 1 + c at column c
-    const int rbot0 = j * S - stop - rband + S - 1;
+    qbase = L.qbase;
     qstep = L.qstep;
-    qrow0 = L.qbase + L.qstep * (rbot0 - 1);
-    const int L1v = L.d.L1;  // the window's query bytes (rows 1..L1) bound every read
-    dlo = (L.qstep > 0 ? L.qbase : L.qbase - (L1v - 1)) >> 2;
-    dhi = (L.qstep > 0 ? L.qbase + (L1v - 1) : L.qbase) >> 2;
   }
   maxL2 = __builtin_amdgcn_readfirstlane(wave_max(L2));
   // the nogap step's constant -2*extend (= +6: k_fill serves single gaps, extend -3)
@@ -518,80 +533,83 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   for (int s = 0; s < NAB; s++) Kab[s] = (j * S + s < stop) ? ABOVE_BIAS : 0;
   const int row0 = j * S - stop - rband;  // row of local slot 0 at column 0
 
-  // profile word of row r from LDS; rows outside 1..L1 get a neutral word
-  // (their cells never feed a reachable in-band cell)
-  auto profw = [&](int r, uint32_t qb, uint32_t ub) -> uint32_t {
-    const bool ok = r >= 1 && r <= L1;
-    return sprof[mtoff + (ok ? (qb & 127u) : 0u)] | sprof[UTAB + (ok ? ub : 255u)];
+  // profile word of row r; rows outside 1..L1 get a neutral word (their cells
+  // never feed a reachable in-band cell)
+  auto row_word = [&](int r) -> uint32_t {
+    uint32_t qb = 0u, ub = 255u;
+    if (r >= 1 && r <= L1) {
+      const int qi = qbase + qstep * (r - 1);
+      qb = (unsigned char)q[qi] & 127u;
+      ub = (unsigned char)qu[qi];
+    }
+    return sprof[mtoff + qb] | sprof[UTAB + ub];
   };
+  const uint64_t gmax = nwords >= 3 ? (nwords - 3) / 3 : 0;  // last whole genome block
 
   int H[S], E[S], F[S];
   uint32_t P[S];
-  // column 0 (dynprog.c:1460-1488) in offset coordinates; rows come from global
-  // memory once here, then only the bottom row enters per column
-  {
-    const Lane L = make_lane(Wn[wi]);
+  // column 0 (dynprog.c:1460-1488) in offset coordinates
 #pragma unroll
-    for (int s = 0; s < S; s++) {
-      const int r = row0 + s;
-      H[s] = (r == 0) ? 0 : NEG;
-      E[s] = NEG;
-      F[s] = (r >= 1) ? open : NEG;  // open + r*ext - r*ext
-      uint32_t qb = 0u, ub = 255u;
-      if (r >= 1 && r <= L1) {
-        const int qi = L.qbase + L.qstep * (r - 1);
-        qb = (unsigned char)q[qi];
-        ub = (unsigned char)qu[qi];
-      }
-      P[s] = profw(r, qb, ub);
-    }
+  for (int s = 0; s < S; s++) {
+    const int r = row0 + s;
+    H[s] = (r == 0) ? 0 : NEG;
+    E[s] = NEG;
+    F[s] = (r >= 1) ? open : NEG;  // open + r*ext - r*ext
+    P[s] = row_word(r);
   }
-  // Per-column inputs of a lane: the dwords holding its bottom row's query
-  // bytes and the 32-nt genome block of its column.  In the steady state they
-  // are loaded two columns ahead into alternating buffers (no register copy
-  // of a load in flight), and turned into the profile word / genome class one
-  // column ahead.
-  const uint32_t* q4 = (const uint32_t*)q;
-  const uint32_t* u4 = (const uint32_t*)qu;
-  const uint64_t gmax = nwords >= 3 ? (nwords - 3) / 3 : 0;  // last whole block
-  struct ColIn {
-    uint32_t qw, uw, gh, gl, gf;
+  // Rings: lane j of a window stages the rows / columns congruent to j mod
+  // LPW.  Lane j's bottom slot holds row t + j*(S-1) + rbase at step t, its
+  // column is t - j.  Before step 1: rows [1+rbase, K+rbase+SPAN], columns
+  // [1, K]; after step t = nK: rows (t+rbase+SPAN, t+K+rbase+SPAN], columns
+  // (t, t+K].  Same-wave LDS writes are visible to later reads in order.
+  uint32_t* rr = ring + g * RG::RR;
+  uint8_t* cr = (uint8_t*)(ring + NG * RG::RR) + g * RG::CR;
+  const int rbase = S - 1 - stop - rband;
+  auto stage = [&](auto nrows_tag, int rlo, int clo) {
+    constexpr int NR = decltype(nrows_tag)::value;
+    constexpr int ER = (NR + LPW - 1) / LPW, EC = (RING_K + LPW - 1) / LPW;
+    // all loads first (clamped addresses, no branches), then the words
+    uint32_t qb[ER], ub[ER], gw[EC], gf[EC];
+#pragma unroll
+    for (int e = 0; e < ER; e++) {
+      const int r = rlo + e * LPW + j;
+      const int rc = (r >= 1 && r <= L1) ? r : 1;
+      const int qi = qbase + qstep * (rc - 1);
+      qb[e] = (unsigned char)q[qi];
+      ub[e] = (unsigned char)qu[qi];
+    }
+#pragma unroll
+    for (int e = 0; e < EC; e++) {
+      const int c = clo + e * LPW + j;
+      const uint32_t pos = gp0 + (uint32_t)(gps * c);
+      const uint64_t b = (uint64_t)(pos >> 5);
+      const uint64_t ptr = (b <= gmax ? b : gmax) * 3u;
+      gw[e] = blocks[ptr + ((pos & 31u) < 16 ? 1 : 0)];
+      gf[e] = blocks[ptr + 2];
+    }
+#pragma unroll
+    for (int e = 0; e < ER; e++) {
+      const int r = rlo + e * LPW + j;
+      const bool ok = r >= 1 && r <= L1;
+      const uint32_t w = sprof[mtoff + (ok ? (qb[e] & 127u) : 0u)] | sprof[UTAB + (ok ? ub[e] : 255u)];
+      if (e * LPW + j < NR) rr[r & (RG::RR - 1)] = w;
+    }
+#pragma unroll
+    for (int e = 0; e < EC; e++) {
+      const int c = clo + e * LPW + j;
+      const uint32_t pos = gp0 + (uint32_t)(gps * c);
+      const uint32_t bit = pos & 31u;
+      const bool ing = (uint64_t)(pos >> 5) <= gmax;  // outside the genome: N
+      const int code = (int)((gw[e] >> ((bit & 15u) * 2u)) & 3u) ^ xorc;
+      const bool inr = c >= cvlo && c <= cvhi;
+      const int k = !inr ? 5 : ((!ing || ((gf[e] >> bit) & 1u)) ? 4 : code);
+      if (e * LPW + j < RING_K) cr[c & (RG::CR - 1)] = (uint8_t)k;
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // nothing of the staging stays in flight into the column loop
   };
-  auto fetch = [&](int c, ColIn& x) {
-#ifdef EXP_NOLOAD
-    x.qw = 0x41434754u + (uint32_t)c; x.uw = x.qw; x.gh = 0x1234567u * (uint32_t)c; x.gl = x.gh ^ 0x55u; x.gf = 0u;
-    return;
-#endif
-    const int qi = qrow0 + qstep * c;
-    const int d = min(max(qi >> 2, dlo), dhi);
-    x.qw = q4[d];
-    x.uw = u4[d];
-    const uint64_t b = (uint64_t)((gp0 + (uint32_t)(gps * c)) >> 5);
-    const uint64_t ptr = (b <= gmax ? b : gmax) * 3u;
-    x.gh = blocks[ptr];
-    x.gl = blocks[ptr + 1];
-    x.gf = blocks[ptr + 2];
-  };
-  auto prof_of = [&](int c, const ColIn& x) -> uint32_t {
-    const int qi = qrow0 + qstep * c;
-    const uint32_t sh = (uint32_t)(qi & 3) * 8u;
-    return profw(row0 + S - 1 + c, (x.qw >> sh) & 0xFFu, (x.uw >> sh) & 0xFFu);
-  };
-  auto class_of = [&](int c, const ColIn& x) -> int {
-    const uint32_t pos = gp0 + (uint32_t)(gps * c);
-    const uint32_t bit = pos & 31u;
-    const bool ing = (uint64_t)(pos >> 5) <= gmax;  // outside the genome: N
-    const uint32_t word = bit < 16 ? x.gl : x.gh;
-    const int code = (int)((word >> ((bit & 15u) * 2u)) & 3u) ^ xorc;
-    const bool inr = c >= cvlo && c <= cvhi;
-    return !inr ? 5 : ((!ing || ((x.gf >> bit) & 1u)) ? 4 : code);
-  };
-  ColIn xa, xb;
-  uint32_t pnext;
-  int gnext;
-  fetch(1, xa);
-  pnext = prof_of(1, xa);
-  gnext = class_of(1, xa);
+  stage(std::integral_constant<int, RING_K + RG::SPAN>(), 1 + rbase, 1);
+  uint32_t pnext = rr[(1 + j * (S - 1) + rbase) & (RG::RR - 1)];
+  int gnext = cr[(1 - j) & (RG::CR - 1)];
   int fin = NEG;
   const int se = stop + L1 - L2 + rband;  // global slot of the endpoint (L1,L2)
   const int je = se / S, sle = se - je * S;
@@ -603,12 +621,8 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
 
   // One skewed step.  MASKED steps (the first and last LPW-1) leave lanes
   // whose column is outside 1..maxL2 untouched.
-  // PIPE 0: inputs of column c+1 loaded and used at the end of the step;
-  // PIPE 1 / 2: xa / xb receives column c+2 while the other buffer (column
-  // c+1, loaded one step earlier) yields the next profile word and class.
-  auto step = [&](auto masked, auto pipe, int t) {
+  auto step = [&](auto masked, int t) {
     constexpr bool MASKED = decltype(masked)::value;
-    constexpr int PIPE = decltype(pipe)::value;
     const int c = t - j;
     const bool act = !MASKED || (c >= 1 && c <= maxL2);
     int hp = NEG, fp = NEG;  // new (nogap, gap2) just above local slot 0
@@ -674,36 +688,18 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
         for (int s = 0; s < S; s++)
           if (c == L2 && j == je && s == sle) fin = H[s];
       }
-      if (PIPE == 0) {
-        ColIn x;
-        fetch(c + 1, x);
-        pnext = prof_of(c + 1, x);
-        gnext = class_of(c + 1, x);
-      } else {
-        ColIn& mine = PIPE == 1 ? xa : xb;
-        ColIn& other = PIPE == 1 ? xb : xa;
-        pnext = prof_of(c + 1, other);
-        gnext = class_of(c + 1, other);
-        fetch(c + 2, mine);
-      }
     }
+    // next column's inputs from the rings (every lane, every step)
+    if (t % RING_K == 0) stage(std::integral_constant<int, RING_K>(), t + 1 + rbase + RG::SPAN, t + 1);
+    pnext = rr[(t + 1 + j * (S - 1) + rbase) & (RG::RR - 1)];
+    gnext = cr[(t + 1 - j) & (RG::CR - 1)];
   };
   using Masked = std::integral_constant<bool, true>;
   using Full = std::integral_constant<bool, false>;
-  using Direct = std::integral_constant<int, 0>;
-  using PipeA = std::integral_constant<int, 1>;
-  using PipeB = std::integral_constant<int, 2>;
   int t = 1;
-  for (; t < LPW && t < maxL2 + LPW; t++) step(Masked(), Direct(), t);
-  if (t + 1 <= maxL2) {
-    fetch(t - j + 1, xb);  // column c+1 of the first pipelined step
-    for (; t + 1 <= maxL2; t += 2) {
-      step(Full(), PipeA(), t);
-      step(Full(), PipeB(), t + 1);
-    }
-  }
-  for (; t <= maxL2; t++) step(Full(), Direct(), t);
-  for (; t < maxL2 + LPW; t++) step(Masked(), Direct(), t);
+  for (; t < LPW && t < maxL2 + LPW; t++) step(Masked(), t);
+  for (; t <= maxL2; t++) step(Full(), t);
+  for (; t < maxL2 + LPW; t++) step(Masked(), t);
   fin = __shfl(fin, gbase + je);
   const int finalscore = fin + (L1 + L2) * ext;
 #ifdef EXP_NOTRACE
@@ -891,6 +887,7 @@ __device__ __noinline__ void fill_task(int t, const AS_GLOBAL gsnapdp_window* Wn
                                        const AS_GLOBAL int* perm1, const AS_GLOBAL char* q1,
                                        const AS_GLOBAL char* qu1, const AS_GLOBAL uint32_t* blocks1,
                                        uint64_t nwords, const AS_LDS uint32_t* sprof3,
+                                       AS_LDS uint32_t* ring3,
                                        AS_GLOBAL uint32_t* D1, AS_GLOBAL gsnapdp_result* res1,
                                        AS_GLOBAL uint32_t* ops1, const AS_GLOBAL int64_t* op_off1) {
   const gsnapdp_window* __restrict__ Wn = (const gsnapdp_window*)Wn1;
@@ -899,6 +896,7 @@ __device__ __noinline__ void fill_task(int t, const AS_GLOBAL gsnapdp_window* Wn
   const char* __restrict__ qu = (const char*)qu1;
   const uint32_t* __restrict__ blocks = (const uint32_t*)blocks1;
   const uint32_t* sprof = (const uint32_t*)sprof3;
+  uint32_t* ring = (uint32_t*)ring3;
   uint32_t* __restrict__ D = (uint32_t*)D1;
   gsnapdp_result* __restrict__ res = (gsnapdp_result*)res1;
   uint32_t* __restrict__ ops = (uint32_t*)ops1;
@@ -913,11 +911,11 @@ __device__ __noinline__ void fill_task(int t, const AS_GLOBAL gsnapdp_window* Wn
   const int wi = active ? wi0 : w0;  // idle groups shadow group 0 (reads only)
   const int jl = __builtin_amdgcn_readfirstlane((int)Wn[w0].jump_late_p);
   if (jl)
-    fill_group<S, LPW, LOW, 1>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, res, ops,
-                               op_off);
+    fill_group<S, LPW, LOW, 1>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, ring,
+                               res, ops, op_off);
   else
-    fill_group<S, LPW, LOW, 0>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, res, ops,
-                               op_off);
+    fill_group<S, LPW, LOW, 0>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, ring,
+                               res, ops, op_off);
 }
 
 // All register-band classes in one persistent launch: the wave-tasks of the
@@ -932,9 +930,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     uint32_t* __restrict__ dirpool, size_t wave_stride, gsnapdp_result* __restrict__ res,
     uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
   __shared__ uint32_t sprof[SPROF_WORDS];
+  __shared__ uint32_t rings[4][RING_WORDS_MAX];  // one per wave of the block
   for (int i = threadIdx.x; i < SPROF_WORDS; i += blockDim.x)
     sprof[i] = i < UTAB ? fill_profile_word(prof[i]) : (i - UTAB < 128 ? prof[i] : 0u);
   __syncthreads();
+  uint32_t* ring = rings[threadIdx.x >> 6];
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nw = (gridDim.x * blockDim.x) >> 6;
   uint32_t* D = dirpool + (size_t)gw * wave_stride;
@@ -955,7 +955,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     fill_task<S_, LPW_, LO>(t, (const AS_GLOBAL gsnapdp_window*)Wn, (const AS_GLOBAL int*)perm, \
                             (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu,                 \
                             (const AS_GLOBAL uint32_t*)blocks, nwords,                           \
-                            (const AS_LDS uint32_t*)sprof, (AS_GLOBAL uint32_t*)D,               \
+                            (const AS_LDS uint32_t*)sprof, (AS_LDS uint32_t*)ring,               \
+                            (AS_GLOBAL uint32_t*)D,                                              \
                             (AS_GLOBAL gsnapdp_result*)res, (AS_GLOBAL uint32_t*)ops,            \
                             (const AS_GLOBAL int64_t*)op_off);                                   \
     break;
