@@ -624,7 +624,8 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   auto step = [&](auto masked, int t) {
     constexpr bool MASKED = decltype(masked)::value;
     const int c = t - j;
-    const bool act = !MASKED || (c >= 1 && c <= maxL2);
+    // a window stops at its own last column, so its registers end on column L2
+    const bool act = !MASKED || (c >= 1 && c <= L2);
     int hp = NEG, fp = NEG;  // new (nogap, gap2) just above local slot 0
     if (LPW > 1) {
       const int h = from_lane_above(H[S - 1]), f = from_lane_above(F[S - 1]);
@@ -643,11 +644,22 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       const int m1 = max(Hd, Ed);
       const int sc = (int)__builtin_amdgcn_ubfe(pw, gsh, 4);  // pairdistance - 2*extend
       const int hn = (s < NAB) ? max(m1, Fd) + sc + Kab[s < NAB ? s : 0] : max(m1, Fd) + sc;
-      av = push_sign(av, JL ? (Fd - m1) : (m1 - Fd));  // v1: nogap from gap2
-      ah = push_sign(ah, JL ? (Ed - Hd) : (Hd - Ed));  // h1: nogap from gap1
-      af = push_sign(af, JL ? (fp - b) : (b - fp));    // dF: gap2 extends
-      ae = push_sign(ae, JL ? (Er - a) : (a - Er));    // dE: gap1 extends
-      macc = (macc << 1) | __builtin_amdgcn_ubfe(pw, msh, 1);
+      const int dv = JL ? (Fd - m1) : (m1 - Fd);  // v1: nogap from gap2
+      const int dh = JL ? (Ed - Hd) : (Hd - Ed);  // h1: nogap from gap1
+      const int df = JL ? (fp - b) : (b - fp);    // dF: gap2 extends
+      const int de = JL ? (Er - a) : (a - Er);    // dE: gap1 extends
+      if (s == 0) {  // first bit of each plane
+        av = (uint32_t)dv >> 31;
+        ah = (uint32_t)dh >> 31;
+        af = (uint32_t)df >> 31;
+        ae = (uint32_t)de >> 31;
+      } else {
+        av = push_sign(av, dv);
+        ah = push_sign(ah, dh);
+        af = push_sign(af, df);
+        ae = push_sign(ae, de);
+      }
+      macc = s == 0 ? __builtin_amdgcn_ubfe(pw, msh, 1) : (macc << 1) | __builtin_amdgcn_ubfe(pw, msh, 1);
       E[s] = max(a, Er);
       const int f = max(b, fp);
       F[s] = f;
@@ -682,12 +694,6 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
 #else
       if (acc == 0x12345678u && macc == 77u) D[0] = 1u;
 #endif
-      // endpoint (L1,L2), captured in the column the window ends (dynprog.c:4545)
-      if (__builtin_amdgcn_ballot_w64(c == L2 && j == je) != 0) {
-#pragma unroll
-        for (int s = 0; s < S; s++)
-          if (c == L2 && j == je && s == sle) fin = H[s];
-      }
     }
     // next column's inputs from the rings (every lane, every step)
     if (t % RING_K == 0) stage(std::integral_constant<int, RING_K>(), t + 1 + rbase + RG::SPAN, t + 1);
@@ -696,10 +702,16 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   };
   using Masked = std::integral_constant<bool, true>;
   using Full = std::integral_constant<bool, false>;
+  // full-rate steps while every lane's column is inside 1..its own L2
+  const int minL2 = __builtin_amdgcn_readfirstlane(-wave_max(active ? -L2 : -maxL2));
   int t = 1;
   for (; t < LPW && t < maxL2 + LPW; t++) step(Masked(), t);
-  for (; t <= maxL2; t++) step(Full(), t);
+  for (; t <= minL2; t++) step(Full(), t);
   for (; t < maxL2 + LPW; t++) step(Masked(), t);
+  // endpoint (L1,L2): the lanes stopped on column L2 (dynprog.c:4545)
+#pragma unroll
+  for (int s = 0; s < S; s++)
+    if (j == je && s == sle) fin = H[s];
   fin = __shfl(fin, gbase + je);
   const int finalscore = fin + (L1 + L2) * ext;
 #ifdef EXP_NOTRACE
