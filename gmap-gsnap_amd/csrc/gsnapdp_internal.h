@@ -24,6 +24,13 @@ constexpr int CLASS_W[NCLASS] = {8, 16, 24, 28, 32, 40, 48};
 constexpr int CLASS_S[NCLASS] = {8, 8, 6, 7, 8, 5, 6};
 constexpr int CLASS_LPW[NCLASS] = {1, 2, 4, 4, 4, 8, 8};
 constexpr int FAST_WMAX = 48;
+GSNAPDP_HD_CONST inline int class_low(int c) { return c == 0 ? 1 : CLASS_W[c - 1] + 1; }
+GSNAPDP_HD_CONST inline bool classes_ok() {
+  for (int c = 0; c < NCLASS; c++)
+    if (CLASS_S[c] * CLASS_LPW[c] != CLASS_W[c] || (c > 0 && CLASS_W[c] <= CLASS_W[c - 1])) return false;
+  return CLASS_W[NCLASS - 1] == FAST_WMAX;
+}
+static_assert(classes_ok(), "k_fill class table");
 GSNAPDP_HD_CONST inline int class_of_w(int W) {
   int c = 0;
   while (c < NCLASS - 1 && W > CLASS_W[c]) c++;

@@ -438,7 +438,9 @@ struct ColStream {
 // wrote (coalesced, prefetched two columns ahead) and the group's traceback
 // lane walks the reference's traceback (dynprog.c:2611-2712) one column per
 // step, so no step waits on a dependent global load.
-constexpr int ABOVE_BIAS = -(1 << 29);
+#ifndef GSNAPDP_FILL_WAVES
+#define GSNAPDP_FILL_WAVES 4  // k_fill waves per SIMD (register budget 512 / waves)
+#endif
 constexpr int FILL_SC_BIAS = 6;  // -2 * SINGLE_EXTEND (dynprog.c:222)
 
 // k_fill's LDS profile word: each signed 4-bit pairdistance nibble s becomes
@@ -527,10 +529,8 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   }
   maxL2 = __builtin_amdgcn_readfirstlane(wave_max(L2));
   // the nogap step's constant -2*extend (= +6: k_fill serves single gaps, extend -3)
-  // is folded into the LDS profile nibbles (FILL_SC_BIAS); above-band slots add a bias
-  int Kab[NAB > 0 ? NAB : 1];
-#pragma unroll
-  for (int s = 0; s < NAB; s++) Kab[s] = (j * S + s < stop) ? ABOVE_BIAS : 0;
+  // is folded into the LDS profile nibbles (FILL_SC_BIAS); the nogap value of a
+  // slot above the band (only lane 0 has them) is held at NEG
   const int row0 = j * S - stop - rband;  // row of local slot 0 at column 0
 
   // profile word of row r; rows outside 1..L1 get a neutral word (their cells
@@ -643,7 +643,8 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       const int b = hp + open;
       const int m1 = max(Hd, Ed);
       const int sc = (int)__builtin_amdgcn_ubfe(pw, gsh, 4);  // pairdistance - 2*extend
-      const int hn = (s < NAB) ? max(m1, Fd) + sc + Kab[s < NAB ? s : 0] : max(m1, Fd) + sc;
+      const bool above = (s < NAB) && (j * S + s < stop);  // loop-invariant lane mask
+      const int hn = above ? NEG : max(m1, Fd) + sc;
       const int dv = JL ? (Fd - m1) : (m1 - Fd);  // v1: nogap from gap2
       const int dh = JL ? (Ed - Hd) : (Hd - Ed);  // h1: nogap from gap1
       const int df = JL ? (fp - b) : (b - fp);    // dF: gap2 extends
@@ -935,7 +936,7 @@ __device__ __noinline__ void fill_task(int t, const AS_GLOBAL gsnapdp_window* Wn
 // the next class's work and empty classes cost nothing.  Register budget:
 // 128 VGPRs (4 waves per SIMD); the few spills this forces sit in the task
 // call's prologue/epilogue and loop preheaders, not in the column loops.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_fill(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FILL_WAVES, 8))) void k_fill(
     const gsnapdp_window* __restrict__ Wn, const int* __restrict__ perm,
     const int* __restrict__ class_start, const char* __restrict__ q, const char* __restrict__ qu,
     const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
@@ -960,25 +961,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 #pragma unroll
     for (int k = 1; k < NCLASS; k++) c += tau >= tfirst[k] ? 1 : 0;
     const int t = class_start[c] / (64 / CLASS_LPW[c]) + (tau - tfirst[c]);
+    static_assert(NCLASS <= 8, "k_fill dispatches at most 8 classes");
     switch (c) {
-#define FILL_CASE(C, S_, LPW_, LO)                                                              \
+#define FILL_CASE(C)                                                                            \
   case C:                                                                                       \
-    static_assert(CLASS_S[C] == S_ && CLASS_LPW[C] == LPW_ && CLASS_W[C] == S_ * LPW_, "class"); \
-    fill_task<S_, LPW_, LO>(t, (const AS_GLOBAL gsnapdp_window*)Wn, (const AS_GLOBAL int*)perm, \
-                            (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu,                 \
-                            (const AS_GLOBAL uint32_t*)blocks, nwords,                           \
-                            (const AS_LDS uint32_t*)sprof, (AS_LDS uint32_t*)ring,               \
-                            (AS_GLOBAL uint32_t*)D,                                              \
-                            (AS_GLOBAL gsnapdp_result*)res, (AS_GLOBAL uint32_t*)ops,            \
-                            (const AS_GLOBAL int64_t*)op_off);                                   \
+    if constexpr (C < NCLASS)                                                                   \
+      fill_task<CLASS_S[C % NCLASS], CLASS_LPW[C % NCLASS],                                     \
+                class_low(C % NCLASS)>(                                                       \
+          t, (const AS_GLOBAL gsnapdp_window*)Wn, (const AS_GLOBAL int*)perm,                   \
+          (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu, (const AS_GLOBAL uint32_t*)blocks, \
+          nwords, (const AS_LDS uint32_t*)sprof, (AS_LDS uint32_t*)ring, (AS_GLOBAL uint32_t*)D, \
+          (AS_GLOBAL gsnapdp_result*)res, (AS_GLOBAL uint32_t*)ops,                             \
+          (const AS_GLOBAL int64_t*)op_off);                                                    \
     break;
-      FILL_CASE(0, 8, 1, 1)
-      FILL_CASE(1, 8, 2, 9)
-      FILL_CASE(2, 6, 4, 17)
-      FILL_CASE(3, 7, 4, 25)
-      FILL_CASE(4, 8, 4, 29)
-      FILL_CASE(5, 5, 8, 33)
-      FILL_CASE(6, 6, 8, 41)
+      FILL_CASE(0) FILL_CASE(1) FILL_CASE(2) FILL_CASE(3)
+      FILL_CASE(4) FILL_CASE(5) FILL_CASE(6) FILL_CASE(7)
 #undef FILL_CASE
     }
   }
@@ -1272,7 +1269,7 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
     delete ctx;
     return nullptr;
   }
-  ctx->fill_waves = prop.multiProcessorCount * 16;  // 4 waves per SIMD (k_fill's register budget)
+  ctx->fill_waves = prop.multiProcessorCount * 4 * GSNAPDP_FILL_WAVES;  // k_fill's occupancy
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     return fail("stream", e);
   if ((e = hipMalloc(&ctx->d_blocks, (nwords + 8) * 4)) != hipSuccess) return fail("malloc blocks", e);
