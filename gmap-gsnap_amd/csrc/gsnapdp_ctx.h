@@ -1,0 +1,66 @@
+// gsnapdp_ctx.h -- the context behind gsnapdp_ctx* (host side), shared by
+// gsnapdp_kernels.hip and gsnapdp_ggap.hip.  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <mutex>
+#include <string>
+
+#include "gsnapdp_internal.h"
+
+void gsnapdp__set_err(const std::string& s);
+struct gsnapdp_ctx;
+// per-stage HIP events around a launch (gsnapdp_profile); stage < 16
+void gsnapdp__mark(gsnapdp_ctx* ctx, hipStream_t st, int stage, int end);
+
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      gsnapdp__set_err(std::string(#x) + ": " + hipGetErrorString(e_));                  \
+      return -1;                                                                         \
+    }                                                                                    \
+  } while (0)
+
+struct gsnapdp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  const uint32_t* h_blocks = nullptr;
+  size_t nwords = 0;
+  uint32_t* d_blocks = nullptr;
+  int mode = 0;
+  uint32_t h_prof[gsnapdp::PROF_WORDS];
+  uint32_t* d_prof = nullptr;
+  double* d_tables = nullptr;
+  size_t ntables = 0;
+  // per-run scratch
+  int cap_n = 0;
+  int* d_keys = nullptr;
+  int* d_perm = nullptr;
+  int* d_big_list = nullptr;
+  int* d_small = nullptr;  // hist[NKEYS] | cursor[NKEYS] | class_start[NCLASS+1] | big_count
+  size_t perm_cap = 0;
+  uint32_t* d_dirpool = nullptr;
+  size_t dirpool_waves = 0;
+  uint32_t* d_bigpool = nullptr;
+  // host-run staging
+  size_t stage_cap = 0;
+  void* d_stage = nullptr;
+  std::string arch;
+  std::mutex mu;
+  int fill_waves = 0;  // waves launched per k_fill class kernel
+  int num_cus = 0;
+  // per-stage event timing (gsnapdp_profile)
+  int prof_on = 0;
+  hipEvent_t ev[2 * 16] = {};
+  int ev_used[16] = {};
+  // genome-gap batches (gsnapdp_ggap.hip)
+  int ggap_cap = 0;
+  int* d_ggap_lists = nullptr;     // per-class window lists, 3 x ggap_cap
+  int* d_ggap_counts = nullptr;    // per-class counts
+  uint32_t* d_ggap_pool = nullptr; // global scratch of the large-window path
+  size_t ggap_stage_cap = 0;
+  void* d_ggap_stage = nullptr;
+};
+

@@ -1,0 +1,757 @@
+// gsnapdp_ggap.hip -- Dynprog_genome_gap (reference src/dynprog.c:4798-5061)
+// on gfx950: the two flank fills (compute_scores_lookup_fwd / _rev,
+// :1424-1736), bridge_intron_gap (:3290-4122, splicing_iit == NULL, score
+// and probability modes), the MaxEnt site probabilities (:3195-3287) and the
+// two tracebacks (:2611-2712) of every intron window, batched.
+//
+// Layout.  Intron windows are small (GMAP: length1 = 2 x maxpeelback ~ 22,
+// length2 = length1 + 8), so a window's query rows map onto the lanes of a
+// lane group (RL = 32 rows: two windows per wave; RL = 64: one).  Lane rho
+// holds row rho, and at step t it computes column t - rho (a skewed wavefront).
+// The inputs from row r-1 come from the lane above by a DPP wave shift.  Each
+// band cell's nogap score and its four direction bits are packed into one
+// dword (H << 4 | nibble) and kept in LDS, band-compressed per row, for both
+// flanks.  The bridge then scans rows in parallel (lane = rL) from LDS, and an
+// ordered argmax over the group reproduces the reference's sequential
+// strict-`>` scan.  The group leader walks both tracebacks with the shared
+// traceback template (gsnapdp_device.h) and emits the op stream.
+//
+// Windows whose rows or band storage exceed the LDS classes run the same code
+// with one window per wave, rows in stripes of 64 (the row above a stripe comes
+// from a boundary buffer), and storage in a per-wave global scratch.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string.h>
+
+#include <mutex>
+#include <type_traits>
+
+#include "gsnapdp_ctx.h"
+#include "gsnapdp_device.h"
+#include "gsnapdp_internal.h"
+
+using namespace gsnapdp;
+
+#define AS_GLOBAL __attribute__((address_space(1)))
+#define AS_LDS __attribute__((address_space(3)))
+
+namespace {
+
+// dynprog.c:142-293, intron.h:10-29
+constexpr int SINGLE_OPEN = -10, SINGLE_EXTEND = -3, PAIRED_OPEN = -18, PAIRED_EXTEND = -3;
+constexpr int GCAG_INTRON = 15, ATAC_INTRON = 12, FINAL_GCAG_INTRON = 20, FINAL_ATAC_INTRON = 12;
+constexpr int LEFT_GT = 0x21, LEFT_GC = 0x10, LEFT_AT = 0x08, LEFT_CT = 0x06;
+constexpr int RIGHT_AG = 0x30, RIGHT_AC = 0x0C, RIGHT_GC = 0x02, RIGHT_AT = 0x01;
+constexpr int GTAG_FWD = 0x20, GCAG_FWD = 0x10, ATAC_FWD = 0x08;
+constexpr int GTAG_REV = 0x04, GCAG_REV = 0x02, ATAC_REV = 0x01;
+constexpr int BRIDGE_INIT = -100000;  // bestscore / bestscoreI start (:3302)
+
+// window classes of the batch
+enum { GG_SMALL = 0, GG_MID = 1, GG_BIG = 2, GG_NCLS = 3 };
+constexpr int GG_SMALL_WORDS = 1536;      // LDS words per window, RL = 32 (2 per wave)
+constexpr int GG_MID_WORDS = 4096;        // LDS words per window, RL = 64
+constexpr size_t GG_BIG_WORDS = (size_t)4 << 20;  // global words per wave of the large path
+constexpr int GG_BIG_WAVES = 32;
+
+__device__ inline bool ggap_needs_tables(const gsnapdp_ggap_window& w) {
+  return w.use_probabilities_p || w.finalp;
+}
+
+// Window geometry: widened fill bands (dynprog.c:1442-1454 with widebandp) and
+// the storage layout of one window (words): H|dirs of the left flank (L1 x WL),
+// of the right flank (L1 x WR), the column classes of both flanks (bytes), the
+// site probabilities (probability mode, doubles) and the stripe boundary row.
+struct GGeo {
+  int L1, L2L, L2R, eb;
+  int lbL, rbL, WL, lbR, rbR, WR;
+  int mt, open, ext, canon;
+  int oHR, oClsL, oClsR, oProbL, oProbR, oBnd, words;
+};
+
+__device__ __host__ inline void fill_bands(int L1, int L2, int eb, int& lb, int& rb) {
+  if (L2 >= L1) {
+    rb = L2 - L1 + eb;
+    lb = eb;
+  } else {
+    lb = L1 - L2 + eb;
+    rb = eb;
+  }
+}
+
+__device__ inline GGeo gg_geo(const gsnapdp_ggap_window& w) {
+  GGeo G;
+  G.L1 = w.length1;
+  G.L2L = w.length2L;
+  G.L2R = w.length2R;
+  G.eb = w.extraband_paired;
+  fill_bands(G.L1, G.L2L, G.eb, G.lbL, G.rbL);
+  fill_bands(G.L1, G.L2R, G.eb, G.lbR, G.rbR);
+  G.WL = G.lbL + G.rbL + 1;
+  G.WR = G.lbR + G.rbR + 1;
+  const double dr = (double)w.defect_rate;  // dynprog.c:4871-4886
+  G.mt = dr < 0.003 ? MT_HIGHQ : (dr < 0.014 ? MT_MEDQ : MT_LOWQ);
+  if (G.L1 > w.maxpeelback * 4) {  // :4888-4896
+    G.open = SINGLE_OPEN;
+    G.ext = SINGLE_EXTEND;
+  } else {
+    G.open = PAIRED_OPEN;
+    G.ext = PAIRED_EXTEND;
+  }
+  const int canon[3] = {10, 16, 22}, fcanon[3] = {30, 36, 42};  // :277-283
+  G.canon = !w.splicingp ? 0 : (w.finalp ? fcanon[G.mt] : canon[G.mt]);
+  const int l1 = G.L1 > 0 ? G.L1 : 0;
+  G.oHR = l1 * G.WL;
+  G.oClsL = G.oHR + l1 * G.WR;
+  G.oClsR = G.oClsL + (G.L2L + 2 + 3) / 4;
+  int o = G.oClsR + (G.L2R + 2 + 3) / 4;
+  o = (o + 1) & ~1;
+  G.oProbL = o;
+  G.oProbR = o + 2 * G.L2L;
+  if (w.use_probabilities_p) o += 2 * (G.L2L + G.L2R);
+  G.oBnd = o;
+  G.words = o;
+  return G;
+}
+
+// intron_score (dynprog.c:3148-3192), non-PMAP
+__device__ inline int intron_score(int& introntype, int leftdi, int rightdi, int cdna_direction,
+                                   int canonical_reward, int finalp) {
+  const int t = leftdi & rightdi;
+  const int gcag = finalp ? FINAL_GCAG_INTRON : GCAG_INTRON;
+  const int atac = finalp ? FINAL_ATAC_INTRON : ATAC_INTRON;
+  introntype = t;
+  if (t == 0) return 0;
+  if (cdna_direction > 0) {
+    if (t == GTAG_FWD) return canonical_reward;
+    if (t == GCAG_FWD) return gcag;
+    if (t == ATAC_FWD) return atac;
+  } else if (cdna_direction < 0) {
+    if (t == GTAG_REV) return canonical_reward;
+    if (t == GCAG_REV) return gcag;
+    if (t == ATAC_REV) return atac;
+  } else {
+    if (t == GTAG_FWD || t == GTAG_REV) return canonical_reward;
+    if (t == GCAG_FWD || t == GCAG_REV) return gcag;
+    if (t == ATAC_FWD || t == ATAC_REV) return atac;
+  }
+  introntype = 0;
+  return 0;
+}
+
+// leftdi / rightdi (dynprog.c:3331-3373) from two genome class codes
+__device__ inline int left_di(int a, int b) {
+  if (a == 2 && b == 3) return LEFT_GT;
+  if (a == 2 && b == 1) return LEFT_GC;
+  if (a == 0 && b == 3) return LEFT_AT;
+  if (a == 1 && b == 3) return LEFT_CT;
+  return 0;
+}
+__device__ inline int right_di(int b, int a) {
+  if (b == 0 && a == 2) return RIGHT_AG;
+  if (b == 0 && a == 1) return RIGHT_AC;
+  if (b == 2 && a == 1) return RIGHT_GC;
+  if (b == 0 && a == 3) return RIGHT_AT;
+  return 0;
+}
+
+// Maxent site probability of a left / right splice column
+// (get_splicesite_probs :3195-3287, probability precompute :3856-3903).
+__device__ inline double left_site_prob(const gsnapdp_ggap_window& w, int cL,
+                                        const uint32_t* blocks, uint64_t nwords, const double* T) {
+  const int cdir = w.cdna_direction;
+  uint32_t pos;
+  if (w.watsonp) {
+    pos = w.chrpos + (uint32_t)w.offset2L + (uint32_t)cL;
+    return maxent_prob(cdir > 0 ? GSNAPDP_DONOR : GSNAPDP_ANTIACCEPTOR, w.chroffset + pos,
+                       w.chroffset, blocks, nwords, T);
+  }
+  pos = w.chrpos + (uint32_t)(w.genomiclength - 1) - (uint32_t)w.offset2L - (uint32_t)cL + 1u;
+  return maxent_prob(cdir > 0 ? GSNAPDP_ANTIDONOR : GSNAPDP_ACCEPTOR, w.chroffset + pos,
+                     w.chroffset, blocks, nwords, T);
+}
+__device__ inline double right_site_prob(const gsnapdp_ggap_window& w, int cR,
+                                         const uint32_t* blocks, uint64_t nwords, const double* T) {
+  const int cdir = w.cdna_direction;
+  uint32_t pos;
+  if (w.watsonp) {
+    pos = w.chrpos + (uint32_t)w.revoffset2R - (uint32_t)cR + 1u;
+    return maxent_prob(cdir > 0 ? GSNAPDP_ACCEPTOR : GSNAPDP_ANTIDONOR, w.chroffset + pos,
+                       w.chroffset, blocks, nwords, T);
+  }
+  pos = w.chrpos + (uint32_t)(w.genomiclength - 1) - (uint32_t)w.revoffset2R + (uint32_t)cR;
+  return maxent_prob(cdir > 0 ? GSNAPDP_ANTIACCEPTOR : GSNAPDP_DONOR, w.chroffset + pos,
+                     w.chroffset, blocks, nwords, T);
+}
+
+// The per-side view the shared traceback template expects (gsnapdp_device.h).
+__device__ inline Lane side_lane(const gsnapdp_ggap_window& w, const GGeo& G, int right) {
+  Lane L;
+  L.d.L1 = G.L1;
+  L.d.L2 = right ? G.L2R : G.L2L;
+  L.d.lband = right ? G.lbR : G.lbL;
+  L.d.rband = right ? G.rbR : G.rbL;
+  L.d.W = L.d.lband + L.d.rband + 1;
+  L.d.mode = 0;
+  L.d.eb = G.eb;
+  L.d.open = G.open;
+  L.d.ext = G.ext;
+  L.d.mt = G.mt;
+  L.d.jl = 0;
+  L.d.rev = right;
+  L.d.status = ST_OK;
+  L.d.early_score = 0;
+  L.d.early_dpi_step = 0;
+  // right flank: query read backwards from sequence1[length1-1] (dynprog.c:4960)
+  L.qbase = right ? (int)w.qpos + G.L1 - 1 : (int)w.qpos;
+  L.qstep = right ? -1 : 1;
+  L.g0 = right ? w.revoffset2R : w.offset2L;
+  L.gstep = right ? -1 : 1;
+  L.base = w.chroffset + w.chrpos;
+  L.glen = (int)w.genomiclength;
+  L.watson = w.watsonp ? 1 : 0;
+  L.allstar = (L.base < w.chroffset) || (L.base >= w.chrhigh);
+  L.off1 = w.offset1;
+  L.off2 = right ? w.revoffset2R : w.offset2L;
+  L.cdna_direction = w.cdna_direction;
+  return L;
+}
+
+template <class P>
+struct CellDirs {  // direction nibble of an in-band cell (r >= 1, c >= 1)
+  P H;
+  int W, lband;
+  __device__ inline uint32_t operator()(int r, int c) const {
+    return (uint32_t)H[(r - 1) * W + (c - r + lband)] & 0xFu;
+  }
+};
+
+__device__ inline int from_above(int v) {  // lane i receives lane i-1's v (DPP wave_shr:1)
+  return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false);
+}
+
+template <class P>
+struct Side {
+  P H;              // L1 x W dwords: H << 4 | nibble (bit0 gap1 HORIZ, bit1 gap2 VERT,
+                    // bit2 nogap HORIZ, bit3 nogap VERT)
+  int L2, lband, rband, W;
+};
+
+// One flank fill (compute_scores_lookup_fwd / _rev, dynprog.c:1424-1736) over
+// the rows of the lane group, in stripes of RL rows.  Every lane of the wave
+// calls it (the DPP shift spans the wave); `T` and `NS` are wave-uniform.
+template <int RL, bool GMEM, class P, class PB>
+__device__ void gg_fill(const Side<P>& sd, PB cls, P bnd, int L1, int rho, int open, int ext,
+                        int jl, const char* __restrict__ q, int qrow0, int qstep,
+                        const uint32_t* __restrict__ ptab, int T, int NS) {
+  const int lband = sd.lband, rband = sd.rband, L2 = sd.L2, W = sd.W;
+  for (int s = 0; s < NS; s++) {
+    const int r = s * RL + rho;
+    // profile word of this lane's row: pairdistance of its query char against
+    // genome classes A C G T N * as signed nibbles (build_profile_table)
+    const int rq = (r >= 1 && r <= L1) ? r : 1;
+    const uint32_t pw = ptab[(unsigned char)q[qrow0 + qstep * (rq - 1)] & 127u];
+    int Hc = NEG, Ec = NEG, Fc = NEG;      // (r, c-1)
+    int Hup = NEG, Eup = NEG, Fup = NEG;   // (r-1, c-1)
+    for (int t = 0; t < T; t++) {
+      const int c = t - rho;
+      int Hn = from_above(Hc), En = from_above(Ec), Fn = from_above(Fc);  // (r-1, c)
+      if (GMEM && rho == 0 && s > 0) {
+        const bool ok = c >= 0 && c <= L2;
+        const int cc = ok ? c : 0;
+        Hn = ok ? (int)bnd[3 * cc] : NEG;
+        En = ok ? (int)bnd[3 * cc + 1] : NEG;
+        Fn = ok ? (int)bnd[3 * cc + 2] : NEG;
+      }
+      int H = NEG, E = NEG, F = NEG;
+      uint32_t nib = 0;
+      bool store = false;
+      if (c >= 0 && c <= L2 && r <= L1) {
+        if (r == 0) {  // row 0 (dynprog.c:1460-1475)
+          H = c == 0 ? 0 : NEG;
+          E = (c >= 1 && c <= rband) ? open + c * ext : NEG;
+        } else if (c == 0) {  // column 0 (:1477-1488)
+          F = r <= lband ? open + r * ext : NEG;
+        } else if (r >= c - rband && r <= c + lband) {
+          // gap1 from (r, c-1), gap2 from (r-1, c), nogap from (r-1, c-1), each
+          // with the sequential tie rule (:1519-1561): x wins ties iff jump_late
+          const int a = Hc + open;
+          const bool tE = Ec > a - jl;
+          E = (tE ? Ec : a) + ext;
+          const int b = Hn + open;
+          const bool tF = Fn > b - jl;
+          F = (tF ? Fn : b) + ext;
+          int best = Hup;
+          uint32_t d = 0;
+          if (Eup > best - jl) {
+            best = Eup;
+            d = 4;
+          }
+          if (Fup > best - jl) {
+            best = Fup;
+            d = 8;
+          }
+          const int g = (int)cls[c];
+          H = best + __builtin_amdgcn_sbfe((int)pw, 4 * g, 4);
+          nib = (tE ? 1u : 0u) | (tF ? 2u : 0u) | d;
+          store = true;
+        }
+      }
+      if (store) sd.H[(r - 1) * W + (c - r + lband)] = ((uint32_t)H << 4) | nib;
+      if (GMEM && rho == RL - 1 && c >= 0 && c <= L2) {
+        bnd[3 * c] = (uint32_t)H;
+        bnd[3 * c + 1] = (uint32_t)E;
+        bnd[3 * c + 2] = (uint32_t)F;
+      }
+      Hup = Hn;
+      Eup = En;
+      Fup = Fn;
+      Hc = H;
+      Ec = E;
+      Fc = F;
+    }
+    if (GMEM) __threadfence();  // the boundary row is read by the next stripe's lane 0
+  }
+}
+
+struct Cand {  // a bridge candidate (dynprog.c:3698-4081)
+  int score;     // scoreL + scoreI + scoreR
+  double prob;   // probL + probR (probability mode)
+  int key;       // scan order: 2*rL + (right loop)
+  int rL, cL, rR, cR, sI, itype;
+};
+
+__device__ inline bool better(const Cand& x, const Cand& y, bool probmode) {
+  // x replaces y in the sequential scan's outcome
+  if (probmode) return x.prob > y.prob || (x.prob == y.prob && x.key < y.key);
+  return x.score > y.score || (x.score == y.score && x.key < y.key);
+}
+
+template <int RL>
+__device__ inline Cand group_best(Cand c, bool probmode) {
+#pragma unroll
+  for (int o = RL / 2; o > 0; o >>= 1) {
+    Cand x;
+    x.score = __shfl_xor(c.score, o);
+    x.prob = __shfl_xor(c.prob, o);
+    x.key = __shfl_xor(c.key, o);
+    x.rL = __shfl_xor(c.rL, o);
+    x.cL = __shfl_xor(c.cL, o);
+    x.rR = __shfl_xor(c.rR, o);
+    x.cR = __shfl_xor(c.cR, o);
+    x.sI = __shfl_xor(c.sI, o);
+    x.itype = __shfl_xor(c.itype, o);
+    if (better(x, c, probmode)) c = x;
+  }
+  return c;
+}
+
+template <int RL, bool GMEM>
+__global__ __launch_bounds__(256) void k_ggap(
+    const gsnapdp_ggap_window* __restrict__ Wn, const int* __restrict__ list,
+    const int* __restrict__ count, const char* __restrict__ q, const char* __restrict__ qu,
+    const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
+    const double* __restrict__ tables, uint32_t* __restrict__ pool, size_t stride,
+    gsnapdp_ggap_result* __restrict__ res, gsnapdp_ggap_trace* __restrict__ trc,
+    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
+  extern __shared__ uint32_t smem[];
+  using P = typename std::conditional<GMEM, AS_GLOBAL uint32_t*, AS_LDS uint32_t*>::type;
+  using PB = typename std::conditional<GMEM, AS_GLOBAL uint8_t*, AS_LDS uint8_t*>::type;
+  using PD = typename std::conditional<GMEM, AS_GLOBAL double*, AS_LDS double*>::type;
+  constexpr int NGW = 64 / RL;
+  const int lane = threadIdx.x & 63, grp = lane / RL, rho = lane % RL;
+  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+  P region;
+  if constexpr (GMEM) {
+    region = (P)(pool + (size_t)gw * stride);
+  } else {
+    region = (P)(smem + ((threadIdx.x >> 6) * NGW + grp) * stride);
+  }
+  const int n = *count;
+  for (int base = gw * NGW; base < n; base += nw * NGW) {
+    const int k = base + grp;
+    const bool act = k < n;
+    const int wi = list[act ? k : base];
+    const gsnapdp_ggap_window w = Wn[wi];
+    GGeo G = gg_geo(w);
+    if (!act) G.L1 = 0;  // a shadow group: no rows, no stores
+    const P HL = region;
+    const P HR = region + G.oHR;
+    const PB clsL = (PB)(region + G.oClsL);
+    const PB clsR = (PB)(region + G.oClsR);
+    const PD lp = (PD)(region + G.oProbL);
+    const PD rp = (PD)(region + G.oProbR);
+    const P bnd = region + G.oBnd;
+    const bool probmode = w.use_probabilities_p != 0;
+    // column genome classes (get_genomic_nt, dynprog.c:403-441), both flanks
+    const Lane LL = side_lane(w, G, 0), LR = side_lane(w, G, 1);
+    if (act) {
+      for (int c = rho; c <= G.L2L + 1; c += RL)
+        clsL[c] = (uint8_t)((c >= 1 && c <= G.L2L) ? gclass(blocks, nwords, LL, w.offset2L + c - 1) : 5);
+      for (int c = rho; c <= G.L2R + 1; c += RL)
+        clsR[c] = (uint8_t)((c >= 1 && c <= G.L2R) ? gclass(blocks, nwords, LR, w.revoffset2R + 1 - c) : 5);
+      if (probmode) {  // :3856-3903
+        for (int c = rho; c < G.L2L; c += RL)
+          lp[c] = c < G.L2L - 1 ? left_site_prob(w, c, blocks, nwords, tables) : 0.0;
+        for (int c = rho; c < G.L2R; c += RL)
+          rp[c] = c < G.L2R - 1 ? right_site_prob(w, c, blocks, nwords, tables) : 0.0;
+      }
+    }
+    if constexpr (GMEM) __threadfence();
+    else __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the class bytes are in LDS
+    // wave-uniform step and stripe counts
+    const int L2max = max(G.L2L, G.L2R);
+    const int T = __builtin_amdgcn_readfirstlane(wave_max(act ? L2max : 0)) + RL;
+    const int NS = __builtin_amdgcn_readfirstlane(wave_max(act ? G.L1 + 1 : 1) + RL - 1) / RL;
+    const uint32_t* ptab = prof + G.mt * 128;
+    const Side<P> SL = {HL, G.L2L, G.lbL, G.rbL, G.WL};
+    const Side<P> SR = {HR, G.L2R, G.lbR, G.rbR, G.WR};
+    // left flank forward with jump_late_p, right flank reversed with !jump_late_p (:4955-4990)
+    const int jl = w.jump_late_p ? 1 : 0;
+    gg_fill<RL, GMEM>(SL, clsL, bnd, G.L1, rho, G.open, G.ext, jl, q, (int)w.qpos, 1, ptab, T, NS);
+    gg_fill<RL, GMEM>(SR, clsR, bnd, G.L1, rho, G.open, G.ext, 1 - jl, q, (int)w.qpos + G.L1 - 1,
+                      -1, ptab, T, NS);
+    if constexpr (GMEM) __threadfence();
+    else __builtin_amdgcn_s_waitcnt(0xc07f);
+
+    // ---- bridge_intron_gap (dynprog.c:3290-4122), lane = rL
+    const int leftoffset = w.offset2L, rightoffset = w.revoffset2R;
+    const int lbandB = G.eb, rbandBL = G.L2L - G.L1 + G.eb, rbandBR = G.L2R - G.L1 + G.eb;
+    auto ldi = [&](int cL) {  // leftdi[cL], 0 past the scanned columns (calloc)
+      return cL >= 0 && cL < G.L2L - 1 ? left_di(clsL[cL + 1], clsL[cL + 2]) : 0;
+    };
+    auto rdi = [&](int cR) {
+      return cR >= 0 && cR < G.L2R - 1 ? right_di(clsR[cR + 2], clsR[cR + 1]) : 0;
+    };
+    auto HLv = [&](int r, int c) { return (int)HL[(r - 1) * G.WL + (c - r + G.lbL)]; };
+    auto HRv = [&](int r, int c) { return (int)HR[(r - 1) * G.WR + (c - r + G.lbR)]; };
+    auto pen = [](int v) { return (v & 12) ? 1 : 0; };  // nogap dir HORIZ or VERT
+    Cand best;
+    best.score = BRIDGE_INIT;
+    best.prob = 0.0;
+    best.key = 0x7fffffff;
+    best.rL = best.cL = best.rR = best.cR = 0;
+    best.sI = BRIDGE_INIT;
+    best.itype = 0;
+    const int rows = __builtin_amdgcn_readfirstlane(wave_max(act ? G.L1 : 0));
+    for (int r0 = 0; r0 < rows; r0 += RL) {
+      const int rL = r0 + rho;
+      if (rL < 1 || rL >= G.L1) continue;
+      const int rR = G.L1 - rL;
+      const int cloL = max(1, rL - lbandB), chighL = min(G.L2L - 1, rL + rbandBL);
+      const int cloR = max(1, rR - lbandB), chighR = min(G.L2R - 1, rR + rbandBR);
+      const int DR = HRv(rR, rR) >> 4;  // (rR, rR): on the right band's main diagonal
+      const int DL = HLv(rL, rL) >> 4;
+      for (int cL = cloL; cL <= chighL; cL++) {  // indel on left
+        const int cR = rR;
+        if (!(cR < rightoffset - leftoffset - cL)) continue;
+        if (probmode) {
+          const double p = lp[cL] + (cR < G.L2R - 1 ? rp[cR] : 0.0);
+          if (!(p > best.prob)) continue;
+          const int v = HLv(rL, cL);
+          int it;
+          const int sI = intron_score(it, ldi(cL), rdi(cR), w.cdna_direction, G.canon, w.finalp);
+          const int tot = (v >> 4) - pen(v) + sI + DR;
+          if (tot >= w.score_threshold) {
+            best.prob = p;
+            best.key = 2 * rL;
+            best.rL = rL; best.cL = cL; best.rR = rR; best.cR = cR;
+          }
+        } else {
+          const int v = HLv(rL, cL);
+          int it;
+          const int sI = intron_score(it, ldi(cL), rdi(cR), w.cdna_direction, G.canon, w.finalp);
+          const int tot = (v >> 4) - pen(v) + sI + DR;
+          if (tot > best.score) {
+            best.score = tot;
+            best.key = 2 * rL;
+            best.sI = sI;
+            best.itype = it;
+            best.rL = rL; best.cL = cL; best.rR = rR; best.cR = cR;
+          }
+        }
+      }
+      for (int cR = cloR; cR <= chighR; cR++) {  // indel on right
+        const int cL = rL;
+        if (!(cL < rightoffset - leftoffset - cR)) continue;
+        if (probmode) {
+          const double p = (cL < G.L2L - 1 ? lp[cL] : 0.0) + rp[cR];
+          if (!(p > best.prob)) continue;
+          const int v = HRv(rR, cR);
+          int it;
+          const int sI = intron_score(it, ldi(cL), rdi(cR), w.cdna_direction, G.canon, w.finalp);
+          const int tot = DL + sI + (v >> 4) - pen(v);
+          if (tot >= w.score_threshold) {
+            best.prob = p;
+            best.key = 2 * rL + 1;
+            best.rL = rL; best.cL = cL; best.rR = rR; best.cR = cR;
+          }
+        } else {
+          const int v = HRv(rR, cR);
+          int it;
+          const int sI = intron_score(it, ldi(cL), rdi(cR), w.cdna_direction, G.canon, w.finalp);
+          const int tot = DL + sI + (v >> 4) - pen(v);
+          if (tot > best.score) {
+            best.score = tot;
+            best.key = 2 * rL + 1;
+            best.sI = sI;
+            best.itype = it;
+            best.rL = rL; best.cL = cL; best.rR = rR; best.cR = cR;
+          }
+        }
+      }
+    }
+    best = group_best<RL>(best, probmode);
+
+    // ---- outcome, probabilities and tracebacks (group leader)
+    if (act && rho == 0) {
+      gsnapdp_ggap_result R;
+      gsnapdp_ggap_trace X;
+      memset(&R, 0, sizeof(R));
+      memset(&X, 0, sizeof(X));
+      R.dynprogindex = w.dynprogindex;
+      R.bridge_ok = 1;
+      X.status = ST_OK;
+      const bool tables_ok = tables != nullptr || !ggap_needs_tables(w);
+      int finalscore = 0, rc;
+      if (!tables_ok) {
+        rc = -2;
+      } else if (probmode) {
+        if (!(best.prob > 0.0)) {
+          rc = -1;  // no candidate: the reference reads uninitialised indices (:4055)
+        } else {
+          const int vl = HLv(best.rL, best.cL), vr = HRv(best.rR, best.cR);
+          int it;
+          const int sI = intron_score(it, ldi(best.cL), rdi(best.cR), w.cdna_direction, G.canon,
+                                      w.finalp);
+          const int sL = (vl >> 4) - pen(vl), sR = (vr >> 4) - pen(vr);
+          finalscore = w.halfp ? sL + sI + sR - sI / 2 : sL + sI + sR;
+          rc = finalscore >= 0;
+        }
+      } else {
+        finalscore = w.halfp ? best.score - best.sI / 2 : best.score;
+        R.introntype = best.score > BRIDGE_INIT ? best.itype : 0;
+        rc = finalscore >= 0;
+      }
+      if (rc == -2) {
+        X.status = ST_UNSUPPORTED;
+        R.returned_null = 1;
+        R.finalscore = NEG;
+      } else if (rc == -1) {
+        R.bridge_ok = 0;
+        R.returned_null = 1;
+        R.finalscore = NEG;
+      } else if (rc == 0) {
+        R.finalscore = finalscore;
+        R.returned_null = 1;
+      } else {
+        R.finalscore = finalscore;
+        if (w.finalp) {  // :4104-4108
+          R.left_prob = left_site_prob(w, best.cL, blocks, nwords, tables);
+          R.right_prob = right_site_prob(w, best.cR, blocks, nwords, tables);
+        }
+        R.new_leftgenomepos = w.offset2L + (best.cL - 1);
+        R.new_rightgenomepos = w.revoffset2R - (best.cR - 1);
+        R.exonhead = (w.offset1 + G.L1 - 1) - (best.rR - 1);
+        X.brL = best.rL;
+        X.bcL = best.cL;
+        X.brR = best.rR;
+        X.bcR = best.cR;
+        // right flank (reversed), the gapholder, then the left flank (:5000-5040)
+        const int64_t o0 = op_off[wi];
+        const int cap = (int)(op_off[wi + 1] - o0);
+        Tally t = {0, 0, 0, 0, 0};
+        OpWriter owR = {ops + o0, cap, 0, 0};
+        traceback(CellDirs<P>{HR, G.WR, G.lbR}, LR, best.rR, best.cR, q, qu, blocks, nwords,
+                  prof, t, owR);
+        const int nR = owR.n < cap ? owR.n : cap;
+        OpWriter owL = {ops + o0 + nR, cap - nR, 0, 0};
+        traceback(CellDirs<P>{HL, G.WL, G.lbL}, LL, best.rL, best.cL, q, qu, blocks, nwords,
+                  prof, t, owL);
+        X.nops_right = nR;
+        X.nops_left = owL.n < owL.cap ? owL.n : owL.cap;
+        if (owR.n > cap || owL.n > owL.cap) X.status = ST_OPS_OVERFLOW;
+        R.nmatches = t.nmatches;
+        R.nmismatches = t.nmismatches;
+        R.nopens = t.nopens;
+        R.nindels = t.nindels;
+        X.npairs = t.npush + 1;  // + the gapholder
+        if (t.npush == 0) {      // only the gapholder: the list is dropped (:5050-5053)
+          R.returned_null = 1;
+          X.npairs = 0;
+        }
+        R.dynprogindex = step_dpi(w.dynprogindex);
+      }
+      res[wi] = R;
+      trc[wi] = X;
+    }
+  }
+}
+
+// Parameters, early returns (dynprog.c:4843-4870) and the class of every
+// window; windows that reach the fills are appended to their class list.
+__global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
+                            gsnapdp_ggap_result* __restrict__ res,
+                            gsnapdp_ggap_trace* __restrict__ trc, int* __restrict__ lists,
+                            int* __restrict__ counts, int cap) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int cls = -1;
+  if (i < n) {
+    const gsnapdp_ggap_window w = Wn[i];
+    const GGeo G = gg_geo(w);
+    gsnapdp_ggap_result R;
+    gsnapdp_ggap_trace X;
+    memset(&R, 0, sizeof(R));
+    memset(&X, 0, sizeof(X));
+    R.dynprogindex = w.dynprogindex;
+    R.bridge_ok = 1;
+    X.status = ST_EARLY;
+    bool done = true;
+    if (G.L1 <= 1) {  // :4855-4858
+      R.finalscore = NEG;
+      R.returned_null = 1;
+    } else if (G.L1 > w.maxlength1 || G.L2L > w.maxlength2 || G.L2R > w.maxlength2) {
+      R.new_leftgenomepos = w.offset2L - 1;  // :4898-4909
+      R.new_rightgenomepos = w.revoffset2R + 1;
+      R.exonhead = w.offset1 + G.L1 - 1;
+      R.dynprogindex = step_dpi(w.dynprogindex);
+      R.finalscore = NEG;
+      R.returned_null = 1;
+    } else if (G.L2L <= 0 || G.L2R <= 0 || G.eb < 0 || G.L2L < G.L1 - 1 || G.L2R < G.L1 - 1) {
+      // the reference aborts (Matrix3_alloc :495) or, with a flank shorter than
+      // length1 - 1, reads the bridge's diagonal cells past its matrix rows
+      R.finalscore = NEG;
+      R.returned_null = 1;
+      X.status = ST_UNSUPPORTED;
+    } else {
+      done = false;
+      if (G.L1 + 1 <= 32 && G.words <= GG_SMALL_WORDS) cls = GG_SMALL;
+      else if (G.L1 + 1 <= 64 && G.words <= GG_MID_WORDS) cls = GG_MID;
+      else if ((size_t)G.words + 3 * (size_t)(max(G.L2L, G.L2R) + 2) <= GG_BIG_WORDS) cls = GG_BIG;
+      else {
+        done = true;
+        R.finalscore = NEG;
+        R.returned_null = 1;
+        X.status = ST_UNSUPPORTED;  // beyond the large path's scratch
+      }
+    }
+    if (done) {
+      res[i] = R;
+      trc[i] = X;
+    }
+  }
+  // one list append per class per wave
+#pragma unroll
+  for (int c = 0; c < GG_NCLS; c++) {
+    const int pos = agg_atomic_inc(counts + c, cls == c ? 0 : -1);
+    if (cls == c) lists[(size_t)c * cap + pos] = i;
+  }
+}
+
+}  // namespace
+
+// ======================================================================
+// Host side (include/gsnapdp.h: gsnapdp_ggap_*)
+// ======================================================================
+static int ggap_capacity(gsnapdp_ctx* ctx, int n) {
+  if (n > ctx->ggap_cap) {
+    const int cap = n + n / 4 + 1024;
+    (void)hipFree(ctx->d_ggap_lists);
+    ctx->d_ggap_lists = nullptr;
+    HIPCHK(hipMalloc(&ctx->d_ggap_lists, (size_t)GG_NCLS * cap * 4));
+    ctx->ggap_cap = cap;
+  }
+  if (!ctx->d_ggap_counts) HIPCHK(hipMalloc(&ctx->d_ggap_counts, 64));
+  return 0;
+}
+
+extern "C" int gsnapdp_ggap_run_device(gsnapdp_ctx* ctx, const gsnapdp_ggap_window* d_windows,
+                                       int n, const char* d_query, const char* d_query_uc,
+                                       gsnapdp_ggap_result* d_results, gsnapdp_ggap_trace* d_traces,
+                                       uint32_t* d_ops, const int64_t* d_op_offsets, void* stream_v) {
+  if (!ctx) return -1;
+  if (n <= 0) return 0;
+  hipStream_t st = stream_v ? (hipStream_t)stream_v : ctx->stream;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  if (ggap_capacity(ctx, n)) return -1;
+  if (!ctx->d_ggap_pool)
+    HIPCHK(hipMalloc(&ctx->d_ggap_pool, (size_t)GG_BIG_WAVES * GG_BIG_WORDS * 4));
+  const uint64_t nw = (uint64_t)ctx->nwords;
+  int* counts = ctx->d_ggap_counts;
+  int* lists = ctx->d_ggap_lists;
+  const int cap = ctx->ggap_cap;
+  HIPCHK(hipMemsetAsync(counts, 0, 4 * GG_NCLS, st));
+  gsnapdp__mark(ctx, st, 4, 0);
+  hipLaunchKernelGGL(k_ggap_plan, dim3((n + 255) / 256), dim3(256), 0, st, d_windows, n,
+                     d_results, d_traces, lists, counts, cap);
+  gsnapdp__mark(ctx, st, 4, 1);
+  gsnapdp__mark(ctx, st, 5, 0);
+  // small windows: 4 waves x 2 windows per block, 3 blocks per CU (LDS)
+  hipLaunchKernelGGL((k_ggap<32, false>), dim3(ctx->num_cus * 3), dim3(256),
+                     (size_t)8 * GG_SMALL_WORDS * 4, st, d_windows, lists, counts + GG_SMALL,
+                     d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_tables,
+                     (uint32_t*)nullptr, (size_t)GG_SMALL_WORDS, d_results, d_traces, d_ops,
+                     d_op_offsets);
+  // rows 32..63: one window per wave, 2 blocks per CU
+  hipLaunchKernelGGL((k_ggap<64, false>), dim3(ctx->num_cus * 2), dim3(256),
+                     (size_t)4 * GG_MID_WORDS * 4, st, d_windows, lists + (size_t)GG_MID * cap,
+                     counts + GG_MID, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
+                     ctx->d_tables, (uint32_t*)nullptr, (size_t)GG_MID_WORDS, d_results, d_traces,
+                     d_ops, d_op_offsets);
+  // the rest: stripes of 64 rows, storage in global scratch
+  hipLaunchKernelGGL((k_ggap<64, true>), dim3(GG_BIG_WAVES), dim3(64), 0, st, d_windows,
+                     lists + (size_t)GG_BIG * cap, counts + GG_BIG, d_query, d_query_uc,
+                     ctx->d_blocks, nw, ctx->d_prof, ctx->d_tables, ctx->d_ggap_pool,
+                     GG_BIG_WORDS, d_results, d_traces, d_ops, d_op_offsets);
+  gsnapdp__mark(ctx, st, 5, 1);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int gsnapdp_ggap_run_host(gsnapdp_ctx* ctx, const gsnapdp_ggap_window* windows, int n,
+                                     const char* query, const char* query_uc, size_t query_bytes,
+                                     gsnapdp_ggap_result* results, gsnapdp_ggap_trace* traces,
+                                     uint32_t* ops, const int64_t* op_offsets) {
+  if (!ctx) return -1;
+  if (n <= 0) return 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t nops = (size_t)op_offsets[n];
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t szw = al((size_t)n * sizeof(gsnapdp_ggap_window));
+  const size_t szq = al(query_bytes + 4);
+  const size_t szr = al((size_t)n * sizeof(gsnapdp_ggap_result));
+  const size_t szt = al((size_t)n * sizeof(gsnapdp_ggap_trace));
+  const size_t szo = al((nops + 1) * 4);
+  const size_t szoff = al((size_t)(n + 1) * 8);
+  const size_t total = szw + 2 * szq + szr + szt + szo + szoff;
+  {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (total > ctx->ggap_stage_cap) {
+      (void)hipFree(ctx->d_ggap_stage);
+      ctx->d_ggap_stage = nullptr;
+      HIPCHK(hipMalloc(&ctx->d_ggap_stage, total));
+      ctx->ggap_stage_cap = total;
+    }
+  }
+  char* b = (char*)ctx->d_ggap_stage;
+  gsnapdp_ggap_window* dw = (gsnapdp_ggap_window*)b;
+  char* dq = b + szw;
+  char* du = dq + szq;
+  gsnapdp_ggap_result* dr = (gsnapdp_ggap_result*)(du + szq);
+  gsnapdp_ggap_trace* dt = (gsnapdp_ggap_trace*)((char*)dr + szr);
+  uint32_t* dops = (uint32_t*)((char*)dt + szt);
+  int64_t* doff = (int64_t*)((char*)dops + szo);
+  hipStream_t st = ctx->stream;
+  HIPCHK(hipMemcpyAsync(dw, windows, (size_t)n * sizeof(gsnapdp_ggap_window), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(dq, query, query_bytes, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(doff, op_offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, st));
+  if (gsnapdp_ggap_run_device(ctx, dw, n, dq, du, dr, dt, dops, doff, st)) return -1;
+  HIPCHK(hipMemcpyAsync(results, dr, (size_t)n * sizeof(gsnapdp_ggap_result), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(traces, dt, (size_t)n * sizeof(gsnapdp_ggap_trace), hipMemcpyDeviceToHost, st));
+  if (nops) HIPCHK(hipMemcpyAsync(ops, dops, nops * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}

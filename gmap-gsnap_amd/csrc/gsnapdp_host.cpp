@@ -115,23 +115,13 @@ struct HostGenome {
 
 }  // namespace
 
-extern "C" int gsnapdp_expand(gsnapdp_ctx* ctx, const gsnapdp_window* w, const gsnapdp_result* res,
-                              const uint32_t* ops, const char* query, const char* query_uc,
-                              gsnapdp_pair* pairs, int cap, int* finalscore) {
-  if (!ctx || !w || !res) return -1;
-  if (finalscore) *finalscore = res->finalscore;
-  if (res->status == ST_EARLY || res->status == ST_ZEROED || res->status == ST_UNSUPPORTED) return 0;
-  if (res->status == ST_OPS_OVERFLOW) return -1;
-  const uint32_t* prof = gsnapdp__host_prof(ctx);
-  HostGenome G = {gsnapdp__host_blocks(ctx), gsnapdp__host_nwords(ctx), w->chroffset, w->chrhigh,
-                  w->chrpos, (int)w->genomiclength, w->watsonp ? 1 : 0};
-  const bool rev = w->kind == GSNAPDP_END5_GAP;
-  const char* q = query + w->qpos;
-  const char* qu = query_uc + w->qpos;
-  const int qoff = w->offset1, goff = w->offset2, dpi = w->dynprogindex;
-  int r = res->bestr, c = res->bestc;
-  std::vector<gsnapdp_pair> p;  // push order
-  p.reserve(256);
+// Replay one traceback's op stream from (r, c) into the pairs the reference
+// pushes, in push order (traceback, dynprog.c:2611-2712; add_genomeskip :2416;
+// add_queryskip :2372).  q / qu point at the query of row 1 (forward) or at
+// sequence1[length1-1] (reversed fills, indexed with negative offsets).
+static void replay(const uint32_t* ops, int nops, int r, int c, const char* q, const char* qu,
+                   int qoff, int goff, bool rev, const HostGenome& G, const uint32_t* prof,
+                   int dpi, std::vector<gsnapdp_pair>& p) {
   auto push = [&](int qpos, int gpos, char cdna, char comp, char g) {
     gsnapdp_pair x;
     memset(&x, 0, sizeof(x));
@@ -147,7 +137,7 @@ extern "C" int gsnapdp_expand(gsnapdp_ctx* ctx, const gsnapdp_window* w, const g
     int gi = g == 'A' ? 0 : g == 'C' ? 1 : g == 'G' ? 2 : g == 'T' ? 3 : 4;
     return (prof[c1 & 127] >> (24 + gi)) & 1u;  // consistent_array is mode-independent per mt
   };
-  for (int k = 0; k < res->nops; k++) {
+  for (int k = 0; k < nops; k++) {
     const uint32_t op = ops[k];
     const int cnt = (int)GSNAPDP_OP_COUNT(op);
     switch (GSNAPDP_OP_TYPE(op)) {
@@ -216,6 +206,26 @@ extern "C" int gsnapdp_expand(gsnapdp_ctx* ctx, const gsnapdp_window* w, const g
       }
     }
   }
+}
+
+extern "C" int gsnapdp_expand(gsnapdp_ctx* ctx, const gsnapdp_window* w, const gsnapdp_result* res,
+                              const uint32_t* ops, const char* query, const char* query_uc,
+                              gsnapdp_pair* pairs, int cap, int* finalscore) {
+  if (!ctx || !w || !res) return -1;
+  if (finalscore) *finalscore = res->finalscore;
+  if (res->status == ST_EARLY || res->status == ST_ZEROED || res->status == ST_UNSUPPORTED) return 0;
+  if (res->status == ST_OPS_OVERFLOW) return -1;
+  const uint32_t* prof = gsnapdp__host_prof(ctx);
+  HostGenome G = {gsnapdp__host_blocks(ctx), gsnapdp__host_nwords(ctx), w->chroffset, w->chrhigh,
+                  w->chrpos, (int)w->genomiclength, w->watsonp ? 1 : 0};
+  const bool rev = w->kind == GSNAPDP_END5_GAP;
+  const char* q = query + w->qpos;
+  const char* qu = query_uc + w->qpos;
+  const int qoff = w->offset1, goff = w->offset2, dpi = w->dynprogindex;
+  int r = res->bestr, c = res->bestc;
+  std::vector<gsnapdp_pair> p;  // push order
+  p.reserve(256);
+  replay(ops, res->nops, r, c, q, qu, qoff, goff, rev, G, prof, dpi, p);
   // final list orientation (dynprog.c:4571, 5264-5283, 5721-5740)
   const int m = (int)p.size();
   int n = 0;
@@ -233,5 +243,49 @@ extern "C" int gsnapdp_expand(gsnapdp_ctx* ctx, const gsnapdp_window* w, const g
         if (n < cap) pairs[n] = p[i];
     }
   }
+  return n;
+}
+
+// Dynprog_genome_gap's list (dynprog.c:5000-5058): traceback of the right flank
+// (reversed), List_reverse, the gapholder, traceback of the left flank, then
+// List_reverse of the whole -- i.e. the right flank's pairs last-pushed first,
+// the gapholder, the left flank's pairs in push order.
+extern "C" int gsnapdp_ggap_expand(gsnapdp_ctx* ctx, const gsnapdp_ggap_window* w,
+                                   const gsnapdp_ggap_result* res, const gsnapdp_ggap_trace* tr,
+                                   const uint32_t* ops, const char* query, const char* query_uc,
+                                   gsnapdp_pair* pairs, int cap) {
+  if (!ctx || !w || !res || !tr) return -1;
+  if (tr->status == ST_OPS_OVERFLOW) return -1;
+  if (res->returned_null || tr->status != ST_OK) return 0;
+  const uint32_t* prof = gsnapdp__host_prof(ctx);
+  HostGenome G = {gsnapdp__host_blocks(ctx), gsnapdp__host_nwords(ctx), w->chroffset, w->chrhigh,
+                  w->chrpos, (int)w->genomiclength, w->watsonp ? 1 : 0};
+  const int L1 = w->length1, dpi = w->dynprogindex;
+  std::vector<gsnapdp_pair> pr, pl;
+  pr.reserve(128);
+  pl.reserve(128);
+  replay(ops, tr->nops_right, tr->brR, tr->bcR, query + w->qpos + L1 - 1,
+         query_uc + w->qpos + L1 - 1, w->offset1 + L1 - 1, w->revoffset2R, true, G, prof, dpi, pr);
+  replay(ops + tr->nops_right, tr->nops_left, tr->brL, tr->bcL, query + w->qpos,
+         query_uc + w->qpos, w->offset1, w->offset2L, false, G, prof, dpi, pl);
+  int n = 0;
+  for (int i = (int)pr.size() - 1; i >= 0; i--, n++)
+    if (n < cap) pairs[n] = pr[i];
+  if (n < cap) {
+    gsnapdp_pair x;
+    memset(&x, 0, sizeof(x));
+    x.querypos = -1;
+    x.genomepos = -1;
+    x.queryjump = GSNAPDP_UNKNOWNJUMP;
+    x.genomejump = GSNAPDP_UNKNOWNJUMP;
+    x.cdna = ' ';
+    x.comp = ' ';
+    x.genome = ' ';
+    x.gapp = 1;
+    pairs[n] = x;
+  }
+  n++;
+  for (size_t i = 0; i < pl.size(); i++, n++)
+    if (n < cap) pairs[n] = pl[i];
   return n;
 }

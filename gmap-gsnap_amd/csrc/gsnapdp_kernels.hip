@@ -20,175 +20,12 @@
 
 #include <type_traits>
 
+#include "gsnapdp_device.h"
 #include "gsnapdp_internal.h"
 
 using namespace gsnapdp;
 
 namespace {
-
-// ------------------------------------------------------------ per-lane view
-struct Lane {
-  Derived d;
-  int qbase, qstep;   // query index of row r: qbase + qstep*(r-1)
-  int g0, gstep;      // genomicpos of column c: g0 + gstep*(c-1)
-  uint32_t base;      // chroffset + chrpos (uint32 wrap, like the reference)
-  int glen;
-  int watson;
-  int allstar;        // chroffset+chrpos overflow or >= chrhigh (dynprog.c:415-419)
-  int off1, off2;     // pair coordinate offsets
-  int cdna_direction;
-};
-
-__device__ inline Lane make_lane(const gsnapdp_window& w) {
-  Lane L;
-  L.d = derive(w);
-  L.qbase = (int)w.qpos;
-  L.qstep = L.d.rev ? -1 : 1;
-  L.g0 = w.offset2;
-  L.gstep = L.d.rev ? -1 : 1;
-  L.base = w.chroffset + w.chrpos;
-  L.glen = (int)w.genomiclength;
-  L.watson = w.watsonp ? 1 : 0;
-  L.allstar = (L.base < w.chroffset) || (L.base >= w.chrhigh);
-  L.off1 = w.offset1;
-  L.off2 = w.offset2;
-  L.cdna_direction = w.cdna_direction;
-  return L;
-}
-
-// get_genomic_nt (dynprog.c:403-441) on the packed blocks (uncompress_one_char,
-// genome.c:9325): class code 0..5 = A C G T N '*'.
-__device__ inline int gclass(const uint32_t* __restrict__ blocks, uint64_t nwords, const Lane& L,
-                             int gpos) {
-  if (gpos < 0 || gpos >= L.glen || L.allstar) return 5;
-  const uint32_t pos = L.watson ? (L.base + (uint32_t)gpos)
-                                : (L.base + (uint32_t)(L.glen - 1) - (uint32_t)gpos);
-  const uint64_t ptr = (uint64_t)(pos >> 5) * 3u;
-  if (ptr + 2 >= nwords) return 4;  // outside the genome (outside the reference's domain)
-  const uint32_t bit = pos & 31u;
-  const uint32_t fl = blocks[ptr + 2];
-  if ((fl >> bit) & 1u) return 4;
-  const uint32_t word = bit < 16 ? blocks[ptr + 1] : blocks[ptr];
-  const int code = (int)((word >> ((bit & 15u) * 2u)) & 3u);
-  return L.watson ? code : 3 - code;
-}
-
-__device__ inline int wave_max(int x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o));
-  return x;
-}
-
-__device__ inline unsigned char qchar(const char* __restrict__ q, int idx) {
-  return (unsigned char)q[idx] & 127u;
-}
-
-// --------------------------------------------------------------- op writer
-struct OpWriter {
-  uint32_t* out;
-  int cap, n;
-  int run;  // pending DIAG steps
-  __device__ inline void put(uint32_t op) {
-    if (n < cap) out[n] = op;
-    n++;
-  }
-  __device__ inline void flush() {
-    if (run > 0) put(GSNAPDP_OP(GSNAPDP_OP_DIAG, run));
-    run = 0;
-  }
-};
-
-// Counts of one traceback
-struct Tally {
-  int nmatches, nmismatches, nopens, nindels;
-};
-
-// Direction nibble: bit0 gap1==HORIZ, bit1 gap2==VERT, bit2 nogap HORIZ, bit3 nogap VERT.
-// `dirs(r, c)` returns the nibble of an in-band cell with r >= 1, c >= 1.
-//
-// traceback (dynprog.c:2611-2712) with the reference's memset semantics for
-// cells outside the band and the row-0 / column-0 initialisation
-// (dynprog.c:1460-1488).
-template <class Dirs>
-__device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c,
-                                 const char* __restrict__ q, const char* __restrict__ qu,
-                                 const uint32_t* __restrict__ blocks, uint64_t nwords,
-                                 const uint32_t* __restrict__ prof, Tally& t, OpWriter& ow) {
-  const int lband = L.d.lband, rband = L.d.rband;
-  auto inband = [&](int rr, int cc) {
-    const int d = rr - cc + rband;
-    return rr >= 1 && cc >= 1 && d >= 0 && d <= lband + rband;
-  };
-  auto gap1_horiz = [&](int rr, int cc) -> bool {
-    if (rr == 0) return cc >= 2 && cc <= rband && cc <= L.d.L2;
-    if (!inband(rr, cc)) return false;
-    return dirs(rr, cc) & 1u;
-  };
-  auto gap2_vert = [&](int rr, int cc) -> bool {
-    if (cc == 0) return rr >= 2 && rr <= lband && rr <= L.d.L1;
-    if (!inband(rr, cc)) return false;
-    return (dirs(rr, cc) >> 1) & 1u;
-  };
-  const uint32_t* ptab = prof + L.d.mt * 128;
-  while (inband(r, c)) {
-    const uint32_t nib = dirs(r, c);
-    // the nogap cell (r,c) itself: one pair unless the genome is '*'
-    const int g = gclass(blocks, nwords, L, L.g0 + L.gstep * (c - 1));
-    if (g != 5) {
-      const int qi = L.qbase + L.qstep * (r - 1);
-      const unsigned char c1 = qchar(q, qi);
-      const unsigned char u1 = (unsigned char)qu[qi];
-      const unsigned char gch = (unsigned char)("ACGTN"[g]);
-      if (u1 == gch || ((ptab[c1] >> (24 + g)) & 1u)) t.nmatches++;
-      else t.nmismatches++;
-    }
-    ow.run++;
-    if (nib & 8u) {  // VERT: query skip (add_queryskip, dynprog.c:2372)
-      int dist = 1;
-      r--;
-      c--;
-      while (gap2_vert(r, c)) {
-        dist++;
-        r--;
-      }
-      r--;
-      ow.flush();
-      ow.put(GSNAPDP_OP(GSNAPDP_OP_VSKIP, dist));
-      t.nopens++;
-      t.nindels += dist;
-    } else if (nib & 4u) {  // HORIZ: genome skip (add_genomeskip, dynprog.c:2416)
-      int dist = 1;
-      r--;
-      c--;
-      while (gap1_horiz(r, c)) {
-        dist++;
-        c--;
-      }
-      c--;
-      bool dashes = true;
-      if (dist >= MICROINTRON_LENGTH) {
-        // columns c+1 .. c+dist are skipped; left = column c+1, right = column c+dist
-        const int cl = c + 1, cr = c + dist;
-        const int gl = L.g0 + L.gstep * (cl - 1), gr = L.g0 + L.gstep * (cr - 1);
-        // in window-coordinate order (leftgenomecoord < rightgenomecoord)
-        const int lo = L.d.rev ? gr : gl, hi = L.d.rev ? gl : gr;
-        const int l1 = gclass(blocks, nwords, L, lo), l2 = gclass(blocks, nwords, L, lo + 1);
-        const int r2 = gclass(blocks, nwords, L, hi - 1), r1 = gclass(blocks, nwords, L, hi);
-        dashes = intron_type_codes(l1, l2, r2, r1, L.cdna_direction) == 0;
-      }
-      ow.flush();
-      ow.put(GSNAPDP_OP(dashes ? GSNAPDP_OP_HDASH : GSNAPDP_OP_HGAP, dist));
-      if (dashes) {
-        t.nopens++;
-        t.nindels += dist;
-      }
-    } else {
-      r--;
-      c--;
-    }
-  }
-  ow.flush();
-}
 
 // Final bookkeeping shared by all paths.
 __device__ inline void write_result(gsnapdp_result* res, const gsnapdp_window& w, const Lane& L,
@@ -215,26 +52,6 @@ __device__ inline void write_result(gsnapdp_result* res, const gsnapdp_window& w
   // QUERYEND_NOGAPS rescoring: dynprog.c:5243 / 5700
   if (L.d.mode == 3) R.finalscore = t.nmatches * 3 + t.nmismatches * (-5);
   *res = R;
-}
-
-// Wave-aggregated "pos = atomicAdd(&counter[key], 1)" for lanes with key >= 0
-// (most lanes of a wave share a key, so one atomic per distinct key per wave).
-// Every lane of the wave must call it.
-__device__ inline int agg_atomic_inc(int* counter, int key) {
-  const int lane = threadIdx.x & 63;
-  int pos = -1;
-  uint64_t todo = __ballot(key >= 0);
-  while (todo) {
-    const int leader = __ffsll((unsigned long long)todo) - 1;
-    const int lkey = __shfl(key, leader);
-    const uint64_t m = __ballot(key == lkey) & todo;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(&counter[lkey], __popcll(m));
-    base = __shfl(base, leader);
-    if (key == lkey) pos = base + __popcll(m & ((1ull << lane) - 1ull));
-    todo &= ~m;
-  }
-  return pos;
 }
 
 // ------------------------------------------------------------------ k_plan
@@ -1102,81 +919,13 @@ __global__ __launch_bounds__(64) void k_big(
 }
 
 // --------------------------------------------------------------- k_maxent
-// Maxent_hr_{donor,acceptor,antidonor,antiacceptor}_prob (maxent_hr.c:27217-27390).
-// The reference's 32 shift-specialised handlers all read a k-mer `off` nt past
-// startpos from the 128-bit window (low, high, nextlow, nexthigh).
-__device__ inline uint32_t kmer_at(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int bit) {
-  // bits [bit, bit+32) of the little-endian 128-bit value w0 | w1<<32 | w2<<64 | w3<<96
-  const uint32_t w[5] = {w0, w1, w2, w3, 0u};
-  const int i = bit >> 5, sh = bit & 31;
-  return sh == 0 ? w[i] : ((w[i] >> sh) | (w[i + 1] << (32 - sh)));
-}
-
 __global__ void k_maxent(const uint8_t* __restrict__ model, const uint32_t* __restrict__ pos,
                          const uint32_t* __restrict__ chroff, double* __restrict__ out, int n,
                          const uint32_t* __restrict__ blocks, uint64_t nwords,
                          const double* __restrict__ T) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int m = model[i];
-  const uint32_t sp = pos[i], co = chroff[i];
-  // table offsets (declaration order of maxent_hr.c:25-22606)
-  const double* donor_p = T;
-  const double* donor_di_p = donor_p + 16384;
-  const double* acc1_p = donor_di_p + 16;
-  const double* acc2_p = acc1_p + 16384;
-  const double* acc3_p = acc2_p + 16384;
-  const double* accdi_p = acc3_p + 16384;
-  const double* acc467_p = accdi_p + 16;
-  const double* acc589_p = acc467_p + 16384;
-  const double* donor_m = acc589_p + 16384;
-  const double* donor_di_m = donor_m + 16384;
-  const double* acc1_m = donor_di_m + 16;
-  const double* acc2_m = acc1_m + 16384;
-  const double* acc3_m = acc2_m + 16384;
-  const double* accdi_m = acc3_m + 16384;
-  const double* acc467_m = accdi_m + 16;
-  const double* acc589_m = acc467_m + 16384;
-  const uint32_t margin = (m == 0) ? 3u : (m == 1) ? 20u : (m == 2) ? 6u : 3u;
-  if (sp < co + margin) {
-    out[i] = 0.0;
-    return;
-  }
-  const uint32_t start = sp - margin;
-  const uint64_t ptr = (uint64_t)(start >> 5) * 3u;
-  if (ptr + 4 >= nwords) {  // outside the genome: outside the reference's domain
-    out[i] = 0.0;
-    return;
-  }
-  const uint32_t high = blocks[ptr], low = blocks[ptr + 1];
-  const uint32_t nexthigh = blocks[ptr + 3], nextlow = blocks[ptr + 4];
-  const int b0 = 2 * (int)(start & 31u);
-  auto seq = [&](int off) { return kmer_at(low, high, nextlow, nexthigh, b0 + 2 * off); };
-  double odds;
-  if (m == 0) {
-    const uint32_t s = seq(0);
-    odds = donor_p[(s & 0x3Fu) | ((s >> 4) & 0x3FC0u)] * donor_di_p[(s >> 6) & 0xFu];
-  } else if (m == 2) {
-    const uint32_t s = seq(0);
-    odds = donor_m[(s & 0xFFu) | ((s >> 4) & 0x3F00u)] * donor_di_m[(s >> 8) & 0xFu];
-  } else if (m == 1) {
-    odds = acc1_p[seq(0) & 0x3FFFu];
-    odds = __dmul_rn(odds, acc2_p[seq(7) & 0x3FFFu]);
-    const uint32_t s = seq(14);
-    odds = __dmul_rn(odds, acc3_p[(s & 0xFFu) | ((s >> 4) & 0x3F00u)]);
-    odds = __dmul_rn(odds, accdi_p[(s >> 8) & 0xFu]);
-    odds = __dmul_rn(odds, acc467_p[seq(4) & 0x3FFFu]);
-    odds = __dmul_rn(odds, acc589_p[seq(11) & 0x3FFFu]);
-  } else {
-    odds = acc1_m[seq(16) & 0x3FFFu];
-    odds = __dmul_rn(odds, acc2_m[seq(9) & 0x3FFFu]);
-    const uint32_t s = seq(0);
-    odds = __dmul_rn(odds, acc3_m[(s & 0x3Fu) | ((s >> 4) & 0x3FC0u)]);
-    odds = __dmul_rn(odds, accdi_m[(s >> 6) & 0xFu]);
-    odds = __dmul_rn(odds, acc467_m[seq(12) & 0x3FFFu]);
-    odds = __dmul_rn(odds, acc589_m[seq(5) & 0x3FFFu]);
-  }
-  out[i] = __ddiv_rn(odds, __dadd_rn(1.0, odds));
+  out[i] = maxent_prob(model[i], pos[i], chroff[i], blocks, nwords, T);
 }
 
 }  // namespace
@@ -1192,50 +941,10 @@ __global__ void k_maxent(const uint8_t* __restrict__ model, const uint32_t* __re
 #include <string>
 #include <vector>
 
+#include "gsnapdp_ctx.h"
+
 static thread_local std::string g_err;
-static void set_err(const std::string& s) { g_err = s; }
-
-#define HIPCHK(x)                                                                        \
-  do {                                                                                   \
-    hipError_t e_ = (x);                                                                 \
-    if (e_ != hipSuccess) {                                                              \
-      set_err(std::string(#x) + ": " + hipGetErrorString(e_));                           \
-      return -1;                                                                         \
-    }                                                                                    \
-  } while (0)
-
-struct gsnapdp_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  const uint32_t* h_blocks = nullptr;
-  size_t nwords = 0;
-  uint32_t* d_blocks = nullptr;
-  int mode = 0;
-  uint32_t h_prof[PROF_WORDS];
-  uint32_t* d_prof = nullptr;
-  double* d_tables = nullptr;
-  size_t ntables = 0;
-  // per-run scratch
-  int cap_n = 0;
-  int* d_keys = nullptr;
-  int* d_perm = nullptr;
-  int* d_big_list = nullptr;
-  int* d_small = nullptr;  // hist[NKEYS] | cursor[NKEYS] | class_start[NCLASS+1] | big_count
-  size_t perm_cap = 0;
-  uint32_t* d_dirpool = nullptr;
-  size_t dirpool_waves = 0;
-  uint32_t* d_bigpool = nullptr;
-  // host-run staging
-  size_t stage_cap = 0;
-  void* d_stage = nullptr;
-  std::string arch;
-  std::mutex mu;
-  int fill_waves = 0;  // waves launched per k_fill class kernel
-  // per-stage event timing (gsnapdp_profile)
-  int prof_on = 0;
-  hipEvent_t ev[2 * 16] = {};
-  int ev_used[16] = {};
-};
+void gsnapdp__set_err(const std::string& s) { g_err = s; }
 
 // per-wave k_fill scratch: direction words (u32) then match bytes, one
 // 64-lane row per column 0 .. FAST_L2MAX + 3 (the traceback reads whole
@@ -1255,7 +964,7 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
   ctx->nwords = nwords;
   ctx->mode = mode;
   auto fail = [&](const char* what, hipError_t e) -> gsnapdp_ctx* {
-    set_err(std::string(what) + ": " + hipGetErrorString(e));
+    gsnapdp__set_err(std::string(what) + ": " + hipGetErrorString(e));
     delete ctx;
     return nullptr;
   };
@@ -1265,11 +974,12 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
   if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return fail("props", e);
   ctx->arch = prop.gcnArchName;
   if (ctx->arch.find("gfx950") == std::string::npos) {
-    set_err("gsnapdp is built for gfx950 only; device is " + ctx->arch);
+    gsnapdp__set_err("gsnapdp is built for gfx950 only; device is " + ctx->arch);
     delete ctx;
     return nullptr;
   }
   ctx->fill_waves = prop.multiProcessorCount * 4 * GSNAPDP_FILL_WAVES;  // k_fill's occupancy
+  ctx->num_cus = prop.multiProcessorCount;
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     return fail("stream", e);
   if ((e = hipMalloc(&ctx->d_blocks, (nwords + 8) * 4)) != hipSuccess) return fail("malloc blocks", e);
@@ -1303,6 +1013,10 @@ extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   (void)hipFree(ctx->d_small);
   (void)hipFree(ctx->d_dirpool);
   (void)hipFree(ctx->d_bigpool);
+  (void)hipFree(ctx->d_ggap_lists);
+  (void)hipFree(ctx->d_ggap_counts);
+  (void)hipFree(ctx->d_ggap_pool);
+  (void)hipFree(ctx->d_ggap_stage);
   (void)hipFree(ctx->d_stage);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -1355,14 +1069,7 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   HIPCHK(hipMemsetAsync(hist, 0, (size_t)NKEYS * 4, st));
   HIPCHK(hipMemsetAsync(big_count, 0, 4, st));
   const int tb = 1024, nb = (n + tb - 1) / tb;
-  // stage timing: events on the launch stream around each kernel
-  auto mark = [&](int stage, int end) {
-    if (!ctx->prof_on) return;
-    hipEvent_t& e = ctx->ev[2 * stage + end];
-    if (!e) (void)hipEventCreate(&e);
-    (void)hipEventRecord(e, st);
-    ctx->ev_used[stage] = 1;
-  };
+  auto mark = [&](int stage, int end) { gsnapdp__mark(ctx, st, stage, end); };
   mark(0, 0);
   hipLaunchKernelGGL(k_plan, dim3(nb), dim3(tb), 0, st, d_windows, n, d_query, d_query_uc,
                      ctx->d_blocks, (uint64_t)ctx->nwords, ctx->d_prof, d_results, d_ops,
@@ -1431,7 +1138,17 @@ extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows,
   return 0;
 }
 
-static const char* const kStageNames[] = {"k_plan", "k_scan+k_scatter", "k_fill", "k_big"};
+// stage timing: events on the launch stream around each kernel
+void gsnapdp__mark(gsnapdp_ctx* ctx, hipStream_t st, int stage, int end) {
+  if (!ctx->prof_on) return;
+  hipEvent_t& e = ctx->ev[2 * stage + end];
+  if (!e) (void)hipEventCreate(&e);
+  (void)hipEventRecord(e, st);
+  ctx->ev_used[stage] = 1;
+}
+
+static const char* const kStageNames[] = {"k_plan", "k_scan+k_scatter", "k_fill", "k_big",
+                                          "k_ggap_plan", "k_ggap"};
 static const int kNStages = (int)(sizeof(kStageNames) / sizeof(kStageNames[0]));
 
 extern "C" const char* gsnapdp_stage_name(int stage) {
@@ -1453,6 +1170,7 @@ extern "C" int gsnapdp_profile_read(gsnapdp_ctx* ctx, double* ms, int nstages) {
     float t = 0.f;
     HIPCHK(hipEventElapsedTime(&t, ctx->ev[2 * i], ctx->ev[2 * i + 1]));
     ms[i] += (double)t;
+    ctx->ev_used[i] = 0;  // each read reports the stages recorded since the last one
   }
   return kNStages;
 }
@@ -1460,7 +1178,7 @@ extern "C" int gsnapdp_profile_read(gsnapdp_ctx* ctx, double* ms, int nstages) {
 extern "C" int gsnapdp_load_maxent_tables(gsnapdp_ctx* ctx, const double* tables, size_t nd) {
   if (!ctx) return -1;
   if (nd != (size_t)12 * 16384 + 4 * 16) {
-    set_err("maxent tables: expected 196672 doubles");
+    gsnapdp__set_err("maxent tables: expected 196672 doubles");
     return -1;
   }
   HIPCHK(hipSetDevice(ctx->device));
@@ -1474,7 +1192,7 @@ extern "C" int gsnapdp_maxent_device(gsnapdp_ctx* ctx, const uint8_t* d_model,
                                      const uint32_t* d_pos, const uint32_t* d_chroff,
                                      double* d_out, int n, void* stream_v) {
   if (!ctx || !ctx->d_tables) {
-    set_err("maxent tables not loaded");
+    gsnapdp__set_err("maxent tables not loaded");
     return -1;
   }
   if (n <= 0) return 0;

@@ -18,7 +18,7 @@ import os
 
 import numpy as np
 
-from .records import MAXENT_IN, PAIR, RESULT, WINDOW  # noqa: F401
+from .records import GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW, MAXENT_IN, PAIR, RESULT, WINDOW  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
@@ -68,6 +68,12 @@ def lib():
         L.gsnapdp_profile_read.restype = i32
         L.gsnapdp_stage_name.argtypes = [i32]
         L.gsnapdp_stage_name.restype = ctypes.c_char_p
+        L.gsnapdp_ggap_run_host.argtypes = [vp, vp, i32, vp, vp, sz, vp, vp, vp, vp]
+        L.gsnapdp_ggap_run_host.restype = i32
+        L.gsnapdp_ggap_run_device.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]
+        L.gsnapdp_ggap_run_device.restype = i32
+        L.gsnapdp_ggap_expand.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i32]
+        L.gsnapdp_ggap_expand.restype = i32
         _lib = L
     return _lib
 
@@ -80,6 +86,15 @@ def op_offsets(windows: np.ndarray) -> np.ndarray:
     """Per-window op capacity: a traceback takes at most L1 + L2 steps and
     every op consumes at least one step."""
     cap = windows["length1"].astype(np.int64).clip(0) + windows["length2"].astype(np.int64).clip(0) + 2
+    off = np.zeros(len(windows) + 1, dtype=np.int64)
+    np.cumsum(cap, out=off[1:])
+    return off
+
+
+def ggap_op_offsets(windows: np.ndarray) -> np.ndarray:
+    """Per-intron-window op capacity: two tracebacks of at most L1 + L2 + 1 steps."""
+    L1 = windows["length1"].astype(np.int64).clip(0)
+    cap = 2 * L1 + windows["length2L"].astype(np.int64).clip(0) + windows["length2R"].astype(np.int64).clip(0) + 4
     off = np.zeros(len(windows) + 1, dtype=np.int64)
     np.cumsum(cap, out=off[1:])
     return off
@@ -153,6 +168,49 @@ class Context:
             p, _ = self.pairs(windows, q, u, results, ops, off, i)
             outs.append(p)
             counts[i] = p.size
+        return (np.concatenate(outs) if outs else np.zeros(0, PAIR)), counts
+
+    def ggap_run(self, windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray):
+        """Dynprog_genome_gap on the GPU.  Returns (results, traces, ops, op_offsets)."""
+        w = np.ascontiguousarray(windows, dtype=GGAP_WINDOW)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        off = ggap_op_offsets(w)
+        res = np.zeros(len(w), dtype=GGAP_RESULT)
+        trc = np.zeros(len(w), dtype=GGAP_TRACE)
+        ops = np.zeros(max(1, int(off[-1])), dtype=np.uint32)
+        rc = lib().gsnapdp_ggap_run_host(self.h, _p(w), len(w), _p(q), _p(u), q.size, _p(res), _p(trc),
+                                         _p(ops), _p(off))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_ggap_run_host: %s" % lib().gsnapdp_last_error().decode())
+        return res, trc, ops, off
+
+    def ggap_run_device(self, d_windows: int, n: int, d_query: int, d_query_uc: int, d_results: int,
+                        d_traces: int, d_ops: int, d_op_offsets: int, stream: int = 0) -> None:
+        rc = lib().gsnapdp_ggap_run_device(
+            self.h, ctypes.c_void_p(d_windows), n, ctypes.c_void_p(d_query), ctypes.c_void_p(d_query_uc),
+            ctypes.c_void_p(d_results), ctypes.c_void_p(d_traces), ctypes.c_void_p(d_ops),
+            ctypes.c_void_p(d_op_offsets), ctypes.c_void_p(stream) if stream else None)
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_ggap_run_device: %s" % lib().gsnapdp_last_error().decode())
+
+    def ggap_all_pairs(self, windows, query, query_uc, results, traces, ops, off):
+        """The lists Dynprog_genome_gap returns, concatenated, and their lengths."""
+        w = np.ascontiguousarray(windows, dtype=GGAP_WINDOW)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        res = np.ascontiguousarray(results, dtype=GGAP_RESULT)
+        trc = np.ascontiguousarray(traces, dtype=GGAP_TRACE)
+        outs, counts = [], np.zeros(len(w), dtype=np.int32)
+        for i in range(len(w)):
+            cap = 2 * int(w["length1"][i]) + int(w["length2L"][i]) + int(w["length2R"][i]) + 8
+            out = np.zeros(cap, dtype=PAIR)
+            n = lib().gsnapdp_ggap_expand(self.h, _p(w[i:i + 1]), _p(res[i:i + 1]), _p(trc[i:i + 1]),
+                                          _p(ops[off[i]:]), _p(q), _p(u), _p(out), cap)
+            if n < 0:
+                raise GsnapdpError("gsnapdp_ggap_expand failed for window %d" % i)
+            outs.append(out[:n])
+            counts[i] = n
         return (np.concatenate(outs) if outs else np.zeros(0, PAIR)), counts
 
     def run_device(self, d_windows: int, n: int, d_query: int, d_query_uc: int, d_results: int,

@@ -45,6 +45,12 @@ GGAP_RESULT = np.dtype([
 ])
 assert GGAP_RESULT.itemsize == 64
 
+GGAP_TRACE = np.dtype([
+    ("brL", "<i4"), ("bcL", "<i4"), ("brR", "<i4"), ("bcR", "<i4"),
+    ("nops_right", "<i4"), ("nops_left", "<i4"), ("status", "<i4"), ("npairs", "<i4"),
+])
+assert GGAP_TRACE.itemsize == 32
+
 MAXENT_IN = np.dtype([("model", "<u4"), ("splice_pos", "<u4"), ("chroffset", "<u4"), ("pad", "<u4")])
 
 # enums (include/gsnapdp.h)

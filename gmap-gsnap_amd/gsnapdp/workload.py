@@ -8,6 +8,12 @@
 * ``random_windows``: broad parity mix over every window kind, strand,
   tie rule, quality bin, band, lowercase / ambiguity codes and chromosome
   edges ('*' columns).
+* ``ggap_windows``: Dynprog_genome_gap intron windows shaped like
+  traverse_genome_gap's (stage3.c:5770-5809), with planted canonical /
+  semi-canonical splice sites, plus (``mix=True``) every parameter the entry
+  point reads, long and odd-shaped windows and the early-return cases.
+* ``c4_windows``: the BASELINE config-4 intron batch (length1 22, length2
+  30, extraband_paired 7), vectorised.
 
 Deterministic for a given seed (numpy PCG64).
 """
@@ -16,8 +22,8 @@ from __future__ import annotations
 import numpy as np
 
 from . import genome as _genome
-from .records import (BEST_LOCAL, END3_GAP, END5_GAP, MAXLENGTH1, MAXLENGTH2, QUERYEND_GAP,
-                      QUERYEND_INDELS, QUERYEND_NOGAPS, SINGLE_GAP, WINDOW)
+from .records import (BEST_LOCAL, END3_GAP, END5_GAP, GGAP_WINDOW, MAXLENGTH1, MAXLENGTH2,
+                      QUERYEND_GAP, QUERYEND_INDELS, QUERYEND_NOGAPS, SINGLE_GAP, WINDOW)
 
 ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
 _COMP = np.arange(256, dtype=np.uint8)
@@ -230,6 +236,200 @@ def random_windows(gseq: np.ndarray, n: int, seed: int, kinds=(SINGLE_GAP, END5_
         qchunks.append(np.full(4, ord("#"), dtype=np.uint8))
         uchunks.append(np.full(4, ord("#"), dtype=np.uint8))
     return Batch(w, np.concatenate(qchunks), np.concatenate(uchunks))
+
+
+_SITES_FWD = (("GT", "AG"), ("GC", "AG"), ("AT", "AC"))
+_SITES_REV = (("CT", "AC"), ("CT", "GC"), ("GT", "AT"))
+
+
+def ggap_windows(gseq: np.ndarray, n: int, seed: int, mix: bool = True):
+    """Intron windows on a copy of gseq (splice sites are planted into it).
+    Returns (genome, Batch of GGAP_WINDOW)."""
+    rng = np.random.default_rng(seed)
+    g = gseq.copy()
+    Gn = g.size
+    w = np.zeros(n, dtype=GGAP_WINDOW)
+    qs, us = [], []
+    qpos = 0
+    for i in range(n):
+        u = rng.random()
+        if not mix:
+            L1 = int(rng.integers(2, 30))
+        elif u < 0.55:
+            L1 = int(rng.integers(2, 32))
+        elif u < 0.80:
+            L1 = int(rng.integers(32, 64))
+        elif u < 0.92:
+            L1 = int(rng.integers(64, 200))
+        elif u < 0.95:
+            L1 = int(rng.integers(200, 400))
+        else:
+            L1 = int(rng.integers(0, 3))
+        if mix and rng.random() < 0.3:
+            L2L = max(1, L1 + int(rng.integers(-1, 41)))
+            L2R = max(1, L1 + int(rng.integers(-1, 41)))
+            if rng.random() < 0.03:
+                L2R = max(1, L1 - int(rng.integers(2, 6)))  # shorter than length1 - 1
+        else:
+            L2L = L2R = L1 + 8
+        intron = int(rng.integers(40, 400))
+        glen = max(L2L, L2R) + L1 + intron + 60
+        chrpos = int(rng.integers(0, Gn - glen - 1))
+        watson = int(rng.integers(0, 2))
+        cdir = int(rng.choice([1, -1, 0]))
+        k = int(rng.integers(0, L1 + 1))
+        offset2L = int(rng.integers(5, 25))
+        donor = offset2L + k
+        acceptor_end = donor + intron
+        revoffset2R = acceptor_end + (L1 - k) - 1
+        if revoffset2R >= glen:
+            revoffset2R = glen - 1
+        if mix and rng.random() < 0.04:  # flanks running off the window: '*' columns
+            if rng.random() < 0.5:
+                offset2L = -int(rng.integers(1, 6))
+            else:
+                glen = revoffset2R - int(rng.integers(0, 4))
+
+        def absolute(x):
+            return chrpos + (x if watson else glen - 1 - x)
+
+        def put(x, ch):
+            if 0 <= x < glen:
+                c = ord(ch)
+                g[absolute(x)] = c if watson else _COMP[c]
+
+        r = rng.random()
+        sites = _SITES_FWD if cdir >= 0 else _SITES_REV
+        site = sites[0] if r < 0.6 else sites[1] if r < 0.75 else sites[2] if r < 0.85 else None
+        if site:
+            put(donor, site[0][0])
+            put(donor + 1, site[0][1])
+            put(acceptor_end - 2, site[1][0])
+            put(acceptor_end - 1, site[1][1])
+        lo, hi = max(0, offset2L), min(glen, acceptor_end + L1)
+        view = np.full(max(hi, 1), ord("A"), dtype=np.uint8)
+        xs = np.arange(lo, hi)
+        if xs.size:
+            view[lo:hi] = g[chrpos + xs] if watson else _COMP[g[chrpos + glen - 1 - xs]]
+        a = view[max(0, offset2L):max(0, offset2L) + k]
+        b = view[acceptor_end:acceptor_end + (L1 - k)] if acceptor_end < view.size else view[:0]
+        q = np.concatenate([a, b])
+        if q.size < L1:
+            q = np.concatenate([q, ACGT[rng.integers(0, 4, size=L1 - q.size)]])
+        q = _mutate(rng, q, 0.04, 0.01)
+        if rng.random() < 0.15 and L1 > 6:
+            p = int(rng.integers(1, L1 - 2))
+            q = np.concatenate([q[:p], q[p + 1:], ACGT[rng.integers(0, 4, size=1)]])
+        quc = q.copy()
+        if mix and rng.random() < 0.1 and L1 > 0:  # lowercase and ambiguity codes
+            m = rng.random(L1) < 0.3
+            q = q.copy()
+            q[m] = np.where(rng.random(int(m.sum())) < 0.7, q[m] + 32, _AMBIG[rng.integers(0, _AMBIG.size, int(m.sum()))])
+            quc = np.where((q >= 97) & (q <= 122), q - 32, q).astype(np.uint8)
+        qs += [q, np.full(4, ord("#"), np.uint8)]
+        us += [quc, np.full(4, ord("#"), np.uint8)]
+        rec = w[i]
+        rec["length1"], rec["length2L"], rec["length2R"] = L1, L2L, L2R
+        rec["offset1"] = int(rng.integers(0, 300))
+        rec["offset2L"], rec["revoffset2R"] = offset2L, revoffset2R
+        rec["chroffset"] = 0
+        rec["chrhigh"] = Gn
+        rec["chrpos"] = chrpos
+        rec["genomiclength"] = glen
+        rec["qpos"] = qpos
+        rec["cdna_direction"] = cdir
+        rec["extraband_paired"] = int(rng.choice([7, 3, 10, 0])) if mix else 7
+        rec["maxpeelback"] = int(rng.choice([11, 5, 40])) if mix else 11
+        rec["dynprogindex"] = int(rng.choice([-1, 2]))
+        small = mix and rng.random() < 0.01
+        rec["maxlength1"] = 20 if small else MAXLENGTH1
+        rec["maxlength2"] = 30 if small else MAXLENGTH2
+        rec["defect_rate"] = float(rng.choice([0.001, 0.005, 0.02]))
+        rec["watsonp"] = watson
+        rec["jump_late_p"] = int(rng.integers(0, 2))
+        rec["halfp"] = int(rng.random() < 0.2)
+        rec["finalp"] = int(rng.random() < 0.6)
+        rec["use_probabilities_p"] = int(rng.random() < 0.35)
+        rec["splicingp"] = int(rng.random() < 0.9)
+        rec["score_threshold"] = int(rng.integers(-20, 40)) if rec["use_probabilities_p"] else 0
+        qpos += L1 + 4
+    return g, Batch(w, np.concatenate(qs), np.concatenate(us))
+
+
+def c4_windows(gseq: np.ndarray, n: int, seed: int = 4, use_probabilities: bool = False,
+               length1: int = 22, extramaterial: int = 8, extraband: int = 7):
+    """BASELINE config 4: one Dynprog_genome_gap per intron, length1 =
+    2 x maxpeelback (11), length2L = length2R = length1 + 8, extraband_paired 7,
+    GT-AG introns of 80-5000 bp (60 % canonical, 25 % semi-canonical, 15 % none),
+    1 % substitutions; splice sites are planted into a copy of gseq.
+    Returns (genome, Batch)."""
+    rng = np.random.default_rng(seed)
+    g = gseq.copy()
+    L1, L2 = length1, length1 + extramaterial
+    intron = rng.integers(80, 5001, size=n)
+    k = rng.integers(0, L1 + 1, size=n)                  # query bases in exon 1
+    offset2L = np.full(n, 10)
+    glen = offset2L + L1 + intron + L2 + 10
+    chrpos = rng.integers(0, g.size - int(glen.max()) - 1, size=n)
+    donor = offset2L + k
+    acc_end = donor + intron
+    revoffset2R = acc_end + (L1 - k) - 1
+    watson = rng.integers(0, 2, size=n)
+    cdir = np.where(rng.random(n) < 0.5, 1, -1)
+    u = rng.random(n)
+    kind = np.where(u < 0.6, 0, np.where(u < 0.85, 1, 2))  # GT-AG, GC-AG, none
+
+    def absolute(x):
+        return np.where(watson == 1, chrpos + x, chrpos + glen - 1 - x)
+
+    def plant(x, chars_fwd, chars_rev, sel):
+        c = np.where(cdir > 0, np.frombuffer(chars_fwd, np.uint8)[kind.clip(0, 1)],
+                     np.frombuffer(chars_rev, np.uint8)[kind.clip(0, 1)])
+        c = np.where(watson == 1, c, _COMP[c])
+        g[absolute(x)[sel]] = c[sel]
+
+    has = kind < 2
+    plant(donor, b"GG", b"CC", has)        # GT / GC   |  CT / CT
+    plant(donor + 1, b"TC", b"TT", has)
+    plant(acc_end - 2, b"AA", b"AG", has)  # AG / AG   |  AC / GC
+    plant(acc_end - 1, b"GG", b"CC", has)
+    # query = exon-1 tail + exon-2 head in window orientation
+    j = np.arange(L1)[None, :]
+    x = np.where(j < k[:, None], offset2L[:, None] + j, acc_end[:, None] + (j - k[:, None]))
+    gi = np.where(watson[:, None] == 1, chrpos[:, None] + x, chrpos[:, None] + glen[:, None] - 1 - x)
+    q = g[gi]
+    q = np.where(watson[:, None] == 1, q, _COMP[q])
+    m = rng.random(q.shape) < 0.01
+    q[m] = ACGT[(np.searchsorted(ACGT, q[m]) + rng.integers(1, 4, size=int(m.sum()))) % 4]
+    q = np.concatenate([q, np.full((n, 4), ord("#"), np.uint8)], axis=1)
+    w = np.zeros(n, dtype=GGAP_WINDOW)
+    w["length1"] = L1
+    w["length2L"] = L2
+    w["length2R"] = L2
+    w["offset1"] = rng.integers(0, 300, size=n)
+    w["offset2L"] = offset2L
+    w["revoffset2R"] = revoffset2R
+    w["chroffset"] = 0
+    w["chrhigh"] = g.size
+    w["chrpos"] = chrpos
+    w["genomiclength"] = glen
+    w["qpos"] = np.arange(n) * (L1 + 4)
+    w["cdna_direction"] = cdir
+    w["extraband_paired"] = extraband
+    w["maxpeelback"] = 11
+    w["dynprogindex"] = 1
+    w["maxlength1"] = MAXLENGTH1
+    w["maxlength2"] = MAXLENGTH2
+    w["defect_rate"] = 0.001
+    w["watsonp"] = watson
+    w["jump_late_p"] = 0
+    w["halfp"] = 0
+    w["finalp"] = 1
+    w["use_probabilities_p"] = 1 if use_probabilities else 0
+    w["splicingp"] = 1
+    w["score_threshold"] = 0
+    qf = q.reshape(-1).copy()
+    return g, Batch(w, qf, qf.copy())
 
 
 def pack_genome(gseq: np.ndarray) -> np.ndarray:

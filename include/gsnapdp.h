@@ -162,6 +162,19 @@ typedef struct gsnapdp_ggap_result {
   double left_prob, right_prob;
 } gsnapdp_ggap_result;
 
+/* Where window i's tracebacks start and how its op stream splits: the right
+ * flank's ops (reversed fill, traced from (brR, bcR)) come first, then the
+ * left flank's (from (brL, bcL)); gsnapdp_ggap_expand replays them.
+ * status: 0 ok, 1 early return, 2 op overflow, 4 unsupported (the reference
+ * aborts or reads outside its matrices, or no MaxEnt tables were loaded for a
+ * window that needs them).  npairs = length of the returned list (0 = NULL). */
+typedef struct gsnapdp_ggap_trace {
+  int32_t brL, bcL, brR, bcR;
+  int32_t nops_right, nops_left;
+  int32_t status;
+  int32_t npairs;
+} gsnapdp_ggap_trace;
+
 /* ---------------------------------------------------------------- context */
 
 typedef struct gsnapdp_ctx gsnapdp_ctx;
@@ -225,6 +238,30 @@ int gsnapdp_maxent_host(gsnapdp_ctx *ctx, const uint8_t *model, const uint32_t *
                         const uint32_t *chroffset, double *out, int n);
 int gsnapdp_maxent_device(gsnapdp_ctx *ctx, const uint8_t *d_model, const uint32_t *d_splice_pos,
                           const uint32_t *d_chroffset, double *d_out, int n, void *stream);
+
+/* --------------------------------------------------------- genome gaps
+ * Dynprog_genome_gap (dynprog.c:4798-5061) for `n` intron windows: both flank
+ * fills, bridge_intron_gap (score or probability mode), the MaxEnt site
+ * probabilities and both tracebacks.  Window i may write at most
+ * op_offsets[i+1]-op_offsets[i] ops; 2*length1 + length2L + length2R + 4 always
+ * suffices.  Windows with use_probabilities_p or finalp need the MaxEnt tables
+ * (gsnapdp_load_maxent_tables).  The device form is asynchronous on `stream`;
+ * the host form copies in, runs and copies out. */
+int gsnapdp_ggap_run_device(gsnapdp_ctx *ctx, const gsnapdp_ggap_window *d_windows, int n,
+                            const char *d_query, const char *d_query_uc,
+                            gsnapdp_ggap_result *d_results, gsnapdp_ggap_trace *d_traces,
+                            uint32_t *d_ops, const int64_t *d_op_offsets, void *stream);
+int gsnapdp_ggap_run_host(gsnapdp_ctx *ctx, const gsnapdp_ggap_window *windows, int n,
+                          const char *query, const char *query_uc, size_t query_bytes,
+                          gsnapdp_ggap_result *results, gsnapdp_ggap_trace *traces, uint32_t *ops,
+                          const int64_t *op_offsets);
+/* Replay window i's two op streams into the reference's returned list (the
+ * right flank's pairs, the gapholder, then the left flank's, dynprog.c:5000-5058).
+ * Writes at most `cap` pairs; returns the list length (0 for NULL) or -1. */
+int gsnapdp_ggap_expand(gsnapdp_ctx *ctx, const gsnapdp_ggap_window *w,
+                        const gsnapdp_ggap_result *res, const gsnapdp_ggap_trace *trace,
+                        const uint32_t *ops, const char *query, const char *query_uc,
+                        gsnapdp_pair *pairs, int cap);
 
 /* Load the MaxEnt parameter tables (12 x 16384 + 4 x 16 doubles, order in
  * DESIGN.md) into the context.  Must be called before gsnapdp_maxent_*. */

@@ -1,0 +1,108 @@
+"""GPU parity of Dynprog_genome_gap (k_ggap_plan + k_ggap, through the C-ABI)
+against the reference's golden vectors and the CPU restatement they pin."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from gsnapdp import Context
+from gsnapdp import workload as W
+from gsnapdp.records import PAIR
+
+pytestmark = pytest.mark.gpu
+
+ALWAYS = ("finalscore", "nmatches", "nmismatches", "nopens", "nindels", "dynprogindex",
+          "returned_null", "bridge_ok")
+WITH_LIST = ("new_leftgenomepos", "new_rightgenomepos", "exonhead", "introntype")
+
+
+def load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+
+
+def unsupported_expected(w):
+    """Windows outside the reference's domain: it aborts (non-positive flank)
+    or its bridge reads diagonal cells past a flank's matrix rows."""
+    L1, L2L, L2R = (w[f].astype(np.int64) for f in ("length1", "length2L", "length2R"))
+    early = (L1 <= 1) | (L1 > w["maxlength1"]) | (L2L > w["maxlength2"]) | (L2R > w["maxlength2"])
+    return ~early & ((L2L <= 0) | (L2R <= 0) | (w["extraband_paired"] < 0) | (L2L < L1 - 1) | (L2R < L1 - 1))
+
+
+def compare(w, res, trc, pairs, npairs, ref, ref_pairs, ref_npairs, what):
+    uns = unsupported_expected(w)
+    assert np.array_equal(trc["status"] == 4, uns), "%s: unsupported set differs" % what
+    assert np.all(trc["status"] != 2), "%s: op stream overflow" % what
+    ok = ~uns
+    for f in ALWAYS:
+        bad = np.nonzero((res[f] != ref[f]) & ok)[0]
+        assert bad.size == 0, "%s: %s differs at %s (gpu %s ref %s)" % (
+            what, f, bad[:8], res[f][bad[:8]], ref[f][bad[:8]])
+    nn = ok & (ref["returned_null"] == 0)
+    for f in WITH_LIST:
+        bad = np.nonzero((res[f] != ref[f]) & nn)[0]
+        assert bad.size == 0, "%s: %s differs at %s" % (what, f, bad[:8])
+    for f in ("left_prob", "right_prob"):
+        bad = np.nonzero((res[f].view(np.uint64) != ref[f].view(np.uint64)) & ok)[0]
+        assert bad.size == 0, "%s: %s differs at %s" % (what, f, bad[:8])
+    bad = np.nonzero((npairs != ref_npairs) & ok)[0]
+    assert bad.size == 0, "%s: list length differs at %s (gpu %s ref %s)" % (
+        what, bad[:8], npairs[bad[:8]], ref_npairs[bad[:8]])
+    goff = np.concatenate([[0], np.cumsum(npairs)])
+    roff = np.concatenate([[0], np.cumsum(ref_npairs)])
+    sel = np.nonzero(ok)[0]
+    got = np.concatenate([pairs[goff[i]:goff[i + 1]] for i in sel] + [np.zeros(0, PAIR)])
+    exp = np.concatenate([ref_pairs[roff[i]:roff[i + 1]] for i in sel] + [np.zeros(0, PAIR)])
+    for f in PAIR.names:
+        bad = np.nonzero(got[f] != exp[f])[0]
+        assert bad.size == 0, "%s: pair field %s differs at pair %s" % (what, f, bad[:8])
+
+
+def run_gpu(blocks, b):
+    ctx = Context(blocks)
+    res, trc, ops, off = ctx.ggap_run(b.windows, b.query, b.query_uc)
+    pairs, npairs = ctx.ggap_all_pairs(b.windows, b.query, b.query_uc, res, trc, ops, off)
+    return res, trc, pairs, npairs
+
+
+def test_gpu_ggap_matches_reference_golden(golden_dir):
+    z = load(golden_dir, "ggap_chr17")
+    ctx = Context(z["blocks"])
+    assert "gfx950" in ctx.arch
+    w = z["windows"]
+    res, trc, ops, off = ctx.ggap_run(w, z["query"], z["query_uc"])
+    pairs, npairs = ctx.ggap_all_pairs(w, z["query"], z["query_uc"], res, trc, ops, off)
+    compare(w, res, trc, pairs, npairs, z["results"], z["pairs"], z["npairs"], "ggap_chr17")
+    assert np.sum(z["results"]["returned_null"] == 0) > len(w) // 2 and z["pairs"].size > 1000
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_gpu_ggap_matches_oracle_mix(seed):
+    """Every class (rows <= 31, <= 63, striped), both modes, odd shapes, early returns."""
+    g, b = W.ggap_windows(W.synthetic_genome(2_000_000, seed=seed, n_rate=0.002), 3000, seed=seed)
+    blocks = W.pack_genome(g)
+    res, trc, pairs, npairs = run_gpu(blocks, b)
+    O.setup(blocks)
+    ores, opairs, ooff, onp = O.run_ggap_batch(b.windows, b.query, b.query_uc)
+    oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
+    compare(b.windows, res, trc, pairs, npairs, ores, oflat, onp, "mix seed %d" % seed)
+    # the mix reaches every class with returned lists, in both bridge modes
+    L1 = b.windows["length1"]
+    listed = ores["returned_null"] == 0
+    for lo, hi in ((2, 32), (32, 64), (64, 400)):
+        assert np.sum(listed & (L1 >= lo) & (L1 < hi)) > 20, (lo, hi)
+    assert np.sum(listed & (b.windows["use_probabilities_p"] == 1)) > 100
+    assert np.sum(ores["bridge_ok"] == 0) > 0 and np.sum(trc["status"] == 1) > 0
+
+
+@pytest.mark.parametrize("prob", [False, True])
+def test_gpu_c4_parity(prob):
+    """BASELINE config 4 shape, score and probability modes."""
+    g, b = W.c4_windows(W.synthetic_genome(8_000_000, seed=4), 20_000, seed=4, use_probabilities=prob)
+    blocks = W.pack_genome(g)
+    res, trc, pairs, npairs = run_gpu(blocks, b)
+    O.setup(blocks)
+    ores, opairs, ooff, onp = O.run_ggap_batch(b.windows, b.query, b.query_uc)
+    oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
+    compare(b.windows, res, trc, pairs, npairs, ores, oflat, onp, "C4 prob=%s" % prob)
+    assert np.mean(ores["returned_null"] == 0) > 0.8 and oflat.size > 20 * len(b.windows)

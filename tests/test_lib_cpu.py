@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import gsnapdp
-from gsnapdp.records import GGAP_RESULT, GGAP_WINDOW, PAIR, RESULT, WINDOW
+from gsnapdp.records import GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW, PAIR, RESULT, WINDOW
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -36,14 +36,14 @@ def test_library_targets_gfx950_only():
 def test_record_layouts_match_c(tmp_path):
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include "%s/include/gsnapdp.h"\n'
-                   'int main(){printf("%%zu %%zu %%zu %%zu %%zu\\n", sizeof(gsnapdp_window), '
+                   'int main(){printf("%%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(gsnapdp_window), '
                    'sizeof(gsnapdp_result), sizeof(gsnapdp_pair), sizeof(gsnapdp_ggap_window), '
-                   'sizeof(gsnapdp_ggap_result));return 0;}\n' % ROOT)
+                   'sizeof(gsnapdp_ggap_result), sizeof(gsnapdp_ggap_trace));return 0;}\n' % ROOT)
     exe = tmp_path / "sz"
     subprocess.check_call(["gcc", "-o", str(exe), str(src)])
     sizes = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     assert sizes == [WINDOW.itemsize, RESULT.itemsize, PAIR.itemsize, GGAP_WINDOW.itemsize,
-                     GGAP_RESULT.itemsize]
+                     GGAP_RESULT.itemsize, GGAP_TRACE.itemsize]
 
 
 def test_no_gpu_means_loud_failure():
