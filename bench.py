@@ -40,6 +40,7 @@ OPS_PER_CELL = 14             # gap1 4 + gap2 4 + nogap 6 int32 
 READS_PER_GPU = 100_000
 GENOME_NT = 64_000_000
 DOMINANT = "k_fill"           # every C2 window is a register-band (k_fill) window
+C4_WINDOWS = 200_000          # intron windows per config-4 step
 
 
 def window_bytes(w: np.ndarray, nops: np.ndarray) -> np.ndarray:
@@ -80,6 +81,64 @@ def pmc_traffic(kernel: str):
     return best
 
 
+def measure_c4(genome, n, steps, warmup, dev, with_cpu):
+    """Side measurement, BASELINE config 4: Dynprog_genome_gap on intron windows
+    (length1 22, length2 30, extraband_paired 7), score and probability modes,
+    device-resident, timed like the main line; CPU restatement (1 core) beside it."""
+    from gsnapdp import ggap_op_offsets
+    from gsnapdp.records import GGAP_RESULT, GGAP_TRACE
+    out = {"workload": "C4: Dynprog_genome_gap, %d intron windows per step, length1 22, "
+                       "length2L/R 30, extraband_paired 7, finalp" % n, "unit": "windows/s"}
+    for mode in ("score", "prob"):
+        g, b = W.c4_windows(genome, n, seed=4, use_probabilities=(mode == "prob"))
+        blocks = W.pack_genome(g)
+        ctx = Context(blocks, mode=0, device=dev.index)
+        off = ggap_op_offsets(b.windows)
+        d_w = torch.from_numpy(b.windows.view(np.uint8).copy()).to(dev)
+        d_q = torch.from_numpy(b.query.copy()).to(dev)
+        d_res = torch.zeros(n * GGAP_RESULT.itemsize, dtype=torch.uint8, device=dev)
+        d_trc = torch.zeros(n * GGAP_TRACE.itemsize, dtype=torch.uint8, device=dev)
+        d_ops = torch.zeros(int(off[-1]) + 1, dtype=torch.int32, device=dev)
+        d_off = torch.from_numpy(off.copy()).to(dev)
+
+        def step():
+            ctx.ggap_run_device(d_w.data_ptr(), n, d_q.data_ptr(), d_q.data_ptr(), d_res.data_ptr(),
+                                d_trc.data_ptr(), d_ops.data_ptr(), d_off.data_ptr())
+        for _ in range(warmup):
+            step()
+        ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        ctx.sync()
+        el = time.perf_counter() - t0
+        names = ctx.profile(True)
+        acc = np.zeros(len(names))
+        for _ in range(steps):
+            step()
+            ctx.profile_read(acc)
+        ctx.profile(False)
+        rec = {"value": round(n * steps / el, 1), "ms_per_step": round(1000 * el / steps, 4),
+               "kernel_ms_per_step": {nm: round(acc[i] / steps, 4) for i, nm in enumerate(names) if acc[i] > 0}}
+        if with_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+            O.setup(blocks)
+            sample = min(n, 40_000)
+            t1 = time.perf_counter()
+            ores, _, _, _ = O.run_ggap_batch(b.windows[:sample], b.query, b.query)
+            cpu = sample / (time.perf_counter() - t1)
+            res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=GGAP_RESULT)[:sample]
+            rec["cpu_baseline"] = {"value": round(cpu, 1), "unit": "windows/s", "cores": 1, "kind": "port",
+                                   "sample": "%d C4 windows, oracle/ restatement, 1 thread" % sample}
+            rec["parity_bit_exact"] = bool(all(np.array_equal(res[f], ores[f]) for f in
+                                               ("finalscore", "nmatches", "nmismatches", "nopens", "nindels",
+                                                "returned_null", "dynprogindex")))
+        out[mode] = rec
+        ctx.close()
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -87,6 +146,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--reads", type=int, default=READS_PER_GPU)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-c4", action="store_true", help="skip the config-4 (genome gap) side line")
+    ap.add_argument("--c4-windows", type=int, default=C4_WINDOWS)
     args = ap.parse_args()
 
     ranks = shard.init_from_env("nccl")
@@ -210,6 +271,8 @@ def main() -> None:
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        if not args.no_c4 and world == 1:
+            out["c4"] = measure_c4(genome, args.c4_windows, args.steps, args.warmup, dev, not args.no_cpu)
         print(json.dumps(out), flush=True)
     shard.finish(ranks)
     ctx.close()

@@ -34,6 +34,7 @@ struct State {
   int device = 0;
   gsnapdp_ctx* ctx = nullptr;
   bool tables = false;
+  bool splicing_iit = false;  // Dynprog_setup got known splice sites
   std::vector<char> q, qu;
   std::vector<uint32_t> ops;
   std::vector<gsnapdp_pair> pairs;
@@ -191,12 +192,16 @@ char* Dynprog_endalign_string(gsnapdp_Endalign_T endalign) {  // dynprog.c:335-3
   }
 }
 
-// Known-site data only feeds Dynprog_genome_gap / splicejunction paths, which
-// this library does not serve yet; the genome arrives through
-// Gsnapdp_dropin_genome.
-void Dynprog_setup(gsnapdp_bool, gsnapdp_IIT_T, int*, int, int, gsnapdp_Genomicpos_T*,
-                   gsnapdp_Splicetype_T*, gsnapdp_Genomicpos_T*, int, unsigned int*,
-                   unsigned int*, unsigned int*, unsigned int*, gsnapdp_Genome_T) {}
+// Known-site data only feeds the known-site modes of bridge_intron_gap and the
+// splicejunction paths, which this library does not serve:
+// Dynprog_genome_gap aborts when a splice-site IIT was given.  The genome
+// arrives through Gsnapdp_dropin_genome.
+void Dynprog_setup(gsnapdp_bool, gsnapdp_IIT_T splicing_iit, int*, int, int,
+                   gsnapdp_Genomicpos_T*, gsnapdp_Splicetype_T*, gsnapdp_Genomicpos_T*, int,
+                   unsigned int*, unsigned int*, unsigned int*, unsigned int*, gsnapdp_Genome_T) {
+  std::lock_guard<std::mutex> lock(g.mu);
+  g.splicing_iit = splicing_iit != nullptr;  // dynprog.c:360
+}
 
 int Dynprog_score(int matches, int mismatches, int qopens, int qindels, int topens, int tindels,
                   double defect_rate) {  // dynprog.c:381-394 (open -10, extend -3 in every bin)
@@ -293,6 +298,120 @@ gsnapdp_List_T Dynprog_end3_gap(
   w.endalign = (uint8_t)endalign;
   return run_one(w, sequence1, sequenceuc1, false, pairpool, dynprogindex, finalscore, nmatches,
                  nmismatches, nopens, nindels);
+}
+
+gsnapdp_List_T Dynprog_genome_gap(
+    int* dynprogindex, int* finalscore, int* new_leftgenomepos, int* new_rightgenomepos,
+    double* left_prob, double* right_prob, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, int* exonhead, int* introntype, gsnapdp_Dynprog_T dynprogL,
+    gsnapdp_Dynprog_T dynprogR, char* sequence1, char* sequenceuc1, char*, char*, char*, char*,
+    int length1, int length2L, int length2R, int offset1, int offset2L, int revoffset2R,
+    int /*chrnum: known sites only*/, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, char* /*genomicuc_ptr*/, gsnapdp_bool use_genomicseg_p,
+    int cdna_direction, gsnapdp_bool watsonp, gsnapdp_bool jump_late_p,
+    gsnapdp_Pairpool_T pairpool, int extraband_paired, double defect_rate, int maxpeelback,
+    gsnapdp_bool halfp, gsnapdp_bool finalp, gsnapdp_bool use_probabilities_p,
+    int score_threshold, gsnapdp_bool splicingp) {  // dynprog.c:4798-5061
+  std::lock_guard<std::mutex> lock(g.mu);
+  if (g.splicing_iit) fatal("Dynprog_genome_gap with a splice-site IIT is not served");
+  if (use_genomicseg_p && (use_probabilities_p || finalp))
+    fatal("Dynprog_genome_gap: genomic-segment MaxEnt probabilities are not served");
+  gsnapdp_ctx* c = ctx();
+  if (use_probabilities_p || finalp) ensure_tables();
+  const Dynprog* dL = (const Dynprog*)dynprogL;
+  const Dynprog* dR = (const Dynprog*)dynprogR;
+  gsnapdp_ggap_window w;
+  memset(&w, 0, sizeof(w));
+  w.length1 = length1;
+  w.length2L = length2L;
+  w.length2R = length2R;
+  w.offset1 = offset1;
+  w.offset2L = offset2L;
+  w.revoffset2R = revoffset2R;
+  w.chroffset = chroffset;
+  w.chrhigh = chrhigh;
+  w.chrpos = chrpos;
+  w.genomiclength = genomiclength;
+  w.qpos = 0;
+  w.cdna_direction = cdna_direction;
+  w.extraband_paired = extraband_paired;
+  w.maxpeelback = maxpeelback;
+  w.score_threshold = score_threshold;
+  w.dynprogindex = *dynprogindex;
+  // the two workspaces' limits (:4898-4927), folded into one exact test
+  const bool too_long = length1 > dL->maxlength1 || length2L > dL->maxlength2 ||
+                        length1 > dR->maxlength1 || length2R > dR->maxlength2;
+  w.maxlength1 = too_long ? -1 : 0x3fffffff;
+  w.maxlength2 = 0x3fffffff;
+  w.defect_rate = defect_rate < 0.003 ? 0.001f : (defect_rate < 0.014 ? 0.01f : 0.5f);
+  w.watsonp = watsonp ? 1 : 0;
+  w.jump_late_p = jump_late_p ? 1 : 0;
+  w.halfp = halfp ? 1 : 0;
+  w.finalp = finalp ? 1 : 0;
+  w.use_probabilities_p = use_probabilities_p ? 1 : 0;
+  w.splicingp = splicingp ? 1 : 0;
+  const int L1 = length1 > 0 ? length1 : 0;
+  g.q.assign((size_t)L1 + 8, 0);
+  g.qu.assign((size_t)L1 + 8, 0);
+  if (L1 > 0) {
+    memcpy(g.q.data(), sequence1, (size_t)L1);
+    memcpy(g.qu.data(), sequenceuc1, (size_t)L1);
+  }
+  const int64_t cap = 2 * (int64_t)L1 + (length2L > 0 ? length2L : 0) + (length2R > 0 ? length2R : 0) + 4;
+  const int64_t off[2] = {0, cap};
+  g.ops.assign((size_t)cap + 1, 0u);
+  gsnapdp_ggap_result r;
+  gsnapdp_ggap_trace t;
+  if (gsnapdp_ggap_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, &t, g.ops.data(), off))
+    fatal(std::string("gsnapdp_ggap_run_host: ") + gsnapdp_last_error());
+  if (t.status == gsnapdp::ST_UNSUPPORTED)
+    fatal("genome-gap window outside the reference's domain (the reference aborts or reads past its matrices)");
+  if (t.status == gsnapdp::ST_OPS_OVERFLOW) fatal("op stream overflow");
+  // out-parameters exactly as the reference writes them on each path
+  *nmatches = *nmismatches = *nopens = *nindels = 0;  // :4853-4854
+  *left_prob = *right_prob = 0.0;
+  *finalscore = r.finalscore;
+  *dynprogindex = r.dynprogindex;
+  if (t.status == gsnapdp::ST_EARLY) {
+    if (too_long) {  // :4898-4927
+      *new_leftgenomepos = r.new_leftgenomepos;
+      *new_rightgenomepos = r.new_rightgenomepos;
+      *exonhead = r.exonhead;
+    }
+    return nullptr;
+  }
+  // probability mode without a qualifying candidate reads uninitialised
+  // indices in the reference (:4055); here it is defined as NULL, NEG_INFINITY
+  if (r.bridge_ok == 0) return nullptr;
+  // bridge_intron_gap writes *introntype only when a score-mode candidate is
+  // taken; none taken leaves bestscore (and bestscoreI) at -100000
+  if (!use_probabilities_p && r.finalscore != (halfp ? -50000 : -100000)) *introntype = r.introntype;
+  if (r.finalscore < 0) return nullptr;  // bridge rejected (:4084)
+  *new_leftgenomepos = r.new_leftgenomepos;
+  *new_rightgenomepos = r.new_rightgenomepos;
+  *exonhead = r.exonhead;
+  *left_prob = r.left_prob;
+  *right_prob = r.right_prob;
+  *nmatches = r.nmatches;
+  *nmismatches = r.nmismatches;
+  *nopens = r.nopens;
+  *nindels = r.nindels;
+  if (r.returned_null) return nullptr;  // only the gapholder (:5050-5053)
+  g.pairs.resize((size_t)cap + 8);
+  const int n = gsnapdp_ggap_expand(c, &w, &r, &t, g.ops.data(), g.q.data(), g.qu.data(),
+                                    g.pairs.data(), (int)g.pairs.size());
+  if (n < 0 || n > (int)g.pairs.size()) fatal("gsnapdp_ggap_expand failed");
+  gsnapdp_List_T list = nullptr;
+  for (int i = n - 1; i >= 0; i--) {
+    const gsnapdp_pair& p = g.pairs[(size_t)i];
+    if (p.gapp)
+      list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump, /*knownp*/ 0);
+    else
+      list = Pairpool_push(list, pairpool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome,
+                           p.dynprogindex);
+  }
+  return list;
 }
 
 void Maxent_hr_setup(unsigned int* ref_blocks) {  // maxent_hr.c:27195

@@ -76,6 +76,20 @@ gsnapdp_List_T Dynprog_single_gap(
     gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_single,
     double defect_rate, int close_indels_mode, gsnapdp_bool widebandp); /* dynprog.c:4450 */
 
+gsnapdp_List_T Dynprog_genome_gap(
+    int* dynprogindex, int* finalscore, int* new_leftgenomepos, int* new_rightgenomepos,
+    double* left_prob, double* right_prob, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, int* exonhead, int* introntype, gsnapdp_Dynprog_T dynprogL,
+    gsnapdp_Dynprog_T dynprogR, char* sequence1, char* sequenceuc1, char* sequence2L,
+    char* sequenceuc2L, char* revsequence2R, char* revsequenceuc2R, int length1, int length2L,
+    int length2R, int offset1, int offset2L, int revoffset2R, int chrnum,
+    gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, char* genomicuc_ptr, gsnapdp_bool use_genomicseg_p,
+    int cdna_direction, gsnapdp_bool watsonp, gsnapdp_bool jump_late_p,
+    gsnapdp_Pairpool_T pairpool, int extraband_paired, double defect_rate, int maxpeelback,
+    gsnapdp_bool halfp, gsnapdp_bool finalp, gsnapdp_bool use_probabilities_p,
+    int score_threshold, gsnapdp_bool splicingp); /* dynprog.c:4798 (non-PMAP; chrnum is Chrnum_T, chrnum.h:8) */
+
 gsnapdp_List_T Dynprog_end5_gap(
     int* dynprogindex, int* finalscore, int* nmatches, int* nmismatches, int* nopens,
     int* nindels, gsnapdp_Dynprog_T dynprog, char* revsequence1, char* revsequenceuc1,

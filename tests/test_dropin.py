@@ -160,3 +160,77 @@ def test_dropin_maxent_matches_reference_golden(golden_dir, tmp_path):
         got = fns[int(z["model"][i])](int(z["splice_pos"][i]), int(z["chroffset"][i]))
         assert np.float64(got).tobytes() == np.float64(z["prob"][i]).tobytes(), i
     L.Dynprog_term()
+
+
+# 4 int*, 2 double*, 6 int* out-parameters, dynprogL, dynprogR; 6 sequences
+GGAP_ARGS = ([ctypes.c_void_p] * 14 + [ctypes.c_char_p] * 6 + [ctypes.c_int] * 6 + [ctypes.c_int]
+             + [ctypes.c_uint] * 4 + [ctypes.c_char_p, ctypes.c_ubyte, ctypes.c_int, ctypes.c_ubyte,
+                                     ctypes.c_ubyte, ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
+                                     ctypes.c_int, ctypes.c_ubyte, ctypes.c_ubyte, ctypes.c_ubyte,
+                                     ctypes.c_int, ctypes.c_ubyte])
+
+
+@pytest.mark.gpu
+def test_dropin_genome_gap_matches_reference_golden(golden_dir, tmp_path):
+    """Dynprog_genome_gap called like traverse_genome_gap (stage3.c:5772) on the
+    reference's golden intron windows: every out-parameter and the list."""
+    z = np.load(os.path.join(golden_dir, "ggap_chr17.npz"), allow_pickle=False)
+    dbl = load_double(tmp_path)
+    L = ctypes.CDLL(DROPIN)
+    L.Dynprog_new.restype = ctypes.c_void_p
+    L.Dynprog_new.argtypes = [ctypes.c_int] * 5
+    L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    L.Dynprog_genome_gap.restype = ctypes.c_void_p
+    L.Dynprog_genome_gap.argtypes = GGAP_ARGS
+    blocks = np.ascontiguousarray(z["blocks"])
+    L.Dynprog_init(600, 10, 11, 10, 8, 0)
+    L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
+    dpL = L.Dynprog_new(600, 10, 11, 10, 8)
+    dpR = L.Dynprog_new(600, 10, 11, 10, 8)
+    q = np.ascontiguousarray(z["query"])
+    qu = np.ascontiguousarray(z["query_uc"])
+    offs = np.zeros(len(z["npairs"]) + 1, dtype=np.int64)
+    np.cumsum(z["npairs"], out=offs[1:])
+    out = np.zeros(8192, dtype=REC)
+    ref = z["results"]
+    W = z["windows"]
+    for i in range(min(300, len(W))):
+        w = W[i]
+        ints = [ctypes.c_int(int(w["dynprogindex"]))] + [ctypes.c_int(-77) for _ in range(3)]
+        probs = [ctypes.c_double(-1.0), ctypes.c_double(-1.0)]
+        counts = [ctypes.c_int(-77) for _ in range(6)]  # nmatches .. introntype
+        seq = ctypes.c_char_p(q.ctypes.data + int(w["qpos"]))
+        sequc = ctypes.c_char_p(qu.ctypes.data + int(w["qpos"]))
+        args = ([ctypes.byref(x) for x in ints] + [ctypes.byref(x) for x in probs]
+                + [ctypes.byref(x) for x in counts] + [dpL, dpR, seq, sequc, None, None, None, None]
+                + [int(w[f]) for f in ("length1", "length2L", "length2R", "offset1", "offset2L",
+                                       "revoffset2R")]
+                + [0] + [int(w[f]) for f in ("chroffset", "chrhigh", "chrpos", "genomiclength")]
+                + [None, 0, int(w["cdna_direction"]), int(w["watsonp"]), int(w["jump_late_p"]), None,
+                   int(w["extraband_paired"]), float(w["defect_rate"]), int(w["maxpeelback"]),
+                   int(w["halfp"]), int(w["finalp"]), int(w["use_probabilities_p"]),
+                   int(w["score_threshold"]), int(w["splicingp"])])
+        lst = L.Dynprog_genome_gap(*args)
+        r = ref[i]
+        assert ints[0].value == r["dynprogindex"] and ints[1].value == r["finalscore"], i
+        assert [c.value for c in counts[:4]] == [int(r[f]) for f in ("nmatches", "nmismatches", "nopens",
+                                                                     "nindels")], i
+        assert np.float64(probs[0].value).view(np.uint64) == np.float64(r["left_prob"]).view(np.uint64), i
+        assert np.float64(probs[1].value).view(np.uint64) == np.float64(r["right_prob"]).view(np.uint64), i
+        if r["returned_null"] == 0:
+            assert [ints[2].value, ints[3].value, counts[4].value] == [
+                int(r[f]) for f in ("new_leftgenomepos", "new_rightgenomepos", "exonhead")], i
+        # *introntype is written only when a score-mode bridge candidate was taken
+        # (dynprog.c:3720-3800); the golden driver passes it in as 0
+        untouched = (w["use_probabilities_p"] == 1 or w["length1"] <= 1
+                     or r["finalscore"] in (-100000, -50000 if w["halfp"] else -100000, -1000000))
+        assert counts[5].value == (-77 if untouched else int(r["introntype"])), i
+        k = dbl.dbl_list_read(lst, out.ctypes.data, out.size) if lst else 0
+        ref_pairs = z["pairs"][offs[i]:offs[i + 1]]
+        assert k == ref_pairs.size, (i, k, ref_pairs.size)
+        assert out[:k].tobytes() == ref_pairs.tobytes(), i
+        if lst:
+            dbl.dbl_list_free(lst)
+    L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dpL)))
+    L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dpR)))
+    L.Dynprog_term()
