@@ -92,11 +92,13 @@ struct Tally {
 // traceback (dynprog.c:2611-2712) with the reference's memset semantics for
 // cells outside the band and the row-0 / column-0 initialisation
 // (dynprog.c:1460-1488).
-template <class Dirs>
-__device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c,
-                                 const char* __restrict__ q, const char* __restrict__ qu,
-                                 const uint32_t* __restrict__ blocks, uint64_t nwords,
-                                 const uint32_t* __restrict__ prof, Tally& t, OpWriter& ow) {
+//
+// `colcls(c)` is the genome class (0..5 = A C G T N *) of column c in 1..L2;
+// `qrow(r)` is row r's query byte | uppercase query byte << 8.
+template <class Dirs, class Col, class QRow>
+__device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c, const QRow& qrow,
+                                 const Col& colcls, const uint32_t* __restrict__ prof, Tally& t,
+                                 OpWriter& ow) {
   const int lband = L.d.lband, rband = L.d.rband;
   auto inband = [&](int rr, int cc) {
     const int d = rr - cc + rband;
@@ -116,11 +118,11 @@ __device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c,
   while (inband(r, c)) {
     const uint32_t nib = dirs(r, c);
     // the nogap cell (r,c) itself: one pair unless the genome is '*'
-    const int g = gclass(blocks, nwords, L, L.g0 + L.gstep * (c - 1));
+    const int g = colcls(c);
     if (g != 5) {
-      const int qi = L.qbase + L.qstep * (r - 1);
-      const unsigned char c1 = qchar(q, qi);
-      const unsigned char u1 = (unsigned char)qu[qi];
+      const uint32_t qq = qrow(r);
+      const unsigned char c1 = (unsigned char)(qq & 127u);
+      const unsigned char u1 = (unsigned char)(qq >> 8);
       const unsigned char gch = (unsigned char)("ACGTN"[g]);
       if (u1 == gch || ((ptab[c1] >> (24 + g)) & 1u)) t.nmatches++;
       else t.nmismatches++;
@@ -152,13 +154,14 @@ __device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c,
       c--;
       bool dashes = true;
       if (dist >= MICROINTRON_LENGTH) {
-        // columns c+1 .. c+dist are skipped; left = column c+1, right = column c+dist
+        // columns c+1 .. c+dist are skipped; left = column c+1, right = column c+dist.
+        // In window-coordinate order (leftgenomecoord < rightgenomecoord) the
+        // dinucleotides sit at the skip's two ends; a reversed fill runs the
+        // columns backwards along the genome.
         const int cl = c + 1, cr = c + dist;
-        const int gl = L.g0 + L.gstep * (cl - 1), gr = L.g0 + L.gstep * (cr - 1);
-        // in window-coordinate order (leftgenomecoord < rightgenomecoord)
-        const int lo = L.d.rev ? gr : gl, hi = L.d.rev ? gl : gr;
-        const int l1 = gclass(blocks, nwords, L, lo), l2 = gclass(blocks, nwords, L, lo + 1);
-        const int r2 = gclass(blocks, nwords, L, hi - 1), r1 = gclass(blocks, nwords, L, hi);
+        const int rv = L.d.rev;
+        const int l1 = colcls(rv ? cr : cl), l2 = colcls(rv ? cr - 1 : cl + 1);
+        const int r2 = colcls(rv ? cl + 1 : cr - 1), r1 = colcls(rv ? cl : cr);
         dashes = intron_type_codes(l1, l2, r2, r1, L.cdna_direction) == 0;
       }
       ow.flush();

@@ -66,7 +66,7 @@ struct GGeo {
   int L1, L2L, L2R, eb;
   int lbL, rbL, WL, lbR, rbR, WR;
   int mt, open, ext, canon;
-  int oHR, oClsL, oClsR, oProbL, oProbR, oBnd, words;
+  int oHR, oClsL, oClsR, oDiL, oDiR, oItab, oQ, oProbL, oProbR, oBnd, words;
 };
 
 __device__ __host__ inline void fill_bands(int L1, int L2, int eb, int& lb, int& rb) {
@@ -104,7 +104,11 @@ __device__ inline GGeo gg_geo(const gsnapdp_ggap_window& w) {
   G.oHR = l1 * G.WL;
   G.oClsL = G.oHR + l1 * G.WR;
   G.oClsR = G.oClsL + (G.L2L + 2 + 3) / 4;
-  int o = G.oClsR + (G.L2R + 2 + 3) / 4;
+  G.oDiL = G.oClsR + (G.L2R + 2 + 3) / 4;     // leftdi[0 .. L2L]   (bytes)
+  G.oDiR = G.oDiL + (G.L2L + 1 + 3) / 4;      // rightdi[0 .. L2R]  (bytes)
+  G.oItab = G.oDiR + (G.L2R + 1 + 3) / 4;     // intron score | type << 8 by leftdi & rightdi (64 x u16)
+  G.oQ = G.oItab + 32;                        // query | uppercase << 8 per query index (u16)
+  int o = G.oQ + (l1 + 1) / 2;
   o = (o + 1) & ~1;
   G.oProbL = o;
   G.oProbR = o + 2 * G.L2L;
@@ -398,32 +402,55 @@ __global__ __launch_bounds__(256) void k_ggap(
           rp[c] = c < G.L2R - 1 ? right_site_prob(w, c, blocks, nwords, tables) : 0.0;
       }
     }
+    using PH = typename std::conditional<GMEM, AS_GLOBAL uint16_t*, AS_LDS uint16_t*>::type;
+    const PB diL = (PB)(region + G.oDiL);
+    const PB diR = (PB)(region + G.oDiR);
+    const PH itab = (PH)(region + G.oItab);
+    const PH qb = (PH)(region + G.oQ);
+    if (act) {
+      for (int i = rho; i < G.L1; i += RL)
+        qb[i] = (uint16_t)((unsigned char)q[w.qpos + i] | ((unsigned)(unsigned char)qu[w.qpos + i] << 8));
+      for (int t = rho; t < 64; t += RL) {  // intron_score by leftdi & rightdi (:3148-3192)
+        int it;
+        const int sI = intron_score(it, t, 0x3F, w.cdna_direction, G.canon, w.finalp);
+        itab[t] = (uint16_t)(sI | (it << 8));
+      }
+    }
     if constexpr (GMEM) __threadfence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the class bytes are in LDS
+    if (act) {  // leftdi / rightdi (:3331-3373); 0 past the scanned columns (calloc)
+      for (int c = rho; c <= G.L2L; c += RL)
+        diL[c] = (uint8_t)(c < G.L2L - 1 ? left_di(clsL[c + 1], clsL[c + 2]) : 0);
+      for (int c = rho; c <= G.L2R; c += RL)
+        diR[c] = (uint8_t)(c < G.L2R - 1 ? right_di(clsR[c + 2], clsR[c + 1]) : 0);
+    }
     // wave-uniform step and stripe counts
     const int L2max = max(G.L2L, G.L2R);
-    const int T = __builtin_amdgcn_readfirstlane(wave_max(act ? L2max : 0)) + RL;
+    // the last row's lane reaches column L2 at step L2 + L1; a striped window's
+    // last lane writes the boundary row through step L2 + RL - 1
+    const int T = __builtin_amdgcn_readfirstlane(
+        wave_max(act ? L2max + (GMEM ? RL : G.L1 + 1) : 0));
     const int NS = __builtin_amdgcn_readfirstlane(wave_max(act ? G.L1 + 1 : 1) + RL - 1) / RL;
     const uint32_t* ptab = prof + G.mt * 128;
     const Side<P> SL = {HL, G.L2L, G.lbL, G.rbL, G.WL};
     const Side<P> SR = {HR, G.L2R, G.lbR, G.rbR, G.WR};
     // left flank forward with jump_late_p, right flank reversed with !jump_late_p (:4955-4990)
     const int jl = w.jump_late_p ? 1 : 0;
+#ifndef GG_EXP_NOFILL
     gg_fill<RL, GMEM>(SL, clsL, bnd, G.L1, rho, G.open, G.ext, jl, q, (int)w.qpos, 1, ptab, T, NS);
+#endif
+#ifndef GG_EXP_NOFILL
     gg_fill<RL, GMEM>(SR, clsR, bnd, G.L1, rho, G.open, G.ext, 1 - jl, q, (int)w.qpos + G.L1 - 1,
                       -1, ptab, T, NS);
+#endif
     if constexpr (GMEM) __threadfence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);
 
     // ---- bridge_intron_gap (dynprog.c:3290-4122), lane = rL
     const int leftoffset = w.offset2L, rightoffset = w.revoffset2R;
     const int lbandB = G.eb, rbandBL = G.L2L - G.L1 + G.eb, rbandBR = G.L2R - G.L1 + G.eb;
-    auto ldi = [&](int cL) {  // leftdi[cL], 0 past the scanned columns (calloc)
-      return cL >= 0 && cL < G.L2L - 1 ? left_di(clsL[cL + 1], clsL[cL + 2]) : 0;
-    };
-    auto rdi = [&](int cR) {
-      return cR >= 0 && cR < G.L2R - 1 ? right_di(clsR[cR + 2], clsR[cR + 1]) : 0;
-    };
+    if constexpr (GMEM) __threadfence();
+    else __builtin_amdgcn_s_waitcnt(0xc07f);  // the dinucleotide codes are in LDS
     auto HLv = [&](int r, int c) { return (int)HL[(r - 1) * G.WL + (c - r + G.lbL)]; };
     auto HRv = [&](int r, int c) { return (int)HR[(r - 1) * G.WR + (c - r + G.lbR)]; };
     auto pen = [](int v) { return (v & 12) ? 1 : 0; };  // nogap dir HORIZ or VERT
@@ -434,72 +461,83 @@ __global__ __launch_bounds__(256) void k_ggap(
     best.rL = best.cL = best.rR = best.cR = 0;
     best.sI = BRIDGE_INIT;
     best.itype = 0;
+#ifdef GG_EXP_NOBRIDGE
+    const int rows = 0;
+#else
     const int rows = __builtin_amdgcn_readfirstlane(wave_max(act ? G.L1 : 0));
+#endif
+    const int span = rightoffset - leftoffset;  // cR < span - cL (:3720, 3760)
     for (int r0 = 0; r0 < rows; r0 += RL) {
       const int rL = r0 + rho;
       if (rL < 1 || rL >= G.L1) continue;
       const int rR = G.L1 - rL;
-      const int cloL = max(1, rL - lbandB), chighL = min(G.L2L - 1, rL + rbandBL);
-      const int cloR = max(1, rR - lbandB), chighR = min(G.L2R - 1, rR + rbandBR);
+      const int cloL = max(1, rL - lbandB), chighL = min(min(G.L2L - 1, rL + rbandBL), span - rR - 1);
+      const int cloR = max(1, rR - lbandB), chighR = min(min(G.L2R - 1, rR + rbandBR), span - rL - 1);
       const int DR = HRv(rR, rR) >> 4;  // (rR, rR): on the right band's main diagonal
       const int DL = HLv(rL, rL) >> 4;
-      for (int cL = cloL; cL <= chighL; cL++) {  // indel on left
-        const int cR = rR;
-        if (!(cR < rightoffset - leftoffset - cL)) continue;
-        if (probmode) {
-          const double p = lp[cL] + (cR < G.L2R - 1 ? rp[cR] : 0.0);
+      const int rdR = diR[rR], ldL = diL[rL];
+      const int baseL = (rL - 1) * G.WL - rL + G.lbL, baseR = (rR - 1) * G.WR - rR + G.lbR;
+      if (probmode) {
+        const double pR = rR < G.L2R - 1 ? rp[rR] : 0.0;
+        const double pL = rL < G.L2L - 1 ? lp[rL] : 0.0;
+        for (int cL = cloL; cL <= chighL; cL++) {  // indel on left, cR = rR
+          const double p = lp[cL] + pR;
           if (!(p > best.prob)) continue;
-          const int v = HLv(rL, cL);
-          int it;
-          const int sI = intron_score(it, ldi(cL), rdi(cR), w.cdna_direction, G.canon, w.finalp);
-          const int tot = (v >> 4) - pen(v) + sI + DR;
+          const int v = (int)HL[baseL + cL];
+          const int tot = (v >> 4) - pen(v) + (itab[diL[cL] & rdR] & 255) + DR;
           if (tot >= w.score_threshold) {
             best.prob = p;
             best.key = 2 * rL;
-            best.rL = rL; best.cL = cL; best.rR = rR; best.cR = cR;
+            best.cL = cL;
+            best.cR = rR;
           }
-        } else {
-          const int v = HLv(rL, cL);
-          int it;
-          const int sI = intron_score(it, ldi(cL), rdi(cR), w.cdna_direction, G.canon, w.finalp);
-          const int tot = (v >> 4) - pen(v) + sI + DR;
+        }
+        for (int cR = cloR; cR <= chighR; cR++) {  // indel on right, cL = rL
+          const double p = pL + rp[cR];
+          if (!(p > best.prob)) continue;
+          const int v = (int)HR[baseR + cR];
+          const int tot = DL + (itab[ldL & diR[cR]] & 255) + (v >> 4) - pen(v);
+          if (tot >= w.score_threshold) {
+            best.prob = p;
+            best.key = 2 * rL + 1;
+            best.cL = rL;
+            best.cR = cR;
+          }
+        }
+      } else {
+        for (int cL = cloL; cL <= chighL; cL++) {  // indel on left, cR = rR
+          const int v = (int)HL[baseL + cL];
+          const int e = itab[diL[cL] & rdR];
+          const int tot = (v >> 4) - pen(v) + (e & 255) + DR;
           if (tot > best.score) {
             best.score = tot;
             best.key = 2 * rL;
-            best.sI = sI;
-            best.itype = it;
-            best.rL = rL; best.cL = cL; best.rR = rR; best.cR = cR;
+            best.sI = e;  // score | type << 8 until the reduction
+            best.cL = cL;
+            best.cR = rR;
+          }
+        }
+        for (int cR = cloR; cR <= chighR; cR++) {  // indel on right, cL = rL
+          const int v = (int)HR[baseR + cR];
+          const int e = itab[ldL & diR[cR]];
+          const int tot = DL + (e & 255) + (v >> 4) - pen(v);
+          if (tot > best.score) {
+            best.score = tot;
+            best.key = 2 * rL + 1;
+            best.sI = e;
+            best.cL = rL;
+            best.cR = cR;
           }
         }
       }
-      for (int cR = cloR; cR <= chighR; cR++) {  // indel on right
-        const int cL = rL;
-        if (!(cL < rightoffset - leftoffset - cR)) continue;
-        if (probmode) {
-          const double p = (cL < G.L2L - 1 ? lp[cL] : 0.0) + rp[cR];
-          if (!(p > best.prob)) continue;
-          const int v = HRv(rR, cR);
-          int it;
-          const int sI = intron_score(it, ldi(cL), rdi(cR), w.cdna_direction, G.canon, w.finalp);
-          const int tot = DL + sI + (v >> 4) - pen(v);
-          if (tot >= w.score_threshold) {
-            best.prob = p;
-            best.key = 2 * rL + 1;
-            best.rL = rL; best.cL = cL; best.rR = rR; best.cR = cR;
-          }
-        } else {
-          const int v = HRv(rR, cR);
-          int it;
-          const int sI = intron_score(it, ldi(cL), rdi(cR), w.cdna_direction, G.canon, w.finalp);
-          const int tot = DL + sI + (v >> 4) - pen(v);
-          if (tot > best.score) {
-            best.score = tot;
-            best.key = 2 * rL + 1;
-            best.sI = sI;
-            best.itype = it;
-            best.rL = rL; best.cL = cL; best.rR = rR; best.cR = cR;
-          }
-        }
+    }
+    // the lane's rows of its best candidate
+    if (best.key != 0x7fffffff) {
+      best.rL = best.key >> 1;
+      best.rR = G.L1 - best.rL;
+      if (!probmode) {
+        best.itype = best.sI >> 8;
+        best.sI &= 255;
       }
     }
     best = group_best<RL>(best, probmode);
@@ -523,7 +561,7 @@ __global__ __launch_bounds__(256) void k_ggap(
         } else {
           const int vl = HLv(best.rL, best.cL), vr = HRv(best.rR, best.cR);
           int it;
-          const int sI = intron_score(it, ldi(best.cL), rdi(best.cR), w.cdna_direction, G.canon,
+          const int sI = intron_score(it, diL[best.cL], diR[best.cR], w.cdna_direction, G.canon,
                                       w.finalp);
           const int sL = (vl >> 4) - pen(vl), sR = (vr >> 4) - pen(vr);
           finalscore = w.halfp ? sL + sI + sR - sI / 2 : sL + sI + sR;
@@ -563,12 +601,19 @@ __global__ __launch_bounds__(256) void k_ggap(
         const int cap = (int)(op_off[wi + 1] - o0);
         Tally t = {0, 0, 0, 0, 0};
         OpWriter owR = {ops + o0, cap, 0, 0};
-        traceback(CellDirs<P>{HR, G.WR, G.lbR}, LR, best.rR, best.cR, q, qu, blocks, nwords,
+#ifndef GG_EXP_NOTRACE
+        const int L1 = G.L1;
+        traceback(CellDirs<P>{HR, G.WR, G.lbR}, LR, best.rR, best.cR,
+                  [&](int r) -> uint32_t { return qb[L1 - r]; }, [&](int c) -> int { return clsR[c]; },
                   prof, t, owR);
+#endif
         const int nR = owR.n < cap ? owR.n : cap;
         OpWriter owL = {ops + o0 + nR, cap - nR, 0, 0};
-        traceback(CellDirs<P>{HL, G.WL, G.lbL}, LL, best.rL, best.cL, q, qu, blocks, nwords,
+#ifndef GG_EXP_NOTRACE
+        traceback(CellDirs<P>{HL, G.WL, G.lbL}, LL, best.rL, best.cL,
+                  [&](int r) -> uint32_t { return qb[r - 1]; }, [&](int c) -> int { return clsL[c]; },
                   prof, t, owL);
+#endif
         X.nops_right = nR;
         X.nops_left = owL.n < owL.cap ? owL.n : owL.cap;
         if (owR.n > cap || owL.n > owL.cap) X.status = ST_OPS_OVERFLOW;

@@ -913,7 +913,12 @@ __global__ __launch_bounds__(64) void k_big(
     BigDirs dirs = {D, NKd, rband};
     Tally t = {0, 0, 0, 0};
     OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
-    traceback(dirs, L, r0, c0, q, qu, blocks, nwords, prof, t, ow);
+    auto colcls = [&](int cc) { return gclass(blocks, nwords, L, L.g0 + L.gstep * (cc - 1)); };
+    auto qrow = [&](int rr) -> uint32_t {
+      const int qi = L.qbase + L.qstep * (rr - 1);
+      return (uint32_t)(unsigned char)q[qi] | ((uint32_t)(unsigned char)qu[qi] << 8);
+    };
+    traceback(dirs, L, r0, c0, qrow, colcls, prof, t, ow);
     write_result(&res[wi], w, L, score, r0, c0, t, ow);
   }
 }
