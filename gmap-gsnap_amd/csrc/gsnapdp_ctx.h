@@ -13,6 +13,11 @@ void gsnapdp__set_err(const std::string& s);
 struct gsnapdp_ctx;
 // per-stage HIP events around a launch (gsnapdp_profile); stage < 16
 void gsnapdp__mark(gsnapdp_ctx* ctx, hipStream_t st, int stage, int end);
+// k_rows over the three row-lane class lists (gsnapdp_ggap.hip)
+int gsnapdp__rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d_windows,
+                         const int* lists, const int* counts, int list_cap, const char* d_query,
+                         const char* d_query_uc, gsnapdp_result* d_results, uint32_t* d_ops,
+                         const int64_t* d_op_offsets);
 
 #define HIPCHK(x)                                                                        \
   do {                                                                                   \
@@ -39,11 +44,11 @@ struct gsnapdp_ctx {
   int* d_keys = nullptr;
   int* d_perm = nullptr;
   int* d_big_list = nullptr;
-  int* d_small = nullptr;  // hist[NKEYS] | cursor[NKEYS] | class_start[NCLASS+1] | big_count
+  int* d_small = nullptr;  // hist[NKEYS] | cursor[NKEYS] | class_start[NCLASS+1] | row-lane counts
   size_t perm_cap = 0;
   uint32_t* d_dirpool = nullptr;
   size_t dirpool_waves = 0;
-  uint32_t* d_bigpool = nullptr;
+  uint32_t* d_bigpool = nullptr;   // global scratch of the large row-lane windows (k_rows)
   // host-run staging
   size_t stage_cap = 0;
   void* d_stage = nullptr;

@@ -199,6 +199,58 @@ __device__ inline int agg_atomic_inc(int* counter, int key) {
   return pos;
 }
 
+// Final bookkeeping shared by all paths.
+__device__ inline void write_result(gsnapdp_result* res, const gsnapdp_window& w, const Lane& L,
+                                    int score, int bestr, int bestc, const Tally& t,
+                                    const OpWriter& ow) {
+  gsnapdp_result R;
+  R.finalscore = score;
+  R.nmatches = t.nmatches;
+  R.nmismatches = t.nmismatches;
+  R.nopens = t.nopens;
+  R.nindels = t.nindels;
+  R.bestr = bestr;
+  R.bestc = bestc;
+  R.nops = ow.n < ow.cap ? ow.n : ow.cap;
+  R.status = ow.n > ow.cap ? ST_OPS_OVERFLOW : ST_OK;
+  R.length1 = L.d.L1;
+  R.length2 = L.d.L2;
+  R.reserved = step_dpi(w.dynprogindex);
+  // end gaps, QUERYEND_GAP / BEST_LOCAL: dynprog.c:5259-5262 / 5715-5718
+  if (L.d.mode == 1 && t.nmatches + 1 < t.nmismatches) {
+    R.finalscore = 0;
+    if (R.status == ST_OK) R.status = ST_ZEROED;
+  }
+  // QUERYEND_NOGAPS rescoring: dynprog.c:5243 / 5700
+  if (L.d.mode == 3) R.finalscore = t.nmatches * 3 + t.nmismatches * (-5);
+  *res = R;
+}
+
+// ------------------------------------------------- row-lane window classes
+// Windows the register-band kernel does not take (end gaps, wide or long
+// single gaps) run on the row-lane kernel k_rows (gsnapdp_ggap.hip): rows on
+// lanes, band cells (H << 4 | dirs) in LDS, or in global scratch when large.
+enum { RW_SMALL = 0, RW_MID = 1, RW_BIG = 2, RW_NCLS = 3 };
+constexpr int RW_SMALL_WORDS = 1280;             // LDS words per window, 32-row groups
+constexpr int RW_MID_WORDS = 4096;               // LDS words per window, 64-row stripes
+constexpr size_t RW_BIG_WORDS = (size_t)2 << 20; // global words per wave
+constexpr int RW_BIG_WAVES = 128;
+
+// storage of one window: band cells, column classes (bytes), query (u16 per
+// row) and, for more than one 64-row stripe, the boundary row (3 words per column)
+__host__ __device__ inline size_t rows_words(int L1, int L2, int W) {
+  const size_t stripes = ((size_t)L1 + 1 + 63) / 64;
+  return (size_t)L1 * W + ((size_t)L2 + 2 + 3) / 4 + ((size_t)L1 + 1) / 2 +
+         (stripes > 1 ? 3 * ((size_t)L2 + 2) : 0);
+}
+__host__ __device__ inline int rows_class(int L1, int L2, int W) {
+  const size_t words = rows_words(L1, L2, W);
+  if (L1 + 1 <= 32 && words <= (size_t)RW_SMALL_WORDS) return RW_SMALL;
+  if (words <= (size_t)RW_MID_WORDS) return RW_MID;
+  if (words <= RW_BIG_WORDS) return RW_BIG;
+  return -1;
+}
+
 // ---------------------------------------------------------------- maxent
 // Maxent_hr_{donor,acceptor,antidonor,antiacceptor}_prob (maxent_hr.c:27217-27390).
 // The reference's 32 shift-specialised handlers all read a k-mer `off` nt past

@@ -49,7 +49,14 @@ constexpr int BRIDGE_INIT = -100000;  // bestscore / bestscoreI start (:3302)
 
 // window classes of the batch
 enum { GG_SMALL = 0, GG_MID = 1, GG_BIG = 2, GG_NCLS = 3 };
-constexpr int GG_SMALL_WORDS = 1536;      // LDS words per window, RL = 32 (2 per wave)
+#ifndef GG_SMALL_WORDS_CFG
+#define GG_SMALL_WORDS_CFG 1280
+#endif
+#ifndef GG_WAVES
+#define GG_WAVES 4
+#endif
+constexpr int GG_SMALL_WORDS = GG_SMALL_WORDS_CFG;  // LDS words per window, RL = 32 (2 per wave)
+constexpr int GG_SMALL_BLOCKS = 160 * 1024 / (8 * GG_SMALL_WORDS * 4);  // blocks per CU that fit in LDS
 constexpr int GG_MID_WORDS = 4096;        // LDS words per window, RL = 64
 constexpr size_t GG_BIG_WORDS = (size_t)4 << 20;  // global words per wave of the large path
 constexpr int GG_BIG_WAVES = 32;
@@ -255,54 +262,53 @@ __device__ void gg_fill(const Side<P>& sd, PB cls, P bnd, int L1, int rho, int o
     // genome classes A C G T N * as signed nibbles (build_profile_table)
     const int rq = (r >= 1 && r <= L1) ? r : 1;
     const uint32_t pw = ptab[(unsigned char)q[qrow0 + qstep * (rq - 1)] & 127u];
+    // this row's band columns [cmin, cmax] (empty for row 0 and rows past L1)
+    const int cmin0 = max(1, r - lband), cmax = min(L2, r + rband);
+    const bool rowok = r >= 1 && r <= L1 && cmax >= cmin0;
+    const int cmin = rowok ? cmin0 : (1 << 30);  // c - cmin < 0: never in band
+    const uint32_t cspan = rowok ? (uint32_t)(cmax - cmin0) : 0u;
+    // initial values (dynprog.c:1460-1488): row 0 E = open + c*extend for
+    // 1 <= c <= rband, H(0,0) = 0; column 0 F = open + r*extend for r <= lband
+    const uint32_t e0span = r == 0 ? (uint32_t)min(rband, L2) : 0u;  // c - 1 < e0span
+    const int hz = r == 0 ? 0 : -(1 << 30);                           // H(r, c) = 0 iff c == hz
+    const int F0 = (r >= 1 && r <= lband && r <= L1) ? open + r * ext : NEG;
+    // store slot: row r's band starts at column r - lband
+    const int sbase = (r - 1) * W - r + lband;
     int Hc = NEG, Ec = NEG, Fc = NEG;      // (r, c-1)
     int Hup = NEG, Eup = NEG, Fup = NEG;   // (r-1, c-1)
+    int erun = open - rho * ext;           // open + c * extend, c = t - rho
+    int g = (int)cls[max(0, min(L2 + 1, -rho))];
     for (int t = 0; t < T; t++) {
       const int c = t - rho;
+      const int gn = (int)cls[max(0, min(L2 + 1, c + 1))];  // next column's class
       int Hn = from_above(Hc), En = from_above(Ec), Fn = from_above(Fc);  // (r-1, c)
-      if (GMEM && rho == 0 && s > 0) {
+      if (rho == 0 && s > 0) {  // row above the stripe: the boundary row
         const bool ok = c >= 0 && c <= L2;
         const int cc = ok ? c : 0;
         Hn = ok ? (int)bnd[3 * cc] : NEG;
         En = ok ? (int)bnd[3 * cc + 1] : NEG;
         Fn = ok ? (int)bnd[3 * cc + 2] : NEG;
       }
-      int H = NEG, E = NEG, F = NEG;
-      uint32_t nib = 0;
-      bool store = false;
-      if (c >= 0 && c <= L2 && r <= L1) {
-        if (r == 0) {  // row 0 (dynprog.c:1460-1475)
-          H = c == 0 ? 0 : NEG;
-          E = (c >= 1 && c <= rband) ? open + c * ext : NEG;
-        } else if (c == 0) {  // column 0 (:1477-1488)
-          F = r <= lband ? open + r * ext : NEG;
-        } else if (r >= c - rband && r <= c + lband) {
-          // gap1 from (r, c-1), gap2 from (r-1, c), nogap from (r-1, c-1), each
-          // with the sequential tie rule (:1519-1561): x wins ties iff jump_late
-          const int a = Hc + open;
-          const bool tE = Ec > a - jl;
-          E = (tE ? Ec : a) + ext;
-          const int b = Hn + open;
-          const bool tF = Fn > b - jl;
-          F = (tF ? Fn : b) + ext;
-          int best = Hup;
-          uint32_t d = 0;
-          if (Eup > best - jl) {
-            best = Eup;
-            d = 4;
-          }
-          if (Fup > best - jl) {
-            best = Fup;
-            d = 8;
-          }
-          const int g = (int)cls[c];
-          H = best + __builtin_amdgcn_sbfe((int)pw, 4 * g, 4);
-          nib = (tE ? 1u : 0u) | (tF ? 2u : 0u) | d;
-          store = true;
-        }
+      // the recurrences (:1519-1561), each with the tie rule "x wins ties iff jump_late"
+      const int a = Hc + open;
+      const bool tE = Ec > a - jl;
+      const int Er = (tE ? Ec : a) + ext;
+      const int b = Hn + open;
+      const bool tF = Fn > b - jl;
+      const int Fr = (tF ? Fn : b) + ext;
+      const bool hE = Eup > Hup - jl;
+      const int m1 = hE ? Eup : Hup;
+      const bool hF = Fup > m1 - jl;
+      const int Hr = (hF ? Fup : m1) + __builtin_amdgcn_sbfe((int)pw, 4 * g, 4);
+      const bool inb = (uint32_t)(c - cmin) <= cspan;
+      const int H = inb ? Hr : (c == hz ? 0 : NEG);
+      const int E = inb ? Er : ((uint32_t)(c - 1) < e0span ? erun : NEG);
+      const int F = inb ? Fr : (c == 0 ? F0 : NEG);
+      if (inb) {
+        const uint32_t nib = (tE ? 1u : 0u) | (tF ? 2u : 0u) | (hF ? 8u : (hE ? 4u : 0u));
+        sd.H[sbase + c] = ((uint32_t)H << 4) | nib;
       }
-      if (store) sd.H[(r - 1) * W + (c - r + lband)] = ((uint32_t)H << 4) | nib;
-      if (GMEM && rho == RL - 1 && c >= 0 && c <= L2) {
+      if (NS > 1 && rho == RL - 1 && c >= 0 && c <= L2) {
         bnd[3 * c] = (uint32_t)H;
         bnd[3 * c + 1] = (uint32_t)E;
         bnd[3 * c + 2] = (uint32_t)F;
@@ -313,8 +319,12 @@ __device__ void gg_fill(const Side<P>& sd, PB cls, P bnd, int L1, int rho, int o
       Hc = H;
       Ec = E;
       Fc = F;
+      erun += ext;
+      g = gn;
     }
-    if (GMEM) __threadfence();  // the boundary row is read by the next stripe's lane 0
+    // the boundary row is read by the next stripe's lane 0
+    if constexpr (GMEM) __threadfence();
+    else __builtin_amdgcn_s_waitcnt(0xc07f);
   }
 }
 
@@ -351,7 +361,7 @@ __device__ inline Cand group_best(Cand c, bool probmode) {
 }
 
 template <int RL, bool GMEM>
-__global__ __launch_bounds__(256) void k_ggap(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8))) void k_ggap(
     const gsnapdp_ggap_window* __restrict__ Wn, const int* __restrict__ list,
     const int* __restrict__ count, const char* __restrict__ q, const char* __restrict__ qu,
     const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
@@ -429,7 +439,7 @@ __global__ __launch_bounds__(256) void k_ggap(
     // the last row's lane reaches column L2 at step L2 + L1; a striped window's
     // last lane writes the boundary row through step L2 + RL - 1
     const int T = __builtin_amdgcn_readfirstlane(
-        wave_max(act ? L2max + (GMEM ? RL : G.L1 + 1) : 0));
+        wave_max(act ? L2max + (G.L1 + 1 > RL ? RL : G.L1 + 1) : 0));
     const int NS = __builtin_amdgcn_readfirstlane(wave_max(act ? G.L1 + 1 : 1) + RL - 1) / RL;
     const uint32_t* ptab = prof + G.mt * 128;
     const Side<P> SL = {HL, G.L2L, G.lbL, G.rbL, G.WL};
@@ -634,6 +644,120 @@ __global__ __launch_bounds__(256) void k_ggap(
   }
 }
 
+// Every window the register-band kernel does not take: end gaps (all
+// endpoint modes but QUERYEND_NOGAPS, which k_plan finishes) and single gaps
+// with W > 48 or L2 > 640.  Fill as in k_ggap (one flank, forward or reversed),
+// then the endpoint -- (L1, L2) for a single gap, find_best_endpoint
+// (dynprog.c:2235-2290) or find_best_endpoint_to_queryend_indels (:2293-2355)
+// for end gaps, as a row-parallel scan with an ordered argmax -- and the
+// traceback (:2611-2712) by the group leader.
+template <int RL, bool GMEM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8))) void k_rows(
+    const gsnapdp_window* __restrict__ Wn, const int* __restrict__ list,
+    const int* __restrict__ count, const char* __restrict__ q, const char* __restrict__ qu,
+    const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
+    uint32_t* __restrict__ pool, size_t stride, gsnapdp_result* __restrict__ res,
+    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
+  extern __shared__ uint32_t smem[];
+  using P = typename std::conditional<GMEM, AS_GLOBAL uint32_t*, AS_LDS uint32_t*>::type;
+  using PB = typename std::conditional<GMEM, AS_GLOBAL uint8_t*, AS_LDS uint8_t*>::type;
+  using PH = typename std::conditional<GMEM, AS_GLOBAL uint16_t*, AS_LDS uint16_t*>::type;
+  constexpr int NGW = 64 / RL;
+  const int lane = threadIdx.x & 63, grp = lane / RL, rho = lane % RL;
+  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+  P region;
+  if constexpr (GMEM) {
+    region = (P)(pool + (size_t)gw * stride);
+  } else {
+    region = (P)(smem + ((threadIdx.x >> 6) * NGW + grp) * stride);
+  }
+  const int n = *count;
+  for (int base = gw * NGW; base < n; base += nw * NGW) {
+    const int k = base + grp;
+    const bool act = k < n;
+    const int wi = list[act ? k : base];
+    const gsnapdp_window w = Wn[wi];
+    const Lane L = make_lane(w);
+    const Derived& d = L.d;
+    const int L1 = act ? d.L1 : 0, L2 = d.L2, W = d.W;
+    const P H = region;
+    const PB cls = (PB)(region + L1 * W);
+    const PH qb = (PH)(region + L1 * W + (L2 + 2 + 3) / 4);
+    const P bnd = region + L1 * W + (L2 + 2 + 3) / 4 + (L1 + 1) / 2;
+    if (act) {
+      for (int c = rho; c <= L2 + 1; c += RL)
+        cls[c] = (uint8_t)((c >= 1 && c <= L2) ? gclass(blocks, nwords, L, L.g0 + L.gstep * (c - 1)) : 5);
+      for (int i = rho; i < L1; i += RL) {
+        const int qi = L.qbase + L.qstep * i;
+        qb[i] = (uint16_t)((unsigned char)q[qi] | ((unsigned)(unsigned char)qu[qi] << 8));
+      }
+    }
+    if constexpr (GMEM) __threadfence();
+    else __builtin_amdgcn_s_waitcnt(0xc07f);
+    const int T = __builtin_amdgcn_readfirstlane(wave_max(act ? L2 + (L1 + 1 > RL ? RL : L1 + 1) : 0));
+    const int NS = __builtin_amdgcn_readfirstlane(wave_max(act ? L1 + 1 : 1) + RL - 1) / RL;
+    const Side<P> sd = {H, L2, d.lband, d.rband, W};
+    gg_fill<RL, GMEM>(sd, cls, bnd, L1, rho, d.open, d.ext, d.jl, q, L.qbase, L.qstep,
+                      prof + d.mt * 128, T, NS);
+    if constexpr (GMEM) __threadfence();
+    else __builtin_amdgcn_s_waitcnt(0xc07f);
+    // ---- endpoint: a row-parallel scan, then the first (or, with jump_late,
+    // the last) best cell in row-major order
+    const int jl = d.jl;
+    int best, key;  // key = r * (L2 + 1) + c
+    if (d.mode == 1) {
+      best = 0;  // find_best_endpoint starts at (0, 0) with 0 (:2243)
+      key = 0;
+    } else {
+      best = NEG;  // queryend_indels starts at (L1, 0) with NEG_INFINITY (:2302)
+      key = L1 * (L2 + 1);
+    }
+    const int rows = __builtin_amdgcn_readfirstlane(wave_max(act && d.mode != 0 ? L1 : 0));
+    for (int r0 = 0; r0 < rows; r0 += RL) {
+      const int r = r0 + rho + 1;
+      if (r > L1 || (d.mode == 2 && r != L1)) continue;
+      // mode 1: the unwidened band |r - c| <= extraband; mode 2: the widened band
+      const int clo = max(1, d.mode == 1 ? r - d.eb : r - d.lband);
+      const int chi = min(L2, d.mode == 1 ? r + d.eb : r + d.rband);
+      const int rb = (r - 1) * W - r + d.lband;
+      for (int c = clo; c <= chi; c++) {
+        const int v = (int)H[rb + c] >> 4;
+        if (v > best - jl) {
+          best = v;
+          key = r * (L2 + 1) + c;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = RL / 2; o > 0; o >>= 1) {
+      const int ob = __shfl_xor(best, o), ok = __shfl_xor(key, o);
+      if (ob > best || (ob == best && (jl ? ok > key : ok < key))) {
+        best = ob;
+        key = ok;
+      }
+    }
+    if (act && rho == 0) {
+      int br, bc, score;
+      if (d.mode == 0) {
+        br = L1;
+        bc = L2;
+        score = (int)H[(L1 - 1) * W + (L2 - L1 + d.lband)] >> 4;  // matrix[L1][L2].nogap (:4534)
+      } else {
+        br = key / (L2 + 1);
+        bc = key - br * (L2 + 1);
+        score = best;
+      }
+      Tally t = {0, 0, 0, 0, 0};
+      OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
+      traceback(CellDirs<P>{H, W, d.lband}, L, br, bc,
+                [&](int r) -> uint32_t { return qb[r - 1]; }, [&](int c) -> int { return cls[c]; },
+                prof, t, ow);
+      write_result(&res[wi], w, L, score, br, bc, t, ow);
+    }
+  }
+}
+
 // Parameters, early returns (dynprog.c:4843-4870) and the class of every
 // window; windows that reach the fills are appended to their class list.
 __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
@@ -671,9 +795,10 @@ __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
       X.status = ST_UNSUPPORTED;
     } else {
       done = false;
+      const int bndw = G.L1 + 1 > 64 ? 3 * (max(G.L2L, G.L2R) + 2) : 0;  // stripe boundary row
       if (G.L1 + 1 <= 32 && G.words <= GG_SMALL_WORDS) cls = GG_SMALL;
-      else if (G.L1 + 1 <= 64 && G.words <= GG_MID_WORDS) cls = GG_MID;
-      else if ((size_t)G.words + 3 * (size_t)(max(G.L2L, G.L2R) + 2) <= GG_BIG_WORDS) cls = GG_BIG;
+      else if (G.words + bndw <= GG_MID_WORDS) cls = GG_MID;
+      else if ((size_t)G.words + bndw <= GG_BIG_WORDS) cls = GG_BIG;
       else {
         done = true;
         R.finalscore = NEG;
@@ -695,6 +820,31 @@ __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
 }
 
 }  // namespace
+
+// ======================================================================
+// Host side (include/gsnapdp.h: gsnapdp_ggap_*; k_rows for gsnapdp_run_device)
+// ======================================================================
+int gsnapdp__rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d_windows,
+                         const int* lists, const int* counts, int list_cap, const char* d_query,
+                         const char* d_query_uc, gsnapdp_result* d_results, uint32_t* d_ops,
+                         const int64_t* d_op_offsets) {
+  const uint64_t nw = (uint64_t)ctx->nwords;
+  constexpr int small_blocks = 160 * 1024 / (8 * RW_SMALL_WORDS * 4);
+  hipLaunchKernelGGL((k_rows<32, false>), dim3(ctx->num_cus * small_blocks), dim3(256),
+                     (size_t)8 * RW_SMALL_WORDS * 4, st, d_windows, lists, counts + RW_SMALL,
+                     d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, (uint32_t*)nullptr,
+                     (size_t)RW_SMALL_WORDS, d_results, d_ops, d_op_offsets);
+  hipLaunchKernelGGL((k_rows<64, false>), dim3(ctx->num_cus * 2), dim3(256),
+                     (size_t)4 * RW_MID_WORDS * 4, st, d_windows, lists + (size_t)RW_MID * list_cap,
+                     counts + RW_MID, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
+                     (uint32_t*)nullptr, (size_t)RW_MID_WORDS, d_results, d_ops, d_op_offsets);
+  hipLaunchKernelGGL((k_rows<64, true>), dim3(RW_BIG_WAVES), dim3(64), 0, st, d_windows,
+                     lists + (size_t)RW_BIG * list_cap, counts + RW_BIG, d_query, d_query_uc,
+                     ctx->d_blocks, nw, ctx->d_prof, ctx->d_bigpool, RW_BIG_WORDS, d_results,
+                     d_ops, d_op_offsets);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
 
 // ======================================================================
 // Host side (include/gsnapdp.h: gsnapdp_ggap_*)
@@ -733,8 +883,8 @@ extern "C" int gsnapdp_ggap_run_device(gsnapdp_ctx* ctx, const gsnapdp_ggap_wind
                      d_results, d_traces, lists, counts, cap);
   gsnapdp__mark(ctx, st, 4, 1);
   gsnapdp__mark(ctx, st, 5, 0);
-  // small windows: 4 waves x 2 windows per block, 3 blocks per CU (LDS)
-  hipLaunchKernelGGL((k_ggap<32, false>), dim3(ctx->num_cus * 3), dim3(256),
+  // small windows: 4 waves x 2 windows per block, as many blocks per CU as LDS holds
+  hipLaunchKernelGGL((k_ggap<32, false>), dim3(ctx->num_cus * GG_SMALL_BLOCKS), dim3(256),
                      (size_t)8 * GG_SMALL_WORDS * 4, st, d_windows, lists, counts + GG_SMALL,
                      d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_tables,
                      (uint32_t*)nullptr, (size_t)GG_SMALL_WORDS, d_results, d_traces, d_ops,

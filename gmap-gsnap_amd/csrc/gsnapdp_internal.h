@@ -39,10 +39,6 @@ GSNAPDP_HD_CONST inline int class_of_w(int W) {
 // k_fill bucket key = (W * (FAST_WMAX+1) + lband) * 2 + jump_late (W <= 48, lband <= 48)
 constexpr int NKEYS = (FAST_WMAX + 1) * (FAST_WMAX + 1) * 2;
 constexpr int KEYS_PER_W = (FAST_WMAX + 1) * 2;
-constexpr int BIG_LANES = 256;         // lanes of the generic (global-memory band) kernel
-constexpr int BIG_WMAX = 2048;
-constexpr int BIG_L2MAX = 2048;
-constexpr int BIG_L1MAX = 2048;
 
 // Mismatch types (dynprog.c:150)
 enum { MT_HIGHQ = 0, MT_MEDQ = 1, MT_LOWQ = 2, MT_ENDQ = 3 };

@@ -13,8 +13,8 @@
 //     counting sort (k_plan / k_scan / k_scatter), so band edges are scalar;
 //   * 4-bit direction nibbles stream to HBM scratch; each lane then walks its
 //     own traceback and emits a compact op stream (include/gsnapdp.h).
-//   Windows too wide (W > 48) or too long (L2 > 640) for registers run the same
-//   recurrences with the band in global memory (k_big).
+//   End gaps and windows too wide (W > 48) or too long (L2 > 640) for
+//   registers run on the row-lane kernel k_rows (gsnapdp_ggap.hip).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,33 +27,6 @@ using namespace gsnapdp;
 
 namespace {
 
-// Final bookkeeping shared by all paths.
-__device__ inline void write_result(gsnapdp_result* res, const gsnapdp_window& w, const Lane& L,
-                                    int score, int bestr, int bestc, const Tally& t,
-                                    const OpWriter& ow) {
-  gsnapdp_result R;
-  R.finalscore = score;
-  R.nmatches = t.nmatches;
-  R.nmismatches = t.nmismatches;
-  R.nopens = t.nopens;
-  R.nindels = t.nindels;
-  R.bestr = bestr;
-  R.bestc = bestc;
-  R.nops = ow.n < ow.cap ? ow.n : ow.cap;
-  R.status = ow.n > ow.cap ? ST_OPS_OVERFLOW : ST_OK;
-  R.length1 = L.d.L1;
-  R.length2 = L.d.L2;
-  R.reserved = step_dpi(w.dynprogindex);
-  // end gaps, QUERYEND_GAP / BEST_LOCAL: dynprog.c:5259-5262 / 5715-5718
-  if (L.d.mode == 1 && t.nmatches + 1 < t.nmismatches) {
-    R.finalscore = 0;
-    if (R.status == ST_OK) R.status = ST_ZEROED;
-  }
-  // QUERYEND_NOGAPS rescoring: dynprog.c:5243 / 5700
-  if (L.d.mode == 3) R.finalscore = t.nmatches * 3 + t.nmismatches * (-5);
-  *res = R;
-}
-
 // ------------------------------------------------------------------ k_plan
 // Early returns, QUERYEND_NOGAPS windows (no fill at all) and bucketing.
 __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* __restrict__ q,
@@ -62,12 +35,12 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
                        gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
                        const int64_t* __restrict__ op_off, int* __restrict__ keys,
                        int* __restrict__ hist, int* __restrict__ big_list,
-                       int* __restrict__ big_count) {
+                       int* __restrict__ big_count, int list_cap) {
   __shared__ int lh[NKEYS];  // block-local histogram: one global atomic per key per block
   for (int k = threadIdx.x; k < NKEYS; k += blockDim.x) lh[k] = 0;
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  int key = -1, big = -1;
+  int key = -1, big = -1;  // k_fill bucket key, or row-lane class
   if (i < n) {
     const gsnapdp_window w = W[i];
     const Lane L = make_lane(w);
@@ -100,13 +73,25 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
     } else if (L.d.mode == 0 && L.d.W <= FAST_WMAX && L.d.L2 <= FAST_L2MAX) {
       key = (L.d.W * (FAST_WMAX + 1) + L.d.lband) * 2 + L.d.jl;
     } else {
-      big = 0;
+      big = rows_class(L.d.L1, L.d.L2, L.d.W);
+      if (big < 0) {  // beyond the row-lane scratch: fail loudly
+        gsnapdp_result R = {};
+        R.finalscore = 0;
+        R.status = ST_UNSUPPORTED;
+        R.length1 = L.d.L1;
+        R.length2 = L.d.L2;
+        R.reserved = w.dynprogindex;
+        res[i] = R;
+      }
     }
     keys[i] = key;
   }
   if (key >= 0) atomicAdd(&lh[key], 1);
-  const int slot = agg_atomic_inc(big_count, big);
-  if (big == 0) big_list[slot] = i;
+#pragma unroll
+  for (int c = 0; c < RW_NCLS; c++) {  // one list append per row-lane class per wave
+    const int slot = agg_atomic_inc(big_count + c, big == c ? 0 : -1);
+    if (big == c) big_list[(size_t)c * list_cap + slot] = i;
+  }
   __syncthreads();
   for (int k = threadIdx.x; k < NKEYS; k += blockDim.x)
     if (lh[k] > 0) atomicAdd(&hist[k], lh[k]);
@@ -798,131 +783,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
   }
 }
 
-// ------------------------------------------------------------------- k_big
-// Same recurrences, band in per-lane global scratch (any width / length).
-struct BigDirs {
-  const uint32_t* D;
-  int NKd, rband;
-  __device__ inline uint32_t operator()(int r, int c) const {
-    const int d = r - c + rband;
-    return (D[(size_t)c * NKd + (d >> 3)] >> ((d & 7) * 4)) & 0xFu;
-  }
-};
-
-__global__ __launch_bounds__(64) void k_big(
-    const gsnapdp_window* __restrict__ Wn, const int* __restrict__ big_list,
-    const int* __restrict__ big_count, const char* __restrict__ q, const char* __restrict__ qu,
-    const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
-    uint32_t* __restrict__ pool, size_t lane_stride, gsnapdp_result* __restrict__ res,
-    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
-  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nl = gridDim.x * blockDim.x;
-  const int nbig = *big_count;
-  int* S = (int*)(pool + (size_t)gl * lane_stride);
-  for (int j = gl; j < nbig; j += nl) {
-    const int wi = big_list[j];
-    const gsnapdp_window w = Wn[wi];
-    const Lane L = make_lane(w);
-    const int rband = L.d.rband, Wd = L.d.W;
-    const int L1 = L.d.L1, L2 = L.d.L2;
-    const int NKd = (Wd + 7) / 8;
-    if (Wd > BIG_WMAX || L2 > BIG_L2MAX || L1 > BIG_L1MAX) {
-      gsnapdp_result R = {};
-      R.status = ST_UNSUPPORTED;
-      res[wi] = R;
-      continue;
-    }
-    int* Hs = S;
-    int* Es = Hs + BIG_WMAX;
-    int* Fs = Es + BIG_WMAX;
-    uint32_t* Pr = (uint32_t*)(Fs + BIG_WMAX);           // per row, rows 0..L1
-    uint32_t* D = Pr + (BIG_L1MAX + 1);                  // (L2+1) x NKd
-    const uint32_t* ptab = prof + L.d.mt * 128;
-    const int open = L.d.open, ext = L.d.ext, jl = L.d.jl, mode = L.d.mode, eb = L.d.eb;
-    for (int r = 1; r <= L1; r++) Pr[r] = ptab[qchar(q, L.qbase + L.qstep * (r - 1))];
-    // slot d (0..Wd-1) holds diagonal d: row r = c - rband + d
-    for (int d = 0; d < Wd; d++) {
-      const int r = d - rband;
-      Hs[d] = (r == 0) ? 0 : NEG;
-      Es[d] = NEG;
-      Fs[d] = (r >= 1) ? open + r * ext : NEG;
-    }
-    int fin = NEG, best = (mode == 1) ? 0 : NEG, bkey = 0, bestc2 = 0;
-    for (int c = 1; c <= L2; c++) {
-      const int g = gclass(blocks, nwords, L, L.g0 + L.gstep * (c - 1));
-      const int start = max(0, rband - c);
-      int hp = NEG, fp = NEG;
-      uint32_t acc = 0u;
-      for (int d = start; d < Wd; d++) {
-        const int r = c - rband + d;
-        const int Hd = Hs[d], Ed = Es[d], Fd = Fs[d];
-        const int Hr = (d + 1 < Wd) ? Hs[d + 1] : NEG;
-        const int Er = (d + 1 < Wd) ? Es[d + 1] : NEG;
-        const int a = Hr + open;
-        const bool dE = jl ? (Er >= a) : (Er > a);
-        const int e = max(a, Er) + ext;
-        const int b = hp + open;
-        const bool dF = jl ? (fp >= b) : (fp > b);
-        const int f = max(b, fp) + ext;
-        const bool h1 = jl ? (Ed >= Hd) : (Ed > Hd);
-        const int m1 = max(Hd, Ed);
-        const bool v1 = jl ? (Fd >= m1) : (Fd > m1);
-        const uint32_t pw = (r >= 1 && r <= L1) ? Pr[r] : 0u;
-        const int hn = max(m1, Fd) + __builtin_amdgcn_sbfe((int)pw, 4u * (uint32_t)g, 4);
-        const uint32_t nib = (dE ? 1u : 0u) | (dF ? 2u : 0u) | (v1 ? 8u : (h1 ? 4u : 0u));
-        acc |= nib << (4 * (d & 7));
-        if ((d & 7) == 7 || d == Wd - 1) {
-          D[(size_t)c * NKd + (d >> 3)] = acc;
-          acc = 0u;
-        }
-        Es[d] = e;
-        Fs[d] = f;
-        Hs[d] = hn;
-        hp = hn;
-        fp = f;
-        if (mode == 1 && r >= 1 && r <= L1 && r - c <= eb && c - r <= eb) {
-          const int key = (r << 12) | c;
-          if (hn > best || (hn == best && (jl ? key > bkey : key < bkey))) {
-            best = hn;
-            bkey = key;
-          }
-        }
-        if (mode == 2 && r == L1) {
-          if (hn > best || (jl && hn == best)) {
-            best = hn;
-            bestc2 = c;
-          }
-        }
-        if (mode == 0 && r == L1 && c == L2) fin = hn;
-      }
-    }
-    int r0, c0, score;
-    if (mode == 0) {
-      r0 = L1;
-      c0 = L2;
-      score = fin;
-    } else if (mode == 1) {
-      r0 = bkey >> 12;
-      c0 = bkey & 4095;
-      score = best;
-    } else {
-      r0 = L1;
-      c0 = bestc2;
-      score = best;
-    }
-    BigDirs dirs = {D, NKd, rband};
-    Tally t = {0, 0, 0, 0};
-    OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
-    auto colcls = [&](int cc) { return gclass(blocks, nwords, L, L.g0 + L.gstep * (cc - 1)); };
-    auto qrow = [&](int rr) -> uint32_t {
-      const int qi = L.qbase + L.qstep * (rr - 1);
-      return (uint32_t)(unsigned char)q[qi] | ((uint32_t)(unsigned char)qu[qi] << 8);
-    };
-    traceback(dirs, L, r0, c0, qrow, colcls, prof, t, ow);
-    write_result(&res[wi], w, L, score, r0, c0, t, ow);
-  }
-}
-
 // --------------------------------------------------------------- k_maxent
 __global__ void k_maxent(const uint8_t* __restrict__ model, const uint32_t* __restrict__ pos,
                          const uint32_t* __restrict__ chroff, double* __restrict__ out, int n,
@@ -956,8 +816,6 @@ void gsnapdp__set_err(const std::string& s) { g_err = s; }
 // 4-column groups)
 static const size_t FILL_COLS = (size_t)FAST_L2MAX + 4;
 static const size_t WAVE_STRIDE_DW = FILL_COLS * 64 + FILL_COLS * 16;
-static const size_t BIG_LANE_STRIDE_DW =
-    (size_t)3 * BIG_WMAX + (BIG_L1MAX + 1) + (size_t)(BIG_L2MAX + 1) * (BIG_WMAX / 8) + 64;
 
 extern "C" const char* gsnapdp_last_error(void) { return g_err.c_str(); }
 
@@ -1001,8 +859,6 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
   ctx->dirpool_waves = (size_t)ctx->fill_waves;
   if ((e = hipMalloc(&ctx->d_dirpool, ctx->dirpool_waves * WAVE_STRIDE_DW * 4)) != hipSuccess)
     return fail("malloc dirpool", e);
-  if ((e = hipMalloc(&ctx->d_bigpool, (size_t)BIG_LANES * BIG_LANE_STRIDE_DW * 4)) != hipSuccess)
-    return fail("malloc bigpool", e);
   return ctx;
 }
 
@@ -1039,7 +895,7 @@ extern "C" size_t gsnapdp_scratch_bytes(gsnapdp_ctx* ctx, int n, int max_length1
   (void)max_length2;
   const size_t waves = (size_t)n / 64 + NKEYS;
   return (size_t)n * 8 + waves * 64 * 4 + (ctx ? ctx->dirpool_waves : 0) * WAVE_STRIDE_DW * 4 +
-         (size_t)BIG_LANES * BIG_LANE_STRIDE_DW * 4;
+         (size_t)RW_BIG_WAVES * RW_BIG_WORDS * 4;
 }
 
 static int ensure_capacity(gsnapdp_ctx* ctx, int n) {
@@ -1049,7 +905,7 @@ static int ensure_capacity(gsnapdp_ctx* ctx, int n) {
   (void)hipFree(ctx->d_perm);
   (void)hipFree(ctx->d_big_list);
   HIPCHK(hipMalloc(&ctx->d_keys, (size_t)cap * 4));
-  HIPCHK(hipMalloc(&ctx->d_big_list, (size_t)cap * 4));
+  HIPCHK(hipMalloc(&ctx->d_big_list, (size_t)RW_NCLS * cap * 4));
   // perm: every bucket padded to a whole wave
   ctx->perm_cap = ((size_t)cap + (size_t)NKEYS * 64 + 63) & ~(size_t)63;
   HIPCHK(hipMalloc(&ctx->d_perm, ctx->perm_cap * 4));
@@ -1070,15 +926,18 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   int* hist = ctx->d_small;
   int* cursor = hist + NKEYS;
   int* class_start = cursor + NKEYS;
-  int* big_count = class_start + NCLASS + 1;
+  int* big_count = class_start + NCLASS + 1;  // RW_NCLS row-lane class counts
   HIPCHK(hipMemsetAsync(hist, 0, (size_t)NKEYS * 4, st));
-  HIPCHK(hipMemsetAsync(big_count, 0, 4, st));
+  HIPCHK(hipMemsetAsync(big_count, 0, 4 * RW_NCLS, st));
+  if (!ctx->d_bigpool)  // global scratch of the large row-lane windows, on first use
+    HIPCHK(hipMalloc(&ctx->d_bigpool, (size_t)RW_BIG_WAVES * RW_BIG_WORDS * 4));
   const int tb = 1024, nb = (n + tb - 1) / tb;
   auto mark = [&](int stage, int end) { gsnapdp__mark(ctx, st, stage, end); };
   mark(0, 0);
   hipLaunchKernelGGL(k_plan, dim3(nb), dim3(tb), 0, st, d_windows, n, d_query, d_query_uc,
                      ctx->d_blocks, (uint64_t)ctx->nwords, ctx->d_prof, d_results, d_ops,
-                     d_op_offsets, ctx->d_keys, hist, ctx->d_big_list, big_count);
+                     d_op_offsets, ctx->d_keys, hist, ctx->d_big_list, big_count,
+                     ctx->cap_n);
   mark(0, 1);
   mark(1, 0);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, hist, cursor, class_start, ctx->d_perm);
@@ -1092,9 +951,9 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
                      WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets);
   mark(2, 1);
   mark(3, 0);
-  hipLaunchKernelGGL(k_big, dim3(BIG_LANES / 64), dim3(64), 0, st, d_windows, ctx->d_big_list,
-                     big_count, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
-                     ctx->d_bigpool, BIG_LANE_STRIDE_DW, d_results, d_ops, d_op_offsets);
+  if (gsnapdp__rows_launch(ctx, st, d_windows, ctx->d_big_list, big_count, ctx->cap_n, d_query,
+                           d_query_uc, d_results, d_ops, d_op_offsets))
+    return -1;
   mark(3, 1);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1152,7 +1011,7 @@ void gsnapdp__mark(gsnapdp_ctx* ctx, hipStream_t st, int stage, int end) {
   ctx->ev_used[stage] = 1;
 }
 
-static const char* const kStageNames[] = {"k_plan", "k_scan+k_scatter", "k_fill", "k_big",
+static const char* const kStageNames[] = {"k_plan", "k_scan+k_scatter", "k_fill", "k_rows",
                                           "k_ggap_plan", "k_ggap"};
 static const int kNStages = (int)(sizeof(kStageNames) / sizeof(kStageNames[0]));
 
