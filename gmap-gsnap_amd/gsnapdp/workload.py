@@ -61,6 +61,19 @@ class Batch:
         return len(self.windows)
 
 
+def concat_batches(parts) -> "Batch":
+    """One batch from several (query positions rebased)."""
+    ws, qs, us, base = [], [], [], 0
+    for b in parts:
+        w = b.windows.copy()
+        w["qpos"] = w["qpos"] + base
+        ws.append(w)
+        qs.append(b.query)
+        us.append(b.query_uc)
+        base += b.query.size
+    return Batch(np.concatenate(ws), np.concatenate(qs), np.concatenate(us))
+
+
 def _mutate(rng, q: np.ndarray, sub_rate: float, n_rate: float) -> np.ndarray:
     q = q.copy()
     m = rng.random(q.size)

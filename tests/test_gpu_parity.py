@@ -8,7 +8,7 @@ import pytest
 import oracle as O
 from gsnapdp import Context
 from gsnapdp import workload as W
-from gsnapdp.records import PAIR
+from gsnapdp.records import END3_GAP, END5_GAP, PAIR
 
 pytestmark = pytest.mark.gpu
 
@@ -92,3 +92,32 @@ def test_gpu_maxent_matches_reference(golden_dir, name):
     ref = z["prob"]
     bad = np.nonzero(got.view(np.uint64) != ref.view(np.uint64))[0]
     assert bad.size == 0, "maxent differs at %s" % bad[:10]
+
+
+def rows_class(L1, L2, W):
+    """gsnapdp_device.h rows_class: 0 small (LDS, 32-row groups), 1 mid (LDS,
+    64-row stripes), 2 big (global scratch)."""
+    stripes = (L1 + 1 + 63) // 64
+    words = L1 * W + (L2 + 2 + 3) // 4 + (L1 + 1) // 2 + (3 * (L2 + 2) if stripes > 1 else 0)
+    if L1 + 1 <= 32 and words <= 1280:
+        return 0
+    return 1 if words <= 4096 else 2
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_gpu_end_gaps_every_row_class(seed):
+    """End gaps (all endpoint modes, both ends) short, striped-in-LDS and global."""
+    g = W.synthetic_genome(2_000_000, seed=200 + seed, n_rate=0.002)
+    blocks = W.pack_genome(g)
+    parts = [W.random_windows(g, 1500, seed=seed * 10 + k, kinds=(END5_GAP, END3_GAP), max_len1=m1,
+                              max_len2=m1 + 20, max_band=b)
+             for k, (m1, b) in enumerate(((30, 6), (250, 5), (600, 12)))]
+    batch = W.concat_batches(parts)
+    w = batch.windows
+    L1, L2 = w["length1"].astype(np.int64), w["length2"].astype(np.int64)
+    eb = w["extraband"].astype(np.int64)
+    Wd = np.abs(L2 - L1) + 2 * eb + 1
+    cls = np.array([rows_class(a, b, c) for a, b, c in zip(L1, L2, Wd)])
+    assert all(np.sum(cls == c) > 50 for c in (0, 1, 2)), np.bincount(cls)
+    res, pairs, npairs, ref, oflat, onp = run_both(blocks, batch)
+    compare(res, pairs, npairs, ref, oflat, onp, "end gaps seed %d" % seed)

@@ -1,4 +1,4 @@
-"""Throughput per window kind (diagnostics): single gaps vs end gaps (k_big)."""
+"""Throughput per window kind (diagnostics): single gaps vs end gaps (k_fill / k_rows)."""
 import json
 import os
 import sys
