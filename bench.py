@@ -41,6 +41,7 @@ READS_PER_GPU = 100_000
 GENOME_NT = 64_000_000
 DOMINANT = "k_fill"           # every C2 window is a register-band (k_fill) window
 C4_WINDOWS = 200_000          # intron windows per config-4 step
+C5_READS = 100_000            # reads per config-5 step (3 DP windows each)
 
 
 def window_bytes(w: np.ndarray, nops: np.ndarray) -> np.ndarray:
@@ -139,6 +140,59 @@ def measure_c4(genome, n, steps, warmup, dev, with_cpu):
     return out
 
 
+def measure_c5(genome, nreads, steps, warmup, dev, with_cpu):
+    """Side measurement, BASELINE config 5 reduced to its DP windows (SURVEY
+    8(d)): per 100 bp read one single gap (extraband 3) and an end5 + end3 gap
+    (length1 1-30, length2 +10, extraband_end 3); whole-batch windows/s."""
+    b = W.c5_windows(genome, nreads, seed=5)
+    n = len(b)
+    ctx = Context(W.pack_genome(genome), mode=0, device=dev.index)
+    off = op_offsets(b.windows)
+    d_w = torch.from_numpy(b.windows.view(np.uint8).copy()).to(dev)
+    d_q = torch.from_numpy(b.query.copy()).to(dev)
+    d_u = torch.from_numpy(b.query_uc.copy()).to(dev)
+    d_off = torch.from_numpy(off.copy()).to(dev)
+    d_res = torch.zeros(n * RESULT.itemsize, dtype=torch.uint8, device=dev)
+    d_ops = torch.zeros(int(off[-1]) + 1, dtype=torch.int32, device=dev)
+
+    def step():
+        ctx.run_device(d_w.data_ptr(), n, d_q.data_ptr(), d_u.data_ptr(), d_res.data_ptr(),
+                       d_ops.data_ptr(), d_off.data_ptr())
+    for _ in range(warmup):
+        step()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ctx.sync()
+    el = time.perf_counter() - t0
+    names = ctx.profile(True)
+    acc = np.zeros(len(names))
+    for _ in range(steps):
+        step()
+        ctx.profile_read(acc)
+    ctx.profile(False)
+    out = {"workload": "C5 (DP part): %d reads x (single gap 100 bp, extraband 3 + end5 + end3 gaps, "
+                       "extraband_end 3, QUERYEND_GAP) = %d windows per step" % (nreads, n),
+           "value": round(n * steps / el, 1), "unit": "windows/s", "reads_per_s": round(nreads * steps / el, 1),
+           "ms_per_step": round(1000 * el / steps, 4),
+           "kernel_ms_per_step": {nm: round(acc[i] / steps, 4) for i, nm in enumerate(names) if acc[i] > 0}}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        O.setup(W.pack_genome(genome))
+        t1 = time.perf_counter()
+        ores, _, _, _ = O.run_batch(b.windows, b.query, b.query_uc, nthreads=16)
+        cpu = n / (time.perf_counter() - t1)
+        res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=RESULT)
+        out["cpu_baseline"] = {"value": round(cpu, 1), "unit": "windows/s", "cores": 16, "kind": "port",
+                               "sample": "the whole %d-window batch once, oracle/ restatement, pthreads" % n}
+        out["parity_bit_exact"] = bool(all(np.array_equal(res[f], ores[f]) for f in
+                                           ("finalscore", "nmatches", "nmismatches", "nopens", "nindels")))
+    ctx.close()
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,6 +202,7 @@ def main() -> None:
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-c4", action="store_true", help="skip the config-4 (genome gap) side line")
     ap.add_argument("--c4-windows", type=int, default=C4_WINDOWS)
+    ap.add_argument("--no-c5", action="store_true", help="skip the config-5 (GSNAP windows) side line")
     args = ap.parse_args()
 
     ranks = shard.init_from_env("nccl")
@@ -273,6 +328,8 @@ def main() -> None:
         }
         if not args.no_c4 and world == 1:
             out["c4"] = measure_c4(genome, args.c4_windows, args.steps, args.warmup, dev, not args.no_cpu)
+        if not args.no_c5 and world == 1:
+            out["c5"] = measure_c5(genome, C5_READS, args.steps, args.warmup, dev, not args.no_cpu)
         print(json.dumps(out), flush=True)
     shard.finish(ranks)
     ctx.close()

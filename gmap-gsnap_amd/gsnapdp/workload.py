@@ -14,6 +14,10 @@
   point reads, long and odd-shaped windows and the early-return cases.
 * ``c4_windows``: the BASELINE config-4 intron batch (length1 22, length2
   30, extraband_paired 7), vectorised.
+* ``c5_windows``: the DP windows GSNAP issues for 100 bp reads (BASELINE
+  config 5 reduced to its DP part): per read one single gap over
+  the read (extraband_single 3) and two end gaps (end5 + end3, length1 1-30,
+  length2 = length1 + extramaterial_end 10, extraband_end 3, QUERYEND_GAP).
 
 Deterministic for a given seed (numpy PCG64).
 """
@@ -443,6 +447,61 @@ def c4_windows(gseq: np.ndarray, n: int, seed: int = 4, use_probabilities: bool 
     w["score_threshold"] = 0
     qf = q.reshape(-1).copy()
     return g, Batch(w, qf, qf.copy())
+
+
+def c5_windows(gseq: np.ndarray, nreads: int, seed: int = 5, read_len: int = 100,
+               extraband_single: int = 3, extraband_end: int = 3, extramaterial_end: int = 10) -> Batch:
+    singles = c2_windows(gseq, nreads, seed=seed, read_len=read_len, extraband=extraband_single)
+    rng = np.random.default_rng(seed + 1000)
+    n = 2 * nreads
+    G = gseq.size
+    margin, stride = 8, 48
+    L1 = rng.integers(1, 31, size=n)
+    L2 = L1 + extramaterial_end
+    end5 = (np.arange(n) % 2) == 0
+    watson = rng.integers(0, 2, size=n).astype(bool)
+    glen = L2 + 2 * margin
+    chrpos = rng.integers(0, G - int(glen.max()) - 1, size=n)
+    # window genome (get_genomic_nt orientation): columns margin .. margin+L2-1
+    j = np.arange(int(glen.max()))[None, :]
+    gi = np.where(watson[:, None], chrpos[:, None] + j, chrpos[:, None] + glen[:, None] - 1 - j)
+    gi = np.minimum(gi, G - 1)
+    seg = gseq[gi]
+    seg = np.where(watson[:, None], seg, _COMP[seg])
+    # the query: end3 aligns its first bases to the first columns, end5 its last
+    # bases to the last columns (read backwards from revoffset2)
+    k = np.arange(30)[None, :]
+    col = np.where(end5[:, None], margin + L2[:, None] - L1[:, None] + k, margin + k)
+    q = np.take_along_axis(seg, np.minimum(col, seg.shape[1] - 1), axis=1)
+    m = rng.random(q.shape) < 0.02
+    q[m] = ACGT[(np.searchsorted(ACGT, q[m]) + rng.integers(1, 4, size=int(m.sum()))) % 4]
+    q[k >= L1[:, None]] = ord("#")
+    qbuf = np.full((n, stride), ord("#"), dtype=np.uint8)
+    qbuf[:, :30] = q
+    w = np.zeros(n, dtype=WINDOW)
+    w["kind"] = np.where(end5, END5_GAP, END3_GAP)
+    w["length1"] = L1
+    w["length2"] = L2
+    w["offset1"] = np.where(end5, L1 - 1, read_len - L1)
+    w["offset2"] = np.where(end5, margin + L2 - 1, margin)
+    w["chroffset"] = 0
+    w["chrhigh"] = G
+    w["chrpos"] = chrpos
+    w["genomiclength"] = glen
+    w["qpos"] = np.arange(n) * stride + np.where(end5, L1 - 1, 0)  # rebased by concat_batches
+    w["cdna_direction"] = 1
+    w["extraband"] = extraband_end
+    w["dynprogindex"] = 1
+    w["maxlength1"] = MAXLENGTH1
+    w["maxlength2"] = MAXLENGTH2
+    w["defect_rate"] = 0.001
+    w["watsonp"] = watson.astype(np.uint8)
+    w["jump_late_p"] = 1 - w["watsonp"]
+    w["widebandp"] = 1
+    w["endalign"] = QUERYEND_GAP
+    ends = Batch(w, qbuf.reshape(-1), qbuf.reshape(-1).copy())
+    both = concat_batches([singles, ends])
+    return Batch(both.windows, both.query, both.query_uc)
 
 
 def pack_genome(gseq: np.ndarray) -> np.ndarray:

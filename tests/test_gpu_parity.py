@@ -121,3 +121,13 @@ def test_gpu_end_gaps_every_row_class(seed):
     assert all(np.sum(cls == c) > 50 for c in (0, 1, 2)), np.bincount(cls)
     res, pairs, npairs, ref, oflat, onp = run_both(blocks, batch)
     compare(res, pairs, npairs, ref, oflat, onp, "end gaps seed %d" % seed)
+
+
+def test_gpu_c5_gsnap_windows_parity():
+    """BASELINE config 5's DP windows: 100 bp single gaps (extraband 3) and end5 / end3 gaps."""
+    g = W.synthetic_genome(8_000_000, seed=5)
+    blocks = W.pack_genome(g)
+    batch = W.c5_windows(g, 20_000, seed=5)
+    res, pairs, npairs, ref, oflat, onp = run_both(blocks, batch)
+    compare(res, pairs, npairs, ref, oflat, onp, "C5 windows")
+    assert np.sum(onp) > 60 * 20_000
