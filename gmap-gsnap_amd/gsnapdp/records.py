@@ -51,6 +51,25 @@ GGAP_TRACE = np.dtype([
 ])
 assert GGAP_TRACE.itemsize == 32
 
+CGAP_WINDOW = np.dtype([
+    ("length1L", "<i4"), ("length1R", "<i4"), ("length2", "<i4"),
+    ("offset1L", "<i4"), ("revoffset1R", "<i4"), ("offset2", "<i4"),
+    ("chroffset", "<u4"), ("chrhigh", "<u4"), ("chrpos", "<u4"), ("genomiclength", "<u4"),
+    ("qposL", "<u4"), ("qposR", "<u4"),
+    ("cdna_direction", "<i4"), ("extraband_paired", "<i4"), ("dynprogindex", "<i4"),
+    ("maxlength1", "<i4"), ("maxlength2", "<i4"), ("defect_rate", "<f4"),
+    ("watsonp", "u1"), ("jump_late_p", "u1"), ("pad0", "u1"), ("pad1", "u1"),
+])
+assert CGAP_WINDOW.itemsize == 76
+
+CGAP_RESULT = np.dtype([
+    ("finalscore", "<i4"), ("dynprogindex", "<i4"), ("incompletep", "<i4"), ("returned_null", "<i4"),
+    ("status", "<i4"), ("npairs", "<i4"), ("finalscore_set", "<i4"), ("insert_pairs", "<i4"),
+    ("brL", "<i4"), ("bcL", "<i4"), ("brR", "<i4"), ("bcR", "<i4"),
+    ("nops_right", "<i4"), ("nops_left", "<i4"), ("reserved0", "<i4"), ("reserved1", "<i4"),
+])
+assert CGAP_RESULT.itemsize == 64
+
 MAXENT_IN = np.dtype([("model", "<u4"), ("splice_pos", "<u4"), ("chroffset", "<u4"), ("pad", "<u4")])
 
 # enums (include/gsnapdp.h)

@@ -14,6 +14,9 @@
   point reads, long and odd-shaped windows and the early-return cases.
 * ``c4_windows``: the BASELINE config-4 intron batch (length1 22, length2
   30, extraband_paired 7), vectorised.
+* ``cgap_windows``: Dynprog_cdna_gap windows shaped like traverse_cdna_gap's
+  (stage3.c:5518-5627): a query gap longer than the genome gap by a cDNA
+  insertion of 10-40 bases; length1L = length1R = genomejump + 8.
 * ``c5_windows``: the DP windows GSNAP issues for 100 bp reads (BASELINE
   config 5 reduced to its DP part): per read one single gap over
   the read (extraband_single 3) and two end gaps (end5 + end3, length1 1-30,
@@ -26,7 +29,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import genome as _genome
-from .records import (BEST_LOCAL, END3_GAP, END5_GAP, GGAP_WINDOW, MAXLENGTH1, MAXLENGTH2,
+from .records import (BEST_LOCAL, CGAP_WINDOW, END3_GAP, END5_GAP, GGAP_WINDOW, MAXLENGTH1, MAXLENGTH2,
                       QUERYEND_GAP, QUERYEND_INDELS, QUERYEND_NOGAPS, SINGLE_GAP, WINDOW)
 
 ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
@@ -447,6 +450,85 @@ def c4_windows(gseq: np.ndarray, n: int, seed: int = 4, use_probabilities: bool 
     w["score_threshold"] = 0
     qf = q.reshape(-1).copy()
     return g, Batch(w, qf, qf.copy())
+
+
+class CgapBatch(Batch):
+    """cDNA-gap windows plus each window's genomic segment (the reference's
+    sequence2 argument, read only by its INSERT_PAIRS branch)."""
+
+    def __init__(self, windows, query, query_uc, gseg, gseg_off):
+        super().__init__(windows, query, query_uc)
+        self.gseg = gseg
+        self.gseg_off = gseg_off
+
+
+def cgap_windows(gseq: np.ndarray, n: int, seed: int, mix: bool = True) -> CgapBatch:
+    rng = np.random.default_rng(seed)
+    Gn = gseq.size
+    w = np.zeros(n, dtype=CGAP_WINDOW)
+    qs, us, segs, soff = [], [], [], [0]
+    qpos = 0
+    for i in range(n):
+        G = int(rng.integers(2, 41)) if not mix or rng.random() < 0.97 else int(rng.integers(0, 2))
+        ins = int(rng.integers(10, 41))
+        glen = 200 + G
+        chrpos = int(rng.integers(0, Gn - glen - 1))
+        watson = int(rng.integers(0, 2))
+        off2 = int(rng.integers(20, 60))
+        xs = np.arange(glen)
+        view = gseq[chrpos + xs] if watson else _COMP[gseq[chrpos + glen - 1 - xs]]
+        a = int(rng.integers(0, G + 1))
+        pad5, pad3 = int(rng.integers(0, 20)), int(rng.integers(0, 20))
+        if mix and G >= 12 and rng.random() < 0.3:
+            # a 9-base genome block replaced by 9 + extra random query bases: the
+            # bridge may leave exactly 9 x 9 unaligned (INSERT_PAIRS, dynprog.c:4730)
+            # (queryjump = genomejump here: outside traverse_cdna_gap's shapes,
+            # inside Dynprog_cdna_gap's domain)
+            a = int(rng.integers(2, G - 9))
+            core = np.concatenate([view[off2:off2 + a], ACGT[rng.integers(0, 4, size=9)],
+                                   view[off2 + a + 9:off2 + G]])
+        else:
+            core = np.concatenate([view[off2:off2 + a], ACGT[rng.integers(0, 4, size=ins)], view[off2 + a:off2 + G]])
+        q = np.concatenate([ACGT[rng.integers(0, 4, size=pad5)], core, ACGT[rng.integers(0, 4, size=pad3)]])
+        q = _mutate(rng, q, 0.02, 0.005)
+        quc = q.copy()
+        if mix and rng.random() < 0.1:
+            m = rng.random(q.size) < 0.3
+            q[m] = np.where(rng.random(int(m.sum())) < 0.7, q[m] + 32,
+                            _AMBIG[rng.integers(0, _AMBIG.size, int(m.sum()))])
+            quc = np.where((q >= 97) & (q <= 122), q - 32, q).astype(np.uint8)
+        Q = core.size
+        qd5 = 100 + pad5          # query coordinate of querydp5
+        rec = w[i]
+        rec["length2"] = G
+        rec["length1L"] = rec["length1R"] = G + 8  # queryjump = genomejump + extramaterial_paired
+        rec["offset1L"] = qd5
+        rec["revoffset1R"] = qd5 + Q - 1
+        rec["offset2"] = off2
+        rec["chroffset"] = 0
+        rec["chrhigh"] = Gn
+        rec["chrpos"] = chrpos
+        rec["genomiclength"] = glen
+        rec["qposL"] = qpos + pad5
+        rec["qposR"] = qpos + pad5 + Q - 1
+        rec["cdna_direction"] = int(rng.choice([1, -1, 0]))
+        rec["extraband_paired"] = int(rng.choice([7, 3, 10])) if mix else 7
+        rec["dynprogindex"] = int(rng.choice([-1, 2]))
+        small = mix and rng.random() < 0.01
+        rec["maxlength1"] = 20 if small else MAXLENGTH1
+        rec["maxlength2"] = 30 if small else MAXLENGTH2
+        rec["defect_rate"] = float(rng.choice([0.001, 0.005, 0.02]))
+        rec["watsonp"] = watson
+        rec["jump_late_p"] = int(rng.integers(0, 2))
+        qs += [q, np.full(4, ord("#"), np.uint8)]
+        us += [quc, np.full(4, ord("#"), np.uint8)]
+        qpos += q.size + 4
+        seg = view[off2:off2 + max(G, 0)] if G > 0 else view[:0]
+        segs.append(np.concatenate([seg, np.zeros(4, np.uint8)]))
+        soff.append(soff[-1] + segs[-1].size)
+    gs = np.concatenate(segs)
+    # sequence2[k] is addressed relative to offset2
+    return CgapBatch(w, np.concatenate(qs), np.concatenate(us), gs, np.array(soff[:-1], dtype=np.int64))
 
 
 def c5_windows(gseq: np.ndarray, nreads: int, seed: int = 5, read_len: int = 100,

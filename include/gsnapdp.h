@@ -175,6 +175,33 @@ typedef struct gsnapdp_ggap_trace {
   int32_t npairs;
 } gsnapdp_ggap_trace;
 
+/* One cDNA-insertion window (Dynprog_cdna_gap, dynprog.c:4578-4793).  The
+ * genome part (length2, from offset2) forms the rows of both fills, the query
+ * the columns: the left fill reads sequence1L = query[qposL ...] forwards, the
+ * right fill reads revsequence1R backwards from query[qposR]. */
+typedef struct gsnapdp_cgap_window {
+  int32_t length1L, length1R, length2;
+  int32_t offset1L, revoffset1R, offset2;
+  uint32_t chroffset, chrhigh, chrpos, genomiclength;
+  uint32_t qposL, qposR;
+  int32_t cdna_direction, extraband_paired, dynprogindex, maxlength1, maxlength2;
+  float defect_rate;
+  uint8_t watsonp, jump_late_p, pad0, pad1;
+} gsnapdp_cgap_window;
+
+/* Out-parameters of Dynprog_cdna_gap and where its tracebacks start.
+ * status: 0 ok, 1 early return (NULL), 2 op overflow, 4 unsupported, 5 the
+ * bridge found no candidate (the reference then traces back from
+ * uninitialised indices; excluded).  finalscore_set: 0 on the early returns,
+ * which leave *finalscore untouched.  incompletep: 1 if the gapholder was
+ * pushed (the only case in which the reference writes *incompletep). */
+typedef struct gsnapdp_cgap_result {
+  int32_t finalscore, dynprogindex, incompletep, returned_null;
+  int32_t status, npairs, finalscore_set, insert_pairs;
+  int32_t brL, bcL, brR, bcR;
+  int32_t nops_right, nops_left, reserved0, reserved1;
+} gsnapdp_cgap_result;
+
 /* ---------------------------------------------------------------- context */
 
 typedef struct gsnapdp_ctx gsnapdp_ctx;

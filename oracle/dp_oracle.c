@@ -1058,6 +1058,338 @@ void orc_genome_gap(orc_list *out, orc_genome_gap_out *o, int dpi, orc_dp *dpL, 
   list_reverse(out);
 }
 
+
+/* ------------------------------------------------------------- cDNA gap */
+
+#define CDNA_OPEN (-10)   /* dynprog.c:230-232, every quality bin */
+#define CDNA_EXTEND (-7)
+#define INSERT_PAIRS 9    /* :140 */
+#define SHORTGAP_COMP '~' /* comp.h:11 */
+
+/* compute_scores_lookup_fwd_12 / _rev_12 (dynprog.c:1742-2044): the genome in
+ * the rows (get_genomic_nt at offset1 +/- (r-1)), the query in the columns,
+ * pairdistance[query][genome] ("Note swap"), row-major with the row-wise
+ * band-edge sentinels. */
+static void fill12(mview *m, orc_dp *dp, int rev, int goff, int Lg, int Lq, const char *qseq,
+                   const gpar *g, int mt, int open, int extend, int extraband, int jump_late_p) {
+  int lband, rband, r, c, clo, chigh, penalty;
+  size_t cells = (size_t)(Lg + 1) * (size_t)(Lq + 1);
+  int32_t *H = dp->nogap, *E = dp->gap1, *F = dp->gap2;
+  uint8_t *dH = dp->dnogap, *dE = dp->dgap1, *dF = dp->dgap2;
+  int stride = Lq + 1;
+  int(*tab)[128] = pd[mt];
+  if (Lg <= 0 || Lq <= 0) {
+    fprintf(stderr, "dynprog: lengths are negative: %d %d\n", Lg, Lq);
+    abort();
+  }
+  m->L1 = Lg;
+  m->L2 = Lq;
+  m->stride = stride;
+  m->H = H;
+  m->E = E;
+  m->F = F;
+  m->dH = dH;
+  m->dE = dE;
+  m->dF = dF;
+  band_widths(Lg, Lq, extraband, 1, &lband, &rband);
+  memset(H, 0, cells * 4);
+  memset(E, 0, cells * 4);
+  memset(F, 0, cells * 4);
+  memset(dH, 0, cells);
+  memset(dE, 0, cells);
+  memset(dF, 0, cells);
+  H[0] = 0;
+  dH[0] = D_STOP;
+  E[0] = F[0] = NEG_INF;
+  penalty = open;
+  for (c = 1; c <= rband && c <= Lq; c++) { /* row 0 */
+    penalty += extend;
+    H[c] = NEG_INF;
+    E[c] = penalty;
+    dE[c] = D_HORIZ;
+    F[c] = NEG_INF;
+  }
+  dE[1] = D_STOP;
+  penalty = open;
+  for (r = 1; r <= lband && r <= Lg; r++) { /* column 0 */
+    size_t i = (size_t)r * stride;
+    penalty += extend;
+    H[i] = NEG_INF;
+    E[i] = NEG_INF;
+    F[i] = penalty;
+    dF[i] = D_VERT;
+  }
+  dF[(size_t)stride] = D_STOP;
+  for (r = 1; r <= Lg; r++) {
+    int na1 = (unsigned char)gnt(g, rev ? goff + 1 - r : goff + r - 1) & 127;
+    if ((clo = r - lband) < 1) {
+      clo = 1;
+    } else {
+      size_t i = (size_t)r * stride + (clo - 1);
+      E[i] = NEG_INF;
+      H[i] = NEG_INF;
+    }
+    if ((chigh = r + rband) > Lq) {
+      chigh = Lq;
+    } else {
+      size_t i = (size_t)(r - 1) * stride + chigh;
+      F[i] = NEG_INF;
+      H[i] = NEG_INF;
+    }
+    for (c = clo; c <= chigh; c++) {
+      size_t i = (size_t)r * stride + c;
+      size_t il = i - 1, iu = i - stride, id = i - stride - 1;
+      int na2 = (unsigned char)(rev ? qseq[1 - c] : qseq[c - 1]) & 127;
+      int best, s;
+      uint8_t dir;
+      best = H[il] + open;
+      dir = D_DIAG;
+      s = E[il];
+      if (s > best || (s == best && jump_late_p)) {
+        best = s;
+        dir = D_HORIZ;
+      }
+      E[i] = best + extend;
+      dE[i] = dir;
+      best = H[iu] + open;
+      dir = D_DIAG;
+      s = F[iu];
+      if (s > best || (s == best && jump_late_p)) {
+        best = s;
+        dir = D_VERT;
+      }
+      F[i] = best + extend;
+      dF[i] = dir;
+      best = H[id];
+      dir = D_DIAG;
+      s = E[id];
+      if (s > best || (s == best && jump_late_p)) {
+        best = s;
+        dir = D_HORIZ;
+      }
+      s = F[id];
+      if (s > best || (s == best && jump_late_p)) {
+        best = s;
+        dir = D_VERT;
+      }
+      H[i] = best + tab[na2][na1];
+      dH[i] = dir;
+    }
+  }
+}
+
+/* bridge_cdna_gap (dynprog.c:3068-3146).  `pen` is 0 for the first right row
+ * and `open` for every later one (the loop resets it to open - extend before
+ * its own += extend).  Returns 0 if no candidate beat -100000 (the reference
+ * then traces back from uninitialised indices). */
+static int bridge_cdna(int *finalscore, int *brL, int *brR, int *bcL, int *bcR, const mview *mL,
+                       const mview *mR, int L2, int L1L, int L1R, int eb, int open, int extend,
+                       int leftoffset, int rightoffset) {
+  int bestscore = -100000, found = 0, rL, rR, cL, cR, pen;
+  int lbandL = eb, rbandL = L1L - L2 + eb, lbandR = eb, rbandR = L1R - L2 + eb;
+  for (rL = 1; rL < L2; rL++) {
+    for (rR = L2 - rL, pen = 0; rR >= 0; rR--, pen += extend) {
+      int cloL = rL - lbandL < 1 ? 1 : rL - lbandL;
+      int chighL = rL + rbandL > L1L - 1 ? L1L - 1 : rL + rbandL;
+      int cloR = rR - lbandR < 1 ? 1 : rR - lbandR;
+      int chighR = rR + rbandR > L1R - 1 ? L1R - 1 : rR + rbandR;
+      for (cL = cloL; cL <= chighL; cL++) {
+        int scoreL = mL->H[IX(mL, rL, cL)];
+        for (cR = cloR; cR <= chighR && cR < rightoffset - leftoffset - cL; cR++) {
+          int scoreR = mR->H[IX(mR, rR, cR)];
+          if (scoreL + scoreR + pen > bestscore) {
+            bestscore = scoreL + scoreR + pen;
+            *brL = rL;
+            *brR = rR;
+            *bcL = cL;
+            *bcR = cR;
+            found = 1;
+          }
+        }
+      }
+      pen = open - extend;
+    }
+  }
+  *finalscore = bestscore;
+  return found;
+}
+
+/* add_queryskip with cdna_gap_p (dynprog.c:2372-2413): query in the columns */
+static void add_queryskip_cdna(orc_list *l, int r, int c, int dist, const char *qseq, int qoff,
+                               int goff, int rev, int dpi) {
+  int j, qc = c - 1, gc = r - 1, step;
+  if (rev) {
+    qc = -qc;
+    gc = -gc;
+    step = +1;
+  } else {
+    gc++;
+    step = -1;
+  }
+  for (j = 0; j < dist; j++) {
+    push_pair(l, qoff + qc, goff + gc, qseq[qc], '-', ' ', dpi);
+    qc += step;
+  }
+}
+
+/* add_genomeskip_cdna (dynprog.c:2516-2608) */
+static int add_genomeskip_cdna(orc_list *l, int r, int c, int dist, int qoff, int goff, int rev,
+                               const gpar *g, int cdna_direction, int dpi) {
+  int j, qc = c - 1, left = r - dist, right = r - 1, gc, step, dashes;
+  if (rev) {
+    int t = left;
+    qc = -qc;
+    left = -right;
+    right = -t;
+    step = +1;
+  } else {
+    qc++;
+    step = -1;
+  }
+  if (dist < MICROINTRON_LENGTH) {
+    dashes = 1;
+  } else {
+    char l1 = gnt(g, goff + left), l2 = gnt(g, goff + left + 1);
+    char r2 = gnt(g, goff + right - 1), r1 = gnt(g, goff + right);
+    dashes = intron_type(l1, l2, r2, r1, cdna_direction) == NONINTRON;
+  }
+  if (dashes) {
+    gc = rev ? left : right;
+    for (j = 0; j < dist; j++) {
+      push_pair(l, qoff + qc, goff + gc, ' ', '-', gnt(g, goff + gc), dpi);
+      gc += step;
+    }
+  } else {
+    push_gapholder(l, GSNAPDP_UNKNOWNJUMP, GSNAPDP_UNKNOWNJUMP);
+  }
+  return dashes;
+}
+
+/* traceback_cdna (dynprog.c:2716-2812): rows are genome, columns query; no
+ * '*' test; consistent_array[genome][query] ("Note swap") */
+static void traceback_cdna(orc_list *l, counts *k, const mview *m, int r, int c, const char *qseq,
+                           const char *qseq_uc, int qoff, int goff, int rev, const gpar *g,
+                           int cdna_direction, int dpi) {
+  while (m->dH[IX(m, r, c)] != D_STOP) {
+    int qc = c - 1, gc = r - 1, dist;
+    char c1, c2;
+    uint8_t d;
+    if (rev) {
+      qc = -qc;
+      gc = -gc;
+    }
+    c1 = qseq[qc];
+    c2 = gnt(g, goff + gc);
+    if (qseq_uc[qc] == c2) {
+      k->nmatches++;
+      push_pair(l, qoff + qc, goff + gc, c1, '*', c2, dpi);
+    } else if (cons[c2 & 127][c1 & 127]) {
+      k->nmatches++;
+      push_pair(l, qoff + qc, goff + gc, c1, ':', c2, dpi);
+    } else {
+      k->nmismatches++;
+      push_pair(l, qoff + qc, goff + gc, c1, ' ', c2, dpi);
+    }
+    d = m->dH[IX(m, r, c)];
+    if (d == D_DIAG) {
+      r--;
+      c--;
+    } else if (d == D_HORIZ) {
+      dist = 1;
+      r--;
+      c--;
+      while (m->dE[IX(m, r, c)] == D_HORIZ) {
+        dist++;
+        c--;
+      }
+      c--;
+      add_queryskip_cdna(l, r, c + dist, dist, qseq, qoff, goff, rev, dpi);
+      k->nopens++;
+      k->nindels += dist;
+    } else {
+      dist = 1;
+      r--;
+      c--;
+      while (m->dF[IX(m, r, c)] == D_VERT) {
+        dist++;
+        r--;
+      }
+      r--;
+      if (add_genomeskip_cdna(l, r + dist, c, dist, qoff, goff, rev, g, cdna_direction, dpi)) {
+        k->nopens++;
+        k->nindels += dist;
+      }
+    }
+  }
+}
+
+/* Dynprog_cdna_gap (dynprog.c:4578-4793) */
+void orc_cdna_gap(orc_list *out, orc_cdna_gap_out *o, int dpi, orc_dp *dpL, orc_dp *dpR,
+                  const char *sequence1L, const char *sequenceuc1L, const char *revsequence1R,
+                  const char *revsequenceuc1R, const char *sequence2, int length1L, int length1R,
+                  int length2, int offset1L, int revoffset1R, int offset2, uint32_t chroffset,
+                  uint32_t chrhigh, uint32_t chrpos, uint32_t genomiclength, int cdna_direction,
+                  int watsonp, int jump_late_p, int extraband_paired, double defect_rate) {
+  int mt, brL = 0, brR = 0, bcL = 0, bcR = 0, revoffset2, queryjump, genomejump, kk;
+  mview mL, mR;
+  counts k = {0, 0, 0, 0};
+  gpar g = {chroffset, chrhigh, chrpos, (int)genomiclength, watsonp};
+  orc_list_clear(out);
+  memset(o, 0, sizeof(*o));
+  o->dynprogindex = dpi;
+  o->bridge_ok = 1;
+  if (length2 <= 1) { /* :4605 */
+    o->returned_null = 1;
+    return;
+  }
+  quality(defect_rate, &mt);
+  if (length2 > dpR->maxlength1 || length1R > dpR->maxlength2 || length2 > dpL->maxlength1 ||
+      length1L > dpL->maxlength2) { /* :4651-4675 */
+    o->dynprogindex = step_index(dpi);
+    o->returned_null = 1;
+    return;
+  }
+  revoffset2 = offset2 + length2 - 1;
+  fill12(&mR, dpR, 1, revoffset2, length2, length1R, revsequence1R, &g, mt, CDNA_OPEN, CDNA_EXTEND,
+         extraband_paired, !jump_late_p);
+  fill12(&mL, dpL, 0, offset2, length2, length1L, sequence1L, &g, mt, CDNA_OPEN, CDNA_EXTEND,
+         extraband_paired, jump_late_p);
+  o->finalscore_set = 1;
+  if (!bridge_cdna(&o->finalscore, &brL, &brR, &bcL, &bcR, &mL, &mR, length2, length1L, length1R,
+                   extraband_paired, CDNA_OPEN, CDNA_EXTEND, offset1L, revoffset1R)) {
+    o->bridge_ok = 0;
+    o->returned_null = 1;
+    return;
+  }
+  o->brL = brL;
+  o->bcL = bcL;
+  o->brR = brR;
+  o->bcR = bcR;
+  traceback_cdna(out, &k, &mR, brR, bcR, revsequence1R, revsequenceuc1R, revoffset1R, revoffset2, 1,
+                 &g, cdna_direction, dpi);
+  list_reverse(out);
+  queryjump = (revoffset1R - bcR) - (offset1L + bcL) + 1;
+  genomejump = (revoffset2 - brR) - (offset2 + brL) + 1;
+  if (queryjump == INSERT_PAIRS && genomejump == INSERT_PAIRS) { /* :4730-4752 */
+    o->insert_pairs = 1;
+    for (kk = revoffset1R - bcR; kk >= offset1L + bcL; kk--)
+      push_pair(out, kk, revoffset2 - brR + 1, sequence1L[kk - offset1L], SHORTGAP_COMP, ' ', dpi);
+    for (kk = revoffset2 - brR; kk >= offset2 + brL; kk--)
+      push_pair(out, offset1L + bcL, kk, ' ', SHORTGAP_COMP, sequence2[kk - offset2], dpi);
+  } else {
+    push_gapholder(out, GSNAPDP_UNKNOWNJUMP, GSNAPDP_UNKNOWNJUMP);
+    o->incompletep = 1;
+  }
+  traceback_cdna(out, &k, &mL, brL, bcL, sequence1L, sequenceuc1L, offset1L, offset2, 0, &g,
+                 cdna_direction, dpi);
+  if (out->n == 1) {
+    orc_list_clear(out);
+    o->returned_null = 1;
+  }
+  o->dynprogindex = step_index(dpi);
+  list_reverse(out);
+}
+
 /* ------------------------------------------------------------------ batch */
 
 typedef struct batch_job {
@@ -1202,6 +1534,51 @@ int orc_run_ggap_batch(const gsnapdp_ggap_window *w, int n, const char *query, c
     r->bridge_ok = o.bridge_ok;
     r->left_prob = o.left_prob;
     r->right_prob = o.right_prob;
+    if (npairs) npairs[i] = l.n;
+    for (t = 0; t < l.n && t < cap; t++) pairs[off + t] = l.buf[l.head + t];
+  }
+  orc_list_free(&l);
+  orc_dp_free(dpL);
+  orc_dp_free(dpR);
+  return 0;
+}
+
+/* Batch driver over gsnapdp_cgap_window records (single thread).  gseg holds
+ * each window's genomic segment (the reference's sequence2, read only by the
+ * INSERT_PAIRS branch) at gseg_off[i]. */
+int orc_run_cgap_batch(const gsnapdp_cgap_window *w, int n, const char *query, const char *query_uc,
+                       const char *gseg, const int64_t *gseg_off, gsnapdp_cgap_result *results,
+                       gsnapdp_pair *pairs, const int64_t *pair_offsets, int32_t *npairs) {
+  orc_dp *dpL = orc_dp_new(600, 10, 11, 10, 8), *dpR = orc_dp_new(600, 10, 11, 10, 8);
+  orc_list l;
+  int i, t;
+  orc_list_init(&l, 1024);
+  for (i = 0; i < n; i++) {
+    const gsnapdp_cgap_window *x = &w[i];
+    orc_cdna_gap_out o;
+    gsnapdp_cgap_result *r = &results[i];
+    int64_t off = pair_offsets ? pair_offsets[i] : 0;
+    int64_t cap = pair_offsets ? pair_offsets[i + 1] - off : 0;
+    dpL->maxlength1 = dpR->maxlength1 = x->maxlength1;
+    dpL->maxlength2 = dpR->maxlength2 = x->maxlength2;
+    orc_cdna_gap(&l, &o, x->dynprogindex, dpL, dpR, query + x->qposL, query_uc + x->qposL,
+                 query + x->qposR, query_uc + x->qposR, gseg + gseg_off[i], x->length1L,
+                 x->length1R, x->length2, x->offset1L, x->revoffset1R, x->offset2, x->chroffset,
+                 x->chrhigh, x->chrpos, x->genomiclength, x->cdna_direction, x->watsonp,
+                 x->jump_late_p, x->extraband_paired, (double)x->defect_rate);
+    memset(r, 0, sizeof(*r));
+    r->finalscore = o.finalscore;
+    r->dynprogindex = o.dynprogindex;
+    r->incompletep = o.incompletep;
+    r->returned_null = o.returned_null;
+    r->status = o.bridge_ok ? 0 : 5;
+    r->finalscore_set = o.finalscore_set;
+    r->insert_pairs = o.insert_pairs;
+    r->brL = o.brL;
+    r->bcL = o.bcL;
+    r->brR = o.brR;
+    r->bcR = o.bcR;
+    r->npairs = l.n;
     if (npairs) npairs[i] = l.n;
     for (t = 0; t < l.n && t < cap; t++) pairs[off + t] = l.buf[l.head + t];
   }

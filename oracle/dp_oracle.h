@@ -101,6 +101,26 @@ void orc_genome_gap(orc_list *out, orc_genome_gap_out *o, int dynprogindex_in,
                     int extraband_paired, double defect_rate, int maxpeelback, int halfp,
                     int finalp, int use_probabilities_p, int score_threshold, int splicingp);
 
+/* Dynprog_cdna_gap (dynprog.c:4578-4793). */
+typedef struct orc_cdna_gap_out {
+  int finalscore, dynprogindex, incompletep, returned_null;
+  int finalscore_set;  /* 0 on the early returns (*finalscore untouched) */
+  int insert_pairs;    /* the INSERT_PAIRS branch (:4730) was taken */
+  int bridge_ok;       /* 0: no bridge candidate (reference UB) */
+  int brL, bcL, brR, bcR;
+} orc_cdna_gap_out;
+
+void orc_cdna_gap(orc_list *out, orc_cdna_gap_out *o, int dpi, orc_dp *dpL, orc_dp *dpR,
+                  const char *sequence1L, const char *sequenceuc1L, const char *revsequence1R,
+                  const char *revsequenceuc1R, const char *sequence2, int length1L, int length1R,
+                  int length2, int offset1L, int revoffset1R, int offset2, uint32_t chroffset,
+                  uint32_t chrhigh, uint32_t chrpos, uint32_t genomiclength, int cdna_direction,
+                  int watsonp, int jump_late_p, int extraband_paired, double defect_rate);
+
+int orc_run_cgap_batch(const gsnapdp_cgap_window *w, int n, const char *query, const char *query_uc,
+                       const char *gseg, const int64_t *gseg_off, gsnapdp_cgap_result *results,
+                       gsnapdp_pair *pairs, const int64_t *pair_offsets, int32_t *npairs);
+
 /* Dynprog_score (dynprog.c:380). */
 int orc_score(int matches, int mismatches, int qopens, int qindels, int topens, int tindels,
               double defect_rate);

@@ -29,8 +29,8 @@ ROOT = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
 from gsnapdp import genome as G  # noqa: E402
 from gsnapdp import workload as W  # noqa: E402
-from gsnapdp.records import (GGAP_RESULT, GGAP_WINDOW, MAXLENGTH1, MAXLENGTH2, PAIR,  # noqa: E402
-                             RESULT)
+from gsnapdp.records import (CGAP_RESULT, GGAP_RESULT, GGAP_WINDOW, MAXLENGTH1, MAXLENGTH2,  # noqa: E402
+                             PAIR, RESULT)
 
 REF_TESTS = "/root/reference/tests"
 DRIVER = os.path.join(HERE, "_ref", "ref_driver")
@@ -176,6 +176,35 @@ def ggap_case(name: str, gseq: np.ndarray, n: int, seed: int) -> None:
           (name, len(w), int((~keep).sum()), pairs.size))
 
 
+def cgap_case(name: str, gseq: np.ndarray, n: int, seed: int) -> None:
+    """Dynprog_cdna_gap windows (W.cgap_windows); windows whose bridge finds no
+    candidate (the reference then reads uninitialised indices) are dropped."""
+    sys.path.insert(0, HERE)
+    import oracle as O  # checker, used only to drop windows the reference cannot run (UB)
+    b = W.cgap_windows(gseq, n, seed)
+    blocks = G.pack(gseq)
+    O.setup(blocks)
+    ores, _, _, _ = O.run_cgap_batch(b.windows, b.query, b.query_uc, b.gseg, b.gseg_off)
+    keep = ores["status"] != 5
+    w, goff = b.windows[keep], b.gseg_off[keep]
+    with tempfile.TemporaryDirectory() as d:
+        w.tofile(os.path.join(d, "cgap_windows.bin"))
+        b.query.tofile(os.path.join(d, "query.bin"))
+        b.query_uc.tofile(os.path.join(d, "query_uc.bin"))
+        b.gseg.tofile(os.path.join(d, "gseg.bin"))
+        goff.astype("<i8").tofile(os.path.join(d, "gseg_off.i64"))
+        blocks.astype("<u4").tofile(os.path.join(d, "genome.u32"))
+        run_driver("cgap", d)
+        res = np.fromfile(os.path.join(d, "cgap_results.bin"), dtype=CGAP_RESULT)
+        npairs = np.fromfile(os.path.join(d, "npairs.i32"), dtype=np.int32)
+        pairs = np.fromfile(os.path.join(d, "pairs.bin"), dtype=PAIR)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), blocks=blocks, windows=w, query=b.query,
+                        query_uc=b.query_uc, gseg=b.gseg, gseg_off=goff, results=res, npairs=npairs,
+                        pairs=pairs, dropped_ub=np.int32((~keep).sum()))
+    print("%s: %d windows (%d dropped: no bridge candidate), %d pairs" %
+          (name, len(w), int((~keep).sum()), pairs.size))
+
+
 def maxent_case(name: str, blocks: np.ndarray, glen: int, n: int, seed: int) -> None:
     rng = np.random.default_rng(seed)
     model = rng.integers(0, 4, size=n).astype(np.uint32)
@@ -232,6 +261,7 @@ def main() -> None:
     dp_case("dp_synth_long", bsyn, W.random_windows(synth, 150, seed=105, max_len1=640,
                                                     max_len2=700, max_band=40))
     ggap_case("ggap_chr17", chr17, 1500, seed=201)
+    cgap_case("cgap_chr17", chr17, 1500, seed=401)
     maxent_case("maxent_chr17", b17, chr17.size, 20000, seed=301)
     maxent_case("maxent_synth", bsyn, synth.size, 6000, seed=302)
 

@@ -16,7 +16,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
-from gsnapdp.records import GGAP_RESULT, GGAP_WINDOW, PAIR, RESULT, WINDOW  # noqa: E402
+from gsnapdp.records import CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_WINDOW, PAIR, RESULT, WINDOW  # noqa: E402
 
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 TABLES_PATH = os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin")
@@ -44,6 +44,7 @@ def lib():
         L.orc_maxent_load.restype = i32
         L.orc_run_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i32]
         L.orc_run_ggap_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
+        L.orc_run_cgap_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp]
         L.orc_maxent_batch.argtypes = [vp, vp, vp, vp, i32]
         L.orc_pairdistance.argtypes = [i32, i32, i32]
         L.orc_pairdistance.restype = i32
@@ -76,6 +77,12 @@ def setup(blocks: np.ndarray, mode: int = 0, tables: np.ndarray | None = None) -
 def pair_offsets_for(windows: np.ndarray, slack: int = 8) -> np.ndarray:
     """Worst-case list length per window: every pair of the window rectangle
     (a diagonal pair per row + a dash per column) + 2 gapholders."""
+    if "length1L" in windows.dtype.names:  # cDNA gaps: both tracebacks + insertion pairs
+        cap = (windows["length1L"].astype(np.int64) + windows["length1R"] + 2 * windows["length2"].astype(np.int64)
+               + 18 + slack)
+        off = np.zeros(len(windows) + 1, dtype=np.int64)
+        np.cumsum(cap.clip(slack), out=off[1:])
+        return off
     l1 = windows["length1"].astype(np.int64) if "length1" in windows.dtype.names else None
     if "length2L" in windows.dtype.names:
         cap = 2 * l1 + windows["length2L"] + windows["length2R"] + slack
@@ -110,6 +117,22 @@ def run_ggap_batch(windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray)
     pairs = np.zeros(int(off[-1]), dtype=PAIR)
     npairs = np.zeros(len(w), dtype=np.int32)
     L.orc_run_ggap_batch(_p(w), len(w), _p(q), _p(u), _p(res), _p(pairs), _p(off), _p(npairs))
+    return res, pairs, off, npairs
+
+
+def run_cgap_batch(windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray, gseg: np.ndarray,
+                   gseg_off: np.ndarray):
+    L = lib()
+    w = np.ascontiguousarray(windows, dtype=CGAP_WINDOW)
+    q = np.ascontiguousarray(query, dtype=np.uint8)
+    u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+    gs = np.ascontiguousarray(gseg, dtype=np.uint8)
+    go = np.ascontiguousarray(gseg_off, dtype=np.int64)
+    res = np.zeros(len(w), dtype=CGAP_RESULT)
+    off = pair_offsets_for(w)
+    pairs = np.zeros(int(off[-1]), dtype=PAIR)
+    npairs = np.zeros(len(w), dtype=np.int32)
+    L.orc_run_cgap_batch(_p(w), len(w), _p(q), _p(u), _p(gs), _p(go), _p(res), _p(pairs), _p(off), _p(npairs))
     return res, pairs, off, npairs
 
 

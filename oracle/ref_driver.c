@@ -8,6 +8,8 @@
  * Usage:
  *   ref_driver dp     <dir>   windows.bin query.bin query_uc.bin genome.u32 -> results.bin pairs.bin npairs.i32
  *   ref_driver ggap   <dir>   ggap_windows.bin query.bin query_uc.bin genome.u32 -> ggap_results.bin pairs.bin npairs.i32
+ *   ref_driver cgap   <dir>   cgap_windows.bin query.bin query_uc.bin gseg.bin gseg_off.i64 genome.u32
+ *                             -> cgap_results.bin pairs.bin npairs.i32
  *   ref_driver maxent <dir>   maxent_in.bin genome.u32 -> maxent_out.f64
  *   ref_driver pdist  <dir>   -> pdist.i32 (4 x 128 x 128 via Dynprog_pairdistance for HIGHQ only) + consistent probe
  * All inputs use the record layouts of include/gsnapdp.h.
@@ -218,6 +220,63 @@ static int run_ggap(const char *dir) {
   return 0;
 }
 
+static int run_cgap(const char *dir) {
+  size_t nw, nq, nu, ng, ns, no;
+  gsnapdp_cgap_window *w = (gsnapdp_cgap_window *)slurp(dir, "cgap_windows.bin", &nw);
+  char *q = (char *)slurp(dir, "query.bin", &nq);
+  char *qu = (char *)slurp(dir, "query_uc.bin", &nu);
+  char *gs = (char *)slurp(dir, "gseg.bin", &ns);
+  int64_t *goff = (int64_t *)slurp(dir, "gseg_off.i64", &no);
+  UINT4 *g = (UINT4 *)slurp(dir, "genome.u32", &ng);
+  int n = (int)(nw / sizeof(gsnapdp_cgap_window)), i;
+  gsnapdp_cgap_result *res = (gsnapdp_cgap_result *)calloc((size_t)n + 1, sizeof(*res));
+  int32_t *npairs = (int32_t *)calloc((size_t)n + 1, sizeof(int32_t));
+  gsnapdp_pair *tmp = (gsnapdp_pair *)malloc(sizeof(gsnapdp_pair) * PAIRCAP);
+  FILE *fp;
+  char path[4096];
+  Dynprog_T dpL = Dynprog_new(600, 10, 11, 10, 8), dpR = Dynprog_new(600, 10, 11, 10, 8);
+  Pairpool_T pool = Pairpool_new();
+
+  Genome_user_setup(g);
+  Maxent_hr_setup(g);
+  snprintf(path, sizeof(path), "%s/pairs.bin", dir);
+  fp = fopen(path, "wb");
+  for (i = 0; i < n; i++) {
+    gsnapdp_cgap_window *x = &w[i];
+    gsnapdp_cgap_result *o = &res[i];
+    int dpi = x->dynprogindex, fs = -777777, k;
+    bool incomplete = false;
+    List_T pairs;
+    char *seg = gs + goff[i];
+    if (x->maxlength1 != 611 || x->maxlength2 != 2000) {
+      /* the too-long returns: shrink the workspaces' limits like Dynprog_new would */
+      ((int *)dpL)[0] = ((int *)dpR)[0] = x->maxlength1;
+      ((int *)dpL)[1] = ((int *)dpR)[1] = x->maxlength2;
+    }
+    Pairpool_reset(pool);
+    pairs = Dynprog_cdna_gap(&dpi, &fs, &incomplete, dpL, dpR, q + x->qposL, qu + x->qposL,
+                             q + x->qposR, qu + x->qposR, seg, seg, x->length1L, x->length1R,
+                             x->length2, x->offset1L, x->revoffset1R, x->offset2, x->chroffset,
+                             x->chrhigh, x->chrpos, x->genomiclength, x->cdna_direction, x->watsonp,
+                             x->jump_late_p, pool, x->extraband_paired, (double)x->defect_rate);
+    ((int *)dpL)[0] = ((int *)dpR)[0] = 611;
+    ((int *)dpL)[1] = ((int *)dpR)[1] = 2000;
+    o->finalscore = fs == -777777 ? 0 : fs;
+    o->finalscore_set = fs != -777777;
+    o->dynprogindex = dpi;
+    o->incompletep = incomplete ? 1 : 0;
+    o->returned_null = pairs == NULL;
+    k = flatten(pairs, tmp, PAIRCAP);
+    npairs[i] = k;
+    o->npairs = k;
+    fwrite(tmp, sizeof(gsnapdp_pair), (size_t)(k < PAIRCAP ? k : PAIRCAP), fp);
+  }
+  fclose(fp);
+  spit(dir, "cgap_results.bin", res, sizeof(*res) * (size_t)n);
+  spit(dir, "npairs.i32", npairs, sizeof(int32_t) * (size_t)n);
+  return 0;
+}
+
 typedef struct maxent_in {
   uint32_t model, splice_pos, chroffset, pad;
 } maxent_in;
@@ -264,6 +323,7 @@ int main(int argc, char **argv) {
                 NULL, NULL, /*genome*/ NULL);
   if (!strcmp(argv[1], "dp")) return run_dp(argv[2]);
   if (!strcmp(argv[1], "ggap")) return run_ggap(argv[2]);
+  if (!strcmp(argv[1], "cgap")) return run_cgap(argv[2]);
   if (!strcmp(argv[1], "maxent")) return run_maxent(argv[2]);
   if (!strcmp(argv[1], "pdist")) return run_pdist(argv[2]);
   return 1;

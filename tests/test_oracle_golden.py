@@ -86,3 +86,22 @@ def test_pairdistance_matches_reference(golden_dir):
     L = O.lib()
     got = np.array([[L.orc_pairdistance(0, a, b) for b in range(128)] for a in range(128)])
     assert np.array_equal(got, z["table"])
+
+
+def test_cgap_oracle_matches_reference(golden_dir):
+    """Dynprog_cdna_gap: out-parameters and the full list, including the
+    INSERT_PAIRS branch (dynprog.c:4730-4752)."""
+    z = load(golden_dir, "cgap_chr17")
+    O.setup(z["blocks"])
+    res, pairs, off, npairs = O.run_cgap_batch(z["windows"], z["query"], z["query_uc"], z["gseg"],
+                                               z["gseg_off"])
+    ref = z["results"]
+    assert np.all(res["status"] != 5)
+    for f in ("finalscore", "finalscore_set", "dynprogindex", "incompletep", "returned_null"):
+        bad = np.nonzero(res[f] != ref[f])[0]
+        assert bad.size == 0, "%s differs at %s (oracle %s ref %s)" % (f, bad[:10], res[f][bad[:10]], ref[f][bad[:10]])
+    assert np.array_equal(npairs, z["npairs"])
+    got = np.concatenate([pairs[off[i]:off[i] + npairs[i]] for i in range(len(npairs))])
+    for f in PAIR.names:
+        assert np.array_equal(got[f], z["pairs"][f]), f
+    assert res["insert_pairs"].sum() > 20 and (res["returned_null"] == 0).sum() > 1000
