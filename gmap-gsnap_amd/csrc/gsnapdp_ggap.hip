@@ -251,17 +251,21 @@ struct Side {
 // One flank fill (compute_scores_lookup_fwd / _rev, dynprog.c:1424-1736) over
 // the rows of the lane group, in stripes of RL rows.  Every lane of the wave
 // calls it (the DPP shift spans the wave); `T` and `NS` are wave-uniform.
-template <int RL, bool GMEM, class P, class PB>
-__device__ void gg_fill(const Side<P>& sd, PB cls, P bnd, int L1, int rho, int open, int ext,
-                        int jl, const char* __restrict__ q, int qrow0, int qstep,
-                        const uint32_t* __restrict__ ptab, int T, int NS) {
+// One flank fill (compute_scores_lookup_fwd / _rev, dynprog.c:1424-1736, or
+// with CD the genome-row _12 fills of Dynprog_cdna_gap, :1742-2044) over the
+// rows of the lane group, in stripes of RL rows.  `rowkey(r)` is the row's
+// profile word (query rows: pairdistance of the query char against genome
+// classes A C G T N * as signed nibbles), or with CD 4 x the genome row's
+// class; `colv[c]` is column c's genome class, or with CD the profile word of
+// its query char.  Every lane of the wave calls it (the DPP shift spans the
+// wave); `T` and `NS` are wave-uniform.
+template <int RL, bool GMEM, bool CD, class P, class PC, class RK>
+__device__ void gg_fill(const Side<P>& sd, PC colv, P bnd, int L1, int rho, int open, int ext,
+                        int jl, const RK& rowkey, int T, int NS) {
   const int lband = sd.lband, rband = sd.rband, L2 = sd.L2, W = sd.W;
   for (int s = 0; s < NS; s++) {
     const int r = s * RL + rho;
-    // profile word of this lane's row: pairdistance of its query char against
-    // genome classes A C G T N * as signed nibbles (build_profile_table)
-    const int rq = (r >= 1 && r <= L1) ? r : 1;
-    const uint32_t pw = ptab[(unsigned char)q[qrow0 + qstep * (rq - 1)] & 127u];
+    const uint32_t rk = rowkey((r >= 1 && r <= L1) ? r : 1);
     // this row's band columns [cmin, cmax] (empty for row 0 and rows past L1)
     const int cmin0 = max(1, r - lband), cmax = min(L2, r + rband);
     const bool rowok = r >= 1 && r <= L1 && cmax >= cmin0;
@@ -277,10 +281,10 @@ __device__ void gg_fill(const Side<P>& sd, PB cls, P bnd, int L1, int rho, int o
     int Hc = NEG, Ec = NEG, Fc = NEG;      // (r, c-1)
     int Hup = NEG, Eup = NEG, Fup = NEG;   // (r-1, c-1)
     int erun = open - rho * ext;           // open + c * extend, c = t - rho
-    int g = (int)cls[max(0, min(L2 + 1, -rho))];
+    uint32_t g = (uint32_t)colv[max(0, min(L2 + 1, -rho))];
     for (int t = 0; t < T; t++) {
       const int c = t - rho;
-      const int gn = (int)cls[max(0, min(L2 + 1, c + 1))];  // next column's class
+      const uint32_t gn = (uint32_t)colv[max(0, min(L2 + 1, c + 1))];  // next column's value
       int Hn = from_above(Hc), En = from_above(Ec), Fn = from_above(Fc);  // (r-1, c)
       if (rho == 0 && s > 0) {  // row above the stripe: the boundary row
         const bool ok = c >= 0 && c <= L2;
@@ -299,7 +303,8 @@ __device__ void gg_fill(const Side<P>& sd, PB cls, P bnd, int L1, int rho, int o
       const bool hE = Eup > Hup - jl;
       const int m1 = hE ? Eup : Hup;
       const bool hF = Fup > m1 - jl;
-      const int Hr = (hF ? Fup : m1) + __builtin_amdgcn_sbfe((int)pw, 4 * g, 4);
+      const int sc = CD ? __builtin_amdgcn_sbfe((int)g, (int)rk, 4) : __builtin_amdgcn_sbfe((int)rk, 4 * (int)g, 4);
+      const int Hr = (hF ? Fup : m1) + sc;
       const bool inb = (uint32_t)(c - cmin) <= cspan;
       const int H = inb ? Hr : (c == hz ? 0 : NEG);
       const int E = inb ? Er : ((uint32_t)(c - 1) < e0span ? erun : NEG);
@@ -447,11 +452,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
     // left flank forward with jump_late_p, right flank reversed with !jump_late_p (:4955-4990)
     const int jl = w.jump_late_p ? 1 : 0;
 #ifndef GG_EXP_NOFILL
-    gg_fill<RL, GMEM>(SL, clsL, bnd, G.L1, rho, G.open, G.ext, jl, q, (int)w.qpos, 1, ptab, T, NS);
+    gg_fill<RL, GMEM, false>(SL, clsL, bnd, G.L1, rho, G.open, G.ext, jl,
+                             [&](int r) { return ptab[(unsigned char)q[w.qpos + r - 1] & 127u]; }, T, NS);
 #endif
 #ifndef GG_EXP_NOFILL
-    gg_fill<RL, GMEM>(SR, clsR, bnd, G.L1, rho, G.open, G.ext, 1 - jl, q, (int)w.qpos + G.L1 - 1,
-                      -1, ptab, T, NS);
+    gg_fill<RL, GMEM, false>(SR, clsR, bnd, G.L1, rho, G.open, G.ext, 1 - jl,
+                             [&](int r) { return ptab[(unsigned char)q[w.qpos + G.L1 - r] & 127u]; }, T, NS);
 #endif
     if constexpr (GMEM) __threadfence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -698,8 +704,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
     const int T = __builtin_amdgcn_readfirstlane(wave_max(act ? L2 + (L1 + 1 > RL ? RL : L1 + 1) : 0));
     const int NS = __builtin_amdgcn_readfirstlane(wave_max(act ? L1 + 1 : 1) + RL - 1) / RL;
     const Side<P> sd = {H, L2, d.lband, d.rband, W};
-    gg_fill<RL, GMEM>(sd, cls, bnd, L1, rho, d.open, d.ext, d.jl, q, L.qbase, L.qstep,
-                      prof + d.mt * 128, T, NS);
+    const uint32_t* ptab = prof + d.mt * 128;
+    gg_fill<RL, GMEM, false>(sd, cls, bnd, L1, rho, d.open, d.ext, d.jl,
+                             [&](int r) { return ptab[(unsigned char)q[L.qbase + L.qstep * (r - 1)] & 127u]; },
+                             T, NS);
     if constexpr (GMEM) __threadfence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);
     // ---- endpoint: a row-parallel scan, then the first (or, with jump_late,
@@ -812,6 +820,335 @@ __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
     }
   }
   // one list append per class per wave
+#pragma unroll
+  for (int c = 0; c < GG_NCLS; c++) {
+    const int pos = agg_atomic_inc(counts + c, cls == c ? 0 : -1);
+    if (cls == c) lists[(size_t)c * cap + pos] = i;
+  }
+}
+
+
+// ------------------------------------------------------------------ cDNA gaps
+constexpr int CDNA_OPEN = -10, CDNA_EXTEND = -7;  // dynprog.c:229-235 (every bin)
+constexpr int INSERT_PAIRS = 9;                   // :140
+
+// traceback_cdna (dynprog.c:2716-2812): genome rows, query columns.  Every
+// nogap cell pushes a pair (no '*' test); the consistency test is swapped
+// (consistent_array[genome][query]); HORIZ runs skip query (add_queryskip with
+// cdna_gap_p, :2372) and VERT runs skip genome (add_genomeskip_cdna, :2516,
+// with the intron test).  Ops: DIAG runs, VSKIP = query skip, HDASH / HGAP =
+// genome skip.  `grow(r)` is genome row r's class, `qcol(c)` column c's
+// query byte | uppercase byte << 8.
+template <class Dirs, class GRow, class QCol>
+__device__ inline void traceback_cdna(const Dirs& dirs, int lband, int rband, int Lr, int Lc,
+                                      int rev, int cdna_direction, int r, int c, const GRow& grow,
+                                      const QCol& qcol, const uint32_t* __restrict__ cons_sw,
+                                      Tally& t, OpWriter& ow) {
+  auto inband = [&](int rr, int cc) {
+    const int d = rr - cc + rband;
+    return rr >= 1 && cc >= 1 && d >= 0 && d <= lband + rband;
+  };
+  auto gap1_horiz = [&](int rr, int cc) -> bool {
+    if (rr == 0) return cc >= 2 && cc <= rband && cc <= Lc;
+    if (!inband(rr, cc)) return false;
+    return dirs(rr, cc) & 1u;
+  };
+  auto gap2_vert = [&](int rr, int cc) -> bool {
+    if (cc == 0) return rr >= 2 && rr <= lband && rr <= Lr;
+    if (!inband(rr, cc)) return false;
+    return (dirs(rr, cc) >> 1) & 1u;
+  };
+  while (inband(r, c)) {
+    const uint32_t nib = dirs(r, c);
+    const int g = grow(r);
+    const uint32_t qq = qcol(c);
+    const unsigned char c1 = (unsigned char)(qq & 127u), u1 = (unsigned char)(qq >> 8);
+    if (u1 == (unsigned char)("ACGTN*"[g]) || (g < 5 && ((cons_sw[c1] >> (24 + g)) & 1u)))
+      t.nmatches++;
+    else
+      t.nmismatches++;
+    t.npush++;
+    ow.run++;
+    if (nib & 8u) {  // VERT: genome skip
+      int dist = 1;
+      r--;
+      c--;
+      while (gap2_vert(r, c)) {
+        dist++;
+        r--;
+      }
+      r--;
+      bool dashes = true;
+      if (dist >= MICROINTRON_LENGTH) {  // rows r+1 .. r+dist are skipped
+        const int rl = r + 1, rh = r + dist;
+        const int l1 = grow(rev ? rh : rl), l2 = grow(rev ? rh - 1 : rl + 1);
+        const int r2 = grow(rev ? rl + 1 : rh - 1), r1 = grow(rev ? rl : rh);
+        dashes = intron_type_codes(l1, l2, r2, r1, cdna_direction) == 0;
+      }
+      ow.flush();
+      ow.put(GSNAPDP_OP(dashes ? GSNAPDP_OP_HDASH : GSNAPDP_OP_HGAP, dist));
+      t.npush += dashes ? dist : 1;
+      if (dashes) {
+        t.nopens++;
+        t.nindels += dist;
+      }
+    } else if (nib & 4u) {  // HORIZ: query skip
+      int dist = 1;
+      r--;
+      c--;
+      while (gap1_horiz(r, c)) {
+        dist++;
+        c--;
+      }
+      c--;
+      ow.flush();
+      ow.put(GSNAPDP_OP(GSNAPDP_OP_VSKIP, dist));
+      t.npush += dist;
+      t.nopens++;
+      t.nindels += dist;
+    } else {
+      r--;
+      c--;
+    }
+  }
+  ow.flush();
+}
+
+struct CGeo {
+  int G, L1L, L1R, eb, mt;
+  int lbL, rbL, WL, lbR, rbR, WR;
+  int oHR, oCwL, oCwR, oQL, oQR, oGL, oGR, oBnd, words, bndw;
+};
+
+__device__ inline CGeo cg_geo(const gsnapdp_cgap_window& w) {
+  CGeo C;
+  C.G = w.length2;
+  C.L1L = w.length1L;
+  C.L1R = w.length1R;
+  C.eb = w.extraband_paired;
+  const double dr = (double)w.defect_rate;  // :4622-4641
+  C.mt = dr < 0.003 ? MT_HIGHQ : (dr < 0.014 ? MT_MEDQ : MT_LOWQ);
+  fill_bands(C.G, C.L1L, C.eb, C.lbL, C.rbL);  // rows = genome, columns = query
+  fill_bands(C.G, C.L1R, C.eb, C.lbR, C.rbR);
+  C.WL = C.lbL + C.rbL + 1;
+  C.WR = C.lbR + C.rbR + 1;
+  const int g = C.G > 0 ? C.G : 0, l1 = C.L1L > 0 ? C.L1L : 0, l2 = C.L1R > 0 ? C.L1R : 0;
+  C.oHR = g * C.WL;
+  C.oCwL = C.oHR + g * C.WR;     // column profile words, 0 .. L1+1
+  C.oCwR = C.oCwL + l1 + 2;
+  C.oQL = C.oCwR + l2 + 2;       // column query | uc << 8 (u16), 0 .. L1+1
+  C.oQR = C.oQL + (l1 + 3) / 2;
+  C.oGL = C.oQR + (l2 + 3) / 2;  // genome row classes (bytes), 0 .. G+1
+  C.oGR = C.oGL + (g + 2 + 3) / 4;
+  C.oBnd = C.oGR + (g + 2 + 3) / 4;
+  C.words = C.oBnd;
+  C.bndw = C.G + 1 > 64 ? 3 * (max(l1, l2) + 2) : 0;
+  return C;
+}
+
+template <int RL, bool GMEM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8))) void k_cgap(
+    const gsnapdp_cgap_window* __restrict__ Wn, const int* __restrict__ list,
+    const int* __restrict__ count, const char* __restrict__ q, const char* __restrict__ qu,
+    const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
+    uint32_t* __restrict__ pool, size_t stride, gsnapdp_cgap_result* __restrict__ res,
+    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
+  extern __shared__ uint32_t smem[];
+  using P = typename std::conditional<GMEM, AS_GLOBAL uint32_t*, AS_LDS uint32_t*>::type;
+  using PB = typename std::conditional<GMEM, AS_GLOBAL uint8_t*, AS_LDS uint8_t*>::type;
+  using PH = typename std::conditional<GMEM, AS_GLOBAL uint16_t*, AS_LDS uint16_t*>::type;
+  constexpr int NGW = 64 / RL;
+  const int lane = threadIdx.x & 63, grp = lane / RL, rho = lane % RL;
+  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+  P region;
+  if constexpr (GMEM) {
+    region = (P)(pool + (size_t)gw * stride);
+  } else {
+    region = (P)(smem + ((threadIdx.x >> 6) * NGW + grp) * stride);
+  }
+  const int n = *count;
+  for (int base = gw * NGW; base < n; base += nw * NGW) {
+    const int k = base + grp;
+    const bool act = k < n;
+    const int wi = list[act ? k : base];
+    const gsnapdp_cgap_window w = Wn[wi];
+    CGeo C = cg_geo(w);
+    if (!act) C.G = 0;
+    const P HL = region, HR = region + C.oHR;
+    const P cwL = region + C.oCwL, cwR = region + C.oCwR;
+    const PH qL = (PH)(region + C.oQL), qR = (PH)(region + C.oQR);
+    const PB gL = (PB)(region + C.oGL), gR = (PB)(region + C.oGR);
+    const P bnd = region + C.oBnd;
+    const int revoffset2 = w.offset2 + w.length2 - 1;
+    // the genome rows of both fills (get_genomic_nt), the query columns
+    Lane LG;  // genome view for gclass
+    LG.base = w.chroffset + w.chrpos;
+    LG.glen = (int)w.genomiclength;
+    LG.watson = w.watsonp ? 1 : 0;
+    LG.allstar = (LG.base < w.chroffset) || (LG.base >= w.chrhigh);
+    const uint32_t* ptab = prof + C.mt * 128;
+    if (act) {
+      for (int r = rho; r <= C.G + 1; r += RL) {
+        const bool in = r >= 1 && r <= C.G;
+        gL[r] = (uint8_t)(in ? gclass(blocks, nwords, LG, w.offset2 + r - 1) : 5);
+        gR[r] = (uint8_t)(in ? gclass(blocks, nwords, LG, revoffset2 + 1 - r) : 5);
+      }
+      for (int c = rho; c <= C.L1L + 1; c += RL) {
+        const bool in = c >= 1 && c <= C.L1L;
+        const int qi = (int)w.qposL + c - 1;
+        const unsigned a = in ? (unsigned char)q[qi] : 0u, u = in ? (unsigned char)qu[qi] : 0u;
+        cwL[c] = ptab[a & 127u];
+        qL[c] = (uint16_t)(a | (u << 8));
+      }
+      for (int c = rho; c <= C.L1R + 1; c += RL) {
+        const bool in = c >= 1 && c <= C.L1R;
+        const int qi = (int)w.qposR + 1 - c;  // revsequence1R[1 - c]
+        const unsigned a = in ? (unsigned char)q[qi] : 0u, u = in ? (unsigned char)qu[qi] : 0u;
+        cwR[c] = ptab[a & 127u];
+        qR[c] = (uint16_t)(a | (u << 8));
+      }
+    }
+    if constexpr (GMEM) __threadfence();
+    else __builtin_amdgcn_s_waitcnt(0xc07f);
+    const int L1max = max(C.L1L, C.L1R);
+    const int T = __builtin_amdgcn_readfirstlane(wave_max(act ? L1max + (C.G + 1 > RL ? RL : C.G + 1) : 0));
+    const int NS = __builtin_amdgcn_readfirstlane(wave_max(act ? C.G + 1 : 1) + RL - 1) / RL;
+    const int jl = w.jump_late_p ? 1 : 0;
+    const Side<P> SR = {HR, C.L1R, C.lbR, C.rbR, C.WR};
+    const Side<P> SL = {HL, C.L1L, C.lbL, C.rbL, C.WL};
+    // right side reversed with !jump_late_p, left side forward (:4680-4710)
+    gg_fill<RL, GMEM, true>(SR, cwR, bnd, C.G, rho, CDNA_OPEN, CDNA_EXTEND, 1 - jl,
+                            [&](int r) { return 4u * (uint32_t)gR[r]; }, T, NS);
+    gg_fill<RL, GMEM, true>(SL, cwL, bnd, C.G, rho, CDNA_OPEN, CDNA_EXTEND, jl,
+                            [&](int r) { return 4u * (uint32_t)gL[r]; }, T, NS);
+    if constexpr (GMEM) __threadfence();
+    else __builtin_amdgcn_s_waitcnt(0xc07f);
+
+    // ---- bridge_cdna_gap (dynprog.c:3068-3146), lane = rL; scan order rL,
+    // rR descending, cL, cR, strict >.  rR = 0 never wins: row 0's nogap is
+    // NEG_INFINITY over the whole range the bridge reads.
+    const int span = w.revoffset1R - w.offset1L;  // cR < span - cL
+    const int rbandBL = C.L1L - C.G + C.eb, rbandBR = C.L1R - C.G + C.eb;
+    int best = BRIDGE_INIT, bkey = 0x7fffffff, bcL = 0, bcR = 0, brR = 0;
+    const int rows = __builtin_amdgcn_readfirstlane(wave_max(act ? C.G : 0));
+    for (int r0 = 0; r0 < rows; r0 += RL) {
+      const int rL = r0 + rho;
+      if (rL < 1 || rL >= C.G) continue;
+      const int cloL = max(1, rL - C.eb), chighL = min(C.L1L - 1, rL + rbandBL);
+      const int baseL = (rL - 1) * C.WL - rL + C.lbL;
+      for (int rR = C.G - rL; rR >= 1; rR--) {
+        const int pen = rR == C.G - rL ? 0 : CDNA_OPEN;
+        const int cloR = max(1, rR - C.eb), chighR = min(C.L1R - 1, rR + rbandBR);
+        const int baseR = (rR - 1) * C.WR - rR + C.lbR;
+        for (int cL = cloL; cL <= chighL; cL++) {
+          const int sL = (int)HL[baseL + cL] >> 4;
+          const int hi = min(chighR, span - cL - 1);
+          for (int cR = cloR; cR <= hi; cR++) {
+            const int tot = sL + ((int)HR[baseR + cR] >> 4) + pen;
+            if (tot > best) {
+              best = tot;
+              bkey = rL;
+              bcL = cL;
+              bcR = cR;
+              brR = rR;
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = RL / 2; o > 0; o >>= 1) {
+      const int ob = __shfl_xor(best, o), ok = __shfl_xor(bkey, o);
+      const int ocL = __shfl_xor(bcL, o), ocR = __shfl_xor(bcR, o), orR = __shfl_xor(brR, o);
+      if (ob > best || (ob == best && ok < bkey)) {
+        best = ob;
+        bkey = ok;
+        bcL = ocL;
+        bcR = ocR;
+        brR = orR;
+      }
+    }
+    if (act && rho == 0) {
+      gsnapdp_cgap_result R;
+      memset(&R, 0, sizeof(R));
+      R.dynprogindex = w.dynprogindex;
+      R.finalscore = best;
+      R.finalscore_set = 1;
+      if (bkey == 0x7fffffff) {
+        R.status = 5;  // no candidate: the reference traces back from uninitialised indices
+        R.returned_null = 1;
+      } else {
+        const int brL = bkey;
+        R.brL = brL;
+        R.bcL = bcL;
+        R.brR = brR;
+        R.bcR = bcR;
+        const int64_t o0 = op_off[wi];
+        const int cap = (int)(op_off[wi + 1] - o0);
+        Tally t = {0, 0, 0, 0, 0};
+        OpWriter owR = {ops + o0, cap, 0, 0};
+        const uint32_t* cons_sw = prof + PROF_CONS_SWAPPED;
+        traceback_cdna(CellDirs<P>{HR, C.WR, C.lbR}, C.lbR, C.rbR, C.G, C.L1R, 1, w.cdna_direction,
+                       brR, bcR, [&](int r) -> int { return gR[r]; },
+                       [&](int c) -> uint32_t { return qR[c]; }, cons_sw, t, owR);
+        const int nR = owR.n < cap ? owR.n : cap;
+        OpWriter owL = {ops + o0 + nR, cap - nR, 0, 0};
+        traceback_cdna(CellDirs<P>{HL, C.WL, C.lbL}, C.lbL, C.rbL, C.G, C.L1L, 0, w.cdna_direction,
+                       brL, bcL, [&](int r) -> int { return gL[r]; },
+                       [&](int c) -> uint32_t { return qL[c]; }, cons_sw, t, owL);
+        R.nops_right = nR;
+        R.nops_left = owL.n < owL.cap ? owL.n : owL.cap;
+        if (owR.n > cap || owL.n > owL.cap) R.status = ST_OPS_OVERFLOW;
+        const int qj = (w.revoffset1R - bcR) - (w.offset1L + bcL) + 1;
+        const int gj = (revoffset2 - brR) - (w.offset2 + brL) + 1;
+        R.insert_pairs = qj == INSERT_PAIRS && gj == INSERT_PAIRS;  // :4730
+        R.incompletep = !R.insert_pairs;
+        R.npairs = t.npush + (R.insert_pairs ? qj + gj : 1);
+        if (R.npairs == 1) {  // only the gapholder (:4779)
+          R.npairs = 0;
+          R.returned_null = 1;
+        }
+        R.dynprogindex = step_dpi(w.dynprogindex);
+      }
+      res[wi] = R;
+    }
+  }
+}
+
+// Early returns (dynprog.c:4605, 4651-4675) and the class of every cDNA-gap window
+__global__ void k_cgap_plan(const gsnapdp_cgap_window* __restrict__ Wn, int n,
+                            gsnapdp_cgap_result* __restrict__ res, int* __restrict__ lists,
+                            int* __restrict__ counts, int cap) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int cls = -1;
+  if (i < n) {
+    const gsnapdp_cgap_window w = Wn[i];
+    const CGeo C = cg_geo(w);
+    gsnapdp_cgap_result R;
+    memset(&R, 0, sizeof(R));
+    R.dynprogindex = w.dynprogindex;
+    R.status = ST_EARLY;
+    R.returned_null = 1;
+    bool done = true;
+    if (C.G <= 1) {
+      // NULL, nothing written
+    } else if (C.G > w.maxlength1 || C.L1R > w.maxlength2 || C.L1L > w.maxlength2) {
+      R.dynprogindex = step_dpi(w.dynprogindex);
+    } else if (C.L1L <= 0 || C.L1R <= 0 || C.eb < 0) {
+      R.status = ST_UNSUPPORTED;  // the reference aborts (Matrix3_alloc :495)
+    } else {
+      done = false;
+      if (C.G + 1 <= 32 && C.words <= GG_SMALL_WORDS) cls = GG_SMALL;
+      else if (C.words + C.bndw <= GG_MID_WORDS) cls = GG_MID;
+      else if ((size_t)C.words + C.bndw <= GG_BIG_WORDS) cls = GG_BIG;
+      else {
+        done = true;
+        R.status = ST_UNSUPPORTED;
+      }
+    }
+    if (done) res[i] = R;
+  }
 #pragma unroll
   for (int c = 0; c < GG_NCLS; c++) {
     const int pos = agg_atomic_inc(counts + c, cls == c ? 0 : -1);
@@ -946,6 +1283,84 @@ extern "C" int gsnapdp_ggap_run_host(gsnapdp_ctx* ctx, const gsnapdp_ggap_window
   if (gsnapdp_ggap_run_device(ctx, dw, n, dq, du, dr, dt, dops, doff, st)) return -1;
   HIPCHK(hipMemcpyAsync(results, dr, (size_t)n * sizeof(gsnapdp_ggap_result), hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(traces, dt, (size_t)n * sizeof(gsnapdp_ggap_trace), hipMemcpyDeviceToHost, st));
+  if (nops) HIPCHK(hipMemcpyAsync(ops, dops, nops * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
+extern "C" int gsnapdp_cgap_run_device(gsnapdp_ctx* ctx, const gsnapdp_cgap_window* d_windows,
+                                       int n, const char* d_query, const char* d_query_uc,
+                                       gsnapdp_cgap_result* d_results, uint32_t* d_ops,
+                                       const int64_t* d_op_offsets, void* stream_v) {
+  if (!ctx) return -1;
+  if (n <= 0) return 0;
+  hipStream_t st = stream_v ? (hipStream_t)stream_v : ctx->stream;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  if (ggap_capacity(ctx, n)) return -1;
+  if (!ctx->d_ggap_pool)
+    HIPCHK(hipMalloc(&ctx->d_ggap_pool, (size_t)GG_BIG_WAVES * GG_BIG_WORDS * 4));
+  const uint64_t nw = (uint64_t)ctx->nwords;
+  int* counts = ctx->d_ggap_counts;
+  int* lists = ctx->d_ggap_lists;
+  const int cap = ctx->ggap_cap;
+  HIPCHK(hipMemsetAsync(counts, 0, 4 * GG_NCLS, st));
+  hipLaunchKernelGGL(k_cgap_plan, dim3((n + 255) / 256), dim3(256), 0, st, d_windows, n, d_results,
+                     lists, counts, cap);
+  hipLaunchKernelGGL((k_cgap<32, false>), dim3(ctx->num_cus * GG_SMALL_BLOCKS), dim3(256),
+                     (size_t)8 * GG_SMALL_WORDS * 4, st, d_windows, lists, counts + GG_SMALL,
+                     d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, (uint32_t*)nullptr,
+                     (size_t)GG_SMALL_WORDS, d_results, d_ops, d_op_offsets);
+  hipLaunchKernelGGL((k_cgap<64, false>), dim3(ctx->num_cus * 2), dim3(256),
+                     (size_t)4 * GG_MID_WORDS * 4, st, d_windows, lists + (size_t)GG_MID * cap,
+                     counts + GG_MID, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
+                     (uint32_t*)nullptr, (size_t)GG_MID_WORDS, d_results, d_ops, d_op_offsets);
+  hipLaunchKernelGGL((k_cgap<64, true>), dim3(GG_BIG_WAVES), dim3(64), 0, st, d_windows,
+                     lists + (size_t)GG_BIG * cap, counts + GG_BIG, d_query, d_query_uc,
+                     ctx->d_blocks, nw, ctx->d_prof, ctx->d_ggap_pool, GG_BIG_WORDS, d_results,
+                     d_ops, d_op_offsets);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int gsnapdp_cgap_run_host(gsnapdp_ctx* ctx, const gsnapdp_cgap_window* windows, int n,
+                                     const char* query, const char* query_uc, size_t query_bytes,
+                                     gsnapdp_cgap_result* results, uint32_t* ops,
+                                     const int64_t* op_offsets) {
+  if (!ctx) return -1;
+  if (n <= 0) return 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t nops = (size_t)op_offsets[n];
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t szw = al((size_t)n * sizeof(gsnapdp_cgap_window));
+  const size_t szq = al(query_bytes + 4);
+  const size_t szr = al((size_t)n * sizeof(gsnapdp_cgap_result));
+  const size_t szo = al((nops + 1) * 4);
+  const size_t szoff = al((size_t)(n + 1) * 8);
+  const size_t total = szw + 2 * szq + szr + szo + szoff;
+  {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (total > ctx->ggap_stage_cap) {
+      (void)hipFree(ctx->d_ggap_stage);
+      ctx->d_ggap_stage = nullptr;
+      HIPCHK(hipMalloc(&ctx->d_ggap_stage, total));
+      ctx->ggap_stage_cap = total;
+    }
+  }
+  char* b = (char*)ctx->d_ggap_stage;
+  gsnapdp_cgap_window* dw = (gsnapdp_cgap_window*)b;
+  char* dq = b + szw;
+  char* du = dq + szq;
+  gsnapdp_cgap_result* dr = (gsnapdp_cgap_result*)(du + szq);
+  uint32_t* dops = (uint32_t*)((char*)dr + szr);
+  int64_t* doff = (int64_t*)((char*)dops + szo);
+  hipStream_t st = ctx->stream;
+  HIPCHK(hipMemcpyAsync(dw, windows, (size_t)n * sizeof(gsnapdp_cgap_window), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(dq, query, query_bytes, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(doff, op_offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, st));
+  if (gsnapdp_cgap_run_device(ctx, dw, n, dq, du, dr, dops, doff, st)) return -1;
+  HIPCHK(hipMemcpyAsync(results, dr, (size_t)n * sizeof(gsnapdp_cgap_result), hipMemcpyDeviceToHost, st));
   if (nops) HIPCHK(hipMemcpyAsync(ops, dops, nops * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   return 0;

@@ -74,6 +74,11 @@ void build_profile_table(int mode, uint32_t prof[PROF_WORDS]) {
       if (u == cls[g]) w |= 1u << (24 + g);
     prof[4 * 128 + u] = w;
   }
+  for (int c = 0; c < 128; c++) {
+    uint32_t w = 0;
+    for (int g = 0; g < 5; g++) w |= (uint32_t)cons_tab[(int)cls[g]][c] << (24 + g);
+    prof[PROF_CONS_SWAPPED + c] = w;
+  }
 }
 
 int host_pairdistance(int mt, int c1, int c2) { return pd_tab[mt][c1 & 127][c2 & 127]; }
@@ -285,6 +290,158 @@ extern "C" int gsnapdp_ggap_expand(gsnapdp_ctx* ctx, const gsnapdp_ggap_window* 
     pairs[n] = x;
   }
   n++;
+  for (size_t i = 0; i < pl.size(); i++, n++)
+    if (n < cap) pairs[n] = pl[i];
+  return n;
+}
+
+// traceback_cdna's pushes (dynprog.c:2716-2812) from an op stream: genome
+// rows r, query columns c; add_queryskip with cdna_gap_p (:2372) for VSKIP,
+// add_genomeskip_cdna (:2516) for HDASH / HGAP.
+static void replay_cdna(const uint32_t* ops, int nops, int r, int c, const char* q, const char* qu,
+                        int qoff, int goff, bool rev, const HostGenome& G, int dpi,
+                        std::vector<gsnapdp_pair>& p) {
+  auto push = [&](int qpos, int gpos, char cdna, char comp, char g) {
+    gsnapdp_pair x;
+    memset(&x, 0, sizeof(x));
+    x.querypos = qpos;
+    x.genomepos = gpos;
+    x.dynprogindex = dpi;
+    x.cdna = cdna;
+    x.comp = comp;
+    x.genome = g;
+    p.push_back(x);
+  };
+  for (int k = 0; k < nops; k++) {
+    const uint32_t op = ops[k];
+    const int cnt = (int)GSNAPDP_OP_COUNT(op);
+    switch (GSNAPDP_OP_TYPE(op)) {
+      case GSNAPDP_OP_DIAG:
+        for (int j = 0; j < cnt; j++, r--, c--) {
+          int qc = c - 1, gc = r - 1;
+          if (rev) {
+            qc = -qc;
+            gc = -gc;
+          }
+          const char c1 = q[qc];
+          const char c2 = G.nt(goff + gc);
+          char comp;
+          if (qu[qc] == c2) comp = GSNAPDP_DYNPROG_MATCH_COMP;
+          else if (host_consistent(c2, c1)) comp = GSNAPDP_AMBIGUOUS_COMP;  // swapped (:2760)
+          else comp = GSNAPDP_MISMATCH_COMP;
+          push(qoff + qc, goff + gc, c1, comp, c2);
+        }
+        break;
+      case GSNAPDP_OP_VSKIP: {  // query skip
+        int qc = c - 1, gc = r - 1, step;
+        if (rev) {
+          qc = -qc;
+          gc = -gc;
+          step = +1;
+        } else {
+          gc++;
+          step = -1;
+        }
+        for (int j = 0; j < cnt; j++, qc += step) push(qoff + qc, goff + gc, q[qc], '-', ' ');
+        c -= cnt;
+        break;
+      }
+      case GSNAPDP_OP_HDASH: {  // genome skip, dashes
+        int qc = c - 1, left = r - cnt, right = r - 1, step;
+        if (rev) {
+          const int t = left;
+          qc = -qc;
+          left = -right;
+          right = -t;
+          step = +1;
+        } else {
+          qc++;
+          step = -1;
+        }
+        int gc = rev ? left : right;
+        for (int j = 0; j < cnt; j++, gc += step) push(qoff + qc, goff + gc, ' ', '-', G.nt(goff + gc));
+        r -= cnt;
+        break;
+      }
+      default: {  // GSNAPDP_OP_HGAP: genome skip as a gapholder
+        gsnapdp_pair x;
+        memset(&x, 0, sizeof(x));
+        x.querypos = -1;
+        x.genomepos = -1;
+        x.queryjump = GSNAPDP_UNKNOWNJUMP;
+        x.genomejump = GSNAPDP_UNKNOWNJUMP;
+        x.cdna = ' ';
+        x.comp = ' ';
+        x.genome = ' ';
+        x.gapp = 1;
+        p.push_back(x);
+        r -= cnt;
+        break;
+      }
+    }
+  }
+}
+
+// Dynprog_cdna_gap's list (dynprog.c:4711-4793): the right side's pairs last
+// pushed first, then the INSERT_PAIRS pairs (or the gapholder), then the left
+// side's pairs.  `sequence2` is the reference's genomic-segment argument (read
+// by the INSERT_PAIRS branch); NULL reads the context genome at the same positions.
+extern "C" int gsnapdp_cgap_expand(gsnapdp_ctx* ctx, const gsnapdp_cgap_window* w,
+                                   const gsnapdp_cgap_result* res, const uint32_t* ops,
+                                   const char* query, const char* query_uc, const char* sequence2,
+                                   gsnapdp_pair* pairs, int cap) {
+  if (!ctx || !w || !res) return -1;
+  if (res->status == ST_OPS_OVERFLOW) return -1;
+  if (res->returned_null || res->status != ST_OK) return 0;
+  HostGenome G = {gsnapdp__host_blocks(ctx), gsnapdp__host_nwords(ctx), w->chroffset, w->chrhigh,
+                  w->chrpos, (int)w->genomiclength, w->watsonp ? 1 : 0};
+  const int dpi = w->dynprogindex, revoffset2 = w->offset2 + w->length2 - 1;
+  std::vector<gsnapdp_pair> pr, pl, pi;
+  replay_cdna(ops, res->nops_right, res->brR, res->bcR, query + w->qposR, query_uc + w->qposR,
+              w->revoffset1R, revoffset2, true, G, dpi, pr);
+  replay_cdna(ops + res->nops_right, res->nops_left, res->brL, res->bcL, query + w->qposL,
+              query_uc + w->qposL, w->offset1L, w->offset2, false, G, dpi, pl);
+  if (res->insert_pairs) {  // :4730-4752
+    for (int k = w->revoffset1R - res->bcR; k >= w->offset1L + res->bcL; k--) {
+      gsnapdp_pair x;
+      memset(&x, 0, sizeof(x));
+      x.querypos = k;
+      x.genomepos = revoffset2 - res->brR + 1;
+      x.dynprogindex = dpi;
+      x.cdna = query[w->qposL + (k - w->offset1L)];
+      x.comp = '~';  // SHORTGAP_COMP
+      x.genome = ' ';
+      pi.push_back(x);
+    }
+    for (int k = revoffset2 - res->brR; k >= w->offset2 + res->brL; k--) {
+      gsnapdp_pair x;
+      memset(&x, 0, sizeof(x));
+      x.querypos = w->offset1L + res->bcL;
+      x.genomepos = k;
+      x.dynprogindex = dpi;
+      x.cdna = ' ';
+      x.comp = '~';
+      x.genome = sequence2 ? sequence2[k - w->offset2] : G.nt(k);
+      pi.push_back(x);
+    }
+  } else {
+    gsnapdp_pair x;
+    memset(&x, 0, sizeof(x));
+    x.querypos = -1;
+    x.genomepos = -1;
+    x.queryjump = GSNAPDP_UNKNOWNJUMP;
+    x.genomejump = GSNAPDP_UNKNOWNJUMP;
+    x.cdna = ' ';
+    x.comp = ' ';
+    x.genome = ' ';
+    x.gapp = 1;
+    pi.push_back(x);
+  }
+  int n = 0;
+  for (int i = (int)pr.size() - 1; i >= 0; i--, n++)
+    if (n < cap) pairs[n] = pr[i];
+  for (size_t i = 0; i < pi.size(); i++, n++)
+    if (n < cap) pairs[n] = pi[i];
   for (size_t i = 0; i < pl.size(); i++, n++)
     if (n < cap) pairs[n] = pl[i];
   return n;

@@ -157,7 +157,10 @@ namespace gsnapdp {
 // signed 4-bit field (g = A C G T N *), bits 24..28 = consistent_array[c][class g].
 // prof[4*128 + u]: bit 24+g set when the uppercase query byte u equals "ACGTN"[g]
 // (the `rsequenceuc[r] == c2` half of the match test, dynprog.c:2650).
-constexpr int PROF_WORDS = 5 * 128;
+// prof[5*128 + c]: bit 24+g = consistent_array[class g][c], the swapped test of
+// traceback_cdna (dynprog.c:2760; consistent_array is asymmetric in the CMET modes).
+constexpr int PROF_WORDS = 6 * 128;
+constexpr int PROF_CONS_SWAPPED = 5 * 128;
 void build_profile_table(int mode, uint32_t prof[PROF_WORDS]);
 int host_pairdistance(int mt, int c1, int c2);
 int host_consistent(int c1, int c2);

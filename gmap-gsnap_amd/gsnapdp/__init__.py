@@ -18,7 +18,8 @@ import os
 
 import numpy as np
 
-from .records import GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW, MAXENT_IN, PAIR, RESULT, WINDOW  # noqa: F401
+from .records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW,  # noqa: F401
+                      MAXENT_IN, PAIR, RESULT, WINDOW)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
@@ -74,6 +75,12 @@ def lib():
         L.gsnapdp_ggap_run_device.restype = i32
         L.gsnapdp_ggap_expand.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i32]
         L.gsnapdp_ggap_expand.restype = i32
+        L.gsnapdp_cgap_run_host.argtypes = [vp, vp, i32, vp, vp, sz, vp, vp, vp]
+        L.gsnapdp_cgap_run_host.restype = i32
+        L.gsnapdp_cgap_run_device.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp]
+        L.gsnapdp_cgap_run_device.restype = i32
+        L.gsnapdp_cgap_expand.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i32]
+        L.gsnapdp_cgap_expand.restype = i32
         _lib = L
     return _lib
 
@@ -95,6 +102,15 @@ def ggap_op_offsets(windows: np.ndarray) -> np.ndarray:
     """Per-intron-window op capacity: two tracebacks of at most L1 + L2 + 1 steps."""
     L1 = windows["length1"].astype(np.int64).clip(0)
     cap = 2 * L1 + windows["length2L"].astype(np.int64).clip(0) + windows["length2R"].astype(np.int64).clip(0) + 4
+    off = np.zeros(len(windows) + 1, dtype=np.int64)
+    np.cumsum(cap, out=off[1:])
+    return off
+
+
+def cgap_op_offsets(windows: np.ndarray) -> np.ndarray:
+    """Per-cDNA-gap-window op capacity: two tracebacks of at most length1 + length2 + 1 steps."""
+    cap = (windows["length1L"].astype(np.int64).clip(0) + windows["length1R"].astype(np.int64).clip(0)
+           + 2 * windows["length2"].astype(np.int64).clip(0) + 4)
     off = np.zeros(len(windows) + 1, dtype=np.int64)
     np.cumsum(cap, out=off[1:])
     return off
@@ -209,6 +225,39 @@ class Context:
                                           _p(ops[off[i]:]), _p(q), _p(u), _p(out), cap)
             if n < 0:
                 raise GsnapdpError("gsnapdp_ggap_expand failed for window %d" % i)
+            outs.append(out[:n])
+            counts[i] = n
+        return (np.concatenate(outs) if outs else np.zeros(0, PAIR)), counts
+
+    def cgap_run(self, windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray):
+        """Dynprog_cdna_gap on the GPU.  Returns (results, ops, op_offsets)."""
+        w = np.ascontiguousarray(windows, dtype=CGAP_WINDOW)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        off = cgap_op_offsets(w)
+        res = np.zeros(len(w), dtype=CGAP_RESULT)
+        ops = np.zeros(max(1, int(off[-1])), dtype=np.uint32)
+        rc = lib().gsnapdp_cgap_run_host(self.h, _p(w), len(w), _p(q), _p(u), q.size, _p(res), _p(ops), _p(off))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_cgap_run_host: %s" % lib().gsnapdp_last_error().decode())
+        return res, ops, off
+
+    def cgap_all_pairs(self, windows, query, query_uc, results, ops, off, gseg=None, gseg_off=None):
+        """The lists Dynprog_cdna_gap returns, concatenated, and their lengths."""
+        w = np.ascontiguousarray(windows, dtype=CGAP_WINDOW)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        res = np.ascontiguousarray(results, dtype=CGAP_RESULT)
+        gs = None if gseg is None else np.ascontiguousarray(gseg, dtype=np.uint8)
+        outs, counts = [], np.zeros(len(w), dtype=np.int32)
+        for i in range(len(w)):
+            cap = int(w["length1L"][i]) + int(w["length1R"][i]) + 2 * int(w["length2"][i]) + 32
+            out = np.zeros(max(cap, 1), dtype=PAIR)
+            s2 = None if gs is None else ctypes.c_void_p(gs.ctypes.data + int(gseg_off[i]))
+            n = lib().gsnapdp_cgap_expand(self.h, _p(w[i:i + 1]), _p(res[i:i + 1]), _p(ops[off[i]:]),
+                                          _p(q), _p(u), s2, _p(out), out.size)
+            if n < 0:
+                raise GsnapdpError("gsnapdp_cgap_expand failed for window %d" % i)
             outs.append(out[:n])
             counts[i] = n
         return (np.concatenate(outs) if outs else np.zeros(0, PAIR)), counts

@@ -462,14 +462,14 @@ class CgapBatch(Batch):
         self.gseg_off = gseg_off
 
 
-def cgap_windows(gseq: np.ndarray, n: int, seed: int, mix: bool = True) -> CgapBatch:
+def cgap_windows(gseq: np.ndarray, n: int, seed: int, mix: bool = True, max_gap: int = 40) -> CgapBatch:
     rng = np.random.default_rng(seed)
     Gn = gseq.size
     w = np.zeros(n, dtype=CGAP_WINDOW)
     qs, us, segs, soff = [], [], [], [0]
     qpos = 0
     for i in range(n):
-        G = int(rng.integers(2, 41)) if not mix or rng.random() < 0.97 else int(rng.integers(0, 2))
+        G = int(rng.integers(2, max_gap + 1)) if not mix or rng.random() < 0.97 else int(rng.integers(0, 2))
         ins = int(rng.integers(10, 41))
         glen = 200 + G
         chrpos = int(rng.integers(0, Gn - glen - 1))

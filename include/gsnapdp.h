@@ -290,6 +290,23 @@ int gsnapdp_ggap_expand(gsnapdp_ctx *ctx, const gsnapdp_ggap_window *w,
                         const uint32_t *ops, const char *query, const char *query_uc,
                         gsnapdp_pair *pairs, int cap);
 
+/* ----------------------------------------------------------- cDNA gaps
+ * Dynprog_cdna_gap (dynprog.c:4578-4793) for `n` windows: both genome-row
+ * fills, bridge_cdna_gap and both tracebacks.  Op capacity per window:
+ * length1L + length1R + 2*length2 + 4.  Expansion rebuilds the list; the
+ * INSERT_PAIRS branch reads `sequence2` (the reference's genomic-segment
+ * argument, indexed from offset2), or the context genome when it is NULL. */
+int gsnapdp_cgap_run_device(gsnapdp_ctx *ctx, const gsnapdp_cgap_window *d_windows, int n,
+                            const char *d_query, const char *d_query_uc,
+                            gsnapdp_cgap_result *d_results, uint32_t *d_ops,
+                            const int64_t *d_op_offsets, void *stream);
+int gsnapdp_cgap_run_host(gsnapdp_ctx *ctx, const gsnapdp_cgap_window *windows, int n,
+                          const char *query, const char *query_uc, size_t query_bytes,
+                          gsnapdp_cgap_result *results, uint32_t *ops, const int64_t *op_offsets);
+int gsnapdp_cgap_expand(gsnapdp_ctx *ctx, const gsnapdp_cgap_window *w,
+                        const gsnapdp_cgap_result *res, const uint32_t *ops, const char *query,
+                        const char *query_uc, const char *sequence2, gsnapdp_pair *pairs, int cap);
+
 /* Load the MaxEnt parameter tables (12 x 16384 + 4 x 16 doubles, order in
  * DESIGN.md) into the context.  Must be called before gsnapdp_maxent_*. */
 int gsnapdp_load_maxent_tables(gsnapdp_ctx *ctx, const double *tables, size_t ndoubles);
