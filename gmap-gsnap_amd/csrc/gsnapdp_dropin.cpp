@@ -414,6 +414,89 @@ gsnapdp_List_T Dynprog_genome_gap(
   return list;
 }
 
+gsnapdp_List_T Dynprog_cdna_gap(
+    int* dynprogindex, int* finalscore, gsnapdp_bool* incompletep, gsnapdp_Dynprog_T dynprogL,
+    gsnapdp_Dynprog_T dynprogR, char* sequence1L, char* sequenceuc1L, char* revsequence1R,
+    char* revsequenceuc1R, char* sequence2, char* /*sequenceuc2*/, int length1L, int length1R,
+    int length2, int offset1L, int revoffset1R, int offset2, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_paired,
+    double defect_rate) {  // dynprog.c:4578-4793
+  std::lock_guard<std::mutex> lock(g.mu);
+  gsnapdp_ctx* c = ctx();
+  const Dynprog* dL = (const Dynprog*)dynprogL;
+  const Dynprog* dR = (const Dynprog*)dynprogR;
+  gsnapdp_cgap_window w;
+  memset(&w, 0, sizeof(w));
+  w.length1L = length1L;
+  w.length1R = length1R;
+  w.length2 = length2;
+  w.offset1L = offset1L;
+  w.revoffset1R = revoffset1R;
+  w.offset2 = offset2;
+  w.chroffset = chroffset;
+  w.chrhigh = chrhigh;
+  w.chrpos = chrpos;
+  w.genomiclength = genomiclength;
+  w.cdna_direction = cdna_direction;
+  w.extraband_paired = extraband_paired;
+  w.dynprogindex = *dynprogindex;
+  // the two workspaces' limits (:4651-4675), folded into one exact test
+  const bool too_long = length2 > dR->maxlength1 || length1R > dR->maxlength2 ||
+                        length2 > dL->maxlength1 || length1L > dL->maxlength2;
+  w.maxlength1 = too_long ? -1 : 0x3fffffff;
+  w.maxlength2 = 0x3fffffff;
+  w.defect_rate = defect_rate < 0.003 ? 0.001f : (defect_rate < 0.014 ? 0.01f : 0.5f);
+  w.watsonp = watsonp ? 1 : 0;
+  w.jump_late_p = jump_late_p ? 1 : 0;
+  // the query the fills read: sequence1L[0 .. length1L) forwards and
+  // revsequence1R[-(length1R-1) .. 0]; INSERT_PAIRS also reads sequence1L up to
+  // revoffset1R - offset1L
+  const int nL = length1L > 0 ? length1L : 0, nR = length1R > 0 ? length1R : 0;
+  const int span = revoffset1R - offset1L + 1 > nL ? revoffset1R - offset1L + 1 : nL;
+  g.q.assign((size_t)span + nR + 8, 0);
+  g.qu.assign(g.q.size(), 0);
+  if (length2 > 1) {
+    memcpy(g.q.data(), sequence1L, (size_t)span);
+    memcpy(g.qu.data(), sequenceuc1L, (size_t)span);
+    memcpy(g.q.data() + span, revsequence1R - (nR - 1), (size_t)nR);
+    memcpy(g.qu.data() + span, revsequenceuc1R - (nR - 1), (size_t)nR);
+  }
+  w.qposL = 0;
+  w.qposR = (uint32_t)(span + nR - 1);
+  const int64_t cap = (int64_t)nL + nR + 2 * (int64_t)(length2 > 0 ? length2 : 0) + 4;
+  const int64_t off[2] = {0, cap};
+  g.ops.assign((size_t)cap + 1, 0u);
+  gsnapdp_cgap_result r;
+  if (gsnapdp_cgap_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, g.ops.data(), off))
+    fatal(std::string("gsnapdp_cgap_run_host: ") + gsnapdp_last_error());
+  if (r.status == gsnapdp::ST_UNSUPPORTED)
+    fatal("cDNA-gap window outside the reference's domain (the reference aborts here)");
+  if (r.status == gsnapdp::ST_OPS_OVERFLOW) fatal("op stream overflow");
+  *dynprogindex = r.dynprogindex;
+  if (r.finalscore_set) *finalscore = r.finalscore;
+  // no bridge candidate: the reference traces back from uninitialised indices;
+  // defined here as NULL with the bridge's score
+  if (r.status != gsnapdp::ST_OK) return nullptr;
+  if (r.incompletep) *incompletep = 1;  // only ever set to true (:4756)
+  if (r.returned_null) return nullptr;
+  g.pairs.resize((size_t)cap + 32);
+  const int n = gsnapdp_cgap_expand(c, &w, &r, g.ops.data(), g.q.data(), g.qu.data(), sequence2,
+                                    g.pairs.data(), (int)g.pairs.size());
+  if (n < 0 || n > (int)g.pairs.size()) fatal("gsnapdp_cgap_expand failed");
+  gsnapdp_List_T list = nullptr;
+  for (int i = n - 1; i >= 0; i--) {
+    const gsnapdp_pair& p = g.pairs[(size_t)i];
+    if (p.gapp)
+      list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump, /*knownp*/ 0);
+    else
+      list = Pairpool_push(list, pairpool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome,
+                           p.dynprogindex);
+  }
+  return list;
+}
+
 void Maxent_hr_setup(unsigned int* ref_blocks) {  // maxent_hr.c:27195
   std::lock_guard<std::mutex> lock(g.mu);
   if (g.blocks && ref_blocks != g.blocks) fatal("Maxent_hr_setup blocks differ from the genome");

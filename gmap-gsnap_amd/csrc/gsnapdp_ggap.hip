@@ -453,11 +453,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
     const int jl = w.jump_late_p ? 1 : 0;
 #ifndef GG_EXP_NOFILL
     gg_fill<RL, GMEM, false>(SL, clsL, bnd, G.L1, rho, G.open, G.ext, jl,
-                             [&](int r) { return ptab[(unsigned char)q[w.qpos + r - 1] & 127u]; }, T, NS);
+                             [&](int r) { return ptab[(unsigned char)q[(int)w.qpos + r - 1] & 127u]; }, T, NS);
 #endif
 #ifndef GG_EXP_NOFILL
     gg_fill<RL, GMEM, false>(SR, clsR, bnd, G.L1, rho, G.open, G.ext, 1 - jl,
-                             [&](int r) { return ptab[(unsigned char)q[w.qpos + G.L1 - r] & 127u]; }, T, NS);
+                             // (a shadow group has L1 = 0: clamp to the window's first query byte)
+                             [&](int r) { return ptab[(unsigned char)q[(int)w.qpos + max(0, G.L1 - r)] & 127u]; },
+                             T, NS);
 #endif
     if constexpr (GMEM) __threadfence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);

@@ -76,6 +76,16 @@ gsnapdp_List_T Dynprog_single_gap(
     gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_single,
     double defect_rate, int close_indels_mode, gsnapdp_bool widebandp); /* dynprog.c:4450 */
 
+gsnapdp_List_T Dynprog_cdna_gap(
+    int* dynprogindex, int* finalscore, gsnapdp_bool* incompletep, gsnapdp_Dynprog_T dynprogL,
+    gsnapdp_Dynprog_T dynprogR, char* sequence1L, char* sequenceuc1L, char* revsequence1R,
+    char* revsequenceuc1R, char* sequence2, char* sequenceuc2, int length1L, int length1R,
+    int length2, int offset1L, int revoffset1R, int offset2, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_paired,
+    double defect_rate); /* dynprog.c:4579 (non-PMAP) */
+
 gsnapdp_List_T Dynprog_genome_gap(
     int* dynprogindex, int* finalscore, int* new_leftgenomepos, int* new_rightgenomepos,
     double* left_prob, double* right_prob, int* nmatches, int* nmismatches, int* nopens,

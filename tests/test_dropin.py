@@ -196,6 +196,8 @@ def test_dropin_genome_gap_matches_reference_golden(golden_dir, tmp_path):
     W = z["windows"]
     for i in range(min(300, len(W))):
         w = W[i]
+        if w["maxlength1"] != 611 or w["maxlength2"] != 2000:
+            continue  # shrunken workspace limits: Dynprog_new cannot make them
         ints = [ctypes.c_int(int(w["dynprogindex"]))] + [ctypes.c_int(-77) for _ in range(3)]
         probs = [ctypes.c_double(-1.0), ctypes.c_double(-1.0)]
         counts = [ctypes.c_int(-77) for _ in range(6)]  # nmatches .. introntype
@@ -231,6 +233,66 @@ def test_dropin_genome_gap_matches_reference_golden(golden_dir, tmp_path):
         assert out[:k].tobytes() == ref_pairs.tobytes(), i
         if lst:
             dbl.dbl_list_free(lst)
+    L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dpL)))
+    L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dpR)))
+    L.Dynprog_term()
+
+
+CGAP_ARGS = ([ctypes.c_void_p] * 5 + [ctypes.c_char_p] * 6 + [ctypes.c_int] * 6 + [ctypes.c_uint] * 4
+             + [ctypes.c_int, ctypes.c_ubyte, ctypes.c_ubyte, ctypes.c_void_p, ctypes.c_int, ctypes.c_double])
+
+
+@pytest.mark.gpu
+def test_dropin_cdna_gap_matches_reference_golden(golden_dir, tmp_path):
+    """Dynprog_cdna_gap called like traverse_cdna_gap (stage3.c:5604) on the
+    reference's golden windows: out-parameters exactly where it writes them,
+    and the list (INSERT_PAIRS included)."""
+    z = np.load(os.path.join(golden_dir, "cgap_chr17.npz"), allow_pickle=False)
+    dbl = load_double(tmp_path)
+    L = ctypes.CDLL(DROPIN)
+    L.Dynprog_new.restype = ctypes.c_void_p
+    L.Dynprog_new.argtypes = [ctypes.c_int] * 5
+    L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    L.Dynprog_cdna_gap.restype = ctypes.c_void_p
+    L.Dynprog_cdna_gap.argtypes = CGAP_ARGS
+    blocks = np.ascontiguousarray(z["blocks"])
+    L.Dynprog_init(600, 10, 11, 10, 8, 0)
+    L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
+    dpL = L.Dynprog_new(600, 10, 11, 10, 8)
+    dpR = L.Dynprog_new(600, 10, 11, 10, 8)
+    q = np.ascontiguousarray(z["query"])
+    qu = np.ascontiguousarray(z["query_uc"])
+    gs = np.ascontiguousarray(z["gseg"])
+    offs = np.concatenate([[0], np.cumsum(z["npairs"])])
+    out = np.zeros(8192, dtype=REC)
+    ref = z["results"]
+    W = z["windows"]
+    inserts = 0
+    for i in range(min(400, len(W))):
+        w, r = W[i], ref[i]
+        if w["maxlength1"] != 611 or w["maxlength2"] != 2000:
+            continue  # shrunken workspace limits: Dynprog_new cannot make them
+        dpi, fs, inc = ctypes.c_int(int(w["dynprogindex"])), ctypes.c_int(-777), ctypes.c_ubyte(0)
+        args = ([ctypes.byref(dpi), ctypes.byref(fs), ctypes.byref(inc), dpL, dpR,
+                 ctypes.c_char_p(q.ctypes.data + int(w["qposL"])), ctypes.c_char_p(qu.ctypes.data + int(w["qposL"])),
+                 ctypes.c_char_p(q.ctypes.data + int(w["qposR"])), ctypes.c_char_p(qu.ctypes.data + int(w["qposR"])),
+                 ctypes.c_char_p(gs.ctypes.data + int(z["gseg_off"][i])), None]
+                + [int(w[f]) for f in ("length1L", "length1R", "length2", "offset1L", "revoffset1R", "offset2")]
+                + [int(w[f]) for f in ("chroffset", "chrhigh", "chrpos", "genomiclength")]
+                + [int(w["cdna_direction"]), int(w["watsonp"]), int(w["jump_late_p"]), None,
+                   int(w["extraband_paired"]), float(w["defect_rate"])])
+        lst = L.Dynprog_cdna_gap(*args)
+        assert dpi.value == r["dynprogindex"], i
+        assert fs.value == (r["finalscore"] if r["finalscore_set"] else -777), i
+        assert inc.value == r["incompletep"], i
+        k = dbl.dbl_list_read(lst, out.ctypes.data, out.size) if lst else 0
+        exp = z["pairs"][offs[i]:offs[i + 1]]
+        assert k == exp.size, (i, k, exp.size)
+        assert out[:k].tobytes() == exp.tobytes(), i
+        inserts += int((exp["comp"] == b"~").any())
+        if lst:
+            dbl.dbl_list_free(lst)
+    assert inserts > 3
     L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dpL)))
     L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dpR)))
     L.Dynprog_term()
