@@ -108,7 +108,9 @@ __device__ inline int padded_bucket(int k, int h) {
 
 // Also writes -1 into every bucket's padding entries of perm, so perm needs
 // no clearing.
-__global__ void k_scan(const int* __restrict__ hist, int* __restrict__ cursor,
+// (also zeroes the histogram for the next batch: the context clears it once at
+// allocation, so no per-batch memset is needed)
+__global__ void k_scan(int* __restrict__ hist, int* __restrict__ cursor,
                        int* __restrict__ class_start, int* __restrict__ perm) {
   __shared__ int part[1024];
   const int tid = threadIdx.x;
@@ -130,6 +132,7 @@ __global__ void k_scan(const int* __restrict__ hist, int* __restrict__ cursor,
     cursor[k] = run;
     for (int e = run + h; e < run + p; e++) perm[e] = -1;
     run += p;
+    hist[k] = 0;
   }
   __syncthreads();
   if (tid == 0) {
@@ -856,6 +859,8 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
     return fail("copy prof", e);
   const size_t small = (size_t)2 * NKEYS + NCLASS + 1 + 1 + 64;
   if ((e = hipMalloc(&ctx->d_small, small * 4)) != hipSuccess) return fail("malloc small", e);
+  if ((e = hipMemset(ctx->d_small, 0, small * 4)) != hipSuccess) return fail("memset small", e);
+
   ctx->dirpool_waves = (size_t)ctx->fill_waves;
   if ((e = hipMalloc(&ctx->d_dirpool, ctx->dirpool_waves * WAVE_STRIDE_DW * 4)) != hipSuccess)
     return fail("malloc dirpool", e);
@@ -927,7 +932,6 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   int* cursor = hist + NKEYS;
   int* class_start = cursor + NKEYS;
   int* big_count = class_start + NCLASS + 1;  // RW_NCLS row-lane class counts
-  HIPCHK(hipMemsetAsync(hist, 0, (size_t)NKEYS * 4, st));
   HIPCHK(hipMemsetAsync(big_count, 0, 4 * RW_NCLS, st));
   if (!ctx->d_bigpool)  // global scratch of the large row-lane windows, on first use
     HIPCHK(hipMalloc(&ctx->d_bigpool, (size_t)RW_BIG_WAVES * RW_BIG_WORDS * 4));
@@ -945,6 +949,8 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   mark(1, 1);
   const int blocks = (int)(ctx->dirpool_waves / 4);
   const uint64_t nw = (uint64_t)ctx->nwords;
+  // (k_fill keeps every CU busy, so k_rows runs after it on the same stream: a
+  // side stream measured slower)
   mark(2, 0);
   hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, st, d_windows, ctx->d_perm, class_start,
                      d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_dirpool,
