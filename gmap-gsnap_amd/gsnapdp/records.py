@@ -70,6 +70,16 @@ CGAP_RESULT = np.dtype([
 ])
 assert CGAP_RESULT.itemsize == 64
 
+SJ_WINDOW = np.dtype([
+    ("kind", "<i4"), ("length1", "<i4"), ("length2", "<i4"), ("offset1", "<i4"),
+    ("offset2_anchor", "<i4"), ("offset2_far", "<i4"), ("contlength", "<i4"),
+    ("qpos", "<u4"), ("spos", "<u4"),
+    ("cdna_direction", "<i4"), ("extraband_end", "<i4"), ("dynprogindex", "<i4"),
+    ("maxlength1", "<i4"), ("maxlength2", "<i4"), ("defect_rate", "<f4"),
+    ("watsonp", "u1"), ("jump_late_p", "u1"), ("pad0", "u1"), ("pad1", "u1"),
+])
+assert SJ_WINDOW.itemsize == 64
+
 MAXENT_IN = np.dtype([("model", "<u4"), ("splice_pos", "<u4"), ("chroffset", "<u4"), ("pad", "<u4")])
 
 # enums (include/gsnapdp.h)

@@ -17,6 +17,12 @@
 * ``cgap_windows``: Dynprog_cdna_gap windows shaped like traverse_cdna_gap's
   (stage3.c:5518-5627): a query gap longer than the genome gap by a cDNA
   insertion of 10-40 bases; length1L = length1R = genomejump + 8.
+* ``sj_windows``: Dynprog_end5/3_splicejunction windows shaped like
+  Splicetrie_solve_end5/3's (splicetrie.c:325-372, 620-660): a query end
+  whose last (end5) or first (end3) ``contlength`` bases continue the anchor
+  exon and whose rest comes from a far exon, against the splice junction
+  Dynprog_make_splicejunction_5/3 builds (distal + proximal genome), plus
+  random segments, planted introns and the early-return cases.
 * ``c5_windows``: the DP windows GSNAP issues for 100 bp reads (BASELINE
   config 5 reduced to its DP part): per read one single gap over
   the read (extraband_single 3) and two end gaps (end5 + end3, length1 1-30,
@@ -29,7 +35,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import genome as _genome
-from .records import (BEST_LOCAL, CGAP_WINDOW, END3_GAP, END5_GAP, GGAP_WINDOW, MAXLENGTH1, MAXLENGTH2,
+from .records import (BEST_LOCAL, CGAP_WINDOW, SJ_WINDOW, END3_GAP, END5_GAP, GGAP_WINDOW, MAXLENGTH1, MAXLENGTH2,
                       QUERYEND_GAP, QUERYEND_INDELS, QUERYEND_NOGAPS, SINGLE_GAP, WINDOW)
 
 ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
@@ -529,6 +535,92 @@ def cgap_windows(gseq: np.ndarray, n: int, seed: int, mix: bool = True, max_gap:
     gs = np.concatenate(segs)
     # sequence2[k] is addressed relative to offset2
     return CgapBatch(w, np.concatenate(qs), np.concatenate(us), gs, np.array(soff[:-1], dtype=np.int64))
+
+
+def sj_windows(gseq: np.ndarray, n: int, seed: int, mix: bool = True) -> Batch:
+    rng = np.random.default_rng(seed)
+    Gn = gseq.size
+    w = np.zeros(n, dtype=SJ_WINDOW)
+    qs, us = [], []
+    qpos = 0
+    for i in range(n):
+        end5 = bool(rng.integers(0, 2))
+        r = rng.random()
+        L1 = int(rng.integers(1, 41)) if r < 0.85 else int(rng.integers(41, 160))
+        extra = 10 if rng.random() < 0.7 else int(rng.integers(0, 40))
+        L2 = L1 + extra
+        cont = int(rng.integers(0, L1))
+        spl = L2 - cont
+        a = int(rng.integers(0, Gn - cont - 1))
+        f = int(rng.integers(0, Gn - spl - 1))
+        prox = gseq[a:a + cont]
+        dist = gseq[f:f + spl]
+        if not bool(rng.integers(0, 2)):  # minus-strand junctions are complemented in place (:6091)
+            prox, dist = _COMP[prox], _COMP[dist]
+        if mix and rng.random() < 0.15:
+            dist = dist.copy()
+            k = int(rng.integers(0, max(1, spl - 30)))
+            dist[k:k + 2] = np.frombuffer(b"GT", np.uint8)[:dist[k:k + 2].size]
+            dist[k + 14:k + 16] = np.frombuffer(b"AG", np.uint8)[:dist[k + 14:k + 16].size]
+        if end5:
+            seg = np.concatenate([dist, prox])          # distal first (:6068), proximal at [splicelength]
+            q = np.concatenate([dist[spl - (L1 - cont):] if L1 > cont else dist[:0], prox])
+        else:
+            seg = np.concatenate([prox, dist])          # proximal first, distal at [contlength] (:6152)
+            q = np.concatenate([prox, dist[:L1 - cont]])
+        if mix and rng.random() < 0.2:
+            seg = ACGT[rng.integers(0, 4, size=L2)]
+        q = _mutate(rng, q, 0.03, 0.01)
+        if mix and rng.random() < 0.2 and L1 > 6:  # a small indel
+            p = int(rng.integers(1, L1 - 2))
+            if rng.random() < 0.5:
+                q = np.concatenate([q[:p], q[p + 1:], ACGT[rng.integers(0, 4, size=1)]])
+            else:
+                q = np.concatenate([q[:p], ACGT[rng.integers(0, 4, size=1)], q[p:-1]])
+        quc = q.copy()
+        if mix and rng.random() < 0.1:
+            m = rng.random(q.size) < 0.3
+            q = q.copy()
+            q[m] = np.where(rng.random(int(m.sum())) < 0.7, q[m] + 32,
+                            _AMBIG[rng.integers(0, _AMBIG.size, int(m.sum()))])
+            quc = np.where((q >= 97) & (q <= 122), q - 32, q).astype(np.uint8)
+        rec = w[i]
+        rec["kind"] = END5_GAP if end5 else END3_GAP
+        rec["length1"] = L1
+        rec["length2"] = L2
+        rec["contlength"] = cont
+        base1 = int(rng.integers(0, 400))
+        anchor = int(rng.integers(50, 400))
+        intron = int(rng.integers(60, 5000))
+        if end5:
+            rec["offset1"] = base1 + L1 - 1                  # revoffset1
+            rec["offset2_anchor"] = anchor
+            rec["offset2_far"] = anchor - intron             # splicetrie.c:346-351
+            rec["qpos"] = qpos + L1 - 1
+            rec["spos"] = qpos + L1 + 4 + L2 - 1
+        else:
+            rec["offset1"] = base1
+            rec["offset2_anchor"] = anchor
+            rec["offset2_far"] = anchor + intron
+            rec["qpos"] = qpos
+            rec["spos"] = qpos + L1 + 4
+        rec["cdna_direction"] = int(rng.choice([1, -1, 0]))
+        rec["extraband_end"] = int(rng.choice([3, 3, 5, 10])) if mix else 3
+        rec["dynprogindex"] = int(rng.choice([-1, 2]))
+        small = mix and rng.random() < 0.02
+        rec["maxlength1"] = 20 if small else MAXLENGTH1
+        rec["maxlength2"] = 30 if small else MAXLENGTH2
+        rec["defect_rate"] = float(rng.choice([0.001, 0.005, 0.02]))
+        rec["watsonp"] = int(rng.integers(0, 2))
+        rec["jump_late_p"] = int(rng.integers(0, 2))
+        pad = np.full(4, ord("#"), np.uint8)
+        qs += [q, pad, seg, pad]
+        us += [quc, pad, seg, pad]
+        qpos += L1 + 4 + L2 + 4
+    if mix and n >= 4:  # early returns: empty query / segment
+        w[0]["length1"] = 0
+        w[1]["length2"] = 0
+    return Batch(w, np.concatenate(qs), np.concatenate(us))
 
 
 def c5_windows(gseq: np.ndarray, nreads: int, seed: int = 5, read_len: int = 100,

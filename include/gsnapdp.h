@@ -10,6 +10,8 @@
  *   - Dynprog_single_gap   dynprog.c:4450-4572   (kind GSNAPDP_SINGLE_GAP)
  *   - Dynprog_end5_gap     dynprog.c:5094-5284   (kind GSNAPDP_END5_GAP)
  *   - Dynprog_end3_gap     dynprog.c:5556-5741   (kind GSNAPDP_END3_GAP)
+ *   - Dynprog_end5_splicejunction dynprog.c:5412-5553 / Dynprog_end3_splicejunction
+ *     :5869-6057 (gsnapdp_sj_*)
  *   - Maxent_hr_*_prob     maxent_hr.c:27217-27390 (gsnapdp_maxent_batch)
  *   - Genome_user_setup / Maxent_hr_setup (genome.c:9989, maxent_hr.c:27195):
  *     the packed genome blocks are uploaded once per context.
@@ -28,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GSNAPDP_ABI_VERSION 1
+#define GSNAPDP_ABI_VERSION 2
 
 /* Window kinds (one reference entry point each). */
 enum {
@@ -133,7 +135,8 @@ typedef struct gsnapdp_pair {
   char cdna;
   char comp;
   char genome;
-  uint8_t gapp;           /* 1 for a gapholder */
+  uint8_t gapp;           /* bit 0: a gapholder (gapp); bit 1: knowngapp, i.e. pushed with
+                           * knownp = true (Pairpool_push_gapholder, pairpool.c:383-390) */
 } gsnapdp_pair;
 
 /* One intron window (Dynprog_genome_gap, dynprog.c:4798-5061), run with
@@ -306,6 +309,52 @@ int gsnapdp_cgap_run_host(gsnapdp_ctx *ctx, const gsnapdp_cgap_window *windows, 
 int gsnapdp_cgap_expand(gsnapdp_ctx *ctx, const gsnapdp_cgap_window *w,
                         const gsnapdp_cgap_result *res, const uint32_t *ops, const char *query,
                         const char *query_uc, const char *sequence2, gsnapdp_pair *pairs, int cap);
+
+/* --------------------------------------------------- splice-junction ends
+ * Dynprog_end5_splicejunction (dynprog.c:5412-5553, kind GSNAPDP_END5_GAP) and
+ * Dynprog_end3_splicejunction (:5869-6057, kind GSNAPDP_END3_GAP): an end gap
+ * against a caller-built genomic segment (the splice junction of
+ * Dynprog_make_splicejunction_5/3, `use_genomicseg_p`), endpoint on the last
+ * query row (find_best_endpoint_to_queryend_indels :2293), and the traceback
+ * split at column `contlength` (traceback_local :2874) around a known
+ * gapholder.  The segment lives in the batch query buffers: query[spos...]
+ * holds sequence2 (read forwards for END3, backwards from revsequence2[0] for
+ * END5, like the query) and query_uc[spos...] sequenceuc2.  The reference
+ * never reads chroffset / chrpos here, so the record does not carry them.
+ * Segments must consist of A C G T N (what Genome_fill_buffer_blocks_noterm
+ * writes, genome.c:8912-8960); other bytes give status UNSUPPORTED. */
+typedef struct gsnapdp_sj_window {
+  int32_t kind;            /* GSNAPDP_END5_GAP or GSNAPDP_END3_GAP */
+  int32_t length1, length2;
+  int32_t offset1;         /* offset1 (END3) or revoffset1 (END5) */
+  int32_t offset2_anchor;  /* (rev)offset2_anchor: genome offset of the second traceback part */
+  int32_t offset2_far;     /* (rev)offset2_far: genome offset of the first part */
+  int32_t contlength;      /* endc of the first traceback part */
+  uint32_t qpos;           /* sequence1[0] / revsequence1[0] in the query buffers */
+  uint32_t spos;           /* sequence2[0] / revsequence2[0] in the query buffers */
+  int32_t cdna_direction, extraband_end, dynprogindex, maxlength1, maxlength2;
+  float defect_rate;
+  uint8_t watsonp, jump_late_p, pad0, pad1;
+} gsnapdp_sj_window;
+
+/* Results use gsnapdp_result: finalscore = the reference's recomputed
+ * 3*nmatches - 5*nmismatches + nopens*open + nindels*extend (:5541 / :6045),
+ * status 1 (early return, NULL list) when a length is <= 0 or above the
+ * workspace maxima (:5446-5461), reserved = *dynprogindex after the call.
+ * Op capacity per window: length1 + length2 + 2 (as gsnapdp_run_*). */
+int gsnapdp_sj_run_device(gsnapdp_ctx *ctx, const gsnapdp_sj_window *d_windows, int n,
+                          const char *d_query, const char *d_query_uc, gsnapdp_result *d_results,
+                          uint32_t *d_ops, const int64_t *d_op_offsets, void *stream);
+int gsnapdp_sj_run_host(gsnapdp_ctx *ctx, const gsnapdp_sj_window *windows, int n,
+                        const char *query, const char *query_uc, size_t query_bytes,
+                        gsnapdp_result *results, uint32_t *ops, const int64_t *op_offsets);
+/* The list the entry point returns: part one (columns > contlength, genome
+ * offset offset2_far), the known gapholder (queryjump 0, genomejump
+ * anchor - far for END5, far - anchor for END3), part two (offset2_anchor),
+ * then INDEL stripping and the END5 List_reverse (:5543-5553 / :6047-6057). */
+int gsnapdp_sj_expand(gsnapdp_ctx *ctx, const gsnapdp_sj_window *w, const gsnapdp_result *res,
+                      const uint32_t *ops, const char *query, const char *query_uc,
+                      gsnapdp_pair *pairs, int cap);
 
 /* Load the MaxEnt parameter tables (12 x 16384 + 4 x 16 doubles, order in
  * DESIGN.md) into the context.  Must be called before gsnapdp_maxent_*. */

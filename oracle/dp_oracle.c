@@ -110,8 +110,12 @@ static void push_pair(orc_list *l, int querypos, int genomepos, char cdna, char 
   p->gapp = 0;
 }
 
-/* Pairpool_push_gapholder (pairpool.c:352-400). */
+/* Pairpool_push_gapholder (pairpool.c:352-400); gapp bit 1 = knowngapp (:383). */
+static void push_gapholder_k(orc_list *l, int queryjump, int genomejump, int knownp);
 static void push_gapholder(orc_list *l, int queryjump, int genomejump) {
+  push_gapholder_k(l, queryjump, genomejump, 0);
+}
+static void push_gapholder_k(orc_list *l, int queryjump, int genomejump, int knownp) {
   gsnapdp_pair *p;
   if (l->head == 0) list_grow(l);
   p = &l->buf[--l->head];
@@ -124,7 +128,7 @@ static void push_gapholder(orc_list *l, int queryjump, int genomejump) {
   p->cdna = ' ';
   p->comp = ' ';
   p->genome = ' ';
-  p->gapp = 1;
+  p->gapp = knownp ? 3 : 1;
 }
 
 /* List_reverse */
@@ -306,9 +310,21 @@ static void band_widths(int L1, int L2, int extraband, int widebandp, int *lband
 
 /* compute_scores_lookup_fwd / _rev (dynprog.c:1424-1578 / 1581-1736).
  * rev: query read as seq1[1-r] and genome at offset2+1-c. */
+static void fill_seg(mview *m, orc_dp *dp, const char *seq1, int rev, int offset2, int L1, int L2,
+                     const gpar *g, const char *seq2, int mt, int open, int extend, int extraband,
+                     int widebandp, int jump_late_p);
 static void fill(mview *m, orc_dp *dp, const char *seq1, int rev, int offset2, int L1, int L2,
                  const gpar *g, int mt, int open, int extend, int extraband, int widebandp,
                  int jump_late_p) {
+  fill_seg(m, dp, seq1, rev, offset2, L1, L2, g, NULL, mt, open, extend, extraband, widebandp,
+           jump_late_p);
+}
+
+/* seq2 != NULL: use_genomicseg_p, the genome of column c is seq2[c-1] (fwd) or
+ * seq2[1-c] (rev) (:1535 / :1690) */
+static void fill_seg(mview *m, orc_dp *dp, const char *seq1, int rev, int offset2, int L1, int L2,
+                     const gpar *g, const char *seq2, int mt, int open, int extend, int extraband,
+                     int widebandp, int jump_late_p) {
   int lband, rband, r, c, rlo, rhigh, penalty;
   size_t cells = (size_t)(L1 + 1) * (size_t)(L2 + 1);
   int32_t *H = dp->nogap, *E = dp->gap1, *F = dp->gap2;
@@ -363,7 +379,8 @@ static void fill(mview *m, orc_dp *dp, const char *seq1, int rev, int offset2, i
   dF[(size_t)stride] = D_STOP; /* (*directions)[1][0].gap2 = STOP */
 
   for (c = 1; c <= L2; c++) {
-    int na2 = (unsigned char)gnt(g, rev ? offset2 + 1 - c : offset2 + c - 1) & 127;
+    int na2 = (unsigned char)(seq2 ? (rev ? seq2[1 - c] : seq2[c - 1])
+                                   : gnt(g, rev ? offset2 + 1 - c : offset2 + c - 1)) & 127;
     if ((rlo = c - rband) < 1) {
       rlo = 1;
     } else {
@@ -764,6 +781,173 @@ void orc_end3_gap(orc_list *out, int *dynprogindex, int *finalscore, int *nmatch
   end_gap(out, 0, dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dp,
           sequence1, sequenceuc1, length1, length2, offset1, offset2, chroffset, chrhigh, chrpos,
           genomiclength, cdna_direction, watsonp, jump_late_p, extraband_end, endalign);
+}
+
+/* ------------------------------------------------- splice-junction ends */
+
+/* add_genomeskip (dynprog.c:2416-2512) with use_genomicseg_p: the intron test
+ * reads gseq_uc, the dashes gseq (window coordinates, rev-indexed like the query). */
+static int add_genomeskip_seg(orc_list *l, int r, int c, int dist, int qoff, int goff, int rev,
+                              const char *gseq, const char *gseq_uc, int cdna_direction, int dpi) {
+  int j, qc = r - 1, left = c - dist, right = c - 1, gc, step, dashes;
+  if (rev) {
+    int t = left;
+    qc = -qc;
+    left = -right;
+    right = -t;
+    step = +1;
+  } else {
+    qc++;
+    step = -1;
+  }
+  if (dist < MICROINTRON_LENGTH) {
+    dashes = 1;
+  } else {
+    dashes = intron_type(gseq_uc[left], gseq_uc[left + 1], gseq_uc[right - 1], gseq_uc[right],
+                         cdna_direction) == NONINTRON;
+  }
+  if (dashes) {
+    gc = rev ? left : right;
+    for (j = 0; j < dist; j++) {
+      push_pair(l, qoff + qc, goff + gc, ' ', '-', gseq[gc], dpi);
+      gc += step;
+    }
+  } else {
+    push_gapholder(l, GSNAPDP_UNKNOWNJUMP, GSNAPDP_UNKNOWNJUMP);
+  }
+  return dashes;
+}
+
+/* traceback_local (dynprog.c:2874-2968): runs while *c > endc, leaves (*r,*c)
+ * where it stopped; genome chars from the segment, every diagonal cell pushes. */
+static void traceback_local(orc_list *l, counts *k, const mview *m, int *pr, int *pc, int endc,
+                            const char *qseq, const char *qseq_uc, const char *gseq,
+                            const char *gseq_uc, int qoff, int goff, int rev, int cdna_direction,
+                            int dpi) {
+  int r = *pr, c = *pc;
+  while (c > endc) {
+    int qc = r - 1, gc = c - 1, dist;
+    char c1, c2;
+    uint8_t d;
+    if (rev) {
+      qc = -qc;
+      gc = -gc;
+    }
+    c1 = qseq[qc];
+    c2 = gseq[gc];
+    if (qseq_uc[qc] == c2) {
+      k->nmatches++;
+      push_pair(l, qoff + qc, goff + gc, c1, '*', c2, dpi);
+    } else if (cons[c1 & 127][c2 & 127]) {
+      k->nmatches++;
+      push_pair(l, qoff + qc, goff + gc, c1, ':', c2, dpi);
+    } else {
+      k->nmismatches++;
+      push_pair(l, qoff + qc, goff + gc, c1, ' ', c2, dpi);
+    }
+    d = m->dH[IX(m, r, c)];
+    if (d == D_DIAG) {
+      r--;
+      c--;
+    } else if (d == D_HORIZ) {
+      dist = 1;
+      r--;
+      c--;
+      while (m->dE[IX(m, r, c)] == D_HORIZ) {
+        dist++;
+        c--;
+      }
+      c--;
+      if (add_genomeskip_seg(l, r, c + dist, dist, qoff, goff, rev, gseq, gseq_uc, cdna_direction,
+                             dpi)) {
+        k->nopens++;
+        k->nindels += dist;
+      }
+    } else {
+      dist = 1;
+      r--;
+      c--;
+      while (m->dF[IX(m, r, c)] == D_VERT) {
+        dist++;
+        r--;
+      }
+      r--;
+      add_queryskip(l, r + dist, c, dist, qseq, qoff, goff, rev, dpi);
+      k->nopens++;
+      k->nindels += dist;
+    }
+  }
+  *pr = r;
+  *pc = c;
+}
+
+/* shared body of Dynprog_end5_splicejunction (:5412-5553, rev) and
+ * Dynprog_end3_splicejunction (:5869-6057) */
+static void end_splicejunction(orc_list *out, int rev, int *dynprogindex, int *finalscore,
+                               int *nmatches, int *nmismatches, int *nopens, int *nindels,
+                               orc_dp *dp, const char *seq1, const char *seq1uc, const char *seq2,
+                               const char *seq2uc, int length1, int length2, int off1,
+                               int off2_anchor, int off2_far, int cdna_direction,
+                               int jump_late_p, int extraband_end, int contlength) {
+  mview m;
+  counts k = {0, 0, 0, 0};
+  gpar g = {0, 0, 0, 0, 1};  /* never read: use_genomicseg_p */
+  int bestr, bestc, jl = rev ? !jump_late_p : jump_late_p;
+  orc_list_clear(out);
+  if (length1 <= 0 || length1 > dp->maxlength1 || length2 <= 0 || length2 > dp->maxlength2) {
+    *nmatches = *nmismatches = *nopens = *nindels = 0; /* :5446-5461 */
+    *finalscore = 0;
+    return;
+  }
+  fill_seg(&m, dp, seq1, rev, off2_anchor, length1, length2, &g, seq2, MT_ENDQ, END_OPEN,
+           END_EXTEND, extraband_end, 1, jl);
+  best_endpoint_indels(finalscore, &bestr, &bestc, &m, length1, length2, extraband_end, jl);
+  traceback_local(out, &k, &m, &bestr, &bestc, contlength, seq1, seq1uc, seq2, seq2uc, off1,
+                  off2_far, rev, cdna_direction, *dynprogindex);
+  push_gapholder_k(out, 0, rev ? off2_anchor - off2_far : off2_far - off2_anchor, 1);
+  traceback_local(out, &k, &m, &bestr, &bestc, 0, seq1, seq1uc, seq2, seq2uc, off1, off2_anchor,
+                  rev, cdna_direction, *dynprogindex);
+  *nmatches = k.nmatches;
+  *nmismatches = k.nmismatches;
+  *nopens = k.nopens;
+  *nindels = k.nindels;
+  *finalscore = k.nmatches * FULLMATCH + k.nmismatches * mismatch_score[MT_ENDQ] +
+                k.nopens * END_OPEN + k.nindels * END_EXTEND; /* :5541 / :6045 */
+  list_reverse(out);
+  while (out->n > 0 && out->buf[out->head].comp == '-') { /* strip INDEL_COMP */
+    out->head++;
+    out->n--;
+  }
+  *dynprogindex = step_index(*dynprogindex);
+  if (rev) list_reverse(out); /* end5 returns List_reverse(pairs); end3 does not */
+}
+
+void orc_end5_splicejunction(orc_list *out, int *dynprogindex, int *finalscore, int *nmatches,
+                             int *nmismatches, int *nopens, int *nindels, orc_dp *dp,
+                             const char *revsequence1, const char *revsequenceuc1,
+                             const char *revsequence2, const char *revsequenceuc2, int length1,
+                             int length2, int revoffset1, int revoffset2_anchor,
+                             int revoffset2_far, int cdna_direction, int jump_late_p,
+                             int extraband_end, double defect_rate, int contlength) {
+  (void)defect_rate; /* END open/extend are equal for all bins (:5429-5438) */
+  end_splicejunction(out, 1, dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dp,
+                     revsequence1, revsequenceuc1, revsequence2, revsequenceuc2, length1, length2,
+                     revoffset1, revoffset2_anchor, revoffset2_far, cdna_direction, jump_late_p,
+                     extraband_end, contlength);
+}
+
+void orc_end3_splicejunction(orc_list *out, int *dynprogindex, int *finalscore, int *nmatches,
+                             int *nmismatches, int *nopens, int *nindels, orc_dp *dp,
+                             const char *sequence1, const char *sequenceuc1, const char *sequence2,
+                             const char *sequenceuc2, int length1, int length2, int offset1,
+                             int offset2_anchor, int offset2_far, int cdna_direction,
+                             int jump_late_p, int extraband_end, double defect_rate,
+                             int contlength) {
+  (void)defect_rate;
+  end_splicejunction(out, 0, dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dp,
+                     sequence1, sequenceuc1, sequence2, sequenceuc2, length1, length2, offset1,
+                     offset2_anchor, offset2_far, cdna_direction, jump_late_p, extraband_end,
+                     contlength);
 }
 
 /* ------------------------------------------------------------- genome gap */
@@ -1585,5 +1769,51 @@ int orc_run_cgap_batch(const gsnapdp_cgap_window *w, int n, const char *query, c
   orc_list_free(&l);
   orc_dp_free(dpL);
   orc_dp_free(dpR);
+  return 0;
+}
+
+/* Batch of splice-junction end gaps (gsnapdp_sj_window), single-threaded. */
+int orc_run_sj_batch(const gsnapdp_sj_window *w, int n, const char *query, const char *query_uc,
+                     gsnapdp_result *results, gsnapdp_pair *pairs, const int64_t *pair_offsets,
+                     int32_t *npairs) {
+  orc_dp *dp = orc_dp_new(600, 10, 11, 10, 8);
+  orc_list l;
+  int i, t;
+  orc_list_init(&l, 1024);
+  for (i = 0; i < n; i++) {
+    const gsnapdp_sj_window *x = &w[i];
+    gsnapdp_result *res = &results[i];
+    int dpi = x->dynprogindex, fs = 0, nm = 0, nmm = 0, no = 0, ni = 0;
+    int64_t off = pair_offsets[i], cap = pair_offsets[i + 1] - off;
+    if (x->maxlength1 > 611 || x->maxlength2 > 2000) {
+      orc_dp_free(dp);
+      dp = orc_dp_new(x->maxlength1 > 500 ? x->maxlength1 : 500, 0, 0, x->maxlength2, 0);
+    }
+    dp->maxlength1 = x->maxlength1;
+    dp->maxlength2 = x->maxlength2;
+    if (x->kind == GSNAPDP_END5_GAP)
+      orc_end5_splicejunction(&l, &dpi, &fs, &nm, &nmm, &no, &ni, dp, query + x->qpos,
+                              query_uc + x->qpos, query + x->spos, query_uc + x->spos, x->length1,
+                              x->length2, x->offset1, x->offset2_anchor, x->offset2_far,
+                              x->cdna_direction, x->jump_late_p, x->extraband_end,
+                              (double)x->defect_rate, x->contlength);
+    else
+      orc_end3_splicejunction(&l, &dpi, &fs, &nm, &nmm, &no, &ni, dp, query + x->qpos,
+                              query_uc + x->qpos, query + x->spos, query_uc + x->spos, x->length1,
+                              x->length2, x->offset1, x->offset2_anchor, x->offset2_far,
+                              x->cdna_direction, x->jump_late_p, x->extraband_end,
+                              (double)x->defect_rate, x->contlength);
+    memset(res, 0, sizeof(*res));
+    res->finalscore = fs;
+    res->nmatches = nm;
+    res->nmismatches = nmm;
+    res->nopens = no;
+    res->nindels = ni;
+    res->reserved = dpi;
+    npairs[i] = l.n;
+    for (t = 0; t < l.n && t < cap; t++) pairs[off + t] = l.buf[l.head + t];
+  }
+  orc_list_free(&l);
+  orc_dp_free(dp);
   return 0;
 }

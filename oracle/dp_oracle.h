@@ -151,6 +151,25 @@ int orc_run_ggap_batch(const gsnapdp_ggap_window *w, int n, const char *query, c
 void orc_maxent_batch(const uint8_t *model, const uint32_t *pos, const uint32_t *chroffset,
                       double *out, int n);
 
+/* Dynprog_end5_splicejunction (dynprog.c:5412) / Dynprog_end3_splicejunction (:5869) */
+void orc_end5_splicejunction(orc_list *out, int *dynprogindex, int *finalscore, int *nmatches,
+                             int *nmismatches, int *nopens, int *nindels, orc_dp *dp,
+                             const char *revsequence1, const char *revsequenceuc1,
+                             const char *revsequence2, const char *revsequenceuc2, int length1,
+                             int length2, int revoffset1, int revoffset2_anchor,
+                             int revoffset2_far, int cdna_direction, int jump_late_p,
+                             int extraband_end, double defect_rate, int contlength);
+void orc_end3_splicejunction(orc_list *out, int *dynprogindex, int *finalscore, int *nmatches,
+                             int *nmismatches, int *nopens, int *nindels, orc_dp *dp,
+                             const char *sequence1, const char *sequenceuc1, const char *sequence2,
+                             const char *sequenceuc2, int length1, int length2, int offset1,
+                             int offset2_anchor, int offset2_far, int cdna_direction,
+                             int jump_late_p, int extraband_end, double defect_rate,
+                             int contlength);
+int orc_run_sj_batch(const gsnapdp_sj_window *w, int n, const char *query, const char *query_uc,
+                     gsnapdp_result *results, gsnapdp_pair *pairs, const int64_t *pair_offsets,
+                     int32_t *npairs);
+
 #ifdef __cplusplus
 }
 #endif

@@ -205,6 +205,24 @@ def cgap_case(name: str, gseq: np.ndarray, n: int, seed: int) -> None:
           (name, len(w), int((~keep).sum()), pairs.size))
 
 
+def sj_case(name: str, gseq: np.ndarray, n: int, seed: int) -> None:
+    b = W.sj_windows(gseq, n, seed)
+    with tempfile.TemporaryDirectory() as d:
+        b.windows.tofile(os.path.join(d, "sj_windows.bin"))
+        b.query.tofile(os.path.join(d, "query.bin"))
+        b.query_uc.tofile(os.path.join(d, "query_uc.bin"))
+        run_driver("sj", d)
+        res = np.fromfile(os.path.join(d, "results.bin"), dtype=RESULT)
+        npairs = np.fromfile(os.path.join(d, "npairs.i32"), dtype=np.int32)
+        pairs = np.fromfile(os.path.join(d, "pairs.bin"), dtype=PAIR)
+    assert pairs.size == int(npairs.sum())
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), windows=b.windows, query=b.query,
+                        query_uc=b.query_uc, finalscore=res["finalscore"], nmatches=res["nmatches"],
+                        nmismatches=res["nmismatches"], nopens=res["nopens"], nindels=res["nindels"],
+                        dynprogindex=res["reserved"], npairs=npairs, pairs=pairs)
+    print("%s: %d windows, %d pairs" % (name, len(b), pairs.size))
+
+
 def maxent_case(name: str, blocks: np.ndarray, glen: int, n: int, seed: int) -> None:
     rng = np.random.default_rng(seed)
     model = rng.integers(0, 4, size=n).astype(np.uint32)
@@ -244,6 +262,7 @@ def pdist_case() -> None:
 
 
 def main() -> None:
+    only = set(sys.argv[1:])  # optional: names of the fixtures to (re)generate
     os.makedirs(OUT, exist_ok=True)
     subprocess.check_call(["make", "-s", "-C", HERE, "ref"])
     chr17 = np.frombuffer(G.read_fasta(os.path.join(REF_TESTS, "ss.chr17test")), dtype=np.uint8).copy()
@@ -253,17 +272,23 @@ def main() -> None:
     synth = W.synthetic_genome(300_000, seed=11, n_rate=0.004)
     bsyn = G.pack(synth)
 
-    pdist_case()
-    dp_case("dp_chr17_mix", b17, W.random_windows(chr17, 2500, seed=101))
-    dp_case("dp_synth_mix", bsyn, W.random_windows(synth, 2500, seed=102, chroms=6))
-    dp_case("dp_synth_cmet", bsyn, W.random_windows(synth, 400, seed=103), mode=1)
-    dp_case("dp_chr17_c2", b17, W.c2_windows(chr17, n=300, seed=104))
-    dp_case("dp_synth_long", bsyn, W.random_windows(synth, 150, seed=105, max_len1=640,
-                                                    max_len2=700, max_band=40))
-    ggap_case("ggap_chr17", chr17, 1500, seed=201)
-    cgap_case("cgap_chr17", chr17, 1500, seed=401)
-    maxent_case("maxent_chr17", b17, chr17.size, 20000, seed=301)
-    maxent_case("maxent_synth", bsyn, synth.size, 6000, seed=302)
+    cases = [
+        ("pairdistance_highq", lambda: pdist_case()),
+        ("dp_chr17_mix", lambda: dp_case("dp_chr17_mix", b17, W.random_windows(chr17, 2500, seed=101))),
+        ("dp_synth_mix", lambda: dp_case("dp_synth_mix", bsyn, W.random_windows(synth, 2500, seed=102, chroms=6))),
+        ("dp_synth_cmet", lambda: dp_case("dp_synth_cmet", bsyn, W.random_windows(synth, 400, seed=103), mode=1)),
+        ("dp_chr17_c2", lambda: dp_case("dp_chr17_c2", b17, W.c2_windows(chr17, n=300, seed=104))),
+        ("dp_synth_long", lambda: dp_case("dp_synth_long", bsyn, W.random_windows(
+            synth, 150, seed=105, max_len1=640, max_len2=700, max_band=40))),
+        ("ggap_chr17", lambda: ggap_case("ggap_chr17", chr17, 1500, seed=201)),
+        ("cgap_chr17", lambda: cgap_case("cgap_chr17", chr17, 1500, seed=401)),
+        ("sj_chr17", lambda: sj_case("sj_chr17", chr17, 2000, seed=501)),
+        ("maxent_chr17", lambda: maxent_case("maxent_chr17", b17, chr17.size, 20000, seed=301)),
+        ("maxent_synth", lambda: maxent_case("maxent_synth", bsyn, synth.size, 6000, seed=302)),
+    ]
+    for name, fn in cases:
+        if not only or name in only:
+            fn()
 
 
 if __name__ == "__main__":

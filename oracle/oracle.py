@@ -16,7 +16,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
-from gsnapdp.records import CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_WINDOW, PAIR, RESULT, WINDOW  # noqa: E402
+from gsnapdp.records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_WINDOW, PAIR, RESULT, SJ_WINDOW,  # noqa: E402
+                             WINDOW)
 
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 TABLES_PATH = os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin")
@@ -45,6 +46,7 @@ def lib():
         L.orc_run_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, i32]
         L.orc_run_ggap_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
         L.orc_run_cgap_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.orc_run_sj_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
         L.orc_maxent_batch.argtypes = [vp, vp, vp, vp, i32]
         L.orc_pairdistance.argtypes = [i32, i32, i32]
         L.orc_pairdistance.restype = i32
@@ -133,6 +135,20 @@ def run_cgap_batch(windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray,
     pairs = np.zeros(int(off[-1]), dtype=PAIR)
     npairs = np.zeros(len(w), dtype=np.int32)
     L.orc_run_cgap_batch(_p(w), len(w), _p(q), _p(u), _p(gs), _p(go), _p(res), _p(pairs), _p(off), _p(npairs))
+    return res, pairs, off, npairs
+
+
+def run_sj_batch(windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray):
+    """Dynprog_end5/3_splicejunction over gsnapdp_sj_window records."""
+    L = lib()
+    w = np.ascontiguousarray(windows, dtype=SJ_WINDOW)
+    q = np.ascontiguousarray(query, dtype=np.uint8)
+    u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+    res = np.zeros(len(w), dtype=RESULT)
+    off = pair_offsets_for(w)
+    pairs = np.zeros(int(off[-1]), dtype=PAIR)
+    npairs = np.zeros(len(w), dtype=np.int32)
+    L.orc_run_sj_batch(_p(w), len(w), _p(q), _p(u), _p(res), _p(pairs), _p(off), _p(npairs))
     return res, pairs, off, npairs
 
 

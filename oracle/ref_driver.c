@@ -10,6 +10,7 @@
  *   ref_driver ggap   <dir>   ggap_windows.bin query.bin query_uc.bin genome.u32 -> ggap_results.bin pairs.bin npairs.i32
  *   ref_driver cgap   <dir>   cgap_windows.bin query.bin query_uc.bin gseg.bin gseg_off.i64 genome.u32
  *                             -> cgap_results.bin pairs.bin npairs.i32
+ *   ref_driver sj     <dir>   sj_windows.bin query.bin query_uc.bin -> results.bin pairs.bin npairs.i32
  *   ref_driver maxent <dir>   maxent_in.bin genome.u32 -> maxent_out.f64
  *   ref_driver pdist  <dir>   -> pdist.i32 (4 x 128 x 128 via Dynprog_pairdistance for HIGHQ only) + consistent probe
  * All inputs use the record layouts of include/gsnapdp.h.
@@ -81,7 +82,7 @@ static int flatten(List_T pairs, gsnapdp_pair *out, int cap) {
       o->cdna = pair->cdna;
       o->comp = pair->comp;
       o->genome = pair->genome;
-      o->gapp = pair->gapp ? 1 : 0;
+      o->gapp = (pair->gapp ? 1 : 0) | (pair->knowngapp ? 2 : 0);
     }
     n++;
   }
@@ -277,6 +278,60 @@ static int run_cgap(const char *dir) {
   return 0;
 }
 
+
+static int run_sj(const char *dir) {
+  size_t nw, nq, nu;
+  gsnapdp_sj_window *w = (gsnapdp_sj_window *)slurp(dir, "sj_windows.bin", &nw);
+  char *q = (char *)slurp(dir, "query.bin", &nq);
+  char *qu = (char *)slurp(dir, "query_uc.bin", &nu);
+  int n = (int)(nw / sizeof(gsnapdp_sj_window)), i;
+  gsnapdp_result *res = (gsnapdp_result *)calloc((size_t)n + 1, sizeof(gsnapdp_result));
+  int32_t *npairs = (int32_t *)calloc((size_t)n + 1, sizeof(int32_t));
+  gsnapdp_pair *tmp = (gsnapdp_pair *)malloc(sizeof(gsnapdp_pair) * PAIRCAP);
+  FILE *fp;
+  char path[4096];
+  Dynprog_T dp = Dynprog_new(600, 10, 11, 10, 8);
+  Pairpool_T pool = Pairpool_new();
+
+  snprintf(path, sizeof(path), "%s/pairs.bin", dir);
+  fp = fopen(path, "wb");
+  for (i = 0; i < n; i++) {
+    gsnapdp_sj_window *x = &w[i];
+    int dpi = x->dynprogindex, fs = -777, nm = -1, nmm = -1, no = -1, ni = -1, k;
+    List_T pairs;
+    ((int *)dp)[0] = x->maxlength1 < 611 ? x->maxlength1 : 611;
+    ((int *)dp)[1] = x->maxlength2 < 2000 ? x->maxlength2 : 2000;
+    Pairpool_reset(pool);
+    if (x->kind == GSNAPDP_END5_GAP)
+      pairs = Dynprog_end5_splicejunction(
+          &dpi, &fs, &nm, &nmm, &no, &ni, dp, q + x->qpos, qu + x->qpos, q + x->spos, qu + x->spos,
+          x->length1, x->length2, x->offset1, x->offset2_anchor, x->offset2_far, 0, 0, 0, 0,
+          x->cdna_direction, x->watsonp, x->jump_late_p, pool, x->extraband_end,
+          (double)x->defect_rate, x->contlength);
+    else
+      pairs = Dynprog_end3_splicejunction(
+          &dpi, &fs, &nm, &nmm, &no, &ni, dp, q + x->qpos, qu + x->qpos, q + x->spos, qu + x->spos,
+          x->length1, x->length2, x->offset1, x->offset2_anchor, x->offset2_far, 0, 0, 0, 0,
+          x->cdna_direction, x->watsonp, x->jump_late_p, pool, x->extraband_end,
+          (double)x->defect_rate, x->contlength);
+    ((int *)dp)[0] = 611;
+    ((int *)dp)[1] = 2000;
+    res[i].finalscore = fs;
+    res[i].nmatches = nm;
+    res[i].nmismatches = nmm;
+    res[i].nopens = no;
+    res[i].nindels = ni;
+    res[i].reserved = dpi;
+    k = flatten(pairs, tmp, PAIRCAP);
+    npairs[i] = k;
+    fwrite(tmp, sizeof(gsnapdp_pair), (size_t)(k < PAIRCAP ? k : PAIRCAP), fp);
+  }
+  fclose(fp);
+  spit(dir, "results.bin", res, sizeof(gsnapdp_result) * (size_t)n);
+  spit(dir, "npairs.i32", npairs, sizeof(int32_t) * (size_t)n);
+  return 0;
+}
+
 typedef struct maxent_in {
   uint32_t model, splice_pos, chroffset, pad;
 } maxent_in;
@@ -325,6 +380,7 @@ int main(int argc, char **argv) {
   if (!strcmp(argv[1], "ggap")) return run_ggap(argv[2]);
   if (!strcmp(argv[1], "cgap")) return run_cgap(argv[2]);
   if (!strcmp(argv[1], "maxent")) return run_maxent(argv[2]);
+  if (!strcmp(argv[1], "sj")) return run_sj(argv[2]);
   if (!strcmp(argv[1], "pdist")) return run_pdist(argv[2]);
   return 1;
 }

@@ -105,3 +105,20 @@ def test_cgap_oracle_matches_reference(golden_dir):
     for f in PAIR.names:
         assert np.array_equal(got[f], z["pairs"][f]), f
     assert res["insert_pairs"].sum() > 20 and (res["returned_null"] == 0).sum() > 1000
+
+
+def test_sj_oracle_matches_reference(golden_dir):
+    """Dynprog_end5/3_splicejunction: scores recomputed from the counts, both
+    traceback_local parts around the known gapholder, INDEL stripping."""
+    z = load(golden_dir, "sj_chr17")
+    O.setup(np.zeros(16, np.uint32))  # the genome is never read (use_genomicseg_p)
+    res, pairs, off, npairs = O.run_sj_batch(z["windows"], z["query"], z["query_uc"])
+    for f in ("finalscore", "nmatches", "nmismatches", "nopens", "nindels"):
+        bad = np.nonzero(res[f] != z[f])[0]
+        assert bad.size == 0, "%s differs at windows %s" % (f, bad[:10])
+    assert np.array_equal(res["reserved"], z["dynprogindex"])
+    assert np.array_equal(npairs, z["npairs"])
+    got = np.concatenate([pairs[off[i]:off[i] + npairs[i]] for i in range(len(npairs))])
+    for f in PAIR.names:
+        assert np.array_equal(got[f], z["pairs"][f]), f
+    assert (z["pairs"]["gapp"] == 3).sum() > 1500  # known gapholders
