@@ -67,5 +67,9 @@ struct gsnapdp_ctx {
   uint32_t* d_ggap_pool = nullptr; // global scratch of the large-window path
   size_t ggap_stage_cap = 0;
   void* d_ggap_stage = nullptr;
+  // splice-junction end gaps (gsnapdp_sj_*)
+  int sj_cap = 0;
+  int* d_sj_lists = nullptr;        // RW_NCLS class lists of sj_cap entries, then the counts
+  gsnapdp_window* d_sj_win = nullptr;  // the end-gap records k_sj_plan derives
 };
 

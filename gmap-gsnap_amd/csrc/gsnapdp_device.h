@@ -55,6 +55,12 @@ __device__ inline int gclass(const uint32_t* __restrict__ blocks, uint64_t nword
   return L.watson ? code : 3 - code;
 }
 
+// Class of a genomic-segment byte (use_genomicseg_p): A C G T N -> 0..4, else 6
+// (outside the domain: the segments of Dynprog_make_splicejunction_5/3 are ACGTN).
+__device__ inline int seg_class(unsigned char a) {
+  return a == 'A' ? 0 : a == 'C' ? 1 : a == 'G' ? 2 : a == 'T' ? 3 : a == 'N' ? 4 : 6;
+}
+
 __device__ inline int wave_max(int x) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o));

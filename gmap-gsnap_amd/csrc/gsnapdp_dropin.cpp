@@ -121,7 +121,7 @@ gsnapdp_List_T run_one(gsnapdp_window& w, const char* seq, const char* sequc, bo
   for (int i = n - 1; i >= 0; i--) {
     const gsnapdp_pair& p = g.pairs[(size_t)i];
     if (p.gapp)
-      list = Pairpool_push_gapholder(list, pool, p.queryjump, p.genomejump, /*knownp*/ 0);
+      list = Pairpool_push_gapholder(list, pool, p.queryjump, p.genomejump, (p.gapp & 2) ? 1 : 0);
     else
       list = Pairpool_push(list, pool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome,
                            p.dynprogindex);
@@ -165,6 +165,117 @@ double maxent_one(int model, unsigned splice_pos, unsigned chroffset) {
   if (gsnapdp_maxent_host(ctx(), &m, &splice_pos, &chroffset, &out, 1))
     fatal(std::string("maxent: ") + gsnapdp_last_error());
   return out;
+}
+
+// Genome_fill_buffer_blocks_noterm (genome.c:10090) on the host copy of the
+// blocks: uncompress_mmap (genome.c:8912) writes "ACGT"[2 bits], 'N' where the
+// flag bit is set.  (Host staging of the caller's splice junction, like the
+// reference's; the DP on it runs on the GPU.)
+void fill_buffer(unsigned left, unsigned length, char* out) {
+  if (!g.blocks) fatal("no genome: call Gsnapdp_dropin_genome before Dynprog_make_splicejunction_*");
+  for (unsigned i = 0; i < length; i++) {
+    const unsigned pos = left + i;
+    const size_t ptr = (size_t)(pos >> 5) * 3;
+    if (ptr + 2 >= g.nwords) fatal("junction outside the genome");
+    const unsigned bit = pos & 31u;
+    if ((g.blocks[ptr + 2] >> bit) & 1u) {
+      out[i] = 'N';
+    } else {
+      const unsigned word = bit < 16 ? g.blocks[ptr + 1] : g.blocks[ptr];
+      out[i] = "ACGT"[(word >> ((bit & 15u) * 2u)) & 3u];
+    }
+  }
+}
+
+// make_complement_inplace (dynprog.c:1392-1406): reverse complement with
+// complCode = COMPLEMENT_LC (complement.h:31)
+void revcomp_inplace(char* s, int length) {
+  static const char* lc =
+      "???????????????????????????????? ??#$%&')(*+,-./0123456789:;>=<??TVGHEFCDIJMLKNOPQYSAABWXRZ]?"
+      "[^_`tvghefcdijmlknopqysaabwxrz}|{~?";
+  auto cc = [&](char c) { return lc[(unsigned char)c & 127u]; };
+  if (length <= 0) return;
+  int i = 0, j = length - 1;
+  for (; i < length / 2; i++, j--) {
+    const char t = cc(s[i]);
+    s[i] = cc(s[j]);
+    s[j] = t;
+  }
+  if (i == j) s[i] = cc(s[i]);
+}
+
+enum { DONOR = 0, ANTIDONOR = 1, ACCEPTOR = 2, ANTIACCEPTOR = 3 };  // splicetrie_build.h:4
+
+// Dynprog_end5/3_splicejunction as a batch of one (gsnapdp_sj_*).
+gsnapdp_List_T run_sj(int kind, const char* seq1, const char* seq1uc, const char* seq2,
+                      const char* seq2uc, int length1, int length2, int offset1, int anchor,
+                      int far, int contlength, int cdna_direction, int watsonp, int jump_late_p,
+                      int extraband_end, double defect_rate, const Dynprog* dp,
+                      gsnapdp_Pairpool_T pool, int* dynprogindex, int* finalscore, int* nmatches,
+                      int* nmismatches, int* nopens, int* nindels) {
+  std::lock_guard<std::mutex> lock(g.mu);
+  gsnapdp_ctx* c = ctx();
+  const bool rev = kind == GSNAPDP_END5_GAP;
+  const int L1 = length1 > 0 ? length1 : 0, L2 = length2 > 0 ? length2 : 0;
+  gsnapdp_sj_window w;
+  memset(&w, 0, sizeof(w));
+  w.kind = kind;
+  w.length1 = length1;
+  w.length2 = length2;
+  w.offset1 = offset1;
+  w.offset2_anchor = anchor;
+  w.offset2_far = far;
+  w.contlength = contlength;
+  w.cdna_direction = cdna_direction;
+  w.extraband_end = extraband_end;
+  w.dynprogindex = *dynprogindex;
+  w.maxlength1 = dp->maxlength1;
+  w.maxlength2 = dp->maxlength2;
+  w.defect_rate = defect_rate < 0.003 ? 0.001f : (defect_rate < 0.014 ? 0.01f : 0.5f);
+  w.watsonp = watsonp ? 1 : 0;
+  w.jump_late_p = jump_late_p ? 1 : 0;
+  // query rows then the junction, each with 4 bytes of slack
+  const bool run = L1 > 0 && L2 > 0 && L1 <= dp->maxlength1 && L2 <= dp->maxlength2;
+  const size_t sbase = (size_t)L1 + 4;
+  g.q.assign(sbase + L2 + 8, 0);
+  g.qu.assign(sbase + L2 + 8, 0);
+  if (run) {
+    memcpy(g.q.data(), rev ? seq1 - (L1 - 1) : seq1, (size_t)L1);
+    memcpy(g.qu.data(), rev ? seq1uc - (L1 - 1) : seq1uc, (size_t)L1);
+    memcpy(g.q.data() + sbase, rev ? seq2 - (L2 - 1) : seq2, (size_t)L2);
+    memcpy(g.qu.data() + sbase, rev ? seq2uc - (L2 - 1) : seq2uc, (size_t)L2);
+  }
+  w.qpos = rev ? (uint32_t)(L1 > 0 ? L1 - 1 : 0) : 0u;
+  w.spos = (uint32_t)(rev ? sbase + (L2 > 0 ? L2 - 1 : 0) : sbase);
+  const int64_t cap = (int64_t)L1 + L2 + 2;
+  const int64_t off[2] = {0, cap};
+  g.ops.assign((size_t)cap + 1, 0u);
+  gsnapdp_result r;
+  if (gsnapdp_sj_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, g.ops.data(), off))
+    fatal(std::string("gsnapdp_sj_run_host: ") + gsnapdp_last_error());
+  if (r.status == gsnapdp::ST_UNSUPPORTED) fatal("splice junction outside A C G T N");
+  if (r.status == gsnapdp::ST_OPS_OVERFLOW) fatal("op stream overflow");
+  *nmatches = r.nmatches;
+  *nmismatches = r.nmismatches;
+  *nopens = r.nopens;
+  *nindels = r.nindels;
+  *finalscore = r.finalscore;
+  *dynprogindex = r.reserved;
+  if (r.status == gsnapdp::ST_EARLY) return nullptr;
+  g.pairs.resize((size_t)cap + 8);
+  const int n = gsnapdp_sj_expand(c, &w, &r, g.ops.data(), g.q.data(), g.qu.data(), g.pairs.data(),
+                                  (int)g.pairs.size());
+  if (n < 0 || n > (int)g.pairs.size()) fatal("gsnapdp_sj_expand failed");
+  gsnapdp_List_T list = nullptr;
+  for (int i = n - 1; i >= 0; i--) {
+    const gsnapdp_pair& p = g.pairs[(size_t)i];
+    if (p.gapp)
+      list = Pairpool_push_gapholder(list, pool, p.queryjump, p.genomejump, (p.gapp & 2) ? 1 : 0);
+    else
+      list = Pairpool_push(list, pool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome,
+                           p.dynprogindex);
+  }
+  return list;
 }
 
 }  // namespace
@@ -495,6 +606,67 @@ gsnapdp_List_T Dynprog_cdna_gap(
                            p.dynprogindex);
   }
   return list;
+}
+
+gsnapdp_List_T Dynprog_end5_splicejunction(
+    int* dynprogindex, int* finalscore, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* revsequence1, char* revsequenceuc1,
+    char* revsequence2, char* revsequenceuc2, int length1, int length2, int revoffset1,
+    int revoffset2_anchor, int revoffset2_far, gsnapdp_Genomicpos_T, gsnapdp_Genomicpos_T,
+    gsnapdp_Genomicpos_T, gsnapdp_Genomicpos_T, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_end,
+    double defect_rate, int contlength) {
+  return run_sj(GSNAPDP_END5_GAP, revsequence1, revsequenceuc1, revsequence2, revsequenceuc2,
+                length1, length2, revoffset1, revoffset2_anchor, revoffset2_far, contlength,
+                cdna_direction, watsonp, jump_late_p, extraband_end, defect_rate,
+                (const Dynprog*)dynprog, pairpool, dynprogindex, finalscore, nmatches,
+                nmismatches, nopens, nindels);
+}
+
+gsnapdp_List_T Dynprog_end3_splicejunction(
+    int* dynprogindex, int* finalscore, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* sequence1, char* sequenceuc1,
+    char* sequence2, char* sequenceuc2, int length1, int length2, int offset1,
+    int offset2_anchor, int offset2_far, gsnapdp_Genomicpos_T, gsnapdp_Genomicpos_T,
+    gsnapdp_Genomicpos_T, gsnapdp_Genomicpos_T, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_end,
+    double defect_rate, int contlength) {
+  return run_sj(GSNAPDP_END3_GAP, sequence1, sequenceuc1, sequence2, sequenceuc2, length1,
+                length2, offset1, offset2_anchor, offset2_far, contlength, cdna_direction,
+                watsonp, jump_late_p, extraband_end, defect_rate, (const Dynprog*)dynprog,
+                pairpool, dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels);
+}
+
+void Dynprog_make_splicejunction_5(char* splicejunction, gsnapdp_Genomicpos_T splicecoord,
+                                   int splicelength, int /*contlength*/,
+                                   gsnapdp_Splicetype_T far_splicetype, gsnapdp_bool watsonp) {
+  // dynprog.c:6061-6100: the distal part at splicejunction[0]
+  char* distal = splicejunction;
+  if (far_splicetype == ACCEPTOR || far_splicetype == ANTIDONOR) {
+    if (splicelength > 0) fill_buffer(splicecoord, (unsigned)splicelength, distal);
+  } else if (far_splicetype == ANTIACCEPTOR || far_splicetype == DONOR) {
+    if (splicelength > 0) fill_buffer(splicecoord - (unsigned)splicelength, (unsigned)splicelength, distal);
+  } else {
+    fprintf(stderr, "Unexpected far_splicetype value %d\n", far_splicetype);
+    abort();
+  }
+  if (!watsonp) revcomp_inplace(distal, splicelength);
+}
+
+void Dynprog_make_splicejunction_3(char* splicejunction, gsnapdp_Genomicpos_T splicecoord,
+                                   int splicelength, int contlength,
+                                   gsnapdp_Splicetype_T far_splicetype, gsnapdp_bool watsonp) {
+  // dynprog.c:6149-6188: the distal part after the contlength proximal bases
+  char* distal = &splicejunction[contlength];
+  if (far_splicetype == DONOR || far_splicetype == ANTIACCEPTOR) {
+    if (splicelength > 0) fill_buffer(splicecoord - (unsigned)splicelength, (unsigned)splicelength, distal);
+  } else if (far_splicetype == ANTIDONOR || far_splicetype == ACCEPTOR) {
+    if (splicelength > 0) fill_buffer(splicecoord, (unsigned)splicelength, distal);
+  } else {
+    fprintf(stderr, "Unexpected far_splicetype value %d\n", far_splicetype);
+    abort();
+  }
+  if (!watsonp) revcomp_inplace(distal, splicelength);
 }
 
 void Maxent_hr_setup(unsigned int* ref_blocks) {  // maxent_hr.c:27195

@@ -659,13 +659,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
 // (dynprog.c:2235-2290) or find_best_endpoint_to_queryend_indels (:2293-2355)
 // for end gaps, as a row-parallel scan with an ordered argmax -- and the
 // traceback (:2611-2712) by the group leader.
-template <int RL, bool GMEM>
+//
+// SEG: the splice-junction end gaps (Dynprog_end5/3_splicejunction,
+// :5412-5553 / :5869-6057).  Wn then holds the end-gap records k_sj_plan
+// derived (endalign QUERYEND_INDELS), the genome of column c is the caller's
+// segment byte at sjw[wi].spos (use_genomicseg_p, :1535 / :1690), and the
+// final score is recomputed from the counts (:5541 / :6045).
+template <int RL, bool GMEM, bool SEG>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8))) void k_rows(
     const gsnapdp_window* __restrict__ Wn, const int* __restrict__ list,
     const int* __restrict__ count, const char* __restrict__ q, const char* __restrict__ qu,
     const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
     uint32_t* __restrict__ pool, size_t stride, gsnapdp_result* __restrict__ res,
-    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
+    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off,
+    const gsnapdp_sj_window* __restrict__ sjw) {
   extern __shared__ uint32_t smem[];
   using P = typename std::conditional<GMEM, AS_GLOBAL uint32_t*, AS_LDS uint32_t*>::type;
   using PB = typename std::conditional<GMEM, AS_GLOBAL uint8_t*, AS_LDS uint8_t*>::type;
@@ -694,8 +701,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
     const PH qb = (PH)(region + L1 * W + (L2 + 2 + 3) / 4);
     const P bnd = region + L1 * W + (L2 + 2 + 3) / 4 + (L1 + 1) / 2;
     if (act) {
-      for (int c = rho; c <= L2 + 1; c += RL)
-        cls[c] = (uint8_t)((c >= 1 && c <= L2) ? gclass(blocks, nwords, L, L.g0 + L.gstep * (c - 1)) : 5);
+      if constexpr (SEG) {
+        const int sp = (int)sjw[wi].spos;
+        for (int c = rho; c <= L2 + 1; c += RL)
+          cls[c] = (uint8_t)((c >= 1 && c <= L2) ? seg_class((unsigned char)q[sp + L.gstep * (c - 1)]) : 5);
+      } else {
+        for (int c = rho; c <= L2 + 1; c += RL)
+          cls[c] = (uint8_t)((c >= 1 && c <= L2) ? gclass(blocks, nwords, L, L.g0 + L.gstep * (c - 1)) : 5);
+      }
       for (int i = rho; i < L1; i += RL) {
         const int qi = L.qbase + L.qstep * i;
         qb[i] = (uint16_t)((unsigned char)q[qi] | ((unsigned)(unsigned char)qu[qi] << 8));
@@ -763,8 +776,75 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
       traceback(CellDirs<P>{H, W, d.lband}, L, br, bc,
                 [&](int r) -> uint32_t { return qb[r - 1]; }, [&](int c) -> int { return cls[c]; },
                 prof, t, ow);
+      if constexpr (SEG)
+        score = t.nmatches * 3 - 5 * t.nmismatches + t.nopens * d.open + t.nindels * d.ext;
       write_result(&res[wi], w, L, score, br, bc, t, ow);
     }
+  }
+}
+
+// Dynprog_end5/3_splicejunction windows -> the end-gap records k_rows runs
+// (QUERYEND_INDELS: find_best_endpoint_to_queryend_indels, ENDQ, END
+// open/extend, the reversed fill's !jump_late_p), early returns (:5446-5461)
+// and the row-lane class of each window.  Segments outside A C G T N (never
+// produced by Dynprog_make_splicejunction_5/3) are marked unsupported.
+__global__ void k_sj_plan(const gsnapdp_sj_window* __restrict__ S, int n,
+                          const char* __restrict__ q, const char* __restrict__ qu,
+                          gsnapdp_window* __restrict__ Wn, gsnapdp_result* __restrict__ res,
+                          int* __restrict__ lists, int* __restrict__ counts, int cap) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int cls = -1;
+  if (i < n) {
+    const gsnapdp_sj_window s = S[i];
+    gsnapdp_window w;
+    memset(&w, 0, sizeof(w));
+    w.kind = s.kind == GSNAPDP_END5_GAP ? GSNAPDP_END5_GAP : GSNAPDP_END3_GAP;
+    w.length1 = s.length1;
+    w.length2 = s.length2;
+    w.offset1 = s.offset1;
+    w.offset2 = s.offset2_anchor;
+    w.qpos = s.qpos;
+    w.cdna_direction = s.cdna_direction;
+    w.extraband = s.extraband_end;
+    w.dynprogindex = s.dynprogindex;
+    w.maxlength1 = s.maxlength1;
+    w.maxlength2 = s.maxlength2;
+    w.defect_rate = s.defect_rate;
+    w.watsonp = s.watsonp;
+    w.jump_late_p = s.jump_late_p;
+    w.widebandp = 1;
+    w.endalign = GSNAPDP_QUERYEND_INDELS;
+    Wn[i] = w;
+    int status = ST_OK;
+    if (s.length1 <= 0 || s.length1 > s.maxlength1 || s.length2 <= 0 || s.length2 > s.maxlength2) {
+      status = ST_EARLY;  // NULL, finalscore 0, counts 0, *dynprogindex untouched
+    } else if (s.kind != GSNAPDP_END5_GAP && s.kind != GSNAPDP_END3_GAP) {
+      status = ST_UNSUPPORTED;
+    } else {
+      const Derived d = derive(w);
+      const int step = s.kind == GSNAPDP_END5_GAP ? -1 : 1;
+      if (d.status != ST_OK) status = ST_UNSUPPORTED;
+      for (int k = 0; k < s.length2 && status == ST_OK; k++) {
+        const unsigned char a = (unsigned char)q[(int)s.spos + step * k];
+        if (seg_class(a) > 4 || (unsigned char)qu[(int)s.spos + step * k] != a) status = ST_UNSUPPORTED;
+      }
+      if (status == ST_OK) {
+        cls = rows_class(d.L1, d.L2, d.W);
+        if (cls < 0) status = ST_UNSUPPORTED;
+      }
+    }
+    if (status != ST_OK) {
+      gsnapdp_result R = {};
+      R.status = status;
+      R.length1 = s.length1;
+      R.length2 = s.length2;
+      R.reserved = s.dynprogindex;
+      res[i] = R;
+    }
+  }
+  for (int c = 0; c < RW_NCLS; c++) {
+    const int slot = agg_atomic_inc(counts + c, cls == c ? 0 : -1);
+    if (cls == c) lists[(size_t)c * cap + slot] = i;
   }
 }
 
@@ -1169,19 +1249,114 @@ int gsnapdp__rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window*
                          const int64_t* d_op_offsets) {
   const uint64_t nw = (uint64_t)ctx->nwords;
   constexpr int small_blocks = 160 * 1024 / (8 * RW_SMALL_WORDS * 4);
-  hipLaunchKernelGGL((k_rows<32, false>), dim3(ctx->num_cus * small_blocks), dim3(256),
+  hipLaunchKernelGGL((k_rows<32, false, false>), dim3(ctx->num_cus * small_blocks), dim3(256),
                      (size_t)8 * RW_SMALL_WORDS * 4, st, d_windows, lists, counts + RW_SMALL,
                      d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, (uint32_t*)nullptr,
-                     (size_t)RW_SMALL_WORDS, d_results, d_ops, d_op_offsets);
-  hipLaunchKernelGGL((k_rows<64, false>), dim3(ctx->num_cus * 2), dim3(256),
+                     (size_t)RW_SMALL_WORDS, d_results, d_ops, d_op_offsets,
+                     (const gsnapdp_sj_window*)nullptr);
+  hipLaunchKernelGGL((k_rows<64, false, false>), dim3(ctx->num_cus * 2), dim3(256),
                      (size_t)4 * RW_MID_WORDS * 4, st, d_windows, lists + (size_t)RW_MID * list_cap,
                      counts + RW_MID, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
-                     (uint32_t*)nullptr, (size_t)RW_MID_WORDS, d_results, d_ops, d_op_offsets);
-  hipLaunchKernelGGL((k_rows<64, true>), dim3(RW_BIG_WAVES), dim3(64), 0, st, d_windows,
+                     (uint32_t*)nullptr, (size_t)RW_MID_WORDS, d_results, d_ops, d_op_offsets,
+                     (const gsnapdp_sj_window*)nullptr);
+  hipLaunchKernelGGL((k_rows<64, true, false>), dim3(RW_BIG_WAVES), dim3(64), 0, st, d_windows,
                      lists + (size_t)RW_BIG * list_cap, counts + RW_BIG, d_query, d_query_uc,
                      ctx->d_blocks, nw, ctx->d_prof, ctx->d_bigpool, RW_BIG_WORDS, d_results,
-                     d_ops, d_op_offsets);
+                     d_ops, d_op_offsets, (const gsnapdp_sj_window*)nullptr);
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// ======================================================================
+// Host side (include/gsnapdp.h: gsnapdp_sj_*)
+// ======================================================================
+extern "C" int gsnapdp_sj_run_device(gsnapdp_ctx* ctx, const gsnapdp_sj_window* d_windows, int n,
+                                     const char* d_query, const char* d_query_uc,
+                                     gsnapdp_result* d_results, uint32_t* d_ops,
+                                     const int64_t* d_op_offsets, void* stream_v) {
+  if (!ctx) return -1;
+  if (n <= 0) return 0;
+  hipStream_t st = stream_v ? (hipStream_t)stream_v : ctx->stream;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  if (n > ctx->sj_cap) {
+    const int cap = n + n / 4 + 1024;
+    (void)hipFree(ctx->d_sj_lists);
+    (void)hipFree(ctx->d_sj_win);
+    ctx->d_sj_lists = nullptr;
+    ctx->d_sj_win = nullptr;
+    HIPCHK(hipMalloc(&ctx->d_sj_lists, (size_t)RW_NCLS * cap * 4 + 64));
+    HIPCHK(hipMalloc(&ctx->d_sj_win, (size_t)cap * sizeof(gsnapdp_window)));
+    ctx->sj_cap = cap;
+  }
+  if (!ctx->d_bigpool)
+    HIPCHK(hipMalloc(&ctx->d_bigpool, (size_t)RW_BIG_WAVES * RW_BIG_WORDS * 4));
+  const int cap = ctx->sj_cap;
+  int* lists = ctx->d_sj_lists;
+  int* counts = lists + (size_t)RW_NCLS * cap;
+  gsnapdp_window* dw = ctx->d_sj_win;
+  const uint64_t nw = (uint64_t)ctx->nwords;
+  HIPCHK(hipMemsetAsync(counts, 0, 4 * RW_NCLS, st));
+  hipLaunchKernelGGL(k_sj_plan, dim3((n + 255) / 256), dim3(256), 0, st, d_windows, n, d_query,
+                     d_query_uc, dw, d_results, lists, counts, cap);
+  constexpr int small_blocks = 160 * 1024 / (8 * RW_SMALL_WORDS * 4);
+  hipLaunchKernelGGL((k_rows<32, false, true>), dim3(ctx->num_cus * small_blocks), dim3(256),
+                     (size_t)8 * RW_SMALL_WORDS * 4, st, dw, lists, counts + RW_SMALL, d_query,
+                     d_query_uc, ctx->d_blocks, nw, ctx->d_prof, (uint32_t*)nullptr,
+                     (size_t)RW_SMALL_WORDS, d_results, d_ops, d_op_offsets, d_windows);
+  hipLaunchKernelGGL((k_rows<64, false, true>), dim3(ctx->num_cus * 2), dim3(256),
+                     (size_t)4 * RW_MID_WORDS * 4, st, dw, lists + (size_t)RW_MID * cap,
+                     counts + RW_MID, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
+                     (uint32_t*)nullptr, (size_t)RW_MID_WORDS, d_results, d_ops, d_op_offsets,
+                     d_windows);
+  hipLaunchKernelGGL((k_rows<64, true, true>), dim3(RW_BIG_WAVES), dim3(64), 0, st, dw,
+                     lists + (size_t)RW_BIG * cap, counts + RW_BIG, d_query, d_query_uc,
+                     ctx->d_blocks, nw, ctx->d_prof, ctx->d_bigpool, RW_BIG_WORDS, d_results,
+                     d_ops, d_op_offsets, d_windows);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int gsnapdp_sj_run_host(gsnapdp_ctx* ctx, const gsnapdp_sj_window* windows, int n,
+                                   const char* query, const char* query_uc, size_t query_bytes,
+                                   gsnapdp_result* results, uint32_t* ops,
+                                   const int64_t* op_offsets) {
+  if (!ctx) return -1;
+  if (n <= 0) return 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t nops = (size_t)op_offsets[n];
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t szw = al((size_t)n * sizeof(gsnapdp_sj_window));
+  const size_t szq = al(query_bytes + 4);
+  const size_t szr = al((size_t)n * sizeof(gsnapdp_result));
+  const size_t szo = al((nops + 1) * 4);
+  const size_t szoff = al((size_t)(n + 1) * 8);
+  const size_t total = szw + 2 * szq + szr + szo + szoff;
+  {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (total > ctx->ggap_stage_cap) {
+      (void)hipFree(ctx->d_ggap_stage);
+      ctx->d_ggap_stage = nullptr;
+      HIPCHK(hipMalloc(&ctx->d_ggap_stage, total));
+      ctx->ggap_stage_cap = total;
+    }
+  }
+  char* b = (char*)ctx->d_ggap_stage;
+  gsnapdp_sj_window* dw = (gsnapdp_sj_window*)b;
+  char* dq = b + szw;
+  char* du = dq + szq;
+  gsnapdp_result* dr = (gsnapdp_result*)(du + szq);
+  uint32_t* dops = (uint32_t*)((char*)dr + szr);
+  int64_t* doff = (int64_t*)((char*)dops + szo);
+  hipStream_t st = ctx->stream;
+  HIPCHK(hipMemcpyAsync(dw, windows, (size_t)n * sizeof(gsnapdp_sj_window), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(dq, query, query_bytes, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(doff, op_offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, st));
+  if (gsnapdp_sj_run_device(ctx, dw, n, dq, du, dr, dops, doff, st)) return -1;
+  HIPCHK(hipMemcpyAsync(results, dr, (size_t)n * sizeof(gsnapdp_result), hipMemcpyDeviceToHost, st));
+  if (nops) HIPCHK(hipMemcpyAsync(ops, dops, nops * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
   return 0;
 }
 

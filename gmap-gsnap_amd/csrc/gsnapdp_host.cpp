@@ -251,6 +251,147 @@ extern "C" int gsnapdp_expand(gsnapdp_ctx* ctx, const gsnapdp_window* w, const g
   return n;
 }
 
+// traceback_local's pushes (dynprog.c:2874-2968) for the splice-junction end
+// gaps: the op stream of the whole traceback is cut at the first loop top
+// whose column is <= endc (part one runs while c > contlength), where the
+// known gapholder goes (:5517 / :6021); part one's coordinates use goff_far,
+// part two's goff_anchor.  Genome chars come from the segment `g` (indexed
+// like q: g[c-1] forwards, g[1-c] reversed), with no '*' test.
+static void replay_local(const uint32_t* ops, int nops, int r, int c, int endc, const char* q,
+                         const char* qu, const char* g, int qoff, int goff_far, int goff_anchor,
+                         int jump, bool rev, const uint32_t* prof, int dpi,
+                         std::vector<gsnapdp_pair>& p) {
+  auto push = [&](int qpos, int gpos, char cdna, char comp, char gc) {
+    gsnapdp_pair x;
+    memset(&x, 0, sizeof(x));
+    x.querypos = qpos;
+    x.genomepos = gpos;
+    x.dynprogindex = dpi;
+    x.cdna = cdna;
+    x.comp = comp;
+    x.genome = gc;
+    p.push_back(x);
+  };
+  bool second = false;
+  int goff = goff_far;
+  auto cut = [&]() {  // Pairpool_push_gapholder(queryjump 0, genomejump, knownp true)
+    gsnapdp_pair x;
+    memset(&x, 0, sizeof(x));
+    x.querypos = -1;
+    x.genomepos = -1;
+    x.queryjump = 0;
+    x.genomejump = jump;
+    x.cdna = ' ';
+    x.comp = ' ';
+    x.genome = ' ';
+    x.gapp = 3;
+    p.push_back(x);
+    second = true;
+    goff = goff_anchor;
+  };
+  auto consistent = [&](unsigned char c1, char gch) -> bool {
+    const int gi = gch == 'A' ? 0 : gch == 'C' ? 1 : gch == 'G' ? 2 : gch == 'T' ? 3 : 4;
+    return (prof[c1 & 127] >> (24 + gi)) & 1u;
+  };
+  for (int k = 0; k < nops; k++) {
+    const uint32_t op = ops[k];
+    const int cnt = (int)GSNAPDP_OP_COUNT(op);
+    switch (GSNAPDP_OP_TYPE(op)) {
+      case GSNAPDP_OP_DIAG:
+        for (int j = 0; j < cnt; j++, r--, c--) {
+          if (!second && c <= endc) cut();
+          int qc = r - 1, gc = c - 1;
+          if (rev) {
+            qc = -qc;
+            gc = -gc;
+          }
+          const char c1 = q[qc];
+          const char c2 = g[gc];
+          char comp;
+          if (qu[qc] == c2) comp = GSNAPDP_DYNPROG_MATCH_COMP;
+          else if (consistent((unsigned char)c1, c2)) comp = GSNAPDP_AMBIGUOUS_COMP;
+          else comp = GSNAPDP_MISMATCH_COMP;
+          push(qoff + qc, goff + gc, c1, comp, c2);
+        }
+        break;
+      case GSNAPDP_OP_HDASH: {
+        int qc = r - 1, left = c - cnt, right = c - 1, step;
+        if (rev) {
+          const int t = left;
+          qc = -qc;
+          left = -right;
+          right = -t;
+          step = +1;
+        } else {
+          qc++;
+          step = -1;
+        }
+        int gc = rev ? left : right;
+        for (int j = 0; j < cnt; j++, gc += step) push(qoff + qc, goff + gc, ' ', '-', g[gc]);
+        c -= cnt;
+        break;
+      }
+      case GSNAPDP_OP_HGAP: {
+        gsnapdp_pair x;
+        memset(&x, 0, sizeof(x));
+        x.querypos = -1;
+        x.genomepos = -1;
+        x.queryjump = GSNAPDP_UNKNOWNJUMP;
+        x.genomejump = GSNAPDP_UNKNOWNJUMP;
+        x.cdna = ' ';
+        x.comp = ' ';
+        x.genome = ' ';
+        x.gapp = 1;
+        p.push_back(x);
+        c -= cnt;
+        break;
+      }
+      default: {
+        int qc = r - 1, gc = c - 1, step;
+        if (rev) {
+          qc = -qc;
+          gc = -gc;
+          step = +1;
+        } else {
+          gc++;
+          step = -1;
+        }
+        for (int j = 0; j < cnt; j++, qc += step) push(qoff + qc, goff + gc, q[qc], '-', ' ');
+        r -= cnt;
+        break;
+      }
+    }
+  }
+  if (!second) cut();
+}
+
+// Dynprog_end5/3_splicejunction's list (dynprog.c:5543-5553 / :6047-6057)
+extern "C" int gsnapdp_sj_expand(gsnapdp_ctx* ctx, const gsnapdp_sj_window* w,
+                                 const gsnapdp_result* res, const uint32_t* ops, const char* query,
+                                 const char* query_uc, gsnapdp_pair* pairs, int cap) {
+  if (!ctx || !w || !res) return -1;
+  if (res->status == ST_EARLY || res->status == ST_UNSUPPORTED) return 0;
+  if (res->status == ST_OPS_OVERFLOW) return -1;
+  const bool rev = w->kind == GSNAPDP_END5_GAP;
+  const int jump = rev ? w->offset2_anchor - w->offset2_far : w->offset2_far - w->offset2_anchor;
+  std::vector<gsnapdp_pair> p;
+  p.reserve(256);
+  replay_local(ops, res->nops, res->bestr, res->bestc, w->contlength, query + w->qpos,
+               query_uc + w->qpos, query + w->spos, w->offset1, w->offset2_far,
+               w->offset2_anchor, jump, rev, gsnapdp__host_prof(ctx), w->dynprogindex, p);
+  const int m = (int)p.size();
+  int j = 0, n = 0;
+  while (j < m && p[j].comp == '-') j++;
+  if (!rev) {
+    for (int i = j; i < m; i++, n++)
+      if (n < cap) pairs[n] = p[i];
+  } else {
+    for (int i = m - 1; i >= j; i--, n++)
+      if (n < cap) pairs[n] = p[i];
+  }
+  return n;
+}
+
 // Dynprog_genome_gap's list (dynprog.c:5000-5058): traceback of the right flank
 // (reversed), List_reverse, the gapholder, traceback of the left flank, then
 // List_reverse of the whole -- i.e. the right flank's pairs last-pushed first,

@@ -883,6 +883,8 @@ extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   (void)hipFree(ctx->d_ggap_counts);
   (void)hipFree(ctx->d_ggap_pool);
   (void)hipFree(ctx->d_ggap_stage);
+  (void)hipFree(ctx->d_sj_lists);
+  (void)hipFree(ctx->d_sj_win);
   (void)hipFree(ctx->d_stage);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

@@ -19,7 +19,7 @@ import os
 import numpy as np
 
 from .records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW,  # noqa: F401
-                      MAXENT_IN, PAIR, RESULT, WINDOW)
+                      MAXENT_IN, PAIR, RESULT, SJ_WINDOW, WINDOW)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
@@ -81,6 +81,12 @@ def lib():
         L.gsnapdp_cgap_run_device.restype = i32
         L.gsnapdp_cgap_expand.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i32]
         L.gsnapdp_cgap_expand.restype = i32
+        L.gsnapdp_sj_run_host.argtypes = [vp, vp, i32, vp, vp, sz, vp, vp, vp]
+        L.gsnapdp_sj_run_host.restype = i32
+        L.gsnapdp_sj_run_device.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp]
+        L.gsnapdp_sj_run_device.restype = i32
+        L.gsnapdp_sj_expand.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32]
+        L.gsnapdp_sj_expand.restype = i32
         _lib = L
     return _lib
 
@@ -258,6 +264,37 @@ class Context:
                                           _p(q), _p(u), s2, _p(out), out.size)
             if n < 0:
                 raise GsnapdpError("gsnapdp_cgap_expand failed for window %d" % i)
+            outs.append(out[:n])
+            counts[i] = n
+        return (np.concatenate(outs) if outs else np.zeros(0, PAIR)), counts
+
+    def sj_run(self, windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray):
+        """Dynprog_end5/3_splicejunction on the GPU.  Returns (results, ops, op_offsets)."""
+        w = np.ascontiguousarray(windows, dtype=SJ_WINDOW)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        off = op_offsets(w)
+        res = np.zeros(len(w), dtype=RESULT)
+        ops = np.zeros(max(1, int(off[-1])), dtype=np.uint32)
+        rc = lib().gsnapdp_sj_run_host(self.h, _p(w), len(w), _p(q), _p(u), q.size, _p(res), _p(ops), _p(off))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_sj_run_host: %s" % lib().gsnapdp_last_error().decode())
+        return res, ops, off
+
+    def sj_all_pairs(self, windows, query, query_uc, results, ops, off):
+        """The lists Dynprog_end5/3_splicejunction return, concatenated, and their lengths."""
+        w = np.ascontiguousarray(windows, dtype=SJ_WINDOW)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        res = np.ascontiguousarray(results, dtype=RESULT)
+        outs, counts = [], np.zeros(len(w), dtype=np.int32)
+        for i in range(len(w)):
+            cap = int(w["length1"][i]) + int(w["length2"][i]) + 8
+            out = np.zeros(max(cap, 1), dtype=PAIR)
+            n = lib().gsnapdp_sj_expand(self.h, _p(w[i:i + 1]), _p(res[i:i + 1]), _p(ops[off[i]:]),
+                                        _p(q), _p(u), _p(out), out.size)
+            if n < 0:
+                raise GsnapdpError("gsnapdp_sj_expand failed for window %d" % i)
             outs.append(out[:n])
             counts[i] = n
         return (np.concatenate(outs) if outs else np.zeros(0, PAIR)), counts

@@ -120,6 +120,34 @@ gsnapdp_List_T Dynprog_end3_gap(
     double defect_rate, gsnapdp_Endalign_T endalign,
     gsnapdp_bool use_genomicseg_p);                                     /* dynprog.c:5556 */
 
+/* --- splice-junction end gaps and their junction builders (dynprog.h:120-173) --- */
+gsnapdp_List_T Dynprog_end5_splicejunction(
+    int* dynprogindex, int* finalscore, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* revsequence1, char* revsequenceuc1,
+    char* revsequence2, char* revsequenceuc2, int length1, int length2, int revoffset1,
+    int revoffset2_anchor, int revoffset2_far, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_end,
+    double defect_rate, int contlength);                                /* dynprog.c:5412 */
+gsnapdp_List_T Dynprog_end3_splicejunction(
+    int* dynprogindex, int* finalscore, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* sequence1, char* sequenceuc1,
+    char* sequence2, char* sequenceuc2, int length1, int length2, int offset1,
+    int offset2_anchor, int offset2_far, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_end,
+    double defect_rate, int contlength);                                /* dynprog.c:5869 */
+void Dynprog_make_splicejunction_5(char* splicejunction, gsnapdp_Genomicpos_T splicecoord,
+                                   int splicelength, int contlength,
+                                   gsnapdp_Splicetype_T far_splicetype,
+                                   gsnapdp_bool watsonp);               /* dynprog.c:6061 */
+void Dynprog_make_splicejunction_3(char* splicejunction, gsnapdp_Genomicpos_T splicecoord,
+                                   int splicelength, int contlength,
+                                   gsnapdp_Splicetype_T far_splicetype,
+                                   gsnapdp_bool watsonp);               /* dynprog.c:6149 */
+
 /* --- MaxEnt splice-site probabilities (maxent_hr.h:6-19) --- */
 void Maxent_hr_setup(unsigned int* ref_blocks);                                 /* maxent_hr.c:27195 */
 double Maxent_hr_donor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomicpos_T chroffset);

@@ -223,6 +223,28 @@ def sj_case(name: str, gseq: np.ndarray, n: int, seed: int) -> None:
     print("%s: %d windows, %d pairs" % (name, len(b), pairs.size))
 
 
+def mksj_case(name: str, gseq: np.ndarray, n: int, seed: int) -> None:
+    """Dynprog_make_splicejunction_5/3 at random coordinates, every splice type, both strands."""
+    rng = np.random.default_rng(seed)
+    blocks = G.pack(gseq)
+    rec = np.zeros(n, dtype=[("end", "<i4"), ("splicecoord", "<i4"), ("splicelength", "<i4"),
+                             ("contlength", "<i4"), ("far_splicetype", "<i4"), ("watsonp", "<i4")])
+    rec["end"] = rng.choice([5, 3], size=n)
+    rec["splicelength"] = rng.integers(0, 120, size=n)
+    rec["contlength"] = rng.integers(0, 40, size=n)
+    rec["splicecoord"] = rng.integers(200, gseq.size - 200, size=n)
+    rec["far_splicetype"] = rng.integers(0, 4, size=n)
+    rec["watsonp"] = rng.integers(0, 2, size=n)
+    with tempfile.TemporaryDirectory() as d:
+        rec.tofile(os.path.join(d, "mksj_in.bin"))
+        blocks.astype("<u4").tofile(os.path.join(d, "genome.u32"))
+        run_driver("mksj", d)
+        out = np.fromfile(os.path.join(d, "mksj_out.bin"), dtype=np.uint8)
+    assert out.size == int((rec["contlength"] + rec["splicelength"]).sum())
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), blocks=blocks, records=rec, junctions=out)
+    print("%s: %d junctions, %d bytes" % (name, n, out.size))
+
+
 def maxent_case(name: str, blocks: np.ndarray, glen: int, n: int, seed: int) -> None:
     rng = np.random.default_rng(seed)
     model = rng.integers(0, 4, size=n).astype(np.uint32)
@@ -283,6 +305,7 @@ def main() -> None:
         ("ggap_chr17", lambda: ggap_case("ggap_chr17", chr17, 1500, seed=201)),
         ("cgap_chr17", lambda: cgap_case("cgap_chr17", chr17, 1500, seed=401)),
         ("sj_chr17", lambda: sj_case("sj_chr17", chr17, 2000, seed=501)),
+        ("mksj_chr17", lambda: mksj_case("mksj_chr17", chr17, 2000, seed=502)),
         ("maxent_chr17", lambda: maxent_case("maxent_chr17", b17, chr17.size, 20000, seed=301)),
         ("maxent_synth", lambda: maxent_case("maxent_synth", bsyn, synth.size, 6000, seed=302)),
     ]

@@ -11,6 +11,7 @@
  *   ref_driver cgap   <dir>   cgap_windows.bin query.bin query_uc.bin gseg.bin gseg_off.i64 genome.u32
  *                             -> cgap_results.bin pairs.bin npairs.i32
  *   ref_driver sj     <dir>   sj_windows.bin query.bin query_uc.bin -> results.bin pairs.bin npairs.i32
+ *   ref_driver mksj   <dir>   mksj_in.bin genome.u32 -> mksj_out.bin
  *   ref_driver maxent <dir>   maxent_in.bin genome.u32 -> maxent_out.f64
  *   ref_driver pdist  <dir>   -> pdist.i32 (4 x 128 x 128 via Dynprog_pairdistance for HIGHQ only) + consistent probe
  * All inputs use the record layouts of include/gsnapdp.h.
@@ -29,6 +30,7 @@
 #include "maxent_hr.h"
 #include "pairdef.h"
 #include "pairpool.h"
+#include "splicetrie_build.h"
 
 /* our record layouts */
 #include "../include/gsnapdp.h"
@@ -332,6 +334,43 @@ static int run_sj(const char *dir) {
   return 0;
 }
 
+/* Dynprog_make_splicejunction_5/3 (dynprog.c:6061, 6149) on the packed genome:
+ * record {end(5|3), splicecoord, splicelength, contlength, far_splicetype,
+ * watsonp}; output = the junction buffer (contlength + splicelength bytes,
+ * pre-filled with '#') per record. */
+typedef struct mksj_in {
+  int32_t end, splicecoord, splicelength, contlength, far_splicetype, watsonp;
+} mksj_in;
+
+static int run_mksj(const char *dir) {
+  size_t ni, ng;
+  mksj_in *in = (mksj_in *)slurp(dir, "mksj_in.bin", &ni);
+  UINT4 *g = (UINT4 *)slurp(dir, "genome.u32", &ng);
+  int n = (int)(ni / sizeof(mksj_in)), i;
+  char path[4096];
+  FILE *fp;
+  Genome_user_setup(g);
+  snprintf(path, sizeof(path), "%s/mksj_out.bin", dir);
+  fp = fopen(path, "wb");
+  for (i = 0; i < n; i++) {
+    int len = in[i].contlength + in[i].splicelength;
+    char *buf = (char *)malloc((size_t)len + 1);
+    memset(buf, '#', (size_t)len + 1);
+    if (in[i].end == 5)
+      Dynprog_make_splicejunction_5(buf, (Genomicpos_T)in[i].splicecoord, in[i].splicelength,
+                                    in[i].contlength, (Splicetype_T)in[i].far_splicetype,
+                                    in[i].watsonp);
+    else
+      Dynprog_make_splicejunction_3(buf, (Genomicpos_T)in[i].splicecoord, in[i].splicelength,
+                                    in[i].contlength, (Splicetype_T)in[i].far_splicetype,
+                                    in[i].watsonp);
+    fwrite(buf, 1, (size_t)len, fp);
+    free(buf);
+  }
+  fclose(fp);
+  return 0;
+}
+
 typedef struct maxent_in {
   uint32_t model, splice_pos, chroffset, pad;
 } maxent_in;
@@ -381,6 +420,7 @@ int main(int argc, char **argv) {
   if (!strcmp(argv[1], "cgap")) return run_cgap(argv[2]);
   if (!strcmp(argv[1], "maxent")) return run_maxent(argv[2]);
   if (!strcmp(argv[1], "sj")) return run_sj(argv[2]);
+  if (!strcmp(argv[1], "mksj")) return run_mksj(argv[2]);
   if (!strcmp(argv[1], "pdist")) return run_pdist(argv[2]);
   return 1;
 }

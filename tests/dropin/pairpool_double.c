@@ -43,7 +43,6 @@ List_T Pairpool_push(List_T list, Pairpool_T pool, int querypos, int genomepos, 
 List_T Pairpool_push_gapholder(List_T list, Pairpool_T pool, int queryjump, int genomejump,
                                unsigned char knownp) {
   (void)pool;
-  (void)knownp;
   Rec* r = (Rec*)calloc(1, sizeof(Rec));
   r->querypos = -1;
   r->genomepos = -1;
@@ -52,7 +51,7 @@ List_T Pairpool_push_gapholder(List_T list, Pairpool_T pool, int queryjump, int 
   r->cdna = ' ';
   r->comp = ' ';
   r->genome = ' ';
-  r->gapp = 1;
+  r->gapp = knownp ? 3 : 1; /* gapp | knowngapp << 1, as gsnapdp_pair */
   return cons(list, r);
 }
 

@@ -296,3 +296,88 @@ def test_dropin_cdna_gap_matches_reference_golden(golden_dir, tmp_path):
     L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dpL)))
     L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dpR)))
     L.Dynprog_term()
+
+
+def test_dropin_make_splicejunction_matches_reference_golden(golden_dir, tmp_path):
+    """Dynprog_make_splicejunction_5/3 (dynprog.c:6061, 6149): the distal part
+    from the genome, reverse-complemented on the minus strand.  Host staging,
+    no GPU needed."""
+    z = np.load(os.path.join(golden_dir, "mksj_chr17.npz"), allow_pickle=False)
+    load_double(tmp_path)
+    L = ctypes.CDLL(DROPIN)
+    blocks = np.ascontiguousarray(z["blocks"])
+    L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
+    args = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_ubyte]
+    L.Dynprog_make_splicejunction_5.argtypes = args
+    L.Dynprog_make_splicejunction_3.argtypes = args
+    pos = 0
+    for r in z["records"]:
+        n = int(r["contlength"] + r["splicelength"])
+        buf = np.full(n + 1, ord("#"), np.uint8)
+        f = L.Dynprog_make_splicejunction_5 if r["end"] == 5 else L.Dynprog_make_splicejunction_3
+        f(buf.ctypes.data, int(r["splicecoord"]), int(r["splicelength"]), int(r["contlength"]),
+          int(r["far_splicetype"]), int(r["watsonp"]))
+        assert buf[:n].tobytes() == z["junctions"][pos:pos + n].tobytes(), r
+        assert buf[n] == ord("#")
+        pos += n
+    assert pos == z["junctions"].size
+    L.Dynprog_term()
+
+
+SJ_ARGS = ([ctypes.c_void_p] * 7 + [ctypes.c_char_p] * 4 + [ctypes.c_int] * 5 + [ctypes.c_uint] * 4
+           + [ctypes.c_int, ctypes.c_ubyte, ctypes.c_ubyte, ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
+              ctypes.c_int])
+
+
+@pytest.mark.gpu
+def test_dropin_splicejunction_matches_reference_golden(golden_dir, tmp_path):
+    """Dynprog_end5/3_splicejunction called like Splicetrie_solve_end5/3
+    (splicetrie.c:352, 640): every out-parameter and the list, known
+    gapholder included."""
+    z = np.load(os.path.join(golden_dir, "sj_chr17.npz"), allow_pickle=False)
+    dbl = load_double(tmp_path)
+    L = ctypes.CDLL(DROPIN)
+    L.Dynprog_new.restype = ctypes.c_void_p
+    L.Dynprog_new.argtypes = [ctypes.c_int] * 5
+    L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    for f in ("Dynprog_end5_splicejunction", "Dynprog_end3_splicejunction"):
+        getattr(L, f).restype = ctypes.c_void_p
+        getattr(L, f).argtypes = SJ_ARGS
+    blocks = np.zeros(64, np.uint32)  # the junction replaces the genome (use_genomicseg_p)
+    L.Dynprog_init(600, 10, 11, 10, 8, 0)
+    L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
+    dp = L.Dynprog_new(600, 10, 11, 10, 8)
+    q = np.ascontiguousarray(z["query"])
+    qu = np.ascontiguousarray(z["query_uc"])
+    offs = np.concatenate([[0], np.cumsum(z["npairs"])])
+    out = np.zeros(8192, dtype=REC)
+    W = z["windows"]
+    known = 0
+    for i in range(min(500, len(W))):
+        w = W[i]
+        if w["maxlength1"] != 611 or w["maxlength2"] != 2000:
+            continue  # shrunken workspace limits: Dynprog_new cannot make them
+        ints = [ctypes.c_int(int(w["dynprogindex"]))] + [ctypes.c_int(-77) for _ in range(5)]
+        args = ([ctypes.byref(x) for x in ints] + [dp]
+                + [ctypes.c_char_p(b.ctypes.data + int(w[k])) for k, b in
+                   (("qpos", q), ("qpos", qu), ("spos", q), ("spos", qu))]
+                + [int(w[f]) for f in ("length1", "length2", "offset1", "offset2_anchor", "offset2_far")]
+                + [0, 0, 0, 0, int(w["cdna_direction"]), int(w["watsonp"]), int(w["jump_late_p"]), None,
+                   int(w["extraband_end"]), float(w["defect_rate"]), int(w["contlength"])])
+        f = L.Dynprog_end5_splicejunction if w["kind"] == END5_GAP else L.Dynprog_end3_splicejunction
+        lst = f(*args)
+        got = [x.value for x in ints]
+        want = [int(z[k][i]) for k in ("dynprogindex", "finalscore", "nmatches", "nmismatches", "nopens",
+                                       "nindels")]
+        assert got == want, (i, got, want)
+        k = dbl.dbl_list_read(lst, out.ctypes.data, out.size) if lst else 0
+        exp = z["pairs"][offs[i]:offs[i + 1]]
+        assert k == exp.size, (i, k, exp.size)
+        assert out[:k].tobytes() == exp.tobytes(), i
+        known += int((exp["gapp"] == 3).any())
+        if lst:
+            dbl.dbl_list_free(lst)
+    assert known > 400
+    L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dp)))
+    L.Dynprog_term()
