@@ -80,6 +80,22 @@ SJ_WINDOW = np.dtype([
 ])
 assert SJ_WINDOW.itemsize == 64
 
+MICRO_WINDOW = np.dtype([
+    ("length1", "<i4"), ("offset1", "<i4"), ("offset2L", "<i4"), ("revoffset2R", "<i4"),
+    ("cdna_direction", "<i4"), ("dynprogindex", "<i4"),
+    ("chroffset", "<u4"), ("chrhigh", "<u4"), ("chrpos", "<u4"), ("genomiclength", "<u4"),
+    ("qpos", "<u4"), ("ppos", "<u4"), ("defect_rate", "<f4"),
+    ("watsonp", "u1"), ("pad0", "u1"), ("pad1", "u1"), ("pad2", "u1"),
+])
+assert MICRO_WINDOW.itemsize == 56
+
+MICRO_RESULT = np.dtype([
+    ("bestprob2", "<f8"), ("bestprob3", "<f8"),
+    ("microintrontype", "<i4"), ("dynprogindex", "<i4"), ("found", "<i4"), ("status", "<i4"),
+    ("bestcL", "<i4"), ("bestcR", "<i4"), ("middlelength", "<i4"), ("offset2M", "<i4"),
+])
+assert MICRO_RESULT.itemsize == 48
+
 MAXENT_IN = np.dtype([("model", "<u4"), ("splice_pos", "<u4"), ("chroffset", "<u4"), ("pad", "<u4")])
 
 # enums (include/gsnapdp.h)

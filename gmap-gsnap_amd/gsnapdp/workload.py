@@ -23,6 +23,10 @@
   exon and whose rest comes from a far exon, against the splice junction
   Dynprog_make_splicejunction_5/3 builds (distal + proximal genome), plus
   random segments, planted introns and the early-return cases.
+* ``micro_windows``: Dynprog_microexon_int calls shaped like
+  traverse_single_gap's (stage3.c:5915): a query gap of cL + microexon + cR
+  bases against an intron gap, with a planted AG-microexon-GT (or the
+  antisense CT..AC) inside, decoys, and windows with nothing to find.
 * ``c5_windows``: the DP windows GSNAP issues for 100 bp reads (BASELINE
   config 5 reduced to its DP part): per read one single gap over
   the read (extraband_single 3) and two end gaps (end5 + end3, length1 1-30,
@@ -35,7 +39,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import genome as _genome
-from .records import (BEST_LOCAL, CGAP_WINDOW, SJ_WINDOW, END3_GAP, END5_GAP, GGAP_WINDOW, MAXLENGTH1, MAXLENGTH2,
+from .records import (BEST_LOCAL, CGAP_WINDOW, MICRO_WINDOW, SJ_WINDOW, END3_GAP, END5_GAP, GGAP_WINDOW, MAXLENGTH1, MAXLENGTH2,
                       QUERYEND_GAP, QUERYEND_INDELS, QUERYEND_NOGAPS, SINGLE_GAP, WINDOW)
 
 ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
@@ -621,6 +625,83 @@ def sj_windows(gseq: np.ndarray, n: int, seed: int, mix: bool = True) -> Batch:
         w[0]["length1"] = 0
         w[1]["length2"] = 0
     return Batch(w, np.concatenate(qs), np.concatenate(us))
+
+
+def micro_windows(gseq: np.ndarray, n: int, seed: int, mix: bool = True):
+    """Returns (genome with the planted sites, Batch of MICRO_WINDOW records)."""
+    rng = np.random.default_rng(seed)
+    g = gseq.copy()
+    Gn = g.size
+    w = np.zeros(n, dtype=MICRO_WINDOW)
+    qs, us = [], []
+    qpos = 0
+    for i in range(n):
+        cdir = 1 if rng.random() < 0.5 else -1
+        cL = int(rng.integers(1, 12))
+        mid = int(rng.integers(3, 13))
+        cR = int(rng.integers(1, 12))
+        L1 = cL + mid + cR
+        I1 = int(rng.integers(20, 400))
+        I2 = int(rng.integers(20, 400))
+        o = int(rng.integers(5, 40))
+        m = o + cL + I1
+        r0 = m + mid + I2
+        rev2R = r0 + cR - 1
+        glen = rev2R + int(rng.integers(5, 40))
+        chrpos = int(rng.integers(0, Gn - glen - 1))
+        watson = int(rng.integers(0, 2))
+
+        def absolute(x):
+            return chrpos + (x if watson else glen - 1 - x)
+
+        def put(x, seq):
+            for k, ch in enumerate(seq):
+                c = ord(ch) if isinstance(ch, str) else int(ch)
+                g[absolute(x + k)] = c if watson else _COMP[c]
+
+        dl, dr = ("GT", "AG") if cdir > 0 else ("CT", "AC")
+        plant = not mix or rng.random() < 0.8
+        if plant:
+            put(o + cL, dl)
+            put(m - 2, dr)
+            put(m + mid, dl)
+            put(r0 - 2, dr)
+            if mix and rng.random() < 0.3:  # a second copy of the microexon (ties, hit order)
+                m2 = o + cL + 9 + int(rng.integers(2, max(3, I1 - mid - 12)))
+                if m2 + mid + 2 < m - 2:
+                    view = [g[absolute(x)] if watson else _COMP[g[absolute(x)]] for x in range(m, m + mid)]
+                    put(m2 - 2, dr)
+                    put(m2, view)
+                    put(m2 + mid, dl)
+        xs = np.arange(glen)
+        view = g[chrpos + xs] if watson else _COMP[g[chrpos + glen - 1 - xs]]
+        q = np.concatenate([view[o:o + cL], view[m:m + mid], view[r0:r0 + cR]])
+        if mix and rng.random() < 0.3:
+            q = _mutate(rng, q, 0.05, 0.0)
+        quc = q.copy()
+        if mix and rng.random() < 0.05:
+            q = q.copy()
+            q[int(rng.integers(0, L1))] += 32  # lowercase query byte
+            quc = np.where((q >= 97) & (q <= 122), q - 32, q).astype(np.uint8)
+        rec = w[i]
+        rec["length1"] = L1
+        rec["offset1"] = int(rng.integers(0, 200))
+        rec["offset2L"] = o
+        rec["revoffset2R"] = rev2R
+        rec["cdna_direction"] = cdir
+        rec["dynprogindex"] = int(rng.choice([-1, 2]))
+        rec["chroffset"] = 0
+        rec["chrhigh"] = Gn
+        rec["chrpos"] = chrpos
+        rec["genomiclength"] = glen
+        rec["qpos"] = qpos
+        rec["ppos"] = qpos
+        rec["defect_rate"] = float(rng.choice([0.001, 0.005, 0.02]))
+        rec["watsonp"] = watson
+        qs += [q, np.full(4, ord("#"), np.uint8)]
+        us += [quc, np.full(4, ord("#"), np.uint8)]
+        qpos += L1 + 4
+    return g, Batch(w, np.concatenate(qs), np.concatenate(us))
 
 
 def c5_windows(gseq: np.ndarray, nreads: int, seed: int = 5, read_len: int = 100,

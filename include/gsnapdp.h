@@ -10,6 +10,7 @@
  *   - Dynprog_single_gap   dynprog.c:4450-4572   (kind GSNAPDP_SINGLE_GAP)
  *   - Dynprog_end5_gap     dynprog.c:5094-5284   (kind GSNAPDP_END5_GAP)
  *   - Dynprog_end3_gap     dynprog.c:5556-5741   (kind GSNAPDP_END3_GAP)
+ *   - Dynprog_microexon_int dynprog.c:7128-7432 (gsnapdp_micro_*)
  *   - Dynprog_end5_splicejunction dynprog.c:5412-5553 / Dynprog_end3_splicejunction
  *     :5869-6057 (gsnapdp_sj_*)
  *   - Maxent_hr_*_prob     maxent_hr.c:27217-27390 (gsnapdp_maxent_batch)
@@ -355,6 +356,52 @@ int gsnapdp_sj_run_host(gsnapdp_ctx *ctx, const gsnapdp_sj_window *windows, int 
 int gsnapdp_sj_expand(gsnapdp_ctx *ctx, const gsnapdp_sj_window *w, const gsnapdp_result *res,
                       const uint32_t *ops, const char *query, const char *query_uc,
                       gsnapdp_pair *pairs, int cap);
+
+/* ------------------------------------------------------------ microexons
+ * Dynprog_microexon_int (dynprog.c:7128-7432, non-PMAP, use_genomicseg_p
+ * false as every caller passes it, stage3.c:9865): splice a 3..12 nt
+ * microexon into an intron gap.  The left / right boundaries (at most one
+ * mismatch, :7241-7290), every GT..AG (CT..AC) pair (cL, cR), every exact hit
+ * of the middle query segment in the intron (BoyerMoore_nt, boyer-moore.c:384,
+ * hits visited last-found first), the flank test and the MaxEnt site
+ * probabilities; the best candidate by prob2 + prob3 under the reference's
+ * strict `>` in its scan order.  The query search segment is sequence1 /
+ * sequenceuc1 at qpos; the pairs read queryseq / queryuc from offset1 on,
+ * staged at ppos (ppos = qpos when sequence1 == &queryseq[offset1], as in
+ * stage3.c:5915).  Needs the MaxEnt tables. */
+typedef struct gsnapdp_micro_window {
+  int32_t length1, offset1, offset2L, revoffset2R, cdna_direction, dynprogindex;
+  uint32_t chroffset, chrhigh, chrpos, genomiclength;
+  uint32_t qpos, ppos;
+  float defect_rate;
+  uint8_t watsonp, pad0, pad1, pad2;
+} gsnapdp_micro_window;
+
+/* Out-parameters of Dynprog_microexon_int and where its pairs come from.
+ * status: 0 ok, 4 unsupported (the reference aborts: cdna_direction 0 or
+ * span <= 0, :7204/:7224; or no MaxEnt tables).  found = 1 when a list is
+ * returned; then the pairs are: bestcL left-segment pairs, a gapholder, the
+ * middle pairs from genome column offset2M (the LAST hit examined, not the
+ * best one: dynprog.c:7412-7413), a gapholder, bestcR right-segment pairs;
+ * gsnapdp_micro_expand rebuilds them. */
+typedef struct gsnapdp_micro_result {
+  double bestprob2, bestprob3;
+  int32_t microintrontype, dynprogindex, found, status;
+  int32_t bestcL, bestcR, middlelength, offset2M;
+} gsnapdp_micro_result;
+
+int gsnapdp_micro_run_device(gsnapdp_ctx *ctx, const gsnapdp_micro_window *d_windows, int n,
+                             const char *d_query, const char *d_query_uc,
+                             gsnapdp_micro_result *d_results, void *stream);
+int gsnapdp_micro_run_host(gsnapdp_ctx *ctx, const gsnapdp_micro_window *windows, int n,
+                           const char *query, const char *query_uc, size_t query_bytes,
+                           gsnapdp_micro_result *results);
+/* The list Dynprog_microexon_int returns (make_microexon_pairs_double,
+ * :6949-7055: the list head is the last pair pushed).  Returns its length
+ * (0 = NULL) or -1. */
+int gsnapdp_micro_expand(gsnapdp_ctx *ctx, const gsnapdp_micro_window *w,
+                         const gsnapdp_micro_result *res, const char *query, const char *query_uc,
+                         gsnapdp_pair *pairs, int cap);
 
 /* Load the MaxEnt parameter tables (12 x 16384 + 4 x 16 doubles, order in
  * DESIGN.md) into the context.  Must be called before gsnapdp_maxent_*. */

@@ -9,6 +9,7 @@
 #include "dp_oracle.h"
 
 #include <ctype.h>
+#include <math.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -1815,5 +1816,226 @@ int orc_run_sj_batch(const gsnapdp_sj_window *w, int n, const char *query, const
   }
   orc_list_free(&l);
   orc_dp_free(dp);
+  return 0;
+}
+
+/* ------------------------------------------------------------- microexons */
+
+/* get_genomic_nt of boyer-moore.c:361-380: no '*' rules, straight from the blocks */
+static char bm_nt(const gpar *g, int pos) {
+  if (g->watsonp) return block_char(g->chroffset + g->chrpos + (uint32_t)pos);
+  return compl_char(block_char(g->chroffset + g->chrpos + (uint32_t)(g->genomiclength - 1) - (uint32_t)pos));
+}
+
+/* BoyerMoore_nt (boyer-moore.c:384-451): every j in [0, textlen-querylen]
+ * where the text matches the (A C G T only, else no hits: query_okay :313)
+ * query exactly.  Written as the plain scan; the reference's good-suffix /
+ * bad-character shifts only skip non-matching j.  hits[] is in the order the
+ * reference's Intlist holds them (pushed while j ascends: largest j first). */
+static int bm_hits(int *hits, int cap, const char *query, int querylen, int textoffset, int textlen,
+                   const gpar *g) {
+  int i, j, n = 0;
+  for (i = 0; i < querylen; i++)
+    if (query[i] != 'A' && query[i] != 'C' && query[i] != 'G' && query[i] != 'T') return 0;
+  for (j = 0; j <= textlen - querylen; j++) {
+    for (i = querylen - 1; i >= 0 && query[i] == bm_nt(g, textoffset + i + j); i--)
+      ;
+    if (i < 0) {
+      if (n < cap) hits[n] = j;
+      n++;
+    }
+  }
+  for (i = 0; i < n / 2 && i < cap; i++) { /* Intlist_push order */
+    int t = hits[i];
+    hits[i] = hits[n - 1 - i];
+    hits[n - 1 - i] = t;
+  }
+  return n;
+}
+
+#define MIN_MICROEXON_LENGTH 3   /* :133 */
+#define MAX_MICROEXON_LENGTH 12  /* :137 (non-PMAP) */
+
+/* Dynprog_microexon_int (dynprog.c:7128-7432), non-PMAP, use_genomicseg_p false.
+ * Returns 1 and fills *o when a list is returned, with the list itself in out. */
+int orc_microexon_int(orc_list *out, orc_micro_out *o, int dynprogindex, const char *sequence1,
+                      const char *sequenceuc1, int length1, int offset1, int offset2L,
+                      int revoffset2R, int cdna_direction, const char *queryseq,
+                      const char *queryuc, uint32_t chroffset, uint32_t chrhigh, uint32_t chrpos,
+                      uint32_t genomiclength, int watsonp, double defect_rate) {
+  gpar g = {chroffset, chrhigh, chrpos, (int)genomiclength, watsonp};
+  int bestcL = -1, bestcR = -1, best_middlelength = 0, candidate = 0, have_candidate = 0;
+  int min_len, span, leftbound, rightbound, nmm, i, cL, cR;
+  char intron1, intron2, intron3, intron4, gapchar;
+  double pvalue, bestprob = 0.0;
+  static int hits[1 << 16];
+  orc_list_clear(out);
+  memset(o, 0, sizeof(*o));
+  o->dynprogindex = dynprogindex;
+  pvalue = defect_rate < 0.003 ? 0.01 : defect_rate < 0.014 ? 0.001 : 0.0001; /* :7171-7177 */
+  if (cdna_direction > 0) {
+    intron1 = 'G'; intron2 = 'T'; intron3 = 'A'; intron4 = 'G';
+    gapchar = '>';
+    o->microintrontype = GTAG_FWD;
+  } else if (cdna_direction < 0) {
+    intron1 = 'C'; intron2 = 'T'; intron3 = 'A'; intron4 = 'C';
+    gapchar = '<';
+    o->microintrontype = GTAG_REV;
+  } else {
+    o->unsupported = 1; /* the reference aborts (:7203-7206) */
+    return 0;
+  }
+  span = revoffset2R - offset2L;
+  if (span <= 0) {
+    o->unsupported = 1; /* :7222-7225 */
+    return 0;
+  }
+  min_len = (int)ceil(-log(1.0 - pow(1.0 - pvalue, 1.0 / (double)span)) / log(4));
+  min_len -= 8;
+  if (min_len > MAX_MICROEXON_LENGTH) {
+    o->microintrontype = NONINTRON;
+    return 0;
+  } else if (min_len < MIN_MICROEXON_LENGTH) {
+    min_len = MIN_MICROEXON_LENGTH;
+  }
+  leftbound = 0; /* :7241-7262 */
+  nmm = 0;
+  while (leftbound < length1 - 1 && nmm <= 1) {
+    if (sequenceuc1[leftbound] != gnt(&g, offset2L + leftbound)) nmm++;
+    leftbound++;
+  }
+  leftbound--;
+  rightbound = 0; /* :7264-7286 */
+  i = length1 - 1;
+  nmm = 0;
+  while (i >= 0 && nmm <= 1) {
+    if (sequenceuc1[i] != gnt(&g, revoffset2R - rightbound)) nmm++;
+    rightbound++;
+    i--;
+  }
+  rightbound--;
+  for (cL = 1; cL <= leftbound; cL++) { /* :7292-7396 */
+    if (gnt(&g, offset2L + cL) == intron1 && gnt(&g, offset2L + cL + 1) == intron2) {
+      int mincR = length1 - MAX_MICROEXON_LENGTH - cL, maxcR = length1 - min_len - cL;
+      if (mincR < 1) mincR = 1;
+      if (maxcR > rightbound) maxcR = rightbound;
+      for (cR = mincR; cR <= maxcR; cR++) {
+        if (gnt(&g, revoffset2R - cR - 1) == intron3 && gnt(&g, revoffset2R - cR) == intron4) {
+          int middlelength = length1 - cL - cR;
+          int textleft = offset2L + cL + MICROINTRON_LENGTH;
+          int textright = revoffset2R - cR - MICROINTRON_LENGTH;
+          int nh = bm_hits(hits, (int)(sizeof(hits) / sizeof(hits[0])), &sequenceuc1[cL],
+                           middlelength, textleft, textright - textleft, &g), h;
+          for (h = 0; h < nh; h++) {
+            candidate = textleft + hits[h];
+            have_candidate = 1;
+            if (gnt(&g, candidate - 2) == intron3 && gnt(&g, candidate - 1) == intron4 &&
+                gnt(&g, candidate + middlelength) == intron1 &&
+                gnt(&g, candidate + middlelength + 1) == intron2) {
+              double prob2, prob3;
+              uint32_t sp;
+              if (watsonp) {
+                if (cdna_direction > 0) {
+                  sp = chrpos + (uint32_t)(candidate - 1) + 1u;
+                  prob2 = orc_maxent_acceptor(chroffset + sp, chroffset);
+                  sp = chrpos + (uint32_t)candidate + (uint32_t)middlelength;
+                  prob3 = orc_maxent_donor(chroffset + sp, chroffset);
+                } else {
+                  sp = chrpos + (uint32_t)(candidate - 1) + 1u;
+                  prob2 = orc_maxent_antidonor(chroffset + sp, chroffset);
+                  sp = chrpos + (uint32_t)candidate + (uint32_t)middlelength;
+                  prob3 = orc_maxent_antiacceptor(chroffset + sp, chroffset);
+                }
+              } else {
+                if (cdna_direction > 0) {
+                  sp = chrpos + (genomiclength - 1u) - (uint32_t)(candidate - 1);
+                  prob2 = orc_maxent_antiacceptor(chroffset + sp, chroffset);
+                  sp = chrpos + (genomiclength - 1u) - (uint32_t)(candidate + middlelength) + 1u;
+                  prob3 = orc_maxent_antidonor(chroffset + sp, chroffset);
+                } else {
+                  sp = chrpos + (genomiclength - 1u) - (uint32_t)(candidate - 1);
+                  prob2 = orc_maxent_donor(chroffset + sp, chroffset);
+                  sp = chrpos + (genomiclength - 1u) - (uint32_t)(candidate + middlelength) + 1u;
+                  prob3 = orc_maxent_acceptor(chroffset + sp, chroffset);
+                }
+              }
+              if (prob2 + prob3 > bestprob) {
+                bestcL = cL;
+                bestcR = cR;
+                best_middlelength = middlelength;
+                o->bestprob2 = prob2;
+                o->bestprob3 = prob3;
+                bestprob = prob2 + prob3;
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  if (bestcL < 0 || bestcR < 0) {
+    o->microintrontype = NONINTRON;
+    return 0;
+  }
+  (void)have_candidate;
+  o->found = 1;
+  o->bestcL = bestcL;
+  o->bestcR = bestcR;
+  o->middlelength = best_middlelength;
+  o->offset2M = candidate; /* the last hit examined (:7412-7413) */
+  {
+    /* make_microexon_pairs_double (:6949-7055) */
+    const int offs1[3] = {offset1, offset1 + bestcL, offset1 + bestcL + best_middlelength};
+    const int offs2[3] = {offset2L, candidate, revoffset2R - bestcR + 1};
+    const int lens[3] = {bestcL, best_middlelength, bestcR};
+    int seg, k;
+    for (seg = 0; seg < 3; seg++) {
+      for (k = 0; k < lens[seg]; k++) {
+        char c1 = queryseq[offs1[seg] + k], c2 = gnt(&g, offs2[seg] + k);
+        char comp = queryuc[offs1[seg] + k] == c2 ? '*' : cons[c1 & 127][c2 & 127] ? ':' : ' ';
+        push_pair(out, offs1[seg] + k, offs2[seg] + k, c1, comp, c2, dynprogindex);
+      }
+      if (seg < 2) {
+        push_gapholder(out, GSNAPDP_UNKNOWNJUMP, GSNAPDP_UNKNOWNJUMP);
+        out->buf[out->head].comp = gapchar; /* gappair->comp = gapchar */
+      }
+    }
+  }
+  o->dynprogindex = step_index(dynprogindex);
+  return 1;
+}
+
+int orc_run_micro_batch(const gsnapdp_micro_window *w, int n, const char *query,
+                        const char *query_uc, gsnapdp_micro_result *results, gsnapdp_pair *pairs,
+                        const int64_t *pair_offsets, int32_t *npairs) {
+  orc_list l;
+  int i, t;
+  orc_list_init(&l, 256);
+  for (i = 0; i < n; i++) {
+    const gsnapdp_micro_window *x = &w[i];
+    gsnapdp_micro_result *r = &results[i];
+    orc_micro_out o;
+    int64_t off = pair_offsets[i], cap = pair_offsets[i + 1] - off;
+    /* queryseq such that queryseq[offset1 + k] is the staged byte at ppos + k */
+    const char *qs = query + (int64_t)x->ppos - x->offset1, *qsu = query_uc + (int64_t)x->ppos - x->offset1;
+    orc_microexon_int(&l, &o, x->dynprogindex, query + x->qpos, query_uc + x->qpos, x->length1,
+                      x->offset1, x->offset2L, x->revoffset2R, x->cdna_direction, qs, qsu,
+                      x->chroffset, x->chrhigh, x->chrpos, x->genomiclength, x->watsonp,
+                      (double)x->defect_rate);
+    memset(r, 0, sizeof(*r));
+    r->bestprob2 = o.bestprob2;
+    r->bestprob3 = o.bestprob3;
+    r->microintrontype = o.microintrontype;
+    r->dynprogindex = o.dynprogindex;
+    r->found = o.found;
+    r->status = o.unsupported ? 4 : 0;
+    r->bestcL = o.bestcL;
+    r->bestcR = o.bestcR;
+    r->middlelength = o.middlelength;
+    r->offset2M = o.offset2M;
+    npairs[i] = l.n;
+    for (t = 0; t < l.n && t < cap; t++) pairs[off + t] = l.buf[l.head + t];
+  }
+  orc_list_free(&l);
   return 0;
 }

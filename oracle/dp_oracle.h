@@ -170,6 +170,21 @@ int orc_run_sj_batch(const gsnapdp_sj_window *w, int n, const char *query, const
                      gsnapdp_result *results, gsnapdp_pair *pairs, const int64_t *pair_offsets,
                      int32_t *npairs);
 
+/* Dynprog_microexon_int (dynprog.c:7128) */
+typedef struct orc_micro_out {
+  double bestprob2, bestprob3;
+  int microintrontype, dynprogindex, found, unsupported;
+  int bestcL, bestcR, middlelength, offset2M;
+} orc_micro_out;
+int orc_microexon_int(orc_list *out, orc_micro_out *o, int dynprogindex, const char *sequence1,
+                      const char *sequenceuc1, int length1, int offset1, int offset2L,
+                      int revoffset2R, int cdna_direction, const char *queryseq,
+                      const char *queryuc, uint32_t chroffset, uint32_t chrhigh, uint32_t chrpos,
+                      uint32_t genomiclength, int watsonp, double defect_rate);
+int orc_run_micro_batch(const gsnapdp_micro_window *w, int n, const char *query,
+                        const char *query_uc, gsnapdp_micro_result *results, gsnapdp_pair *pairs,
+                        const int64_t *pair_offsets, int32_t *npairs);
+
 #ifdef __cplusplus
 }
 #endif

@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
 from gsnapdp import genome as G  # noqa: E402
 from gsnapdp import workload as W  # noqa: E402
 from gsnapdp.records import (CGAP_RESULT, GGAP_RESULT, GGAP_WINDOW, MAXLENGTH1, MAXLENGTH2,  # noqa: E402
-                             PAIR, RESULT)
+                             MICRO_RESULT, PAIR, RESULT)
 
 REF_TESTS = "/root/reference/tests"
 DRIVER = os.path.join(HERE, "_ref", "ref_driver")
@@ -245,6 +245,23 @@ def mksj_case(name: str, gseq: np.ndarray, n: int, seed: int) -> None:
     print("%s: %d junctions, %d bytes" % (name, n, out.size))
 
 
+def micro_case(name: str, gseq: np.ndarray, n: int, seed: int) -> None:
+    g, b = W.micro_windows(gseq, n, seed)
+    blocks = G.pack(g)
+    with tempfile.TemporaryDirectory() as d:
+        b.windows.tofile(os.path.join(d, "micro_windows.bin"))
+        b.query.tofile(os.path.join(d, "query.bin"))
+        b.query_uc.tofile(os.path.join(d, "query_uc.bin"))
+        blocks.astype("<u4").tofile(os.path.join(d, "genome.u32"))
+        run_driver("micro", d)
+        res = np.fromfile(os.path.join(d, "micro_results.bin"), dtype=MICRO_RESULT)
+        npairs = np.fromfile(os.path.join(d, "npairs.i32"), dtype=np.int32)
+        pairs = np.fromfile(os.path.join(d, "pairs.bin"), dtype=PAIR)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), blocks=blocks, windows=b.windows, query=b.query,
+                        query_uc=b.query_uc, results=res, npairs=npairs, pairs=pairs)
+    print("%s: %d windows (%d found), %d pairs" % (name, len(b), int(res["found"].sum()), pairs.size))
+
+
 def maxent_case(name: str, blocks: np.ndarray, glen: int, n: int, seed: int) -> None:
     rng = np.random.default_rng(seed)
     model = rng.integers(0, 4, size=n).astype(np.uint32)
@@ -306,6 +323,7 @@ def main() -> None:
         ("cgap_chr17", lambda: cgap_case("cgap_chr17", chr17, 1500, seed=401)),
         ("sj_chr17", lambda: sj_case("sj_chr17", chr17, 2000, seed=501)),
         ("mksj_chr17", lambda: mksj_case("mksj_chr17", chr17, 2000, seed=502)),
+        ("micro_chr17", lambda: micro_case("micro_chr17", chr17, 1500, seed=601)),
         ("maxent_chr17", lambda: maxent_case("maxent_chr17", b17, chr17.size, 20000, seed=301)),
         ("maxent_synth", lambda: maxent_case("maxent_synth", bsyn, synth.size, 6000, seed=302)),
     ]

@@ -16,8 +16,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
-from gsnapdp.records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_WINDOW, PAIR, RESULT, SJ_WINDOW,  # noqa: E402
-                             WINDOW)
+from gsnapdp.records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_WINDOW, MICRO_RESULT,  # noqa: E402
+                             MICRO_WINDOW, PAIR, RESULT, SJ_WINDOW, WINDOW)
 
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 TABLES_PATH = os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin")
@@ -47,6 +47,7 @@ def lib():
         L.orc_run_ggap_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
         L.orc_run_cgap_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp]
         L.orc_run_sj_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
+        L.orc_run_micro_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
         L.orc_maxent_batch.argtypes = [vp, vp, vp, vp, i32]
         L.orc_pairdistance.argtypes = [i32, i32, i32]
         L.orc_pairdistance.restype = i32
@@ -86,6 +87,10 @@ def pair_offsets_for(windows: np.ndarray, slack: int = 8) -> np.ndarray:
         np.cumsum(cap.clip(slack), out=off[1:])
         return off
     l1 = windows["length1"].astype(np.int64) if "length1" in windows.dtype.names else None
+    if "revoffset2R" in windows.dtype.names and "length2L" not in windows.dtype.names:  # microexons
+        off = np.zeros(len(windows) + 1, dtype=np.int64)
+        np.cumsum(l1 + 2 + slack, out=off[1:])
+        return off
     if "length2L" in windows.dtype.names:
         cap = 2 * l1 + windows["length2L"] + windows["length2R"] + slack
     else:
@@ -149,6 +154,20 @@ def run_sj_batch(windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray):
     pairs = np.zeros(int(off[-1]), dtype=PAIR)
     npairs = np.zeros(len(w), dtype=np.int32)
     L.orc_run_sj_batch(_p(w), len(w), _p(q), _p(u), _p(res), _p(pairs), _p(off), _p(npairs))
+    return res, pairs, off, npairs
+
+
+def run_micro_batch(windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray):
+    """Dynprog_microexon_int over gsnapdp_micro_window records (needs setup())."""
+    L = lib()
+    w = np.ascontiguousarray(windows, dtype=MICRO_WINDOW)
+    q = np.ascontiguousarray(query, dtype=np.uint8)
+    u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+    res = np.zeros(len(w), dtype=MICRO_RESULT)
+    off = pair_offsets_for(w)
+    pairs = np.zeros(int(off[-1]), dtype=PAIR)
+    npairs = np.zeros(len(w), dtype=np.int32)
+    L.orc_run_micro_batch(_p(w), len(w), _p(q), _p(u), _p(res), _p(pairs), _p(off), _p(npairs))
     return res, pairs, off, npairs
 
 

@@ -12,6 +12,7 @@
  *                             -> cgap_results.bin pairs.bin npairs.i32
  *   ref_driver sj     <dir>   sj_windows.bin query.bin query_uc.bin -> results.bin pairs.bin npairs.i32
  *   ref_driver mksj   <dir>   mksj_in.bin genome.u32 -> mksj_out.bin
+ *   ref_driver micro  <dir>   micro_windows.bin query.bin query_uc.bin genome.u32 -> micro_results.bin pairs.bin npairs.i32
  *   ref_driver maxent <dir>   maxent_in.bin genome.u32 -> maxent_out.f64
  *   ref_driver pdist  <dir>   -> pdist.i32 (4 x 128 x 128 via Dynprog_pairdistance for HIGHQ only) + consistent probe
  * All inputs use the record layouts of include/gsnapdp.h.
@@ -371,6 +372,52 @@ static int run_mksj(const char *dir) {
   return 0;
 }
 
+static int run_micro(const char *dir) {
+  size_t nw, nq, nu, ng;
+  gsnapdp_micro_window *w = (gsnapdp_micro_window *)slurp(dir, "micro_windows.bin", &nw);
+  char *q = (char *)slurp(dir, "query.bin", &nq);
+  char *qu = (char *)slurp(dir, "query_uc.bin", &nu);
+  UINT4 *g = (UINT4 *)slurp(dir, "genome.u32", &ng);
+  int n = (int)(nw / sizeof(gsnapdp_micro_window)), i;
+  gsnapdp_micro_result *res = (gsnapdp_micro_result *)calloc((size_t)n + 1, sizeof(*res));
+  int32_t *npairs = (int32_t *)calloc((size_t)n + 1, sizeof(int32_t));
+  gsnapdp_pair *tmp = (gsnapdp_pair *)malloc(sizeof(gsnapdp_pair) * PAIRCAP);
+  FILE *fp;
+  char path[4096];
+  Pairpool_T pool = Pairpool_new();
+
+  Genome_user_setup(g);
+  Maxent_hr_setup(g);
+  snprintf(path, sizeof(path), "%s/pairs.bin", dir);
+  fp = fopen(path, "wb");
+  for (i = 0; i < n; i++) {
+    gsnapdp_micro_window *x = &w[i];
+    gsnapdp_micro_result *o = &res[i];
+    double p2 = -1, p3 = -1;
+    int dpi = x->dynprogindex, it = -77, k;
+    List_T pairs;
+    char *qs = q + (long)x->ppos - x->offset1, *qsu = qu + (long)x->ppos - x->offset1;
+    Pairpool_reset(pool);
+    pairs = Dynprog_microexon_int(&p2, &p3, &dpi, &it, q + x->qpos, qu + x->qpos, NULL, NULL, NULL,
+                                  NULL, x->length1, 0, 0, x->offset1, x->offset2L, x->revoffset2R,
+                                  x->cdna_direction, qs, qsu, NULL, NULL, x->chroffset, x->chrhigh,
+                                  x->chrpos, x->genomiclength, x->watsonp, false, pool,
+                                  (double)x->defect_rate);
+    o->bestprob2 = p2;
+    o->bestprob3 = p3;
+    o->microintrontype = it;
+    o->dynprogindex = dpi;
+    o->found = pairs != NULL;
+    k = flatten(pairs, tmp, PAIRCAP);
+    npairs[i] = k;
+    fwrite(tmp, sizeof(gsnapdp_pair), (size_t)(k < PAIRCAP ? k : PAIRCAP), fp);
+  }
+  fclose(fp);
+  spit(dir, "micro_results.bin", res, sizeof(*res) * (size_t)n);
+  spit(dir, "npairs.i32", npairs, sizeof(int32_t) * (size_t)n);
+  return 0;
+}
+
 typedef struct maxent_in {
   uint32_t model, splice_pos, chroffset, pad;
 } maxent_in;
@@ -421,6 +468,7 @@ int main(int argc, char **argv) {
   if (!strcmp(argv[1], "maxent")) return run_maxent(argv[2]);
   if (!strcmp(argv[1], "sj")) return run_sj(argv[2]);
   if (!strcmp(argv[1], "mksj")) return run_mksj(argv[2]);
+  if (!strcmp(argv[1], "micro")) return run_micro(argv[2]);
   if (!strcmp(argv[1], "pdist")) return run_pdist(argv[2]);
   return 1;
 }

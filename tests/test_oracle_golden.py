@@ -122,3 +122,22 @@ def test_sj_oracle_matches_reference(golden_dir):
     for f in PAIR.names:
         assert np.array_equal(got[f], z["pairs"][f]), f
     assert (z["pairs"]["gapp"] == 3).sum() > 1500  # known gapholders
+
+
+def test_micro_oracle_matches_reference(golden_dir):
+    """Dynprog_microexon_int: out-parameters (f64 probabilities bit for bit) and
+    the list, including the reference's last-hit offset for the middle pairs."""
+    z = load(golden_dir, "micro_chr17")
+    O.setup(z["blocks"])
+    res, pairs, off, npairs = O.run_micro_batch(z["windows"], z["query"], z["query_uc"])
+    ref = z["results"]
+    for f in ("microintrontype", "dynprogindex", "found"):
+        bad = np.nonzero(res[f] != ref[f])[0]
+        assert bad.size == 0, "%s differs at %s" % (f, bad[:10])
+    for f in ("bestprob2", "bestprob3"):
+        assert np.array_equal(res[f].view(np.uint64), ref[f].view(np.uint64)), f
+    assert np.array_equal(npairs, z["npairs"])
+    got = np.concatenate([pairs[off[i]:off[i] + npairs[i]] for i in range(len(npairs))])
+    for f in PAIR.names:
+        assert np.array_equal(got[f], z["pairs"][f]), f
+    assert ref["found"].sum() > 500
