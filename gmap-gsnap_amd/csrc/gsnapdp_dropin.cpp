@@ -278,6 +278,20 @@ gsnapdp_List_T run_sj(int kind, const char* seq1, const char* seq1uc, const char
   return list;
 }
 
+// The head of the reference's Pair_T (pairdef.h:9-23) and List_T (listdef.h):
+// make_microexon_pairs_double writes the gapholders' comp in place
+// (dynprog.c:6990-6991), so the shim does the same through the host's layout.
+struct RefPairHead {
+  int querypos;
+  unsigned genomepos;
+  int refquerypos, aapos, queryjump, genomejump, aaphase_g, aaphase_e, dynprogindex;
+  char cdna, comp, genome;
+};
+struct RefList {
+  void* first;
+  RefList* rest;
+};
+
 }  // namespace
 
 extern "C" {
@@ -667,6 +681,81 @@ void Dynprog_make_splicejunction_3(char* splicejunction, gsnapdp_Genomicpos_T sp
     abort();
   }
   if (!watsonp) revcomp_inplace(distal, splicelength);
+}
+
+gsnapdp_List_T Dynprog_microexon_int(
+    double* bestprob2, double* bestprob3, int* dynprogindex, int* microintrontype,
+    char* sequence1, char* sequenceuc1, char*, char*, char*, char*, int length1, int, int,
+    int offset1, int offset2L, int revoffset2R, int cdna_direction, char* queryseq,
+    char* queryuc, char*, char*, gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh,
+    gsnapdp_Genomicpos_T chrpos, gsnapdp_Genomicpos_T genomiclength, gsnapdp_bool watsonp,
+    gsnapdp_bool use_genomicseg_p, gsnapdp_Pairpool_T pairpool, double defect_rate) {
+  *bestprob2 = *bestprob3 = 0.0;  // :7168
+  if (cdna_direction == 0) {      // :7203-7206
+    fprintf(stderr, "cdna_direction is 0 in Dynprog_microexon_int\n");
+    abort();
+  }
+  if (revoffset2R - offset2L <= 0) {  // :7222-7225
+    fprintf(stderr, "Bug in Dynprog_microexon_int.  span %d <= 0.  Please report to twu@gene.com\n",
+            revoffset2R - offset2L);
+    abort();
+  }
+  if (use_genomicseg_p) fatal("Dynprog_microexon_int with use_genomicseg_p (no caller passes it)");
+  std::lock_guard<std::mutex> lock(g.mu);
+  ensure_tables();
+  gsnapdp_ctx* c = ctx();
+  const int L1 = length1 > 0 ? length1 : 0;
+  // sequence1 / sequenceuc1 for the search, queryseq / queryuc from offset1 for the pairs
+  g.q.assign(2 * (size_t)L1 + 16, 0);
+  g.qu.assign(2 * (size_t)L1 + 16, 0);
+  const size_t pbase = (size_t)L1 + 8;
+  if (L1 > 0) {
+    memcpy(g.q.data(), sequence1, (size_t)L1);
+    memcpy(g.qu.data(), sequenceuc1, (size_t)L1);
+    memcpy(g.q.data() + pbase, queryseq + offset1, (size_t)L1);
+    memcpy(g.qu.data() + pbase, queryuc + offset1, (size_t)L1);
+  }
+  gsnapdp_micro_window w;
+  memset(&w, 0, sizeof(w));
+  w.length1 = length1;
+  w.offset1 = offset1;
+  w.offset2L = offset2L;
+  w.revoffset2R = revoffset2R;
+  w.cdna_direction = cdna_direction;
+  w.dynprogindex = *dynprogindex;
+  w.chroffset = chroffset;
+  w.chrhigh = chrhigh;
+  w.chrpos = chrpos;
+  w.genomiclength = genomiclength;
+  w.qpos = 0;
+  w.ppos = (uint32_t)pbase;
+  w.defect_rate = defect_rate < 0.003 ? 0.001f : (defect_rate < 0.014 ? 0.01f : 0.5f);
+  w.watsonp = watsonp ? 1 : 0;
+  gsnapdp_micro_result r;
+  if (gsnapdp_micro_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r))
+    fatal(std::string("gsnapdp_micro_run_host: ") + gsnapdp_last_error());
+  if (r.status != 0) fatal("microexon window outside the reference's domain");
+  *bestprob2 = r.bestprob2;
+  *bestprob3 = r.bestprob3;
+  *microintrontype = r.microintrontype;
+  *dynprogindex = r.dynprogindex;
+  if (!r.found) return nullptr;
+  g.pairs.resize((size_t)L1 + 4);
+  const int n = gsnapdp_micro_expand(c, &w, &r, g.q.data(), g.qu.data(), g.pairs.data(),
+                                     (int)g.pairs.size());
+  if (n <= 0 || n > (int)g.pairs.size()) fatal("gsnapdp_micro_expand failed");
+  gsnapdp_List_T list = nullptr;
+  for (int i = n - 1; i >= 0; i--) {
+    const gsnapdp_pair& p = g.pairs[(size_t)i];
+    if (p.gapp) {
+      list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump, 0);
+      ((RefPairHead*)((RefList*)list)->first)->comp = p.comp;  // gappair->comp = gapchar
+    } else {
+      list = Pairpool_push(list, pairpool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome,
+                           p.dynprogindex);
+    }
+  }
+  return list;
 }
 
 void Maxent_hr_setup(unsigned int* ref_blocks) {  // maxent_hr.c:27195

@@ -392,6 +392,66 @@ extern "C" int gsnapdp_sj_expand(gsnapdp_ctx* ctx, const gsnapdp_sj_window* w,
   return n;
 }
 
+// Dynprog_microexon_int's list (make_microexon_pairs_double, dynprog.c:6949-7055):
+// the left segment, a gapholder with comp = the intron's gapchar, the middle
+// from genome column offset2M, a second gapholder, the right segment; the
+// returned list starts at the last pair pushed.
+extern "C" int gsnapdp_micro_expand(gsnapdp_ctx* ctx, const gsnapdp_micro_window* w,
+                                    const gsnapdp_micro_result* res, const char* query,
+                                    const char* query_uc, gsnapdp_pair* pairs, int cap) {
+  if (!ctx || !w || !res) return -1;
+  if (res->status != ST_OK || !res->found) return 0;
+  HostGenome G = {gsnapdp__host_blocks(ctx), gsnapdp__host_nwords(ctx), w->chroffset, w->chrhigh,
+                  w->chrpos, (int)w->genomiclength, w->watsonp ? 1 : 0};
+  const uint32_t* prof = gsnapdp__host_prof(ctx);
+  const char gapchar = w->cdna_direction > 0 ? '>' : '<';  // FWD/REV_CANONICAL_INTRON_COMP
+  // queryseq[offset1 + k] is the staged byte ppos + k
+  const char* qs = query + w->ppos;
+  const char* qsu = query_uc + w->ppos;
+  const int offs1[3] = {0, res->bestcL, res->bestcL + res->middlelength};
+  const int offs2[3] = {w->offset2L, res->offset2M, w->revoffset2R - res->bestcR + 1};
+  const int lens[3] = {res->bestcL, res->middlelength, res->bestcR};
+  std::vector<gsnapdp_pair> p;
+  p.reserve((size_t)w->length1 + 2);
+  for (int seg = 0; seg < 3; seg++) {
+    for (int k = 0; k < lens[seg]; k++) {
+      const int qi = offs1[seg] + k;
+      const char c1 = qs[qi], c2 = G.nt(offs2[seg] + k);
+      const int gi = c2 == 'A' ? 0 : c2 == 'C' ? 1 : c2 == 'G' ? 2 : c2 == 'T' ? 3 : c2 == 'N' ? 4 : -1;
+      char comp;
+      if (qsu[qi] == c2) comp = GSNAPDP_DYNPROG_MATCH_COMP;
+      else if (gi >= 0 && ((prof[(unsigned char)c1 & 127] >> (24 + gi)) & 1u)) comp = GSNAPDP_AMBIGUOUS_COMP;
+      else comp = GSNAPDP_MISMATCH_COMP;
+      gsnapdp_pair x;
+      memset(&x, 0, sizeof(x));
+      x.querypos = w->offset1 + qi;
+      x.genomepos = offs2[seg] + k;
+      x.dynprogindex = w->dynprogindex;
+      x.cdna = c1;
+      x.comp = comp;
+      x.genome = c2;
+      p.push_back(x);
+    }
+    if (seg < 2) {
+      gsnapdp_pair x;
+      memset(&x, 0, sizeof(x));
+      x.querypos = -1;
+      x.genomepos = -1;
+      x.queryjump = GSNAPDP_UNKNOWNJUMP;
+      x.genomejump = GSNAPDP_UNKNOWNJUMP;
+      x.cdna = ' ';
+      x.comp = gapchar;
+      x.genome = ' ';
+      x.gapp = 1;
+      p.push_back(x);
+    }
+  }
+  int n = 0;
+  for (int i = (int)p.size() - 1; i >= 0; i--, n++)
+    if (n < cap) pairs[n] = p[(size_t)i];
+  return n;
+}
+
 // Dynprog_genome_gap's list (dynprog.c:5000-5058): traceback of the right flank
 // (reversed), List_reverse, the gapholder, traceback of the left flank, then
 // List_reverse of the whole -- i.e. the right flank's pairs last-pushed first,

@@ -19,7 +19,7 @@ import os
 import numpy as np
 
 from .records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW,  # noqa: F401
-                      MAXENT_IN, PAIR, RESULT, SJ_WINDOW, WINDOW)
+                      MAXENT_IN, MICRO_RESULT, MICRO_WINDOW, PAIR, RESULT, SJ_WINDOW, WINDOW)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
@@ -87,6 +87,12 @@ def lib():
         L.gsnapdp_sj_run_device.restype = i32
         L.gsnapdp_sj_expand.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32]
         L.gsnapdp_sj_expand.restype = i32
+        L.gsnapdp_micro_run_host.argtypes = [vp, vp, i32, vp, vp, sz, vp]
+        L.gsnapdp_micro_run_host.restype = i32
+        L.gsnapdp_micro_run_device.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+        L.gsnapdp_micro_run_device.restype = i32
+        L.gsnapdp_micro_expand.argtypes = [vp, vp, vp, vp, vp, vp, i32]
+        L.gsnapdp_micro_expand.restype = i32
         _lib = L
     return _lib
 
@@ -295,6 +301,34 @@ class Context:
                                         _p(q), _p(u), _p(out), out.size)
             if n < 0:
                 raise GsnapdpError("gsnapdp_sj_expand failed for window %d" % i)
+            outs.append(out[:n])
+            counts[i] = n
+        return (np.concatenate(outs) if outs else np.zeros(0, PAIR)), counts
+
+    def micro_run(self, windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray) -> np.ndarray:
+        """Dynprog_microexon_int on the GPU.  Returns the MICRO_RESULT records."""
+        w = np.ascontiguousarray(windows, dtype=MICRO_WINDOW)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        res = np.zeros(len(w), dtype=MICRO_RESULT)
+        rc = lib().gsnapdp_micro_run_host(self.h, _p(w), len(w), _p(q), _p(u), q.size, _p(res))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_micro_run_host: %s" % lib().gsnapdp_last_error().decode())
+        return res
+
+    def micro_all_pairs(self, windows, query, query_uc, results):
+        """The lists Dynprog_microexon_int returns, concatenated, and their lengths."""
+        w = np.ascontiguousarray(windows, dtype=MICRO_WINDOW)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        u = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        res = np.ascontiguousarray(results, dtype=MICRO_RESULT)
+        outs, counts = [], np.zeros(len(w), dtype=np.int32)
+        for i in range(len(w)):
+            out = np.zeros(int(w["length1"][i]) + 4, dtype=PAIR)
+            n = lib().gsnapdp_micro_expand(self.h, _p(w[i:i + 1]), _p(res[i:i + 1]), _p(q), _p(u), _p(out),
+                                           out.size)
+            if n < 0:
+                raise GsnapdpError("gsnapdp_micro_expand failed for window %d" % i)
             outs.append(out[:n])
             counts[i] = n
         return (np.concatenate(outs) if outs else np.zeros(0, PAIR)), counts

@@ -148,6 +148,18 @@ void Dynprog_make_splicejunction_3(char* splicejunction, gsnapdp_Genomicpos_T sp
                                    gsnapdp_Splicetype_T far_splicetype,
                                    gsnapdp_bool watsonp);               /* dynprog.c:6149 */
 
+/* --- microexon search (dynprog.h:281-292; _5 / _3 are declared but never
+ * defined by the reference, dynprog.c:7467-7762 is #if 0) --- */
+gsnapdp_List_T Dynprog_microexon_int(
+    double* bestprob2, double* bestprob3, int* dynprogindex, int* microintrontype,
+    char* sequence1, char* sequenceuc1, char* sequence2L, char* sequenceuc2L,
+    char* revsequence2R, char* revsequenceuc2R, int length1, int length2L, int length2R,
+    int offset1, int offset2L, int revoffset2R, int cdna_direction, char* queryseq,
+    char* queryuc, char* genomicseg, char* genomicuc, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genomicpos_T genomiclength, gsnapdp_bool watsonp, gsnapdp_bool use_genomicseg_p,
+    gsnapdp_Pairpool_T pairpool, double defect_rate);                 /* dynprog.c:7128 */
+
 /* --- MaxEnt splice-site probabilities (maxent_hr.h:6-19) --- */
 void Maxent_hr_setup(unsigned int* ref_blocks);                                 /* maxent_hr.c:27195 */
 double Maxent_hr_donor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomicpos_T chroffset);

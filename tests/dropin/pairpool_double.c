@@ -1,18 +1,39 @@
 /* Test double for the host program's Pairpool_push / Pairpool_push_gapholder
- * (reference pairpool.c:169, 352): a list of records in the field order of
- * gsnapdp_pair, so tests can compare the drop-in's List_T with the golden
- * pair lists.  Test infrastructure only; the real host links pairpool.o. */
+ * (reference pairpool.c:169, 352), Pairpool_pop (pairpool.c) and Pair_protect
+ * (pair.c).  Cells use the reference's own List_T / Pair_T layouts (listdef.h,
+ * pairdef.h:9-49), as the real host program's would, so the drop-in sees the
+ * same memory it sees in a gmap/gsnap link; dbl_list_read flattens a list into
+ * gsnapdp_pair records for the tests.  Test infrastructure only; the real host
+ * links pairpool.o / pair.o. */
 #include <stdlib.h>
 #include <string.h>
 
-typedef struct Rec {
+typedef struct PairRec { /* pairdef.h:9-49, field for field */
+  int querypos;
+  unsigned int genomepos;
+  int refquerypos;
+  int aapos;
+  int queryjump;
+  int genomejump;
+  int aaphase_g;
+  int aaphase_e;
+  int dynprogindex;
+  char cdna, comp, genome, aa_g, aa_e;
+  unsigned char gapp, knowngapp, extraexonp, shortexonp;
+  int state, vstate_good, vstate_bad;
+  unsigned char protectedp, disallowedp;
+  double donor_prob, acceptor_prob;
+  unsigned char end_intron_p;
+} PairRec;
+
+typedef struct Rec { /* gsnapdp_pair */
   int querypos, genomepos, queryjump, genomejump, dynprogindex;
   char cdna, comp, genome;
   unsigned char gapp;
 } Rec;
 
-typedef struct List_T {
-  Rec* first;
+typedef struct List_T { /* listdef.h */
+  void* first;
   struct List_T* rest;
 } * List_T;
 
@@ -20,7 +41,7 @@ typedef struct Pairpool_T {
   int dummy;
 } * Pairpool_T;
 
-static List_T cons(List_T list, Rec* r) {
+static List_T cons(List_T list, PairRec* r) {
   List_T n = (List_T)malloc(sizeof(*n));
   n->first = r;
   n->rest = list;
@@ -30,9 +51,9 @@ static List_T cons(List_T list, Rec* r) {
 List_T Pairpool_push(List_T list, Pairpool_T pool, int querypos, int genomepos, char cdna, char comp,
                      char genome, int dynprogindex) {
   (void)pool;
-  Rec* r = (Rec*)calloc(1, sizeof(Rec));
+  PairRec* r = (PairRec*)calloc(1, sizeof(PairRec));
   r->querypos = querypos;
-  r->genomepos = genomepos;
+  r->genomepos = (unsigned int)genomepos;
   r->dynprogindex = dynprogindex;
   r->cdna = cdna;
   r->comp = comp;
@@ -43,24 +64,65 @@ List_T Pairpool_push(List_T list, Pairpool_T pool, int querypos, int genomepos, 
 List_T Pairpool_push_gapholder(List_T list, Pairpool_T pool, int queryjump, int genomejump,
                                unsigned char knownp) {
   (void)pool;
-  Rec* r = (Rec*)calloc(1, sizeof(Rec));
+  PairRec* r = (PairRec*)calloc(1, sizeof(PairRec));
   r->querypos = -1;
-  r->genomepos = -1;
+  r->genomepos = (unsigned int)-1;
   r->queryjump = queryjump;
   r->genomejump = genomejump;
   r->cdna = ' ';
   r->comp = ' ';
   r->genome = ' ';
-  r->gapp = knownp ? 3 : 1; /* gapp | knowngapp << 1, as gsnapdp_pair */
+  r->gapp = 1;
+  r->knowngapp = knownp ? 1 : 0;
+  r->donor_prob = r->acceptor_prob = knownp ? 2.0 : 0.0;
   return cons(list, r);
 }
 
-/* Copy the list (head first) into out[cap]; returns its length. */
+/* pairpool.c Pairpool_pop: the head cell's pair and the rest of the list */
+List_T Pairpool_pop(List_T list, PairRec** x) {
+  List_T rest;
+  if (!list) return NULL;
+  *x = (PairRec*)list->first;
+  rest = list->rest;
+  free(list); /* the pair itself stays (pool memory in the reference) */
+  return rest;
+}
+
+/* pair.c Pair_protect: mark every pair protected, return the list */
+List_T Pair_protect(List_T list) {
+  List_T p;
+  for (p = list; p; p = p->rest) ((PairRec*)p->first)->protectedp = 1;
+  return list;
+}
+
+/* Copy the list (head first) into out[cap] as gsnapdp_pair records (gapp bit 1
+ * = knowngapp); returns its length. */
 int dbl_list_read(List_T list, Rec* out, int cap) {
   int n = 0;
-  for (; list; list = list->rest, n++)
-    if (n < cap) out[n] = *list->first;
+  for (; list; list = list->rest, n++) {
+    const PairRec* p = (const PairRec*)list->first;
+    if (n < cap) {
+      Rec* o = &out[n];
+      memset(o, 0, sizeof(*o));
+      o->querypos = p->querypos;
+      o->genomepos = (int)p->genomepos;
+      o->queryjump = p->gapp ? p->queryjump : 0;
+      o->genomejump = p->gapp ? p->genomejump : 0;
+      o->dynprogindex = p->dynprogindex;
+      o->cdna = p->cdna;
+      o->comp = p->comp;
+      o->genome = p->genome;
+      o->gapp = (unsigned char)((p->gapp ? 1 : 0) | (p->knowngapp ? 2 : 0));
+    }
+  }
   return n;
+}
+
+/* 1 if every pair of the list is protected (Pair_protect) */
+int dbl_list_protected(List_T list) {
+  for (; list; list = list->rest)
+    if (!((PairRec*)list->first)->protectedp) return 0;
+  return 1;
 }
 
 void dbl_list_free(List_T list) {

@@ -381,3 +381,52 @@ def test_dropin_splicejunction_matches_reference_golden(golden_dir, tmp_path):
     assert known > 400
     L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dp)))
     L.Dynprog_term()
+
+
+MICRO_ARGS = ([ctypes.c_void_p] * 4 + [ctypes.c_char_p] * 6 + [ctypes.c_int] * 7 + [ctypes.c_char_p] * 4
+              + [ctypes.c_uint] * 4 + [ctypes.c_ubyte, ctypes.c_ubyte, ctypes.c_void_p, ctypes.c_double])
+
+
+@pytest.mark.gpu
+def test_dropin_microexon_matches_reference_golden(golden_dir, tmp_path):
+    """Dynprog_microexon_int called like traverse_single_gap (stage3.c:5915):
+    out-parameters (probabilities bit for bit) and the list, including the
+    gapholders' comp written in place."""
+    z = np.load(os.path.join(golden_dir, "micro_chr17.npz"), allow_pickle=False)
+    dbl = load_double(tmp_path)
+    L = ctypes.CDLL(DROPIN)
+    L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    L.Dynprog_microexon_int.restype = ctypes.c_void_p
+    L.Dynprog_microexon_int.argtypes = MICRO_ARGS
+    blocks = np.ascontiguousarray(z["blocks"])
+    L.Dynprog_init(600, 10, 11, 10, 8, 0)
+    L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
+    q = np.ascontiguousarray(z["query"])
+    qu = np.ascontiguousarray(z["query_uc"])
+    offs = np.concatenate([[0], np.cumsum(z["npairs"])])
+    out = np.zeros(256, dtype=REC)
+    ref = z["results"]
+    W = z["windows"]
+    for i in range(min(300, len(W))):
+        w, r = W[i], ref[i]
+        p2, p3 = ctypes.c_double(-1), ctypes.c_double(-1)
+        dpi, it = ctypes.c_int(int(w["dynprogindex"])), ctypes.c_int(-77)
+        base_q = q.ctypes.data + int(w["ppos"]) - int(w["offset1"])
+        base_u = qu.ctypes.data + int(w["ppos"]) - int(w["offset1"])
+        lst = L.Dynprog_microexon_int(
+            ctypes.byref(p2), ctypes.byref(p3), ctypes.byref(dpi), ctypes.byref(it),
+            ctypes.c_char_p(q.ctypes.data + int(w["qpos"])), ctypes.c_char_p(qu.ctypes.data + int(w["qpos"])),
+            None, None, None, None, int(w["length1"]), 0, 0, int(w["offset1"]), int(w["offset2L"]),
+            int(w["revoffset2R"]), int(w["cdna_direction"]), ctypes.c_char_p(base_q), ctypes.c_char_p(base_u),
+            None, None, int(w["chroffset"]), int(w["chrhigh"]), int(w["chrpos"]), int(w["genomiclength"]),
+            int(w["watsonp"]), 0, None, float(w["defect_rate"]))
+        assert np.float64(p2.value).tobytes() == np.float64(r["bestprob2"]).tobytes(), i
+        assert np.float64(p3.value).tobytes() == np.float64(r["bestprob3"]).tobytes(), i
+        assert (dpi.value, it.value) == (r["dynprogindex"], r["microintrontype"]), i
+        k = dbl.dbl_list_read(lst, out.ctypes.data, out.size) if lst else 0
+        exp = z["pairs"][offs[i]:offs[i + 1]]
+        assert k == exp.size, (i, k, exp.size)
+        assert out[:k].tobytes() == exp.tobytes(), i
+        if lst:
+            dbl.dbl_list_free(lst)
+    L.Dynprog_term()
