@@ -35,6 +35,12 @@ struct State {
   gsnapdp_ctx* ctx = nullptr;
   bool tables = false;
   bool splicing_iit = false;  // Dynprog_setup got known splice sites
+  // known splice sites and their tries (Dynprog_setup, dynprog.c:350-376)
+  const unsigned* splicesites = nullptr;
+  const int* splicetypes = nullptr;
+  int nsplicesites = 0;
+  unsigned *trieoffsets_obs = nullptr, *triecontents_obs = nullptr;
+  unsigned *trieoffsets_max = nullptr, *triecontents_max = nullptr;
   std::vector<char> q, qu;
   std::vector<uint32_t> ops;
   std::vector<gsnapdp_pair> pairs;
@@ -292,6 +298,43 @@ struct RefList {
   RefList* rest;
 };
 
+// binary_search (dynprog.c:5068-5090)
+int binary_search(int lowi, int highi, const unsigned* positions, unsigned goal) {
+  while (lowi < highi) {
+    const int middlei = (lowi + highi) / 2;
+    if (goal < positions[middlei]) highi = middlei;
+    else if (goal > positions[middlei]) lowi = middlei + 1;
+    else return middlei;
+  }
+  return highi;
+}
+
+// The host program's Splicetrie_solve_end5/3 (splicetrie.c:881, 953).  Weak
+// references: a gmap/gsnap link binds them to its splicetrie.o; a host that
+// loads the shim before its splicetrie code (dlopen) is served by a lookup at
+// the first call.  Without either, the known-site ends fail loudly.
+extern "C" __attribute__((weak)) gsnapdp_List_T Splicetrie_solve_end5(
+    gsnapdp_List_T, unsigned int*, unsigned int*, int, gsnapdp_Genomicpos_T, gsnapdp_Genomicpos_T,
+    int*, int*, int*, int*, int*, gsnapdp_bool*, int*, int*, int, int, gsnapdp_Genomicpos_T, char*,
+    int, int, gsnapdp_Splicetype_T, gsnapdp_Genomicpos_T, gsnapdp_Genomicpos_T, gsnapdp_Genomicpos_T,
+    int, int*, gsnapdp_Dynprog_T, char*, char*, int, int, int, int, int, gsnapdp_bool, gsnapdp_bool,
+    gsnapdp_Pairpool_T, int, double);
+extern "C" __attribute__((weak)) gsnapdp_List_T Splicetrie_solve_end3(
+    gsnapdp_List_T, unsigned int*, unsigned int*, int, gsnapdp_Genomicpos_T, gsnapdp_Genomicpos_T,
+    int*, int*, int*, int*, int*, gsnapdp_bool*, int*, int*, int, int, gsnapdp_Genomicpos_T, char*,
+    int, int, gsnapdp_Splicetype_T, gsnapdp_Genomicpos_T, gsnapdp_Genomicpos_T, gsnapdp_Genomicpos_T,
+    int, int*, gsnapdp_Dynprog_T, char*, char*, int, int, int, int, int, gsnapdp_bool, gsnapdp_bool,
+    gsnapdp_Pairpool_T, int, double);
+using SolveFn = decltype(&Splicetrie_solve_end5);
+
+SolveFn solver(bool end5) {
+  SolveFn f = end5 ? &Splicetrie_solve_end5 : &Splicetrie_solve_end3;
+  if (f) return f;
+  f = (SolveFn)dlsym(RTLD_DEFAULT, end5 ? "Splicetrie_solve_end5" : "Splicetrie_solve_end3");
+  if (!f) fatal("Splicetrie_solve_end5/3 not found: link the host program's splicetrie.o");
+  return f;
+}
+
 }  // namespace
 
 extern "C" {
@@ -317,15 +360,24 @@ char* Dynprog_endalign_string(gsnapdp_Endalign_T endalign) {  // dynprog.c:335-3
   }
 }
 
-// Known-site data only feeds the known-site modes of bridge_intron_gap and the
-// splicejunction paths, which this library does not serve:
-// Dynprog_genome_gap aborts when a splice-site IIT was given.  The genome
-// arrives through Gsnapdp_dropin_genome.
+// The splice sites and their tries feed Dynprog_end5/3_known.  The splicing IIT
+// only feeds the known-site modes of bridge_intron_gap, which this library does
+// not serve: Dynprog_genome_gap aborts when one was given.
+// The genome arrives through Gsnapdp_dropin_genome.
 void Dynprog_setup(gsnapdp_bool, gsnapdp_IIT_T splicing_iit, int*, int, int,
-                   gsnapdp_Genomicpos_T*, gsnapdp_Splicetype_T*, gsnapdp_Genomicpos_T*, int,
-                   unsigned int*, unsigned int*, unsigned int*, unsigned int*, gsnapdp_Genome_T) {
+                   gsnapdp_Genomicpos_T* splicesites, gsnapdp_Splicetype_T* splicetypes,
+                   gsnapdp_Genomicpos_T*, int nsplicesites, unsigned int* trieoffsets_obs,
+                   unsigned int* triecontents_obs, unsigned int* trieoffsets_max,
+                   unsigned int* triecontents_max, gsnapdp_Genome_T) {
   std::lock_guard<std::mutex> lock(g.mu);
   g.splicing_iit = splicing_iit != nullptr;  // dynprog.c:360
+  g.splicesites = splicesites;
+  g.splicetypes = splicetypes;
+  g.nsplicesites = nsplicesites;
+  g.trieoffsets_obs = trieoffsets_obs;
+  g.triecontents_obs = triecontents_obs;
+  g.trieoffsets_max = trieoffsets_max;
+  g.triecontents_max = triecontents_max;
 }
 
 int Dynprog_score(int matches, int mismatches, int qopens, int qindels, int topens, int tindels,
@@ -756,6 +808,240 @@ gsnapdp_List_T Dynprog_microexon_int(
     }
   }
   return list;
+}
+
+// Dynprog_end5_known (dynprog.c:6414-6677): the plain QUERYEND_NOGAPS end gap,
+// then every anchor splice site of the right type in the end's genomic range
+// tried through the host program's Splicetrie_solve_end5 (which calls back
+// into Dynprog_make_splicejunction_5 / Dynprog_end5_splicejunction here), then
+// the reference's fallbacks: BEST_LOCAL when nothing spliced, or the ambiguous
+// part cut off.  Host control flow; every DP runs on the GPU.
+gsnapdp_List_T Dynprog_end5_known(
+    gsnapdp_bool* knownsplicep, int* dynprogindex, int* finalscore, int* ambig_end_length,
+    gsnapdp_Splicetype_T* ambig_splicetype, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* revsequence1, char* revsequenceuc1,
+    char* revsequence2, char* revsequenceuc2, int length1, int length2, int revoffset1,
+    int revoffset2, gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh,
+    gsnapdp_Genomicpos_T chrpos, int genomiclength, gsnapdp_Genomicpos_T knownsplice_limit_low,
+    gsnapdp_Genomicpos_T knownsplice_limit_high, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_end,
+    double defect_rate) {
+  const Dynprog* dp = (const Dynprog*)dynprog;
+  *ambig_end_length = 0;
+  if (length1 <= 0 || length2 <= 0) {  // :6451-6464
+    *finalscore = 0;
+    *knownsplicep = 0;
+    return nullptr;
+  }
+  const int perfect_score = length1 * 3;
+  const SolveFn solve = solver(true);
+  gsnapdp_List_T best_pairs = Dynprog_end5_gap(
+      dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog, revsequence1,
+      revsequenceuc1, revsequence2, revsequenceuc2, length1, length2, revoffset1, revoffset2,
+      chroffset, chrhigh, chrpos, (gsnapdp_Genomicpos_T)genomiclength, cdna_direction, watsonp,
+      jump_late_p, pairpool, extraband_end, defect_rate, GSNAPDP_QUERYEND_NOGAPS, 0);
+  const int orig_score = *finalscore;
+  gsnapdp_List_T orig_pairs = best_pairs;
+  int threshold_miss_score = perfect_score - orig_score;
+  *knownsplicep = 0;
+  int anchor_splicetype = 0;
+  if (threshold_miss_score > 0 && length2 > 0) {  // :6488-6602
+    std::vector<char> splicejunction((size_t)length2 + 1, 0);
+    const int endlength = length1;
+    unsigned low, high;
+    int far_splicetype;
+    if (watsonp) {
+      low = chroffset + chrpos + (unsigned)(revoffset2 - endlength + 2);
+      high = chroffset + chrpos + (unsigned)(revoffset2 + 1);
+      anchor_splicetype = cdna_direction > 0 ? ACCEPTOR : ANTIDONOR;
+      far_splicetype = cdna_direction > 0 ? DONOR : ANTIACCEPTOR;
+    } else {
+      low = chroffset + chrpos + (unsigned)(genomiclength - 1) - (unsigned)revoffset2;
+      high = chroffset + chrpos + (unsigned)(genomiclength - 1) - (unsigned)(revoffset2 - endlength) - 1u;
+      anchor_splicetype = cdna_direction > 0 ? ANTIACCEPTOR : DONOR;
+      far_splicetype = cdna_direction > 0 ? ANTIDONOR : ACCEPTOR;
+    }
+    unsigned far_limit_low = knownsplice_limit_low, far_limit_high = knownsplice_limit_high;
+    int j = binary_search(0, g.nsplicesites, g.splicesites, low);
+    while (j < g.nsplicesites && g.splicesites[j] <= high) {
+      if (g.splicetypes[j] == anchor_splicetype) {
+        const int contlength = watsonp ? (int)(high - g.splicesites[j]) : (int)(g.splicesites[j] - low);
+        const int splicelength = length2 - contlength;
+        // make_contjunction_5 (dynprog.c:5998-6035): the proximal part after the distal one
+        char* proximal = &splicejunction[(size_t)splicelength];
+        if (anchor_splicetype == ACCEPTOR || anchor_splicetype == ANTIDONOR)
+          fill_buffer(g.splicesites[j], (unsigned)contlength, proximal);
+        else
+          fill_buffer(g.splicesites[j] - (unsigned)contlength, (unsigned)contlength, proximal);
+        if (!watsonp) revcomp_inplace(proximal, contlength);
+        if (watsonp) far_limit_high = g.splicesites[j];
+        else far_limit_low = g.splicesites[j];
+        int obsmax_penalty = 0;
+        if (g.trieoffsets_obs != nullptr) {
+          best_pairs = solve(
+              best_pairs, g.triecontents_obs, g.trieoffsets_obs, j, far_limit_low, far_limit_high,
+              finalscore, nmatches, nmismatches, nopens, nindels, knownsplicep, ambig_end_length,
+              &threshold_miss_score, 0, perfect_score, g.splicesites[j], splicejunction.data(),
+              splicelength, contlength, far_splicetype, chroffset, chrhigh, chrpos, genomiclength,
+              dynprogindex, dynprog, revsequence1, revsequenceuc1, length1, length2, revoffset1,
+              revoffset2, cdna_direction, watsonp, jump_late_p, pairpool, extraband_end,
+              defect_rate);
+          obsmax_penalty += 3;  // FULLMATCH
+        }
+        if (threshold_miss_score - obsmax_penalty > 0 && g.trieoffsets_max != nullptr) {
+          best_pairs = solve(
+              best_pairs, g.triecontents_max, g.trieoffsets_max, j, far_limit_low, far_limit_high,
+              finalscore, nmatches, nmismatches, nopens, nindels, knownsplicep, ambig_end_length,
+              &threshold_miss_score, obsmax_penalty, perfect_score, g.splicesites[j],
+              splicejunction.data(), splicelength, contlength, far_splicetype, chroffset, chrhigh,
+              chrpos, genomiclength, dynprogindex, dynprog, revsequence1, revsequenceuc1, length1,
+              length2, revoffset1, revoffset2, cdna_direction, watsonp, jump_late_p, pairpool,
+              extraband_end, defect_rate);
+        }
+      }
+      j++;
+    }
+  }
+  if (best_pairs == nullptr) {  // :6605-6660
+    if (*ambig_end_length == 0) {
+      if (length1 > dp->maxlength1) length1 = dp->maxlength1;
+      if (length2 > dp->maxlength2) length2 = dp->maxlength2;
+      orig_pairs = Dynprog_end5_gap(
+          dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog,
+          revsequence1, revsequenceuc1, revsequence2, revsequenceuc2, length1, length2,
+          revoffset1, revoffset2, chroffset, chrhigh, chrpos, (gsnapdp_Genomicpos_T)genomiclength,
+          cdna_direction, watsonp, jump_late_p, pairpool, extraband_end, defect_rate,
+          GSNAPDP_BEST_LOCAL, 0);
+      *knownsplicep = 0;
+      return orig_pairs;
+    }
+    *ambig_splicetype = anchor_splicetype;
+    orig_pairs = List_reverse(orig_pairs);  // truncate the ambiguous part; querypos increasing
+    while (orig_pairs != nullptr &&
+           ((RefPairHead*)((RefList*)orig_pairs)->first)->querypos < *ambig_end_length) {
+      void* pair;
+      orig_pairs = Pairpool_pop(orig_pairs, &pair);
+    }
+    orig_pairs = List_reverse(orig_pairs);
+    *knownsplicep = 0;
+    *finalscore = orig_score;
+    return orig_pairs;
+  }
+  *ambig_end_length = 0;
+  return *knownsplicep ? Pair_protect(best_pairs) : best_pairs;
+}
+
+// Dynprog_end3_known (dynprog.c:6680-6943), the 3' mirror of the above.
+gsnapdp_List_T Dynprog_end3_known(
+    gsnapdp_bool* knownsplicep, int* dynprogindex, int* finalscore, int* ambig_end_length,
+    gsnapdp_Splicetype_T* ambig_splicetype, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* sequence1, char* sequenceuc1,
+    char* sequence2, char* sequenceuc2, int length1, int length2, int offset1, int offset2,
+    int querylength, gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh,
+    gsnapdp_Genomicpos_T chrpos, int genomiclength, gsnapdp_Genomicpos_T knownsplice_limit_low,
+    gsnapdp_Genomicpos_T knownsplice_limit_high, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_end,
+    double defect_rate) {
+  const Dynprog* dp = (const Dynprog*)dynprog;
+  *ambig_end_length = 0;
+  if (length1 <= 0 || length2 <= 0) {  // :6716-6729
+    *finalscore = 0;
+    *knownsplicep = 0;
+    return nullptr;
+  }
+  const int perfect_score = length1 * 3;
+  const SolveFn solve = solver(false);
+  gsnapdp_List_T best_pairs = Dynprog_end3_gap(
+      dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog, sequence1,
+      sequenceuc1, sequence2, sequenceuc2, length1, length2, offset1, offset2, chroffset,
+      chrhigh, chrpos, (gsnapdp_Genomicpos_T)genomiclength, cdna_direction, watsonp, jump_late_p,
+      pairpool, extraband_end, defect_rate, GSNAPDP_QUERYEND_NOGAPS, 0);
+  const int orig_score = *finalscore;
+  gsnapdp_List_T orig_pairs = best_pairs;
+  int threshold_miss_score = perfect_score - orig_score;
+  *knownsplicep = 0;
+  int anchor_splicetype = 0;
+  if (threshold_miss_score > 0 && length2 > 0) {  // :6753-6866
+    std::vector<char> splicejunction((size_t)length2 + 1, 0);
+    const int endlength = length1;
+    unsigned low, high;
+    int far_splicetype;
+    if (watsonp) {
+      low = chroffset + chrpos + (unsigned)offset2;
+      high = chroffset + chrpos + (unsigned)(offset2 + endlength - 1);
+      anchor_splicetype = cdna_direction > 0 ? DONOR : ANTIACCEPTOR;
+      far_splicetype = cdna_direction > 0 ? ACCEPTOR : ANTIDONOR;
+    } else {
+      low = chroffset + chrpos + (unsigned)(genomiclength - 1) - (unsigned)(offset2 + endlength) + 2u;
+      high = chroffset + chrpos + (unsigned)(genomiclength - 1) - (unsigned)offset2 + 1u;
+      anchor_splicetype = cdna_direction > 0 ? ANTIDONOR : ACCEPTOR;
+      far_splicetype = cdna_direction > 0 ? ANTIACCEPTOR : DONOR;
+    }
+    unsigned far_limit_low = knownsplice_limit_low, far_limit_high = knownsplice_limit_high;
+    int j = binary_search(0, g.nsplicesites, g.splicesites, low);
+    while (j < g.nsplicesites && g.splicesites[j] <= high) {
+      if (g.splicetypes[j] == anchor_splicetype) {
+        const int contlength = watsonp ? (int)(g.splicesites[j] - low) : (int)(high - g.splicesites[j]);
+        const int splicelength = length2 - contlength;
+        // make_contjunction_3 (dynprog.c:6103-6140): the proximal part first
+        char* proximal = splicejunction.data();
+        if (anchor_splicetype == DONOR || anchor_splicetype == ANTIACCEPTOR)
+          fill_buffer(g.splicesites[j] - (unsigned)contlength, (unsigned)contlength, proximal);
+        else
+          fill_buffer(g.splicesites[j], (unsigned)contlength, proximal);
+        if (!watsonp) revcomp_inplace(proximal, contlength);
+        if (watsonp) far_limit_low = g.splicesites[j];
+        else far_limit_high = g.splicesites[j];
+        int obsmax_penalty = 0;
+        if (g.trieoffsets_obs != nullptr) {
+          best_pairs = solve(
+              best_pairs, g.triecontents_obs, g.trieoffsets_obs, j, far_limit_low, far_limit_high,
+              finalscore, nmatches, nmismatches, nopens, nindels, knownsplicep, ambig_end_length,
+              &threshold_miss_score, 0, perfect_score, g.splicesites[j], splicejunction.data(),
+              splicelength, contlength, far_splicetype, chroffset, chrhigh, chrpos, genomiclength,
+              dynprogindex, dynprog, sequence1, sequenceuc1, length1, length2, offset1, offset2,
+              cdna_direction, watsonp, jump_late_p, pairpool, extraband_end, defect_rate);
+          obsmax_penalty += 3;  // FULLMATCH
+        }
+        if (threshold_miss_score - obsmax_penalty > 0 && g.trieoffsets_max != nullptr) {
+          best_pairs = solve(
+              best_pairs, g.triecontents_max, g.trieoffsets_max, j, far_limit_low, far_limit_high,
+              finalscore, nmatches, nmismatches, nopens, nindels, knownsplicep, ambig_end_length,
+              &threshold_miss_score, obsmax_penalty, perfect_score, g.splicesites[j],
+              splicejunction.data(), splicelength, contlength, far_splicetype, chroffset, chrhigh,
+              chrpos, genomiclength, dynprogindex, dynprog, sequence1, sequenceuc1, length1,
+              length2, offset1, offset2, cdna_direction, watsonp, jump_late_p, pairpool,
+              extraband_end, defect_rate);
+        }
+      }
+      j++;
+    }
+  }
+  if (best_pairs == nullptr) {  // :6869-6930
+    if (*ambig_end_length == 0) {
+      if (length1 > dp->maxlength1) length1 = dp->maxlength1;
+      if (length2 > dp->maxlength2) length2 = dp->maxlength2;
+      orig_pairs = Dynprog_end3_gap(
+          dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog, sequence1,
+          sequenceuc1, sequence2, sequenceuc2, length1, length2, offset1, offset2, chroffset,
+          chrhigh, chrpos, (gsnapdp_Genomicpos_T)genomiclength, cdna_direction, watsonp,
+          jump_late_p, pairpool, extraband_end, defect_rate, GSNAPDP_BEST_LOCAL, 0);
+      *knownsplicep = 0;
+      return orig_pairs;
+    }
+    *ambig_splicetype = anchor_splicetype;
+    // truncate the ambiguous part; querypos decreasing
+    while (orig_pairs != nullptr && ((RefPairHead*)((RefList*)orig_pairs)->first)->querypos >=
+                                        querylength - *ambig_end_length) {
+      void* pair;
+      orig_pairs = Pairpool_pop(orig_pairs, &pair);
+    }
+    *knownsplicep = 0;
+    *finalscore = orig_score;
+    return orig_pairs;
+  }
+  *ambig_end_length = 0;
+  return *knownsplicep ? Pair_protect(best_pairs) : best_pairs;
 }
 
 void Maxent_hr_setup(unsigned int* ref_blocks) {  // maxent_hr.c:27195

@@ -47,6 +47,38 @@ gsnapdp_List_T Pairpool_push_gapholder(gsnapdp_List_T list, gsnapdp_Pairpool_T p
                                        int queryjump, int genomejump,
                                        gsnapdp_bool knownp);        /* pairpool.h:28 */
 
+/* --- provided by the host program (reference splicetrie.c, list.c, pairpool.c,
+ * pair.c), used by Dynprog_end5_known / Dynprog_end3_known (the shim references
+ * Splicetrie_solve_end5/3 weakly and looks them up at the first call if the
+ * host loaded the shim first) --- */
+gsnapdp_List_T Splicetrie_solve_end5(
+    gsnapdp_List_T best_pairs, unsigned int* triecontents, unsigned int* trieoffsets, int j,
+    gsnapdp_Genomicpos_T knownsplice_limit_low, gsnapdp_Genomicpos_T knownsplice_limit_high,
+    int* finalscore, int* nmatches, int* nmismatches, int* nopens, int* nindels,
+    gsnapdp_bool* knownsplicep, int* ambig_end_length, int* threshold_miss_score,
+    int obsmax_penalty, int perfect_score, gsnapdp_Genomicpos_T anchor_splicesite,
+    char* splicejunction, int splicelength, int contlength, gsnapdp_Splicetype_T far_splicetype,
+    gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    int genomiclength, int* dynprogindex, gsnapdp_Dynprog_T dynprog, char* revsequence1,
+    char* revsequenceuc1, int length1, int length2, int revoffset1, int revoffset2,
+    int cdna_direction, gsnapdp_bool watsonp, gsnapdp_bool jump_late_p,
+    gsnapdp_Pairpool_T pairpool, int extraband_end, double defect_rate); /* splicetrie.h:32 */
+gsnapdp_List_T Splicetrie_solve_end3(
+    gsnapdp_List_T best_pairs, unsigned int* triecontents, unsigned int* trieoffsets, int j,
+    gsnapdp_Genomicpos_T knownsplice_limit_low, gsnapdp_Genomicpos_T knownsplice_limit_high,
+    int* finalscore, int* nmatches, int* nmismatches, int* nopens, int* nindels,
+    gsnapdp_bool* knownsplicep, int* ambig_end_length, int* threshold_miss_score,
+    int obsmax_penalty, int perfect_score, gsnapdp_Genomicpos_T anchor_splicesite,
+    char* splicejunction, int splicelength, int contlength, gsnapdp_Splicetype_T far_splicetype,
+    gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    int genomiclength, int* dynprogindex, gsnapdp_Dynprog_T dynprog, char* sequence1,
+    char* sequenceuc1, int length1, int length2, int offset1, int offset2, int cdna_direction,
+    gsnapdp_bool watsonp, gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool,
+    int extraband_end, double defect_rate);                           /* splicetrie.h:53 */
+gsnapdp_List_T List_reverse(gsnapdp_List_T list);                    /* list.h */
+gsnapdp_List_T Pairpool_pop(gsnapdp_List_T list, void** x);          /* pairpool.h (Pair_T *x) */
+gsnapdp_List_T Pair_protect(gsnapdp_List_T list);                    /* pair.h */
+
 /* --- setup / workspace (dynprog.h:34-72) --- */
 char* Dynprog_endalign_string(gsnapdp_Endalign_T endalign);                    /* dynprog.c:335 */
 void Dynprog_setup(gsnapdp_bool novelsplicingp, gsnapdp_IIT_T splicesites_iit,
@@ -147,6 +179,28 @@ void Dynprog_make_splicejunction_3(char* splicejunction, gsnapdp_Genomicpos_T sp
                                    int splicelength, int contlength,
                                    gsnapdp_Splicetype_T far_splicetype,
                                    gsnapdp_bool watsonp);               /* dynprog.c:6149 */
+
+/* --- end gaps against known splice sites (dynprog.h:194-236; non-GSNAP-shortcut form) --- */
+gsnapdp_List_T Dynprog_end5_known(
+    gsnapdp_bool* knownsplicep, int* dynprogindex, int* finalscore, int* ambig_end_length,
+    gsnapdp_Splicetype_T* ambig_splicetype, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* revsequence1, char* revsequenceuc1,
+    char* revsequence2, char* revsequenceuc2, int length1, int length2, int revoffset1,
+    int revoffset2, gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh,
+    gsnapdp_Genomicpos_T chrpos, int genomiclength, gsnapdp_Genomicpos_T knownsplice_limit_low,
+    gsnapdp_Genomicpos_T knownsplice_limit_high, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_end,
+    double defect_rate);                                                /* dynprog.c:6414 */
+gsnapdp_List_T Dynprog_end3_known(
+    gsnapdp_bool* knownsplicep, int* dynprogindex, int* finalscore, int* ambig_end_length,
+    gsnapdp_Splicetype_T* ambig_splicetype, int* nmatches, int* nmismatches, int* nopens,
+    int* nindels, gsnapdp_Dynprog_T dynprog, char* sequence1, char* sequenceuc1,
+    char* sequence2, char* sequenceuc2, int length1, int length2, int offset1, int offset2,
+    int querylength, gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh,
+    gsnapdp_Genomicpos_T chrpos, int genomiclength, gsnapdp_Genomicpos_T knownsplice_limit_low,
+    gsnapdp_Genomicpos_T knownsplice_limit_high, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_end,
+    double defect_rate);                                                /* dynprog.c:6680 */
 
 /* --- microexon search (dynprog.h:281-292; _5 / _3 are declared but never
  * defined by the reference, dynprog.c:7467-7762 is #if 0) --- */

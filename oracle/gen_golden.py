@@ -262,6 +262,195 @@ def micro_case(name: str, gseq: np.ndarray, n: int, seed: int) -> None:
     print("%s: %d windows (%d found), %d pairs" % (name, len(b), int(res["found"].sum()), pairs.size))
 
 
+# ----------------------------------------------------------- known splice sites
+DONOR, ANTIDONOR, ACCEPTOR, ANTIACCEPTOR = 0, 1, 2, 3  # splicetrie_build.h:4
+NULL_POINTER = 0xFFFFFFFF                              # splicetrie_build.h:18
+INTERNAL_NODE = 0xFFFFFFFF                             # splicetrie_build.h:23
+KNOWN_IN = np.dtype([(f, "<i4") for f in ("end", "length1", "length2", "offset1", "offset2", "querylength",
+                                          "genomiclength", "cdna_direction", "watsonp", "jump_late_p",
+                                          "extraband_end", "dynprogindex")]
+                    + [(f, "<u4") for f in ("chroffset", "chrhigh", "chrpos", "limit_low", "limit_high", "qpos")]
+                    + [("defect_rate", "<f4"), ("pad", "<i4")])
+KNOWN_OUT = np.dtype([(f, "<i4") for f in ("knownsplicep", "dynprogindex", "finalscore", "ambig_end_length",
+                                           "ambig_splicetype", "nmatches", "nmismatches", "nopens", "nindels",
+                                           "protectedp", "returned_null", "pad")])
+
+
+def _canon(blocks: np.ndarray, n: int) -> np.ndarray:
+    """The characters Genome_fill_buffer_blocks_noterm reads back (ACGT, N where flagged)."""
+    pos = np.arange(n, dtype=np.int64)
+    b = blocks.astype(np.int64)
+    ptr = (pos >> 5) * 3
+    bit = pos & 31
+    word = np.where(bit < 16, b[ptr + 1], b[ptr])
+    code = (word >> ((bit & 15) * 2)) & 3
+    c = np.frombuffer(b"ACGT", np.uint8)[code]
+    return np.where((b[ptr + 2] >> bit) & 1, ord("N"), c).astype(np.uint8)
+
+
+def _revcomp(x: np.ndarray) -> np.ndarray:
+    return W._COMP[x[::-1]]
+
+
+def _junction(canon, end, anchor_site, far_site, contlength, splicelength, anchor_type, far_type, watson):
+    """What Dynprog_make_splicejunction_5/3 + make_contjunction_5/3 (dynprog.c:5998-6188) build."""
+    def fill(left, n):
+        return canon[left:left + n]
+    if end == 5:
+        distal = fill(far_site, splicelength) if far_type in (ACCEPTOR, ANTIDONOR) else \
+            fill(far_site - splicelength, splicelength)
+        prox = fill(anchor_site, contlength) if anchor_type in (ACCEPTOR, ANTIDONOR) else \
+            fill(anchor_site - contlength, contlength)
+        if not watson:
+            distal, prox = _revcomp(distal), _revcomp(prox)
+        return np.concatenate([distal, prox])
+    distal = fill(far_site - splicelength, splicelength) if far_type in (DONOR, ANTIACCEPTOR) else \
+        fill(far_site, splicelength)
+    prox = fill(anchor_site - contlength, contlength) if anchor_type in (DONOR, ANTIACCEPTOR) else \
+        fill(anchor_site, contlength)
+    if not watson:
+        distal, prox = _revcomp(distal), _revcomp(prox)
+    return np.concatenate([prox, distal])
+
+
+def _write_trie(contents: list, leaves: list, rng) -> int:
+    """Append a trie over `leaves` (site indices) in the layout Splicetrie_solve
+    walks (splicetrie.c:255-300): a leaf, a leaf list, or an internal node whose
+    children sit below it.  Returns the offset of its root."""
+    if len(leaves) == 1:  # (a one-leaf list would read as INTERNAL_NODE, -1U)
+        contents.append(leaves[0])
+        return len(contents) - 1
+    if rng.random() < 0.5:
+        contents.append((-len(leaves)) & 0xFFFFFFFF)
+        contents.extend(leaves)
+        return len(contents) - 1 - len(leaves)
+    kids = [[] for _ in range(4)]
+    for x in leaves:
+        kids[int(rng.integers(0, 4))].append(x)
+    roots = [(_write_trie(contents, k, rng) if k else None) for k in kids]
+    contents.append(INTERNAL_NODE)
+    node = len(contents) - 1
+    contents.extend([(node - r) if r is not None else 0 for r in roots])
+    return node
+
+
+def known_case(name: str, gseq: np.ndarray, n: int, seed: int, amb_closest: int = 0) -> None:
+    """Dynprog_end5_known / Dynprog_end3_known over planted known splices."""
+    rng = np.random.default_rng(seed)
+    g = gseq.copy()
+    Gn = g.size
+    canon = _canon(G.pack(g), Gn)
+    w = np.zeros(n, dtype=KNOWN_IN)
+    sites = {}                      # coordinate -> type
+    partners = []                   # (anchor coord, [far coords], [max far coords])
+    qs, us, qpos = [], [], 0
+    for i in range(n):
+        end = 5 if rng.random() < 0.5 else 3
+        watson = int(rng.integers(0, 2))
+        cdir = 1 if rng.random() < 0.5 else -1
+        L1 = int(rng.integers(6, 40))
+        L2 = L1 + 10
+        glen = 1200
+        chrpos = int(rng.integers(6000, Gn - glen - 6000))
+        off2 = int(rng.integers(300, 800))
+        if end == 5:
+            if watson:
+                low, high = chrpos + off2 - L1 + 2, chrpos + off2 + 1
+                at, ft = (ACCEPTOR, DONOR) if cdir > 0 else (ANTIDONOR, ANTIACCEPTOR)
+            else:
+                low, high = chrpos + glen - 1 - off2, chrpos + glen - 1 - (off2 - L1) - 1
+                at, ft = (ANTIACCEPTOR, ANTIDONOR) if cdir > 0 else (DONOR, ACCEPTOR)
+        else:
+            if watson:
+                low, high = chrpos + off2, chrpos + off2 + L1 - 1
+                at, ft = (DONOR, ACCEPTOR) if cdir > 0 else (ANTIACCEPTOR, ANTIDONOR)
+            else:
+                low, high = chrpos + glen - 1 - (off2 + L1) + 2, chrpos + glen - 1 - off2 + 1
+                at, ft = (ANTIDONOR, ANTIACCEPTOR) if cdir > 0 else (ACCEPTOR, DONOR)
+        far_up = (end == 5) == bool(watson)  # far exon upstream in genome coordinates
+        cont = int(rng.integers(1, L1 - 1)) if L1 > 3 else 1
+        from_high = (end == 5 and watson) or (end == 3 and not watson)
+        s0 = high - cont if from_high else low + cont
+        dist = int(rng.integers(200, 4000))
+        f0 = s0 - dist if far_up else s0 + dist
+        fars = [f0] + [f0 + int(d) for d in rng.integers(-150, 150, size=int(rng.integers(0, 3)))]
+        if rng.random() < 0.15:  # a second far site with the same junction: ambiguous
+            spl = L2 - cont
+            f1 = f0 - int(rng.integers(60, 150)) if far_up else f0 + int(rng.integers(60, 150))
+            span0 = (f0 - spl, f0) if ft in (DONOR, ANTIACCEPTOR) else (f0, f0 + spl)
+            g[span0[0] + (f1 - f0):span0[1] + (f1 - f0)] = g[span0[0]:span0[1]]
+            canon = _canon(G.pack(g), Gn)
+            fars.append(f1)
+        J = _junction(canon, end, s0, f0, cont, L2 - cont, at, ft, watson)
+        q = J[L2 - L1:] if end == 5 else J[:L1]
+        q = W._mutate(rng, q, 0.02 if rng.random() < 0.5 else 0.0, 0.0)
+        maxfars = [f0 + int(d) for d in rng.integers(-300, 300, size=int(rng.integers(0, 3)))]
+        if rng.random() < 0.3:
+            maxfars.append(f0)
+        for f in fars + maxfars:
+            sites.setdefault(f, ft)
+        sites[s0] = at
+        for _ in range(int(rng.integers(0, 3))):  # other sites in the range
+            x = int(rng.integers(low, high + 1))
+            sites.setdefault(x, int(rng.integers(0, 4)))
+        if rng.random() < 0.8:
+            partners.append((s0, fars, maxfars))
+        rec = w[i]
+        rec["end"], rec["length1"], rec["length2"] = end, L1, L2
+        rec["offset1"] = int(rng.integers(0, 200)) + (L1 - 1 if end == 5 else 0)
+        rec["offset2"] = off2
+        rec["querylength"] = int(rec["offset1"]) + L1 + 5 if end == 3 else 0
+        rec["genomiclength"], rec["cdna_direction"], rec["watsonp"] = glen, cdir, watson
+        rec["jump_late_p"] = int(rng.integers(0, 2))
+        rec["extraband_end"] = int(rng.choice([3, 3, 5]))
+        rec["dynprogindex"] = int(rng.choice([-1, 2]))
+        rec["chroffset"], rec["chrhigh"], rec["chrpos"] = 0, Gn, chrpos
+        rec["limit_low"], rec["limit_high"] = chrpos - 5000, chrpos + glen + 5000
+        rec["qpos"] = qpos + (L1 - 1 if end == 5 else 0)
+        rec["defect_rate"] = float(rng.choice([0.001, 0.02]))
+        qs += [q, np.full(4, ord("#"), np.uint8)]
+        us += [q, np.full(4, ord("#"), np.uint8)]
+        qpos += L1 + 4
+    coords = np.array(sorted(sites), dtype=np.uint32)
+    types = np.array([sites[c] for c in coords.tolist()], dtype=np.int32)
+    index = {c: k for k, c in enumerate(coords.tolist())}
+    tobs = np.full(coords.size, NULL_POINTER, np.uint32)
+    tmax = np.full(coords.size, NULL_POINTER, np.uint32)
+    cobs, cmax = [], []
+    for s0, fars, maxfars in partners:
+        j = index[s0]
+        if fars and tobs[j] == NULL_POINTER:
+            tobs[j] = _write_trie(cobs, [index[f] for f in fars], rng)
+        if maxfars and tmax[j] == NULL_POINTER:
+            tmax[j] = _write_trie(cmax, [index[f] for f in maxfars], rng)
+    cobs = np.array(cobs, dtype=np.uint32)
+    cmax = np.array(cmax, dtype=np.uint32)
+    blocks = G.pack(g)
+    q, u = np.concatenate(qs), np.concatenate(us)
+    with tempfile.TemporaryDirectory() as d:
+        w.tofile(os.path.join(d, "known_windows.bin"))
+        q.tofile(os.path.join(d, "query.bin"))
+        u.tofile(os.path.join(d, "query_uc.bin"))
+        blocks.astype("<u4").tofile(os.path.join(d, "genome.u32"))
+        coords.tofile(os.path.join(d, "sites.u32"))
+        types.tofile(os.path.join(d, "types.i32"))
+        tobs.tofile(os.path.join(d, "tobs.u32"))
+        cobs.tofile(os.path.join(d, "cobs.u32"))
+        tmax.tofile(os.path.join(d, "tmax.u32"))
+        cmax.tofile(os.path.join(d, "cmax.u32"))
+        subprocess.check_call([DRIVER, "known", d, "0", str(amb_closest)])
+        res = np.fromfile(os.path.join(d, "known_results.bin"), dtype=KNOWN_OUT)
+        npairs = np.fromfile(os.path.join(d, "npairs.i32"), dtype=np.int32)
+        pairs = np.fromfile(os.path.join(d, "pairs.bin"), dtype=PAIR)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), blocks=blocks, windows=w, query=q, query_uc=u,
+                        sites=coords, types=types, tobs=tobs, cobs=cobs, tmax=tmax, cmax=cmax,
+                        amb_closest=np.int32(amb_closest), results=res, npairs=npairs, pairs=pairs)
+    print("%s: %d windows (%d known splices, %d ambiguous cuts, %d null), %d sites, %d pairs" % (
+        name, n, int(res["knownsplicep"].sum()), int((res["ambig_end_length"] > 0).sum()),
+        int(res["returned_null"].sum()), coords.size, pairs.size))
+
+
+
 def maxent_case(name: str, blocks: np.ndarray, glen: int, n: int, seed: int) -> None:
     rng = np.random.default_rng(seed)
     model = rng.integers(0, 4, size=n).astype(np.uint32)
@@ -324,6 +513,7 @@ def main() -> None:
         ("sj_chr17", lambda: sj_case("sj_chr17", chr17, 2000, seed=501)),
         ("mksj_chr17", lambda: mksj_case("mksj_chr17", chr17, 2000, seed=502)),
         ("micro_chr17", lambda: micro_case("micro_chr17", chr17, 1500, seed=601)),
+        ("known_chr17", lambda: known_case("known_chr17", chr17, 600, seed=701)),
         ("maxent_chr17", lambda: maxent_case("maxent_chr17", b17, chr17.size, 20000, seed=301)),
         ("maxent_synth", lambda: maxent_case("maxent_synth", bsyn, synth.size, 6000, seed=302)),
     ]

@@ -13,6 +13,8 @@
  *   ref_driver sj     <dir>   sj_windows.bin query.bin query_uc.bin -> results.bin pairs.bin npairs.i32
  *   ref_driver mksj   <dir>   mksj_in.bin genome.u32 -> mksj_out.bin
  *   ref_driver micro  <dir>   micro_windows.bin query.bin query_uc.bin genome.u32 -> micro_results.bin pairs.bin npairs.i32
+ *   ref_driver known  <dir> 0 [amb_closest]  known_windows.bin query*.bin genome.u32 sites.u32 types.i32
+ *                             [tobs cobs tmax cmax].u32 -> known_results.bin pairs.bin npairs.i32
  *   ref_driver maxent <dir>   maxent_in.bin genome.u32 -> maxent_out.f64
  *   ref_driver pdist  <dir>   -> pdist.i32 (4 x 128 x 128 via Dynprog_pairdistance for HIGHQ only) + consistent probe
  * All inputs use the record layouts of include/gsnapdp.h.
@@ -32,6 +34,7 @@
 #include "pairdef.h"
 #include "pairpool.h"
 #include "splicetrie_build.h"
+#include "splicetrie.h"
 
 /* our record layouts */
 #include "../include/gsnapdp.h"
@@ -418,6 +421,99 @@ static int run_micro(const char *dir) {
   return 0;
 }
 
+/* Dynprog_end5_known / Dynprog_end3_known (dynprog.c:6414, 6680) with known
+ * splice sites and their tries (Dynprog_setup + Splicetrie_setup). */
+typedef struct known_in {
+  int32_t end, length1, length2, offset1, offset2, querylength, genomiclength, cdna_direction;
+  int32_t watsonp, jump_late_p, extraband_end, dynprogindex;
+  uint32_t chroffset, chrhigh, chrpos, limit_low, limit_high, qpos;
+  float defect_rate;
+  int32_t pad;
+} known_in;
+
+typedef struct known_out {
+  int32_t knownsplicep, dynprogindex, finalscore, ambig_end_length, ambig_splicetype;
+  int32_t nmatches, nmismatches, nopens, nindels, protectedp, returned_null, pad;
+} known_out;
+
+static void *slurp_or_null(const char *dir, const char *name, size_t *n) {
+  void *p = slurp(dir, name, n);
+  return *n ? p : NULL;
+}
+
+static int run_known(const char *dir, int amb_closest) {
+  size_t nw, nq, nu, ng, ns, nt, n1, n2, n3, n4;
+  known_in *w = (known_in *)slurp(dir, "known_windows.bin", &nw);
+  char *q = (char *)slurp(dir, "query.bin", &nq);
+  char *qu = (char *)slurp(dir, "query_uc.bin", &nu);
+  UINT4 *g = (UINT4 *)slurp(dir, "genome.u32", &ng);
+  Genomicpos_T *sites = (Genomicpos_T *)slurp(dir, "sites.u32", &ns);
+  Splicetype_T *types = (Splicetype_T *)slurp(dir, "types.i32", &nt);
+  unsigned int *tobs = (unsigned int *)slurp_or_null(dir, "tobs.u32", &n1);
+  unsigned int *cobs = (unsigned int *)slurp_or_null(dir, "cobs.u32", &n2);
+  unsigned int *tmax = (unsigned int *)slurp_or_null(dir, "tmax.u32", &n3);
+  unsigned int *cmax = (unsigned int *)slurp_or_null(dir, "cmax.u32", &n4);
+  int n = (int)(nw / sizeof(known_in)), i;
+  known_out *res = (known_out *)calloc((size_t)n + 1, sizeof(known_out));
+  int32_t *npairs = (int32_t *)calloc((size_t)n + 1, sizeof(int32_t));
+  gsnapdp_pair *tmp = (gsnapdp_pair *)malloc(sizeof(gsnapdp_pair) * PAIRCAP);
+  FILE *fp;
+  char path[4096];
+  Dynprog_T dp = Dynprog_new(600, 10, 11, 10, 8);
+  Pairpool_T pool = Pairpool_new();
+
+  Genome_user_setup(g);
+  Maxent_hr_setup(g);
+  Dynprog_setup(false, NULL, NULL, -1, -1, sites, types, NULL, (int)(ns / 4), tobs, cobs, tmax, cmax,
+                NULL);
+  Splicetrie_setup(sites, NULL, NULL, tobs, cobs, tmax, cmax, false, amb_closest, false, 0);
+  snprintf(path, sizeof(path), "%s/pairs.bin", dir);
+  fp = fopen(path, "wb");
+  for (i = 0; i < n; i++) {
+    known_in *x = &w[i];
+    known_out *o = &res[i];
+    bool known = 77;
+    int dpi = x->dynprogindex, fs = -777, amb = -777, nm = -1, nmm = -1, no = -1, ni = -1, k;
+    Splicetype_T at = (Splicetype_T)77;
+    List_T pairs, p;
+    Pairpool_reset(pool);
+    if (x->end == 5)
+      pairs = Dynprog_end5_known(&known, &dpi, &fs, &amb, &at, &nm, &nmm, &no, &ni, dp,
+                                 q + x->qpos, qu + x->qpos, NULL, NULL, x->length1, x->length2,
+                                 x->offset1, x->offset2, x->chroffset, x->chrhigh, x->chrpos,
+                                 x->genomiclength, x->limit_low, x->limit_high, x->cdna_direction,
+                                 x->watsonp, x->jump_late_p, pool, x->extraband_end,
+                                 (double)x->defect_rate);
+    else
+      pairs = Dynprog_end3_known(&known, &dpi, &fs, &amb, &at, &nm, &nmm, &no, &ni, dp,
+                                 q + x->qpos, qu + x->qpos, NULL, NULL, x->length1, x->length2,
+                                 x->offset1, x->offset2, x->querylength, x->chroffset, x->chrhigh,
+                                 x->chrpos, x->genomiclength, x->limit_low, x->limit_high,
+                                 x->cdna_direction, x->watsonp, x->jump_late_p, pool,
+                                 x->extraband_end, (double)x->defect_rate);
+    o->knownsplicep = known;
+    o->dynprogindex = dpi;
+    o->finalscore = fs;
+    o->ambig_end_length = amb;
+    o->ambig_splicetype = (int32_t)at;
+    o->nmatches = nm;
+    o->nmismatches = nmm;
+    o->nopens = no;
+    o->nindels = ni;
+    o->returned_null = pairs == NULL;
+    o->protectedp = pairs != NULL;
+    for (p = pairs; p != NULL; p = p->rest)
+      if (!((Pair_T)p->first)->protectedp) o->protectedp = 0;
+    k = flatten(pairs, tmp, PAIRCAP);
+    npairs[i] = k;
+    fwrite(tmp, sizeof(gsnapdp_pair), (size_t)(k < PAIRCAP ? k : PAIRCAP), fp);
+  }
+  fclose(fp);
+  spit(dir, "known_results.bin", res, sizeof(known_out) * (size_t)n);
+  spit(dir, "npairs.i32", npairs, sizeof(int32_t) * (size_t)n);
+  return 0;
+}
+
 typedef struct maxent_in {
   uint32_t model, splice_pos, chroffset, pad;
 } maxent_in;
@@ -469,6 +565,7 @@ int main(int argc, char **argv) {
   if (!strcmp(argv[1], "sj")) return run_sj(argv[2]);
   if (!strcmp(argv[1], "mksj")) return run_mksj(argv[2]);
   if (!strcmp(argv[1], "micro")) return run_micro(argv[2]);
+  if (!strcmp(argv[1], "known")) return run_known(argv[2], argc > 4 ? atoi(argv[4]) : 0);
   if (!strcmp(argv[1], "pdist")) return run_pdist(argv[2]);
   return 1;
 }

@@ -5,8 +5,23 @@
  * same memory it sees in a gmap/gsnap link; dbl_list_read flattens a list into
  * gsnapdp_pair records for the tests.  Test infrastructure only; the real host
  * links pairpool.o / pair.o. */
+#include <execinfo.h>
+#include <signal.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
+
+/* a crash inside the shim or the host-side code prints its C frames */
+static void on_segv(int sig) {
+  void* frames[64];
+  int n = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+__attribute__((constructor)) static void install_segv_handler(void) {
+  if (getenv("DBL_BACKTRACE")) signal(SIGSEGV, on_segv);
+}
 
 typedef struct PairRec { /* pairdef.h:9-49, field for field */
   int querypos;
@@ -86,6 +101,17 @@ List_T Pairpool_pop(List_T list, PairRec** x) {
   rest = list->rest;
   free(list); /* the pair itself stays (pool memory in the reference) */
   return rest;
+}
+
+/* list.c List_reverse */
+List_T List_reverse(List_T list) {
+  List_T head = NULL, next;
+  for (; list; list = next) {
+    next = list->rest;
+    list->rest = head;
+    head = list;
+  }
+  return head;
 }
 
 /* pair.c Pair_protect: mark every pair protected, return the list */

@@ -41,6 +41,25 @@ def test_dropin_exports_every_declared_entry_point():
     assert "Pairpool_push" in undef and "Pairpool_push_gapholder" in undef
 
 
+# Every function dynprog.o and maxent_hr.o define in a non-PMAP build (nm of
+# the reference compiled from its sources, oracle/_ref): the drop-in must
+# export all of them for gmap / gsnap to link against it instead.
+REFERENCE_DEFINED = (
+    "Dynprog_cdna_gap Dynprog_end3_gap Dynprog_end3_known Dynprog_end3_splicejunction Dynprog_end5_gap "
+    "Dynprog_end5_known Dynprog_end5_splicejunction Dynprog_endalign_string Dynprog_free Dynprog_genome_gap "
+    "Dynprog_init Dynprog_make_splicejunction_3 Dynprog_make_splicejunction_5 Dynprog_microexon_int "
+    "Dynprog_new Dynprog_pairdistance Dynprog_score Dynprog_setup Dynprog_single_gap Dynprog_term "
+    "Maxent_hr_acceptor_prob Maxent_hr_antiacceptor_prob Maxent_hr_antidonor_prob Maxent_hr_donor_prob "
+    "Maxent_hr_setup").split()
+
+
+def test_dropin_exports_everything_the_reference_defines():
+    out = subprocess.run(["nm", "-D", "--defined-only", DROPIN], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r" T (\w+)", out))
+    assert not [f for f in REFERENCE_DEFINED if f not in exported]
+
+
 def test_dropin_host_helpers_match_reference(tmp_path):
     """Dynprog_new's length limits (dynprog.c:831-852), Dynprog_score (:381) and
     Dynprog_pairdistance (:1049) need no GPU."""
@@ -429,4 +448,87 @@ def test_dropin_microexon_matches_reference_golden(golden_dir, tmp_path):
         assert out[:k].tobytes() == exp.tobytes(), i
         if lst:
             dbl.dbl_list_free(lst)
+    L.Dynprog_term()
+
+
+REF_SPLICETRIE = os.path.join(ROOT, "oracle", "_ref", "libref_splicetrie.so")
+KNOWN_ARGS = ([ctypes.c_void_p] * 10 + [ctypes.c_char_p] * 4 + [ctypes.c_int] * 4)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_SPLICETRIE),
+                    reason="the host-program side (reference splicetrie.c) is built by `make -C oracle ref`")
+def test_dropin_known_splicing_matches_reference_golden(golden_dir, tmp_path):
+    """Dynprog_end5_known / Dynprog_end3_known (dynprog.c:6414, 6680) with known
+    splice sites and tries, the host program's Splicetrie_solve_end5/3 being the
+    reference's own splicetrie.c calling back into the drop-in: every
+    out-parameter, the list and its protection, against the reference run
+    end to end (the golden vectors)."""
+    z = np.load(os.path.join(golden_dir, "known_chr17.npz"), allow_pickle=False)
+    dbl = load_double(tmp_path)
+    dbl.dbl_list_protected.argtypes = [ctypes.c_void_p]
+    L = ctypes.CDLL(DROPIN, mode=ctypes.RTLD_GLOBAL)       # Dynprog_* for the splicetrie code
+    S = ctypes.CDLL(REF_SPLICETRIE, mode=ctypes.RTLD_GLOBAL)  # Splicetrie_solve_end5/3 for the shim
+    L.Dynprog_new.restype = ctypes.c_void_p
+    L.Dynprog_new.argtypes = [ctypes.c_int] * 5
+    L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    blocks = np.ascontiguousarray(z["blocks"])
+    sites = np.ascontiguousarray(z["sites"])
+    types = np.ascontiguousarray(z["types"])
+    tries = [np.ascontiguousarray(z[k]) for k in ("tobs", "cobs", "tmax", "cmax")]
+    tp = [t.ctypes.data if t.size else None for t in tries]
+    S.Splicetrie_setup.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_ubyte] * 3 + [ctypes.c_int]
+    S.Splicetrie_setup(sites.ctypes.data, None, None, tp[0], tp[1], tp[2], tp[3], 0, int(z["amb_closest"]), 0, 0)
+    L.Dynprog_init(600, 10, 11, 10, 8, 0)
+    L.Dynprog_setup.argtypes = ([ctypes.c_ubyte, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+                                + [ctypes.c_void_p] * 3 + [ctypes.c_int] + [ctypes.c_void_p] * 5)
+    L.Dynprog_setup(0, None, None, -1, -1, sites.ctypes.data, types.ctypes.data, None, sites.size,
+                    tp[0], tp[1], tp[2], tp[3], None)
+    L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
+    L.Maxent_hr_setup.argtypes = [ctypes.c_void_p]
+    L.Maxent_hr_setup(blocks.ctypes.data)
+    dp = L.Dynprog_new(600, 10, 11, 10, 8)
+    L.Dynprog_end5_known.restype = ctypes.c_void_p
+    L.Dynprog_end3_known.restype = ctypes.c_void_p
+    tail = [ctypes.c_uint] * 3 + [ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_int, ctypes.c_ubyte,
+                                  ctypes.c_ubyte, ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
+    L.Dynprog_end5_known.argtypes = KNOWN_ARGS + tail
+    L.Dynprog_end3_known.argtypes = KNOWN_ARGS + [ctypes.c_int] + tail
+    q = np.ascontiguousarray(z["query"])
+    qu = np.ascontiguousarray(z["query_uc"])
+    offs = np.concatenate([[0], np.cumsum(z["npairs"])])
+    out = np.zeros(1024, dtype=REC)
+    ref = z["results"]
+    for i, w in enumerate(z["windows"]):
+        r = ref[i]
+        known = ctypes.c_ubyte(77)
+        ints = [ctypes.c_int(int(w["dynprogindex"]))] + [ctypes.c_int(-777) for _ in range(7)]
+        dpi, fs, amb, at, nm, nmm, no, ni = ints
+        head = ([ctypes.byref(known)] + [ctypes.byref(x) for x in ints] + [dp]
+                + [ctypes.c_char_p(q.ctypes.data + int(w["qpos"])), ctypes.c_char_p(qu.ctypes.data + int(w["qpos"])),
+                   None, None] + [int(w[f]) for f in ("length1", "length2", "offset1", "offset2")])
+        # the reference passes the Splicetype_T* as ambig_splicetype: reorder (known, dpi, fs, amb, at, ...)
+        head[1:9] = [ctypes.byref(dpi), ctypes.byref(fs), ctypes.byref(amb), ctypes.byref(at), ctypes.byref(nm),
+                     ctypes.byref(nmm), ctypes.byref(no), ctypes.byref(ni)]
+        rest = ([int(w["chroffset"]), int(w["chrhigh"]), int(w["chrpos"]), int(w["genomiclength"]),
+                 int(w["limit_low"]), int(w["limit_high"]), int(w["cdna_direction"]), int(w["watsonp"]),
+                 int(w["jump_late_p"]), None, int(w["extraband_end"]), float(w["defect_rate"])])
+        if w["end"] == 5:
+            lst = L.Dynprog_end5_known(*head, *rest)
+        else:
+            lst = L.Dynprog_end3_known(*head, int(w["querylength"]), *rest)
+        got = [known.value, dpi.value, fs.value, amb.value, nm.value, nmm.value, no.value, ni.value]
+        want = [int(r[f]) for f in ("knownsplicep", "dynprogindex", "finalscore", "ambig_end_length", "nmatches",
+                                    "nmismatches", "nopens", "nindels")]
+        assert got == want, (i, got, want)
+        if r["ambig_end_length"] > 0:
+            assert at.value == r["ambig_splicetype"], i
+        assert (lst is None) == bool(r["returned_null"]), i
+        k = dbl.dbl_list_read(lst, out.ctypes.data, out.size) if lst else 0
+        exp = z["pairs"][offs[i]:offs[i + 1]]
+        assert k == exp.size, (i, k, exp.size)
+        assert out[:k].tobytes() == exp.tobytes(), i
+        if lst:
+            assert dbl.dbl_list_protected(lst) == r["protectedp"], i
+    L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dp)))
     L.Dynprog_term()
