@@ -465,7 +465,9 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
         af = push_sign(af, df);
         ae = push_sign(ae, de);
       }
+#ifndef EXP_NOMATCH
       macc = s == 0 ? __builtin_amdgcn_ubfe(pw, msh, 1) : (macc << 1) | __builtin_amdgcn_ubfe(pw, msh, 1);
+#endif
       E[s] = max(a, Er);
       const int f = max(b, fp);
       F[s] = f;
@@ -496,7 +498,9 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       const uint32_t acc = (((((av << S) | ah) << S) | af) << S) | ae;
 #ifndef EXP_NOSTORE
       D[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = acc;
+#ifndef EXP_NOMATCH
       M[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = (uint8_t)macc;
+#endif
 #else
       if (acc == 0x12345678u && macc == 77u) D[0] = 1u;
 #endif
