@@ -193,6 +193,87 @@ def measure_c5(genome, nreads, steps, warmup, dev, with_cpu):
     return out
 
 
+def timed(step, sync, steps, warmup):
+    for _ in range(warmup):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    return time.perf_counter() - t0
+
+
+def measure_sj(genome, n, steps, warmup, dev, with_cpu):
+    """Side measurement: Dynprog_end5/3_splicejunction (the known-splice end
+    candidates Splicetrie_solve_end5/3 issue), device-resident; CPU restatement
+    (1 core) on a sample beside it."""
+    b = W.sj_windows(genome, n, seed=9, mix=False)
+    ctx = Context(np.zeros(64, np.uint32), mode=0, device=dev.index)
+    off = op_offsets(b.windows)
+    d_w = torch.from_numpy(b.windows.view(np.uint8).copy()).to(dev)
+    d_q = torch.from_numpy(b.query.copy()).to(dev)
+    d_u = torch.from_numpy(b.query_uc.copy()).to(dev)
+    d_off = torch.from_numpy(off.copy()).to(dev)
+    d_res = torch.zeros(n * RESULT.itemsize, dtype=torch.uint8, device=dev)
+    d_ops = torch.zeros(int(off[-1]) + 1, dtype=torch.int32, device=dev)
+    el = timed(lambda: ctx.sj_run_device(d_w.data_ptr(), n, d_q.data_ptr(), d_u.data_ptr(), d_res.data_ptr(),
+                                         d_ops.data_ptr(), d_off.data_ptr()), ctx.sync, steps, warmup)
+    out = {"workload": "Dynprog_end5/3_splicejunction: %d junction end gaps per step (length1 1-160, "
+                       "length2 = length1 + 10..40, extraband_end 3)" % n,
+           "value": round(n * steps / el, 1), "unit": "windows/s", "ms_per_step": round(1000 * el / steps, 4)}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        O.setup(np.zeros(16, np.uint32))
+        sample = min(n, 20_000)
+        t1 = time.perf_counter()
+        ores, _, _, _ = O.run_sj_batch(b.windows[:sample], b.query, b.query_uc)
+        cpu = sample / (time.perf_counter() - t1)
+        res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=RESULT)[:sample]
+        out["cpu_baseline"] = {"value": round(cpu, 1), "unit": "windows/s", "cores": 1, "kind": "port",
+                               "sample": "%d windows, oracle/ restatement, 1 thread" % sample}
+        out["parity_bit_exact"] = bool(all(np.array_equal(res[f], ores[f]) for f in
+                                           ("finalscore", "nmatches", "nmismatches", "nopens", "nindels")))
+    ctx.close()
+    return out
+
+
+def measure_micro(genome, n, steps, warmup, dev, with_cpu):
+    """Side measurement: Dynprog_microexon_int (intron gaps of 40-800 nt with a
+    planted 3-12 nt microexon), device-resident; CPU restatement (1 core) on a
+    sample beside it."""
+    from gsnapdp.records import MICRO_RESULT
+    g, b = W.micro_windows(genome[:8_000_000], n, seed=10, mix=False)
+    blocks = W.pack_genome(g)
+    ctx = Context(blocks, mode=0, device=dev.index)
+    d_w = torch.from_numpy(b.windows.view(np.uint8).copy()).to(dev)
+    d_q = torch.from_numpy(b.query.copy()).to(dev)
+    d_u = torch.from_numpy(b.query_uc.copy()).to(dev)
+    d_res = torch.zeros(n * MICRO_RESULT.itemsize, dtype=torch.uint8, device=dev)
+    el = timed(lambda: ctx.micro_run_device(d_w.data_ptr(), n, d_q.data_ptr(), d_u.data_ptr(), d_res.data_ptr()),
+               ctx.sync, steps, warmup)
+    out = {"workload": "Dynprog_microexon_int: %d intron gaps per step (span 40-800 nt, planted microexon)" % n,
+           "value": round(n * steps / el, 1), "unit": "windows/s", "ms_per_step": round(1000 * el / steps, 4)}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        O.setup(blocks)
+        sample = min(n, 5_000)
+        t1 = time.perf_counter()
+        ores, _, _, _ = O.run_micro_batch(b.windows[:sample], b.query, b.query_uc)
+        cpu = sample / (time.perf_counter() - t1)
+        res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=MICRO_RESULT)[:sample]
+        out["cpu_baseline"] = {"value": round(cpu, 1), "unit": "windows/s", "cores": 1, "kind": "port",
+                               "sample": "%d windows, oracle/ restatement, 1 thread" % sample}
+        out["parity_bit_exact"] = bool(all(np.array_equal(res[f], ores[f]) for f in
+                                           ("found", "microintrontype", "dynprogindex", "bestcL", "bestcR")) and
+                                       np.array_equal(res["bestprob2"].view(np.uint64),
+                                                      ores["bestprob2"].view(np.uint64)))
+    ctx.close()
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,6 +284,8 @@ def main() -> None:
     ap.add_argument("--no-c4", action="store_true", help="skip the config-4 (genome gap) side line")
     ap.add_argument("--c4-windows", type=int, default=C4_WINDOWS)
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 (GSNAP windows) side line")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the splice-junction / microexon side lines")
     args = ap.parse_args()
 
     ranks = shard.init_from_env("nccl")
@@ -330,6 +413,9 @@ def main() -> None:
             out["c4"] = measure_c4(genome, args.c4_windows, args.steps, args.warmup, dev, not args.no_cpu)
         if not args.no_c5 and world == 1:
             out["c5"] = measure_c5(genome, C5_READS, args.steps, args.warmup, dev, not args.no_cpu)
+        if not args.no_extra and world == 1:
+            out["splicejunction"] = measure_sj(genome, 100_000, args.steps, args.warmup, dev, not args.no_cpu)
+            out["microexon"] = measure_micro(genome, 20_000, args.steps, args.warmup, dev, not args.no_cpu)
         print(json.dumps(out), flush=True)
     shard.finish(ranks)
     ctx.close()

@@ -287,6 +287,23 @@ class Context:
             raise GsnapdpError("gsnapdp_sj_run_host: %s" % lib().gsnapdp_last_error().decode())
         return res, ops, off
 
+    def sj_run_device(self, d_windows: int, n: int, d_query: int, d_query_uc: int, d_results: int, d_ops: int,
+                      d_op_offsets: int, stream: int = 0) -> None:
+        rc = lib().gsnapdp_sj_run_device(self.h, ctypes.c_void_p(d_windows), n, ctypes.c_void_p(d_query),
+                                         ctypes.c_void_p(d_query_uc), ctypes.c_void_p(d_results),
+                                         ctypes.c_void_p(d_ops), ctypes.c_void_p(d_op_offsets),
+                                         ctypes.c_void_p(stream) if stream else None)
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_sj_run_device: %s" % lib().gsnapdp_last_error().decode())
+
+    def micro_run_device(self, d_windows: int, n: int, d_query: int, d_query_uc: int, d_results: int,
+                         stream: int = 0) -> None:
+        rc = lib().gsnapdp_micro_run_device(self.h, ctypes.c_void_p(d_windows), n, ctypes.c_void_p(d_query),
+                                            ctypes.c_void_p(d_query_uc), ctypes.c_void_p(d_results),
+                                            ctypes.c_void_p(stream) if stream else None)
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_micro_run_device: %s" % lib().gsnapdp_last_error().decode())
+
     def sj_all_pairs(self, windows, query, query_uc, results, ops, off):
         """The lists Dynprog_end5/3_splicejunction return, concatenated, and their lengths."""
         w = np.ascontiguousarray(windows, dtype=SJ_WINDOW)
