@@ -652,13 +652,16 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   fetch_group(ga, G, jj);
   fetch_group(gb, G >= 1 ? G - 1 : 0, jj);
   const uint32_t invall = JL ? 0xFFFFFFFFu : 0u;
-  bool fast4 = false;
-  for (int c = maxL2; c >= 0; c--) {
-    const int k = c & 3;
-    if (k == 3) {
+  // one iteration per 4-column group G; its columns are visited one by one
+  // only when some lane of the wave cannot take the group in one bulk step
+  for (; G >= 0; G--) {
+    const int chi = min(4 * G + 3, maxL2);  // the first group may be partial
+    bool fast4 = false;
+    if (chi == 4 * G + 3) {
       // Four diagonal steps at once: the path stays on its diagonal through
       // columns c .. c-3 (no v1/h1 there), inside the band and the query, and
       // the four columns are all inside or all outside the window's genome.
+      const int c = chi;
       const int dd = (S - 1 - pb) + jj * S - stop;  // the diagonal's offset in the band
       fast4 = st == T_DIAG && jj == ga.jw && r >= 4 && c >= 4 && dd >= 0 && dd <= wband;
       if (fast4) {
@@ -680,18 +683,24 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
         }
       }
     }
-    if (!fast4 && st != T_DONE && (st != T_WAIT || c == L2)) {
-      const uint32_t wk = k == 0 ? ga.w[0] : k == 1 ? ga.w[1] : k == 2 ? ga.w[2] : ga.w[3];
-      const uint32_t mk = k == 0 ? ga.m[0] : k == 1 ? ga.m[1] : k == 2 ? ga.m[2] : ga.m[3];
-      column(c, wk, mk, ga.jw);
+    // lanes with nothing to do in this group: bulk-stepped, done, or still
+    // waiting for their own L2
+    const bool idle = fast4 || st == T_DONE || (st == T_WAIT && L2 < 4 * G);
+    if (__builtin_amdgcn_ballot_w64(!idle) != 0) {
+      for (int c = chi; c >= 4 * G; c--) {
+        const int k = c & 3;
+        if (!fast4 && st != T_DONE && (st != T_WAIT || c == L2)) {
+          const uint32_t wk = k == 0 ? ga.w[0] : k == 1 ? ga.w[1] : k == 2 ? ga.w[2] : ga.w[3];
+          const uint32_t mk = k == 0 ? ga.m[0] : k == 1 ? ga.m[1] : k == 2 ? ga.m[2] : ga.m[3];
+          column(c, wk, mk, ga.jw);
+        }
+      }
     }
-    if (k == 0) {  // leaving group G
-      if (__builtin_amdgcn_ballot_w64(st != T_DONE) == 0) break;
-      ga = gb;
-      G--;
-      if (G >= 1) fetch_group(gb, G - 1, jj);  // the path's diagonal, predicted unchanged
-      fast4 = false;
-    }
+    // leaving group G
+    if (__builtin_amdgcn_ballot_w64(st != T_DONE) == 0) break;
+    ga = gb;
+    if (G >= 1 && ga.jw != jj) fetch_group(ga, G - 1, jj);  // a gap moved the path to another lane
+    if (G >= 2) fetch_group(gb, G - 2, jj);  // the path's diagonal, predicted unchanged
   }
   if (st != T_DONE && st != T_WAIT) column(-1, 0u, 0u, -1);
   ow.flush();

@@ -10,7 +10,7 @@ from gsnapdp.records import RESULT
 
 genome = W.synthetic_genome(64_000_000, seed=1)
 blocks = W.pack_genome(genome)
-batch = W.c2_windows(genome, n=100_000, seed=2)
+batch = W.c2_windows(genome, n=100_000, seed=2, indel_frac=float(os.environ.get("INDEL_FRAC", "0.3")))
 n = len(batch)
 off = op_offsets(batch.windows)
 ctx = Context(blocks, mode=0, device=0)
