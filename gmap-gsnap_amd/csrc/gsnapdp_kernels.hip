@@ -261,7 +261,14 @@ __device__ inline uint32_t fill_profile_word(uint32_t w) {
   return o;
 }
 constexpr int UTAB = 4 * 128;  // LDS profile: 4 x 128 pairdistance words, then 256 uppercase words
-constexpr int SPROF_WORDS = 4 * 128 + 256;
+constexpr int MLUT = UTAB + 256;  // then 32 uint64: the 5 match bits of a profile word spread to bit 7 of bytes 0..4
+constexpr int SPROF_WORDS = MLUT + 64;
+__host__ __device__ constexpr uint64_t spread_match(uint32_t m5) {
+  uint64_t x = 0;
+  for (int k = 0; k < 5; k++)
+    if ((m5 >> k) & 1u) x |= (uint64_t)1 << (8 * k + 7);
+  return x;
+}
 
 __device__ inline uint32_t push_sign(uint32_t acc, int d) {
   return __builtin_amdgcn_alignbit(acc, (uint32_t)d, 31u);  // (acc << 1) | (d < 0)
@@ -353,6 +360,15 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
 
   int H[S], E[S], F[S];
   uint32_t P[S];
+  // Match bits of the lane's S rows against each genome class: byte k of MB
+  // holds, in bits 0..S-1, whether slot s's query row matches class k
+  // (consistent_array or uppercase equality, dynprog.c:2650-2656).  The rows
+  // move up one slot per column, so MB shifts right by one and the entering
+  // row's bits come in at bit S-1 of each byte (from the LDS lookup table).
+  const uint64_t* mlut = (const uint64_t*)(sprof + MLUT);
+  constexpr uint64_t MB_KEEP = 0x0101010101ull * ((1u << (S - 1)) - 1u);
+  auto row_spread = [&](uint32_t pw) -> uint64_t { return mlut[(pw >> 24) & 31u] >> (8 - S); };
+  uint64_t MB = 0;
   // column 0 (dynprog.c:1460-1488) in offset coordinates
 #pragma unroll
   for (int s = 0; s < S; s++) {
@@ -361,6 +377,7 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
     E[s] = NEG;
     F[s] = (r >= 1) ? open : NEG;  // open + r*ext - r*ext
     P[s] = row_word(r);
+    MB = ((MB >> 1) & MB_KEEP) | row_spread(P[s]);
   }
   // Rings: lane j of a window stages the rows / columns congruent to j mod
   // LPW.  Lane j's bottom slot holds row t + j*(S-1) + rbase at step t, its
@@ -440,7 +457,7 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       }
     }
     // four bit planes (v1, h1, dF, dE), each a short independent chain
-    uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u, macc = 0u, gsh = 0u, msh = 0u;
+    uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u, gsh = 0u;
     auto cell = [&](int s, int Hr, int Er) {
       const int Hd = H[s], Ed = E[s], Fd = F[s];
       const uint32_t pw = P[s];
@@ -465,9 +482,6 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
         af = push_sign(af, df);
         ae = push_sign(ae, de);
       }
-#ifndef EXP_NOMATCH
-      macc = s == 0 ? __builtin_amdgcn_ubfe(pw, msh, 1) : (macc << 1) | __builtin_amdgcn_ubfe(pw, msh, 1);
-#endif
       E[s] = max(a, Er);
       const int f = max(b, fp);
       F[s] = f;
@@ -475,12 +489,14 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       hp = hn;
       fp = f;
     };
+    uint32_t macc = 0u;  // this column's match bits, bit s = slot s
     if (act) {
 #pragma unroll
       for (int s = 0; s < S - 1; s++) P[s] = P[s + 1];
       P[S - 1] = pnext;
+      MB = ((MB >> 1) & MB_KEEP) | row_spread(pnext);
       gsh = 4u * (uint32_t)gnext;
-      msh = 24u + (uint32_t)gnext;
+      macc = (uint32_t)(MB >> (8u * (uint32_t)gnext));
       cell(0, H[1], E[1]);
     }
     int hb = NEG, eb = NEG;  // old (nogap, gap1) just below the lowest local slot
@@ -629,7 +645,7 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       } else {
         const uint32_t x = ((jj == jw) ? wk : ldw(c, jj)) >> pb;
         if (c >= cvlo && c <= cvhi) {  // not a '*' column (dynprog.c:2644)
-          const uint32_t mb = (((jj == jw) ? mk : ldm(c, jj)) >> pb) & 1u;
+          const uint32_t mb = (((jj == jw) ? mk : ldm(c, jj)) >> (S - 1 - pb)) & 1u;
           tal.nmatches += (int)mb;
           tal.nmismatches += 1 - (int)mb;
         }
@@ -673,8 +689,9 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
         fast4 = ((x0 | x1 | x2 | x3) & vh) == 0u && (inside || outside);
         if (fast4) {
           if (inside) {
-            const int mcount = (int)(((ga.m[0] >> pb) & 1u) + ((ga.m[1] >> pb) & 1u) +
-                                     ((ga.m[2] >> pb) & 1u) + ((ga.m[3] >> pb) & 1u));
+            const int mb = S - 1 - pb;  // match bit of the diagonal's slot
+            const int mcount = (int)(((ga.m[0] >> mb) & 1u) + ((ga.m[1] >> mb) & 1u) +
+                                     ((ga.m[2] >> mb) & 1u) + ((ga.m[3] >> mb) & 1u));
             tal.nmatches += mcount;
             tal.nmismatches += 4 - mcount;
           }
@@ -760,10 +777,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
     const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
     uint32_t* __restrict__ dirpool, size_t wave_stride, gsnapdp_result* __restrict__ res,
     uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
-  __shared__ uint32_t sprof[SPROF_WORDS];
+  __shared__ alignas(8) uint32_t sprof[SPROF_WORDS];
   __shared__ uint32_t rings[4][RING_WORDS_MAX];  // one per wave of the block
-  for (int i = threadIdx.x; i < SPROF_WORDS; i += blockDim.x)
+  for (int i = threadIdx.x; i < MLUT; i += blockDim.x)
     sprof[i] = i < UTAB ? fill_profile_word(prof[i]) : (i - UTAB < 128 ? prof[i] : 0u);
+  for (int i = threadIdx.x; i < 32; i += blockDim.x) {
+    const uint64_t x = spread_match((uint32_t)i);
+    sprof[MLUT + 2 * i] = (uint32_t)x;
+    sprof[MLUT + 2 * i + 1] = (uint32_t)(x >> 32);
+  }
   __syncthreads();
   uint32_t* ring = rings[threadIdx.x >> 6];
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
