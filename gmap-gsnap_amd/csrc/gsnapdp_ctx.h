@@ -13,11 +13,13 @@ void gsnapdp__set_err(const std::string& s);
 struct gsnapdp_ctx;
 // per-stage HIP events around a launch (gsnapdp_profile); stage < 16
 void gsnapdp__mark(gsnapdp_ctx* ctx, hipStream_t st, int stage, int end);
-// k_rows over the three row-lane class lists (gsnapdp_ggap.hip)
+// k_rows over the RW_NCLS row-lane class lists (gsnapdp_ggap.hip)
 int gsnapdp__rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d_windows,
                          const int* lists, const int* counts, int list_cap, const char* d_query,
                          const char* d_query_uc, gsnapdp_result* d_results, uint32_t* d_ops,
                          const int64_t* d_op_offsets);
+// allocate the row-lane classes' global scratch on first use
+int gsnapdp__rows_pools(gsnapdp_ctx* ctx);
 
 #define HIPCHK(x)                                                                        \
   do {                                                                                   \
@@ -48,7 +50,8 @@ struct gsnapdp_ctx {
   size_t perm_cap = 0;
   uint32_t* d_dirpool = nullptr;
   size_t dirpool_waves = 0;
-  uint32_t* d_bigpool = nullptr;   // global scratch of the large row-lane windows (k_rows)
+  uint32_t* d_bigpool = nullptr;   // global scratch of the largest row-lane windows (k_rows)
+  uint32_t* d_largepool = nullptr; // global scratch of the RW_LARGE row-lane windows
   // host-run staging
   size_t stage_cap = 0;
   void* d_stage = nullptr;

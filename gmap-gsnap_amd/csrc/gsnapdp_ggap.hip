@@ -1243,28 +1243,49 @@ __global__ void k_cgap_plan(const gsnapdp_cgap_window* __restrict__ Wn, int n,
 // ======================================================================
 // Host side (include/gsnapdp.h: gsnapdp_ggap_*; k_rows for gsnapdp_run_device)
 // ======================================================================
+// global scratch of the row-lane classes that do not fit LDS, on first use
+int gsnapdp__rows_pools(gsnapdp_ctx* ctx) {
+  if (!ctx->d_bigpool) HIPCHK(hipMalloc(&ctx->d_bigpool, (size_t)RW_BIG_WAVES * RW_BIG_WORDS * 4));
+  if (!ctx->d_largepool)
+    HIPCHK(hipMalloc(&ctx->d_largepool,
+                     (size_t)ctx->num_cus * RW_LARGE_WAVES_PER_CU * RW_LARGE_WORDS * 4));
+  return 0;
+}
+
+// the four row-lane classes, one launch each (lists[c * list_cap ...], counts[c])
+template <bool SEG>
+static int rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* dw, const int* lists,
+                       const int* counts, int list_cap, const char* d_query, const char* d_query_uc,
+                       gsnapdp_result* d_results, uint32_t* d_ops, const int64_t* d_op_offsets,
+                       const gsnapdp_sj_window* sjw) {
+  const uint64_t nw = (uint64_t)ctx->nwords;
+  constexpr int small_blocks = 160 * 1024 / (8 * RW_SMALL_WORDS * 4);
+  hipLaunchKernelGGL((k_rows<32, false, SEG>), dim3(ctx->num_cus * small_blocks), dim3(256),
+                     (size_t)8 * RW_SMALL_WORDS * 4, st, dw, lists, counts + RW_SMALL, d_query,
+                     d_query_uc, ctx->d_blocks, nw, ctx->d_prof, (uint32_t*)nullptr,
+                     (size_t)RW_SMALL_WORDS, d_results, d_ops, d_op_offsets, sjw);
+  hipLaunchKernelGGL((k_rows<64, false, SEG>), dim3(ctx->num_cus * 2), dim3(256),
+                     (size_t)4 * RW_MID_WORDS * 4, st, dw, lists + (size_t)RW_MID * list_cap,
+                     counts + RW_MID, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
+                     (uint32_t*)nullptr, (size_t)RW_MID_WORDS, d_results, d_ops, d_op_offsets, sjw);
+  hipLaunchKernelGGL((k_rows<64, true, SEG>), dim3(ctx->num_cus * RW_LARGE_WAVES_PER_CU / 4),
+                     dim3(256), 0, st, dw, lists + (size_t)RW_LARGE * list_cap, counts + RW_LARGE,
+                     d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_largepool,
+                     (size_t)RW_LARGE_WORDS, d_results, d_ops, d_op_offsets, sjw);
+  hipLaunchKernelGGL((k_rows<64, true, SEG>), dim3(RW_BIG_WAVES), dim3(64), 0, st, dw,
+                     lists + (size_t)RW_BIG * list_cap, counts + RW_BIG, d_query, d_query_uc,
+                     ctx->d_blocks, nw, ctx->d_prof, ctx->d_bigpool, RW_BIG_WORDS, d_results,
+                     d_ops, d_op_offsets, sjw);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int gsnapdp__rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d_windows,
                          const int* lists, const int* counts, int list_cap, const char* d_query,
                          const char* d_query_uc, gsnapdp_result* d_results, uint32_t* d_ops,
                          const int64_t* d_op_offsets) {
-  const uint64_t nw = (uint64_t)ctx->nwords;
-  constexpr int small_blocks = 160 * 1024 / (8 * RW_SMALL_WORDS * 4);
-  hipLaunchKernelGGL((k_rows<32, false, false>), dim3(ctx->num_cus * small_blocks), dim3(256),
-                     (size_t)8 * RW_SMALL_WORDS * 4, st, d_windows, lists, counts + RW_SMALL,
-                     d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, (uint32_t*)nullptr,
-                     (size_t)RW_SMALL_WORDS, d_results, d_ops, d_op_offsets,
-                     (const gsnapdp_sj_window*)nullptr);
-  hipLaunchKernelGGL((k_rows<64, false, false>), dim3(ctx->num_cus * 2), dim3(256),
-                     (size_t)4 * RW_MID_WORDS * 4, st, d_windows, lists + (size_t)RW_MID * list_cap,
-                     counts + RW_MID, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
-                     (uint32_t*)nullptr, (size_t)RW_MID_WORDS, d_results, d_ops, d_op_offsets,
-                     (const gsnapdp_sj_window*)nullptr);
-  hipLaunchKernelGGL((k_rows<64, true, false>), dim3(RW_BIG_WAVES), dim3(64), 0, st, d_windows,
-                     lists + (size_t)RW_BIG * list_cap, counts + RW_BIG, d_query, d_query_uc,
-                     ctx->d_blocks, nw, ctx->d_prof, ctx->d_bigpool, RW_BIG_WORDS, d_results,
-                     d_ops, d_op_offsets, (const gsnapdp_sj_window*)nullptr);
-  HIPCHK(hipGetLastError());
-  return 0;
+  return rows_launch<false>(ctx, st, d_windows, lists, counts, list_cap, d_query, d_query_uc,
+                            d_results, d_ops, d_op_offsets, nullptr);
 }
 
 // ======================================================================
@@ -1289,32 +1310,16 @@ extern "C" int gsnapdp_sj_run_device(gsnapdp_ctx* ctx, const gsnapdp_sj_window* 
     HIPCHK(hipMalloc(&ctx->d_sj_win, (size_t)cap * sizeof(gsnapdp_window)));
     ctx->sj_cap = cap;
   }
-  if (!ctx->d_bigpool)
-    HIPCHK(hipMalloc(&ctx->d_bigpool, (size_t)RW_BIG_WAVES * RW_BIG_WORDS * 4));
+  if (gsnapdp__rows_pools(ctx)) return -1;
   const int cap = ctx->sj_cap;
   int* lists = ctx->d_sj_lists;
   int* counts = lists + (size_t)RW_NCLS * cap;
   gsnapdp_window* dw = ctx->d_sj_win;
-  const uint64_t nw = (uint64_t)ctx->nwords;
   HIPCHK(hipMemsetAsync(counts, 0, 4 * RW_NCLS, st));
   hipLaunchKernelGGL(k_sj_plan, dim3((n + 255) / 256), dim3(256), 0, st, d_windows, n, d_query,
                      d_query_uc, dw, d_results, lists, counts, cap);
-  constexpr int small_blocks = 160 * 1024 / (8 * RW_SMALL_WORDS * 4);
-  hipLaunchKernelGGL((k_rows<32, false, true>), dim3(ctx->num_cus * small_blocks), dim3(256),
-                     (size_t)8 * RW_SMALL_WORDS * 4, st, dw, lists, counts + RW_SMALL, d_query,
-                     d_query_uc, ctx->d_blocks, nw, ctx->d_prof, (uint32_t*)nullptr,
-                     (size_t)RW_SMALL_WORDS, d_results, d_ops, d_op_offsets, d_windows);
-  hipLaunchKernelGGL((k_rows<64, false, true>), dim3(ctx->num_cus * 2), dim3(256),
-                     (size_t)4 * RW_MID_WORDS * 4, st, dw, lists + (size_t)RW_MID * cap,
-                     counts + RW_MID, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
-                     (uint32_t*)nullptr, (size_t)RW_MID_WORDS, d_results, d_ops, d_op_offsets,
-                     d_windows);
-  hipLaunchKernelGGL((k_rows<64, true, true>), dim3(RW_BIG_WAVES), dim3(64), 0, st, dw,
-                     lists + (size_t)RW_BIG * cap, counts + RW_BIG, d_query, d_query_uc,
-                     ctx->d_blocks, nw, ctx->d_prof, ctx->d_bigpool, RW_BIG_WORDS, d_results,
-                     d_ops, d_op_offsets, d_windows);
-  HIPCHK(hipGetLastError());
-  return 0;
+  return rows_launch<true>(ctx, st, dw, lists, counts, cap, d_query, d_query_uc, d_results, d_ops,
+                           d_op_offsets, d_windows);
 }
 
 extern "C" int gsnapdp_sj_run_host(gsnapdp_ctx* ctx, const gsnapdp_sj_window* windows, int n,

@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "gsnapdp_device.h"
 #include "gsnapdp_internal.h"
@@ -270,6 +271,11 @@ __host__ __device__ constexpr uint64_t spread_match(uint32_t m5) {
   return x;
 }
 
+// f(integral_constant<int, U>) for U in the sequence, in order
+template <int... U, class F>
+__device__ inline void unroll_seq(std::integer_sequence<int, U...>, F&& f) {
+  (f(std::integral_constant<int, U>()), ...);
+}
 __device__ inline uint32_t push_sign(uint32_t acc, int d) {
   return __builtin_amdgcn_alignbit(acc, (uint32_t)d, 31u);  // (acc << 1) | (d < 0)
 }
@@ -443,8 +449,15 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
 
   // One skewed step.  MASKED steps (the first and last LPW-1) leave lanes
   // whose column is outside 1..maxL2 untouched.
-  auto step = [&](auto masked, int t) {
+  // ROT < 0: the row words shift down one slot per step (P[s] = P[s+1]).
+  // ROT = u >= 0 (full steps unrolled S at a time): the words stay put and
+  // slot s reads P[(s + u + 1) % S], the entering row overwriting P[u], so
+  // after S steps the layout is back where it started.
+  auto step = [&](auto masked, auto rot, int t) {
     constexpr bool MASKED = decltype(masked)::value;
+    constexpr int ROT = decltype(rot)::value;
+    static_assert(!MASKED || ROT < 0, "rotating steps are full steps");
+    auto pslot = [&](int s) -> uint32_t { return ROT < 0 ? P[s] : P[(s + ROT + 1) % S]; };
     const int c = t - j;
     // a window stops at its own last column, so its registers end on column L2
     const bool act = !MASKED || (c >= 1 && c <= L2);
@@ -460,7 +473,7 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
     uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u, gsh = 0u;
     auto cell = [&](int s, int Hr, int Er) {
       const int Hd = H[s], Ed = E[s], Fd = F[s];
-      const uint32_t pw = P[s];
+      const uint32_t pw = pslot(s);
       const int a = Hr + open;
       const int b = hp + open;
       const int m1 = max(Hd, Ed);
@@ -471,17 +484,10 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       const int dh = JL ? (Ed - Hd) : (Hd - Ed);  // h1: nogap from gap1
       const int df = JL ? (fp - b) : (b - fp);    // dF: gap2 extends
       const int de = JL ? (Er - a) : (a - Er);    // dE: gap1 extends
-      if (s == 0) {  // first bit of each plane
-        av = (uint32_t)dv >> 31;
-        ah = (uint32_t)dh >> 31;
-        af = (uint32_t)df >> 31;
-        ae = (uint32_t)de >> 31;
-      } else {
-        av = push_sign(av, dv);
-        ah = push_sign(ah, dh);
-        af = push_sign(af, df);
-        ae = push_sign(ae, de);
-      }
+      av = push_sign(av, dv);  // (the first push shifts in zeros: one op, not a compare)
+      ah = push_sign(ah, dh);
+      af = push_sign(af, df);
+      ae = push_sign(ae, de);
       E[s] = max(a, Er);
       const int f = max(b, fp);
       F[s] = f;
@@ -491,9 +497,13 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
     };
     uint32_t macc = 0u;  // this column's match bits, bit s = slot s
     if (act) {
+      if constexpr (ROT < 0) {
 #pragma unroll
-      for (int s = 0; s < S - 1; s++) P[s] = P[s + 1];
-      P[S - 1] = pnext;
+        for (int s = 0; s < S - 1; s++) P[s] = P[s + 1];
+        P[S - 1] = pnext;
+      } else {
+        P[ROT] = pnext;
+      }
       MB = ((MB >> 1) & MB_KEEP) | row_spread(pnext);
       gsh = 4u * (uint32_t)gnext;
       macc = (uint32_t)(MB >> (8u * (uint32_t)gnext));
@@ -528,12 +538,18 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   };
   using Masked = std::integral_constant<bool, true>;
   using Full = std::integral_constant<bool, false>;
+  using Shift = std::integral_constant<int, -1>;
   // full-rate steps while every lane's column is inside 1..its own L2
   const int minL2 = __builtin_amdgcn_readfirstlane(-wave_max(active ? -L2 : -maxL2));
   int t = 1;
-  for (; t < LPW && t < maxL2 + LPW; t++) step(Masked(), t);
-  for (; t <= minL2; t++) step(Full(), t);
-  for (; t < maxL2 + LPW; t++) step(Masked(), t);
+  for (; t < LPW && t < maxL2 + LPW; t++) step(Masked(), Shift(), t);
+#ifndef EXP_NOROT
+  for (; t + S - 1 <= minL2; t += S)
+    unroll_seq(std::make_integer_sequence<int, S>(),
+               [&](auto u) { step(Full(), u, t + decltype(u)::value); });
+#endif
+  for (; t <= minL2; t++) step(Full(), Shift(), t);
+  for (; t < maxL2 + LPW; t++) step(Masked(), Shift(), t);
   // endpoint (L1,L2): the lanes stopped on column L2 (dynprog.c:4545)
 #pragma unroll
   for (int s = 0; s < S; s++)
@@ -914,6 +930,7 @@ extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   (void)hipFree(ctx->d_small);
   (void)hipFree(ctx->d_dirpool);
   (void)hipFree(ctx->d_bigpool);
+  (void)hipFree(ctx->d_largepool);
   (void)hipFree(ctx->d_ggap_lists);
   (void)hipFree(ctx->d_ggap_counts);
   (void)hipFree(ctx->d_ggap_pool);
@@ -937,7 +954,8 @@ extern "C" size_t gsnapdp_scratch_bytes(gsnapdp_ctx* ctx, int n, int max_length1
   (void)max_length2;
   const size_t waves = (size_t)n / 64 + NKEYS;
   return (size_t)n * 8 + waves * 64 * 4 + (ctx ? ctx->dirpool_waves : 0) * WAVE_STRIDE_DW * 4 +
-         (size_t)RW_BIG_WAVES * RW_BIG_WORDS * 4;
+         (size_t)RW_BIG_WAVES * RW_BIG_WORDS * 4 +
+         (size_t)(ctx ? ctx->num_cus : 256) * RW_LARGE_WAVES_PER_CU * RW_LARGE_WORDS * 4;
 }
 
 static int ensure_capacity(gsnapdp_ctx* ctx, int n) {
@@ -970,8 +988,7 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   int* class_start = cursor + NKEYS;
   int* big_count = class_start + NCLASS + 1;  // RW_NCLS row-lane class counts
   HIPCHK(hipMemsetAsync(big_count, 0, 4 * RW_NCLS, st));
-  if (!ctx->d_bigpool)  // global scratch of the large row-lane windows, on first use
-    HIPCHK(hipMalloc(&ctx->d_bigpool, (size_t)RW_BIG_WAVES * RW_BIG_WORDS * 4));
+  if (gsnapdp__rows_pools(ctx)) return -1;
   const int tb = 1024, nb = (n + tb - 1) / tb;
   auto mark = [&](int stage, int end) { gsnapdp__mark(ctx, st, stage, end); };
   mark(0, 0);
