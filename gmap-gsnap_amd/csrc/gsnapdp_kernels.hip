@@ -248,6 +248,10 @@ struct ColStream {
 #define GSNAPDP_FILL_WAVES 4  // k_fill waves per SIMD (register budget 512 / waves)
 #endif
 constexpr int FILL_SC_BIAS = 6;  // -2 * SINGLE_EXTEND (dynprog.c:222)
+#ifndef GSNAPDP_TB_AHEAD
+#define GSNAPDP_TB_AHEAD 1
+#endif
+constexpr int TB_AHEAD = GSNAPDP_TB_AHEAD;  // traceback prefetch distance, in 4-column groups
 
 // k_fill's LDS profile word: each signed 4-bit pairdistance nibble s becomes
 // the unsigned nibble s + 6 (s in -5..3, so 1..9); match bits unchanged.
@@ -276,6 +280,32 @@ template <int... U, class F>
 __device__ inline void unroll_seq(std::integer_sequence<int, U...>, F&& f) {
   (f(std::integral_constant<int, U>()), ...);
 }
+// k_fill's cell values.  By default they are 16-bit: value + FV_BIAS, NEG-like
+// values from FV_NEG up, all zero-extended in 32-bit registers, so the maxima
+// are v_max_u16 (twice the issue rate of v_max_i32 on gfx950; 16-bit VOP2
+// results zero bits 16-31) while sums and differences stay 32-bit adds.
+// In-band reachable values lie in [2*open + 1, 9 * steps] (offset
+// coordinates, open >= -12 for the single gaps k_fill serves), NEG-like ones
+// in [FV_NEG + open, FV_NEG + 9 * steps]; with at most 688 steps both ranges
+// stay apart and inside 0..65535 (static_assert below).
+#ifndef GSNAPDP_FILL32
+using FV = uint32_t;
+constexpr uint32_t FV_NEG = 1024u;
+constexpr uint32_t FV_BIAS = 16384u;
+__device__ inline FV fv_max(FV a, FV b) {
+  FV d;
+  asm("v_max_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+static_assert(FV_NEG >= 12 && FV_NEG + 9u * 688u < FV_BIAS - 2u * 12u &&
+                  FV_BIAS + 9u * 688u < 65536u && FAST_L2MAX + 48 <= 688,
+              "16-bit k_fill value ranges");
+#else
+using FV = int;
+constexpr int FV_NEG = NEG;
+constexpr int FV_BIAS = 0;
+__device__ inline FV fv_max(FV a, FV b) { return max(a, b); }
+#endif
 __device__ inline uint32_t push_sign(uint32_t acc, int d) {
   return __builtin_amdgcn_alignbit(acc, (uint32_t)d, 31u);  // (acc << 1) | (d < 0)
 }
@@ -364,7 +394,7 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   };
   const uint64_t gmax = nwords >= 3 ? (nwords - 3) / 3 : 0;  // last whole genome block
 
-  int H[S], E[S], F[S];
+  FV H[S], E[S], F[S];
   uint32_t P[S];
   // Match bits of the lane's S rows against each genome class: byte k of MB
   // holds, in bits 0..S-1, whether slot s's query row matches class k
@@ -379,9 +409,9 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
 #pragma unroll
   for (int s = 0; s < S; s++) {
     const int r = row0 + s;
-    H[s] = (r == 0) ? 0 : NEG;
-    E[s] = NEG;
-    F[s] = (r >= 1) ? open : NEG;  // open + r*ext - r*ext
+    H[s] = (r == 0) ? FV_BIAS : FV_NEG;
+    E[s] = FV_NEG;
+    F[s] = (r >= 1) ? FV_BIAS + open : FV_NEG;  // open + r*ext - r*ext
     P[s] = row_word(r);
     MB = ((MB >> 1) & MB_KEEP) | row_spread(P[s]);
   }
@@ -438,7 +468,7 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   stage(std::integral_constant<int, RING_K + RG::SPAN>(), 1 + rbase, 1);
   uint32_t pnext = rr[(1 + j * (S - 1) + rbase) & (RG::RR - 1)];
   int gnext = cr[(1 - j) & (RG::CR - 1)];
-  int fin = NEG;
+  FV fin = FV_NEG;
   const int se = stop + L1 - L2 + rband;  // global slot of the endpoint (L1,L2)
   const int je = se / S, sle = se - je * S;
   // scratch layout: column c's words are D[c*64 + (j*NG + g)], one 256-byte
@@ -461,9 +491,9 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
     const int c = t - j;
     // a window stops at its own last column, so its registers end on column L2
     const bool act = !MASKED || (c >= 1 && c <= L2);
-    int hp = NEG, fp = NEG;  // new (nogap, gap2) just above local slot 0
+    FV hp = FV_NEG, fp = FV_NEG;  // new (nogap, gap2) just above local slot 0
     if (LPW > 1) {
-      const int h = from_lane_above(H[S - 1]), f = from_lane_above(F[S - 1]);
+      const FV h = (FV)from_lane_above((int)H[S - 1]), f = (FV)from_lane_above((int)F[S - 1]);
       if (j != 0) {
         hp = h;
         fp = f;
@@ -471,25 +501,25 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
     }
     // four bit planes (v1, h1, dF, dE), each a short independent chain
     uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u, gsh = 0u;
-    auto cell = [&](int s, int Hr, int Er) {
-      const int Hd = H[s], Ed = E[s], Fd = F[s];
+    auto cell = [&](int s, FV Hr, FV Er) {
+      const FV Hd = H[s], Ed = E[s], Fd = F[s];
       const uint32_t pw = pslot(s);
-      const int a = Hr + open;
-      const int b = hp + open;
-      const int m1 = max(Hd, Ed);
-      const int sc = (int)__builtin_amdgcn_ubfe(pw, gsh, 4);  // pairdistance - 2*extend
+      const FV a = Hr + open;
+      const FV b = hp + open;
+      const FV m1 = fv_max(Hd, Ed);
+      const FV sc = (FV)__builtin_amdgcn_ubfe(pw, gsh, 4);  // pairdistance - 2*extend
       const bool above = (s < NAB) && (j * S + s < stop);  // loop-invariant lane mask
-      const int hn = above ? NEG : max(m1, Fd) + sc;
-      const int dv = JL ? (Fd - m1) : (m1 - Fd);  // v1: nogap from gap2
-      const int dh = JL ? (Ed - Hd) : (Hd - Ed);  // h1: nogap from gap1
-      const int df = JL ? (fp - b) : (b - fp);    // dF: gap2 extends
-      const int de = JL ? (Er - a) : (a - Er);    // dE: gap1 extends
+      const FV hn = above ? FV_NEG : fv_max(m1, Fd) + sc;
+      const int dv = JL ? (int)(Fd - m1) : (int)(m1 - Fd);  // v1: nogap from gap2
+      const int dh = JL ? (int)(Ed - Hd) : (int)(Hd - Ed);  // h1: nogap from gap1
+      const int df = JL ? (int)(fp - b) : (int)(b - fp);    // dF: gap2 extends
+      const int de = JL ? (int)(Er - a) : (int)(a - Er);    // dE: gap1 extends
       av = push_sign(av, dv);  // (the first push shifts in zeros: one op, not a compare)
       ah = push_sign(ah, dh);
       af = push_sign(af, df);
       ae = push_sign(ae, de);
-      E[s] = max(a, Er);
-      const int f = max(b, fp);
+      E[s] = fv_max(a, Er);
+      const FV f = fv_max(b, fp);
       F[s] = f;
       H[s] = hn;
       hp = hn;
@@ -509,9 +539,9 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
       macc = (uint32_t)(MB >> (8u * (uint32_t)gnext));
       cell(0, H[1], E[1]);
     }
-    int hb = NEG, eb = NEG;  // old (nogap, gap1) just below the lowest local slot
+    FV hb = FV_NEG, eb = FV_NEG;  // old (nogap, gap1) just below the lowest local slot
     if (LPW > 1) {
-      const int h = from_lane_below(H[0]), e = from_lane_below(E[0]);
+      const FV h = (FV)from_lane_below((int)H[0]), e = (FV)from_lane_below((int)E[0]);
       if (j != LPW - 1) {
         hb = h;
         eb = e;
@@ -555,7 +585,7 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   for (int s = 0; s < S; s++)
     if (j == je && s == sle) fin = H[s];
   fin = __shfl(fin, gbase + je);
-  const int finalscore = fin + (L1 + L2) * ext;
+  const int finalscore = (int)(fin - FV_BIAS) + (L1 + L2) * ext;
 #ifdef EXP_NOTRACE
   if (active && j == 0) res[wi].finalscore = finalscore;
   return;
@@ -680,9 +710,12 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   // wave-uniform sweep from the wave's longest window down to column -1
   int G = maxL2 >> 2;
   set_diag(L1, L2);
-  Grp ga, gb;
-  fetch_group(ga, G, jj);
-  fetch_group(gb, G >= 1 ? G - 1 : 0, jj);
+  // pre[0] is the group being visited, pre[1..TB_AHEAD] the next ones,
+  // loaded TB_AHEAD groups ahead of their visit (global scratch latency)
+  Grp pre[TB_AHEAD + 1];
+#pragma unroll
+  for (int i = 0; i <= TB_AHEAD; i++) fetch_group(pre[i], G - i >= 0 ? G - i : 0, jj);
+  Grp& ga = pre[0];
   const uint32_t invall = JL ? 0xFFFFFFFFu : 0u;
   // one iteration per 4-column group G; its columns are visited one by one
   // only when some lane of the wave cannot take the group in one bulk step
@@ -731,9 +764,13 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
     }
     // leaving group G
     if (__builtin_amdgcn_ballot_w64(st != T_DONE) == 0) break;
-    ga = gb;
-    if (G >= 1 && ga.jw != jj) fetch_group(ga, G - 1, jj);  // a gap moved the path to another lane
-    if (G >= 2) fetch_group(gb, G - 2, jj);  // the path's diagonal, predicted unchanged
+#pragma unroll
+    for (int i = 0; i < TB_AHEAD; i++) {
+      pre[i] = pre[i + 1];
+      // a gap moved the path to another lane: reload the groups already in flight
+      if (G - 1 - i >= 0 && pre[i].jw != jj) fetch_group(pre[i], G - 1 - i, jj);
+    }
+    if (G - 1 - TB_AHEAD >= 0) fetch_group(pre[TB_AHEAD], G - 1 - TB_AHEAD, jj);  // predicted unchanged
   }
   if (st != T_DONE && st != T_WAIT) column(-1, 0u, 0u, -1);
   ow.flush();
