@@ -44,8 +44,23 @@ struct State {
   std::vector<char> q, qu;
   std::vector<uint32_t> ops;
   std::vector<gsnapdp_pair> pairs;
+  // GPU launches per entry-point family, reported at exit under
+  // $GSNAPDP_DROPIN_STATS (shows a host program really ran its DP here)
+  unsigned long ncalls[6] = {0, 0, 0, 0, 0, 0};
 };
 State g;
+enum { CALL_GAP, CALL_SJ, CALL_GGAP, CALL_CGAP, CALL_MICRO, CALL_MAXENT };
+
+struct StatsAtExit {
+  ~StatsAtExit() {
+    if (!getenv("GSNAPDP_DROPIN_STATS")) return;
+    fprintf(stderr,
+            "gsnapdp_dropin: GPU calls: gap %lu, splicejunction %lu, genome_gap %lu, cdna_gap %lu, "
+            "microexon %lu, maxent %lu\n",
+            g.ncalls[CALL_GAP], g.ncalls[CALL_SJ], g.ncalls[CALL_GGAP], g.ncalls[CALL_CGAP],
+            g.ncalls[CALL_MICRO], g.ncalls[CALL_MAXENT]);
+  }
+} stats_at_exit;
 
 [[noreturn]] void fatal(const std::string& msg) {
   fprintf(stderr, "gsnapdp drop-in: %s\n", msg.c_str());
@@ -107,6 +122,7 @@ gsnapdp_List_T run_one(gsnapdp_window& w, const char* seq, const char* sequc, bo
   const int64_t off[2] = {0, cap};
   g.ops.assign((size_t)cap + 1, 0u);
   gsnapdp_result r;
+  g.ncalls[CALL_GAP]++;
   if (gsnapdp_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, g.ops.data(), off))
     fatal(std::string("gsnapdp_run_host: ") + gsnapdp_last_error());
   if (r.status == gsnapdp::ST_UNSUPPORTED)
@@ -168,6 +184,7 @@ double maxent_one(int model, unsigned splice_pos, unsigned chroffset) {
   ensure_tables();
   const uint8_t m = (uint8_t)model;
   double out = 0.0;
+  g.ncalls[CALL_MAXENT]++;
   if (gsnapdp_maxent_host(ctx(), &m, &splice_pos, &chroffset, &out, 1))
     fatal(std::string("maxent: ") + gsnapdp_last_error());
   return out;
@@ -257,6 +274,7 @@ gsnapdp_List_T run_sj(int kind, const char* seq1, const char* seq1uc, const char
   const int64_t off[2] = {0, cap};
   g.ops.assign((size_t)cap + 1, 0u);
   gsnapdp_result r;
+  g.ncalls[CALL_SJ]++;
   if (gsnapdp_sj_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, g.ops.data(), off))
     fatal(std::string("gsnapdp_sj_run_host: ") + gsnapdp_last_error());
   if (r.status == gsnapdp::ST_UNSUPPORTED) fatal("splice junction outside A C G T N");
@@ -540,6 +558,7 @@ gsnapdp_List_T Dynprog_genome_gap(
   g.ops.assign((size_t)cap + 1, 0u);
   gsnapdp_ggap_result r;
   gsnapdp_ggap_trace t;
+  g.ncalls[CALL_GGAP]++;
   if (gsnapdp_ggap_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, &t, g.ops.data(), off))
     fatal(std::string("gsnapdp_ggap_run_host: ") + gsnapdp_last_error());
   if (t.status == gsnapdp::ST_UNSUPPORTED)
@@ -646,6 +665,7 @@ gsnapdp_List_T Dynprog_cdna_gap(
   const int64_t off[2] = {0, cap};
   g.ops.assign((size_t)cap + 1, 0u);
   gsnapdp_cgap_result r;
+  g.ncalls[CALL_CGAP]++;
   if (gsnapdp_cgap_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, g.ops.data(), off))
     fatal(std::string("gsnapdp_cgap_run_host: ") + gsnapdp_last_error());
   if (r.status == gsnapdp::ST_UNSUPPORTED)
@@ -784,6 +804,7 @@ gsnapdp_List_T Dynprog_microexon_int(
   w.defect_rate = defect_rate < 0.003 ? 0.001f : (defect_rate < 0.014 ? 0.01f : 0.5f);
   w.watsonp = watsonp ? 1 : 0;
   gsnapdp_micro_result r;
+  g.ncalls[CALL_MICRO]++;
   if (gsnapdp_micro_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r))
     fatal(std::string("gsnapdp_micro_run_host: ") + gsnapdp_last_error());
   if (r.status != 0) fatal("microexon window outside the reference's domain");

@@ -761,3 +761,85 @@ def c5_windows(gseq: np.ndarray, nreads: int, seed: int = 5, read_len: int = 100
 
 def pack_genome(gseq: np.ndarray) -> np.ndarray:
     return _genome.pack(gseq)
+
+
+def synthetic_transcripts(seed: int = 7, ngenes: int = 16, genome_len: int = 160_000):
+    """End-to-end gmap inputs (tests/test_gmap_e2e.py): a genomic segment
+    carrying ``ngenes`` spliced genes and one cDNA per gene.
+
+    Each gene has 2-12 exons of 12-260 nt (a few microexon-sized ones) and
+    introns of 70-1500 nt.  Intron ends are GT-AG (80 %), GC-AG (8 %), AT-AC
+    (5 %) or random (7 %); the canonical ones sit in splice-site context
+    (exon ..AG | GTRAGT donor, a pyrimidine tract and YAG | G acceptor) so that
+    GMAP's MaxEnt-guided stage 3 accepts them.  A third of the genes lie on
+    the minus strand, and their cDNAs are given reverse-complemented (gmap -g
+    at this version reports no alignment on the segment's minus strand, even
+    with its own dynprog.o, so every cDNA is placed to align on the plus
+    strand: sense or antisense).  The
+    cDNAs carry 1 % substitutions, occasional N, a 1-6 nt indel in a third of
+    them, and a poly-A tail on some.  Returns (genome bytes, [(name, cDNA)]).
+    """
+    rng = np.random.default_rng(seed)
+    g = ACGT[rng.integers(0, 4, size=genome_len)]
+    b = lambda t: np.frombuffer(t, np.uint8)  # noqa: E731
+    queries = []
+    pos = 2000
+    for k in range(ngenes):
+        nex = int(rng.integers(2, 13))
+        exl = rng.integers(40, 261, size=nex)
+        small = rng.random(nex) < 0.12
+        exl[small] = rng.integers(12, 30, size=int(small.sum()))
+        exl[0] = max(exl[0], 60)
+        exl[-1] = max(exl[-1], 60)
+        inl = rng.integers(70, 1501, size=nex - 1)
+        span = int(exl.sum() + inl.sum())
+        if pos + span + 2000 > genome_len:
+            break
+        gene = g[pos:pos + span].copy()
+        spans, p = [], 0
+        for e in range(nex):
+            spans.append((p, int(exl[e])))
+            p += int(exl[e])
+            if e == nex - 1:
+                break
+            r, n = rng.random(), int(inl[e])
+            kind = 0 if r < 0.80 else 1 if r < 0.88 else 2 if r < 0.93 else 3
+            if kind < 3:
+                donor = (b"GT", b"GC", b"AT")[kind] + (b"AAGT", b"GAGT", b"AAGA")[int(rng.integers(0, 3))]
+                accept = b"AG" if kind < 2 else b"AC"
+                gene[p:p + 6] = b(donor)
+                gene[p - 2:p] = b(b"AG")
+                tract = np.where(rng.random(14) < 0.9, b(b"CT")[rng.integers(0, 2, size=14)],
+                                 ACGT[rng.integers(0, 4, size=14)])
+                gene[p + n - 18:p + n - 4] = tract
+                gene[p + n - 3:p + n] = b(b"C" + accept)
+                gene[p + n] = ord("G")
+            p += n
+        exons = [gene[s0:s0 + L].copy() for s0, L in spans]
+        minus = rng.random() < 1 / 3
+        g[pos:pos + span] = revcomp(gene) if minus else gene
+        cdna = np.concatenate(exons)
+        cdna = _mutate(rng, cdna, 0.01, 0.001)
+        if rng.random() < 1 / 3:
+            at = int(rng.integers(30, cdna.size - 30))
+            n = int(rng.integers(1, 7))
+            if rng.random() < 0.5:
+                cdna = np.concatenate([cdna[:at], cdna[at + n:]])
+            else:
+                cdna = np.concatenate([cdna[:at], ACGT[rng.integers(0, 4, size=n)], cdna[at:]])
+        if rng.random() < 0.3:
+            cdna = np.concatenate([cdna, np.full(int(rng.integers(10, 30)), ord("A"), np.uint8)])
+        if minus:
+            cdna = revcomp(cdna)
+        queries.append(("synth%02d" % k, cdna.tobytes()))
+        pos += span + int(rng.integers(500, 3000))
+    return g.tobytes(), queries
+
+
+def write_fasta(path: str, records, width: int = 60) -> None:
+    """records: [(name, bytes)] -> FASTA file."""
+    with open(path, "wb") as f:
+        for name, seq in records:
+            f.write(b">" + name.encode() + b"\n")
+            for i in range(0, len(seq), width):
+                f.write(seq[i:i + width] + b"\n")

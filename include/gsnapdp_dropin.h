@@ -229,6 +229,27 @@ double Maxent_hr_antiacceptor_prob(gsnapdp_Genomicpos_T splice_pos,
  * (3 per 32 nt plus the reference's padding).  `device` = HIP device index. */
 int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device);
 
+/* ---- genome_hr subset (the reference's genome_hr.c is a missing blob;
+ * gmap-gsnap_amd/csrc/genome_hr_sites.c): the setup calls gmap.c makes
+ * (gmap.c:3801, 3810) and the splice-site dinucleotide queries of stage 2
+ * (stage2.c:916-959, 1504-1919).  Host code, exported by the drop-in so a
+ * gmap linked against it needs no genome_hr.o. */
+void Genome_hr_setup(unsigned int* ref_blocks_in, unsigned int* snp_blocks_in,  /* genome_hr.h:12 */
+                     gsnapdp_bool query_unk_mismatch_p_in, gsnapdp_bool genome_unk_mismatch_p_in,
+                     gsnapdp_Mode_T mode_in);
+void Genome_hr_user_setup(unsigned int* ref_blocks_in,                          /* genome_hr.h:17 */
+                          gsnapdp_bool query_unk_mismatch_p_in,
+                          gsnapdp_bool genome_unk_mismatch_p_in, gsnapdp_Mode_T mode_in);
+int Genome_prev_donor_position(int pos, gsnapdp_Genomicpos_T genomicstart,      /* genome_hr.h:106 */
+                               gsnapdp_Genomicpos_T genomicend, int pos5, gsnapdp_bool plusp);
+int Genome_prev_acceptor_position(int pos, gsnapdp_Genomicpos_T genomicstart,   /* genome_hr.h:108 */
+                                  gsnapdp_Genomicpos_T genomicend, int pos5, gsnapdp_bool plusp);
+int Genome_prev_antidonor_position(int pos, gsnapdp_Genomicpos_T genomicstart,  /* genome_hr.h:110 */
+                                   gsnapdp_Genomicpos_T genomicend, int pos5, gsnapdp_bool plusp);
+int Genome_prev_antiacceptor_position(int pos,                                  /* genome_hr.h:112 */
+                                      gsnapdp_Genomicpos_T genomicstart,
+                                      gsnapdp_Genomicpos_T genomicend, int pos5, gsnapdp_bool plusp);
+
 #ifdef __cplusplus
 }
 #endif

@@ -489,6 +489,72 @@ def pdist_case() -> None:
     print("pairdistance_highq: 128x128")
 
 
+GMAP_TRACE = os.path.join(HERE, "_ref", "gmap_trace")
+RECORDED = np.dtype([("finalscore", "<i4"), ("nmatches", "<i4"), ("nmismatches", "<i4"), ("nopens", "<i4"),
+                     ("nindels", "<i4"), ("dynprogindex", "<i4"), ("npairs", "<i4"), ("pad", "<i4")])
+
+
+def gmap_trace_case(seed: int = 7) -> None:
+    """The gap windows the reference's own gmap issues (oracle/gmap_trace.c) while
+    aligning synthetic spliced cDNAs (workload.synthetic_transcripts) with
+    `gmap -A -g`, replayed through ref_driver for the full outputs; each replay
+    is checked against the result gmap itself got from the call."""
+    sys.path.insert(0, HERE)
+    import oracle as O  # checker, used only to drop windows the reference cannot run (UB)
+    g, q = W.synthetic_transcripts(seed=seed, ngenes=40, genome_len=300_000)
+    with tempfile.TemporaryDirectory() as d:
+        W.write_fasta(os.path.join(d, "g.fa"), [("synthchr", g)])
+        W.write_fasta(os.path.join(d, "q.fa"), q)
+        env = dict(os.environ, GMAP_TRACE_DIR=os.path.join(d, "trace"))
+        subprocess.check_call([GMAP_TRACE, "-A", "-g", os.path.join(d, "g.fa"), os.path.join(d, "q.fa")],
+                              env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        t = os.path.join(d, "trace", "dp")
+        blocks = np.fromfile(os.path.join(t, "genome.u32"), dtype="<u4")
+        w = np.fromfile(os.path.join(t, "windows.bin"), dtype=W.WINDOW)
+        qb = np.fromfile(os.path.join(t, "query.bin"), dtype=np.uint8)
+        ub = np.fromfile(os.path.join(t, "query_uc.bin"), dtype=np.uint8)
+        got = np.fromfile(os.path.join(t, "gmap_results.bin"), dtype=RECORDED)
+        run_driver("dp", t)
+        res = np.fromfile(os.path.join(t, "results.bin"), dtype=RESULT)
+        npairs = np.fromfile(os.path.join(t, "npairs.i32"), dtype=np.int32)
+        pairs = np.fromfile(os.path.join(t, "pairs.bin"), dtype=PAIR)
+        for f in ("finalscore", "nmatches", "nmismatches", "nopens", "nindels"):
+            assert np.array_equal(res[f], got[f]), f
+        assert np.array_equal(res["reserved"], got["dynprogindex"]) and np.array_equal(npairs, got["npairs"])
+        np.savez_compressed(os.path.join(OUT, "gmap_synth_gap.npz"), blocks=blocks, windows=w, query=qb,
+                            query_uc=ub, mode=np.int32(0), finalscore=res["finalscore"],
+                            nmatches=res["nmatches"], nmismatches=res["nmismatches"], nopens=res["nopens"],
+                            nindels=res["nindels"], dynprogindex=res["reserved"], npairs=npairs, pairs=pairs)
+        print("gmap_synth_gap: %d windows (%s), %d pairs" % (
+            len(w), ", ".join("kind %d: %d" % (k, int((w["kind"] == k).sum())) for k in np.unique(w["kind"])),
+            pairs.size))
+
+        t = os.path.join(d, "trace", "ggap")
+        w = np.fromfile(os.path.join(t, "ggap_windows.bin"), dtype=GGAP_WINDOW)
+        qb = np.fromfile(os.path.join(t, "query.bin"), dtype=np.uint8)
+        ub = np.fromfile(os.path.join(t, "query_uc.bin"), dtype=np.uint8)
+        got = np.fromfile(os.path.join(t, "gmap_results.bin"), dtype=GGAP_RESULT)
+        O.setup(blocks)
+        ores, _, _, _ = O.run_ggap_batch(w, qb, ub)
+        keep = ores["bridge_ok"] == 1  # dynprog.c:4055 reads uninitialised indices otherwise
+        w, got = w[keep], got[keep]
+        w.tofile(os.path.join(t, "ggap_windows.bin"))
+        run_driver("ggap", t)
+        res = np.fromfile(os.path.join(t, "ggap_results.bin"), dtype=GGAP_RESULT)
+        npairs = np.fromfile(os.path.join(t, "npairs.i32"), dtype=np.int32)
+        pairs = np.fromfile(os.path.join(t, "pairs.bin"), dtype=PAIR)
+        # probability mode never writes *introntype (bridge_intron_gap, dynprog.c:3829-4081): gmap's
+        # variable keeps an earlier call's value, ref_driver's starts at 0
+        prob = w["use_probabilities_p"] == 1
+        got["introntype"][prob] = res["introntype"][prob]
+        assert res.tobytes() == got.tobytes()
+        np.savez_compressed(os.path.join(OUT, "gmap_synth_ggap.npz"), blocks=blocks, windows=w, query=qb,
+                            query_uc=ub, results=res, npairs=npairs, pairs=pairs,
+                            dropped_ub=np.int32((~keep).sum()))
+        print("gmap_synth_ggap: %d windows (%d dropped: probability-mode UB; %d probability mode), %d pairs" %
+              (len(w), int((~keep).sum()), int(w["use_probabilities_p"].sum()), pairs.size))
+
+
 def main() -> None:
     only = set(sys.argv[1:])  # optional: names of the fixtures to (re)generate
     os.makedirs(OUT, exist_ok=True)
@@ -516,6 +582,7 @@ def main() -> None:
         ("known_chr17", lambda: known_case("known_chr17", chr17, 600, seed=701)),
         ("maxent_chr17", lambda: maxent_case("maxent_chr17", b17, chr17.size, 20000, seed=301)),
         ("maxent_synth", lambda: maxent_case("maxent_synth", bsyn, synth.size, 6000, seed=302)),
+        ("gmap_trace", lambda: gmap_trace_case()),
     ]
     for name, fn in cases:
         if not only or name in only:

@@ -1,0 +1,287 @@
+/*
+ * gmap_trace.c -- TEST INFRASTRUCTURE ONLY (linked into oracle/_ref/gmap_trace,
+ * dev container only, never shipped, never sent to the GPU box).
+ *
+ * Records the DP windows the reference's gmap program issues, as golden-vector
+ * inputs in the record layouts of include/gsnapdp.h.  The reference's own gmap
+ * objects are linked with -Wl,--wrap for the gap fillers, so each call stage 3
+ * makes (stage3.c:5442-7003) lands here, is recorded, and then runs the
+ * reference's own function (__real_*), so gmap's output is unchanged.  The
+ * reference's result is recorded too, so that gen_golden.py can check that
+ * ref_driver's replay of each recorded window reproduces what gmap got.
+ *
+ * At exit, with $GMAP_TRACE_DIR set, writes
+ *   $GMAP_TRACE_DIR/dp/{windows.bin,query.bin,query_uc.bin,genome.u32,gmap_results.bin}
+ *   $GMAP_TRACE_DIR/ggap/{ggap_windows.bin,query.bin,query_uc.bin,genome.u32,gmap_results.bin}
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+
+#include "bool.h"
+#include "dynprog.h"
+#include "list.h"
+
+#include "../include/gsnapdp.h"
+
+typedef struct {
+  char *p;
+  size_t n, cap;
+} Buf;
+
+static void put(Buf *b, const void *src, size_t n) {
+  if (b->n + n > b->cap) {
+    b->cap = (b->n + n) * 2 + 4096;
+    b->p = (char *)realloc(b->p, b->cap);
+    if (!b->p) abort();
+  }
+  memcpy(b->p + b->n, src, n);
+  b->n += n;
+}
+
+/* per-kind trace: window records, query bytes, reference results */
+typedef struct {
+  Buf win, q, qu, res;
+} Trace;
+
+static Trace dp, gg;
+static const unsigned int *genome_blocks = NULL;
+static size_t genome_nwords = 0;
+
+/* result of the real call, as the test compares it */
+typedef struct {
+  int32_t finalscore, nmatches, nmismatches, nopens, nindels, dynprogindex, npairs, pad;
+} Recorded;
+
+/* query bytes the reference may read: [0, L1) forwards, or [-(L1-1), 0] behind a rev pointer;
+ * padded to a 4-byte boundary (the batch buffers are read with dword loads) */
+static uint32_t put_query(Trace *t, const char *s, const char *su, int L1, int rev) {
+  const int n = L1 > 0 ? L1 : 0;
+  const uint32_t base = (uint32_t)t->q.n;
+  static const char zero[8] = {0};
+  if (n) {
+    put(&t->q, rev ? s - (n - 1) : s, (size_t)n);
+    put(&t->qu, rev ? su - (n - 1) : su, (size_t)n);
+  }
+  put(&t->q, zero, 8 - (size_t)(n & 3));
+  put(&t->qu, zero, 8 - (size_t)(n & 3));
+  return rev ? base + (uint32_t)(n ? n - 1 : 0) : base;
+}
+
+static float bin(double defect_rate) { /* dynprog.c:4471-4486: only the bin matters */
+  return defect_rate < 0.003 ? 0.001f : (defect_rate < 0.014 ? 0.01f : 0.5f);
+}
+
+static void record_result(Trace *t, int dpi, int fs, int nm, int nmm, int no, int ni, List_T pairs) {
+  Recorded r = {fs, nm, nmm, no, ni, dpi, List_length(pairs), 0};
+  put(&t->res, &r, sizeof(r));
+}
+
+static void base_window(gsnapdp_window *w, int kind, Dynprog_T dynprog, int dpi, int length1, int length2,
+                        int offset1, int offset2, Genomicpos_T chroffset, Genomicpos_T chrhigh,
+                        Genomicpos_T chrpos, Genomicpos_T genomiclength, int cdna_direction, bool watsonp,
+                        bool jump_late_p, int extraband, double defect_rate) {
+  memset(w, 0, sizeof(*w));
+  w->kind = kind;
+  w->length1 = length1;
+  w->length2 = length2;
+  w->offset1 = offset1;
+  w->offset2 = offset2;
+  w->chroffset = chroffset;
+  w->chrhigh = chrhigh;
+  w->chrpos = chrpos;
+  w->genomiclength = genomiclength;
+  w->cdna_direction = cdna_direction;
+  w->extraband = extraband;
+  w->dynprogindex = dpi;
+  w->maxlength1 = ((int *)dynprog)[0]; /* struct Dynprog_T starts maxlength1, maxlength2 (dynprog.c:823-825) */
+  w->maxlength2 = ((int *)dynprog)[1];
+  w->defect_rate = bin(defect_rate);
+  w->watsonp = watsonp ? 1 : 0;
+  w->jump_late_p = jump_late_p ? 1 : 0;
+}
+
+extern unsigned int *__real_Genome_create_blocks(char *genomicseg, unsigned int genomelength);
+unsigned int *__wrap_Genome_create_blocks(char *genomicseg, unsigned int genomelength) {
+  unsigned int *b = __real_Genome_create_blocks(genomicseg, genomelength);
+  /* a copy: gmap frees its blocks before exit (gmap.c:4013) */
+  genome_nwords = (size_t)((genomelength + 31) / 32U) * 3 + 4; /* genome-write.c:809-810 */
+  genome_blocks = (unsigned int *)malloc(genome_nwords * sizeof(unsigned int));
+  memcpy((void *)genome_blocks, b, genome_nwords * sizeof(unsigned int));
+  return b;
+}
+
+extern List_T __real_Dynprog_single_gap(int *, int *, int *, int *, int *, int *, Dynprog_T, char *, char *,
+                                        char *, char *, int, int, int, int, Genomicpos_T, Genomicpos_T,
+                                        Genomicpos_T, Genomicpos_T, int, bool, bool, Pairpool_T, int, double,
+                                        int, bool);
+List_T __wrap_Dynprog_single_gap(int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches,
+                                 int *nopens, int *nindels, Dynprog_T dynprog, char *sequence1,
+                                 char *sequenceuc1, char *sequence2, char *sequenceuc2, int length1,
+                                 int length2, int offset1, int offset2, Genomicpos_T chroffset,
+                                 Genomicpos_T chrhigh, Genomicpos_T chrpos, Genomicpos_T genomiclength,
+                                 int cdna_direction, bool watsonp, bool jump_late_p, Pairpool_T pairpool,
+                                 int extraband_single, double defect_rate, int close_indels_mode,
+                                 bool widebandp) {
+  gsnapdp_window w;
+  List_T pairs;
+  base_window(&w, GSNAPDP_SINGLE_GAP, dynprog, *dynprogindex, length1, length2, offset1, offset2, chroffset,
+              chrhigh, chrpos, genomiclength, cdna_direction, watsonp, jump_late_p, extraband_single,
+              defect_rate);
+  w.widebandp = widebandp ? 1 : 0;
+  w.qpos = put_query(&dp, sequence1, sequenceuc1, length1, 0);
+  put(&dp.win, &w, sizeof(w));
+  pairs = __real_Dynprog_single_gap(dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog,
+                                    sequence1, sequenceuc1, sequence2, sequenceuc2, length1, length2, offset1,
+                                    offset2, chroffset, chrhigh, chrpos, genomiclength, cdna_direction,
+                                    watsonp, jump_late_p, pairpool, extraband_single, defect_rate,
+                                    close_indels_mode, widebandp);
+  record_result(&dp, *dynprogindex, *finalscore, *nmatches, *nmismatches, *nopens, *nindels, pairs);
+  return pairs;
+}
+
+#define END_ARGS                                                                                          \
+  int *dynprogindex, int *finalscore, int *nmatches, int *nmismatches, int *nopens, int *nindels,         \
+      Dynprog_T dynprog, char *sequence1, char *sequenceuc1, char *sequence2, char *sequenceuc2,          \
+      int length1, int length2, int offset1, int offset2, Genomicpos_T chroffset, Genomicpos_T chrhigh,   \
+      Genomicpos_T chrpos, Genomicpos_T genomiclength, int cdna_direction, bool watsonp,                  \
+      bool jump_late_p, Pairpool_T pairpool, int extraband_end, double defect_rate, Endalign_T endalign, \
+      bool use_genomicseg_p
+#define END_CALL                                                                                         \
+  dynprogindex, finalscore, nmatches, nmismatches, nopens, nindels, dynprog, sequence1, sequenceuc1,     \
+      sequence2, sequenceuc2, length1, length2, offset1, offset2, chroffset, chrhigh, chrpos,            \
+      genomiclength, cdna_direction, watsonp, jump_late_p, pairpool, extraband_end, defect_rate, endalign, \
+      use_genomicseg_p
+
+static List_T end_gap(int kind, List_T (*real)(END_ARGS), END_ARGS) {
+  gsnapdp_window w;
+  List_T pairs;
+  if (use_genomicseg_p) {
+    fprintf(stderr, "gmap_trace: use_genomicseg_p end gap (never issued by stage 3, stage3.c:9865)\n");
+    abort();
+  }
+  base_window(&w, kind, dynprog, *dynprogindex, length1, length2, offset1, offset2, chroffset, chrhigh, chrpos,
+              genomiclength, cdna_direction, watsonp, jump_late_p, extraband_end, defect_rate);
+  w.endalign = (uint8_t)endalign;
+  w.qpos = put_query(&dp, sequence1, sequenceuc1, length1, kind == GSNAPDP_END5_GAP);
+  put(&dp.win, &w, sizeof(w));
+  pairs = real(END_CALL);
+  record_result(&dp, *dynprogindex, *finalscore, *nmatches, *nmismatches, *nopens, *nindels, pairs);
+  return pairs;
+}
+
+extern List_T __real_Dynprog_end5_gap(END_ARGS);
+extern List_T __real_Dynprog_end3_gap(END_ARGS);
+List_T __wrap_Dynprog_end5_gap(END_ARGS) { return end_gap(GSNAPDP_END5_GAP, __real_Dynprog_end5_gap, END_CALL); }
+List_T __wrap_Dynprog_end3_gap(END_ARGS) { return end_gap(GSNAPDP_END3_GAP, __real_Dynprog_end3_gap, END_CALL); }
+
+extern List_T __real_Dynprog_genome_gap(int *, int *, int *, int *, double *, double *, int *, int *, int *, int *,
+                                        int *, int *, Dynprog_T, Dynprog_T, char *, char *, char *, char *, char *,
+                                        char *, int, int, int, int, int, int, Chrnum_T, Genomicpos_T,
+                                        Genomicpos_T, Genomicpos_T, Genomicpos_T, char *, bool, int, bool, bool,
+                                        Pairpool_T, int, double, int, bool, bool, bool, int, bool);
+List_T __wrap_Dynprog_genome_gap(int *dynprogindex, int *finalscore, int *new_leftgenomepos,
+                                 int *new_rightgenomepos, double *left_prob, double *right_prob, int *nmatches,
+                                 int *nmismatches, int *nopens, int *nindels, int *exonhead, int *introntype,
+                                 Dynprog_T dynprogL, Dynprog_T dynprogR, char *sequence1, char *sequenceuc1,
+                                 char *sequence2L, char *sequenceuc2L, char *revsequence2R,
+                                 char *revsequenceuc2R, int length1, int length2L, int length2R, int offset1,
+                                 int offset2L, int revoffset2R, Chrnum_T chrnum, Genomicpos_T chroffset,
+                                 Genomicpos_T chrhigh, Genomicpos_T chrpos, Genomicpos_T genomiclength,
+                                 char *genomicuc_ptr, bool use_genomicseg_p, int cdna_direction, bool watsonp,
+                                 bool jump_late_p, Pairpool_T pairpool, int extraband_paired,
+                                 double defect_rate, int maxpeelback, bool halfp, bool finalp,
+                                 bool use_probabilities_p, int score_threshold, bool splicingp) {
+  gsnapdp_ggap_window w;
+  gsnapdp_ggap_result r;
+  List_T pairs;
+  if (use_genomicseg_p) {
+    fprintf(stderr, "gmap_trace: use_genomicseg_p genome gap (never issued by stage 3, stage3.c:9865)\n");
+    abort();
+  }
+  memset(&w, 0, sizeof(w));
+  w.length1 = length1;
+  w.length2L = length2L;
+  w.length2R = length2R;
+  w.offset1 = offset1;
+  w.offset2L = offset2L;
+  w.revoffset2R = revoffset2R;
+  w.chroffset = chroffset;
+  w.chrhigh = chrhigh;
+  w.chrpos = chrpos;
+  w.genomiclength = genomiclength;
+  w.cdna_direction = cdna_direction;
+  w.extraband_paired = extraband_paired;
+  w.maxpeelback = maxpeelback;
+  w.score_threshold = score_threshold;
+  w.dynprogindex = *dynprogindex;
+  w.maxlength1 = ((int *)dynprogL)[0];
+  w.maxlength2 = ((int *)dynprogL)[1];
+  w.defect_rate = bin(defect_rate);
+  w.watsonp = watsonp ? 1 : 0;
+  w.jump_late_p = jump_late_p ? 1 : 0;
+  w.halfp = halfp ? 1 : 0;
+  w.finalp = finalp ? 1 : 0;
+  w.use_probabilities_p = use_probabilities_p ? 1 : 0;
+  w.splicingp = splicingp ? 1 : 0;
+  w.qpos = put_query(&gg, sequence1, sequenceuc1, length1, 0);
+  put(&gg.win, &w, sizeof(w));
+  pairs = __real_Dynprog_genome_gap(dynprogindex, finalscore, new_leftgenomepos, new_rightgenomepos, left_prob,
+                                    right_prob, nmatches, nmismatches, nopens, nindels, exonhead, introntype,
+                                    dynprogL, dynprogR, sequence1, sequenceuc1, sequence2L, sequenceuc2L,
+                                    revsequence2R, revsequenceuc2R, length1, length2L, length2R, offset1,
+                                    offset2L, revoffset2R, chrnum, chroffset, chrhigh, chrpos, genomiclength,
+                                    genomicuc_ptr, use_genomicseg_p, cdna_direction, watsonp, jump_late_p,
+                                    pairpool, extraband_paired, defect_rate, maxpeelback, halfp, finalp,
+                                    use_probabilities_p, score_threshold, splicingp);
+  memset(&r, 0, sizeof(r));
+  r.finalscore = *finalscore;
+  r.new_leftgenomepos = *new_leftgenomepos;
+  r.new_rightgenomepos = *new_rightgenomepos;
+  r.nmatches = *nmatches;
+  r.nmismatches = *nmismatches;
+  r.nopens = *nopens;
+  r.nindels = *nindels;
+  r.exonhead = *exonhead;
+  r.introntype = *introntype;
+  r.dynprogindex = *dynprogindex;
+  r.returned_null = pairs == NULL;
+  r.bridge_ok = 1;
+  r.left_prob = *left_prob;
+  r.right_prob = *right_prob;
+  put(&gg.res, &r, sizeof(r));
+  return pairs;
+}
+
+static void spit(const char *dir, const char *name, const void *p, size_t n) {
+  char path[4096];
+  FILE *f;
+  snprintf(path, sizeof(path), "%s/%s", dir, name);
+  if (!(f = fopen(path, "wb"))) {
+    perror(path);
+    exit(3);
+  }
+  if (n) fwrite(p, 1, n, f);
+  fclose(f);
+}
+
+static void dump(const char *root, const char *sub, const char *winname, Trace *t) {
+  char dir[4096];
+  snprintf(dir, sizeof(dir), "%s/%s", root, sub);
+  mkdir(dir, 0755);
+  spit(dir, winname, t->win.p, t->win.n);
+  spit(dir, "query.bin", t->q.p, t->q.n);
+  spit(dir, "query_uc.bin", t->qu.p, t->qu.n);
+  spit(dir, "gmap_results.bin", t->res.p, t->res.n);
+  spit(dir, "genome.u32", genome_blocks, genome_nwords * sizeof(unsigned int));
+}
+
+__attribute__((destructor)) static void write_trace(void) {
+  const char *root = getenv("GMAP_TRACE_DIR");
+  if (!root || !genome_blocks) return;
+  mkdir(root, 0755);
+  dump(root, "dp", "windows.bin", &dp);
+  dump(root, "ggap", "ggap_windows.bin", &gg);
+}

@@ -6,6 +6,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -24,7 +25,7 @@ assert REC.itemsize == PAIR.itemsize
 
 def declared_functions():
     text = open(HEADER).read()
-    names = re.findall(r"\b((?:Dynprog|Maxent_hr|Gsnapdp_dropin)_\w+)\s*\(", text)
+    names = re.findall(r"\b((?:Dynprog|Maxent_hr|Gsnapdp_dropin|Genome_hr|Genome_prev)_\w+)\s*\(", text)
     return sorted(set(names))
 
 
@@ -100,7 +101,7 @@ GAP_ARGS = ([ctypes.c_void_p] * 7 + [ctypes.c_char_p] * 4 + [ctypes.c_int] * 4 +
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,limit", [("dp_chr17_mix", 400), ("dp_synth_cmet", 150)])
+@pytest.mark.parametrize("name,limit", [("dp_chr17_mix", 400), ("dp_synth_cmet", 150), ("gmap_synth_gap", 100000)])
 def test_dropin_gap_fillers_match_reference_golden(golden_dir, tmp_path, name, limit):
     z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
     dbl = load_double(tmp_path)
@@ -190,10 +191,11 @@ GGAP_ARGS = ([ctypes.c_void_p] * 14 + [ctypes.c_char_p] * 6 + [ctypes.c_int] * 6
 
 
 @pytest.mark.gpu
-def test_dropin_genome_gap_matches_reference_golden(golden_dir, tmp_path):
+@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap"])
+def test_dropin_genome_gap_matches_reference_golden(golden_dir, tmp_path, name):
     """Dynprog_genome_gap called like traverse_genome_gap (stage3.c:5772) on the
     reference's golden intron windows: every out-parameter and the list."""
-    z = np.load(os.path.join(golden_dir, "ggap_chr17.npz"), allow_pickle=False)
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
     dbl = load_double(tmp_path)
     L = ctypes.CDLL(DROPIN)
     L.Dynprog_new.restype = ctypes.c_void_p
@@ -532,3 +534,65 @@ def test_dropin_known_splicing_matches_reference_golden(golden_dir, tmp_path):
             assert dbl.dbl_list_protected(lst) == r["protectedp"], i
     L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dp)))
     L.Dynprog_term()
+
+
+def _last_sites_string_scan(s):
+    """find_canonical_dinucleotides (stage2.c:742-850) restated over a segment
+    string s (uppercase): lastGT/lastAG/lastCT/lastAC per position, -1 = none."""
+    n = len(s)
+    out = {k: [-1] * (n + 20) for k in ("GT", "AG", "CT", "AC")}
+    gt = ag = ct = ac = -1
+    for pos in range(1, n - 3 + 1):  # pos <= genomiclength-4 (+ the tail step at genomiclength-3)
+        if pos + 2 >= n:
+            break
+        c1, c2 = s[pos + 1], s[pos + 2]
+        if c1 == "G" and c2 == "T":
+            gt = pos
+        if c1 == "C" and c2 == "T":
+            ct = pos
+        if c1 == "A" and c2 == "G":
+            ag = pos + 3
+        if c1 == "A" and c2 == "C":
+            ac = pos + 3
+        out["GT"][pos] = gt
+        out["CT"][pos] = ct
+        out["AG"][pos + 3] = ag
+        out["AC"][pos + 3] = ac
+    return out
+
+
+def test_dropin_genome_hr_prev_sites_match_stage2_string_scan(tmp_path):
+    """Genome_prev_*_position (genome_hr.h:106-112) must agree with stage 2's own
+    string scan wherever that scan found a site (check_canonical_dinucleotides_hr,
+    stage2.c:900-970, pos5 = 1), on both strands of a segment inside a genome."""
+    sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
+    from gsnapdp import workload as W
+
+    dbl = load_double(tmp_path)
+    L = ctypes.CDLL(DROPIN)
+    g = W.synthetic_genome(20_000, seed=11, n_rate=0.01)
+    blocks = W.pack_genome(g)
+    buf = (ctypes.c_uint * blocks.size).from_buffer_copy(blocks.tobytes())
+    L.Genome_hr_user_setup(buf, ctypes.c_ubyte(0), ctypes.c_ubyte(1), 0)
+    fns = {"GT": L.Genome_prev_donor_position, "AG": L.Genome_prev_acceptor_position,
+           "AC": L.Genome_prev_antidonor_position, "CT": L.Genome_prev_antiacceptor_position}
+    for f in fns.values():
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_int, ctypes.c_ubyte]
+    gs = bytes(g).decode()
+    for start, length in ((1000, 3000), (7777, 1234), (15000, 4000)):
+        seg = gs[start:start + length]
+        for plusp, s in ((1, seg), (0, bytes(W.revcomp(np.frombuffer(seg.encode(), np.uint8))).decode())):
+            want = _last_sites_string_scan(s)
+            for key, f in fns.items():
+                for pos in range(6, length - 3):
+                    w = want[key][pos]
+                    got = f(pos, start, start + length, 1, plusp)
+                    if w != -1:
+                        assert got == w, (key, plusp, pos, got, w)
+                    else:
+                        assert got == -1 or got < 4, (key, plusp, pos, got)
+            # find_shifted_canonical's bound (pos5 = 3): nothing below it
+            assert fns["GT"](length - 4, start, start + length, 3, plusp) >= 3 or \
+                fns["GT"](length - 4, start, start + length, 3, plusp) == -1
+    del dbl

@@ -65,14 +65,15 @@ def run_gpu(blocks, b):
     return res, trc, pairs, npairs
 
 
-def test_gpu_ggap_matches_reference_golden(golden_dir):
-    z = load(golden_dir, "ggap_chr17")
+@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap"])
+def test_gpu_ggap_matches_reference_golden(golden_dir, name):
+    z = load(golden_dir, name)
     ctx = Context(z["blocks"])
     assert "gfx950" in ctx.arch
     w = z["windows"]
     res, trc, ops, off = ctx.ggap_run(w, z["query"], z["query_uc"])
     pairs, npairs = ctx.ggap_all_pairs(w, z["query"], z["query_uc"], res, trc, ops, off)
-    compare(w, res, trc, pairs, npairs, z["results"], z["pairs"], z["npairs"], "ggap_chr17")
+    compare(w, res, trc, pairs, npairs, z["results"], z["pairs"], z["npairs"], name)
     assert np.sum(z["results"]["returned_null"] == 0) > len(w) // 2 and z["pairs"].size > 1000
 
 

@@ -13,7 +13,8 @@ import pytest
 import oracle as O
 from gsnapdp.records import PAIR
 
-DP_CASES = ["dp_chr17_mix", "dp_synth_mix", "dp_synth_cmet", "dp_chr17_c2", "dp_synth_long"]
+DP_CASES = ["dp_chr17_mix", "dp_synth_mix", "dp_synth_cmet", "dp_chr17_c2", "dp_synth_long",
+            "gmap_synth_gap"]  # the last: windows the reference gmap issued (oracle/gmap_trace.c)
 
 
 def load(golden_dir, name):
@@ -45,8 +46,9 @@ def test_dp_oracle_matches_reference(golden_dir, name):
     assert goff[-1] == got.size
 
 
-def test_ggap_oracle_matches_reference(golden_dir):
-    z = load(golden_dir, "ggap_chr17")
+@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap"])
+def test_ggap_oracle_matches_reference(golden_dir, name):
+    z = load(golden_dir, name)
     O.setup(z["blocks"])
     res, pairs, off, npairs = O.run_ggap_batch(z["windows"], z["query"], z["query_uc"])
     ref = z["results"]
