@@ -282,16 +282,24 @@ __device__ void gg_fill(const Side<P>& sd, PC colv, P bnd, int L1, int rho, int 
     int Hup = NEG, Eup = NEG, Fup = NEG;   // (r-1, c-1)
     int erun = open - rho * ext;           // open + c * extend, c = t - rho
     uint32_t g = (uint32_t)colv[max(0, min(L2 + 1, -rho))];
+    // Per step: every value is computed, then selected (no per-lane branch but
+    // the in-band store).  Out of band a cell takes its initial value
+    // (dynprog.c:1460-1488) or NEG; row 0 and column 0 are never in band.
+    const bool top = rho == 0 && s > 0;  // this lane reads the stripe's boundary row
+    // the column loop, unswitched on whether the window is striped (NS > 1)
+    auto columns = [&](auto striped) {
+    constexpr bool STRIPED = decltype(striped)::value;
     for (int t = 0; t < T; t++) {
       const int c = t - rho;
       const uint32_t gn = (uint32_t)colv[max(0, min(L2 + 1, c + 1))];  // next column's value
       int Hn = from_above(Hc), En = from_above(Ec), Fn = from_above(Fc);  // (r-1, c)
-      if (rho == 0 && s > 0) {  // row above the stripe: the boundary row
-        const bool ok = c >= 0 && c <= L2;
+      if (STRIPED && s > 0) {  // wave-uniform: only striped windows read a boundary row
+        const bool ok = top && c >= 0 && c <= L2;
         const int cc = ok ? c : 0;
-        Hn = ok ? (int)bnd[3 * cc] : NEG;
-        En = ok ? (int)bnd[3 * cc + 1] : NEG;
-        Fn = ok ? (int)bnd[3 * cc + 2] : NEG;
+        const int bh = (int)bnd[3 * cc], be = (int)bnd[3 * cc + 1], bf = (int)bnd[3 * cc + 2];
+        Hn = top ? (ok ? bh : NEG) : Hn;
+        En = top ? (ok ? be : NEG) : En;
+        Fn = top ? (ok ? bf : NEG) : Fn;
       }
       // the recurrences (:1519-1561), each with the tie rule "x wins ties iff jump_late"
       const int a = Hc + open;
@@ -306,14 +314,16 @@ __device__ void gg_fill(const Side<P>& sd, PC colv, P bnd, int L1, int rho, int 
       const int sc = CD ? __builtin_amdgcn_sbfe((int)g, (int)rk, 4) : __builtin_amdgcn_sbfe((int)rk, 4 * (int)g, 4);
       const int Hr = (hF ? Fup : m1) + sc;
       const bool inb = (uint32_t)(c - cmin) <= cspan;
-      const int H = inb ? Hr : (c == hz ? 0 : NEG);
-      const int E = inb ? Er : ((uint32_t)(c - 1) < e0span ? erun : NEG);
-      const int F = inb ? Fr : (c == 0 ? F0 : NEG);
-      if (inb) {
-        const uint32_t nib = (tE ? 1u : 0u) | (tF ? 2u : 0u) | (hF ? 8u : (hE ? 4u : 0u));
-        sd.H[sbase + c] = ((uint32_t)H << 4) | nib;
-      }
-      if (NS > 1 && rho == RL - 1 && c >= 0 && c <= L2) {
+      const int Ho = c == hz ? 0 : NEG;
+      const int Eo = (uint32_t)(c - 1) < e0span ? erun : NEG;
+      const int Fo = c == 0 ? F0 : NEG;
+      const int H = inb ? Hr : Ho;
+      const int E = inb ? Er : Eo;
+      const int F = inb ? Fr : Fo;
+      const uint32_t nib = (tE ? 1u : 0u) | (tF ? 2u : 0u) | (hF ? 8u : (hE ? 4u : 0u));
+      const uint32_t word = ((uint32_t)H << 4) | nib;
+      if (inb) sd.H[sbase + c] = word;
+      if (STRIPED && rho == RL - 1 && c >= 0 && c <= L2) {
         bnd[3 * c] = (uint32_t)H;
         bnd[3 * c + 1] = (uint32_t)E;
         bnd[3 * c + 2] = (uint32_t)F;
@@ -327,6 +337,9 @@ __device__ void gg_fill(const Side<P>& sd, PC colv, P bnd, int L1, int rho, int 
       erun += ext;
       g = gn;
     }
+    };
+    if (NS > 1) columns(std::true_type{});
+    else columns(std::false_type{});
     // the boundary row is read by the next stripe's lane 0
     if constexpr (GMEM) __threadfence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);
