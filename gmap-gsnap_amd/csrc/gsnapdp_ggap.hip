@@ -241,6 +241,13 @@ __device__ inline int from_above(int v) {  // lane i receives lane i-1's v (DPP 
   return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false);
 }
 
+// The same shift into a fresh register: lane 0 of the wave reads 0 (bound_ctrl),
+// which gg_fill never uses (a group's first lane is row 0 or reads the stripe's
+// boundary row instead).
+__device__ inline int from_above_fresh(int v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true);
+}
+
 template <class P>
 struct Side {
   P H;              // L1 x W dwords: H << 4 | nibble (bit0 gap1 HORIZ, bit1 gap2 VERT,
@@ -289,10 +296,10 @@ __device__ void gg_fill(const Side<P>& sd, PC colv, P bnd, int L1, int rho, int 
     // the column loop, unswitched on whether the window is striped (NS > 1)
     auto columns = [&](auto striped) {
     constexpr bool STRIPED = decltype(striped)::value;
-    for (int t = 0; t < T; t++) {
+    auto step = [&](int t) {
       const int c = t - rho;
       const uint32_t gn = (uint32_t)colv[max(0, min(L2 + 1, c + 1))];  // next column's value
-      int Hn = from_above(Hc), En = from_above(Ec), Fn = from_above(Fc);  // (r-1, c)
+      int Hn = from_above_fresh(Hc), En = from_above_fresh(Ec), Fn = from_above_fresh(Fc);  // (r-1, c)
       if (STRIPED && s > 0) {  // wave-uniform: only striped windows read a boundary row
         const bool ok = top && c >= 0 && c <= L2;
         const int cc = ok ? c : 0;
@@ -336,7 +343,14 @@ __device__ void gg_fill(const Side<P>& sd, PC colv, P bnd, int L1, int rho, int 
       Fc = F;
       erun += ext;
       g = gn;
+    };
+    // two steps per iteration: the (r-1, c-1) values rotate without register copies
+    int t = 0;
+    for (; t + 1 < T; t += 2) {
+      step(t);
+      step(t + 1);
     }
+    if (t < T) step(t);
     };
     if (NS > 1) columns(std::true_type{});
     else columns(std::false_type{});
