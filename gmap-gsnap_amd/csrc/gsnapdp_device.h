@@ -236,7 +236,8 @@ __device__ inline void write_result(gsnapdp_result* res, const gsnapdp_window& w
 // Windows the register-band kernel does not take (end gaps, wide or long
 // single gaps) run on the row-lane kernel k_rows (gsnapdp_ggap.hip): rows on
 // lanes, band cells (H << 4 | dirs) in LDS, or in global scratch when large.
-enum { RW_SMALL = 0, RW_MID = 1, RW_LARGE = 2, RW_BIG = 3, RW_NCLS = 4 };
+enum { RW_SMALL = 0, RW_MID = 1, RW_LARGE = 2, RW_BIG = 3, RW_TINY = 4, RW_NCLS = 5 };
+constexpr int RW_TINY_WORDS = 640;               // LDS words per window, 16-row groups (4 per wave)
 constexpr int RW_SMALL_WORDS = 1280;             // LDS words per window, 32-row groups
 constexpr int RW_MID_WORDS = 4096;               // LDS words per window, 64-row stripes
 constexpr int RW_LARGE_WORDS = 16384;            // global words per wave (64 KB)
@@ -253,6 +254,7 @@ __host__ __device__ inline size_t rows_words(int L1, int L2, int W) {
 }
 __host__ __device__ inline int rows_class(int L1, int L2, int W) {
   const size_t words = rows_words(L1, L2, W);
+  if (L1 + 1 <= 16 && words <= (size_t)RW_TINY_WORDS) return RW_TINY;
   if (L1 + 1 <= 32 && words <= (size_t)RW_SMALL_WORDS) return RW_SMALL;
   if (words <= (size_t)RW_MID_WORDS) return RW_MID;
   if (words <= (size_t)RW_LARGE_WORDS) return RW_LARGE;

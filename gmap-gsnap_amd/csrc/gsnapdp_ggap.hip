@@ -1279,13 +1279,18 @@ int gsnapdp__rows_pools(gsnapdp_ctx* ctx) {
   return 0;
 }
 
-// the four row-lane classes, one launch each (lists[c * list_cap ...], counts[c])
+// the row-lane classes, one launch each (lists[c * list_cap ...], counts[c])
 template <bool SEG>
 static int rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* dw, const int* lists,
                        const int* counts, int list_cap, const char* d_query, const char* d_query_uc,
                        gsnapdp_result* d_results, uint32_t* d_ops, const int64_t* d_op_offsets,
                        const gsnapdp_sj_window* sjw) {
   const uint64_t nw = (uint64_t)ctx->nwords;
+  constexpr int tiny_blocks = 160 * 1024 / (16 * RW_TINY_WORDS * 4);
+  hipLaunchKernelGGL((k_rows<16, false, SEG>), dim3(ctx->num_cus * tiny_blocks), dim3(256),
+                     (size_t)16 * RW_TINY_WORDS * 4, st, dw, lists + (size_t)RW_TINY * list_cap,
+                     counts + RW_TINY, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
+                     (uint32_t*)nullptr, (size_t)RW_TINY_WORDS, d_results, d_ops, d_op_offsets, sjw);
   constexpr int small_blocks = 160 * 1024 / (8 * RW_SMALL_WORDS * 4);
   hipLaunchKernelGGL((k_rows<32, false, SEG>), dim3(ctx->num_cus * small_blocks), dim3(256),
                      (size_t)8 * RW_SMALL_WORDS * 4, st, dw, lists, counts + RW_SMALL, d_query,

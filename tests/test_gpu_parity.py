@@ -96,10 +96,12 @@ def test_gpu_maxent_matches_reference(golden_dir, name):
 
 
 def rows_class(L1, L2, W):
-    """gsnapdp_device.h rows_class: 0 small (LDS, 32-row groups), 1 mid (LDS,
-    64-row stripes), 2 big (global scratch)."""
+    """gsnapdp_device.h rows_class: 4 tiny (LDS, 16-row groups), 0 small (LDS,
+    32-row groups), 1 mid (LDS, 64-row stripes), 2 big (global scratch)."""
     stripes = (L1 + 1 + 63) // 64
     words = L1 * W + (L2 + 2 + 3) // 4 + (L1 + 1) // 2 + (3 * (L2 + 2) if stripes > 1 else 0)
+    if L1 + 1 <= 16 and words <= 640:
+        return 4
     if L1 + 1 <= 32 and words <= 1280:
         return 0
     return 1 if words <= 4096 else 2
@@ -119,7 +121,7 @@ def test_gpu_end_gaps_every_row_class(seed):
     eb = w["extraband"].astype(np.int64)
     Wd = np.abs(L2 - L1) + 2 * eb + 1
     cls = np.array([rows_class(a, b, c) for a, b, c in zip(L1, L2, Wd)])
-    assert all(np.sum(cls == c) > 50 for c in (0, 1, 2)), np.bincount(cls)
+    assert all(np.sum(cls == c) > 50 for c in (0, 1, 2, 4)), np.bincount(cls)
     res, pairs, npairs, ref, oflat, onp = run_both(blocks, batch)
     compare(res, pairs, npairs, ref, oflat, onp, "end gaps seed %d" % seed)
 
