@@ -409,6 +409,18 @@ def main() -> None:
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        if world == 1:
+            # the host-buffer boundary (gsnapdp_run_host: H2D of windows and queries, the same
+            # kernels, D2H of results and op streams) on the same batch -- never `value`
+            ctx.run(batch.windows, batch.query, batch.query_uc)
+            reps = 5
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.run(batch.windows, batch.query, batch.query_uc)
+            host_ms = 1000.0 * (time.perf_counter() - t0) / reps
+            out["pcie_inclusive"] = {"value": round(n / (host_ms * 1e-3), 1), "unit": "reads/s",
+                                     "ms_per_batch": round(host_ms, 4), "reads": n,
+                                     "entry": "gsnapdp_run_host (host buffers in and out)"}
         if not args.no_c4 and world == 1:
             out["c4"] = measure_c4(genome, args.c4_windows, args.steps, args.warmup, dev, not args.no_cpu)
         if not args.no_c5 and world == 1:

@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -51,16 +52,6 @@ struct State {
 State g;
 enum { CALL_GAP, CALL_SJ, CALL_GGAP, CALL_CGAP, CALL_MICRO, CALL_MAXENT };
 
-struct StatsAtExit {
-  ~StatsAtExit() {
-    if (!getenv("GSNAPDP_DROPIN_STATS")) return;
-    fprintf(stderr,
-            "gsnapdp_dropin: GPU calls: gap %lu, splicejunction %lu, genome_gap %lu, cdna_gap %lu, "
-            "microexon %lu, maxent %lu\n",
-            g.ncalls[CALL_GAP], g.ncalls[CALL_SJ], g.ncalls[CALL_GGAP], g.ncalls[CALL_CGAP],
-            g.ncalls[CALL_MICRO], g.ncalls[CALL_MAXENT]);
-  }
-} stats_at_exit;
 
 [[noreturn]] void fatal(const std::string& msg) {
   fprintf(stderr, "gsnapdp drop-in: %s\n", msg.c_str());
@@ -102,37 +93,131 @@ void ensure_tables() {
 
 // One window through the GPU; pushes its pairs (final list order) into the
 // pool, last pair first, so the list head is the first pair.
+// ---- gap windows from concurrent callers, combined into batches
+// gmap / gsnap call Dynprog_single_gap / end5 / end3 synchronously from each
+// worker thread.  A caller queues its window; whichever caller finds no batch
+// in flight becomes the leader, takes every queued window, runs them as one
+// gsnapdp_run_host batch and wakes their owners, which expand their own op
+// streams into their own Pairpools.  One thread alone sees one-window batches.
+struct GapReq {
+  gsnapdp_window w;  // qpos relative to q / qu below
+  std::vector<char> q, qu;
+  int64_t cap = 0;
+  gsnapdp_result r;
+  std::vector<uint32_t> ops;
+  bool done = false;
+};
+
+struct GapCombiner {
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<GapReq*> pending;
+  bool busy = false;
+  std::vector<gsnapdp_window> W;
+  std::vector<char> Q, QU;
+  std::vector<gsnapdp_result> R;
+  std::vector<uint32_t> OPS;
+  std::vector<int64_t> OFF;
+  unsigned long batches = 0, maxbatch = 0;
+};
+GapCombiner gcomb;
+
+struct StatsAtExit {
+  ~StatsAtExit() {
+    if (!getenv("GSNAPDP_DROPIN_STATS")) return;
+    fprintf(stderr,
+            "gsnapdp_dropin: GPU calls: gap %lu, splicejunction %lu, genome_gap %lu, cdna_gap %lu, "
+            "microexon %lu, maxent %lu; gap batches %lu (largest %lu)\n",
+            g.ncalls[CALL_GAP], g.ncalls[CALL_SJ], g.ncalls[CALL_GGAP], g.ncalls[CALL_CGAP],
+            g.ncalls[CALL_MICRO], g.ncalls[CALL_MAXENT], gcomb.batches, gcomb.maxbatch);
+  }
+} stats_at_exit;
+
+// the leader, without gcomb.m held: one batch over the taken requests
+void run_gap_batch(gsnapdp_ctx* c, const std::vector<GapReq*>& b) {
+  GapCombiner& G = gcomb;
+  const size_t n = b.size();
+  size_t qn = 0;
+  for (const GapReq* x : b) qn += x->q.size();
+  G.W.resize(n);
+  G.R.resize(n);
+  G.OFF.assign(n + 1, 0);
+  G.Q.resize(qn);
+  G.QU.resize(qn);
+  size_t qo = 0;
+  for (size_t i = 0; i < n; i++) {
+    const GapReq* x = b[i];
+    G.W[i] = x->w;
+    G.W[i].qpos = x->w.qpos + (uint32_t)qo;
+    memcpy(G.Q.data() + qo, x->q.data(), x->q.size());
+    memcpy(G.QU.data() + qo, x->qu.data(), x->qu.size());
+    qo += x->q.size();
+    G.OFF[i + 1] = G.OFF[i] + x->cap;
+  }
+  G.OPS.assign((size_t)G.OFF[n] + 1, 0u);
+  if (gsnapdp_run_host(c, G.W.data(), (int)n, G.Q.data(), G.QU.data(), G.Q.size(), G.R.data(),
+                       G.OPS.data(), G.OFF.data()))
+    fatal(std::string("gsnapdp_run_host: ") + gsnapdp_last_error());
+  for (size_t i = 0; i < n; i++) {
+    b[i]->r = G.R[i];
+    b[i]->ops.assign(G.OPS.begin() + G.OFF[i], G.OPS.begin() + G.OFF[i + 1]);
+  }
+}
+
 gsnapdp_List_T run_one(gsnapdp_window& w, const char* seq, const char* sequc, bool rev,
                        gsnapdp_Pairpool_T pool, int* dynprogindex, int* finalscore,
                        int* nmatches, int* nmismatches, int* nopens, int* nindels) {
-  std::lock_guard<std::mutex> lock(g.mu);
-  gsnapdp_ctx* c = ctx();
+  gsnapdp_ctx* c;
+  {
+    std::lock_guard<std::mutex> lock(g.mu);
+    c = ctx();
+  }
+  GapReq req;
   const int L1 = w.length1 > 0 ? w.length1 : 0;
-  // query bytes the reference may read: sequence1[0..L1) or revsequence1[-(L1-1)..0]
-  g.q.assign((size_t)L1 + 8, 0);
-  g.qu.assign((size_t)L1 + 8, 0);
+  // query bytes the reference may read: sequence1[0..L1) or revsequence1[-(L1-1)..0],
+  // padded to a 4-byte multiple (the kernels read dwords)
+  const size_t qsz = ((size_t)L1 + 8 + 3) & ~(size_t)3;
+  req.q.assign(qsz, 0);
+  req.qu.assign(qsz, 0);
   if (L1 > 0) {
-    const char* s = rev ? seq - (L1 - 1) : seq;
-    const char* u = rev ? sequc - (L1 - 1) : sequc;
-    memcpy(g.q.data(), s, (size_t)L1);
-    memcpy(g.qu.data(), u, (size_t)L1);
+    memcpy(req.q.data(), rev ? seq - (L1 - 1) : seq, (size_t)L1);
+    memcpy(req.qu.data(), rev ? sequc - (L1 - 1) : sequc, (size_t)L1);
   }
   w.qpos = rev ? (uint32_t)(L1 > 0 ? L1 - 1 : 0) : 0u;
-  const int64_t cap = (int64_t)L1 + (w.length2 > 0 ? w.length2 : 0) + 2;
-  const int64_t off[2] = {0, cap};
-  g.ops.assign((size_t)cap + 1, 0u);
-  gsnapdp_result r;
-  g.ncalls[CALL_GAP]++;
-  if (gsnapdp_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, g.ops.data(), off))
-    fatal(std::string("gsnapdp_run_host: ") + gsnapdp_last_error());
+  req.w = w;
+  req.cap = (int64_t)L1 + (w.length2 > 0 ? w.length2 : 0) + 2;
+  {
+    std::unique_lock<std::mutex> lk(gcomb.m);
+    gcomb.pending.push_back(&req);
+    while (!req.done) {
+      if (!gcomb.busy) {
+        gcomb.busy = true;
+        std::vector<GapReq*> batch;
+        batch.swap(gcomb.pending);
+        lk.unlock();
+        run_gap_batch(c, batch);
+        lk.lock();
+        for (GapReq* x : batch) x->done = true;
+        g.ncalls[CALL_GAP] += batch.size();
+        gcomb.batches++;
+        if (batch.size() > gcomb.maxbatch) gcomb.maxbatch = batch.size();
+        gcomb.busy = false;
+        gcomb.cv.notify_all();
+      } else {
+        gcomb.cv.wait(lk);
+      }
+    }
+  }
+  const gsnapdp_result& r = req.r;
   if (r.status == gsnapdp::ST_UNSUPPORTED)
     fatal("window outside the reference's domain (the reference aborts here)");
   if (r.status == gsnapdp::ST_OPS_OVERFLOW) fatal("op stream overflow");
-  g.pairs.resize((size_t)cap + 8);
+  thread_local std::vector<gsnapdp_pair> pairs;
+  pairs.resize((size_t)req.cap + 8);
   int fs = 0;
-  const int n = gsnapdp_expand(c, &w, &r, g.ops.data(), g.q.data(), g.qu.data(), g.pairs.data(),
-                               (int)g.pairs.size(), &fs);
-  if (n < 0 || n > (int)g.pairs.size()) fatal("gsnapdp_expand failed");
+  const int n = gsnapdp_expand(c, &w, &r, req.ops.data(), req.q.data(), req.qu.data(), pairs.data(),
+                               (int)pairs.size(), &fs);
+  if (n < 0 || n > (int)pairs.size()) fatal("gsnapdp_expand failed");
   *dynprogindex = r.reserved;  // the stepped *dynprogindex
   *finalscore = r.finalscore;
   *nmatches = r.nmatches;
@@ -141,7 +226,7 @@ gsnapdp_List_T run_one(gsnapdp_window& w, const char* seq, const char* sequc, bo
   *nindels = r.nindels;
   gsnapdp_List_T list = nullptr;
   for (int i = n - 1; i >= 0; i--) {
-    const gsnapdp_pair& p = g.pairs[(size_t)i];
+    const gsnapdp_pair& p = pairs[(size_t)i];
     if (p.gapp)
       list = Pairpool_push_gapholder(list, pool, p.queryjump, p.genomejump, (p.gapp & 2) ? 1 : 0);
     else
@@ -356,6 +441,15 @@ SolveFn solver(bool end5) {
 }  // namespace
 
 extern "C" {
+
+int Gsnapdp_dropin_stats(unsigned long* out, int n) {
+  const unsigned long v[8] = {g.ncalls[CALL_GAP], g.ncalls[CALL_SJ], g.ncalls[CALL_GGAP],
+                              g.ncalls[CALL_CGAP], g.ncalls[CALL_MICRO], g.ncalls[CALL_MAXENT],
+                              gcomb.batches, gcomb.maxbatch};
+  std::lock_guard<std::mutex> lock(gcomb.m);
+  for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
+  return 8;
+}
 
 int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device) {
   std::lock_guard<std::mutex> lock(g.mu);

@@ -229,6 +229,12 @@ double Maxent_hr_antiacceptor_prob(gsnapdp_Genomicpos_T splice_pos,
  * (3 per 32 nt plus the reference's padding).  `device` = HIP device index. */
 int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device);
 
+/* Counters of this process's GPU work: out[0..5] = windows run for the gap,
+ * splice-junction, genome-gap, cDNA-gap, microexon and MaxEnt entry points;
+ * out[6] = gap batches, out[7] = the largest (concurrent Dynprog_single_gap /
+ * end5 / end3 callers are combined into one batch).  Returns 8. */
+int Gsnapdp_dropin_stats(unsigned long* out, int n);
+
 /* ---- genome_hr subset (the reference's genome_hr.c is a missing blob;
  * gmap-gsnap_amd/csrc/genome_hr_sites.c): the setup calls gmap.c makes
  * (gmap.c:3801, 3810) and the splice-site dinucleotide queries of stage 2

@@ -596,3 +596,81 @@ def test_dropin_genome_hr_prev_sites_match_stage2_string_scan(tmp_path):
             assert fns["GT"](length - 4, start, start + length, 3, plusp) >= 3 or \
                 fns["GT"](length - 4, start, start + length, 3, plusp) == -1
     del dbl
+
+
+@pytest.mark.gpu
+def test_dropin_concurrent_callers_are_batched(golden_dir, tmp_path):
+    """Worker threads calling Dynprog_single_gap / end5 / end3 at once (gmap -t N)
+    get their windows combined into shared GPU batches, with every result still
+    the reference's: the gap windows gmap itself issued (gmap_synth_gap)."""
+    import threading
+    import time
+
+    z = np.load(os.path.join(golden_dir, "gmap_synth_gap.npz"), allow_pickle=False)
+    dbl = load_double(tmp_path)
+    L = ctypes.CDLL(DROPIN)
+    L.Dynprog_new.restype = ctypes.c_void_p
+    L.Dynprog_new.argtypes = [ctypes.c_int] * 5
+    L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    for f in ("Dynprog_single_gap", "Dynprog_end5_gap", "Dynprog_end3_gap"):
+        getattr(L, f).restype = ctypes.c_void_p
+        getattr(L, f).argtypes = GAP_ARGS + [ctypes.c_int, ctypes.c_ubyte]
+    stats = (ctypes.c_ulong * 8)()
+    blocks = np.ascontiguousarray(z["blocks"])
+    L.Dynprog_init(600, 10, 11, 10, 8, int(z["mode"]))
+    L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
+    q = np.ascontiguousarray(z["query"])
+    qu = np.ascontiguousarray(z["query_uc"])
+    offs = np.zeros(len(z["npairs"]) + 1, dtype=np.int64)
+    np.cumsum(z["npairs"], out=offs[1:])
+    W = z["windows"]
+    want = np.stack([z[f] for f in ("dynprogindex", "finalscore", "nmatches", "nmismatches", "nopens",
+                                    "nindels")], axis=1)
+
+    def worker(idx, bad):
+        dp = L.Dynprog_new(600, 10, 11, 10, 8)  # one Dynprog_T per thread, as gmap's workers
+        out = np.zeros(8192, dtype=REC)
+        for i in idx:
+            w = W[i]
+            ints = [ctypes.c_int(int(w["dynprogindex"]))] + [ctypes.c_int(0) for _ in range(5)]
+            common = [ctypes.byref(x) for x in ints] + [
+                dp, ctypes.c_char_p(q.ctypes.data + int(w["qpos"])),
+                ctypes.c_char_p(qu.ctypes.data + int(w["qpos"])), None, None, int(w["length1"]),
+                int(w["length2"]), int(w["offset1"]), int(w["offset2"]), int(w["chroffset"]),
+                int(w["chrhigh"]), int(w["chrpos"]), int(w["genomiclength"]), int(w["cdna_direction"]),
+                int(w["watsonp"]), int(w["jump_late_p"]), None, int(w["extraband"]), float(w["defect_rate"])]
+            kind = int(w["kind"])
+            if kind == SINGLE_GAP:
+                lst = L.Dynprog_single_gap(*common, 0, int(w["widebandp"]))
+            elif kind == END5_GAP:
+                lst = L.Dynprog_end5_gap(*common, int(w["endalign"]), 0)
+            else:
+                lst = L.Dynprog_end3_gap(*common, int(w["endalign"]), 0)
+            k = dbl.dbl_list_read(lst, out.ctypes.data, out.size)
+            if [x.value for x in ints] != want[i].tolist() or k != int(z["npairs"][i]) or \
+                    out[:k].tobytes() != z["pairs"][offs[i]:offs[i + 1]].tobytes():
+                bad.append(i)
+            dbl.dbl_list_free(lst)
+        L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dp)))
+
+    def run(nthreads):
+        L.Gsnapdp_dropin_stats(stats, 8)
+        b0 = stats[6]
+        bad = []
+        ts = [threading.Thread(target=worker, args=(range(t, len(W), nthreads), bad)) for t in range(nthreads)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        el = time.perf_counter() - t0
+        L.Gsnapdp_dropin_stats(stats, 8)
+        return el, stats[6] - b0, bad
+
+    t1, b1, bad1 = run(1)
+    t16, b16, bad16 = run(16)
+    print("%d gmap gap windows: 1 thread %.3f s (%d batches), 16 threads %.3f s (%d batches, largest %d)"
+          % (len(W), t1, b1, t16, b16, stats[7]))
+    assert not bad1 and not bad16, (bad1[:5], bad16[:5])
+    assert b1 == len(W) and b16 < len(W) and stats[7] > 1
+    L.Dynprog_term()
