@@ -38,7 +38,9 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
                        int* __restrict__ hist, int* __restrict__ big_list,
                        int* __restrict__ big_count, int list_cap) {
   __shared__ int lh[NKEYS];  // block-local histogram: one global atomic per key per block
+  __shared__ int lbig[RW_NCLS], lbase[RW_NCLS];  // block-local row-lane list appends
   for (int k = threadIdx.x; k < NKEYS; k += blockDim.x) lh[k] = 0;
+  if (threadIdx.x < RW_NCLS) lbig[threadIdx.x] = 0;
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   int key = -1, big = -1;  // k_fill bucket key, or row-lane class
@@ -88,14 +90,16 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
     keys[i] = key;
   }
   if (key >= 0) atomicAdd(&lh[key], 1);
-#pragma unroll
-  for (int c = 0; c < RW_NCLS; c++) {  // one list append per row-lane class per wave
-    const int slot = agg_atomic_inc(big_count + c, big == c ? 0 : -1);
-    if (big == c) big_list[(size_t)c * list_cap + slot] = i;
-  }
+  const int lslot = big >= 0 ? atomicAdd(&lbig[big], 1) : 0;
   __syncthreads();
+  // one global append per non-empty row-lane class per block (list order is free:
+  // k_rows writes each window's own result slot)
+  if (threadIdx.x < RW_NCLS)
+    lbase[threadIdx.x] = lbig[threadIdx.x] > 0 ? atomicAdd(big_count + threadIdx.x, lbig[threadIdx.x]) : 0;
   for (int k = threadIdx.x; k < NKEYS; k += blockDim.x)
     if (lh[k] > 0) atomicAdd(&hist[k], lh[k]);
+  __syncthreads();
+  if (big >= 0) big_list[(size_t)big * list_cap + lbase[big] + lslot] = i;
 }
 
 // Exclusive scan of bucket sizes, each padded to whole waves of its class
