@@ -1,15 +1,20 @@
 #!/usr/bin/env python3
-"""Benchmark: GMAP/GSNAP stage-3 single-gap DP on MI355X (BASELINE config 2).
+"""Benchmark: GMAP/GSNAP stage-3 single-gap DP on MI355X (BASELINE config 3).
 
-One step = one pass of the hot path (Dynprog_single_gap fill + endpoint +
-traceback, batched through gsnapdp_run_device) over one batch of 100k
-synthetic 150 bp reads (band 31, 2 % substitutions, 30 % with a 1-3 bp indel)
-already resident in HBM.  N GPUs: one process per GPU, each aligning its own
-100k-read shard against a replicated genome (weak scaling, no data-path
-collective: windows are independent).
+One step = one pass of the hot path over ONE read batch: 1,000,000 synthetic
+150 bp reads (2 % substitutions, 30 % with a 1-3 bp indel, band 31) against a
+GRCh38-sized synthetic genome (24 chromosomes with the GRCh38 lengths, 3.09
+Gnt, 1.16 GB packed, resident in HBM), each read one Dynprog_single_gap window
+(fill + endpoint + traceback through gsnapdp_run_device), plus the op-stream
+compaction, and -- for N GPUs -- the RCCL gather of every rank's result
+records and compact op streams to rank 0.  The batch is FIXED: N GPUs split it
+per read into slices balanced by in-band cells (strong scaling, SURVEY.md
+8(e)).  Side lines at N=1: C2 (100k reads, 64 Mbp genome), C4, C5 (DP part),
+splice-junction ends, microexons, the PCIe-inclusive host-buffer rate.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1 under torch.distributed.run, see the task contract)
+       --gpus N > 1 without a launcher re-runs itself under
+       torch.distributed.run (one process per GPU) before touching the GPU.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -27,7 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
 
 import torch  # noqa: E402
 
-from gsnapdp import Context, op_offsets, shard  # noqa: E402
+from gsnapdp import Context, gather, op_offsets, shard  # noqa: E402
 from gsnapdp import workload as W  # noqa: E402
 from gsnapdp.records import RESULT  # noqa: E402
 
@@ -37,8 +42,10 @@ HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # SIMD (fp32 FMA issues at 2 cycles): 256 CU x 4 SIMD x 16 lanes x 2.4 GHz
 VALU_INT32_PEAK = 256 * 4 * 16 * 2.4e9
 OPS_PER_CELL = 14             # gap1 4 + gap2 4 + nogap 6 int32 ops
-READS_PER_GPU = 100_000
-GENOME_NT = 64_000_000
+C3_READS = 1_000_000          # BASELINE config 3: one fixed batch, split across the GPUs
+C2_READS = 100_000            # side line: BASELINE config 2
+GENOME_NT = 64_000_000        # side-line genome (C2, C4, C5, ...)
+MIN_STEADY_S = 1.0            # steady-state figure: at least this many seconds of steps
 DOMINANT = "k_fill"           # every C2 window is a register-band (k_fill) window
 C4_WINDOWS = 200_000          # intron windows per config-4 step
 C5_READS = 100_000            # reads per config-5 step (3 DP windows each)
@@ -67,9 +74,10 @@ def band_cells(w: np.ndarray) -> int:
     return total
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/*_traffic.json, written by tools/pmc_traffic.py), or None."""
+def pmc_traffic(kernel: str, workload: str):
+    """HBM bytes per launch of `kernel` on `workload` from the committed
+    rocprofv3 PMC passes (profiles/*_traffic.json, written by
+    tools/pmc_traffic.py), or None.  Last file by name wins."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
@@ -77,9 +85,50 @@ def pmc_traffic(kernel: str):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("kernel") == kernel:
-            best = (d["traffic_bytes"], os.path.basename(f))
+        if d.get("kernel") == kernel and d.get("workload", "C2") == workload:
+            best = (d["traffic_bytes"], os.path.basename(f), d.get("dispatches"))
     return best
+
+
+def rocprof_kernel_ms(kernel: str, workload: str):
+    """Average duration (ms) of `kernel` in the committed rocprofv3
+    --kernel-trace --stats summary of this bench on `workload`
+    (profiles/*_<workload>_kernel_stats.csv), or None."""
+    import csv
+    import glob
+    best = None
+    pat = os.path.join(ROOT, "profiles", "*_%s_kernel_stats.csv" % workload.lower())
+    for f in sorted(glob.glob(pat)):
+        try:
+            for row in csv.DictReader(open(f)):
+                if row.get("Name", "").split("(")[0].strip().endswith(kernel):
+                    best = (float(row["AverageNs"]) / 1e6, os.path.basename(f))
+        except (OSError, ValueError, KeyError):
+            continue
+    return best
+
+
+def cells_per_window(w: np.ndarray) -> np.ndarray:
+    """In-band cells of every window (band_cells per distinct shape)."""
+    key = np.stack([w["length1"], w["length2"], w["extraband"]], axis=1).astype(np.int64)
+    shapes, inv = np.unique(key, axis=0, return_inverse=True)
+    per = np.array([band_cells(w[np.flatnonzero(inv.reshape(-1) == k)[:1]]) for k in range(len(shapes))],
+                   dtype=np.int64)
+    return per[inv.reshape(-1)]
+
+
+def cpu_info():
+    """(allotted threads, host CPU count, CPU model string)."""
+    threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, os.cpu_count(), model
 
 
 def measure_c4(genome, n, steps, warmup, dev, with_cpu):
@@ -274,47 +323,122 @@ def measure_micro(genome, n, steps, warmup, dev, with_cpu):
     return out
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--reads", type=int, default=READS_PER_GPU)
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--no-c4", action="store_true", help="skip the config-4 (genome gap) side line")
-    ap.add_argument("--c4-windows", type=int, default=C4_WINDOWS)
-    ap.add_argument("--no-c5", action="store_true", help="skip the config-5 (GSNAP windows) side line")
-    ap.add_argument("--no-extra", action="store_true",
-                    help="skip the splice-junction / microexon side lines")
-    args = ap.parse_args()
-
-    ranks = shard.init_from_env("nccl")
-    world, rank, local = ranks.world, ranks.rank, ranks.local
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    # ---- workload (identical genome on every rank, a disjoint read shard per rank)
-    genome = W.synthetic_genome(GENOME_NT, seed=1)
-    blocks = W.pack_genome(genome)
-    batch = W.c2_windows(genome, n=args.reads, seed=shard.shard_seed(2, rank))
-    n = len(batch)
+def measure_c2(genome, n, steps, warmup, dev):
+    """Side line, BASELINE config 2 (round-1 headline): 100k reads on the 64 Mbp
+    genome, one GPU, device-resident; per-kernel event times."""
+    batch = W.c2_windows(genome, n=n, seed=2)
+    ctx = Context(W.pack_genome(genome), mode=0, device=dev.index)
     off = op_offsets(batch.windows)
-    ctx = Context(blocks, mode=0, device=local)
-
     d_w = torch.from_numpy(batch.windows.view(np.uint8).copy()).to(dev)
     d_q = torch.from_numpy(batch.query.copy()).to(dev)
     d_u = torch.from_numpy(batch.query_uc.copy()).to(dev)
     d_off = torch.from_numpy(off.copy()).to(dev)
     d_res = torch.zeros(n * RESULT.itemsize, dtype=torch.uint8, device=dev)
     d_ops = torch.zeros(int(off[-1]) + 1, dtype=torch.int32, device=dev)
-    torch.cuda.synchronize()
 
     def step():
         ctx.run_device(d_w.data_ptr(), n, d_q.data_ptr(), d_u.data_ptr(), d_res.data_ptr(),
                        d_ops.data_ptr(), d_off.data_ptr())
+    el = timed(step, ctx.sync, steps, warmup)
+    names = ctx.profile(True)
+    acc = np.zeros(len(names))
+    for _ in range(steps):
+        step()
+        ctx.profile_read(acc)
+    ctx.profile(False)
+    ctx.close()
+    return {"workload": "C2: Dynprog_single_gap, %d x 150 bp reads, 64 Mbp genome, extraband 15" % n,
+            "value": round(n * steps / el, 1), "unit": "reads/s", "ms_per_step": round(1000 * el / steps, 4),
+            "kernel_ms_per_step": {nm: round(acc[i] / steps, 4) for i, nm in enumerate(names) if acc[i] > 0}}
+
+
+def relaunch_if_needed(args) -> None:
+    """--gpus N > 1 without a launcher: run this script under
+    torch.distributed.run as a child (before anything touches the GPU) and
+    exit with its status.  Under a launcher, WORLD_SIZE must equal N."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None and args.gpus > 1:
+        import socket
+        import subprocess
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    if int(world or "1") != args.gpus:
+        sys.stderr.write("bench.py: --gpus %d but WORLD_SIZE=%s\n" % (args.gpus, world))
+        sys.exit(2)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--reads", type=int, default=C3_READS, help="reads in the (fixed) batch")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
+    ap.add_argument("--no-side", action="store_true", help="skip every side line (C2, C4, C5, sj, micro, PCIe)")
+    ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--no-c5", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the splice-junction / microexon side lines")
+    ap.add_argument("--c4-windows", type=int, default=C4_WINDOWS)
+    args = ap.parse_args()
+    relaunch_if_needed(args)
+
+    ranks = shard.init_from_env("nccl")
+    world, rank, local = ranks.world, ranks.rank, ranks.local
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    # ---- workload: the same fixed batch on every rank, sliced per read (balanced by in-band cells)
+    g = W.c3_genome(seed=3)
+    batch = W.c3_windows(g, n=args.reads, seed=33)
+    cells = cells_per_window(batch.windows)
+    spans = shard.balanced_ranges(cells, world)
+    lo, hi = spans[rank]
+    sizes = [b - a for a, b in spans]
+    n = hi - lo
+    stride = int(batch.windows["qpos"][1] - batch.windows["qpos"][0]) if len(batch) > 1 else 158
+    wl = batch.windows[lo:hi].copy()
+    wl["qpos"] -= np.uint32(lo * stride)
+    ql = batch.query[lo * stride:hi * stride]
+    off = op_offsets(wl)
+    ctx = Context(g.blocks, mode=0, device=local)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    d_w = torch.from_numpy(wl.view(np.uint8).copy()).to(dev)
+    d_q = torch.from_numpy(ql.copy()).to(dev)
+    d_off = torch.from_numpy(off.copy()).to(dev)
+    d_ops = torch.zeros(int(off[-1]) + 1, dtype=torch.int32, device=dev)
+    lay = gather.Layout(max(sizes), gather.op_budget(max(sizes)))
+    pay = [torch.zeros(lay.nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+    recv = [[torch.zeros(lay.nbytes, dtype=torch.uint8, device=dev) for _ in range(world)]
+            if (rank == 0 and world > 1) else None for _ in range(2)]
+    pending = [None, None]
+    nstep = [0]
+    torch.cuda.synchronize()
+
+    def step():
+        b = nstep[0] & 1
+        nstep[0] += 1
+        if pending[b] is not None:  # the gather that last read this payload (stream-ordered wait)
+            pending[b].wait()
+            pending[b] = None
+        base = pay[b].data_ptr()
+        ctx.run_device(d_w.data_ptr(), n, d_q.data_ptr(), d_q.data_ptr(), base + lay.res_off,
+                       d_ops.data_ptr(), d_off.data_ptr(), stream=sp)
+        ctx.compact_ops_device(base + lay.res_off, n, d_ops.data_ptr(), d_off.data_ptr(), base + lay.ops_off,
+                               lay.budget, base, stream=sp)
+        if world > 1:
+            pending[b] = shard.gather_to_root(ranks, pay[b], recv[b], async_op=True)
 
     def sync():
-        ctx.sync()
+        for b in (0, 1):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -324,7 +448,13 @@ def main() -> None:
     # ---- timed region: exactly K steps, barrier + sync on both sides, max over ranks
     elapsed = shard.timed_steps(ranks, step, args.steps, sync)
     ms_per_step = 1000.0 * elapsed / args.steps
-    value = shard.aggregate_rate(n, ranks, args.steps, elapsed)
+    value = args.reads * args.steps / elapsed  # the whole fixed batch per step, all ranks together
+    steady = None
+    if elapsed < MIN_STEADY_S:
+        k2 = int(np.ceil(MIN_STEADY_S / (elapsed / args.steps)))
+        el2 = shard.timed_steps(ranks, step, k2, sync)
+        steady = {"steps": k2, "seconds": round(el2, 4), "value": round(args.reads * k2 / el2, 1),
+                  "ms_per_step": round(1000.0 * el2 / k2, 4)}
 
     # ---- per-kernel durations (HIP events on the launch stream), same K steps
     names = ctx.profile(True)
@@ -333,48 +463,68 @@ def main() -> None:
         step()
         ctx.profile_read(acc)
     ctx.profile(False)
+    sync()
     kernel_ms = {nm: acc[i] / args.steps for i, nm in enumerate(names) if acc[i] > 0}
+    last = (nstep[0] - 1) & 1
 
-    # ---- results of the last step: sanity + algorithmic bytes
-    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=RESULT)
-    Wd = (batch.windows["extraband"].astype(np.int64) * 2 + 1
-          + np.abs(batch.windows["length2"].astype(np.int64) - batch.windows["length1"]))
-    dom = (Wd <= 48) & (batch.windows["length2"] <= 640)  # k_fill's windows (FAST_WMAX, FAST_L2MAX)
-    dom_bytes = float(window_bytes(batch.windows[dom], res["nops"][dom]).sum())
+    # ---- this rank's results (last step): sanity + algorithmic bytes of the dominant kernel
+    res_l = np.frombuffer(pay[last][lay.res_off:lay.res_off + n * RESULT.itemsize].cpu().numpy().tobytes(),
+                          dtype=RESULT)
+    Wd = (wl["extraband"].astype(np.int64) * 2 + 1 + np.abs(wl["length2"].astype(np.int64) - wl["length1"]))
+    dom = (Wd <= 48) & (wl["length2"] <= 640)  # k_fill's windows (FAST_WMAX, FAST_L2MAX)
+    dom_bytes = float(window_bytes(wl[dom], res_l["nops"][dom]).sum())
     dom_ms = kernel_ms.get(DOMINANT, float("nan"))
     achieved_gbs = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms == dom_ms else None
-    cells = band_cells(batch.windows)
     fill_ms = sum(v for k, v in kernel_ms.items() if k.startswith("k_fill"))
+    cells_local = int(cells[lo:hi].sum())
+    traffic = pmc_traffic(DOMINANT, "C3")
+    rp = rocprof_kernel_ms(DOMINANT, "C3")
 
-    traffic = pmc_traffic(DOMINANT)
     out = None
     if rank == 0:
-        cpu = None
-        parity = None
+        # ---- the gathered batch (every rank's payload of the last step) on the root
+        bufs = ([t.cpu().numpy() for t in recv[last]] if world > 1 else [pay[last].cpu().numpy()])
+        res, cops, coff = gather.reassemble(lay, bufs, sizes)
+        threads, host_cpus, cpu_model = cpu_info()
+        cpu = parity = None
         if not args.no_cpu:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle as O  # CPU restatement: baseline + checker only
-            O.setup(blocks)
-            cores = 16
-            sample = min(n, 100_000)
-            ws = batch.windows[:sample]
-            t1 = time.perf_counter()
-            reps = 0
-            while True:
-                ores, _, _, _ = O.run_batch(ws, batch.query, batch.query_uc, nthreads=cores)
-                reps += 1
-                if time.perf_counter() - t1 > 3.0:
-                    break
-            cpu_rate = reps * sample / (time.perf_counter() - t1)
+            O.setup(g.blocks)
+            fields = ("finalscore", "nmatches", "nmismatches", "nopens", "nindels", "reserved")
+            same = True
+            t_cpu = 0.0
+            chunk = 125_000
+            for a in range(0, args.reads, chunk):
+                ws = batch.windows[a:a + chunk]
+                t1 = time.perf_counter()
+                ores, _, _, _ = O.run_batch(ws, batch.query, batch.query_uc, nthreads=threads)
+                t_cpu += time.perf_counter() - t1
+                same = same and all(np.array_equal(res[f][a:a + chunk], ores[f]) for f in fields)
             t2 = time.perf_counter()
-            O.run_batch(ws[:10_000], batch.query, batch.query_uc, nthreads=1)
-            cpu1 = 10_000 / (time.perf_counter() - t2)
-            same = all(np.array_equal(res[f][:sample], ores[f]) for f in
-                       ("finalscore", "nmatches", "nmismatches", "nopens", "nindels"))
-            parity = {"windows_checked": sample, "scores_and_counts_bit_exact": bool(same)}
-            cpu = {"value": round(cpu_rate, 1), "unit": "reads/s", "cores": cores, "kind": "port",
-                   "sample": "%d C2 windows x %d passes (oracle/ restatement, pthreads); 1 core: %.0f reads/s"
-                             % (sample, reps, cpu1)}
+            one = min(args.reads, 20_000)
+            O.run_batch(batch.windows[:one], batch.query, batch.query_uc, nthreads=1)
+            cpu1 = one / (time.perf_counter() - t2)
+            # full pair lists of a sample, expanded from the GATHERED compact op streams
+            rng = np.random.default_rng(0)
+            samp = np.unique(np.concatenate([np.arange(min(500, args.reads)),
+                                             rng.integers(0, args.reads, size=min(1500, args.reads))]))
+            ores, opairs, ooff, onp = O.run_batch(batch.windows[samp], batch.query, batch.query_uc,
+                                                  nthreads=threads)
+            pairs_ok = True
+            for j, i in enumerate(samp.tolist()):
+                p, _ = ctx.pairs(batch.windows, batch.query, batch.query_uc, res, cops, coff, i)
+                if p.tobytes() != opairs[ooff[j]:ooff[j] + onp[j]].tobytes():
+                    pairs_ok = False
+                    break
+            parity = {"windows_checked": args.reads, "fields": list(fields), "scores_and_counts_bit_exact": bool(same),
+                      "pair_lists_checked": int(samp.size), "pair_lists_bit_exact": bool(pairs_ok),
+                      "source": "results + compact op streams gathered to rank 0 (%d rank%s)"
+                                % (world, "s" if world > 1 else "")}
+            cpu = {"value": round(args.reads / t_cpu, 1), "unit": "reads/s", "cores": threads, "kind": "port",
+                   "host_cpus": host_cpus, "cpu_model": cpu_model,
+                   "sample": "the whole %d-read C3 batch once (oracle/ restatement, %d pthreads, %.1f s); "
+                             "1 thread: %.0f reads/s on %d reads" % (args.reads, threads, t_cpu, cpu1, one)}
         out = {
             "metric": "aligned reads/sec (whole node), 150 bp vs GRCh38; bit-exact vs CPU dynprog",
             "value": round(value, 1),
@@ -384,50 +534,60 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (64 Mbp uniform genome with N runs; 150 bp reads, 2% subs, 30% 1-3 bp indels)",
-            "config": {"workload": "C2: Dynprog_single_gap, %d x 150 bp reads per GPU, extraband 15 (band 31), "
-                                   "widebandp, HIGHQ, both strands" % n,
-                       "reads_per_gpu": n, "genome_nt": GENOME_NT, "parallelism": "dp%d" % world},
+            "data": "synthetic (GRCh38-shaped genome: 24 chromosomes with the GRCh38 lengths, uniform ACGT, 0.1% N "
+                    "runs; 150 bp reads from both strands, 2% subs, 0.1% N, 30% with a 1-3 bp indel)",
+            "config": {"workload": "C3: Dynprog_single_gap, one fixed batch of %d x 150 bp reads vs a %.2f Gnt "
+                                   "GRCh38-sized genome, extraband 15 (band 31), widebandp, HIGHQ, both strands; "
+                                   "split per read over %d GPU%s, RCCL gather of results + compact op streams "
+                                   "to rank 0" % (args.reads, g.total / 1e9, world, "s" if world > 1 else ""),
+                       "reads": args.reads, "genome_nt": g.total, "reads_per_gpu": sizes,
+                       "parallelism": "dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2) if achieved_gbs else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 5) if achieved_gbs else None,
                          "traffic": traffic[0] if traffic else None,
                          "traffic_source": traffic[1] if traffic else None,
                          "algorithmic_bytes": round(dom_bytes), "kernel": DOMINANT,
-                         "kernel_ms": round(dom_ms, 4), "windows_in_kernel": int(dom.sum())},
+                         "kernel_ms": round(dom_ms, 4), "kernel_ms_rocprof": round(rp[0], 4) if rp else None,
+                         "rocprof_source": rp[1] if rp else None, "windows_in_kernel": int(dom.sum())},
             "roofline_valu": {"bound": "valu-int32", "unit": "int32 ops/s",
-                              "achieved": round(cells * OPS_PER_CELL / (fill_ms * 1e-3), 1) if fill_ms else None,
+                              "achieved": round(cells_local * OPS_PER_CELL / (fill_ms * 1e-3), 1) if fill_ms else None,
                               "peak": VALU_INT32_PEAK,
-                              "frac": round(cells * OPS_PER_CELL / (fill_ms * 1e-3) / VALU_INT32_PEAK, 4)
+                              "frac": round(cells_local * OPS_PER_CELL / (fill_ms * 1e-3) / VALU_INT32_PEAK, 4)
                               if fill_ms else None,
-                              "note": "14 ops per in-band cell over all k_fill launches (SURVEY.md 8(d))"},
+                              "note": "14 ops per in-band cell over all k_fill launches (SURVEY.md 8(d)); peak at "
+                                      "the measured 4-cycle int32 issue (tools/ubench/valu_rate.hip)"},
             "kernel_ms_per_step": {k: round(v, 4) for k, v in kernel_ms.items()},
-            "gcups": round(cells * args.steps * world / elapsed / 1e9, 2),
+            "gcups": round(float(cells.sum()) * args.steps / elapsed / 1e9, 2),
+            "steady_state": steady,
             "cpu_baseline": cpu,
             "parity": parity,
         }
-        if world == 1:
+        if world == 1 and not args.no_side:
+            genome = W.synthetic_genome(GENOME_NT, seed=1)
+            out["c2"] = measure_c2(genome, C2_READS, 20, args.warmup, dev)
             # the host-buffer boundary (gsnapdp_run_host: H2D of windows and queries, the same
-            # kernels, D2H of results and op streams) on the same batch -- never `value`
-            ctx.run(batch.windows, batch.query, batch.query_uc)
+            # kernels, D2H of results and op streams) on 100k reads of the batch -- never `value`
+            sub = W.Batch(batch.windows[:100_000], batch.query[:100_000 * stride], batch.query_uc[:100_000 * stride])
+            ctx.run(sub.windows, sub.query, sub.query_uc)
             reps = 5
             t0 = time.perf_counter()
             for _ in range(reps):
-                ctx.run(batch.windows, batch.query, batch.query_uc)
+                ctx.run(sub.windows, sub.query, sub.query_uc)
             host_ms = 1000.0 * (time.perf_counter() - t0) / reps
-            out["pcie_inclusive"] = {"value": round(n / (host_ms * 1e-3), 1), "unit": "reads/s",
-                                     "ms_per_batch": round(host_ms, 4), "reads": n,
+            out["pcie_inclusive"] = {"value": round(len(sub) / (host_ms * 1e-3), 1), "unit": "reads/s",
+                                     "ms_per_batch": round(host_ms, 4), "reads": len(sub),
                                      "entry": "gsnapdp_run_host (host buffers in and out)"}
-        if not args.no_c4 and world == 1:
-            out["c4"] = measure_c4(genome, args.c4_windows, args.steps, args.warmup, dev, not args.no_cpu)
-        if not args.no_c5 and world == 1:
-            out["c5"] = measure_c5(genome, C5_READS, args.steps, args.warmup, dev, not args.no_cpu)
-        if not args.no_extra and world == 1:
-            out["splicejunction"] = measure_sj(genome, 100_000, args.steps, args.warmup, dev, not args.no_cpu)
-            out["microexon"] = measure_micro(genome, 20_000, args.steps, args.warmup, dev, not args.no_cpu)
+            if not args.no_c4:
+                out["c4"] = measure_c4(genome, args.c4_windows, 20, args.warmup, dev, not args.no_cpu)
+            if not args.no_c5:
+                out["c5"] = measure_c5(genome, C5_READS, 20, args.warmup, dev, not args.no_cpu)
+            if not args.no_extra:
+                out["splicejunction"] = measure_sj(genome, 100_000, 20, args.warmup, dev, not args.no_cpu)
+                out["microexon"] = measure_micro(genome, 20_000, 20, args.warmup, dev, not args.no_cpu)
         print(json.dumps(out), flush=True)
     shard.finish(ranks)
     ctx.close()

@@ -74,5 +74,8 @@ struct gsnapdp_ctx {
   int sj_cap = 0;
   int* d_sj_lists = nullptr;        // RW_NCLS class lists of sj_cap entries, then the counts
   gsnapdp_window* d_sj_win = nullptr;  // the end-gap records k_sj_plan derives
+  // op-stream compaction (gsnapdp_gather.hip): per-block op counts
+  int csum_cap = 0;
+  int64_t* d_csum = nullptr;
 };
 

@@ -979,6 +979,7 @@ extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   (void)hipFree(ctx->d_sj_lists);
   (void)hipFree(ctx->d_sj_win);
   (void)hipFree(ctx->d_stage);
+  (void)hipFree(ctx->d_csum);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

@@ -93,6 +93,8 @@ def lib():
         L.gsnapdp_micro_run_device.restype = i32
         L.gsnapdp_micro_expand.argtypes = [vp, vp, vp, vp, vp, vp, i32]
         L.gsnapdp_micro_expand.restype = i32
+        L.gsnapdp_compact_ops_device.argtypes = [vp, vp, i32, vp, vp, vp, ctypes.c_int64, vp, vp]
+        L.gsnapdp_compact_ops_device.restype = i32
         _lib = L
     return _lib
 
@@ -359,6 +361,17 @@ class Context:
                                       ctypes.c_void_p(stream) if stream else None)
         if rc != 0:
             raise GsnapdpError("gsnapdp_run_device: %s" % lib().gsnapdp_last_error().decode())
+
+    def compact_ops_device(self, d_results: int, n: int, d_ops: int, d_op_offsets: int, d_out: int,
+                           out_cap: int, d_header: int, stream: int = 0) -> None:
+        """Op streams of a finished batch, packed in window order (gsnapdp_compact_ops_device);
+        d_header (2 x int64) receives {total ops, overflow}."""
+        rc = lib().gsnapdp_compact_ops_device(self.h, ctypes.c_void_p(d_results), n, ctypes.c_void_p(d_ops),
+                                              ctypes.c_void_p(d_op_offsets), ctypes.c_void_p(d_out), out_cap,
+                                              ctypes.c_void_p(d_header),
+                                              ctypes.c_void_p(stream) if stream else None)
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_compact_ops_device: %s" % lib().gsnapdp_last_error().decode())
 
     def profile(self, enable: bool) -> list:
         """Enable per-kernel HIP-event timing; returns the stage names."""

@@ -1,9 +1,12 @@
 """Multi-GPU plumbing of the benchmark and of batch drivers.
 
-Windows are independent, so N GPUs run N disjoint shards
-against a replicated genome with no data-path collective: one process per GPU,
-torch.distributed only for the start/stop barrier and the max-over-ranks time.
-The same functions run under the ``gloo`` backend on CPU for the tests.
+Windows are independent: one read batch is split per read
+into contiguous slices balanced by in-band cells (``balanced_ranges``), every
+rank aligns its slice against a replicated genome, and the result records +
+compact op streams come back to the root rank in ONE collective per batch
+(``gather_to_root``: RCCL over xGMI on the GPUs).  One process per GPU;
+torch.distributed also carries the start/stop barrier and the max-over-ranks
+time.  The same functions run under the ``gloo`` backend on CPU for the tests.
 """
 from __future__ import annotations
 
@@ -49,6 +52,39 @@ def shard_range(n_total: int, rank: int, world: int) -> tuple[int, int]:
     per = (n_total + world - 1) // world
     lo = min(n_total, rank * per)
     return lo, min(n_total, lo + per)
+
+
+def balanced_ranges(weights, world: int) -> list[tuple[int, int]]:
+    """Contiguous [lo, hi) slices of a batch, one per rank, balanced by the
+    windows' weights (in-band cells); every window lands in
+    exactly one slice and slices follow batch order."""
+    import numpy as np
+    w = np.asarray(weights, dtype=np.float64)
+    n = w.size
+    if world <= 1 or n == 0:
+        return [(0, n)] + [(n, n)] * max(0, world - 1)
+    cum = np.concatenate([[0.0], np.cumsum(w)])  # cum[c] = weight of windows [0, c)
+    cuts = [0]
+    for k in range(1, world):
+        t = cum[-1] * k / world
+        c = int(np.searchsorted(cum, t, side="left"))  # first cut with weight >= t
+        if c > 0 and t - cum[c - 1] <= cum[min(c, n)] - t:
+            c -= 1
+        cuts.append(c)
+    cuts.append(n)
+    cuts = np.maximum.accumulate(np.clip(cuts, 0, n))
+    return [(int(cuts[k]), int(cuts[k + 1])) for k in range(world)]
+
+
+def gather_to_root(r: Ranks, payload, recv: Optional[list] = None, async_op: bool = False):
+    """Gather every rank's payload (equal-size tensors) into `recv` on rank 0:
+    one collective (RCCL gather over xGMI on the GPUs, gloo on CPU).  Returns
+    the work handle when async_op."""
+    if r.dist is None:
+        if recv is not None:
+            recv[0].copy_(payload)
+        return None
+    return r.dist.gather(payload, gather_list=recv if r.rank == 0 else None, dst=0, async_op=async_op)
 
 
 def timed_steps(r: Ranks, step: Callable[[], None], steps: int, sync: Callable[[], None]) -> float:

@@ -843,3 +843,151 @@ def write_fasta(path: str, records, width: int = 60) -> None:
             f.write(b">" + name.encode() + b"\n")
             for i in range(0, len(seq), width):
                 f.write(seq[i:i + width] + b"\n")
+
+
+# ---------------------------------------------------------------------------
+# BASELINE config 3: 150 bp reads against a GRCh38-sized genome.
+# No GRCh38 index exists here (no network), so the genome is synthetic with
+# the 24 primary GRCh38 chromosome lengths (chr1..chr22, X, Y; 3.09 Gnt, 1.16 GB
+# packed), generated directly in the packed block format: for a uniform ACGT
+# genome the (high, low) words of a block are uniform random 32-bit words.
+GRCH38_CHROMS = (
+    ("chr1", 248956422), ("chr2", 242193529), ("chr3", 198295559), ("chr4", 190214555),
+    ("chr5", 181538259), ("chr6", 170805979), ("chr7", 159345973), ("chr8", 145138636),
+    ("chr9", 138394717), ("chr10", 133797422), ("chr11", 135086622), ("chr12", 133275309),
+    ("chr13", 114364328), ("chr14", 107043718), ("chr15", 101991189), ("chr16", 90338345),
+    ("chr17", 83257441), ("chr18", 80373285), ("chr19", 58617616), ("chr20", 64444167),
+    ("chr21", 46709983), ("chr22", 50818468), ("chrX", 156040895), ("chrY", 57227415),
+)
+
+
+class PackedGenome:
+    """Packed blocks (genome.c:9325 layout, +4 guard words) plus the chromosome
+    table GMAP keeps beside them (chroffset = cumulative start, chrhigh =
+    chroffset + length)."""
+
+    def __init__(self, blocks: np.ndarray, names, lengths: np.ndarray):
+        self.blocks = blocks
+        self.names = list(names)
+        self.lengths = np.asarray(lengths, dtype=np.int64)
+        self.offsets = np.concatenate([[0], np.cumsum(self.lengths)[:-1]]).astype(np.int64)
+        self.total = int(self.lengths.sum())
+
+    def decode(self, pos: np.ndarray) -> np.ndarray:
+        """Genome characters at absolute positions (uncompress_one_char, genome.c:9325)."""
+        return decode_blocks(self.blocks, pos)
+
+
+def decode_blocks(blocks: np.ndarray, pos: np.ndarray) -> np.ndarray:
+    pos = np.asarray(pos, dtype=np.int64)
+    ptr = (pos >> 5) * 3
+    bit = (pos & 31).astype(np.uint32)
+    word = np.where(bit < 16, blocks[ptr + 1], blocks[ptr])
+    c = (word >> ((bit & 15) * 2)) & 3
+    ch = ACGT[c]
+    return np.where(((blocks[ptr + 2] >> bit) & 1) == 1, np.uint8(ord("N")), ch).astype(np.uint8)
+
+
+def c3_genome(seed: int = 3, scale: float = 1.0, n_rate: float = 0.001) -> PackedGenome:
+    """GRCh38-shaped synthetic genome in packed form.  `scale` < 1 shrinks every
+    chromosome (tests); 1.0 is the C3 size.  ~n_rate N bases in runs of 1-10."""
+    rng = np.random.default_rng(seed)
+    lengths = np.array([max(4096, int(l * scale)) for _, l in GRCH38_CHROMS], dtype=np.int64)
+    total = int(lengths.sum())
+    nblocks = (total + 31) // 32
+    hl = rng.integers(0, 1 << 32, size=2 * nblocks, dtype=np.uint32)
+    high, low = hl[:nblocks], hl[nblocks:]
+    flags = np.zeros(nblocks, dtype=np.uint32)
+    nruns = int(total * n_rate / 5.5)
+    if nruns:
+        starts = rng.integers(0, total, size=nruns)
+        lens = rng.integers(1, 11, size=nruns)
+        pos = np.repeat(starts, lens) + (np.arange(int(lens.sum())) - np.repeat(np.cumsum(lens) - lens, lens))
+        pos = np.unique(pos[pos < total])
+        blk, bit = pos >> 5, (pos & 31).astype(np.uint32)
+        np.bitwise_or.at(flags, blk, np.uint32(1) << bit)
+        lo = bit < 16  # N = A + flag: clear the 2-bit code
+        np.bitwise_and.at(low, blk[lo], ~(np.uint32(3) << (2 * bit[lo])))
+        np.bitwise_and.at(high, blk[~lo], ~(np.uint32(3) << (2 * (bit[~lo] - 16))))
+    tail = nblocks * 32 - total  # X past the end (Genome_create_blocks)
+    if tail:
+        for b in range(32 - tail, 32):
+            flags[-1] |= np.uint32(1) << np.uint32(b)
+            if b < 16:
+                low[-1] |= np.uint32(3) << np.uint32(2 * b)
+            else:
+                high[-1] |= np.uint32(3) << np.uint32(2 * (b - 16))
+    blocks = np.empty(3 * nblocks + 4, dtype=np.uint32)
+    blocks[0:3 * nblocks:3] = high
+    blocks[1:3 * nblocks:3] = low
+    blocks[2:3 * nblocks:3] = flags
+    blocks[3 * nblocks:] = 0xFFFFFFFF
+    return PackedGenome(blocks, [n for n, _ in GRCH38_CHROMS], lengths)
+
+
+def c3_windows(g: PackedGenome, n: int = 1_000_000, seed: int = 33, read_len: int = 150,
+               extraband: int = 15, indel_frac: float = 0.3, sub_rate: float = 0.02,
+               n_rate: float = 0.001, margin: int = 8, chunk: int = 131072) -> Batch:
+    """BASELINE config 3: `n` Dynprog_single_gap windows of 150 bp reads drawn
+    from every chromosome (length-weighted), either strand, 2 % substitutions,
+    0.1 % N, 30 % with one 1-3 bp indel; extraband 15, widebandp, HIGHQ,
+    jump_late_p = !watsonp (stage1hr.c:11288).  Vectorised (same read model as
+    c2_windows, its own random stream)."""
+    rng = np.random.default_rng(seed)
+    stride = read_len + 8
+    w = np.zeros(n, dtype=WINDOW)
+    qbuf = np.full((n, stride), ord("#"), dtype=np.uint8)
+    ci = rng.choice(len(g.lengths), size=n, p=g.lengths / g.lengths.sum())
+    chrlen = g.lengths[ci]
+    has = rng.random(n) < indel_frac
+    ilen = rng.integers(1, 4, size=n)
+    sign = rng.integers(0, 2, size=n) * 2 - 1  # +1: genome longer (deletion in the read)
+    L2 = read_len + np.where(has, sign * ilen, 0)
+    watson = rng.integers(0, 2, size=n).astype(bool)
+    start = (rng.random(n) * (chrlen - read_len - 16 - 3 * margin)).astype(np.int64) + 2 * margin
+    seg_start = start - margin
+    glen = L2 + 2 * margin
+    kdel = np.maximum(L2 - read_len, 0)
+    kins = np.maximum(read_len - L2, 0)
+    p = np.where(kdel > 0, rng.integers(10, read_len - 10, size=n),
+                 (rng.random(n) * (L2 - 20)).astype(np.int64) + 10)
+    ins_bases = rng.integers(0, 4, size=(n, 3))
+    k = np.arange(read_len)[None, :]
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        s = slice(lo, hi)
+        pk, kd, ki = p[s, None], kdel[s, None], kins[s, None]
+        j = k + np.where(k >= pk, kd, 0) - np.where(k >= pk + ki, ki, 0)  # window column of base k
+        inserted = (k >= pk) & (k < pk + ki)
+        base = g.offsets[ci[s], None] + seg_start[s, None]
+        gp = np.where(watson[s, None], base + margin + j, base + glen[s, None] - 1 - margin - j)
+        q = g.decode(np.where(inserted, base + margin, gp))
+        q = np.where(watson[s, None], q, _COMP[q])
+        rnd = ACGT[ins_bases[s][np.arange(hi - lo)[:, None], np.clip(k - pk, 0, 2)]]
+        q = np.where(inserted, rnd, q)
+        m = rng.random(q.shape)
+        sub = m < sub_rate
+        q[sub] = ACGT[(np.searchsorted(ACGT, q[sub]) + rng.integers(1, 4, size=int(sub.sum()))) % 4]
+        q[(m >= sub_rate) & (m < sub_rate + n_rate)] = ord("N")
+        qbuf[s, :read_len] = q
+    w["kind"] = SINGLE_GAP
+    w["length1"] = read_len
+    w["length2"] = L2
+    w["offset1"] = 0
+    w["offset2"] = margin
+    w["chroffset"] = g.offsets[ci]
+    w["chrhigh"] = g.offsets[ci] + chrlen
+    w["chrpos"] = seg_start
+    w["genomiclength"] = glen
+    w["qpos"] = np.arange(n, dtype=np.int64) * stride
+    w["cdna_direction"] = 1
+    w["extraband"] = extraband
+    w["dynprogindex"] = 1
+    w["maxlength1"] = MAXLENGTH1
+    w["maxlength2"] = MAXLENGTH2
+    w["defect_rate"] = 0.001
+    w["watsonp"] = watson.astype(np.uint8)
+    w["jump_late_p"] = 1 - w["watsonp"]
+    w["widebandp"] = 1
+    q = qbuf.reshape(-1)
+    return Batch(w, q, q.copy())

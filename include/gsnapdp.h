@@ -248,6 +248,18 @@ int gsnapdp_run_device(gsnapdp_ctx *ctx, const gsnapdp_window *d_windows, int n,
  * the context and grown on demand; this is informational. */
 size_t gsnapdp_scratch_bytes(gsnapdp_ctx *ctx, int n, int max_length1, int max_length2);
 
+/* Compact a finished batch's op streams for the multi-GPU gather (SURVEY.md
+ * 8(e): result records + compact op streams are all that leave a GPU).
+ * Window i's min(results[i].nops, op_offsets[i+1]-op_offsets[i]) ops are
+ * written consecutively, windows in batch order, to d_out, so a receiver
+ * rebuilds every window's offset from the nops column (exclusive prefix sum).
+ * d_header (2 x int64, device) receives {total ops, overflow}: overflow = 1
+ * when total > out_cap, in which case only the windows that fit entirely
+ * were written.  Asynchronous on `stream` (NULL = context stream). */
+int gsnapdp_compact_ops_device(gsnapdp_ctx *ctx, const gsnapdp_result *d_results, int n,
+                               const uint32_t *d_ops, const int64_t *d_op_offsets, uint32_t *d_out,
+                               int64_t out_cap, int64_t *d_header, void *stream);
+
 /* Synchronise the context stream. */
 int gsnapdp_sync(gsnapdp_ctx *ctx);
 

@@ -499,60 +499,78 @@ def gmap_trace_case(seed: int = 7) -> None:
     aligning synthetic spliced cDNAs (workload.synthetic_transcripts) with
     `gmap -A -g`, replayed through ref_driver for the full outputs; each replay
     is checked against the result gmap itself got from the call."""
-    sys.path.insert(0, HERE)
-    import oracle as O  # checker, used only to drop windows the reference cannot run (UB)
     g, q = W.synthetic_transcripts(seed=seed, ngenes=40, genome_len=300_000)
     with tempfile.TemporaryDirectory() as d:
         W.write_fasta(os.path.join(d, "g.fa"), [("synthchr", g)])
         W.write_fasta(os.path.join(d, "q.fa"), q)
-        env = dict(os.environ, GMAP_TRACE_DIR=os.path.join(d, "trace"))
-        subprocess.check_call([GMAP_TRACE, "-A", "-g", os.path.join(d, "g.fa"), os.path.join(d, "q.fa")],
-                              env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-        t = os.path.join(d, "trace", "dp")
-        blocks = np.fromfile(os.path.join(t, "genome.u32"), dtype="<u4")
-        w = np.fromfile(os.path.join(t, "windows.bin"), dtype=W.WINDOW)
-        qb = np.fromfile(os.path.join(t, "query.bin"), dtype=np.uint8)
-        ub = np.fromfile(os.path.join(t, "query_uc.bin"), dtype=np.uint8)
-        got = np.fromfile(os.path.join(t, "gmap_results.bin"), dtype=RECORDED)
-        run_driver("dp", t)
-        res = np.fromfile(os.path.join(t, "results.bin"), dtype=RESULT)
-        npairs = np.fromfile(os.path.join(t, "npairs.i32"), dtype=np.int32)
-        pairs = np.fromfile(os.path.join(t, "pairs.bin"), dtype=PAIR)
-        for f in ("finalscore", "nmatches", "nmismatches", "nopens", "nindels"):
-            assert np.array_equal(res[f], got[f]), f
-        assert np.array_equal(res["reserved"], got["dynprogindex"]) and np.array_equal(npairs, got["npairs"])
-        np.savez_compressed(os.path.join(OUT, "gmap_synth_gap.npz"), blocks=blocks, windows=w, query=qb,
-                            query_uc=ub, mode=np.int32(0), finalscore=res["finalscore"],
-                            nmatches=res["nmatches"], nmismatches=res["nmismatches"], nopens=res["nopens"],
-                            nindels=res["nindels"], dynprogindex=res["reserved"], npairs=npairs, pairs=pairs)
-        print("gmap_synth_gap: %d windows (%s), %d pairs" % (
-            len(w), ", ".join("kind %d: %d" % (k, int((w["kind"] == k).sum())) for k in np.unique(w["kind"])),
-            pairs.size))
+        trace_gmap_run("gmap_synth", os.path.join(d, "g.fa"), os.path.join(d, "q.fa"), d)
 
-        t = os.path.join(d, "trace", "ggap")
-        w = np.fromfile(os.path.join(t, "ggap_windows.bin"), dtype=GGAP_WINDOW)
-        qb = np.fromfile(os.path.join(t, "query.bin"), dtype=np.uint8)
-        ub = np.fromfile(os.path.join(t, "query_uc.bin"), dtype=np.uint8)
-        got = np.fromfile(os.path.join(t, "gmap_results.bin"), dtype=GGAP_RESULT)
-        O.setup(blocks)
-        ores, _, _, _ = O.run_ggap_batch(w, qb, ub)
-        keep = ores["bridge_ok"] == 1  # dynprog.c:4055 reads uninitialised indices otherwise
-        w, got = w[keep], got[keep]
-        w.tofile(os.path.join(t, "ggap_windows.bin"))
-        run_driver("ggap", t)
-        res = np.fromfile(os.path.join(t, "ggap_results.bin"), dtype=GGAP_RESULT)
-        npairs = np.fromfile(os.path.join(t, "npairs.i32"), dtype=np.int32)
-        pairs = np.fromfile(os.path.join(t, "pairs.bin"), dtype=PAIR)
-        # probability mode never writes *introntype (bridge_intron_gap, dynprog.c:3829-4081): gmap's
-        # variable keeps an earlier call's value, ref_driver's starts at 0
-        prob = w["use_probabilities_p"] == 1
-        got["introntype"][prob] = res["introntype"][prob]
-        assert res.tobytes() == got.tobytes()
-        np.savez_compressed(os.path.join(OUT, "gmap_synth_ggap.npz"), blocks=blocks, windows=w, query=qb,
-                            query_uc=ub, results=res, npairs=npairs, pairs=pairs,
-                            dropped_ub=np.int32((~keep).sum()))
-        print("gmap_synth_ggap: %d windows (%d dropped: probability-mode UB; %d probability mode), %d pairs" %
-              (len(w), int((~keep).sum()), int(w["use_probabilities_p"].sum()), pairs.size))
+
+def gmap_her2_case() -> None:
+    """BASELINE config 1: the gap windows of `gmap -A -g ss.chr17test ss.her2`
+    (the reference's own align.test, tests/align.test.in:9-10), whose output
+    gmap_trace reproduces byte for byte (tests/align.test.ok)."""
+    with tempfile.TemporaryDirectory() as d:
+        out = trace_gmap_run("gmap_her2", os.path.join(REF_TESTS, "ss.chr17test"),
+                             os.path.join(REF_TESTS, "ss.her2"), d)
+        with open(os.path.join(REF_TESTS, "align.test.ok"), "rb") as f:
+            assert out == f.read(), "gmap_trace output differs from align.test.ok"
+
+
+def trace_gmap_run(prefix: str, genome_fa: str, query_fa: str, d: str) -> bytes:
+    """Run gmap_trace on (genome, queries), replay every recorded window through
+    ref_driver, check it against what gmap got, write PREFIX_gap / PREFIX_ggap."""
+    sys.path.insert(0, HERE)
+    import oracle as O  # checker, used only to drop windows the reference cannot run (UB)
+    env = dict(os.environ, GMAP_TRACE_DIR=os.path.join(d, "trace"))
+    out = subprocess.run([GMAP_TRACE, "-A", "-g", genome_fa, query_fa], env=env, stdout=subprocess.PIPE,
+                         stderr=subprocess.DEVNULL, check=True).stdout
+    t = os.path.join(d, "trace", "dp")
+    blocks = np.fromfile(os.path.join(t, "genome.u32"), dtype="<u4")
+    w = np.fromfile(os.path.join(t, "windows.bin"), dtype=W.WINDOW)
+    qb = np.fromfile(os.path.join(t, "query.bin"), dtype=np.uint8)
+    ub = np.fromfile(os.path.join(t, "query_uc.bin"), dtype=np.uint8)
+    got = np.fromfile(os.path.join(t, "gmap_results.bin"), dtype=RECORDED)
+    run_driver("dp", t)
+    res = np.fromfile(os.path.join(t, "results.bin"), dtype=RESULT)
+    npairs = np.fromfile(os.path.join(t, "npairs.i32"), dtype=np.int32)
+    pairs = np.fromfile(os.path.join(t, "pairs.bin"), dtype=PAIR)
+    for f in ("finalscore", "nmatches", "nmismatches", "nopens", "nindels"):
+        assert np.array_equal(res[f], got[f]), f
+    assert np.array_equal(res["reserved"], got["dynprogindex"]) and np.array_equal(npairs, got["npairs"])
+    np.savez_compressed(os.path.join(OUT, prefix + "_gap.npz"), blocks=blocks, windows=w, query=qb,
+                        query_uc=ub, mode=np.int32(0), finalscore=res["finalscore"],
+                        nmatches=res["nmatches"], nmismatches=res["nmismatches"], nopens=res["nopens"],
+                        nindels=res["nindels"], dynprogindex=res["reserved"], npairs=npairs, pairs=pairs)
+    print("%s_gap: %d windows (%s), %d pairs" % (
+        prefix, len(w), ", ".join("kind %d: %d" % (k, int((w["kind"] == k).sum())) for k in np.unique(w["kind"])),
+        pairs.size))
+
+    t = os.path.join(d, "trace", "ggap")
+    w = np.fromfile(os.path.join(t, "ggap_windows.bin"), dtype=GGAP_WINDOW)
+    qb = np.fromfile(os.path.join(t, "query.bin"), dtype=np.uint8)
+    ub = np.fromfile(os.path.join(t, "query_uc.bin"), dtype=np.uint8)
+    got = np.fromfile(os.path.join(t, "gmap_results.bin"), dtype=GGAP_RESULT)
+    O.setup(blocks)
+    ores, _, _, _ = O.run_ggap_batch(w, qb, ub)
+    keep = ores["bridge_ok"] == 1  # dynprog.c:4055 reads uninitialised indices otherwise
+    w, got = w[keep], got[keep]
+    w.tofile(os.path.join(t, "ggap_windows.bin"))
+    run_driver("ggap", t)
+    res = np.fromfile(os.path.join(t, "ggap_results.bin"), dtype=GGAP_RESULT)
+    npairs = np.fromfile(os.path.join(t, "npairs.i32"), dtype=np.int32)
+    pairs = np.fromfile(os.path.join(t, "pairs.bin"), dtype=PAIR)
+    # probability mode never writes *introntype (bridge_intron_gap, dynprog.c:3829-4081): gmap's
+    # variable keeps an earlier call's value, ref_driver's starts at 0
+    prob = w["use_probabilities_p"] == 1
+    got["introntype"][prob] = res["introntype"][prob]
+    assert res.tobytes() == got.tobytes()
+    np.savez_compressed(os.path.join(OUT, prefix + "_ggap.npz"), blocks=blocks, windows=w, query=qb,
+                        query_uc=ub, results=res, npairs=npairs, pairs=pairs,
+                        dropped_ub=np.int32((~keep).sum()))
+    print("%s_ggap: %d windows (%d dropped: probability-mode UB; %d probability mode), %d pairs" %
+          (prefix, len(w), int((~keep).sum()), int(w["use_probabilities_p"].sum()), pairs.size))
+    return out
 
 
 def main() -> None:
@@ -583,6 +601,7 @@ def main() -> None:
         ("maxent_chr17", lambda: maxent_case("maxent_chr17", b17, chr17.size, 20000, seed=301)),
         ("maxent_synth", lambda: maxent_case("maxent_synth", bsyn, synth.size, 6000, seed=302)),
         ("gmap_trace", lambda: gmap_trace_case()),
+        ("gmap_her2", lambda: gmap_her2_case()),
     ]
     for name, fn in cases:
         if not only or name in only:

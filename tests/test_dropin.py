@@ -101,7 +101,8 @@ GAP_ARGS = ([ctypes.c_void_p] * 7 + [ctypes.c_char_p] * 4 + [ctypes.c_int] * 4 +
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,limit", [("dp_chr17_mix", 400), ("dp_synth_cmet", 150), ("gmap_synth_gap", 100000)])
+@pytest.mark.parametrize("name,limit", [("dp_chr17_mix", 400), ("dp_synth_cmet", 150), ("gmap_synth_gap", 100000),
+                                        ("gmap_her2_gap", 100000)])
 def test_dropin_gap_fillers_match_reference_golden(golden_dir, tmp_path, name, limit):
     z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
     dbl = load_double(tmp_path)
@@ -191,7 +192,7 @@ GGAP_ARGS = ([ctypes.c_void_p] * 14 + [ctypes.c_char_p] * 6 + [ctypes.c_int] * 6
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap"])
+@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap", "gmap_her2_ggap"])
 def test_dropin_genome_gap_matches_reference_golden(golden_dir, tmp_path, name):
     """Dynprog_genome_gap called like traverse_genome_gap (stage3.c:5772) on the
     reference's golden intron windows: every out-parameter and the list."""

@@ -65,7 +65,7 @@ def run_gpu(blocks, b):
     return res, trc, pairs, npairs
 
 
-@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap"])
+@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap", "gmap_her2_ggap"])
 def test_gpu_ggap_matches_reference_golden(golden_dir, name):
     z = load(golden_dir, name)
     ctx = Context(z["blocks"])

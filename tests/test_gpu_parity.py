@@ -13,7 +13,7 @@ from gsnapdp.records import END3_GAP, END5_GAP, PAIR
 pytestmark = pytest.mark.gpu
 
 DP_CASES = ["dp_chr17_mix", "dp_synth_mix", "dp_synth_cmet", "dp_chr17_c2", "dp_synth_long",
-            "gmap_synth_gap"]  # the last: windows the reference gmap issued (oracle/gmap_trace.c)
+            "gmap_synth_gap", "gmap_her2_gap"]  # the last two: windows the reference gmap issued (oracle/gmap_trace.c)
 
 
 def load(golden_dir, name):

@@ -1,7 +1,11 @@
-"""The N>1 path of bench.py / batch drivers (gsnapdp.shard) on CPU: two ranks
-under the gloo backend, each aligning its own shard with the CPU restatement
-(the GPU step's stand-in here), timed by the same barrier + max-over-ranks
-code the benchmark uses."""
+"""The N>1 path of bench.py / batch drivers (gsnapdp.shard, gsnapdp.gather) on
+CPU: ranks under the gloo backend split ONE batch per read
+(shard.balanced_ranges), align their slices with the CPU restatement (the GPU
+step's stand-in here), build the payload the GPU path builds (result records +
+compact variable-length streams), gather it to rank 0 with the same
+shard.gather_to_root call bench.py makes, and rank 0 reassembles the batch.
+The reassembled batch must be byte-identical to a single-rank run of the whole
+batch; timing uses the same barrier + max-over-ranks code as the benchmark."""
 import json
 import os
 import socket
@@ -60,6 +64,120 @@ def _rank_main(rank, world, port, outdir):
                "total": int(total), "rate": rate, "score_sum": out["score_sum"]},
               open(os.path.join(outdir, "rank%d.json" % r.rank), "w"))
     S.finish(r)
+
+
+def _batch():
+    from gsnapdp import workload as W
+    g = W.c3_genome(seed=3, scale=0.002)
+    return g, W.c3_windows(g, n=1203, seed=33)
+
+
+def _payload_of(res, pairs, poff, npairs):
+    """The payload's variable-length stream on CPU: each window's pair records
+    (6 words each) stand in for its op stream, so `nops` = 6 x npairs and the
+    capacity offsets are the pair offsets x 6."""
+    from gsnapdp import gather as G
+    r = res.copy()
+    r["nops"] = 6 * npairs
+    words = pairs.view(np.uint32)
+    comp = G.compact_ops(r, words, 6 * poff)
+    return r, comp
+
+
+def _gather_main(rank, world, port, outdir):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch
+    import oracle as O
+    from gsnapdp import gather as G
+    from gsnapdp import shard as S
+    from gsnapdp.records import PAIR
+
+    r = S.init_from_env("gloo")
+    g, batch = _batch()
+    cells = np.full(len(batch), 4410) + (np.arange(len(batch)) % 7)  # uneven weights
+    spans = S.balanced_ranges(cells, world)
+    sizes = [b - a for a, b in spans]
+    lo, hi = spans[r.rank]
+    O.setup(g.blocks)
+    res, pairs, poff, npairs = O.run_batch(batch.windows[lo:hi], batch.query, batch.query_uc, nthreads=1)
+    rr, comp = _payload_of(res, pairs, poff, npairs)
+    lay = G.Layout(max(sizes), 6 * 200 * max(sizes))
+    mine = torch.from_numpy(G.pack(lay, rr, comp))
+    recv = [torch.zeros(lay.nbytes, dtype=torch.uint8) for _ in range(world)] if r.rank == 0 else None
+    S.gather_to_root(r, mine, recv)
+    if r.rank == 0:
+        allres, allops, alloff = G.reassemble(lay, [t.numpy() for t in recv], sizes)
+        np.save(os.path.join(outdir, "res.npy"), allres)
+        np.save(os.path.join(outdir, "ops.npy"), allops)
+        np.save(os.path.join(outdir, "off.npy"), alloff)
+        json.dump({"spans": spans}, open(os.path.join(outdir, "spans.json"), "w"))
+    S.finish(r)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_gather_equals_single_rank(tmp_path, world):
+    """One batch split per read over `world` gloo ranks, gathered to rank 0:
+    byte-identical to the single-rank results and streams."""
+    mp.spawn(_gather_main, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    import oracle as O
+    from gsnapdp import gather as G
+    from gsnapdp.records import RESULT
+    g, batch = _batch()
+    O.setup(g.blocks)
+    res, pairs, poff, npairs = O.run_batch(batch.windows, batch.query, batch.query_uc, nthreads=4)
+    rr, comp = _payload_of(res, pairs, poff, npairs)
+    got_res = np.load(os.path.join(str(tmp_path), "res.npy"), allow_pickle=False)
+    got_ops = np.load(os.path.join(str(tmp_path), "ops.npy"), allow_pickle=False)
+    got_off = np.load(os.path.join(str(tmp_path), "off.npy"), allow_pickle=False)
+    spans = json.load(open(os.path.join(str(tmp_path), "spans.json")))["spans"]
+    assert spans[0][0] == 0 and spans[-1][1] == len(batch)
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert all(b - a > 0 for a, b in spans)
+    assert got_res.dtype == RESULT and got_res.tobytes() == rr.tobytes()
+    assert got_ops.tobytes() == comp.tobytes()
+    assert np.array_equal(got_off, G.offsets_from_nops(rr))
+
+
+def test_payload_round_trip_and_overflow():
+    from gsnapdp import gather as G
+    from gsnapdp.records import RESULT
+    rng = np.random.default_rng(1)
+    n = 300
+    res = np.zeros(n, dtype=RESULT)
+    cap = rng.integers(1, 12, size=n)
+    off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(cap, out=off[1:])
+    res["nops"] = rng.integers(0, 12, size=n)
+    res["nops"] = np.minimum(res["nops"], cap)
+    res["finalscore"] = rng.integers(-100, 450, size=n)
+    ops = rng.integers(0, 1 << 32, size=int(off[-1]), dtype=np.uint32)
+    comp = G.compact_ops(res, ops, off)
+    assert comp.size == int(res["nops"].sum())
+    lay = G.Layout(n, comp.size)
+    r2, o2, f2 = G.unpack(lay, G.pack(lay, res, comp), n)
+    assert r2.tobytes() == res.tobytes() and o2.tobytes() == comp.tobytes()
+    for i in range(n):
+        assert np.array_equal(o2[f2[i]:f2[i + 1]], ops[off[i]:off[i] + res["nops"][i]])
+    small = G.Layout(n, comp.size - 1)
+    with pytest.raises(RuntimeError):
+        G.unpack(small, G.pack(small, res, comp), n)
+
+
+def test_balanced_ranges():
+    w = np.array([1, 1, 1, 1, 10, 1, 1, 1], dtype=float)
+    spans = shard.balanced_ranges(w, 2)
+    assert spans[0][0] == 0 and spans[1][1] == 8 and spans[0][1] == spans[1][0]
+    for n in (0, 1, 5, 1000):
+        for world in (1, 2, 3, 8):
+            spans = shard.balanced_ranges(np.ones(n), world)
+            assert [i for a, b in spans for i in range(a, b)] == list(range(n))
+            if n >= world:
+                sz = [b - a for a, b in spans]
+                assert max(sz) - min(sz) <= 1
 
 
 def test_shard_range_covers_batch_exactly():

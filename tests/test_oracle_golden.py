@@ -14,7 +14,7 @@ import oracle as O
 from gsnapdp.records import PAIR
 
 DP_CASES = ["dp_chr17_mix", "dp_synth_mix", "dp_synth_cmet", "dp_chr17_c2", "dp_synth_long",
-            "gmap_synth_gap"]  # the last: windows the reference gmap issued (oracle/gmap_trace.c)
+            "gmap_synth_gap", "gmap_her2_gap"]  # the last two: windows the reference gmap issued (oracle/gmap_trace.c)
 
 
 def load(golden_dir, name):
@@ -46,7 +46,7 @@ def test_dp_oracle_matches_reference(golden_dir, name):
     assert goff[-1] == got.size
 
 
-@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap"])
+@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap", "gmap_her2_ggap"])
 def test_ggap_oracle_matches_reference(golden_dir, name):
     z = load(golden_dir, name)
     O.setup(z["blocks"])

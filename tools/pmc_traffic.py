@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-launch HBM traffic of one kernel from two rocprofv3 --pmc passes.
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR OUT_JSON
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR OUT_JSON [WORKLOAD]
 
 FETCH_SIZE / WRITE_SIZE are in KB per dispatch.  On gfx950 FETCH_SIZE counts
 half the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM), so the read
@@ -29,9 +29,10 @@ def per_dispatch(d, counter, ksub):
 
 def main():
     fdir, wdir, ksub, out = sys.argv[1:5]
+    workload = sys.argv[5] if len(sys.argv) > 5 else "C2"
     fetch_kb, nf = per_dispatch(fdir, "FETCH_SIZE", ksub)
     write_kb, nw = per_dispatch(wdir, "WRITE_SIZE", ksub)
-    res = {"kernel": ksub, "dispatches": [nf, nw], "fetch_size_kb": round(fetch_kb, 1),
+    res = {"kernel": ksub, "workload": workload, "dispatches": [nf, nw], "fetch_size_kb": round(fetch_kb, 1),
            "write_size_kb": round(write_kb, 1),
            "traffic_bytes": round((2.0 * fetch_kb + write_kb) * 1024.0),
            "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halving)"}
