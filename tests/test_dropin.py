@@ -454,24 +454,25 @@ def test_dropin_microexon_matches_reference_golden(golden_dir, tmp_path):
     L.Dynprog_term()
 
 
-REF_SPLICETRIE = os.path.join(ROOT, "oracle", "_ref", "libref_splicetrie.so")
+SPLICETRIE_DOUBLE_SRC = os.path.join(ROOT, "tests", "dropin", "splicetrie_double.c")
 KNOWN_ARGS = ([ctypes.c_void_p] * 10 + [ctypes.c_char_p] * 4 + [ctypes.c_int] * 4)
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(not os.path.exists(REF_SPLICETRIE),
-                    reason="the host-program side (reference splicetrie.c) is built by `make -C oracle ref`")
 def test_dropin_known_splicing_matches_reference_golden(golden_dir, tmp_path):
     """Dynprog_end5_known / Dynprog_end3_known (dynprog.c:6414, 6680) with known
     splice sites and tries, the host program's Splicetrie_solve_end5/3 being the
-    reference's own splicetrie.c calling back into the drop-in: every
-    out-parameter, the list and its protection, against the reference run
-    end to end (the golden vectors)."""
+    clean-room test double (tests/dropin/splicetrie_double.c, pinned to the
+    reference's splicetrie.c by test_oracle_golden) calling back into the
+    drop-in: every out-parameter, the list and its protection, against the
+    reference run end to end (the golden vectors)."""
     z = np.load(os.path.join(golden_dir, "known_chr17.npz"), allow_pickle=False)
     dbl = load_double(tmp_path)
     dbl.dbl_list_protected.argtypes = [ctypes.c_void_p]
     L = ctypes.CDLL(DROPIN, mode=ctypes.RTLD_GLOBAL)       # Dynprog_* for the splicetrie code
-    S = ctypes.CDLL(REF_SPLICETRIE, mode=ctypes.RTLD_GLOBAL)  # Splicetrie_solve_end5/3 for the shim
+    so = os.path.join(str(tmp_path), "libsplicetrie_double.so")
+    subprocess.check_call(["gcc", "-O1", "-shared", "-fPIC", "-o", so, SPLICETRIE_DOUBLE_SRC])
+    S = ctypes.CDLL(so, mode=ctypes.RTLD_GLOBAL)  # Splicetrie_solve_end5/3 for the shim
     L.Dynprog_new.restype = ctypes.c_void_p
     L.Dynprog_new.argtypes = [ctypes.c_int] * 5
     L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]

@@ -143,3 +143,37 @@ def test_micro_oracle_matches_reference(golden_dir):
     for f in PAIR.names:
         assert np.array_equal(got[f], z["pairs"][f]), f
     assert ref["found"].sum() > 500
+
+
+REF_DRIVER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref")
+
+
+@pytest.mark.parametrize("amb_closest", [0, 1])
+def test_splicetrie_double_matches_reference_splicetrie(golden_dir, tmp_path, amb_closest):
+    """The clean-room Splicetrie_solve_end5/3 test double (tests/dropin/
+    splicetrie_double.c, used by the GPU drop-in test instead of reference
+    code) against the reference's splicetrie.c: ref_driver's known-site mode
+    linked with each, on the known_chr17 inputs, every output byte-identical
+    (and the reference build equal to the committed golden vectors)."""
+    import subprocess
+    ref, dbl = os.path.join(REF_DRIVER, "ref_driver"), os.path.join(REF_DRIVER, "ref_driver_dbl")
+    if not (os.path.exists(ref) and os.path.exists(dbl)):
+        pytest.skip("reference drivers are built only in the dev container (make -C oracle ref)")
+    z = load(golden_dir, "known_chr17")
+    outs = {}
+    for tag, exe in (("ref", ref), ("dbl", dbl)):
+        d = tmp_path / tag
+        d.mkdir()
+        z["windows"].tofile(str(d / "known_windows.bin"))
+        z["query"].tofile(str(d / "query.bin"))
+        z["query_uc"].tofile(str(d / "query_uc.bin"))
+        z["blocks"].astype("<u4").tofile(str(d / "genome.u32"))
+        z["sites"].tofile(str(d / "sites.u32"))
+        z["types"].tofile(str(d / "types.i32"))
+        for k in ("tobs", "cobs", "tmax", "cmax"):
+            z[k].tofile(str(d / (k + ".u32")))
+        subprocess.check_call([exe, "known", str(d), "0", str(amb_closest)])
+        outs[tag] = [open(str(d / f), "rb").read() for f in ("known_results.bin", "npairs.i32", "pairs.bin")]
+    assert outs["ref"] == outs["dbl"]
+    if amb_closest == int(z["amb_closest"]):
+        assert outs["ref"][0] == z["results"].tobytes()
