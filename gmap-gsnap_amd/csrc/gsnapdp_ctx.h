@@ -6,6 +6,7 @@
 
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "gsnapdp_internal.h"
 
@@ -77,5 +78,9 @@ struct gsnapdp_ctx {
   // op-stream compaction (gsnapdp_gather.hip): per-block op counts
   int csum_cap = 0;
   int64_t* d_csum = nullptr;
+  // host round trips (gsnapdp_run_host): one at a time per context
+  std::mutex host_mu;
+  void* h_small = nullptr;          // pinned: the compaction header
+  std::vector<uint32_t> h_comp;     // compacted ops on their way to op_offsets
 };
 

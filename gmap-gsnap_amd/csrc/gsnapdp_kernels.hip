@@ -980,6 +980,7 @@ extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   (void)hipFree(ctx->d_sj_win);
   (void)hipFree(ctx->d_stage);
   (void)hipFree(ctx->d_csum);
+  if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1068,6 +1069,8 @@ extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows,
   if (!ctx) return -1;
   if (n <= 0) return 0;
   HIPCHK(hipSetDevice(ctx->device));
+  // one host round trip at a time per context (the staging buffers are shared)
+  std::lock_guard<std::mutex> host_lock(ctx->host_mu);
   const size_t nops = (size_t)op_offsets[n];
   const size_t szw = (size_t)n * sizeof(gsnapdp_window);
   const size_t szq = (query_bytes + 255) & ~(size_t)255;
@@ -1075,7 +1078,7 @@ extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows,
   const size_t szo = (nops + 1) * 4;
   const size_t szoff = (size_t)(n + 1) * 8;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t total = al(szw) + 2 * al(szq) + al(szr) + al(szo) + al(szoff);
+  const size_t total = al(szw) + 2 * al(szq) + al(szr) + 2 * al(szo) + al(szoff) + 256;
   {
     std::lock_guard<std::mutex> lock(ctx->mu);
     if (total > ctx->stage_cap) {
@@ -1084,6 +1087,7 @@ extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows,
       HIPCHK(hipMalloc(&ctx->d_stage, total));
       ctx->stage_cap = total;
     }
+    if (!ctx->h_small) HIPCHK(hipHostMalloc(&ctx->h_small, 256));
   }
   char* base = (char*)ctx->d_stage;
   gsnapdp_window* dw = (gsnapdp_window*)base;
@@ -1091,17 +1095,54 @@ extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows,
   char* du = dq + al(szq);
   gsnapdp_result* dr = (gsnapdp_result*)(du + al(szq));
   uint32_t* dops = (uint32_t*)((char*)dr + al(szr));
-  int64_t* doff = (int64_t*)((char*)dops + al(szo));
+  uint32_t* dcomp = (uint32_t*)((char*)dops + al(szo));
+  int64_t* doff = (int64_t*)((char*)dcomp + al(szo));
+  int64_t* dhdr = (int64_t*)((char*)doff + al(szoff));
   hipStream_t st = ctx->stream;
   HIPCHK(hipMemcpyAsync(dw, windows, szw, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(dq, query, query_bytes, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(doff, op_offsets, szoff, hipMemcpyHostToDevice, st));
   if (gsnapdp_run_device(ctx, dw, n, dq, du, dr, dops, doff, st)) return -1;
+  // only the ops each window wrote come back: compacted on the device, then
+  // scattered to op_offsets on the host (the capacity layout is ~100x larger)
+  if (gsnapdp_compact_ops_device(ctx, dr, n, dops, doff, dcomp, (int64_t)nops, dhdr, st)) return -1;
   HIPCHK(hipMemcpyAsync(results, dr, szr, hipMemcpyDeviceToHost, st));
-  if (nops) HIPCHK(hipMemcpyAsync(ops, dops, nops * 4, hipMemcpyDeviceToHost, st));
+  int64_t* hdr = (int64_t*)ctx->h_small;
+  HIPCHK(hipMemcpyAsync(hdr, dhdr, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  const int64_t got = hdr[0];
+  if (got < 0 || (size_t)got > nops) {
+    gsnapdp__set_err("gsnapdp_run_host: compacted op count out of range");
+    return -1;
+  }
+  if (got == 0) return 0;
+  std::vector<uint32_t>& comp = ctx->h_comp;
+  comp.resize((size_t)got);
+  HIPCHK(hipMemcpyAsync(comp.data(), dcomp, (size_t)got * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  size_t k = 0;
+  for (int i = 0; i < n; i++) {
+    int64_t c = results[i].nops < 0 ? 0 : results[i].nops;
+    const int64_t cap = op_offsets[i + 1] - op_offsets[i];
+    if (c > cap) c = cap;
+    if (c) memcpy(ops + op_offsets[i], comp.data() + k, (size_t)c * 4);
+    k += (size_t)c;
+  }
   return 0;
+}
+
+extern "C" void* gsnapdp_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+    gsnapdp__set_err("hipHostMalloc failed");
+    return nullptr;
+  }
+  return p;
+}
+
+extern "C" void gsnapdp_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
 }
 
 // stage timing: events on the launch stream around each kernel

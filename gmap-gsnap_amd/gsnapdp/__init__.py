@@ -93,6 +93,9 @@ def lib():
         L.gsnapdp_micro_run_device.restype = i32
         L.gsnapdp_micro_expand.argtypes = [vp, vp, vp, vp, vp, vp, i32]
         L.gsnapdp_micro_expand.restype = i32
+        L.gsnapdp_host_alloc.argtypes = [sz]
+        L.gsnapdp_host_alloc.restype = vp
+        L.gsnapdp_host_free.argtypes = [vp]
         L.gsnapdp_compact_ops_device.argtypes = [vp, vp, i32, vp, vp, vp, ctypes.c_int64, vp, vp]
         L.gsnapdp_compact_ops_device.restype = i32
         _lib = L
@@ -101,6 +104,36 @@ def lib():
 
 def _p(a):
     return ctypes.c_void_p(a.ctypes.data)
+
+
+class _Pinned:
+    """Page-locked host memory (gsnapdp_host_alloc) exposed to numpy."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = max(1, int(nbytes))
+        self.p = lib().gsnapdp_host_alloc(self.nbytes)
+        if not self.p:
+            raise GsnapdpError("gsnapdp_host_alloc(%d) failed" % self.nbytes)
+        self.__array_interface__ = {"shape": (self.nbytes,), "typestr": "|u1", "data": (self.p, False),
+                                    "version": 3}
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            lib().gsnapdp_host_free(self.p)
+            self.p = None
+
+
+def pinned_empty(n: int, dtype) -> np.ndarray:
+    """An uninitialised numpy array of n elements in page-locked host memory
+    (the buffer lives as long as the array)."""
+    dt = np.dtype(dtype)
+    return np.asarray(_Pinned(n * dt.itemsize))[:n * dt.itemsize].view(dt)
+
+
+def pinned_copy(a: np.ndarray) -> np.ndarray:
+    out = pinned_empty(a.size, a.dtype)
+    out[...] = a.reshape(-1)
+    return out
 
 
 def op_offsets(windows: np.ndarray) -> np.ndarray:
@@ -164,14 +197,18 @@ class Context:
     def arch(self) -> str:
         return lib().gsnapdp_device_arch(self.h).decode()
 
-    def run(self, windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray):
-        """Fill + endpoint + traceback on the GPU.  Returns (results, ops, op_offsets)."""
+    def run(self, windows: np.ndarray, query: np.ndarray, query_uc: np.ndarray, out=None):
+        """Fill + endpoint + traceback on the GPU (gsnapdp_run_host).  Returns
+        (results, ops, op_offsets); `out` = preallocated (results, ops, op_offsets)."""
         w = np.ascontiguousarray(windows, dtype=WINDOW)
         q = np.ascontiguousarray(query, dtype=np.uint8)
         u = np.ascontiguousarray(query_uc, dtype=np.uint8)
-        off = op_offsets(w)
-        res = np.zeros(len(w), dtype=RESULT)
-        ops = np.zeros(max(1, int(off[-1])), dtype=np.uint32)
+        if out is not None:
+            res, ops, off = out
+        else:
+            off = op_offsets(w)
+            res = np.zeros(len(w), dtype=RESULT)
+            ops = np.zeros(max(1, int(off[-1])), dtype=np.uint32)
         rc = lib().gsnapdp_run_host(self.h, _p(w), len(w), _p(q), _p(u), q.size, _p(res), _p(ops), _p(off))
         if rc != 0:
             raise GsnapdpError("gsnapdp_run_host: %s" % lib().gsnapdp_last_error().decode())

@@ -226,7 +226,10 @@ const char *gsnapdp_device_arch(gsnapdp_ctx *ctx);
 /* ------------------------------------------------------------ host batches
  * Fill + endpoint + traceback for `n` windows.  Inputs are host buffers;
  * this call copies them to HBM, runs the kernels on the context stream and
- * copies results back (synchronous).  `op_offsets[i]` is where window i's
+ * copies results back (synchronous; concurrent calls on one context run one
+ * after the other).  Only the ops each window wrote cross PCIe (compacted on
+ * the device, scattered to op_offsets on the host).  Buffers from
+ * gsnapdp_host_alloc avoid the driver's pageable staging.  `op_offsets[i]` is where window i's
  * op stream starts in `ops`; window i may write at most
  * op_offsets[i+1]-op_offsets[i] ops (op_offsets has n+1 entries).
  * Returns 0 on success. */
@@ -259,6 +262,12 @@ size_t gsnapdp_scratch_bytes(gsnapdp_ctx *ctx, int n, int max_length1, int max_l
 int gsnapdp_compact_ops_device(gsnapdp_ctx *ctx, const gsnapdp_result *d_results, int n,
                                const uint32_t *d_ops, const int64_t *d_op_offsets, uint32_t *d_out,
                                int64_t out_cap, int64_t *d_header, void *stream);
+
+/* Page-locked host memory (hipHostMalloc) for batch buffers handed to the
+ * *_run_host entry points: copies from / to it run as DMA without staging.
+ * Returns NULL on failure.  Free with gsnapdp_host_free. */
+void *gsnapdp_host_alloc(size_t bytes);
+void gsnapdp_host_free(void *p);
 
 /* Synchronise the context stream. */
 int gsnapdp_sync(gsnapdp_ctx *ctx);

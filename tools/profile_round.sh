@@ -11,9 +11,9 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$TAG; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > $O/pytest_gpu.txt 2>&1
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
-B="--steps 20 --warmup 2 --no-cpu --no-side"
+B="--steps 20 --warmup 2 --no-cpu --no-side --no-steady"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py $B > $O/trace_bench.json 2> $O/trace.err
-B="--steps 3 --warmup 1 --no-cpu --no-side"
+B="--steps 3 --warmup 1 --no-cpu --no-side --no-steady"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 bench.py $B > /dev/null 2> $O/pmc1.err
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 bench.py $B > /dev/null 2> $O/pmc2.err
 python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write k_fill $O/traffic.json C3
