@@ -8,6 +8,7 @@
 // There is no CPU fallback: without a gfx950 device the first call aborts,
 // as the reference aborts on its own fatal conditions.
 #include <dlfcn.h>
+#include <malloc.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -33,6 +34,7 @@ struct State {
   const unsigned int* blocks = nullptr;
   size_t nwords = 0;
   int device = 0;
+  bool explicit_genome = false;  // Gsnapdp_dropin_genome was called
   gsnapdp_ctx* ctx = nullptr;
   bool tables = false;
   bool splicing_iit = false;  // Dynprog_setup got known splice sites
@@ -58,10 +60,20 @@ enum { CALL_GAP, CALL_SJ, CALL_GGAP, CALL_CGAP, CALL_MICRO, CALL_MAXENT };
   abort();
 }
 
-// Context on first use (after Dynprog_init and Gsnapdp_dropin_genome).
+// Context on first use.  The genome comes from the host program's own setup
+// calls, so gmap / gsnap link the library unchanged:
+//  * index genome: Dynprog_setup's Genome_T (gmap.c:3828, gsnap.c:2366) gives
+//    Genome_blocks / Genome_totallength (genome.c:96-107), resolved in the host;
+//  * user segment (gmap -g): Dynprog_setup gets NULL and the blocks arrive in
+//    Maxent_hr_setup (gmap.c:3803) from Genome_create_blocks, a CALLOC of
+//    ((len+31)/32)*3 + 4 words (genome-write.c:809-810); the allocation's
+//    usable size covers every block the DP can address.
+// Gsnapdp_dropin_genome(blocks, nwords, device) still overrides both.
 gsnapdp_ctx* ctx() {
   if (g.ctx) return g.ctx;
-  if (!g.blocks) fatal("no genome: call Gsnapdp_dropin_genome(blocks, nwords, device) after Genome_new");
+  if (!g.blocks) fatal("no genome: neither Dynprog_setup nor Maxent_hr_setup gave the genome blocks");
+  if (!g.nwords) g.nwords = malloc_usable_size((void*)g.blocks) / sizeof(unsigned int);
+  if (!g.nwords) fatal("cannot size the genome blocks; call Gsnapdp_dropin_genome(blocks, nwords, device)");
   g.ctx = gsnapdp_create(g.device, g.blocks, g.nwords, g.mode);
   if (!g.ctx) fatal(std::string("gsnapdp_create: ") + gsnapdp_last_error());
   return g.ctx;
@@ -430,6 +442,10 @@ extern "C" __attribute__((weak)) gsnapdp_List_T Splicetrie_solve_end3(
     gsnapdp_Pairpool_T, int, double);
 using SolveFn = decltype(&Splicetrie_solve_end5);
 
+// The host program's genome accessors (genome.c:96-107), for Dynprog_setup.
+extern "C" __attribute__((weak)) unsigned int* Genome_blocks(gsnapdp_Genome_T);
+extern "C" __attribute__((weak)) gsnapdp_Genomicpos_T Genome_totallength(gsnapdp_Genome_T);
+
 SolveFn solver(bool end5) {
   SolveFn f = end5 ? &Splicetrie_solve_end5 : &Splicetrie_solve_end3;
   if (f) return f;
@@ -457,6 +473,7 @@ int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device)
   g.blocks = blocks;
   g.nwords = nwords;
   g.device = device;
+  g.explicit_genome = true;
   return 0;
 }
 
@@ -480,8 +497,15 @@ void Dynprog_setup(gsnapdp_bool, gsnapdp_IIT_T splicing_iit, int*, int, int,
                    gsnapdp_Genomicpos_T* splicesites, gsnapdp_Splicetype_T* splicetypes,
                    gsnapdp_Genomicpos_T*, int nsplicesites, unsigned int* trieoffsets_obs,
                    unsigned int* triecontents_obs, unsigned int* trieoffsets_max,
-                   unsigned int* triecontents_max, gsnapdp_Genome_T) {
+                   unsigned int* triecontents_max, gsnapdp_Genome_T genome) {
   std::lock_guard<std::mutex> lock(g.mu);
+  if (genome && !g.explicit_genome && Genome_blocks && Genome_totallength) {
+    unsigned int* blocks = Genome_blocks(genome);
+    if (!blocks) fatal("Dynprog_setup: the genome is not in packed blocks (genomecomp)");
+    if (g.ctx && blocks != g.blocks) fatal("genome changed after first use");
+    g.blocks = blocks;
+    g.nwords = (size_t)((Genome_totallength(genome) + 31U) / 32U) * 3;
+  }
   g.splicing_iit = splicing_iit != nullptr;  // dynprog.c:360
   g.splicesites = splicesites;
   g.splicetypes = splicetypes;
@@ -1162,7 +1186,7 @@ gsnapdp_List_T Dynprog_end3_known(
 void Maxent_hr_setup(unsigned int* ref_blocks) {  // maxent_hr.c:27195
   std::lock_guard<std::mutex> lock(g.mu);
   if (g.blocks && ref_blocks != g.blocks) fatal("Maxent_hr_setup blocks differ from the genome");
-  if (!g.blocks) g.blocks = ref_blocks;  // length still needed: Gsnapdp_dropin_genome
+  if (!g.blocks) g.blocks = ref_blocks;  // sized in ctx() unless Dynprog_setup sizes it
 }
 
 double Maxent_hr_donor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomicpos_T chroffset) {

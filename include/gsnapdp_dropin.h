@@ -222,11 +222,13 @@ double Maxent_hr_antidonor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomic
 double Maxent_hr_antiacceptor_prob(gsnapdp_Genomicpos_T splice_pos,
                                    gsnapdp_Genomicpos_T chroffset);
 
-/* --- one addition: the reference hands the packed genome to Genome_T /
- * Maxent_hr_setup without its length; the host calls this once after
- * Genome_new (gmap.c:3801 / gsnap.c:1064), before the first DP call. ---
- * `blocks` = Genome_blocks(genome), `nwords` = its length in UINT4 words
- * (3 per 32 nt plus the reference's padding).  `device` = HIP device index. */
+/* --- optional additions (not in the reference) ---
+ * The shim finds the packed genome on its own: Dynprog_setup's Genome_T
+ * (Genome_blocks / Genome_totallength, genome.c:96-107) for an index genome,
+ * or the Genome_create_blocks allocation given to Maxent_hr_setup for a user
+ * segment.  This call overrides both, before the first DP
+ * call: `blocks` and `nwords` = its length in UINT4 words (3 per 32 nt plus
+ * any padding), `device` = HIP device index. */
 int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device);
 
 /* Counters of this process's GPU work: out[0..5] = windows run for the gap,
