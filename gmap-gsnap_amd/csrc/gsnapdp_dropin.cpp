@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <condition_variable>
+#include <utility>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -38,6 +39,11 @@ struct State {
   gsnapdp_ctx* ctx = nullptr;
   bool tables = false;
   bool splicing_iit = false;  // Dynprog_setup got known splice sites
+  // the splicing IIT itself and how Dynprog_setup described it (dynprog.c:350-376)
+  gsnapdp_IIT_T iit = nullptr;
+  int* divint_crosstable = nullptr;
+  int donor_typeint = -1, acceptor_typeint = -1;
+  bool novelsplicingp = true;
   // known splice sites and their tries (Dynprog_setup, dynprog.c:350-376)
   const unsigned* splicesites = nullptr;
   const int* splicetypes = nullptr;
@@ -446,6 +452,98 @@ using SolveFn = decltype(&Splicetrie_solve_end5);
 extern "C" __attribute__((weak)) unsigned int* Genome_blocks(gsnapdp_Genome_T);
 extern "C" __attribute__((weak)) gsnapdp_Genomicpos_T Genome_totallength(gsnapdp_Genome_T);
 
+// The host program's splicing-IIT queries (iit-read.c:3770, 3808, 3973, 4011),
+// used exactly where bridge_intron_gap makes them (dynprog.c:3375-3550, 3598-3612).
+extern "C" __attribute__((weak)) gsnapdp_bool IIT_exists_with_divno_typed_signed(
+    gsnapdp_IIT_T, int divno, unsigned int x, unsigned int y, int type, int sign);
+extern "C" __attribute__((weak)) gsnapdp_bool IIT_low_exists_signed_p(gsnapdp_IIT_T, int divno,
+                                                                      unsigned int x, int sign);
+extern "C" __attribute__((weak)) gsnapdp_bool IIT_high_exists_signed_p(gsnapdp_IIT_T, int divno,
+                                                                       unsigned int x, int sign);
+extern "C" __attribute__((weak)) gsnapdp_bool IIT_exists_with_divno_signed(
+    gsnapdp_IIT_T, int divno, unsigned int x, unsigned int y, int sign);
+
+// Appends one window's known-site record (left_known[L2L], right_known[L2R],
+// the KNOWN_INTRONS pair list) to `q` and returns its known_mode.
+int known_site_record(std::vector<char>& q, size_t at, int chrnum, unsigned chrpos,
+                      unsigned genomiclength, int leftoffset, int rightoffset, int L2L, int L2R,
+                      int cdna_direction, bool watsonp) {
+  // weak references bound at link time, else looked up in the process (a host
+  // that dlopens the shim before its iit-read code)
+  auto resolve = [](auto f, const char* name) {
+    if (!f) f = (decltype(f))dlsym(RTLD_DEFAULT, name);
+    if (!f) fatal(std::string("a splicing IIT was given but the host program's ") + name + " is not linked");
+    return f;
+  };
+  const auto typed = resolve(&IIT_exists_with_divno_typed_signed, "IIT_exists_with_divno_typed_signed");
+  const auto lowp = resolve(&IIT_low_exists_signed_p, "IIT_low_exists_signed_p");
+  const auto highp = resolve(&IIT_high_exists_signed_p, "IIT_high_exists_signed_p");
+  const auto exact = resolve(&IIT_exists_with_divno_signed, "IIT_exists_with_divno_signed");
+  const int divno = g.divint_crosstable[chrnum];
+  const bool sites = g.donor_typeint >= 0 && g.acceptor_typeint >= 0;
+  const bool fwd = cdna_direction > 0;
+  const unsigned gl1 = genomiclength - 1U;
+  q.resize(at + (size_t)L2L + (size_t)L2R + 2, 0);
+  char* left = q.data() + at;
+  char* right = left + L2L;
+  for (int cL = 0; cL < L2L - 1; cL++) {  // :3379-3530, left half of each case
+    const unsigned pos = watsonp ? chrpos + leftoffset + cL : chrpos + gl1 - leftoffset - cL + 1U;
+    bool k;
+    if (sites)
+      k = typed(g.iit, divno, pos, pos + 1U, fwd ? g.donor_typeint : g.acceptor_typeint,
+                watsonp ? (fwd ? +1 : -1) : (fwd ? -1 : +1));
+    else if (watsonp)
+      k = lowp(g.iit, divno, pos, fwd ? +1 : -1);
+    else
+      k = highp(g.iit, divno, pos + 1U, fwd ? -1 : +1);
+    left[cL] = k ? 1 : 0;
+  }
+  for (int cR = 0; cR < L2R - 1; cR++) {  // right half of each case
+    const unsigned pos = watsonp ? chrpos + rightoffset - cR + 1U : chrpos + gl1 - rightoffset + cR;
+    bool k;
+    if (sites)
+      k = typed(g.iit, divno, pos, pos + 1U, fwd ? g.acceptor_typeint : g.donor_typeint,
+                watsonp ? (fwd ? +1 : -1) : (fwd ? -1 : +1));
+    else if (watsonp)
+      k = highp(g.iit, divno, pos + 1U, fwd ? +1 : -1);
+    else
+      k = lowp(g.iit, divno, pos, fwd ? -1 : +1);
+    right[cR] = k ? 1 : 0;
+  }
+  int mode;
+  if (g.novelsplicingp) mode = GSNAPDP_KNOWN_REWARD;
+  else if (sites) mode = GSNAPDP_KNOWN_SITES;
+  else mode = GSNAPDP_KNOWN_INTRONS;
+  if (mode == GSNAPDP_KNOWN_INTRONS) {  // the introns the constrained bridge may take (:3598-3612)
+    std::vector<std::pair<int, int>> pairs;
+    for (int cL = 0; cL < L2L - 1; cL++) {
+      if (!q[at + cL]) continue;
+      for (int cR = 0; cR < L2R - 1; cR++) {
+        if (!q[at + L2L + cR]) continue;
+        bool ok;
+        if (watsonp)
+          ok = exact(g.iit, divno, chrpos + leftoffset + cL,
+                                            chrpos + rightoffset - cR + 1U + 1U, cdna_direction);
+        else
+          ok = exact(g.iit, divno, chrpos + gl1 - rightoffset + cR,
+                                            chrpos + gl1 - leftoffset - cL + 1U + 1U, -cdna_direction);
+        if (ok) pairs.emplace_back(cL, cR);
+      }
+    }
+    if (pairs.size() > 0xffff) fatal("more than 65535 known introns in one genome-gap window");
+    const size_t p0 = at + (size_t)L2L + (size_t)L2R;
+    q[p0] = (char)(pairs.size() & 255);
+    q[p0 + 1] = (char)(pairs.size() >> 8);
+    for (const auto& pr : pairs) {
+      const unsigned char e[4] = {(unsigned char)(pr.first & 255), (unsigned char)(pr.first >> 8),
+                                  (unsigned char)(pr.second & 255), (unsigned char)(pr.second >> 8)};
+      q.insert(q.end(), (const char*)e, (const char*)e + 4);
+    }
+  }
+  q.resize(q.size() + 8, 0);
+  return mode;
+}
+
 SolveFn solver(bool end5) {
   SolveFn f = end5 ? &Splicetrie_solve_end5 : &Splicetrie_solve_end3;
   if (f) return f;
@@ -489,11 +587,11 @@ char* Dynprog_endalign_string(gsnapdp_Endalign_T endalign) {  // dynprog.c:335-3
   }
 }
 
-// The splice sites and their tries feed Dynprog_end5/3_known.  The splicing IIT
-// only feeds the known-site modes of bridge_intron_gap, which this library does
-// not serve: Dynprog_genome_gap aborts when one was given.
-// The genome arrives through Gsnapdp_dropin_genome.
-void Dynprog_setup(gsnapdp_bool, gsnapdp_IIT_T splicing_iit, int*, int, int,
+// The splice sites and their tries feed Dynprog_end5/3_known; the splicing IIT
+// feeds the known-site modes of bridge_intron_gap (Dynprog_genome_gap builds
+// each window's known-site record from it with the host program's IIT calls).
+void Dynprog_setup(gsnapdp_bool novelsplicingp, gsnapdp_IIT_T splicing_iit,
+                   int* splicing_divint_crosstable, int donor_typeint, int acceptor_typeint,
                    gsnapdp_Genomicpos_T* splicesites, gsnapdp_Splicetype_T* splicetypes,
                    gsnapdp_Genomicpos_T*, int nsplicesites, unsigned int* trieoffsets_obs,
                    unsigned int* triecontents_obs, unsigned int* trieoffsets_max,
@@ -506,7 +604,12 @@ void Dynprog_setup(gsnapdp_bool, gsnapdp_IIT_T splicing_iit, int*, int, int,
     g.blocks = blocks;
     g.nwords = (size_t)((Genome_totallength(genome) + 31U) / 32U) * 3;
   }
-  g.splicing_iit = splicing_iit != nullptr;  // dynprog.c:360
+  g.splicing_iit = splicing_iit != nullptr;  // dynprog.c:358-366
+  g.iit = splicing_iit;
+  g.divint_crosstable = splicing_divint_crosstable;
+  g.donor_typeint = donor_typeint;
+  g.acceptor_typeint = acceptor_typeint;
+  g.novelsplicingp = novelsplicingp != 0;
   g.splicesites = splicesites;
   g.splicetypes = splicetypes;
   g.nsplicesites = nsplicesites;
@@ -619,7 +722,7 @@ gsnapdp_List_T Dynprog_genome_gap(
     int* nindels, int* exonhead, int* introntype, gsnapdp_Dynprog_T dynprogL,
     gsnapdp_Dynprog_T dynprogR, char* sequence1, char* sequenceuc1, char*, char*, char*, char*,
     int length1, int length2L, int length2R, int offset1, int offset2L, int revoffset2R,
-    int /*chrnum: known sites only*/, gsnapdp_Genomicpos_T chroffset,
+    int chrnum, gsnapdp_Genomicpos_T chroffset,
     gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
     gsnapdp_Genomicpos_T genomiclength, char* /*genomicuc_ptr*/, gsnapdp_bool use_genomicseg_p,
     int cdna_direction, gsnapdp_bool watsonp, gsnapdp_bool jump_late_p,
@@ -627,7 +730,6 @@ gsnapdp_List_T Dynprog_genome_gap(
     gsnapdp_bool halfp, gsnapdp_bool finalp, gsnapdp_bool use_probabilities_p,
     int score_threshold, gsnapdp_bool splicingp) {  // dynprog.c:4798-5061
   std::lock_guard<std::mutex> lock(g.mu);
-  if (g.splicing_iit) fatal("Dynprog_genome_gap with a splice-site IIT is not served");
   if (use_genomicseg_p && (use_probabilities_p || finalp))
     fatal("Dynprog_genome_gap: genomic-segment MaxEnt probabilities are not served");
   gsnapdp_ctx* c = ctx();
@@ -671,6 +773,13 @@ gsnapdp_List_T Dynprog_genome_gap(
     memcpy(g.q.data(), sequence1, (size_t)L1);
     memcpy(g.qu.data(), sequenceuc1, (size_t)L1);
   }
+  if (g.splicing_iit && L1 > 1 && length2L > 0 && length2R > 0 && !too_long) {
+    // the known-site record follows the query rows (include/gsnapdp.h)
+    w.known_mode = known_site_record(g.q, (size_t)L1, chrnum, chrpos, genomiclength,
+                                     offset2L, revoffset2R, length2L, length2R, cdna_direction,
+                                     watsonp != 0);
+    g.qu.resize(g.q.size(), 0);
+  }
   const int64_t cap = 2 * (int64_t)L1 + (length2L > 0 ? length2L : 0) + (length2R > 0 ? length2R : 0) + 4;
   const int64_t off[2] = {0, cap};
   g.ops.assign((size_t)cap + 1, 0u);
@@ -699,9 +808,11 @@ gsnapdp_List_T Dynprog_genome_gap(
   // indices in the reference (:4055); here it is defined as NULL, NEG_INFINITY
   if (r.bridge_ok == 0) return nullptr;
   // bridge_intron_gap writes *introntype only when a score-mode candidate is
-  // taken; none taken leaves bestscore (and bestscoreI) at -100000
-  if (!use_probabilities_p && r.finalscore != (halfp ? -50000 : -100000)) *introntype = r.introntype;
-  if (r.finalscore < 0) return nullptr;  // bridge rejected (:4084)
+  // taken (none taken leaves bestscore and bestscoreI at -100000), and always
+  // in the constrained known-intron mode (NONINTRON, :3695)
+  if (w.known_mode == GSNAPDP_KNOWN_INTRONS) *introntype = 0;
+  else if (!use_probabilities_p && r.finalscore != (halfp ? -50000 : -100000)) *introntype = r.introntype;
+  if (t.brL == 0) return nullptr;  // bridge rejected (:4084-4101)
   *new_leftgenomepos = r.new_leftgenomepos;
   *new_rightgenomepos = r.new_rightgenomepos;
   *exonhead = r.exonhead;

@@ -150,6 +150,23 @@ __device__ inline int intron_score(int& introntype, int leftdi, int rightdi, int
   return 0;
 }
 
+// Known splice sites: bit 7 of a leftdi / rightdi byte (the dinucleotide codes
+// use 6 bits, intron.h:10-18) carries left_known / right_known.
+constexpr int KNOWN_BIT = 0x80, DI_MASK = 0x3F;
+constexpr int KNOWN_REWARD = 20;  // KNOWN_SPLICESITE_REWARD (dynprog.c:285)
+__device__ inline int kreward(int d) { return (d >> 7) * KNOWN_REWARD; }
+__device__ inline bool kflag(const unsigned char* f, int km, int c) { return km != 0 && f[c] != 0; }
+// IIT_exists_with_divno_signed on the intron (cL, cR) (:3598-3612), from the
+// caller's pair list
+__device__ inline bool known_intron(const unsigned char* p, int cL, int cR) {
+  const int n = p[0] | (p[1] << 8);
+  for (int i = 0; i < n; i++) {
+    const unsigned char* e = p + 2 + 4 * i;
+    if ((e[0] | (e[1] << 8)) == cL && (e[2] | (e[3] << 8)) == cR) return true;
+  }
+  return false;
+}
+
 // leftdi / rightdi (dynprog.c:3331-3373) from two genome class codes
 __device__ inline int left_di(int a, int b) {
   if (a == 2 && b == 3) return LEFT_GT;
@@ -430,6 +447,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
     const PD rp = (PD)(region + G.oProbR);
     const P bnd = region + G.oBnd;
     const bool probmode = w.use_probabilities_p != 0;
+    // known splice sites (a splicing IIT, dynprog.c:3375-3550): the caller's
+    // record follows the query rows (include/gsnapdp.h, gsnapdp_ggap_window)
+    const int km = act ? w.known_mode : GSNAPDP_KNOWN_NONE;
+    const unsigned char* krec = (const unsigned char*)q + w.qpos + (act ? G.L1 : 0);
     // column genome classes (get_genomic_nt, dynprog.c:403-441), both flanks
     const Lane LL = side_lane(w, G, 0), LR = side_lane(w, G, 1);
     if (act) {
@@ -437,11 +458,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
         clsL[c] = (uint8_t)((c >= 1 && c <= G.L2L) ? gclass(blocks, nwords, LL, w.offset2L + c - 1) : 5);
       for (int c = rho; c <= G.L2R + 1; c += RL)
         clsR[c] = (uint8_t)((c >= 1 && c <= G.L2R) ? gclass(blocks, nwords, LR, w.revoffset2R + 1 - c) : 5);
-      if (probmode) {  // :3856-3903
+      if (probmode) {  // :3856-3903 (a known site has probability 1.0)
         for (int c = rho; c < G.L2L; c += RL)
-          lp[c] = c < G.L2L - 1 ? left_site_prob(w, c, blocks, nwords, tables) : 0.0;
+          lp[c] = c < G.L2L - 1 ? (kflag(krec, km, c) ? 1.0 : left_site_prob(w, c, blocks, nwords, tables)) : 0.0;
         for (int c = rho; c < G.L2R; c += RL)
-          rp[c] = c < G.L2R - 1 ? right_site_prob(w, c, blocks, nwords, tables) : 0.0;
+          rp[c] = c < G.L2R - 1 ? (kflag(krec + G.L2L, km, c) ? 1.0 : right_site_prob(w, c, blocks, nwords, tables))
+                                : 0.0;
       }
     }
     using PH = typename std::conditional<GMEM, AS_GLOBAL uint16_t*, AS_LDS uint16_t*>::type;
@@ -460,11 +482,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
     }
     if constexpr (GMEM) __threadfence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the class bytes are in LDS
-    if (act) {  // leftdi / rightdi (:3331-3373); 0 past the scanned columns (calloc)
+    if (act) {  // leftdi / rightdi (:3331-3373); 0 past the scanned columns (calloc);
+                // bit 7: left_known / right_known (:3375-3550)
       for (int c = rho; c <= G.L2L; c += RL)
-        diL[c] = (uint8_t)(c < G.L2L - 1 ? left_di(clsL[c + 1], clsL[c + 2]) : 0);
+        diL[c] = (uint8_t)((c < G.L2L - 1 ? left_di(clsL[c + 1], clsL[c + 2]) : 0) |
+                           (c < G.L2L && kflag(krec, km, c) ? KNOWN_BIT : 0));
       for (int c = rho; c <= G.L2R; c += RL)
-        diR[c] = (uint8_t)(c < G.L2R - 1 ? right_di(clsR[c + 2], clsR[c + 1]) : 0);
+        diR[c] = (uint8_t)((c < G.L2R - 1 ? right_di(clsR[c + 2], clsR[c + 1]) : 0) |
+                           (c < G.L2R && kflag(krec + G.L2L, km, c) ? KNOWN_BIT : 0));
     }
     // wave-uniform step and stripe counts
     const int L2max = max(G.L2L, G.L2R);
@@ -518,18 +543,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
       const int rR = G.L1 - rL;
       const int cloL = max(1, rL - lbandB), chighL = min(min(G.L2L - 1, rL + rbandBL), span - rR - 1);
       const int cloR = max(1, rR - lbandB), chighR = min(min(G.L2R - 1, rR + rbandBR), span - rL - 1);
-      const int DR = HRv(rR, rR) >> 4;  // (rR, rR): on the right band's main diagonal
-      const int DL = HLv(rL, rL) >> 4;
       const int rdR = diR[rR], ldL = diL[rL];
+      // (rR, rR): on the right band's main diagonal; + right_known[rR] (:3727)
+      const int DR = (HRv(rR, rR) >> 4) + kreward(rdR);
+      const int DL = (HLv(rL, rL) >> 4) + kreward(ldL);
       const int baseL = (rL - 1) * G.WL - rL + G.lbL, baseR = (rR - 1) * G.WR - rR + G.lbR;
-      if (probmode) {
+      if (km == GSNAPDP_KNOWN_INTRONS) {  // constrain to given introns (:3552-3697)
+        if (rdR & KNOWN_BIT) {
+          for (int cL = cloL; cL <= chighL; cL++) {  // indel on left, cR = rR
+            if (!(diL[cL] & KNOWN_BIT)) continue;
+            const int v = (int)HL[baseL + cL];
+            const int tot = (v >> 4) - pen(v) + (DR - KNOWN_REWARD);
+            if (tot > best.score && known_intron(krec + G.L2L + G.L2R, cL, rR)) {
+              best.score = tot;
+              best.key = 2 * rL;
+              best.sI = 0;
+              best.cL = cL;
+              best.cR = rR;
+            }
+          }
+        }
+        if (ldL & KNOWN_BIT) {
+          for (int cR = cloR; cR <= chighR; cR++) {  // indel on right, cL = rL
+            if (!(diR[cR] & KNOWN_BIT)) continue;
+            const int v = (int)HR[baseR + cR];
+            const int tot = (DL - KNOWN_REWARD) + (v >> 4) - pen(v);
+            if (tot > best.score && known_intron(krec + G.L2L + G.L2R, rL, cR)) {
+              best.score = tot;
+              best.key = 2 * rL + 1;
+              best.sI = 0;
+              best.cL = rL;
+              best.cR = cR;
+            }
+          }
+        }
+      } else if (probmode) {
         const double pR = rR < G.L2R - 1 ? rp[rR] : 0.0;
         const double pL = rL < G.L2L - 1 ? lp[rL] : 0.0;
         for (int cL = cloL; cL <= chighL; cL++) {  // indel on left, cR = rR
           const double p = lp[cL] + pR;
           if (!(p > best.prob)) continue;
-          const int v = (int)HL[baseL + cL];
-          const int tot = (v >> 4) - pen(v) + (itab[diL[cL] & rdR] & 255) + DR;
+          const int v = (int)HL[baseL + cL], d = diL[cL];
+          const int tot = (v >> 4) - pen(v) + kreward(d) + (itab[d & rdR & DI_MASK] & 255) + DR;
           if (tot >= w.score_threshold) {
             best.prob = p;
             best.key = 2 * rL;
@@ -540,8 +595,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
         for (int cR = cloR; cR <= chighR; cR++) {  // indel on right, cL = rL
           const double p = pL + rp[cR];
           if (!(p > best.prob)) continue;
-          const int v = (int)HR[baseR + cR];
-          const int tot = DL + (itab[ldL & diR[cR]] & 255) + (v >> 4) - pen(v);
+          const int v = (int)HR[baseR + cR], d = diR[cR];
+          const int tot = DL + (itab[ldL & d & DI_MASK] & 255) + (v >> 4) - pen(v) + kreward(d);
           if (tot >= w.score_threshold) {
             best.prob = p;
             best.key = 2 * rL + 1;
@@ -551,9 +606,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
         }
       } else {
         for (int cL = cloL; cL <= chighL; cL++) {  // indel on left, cR = rR
-          const int v = (int)HL[baseL + cL];
-          const int e = itab[diL[cL] & rdR];
-          const int tot = (v >> 4) - pen(v) + (e & 255) + DR;
+          const int v = (int)HL[baseL + cL], d = diL[cL];
+          const int e = itab[d & rdR & DI_MASK];
+          const int tot = (v >> 4) - pen(v) + kreward(d) + (e & 255) + DR;
           if (tot > best.score) {
             best.score = tot;
             best.key = 2 * rL;
@@ -563,9 +618,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
           }
         }
         for (int cR = cloR; cR <= chighR; cR++) {  // indel on right, cL = rL
-          const int v = (int)HR[baseR + cR];
-          const int e = itab[ldL & diR[cR]];
-          const int tot = DL + (e & 255) + (v >> 4) - pen(v);
+          const int v = (int)HR[baseR + cR], d = diR[cR];
+          const int e = itab[ldL & d & DI_MASK];
+          const int tot = DL + (e & 255) + (v >> 4) - pen(v) + kreward(d);
           if (tot > best.score) {
             best.score = tot;
             best.key = 2 * rL + 1;
@@ -605,18 +660,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
           rc = -1;  // no candidate: the reference reads uninitialised indices (:4055)
         } else {
           const int vl = HLv(best.rL, best.cL), vr = HRv(best.rR, best.cR);
+          const int dl = diL[best.cL], dr = diR[best.cR];
           int it;
-          const int sI = intron_score(it, diL[best.cL], diR[best.cR], w.cdna_direction, G.canon,
+          const int sI = intron_score(it, dl & DI_MASK, dr & DI_MASK, w.cdna_direction, G.canon,
                                       w.finalp);
-          const int sL = (vl >> 4) - pen(vl), sR = (vr >> 4) - pen(vr);
+          const int sL = (vl >> 4) - pen(vl) + kreward(dl), sR = (vr >> 4) - pen(vr) + kreward(dr);
           finalscore = w.halfp ? sL + sI + sR - sI / 2 : sL + sI + sR;
           rc = finalscore >= 0;
         }
+      } else if (km == GSNAPDP_KNOWN_INTRONS) {
+        finalscore = best.score;  // no intron score, no halfp (:3694-3695)
+        rc = finalscore >= 0;
       } else {
         finalscore = w.halfp ? best.score - best.sI / 2 : best.score;
         R.introntype = best.score > BRIDGE_INIT ? best.itype : 0;
         rc = finalscore >= 0;
       }
+      // novel splicing off with a site-level IIT: both chosen sites must be known (:4090-4096)
+      if (rc == 1 && km == GSNAPDP_KNOWN_SITES)
+        rc = (diL[best.cL] & KNOWN_BIT) && (diR[best.cR] & KNOWN_BIT);
       if (rc == -2) {
         X.status = ST_UNSUPPORTED;
         R.returned_null = 1;
@@ -630,9 +692,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
         R.returned_null = 1;
       } else {
         R.finalscore = finalscore;
-        if (w.finalp) {  // :4104-4108
-          R.left_prob = left_site_prob(w, best.cL, blocks, nwords, tables);
-          R.right_prob = right_site_prob(w, best.cR, blocks, nwords, tables);
+        if (w.finalp) {  // :4104-4108 (get_splicesite_probs: a known site is 1.0, :3215, :3255)
+          R.left_prob = (diL[best.cL] & KNOWN_BIT) ? 1.0 : left_site_prob(w, best.cL, blocks, nwords, tables);
+          R.right_prob = (diR[best.cR] & KNOWN_BIT) ? 1.0 : right_site_prob(w, best.cR, blocks, nwords, tables);
         }
         R.new_leftgenomepos = w.offset2L + (best.cL - 1);
         R.new_rightgenomepos = w.revoffset2R - (best.cR - 1);
@@ -904,9 +966,11 @@ __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
       R.dynprogindex = step_dpi(w.dynprogindex);
       R.finalscore = NEG;
       R.returned_null = 1;
-    } else if (G.L2L <= 0 || G.L2R <= 0 || G.eb < 0 || G.L2L < G.L1 - 1 || G.L2R < G.L1 - 1) {
+    } else if (G.L2L <= 0 || G.L2R <= 0 || G.eb < 0 || G.L2L < G.L1 - 1 || G.L2R < G.L1 - 1 ||
+               w.known_mode > GSNAPDP_KNOWN_INTRONS) {
       // the reference aborts (Matrix3_alloc :495) or, with a flank shorter than
       // length1 - 1, reads the bridge's diagonal cells past its matrix rows
+      // (or: an unknown known-site mode)
       R.finalscore = NEG;
       R.returned_null = 1;
       X.status = ST_UNSUPPORTED;

@@ -33,7 +33,7 @@ GGAP_WINDOW = np.dtype([
     ("score_threshold", "<i4"), ("dynprogindex", "<i4"), ("maxlength1", "<i4"), ("maxlength2", "<i4"),
     ("defect_rate", "<f4"),
     ("watsonp", "u1"), ("jump_late_p", "u1"), ("halfp", "u1"), ("finalp", "u1"),
-    ("use_probabilities_p", "u1"), ("splicingp", "u1"), ("pad0", "u1"), ("pad1", "u1"),
+    ("use_probabilities_p", "u1"), ("splicingp", "u1"), ("known_mode", "u1"), ("pad1", "u1"),
 ])
 assert GGAP_WINDOW.itemsize == 84
 

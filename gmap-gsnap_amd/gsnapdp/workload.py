@@ -991,3 +991,172 @@ def c3_windows(g: PackedGenome, n: int = 1_000_000, seed: int = 33, read_len: in
     w["widebandp"] = 1
     q = qbuf.reshape(-1)
     return Batch(w, q, q.copy())
+
+
+# ---------------------------------------------------------------- known splice sites
+class SpliceSiteSet:
+    """A splicing IIT's intervals, answering the four queries bridge_intron_gap
+    makes of it (dynprog.c:3375-3550, 3598-3612), restated over plain sets:
+
+    * ``IIT_exists_with_divno_typed_signed(x, y, type, sign)`` (iit-read.c:4011):
+      an interval with low == x, high == y, that type and sign;
+    * ``IIT_low_exists_signed_p(x, sign)`` / ``IIT_high_exists_signed_p`` (:3770, :3808):
+      an interval whose low (high) end is x, with that sign;
+    * ``IIT_exists_with_divno_signed(x, y, sign)`` (:3973): low == x, high == y, sign.
+
+    Intervals are given as iit_store writes them (``start..end``; start > end
+    means the minus sign, Interval_new, interval.c:22-40).  One division only:
+    the windows' chrnum maps to it."""
+
+    def __init__(self, intervals):
+        self.typed, self.exact, self.lows, self.highs = set(), set(), set(), set()
+        self.intervals = list(intervals)
+        for start, end, typ in self.intervals:
+            lo, hi = min(start, end), max(start, end)
+            sign = 1 if start < end else (-1 if start > end else 0)
+            self.typed.add((lo, hi, typ, sign))
+            self.exact.add((lo, hi, sign))
+            self.lows.add((lo, sign))
+            self.highs.add((hi, sign))
+        self.site_level = any(t == "donor" for _, _, t in self.intervals) and \
+            any(t == "acceptor" for _, _, t in self.intervals)
+
+    def iit_text(self, div: str) -> str:
+        """iit_store FASTA input (">label div:start..end [type]")."""
+        out = []
+        for i, (start, end, typ) in enumerate(self.intervals):
+            out.append(">s%d %s:%d..%d%s\n" % (i, div, start, end, " " + typ if typ else ""))
+        return "".join(out)
+
+    def flags(self, w) -> tuple:
+        """left_known / right_known of one gsnapdp_ggap_window (dynprog.c:3375-3550)."""
+        L2L, L2R = int(w["length2L"]), int(w["length2R"])
+        lo, ro = int(w["offset2L"]), int(w["revoffset2R"])
+        chrpos, gl = int(w["chrpos"]), int(w["genomiclength"])
+        watson, fwd = bool(w["watsonp"]), int(w["cdna_direction"]) > 0
+        left, right = np.zeros(L2L, np.uint8), np.zeros(L2R, np.uint8)
+        for cL in range(L2L - 1):
+            pos = chrpos + lo + cL if watson else chrpos + (gl - 1) - lo - cL + 1
+            if self.site_level:
+                typ = "donor" if fwd else "acceptor"
+                sign = (1 if fwd else -1) if watson else (-1 if fwd else 1)
+                left[cL] = (pos, pos + 1, typ, sign) in self.typed
+            elif watson:
+                left[cL] = (pos, 1 if fwd else -1) in self.lows
+            else:
+                left[cL] = (pos + 1, -1 if fwd else 1) in self.highs
+        for cR in range(L2R - 1):
+            pos = chrpos + ro - cR + 1 if watson else chrpos + (gl - 1) - ro + cR
+            if self.site_level:
+                typ = "acceptor" if fwd else "donor"
+                sign = (1 if fwd else -1) if watson else (-1 if fwd else 1)
+                right[cR] = (pos, pos + 1, typ, sign) in self.typed
+            elif watson:
+                right[cR] = (pos + 1, 1 if fwd else -1) in self.highs
+            else:
+                right[cR] = (pos, -1 if fwd else 1) in self.lows
+        return left, right
+
+    def intron_pairs(self, w, left, right) -> list:
+        """(cL, cR), both flagged, whose intron the IIT holds (dynprog.c:3598-3612)."""
+        lo, ro = int(w["offset2L"]), int(w["revoffset2R"])
+        chrpos, gl, cdir = int(w["chrpos"]), int(w["genomiclength"]), int(w["cdna_direction"])
+        out = []
+        for cL in np.flatnonzero(left):
+            for cR in np.flatnonzero(right):
+                if w["watsonp"]:
+                    x, y, s = chrpos + lo + cL, chrpos + ro - cR + 1 + 1, cdir
+                else:
+                    x, y, s = chrpos + (gl - 1) - ro + cR, chrpos + (gl - 1) - lo - cL + 1 + 1, -cdir
+                if (x, y, s) in self.exact:
+                    out.append((int(cL), int(cR)))
+        return out
+
+
+def with_known_sites(windows, query, query_uc, sites: SpliceSiteSet, novelsplicingp: bool):
+    """Copy of a genome-gap batch with each window's known-site record placed
+    after its query rows (include/gsnapdp.h, gsnapdp_ggap_window) and known_mode
+    set the way Dynprog_setup's IIT and novelsplicingp select it (dynprog.c:3552,
+    :4084-4101)."""
+    if novelsplicingp:
+        mode = 1  # GSNAPDP_KNOWN_REWARD
+    else:
+        mode = 2 if sites.site_level else 3  # GSNAPDP_KNOWN_SITES / GSNAPDP_KNOWN_INTRONS
+    w = windows.copy()
+    qs, us, pos = [], [], 0
+    for i in range(len(w)):
+        L1, q0 = int(w[i]["length1"]), int(w[i]["qpos"])
+        left, right = sites.flags(w[i])
+        rec = [left, right]
+        pairs = sites.intron_pairs(w[i], left, right) if mode == 3 else []
+        rec.append(np.array([len(pairs) & 255, len(pairs) >> 8], np.uint8))
+        for cL, cR in pairs:
+            rec.append(np.array([cL & 255, cL >> 8, cR & 255, cR >> 8], np.uint8))
+        rec = np.concatenate(rec)
+        pad = np.full(4, ord("#"), np.uint8)
+        qs += [query[q0:q0 + L1], rec, pad]
+        us += [query_uc[q0:q0 + L1], rec, pad]
+        w[i]["qpos"] = pos
+        w[i]["known_mode"] = mode
+        pos += L1 + rec.size + 4
+    return w, np.concatenate(qs), np.concatenate(us)
+
+
+def known_site_intervals(w, res, rng, site_level: bool) -> list:
+    """Splice sites / introns around each genome-gap window (test workloads):
+    the sites the bridge picks without an IIT (`res`, a gsnapdp_ggap_result
+    array, or None), random columns, and decoys of the wrong type or sign.  Coordinates as bridge_intron_gap queries them
+    (dynprog.c:3375-3550, 3598-3612)."""
+    out = []
+
+    def lpos(x, cL):
+        return (int(x["chrpos"]) + int(x["offset2L"]) + cL if x["watsonp"] else
+                int(x["chrpos"]) + (int(x["genomiclength"]) - 1) - int(x["offset2L"]) - cL + 1)
+
+    def rpos(x, cR):
+        return (int(x["chrpos"]) + int(x["revoffset2R"]) - cR + 1 if x["watsonp"] else
+                int(x["chrpos"]) + (int(x["genomiclength"]) - 1) - int(x["revoffset2R"]) + cR)
+
+    for x, r in zip(w, res if res is not None else [None] * len(w)):
+        L2L, L2R = int(x["length2L"]), int(x["length2R"])
+        if L2L < 2 or L2R < 2:
+            continue
+        fwd = int(x["cdna_direction"]) > 0
+        if r is not None and r["returned_null"] == 0:
+            cl0 = int(r["new_leftgenomepos"]) - int(x["offset2L"]) + 1
+            cr0 = int(x["revoffset2R"]) - int(r["new_rightgenomepos"]) + 1
+        else:
+            cl0, cr0 = int(rng.integers(0, L2L - 1)), int(rng.integers(0, L2R - 1))
+        cls = {cl0} | {int(c) for c in rng.integers(0, L2L - 1, size=3)}
+        crs = {cr0} | {int(c) for c in rng.integers(0, L2R - 1, size=3)}
+        if site_level:
+            sign = (1 if fwd else -1) if x["watsonp"] else (-1 if fwd else 1)
+            lt, rt = ("donor", "acceptor") if fwd else ("acceptor", "donor")
+            for cL in cls:
+                p = lpos(x, cL)
+                t = lt if rng.random() < 0.85 else rt           # decoy: wrong type
+                sg = sign if rng.random() < 0.9 else -sign      # decoy: wrong sign
+                out.append((p, p + 1, t) if sg > 0 else (p + 1, p, t))
+            for cR in crs:
+                p = rpos(x, cR)
+                t = rt if rng.random() < 0.85 else lt
+                sg = sign if rng.random() < 0.9 else -sign
+                out.append((p, p + 1, t) if sg > 0 else (p + 1, p, t))
+        else:
+            cdir = int(x["cdna_direction"])
+            for cL in cls:
+                for cR in crs:
+                    if rng.random() < (0.9 if (cL, cR) == (cl0, cr0) else 0.25):
+                        if x["watsonp"]:
+                            lo_, hi_, sg = lpos(x, cL), rpos(x, cR) + 1, cdir
+                        else:
+                            lo_, hi_, sg = rpos(x, cR), lpos(x, cL) + 1, -cdir
+                        if sg == 0:
+                            sg = 1 if rng.random() < 0.5 else -1
+                        if lo_ < hi_:
+                            out.append((lo_, hi_, None) if sg > 0 else (hi_, lo_, None))
+            for cL in cls:  # lone donor ends (intron-level left_known without a partner)
+                if rng.random() < 0.3:
+                    p = lpos(x, cL)
+                    out.append((p, p + 500, None) if rng.random() < 0.5 else (p + 500, p, None))
+    return out

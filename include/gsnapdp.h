@@ -140,10 +140,31 @@ typedef struct gsnapdp_pair {
                            * knownp = true (Pairpool_push_gapholder, pairpool.c:383-390) */
 } gsnapdp_pair;
 
-/* One intron window (Dynprog_genome_gap, dynprog.c:4798-5061), run with
- * splicing_iit == NULL (no known-site rewards, Dynprog_setup :350).  The query
+/* One intron window (Dynprog_genome_gap, dynprog.c:4798-5061).  The query
  * is sequence1[0..length1) at qpos; genome flanks are addressed through
- * offset2L (left, fwd) and revoffset2R (right, rev) like the reference. */
+ * offset2L (left, fwd) and revoffset2R (right, rev) like the reference.
+ *
+ * Known splice sites (a splicing IIT given to Dynprog_setup, dynprog.c:350;
+ * bridge_intron_gap :3375-3697, :4084-4101) are described by known_mode:
+ *   GSNAPDP_KNOWN_NONE        splicing_iit == NULL
+ *   GSNAPDP_KNOWN_REWARD      novelsplicingp: known sites add
+ *                             KNOWN_SPLICESITE_REWARD (20) to the flank scores
+ *                             and have probability 1.0
+ *   GSNAPDP_KNOWN_SITES       site-level IIT (donor/acceptor types) without
+ *                             novel splicing: rewards, and the result requires
+ *                             both chosen sites to be known (:4090-4096)
+ *   GSNAPDP_KNOWN_INTRONS     intron-level IIT without novel splicing: only
+ *                             known introns are candidates (:3552-3697)
+ * For every mode but NONE the caller places a known-site record right after
+ * the window's query rows, at query[qpos + length1]:
+ *   uint8  left_known[length2L]    1 where the reference sets left_known[cL]
+ *   uint8  right_known[length2R]   1 where it sets right_known[cR]
+ *   uint16 npairs (little endian)  KNOWN_INTRONS: the (cL, cR) pairs, both
+ *   uint16 cL, cR  x npairs        flagged, for which the reference's
+ *                                  IIT_exists_with_divno_signed holds
+ * (gsnapdp_dropin.cpp builds it from the host program's IIT queries.) */
+enum { GSNAPDP_KNOWN_NONE = 0, GSNAPDP_KNOWN_REWARD = 1, GSNAPDP_KNOWN_SITES = 2,
+       GSNAPDP_KNOWN_INTRONS = 3 };
 typedef struct gsnapdp_ggap_window {
   int32_t length1, length2L, length2R;
   int32_t offset1, offset2L, revoffset2R;
@@ -153,7 +174,7 @@ typedef struct gsnapdp_ggap_window {
   int32_t maxlength1, maxlength2;
   float defect_rate;
   uint8_t watsonp, jump_late_p, halfp, finalp;
-  uint8_t use_probabilities_p, splicingp, pad0, pad1;
+  uint8_t use_probabilities_p, splicingp, known_mode, pad1;
 } gsnapdp_ggap_window;
 
 /* Out-parameters of Dynprog_genome_gap for one window. */

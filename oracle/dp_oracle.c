@@ -1007,7 +1007,35 @@ static double right_site_prob(int cR, int rightoffset, const gpar *g, int cdna_d
 
 static inline int gapdir_penalty(uint8_t d) { return (d == D_HORIZ || d == D_VERT) ? 1 : 0; }
 
-/* bridge_intron_gap (dynprog.c:3290-4122) with splicing_iit == NULL.
+#define KNOWN_SPLICESITE_REWARD 20 /* dynprog.c:285 */
+
+/* Known-site record of a window (include/gsnapdp.h, gsnapdp_ggap_window):
+ * left_known[L2L], right_known[L2R] flags, then the KNOWN_INTRONS pair list. */
+typedef struct {
+  int mode;
+  const unsigned char *rec;
+  int L2L, L2R;
+} known_t;
+
+static int known_left(const known_t *k, int cL) { /* left_known[cL] (:3375-3550) */
+  return (k->mode && cL >= 0 && cL < k->L2L && k->rec[cL]) ? KNOWN_SPLICESITE_REWARD : 0;
+}
+static int known_right(const known_t *k, int cR) {
+  return (k->mode && cR >= 0 && cR < k->L2R && k->rec[k->L2L + cR]) ? KNOWN_SPLICESITE_REWARD : 0;
+}
+/* IIT_exists_with_divno_signed on the intron (cL, cR) (:3598-3612) */
+static int known_intron(const known_t *k, int cL, int cR) {
+  const unsigned char *p = k->rec + k->L2L + k->L2R;
+  int n = p[0] | (p[1] << 8), i;
+  for (i = 0; i < n; i++) {
+    const unsigned char *e = p + 2 + 4 * i;
+    if ((e[0] | (e[1] << 8)) == cL && (e[2] | (e[3] << 8)) == cR) return 1;
+  }
+  return 0;
+}
+
+/* bridge_intron_gap (dynprog.c:3290-4122).  k->mode selects the splicing-IIT
+ * behaviour (include/gsnapdp.h GSNAPDP_KNOWN_*).
  * Returns 1 = accepted, 0 = rejected, -1 = probability mode found nothing
  * (the reference then reads uninitialised indices, :4055). */
 static int bridge_intron(int *finalscore, int *brL, int *brR, int *bcL, int *bcR, int *best_type,
@@ -1015,7 +1043,8 @@ static int bridge_intron(int *finalscore, int *brL, int *brR, int *bcL, int *bcR
                          int offset2L, int revoffset2R, int L1, int L2L, int L2R,
                          int cdna_direction, const gpar *g, int extraband_paired,
                          int canonical_reward, int leftoffset, int rightoffset, int halfp,
-                         int finalp, int use_probabilities_p, int score_threshold) {
+                         int finalp, int use_probabilities_p, int score_threshold,
+                         const known_t *kn) {
   int bestscore = -100000, bestscoreI = -100000, scoreL, scoreR, scoreI, introntype;
   int rL, rR, cL, cR, cloL, chighL, cloR, chighR;
   int lbandL = extraband_paired, rbandL = L2L - L1 + extraband_paired;
@@ -1041,17 +1070,58 @@ static int bridge_intron(int *finalscore, int *brL, int *brR, int *bcL, int *bcR
                                            : 0;
   }
 
-  if (!use_probabilities_p) { /* :3698-3827 */
+  if (kn->mode == GSNAPDP_KNOWN_INTRONS) { /* constrain to given introns, :3552-3697 */
     for (rL = 1, rR = L1 - 1; rL < L1; rL++, rR--) {
       cloL = rL - lbandL < 1 ? 1 : rL - lbandL;
       chighL = rL + rbandL > L2L - 1 ? L2L - 1 : rL + rbandL;
       cloR = rR - lbandR < 1 ? 1 : rR - lbandR;
       chighR = rR + rbandR > L2R - 1 ? L2R - 1 : rR + rbandR;
       for (cL = cloL; cL <= chighL; cL++) { /* indel on left */
-        scoreL = mL->H[IX(mL, rL, cL)] - gapdir_penalty(mL->dH[IX(mL, rL, cL)]);
+        if (known_left(kn, cL) > 0) {
+          scoreL = mL->H[IX(mL, rL, cL)] - gapdir_penalty(mL->dH[IX(mL, rL, cL)]);
+          cR = rR;
+          if (cR < rightoffset - leftoffset - cL && known_right(kn, cR) > 0) {
+            scoreR = mR->H[IX(mR, rR, cR)];
+            if (scoreL + scoreR > bestscore && known_intron(kn, cL, cR)) {
+              bestscore = scoreL + scoreR;
+              *brL = rL;
+              *brR = rR;
+              *bcL = cL;
+              *bcR = cR;
+            }
+          }
+        }
+      }
+      for (cR = cloR; cR <= chighR; cR++) { /* indel on right */
+        if (known_right(kn, cR) > 0) {
+          scoreR = mR->H[IX(mR, rR, cR)] - gapdir_penalty(mR->dH[IX(mR, rR, cR)]);
+          cL = rL;
+          if (cL < rightoffset - leftoffset - cR && known_left(kn, cL) > 0) {
+            scoreL = mL->H[IX(mL, rL, cL)];
+            if (scoreL + scoreR > bestscore && known_intron(kn, cL, cR)) {
+              bestscore = scoreL + scoreR;
+              *brL = rL;
+              *brR = rR;
+              *bcL = cL;
+              *bcR = cR;
+            }
+          }
+        }
+      }
+    }
+    *finalscore = bestscore;
+    *best_type = 0; /* NONINTRON */
+  } else if (!use_probabilities_p) { /* :3698-3827 */
+    for (rL = 1, rR = L1 - 1; rL < L1; rL++, rR--) {
+      cloL = rL - lbandL < 1 ? 1 : rL - lbandL;
+      chighL = rL + rbandL > L2L - 1 ? L2L - 1 : rL + rbandL;
+      cloR = rR - lbandR < 1 ? 1 : rR - lbandR;
+      chighR = rR + rbandR > L2R - 1 ? L2R - 1 : rR + rbandR;
+      for (cL = cloL; cL <= chighL; cL++) { /* indel on left */
+        scoreL = mL->H[IX(mL, rL, cL)] + known_left(kn, cL) - gapdir_penalty(mL->dH[IX(mL, rL, cL)]);
         cR = rR;
         if (cR < rightoffset - leftoffset - cL) {
-          scoreR = mR->H[IX(mR, rR, cR)];
+          scoreR = mR->H[IX(mR, rR, cR)] + known_right(kn, cR);
           scoreI = intron_score(&introntype, leftdi[cL], rightdi[cR], cdna_direction,
                                 canonical_reward, finalp);
           if (scoreL + scoreI + scoreR > bestscore) {
@@ -1066,10 +1136,10 @@ static int bridge_intron(int *finalscore, int *brL, int *brR, int *bcL, int *bcR
         }
       }
       for (cR = cloR; cR <= chighR; cR++) { /* indel on right */
-        scoreR = mR->H[IX(mR, rR, cR)] - gapdir_penalty(mR->dH[IX(mR, rR, cR)]);
+        scoreR = mR->H[IX(mR, rR, cR)] + known_right(kn, cR) - gapdir_penalty(mR->dH[IX(mR, rR, cR)]);
         cL = rL;
         if (cL < rightoffset - leftoffset - cR) {
-          scoreL = mL->H[IX(mL, rL, cL)];
+          scoreL = mL->H[IX(mL, rL, cL)] + known_left(kn, cL);
           scoreI = intron_score(&introntype, leftdi[cL], rightdi[cR], cdna_direction,
                                 canonical_reward, finalp);
           if (scoreL + scoreI + scoreR > bestscore) {
@@ -1089,8 +1159,10 @@ static int bridge_intron(int *finalscore, int *brL, int *brR, int *bcL, int *bcR
     double *lp = (double *)calloc((size_t)L2L + 1, sizeof(double));
     double *rp = (double *)calloc((size_t)L2R + 1, sizeof(double));
     double bestprob = 0.0, probL, probR;
-    for (cL = 0; cL < L2L - 1; cL++) lp[cL] = left_site_prob(cL, leftoffset, g, cdna_direction);
-    for (cR = 0; cR < L2R - 1; cR++) rp[cR] = right_site_prob(cR, rightoffset, g, cdna_direction);
+    for (cL = 0; cL < L2L - 1; cL++)
+      lp[cL] = known_left(kn, cL) ? 1.0 : left_site_prob(cL, leftoffset, g, cdna_direction);
+    for (cR = 0; cR < L2R - 1; cR++)
+      rp[cR] = known_right(kn, cR) ? 1.0 : right_site_prob(cR, rightoffset, g, cdna_direction);
     for (rL = 1, rR = L1 - 1; rL < L1; rL++, rR--) {
       cloL = rL - lbandL < 1 ? 1 : rL - lbandL;
       chighL = rL + rbandL > L2L - 1 ? L2L - 1 : rL + rbandL;
@@ -1102,8 +1174,8 @@ static int bridge_intron(int *finalscore, int *brL, int *brR, int *bcL, int *bcR
         if (cR < rightoffset - leftoffset - cL) {
           probR = rp[cR];
           if (!(probL + probR <= bestprob)) {
-            scoreL = mL->H[IX(mL, rL, cL)] - gapdir_penalty(mL->dH[IX(mL, rL, cL)]);
-            scoreR = mR->H[IX(mR, rR, cR)];
+            scoreL = mL->H[IX(mL, rL, cL)] + known_left(kn, cL) - gapdir_penalty(mL->dH[IX(mL, rL, cL)]);
+            scoreR = mR->H[IX(mR, rR, cR)] + known_right(kn, cR);
             scoreI = intron_score(&introntype, leftdi[cL], rightdi[cR], cdna_direction,
                                   canonical_reward, finalp);
             if (scoreL + scoreI + scoreR >= score_threshold) {
@@ -1123,8 +1195,8 @@ static int bridge_intron(int *finalscore, int *brL, int *brR, int *bcL, int *bcR
         if (cL < rightoffset - leftoffset - cR) {
           probL = lp[cL];
           if (!(probL + probR <= bestprob)) {
-            scoreL = mL->H[IX(mL, rL, cL)];
-            scoreR = mR->H[IX(mR, rR, cR)] - gapdir_penalty(mR->dH[IX(mR, rR, cR)]);
+            scoreL = mL->H[IX(mL, rL, cL)] + known_left(kn, cL);
+            scoreR = mR->H[IX(mR, rR, cR)] + known_right(kn, cR) - gapdir_penalty(mR->dH[IX(mR, rR, cR)]);
             scoreI = intron_score(&introntype, leftdi[cL], rightdi[cR], cdna_direction,
                                   canonical_reward, finalp);
             if (scoreL + scoreI + scoreR >= score_threshold) {
@@ -1146,16 +1218,18 @@ static int bridge_intron(int *finalscore, int *brL, int *brR, int *bcL, int *bcR
       free(rightdi);
       return -1;
     }
-    scoreL = mL->H[IX(mL, *brL, *bcL)] - gapdir_penalty(mL->dH[IX(mL, *brL, *bcL)]);
-    scoreR = mR->H[IX(mR, *brR, *bcR)] - gapdir_penalty(mR->dH[IX(mR, *brR, *bcR)]);
+    scoreL = mL->H[IX(mL, *brL, *bcL)] + known_left(kn, *bcL) - gapdir_penalty(mL->dH[IX(mL, *brL, *bcL)]);
+    scoreR = mR->H[IX(mR, *brR, *bcR)] + known_right(kn, *bcR) - gapdir_penalty(mR->dH[IX(mR, *brR, *bcR)]);
     scoreI = intron_score(&introntype, leftdi[*bcL], rightdi[*bcR], cdna_direction,
                           canonical_reward, finalp);
     *finalscore = halfp ? scoreL + scoreI + scoreR - scoreI / 2 : scoreL + scoreI + scoreR;
   }
-  result = *finalscore >= 0; /* :4084-4101 with splicing_iit == NULL */
-  if (finalp && result) {   /* :4104-4108 */
-    *left_prob = left_site_prob(*bcL, leftoffset, g, cdna_direction);
-    *right_prob = right_site_prob(*bcR, rightoffset, g, cdna_direction);
+  result = *finalscore >= 0; /* :4084-4101 */
+  if (result && kn->mode == GSNAPDP_KNOWN_SITES)  /* novel splicing off: both sites known */
+    result = known_left(kn, *bcL) > 0 && known_right(kn, *bcR) > 0;
+  if (finalp && result) {   /* :4104-4108, get_splicesite_probs :3195-3287 */
+    *left_prob = known_left(kn, *bcL) ? 1.0 : left_site_prob(*bcL, leftoffset, g, cdna_direction);
+    *right_prob = known_right(kn, *bcR) ? 1.0 : right_site_prob(*bcR, rightoffset, g, cdna_direction);
   }
   free(leftdi);
   free(rightdi);
@@ -1169,8 +1243,9 @@ void orc_genome_gap(orc_list *out, orc_genome_gap_out *o, int dpi, orc_dp *dpL, 
                     uint32_t chrhigh, uint32_t chrpos, uint32_t genomiclength, int cdna_direction,
                     int watsonp, int jump_late_p, int extraband_paired, double defect_rate,
                     int maxpeelback, int halfp, int finalp, int use_probabilities_p,
-                    int score_threshold, int splicingp) {
+                    int score_threshold, int splicingp, int known_mode) {
   int mt, open, extend, canonical_reward, revoffset1, brL = 0, brR = 0, bcL = 0, bcR = 0, rc;
+  known_t kn;
   mview mL, mR;
   counts k = {0, 0, 0, 0};
   gpar g = {chroffset, chrhigh, chrpos, (int)genomiclength, watsonp};
@@ -1208,10 +1283,14 @@ void orc_genome_gap(orc_list *out, orc_genome_gap_out *o, int dpi, orc_dp *dpL, 
        1, jump_late_p);
   fill(&mR, dpR, &sequence1[length1 - 1], 1, revoffset2R, length1, length2R, &g, mt, open, extend,
        extraband_paired, 1, !jump_late_p);
+  kn.mode = known_mode;
+  kn.rec = (const unsigned char *)sequence1 + length1; /* the record follows the query rows */
+  kn.L2L = length2L;
+  kn.L2R = length2R;
   rc = bridge_intron(&o->finalscore, &brL, &brR, &bcL, &bcR, &o->introntype, &o->left_prob,
                      &o->right_prob, &mL, &mR, offset2L, revoffset2R, length1, length2L, length2R,
                      cdna_direction, &g, extraband_paired, canonical_reward, offset2L,
-                     revoffset2R, halfp, finalp, use_probabilities_p, score_threshold);
+                     revoffset2R, halfp, finalp, use_probabilities_p, score_threshold, &kn);
   if (rc < 0) {
     o->bridge_ok = 0;
     o->returned_null = 1;
@@ -1703,7 +1782,7 @@ int orc_run_ggap_batch(const gsnapdp_ggap_window *w, int n, const char *query, c
                    x->chroffset, x->chrhigh, x->chrpos, x->genomiclength, x->cdna_direction,
                    x->watsonp, x->jump_late_p, x->extraband_paired, (double)x->defect_rate,
                    x->maxpeelback, x->halfp, x->finalp, x->use_probabilities_p,
-                   x->score_threshold, x->splicingp);
+                   x->score_threshold, x->splicingp, x->known_mode);
     memset(r, 0, sizeof(*r));
     r->finalscore = o.finalscore;
     r->new_leftgenomepos = o.new_leftgenomepos;

@@ -99,7 +99,8 @@ void orc_genome_gap(orc_list *out, orc_genome_gap_out *o, int dynprogindex_in,
                     int revoffset2R, uint32_t chroffset, uint32_t chrhigh, uint32_t chrpos,
                     uint32_t genomiclength, int cdna_direction, int watsonp, int jump_late_p,
                     int extraband_paired, double defect_rate, int maxpeelback, int halfp,
-                    int finalp, int use_probabilities_p, int score_threshold, int splicingp);
+                    int finalp, int use_probabilities_p, int score_threshold, int splicingp,
+                    int known_mode); /* GSNAPDP_KNOWN_*: record at sequence1[length1] */
 
 /* Dynprog_cdna_gap (dynprog.c:4578-4793). */
 typedef struct orc_cdna_gap_out {

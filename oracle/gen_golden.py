@@ -176,6 +176,48 @@ def ggap_case(name: str, gseq: np.ndarray, n: int, seed: int) -> None:
           (name, len(w), int((~keep).sum()), pairs.size))
 
 
+def ggap_known_case(name: str, gseq: np.ndarray, n: int, seed: int, site_level: bool,
+                    novel: bool) -> None:
+    """Dynprog_genome_gap with a splicing IIT (dynprog.c:3375-3697, :4084-4101):
+    site-level (donor / acceptor types) or intron-level intervals written by the
+    reference's own iit_store, novel splicing on or off; windows as ggap_case."""
+    sys.path.insert(0, HERE)
+    import oracle as O  # checker: picks the no-IIT bridge sites, drops UB windows
+    rng = np.random.default_rng(seed + 7)
+    g, w, q, u = ggap_windows(gseq, n, seed)
+    blocks = G.pack(g)
+    O.setup(blocks)
+    res0, _, _, _ = O.run_ggap_batch(w, q, u)
+    sites = W.SpliceSiteSet(W.known_site_intervals(w, res0, rng, site_level))
+    assert sites.site_level == site_level
+    wk, qk, uk = W.with_known_sites(w, q, u, sites, novel)
+    ores, _, _, _ = O.run_ggap_batch(wk, qk, uk)
+    keep = ores["bridge_ok"] == 1  # dynprog.c:4055 reads uninitialised indices otherwise
+    wk = wk[keep]
+    with tempfile.TemporaryDirectory() as d:
+        with open(os.path.join(d, "sites.txt"), "w") as f:
+            f.write(sites.iit_text("chr17test"))
+        subprocess.check_call([os.path.join(HERE, "_ref", "iit_store"), "-o", os.path.join(d, "sites"),
+                               os.path.join(d, "sites.txt")], stdout=subprocess.DEVNULL)
+        wk.tofile(os.path.join(d, "ggap_windows.bin"))
+        qk.tofile(os.path.join(d, "query.bin"))
+        uk.tofile(os.path.join(d, "query_uc.bin"))
+        blocks.astype("<u4").tofile(os.path.join(d, "genome.u32"))
+        subprocess.check_call([DRIVER, "ggapk", d, "0", os.path.join(d, "sites.iit"), "chr17test",
+                               str(int(novel))])
+        res = np.fromfile(os.path.join(d, "ggap_results.bin"), dtype=GGAP_RESULT)
+        npairs = np.fromfile(os.path.join(d, "npairs.i32"), dtype=np.int32)
+        pairs = np.fromfile(os.path.join(d, "pairs.bin"), dtype=PAIR)
+    iv = np.array([(a, b, {None: 0, "donor": 1, "acceptor": 2}[t]) for a, b, t in sites.intervals],
+                  dtype=np.int64)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), blocks=blocks, windows=wk, query=qk,
+                        query_uc=uk, results=res, npairs=npairs, pairs=pairs, intervals=iv,
+                        novelsplicingp=np.int32(novel), dropped_ub=np.int32((~keep).sum()))
+    print("%s: %d windows (%d dropped: probability-mode UB), %d intervals, %d pairs, %d NULL" %
+          (name, len(wk), int((~keep).sum()), len(sites.intervals), pairs.size,
+           int(res["returned_null"].sum())))
+
+
 def cgap_case(name: str, gseq: np.ndarray, n: int, seed: int) -> None:
     """Dynprog_cdna_gap windows (W.cgap_windows); windows whose bridge finds no
     candidate (the reference then reads uninitialised indices) are dropped."""
@@ -593,6 +635,14 @@ def main() -> None:
         ("dp_synth_long", lambda: dp_case("dp_synth_long", bsyn, W.random_windows(
             synth, 150, seed=105, max_len1=640, max_len2=700, max_band=40))),
         ("ggap_chr17", lambda: ggap_case("ggap_chr17", chr17, 1500, seed=201)),
+        ("ggap_known_sites", lambda: ggap_known_case("ggap_known_sites", chr17, 800, seed=211,
+                                                     site_level=True, novel=False)),
+        ("ggap_known_sites_novel", lambda: ggap_known_case("ggap_known_sites_novel", chr17, 800,
+                                                           seed=212, site_level=True, novel=True)),
+        ("ggap_known_introns", lambda: ggap_known_case("ggap_known_introns", chr17, 800, seed=213,
+                                                       site_level=False, novel=False)),
+        ("ggap_known_introns_novel", lambda: ggap_known_case("ggap_known_introns_novel", chr17, 800,
+                                                             seed=214, site_level=False, novel=True)),
         ("cgap_chr17", lambda: cgap_case("cgap_chr17", chr17, 1500, seed=401)),
         ("sj_chr17", lambda: sj_case("sj_chr17", chr17, 2000, seed=501)),
         ("mksj_chr17", lambda: mksj_case("mksj_chr17", chr17, 2000, seed=502)),

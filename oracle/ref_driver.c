@@ -8,6 +8,9 @@
  * Usage:
  *   ref_driver dp     <dir>   windows.bin query.bin query_uc.bin genome.u32 -> results.bin pairs.bin npairs.i32
  *   ref_driver ggap   <dir>   ggap_windows.bin query.bin query_uc.bin genome.u32 -> ggap_results.bin pairs.bin npairs.i32
+ *   ref_driver ggapk  <dir> 0 <splicing.iit> <div> <novelsplicingp>
+ *                             the same with a splicing IIT given to Dynprog_setup (known-site
+ *                             rewards / constrained introns, dynprog.c:3375-3697); chrnum 1 maps to <div>
  *   ref_driver cgap   <dir>   cgap_windows.bin query.bin query_uc.bin gseg.bin gseg_off.i64 genome.u32
  *                             -> cgap_results.bin pairs.bin npairs.i32
  *   ref_driver sj     <dir>   sj_windows.bin query.bin query_uc.bin -> results.bin pairs.bin npairs.i32
@@ -35,6 +38,7 @@
 #include "pairpool.h"
 #include "splicetrie_build.h"
 #include "splicetrie.h"
+#include "iit-read.h"
 
 /* our record layouts */
 #include "../include/gsnapdp.h"
@@ -548,6 +552,25 @@ static int run_pdist(const char *dir) {
   return 0;
 }
 
+/* Dynprog_setup with the splicing IIT, as gmap.c:3283-3302 / 3729-3731 set it up */
+static int setup_splicing_iit(const char *iitfile, const char *div, int novelsplicingp) {
+  static int crosstable[2];
+  IIT_T iit = IIT_read((char *)iitfile, NULL, true, READ_ALL, NULL, false, false);
+  int donor_typeint, acceptor_typeint;
+  if (!iit) {
+    fprintf(stderr, "cannot read %s\n", iitfile);
+    exit(2);
+  }
+  crosstable[0] = -1;
+  crosstable[1] = IIT_divint(iit, (char *)div);
+  if ((donor_typeint = IIT_typeint(iit, "donor")) < 0 || (acceptor_typeint = IIT_typeint(iit, "acceptor")) < 0) {
+    donor_typeint = acceptor_typeint = -1;  /* an introns file */
+  }
+  Dynprog_setup(novelsplicingp, iit, crosstable, donor_typeint, acceptor_typeint, NULL, NULL, NULL, 0,
+                NULL, NULL, NULL, NULL, /*genome*/ NULL);
+  return 0;
+}
+
 int main(int argc, char **argv) {
   int mode = 0; /* STANDARD */
   if (argc < 3) {
@@ -560,6 +583,10 @@ int main(int argc, char **argv) {
                 NULL, NULL, /*genome*/ NULL);
   if (!strcmp(argv[1], "dp")) return run_dp(argv[2]);
   if (!strcmp(argv[1], "ggap")) return run_ggap(argv[2]);
+  if (!strcmp(argv[1], "ggapk") && argc > 6) {
+    setup_splicing_iit(argv[4], argv[5], atoi(argv[6]));
+    return run_ggap(argv[2]);
+  }
   if (!strcmp(argv[1], "cgap")) return run_cgap(argv[2]);
   if (!strcmp(argv[1], "maxent")) return run_maxent(argv[2]);
   if (!strcmp(argv[1], "sj")) return run_sj(argv[2]);

@@ -191,14 +191,52 @@ GGAP_ARGS = ([ctypes.c_void_p] * 14 + [ctypes.c_char_p] * 6 + [ctypes.c_int] * 6
                                      ctypes.c_int, ctypes.c_ubyte])
 
 
+IIT_DOUBLE_SRC = os.path.join(ROOT, "tests", "dropin", "iit_double.c")
+SETUP_ARGS = ([ctypes.c_ubyte, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+              + [ctypes.c_void_p] * 3 + [ctypes.c_int] + [ctypes.c_void_p] * 5)
+
+
+def load_iit_double(tmp_path, z):
+    """The splicing IIT of a ggap_known_* set, served by tests/dropin/iit_double.c."""
+    so = os.path.join(str(tmp_path), "libiit_double.so")
+    subprocess.check_call(["gcc", "-O1", "-shared", "-fPIC", "-o", so, IIT_DOUBLE_SRC])
+    lib = ctypes.CDLL(so, mode=ctypes.RTLD_GLOBAL)  # the shim looks the IIT_* queries up in the process
+    iv = np.ascontiguousarray(z["intervals"])
+    start = np.ascontiguousarray(iv[:, 0])
+    end = np.ascontiguousarray(iv[:, 1])
+    typ = np.ascontiguousarray(iv[:, 2].astype(np.int32))
+    lib.iitdbl_new.restype = ctypes.c_void_p
+    lib.iitdbl_new.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3
+    h = lib.iitdbl_new(len(iv), start.ctypes.data, end.ctypes.data, typ.ctypes.data)
+    site_level = bool(np.any(typ == 1) and np.any(typ == 2))
+    # donor / acceptor type numbers (IIT_typeint): the double's own codes 1 and 2
+    return lib, h, (1, 2) if site_level else (-1, -1)
+
+
+KNOWN_SETS = ["ggap_known_sites", "ggap_known_sites_novel", "ggap_known_introns",
+              "ggap_known_introns_novel"]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap", "gmap_her2_ggap"])
+@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap", "gmap_her2_ggap"] + KNOWN_SETS)
 def test_dropin_genome_gap_matches_reference_golden(golden_dir, tmp_path, name):
     """Dynprog_genome_gap called like traverse_genome_gap (stage3.c:5772) on the
-    reference's golden intron windows: every out-parameter and the list."""
+    reference's golden intron windows: every out-parameter and the list.  The
+    ggap_known_* sets give Dynprog_setup a splicing IIT (an IIT test double over
+    the intervals the reference's iit_store wrote), from which the shim builds
+    each window's known-site record with the IIT queries bridge_intron_gap makes."""
     z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
     dbl = load_double(tmp_path)
     L = ctypes.CDLL(DROPIN)
+    L.Dynprog_setup.argtypes = SETUP_ARGS
+    known = "intervals" in z.files
+    crosstable = (ctypes.c_int * 2)(-1, 0)  # chrnum 1 -> the IIT's one division
+    if known:
+        iitlib, iit, (dtype, atype) = load_iit_double(tmp_path, z)
+        L.Dynprog_setup(int(z["novelsplicingp"]), iit, ctypes.addressof(crosstable), dtype, atype,
+                        None, None, None, 0, None, None, None, None, None)
+    else:
+        L.Dynprog_setup(1, None, None, -1, -1, None, None, None, 0, None, None, None, None, None)
     L.Dynprog_new.restype = ctypes.c_void_p
     L.Dynprog_new.argtypes = [ctypes.c_int] * 5
     L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
@@ -229,7 +267,7 @@ def test_dropin_genome_gap_matches_reference_golden(golden_dir, tmp_path, name):
                 + [ctypes.byref(x) for x in counts] + [dpL, dpR, seq, sequc, None, None, None, None]
                 + [int(w[f]) for f in ("length1", "length2L", "length2R", "offset1", "offset2L",
                                        "revoffset2R")]
-                + [0] + [int(w[f]) for f in ("chroffset", "chrhigh", "chrpos", "genomiclength")]
+                + [1] + [int(w[f]) for f in ("chroffset", "chrhigh", "chrpos", "genomiclength")]
                 + [None, 0, int(w["cdna_direction"]), int(w["watsonp"]), int(w["jump_late_p"]), None,
                    int(w["extraband_paired"]), float(w["defect_rate"]), int(w["maxpeelback"]),
                    int(w["halfp"]), int(w["finalp"]), int(w["use_probabilities_p"]),
@@ -245,9 +283,14 @@ def test_dropin_genome_gap_matches_reference_golden(golden_dir, tmp_path, name):
             assert [ints[2].value, ints[3].value, counts[4].value] == [
                 int(r[f]) for f in ("new_leftgenomepos", "new_rightgenomepos", "exonhead")], i
         # *introntype is written only when a score-mode bridge candidate was taken
-        # (dynprog.c:3720-3800); the golden driver passes it in as 0
-        untouched = (w["use_probabilities_p"] == 1 or w["length1"] <= 1
-                     or r["finalscore"] in (-100000, -50000 if w["halfp"] else -100000, -1000000))
+        # (dynprog.c:3720-3800), or always by the constrained known-intron bridge
+        # (:3695); the golden driver passes it in as 0
+        early = w["length1"] <= 1 or r["finalscore"] == -1000000
+        if "known_mode" in W.dtype.names and w["known_mode"] == 3:
+            untouched = early
+        else:
+            untouched = (w["use_probabilities_p"] == 1 or early
+                         or r["finalscore"] in (-100000, -50000 if w["halfp"] else -100000))
         assert counts[5].value == (-77 if untouched else int(r["introntype"])), i
         k = dbl.dbl_list_read(lst, out.ctypes.data, out.size) if lst else 0
         ref_pairs = z["pairs"][offs[i]:offs[i + 1]]
@@ -257,6 +300,10 @@ def test_dropin_genome_gap_matches_reference_golden(golden_dir, tmp_path, name):
             dbl.dbl_list_free(lst)
     L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dpL)))
     L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dpR)))
+    if known:  # back to no IIT for the other tests of this process
+        L.Dynprog_setup(1, None, None, -1, -1, None, None, None, 0, None, None, None, None, None)
+        iitlib.iitdbl_free.argtypes = [ctypes.c_void_p]
+        iitlib.iitdbl_free(iit)
     L.Dynprog_term()
 
 

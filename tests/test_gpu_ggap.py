@@ -65,7 +65,14 @@ def run_gpu(blocks, b):
     return res, trc, pairs, npairs
 
 
-@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap", "gmap_her2_ggap"])
+GOLDEN = ["ggap_chr17", "gmap_synth_ggap", "gmap_her2_ggap",
+          # a splicing IIT (reference iit_store) given to Dynprog_setup: site-level and
+          # intron-level, novel splicing on and off (dynprog.c:3375-3697, :4084-4101)
+          "ggap_known_sites", "ggap_known_sites_novel", "ggap_known_introns",
+          "ggap_known_introns_novel"]
+
+
+@pytest.mark.parametrize("name", GOLDEN)
 def test_gpu_ggap_matches_reference_golden(golden_dir, name):
     z = load(golden_dir, name)
     ctx = Context(z["blocks"])
@@ -94,6 +101,28 @@ def test_gpu_ggap_matches_oracle_mix(seed):
         assert np.sum(listed & (L1 >= lo) & (L1 < hi)) > 20, (lo, hi)
     assert np.sum(listed & (b.windows["use_probabilities_p"] == 1)) > 100
     assert np.sum(ores["bridge_ok"] == 0) > 0 and np.sum(trc["status"] == 1) > 0
+
+
+@pytest.mark.parametrize("site_level,novel", [(True, False), (True, True), (False, False),
+                                              (False, True)])
+def test_gpu_ggap_known_sites_matches_oracle_mix(site_level, novel):
+    """Known-site modes in every storage class (rows <= 31, <= 63, striped)."""
+    g, b = W.ggap_windows(W.synthetic_genome(2_000_000, seed=21, n_rate=0.002), 1500, seed=21)
+    blocks = W.pack_genome(g)
+    O.setup(blocks)
+    ores0, _, _, _ = O.run_ggap_batch(b.windows, b.query, b.query_uc)
+    sites = W.SpliceSiteSet(W.known_site_intervals(b.windows, ores0, np.random.default_rng(5),
+                                                   site_level))
+    w, q, u = W.with_known_sites(b.windows, b.query, b.query_uc, sites, novel)
+    ctx = Context(blocks)
+    res, trc, ops, off = ctx.ggap_run(w, q, u)
+    pairs, npairs = ctx.ggap_all_pairs(w, q, u, res, trc, ops, off)
+    ores, opairs, ooff, onp = O.run_ggap_batch(w, q, u)
+    oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
+    compare(w, res, trc, pairs, npairs, ores, oflat, onp, "known %d %d" % (site_level, novel))
+    assert np.sum(ores["returned_null"] == 0) > 200
+    L1 = w["length1"]
+    assert np.sum((ores["returned_null"] == 0) & (L1 >= 64)) > 5
 
 
 @pytest.mark.parametrize("prob", [False, True])

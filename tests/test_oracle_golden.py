@@ -46,7 +46,11 @@ def test_dp_oracle_matches_reference(golden_dir, name):
     assert goff[-1] == got.size
 
 
-@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap", "gmap_her2_ggap"])
+GGAP_SETS = ["ggap_chr17", "gmap_synth_ggap", "gmap_her2_ggap", "ggap_known_sites",
+             "ggap_known_sites_novel", "ggap_known_introns", "ggap_known_introns_novel"]
+
+
+@pytest.mark.parametrize("name", GGAP_SETS)
 def test_ggap_oracle_matches_reference(golden_dir, name):
     z = load(golden_dir, name)
     O.setup(z["blocks"])
