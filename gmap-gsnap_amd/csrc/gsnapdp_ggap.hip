@@ -446,7 +446,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
     const PD lp = (PD)(region + G.oProbL);
     const PD rp = (PD)(region + G.oProbR);
     const P bnd = region + G.oBnd;
-    const bool probmode = w.use_probabilities_p != 0;
+    // the constrained known-intron mode precedes (and ignores) probability mode (:3552)
+    const bool probmode = w.use_probabilities_p != 0 && w.known_mode != GSNAPDP_KNOWN_INTRONS;
     // known splice sites (a splicing IIT, dynprog.c:3375-3550): the caller's
     // record follows the query rows (include/gsnapdp.h, gsnapdp_ggap_window)
     const int km = act ? w.known_mode : GSNAPDP_KNOWN_NONE;
