@@ -576,7 +576,7 @@ def main() -> None:
             from gsnapdp import pinned_copy, pinned_empty
             m = 100_000
             hw, hq = pinned_copy(batch.windows[:m]), pinned_copy(batch.query[:m * stride])
-            hoff = op_offsets(hw)
+            hoff = pinned_copy(op_offsets(hw))
             hres, hops = pinned_empty(m, RESULT), pinned_empty(int(hoff[-1]) + 1, np.uint32)
             ctx.run(hw, hq, hq, out=(hres, hops, hoff))
             reps = 10
@@ -586,8 +586,8 @@ def main() -> None:
             host_ms = 1000.0 * (time.perf_counter() - t0) / reps
             out["pcie_inclusive"] = {"value": round(m / (host_ms * 1e-3), 1), "unit": "reads/s",
                                      "ms_per_batch": round(host_ms, 4), "reads": m,
-                                     "entry": "gsnapdp_run_host (page-locked host buffers in and out; "
-                                              "compacted op streams D2H)"}
+                                     "entry": "gsnapdp_run_host (page-locked host buffers in and out, "
+                                              "one buffer for query and query_uc; compacted op streams D2H)"}
             if not args.no_c4:
                 out["c4"] = measure_c4(genome, args.c4_windows, 20, args.warmup, dev, not args.no_cpu)
             if not args.no_c5:

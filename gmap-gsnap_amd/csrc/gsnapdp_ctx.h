@@ -81,6 +81,12 @@ struct gsnapdp_ctx {
   // host round trips (gsnapdp_run_host): one at a time per context
   std::mutex host_mu;
   void* h_small = nullptr;          // pinned: the compaction header
+  void* h_in = nullptr;             // pinned: a small batch's inputs, packed for one H2D copy
+  size_t h_in_cap = 0;
+  char* d_mx_stage = nullptr;       // gsnapdp_maxent_host: positions in, probabilities out
+  size_t mx_cap = 0;
+  void* h_mx = nullptr;             // pinned: its packed inputs / outputs
+  size_t h_mx_cap = 0;
   std::vector<uint32_t> h_comp;     // compacted ops on their way to op_offsets
 };
 

@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <utility>
 #include <mutex>
@@ -50,15 +51,8 @@ struct State {
   int nsplicesites = 0;
   unsigned *trieoffsets_obs = nullptr, *triecontents_obs = nullptr;
   unsigned *trieoffsets_max = nullptr, *triecontents_max = nullptr;
-  std::vector<char> q, qu;
-  std::vector<uint32_t> ops;
-  std::vector<gsnapdp_pair> pairs;
-  // GPU launches per entry-point family, reported at exit under
-  // $GSNAPDP_DROPIN_STATS (shows a host program really ran its DP here)
-  unsigned long ncalls[6] = {0, 0, 0, 0, 0, 0};
 };
 State g;
-enum { CALL_GAP, CALL_SJ, CALL_GGAP, CALL_CGAP, CALL_MICRO, CALL_MAXENT };
 
 
 [[noreturn]] void fatal(const std::string& msg) {
@@ -109,87 +103,307 @@ void ensure_tables() {
   g.tables = true;
 }
 
-// One window through the GPU; pushes its pairs (final list order) into the
-// pool, last pair first, so the list head is the first pair.
-// ---- gap windows from concurrent callers, combined into batches
-// gmap / gsnap call Dynprog_single_gap / end5 / end3 synchronously from each
-// worker thread.  A caller queues its window; whichever caller finds no batch
-// in flight becomes the leader, takes every queued window, runs them as one
-// gsnapdp_run_host batch and wakes their owners, which expand their own op
-// streams into their own Pairpools.  One thread alone sees one-window batches.
-struct GapReq {
-  gsnapdp_window w;  // qpos relative to q / qu below
-  std::vector<char> q, qu;
-  int64_t cap = 0;
-  gsnapdp_result r;
-  std::vector<uint32_t> ops;
+// ---- windows from concurrent callers, combined into batches
+// gmap / gsnap call the Dynprog_* / Maxent_hr_* entry points synchronously
+// from each worker thread (gmap -t N).  A caller queues its request (one
+// window of any family, or one MaxEnt position); whichever caller finds no
+// batch in flight becomes the leader, takes every queued request, runs one
+// batch per family through the batched C-ABI (page-locked staging) and wakes
+// the owners, which expand their own op streams into their own Pairpools.
+// No global lock is held across a GPU round trip; one thread alone sees
+// batches of one.
+enum Fam { F_GAP, F_GGAP, F_CGAP, F_SJ, F_MICRO, F_MAXENT, F_N };
+
+struct Req {
+  int fam;
   bool done = false;
+  std::vector<char> q, qu;  // this window's query bytes; positions in w are relative to them
+  int64_t cap = 0;          // op capacity
+  std::vector<uint32_t> ops;
+  explicit Req(int f) : fam(f) {}
+};
+struct GapReq : Req {
+  gsnapdp_window w;
+  gsnapdp_result r;
+  GapReq() : Req(F_GAP) {}
+};
+struct GgapReq : Req {
+  gsnapdp_ggap_window w;
+  gsnapdp_ggap_result r;
+  gsnapdp_ggap_trace t;
+  GgapReq() : Req(F_GGAP) {}
+};
+struct CgapReq : Req {
+  gsnapdp_cgap_window w;
+  gsnapdp_cgap_result r;
+  CgapReq() : Req(F_CGAP) {}
+};
+struct SjReq : Req {
+  gsnapdp_sj_window w;
+  gsnapdp_result r;
+  SjReq() : Req(F_SJ) {}
+};
+struct MicroReq : Req {
+  gsnapdp_micro_window w;
+  gsnapdp_micro_result r;
+  MicroReq() : Req(F_MICRO) {}
+};
+struct MaxReq : Req {
+  uint8_t model;
+  unsigned pos, chroffset;
+  double out = 0.0;
+  MaxReq() : Req(F_MAXENT) {}
 };
 
-struct GapCombiner {
+// Page-locked host arrays of the leader's batches (gsnapdp_host_alloc), grown
+// geometrically and kept for the life of the process.
+template <class T>
+struct Pinned {
+  T* p = nullptr;
+  size_t cap = 0;
+  T* get(size_t n) {
+    if (n > cap) {
+      if (p) gsnapdp_host_free(p);
+      cap = n + n / 2 + 64;
+      p = (T*)gsnapdp_host_alloc(cap * sizeof(T));
+      if (!p) fatal(std::string("page-locked staging: ") + gsnapdp_last_error());
+    }
+    return p;
+  }
+};
+
+struct Batcher {
   std::mutex m;
   std::condition_variable cv;
-  std::vector<GapReq*> pending;
+  std::vector<Req*> pending;
   bool busy = false;
-  std::vector<gsnapdp_window> W;
-  std::vector<char> Q, QU;
-  std::vector<gsnapdp_result> R;
-  std::vector<uint32_t> OPS;
-  std::vector<int64_t> OFF;
-  unsigned long batches = 0, maxbatch = 0;
+  unsigned long batches[F_N] = {}, maxbatch[F_N] = {}, windows[F_N] = {};
+  double gpu_s[F_N] = {};  // leader time in each family's batched round trip
+  // leader-only staging
+  Pinned<char> Q, QU;
+  Pinned<int64_t> OFF;
+  Pinned<uint32_t> OPS;
+  Pinned<unsigned char> W, R, T;
 };
-GapCombiner gcomb;
+Batcher gb;
 
 struct StatsAtExit {
   ~StatsAtExit() {
     if (!getenv("GSNAPDP_DROPIN_STATS")) return;
-    fprintf(stderr,
-            "gsnapdp_dropin: GPU calls: gap %lu, splicejunction %lu, genome_gap %lu, cdna_gap %lu, "
-            "microexon %lu, maxent %lu; gap batches %lu (largest %lu)\n",
-            g.ncalls[CALL_GAP], g.ncalls[CALL_SJ], g.ncalls[CALL_GGAP], g.ncalls[CALL_CGAP],
-            g.ncalls[CALL_MICRO], g.ncalls[CALL_MAXENT], gcomb.batches, gcomb.maxbatch);
+    static const char* names[F_N] = {"gap", "genome_gap", "cdna_gap", "splicejunction", "microexon",
+                                     "maxent"};
+    fprintf(stderr, "gsnapdp_dropin:");
+    for (int f = 0; f < F_N; f++)
+      fprintf(stderr, " %s %lu in %lu batches (largest %lu, %.3f s);", names[f], gb.windows[f],
+              gb.batches[f], gb.maxbatch[f], gb.gpu_s[f]);
+    fprintf(stderr, "\n");
   }
 } stats_at_exit;
 
-// the leader, without gcomb.m held: one batch over the taken requests
-void run_gap_batch(gsnapdp_ctx* c, const std::vector<GapReq*>& b) {
-  GapCombiner& G = gcomb;
-  const size_t n = b.size();
+// Concatenates the requests' query bytes and op ranges into the staging
+// arrays; returns each request's query offset.
+template <class X>
+std::vector<size_t> pack(const std::vector<X*>& b, size_t* qbytes) {
   size_t qn = 0;
-  for (const GapReq* x : b) qn += x->q.size();
-  G.W.resize(n);
-  G.R.resize(n);
-  G.OFF.assign(n + 1, 0);
-  G.Q.resize(qn);
-  G.QU.resize(qn);
-  size_t qo = 0;
-  for (size_t i = 0; i < n; i++) {
-    const GapReq* x = b[i];
-    G.W[i] = x->w;
-    G.W[i].qpos = x->w.qpos + (uint32_t)qo;
-    memcpy(G.Q.data() + qo, x->q.data(), x->q.size());
-    memcpy(G.QU.data() + qo, x->qu.data(), x->qu.size());
-    qo += x->q.size();
-    G.OFF[i + 1] = G.OFF[i] + x->cap;
+  for (const X* x : b) qn += x->q.size();
+  char* Q = gb.Q.get(qn + 8);
+  char* QU = gb.QU.get(qn + 8);
+  int64_t* OFF = gb.OFF.get(b.size() + 1);
+  std::vector<size_t> qo(b.size());
+  size_t o = 0;
+  OFF[0] = 0;
+  for (size_t i = 0; i < b.size(); i++) {
+    memcpy(Q + o, b[i]->q.data(), b[i]->q.size());
+    memcpy(QU + o, b[i]->qu.data(), b[i]->qu.size());
+    qo[i] = o;
+    o += b[i]->q.size();
+    OFF[i + 1] = OFF[i] + b[i]->cap;
   }
-  G.OPS.assign((size_t)G.OFF[n] + 1, 0u);
-  if (gsnapdp_run_host(c, G.W.data(), (int)n, G.Q.data(), G.QU.data(), G.Q.size(), G.R.data(),
-                       G.OPS.data(), G.OFF.data()))
-    fatal(std::string("gsnapdp_run_host: ") + gsnapdp_last_error());
-  for (size_t i = 0; i < n; i++) {
-    b[i]->r = G.R[i];
-    b[i]->ops.assign(G.OPS.begin() + G.OFF[i], G.OPS.begin() + G.OFF[i + 1]);
+  gb.OPS.get((size_t)OFF[b.size()] + 1);
+  *qbytes = o;
+  return qo;
+}
+template <class X>
+void unpack_ops(const std::vector<X*>& b) {
+  const int64_t* OFF = gb.OFF.p;
+  for (size_t i = 0; i < b.size(); i++) b[i]->ops.assign(gb.OPS.p + OFF[i], gb.OPS.p + OFF[i + 1]);
+}
+template <class Win>
+Win* windows_of(size_t n) { return (Win*)gb.W.get(n * sizeof(Win)); }
+template <class Res>
+Res* results_of(size_t n) { return (Res*)gb.R.get(n * sizeof(Res)); }
+
+void check(int rc, const char* what) {
+  if (rc) fatal(std::string(what) + ": " + gsnapdp_last_error());
+}
+
+// the leader, without gb.m held: one batch per family
+void run_family(gsnapdp_ctx* c, int fam, std::vector<Req*>& reqs) {
+  const size_t n = reqs.size();
+  size_t qb = 0;
+  switch (fam) {
+    case F_GAP: {
+      std::vector<GapReq*> b;
+      for (Req* r : reqs) b.push_back((GapReq*)r);
+      const std::vector<size_t> qo = pack(b, &qb);
+      gsnapdp_window* W = windows_of<gsnapdp_window>(n);
+      gsnapdp_result* R = results_of<gsnapdp_result>(n);
+      for (size_t i = 0; i < n; i++) {
+        W[i] = b[i]->w;
+        W[i].qpos += (uint32_t)qo[i];
+      }
+      check(gsnapdp_run_host(c, W, (int)n, gb.Q.p, gb.QU.p, qb, R, gb.OPS.p, gb.OFF.p), "gsnapdp_run_host");
+      for (size_t i = 0; i < n; i++) b[i]->r = R[i];
+      unpack_ops(b);
+      break;
+    }
+    case F_GGAP: {
+      std::vector<GgapReq*> b;
+      for (Req* r : reqs) b.push_back((GgapReq*)r);
+      const std::vector<size_t> qo = pack(b, &qb);
+      gsnapdp_ggap_window* W = windows_of<gsnapdp_ggap_window>(n);
+      gsnapdp_ggap_result* R = results_of<gsnapdp_ggap_result>(n);
+      gsnapdp_ggap_trace* T = (gsnapdp_ggap_trace*)gb.T.get(n * sizeof(gsnapdp_ggap_trace));
+      for (size_t i = 0; i < n; i++) {
+        W[i] = b[i]->w;
+        W[i].qpos += (uint32_t)qo[i];
+      }
+      check(gsnapdp_ggap_run_host(c, W, (int)n, gb.Q.p, gb.QU.p, qb, R, T, gb.OPS.p, gb.OFF.p),
+            "gsnapdp_ggap_run_host");
+      for (size_t i = 0; i < n; i++) {
+        b[i]->r = R[i];
+        b[i]->t = T[i];
+      }
+      unpack_ops(b);
+      break;
+    }
+    case F_CGAP: {
+      std::vector<CgapReq*> b;
+      for (Req* r : reqs) b.push_back((CgapReq*)r);
+      const std::vector<size_t> qo = pack(b, &qb);
+      gsnapdp_cgap_window* W = windows_of<gsnapdp_cgap_window>(n);
+      gsnapdp_cgap_result* R = results_of<gsnapdp_cgap_result>(n);
+      for (size_t i = 0; i < n; i++) {
+        W[i] = b[i]->w;
+        W[i].qposL += (uint32_t)qo[i];
+        W[i].qposR += (uint32_t)qo[i];
+      }
+      check(gsnapdp_cgap_run_host(c, W, (int)n, gb.Q.p, gb.QU.p, qb, R, gb.OPS.p, gb.OFF.p),
+            "gsnapdp_cgap_run_host");
+      for (size_t i = 0; i < n; i++) b[i]->r = R[i];
+      unpack_ops(b);
+      break;
+    }
+    case F_SJ: {
+      std::vector<SjReq*> b;
+      for (Req* r : reqs) b.push_back((SjReq*)r);
+      const std::vector<size_t> qo = pack(b, &qb);
+      gsnapdp_sj_window* W = windows_of<gsnapdp_sj_window>(n);
+      gsnapdp_result* R = results_of<gsnapdp_result>(n);
+      for (size_t i = 0; i < n; i++) {
+        W[i] = b[i]->w;
+        W[i].qpos += (uint32_t)qo[i];
+        W[i].spos += (uint32_t)qo[i];
+      }
+      check(gsnapdp_sj_run_host(c, W, (int)n, gb.Q.p, gb.QU.p, qb, R, gb.OPS.p, gb.OFF.p),
+            "gsnapdp_sj_run_host");
+      for (size_t i = 0; i < n; i++) b[i]->r = R[i];
+      unpack_ops(b);
+      break;
+    }
+    case F_MICRO: {
+      std::vector<MicroReq*> b;
+      for (Req* r : reqs) b.push_back((MicroReq*)r);
+      const std::vector<size_t> qo = pack(b, &qb);
+      gsnapdp_micro_window* W = windows_of<gsnapdp_micro_window>(n);
+      gsnapdp_micro_result* R = results_of<gsnapdp_micro_result>(n);
+      for (size_t i = 0; i < n; i++) {
+        W[i] = b[i]->w;
+        W[i].qpos += (uint32_t)qo[i];
+        W[i].ppos += (uint32_t)qo[i];
+      }
+      check(gsnapdp_micro_run_host(c, W, (int)n, gb.Q.p, gb.QU.p, qb, R), "gsnapdp_micro_run_host");
+      for (size_t i = 0; i < n; i++) b[i]->r = R[i];
+      break;
+    }
+    case F_MAXENT: {
+      uint8_t* M = (uint8_t*)gb.Q.get(n + 8);
+      unsigned* P = (unsigned*)gb.W.get(2 * n * sizeof(unsigned));
+      double* O = (double*)gb.R.get(n * sizeof(double));
+      for (size_t i = 0; i < n; i++) {
+        const MaxReq* x = (const MaxReq*)reqs[i];
+        M[i] = x->model;
+        P[i] = x->pos;
+        P[n + i] = x->chroffset;
+      }
+      check(gsnapdp_maxent_host(c, M, P, P + n, O, (int)n), "maxent");
+      for (size_t i = 0; i < n; i++) ((MaxReq*)reqs[i])->out = O[i];
+      break;
+    }
   }
+}
+
+// Queue `r` and return once its batch ran (this thread may be the leader).
+void submit(gsnapdp_ctx* c, Req* r) {
+  std::unique_lock<std::mutex> lk(gb.m);
+  gb.pending.push_back(r);
+  while (!r->done) {
+    if (!gb.busy) {
+      gb.busy = true;
+      std::vector<Req*> batch;
+      batch.swap(gb.pending);
+      lk.unlock();
+      std::vector<Req*> fam[F_N];
+      for (Req* x : batch) fam[x->fam].push_back(x);
+      double dt[F_N] = {};
+      for (int f = 0; f < F_N; f++) {
+        if (fam[f].empty()) continue;
+        const auto t0 = std::chrono::steady_clock::now();
+        run_family(c, f, fam[f]);
+        dt[f] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      }
+      lk.lock();
+      for (int f = 0; f < F_N; f++) {
+        if (fam[f].empty()) continue;
+        gb.gpu_s[f] += dt[f];
+        gb.batches[f]++;
+        gb.windows[f] += fam[f].size();
+        if (fam[f].size() > gb.maxbatch[f]) gb.maxbatch[f] = fam[f].size();
+      }
+      for (Req* x : batch) x->done = true;
+      gb.busy = false;
+      gb.cv.notify_all();
+    } else {
+      gb.cv.wait(lk);
+    }
+  }
+}
+
+gsnapdp_ctx* shared_ctx(bool tables) {
+  std::lock_guard<std::mutex> lock(g.mu);
+  if (tables) ensure_tables();
+  return ctx();
+}
+
+// pushes a pair list (final order) into the caller's pool, last pair first
+// (gapp bit 1: a knownp gapholder)
+gsnapdp_List_T push_pairs(const gsnapdp_pair* pairs, int n, gsnapdp_Pairpool_T pool) {
+  gsnapdp_List_T list = nullptr;
+  for (int i = n - 1; i >= 0; i--) {
+    const gsnapdp_pair& p = pairs[i];
+    if (p.gapp)
+      list = Pairpool_push_gapholder(list, pool, p.queryjump, p.genomejump, (p.gapp & 2) ? 1 : 0);
+    else
+      list = Pairpool_push(list, pool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome,
+                           p.dynprogindex);
+  }
+  return list;
 }
 
 gsnapdp_List_T run_one(gsnapdp_window& w, const char* seq, const char* sequc, bool rev,
                        gsnapdp_Pairpool_T pool, int* dynprogindex, int* finalscore,
                        int* nmatches, int* nmismatches, int* nopens, int* nindels) {
-  gsnapdp_ctx* c;
-  {
-    std::lock_guard<std::mutex> lock(g.mu);
-    c = ctx();
-  }
+  gsnapdp_ctx* c = shared_ctx(false);
   GapReq req;
   const int L1 = w.length1 > 0 ? w.length1 : 0;
   // query bytes the reference may read: sequence1[0..L1) or revsequence1[-(L1-1)..0],
@@ -204,28 +418,7 @@ gsnapdp_List_T run_one(gsnapdp_window& w, const char* seq, const char* sequc, bo
   w.qpos = rev ? (uint32_t)(L1 > 0 ? L1 - 1 : 0) : 0u;
   req.w = w;
   req.cap = (int64_t)L1 + (w.length2 > 0 ? w.length2 : 0) + 2;
-  {
-    std::unique_lock<std::mutex> lk(gcomb.m);
-    gcomb.pending.push_back(&req);
-    while (!req.done) {
-      if (!gcomb.busy) {
-        gcomb.busy = true;
-        std::vector<GapReq*> batch;
-        batch.swap(gcomb.pending);
-        lk.unlock();
-        run_gap_batch(c, batch);
-        lk.lock();
-        for (GapReq* x : batch) x->done = true;
-        g.ncalls[CALL_GAP] += batch.size();
-        gcomb.batches++;
-        if (batch.size() > gcomb.maxbatch) gcomb.maxbatch = batch.size();
-        gcomb.busy = false;
-        gcomb.cv.notify_all();
-      } else {
-        gcomb.cv.wait(lk);
-      }
-    }
-  }
+  submit(c, &req);
   const gsnapdp_result& r = req.r;
   if (r.status == gsnapdp::ST_UNSUPPORTED)
     fatal("window outside the reference's domain (the reference aborts here)");
@@ -242,16 +435,7 @@ gsnapdp_List_T run_one(gsnapdp_window& w, const char* seq, const char* sequc, bo
   *nmismatches = r.nmismatches;
   *nopens = r.nopens;
   *nindels = r.nindels;
-  gsnapdp_List_T list = nullptr;
-  for (int i = n - 1; i >= 0; i--) {
-    const gsnapdp_pair& p = pairs[(size_t)i];
-    if (p.gapp)
-      list = Pairpool_push_gapholder(list, pool, p.queryjump, p.genomejump, (p.gapp & 2) ? 1 : 0);
-    else
-      list = Pairpool_push(list, pool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome,
-                           p.dynprogindex);
-  }
-  return list;
+  return push_pairs(pairs.data(), n, pool);
 }
 
 gsnapdp_window base_window(int kind, int length1, int length2, int offset1, int offset2,
@@ -283,14 +467,13 @@ gsnapdp_window base_window(int kind, int length1, int length2, int offset1, int 
 }
 
 double maxent_one(int model, unsigned splice_pos, unsigned chroffset) {
-  std::lock_guard<std::mutex> lock(g.mu);
-  ensure_tables();
-  const uint8_t m = (uint8_t)model;
-  double out = 0.0;
-  g.ncalls[CALL_MAXENT]++;
-  if (gsnapdp_maxent_host(ctx(), &m, &splice_pos, &chroffset, &out, 1))
-    fatal(std::string("maxent: ") + gsnapdp_last_error());
-  return out;
+  gsnapdp_ctx* c = shared_ctx(true);
+  MaxReq req;
+  req.model = (uint8_t)model;
+  req.pos = splice_pos;
+  req.chroffset = chroffset;
+  submit(c, &req);
+  return req.out;
 }
 
 // Genome_fill_buffer_blocks_noterm (genome.c:10090) on the host copy of the
@@ -339,11 +522,11 @@ gsnapdp_List_T run_sj(int kind, const char* seq1, const char* seq1uc, const char
                       int extraband_end, double defect_rate, const Dynprog* dp,
                       gsnapdp_Pairpool_T pool, int* dynprogindex, int* finalscore, int* nmatches,
                       int* nmismatches, int* nopens, int* nindels) {
-  std::lock_guard<std::mutex> lock(g.mu);
-  gsnapdp_ctx* c = ctx();
+  gsnapdp_ctx* c = shared_ctx(false);
+  SjReq req;
+  gsnapdp_sj_window& w = req.w;
   const bool rev = kind == GSNAPDP_END5_GAP;
   const int L1 = length1 > 0 ? length1 : 0, L2 = length2 > 0 ? length2 : 0;
-  gsnapdp_sj_window w;
   memset(&w, 0, sizeof(w));
   w.kind = kind;
   w.length1 = length1;
@@ -363,23 +546,20 @@ gsnapdp_List_T run_sj(int kind, const char* seq1, const char* seq1uc, const char
   // query rows then the junction, each with 4 bytes of slack
   const bool run = L1 > 0 && L2 > 0 && L1 <= dp->maxlength1 && L2 <= dp->maxlength2;
   const size_t sbase = (size_t)L1 + 4;
-  g.q.assign(sbase + L2 + 8, 0);
-  g.qu.assign(sbase + L2 + 8, 0);
+  req.q.assign((sbase + L2 + 8 + 3) & ~(size_t)3, 0);
+  req.qu.assign(req.q.size(), 0);
   if (run) {
-    memcpy(g.q.data(), rev ? seq1 - (L1 - 1) : seq1, (size_t)L1);
-    memcpy(g.qu.data(), rev ? seq1uc - (L1 - 1) : seq1uc, (size_t)L1);
-    memcpy(g.q.data() + sbase, rev ? seq2 - (L2 - 1) : seq2, (size_t)L2);
-    memcpy(g.qu.data() + sbase, rev ? seq2uc - (L2 - 1) : seq2uc, (size_t)L2);
+    memcpy(req.q.data(), rev ? seq1 - (L1 - 1) : seq1, (size_t)L1);
+    memcpy(req.qu.data(), rev ? seq1uc - (L1 - 1) : seq1uc, (size_t)L1);
+    memcpy(req.q.data() + sbase, rev ? seq2 - (L2 - 1) : seq2, (size_t)L2);
+    memcpy(req.qu.data() + sbase, rev ? seq2uc - (L2 - 1) : seq2uc, (size_t)L2);
   }
   w.qpos = rev ? (uint32_t)(L1 > 0 ? L1 - 1 : 0) : 0u;
   w.spos = (uint32_t)(rev ? sbase + (L2 > 0 ? L2 - 1 : 0) : sbase);
   const int64_t cap = (int64_t)L1 + L2 + 2;
-  const int64_t off[2] = {0, cap};
-  g.ops.assign((size_t)cap + 1, 0u);
-  gsnapdp_result r;
-  g.ncalls[CALL_SJ]++;
-  if (gsnapdp_sj_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, g.ops.data(), off))
-    fatal(std::string("gsnapdp_sj_run_host: ") + gsnapdp_last_error());
+  req.cap = cap;
+  submit(c, &req);
+  const gsnapdp_result& r = req.r;
   if (r.status == gsnapdp::ST_UNSUPPORTED) fatal("splice junction outside A C G T N");
   if (r.status == gsnapdp::ST_OPS_OVERFLOW) fatal("op stream overflow");
   *nmatches = r.nmatches;
@@ -389,20 +569,12 @@ gsnapdp_List_T run_sj(int kind, const char* seq1, const char* seq1uc, const char
   *finalscore = r.finalscore;
   *dynprogindex = r.reserved;
   if (r.status == gsnapdp::ST_EARLY) return nullptr;
-  g.pairs.resize((size_t)cap + 8);
-  const int n = gsnapdp_sj_expand(c, &w, &r, g.ops.data(), g.q.data(), g.qu.data(), g.pairs.data(),
-                                  (int)g.pairs.size());
-  if (n < 0 || n > (int)g.pairs.size()) fatal("gsnapdp_sj_expand failed");
-  gsnapdp_List_T list = nullptr;
-  for (int i = n - 1; i >= 0; i--) {
-    const gsnapdp_pair& p = g.pairs[(size_t)i];
-    if (p.gapp)
-      list = Pairpool_push_gapholder(list, pool, p.queryjump, p.genomejump, (p.gapp & 2) ? 1 : 0);
-    else
-      list = Pairpool_push(list, pool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome,
-                           p.dynprogindex);
-  }
-  return list;
+  thread_local std::vector<gsnapdp_pair> pairs;
+  pairs.resize((size_t)cap + 8);
+  const int n = gsnapdp_sj_expand(c, &w, &r, req.ops.data(), req.q.data(), req.qu.data(), pairs.data(),
+                                  (int)pairs.size());
+  if (n < 0 || n > (int)pairs.size()) fatal("gsnapdp_sj_expand failed");
+  return push_pairs(pairs.data(), n, pool);
 }
 
 // The head of the reference's Pair_T (pairdef.h:9-23) and List_T (listdef.h):
@@ -557,12 +729,14 @@ SolveFn solver(bool end5) {
 extern "C" {
 
 int Gsnapdp_dropin_stats(unsigned long* out, int n) {
-  const unsigned long v[8] = {g.ncalls[CALL_GAP], g.ncalls[CALL_SJ], g.ncalls[CALL_GGAP],
-                              g.ncalls[CALL_CGAP], g.ncalls[CALL_MICRO], g.ncalls[CALL_MAXENT],
-                              gcomb.batches, gcomb.maxbatch};
-  std::lock_guard<std::mutex> lock(gcomb.m);
-  for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
-  return 8;
+  static const int order[6] = {F_GAP, F_SJ, F_GGAP, F_CGAP, F_MICRO, F_MAXENT};
+  std::lock_guard<std::mutex> lock(gb.m);
+  for (int i = 0; i < 6; i++) {
+    if (i < n) out[i] = gb.windows[order[i]];
+    if (6 + i < n) out[6 + i] = gb.batches[order[i]];
+    if (12 + i < n) out[12 + i] = gb.maxbatch[order[i]];
+  }
+  return 18;
 }
 
 int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device) {
@@ -729,14 +903,13 @@ gsnapdp_List_T Dynprog_genome_gap(
     gsnapdp_Pairpool_T pairpool, int extraband_paired, double defect_rate, int maxpeelback,
     gsnapdp_bool halfp, gsnapdp_bool finalp, gsnapdp_bool use_probabilities_p,
     int score_threshold, gsnapdp_bool splicingp) {  // dynprog.c:4798-5061
-  std::lock_guard<std::mutex> lock(g.mu);
   if (use_genomicseg_p && (use_probabilities_p || finalp))
     fatal("Dynprog_genome_gap: genomic-segment MaxEnt probabilities are not served");
-  gsnapdp_ctx* c = ctx();
-  if (use_probabilities_p || finalp) ensure_tables();
+  gsnapdp_ctx* c = shared_ctx(use_probabilities_p || finalp);
   const Dynprog* dL = (const Dynprog*)dynprogL;
   const Dynprog* dR = (const Dynprog*)dynprogR;
-  gsnapdp_ggap_window w;
+  GgapReq req;
+  gsnapdp_ggap_window& w = req.w;
   memset(&w, 0, sizeof(w));
   w.length1 = length1;
   w.length2L = length2L;
@@ -767,27 +940,25 @@ gsnapdp_List_T Dynprog_genome_gap(
   w.use_probabilities_p = use_probabilities_p ? 1 : 0;
   w.splicingp = splicingp ? 1 : 0;
   const int L1 = length1 > 0 ? length1 : 0;
-  g.q.assign((size_t)L1 + 8, 0);
-  g.qu.assign((size_t)L1 + 8, 0);
+  req.q.assign((size_t)L1 + 8, 0);
+  req.qu.assign((size_t)L1 + 8, 0);
   if (L1 > 0) {
-    memcpy(g.q.data(), sequence1, (size_t)L1);
-    memcpy(g.qu.data(), sequenceuc1, (size_t)L1);
+    memcpy(req.q.data(), sequence1, (size_t)L1);
+    memcpy(req.qu.data(), sequenceuc1, (size_t)L1);
   }
   if (g.splicing_iit && L1 > 1 && length2L > 0 && length2R > 0 && !too_long) {
     // the known-site record follows the query rows (include/gsnapdp.h)
-    w.known_mode = known_site_record(g.q, (size_t)L1, chrnum, chrpos, genomiclength,
+    w.known_mode = known_site_record(req.q, (size_t)L1, chrnum, chrpos, genomiclength,
                                      offset2L, revoffset2R, length2L, length2R, cdna_direction,
                                      watsonp != 0);
-    g.qu.resize(g.q.size(), 0);
   }
+  req.q.resize((req.q.size() + 3) & ~(size_t)3, 0);
+  req.qu.resize(req.q.size(), 0);
   const int64_t cap = 2 * (int64_t)L1 + (length2L > 0 ? length2L : 0) + (length2R > 0 ? length2R : 0) + 4;
-  const int64_t off[2] = {0, cap};
-  g.ops.assign((size_t)cap + 1, 0u);
-  gsnapdp_ggap_result r;
-  gsnapdp_ggap_trace t;
-  g.ncalls[CALL_GGAP]++;
-  if (gsnapdp_ggap_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, &t, g.ops.data(), off))
-    fatal(std::string("gsnapdp_ggap_run_host: ") + gsnapdp_last_error());
+  req.cap = cap;
+  submit(c, &req);
+  const gsnapdp_ggap_result& r = req.r;
+  const gsnapdp_ggap_trace& t = req.t;
   if (t.status == gsnapdp::ST_UNSUPPORTED)
     fatal("genome-gap window outside the reference's domain (the reference aborts or reads past its matrices)");
   if (t.status == gsnapdp::ST_OPS_OVERFLOW) fatal("op stream overflow");
@@ -823,20 +994,12 @@ gsnapdp_List_T Dynprog_genome_gap(
   *nopens = r.nopens;
   *nindels = r.nindels;
   if (r.returned_null) return nullptr;  // only the gapholder (:5050-5053)
-  g.pairs.resize((size_t)cap + 8);
-  const int n = gsnapdp_ggap_expand(c, &w, &r, &t, g.ops.data(), g.q.data(), g.qu.data(),
-                                    g.pairs.data(), (int)g.pairs.size());
-  if (n < 0 || n > (int)g.pairs.size()) fatal("gsnapdp_ggap_expand failed");
-  gsnapdp_List_T list = nullptr;
-  for (int i = n - 1; i >= 0; i--) {
-    const gsnapdp_pair& p = g.pairs[(size_t)i];
-    if (p.gapp)
-      list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump, /*knownp*/ 0);
-    else
-      list = Pairpool_push(list, pairpool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome,
-                           p.dynprogindex);
-  }
-  return list;
+  thread_local std::vector<gsnapdp_pair> pairs;
+  pairs.resize((size_t)cap + 8);
+  const int n = gsnapdp_ggap_expand(c, &w, &r, &t, req.ops.data(), req.q.data(), req.qu.data(),
+                                    pairs.data(), (int)pairs.size());
+  if (n < 0 || n > (int)pairs.size()) fatal("gsnapdp_ggap_expand failed");
+  return push_pairs(pairs.data(), n, pairpool);
 }
 
 gsnapdp_List_T Dynprog_cdna_gap(
@@ -848,11 +1011,11 @@ gsnapdp_List_T Dynprog_cdna_gap(
     gsnapdp_Genomicpos_T genomiclength, int cdna_direction, gsnapdp_bool watsonp,
     gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool, int extraband_paired,
     double defect_rate) {  // dynprog.c:4578-4793
-  std::lock_guard<std::mutex> lock(g.mu);
-  gsnapdp_ctx* c = ctx();
+  gsnapdp_ctx* c = shared_ctx(false);
   const Dynprog* dL = (const Dynprog*)dynprogL;
   const Dynprog* dR = (const Dynprog*)dynprogR;
-  gsnapdp_cgap_window w;
+  CgapReq req;
+  gsnapdp_cgap_window& w = req.w;
   memset(&w, 0, sizeof(w));
   w.length1L = length1L;
   w.length1R = length1R;
@@ -880,23 +1043,20 @@ gsnapdp_List_T Dynprog_cdna_gap(
   // revoffset1R - offset1L
   const int nL = length1L > 0 ? length1L : 0, nR = length1R > 0 ? length1R : 0;
   const int span = revoffset1R - offset1L + 1 > nL ? revoffset1R - offset1L + 1 : nL;
-  g.q.assign((size_t)span + nR + 8, 0);
-  g.qu.assign(g.q.size(), 0);
+  req.q.assign(((size_t)span + nR + 8 + 3) & ~(size_t)3, 0);
+  req.qu.assign(req.q.size(), 0);
   if (length2 > 1) {
-    memcpy(g.q.data(), sequence1L, (size_t)span);
-    memcpy(g.qu.data(), sequenceuc1L, (size_t)span);
-    memcpy(g.q.data() + span, revsequence1R - (nR - 1), (size_t)nR);
-    memcpy(g.qu.data() + span, revsequenceuc1R - (nR - 1), (size_t)nR);
+    memcpy(req.q.data(), sequence1L, (size_t)span);
+    memcpy(req.qu.data(), sequenceuc1L, (size_t)span);
+    memcpy(req.q.data() + span, revsequence1R - (nR - 1), (size_t)nR);
+    memcpy(req.qu.data() + span, revsequenceuc1R - (nR - 1), (size_t)nR);
   }
   w.qposL = 0;
   w.qposR = (uint32_t)(span + nR - 1);
   const int64_t cap = (int64_t)nL + nR + 2 * (int64_t)(length2 > 0 ? length2 : 0) + 4;
-  const int64_t off[2] = {0, cap};
-  g.ops.assign((size_t)cap + 1, 0u);
-  gsnapdp_cgap_result r;
-  g.ncalls[CALL_CGAP]++;
-  if (gsnapdp_cgap_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r, g.ops.data(), off))
-    fatal(std::string("gsnapdp_cgap_run_host: ") + gsnapdp_last_error());
+  req.cap = cap;
+  submit(c, &req);
+  const gsnapdp_cgap_result& r = req.r;
   if (r.status == gsnapdp::ST_UNSUPPORTED)
     fatal("cDNA-gap window outside the reference's domain (the reference aborts here)");
   if (r.status == gsnapdp::ST_OPS_OVERFLOW) fatal("op stream overflow");
@@ -907,20 +1067,12 @@ gsnapdp_List_T Dynprog_cdna_gap(
   if (r.status != gsnapdp::ST_OK) return nullptr;
   if (r.incompletep) *incompletep = 1;  // only ever set to true (:4756)
   if (r.returned_null) return nullptr;
-  g.pairs.resize((size_t)cap + 32);
-  const int n = gsnapdp_cgap_expand(c, &w, &r, g.ops.data(), g.q.data(), g.qu.data(), sequence2,
-                                    g.pairs.data(), (int)g.pairs.size());
-  if (n < 0 || n > (int)g.pairs.size()) fatal("gsnapdp_cgap_expand failed");
-  gsnapdp_List_T list = nullptr;
-  for (int i = n - 1; i >= 0; i--) {
-    const gsnapdp_pair& p = g.pairs[(size_t)i];
-    if (p.gapp)
-      list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump, /*knownp*/ 0);
-    else
-      list = Pairpool_push(list, pairpool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome,
-                           p.dynprogindex);
-  }
-  return list;
+  thread_local std::vector<gsnapdp_pair> pairs;
+  pairs.resize((size_t)cap + 32);
+  const int n = gsnapdp_cgap_expand(c, &w, &r, req.ops.data(), req.q.data(), req.qu.data(), sequence2,
+                                    pairs.data(), (int)pairs.size());
+  if (n < 0 || n > (int)pairs.size()) fatal("gsnapdp_cgap_expand failed");
+  return push_pairs(pairs.data(), n, pairpool);
 }
 
 gsnapdp_List_T Dynprog_end5_splicejunction(
@@ -1002,21 +1154,20 @@ gsnapdp_List_T Dynprog_microexon_int(
     abort();
   }
   if (use_genomicseg_p) fatal("Dynprog_microexon_int with use_genomicseg_p (no caller passes it)");
-  std::lock_guard<std::mutex> lock(g.mu);
-  ensure_tables();
-  gsnapdp_ctx* c = ctx();
+  gsnapdp_ctx* c = shared_ctx(true);
+  MicroReq req;
   const int L1 = length1 > 0 ? length1 : 0;
   // sequence1 / sequenceuc1 for the search, queryseq / queryuc from offset1 for the pairs
-  g.q.assign(2 * (size_t)L1 + 16, 0);
-  g.qu.assign(2 * (size_t)L1 + 16, 0);
-  const size_t pbase = (size_t)L1 + 8;
+  const size_t pbase = ((size_t)L1 + 8 + 3) & ~(size_t)3;
+  req.q.assign(pbase + (((size_t)L1 + 8 + 3) & ~(size_t)3), 0);
+  req.qu.assign(req.q.size(), 0);
   if (L1 > 0) {
-    memcpy(g.q.data(), sequence1, (size_t)L1);
-    memcpy(g.qu.data(), sequenceuc1, (size_t)L1);
-    memcpy(g.q.data() + pbase, queryseq + offset1, (size_t)L1);
-    memcpy(g.qu.data() + pbase, queryuc + offset1, (size_t)L1);
+    memcpy(req.q.data(), sequence1, (size_t)L1);
+    memcpy(req.qu.data(), sequenceuc1, (size_t)L1);
+    memcpy(req.q.data() + pbase, queryseq + offset1, (size_t)L1);
+    memcpy(req.qu.data() + pbase, queryuc + offset1, (size_t)L1);
   }
-  gsnapdp_micro_window w;
+  gsnapdp_micro_window& w = req.w;
   memset(&w, 0, sizeof(w));
   w.length1 = length1;
   w.offset1 = offset1;
@@ -1032,23 +1183,22 @@ gsnapdp_List_T Dynprog_microexon_int(
   w.ppos = (uint32_t)pbase;
   w.defect_rate = defect_rate < 0.003 ? 0.001f : (defect_rate < 0.014 ? 0.01f : 0.5f);
   w.watsonp = watsonp ? 1 : 0;
-  gsnapdp_micro_result r;
-  g.ncalls[CALL_MICRO]++;
-  if (gsnapdp_micro_run_host(c, &w, 1, g.q.data(), g.qu.data(), g.q.size(), &r))
-    fatal(std::string("gsnapdp_micro_run_host: ") + gsnapdp_last_error());
+  submit(c, &req);
+  const gsnapdp_micro_result& r = req.r;
   if (r.status != 0) fatal("microexon window outside the reference's domain");
   *bestprob2 = r.bestprob2;
   *bestprob3 = r.bestprob3;
   *microintrontype = r.microintrontype;
   *dynprogindex = r.dynprogindex;
   if (!r.found) return nullptr;
-  g.pairs.resize((size_t)L1 + 4);
-  const int n = gsnapdp_micro_expand(c, &w, &r, g.q.data(), g.qu.data(), g.pairs.data(),
-                                     (int)g.pairs.size());
-  if (n <= 0 || n > (int)g.pairs.size()) fatal("gsnapdp_micro_expand failed");
+  thread_local std::vector<gsnapdp_pair> pairs;
+  pairs.resize((size_t)L1 + 4);
+  const int n = gsnapdp_micro_expand(c, &w, &r, req.q.data(), req.qu.data(), pairs.data(),
+                                     (int)pairs.size());
+  if (n <= 0 || n > (int)pairs.size()) fatal("gsnapdp_micro_expand failed");
   gsnapdp_List_T list = nullptr;
   for (int i = n - 1; i >= 0; i--) {
-    const gsnapdp_pair& p = g.pairs[(size_t)i];
+    const gsnapdp_pair& p = pairs[(size_t)i];
     if (p.gapp) {
       list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump, 0);
       ((RefPairHead*)((RefList*)list)->first)->comp = p.comp;  // gappair->comp = gapchar

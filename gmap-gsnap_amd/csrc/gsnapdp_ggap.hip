@@ -1453,7 +1453,9 @@ extern "C" int gsnapdp_sj_run_host(gsnapdp_ctx* ctx, const gsnapdp_sj_window* wi
   hipStream_t st = ctx->stream;
   HIPCHK(hipMemcpyAsync(dw, windows, (size_t)n * sizeof(gsnapdp_sj_window), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(dq, query, query_bytes, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
+  // a caller that passes one buffer for both (query already upper case) pays one copy
+  if (query_uc == query) du = dq;
+  else HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(doff, op_offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, st));
   if (gsnapdp_sj_run_device(ctx, dw, n, dq, du, dr, dops, doff, st)) return -1;
   HIPCHK(hipMemcpyAsync(results, dr, (size_t)n * sizeof(gsnapdp_result), hipMemcpyDeviceToHost, st));
@@ -1536,7 +1538,13 @@ extern "C" int gsnapdp_ggap_run_host(gsnapdp_ctx* ctx, const gsnapdp_ggap_window
   const size_t szt = al((size_t)n * sizeof(gsnapdp_ggap_trace));
   const size_t szo = al((nops + 1) * 4);
   const size_t szoff = al((size_t)(n + 1) * 8);
-  const size_t total = szw + 2 * szq + szr + szt + szo + szoff;
+  const bool alias = query_uc == query;  // one buffer for both (query already upper case): one copy
+  // inputs first (windows, query, query_uc, op offsets), then the outputs
+  const size_t in_bytes = szw + (alias ? 1 : 2) * szq + szoff;
+  const size_t total = in_bytes + szr + szt + szo;
+  const bool small = in_bytes <= ((size_t)1 << 20);  // one packed H2D copy (the per-call drop-in)
+  // one host round trip at a time per context (the staging buffers are shared)
+  std::lock_guard<std::mutex> host_lock(ctx->host_mu);
   {
     std::lock_guard<std::mutex> lock(ctx->mu);
     if (total > ctx->ggap_stage_cap) {
@@ -1545,20 +1553,36 @@ extern "C" int gsnapdp_ggap_run_host(gsnapdp_ctx* ctx, const gsnapdp_ggap_window
       HIPCHK(hipMalloc(&ctx->d_ggap_stage, total));
       ctx->ggap_stage_cap = total;
     }
+    if (small && in_bytes > ctx->h_in_cap) {
+      if (ctx->h_in) (void)hipHostFree(ctx->h_in);
+      ctx->h_in = nullptr;
+      HIPCHK(hipHostMalloc(&ctx->h_in, (size_t)1 << 20));
+      ctx->h_in_cap = (size_t)1 << 20;
+    }
   }
   char* b = (char*)ctx->d_ggap_stage;
+  const size_t o_q = szw, o_u = szw + szq, o_off = o_u + (alias ? 0 : szq);
   gsnapdp_ggap_window* dw = (gsnapdp_ggap_window*)b;
-  char* dq = b + szw;
-  char* du = dq + szq;
-  gsnapdp_ggap_result* dr = (gsnapdp_ggap_result*)(du + szq);
+  char* dq = b + o_q;
+  char* du = alias ? dq : b + o_u;
+  int64_t* doff = (int64_t*)(b + o_off);
+  gsnapdp_ggap_result* dr = (gsnapdp_ggap_result*)(b + in_bytes);
   gsnapdp_ggap_trace* dt = (gsnapdp_ggap_trace*)((char*)dr + szr);
   uint32_t* dops = (uint32_t*)((char*)dt + szt);
-  int64_t* doff = (int64_t*)((char*)dops + szo);
   hipStream_t st = ctx->stream;
-  HIPCHK(hipMemcpyAsync(dw, windows, (size_t)n * sizeof(gsnapdp_ggap_window), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(dq, query, query_bytes, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(doff, op_offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, st));
+  if (small) {
+    char* h = (char*)ctx->h_in;
+    memcpy(h, windows, (size_t)n * sizeof(gsnapdp_ggap_window));
+    memcpy(h + o_q, query, query_bytes);
+    if (!alias) memcpy(h + o_u, query_uc, query_bytes);
+    memcpy(h + o_off, op_offsets, (size_t)(n + 1) * 8);
+    HIPCHK(hipMemcpyAsync(b, h, o_off + (size_t)(n + 1) * 8, hipMemcpyHostToDevice, st));
+  } else {
+    HIPCHK(hipMemcpyAsync(dw, windows, (size_t)n * sizeof(gsnapdp_ggap_window), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dq, query, query_bytes, hipMemcpyHostToDevice, st));
+    if (!alias) HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(doff, op_offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, st));
+  }
   if (gsnapdp_ggap_run_device(ctx, dw, n, dq, du, dr, dt, dops, doff, st)) return -1;
   HIPCHK(hipMemcpyAsync(results, dr, (size_t)n * sizeof(gsnapdp_ggap_result), hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(traces, dt, (size_t)n * sizeof(gsnapdp_ggap_trace), hipMemcpyDeviceToHost, st));
@@ -1636,7 +1660,9 @@ extern "C" int gsnapdp_cgap_run_host(gsnapdp_ctx* ctx, const gsnapdp_cgap_window
   hipStream_t st = ctx->stream;
   HIPCHK(hipMemcpyAsync(dw, windows, (size_t)n * sizeof(gsnapdp_cgap_window), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(dq, query, query_bytes, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
+  // a caller that passes one buffer for both (query already upper case) pays one copy
+  if (query_uc == query) du = dq;
+  else HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(doff, op_offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, st));
   if (gsnapdp_cgap_run_device(ctx, dw, n, dq, du, dr, dops, doff, st)) return -1;
   HIPCHK(hipMemcpyAsync(results, dr, (size_t)n * sizeof(gsnapdp_cgap_result), hipMemcpyDeviceToHost, st));

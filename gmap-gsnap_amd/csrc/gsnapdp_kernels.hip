@@ -981,6 +981,9 @@ extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   (void)hipFree(ctx->d_stage);
   (void)hipFree(ctx->d_csum);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
+  if (ctx->h_in) (void)hipHostFree(ctx->h_in);
+  if (ctx->h_mx) (void)hipHostFree(ctx->h_mx);
+  (void)hipFree(ctx->d_mx_stage);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1078,7 +1081,13 @@ extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows,
   const size_t szo = (nops + 1) * 4;
   const size_t szoff = (size_t)(n + 1) * 8;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t total = al(szw) + 2 * al(szq) + al(szr) + 2 * al(szo) + al(szoff) + 256;
+  const bool alias = query_uc == query;  // one buffer for both (query already upper case): one copy
+  // inputs first (windows, query, query_uc, op offsets), then the outputs
+  const size_t in_bytes = al(szw) + (alias ? 1 : 2) * al(szq) + al(szoff);
+  const size_t total = in_bytes + al(szr) + 2 * al(szo) + 256;
+  // a small batch (the per-call drop-in's) is one packed H2D copy, the kernels,
+  // and its results and uncompacted ops back in the same synchronisation
+  const bool small = in_bytes <= ((size_t)1 << 20) && szo <= ((size_t)1 << 20);
   {
     std::lock_guard<std::mutex> lock(ctx->mu);
     if (total > ctx->stage_cap) {
@@ -1088,20 +1097,40 @@ extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows,
       ctx->stage_cap = total;
     }
     if (!ctx->h_small) HIPCHK(hipHostMalloc(&ctx->h_small, 256));
+    if (small && in_bytes > ctx->h_in_cap) {
+      if (ctx->h_in) (void)hipHostFree(ctx->h_in);
+      ctx->h_in = nullptr;
+      HIPCHK(hipHostMalloc(&ctx->h_in, (size_t)1 << 20));
+      ctx->h_in_cap = (size_t)1 << 20;
+    }
   }
   char* base = (char*)ctx->d_stage;
+  const size_t o_q = al(szw), o_u = o_q + al(szq), o_off = o_u + (alias ? 0 : al(szq));
   gsnapdp_window* dw = (gsnapdp_window*)base;
-  char* dq = base + al(szw);
-  char* du = dq + al(szq);
-  gsnapdp_result* dr = (gsnapdp_result*)(du + al(szq));
+  char* dq = base + o_q;
+  char* du = alias ? dq : base + o_u;
+  int64_t* doff = (int64_t*)(base + o_off);
+  gsnapdp_result* dr = (gsnapdp_result*)(base + in_bytes);
   uint32_t* dops = (uint32_t*)((char*)dr + al(szr));
   uint32_t* dcomp = (uint32_t*)((char*)dops + al(szo));
-  int64_t* doff = (int64_t*)((char*)dcomp + al(szo));
-  int64_t* dhdr = (int64_t*)((char*)doff + al(szoff));
+  int64_t* dhdr = (int64_t*)((char*)dcomp + al(szo));
   hipStream_t st = ctx->stream;
+  if (small) {
+    char* h = (char*)ctx->h_in;
+    memcpy(h, windows, szw);
+    memcpy(h + o_q, query, query_bytes);
+    if (!alias) memcpy(h + o_u, query_uc, query_bytes);
+    memcpy(h + o_off, op_offsets, szoff);
+    HIPCHK(hipMemcpyAsync(base, h, o_off + szoff, hipMemcpyHostToDevice, st));
+    if (gsnapdp_run_device(ctx, dw, n, dq, du, dr, dops, doff, st)) return -1;
+    HIPCHK(hipMemcpyAsync(results, dr, szr, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(ops, dops, nops * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));  // the pinned staging is reused by the next call
+    return 0;
+  }
   HIPCHK(hipMemcpyAsync(dw, windows, szw, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(dq, query, query_bytes, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
+  if (!alias) HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(doff, op_offsets, szoff, hipMemcpyHostToDevice, st));
   if (gsnapdp_run_device(ctx, dw, n, dq, du, dr, dops, doff, st)) return -1;
   // only the ops each window wrote come back: compacted on the device, then
@@ -1215,25 +1244,42 @@ extern "C" int gsnapdp_maxent_host(gsnapdp_ctx* ctx, const uint8_t* model, const
   if (!ctx) return -1;
   if (n <= 0) return 0;
   HIPCHK(hipSetDevice(ctx->device));
-  uint8_t* dm;
-  uint32_t *dp, *dc;
-  double* dout;
-  HIPCHK(hipMalloc(&dm, (size_t)n));
-  HIPCHK(hipMalloc(&dp, (size_t)n * 4));
-  HIPCHK(hipMalloc(&dc, (size_t)n * 4));
-  HIPCHK(hipMalloc(&dout, (size_t)n * 8));
-  HIPCHK(hipMemcpy(dm, model, (size_t)n, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(dp, pos, (size_t)n * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(dc, chroff, (size_t)n * 4, hipMemcpyHostToDevice));
-  int rc = gsnapdp_maxent_device(ctx, dm, dp, dc, dout, n, ctx->stream);
-  if (rc == 0) {
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    HIPCHK(hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost));
+  // persistent device staging and one packed page-locked H2D copy:
+  // positions | chromosome offsets | models, then the probabilities
+  const size_t o_c = (size_t)n * 4, o_m = 2 * o_c, o_out = (o_m + n + 7) & ~(size_t)7;
+  const size_t total = o_out + (size_t)n * 8;
+  std::lock_guard<std::mutex> host_lock(ctx->host_mu);
+  {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (total > ctx->mx_cap) {
+      (void)hipFree(ctx->d_mx_stage);
+      ctx->d_mx_stage = nullptr;
+      const size_t cap = total + total / 2 + 4096;
+      HIPCHK(hipMalloc(&ctx->d_mx_stage, cap));
+      ctx->mx_cap = cap;
+    }
+    if (total > ctx->h_mx_cap) {
+      if (ctx->h_mx) (void)hipHostFree(ctx->h_mx);
+      ctx->h_mx = nullptr;
+      const size_t cap = total + total / 2 + 4096;
+      HIPCHK(hipHostMalloc(&ctx->h_mx, cap));
+      ctx->h_mx_cap = cap;
+    }
   }
-  (void)hipFree(dm);
-  (void)hipFree(dp);
-  (void)hipFree(dc);
-  (void)hipFree(dout);
+  char* h = (char*)ctx->h_mx;
+  char* d = ctx->d_mx_stage;
+  memcpy(h, pos, (size_t)n * 4);
+  memcpy(h + o_c, chroff, (size_t)n * 4);
+  memcpy(h + o_m, model, (size_t)n);
+  hipStream_t st = ctx->stream;
+  HIPCHK(hipMemcpyAsync(d, h, o_m + n, hipMemcpyHostToDevice, st));
+  int rc = gsnapdp_maxent_device(ctx, (const uint8_t*)(d + o_m), (const uint32_t*)d,
+                                 (const uint32_t*)(d + o_c), (double*)(d + o_out), n, st);
+  if (rc == 0) {
+    HIPCHK(hipMemcpyAsync(h + o_out, d + o_out, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    memcpy(out, h + o_out, (size_t)n * 8);
+  }
   return rc;
 }
 

@@ -369,7 +369,9 @@ extern "C" int gsnapdp_micro_run_host(gsnapdp_ctx* ctx, const gsnapdp_micro_wind
   hipStream_t st = ctx->stream;
   HIPCHK(hipMemcpyAsync(dw, windows, (size_t)n * sizeof(gsnapdp_micro_window), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(dq, query, query_bytes, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
+  // a caller that passes one buffer for both (query already upper case) pays one copy
+  if (query_uc == query) du = dq;
+  else HIPCHK(hipMemcpyAsync(du, query_uc, query_bytes, hipMemcpyHostToDevice, st));
   if (gsnapdp_micro_run_device(ctx, dw, n, dq, du, dr, st)) return -1;
   HIPCHK(hipMemcpyAsync(results, dr, (size_t)n * sizeof(gsnapdp_micro_result), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));

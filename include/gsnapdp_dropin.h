@@ -231,10 +231,11 @@ double Maxent_hr_antiacceptor_prob(gsnapdp_Genomicpos_T splice_pos,
  * any padding), `device` = HIP device index. */
 int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device);
 
-/* Counters of this process's GPU work: out[0..5] = windows run for the gap,
- * splice-junction, genome-gap, cDNA-gap, microexon and MaxEnt entry points;
- * out[6] = gap batches, out[7] = the largest (concurrent Dynprog_single_gap /
- * end5 / end3 callers are combined into one batch).  Returns 8. */
+/* Counters of this process's GPU work, per entry-point family in the order
+ * gap (single / end5 / end3), splice junction, genome gap, cDNA gap, microexon,
+ * MaxEnt: out[0..5] = windows (or positions) run, out[6..11] = GPU batches,
+ * out[12..17] = the largest batch (concurrent callers of any entry point are
+ * combined into shared batches).  Writes min(n, 18) values; returns 18. */
 int Gsnapdp_dropin_stats(unsigned long* out, int n);
 
 /* ---- genome_hr subset (the reference's genome_hr.c is a missing blob;

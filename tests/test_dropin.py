@@ -104,7 +104,7 @@ GAP_ARGS = ([ctypes.c_void_p] * 7 + [ctypes.c_char_p] * 4 + [ctypes.c_int] * 4 +
 @pytest.mark.parametrize("name,limit", [("dp_chr17_mix", 400), ("dp_synth_cmet", 150), ("gmap_synth_gap", 100000),
                                         ("gmap_her2_gap", 100000)])
 def test_dropin_gap_fillers_match_reference_golden(golden_dir, tmp_path, name, limit):
-    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    z = dict(np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False))
     dbl = load_double(tmp_path)
     L = ctypes.CDLL(DROPIN)
     L.Dynprog_new.restype = ctypes.c_void_p
@@ -163,7 +163,7 @@ def test_dropin_gap_fillers_match_reference_golden(golden_dir, tmp_path, name, l
 
 @pytest.mark.gpu
 def test_dropin_maxent_matches_reference_golden(golden_dir, tmp_path):
-    z = np.load(os.path.join(golden_dir, "maxent_chr17.npz"), allow_pickle=False)
+    z = dict(np.load(os.path.join(golden_dir, "maxent_chr17.npz"), allow_pickle=False))
     load_double(tmp_path)
     L = ctypes.CDLL(DROPIN)
     blocks = np.ascontiguousarray(z["blocks"])
@@ -225,11 +225,11 @@ def test_dropin_genome_gap_matches_reference_golden(golden_dir, tmp_path, name):
     ggap_known_* sets give Dynprog_setup a splicing IIT (an IIT test double over
     the intervals the reference's iit_store wrote), from which the shim builds
     each window's known-site record with the IIT queries bridge_intron_gap makes."""
-    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    z = dict(np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False))
     dbl = load_double(tmp_path)
     L = ctypes.CDLL(DROPIN)
     L.Dynprog_setup.argtypes = SETUP_ARGS
-    known = "intervals" in z.files
+    known = "intervals" in z
     crosstable = (ctypes.c_int * 2)(-1, 0)  # chrnum 1 -> the IIT's one division
     if known:
         iitlib, iit, (dtype, atype) = load_iit_double(tmp_path, z)
@@ -316,7 +316,7 @@ def test_dropin_cdna_gap_matches_reference_golden(golden_dir, tmp_path):
     """Dynprog_cdna_gap called like traverse_cdna_gap (stage3.c:5604) on the
     reference's golden windows: out-parameters exactly where it writes them,
     and the list (INSERT_PAIRS included)."""
-    z = np.load(os.path.join(golden_dir, "cgap_chr17.npz"), allow_pickle=False)
+    z = dict(np.load(os.path.join(golden_dir, "cgap_chr17.npz"), allow_pickle=False))
     dbl = load_double(tmp_path)
     L = ctypes.CDLL(DROPIN)
     L.Dynprog_new.restype = ctypes.c_void_p
@@ -371,7 +371,7 @@ def test_dropin_make_splicejunction_matches_reference_golden(golden_dir, tmp_pat
     """Dynprog_make_splicejunction_5/3 (dynprog.c:6061, 6149): the distal part
     from the genome, reverse-complemented on the minus strand.  Host staging,
     no GPU needed."""
-    z = np.load(os.path.join(golden_dir, "mksj_chr17.npz"), allow_pickle=False)
+    z = dict(np.load(os.path.join(golden_dir, "mksj_chr17.npz"), allow_pickle=False))
     load_double(tmp_path)
     L = ctypes.CDLL(DROPIN)
     blocks = np.ascontiguousarray(z["blocks"])
@@ -404,7 +404,7 @@ def test_dropin_splicejunction_matches_reference_golden(golden_dir, tmp_path):
     """Dynprog_end5/3_splicejunction called like Splicetrie_solve_end5/3
     (splicetrie.c:352, 640): every out-parameter and the list, known
     gapholder included."""
-    z = np.load(os.path.join(golden_dir, "sj_chr17.npz"), allow_pickle=False)
+    z = dict(np.load(os.path.join(golden_dir, "sj_chr17.npz"), allow_pickle=False))
     dbl = load_double(tmp_path)
     L = ctypes.CDLL(DROPIN)
     L.Dynprog_new.restype = ctypes.c_void_p
@@ -461,7 +461,7 @@ def test_dropin_microexon_matches_reference_golden(golden_dir, tmp_path):
     """Dynprog_microexon_int called like traverse_single_gap (stage3.c:5915):
     out-parameters (probabilities bit for bit) and the list, including the
     gapholders' comp written in place."""
-    z = np.load(os.path.join(golden_dir, "micro_chr17.npz"), allow_pickle=False)
+    z = dict(np.load(os.path.join(golden_dir, "micro_chr17.npz"), allow_pickle=False))
     dbl = load_double(tmp_path)
     L = ctypes.CDLL(DROPIN)
     L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
@@ -513,7 +513,7 @@ def test_dropin_known_splicing_matches_reference_golden(golden_dir, tmp_path):
     reference's splicetrie.c by test_oracle_golden) calling back into the
     drop-in: every out-parameter, the list and its protection, against the
     reference run end to end (the golden vectors)."""
-    z = np.load(os.path.join(golden_dir, "known_chr17.npz"), allow_pickle=False)
+    z = dict(np.load(os.path.join(golden_dir, "known_chr17.npz"), allow_pickle=False))
     dbl = load_double(tmp_path)
     dbl.dbl_list_protected.argtypes = [ctypes.c_void_p]
     L = ctypes.CDLL(DROPIN, mode=ctypes.RTLD_GLOBAL)       # Dynprog_* for the splicetrie code
@@ -655,7 +655,7 @@ def test_dropin_concurrent_callers_are_batched(golden_dir, tmp_path):
     import threading
     import time
 
-    z = np.load(os.path.join(golden_dir, "gmap_synth_gap.npz"), allow_pickle=False)
+    z = dict(np.load(os.path.join(golden_dir, "gmap_synth_gap.npz"), allow_pickle=False))
     dbl = load_double(tmp_path)
     L = ctypes.CDLL(DROPIN)
     L.Dynprog_new.restype = ctypes.c_void_p
@@ -664,7 +664,7 @@ def test_dropin_concurrent_callers_are_batched(golden_dir, tmp_path):
     for f in ("Dynprog_single_gap", "Dynprog_end5_gap", "Dynprog_end3_gap"):
         getattr(L, f).restype = ctypes.c_void_p
         getattr(L, f).argtypes = GAP_ARGS + [ctypes.c_int, ctypes.c_ubyte]
-    stats = (ctypes.c_ulong * 8)()
+    stats = (ctypes.c_ulong * 18)()
     blocks = np.ascontiguousarray(z["blocks"])
     L.Dynprog_init(600, 10, 11, 10, 8, int(z["mode"]))
     L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
@@ -673,6 +673,7 @@ def test_dropin_concurrent_callers_are_batched(golden_dir, tmp_path):
     offs = np.zeros(len(z["npairs"]) + 1, dtype=np.int64)
     np.cumsum(z["npairs"], out=offs[1:])
     W = z["windows"]
+    NP, P = z["npairs"], z["pairs"]  # materialised once (an NpzFile re-reads on every access)
     want = np.stack([z[f] for f in ("dynprogindex", "finalscore", "nmatches", "nmismatches", "nopens",
                                     "nindels")], axis=1)
 
@@ -696,14 +697,14 @@ def test_dropin_concurrent_callers_are_batched(golden_dir, tmp_path):
             else:
                 lst = L.Dynprog_end3_gap(*common, int(w["endalign"]), 0)
             k = dbl.dbl_list_read(lst, out.ctypes.data, out.size)
-            if [x.value for x in ints] != want[i].tolist() or k != int(z["npairs"][i]) or \
-                    out[:k].tobytes() != z["pairs"][offs[i]:offs[i + 1]].tobytes():
+            if [x.value for x in ints] != want[i].tolist() or k != int(NP[i]) or \
+                    out[:k].tobytes() != P[offs[i]:offs[i + 1]].tobytes():
                 bad.append(i)
             dbl.dbl_list_free(lst)
         L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dp)))
 
     def run(nthreads):
-        L.Gsnapdp_dropin_stats(stats, 8)
+        L.Gsnapdp_dropin_stats(stats, 18)
         b0 = stats[6]
         bad = []
         ts = [threading.Thread(target=worker, args=(range(t, len(W), nthreads), bad)) for t in range(nthreads)]
@@ -713,13 +714,161 @@ def test_dropin_concurrent_callers_are_batched(golden_dir, tmp_path):
         for t in ts:
             t.join()
         el = time.perf_counter() - t0
-        L.Gsnapdp_dropin_stats(stats, 8)
+        L.Gsnapdp_dropin_stats(stats, 18)
         return el, stats[6] - b0, bad
 
     t1, b1, bad1 = run(1)
     t16, b16, bad16 = run(16)
     print("%d gmap gap windows: 1 thread %.3f s (%d batches), 16 threads %.3f s (%d batches, largest %d)"
-          % (len(W), t1, b1, t16, b16, stats[7]))
+          % (len(W), t1, b1, t16, b16, stats[12]))
     assert not bad1 and not bad16, (bad1[:5], bad16[:5])
-    assert b1 == len(W) and b16 < len(W) and stats[7] > 1
+    assert b1 == len(W) and b16 < len(W) and stats[12] > 1
+    L.Dynprog_term()
+
+
+@pytest.mark.gpu
+def test_dropin_mixed_families_concurrent_callers_are_batched(golden_dir, tmp_path):
+    """16 threads call Dynprog_single_gap / end5 / end3, Dynprog_genome_gap and
+    Maxent_hr_* at once, as gmap -t 16 workers do (stage3.c traverse_* and
+    score_introns): every family is combined into shared GPU batches, and every
+    result stays bit-exact (the gap windows gmap itself issued, gmap_synth_*;
+    MaxEnt positions on the same genome against the CPU restatement)."""
+    import threading
+
+    import oracle as O
+
+    # materialised once: an NpzFile re-reads (and decompresses) on every access
+    zg = dict(np.load(os.path.join(golden_dir, "gmap_synth_gap.npz"), allow_pickle=False))
+    zk = dict(np.load(os.path.join(golden_dir, "gmap_synth_ggap.npz"), allow_pickle=False))
+    assert np.array_equal(zg["blocks"], zk["blocks"])
+    dbl = load_double(tmp_path)
+    L = ctypes.CDLL(DROPIN)
+    L.Dynprog_new.restype = ctypes.c_void_p
+    L.Dynprog_new.argtypes = [ctypes.c_int] * 5
+    L.Dynprog_setup.argtypes = SETUP_ARGS
+    L.Gsnapdp_dropin_genome.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    for f in ("Dynprog_single_gap", "Dynprog_end5_gap", "Dynprog_end3_gap"):
+        getattr(L, f).restype = ctypes.c_void_p
+        getattr(L, f).argtypes = GAP_ARGS + [ctypes.c_int, ctypes.c_ubyte]
+    L.Dynprog_genome_gap.restype = ctypes.c_void_p
+    L.Dynprog_genome_gap.argtypes = GGAP_ARGS
+    names = ("Maxent_hr_donor_prob", "Maxent_hr_acceptor_prob", "Maxent_hr_antidonor_prob",
+             "Maxent_hr_antiacceptor_prob")
+    for f in names:
+        getattr(L, f).restype = ctypes.c_double
+        getattr(L, f).argtypes = [ctypes.c_uint, ctypes.c_uint]
+    blocks = np.ascontiguousarray(zg["blocks"])
+    L.Dynprog_init(600, 10, 11, 10, 8, 0)
+    L.Dynprog_setup(1, None, None, -1, -1, None, None, None, 0, None, None, None, None, None)
+    L.Maxent_hr_setup.argtypes = [ctypes.c_void_p]
+    L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
+    L.Maxent_hr_setup(blocks.ctypes.data)
+
+    gq, gqu = np.ascontiguousarray(zg["query"]), np.ascontiguousarray(zg["query_uc"])
+    goff = np.concatenate([[0], np.cumsum(zg["npairs"])])
+    gwant = np.stack([zg[f] for f in ("dynprogindex", "finalscore", "nmatches", "nmismatches", "nopens",
+                                      "nindels")], axis=1)
+    kq, kqu = np.ascontiguousarray(zk["query"]), np.ascontiguousarray(zk["query_uc"])
+    koff = np.concatenate([[0], np.cumsum(zk["npairs"])])
+    KW, KR = zk["windows"], zk["results"]
+    kidx = [i for i in range(len(KW)) if KW[i]["maxlength1"] == 611 and KW[i]["maxlength2"] == 2000]
+    rng = np.random.default_rng(17)
+    nm = 3000
+    model = rng.integers(0, 4, nm).astype(np.uint8)
+    glen = int((blocks.size - 4) // 3 * 32)
+    pos = rng.integers(0, glen - 64, nm).astype(np.uint32)
+    O.setup(blocks)
+    mwant = O.maxent(model, pos, np.zeros(nm, np.uint32))
+    tasks = [("gap", i) for i in range(len(zg["windows"]))] + [("ggap", i) for i in kidx] + \
+        [("maxent", i) for i in range(nm)]
+    order = rng.permutation(len(tasks))
+
+    def do_gap(dp, out, i):
+        w = zg["windows"][i]
+        ints = [ctypes.c_int(int(w["dynprogindex"]))] + [ctypes.c_int(0) for _ in range(5)]
+        common = [ctypes.byref(x) for x in ints] + [
+            dp, ctypes.c_char_p(gq.ctypes.data + int(w["qpos"])),
+            ctypes.c_char_p(gqu.ctypes.data + int(w["qpos"])), None, None, int(w["length1"]),
+            int(w["length2"]), int(w["offset1"]), int(w["offset2"]), int(w["chroffset"]),
+            int(w["chrhigh"]), int(w["chrpos"]), int(w["genomiclength"]), int(w["cdna_direction"]),
+            int(w["watsonp"]), int(w["jump_late_p"]), None, int(w["extraband"]), float(w["defect_rate"])]
+        kind = int(w["kind"])
+        if kind == SINGLE_GAP:
+            lst = L.Dynprog_single_gap(*common, 0, int(w["widebandp"]))
+        elif kind == END5_GAP:
+            lst = L.Dynprog_end5_gap(*common, int(w["endalign"]), 0)
+        else:
+            lst = L.Dynprog_end3_gap(*common, int(w["endalign"]), 0)
+        k = dbl.dbl_list_read(lst, out.ctypes.data, out.size) if lst else 0
+        ok = [x.value for x in ints] == gwant[i].tolist() and k == int(zg["npairs"][i]) and \
+            out[:k].tobytes() == zg["pairs"][goff[i]:goff[i + 1]].tobytes()
+        if lst:
+            dbl.dbl_list_free(lst)
+        return ok
+
+    def do_ggap(dpL, dpR, out, i):
+        w, r = KW[i], KR[i]
+        ints = [ctypes.c_int(int(w["dynprogindex"]))] + [ctypes.c_int(-77) for _ in range(3)]
+        probs = [ctypes.c_double(-1.0), ctypes.c_double(-1.0)]
+        counts = [ctypes.c_int(-77) for _ in range(6)]
+        args = ([ctypes.byref(x) for x in ints] + [ctypes.byref(x) for x in probs]
+                + [ctypes.byref(x) for x in counts]
+                + [dpL, dpR, ctypes.c_char_p(kq.ctypes.data + int(w["qpos"])),
+                   ctypes.c_char_p(kqu.ctypes.data + int(w["qpos"])), None, None, None, None]
+                + [int(w[f]) for f in ("length1", "length2L", "length2R", "offset1", "offset2L",
+                                       "revoffset2R")]
+                + [1] + [int(w[f]) for f in ("chroffset", "chrhigh", "chrpos", "genomiclength")]
+                + [None, 0, int(w["cdna_direction"]), int(w["watsonp"]), int(w["jump_late_p"]), None,
+                   int(w["extraband_paired"]), float(w["defect_rate"]), int(w["maxpeelback"]),
+                   int(w["halfp"]), int(w["finalp"]), int(w["use_probabilities_p"]),
+                   int(w["score_threshold"]), int(w["splicingp"])])
+        lst = L.Dynprog_genome_gap(*args)
+        k = dbl.dbl_list_read(lst, out.ctypes.data, out.size) if lst else 0
+        ok = ints[0].value == r["dynprogindex"] and ints[1].value == r["finalscore"] and \
+            [c.value for c in counts[:4]] == [int(r[f]) for f in ("nmatches", "nmismatches", "nopens",
+                                                                  "nindels")] and \
+            np.float64(probs[0].value).view(np.uint64) == np.float64(r["left_prob"]).view(np.uint64) and \
+            np.float64(probs[1].value).view(np.uint64) == np.float64(r["right_prob"]).view(np.uint64) and \
+            k == int(zk["npairs"][i]) and out[:k].tobytes() == zk["pairs"][koff[i]:koff[i + 1]].tobytes()
+        if lst:
+            dbl.dbl_list_free(lst)
+        return ok
+
+    def worker(idx, bad):
+        dp = L.Dynprog_new(600, 10, 11, 10, 8)
+        dpL = L.Dynprog_new(600, 10, 11, 10, 8)
+        dpR = L.Dynprog_new(600, 10, 11, 10, 8)
+        out = np.zeros(8192, dtype=REC)
+        for t in idx:
+            fam, i = tasks[order[t]]
+            if fam == "gap":
+                ok = do_gap(dp, out, i)
+            elif fam == "ggap":
+                ok = do_ggap(dpL, dpR, out, i)
+            else:
+                got = getattr(L, names[model[i]])(int(pos[i]), 0)
+                ok = np.float64(got).view(np.uint64) == mwant[i].view(np.uint64)
+            if not ok:
+                bad.append((fam, i))
+        for d in (dp, dpL, dpR):
+            L.Dynprog_free(ctypes.byref(ctypes.c_void_p(d)))
+
+    stats0 = (ctypes.c_ulong * 18)()
+    L.Gsnapdp_dropin_stats(stats0, 18)
+    bad = []
+    ts = [threading.Thread(target=worker, args=(range(t, len(tasks), 16), bad)) for t in range(16)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    stats = (ctypes.c_ulong * 18)()
+    L.Gsnapdp_dropin_stats(stats, 18)
+    d = [stats[k] - stats0[k] for k in range(12)]
+    print("mixed families, 16 threads: windows gap %d ggap %d maxent %d; batches gap %d ggap %d maxent %d; "
+          "largest gap %d ggap %d maxent %d" % (d[0], d[2], d[5], d[6], d[8], d[11], stats[12], stats[14],
+                                                 stats[17]))
+    assert not bad, bad[:10]
+    assert d[0] == len(zg["windows"]) and d[2] == len(kidx) and d[5] == nm
+    for fam in (0, 2, 5):  # every family ran in batches larger than one
+        assert d[6 + fam] < d[fam] and stats[12 + fam] > 1, fam
     L.Dynprog_term()
