@@ -781,20 +781,24 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   write_result(res + wi, w, L, finalscore, L1, L2, tal, ow);
 }
 
-// One wave-task of class (S, LPW, LOW): the 64/LPW windows perm[t*NG ..].
-// Not inlined, so each class gets its own register allocation; its pointers
-// carry their address spaces (global / LDS) so that the body still compiles
-// to global_* and ds_* accesses rather than flat ones.
+// This wave's wave-tasks of class (S, LPW, LOW): task t covers the 64/LPW
+// windows perm[t*NG ..]; the wave runs t = t0, t0 + stride, ... < t1.  Not
+// inlined, so each class gets its own register allocation (inlining the
+// classes into the kernel spills across them); called once per wave and
+// class rather than once per task, so the call's callee-saved VGPR saves and
+// restores (48 VGPRs to scratch, ~24 KB per call) are paid per wave, not per
+// task.  The pointers carry their address spaces (global / LDS) so that the
+// body still compiles to global_* and ds_* accesses rather than flat ones.
 #define AS_GLOBAL __attribute__((address_space(1)))
 #define AS_LDS __attribute__((address_space(3)))
 template <int S, int LPW, int LOW>
-__device__ __noinline__ void fill_task(int t, const AS_GLOBAL gsnapdp_window* Wn1,
-                                       const AS_GLOBAL int* perm1, const AS_GLOBAL char* q1,
-                                       const AS_GLOBAL char* qu1, const AS_GLOBAL uint32_t* blocks1,
-                                       uint64_t nwords, const AS_LDS uint32_t* sprof3,
-                                       AS_LDS uint32_t* ring3,
-                                       AS_GLOBAL uint32_t* D1, AS_GLOBAL gsnapdp_result* res1,
-                                       AS_GLOBAL uint32_t* ops1, const AS_GLOBAL int64_t* op_off1) {
+__device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLOBAL gsnapdp_window* Wn1,
+                                        const AS_GLOBAL int* perm1, const AS_GLOBAL char* q1,
+                                        const AS_GLOBAL char* qu1, const AS_GLOBAL uint32_t* blocks1,
+                                        uint64_t nwords, const AS_LDS uint32_t* sprof3,
+                                        AS_LDS uint32_t* ring3,
+                                        AS_GLOBAL uint32_t* D1, AS_GLOBAL gsnapdp_result* res1,
+                                        AS_GLOBAL uint32_t* ops1, const AS_GLOBAL int64_t* op_off1) {
   const gsnapdp_window* __restrict__ Wn = (const gsnapdp_window*)Wn1;
   const int* __restrict__ perm = (const int*)perm1;
   const char* __restrict__ q = (const char*)q1;
@@ -810,17 +814,19 @@ __device__ __noinline__ void fill_task(int t, const AS_GLOBAL gsnapdp_window* Wn
   const int lane = threadIdx.x & 63;
   uint8_t* M = (uint8_t*)(D + (size_t)(FAST_L2MAX + 4) * 64);
   const int g = lane / LPW;
-  const int wi0 = perm[(size_t)t * NG + g];
-  const int w0 = __builtin_amdgcn_readfirstlane(perm[(size_t)t * NG]);  // group 0: a real window
-  const bool active = wi0 >= 0;
-  const int wi = active ? wi0 : w0;  // idle groups shadow group 0 (reads only)
-  const int jl = __builtin_amdgcn_readfirstlane((int)Wn[w0].jump_late_p);
-  if (jl)
-    fill_group<S, LPW, LOW, 1>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, ring,
-                               res, ops, op_off);
-  else
-    fill_group<S, LPW, LOW, 0>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, ring,
-                               res, ops, op_off);
+  for (int t = t0; t < t1; t += stride) {
+    const int wi0 = perm[(size_t)t * NG + g];
+    const int w0 = __builtin_amdgcn_readfirstlane(perm[(size_t)t * NG]);  // group 0: a real window
+    const bool active = wi0 >= 0;
+    const int wi = active ? wi0 : w0;  // idle groups shadow group 0 (reads only)
+    const int jl = __builtin_amdgcn_readfirstlane((int)Wn[w0].jump_late_p);
+    if (jl)
+      fill_group<S, LPW, LOW, 1>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, ring,
+                                 res, ops, op_off);
+    else
+      fill_group<S, LPW, LOW, 0>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, ring,
+                                 res, ops, op_off);
+  }
 }
 
 // All register-band classes in one persistent launch: the wave-tasks of the
@@ -853,29 +859,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
 #pragma unroll
   for (int c = 0; c < NCLASS; c++)
     tfirst[c + 1] = tfirst[c] + (class_start[c + 1] - class_start[c]) / (64 / CLASS_LPW[c]);
-  for (int tau = gw; tau < tfirst[NCLASS]; tau += nw) {
-    int c = 0;
-#pragma unroll
-    for (int k = 1; k < NCLASS; k++) c += tau >= tfirst[k] ? 1 : 0;
-    const int t = class_start[c] / (64 / CLASS_LPW[c]) + (tau - tfirst[c]);
-    static_assert(NCLASS <= 8, "k_fill dispatches at most 8 classes");
-    switch (c) {
-#define FILL_CASE(C)                                                                            \
-  case C:                                                                                       \
-    if constexpr (C < NCLASS)                                                                   \
-      fill_task<CLASS_S[C % NCLASS], CLASS_LPW[C % NCLASS],                                     \
-                class_low(C % NCLASS)>(                                                       \
-          t, (const AS_GLOBAL gsnapdp_window*)Wn, (const AS_GLOBAL int*)perm,                   \
-          (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu, (const AS_GLOBAL uint32_t*)blocks, \
-          nwords, (const AS_LDS uint32_t*)sprof, (AS_LDS uint32_t*)ring, (AS_GLOBAL uint32_t*)D, \
-          (AS_GLOBAL gsnapdp_result*)res, (AS_GLOBAL uint32_t*)ops,                             \
-          (const AS_GLOBAL int64_t*)op_off);                                                    \
-    break;
-      FILL_CASE(0) FILL_CASE(1) FILL_CASE(2) FILL_CASE(3)
-      FILL_CASE(4) FILL_CASE(5) FILL_CASE(6) FILL_CASE(7)
-#undef FILL_CASE
-    }
+  // the wave takes global task indices tau = gw, gw + nw, ...; those of class c
+  // are its tasks t = base_c + (tau - tfirst[c]), visited class by class
+  static_assert(NCLASS <= 8, "k_fill dispatches at most 8 classes");
+#define FILL_CLASS(C)                                                                            \
+  if constexpr (C < NCLASS) {                                                                    \
+    const int lo = tfirst[C], hi = tfirst[C + 1];                                                \
+    const int tau0 = gw >= lo ? gw : gw + (lo - gw + nw - 1) / nw * nw;                          \
+    if (tau0 < hi) {                                                                             \
+      const int base = class_start[C] / (64 / CLASS_LPW[C]) - lo;                                \
+      fill_tasks<CLASS_S[C % NCLASS], CLASS_LPW[C % NCLASS], class_low(C % NCLASS)>(             \
+          base + tau0, base + hi, nw, (const AS_GLOBAL gsnapdp_window*)Wn,                        \
+          (const AS_GLOBAL int*)perm, (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu,        \
+          (const AS_GLOBAL uint32_t*)blocks, nwords, (const AS_LDS uint32_t*)sprof,               \
+          (AS_LDS uint32_t*)ring, (AS_GLOBAL uint32_t*)D, (AS_GLOBAL gsnapdp_result*)res,         \
+          (AS_GLOBAL uint32_t*)ops, (const AS_GLOBAL int64_t*)op_off);                            \
+    }                                                                                            \
   }
+  FILL_CLASS(0) FILL_CLASS(1) FILL_CLASS(2) FILL_CLASS(3)
+  FILL_CLASS(4) FILL_CLASS(5) FILL_CLASS(6) FILL_CLASS(7)
+#undef FILL_CLASS
 }
 
 // --------------------------------------------------------------- k_maxent
