@@ -101,7 +101,8 @@ def rocprof_kernel_ms(kernel: str, workload: str):
     for f in sorted(glob.glob(pat)):
         try:
             for row in csv.DictReader(open(f)):
-                if row.get("Name", "").split("(")[0].strip().endswith(kernel):
+                name = row.get("Name", "").replace("(anonymous namespace)::", "")
+                if name.split("(")[0].strip().endswith(kernel):
                     best = (float(row["AverageNs"]) / 1e6, os.path.basename(f))
         except (OSError, ValueError, KeyError):
             continue
