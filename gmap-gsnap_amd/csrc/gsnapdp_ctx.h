@@ -21,6 +21,11 @@ int gsnapdp__rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window*
                          const int64_t* d_op_offsets);
 // allocate the row-lane classes' global scratch on first use
 int gsnapdp__rows_pools(gsnapdp_ctx* ctx);
+// k_gband over the register-band lists of a genome-gap batch (gsnapdp_gband.hip)
+int gsnapdp__gband_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_ggap_window* d_windows,
+                          const int* lists, const int* counts, int list_cap, const char* d_query,
+                          const char* d_query_uc, gsnapdp_ggap_result* d_results,
+                          gsnapdp_ggap_trace* d_traces, uint32_t* d_ops, const int64_t* d_op_offsets);
 
 #define HIPCHK(x)                                                                        \
   do {                                                                                   \
@@ -66,9 +71,11 @@ struct gsnapdp_ctx {
   int ev_used[16] = {};
   // genome-gap batches (gsnapdp_ggap.hip)
   int ggap_cap = 0;
-  int* d_ggap_lists = nullptr;     // per-class window lists, 3 x ggap_cap
+  int* d_ggap_lists = nullptr;     // per-class window lists, GG_NLISTS x ggap_cap
   int* d_ggap_counts = nullptr;    // per-class counts
   uint32_t* d_ggap_pool = nullptr; // global scratch of the large-window path
+  uint32_t* d_gband_pool = nullptr; // per-wave scratch of the register-band path (k_gband)
+  int ggap_rowlane_only = 0;        // GSNAPDP_GGAP_ROWLANE=1: every window on k_ggap (A/B tests)
   size_t ggap_stage_cap = 0;
   void* d_ggap_stage = nullptr;
   // splice-junction end gaps (gsnapdp_sj_*)

@@ -29,6 +29,7 @@
 
 #include "gsnapdp_ctx.h"
 #include "gsnapdp_device.h"
+#include "gsnapdp_ggap.h"
 #include "gsnapdp_internal.h"
 
 using namespace gsnapdp;
@@ -38,17 +39,9 @@ using namespace gsnapdp;
 
 namespace {
 
-// dynprog.c:142-293, intron.h:10-29
-constexpr int SINGLE_OPEN = -10, SINGLE_EXTEND = -3, PAIRED_OPEN = -18, PAIRED_EXTEND = -3;
-constexpr int GCAG_INTRON = 15, ATAC_INTRON = 12, FINAL_GCAG_INTRON = 20, FINAL_ATAC_INTRON = 12;
-constexpr int LEFT_GT = 0x21, LEFT_GC = 0x10, LEFT_AT = 0x08, LEFT_CT = 0x06;
-constexpr int RIGHT_AG = 0x30, RIGHT_AC = 0x0C, RIGHT_GC = 0x02, RIGHT_AT = 0x01;
-constexpr int GTAG_FWD = 0x20, GCAG_FWD = 0x10, ATAC_FWD = 0x08;
-constexpr int GTAG_REV = 0x04, GCAG_REV = 0x02, ATAC_REV = 0x01;
-constexpr int BRIDGE_INIT = -100000;  // bestscore / bestscoreI start (:3302)
-
 // window classes of the batch
 enum { GG_SMALL = 0, GG_MID = 1, GG_BIG = 2, GG_NCLS = 3 };
+static_assert(GB_LIST0 == GG_NCLS && GG_NLISTS <= 16, "genome-gap lists (the counts buffer holds 16)");
 #ifndef GG_SMALL_WORDS_CFG
 #define GG_SMALL_WORDS_CFG 1280
 #endif
@@ -60,190 +53,6 @@ constexpr int GG_SMALL_BLOCKS = 160 * 1024 / (8 * GG_SMALL_WORDS * 4);  // block
 constexpr int GG_MID_WORDS = 4096;        // LDS words per window, RL = 64
 constexpr size_t GG_BIG_WORDS = (size_t)4 << 20;  // global words per wave of the large path
 constexpr int GG_BIG_WAVES = 32;
-
-__device__ inline bool ggap_needs_tables(const gsnapdp_ggap_window& w) {
-  return w.use_probabilities_p || w.finalp;
-}
-
-// Window geometry: widened fill bands (dynprog.c:1442-1454 with widebandp) and
-// the storage layout of one window (words): H|dirs of the left flank (L1 x WL),
-// of the right flank (L1 x WR), the column classes of both flanks (bytes), the
-// site probabilities (probability mode, doubles) and the stripe boundary row.
-struct GGeo {
-  int L1, L2L, L2R, eb;
-  int lbL, rbL, WL, lbR, rbR, WR;
-  int mt, open, ext, canon;
-  int oHR, oClsL, oClsR, oDiL, oDiR, oItab, oQ, oProbL, oProbR, oBnd, words;
-};
-
-__device__ __host__ inline void fill_bands(int L1, int L2, int eb, int& lb, int& rb) {
-  if (L2 >= L1) {
-    rb = L2 - L1 + eb;
-    lb = eb;
-  } else {
-    lb = L1 - L2 + eb;
-    rb = eb;
-  }
-}
-
-__device__ inline GGeo gg_geo(const gsnapdp_ggap_window& w) {
-  GGeo G;
-  G.L1 = w.length1;
-  G.L2L = w.length2L;
-  G.L2R = w.length2R;
-  G.eb = w.extraband_paired;
-  fill_bands(G.L1, G.L2L, G.eb, G.lbL, G.rbL);
-  fill_bands(G.L1, G.L2R, G.eb, G.lbR, G.rbR);
-  G.WL = G.lbL + G.rbL + 1;
-  G.WR = G.lbR + G.rbR + 1;
-  const double dr = (double)w.defect_rate;  // dynprog.c:4871-4886
-  G.mt = dr < 0.003 ? MT_HIGHQ : (dr < 0.014 ? MT_MEDQ : MT_LOWQ);
-  if (G.L1 > w.maxpeelback * 4) {  // :4888-4896
-    G.open = SINGLE_OPEN;
-    G.ext = SINGLE_EXTEND;
-  } else {
-    G.open = PAIRED_OPEN;
-    G.ext = PAIRED_EXTEND;
-  }
-  const int canon[3] = {10, 16, 22}, fcanon[3] = {30, 36, 42};  // :277-283
-  G.canon = !w.splicingp ? 0 : (w.finalp ? fcanon[G.mt] : canon[G.mt]);
-  const int l1 = G.L1 > 0 ? G.L1 : 0;
-  G.oHR = l1 * G.WL;
-  G.oClsL = G.oHR + l1 * G.WR;
-  G.oClsR = G.oClsL + (G.L2L + 2 + 3) / 4;
-  G.oDiL = G.oClsR + (G.L2R + 2 + 3) / 4;     // leftdi[0 .. L2L]   (bytes)
-  G.oDiR = G.oDiL + (G.L2L + 1 + 3) / 4;      // rightdi[0 .. L2R]  (bytes)
-  G.oItab = G.oDiR + (G.L2R + 1 + 3) / 4;     // intron score | type << 8 by leftdi & rightdi (64 x u16)
-  G.oQ = G.oItab + 32;                        // query | uppercase << 8 per query index (u16)
-  int o = G.oQ + (l1 + 1) / 2;
-  o = (o + 1) & ~1;
-  G.oProbL = o;
-  G.oProbR = o + 2 * G.L2L;
-  if (w.use_probabilities_p) o += 2 * (G.L2L + G.L2R);
-  G.oBnd = o;
-  G.words = o;
-  return G;
-}
-
-// intron_score (dynprog.c:3148-3192), non-PMAP
-__device__ inline int intron_score(int& introntype, int leftdi, int rightdi, int cdna_direction,
-                                   int canonical_reward, int finalp) {
-  const int t = leftdi & rightdi;
-  const int gcag = finalp ? FINAL_GCAG_INTRON : GCAG_INTRON;
-  const int atac = finalp ? FINAL_ATAC_INTRON : ATAC_INTRON;
-  introntype = t;
-  if (t == 0) return 0;
-  if (cdna_direction > 0) {
-    if (t == GTAG_FWD) return canonical_reward;
-    if (t == GCAG_FWD) return gcag;
-    if (t == ATAC_FWD) return atac;
-  } else if (cdna_direction < 0) {
-    if (t == GTAG_REV) return canonical_reward;
-    if (t == GCAG_REV) return gcag;
-    if (t == ATAC_REV) return atac;
-  } else {
-    if (t == GTAG_FWD || t == GTAG_REV) return canonical_reward;
-    if (t == GCAG_FWD || t == GCAG_REV) return gcag;
-    if (t == ATAC_FWD || t == ATAC_REV) return atac;
-  }
-  introntype = 0;
-  return 0;
-}
-
-// Known splice sites: bit 7 of a leftdi / rightdi byte (the dinucleotide codes
-// use 6 bits, intron.h:10-18) carries left_known / right_known.
-constexpr int KNOWN_BIT = 0x80, DI_MASK = 0x3F;
-constexpr int KNOWN_REWARD = 20;  // KNOWN_SPLICESITE_REWARD (dynprog.c:285)
-__device__ inline int kreward(int d) { return (d >> 7) * KNOWN_REWARD; }
-__device__ inline bool kflag(const unsigned char* f, int km, int c) { return km != 0 && f[c] != 0; }
-// IIT_exists_with_divno_signed on the intron (cL, cR) (:3598-3612), from the
-// caller's pair list
-__device__ inline bool known_intron(const unsigned char* p, int cL, int cR) {
-  const int n = p[0] | (p[1] << 8);
-  for (int i = 0; i < n; i++) {
-    const unsigned char* e = p + 2 + 4 * i;
-    if ((e[0] | (e[1] << 8)) == cL && (e[2] | (e[3] << 8)) == cR) return true;
-  }
-  return false;
-}
-
-// leftdi / rightdi (dynprog.c:3331-3373) from two genome class codes
-__device__ inline int left_di(int a, int b) {
-  if (a == 2 && b == 3) return LEFT_GT;
-  if (a == 2 && b == 1) return LEFT_GC;
-  if (a == 0 && b == 3) return LEFT_AT;
-  if (a == 1 && b == 3) return LEFT_CT;
-  return 0;
-}
-__device__ inline int right_di(int b, int a) {
-  if (b == 0 && a == 2) return RIGHT_AG;
-  if (b == 0 && a == 1) return RIGHT_AC;
-  if (b == 2 && a == 1) return RIGHT_GC;
-  if (b == 0 && a == 3) return RIGHT_AT;
-  return 0;
-}
-
-// Maxent site probability of a left / right splice column
-// (get_splicesite_probs :3195-3287, probability precompute :3856-3903).
-__device__ inline double left_site_prob(const gsnapdp_ggap_window& w, int cL,
-                                        const uint32_t* blocks, uint64_t nwords, const double* T) {
-  const int cdir = w.cdna_direction;
-  uint32_t pos;
-  if (w.watsonp) {
-    pos = w.chrpos + (uint32_t)w.offset2L + (uint32_t)cL;
-    return maxent_prob(cdir > 0 ? GSNAPDP_DONOR : GSNAPDP_ANTIACCEPTOR, w.chroffset + pos,
-                       w.chroffset, blocks, nwords, T);
-  }
-  pos = w.chrpos + (uint32_t)(w.genomiclength - 1) - (uint32_t)w.offset2L - (uint32_t)cL + 1u;
-  return maxent_prob(cdir > 0 ? GSNAPDP_ANTIDONOR : GSNAPDP_ACCEPTOR, w.chroffset + pos,
-                     w.chroffset, blocks, nwords, T);
-}
-__device__ inline double right_site_prob(const gsnapdp_ggap_window& w, int cR,
-                                         const uint32_t* blocks, uint64_t nwords, const double* T) {
-  const int cdir = w.cdna_direction;
-  uint32_t pos;
-  if (w.watsonp) {
-    pos = w.chrpos + (uint32_t)w.revoffset2R - (uint32_t)cR + 1u;
-    return maxent_prob(cdir > 0 ? GSNAPDP_ACCEPTOR : GSNAPDP_ANTIDONOR, w.chroffset + pos,
-                       w.chroffset, blocks, nwords, T);
-  }
-  pos = w.chrpos + (uint32_t)(w.genomiclength - 1) - (uint32_t)w.revoffset2R + (uint32_t)cR;
-  return maxent_prob(cdir > 0 ? GSNAPDP_ANTIACCEPTOR : GSNAPDP_DONOR, w.chroffset + pos,
-                     w.chroffset, blocks, nwords, T);
-}
-
-// The per-side view the shared traceback template expects (gsnapdp_device.h).
-__device__ inline Lane side_lane(const gsnapdp_ggap_window& w, const GGeo& G, int right) {
-  Lane L;
-  L.d.L1 = G.L1;
-  L.d.L2 = right ? G.L2R : G.L2L;
-  L.d.lband = right ? G.lbR : G.lbL;
-  L.d.rband = right ? G.rbR : G.rbL;
-  L.d.W = L.d.lband + L.d.rband + 1;
-  L.d.mode = 0;
-  L.d.eb = G.eb;
-  L.d.open = G.open;
-  L.d.ext = G.ext;
-  L.d.mt = G.mt;
-  L.d.jl = 0;
-  L.d.rev = right;
-  L.d.status = ST_OK;
-  L.d.early_score = 0;
-  L.d.early_dpi_step = 0;
-  // right flank: query read backwards from sequence1[length1-1] (dynprog.c:4960)
-  L.qbase = right ? (int)w.qpos + G.L1 - 1 : (int)w.qpos;
-  L.qstep = right ? -1 : 1;
-  L.g0 = right ? w.revoffset2R : w.offset2L;
-  L.gstep = right ? -1 : 1;
-  L.base = w.chroffset + w.chrpos;
-  L.glen = (int)w.genomiclength;
-  L.watson = w.watsonp ? 1 : 0;
-  L.allstar = (L.base < w.chroffset) || (L.base >= w.chrhigh);
-  L.off1 = w.offset1;
-  L.off2 = right ? w.revoffset2R : w.offset2L;
-  L.cdna_direction = w.cdna_direction;
-  return L;
-}
 
 template <class P>
 struct CellDirs {  // direction nibble of an in-band cell (r >= 1, c >= 1)
@@ -372,7 +181,7 @@ __device__ void gg_fill(const Side<P>& sd, PC colv, P bnd, int L1, int rho, int 
     if (NS > 1) columns(std::true_type{});
     else columns(std::false_type{});
     // the boundary row is read by the next stripe's lane 0
-    if constexpr (GMEM) __threadfence();
+    if constexpr (GMEM) wave_fence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);
   }
 }
@@ -481,7 +290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
         itab[t] = (uint16_t)(sI | (it << 8));
       }
     }
-    if constexpr (GMEM) __threadfence();
+    if constexpr (GMEM) wave_fence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the class bytes are in LDS
     if (act) {  // leftdi / rightdi (:3331-3373); 0 past the scanned columns (calloc);
                 // bit 7: left_known / right_known (:3375-3550)
@@ -514,13 +323,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
                              [&](int r) { return ptab[(unsigned char)q[(int)w.qpos + max(0, G.L1 - r)] & 127u]; },
                              T, NS);
 #endif
-    if constexpr (GMEM) __threadfence();
+    if constexpr (GMEM) wave_fence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);
 
     // ---- bridge_intron_gap (dynprog.c:3290-4122), lane = rL
     const int leftoffset = w.offset2L, rightoffset = w.revoffset2R;
     const int lbandB = G.eb, rbandBL = G.L2L - G.L1 + G.eb, rbandBR = G.L2R - G.L1 + G.eb;
-    if constexpr (GMEM) __threadfence();
+    if constexpr (GMEM) wave_fence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);  // the dinucleotide codes are in LDS
     auto HLv = [&](int r, int c) { return (int)HL[(r - 1) * G.WL + (c - r + G.lbL)]; };
     auto HRv = [&](int r, int c) { return (int)HR[(r - 1) * G.WR + (c - r + G.lbR)]; };
@@ -804,7 +613,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
         qb[i] = (uint16_t)((unsigned char)q[qi] | ((unsigned)(unsigned char)qu[qi] << 8));
       }
     }
-    if constexpr (GMEM) __threadfence();
+    if constexpr (GMEM) wave_fence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);
     const int T = __builtin_amdgcn_readfirstlane(wave_max(act ? L2 + (L1 + 1 > RL ? RL : L1 + 1) : 0));
     const int NS = __builtin_amdgcn_readfirstlane(wave_max(act ? L1 + 1 : 1) + RL - 1) / RL;
@@ -813,7 +622,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
     gg_fill<RL, GMEM, false>(sd, cls, bnd, L1, rho, d.open, d.ext, d.jl,
                              [&](int r) { return ptab[(unsigned char)q[L.qbase + L.qstep * (r - 1)] & 127u]; },
                              T, NS);
-    if constexpr (GMEM) __threadfence();
+    if constexpr (GMEM) wave_fence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);
     // ---- endpoint: a row-parallel scan, then the first (or, with jump_late,
     // the last) best cell in row-major order
@@ -943,7 +752,7 @@ __global__ void k_sj_plan(const gsnapdp_sj_window* __restrict__ S, int n,
 __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
                             gsnapdp_ggap_result* __restrict__ res,
                             gsnapdp_ggap_trace* __restrict__ trc, int* __restrict__ lists,
-                            int* __restrict__ counts, int cap) {
+                            int* __restrict__ counts, int cap, int use_band) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   int cls = -1;
   if (i < n) {
@@ -977,8 +786,10 @@ __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
       X.status = ST_UNSUPPORTED;
     } else {
       done = false;
+      cls = use_band ? gband_list(w, G) : -1;  // the register band (k_gband) when it can
       const int bndw = G.L1 + 1 > 64 ? 3 * (max(G.L2L, G.L2R) + 2) : 0;  // stripe boundary row
-      if (G.L1 + 1 <= 32 && G.words <= GG_SMALL_WORDS) cls = GG_SMALL;
+      if (cls >= 0) {
+      } else if (G.L1 + 1 <= 32 && G.words <= GG_SMALL_WORDS) cls = GG_SMALL;
       else if (G.words + bndw <= GG_MID_WORDS) cls = GG_MID;
       else if ((size_t)G.words + bndw <= GG_BIG_WORDS) cls = GG_BIG;
       else {
@@ -995,7 +806,7 @@ __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
   }
   // one list append per class per wave
 #pragma unroll
-  for (int c = 0; c < GG_NCLS; c++) {
+  for (int c = 0; c < GG_NLISTS; c++) {
     const int pos = agg_atomic_inc(counts + c, cls == c ? 0 : -1);
     if (cls == c) lists[(size_t)c * cap + pos] = i;
   }
@@ -1183,7 +994,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
         qR[c] = (uint16_t)(a | (u << 8));
       }
     }
-    if constexpr (GMEM) __threadfence();
+    if constexpr (GMEM) wave_fence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);
     const int L1max = max(C.L1L, C.L1R);
     const int T = __builtin_amdgcn_readfirstlane(wave_max(act ? L1max + (C.G + 1 > RL ? RL : C.G + 1) : 0));
@@ -1196,7 +1007,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
                             [&](int r) { return 4u * (uint32_t)gR[r]; }, T, NS);
     gg_fill<RL, GMEM, true>(SL, cwL, bnd, C.G, rho, CDNA_OPEN, CDNA_EXTEND, jl,
                             [&](int r) { return 4u * (uint32_t)gL[r]; }, T, NS);
-    if constexpr (GMEM) __threadfence();
+    if constexpr (GMEM) wave_fence();
     else __builtin_amdgcn_s_waitcnt(0xc07f);
 
     // ---- bridge_cdna_gap (dynprog.c:3068-3146), lane = rL; scan order rL,
@@ -1472,7 +1283,7 @@ static int ggap_capacity(gsnapdp_ctx* ctx, int n) {
     const int cap = n + n / 4 + 1024;
     (void)hipFree(ctx->d_ggap_lists);
     ctx->d_ggap_lists = nullptr;
-    HIPCHK(hipMalloc(&ctx->d_ggap_lists, (size_t)GG_NCLS * cap * 4));
+    HIPCHK(hipMalloc(&ctx->d_ggap_lists, (size_t)GG_NLISTS * cap * 4));
     ctx->ggap_cap = cap;
   }
   if (!ctx->d_ggap_counts) HIPCHK(hipMalloc(&ctx->d_ggap_counts, 64));
@@ -1495,11 +1306,17 @@ extern "C" int gsnapdp_ggap_run_device(gsnapdp_ctx* ctx, const gsnapdp_ggap_wind
   int* counts = ctx->d_ggap_counts;
   int* lists = ctx->d_ggap_lists;
   const int cap = ctx->ggap_cap;
-  HIPCHK(hipMemsetAsync(counts, 0, 4 * GG_NCLS, st));
+  HIPCHK(hipMemsetAsync(counts, 0, 4 * GG_NLISTS, st));
   gsnapdp__mark(ctx, st, 4, 0);
   hipLaunchKernelGGL(k_ggap_plan, dim3((n + 255) / 256), dim3(256), 0, st, d_windows, n,
-                     d_results, d_traces, lists, counts, cap);
+                     d_results, d_traces, lists, counts, cap, ctx->ggap_rowlane_only ? 0 : 1);
   gsnapdp__mark(ctx, st, 4, 1);
+  gsnapdp__mark(ctx, st, 6, 0);
+  if (!ctx->ggap_rowlane_only &&
+      gsnapdp__gband_launch(ctx, st, d_windows, lists, counts, cap, d_query, d_query_uc, d_results,
+                            d_traces, d_ops, d_op_offsets))
+    return -1;
+  gsnapdp__mark(ctx, st, 6, 1);
   gsnapdp__mark(ctx, st, 5, 0);
   // small windows: 4 waves x 2 windows per block, as many blocks per CU as LDS holds
   hipLaunchKernelGGL((k_ggap<32, false>), dim3(ctx->num_cus * GG_SMALL_BLOCKS), dim3(256),

@@ -136,3 +136,21 @@ def test_gpu_c4_parity(prob):
     oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
     compare(b.windows, res, trc, pairs, npairs, ores, oflat, onp, "C4 prob=%s" % prob)
     assert np.mean(ores["returned_null"] == 0) > 0.8 and oflat.size > 20 * len(b.windows)
+
+
+@pytest.mark.parametrize("n", [1, 5, 17, 33])
+def test_gpu_ggap_ragged_batches_with_shadow_groups(n):
+    """Batches that leave window groups of a register-band wave empty: the
+    shadow groups replay the task's first window (here at query offset 0)
+    without touching memory outside the batch."""
+    g, b = W.c4_windows(W.synthetic_genome(2_000_000, seed=9), 64, seed=9, use_probabilities=False)
+    w = b.windows[:n].copy()
+    assert w["qpos"][0] == 0
+    blocks = W.pack_genome(g)
+    ctx = Context(blocks)
+    res, trc, ops, off = ctx.ggap_run(w, b.query, b.query_uc)
+    pairs, npairs = ctx.ggap_all_pairs(w, b.query, b.query_uc, res, trc, ops, off)
+    O.setup(blocks)
+    ores, opairs, ooff, onp = O.run_ggap_batch(w, b.query, b.query_uc)
+    oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
+    compare(w, res, trc, pairs, npairs, ores, oflat, onp, "ragged %d" % n)
