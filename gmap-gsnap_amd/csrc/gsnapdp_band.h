@@ -169,12 +169,13 @@ constexpr int RING_WORDS_MAX = 1280;  // max Rings<S,LPW>::WORDS over the classe
 // D / M: the wave's direction words and match bytes (column c's 64-lane row at
 // c * 64, lane (j, g) at j * NG + g); (r, cstart): the start cell; maxC: the
 // wave's largest start column (every lane of the wave computes it; the
-// callers' other lanes have returned).  Adds to `tal` (npush: the HGAP
-// gapholders only) and writes `ow`.
-template <int S, int LPW, int JL>
+// callers' other lanes have returned); JL: the fill's tie rule (its direction
+// bits are stored complemented).  Adds to `tal` (npush: the HGAP gapholders
+// only) and writes `ow`.
+template <int S, int LPW>
 __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint8_t* __restrict__ M,
                                       int g, int r, int cstart, int maxC, int lband, int rband,
-                                      int stop, int cvlo, int cvhi, const Lane& L,
+                                      int stop, int cvlo, int cvhi, int JL, const Lane& L,
                                       const uint32_t* __restrict__ blocks, uint64_t nwords,
                                       Tally& tal, OpWriter& ow) {
   constexpr int WMAX = S * LPW;

@@ -707,12 +707,12 @@ __device__ __noinline__ void gband_group(const gsnapdp_ggap_window* __restrict__
     const int cap = (int)(op_off[wi + 1] - o0);
     Tally t = {0, 0, 0, 0, 0};
     OpWriter owR = {ops + o0, cap, 0, 0};
-    band_traceback<S, LPW, 1 - JL>(Dr, Mr, g, rRb, best.cR, maxCR, G.lbR, G.rbR,
-                                   S * LPW - G.WR, csR.cvlo, csR.cvhi, LR, blocks, nwords, t, owR);
+    band_traceback<S, LPW>(Dr, Mr, g, rRb, best.cR, maxCR, G.lbR, G.rbR, S * LPW - G.WR, csR.cvlo,
+                           csR.cvhi, 1 - JL, LR, blocks, nwords, t, owR);
     const int nR = owR.n < cap ? owR.n : cap;
     OpWriter owL = {ops + o0 + nR, cap - nR, 0, 0};
-    band_traceback<S, LPW, JL>(Dl, Ml, g, rLb, best.cL, maxCL, G.lbL, G.rbL, S * LPW - G.WL,
-                               csL.cvlo, csL.cvhi, LL, blocks, nwords, t, owL);
+    band_traceback<S, LPW>(Dl, Ml, g, rLb, best.cL, maxCL, G.lbL, G.rbL, S * LPW - G.WL, csL.cvlo,
+                           csL.cvhi, JL, LL, blocks, nwords, t, owL);
     X.nops_right = nR;
     X.nops_left = owL.n < owL.cap ? owL.n : owL.cap;
     if (owR.n > cap || owL.n > owL.cap) X.status = ST_OPS_OVERFLOW;

@@ -204,14 +204,22 @@ __global__ void k_scatter(const int* __restrict__ keys, int n, int* __restrict__
 // wrote (coalesced, prefetched two columns ahead) and the group's traceback
 // lane walks the reference's traceback (dynprog.c:2611-2712) one column per
 // step, so no step waits on a dependent global load.
+// per-wave k_fill scratch: TB_BATCH regions of direction words (u32) then match
+// bytes, one 64-lane row per column 0 .. FAST_L2MAX + 3 (the traceback reads
+// whole 4-column groups)
+#ifndef GSNAPDP_TB_BATCH
+#define GSNAPDP_TB_BATCH 4
+#endif
+constexpr int TB_BATCH = GSNAPDP_TB_BATCH;
+constexpr size_t FILL_COLS_DEV = (size_t)FAST_L2MAX + 4;
+constexpr size_t FILL_REGION_DW = FILL_COLS_DEV * 64 + FILL_COLS_DEV * 16;
+
 template <int S, int LPW, int LOW, int JL>
-__device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool active, int lane,
-                           uint32_t* __restrict__ D, uint8_t* __restrict__ M,
-                           const char* __restrict__ q, const char* __restrict__ qu,
-                           const uint32_t* __restrict__ blocks, uint64_t nwords,
-                           const uint32_t* sprof, uint32_t* ring,
-                           gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
-                           const int64_t* __restrict__ op_off) {
+__device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool active, int lane,
+                          uint32_t* __restrict__ D, uint8_t* __restrict__ M,
+                          const char* __restrict__ q, const char* __restrict__ qu,
+                          const uint32_t* __restrict__ blocks, uint64_t nwords,
+                          const uint32_t* sprof, uint32_t* ring) {
   static_assert(S >= 2 && S <= 8 && LPW <= 16 && 64 % LPW == 0, "class shape");
   using RG = Rings<S, LPW>;
   static_assert(RG::WORDS <= RING_WORDS_MAX, "LDS ring budget");
@@ -453,23 +461,46 @@ __device__ void fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool a
   for (int s = 0; s < S; s++)
     if (j == je && s == sle) fin = H[s];
   fin = __shfl(fin, gbase + je);
-  const int finalscore = (int)(fin - FV_BIAS) + (L1 + L2) * ext;
+  return (int)(fin - FV_BIAS) + (L1 + L2) * ext;
+}
+
+// The tracebacks of up to TB_BATCH wave-tasks of one class in ONE backward
+// sweep, one window per lane: lane k * NG + g traces group g of the batch's
+// task k (direction scratch region k).  A task's own sweep would run on lane 0
+// of each group only (NG of the 64 lanes); this sweep keeps up to
+// TB_BATCH * NG lanes busy.  wi < 0: no window on this lane.
+template <int S, int LPW>
+__device__ void trace_batch(int lane, int wi, int finalscore, int jl,
+                            const gsnapdp_window* __restrict__ Wn, const uint32_t* __restrict__ D,
+                            const uint32_t* __restrict__ blocks, uint64_t nwords,
+                            gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
+                            const int64_t* __restrict__ op_off) {
+  constexpr int NG = 64 / LPW;
+  constexpr int WMAX = S * LPW;
+  const int k = lane / NG, g = lane % NG;
+  const bool tr = wi >= 0;
+  const gsnapdp_window w = Wn[tr ? wi : 0];
+  const Lane L = make_lane(w);
+  const int L1 = L.d.L1, L2 = L.d.L2;
+  const int maxC = __builtin_amdgcn_readfirstlane(wave_max(tr ? L2 : 0));
 #ifdef EXP_NOTRACE
-  if (active && j == 0) res[wi].finalscore = finalscore;
+  if (tr) res[wi].finalscore = finalscore;
   return;
 #endif
-  if (!active || j != 0) return;
-
-  const gsnapdp_window w = Wn[wi];
-  const Lane L = make_lane(w);
+  if (!tr) return;
+  const uint32_t* Dk = D + (size_t)k * FILL_REGION_DW;
+  const uint8_t* Mk = (const uint8_t*)(Dk + FILL_COLS_DEV * 64);
+  ColStream cs;
+  cs.init(L);
   Tally tal = {0, 0, 0, 0, 0};
   OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
-  band_traceback<S, LPW, JL>(D, M, g, L1, L2, maxL2, lband, rband, stop, cvlo, cvhi, L, blocks,
-                             nwords, tal, ow);
+  band_traceback<S, LPW>(Dk, Mk, g, L1, L2, maxC, L.d.lband, L.d.rband, WMAX - L.d.W, cs.cvlo,
+                         cs.cvhi, jl, L, blocks, nwords, tal, ow);
   write_result(res + wi, w, L, finalscore, L1, L2, tal, ow);
 }
 
-// This wave's wave-tasks of class (S, LPW, LOW): task t covers the 64/LPW
+// This wave's wave-tasks of class (S, LPW, LOW), in batches of B (<= TB_BATCH)
+// tasks whose tracebacks share one sweep: task t covers the 64/LPW
 // windows perm[t*NG ..]; the wave runs t = t0, t0 + stride, ... < t1.  Not
 // inlined, so each class gets its own register allocation (inlining the
 // classes into the kernel spills across them); called once per wave and
@@ -497,21 +528,35 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
   uint32_t* __restrict__ ops = (uint32_t*)ops1;
   const int64_t* __restrict__ op_off = (const int64_t*)op_off1;
   constexpr int NG = 64 / LPW;
+  constexpr int B = LPW < TB_BATCH ? LPW : TB_BATCH;  // tasks per traceback sweep
   const int lane = threadIdx.x & 63;
-  uint8_t* M = (uint8_t*)(D + (size_t)(FAST_L2MAX + 4) * 64);
   const int g = lane / LPW;
-  for (int t = t0; t < t1; t += stride) {
-    const int wi0 = perm[(size_t)t * NG + g];
-    const int w0 = __builtin_amdgcn_readfirstlane(perm[(size_t)t * NG]);  // group 0: a real window
-    const bool active = wi0 >= 0;
-    const int wi = active ? wi0 : w0;  // idle groups shadow group 0 (reads only)
-    const int jl = __builtin_amdgcn_readfirstlane((int)Wn[w0].jump_late_p);
-    if (jl)
-      fill_group<S, LPW, LOW, 1>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, ring,
-                                 res, ops, op_off);
-    else
-      fill_group<S, LPW, LOW, 0>(Wn, wi, active, lane, D, M, q, qu, blocks, nwords, sprof, ring,
-                                 res, ops, op_off);
+  for (int tb = t0; tb < t1; tb += B * stride) {
+    // this lane's window in the batch's sweep: group (lane % NG) of task lane / NG
+    int my_wi = -1, my_fs = 0, my_jl = 0;
+    for (int k = 0; k < B; k++) {
+      const int t = tb + k * stride;
+      if (t >= t1) break;
+      uint32_t* Dk = D + (size_t)k * FILL_REGION_DW;
+      uint8_t* Mk = (uint8_t*)(Dk + FILL_COLS_DEV * 64);
+      const int wi0 = perm[(size_t)t * NG + g];
+      const int w0 = __builtin_amdgcn_readfirstlane(perm[(size_t)t * NG]);  // group 0: a real window
+      const bool active = wi0 >= 0;
+      const int wi = active ? wi0 : w0;  // idle groups shadow group 0 (reads only)
+      const int jl = __builtin_amdgcn_readfirstlane((int)Wn[w0].jump_late_p);
+      const int fs = jl ? fill_group<S, LPW, LOW, 1>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords,
+                                                     sprof, ring)
+                        : fill_group<S, LPW, LOW, 0>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords,
+                                                     sprof, ring);
+      const int src = (lane % NG) * LPW;  // lane 0 of group lane % NG
+      const int v_wi = __shfl(wi0, src), v_fs = __shfl(fs, src);
+      if (lane / NG == k) {
+        my_wi = v_wi;
+        my_fs = v_fs;
+        my_jl = jl;
+      }
+    }
+    trace_batch<S, LPW>(lane, my_wi, my_fs, my_jl, Wn, D, blocks, nwords, res, ops, op_off);
   }
 }
 
@@ -595,11 +640,8 @@ __global__ void k_maxent(const uint8_t* __restrict__ model, const uint32_t* __re
 static thread_local std::string g_err;
 void gsnapdp__set_err(const std::string& s) { g_err = s; }
 
-// per-wave k_fill scratch: direction words (u32) then match bytes, one
-// 64-lane row per column 0 .. FAST_L2MAX + 3 (the traceback reads whole
-// 4-column groups)
-static const size_t FILL_COLS = (size_t)FAST_L2MAX + 4;
-static const size_t WAVE_STRIDE_DW = FILL_COLS * 64 + FILL_COLS * 16;
+// per-wave k_fill scratch: TB_BATCH regions (see FILL_REGION_DW)
+static const size_t WAVE_STRIDE_DW = (size_t)TB_BATCH * FILL_REGION_DW;
 
 extern "C" const char* gsnapdp_last_error(void) { return g_err.c_str(); }
 
