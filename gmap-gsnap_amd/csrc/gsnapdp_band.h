@@ -75,13 +75,16 @@ constexpr int TB_AHEAD = GSNAPDP_TB_AHEAD;  // traceback prefetch distance, in 4
 
 // k_fill's LDS profile word: each signed 4-bit pairdistance nibble s becomes
 // the unsigned nibble s + 6 (s in -5..3, so 1..9); match bits unchanged.
-__device__ inline uint32_t fill_profile_word(uint32_t w) {
+// END_SC_BIAS: the end gaps' ENDQ table (extend -1) folds -2 * END_EXTEND =
+// +2 instead and stays signed (-3..5, read with a signed bfe).
+constexpr int END_SC_BIAS = 2;  // -2 * END_EXTEND (dynprog.c:245)
+__device__ inline uint32_t fill_profile_word(uint32_t w, int bias = FILL_SC_BIAS) {
   uint32_t o = w & 0xFF000000u;
 #pragma unroll
   for (int g = 0; g < 6; g++) {
     const int n = (int)((w >> (4 * g)) & 0xFu);
     const int sn = n >= 8 ? n - 16 : n;
-    o |= (uint32_t)((sn + FILL_SC_BIAS) & 0xF) << (4 * g);
+    o |= (uint32_t)((sn + bias) & 0xF) << (4 * g);
   }
   return o;
 }
@@ -117,14 +120,33 @@ __device__ inline FV fv_max(FV a, FV b) {
   asm("v_max_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
   return d;
 }
+// min(x, bits 16..31 of w) (both 16-bit), the upper half of the result zeroed
+__device__ inline FV fv_cap_hi(FV x, uint32_t w) {
+  FV d;
+  asm("v_min_u16_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_1"
+      : "=v"(d)
+      : "v"(x), "v"(w));
+  return d;
+}
 static_assert(FV_NEG >= 12 && FV_NEG + 9u * 688u < FV_BIAS - 2u * 12u &&
                   FV_BIAS + 9u * 688u < 65536u && FAST_L2MAX + 48 <= 688,
               "16-bit k_fill value ranges");
+// End gaps (ENDQ, open -12, extend -1): a diagonal step changes an offset value
+// by pairdistance + 2 in -3..5, so values fall as well as rise.  Their NEG-like
+// values start higher, at FV_NEG_END, and stay in [FV_NEG_END - 24 - 3*688,
+// FV_NEG_END + 5*688], below the reachable [FV_BIAS - 24 - 3*688, FV_BIAS +
+// 5*688], which stays under bit 15 (the live-row cap, k_fill).
+constexpr uint32_t FV_NEG_END = 4096u;
+static_assert(FV_NEG_END >= 24u + 3u * 688u && FV_NEG_END + 5u * 688u < FV_BIAS - 24u - 3u * 688u &&
+                  FV_BIAS + 5u * 688u < 32768u,
+              "16-bit k_fill end-gap value ranges");
 #else
 using FV = int;
 constexpr int FV_NEG = NEG;
 constexpr int FV_BIAS = 0;
+constexpr int FV_NEG_END = NEG;
 __device__ inline FV fv_max(FV a, FV b) { return max(a, b); }
+__device__ inline FV fv_cap_hi(FV x, uint32_t) { return x; }  // (k_plan keeps end gaps off this build)
 #endif
 __device__ inline uint32_t push_sign(uint32_t acc, int d) {
   return __builtin_amdgcn_alignbit(acc, (uint32_t)d, 31u);  // (acc << 1) | (d < 0)

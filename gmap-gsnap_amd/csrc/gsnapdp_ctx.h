@@ -76,6 +76,7 @@ struct gsnapdp_ctx {
   uint32_t* d_ggap_pool = nullptr; // global scratch of the large-window path
   uint32_t* d_gband_pool = nullptr; // per-wave scratch of the register-band path (k_gband)
   int ggap_rowlane_only = 0;        // GSNAPDP_GGAP_ROWLANE=1: every window on k_ggap (A/B tests)
+  int ends_rowlane = 0;             // GSNAPDP_ENDS_ROWLANE=1: every end gap on k_rows (A/B tests)
   size_t ggap_stage_cap = 0;
   void* d_ggap_stage = nullptr;
   // splice-junction end gaps (gsnapdp_sj_*)

@@ -36,9 +36,20 @@ GSNAPDP_HD_CONST inline int class_of_w(int W) {
   while (c < NCLASS - 1 && W > CLASS_W[c]) c++;
   return c;
 }
-// k_fill bucket key = (W * (FAST_WMAX+1) + lband) * 2 + jump_late (W <= 48, lband <= 48)
-constexpr int NKEYS = (FAST_WMAX + 1) * (FAST_WMAX + 1) * 2;
-constexpr int KEYS_PER_W = (FAST_WMAX + 1) * 2;
+// k_fill bucket key = ((W(W-1)/2 + lband) * 2 + jl) * 2 + end: W-major over
+// the (W, lband < W) triangle (W <= 48; jl the fill's tie rule; end: an end gap
+// scanned by find_best_endpoint, whose open/extend differ from a single gap's)
+GSNAPDP_HD_CONST inline int key_tri(int W) { return W * (W - 1) / 2; }
+constexpr int NKEYS = key_tri(FAST_WMAX + 1) * 4;
+GSNAPDP_HD_CONST inline int fill_key(int W, int lband, int jl, int end) {
+  return ((key_tri(W) + lband) * 2 + jl) * 2 + end;
+}
+GSNAPDP_HD_CONST inline int first_key_of_w(int W) { return key_tri(W) * 4; }
+GSNAPDP_HD_CONST inline int w_of_key(int k) {  // the W whose keys hold k
+  int W = 1;
+  while (W < FAST_WMAX && first_key_of_w(W + 1) <= k) W++;
+  return W;
+}
 
 // Mismatch types (dynprog.c:150)
 enum { MT_HIGHQ = 0, MT_MEDQ = 1, MT_LOWQ = 2, MT_ENDQ = 3 };

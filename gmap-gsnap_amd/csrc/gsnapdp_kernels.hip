@@ -29,6 +29,18 @@ using namespace gsnapdp;
 
 namespace {
 
+// End gaps that k_fill scans (its END fill, below): the rank of a band cell
+// must fit END_RANK_BITS.
+constexpr int END_RANK_BITS = 14;
+constexpr int END_RANK_MAX = (1 << END_RANK_BITS) - 1;
+__device__ inline bool end_on_band(const Derived& d) {  // k_plan: the END fill's limits
+#ifdef GSNAPDP_FILL32
+  return false;  // (the live-row cap needs the 16-bit values)
+#endif
+  return d.mode == 1 && d.W <= FAST_WMAX && d.L2 <= FAST_L2MAX && d.eb <= FAST_WMAX &&
+         2 * d.eb * d.L1 + d.L2 + d.eb <= END_RANK_MAX;
+}
+
 // ------------------------------------------------------------------ k_plan
 // Early returns, QUERYEND_NOGAPS windows (no fill at all) and bucketing.
 __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* __restrict__ q,
@@ -37,7 +49,7 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
                        gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
                        const int64_t* __restrict__ op_off, int* __restrict__ keys,
                        int* __restrict__ hist, int* __restrict__ big_list,
-                       int* __restrict__ big_count, int list_cap) {
+                       int* __restrict__ big_count, int list_cap, int ends_on_band) {
   __shared__ int lh[NKEYS];  // block-local histogram: one global atomic per key per block
   __shared__ int lbig[RW_NCLS], lbase[RW_NCLS];  // block-local row-lane list appends
   for (int k = threadIdx.x; k < NKEYS; k += blockDim.x) lh[k] = 0;
@@ -75,7 +87,10 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
       ow.flush();
       write_result(&res[i], w, L, 0, m, m, t, ow);
     } else if (L.d.mode == 0 && L.d.W <= FAST_WMAX && L.d.L2 <= FAST_L2MAX) {
-      key = (L.d.W * (FAST_WMAX + 1) + L.d.lband) * 2 + L.d.jl;
+      key = fill_key(L.d.W, L.d.lband, L.d.jl, 0);
+    } else if (ends_on_band && end_on_band(L.d)) {
+      key = fill_key(L.d.W, L.d.lband, L.d.jl, 1);
+      big_count[RW_NCLS] = 1;  // k_fill: this batch has END tasks
     } else {
       big = rows_class(L.d.L1, L.d.L2, L.d.W);
       if (big < 0) {  // beyond the row-lane scratch: fail loudly
@@ -107,8 +122,8 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
 // (64 / CLASS_LPW windows).  cursor[k] = first perm entry of bucket k;
 // class_start[c] = first perm entry of class c (a multiple of its wave size,
 // since wave sizes shrink as W grows and are powers of two).
-__device__ inline int padded_bucket(int k, int h) {
-  const int ng = 64 / CLASS_LPW[class_of_w(k / KEYS_PER_W)];
+__device__ inline int padded_bucket(int W, int h) {
+  const int ng = 64 / CLASS_LPW[class_of_w(W)];
   return (h + ng - 1) / ng * ng;
 }
 
@@ -119,11 +134,20 @@ __device__ inline int padded_bucket(int k, int h) {
 __global__ void k_scan(int* __restrict__ hist, int* __restrict__ cursor,
                        int* __restrict__ class_start, int* __restrict__ perm) {
   __shared__ int part[1024];
+  constexpr int PER = (NKEYS + 1023) / 1024;
   const int tid = threadIdx.x;
-  const int per = (NKEYS + 1023) / 1024;
-  const int lo = tid * per, hi = min(NKEYS, lo + per);
-  int s = 0;
-  for (int k = lo; k < hi; k++) s += padded_bucket(k, hist[k]);
+  const int lo = tid * PER;
+  // this thread's keys: counts and padded sizes (W steps along the keys)
+  int h[PER], p[PER];
+  int s = 0, W = w_of_key(lo);
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    const int k = lo + i;
+    while (W < FAST_WMAX && first_key_of_w(W + 1) <= k) W++;
+    h[i] = k < NKEYS ? hist[k] : 0;
+    p[i] = padded_bucket(W, h[i]);
+    s += p[i];
+  }
   part[tid] = s;
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
@@ -133,11 +157,13 @@ __global__ void k_scan(int* __restrict__ hist, int* __restrict__ cursor,
     __syncthreads();
   }
   int run = part[tid] - s;
-  for (int k = lo; k < hi; k++) {
-    const int h = hist[k], p = padded_bucket(k, h);
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    const int k = lo + i;
+    if (k >= NKEYS) break;
     cursor[k] = run;
-    for (int e = run + h; e < run + p; e++) perm[e] = -1;
-    run += p;
+    for (int e = run + h[i]; e < run + p[i]; e++) perm[e] = -1;
+    run += p[i];
     hist[k] = 0;
   }
   __syncthreads();
@@ -145,7 +171,7 @@ __global__ void k_scan(int* __restrict__ hist, int* __restrict__ cursor,
     // class c covers W in (CLASS_W[c-1], CLASS_W[c]]; keys are W-major
     int wlo = 0;
     for (int c = 0; c < NCLASS; c++) {
-      const int kfirst = (wlo + 1) * KEYS_PER_W;
+      const int kfirst = first_key_of_w(wlo + 1);
       class_start[c] = kfirst < NKEYS ? cursor[kfirst] : part[1023];
       wlo = CLASS_W[c];
     }
@@ -214,18 +240,38 @@ constexpr int TB_BATCH = GSNAPDP_TB_BATCH;
 constexpr size_t FILL_COLS_DEV = (size_t)FAST_L2MAX + 4;
 constexpr size_t FILL_REGION_DW = FILL_COLS_DEV * 64 + FILL_COLS_DEV * 16;
 
-template <int S, int LPW, int LOW, int JL>
-__device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool active, int lane,
-                          uint32_t* __restrict__ D, uint8_t* __restrict__ M,
-                          const char* __restrict__ q, const char* __restrict__ qu,
-                          const uint32_t* __restrict__ blocks, uint64_t nwords,
-                          const uint32_t* sprof, uint32_t* ring) {
+// End gaps in find_best_endpoint mode (QUERYEND_GAP / BEST_LOCAL, dynprog.c:
+// 2235-2290) on the register band (END = 1).  Three changes to the fill:
+//  * rows below L1 are capped to a NEG-like value: their profile word carries
+//    FV_NEG_END in bits 16..31 where a live row's has bit 31 set, and the
+//    nogap value is min'ed with that half (they never feed a live row);
+//  * the ENDQ nibbles are signed (END_SC_BIAS) and NEG-like values start at
+//    FV_NEG_END (gsnapdp_band.h);
+//  * every cell of the unwidened band |c - r| <= extraband offers
+//    key = score * 2^14 + (row-major rank or its complement) to a per-lane
+//    maximum, so that one max per cell reproduces the reference's scan order:
+//    the first best cell for '>', the last for the jump-late '>='.  The rank
+//    of (r, c) is 2*eb*r + c + eb (the band's cells in row-major order); the
+//    start (0, 0) with 0 has rank eb, below every cell's.
+struct FillOut {
+  int score, br, bc;  // finalscore and the traceback's start cell
+};
+
+template <int S, int LPW, int LOW, int JL, int END>
+__device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool active, int lane,
+                              uint32_t* __restrict__ D, uint8_t* __restrict__ M,
+                              const char* __restrict__ q, const char* __restrict__ qu,
+                              const uint32_t* __restrict__ blocks, uint64_t nwords,
+                              const uint32_t* sprof, uint32_t* ring) {
   static_assert(S >= 2 && S <= 8 && LPW <= 16 && 64 % LPW == 0, "class shape");
   using RG = Rings<S, LPW>;
   static_assert(RG::WORDS <= RING_WORDS_MAX, "LDS ring budget");
   constexpr int WMAX = S * LPW;
   constexpr int NG = 64 / LPW;
   constexpr int NAB = (WMAX - LOW) < S ? (WMAX - LOW) : S;  // local slots that may lie above the band
+  constexpr FV NEGV = END ? (FV)FV_NEG_END : (FV)FV_NEG;
+  constexpr uint32_t LIVE = END ? 0x80000000u : 0u;  // END: a live row's cap (bits 16..31) is >= 2^15
+  constexpr uint32_t DEAD = (uint32_t)NEGV << 16;     // END: a row below L1
   const int j = lane % LPW;
   const int gbase = lane - j;
   const int g = lane / LPW;
@@ -266,7 +312,8 @@ __device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
       qb = (unsigned char)q[qi] & 127u;
       ub = (unsigned char)qu[qi];
     }
-    return sprof[mtoff + qb] | sprof[UTAB + ub];
+    if (END && r > L1) return DEAD;
+    return sprof[mtoff + qb] | sprof[UTAB + ub] | LIVE;
   };
   const uint64_t gmax = nwords >= 3 ? (nwords - 3) / 3 : 0;  // last whole genome block
 
@@ -285,9 +332,9 @@ __device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
 #pragma unroll
   for (int s = 0; s < S; s++) {
     const int r = row0 + s;
-    H[s] = (r == 0) ? FV_BIAS : FV_NEG;
-    E[s] = FV_NEG;
-    F[s] = (r >= 1) ? FV_BIAS + open : FV_NEG;  // open + r*ext - r*ext
+    H[s] = (r == 0) ? FV_BIAS : NEGV;
+    E[s] = NEGV;
+    F[s] = (r >= 1) ? FV_BIAS + open : NEGV;  // open + r*ext - r*ext
     P[s] = row_word(r);
     MB = ((MB >> 1) & MB_KEEP) | row_spread(P[s]);
   }
@@ -325,7 +372,8 @@ __device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
     for (int e = 0; e < ER; e++) {
       const int r = rlo + e * LPW + j;
       const bool ok = r >= 1 && r <= L1;
-      const uint32_t w = sprof[mtoff + (ok ? (qb[e] & 127u) : 0u)] | sprof[UTAB + (ok ? ub[e] : 255u)];
+      uint32_t w = sprof[mtoff + (ok ? (qb[e] & 127u) : 0u)] | sprof[UTAB + (ok ? ub[e] : 255u)] | LIVE;
+      if (END && r > L1) w = DEAD;
       if (e * LPW + j < NR) rr[r & (RG::RR - 1)] = w;
     }
 #pragma unroll
@@ -344,9 +392,30 @@ __device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
   stage(std::integral_constant<int, RING_K + RG::SPAN>(), 1 + rbase, 1);
   uint32_t pnext = rr[(1 + j * (S - 1) + rbase) & (RG::RR - 1)];
   int gnext = cr[(1 - j) & (RG::CR - 1)];
-  FV fin = FV_NEG;
+  FV fin = NEGV;
   const int se = stop + L1 - L2 + rband;  // global slot of the endpoint (L1,L2)
   const int je = se / S, sle = se - je * S;
+  // END: the scan key of slot s is (H << 14) + Qs[s] + R(c); Qs[s] holds the
+  // slot's diagonal d = c - r (or kills a slot outside |d| <= eb), R(c) the
+  // column's share, kept in Rc and stepped by dR with the lane's column.
+  int ebw = 0, Rc = 0, dR = 0, Bt = 0;
+  int Qs[S];
+  if constexpr (END) {
+    ebw = min(lband, rband);  // wave-uniform: derive() widens one side only
+    const int kq = -ext * (1 << END_RANK_BITS) + (JL ? -2 * ebw : 2 * ebw);
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const int d = rband + stop - j * S - s;
+      Qs[s] = (d >= -ebw && d <= ebw) ? d * kq : -(1 << 30);
+    }
+    auto Rof = [&](int c) {
+      return (2 * c * ext - (int)FV_BIAS) * (1 << END_RANK_BITS) +
+             (JL ? (2 * ebw + 1) * c + ebw : END_RANK_MAX - (2 * ebw + 1) * c - ebw);
+    };
+    Rc = Rof(1 - j);  // the lane's column at step 1
+    dR = Rof(2 - j) - Rc;
+    Bt = JL ? ebw : END_RANK_MAX - ebw;  // find_best_endpoint's start: (0, 0) with 0 (:2243)
+  }
   // scratch layout: column c's words are D[c*64 + (j*NG + g)], one 256-byte
   // row per column (coalesced stores); the match bytes likewise in M.  Lane
   // (j, g) stores column c = t - j at the wave-uniform row t-(LPW-1) plus a
@@ -367,7 +436,7 @@ __device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
     const int c = t - j;
     // a window stops at its own last column, so its registers end on column L2
     const bool act = !MASKED || (c >= 1 && c <= L2);
-    FV hp = FV_NEG, fp = FV_NEG;  // new (nogap, gap2) just above local slot 0
+    FV hp = NEGV, fp = NEGV;  // new (nogap, gap2) just above local slot 0
     if (LPW > 1) {
       const FV h = (FV)from_lane_above((int)H[S - 1]), f = (FV)from_lane_above((int)F[S - 1]);
       if (j != 0) {
@@ -377,15 +446,20 @@ __device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
     }
     // four bit planes (v1, h1, dF, dE), each a short independent chain
     uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u, gsh = 0u;
+    int bstep = -(1 << 30);  // END: this column's best scan key, less R(c)
     auto cell = [&](int s, FV Hr, FV Er) {
       const FV Hd = H[s], Ed = E[s], Fd = F[s];
       const uint32_t pw = pslot(s);
       const FV a = Hr + open;
       const FV b = hp + open;
       const FV m1 = fv_max(Hd, Ed);
-      const FV sc = (FV)__builtin_amdgcn_ubfe(pw, gsh, 4);  // pairdistance - 2*extend
+      // pairdistance - 2*extend
+      const FV sc = END ? (FV)__builtin_amdgcn_sbfe((int)pw, (int)gsh, 4) : (FV)__builtin_amdgcn_ubfe(pw, gsh, 4);
       const bool above = (s < NAB) && (j * S + s < stop);  // loop-invariant lane mask
-      const FV hn = above ? FV_NEG : fv_max(m1, Fd) + sc;
+      FV hn = fv_max(m1, Fd) + sc;
+      if constexpr (END) hn = fv_cap_hi(hn, pw);  // rows below L1
+      hn = above ? NEGV : hn;
+      if constexpr (END) bstep = max(bstep, (int)(hn << END_RANK_BITS) + Qs[s]);
       const int dv = JL ? (int)(Fd - m1) : (int)(m1 - Fd);  // v1: nogap from gap2
       const int dh = JL ? (int)(Ed - Hd) : (int)(Hd - Ed);  // h1: nogap from gap1
       const int df = JL ? (int)(fp - b) : (int)(b - fp);    // dF: gap2 extends
@@ -415,7 +489,7 @@ __device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
       macc = (uint32_t)(MB >> (8u * (uint32_t)gnext));
       cell(0, H[1], E[1]);
     }
-    FV hb = FV_NEG, eb = FV_NEG;  // old (nogap, gap1) just below the lowest local slot
+    FV hb = NEGV, eb = NEGV;  // old (nogap, gap1) just below the lowest local slot
     if (LPW > 1) {
       const FV h = (FV)from_lane_below((int)H[0]), e = (FV)from_lane_below((int)E[0]);
       if (j != LPW - 1) {
@@ -427,6 +501,7 @@ __device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
 #pragma unroll
       for (int s = 1; s < S - 1; s++) cell(s, H[s + 1], E[s + 1]);
       cell(S - 1, hb, eb);
+      if constexpr (END) Bt = max(Bt, bstep + Rc);
       const uint32_t acc = (((((av << S) | ah) << S) | af) << S) | ae;
 #ifndef EXP_NOSTORE
       D[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = acc;
@@ -437,6 +512,7 @@ __device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
       if (acc == 0x12345678u && macc == 77u) D[0] = 1u;
 #endif
     }
+    if constexpr (END) Rc += dR;
     // next column's inputs from the rings (every lane, every step)
     if (t % RING_K == 0) stage(std::integral_constant<int, RING_K>(), t + 1 + rbase + RG::SPAN, t + 1);
     pnext = rr[(t + 1 + j * (S - 1) + rbase) & (RG::RR - 1)];
@@ -456,12 +532,21 @@ __device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
 #endif
   for (; t <= minL2; t++) step(Full(), Shift(), t);
   for (; t < maxL2 + LPW; t++) step(Masked(), Shift(), t);
+  if constexpr (END) {
+    // the group's best key: score, then rank (row-major order)
+#pragma unroll
+    for (int o = LPW / 2; o > 0; o >>= 1) Bt = max(Bt, __shfl_xor(Bt, o));
+    const int post = Bt & END_RANK_MAX;
+    const int rank = JL ? post : END_RANK_MAX - post;
+    const int br = rank / (2 * ebw + 1);
+    return FillOut{Bt >> END_RANK_BITS, br, br + rank - br * (2 * ebw + 1) - ebw};
+  }
   // endpoint (L1,L2): the lanes stopped on column L2 (dynprog.c:4545)
 #pragma unroll
   for (int s = 0; s < S; s++)
     if (j == je && s == sle) fin = H[s];
   fin = __shfl(fin, gbase + je);
-  return (int)(fin - FV_BIAS) + (L1 + L2) * ext;
+  return FillOut{(int)(fin - FV_BIAS) + (L1 + L2) * ext, L1, L2};
 }
 
 // The tracebacks of up to TB_BATCH wave-tasks of one class in ONE backward
@@ -470,7 +555,7 @@ __device__ int fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool ac
 // of each group only (NG of the 64 lanes); this sweep keeps up to
 // TB_BATCH * NG lanes busy.  wi < 0: no window on this lane.
 template <int S, int LPW>
-__device__ void trace_batch(int lane, int wi, int finalscore, int jl,
+__device__ void trace_batch(int lane, int wi, const FillOut& fo, int jl,
                             const gsnapdp_window* __restrict__ Wn, const uint32_t* __restrict__ D,
                             const uint32_t* __restrict__ blocks, uint64_t nwords,
                             gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
@@ -481,10 +566,9 @@ __device__ void trace_batch(int lane, int wi, int finalscore, int jl,
   const bool tr = wi >= 0;
   const gsnapdp_window w = Wn[tr ? wi : 0];
   const Lane L = make_lane(w);
-  const int L1 = L.d.L1, L2 = L.d.L2;
-  const int maxC = __builtin_amdgcn_readfirstlane(wave_max(tr ? L2 : 0));
+  const int maxC = __builtin_amdgcn_readfirstlane(wave_max(tr ? fo.bc : 0));
 #ifdef EXP_NOTRACE
-  if (tr) res[wi].finalscore = finalscore;
+  if (tr) res[wi].finalscore = fo.score;
   return;
 #endif
   if (!tr) return;
@@ -494,9 +578,9 @@ __device__ void trace_batch(int lane, int wi, int finalscore, int jl,
   cs.init(L);
   Tally tal = {0, 0, 0, 0, 0};
   OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
-  band_traceback<S, LPW>(Dk, Mk, g, L1, L2, maxC, L.d.lband, L.d.rband, WMAX - L.d.W, cs.cvlo,
+  band_traceback<S, LPW>(Dk, Mk, g, fo.br, fo.bc, maxC, L.d.lband, L.d.rband, WMAX - L.d.W, cs.cvlo,
                          cs.cvhi, jl, L, blocks, nwords, tal, ow);
-  write_result(res + wi, w, L, finalscore, L1, L2, tal, ow);
+  write_result(res + wi, w, L, fo.score, fo.br, fo.bc, tal, ow);
 }
 
 // This wave's wave-tasks of class (S, LPW, LOW), in batches of B (<= TB_BATCH)
@@ -508,7 +592,7 @@ __device__ void trace_batch(int lane, int wi, int finalscore, int jl,
 // restores (48 VGPRs to scratch, ~24 KB per call) are paid per wave, not per
 // task.  The pointers carry their address spaces (global / LDS) so that the
 // body still compiles to global_* and ds_* accesses rather than flat ones.
-template <int S, int LPW, int LOW>
+template <int S, int LPW, int LOW, int END>
 __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLOBAL gsnapdp_window* Wn1,
                                         const AS_GLOBAL int* perm1, const AS_GLOBAL char* q1,
                                         const AS_GLOBAL char* qu1, const AS_GLOBAL uint32_t* blocks1,
@@ -531,32 +615,41 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
   constexpr int B = LPW < TB_BATCH ? LPW : TB_BATCH;  // tasks per traceback sweep
   const int lane = threadIdx.x & 63;
   const int g = lane / LPW;
-  for (int tb = t0; tb < t1; tb += B * stride) {
+  // the class's single-gap and end-gap tasks (bucket keys end in the END bit)
+  // run in two calls, END = 0 then 1, each over the tasks of its kind only
+  auto kind_of = [&](int t) {
+    return __builtin_amdgcn_readfirstlane(derive(Wn[perm[(size_t)t * NG]]).mode == 1 ? 1 : 0);
+  };
+  int t = t0;
+  while (t < t1 && kind_of(t) != END) t += stride;
+  while (t < t1) {
     // this lane's window in the batch's sweep: group (lane % NG) of task lane / NG
-    int my_wi = -1, my_fs = 0, my_jl = 0;
-    for (int k = 0; k < B; k++) {
-      const int t = tb + k * stride;
-      if (t >= t1) break;
+    int my_wi = -1, my_jl = 0;
+    FillOut my = {0, 0, 0};
+    for (int k = 0; k < B && t < t1; k++) {
       uint32_t* Dk = D + (size_t)k * FILL_REGION_DW;
       uint8_t* Mk = (uint8_t*)(Dk + FILL_COLS_DEV * 64);
       const int wi0 = perm[(size_t)t * NG + g];
       const int w0 = __builtin_amdgcn_readfirstlane(perm[(size_t)t * NG]);  // group 0: a real window
       const bool active = wi0 >= 0;
       const int wi = active ? wi0 : w0;  // idle groups shadow group 0 (reads only)
-      const int jl = __builtin_amdgcn_readfirstlane((int)Wn[w0].jump_late_p);
-      const int fs = jl ? fill_group<S, LPW, LOW, 1>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords,
-                                                     sprof, ring)
-                        : fill_group<S, LPW, LOW, 0>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords,
-                                                     sprof, ring);
+      // the bucket's tie rule (an end5 gap's fill is reversed with !jump_late_p)
+      const int jl = __builtin_amdgcn_readfirstlane(derive(Wn[w0]).jl);
+      const FillOut fo =
+          jl ? fill_group<S, LPW, LOW, 1, END>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords, sprof, ring)
+             : fill_group<S, LPW, LOW, 0, END>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords, sprof, ring);
       const int src = (lane % NG) * LPW;  // lane 0 of group lane % NG
-      const int v_wi = __shfl(wi0, src), v_fs = __shfl(fs, src);
+      const int v_wi = __shfl(wi0, src);
+      const FillOut v = {__shfl(fo.score, src), __shfl(fo.br, src), __shfl(fo.bc, src)};
       if (lane / NG == k) {
         my_wi = v_wi;
-        my_fs = v_fs;
+        my = v;
         my_jl = jl;
       }
+      do t += stride;
+      while (t < t1 && kind_of(t) != END);
     }
-    trace_batch<S, LPW>(lane, my_wi, my_fs, my_jl, Wn, D, blocks, nwords, res, ops, op_off);
+    trace_batch<S, LPW>(lane, my_wi, my, my_jl, Wn, D, blocks, nwords, res, ops, op_off);
   }
 }
 
@@ -570,11 +663,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
     const int* __restrict__ class_start, const char* __restrict__ q, const char* __restrict__ qu,
     const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
     uint32_t* __restrict__ dirpool, size_t wave_stride, gsnapdp_result* __restrict__ res,
-    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
+    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off, const int* __restrict__ end_flag) {
   __shared__ alignas(8) uint32_t sprof[SPROF_WORDS];
   __shared__ uint32_t rings[4][RING_WORDS_MAX];  // one per wave of the block
   for (int i = threadIdx.x; i < MLUT; i += blockDim.x)
-    sprof[i] = i < UTAB ? fill_profile_word(prof[i]) : (i - UTAB < 128 ? prof[i] : 0u);
+    sprof[i] = i < UTAB ? fill_profile_word(prof[i], i >= MT_ENDQ * 128 ? END_SC_BIAS : FILL_SC_BIAS)
+                        : (i - UTAB < 128 ? prof[i] : 0u);
   for (int i = threadIdx.x; i < 32; i += blockDim.x) {
     const uint64_t x = spread_match((uint32_t)i);
     sprof[MLUT + 2 * i] = (uint32_t)x;
@@ -585,6 +679,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nw = (gridDim.x * blockDim.x) >> 6;
   uint32_t* D = dirpool + (size_t)gw * wave_stride;
+  const bool has_end = *end_flag != 0;  // (the END bodies' calls are skipped otherwise)
   int tfirst[NCLASS + 1];  // first task index of each class, then the total
   tfirst[0] = 0;
 #pragma unroll
@@ -599,12 +694,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
     const int tau0 = gw >= lo ? gw : gw + (lo - gw + nw - 1) / nw * nw;                          \
     if (tau0 < hi) {                                                                             \
       const int base = class_start[C] / (64 / CLASS_LPW[C]) - lo;                                \
-      fill_tasks<CLASS_S[C % NCLASS], CLASS_LPW[C % NCLASS], class_low(C % NCLASS)>(             \
+      fill_tasks<CLASS_S[C % NCLASS], CLASS_LPW[C % NCLASS], class_low(C % NCLASS), 0>(          \
           base + tau0, base + hi, nw, (const AS_GLOBAL gsnapdp_window*)Wn,                        \
           (const AS_GLOBAL int*)perm, (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu,        \
           (const AS_GLOBAL uint32_t*)blocks, nwords, (const AS_LDS uint32_t*)sprof,               \
           (AS_LDS uint32_t*)ring, (AS_GLOBAL uint32_t*)D, (AS_GLOBAL gsnapdp_result*)res,         \
           (AS_GLOBAL uint32_t*)ops, (const AS_GLOBAL int64_t*)op_off);                            \
+      if (has_end)                                                                                \
+        fill_tasks<CLASS_S[C % NCLASS], CLASS_LPW[C % NCLASS], class_low(C % NCLASS), 1>(        \
+            base + tau0, base + hi, nw, (const AS_GLOBAL gsnapdp_window*)Wn,                      \
+            (const AS_GLOBAL int*)perm, (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu,      \
+            (const AS_GLOBAL uint32_t*)blocks, nwords, (const AS_LDS uint32_t*)sprof,             \
+            (AS_LDS uint32_t*)ring, (AS_GLOBAL uint32_t*)D, (AS_GLOBAL gsnapdp_result*)res,       \
+            (AS_GLOBAL uint32_t*)ops, (const AS_GLOBAL int64_t*)op_off);                          \
     }                                                                                            \
   }
   FILL_CLASS(0) FILL_CLASS(1) FILL_CLASS(2) FILL_CLASS(3)
@@ -672,6 +774,8 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
   {
     const char* e = getenv("GSNAPDP_GGAP_ROWLANE");
     ctx->ggap_rowlane_only = (e && e[0] == '1') ? 1 : 0;
+    const char* f = getenv("GSNAPDP_ENDS_ROWLANE");
+    ctx->ends_rowlane = (f && f[0] == '1') ? 1 : 0;
   }
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     return fail("stream", e);
@@ -769,7 +873,7 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   int* cursor = hist + NKEYS;
   int* class_start = cursor + NKEYS;
   int* big_count = class_start + NCLASS + 1;  // RW_NCLS row-lane class counts
-  HIPCHK(hipMemsetAsync(big_count, 0, 4 * RW_NCLS, st));
+  HIPCHK(hipMemsetAsync(big_count, 0, 4 * (RW_NCLS + 1), st));  // + k_fill's END flag
   if (gsnapdp__rows_pools(ctx)) return -1;
   const int tb = 1024, nb = (n + tb - 1) / tb;
   auto mark = [&](int stage, int end) { gsnapdp__mark(ctx, st, stage, end); };
@@ -777,7 +881,7 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   hipLaunchKernelGGL(k_plan, dim3(nb), dim3(tb), 0, st, d_windows, n, d_query, d_query_uc,
                      ctx->d_blocks, (uint64_t)ctx->nwords, ctx->d_prof, d_results, d_ops,
                      d_op_offsets, ctx->d_keys, hist, ctx->d_big_list, big_count,
-                     ctx->cap_n);
+                     ctx->cap_n, ctx->ends_rowlane ? 0 : 1);
   mark(0, 1);
   mark(1, 0);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, hist, cursor, class_start, ctx->d_perm);
@@ -790,7 +894,7 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   mark(2, 0);
   hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, st, d_windows, ctx->d_perm, class_start,
                      d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_dirpool,
-                     WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets);
+                     WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets, big_count + RW_NCLS);
   mark(2, 1);
   mark(3, 0);
   if (gsnapdp__rows_launch(ctx, st, d_windows, ctx->d_big_list, big_count, ctx->cap_n, d_query,

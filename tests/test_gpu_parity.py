@@ -134,3 +134,29 @@ def test_gpu_c5_gsnap_windows_parity():
     res, pairs, npairs, ref, oflat, onp = run_both(blocks, batch)
     compare(res, pairs, npairs, ref, oflat, onp, "C5 windows")
     assert np.sum(onp) > 60 * 20_000
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_gpu_end_gaps_on_register_band(seed, monkeypatch):
+    """find_best_endpoint end gaps (QUERYEND_GAP, BEST_LOCAL) on k_fill's END fill:
+    both ends and tie rules, extraband 0-12, L1 up to 300, and a low-complexity
+    genome stretch so that many cells tie for the best score (the scan's
+    row-major order decides).  The same batch through k_rows
+    (GSNAPDP_ENDS_ROWLANE=1) and the restatement must agree bit for bit."""
+    g = W.synthetic_genome(2_000_000, seed=300 + seed, n_rate=0.002)
+    g[:400_000] = np.resize(np.frombuffer(b"AACAC", np.uint8), 400_000)  # repeats: ties
+    blocks = W.pack_genome(g)
+    parts = [W.random_windows(g, 2500, seed=seed * 10 + k, kinds=(END5_GAP, END3_GAP), max_len1=m1,
+                              max_len2=m1 + 24, max_band=b, endaligns=(W.QUERYEND_GAP, W.BEST_LOCAL))
+             for k, (m1, b) in enumerate(((30, 12), (120, 6), (300, 3)))]
+    batch = W.concat_batches(parts)
+    res, pairs, npairs, ref, oflat, onp = run_both(blocks, batch)
+    compare(res, pairs, npairs, ref, oflat, onp, "end gaps on the band seed %d" % seed)
+    monkeypatch.setenv("GSNAPDP_ENDS_ROWLANE", "1")
+    ctx = Context(blocks)
+    res2, ops2, off2 = ctx.run(batch.windows, batch.query, batch.query_uc)
+    pairs2, np2 = ctx.all_pairs(batch.windows, batch.query, batch.query_uc, res2, ops2, off2)
+    compare(res2, pairs2, np2, ref, oflat, onp, "end gaps on k_rows seed %d" % seed)
+    for f in ("bestr", "bestc", "status"):
+        assert np.array_equal(res[f], res2[f]), f
+    assert np.sum(res["bestc"] == 0) > 0 and np.sum(res["bestr"] > 0) > 5000
