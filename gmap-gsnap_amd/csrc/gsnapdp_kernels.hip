@@ -13,7 +13,8 @@
 //     counting sort (k_plan / k_scan / k_scatter), so band edges are scalar;
 //   * 4-bit direction nibbles stream to HBM scratch; each lane then walks its
 //     own traceback and emits a compact op stream (include/gsnapdp.h).
-//   End gaps and windows too wide (W > 48) or too long (L2 > 640) for
+//   End gaps in find_best_endpoint mode run here too (the END fills); the
+//   other end gaps and windows too wide (W > 48) or too long (L2 > 640) for
 //   registers run on the row-lane kernel k_rows (gsnapdp_ggap.hip).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
