@@ -120,6 +120,11 @@ __device__ inline FV fv_max(FV a, FV b) {
   asm("v_max_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
   return d;
 }
+__device__ inline FV fv_min(FV a, uint32_t b) {  // 16-bit min (b's low half)
+  FV d;
+  asm("v_min_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
 // min(x, bits 16..31 of w) (both 16-bit), the upper half of the result zeroed
 __device__ inline FV fv_cap_hi(FV x, uint32_t w) {
   FV d;
@@ -147,6 +152,7 @@ constexpr int FV_BIAS = 0;
 constexpr int FV_NEG_END = NEG;
 __device__ inline FV fv_max(FV a, FV b) { return max(a, b); }
 __device__ inline FV fv_cap_hi(FV x, uint32_t) { return x; }  // (k_plan keeps end gaps off this build)
+__device__ inline FV fv_min(FV a, uint32_t b) { return a; }
 #endif
 __device__ inline uint32_t push_sign(uint32_t acc, int d) {
   return __builtin_amdgcn_alignbit(acc, (uint32_t)d, 31u);  // (acc << 1) | (d < 0)
@@ -194,12 +200,18 @@ constexpr int RING_WORDS_MAX = 1280;  // max Rings<S,LPW>::WORDS over the classe
 // callers' other lanes have returned); JL: the fill's tie rule (its direction
 // bits are stored complemented).  Adds to `tal` (npush: the HGAP gapholders
 // only) and writes `ow`.
+// The genome of a window's columns for the traceback's intron test: the packed
+// genome, or (seg != nullptr) the caller's segment, genome position p at seg[p - g0].
+struct SegCls {
+  const unsigned char* seg;
+  int g0;
+};
 template <int S, int LPW>
 __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint8_t* __restrict__ M,
                                       int g, int r, int cstart, int maxC, int lband, int rband,
                                       int stop, int cvlo, int cvhi, int JL, const Lane& L,
                                       const uint32_t* __restrict__ blocks, uint64_t nwords,
-                                      Tally& tal, OpWriter& ow) {
+                                      Tally& tal, OpWriter& ow, const SegCls& sg = SegCls{nullptr, 0}) {
   constexpr int WMAX = S * LPW;
   constexpr int NG = 64 / LPW;
   enum { T_WAIT = 0, T_DIAG = 1, T_VERT = 2, T_HORIZ = 3, T_DONE = 4 };
@@ -270,8 +282,9 @@ __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint
           const int cl = c, cr = c + dist - 1;
           const int gl = L.g0 + L.gstep * (cl - 1), gr = L.g0 + L.gstep * (cr - 1);
           const int lo = L.d.rev ? gr : gl, hi = L.d.rev ? gl : gr;
-          const int l1 = gclass(blocks, nwords, L, lo), l2 = gclass(blocks, nwords, L, lo + 1);
-          const int r2 = gclass(blocks, nwords, L, hi - 1), r1 = gclass(blocks, nwords, L, hi);
+          auto cls = [&](int p) { return sg.seg ? seg_class(sg.seg[p - sg.g0]) : gclass(blocks, nwords, L, p); };
+          const int l1 = cls(lo), l2 = cls(lo + 1);
+          const int r2 = cls(hi - 1), r1 = cls(hi);
           dashes = intron_type_codes(l1, l2, r2, r1, L.cdna_direction) == 0;
         }
         ow.flush();

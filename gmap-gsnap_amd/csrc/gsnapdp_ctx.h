@@ -18,7 +18,12 @@ void gsnapdp__mark(gsnapdp_ctx* ctx, hipStream_t st, int stage, int end);
 int gsnapdp__rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d_windows,
                          const int* lists, const int* counts, int list_cap, const char* d_query,
                          const char* d_query_uc, gsnapdp_result* d_results, uint32_t* d_ops,
-                         const int64_t* d_op_offsets);
+                         const int64_t* d_op_offsets, const gsnapdp_sj_window* sjw);
+// plan + bucketing + k_fill + k_rows over device windows (caller holds ctx->mu);
+// sjw != nullptr: splice-junction windows on their segments
+int gsnapdp__fill_pipeline(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d_windows, int n,
+                           const char* d_query, const char* d_query_uc, gsnapdp_result* d_results,
+                           uint32_t* d_ops, const int64_t* d_op_offsets, const gsnapdp_sj_window* sjw);
 // allocate the row-lane classes' global scratch on first use
 int gsnapdp__rows_pools(gsnapdp_ctx* ctx);
 // k_gband over the register-band lists of a genome-gap batch (gsnapdp_gband.hip)
@@ -81,7 +86,6 @@ struct gsnapdp_ctx {
   void* d_ggap_stage = nullptr;
   // splice-junction end gaps (gsnapdp_sj_*)
   int sj_cap = 0;
-  int* d_sj_lists = nullptr;        // RW_NCLS class lists of sj_cap entries, then the counts
   gsnapdp_window* d_sj_win = nullptr;  // the end-gap records k_sj_plan derives
   // op-stream compaction (gsnapdp_gather.hip): per-block op counts
   int csum_cap = 0;

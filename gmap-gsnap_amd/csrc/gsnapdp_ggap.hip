@@ -689,10 +689,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
 // produced by Dynprog_make_splicejunction_5/3) are marked unsupported.
 __global__ void k_sj_plan(const gsnapdp_sj_window* __restrict__ S, int n,
                           const char* __restrict__ q, const char* __restrict__ qu,
-                          gsnapdp_window* __restrict__ Wn, gsnapdp_result* __restrict__ res,
-                          int* __restrict__ lists, int* __restrict__ counts, int cap) {
+                          gsnapdp_window* __restrict__ Wn, gsnapdp_result* __restrict__ res) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  int cls = -1;
   if (i < n) {
     const gsnapdp_sj_window s = S[i];
     gsnapdp_window w;
@@ -727,10 +725,6 @@ __global__ void k_sj_plan(const gsnapdp_sj_window* __restrict__ S, int n,
         const unsigned char a = (unsigned char)q[(int)s.spos + step * k];
         if (seg_class(a) > 4 || (unsigned char)qu[(int)s.spos + step * k] != a) status = ST_UNSUPPORTED;
       }
-      if (status == ST_OK) {
-        cls = rows_class(d.L1, d.L2, d.W);
-        if (cls < 0) status = ST_UNSUPPORTED;
-      }
     }
     if (status != ST_OK) {
       gsnapdp_result R = {};
@@ -739,11 +733,8 @@ __global__ void k_sj_plan(const gsnapdp_sj_window* __restrict__ S, int n,
       R.length2 = s.length2;
       R.reserved = s.dynprogindex;
       res[i] = R;
+      Wn[i].kind = KIND_SKIP;  // finished here: the fill pipeline's planner skips it
     }
-  }
-  for (int c = 0; c < RW_NCLS; c++) {
-    const int slot = agg_atomic_inc(counts + c, cls == c ? 0 : -1);
-    if (cls == c) lists[(size_t)c * cap + slot] = i;
   }
 }
 
@@ -1191,7 +1182,10 @@ static int rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d
 int gsnapdp__rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d_windows,
                          const int* lists, const int* counts, int list_cap, const char* d_query,
                          const char* d_query_uc, gsnapdp_result* d_results, uint32_t* d_ops,
-                         const int64_t* d_op_offsets) {
+                         const int64_t* d_op_offsets, const gsnapdp_sj_window* sjw) {
+  if (sjw)
+    return rows_launch<true>(ctx, st, d_windows, lists, counts, list_cap, d_query, d_query_uc,
+                             d_results, d_ops, d_op_offsets, sjw);
   return rows_launch<false>(ctx, st, d_windows, lists, counts, list_cap, d_query, d_query_uc,
                             d_results, d_ops, d_op_offsets, nullptr);
 }
@@ -1210,24 +1204,19 @@ extern "C" int gsnapdp_sj_run_device(gsnapdp_ctx* ctx, const gsnapdp_sj_window* 
   HIPCHK(hipSetDevice(ctx->device));
   if (n > ctx->sj_cap) {
     const int cap = n + n / 4 + 1024;
-    (void)hipFree(ctx->d_sj_lists);
     (void)hipFree(ctx->d_sj_win);
-    ctx->d_sj_lists = nullptr;
     ctx->d_sj_win = nullptr;
-    HIPCHK(hipMalloc(&ctx->d_sj_lists, (size_t)RW_NCLS * cap * 4 + 64));
     HIPCHK(hipMalloc(&ctx->d_sj_win, (size_t)cap * sizeof(gsnapdp_window)));
     ctx->sj_cap = cap;
   }
-  if (gsnapdp__rows_pools(ctx)) return -1;
-  const int cap = ctx->sj_cap;
-  int* lists = ctx->d_sj_lists;
-  int* counts = lists + (size_t)RW_NCLS * cap;
   gsnapdp_window* dw = ctx->d_sj_win;
-  HIPCHK(hipMemsetAsync(counts, 0, 4 * RW_NCLS, st));
+  // the end-gap windows of the records (early returns finished here), then the
+  // single/end-gap pipeline on their segments: the register band (k_fill's
+  // END = 2 fill) or k_rows in segment mode
   hipLaunchKernelGGL(k_sj_plan, dim3((n + 255) / 256), dim3(256), 0, st, d_windows, n, d_query,
-                     d_query_uc, dw, d_results, lists, counts, cap);
-  return rows_launch<true>(ctx, st, dw, lists, counts, cap, d_query, d_query_uc, d_results, d_ops,
-                           d_op_offsets, d_windows);
+                     d_query_uc, dw, d_results);
+  return gsnapdp__fill_pipeline(ctx, st, dw, n, d_query, d_query_uc, d_results, d_ops, d_op_offsets,
+                                d_windows);
 }
 
 extern "C" int gsnapdp_sj_run_host(gsnapdp_ctx* ctx, const gsnapdp_sj_window* windows, int n,

@@ -36,15 +36,19 @@ GSNAPDP_HD_CONST inline int class_of_w(int W) {
   while (c < NCLASS - 1 && W > CLASS_W[c]) c++;
   return c;
 }
-// k_fill bucket key = ((W(W-1)/2 + lband) * 2 + jl) * 2 + end: W-major over
-// the (W, lband < W) triangle (W <= 48; jl the fill's tie rule; end: an end gap
-// scanned by find_best_endpoint, whose open/extend differ from a single gap's)
+// k_fill bucket key = ((W(W-1)/2 + lband) * 2 + jl) * 3 + end: W-major over
+// the (W, lband < W) triangle (W <= 48; jl the fill's tie rule; end: 0 a single
+// gap, 1 an end gap scanned by find_best_endpoint, 2 one scanned by
+// find_best_endpoint_to_queryend_indels -- end gaps' open/extend differ)
+constexpr int NEND = 3;
 GSNAPDP_HD_CONST inline int key_tri(int W) { return W * (W - 1) / 2; }
-constexpr int NKEYS = key_tri(FAST_WMAX + 1) * 4;
+constexpr int NKEYS = key_tri(FAST_WMAX + 1) * 2 * NEND;
 GSNAPDP_HD_CONST inline int fill_key(int W, int lband, int jl, int end) {
-  return ((key_tri(W) + lband) * 2 + jl) * 2 + end;
+  return ((key_tri(W) + lband) * 2 + jl) * NEND + end;
 }
-GSNAPDP_HD_CONST inline int first_key_of_w(int W) { return key_tri(W) * 4; }
+GSNAPDP_HD_CONST inline int first_key_of_w(int W) { return key_tri(W) * 2 * NEND; }
+// gsnapdp_window.kind of a window the planner skips (its result is already written)
+constexpr int KIND_SKIP = 0x5c;
 GSNAPDP_HD_CONST inline int w_of_key(int k) {  // the W whose keys hold k
   int W = 1;
   while (W < FAST_WMAX && first_key_of_w(W + 1) <= k) W++;

@@ -30,16 +30,18 @@ using namespace gsnapdp;
 
 namespace {
 
-// End gaps that k_fill scans (its END fill, below): the rank of a band cell
-// must fit END_RANK_BITS.
+// End gaps that k_fill scans (its END fills, below): 1 find_best_endpoint
+// (the rank of a band cell must fit END_RANK_BITS), 2 the last row's scan of
+// find_best_endpoint_to_queryend_indels; 0 not on the register band.
 constexpr int END_RANK_BITS = 14;
 constexpr int END_RANK_MAX = (1 << END_RANK_BITS) - 1;
-__device__ inline bool end_on_band(const Derived& d) {  // k_plan: the END fill's limits
+__device__ inline int end_kind(const Derived& d) {
 #ifdef GSNAPDP_FILL32
-  return false;  // (the live-row cap needs the 16-bit values)
+  return 0;  // (the END fills need the 16-bit values)
 #endif
-  return d.mode == 1 && d.W <= FAST_WMAX && d.L2 <= FAST_L2MAX && d.eb <= FAST_WMAX &&
-         2 * d.eb * d.L1 + d.L2 + d.eb <= END_RANK_MAX;
+  if (d.W > FAST_WMAX || d.L2 > FAST_L2MAX) return 0;
+  if (d.mode == 1) return d.eb <= FAST_WMAX && 2 * d.eb * d.L1 + d.L2 + d.eb <= END_RANK_MAX ? 1 : 0;
+  return d.mode == 2 ? 2 : 0;
 }
 
 // ------------------------------------------------------------------ k_plan
@@ -58,9 +60,10 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   int key = -1, big = -1;  // k_fill bucket key, or row-lane class
-  if (i < n) {
+  if (i < n && W[i].kind != KIND_SKIP) {
     const gsnapdp_window w = W[i];
     const Lane L = make_lane(w);
+    int ek = 0;
     if (L.d.status != ST_OK) {
       gsnapdp_result R = {};
       R.finalscore = L.d.early_score;
@@ -89,9 +92,9 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
       write_result(&res[i], w, L, 0, m, m, t, ow);
     } else if (L.d.mode == 0 && L.d.W <= FAST_WMAX && L.d.L2 <= FAST_L2MAX) {
       key = fill_key(L.d.W, L.d.lband, L.d.jl, 0);
-    } else if (ends_on_band && end_on_band(L.d)) {
-      key = fill_key(L.d.W, L.d.lband, L.d.jl, 1);
-      big_count[RW_NCLS] = 1;  // k_fill: this batch has END tasks
+    } else if (ends_on_band && (ek = end_kind(L.d)) != 0) {
+      key = fill_key(L.d.W, L.d.lband, L.d.jl, ek);
+      atomicOr(big_count + RW_NCLS, 1 << ek);  // k_fill: this batch has END tasks of kind ek
     } else {
       big = rows_class(L.d.L1, L.d.L2, L.d.W);
       if (big < 0) {  // beyond the row-lane scratch: fail loudly
@@ -104,8 +107,8 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
         res[i] = R;
       }
     }
-    keys[i] = key;
   }
+  if (i < n) keys[i] = key;
   if (key >= 0) atomicAdd(&lh[key], 1);
   const int lslot = big >= 0 ? atomicAdd(&lbig[big], 1) : 0;
   __syncthreads();
@@ -254,16 +257,27 @@ constexpr size_t FILL_REGION_DW = FILL_COLS_DEV * 64 + FILL_COLS_DEV * 16;
 //    the first best cell for '>', the last for the jump-late '>='.  The rank
 //    of (r, c) is 2*eb*r + c + eb (the band's cells in row-major order); the
 //    start (0, 0) with 0 has rank eb, below every cell's.
+// END = 2: find_best_endpoint_to_queryend_indels (:2293-2355) scans the last
+// row only.  Row L1's profile word alone has bit 31 set (no cap: rows below L1
+// cannot reach row L1), a cell offers min(H, that bit spread over 16 bits) --
+// its nogap value in row L1, 0 elsewhere -- to the column's maximum, and the
+// column's key is that value * 2^14 + (column or its complement).
+// Segment windows (seg != nullptr; Dynprog_end5/3_splicejunction,
+// use_genomicseg_p, :1535 / :1690): column c's genome is the caller's segment
+// byte seg[spos + gstep * (c - 1)] instead of the packed genome.
 struct FillOut {
   int score, br, bc;  // finalscore and the traceback's start cell
 };
 
+// (always inlined into fill_tasks: an outlined call costs a callee-saved
+// register spill per task and its own register allocation)
 template <int S, int LPW, int LOW, int JL, int END>
-__device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool active, int lane,
+__device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, bool active, int lane,
                               uint32_t* __restrict__ D, uint8_t* __restrict__ M,
                               const char* __restrict__ q, const char* __restrict__ qu,
                               const uint32_t* __restrict__ blocks, uint64_t nwords,
-                              const uint32_t* sprof, uint32_t* ring) {
+                              const uint32_t* sprof, uint32_t* ring,
+                              const gsnapdp_sj_window* __restrict__ sjw) {
   static_assert(S >= 2 && S <= 8 && LPW <= 16 && 64 % LPW == 0, "class shape");
   using RG = Rings<S, LPW>;
   static_assert(RG::WORDS <= RING_WORDS_MAX, "LDS ring budget");
@@ -271,8 +285,9 @@ __device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, boo
   constexpr int NG = 64 / LPW;
   constexpr int NAB = (WMAX - LOW) < S ? (WMAX - LOW) : S;  // local slots that may lie above the band
   constexpr FV NEGV = END ? (FV)FV_NEG_END : (FV)FV_NEG;
-  constexpr uint32_t LIVE = END ? 0x80000000u : 0u;  // END: a live row's cap (bits 16..31) is >= 2^15
-  constexpr uint32_t DEAD = (uint32_t)NEGV << 16;     // END: a row below L1
+  constexpr uint32_t LIVE = END == 1 ? 0x80000000u : 0u;  // END 1: a live row's cap (bits 16..31) is >= 2^15
+  constexpr uint32_t DEAD = (uint32_t)NEGV << 16;          // END 1: a row below L1
+  constexpr uint32_t LAST = 0x80000000u;                   // END 2: row L1
   const int j = lane % LPW;
   const int gbase = lane - j;
   const int g = lane / LPW;
@@ -295,9 +310,16 @@ __device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, boo
     gp0 = cs.P0;
     gps = cs.PS;
     xorc = cs.xorc;
+    if (sjw) {  // a segment: every column 1..L2 is inside it
+      cvlo = 1;
+      cvhi = L2;
+      gp0 = sjw[wi].spos - L.gstep;  // segment byte of column c: gp0 + gps*c
+      gps = L.gstep;
+    }
     qbase = L.qbase;
     qstep = L.qstep;
   }
+  const bool segw = sjw != nullptr;  // wave-uniform (a kernel argument)
   maxL2 = __builtin_amdgcn_readfirstlane(wave_max(L2));
   // the nogap step's constant -2*extend (= +6: k_fill serves single gaps, extend -3)
   // is folded into the LDS profile nibbles (FILL_SC_BIAS); the nogap value of a
@@ -313,8 +335,8 @@ __device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, boo
       qb = (unsigned char)q[qi] & 127u;
       ub = (unsigned char)qu[qi];
     }
-    if (END && r > L1) return DEAD;
-    return sprof[mtoff + qb] | sprof[UTAB + ub] | LIVE;
+    if (END == 1 && r > L1) return DEAD;
+    return sprof[mtoff + qb] | sprof[UTAB + ub] | LIVE | (END == 2 && r == L1 ? LAST : 0u);
   };
   const uint64_t gmax = nwords >= 3 ? (nwords - 3) / 3 : 0;  // last whole genome block
 
@@ -363,18 +385,25 @@ __device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, boo
 #pragma unroll
     for (int e = 0; e < EC; e++) {
       const int c = clo + e * LPW + j;
-      const uint32_t pos = gp0 + (uint32_t)(gps * c);
-      const uint64_t b = (uint64_t)(pos >> 5);
-      const uint64_t ptr = (b <= gmax ? b : gmax) * 3u;
-      gw[e] = blocks[ptr + ((pos & 31u) < 16 ? 1 : 0)];
-      gf[e] = blocks[ptr + 2];
+      if (segw) {  // the segment byte of column c (clamped into 1..L2; a shadow group's L2 is 0)
+        const int cc = max(1, min(c, L2));
+        gw[e] = (unsigned char)q[gp0 + (uint32_t)(gps * cc)];
+        gf[e] = 0u;
+      } else {
+        const uint32_t pos = gp0 + (uint32_t)(gps * c);
+        const uint64_t b = (uint64_t)(pos >> 5);
+        const uint64_t ptr = (b <= gmax ? b : gmax) * 3u;
+        gw[e] = blocks[ptr + ((pos & 31u) < 16 ? 1 : 0)];
+        gf[e] = blocks[ptr + 2];
+      }
     }
 #pragma unroll
     for (int e = 0; e < ER; e++) {
       const int r = rlo + e * LPW + j;
       const bool ok = r >= 1 && r <= L1;
       uint32_t w = sprof[mtoff + (ok ? (qb[e] & 127u) : 0u)] | sprof[UTAB + (ok ? ub[e] : 255u)] | LIVE;
-      if (END && r > L1) w = DEAD;
+      if (END == 1 && r > L1) w = DEAD;
+      if (END == 2 && r == L1) w |= LAST;
       if (e * LPW + j < NR) rr[r & (RG::RR - 1)] = w;
     }
 #pragma unroll
@@ -385,7 +414,8 @@ __device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, boo
       const bool ing = (uint64_t)(pos >> 5) <= gmax;  // outside the genome: N
       const int code = (int)((gw[e] >> ((bit & 15u) * 2u)) & 3u) ^ xorc;
       const bool inr = c >= cvlo && c <= cvhi;
-      const int k = !inr ? 5 : ((!ing || ((gf[e] >> bit) & 1u)) ? 4 : code);
+      int k = !inr ? 5 : ((!ing || ((gf[e] >> bit) & 1u)) ? 4 : code);
+      if (segw) k = inr ? seg_class((unsigned char)gw[e]) : 5;
       if (e * LPW + j < RING_K) cr[c & (RG::CR - 1)] = (uint8_t)k;
     }
     __builtin_amdgcn_s_waitcnt(0);  // nothing of the staging stays in flight into the column loop
@@ -401,7 +431,15 @@ __device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, boo
   // column's share, kept in Rc and stepped by dR with the lane's column.
   int ebw = 0, Rc = 0, dR = 0, Bt = 0;
   int Qs[S];
-  if constexpr (END) {
+  if constexpr (END == 2) {  // the last row's scan: R(c) = the column's share of the key
+    auto Rof = [&](int c) {
+      return ((L1 + c) * ext - (int)FV_BIAS) * (1 << END_RANK_BITS) + (JL ? c : END_RANK_MAX - c);
+    };
+    Rc = Rof(1 - j);
+    dR = Rof(2 - j) - Rc;
+    Bt = -(1 << 30);  // below every cell's key: the start (L1, 0) with NEG_INFINITY (:2302)
+  }
+  if constexpr (END == 1) {
     ebw = min(lband, rband);  // wave-uniform: derive() widens one side only
     const int kq = -ext * (1 << END_RANK_BITS) + (JL ? -2 * ebw : 2 * ebw);
 #pragma unroll
@@ -447,7 +485,7 @@ __device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, boo
     }
     // four bit planes (v1, h1, dF, dE), each a short independent chain
     uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u, gsh = 0u;
-    int bstep = -(1 << 30);  // END: this column's best scan key, less R(c)
+    int bstep = END == 2 ? 0 : -(1 << 30);  // END: this column's best scan key (END 2: value), less R(c)
     auto cell = [&](int s, FV Hr, FV Er) {
       const FV Hd = H[s], Ed = E[s], Fd = F[s];
       const uint32_t pw = pslot(s);
@@ -458,9 +496,10 @@ __device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, boo
       const FV sc = END ? (FV)__builtin_amdgcn_sbfe((int)pw, (int)gsh, 4) : (FV)__builtin_amdgcn_ubfe(pw, gsh, 4);
       const bool above = (s < NAB) && (j * S + s < stop);  // loop-invariant lane mask
       FV hn = fv_max(m1, Fd) + sc;
-      if constexpr (END) hn = fv_cap_hi(hn, pw);  // rows below L1
+      if constexpr (END == 1) hn = fv_cap_hi(hn, pw);  // rows below L1
       hn = above ? NEGV : hn;
-      if constexpr (END) bstep = max(bstep, (int)(hn << END_RANK_BITS) + Qs[s]);
+      if constexpr (END == 1) bstep = max(bstep, (int)(hn << END_RANK_BITS) + Qs[s]);
+      if constexpr (END == 2) bstep = (int)fv_max((FV)bstep, fv_min(hn, (uint32_t)((int)pw >> 31)));  // row L1 only
       const int dv = JL ? (int)(Fd - m1) : (int)(m1 - Fd);  // v1: nogap from gap2
       const int dh = JL ? (int)(Ed - Hd) : (int)(Hd - Ed);  // h1: nogap from gap1
       const int df = JL ? (int)(fp - b) : (int)(b - fp);    // dF: gap2 extends
@@ -502,7 +541,8 @@ __device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, boo
 #pragma unroll
       for (int s = 1; s < S - 1; s++) cell(s, H[s + 1], E[s + 1]);
       cell(S - 1, hb, eb);
-      if constexpr (END) Bt = max(Bt, bstep + Rc);
+      if constexpr (END == 1) Bt = max(Bt, bstep + Rc);
+      if constexpr (END == 2) Bt = max(Bt, (bstep << END_RANK_BITS) + Rc);
       const uint32_t acc = (((((av << S) | ah) << S) | af) << S) | ae;
 #ifndef EXP_NOSTORE
       D[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = acc;
@@ -533,7 +573,13 @@ __device__ FillOut fill_group(const gsnapdp_window* __restrict__ Wn, int wi, boo
 #endif
   for (; t <= minL2; t++) step(Full(), Shift(), t);
   for (; t < maxL2 + LPW; t++) step(Masked(), Shift(), t);
-  if constexpr (END) {
+  if constexpr (END == 2) {
+#pragma unroll
+    for (int o = LPW / 2; o > 0; o >>= 1) Bt = max(Bt, __shfl_xor(Bt, o));
+    const int post = Bt & END_RANK_MAX;
+    return FillOut{Bt >> END_RANK_BITS, L1, JL ? post : END_RANK_MAX - post};
+  }
+  if constexpr (END == 1) {
     // the group's best key: score, then rank (row-major order)
 #pragma unroll
     for (int o = LPW / 2; o > 0; o >>= 1) Bt = max(Bt, __shfl_xor(Bt, o));
@@ -560,7 +606,8 @@ __device__ void trace_batch(int lane, int wi, const FillOut& fo, int jl,
                             const gsnapdp_window* __restrict__ Wn, const uint32_t* __restrict__ D,
                             const uint32_t* __restrict__ blocks, uint64_t nwords,
                             gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
-                            const int64_t* __restrict__ op_off) {
+                            const int64_t* __restrict__ op_off, const gsnapdp_sj_window* __restrict__ sjw,
+                            const char* __restrict__ q) {
   constexpr int NG = 64 / LPW;
   constexpr int WMAX = S * LPW;
   const int k = lane / NG, g = lane % NG;
@@ -579,9 +626,14 @@ __device__ void trace_batch(int lane, int wi, const FillOut& fo, int jl,
   cs.init(L);
   Tally tal = {0, 0, 0, 0, 0};
   OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
-  band_traceback<S, LPW>(Dk, Mk, g, fo.br, fo.bc, maxC, L.d.lband, L.d.rband, WMAX - L.d.W, cs.cvlo,
-                         cs.cvhi, jl, L, blocks, nwords, tal, ow);
-  write_result(res + wi, w, L, fo.score, fo.br, fo.bc, tal, ow);
+  // a segment window's genome classes (the long-gap intron test) come from its segment
+  const SegCls sc = {sjw ? (const unsigned char*)q + sjw[wi].spos : nullptr, L.g0};
+  band_traceback<S, LPW>(Dk, Mk, g, fo.br, fo.bc, maxC, L.d.lband, L.d.rband, WMAX - L.d.W,
+                         sjw ? 1 : cs.cvlo, sjw ? L.d.L2 : cs.cvhi, jl, L, blocks, nwords, tal, ow, sc);
+  // Dynprog_end5/3_splicejunction score the alignment from its counts (:5541 / :6045)
+  const int score = sjw ? tal.nmatches * 3 - 5 * tal.nmismatches + tal.nopens * L.d.open + tal.nindels * L.d.ext
+                        : fo.score;
+  write_result(res + wi, w, L, score, fo.br, fo.bc, tal, ow);
 }
 
 // This wave's wave-tasks of class (S, LPW, LOW), in batches of B (<= TB_BATCH)
@@ -600,7 +652,8 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
                                         uint64_t nwords, const AS_LDS uint32_t* sprof3,
                                         AS_LDS uint32_t* ring3,
                                         AS_GLOBAL uint32_t* D1, AS_GLOBAL gsnapdp_result* res1,
-                                        AS_GLOBAL uint32_t* ops1, const AS_GLOBAL int64_t* op_off1) {
+                                        AS_GLOBAL uint32_t* ops1, const AS_GLOBAL int64_t* op_off1,
+                                        const AS_GLOBAL gsnapdp_sj_window* sjw1) {
   const gsnapdp_window* __restrict__ Wn = (const gsnapdp_window*)Wn1;
   const int* __restrict__ perm = (const int*)perm1;
   const char* __restrict__ q = (const char*)q1;
@@ -612,6 +665,7 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
   gsnapdp_result* __restrict__ res = (gsnapdp_result*)res1;
   uint32_t* __restrict__ ops = (uint32_t*)ops1;
   const int64_t* __restrict__ op_off = (const int64_t*)op_off1;
+  const gsnapdp_sj_window* __restrict__ sjw = (const gsnapdp_sj_window*)sjw1;
   constexpr int NG = 64 / LPW;
   constexpr int B = LPW < TB_BATCH ? LPW : TB_BATCH;  // tasks per traceback sweep
   const int lane = threadIdx.x & 63;
@@ -619,7 +673,8 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
   // the class's single-gap and end-gap tasks (bucket keys end in the END bit)
   // run in two calls, END = 0 then 1, each over the tasks of its kind only
   auto kind_of = [&](int t) {
-    return __builtin_amdgcn_readfirstlane(derive(Wn[perm[(size_t)t * NG]]).mode == 1 ? 1 : 0);
+    const int m = derive(Wn[perm[(size_t)t * NG]]).mode;
+    return __builtin_amdgcn_readfirstlane(m == 1 || m == 2 ? m : 0);
   };
   int t = t0;
   while (t < t1 && kind_of(t) != END) t += stride;
@@ -637,8 +692,8 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
       // the bucket's tie rule (an end5 gap's fill is reversed with !jump_late_p)
       const int jl = __builtin_amdgcn_readfirstlane(derive(Wn[w0]).jl);
       const FillOut fo =
-          jl ? fill_group<S, LPW, LOW, 1, END>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords, sprof, ring)
-             : fill_group<S, LPW, LOW, 0, END>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords, sprof, ring);
+          jl ? fill_group<S, LPW, LOW, 1, END>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords, sprof, ring, sjw)
+             : fill_group<S, LPW, LOW, 0, END>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords, sprof, ring, sjw);
       const int src = (lane % NG) * LPW;  // lane 0 of group lane % NG
       const int v_wi = __shfl(wi0, src);
       const FillOut v = {__shfl(fo.score, src), __shfl(fo.br, src), __shfl(fo.bc, src)};
@@ -650,7 +705,7 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
       do t += stride;
       while (t < t1 && kind_of(t) != END);
     }
-    trace_batch<S, LPW>(lane, my_wi, my, my_jl, Wn, D, blocks, nwords, res, ops, op_off);
+    trace_batch<S, LPW>(lane, my_wi, my, my_jl, Wn, D, blocks, nwords, res, ops, op_off, sjw, q);
   }
 }
 
@@ -664,7 +719,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
     const int* __restrict__ class_start, const char* __restrict__ q, const char* __restrict__ qu,
     const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
     uint32_t* __restrict__ dirpool, size_t wave_stride, gsnapdp_result* __restrict__ res,
-    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off, const int* __restrict__ end_flag) {
+    uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off, const int* __restrict__ end_flag,
+    const gsnapdp_sj_window* __restrict__ sjw) {
   __shared__ alignas(8) uint32_t sprof[SPROF_WORDS];
   __shared__ uint32_t rings[4][RING_WORDS_MAX];  // one per wave of the block
   for (int i = threadIdx.x; i < MLUT; i += blockDim.x)
@@ -680,7 +736,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nw = (gridDim.x * blockDim.x) >> 6;
   uint32_t* D = dirpool + (size_t)gw * wave_stride;
-  const bool has_end = *end_flag != 0;  // (the END bodies' calls are skipped otherwise)
+  // the kinds of task in the batch (bit e: END = e; k_plan sets bits 1, 2; a
+  // segment batch has end gaps only): each kind's bodies are called only when present
+  const int ends = (sjw ? 0 : 1) | *end_flag;
   int tfirst[NCLASS + 1];  // first task index of each class, then the total
   tfirst[0] = 0;
 #pragma unroll
@@ -689,29 +747,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
   // the wave takes global task indices tau = gw, gw + nw, ...; those of class c
   // are its tasks t = base_c + (tau - tfirst[c]), visited class by class
   static_assert(NCLASS <= 8, "k_fill dispatches at most 8 classes");
+#define FILL_BODY(C, E)                                                                          \
+  fill_tasks<CLASS_S[C % NCLASS], CLASS_LPW[C % NCLASS], class_low(C % NCLASS), E>(               \
+      base + tau0, base + hi, nw, (const AS_GLOBAL gsnapdp_window*)Wn, (const AS_GLOBAL int*)perm, \
+      (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu, (const AS_GLOBAL uint32_t*)blocks,      \
+      nwords, (const AS_LDS uint32_t*)sprof, (AS_LDS uint32_t*)ring, (AS_GLOBAL uint32_t*)D,       \
+      (AS_GLOBAL gsnapdp_result*)res, (AS_GLOBAL uint32_t*)ops, (const AS_GLOBAL int64_t*)op_off,  \
+      (const AS_GLOBAL gsnapdp_sj_window*)sjw);
 #define FILL_CLASS(C)                                                                            \
   if constexpr (C < NCLASS) {                                                                    \
     const int lo = tfirst[C], hi = tfirst[C + 1];                                                \
     const int tau0 = gw >= lo ? gw : gw + (lo - gw + nw - 1) / nw * nw;                          \
     if (tau0 < hi) {                                                                             \
       const int base = class_start[C] / (64 / CLASS_LPW[C]) - lo;                                \
-      fill_tasks<CLASS_S[C % NCLASS], CLASS_LPW[C % NCLASS], class_low(C % NCLASS), 0>(          \
-          base + tau0, base + hi, nw, (const AS_GLOBAL gsnapdp_window*)Wn,                        \
-          (const AS_GLOBAL int*)perm, (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu,        \
-          (const AS_GLOBAL uint32_t*)blocks, nwords, (const AS_LDS uint32_t*)sprof,               \
-          (AS_LDS uint32_t*)ring, (AS_GLOBAL uint32_t*)D, (AS_GLOBAL gsnapdp_result*)res,         \
-          (AS_GLOBAL uint32_t*)ops, (const AS_GLOBAL int64_t*)op_off);                            \
-      if (has_end)                                                                                \
-        fill_tasks<CLASS_S[C % NCLASS], CLASS_LPW[C % NCLASS], class_low(C % NCLASS), 1>(        \
-            base + tau0, base + hi, nw, (const AS_GLOBAL gsnapdp_window*)Wn,                      \
-            (const AS_GLOBAL int*)perm, (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu,      \
-            (const AS_GLOBAL uint32_t*)blocks, nwords, (const AS_LDS uint32_t*)sprof,             \
-            (AS_LDS uint32_t*)ring, (AS_GLOBAL uint32_t*)D, (AS_GLOBAL gsnapdp_result*)res,       \
-            (AS_GLOBAL uint32_t*)ops, (const AS_GLOBAL int64_t*)op_off);                          \
+      if (ends & 1) FILL_BODY(C, 0)                                                              \
+      if (ends & 2) FILL_BODY(C, 1)                                                              \
+      if (ends & 4) FILL_BODY(C, 2)                                                              \
     }                                                                                            \
   }
   FILL_CLASS(0) FILL_CLASS(1) FILL_CLASS(2) FILL_CLASS(3)
   FILL_CLASS(4) FILL_CLASS(5) FILL_CLASS(6) FILL_CLASS(7)
+#undef FILL_BODY
 #undef FILL_CLASS
 }
 
@@ -817,7 +873,6 @@ extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   (void)hipFree(ctx->d_ggap_pool);
   (void)hipFree(ctx->d_gband_pool);
   (void)hipFree(ctx->d_ggap_stage);
-  (void)hipFree(ctx->d_sj_lists);
   (void)hipFree(ctx->d_sj_win);
   (void)hipFree(ctx->d_stage);
   (void)hipFree(ctx->d_csum);
@@ -860,21 +915,19 @@ static int ensure_capacity(gsnapdp_ctx* ctx, int n) {
   return 0;
 }
 
-extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_windows, int n,
-                                  const char* d_query, const char* d_query_uc,
-                                  gsnapdp_result* d_results, uint32_t* d_ops,
-                                  const int64_t* d_op_offsets, void* stream_v) {
-  if (!ctx) return -1;
-  if (n <= 0) return 0;
-  hipStream_t st = stream_v ? (hipStream_t)stream_v : ctx->stream;
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  HIPCHK(hipSetDevice(ctx->device));
+// The single/end-gap pipeline over windows already on the device: plan, bucket,
+// k_fill, then k_rows for the windows the register band does not take.  sjw:
+// the splice-junction records the windows were derived from (segment genome),
+// or nullptr.  The caller holds ctx->mu.
+int gsnapdp__fill_pipeline(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d_windows, int n,
+                           const char* d_query, const char* d_query_uc, gsnapdp_result* d_results,
+                           uint32_t* d_ops, const int64_t* d_op_offsets, const gsnapdp_sj_window* sjw) {
   if (ensure_capacity(ctx, n)) return -1;
   int* hist = ctx->d_small;
   int* cursor = hist + NKEYS;
   int* class_start = cursor + NKEYS;
   int* big_count = class_start + NCLASS + 1;  // RW_NCLS row-lane class counts
-  HIPCHK(hipMemsetAsync(big_count, 0, 4 * (RW_NCLS + 1), st));  // + k_fill's END flag
+  HIPCHK(hipMemsetAsync(big_count, 0, 4 * (RW_NCLS + 1), st));  // + k_fill's END flags
   if (gsnapdp__rows_pools(ctx)) return -1;
   const int tb = 1024, nb = (n + tb - 1) / tb;
   auto mark = [&](int stage, int end) { gsnapdp__mark(ctx, st, stage, end); };
@@ -895,15 +948,28 @@ extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_wind
   mark(2, 0);
   hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, st, d_windows, ctx->d_perm, class_start,
                      d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_dirpool,
-                     WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets, big_count + RW_NCLS);
+                     WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets, big_count + RW_NCLS, sjw);
   mark(2, 1);
   mark(3, 0);
   if (gsnapdp__rows_launch(ctx, st, d_windows, ctx->d_big_list, big_count, ctx->cap_n, d_query,
-                           d_query_uc, d_results, d_ops, d_op_offsets))
+                           d_query_uc, d_results, d_ops, d_op_offsets, sjw))
     return -1;
   mark(3, 1);
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+extern "C" int gsnapdp_run_device(gsnapdp_ctx* ctx, const gsnapdp_window* d_windows, int n,
+                                  const char* d_query, const char* d_query_uc,
+                                  gsnapdp_result* d_results, uint32_t* d_ops,
+                                  const int64_t* d_op_offsets, void* stream_v) {
+  if (!ctx) return -1;
+  if (n <= 0) return 0;
+  hipStream_t st = stream_v ? (hipStream_t)stream_v : ctx->stream;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  return gsnapdp__fill_pipeline(ctx, st, d_windows, n, d_query, d_query_uc, d_results, d_ops,
+                                d_op_offsets, nullptr);
 }
 
 extern "C" int gsnapdp_run_host(gsnapdp_ctx* ctx, const gsnapdp_window* windows, int n,

@@ -57,3 +57,24 @@ def test_gpu_sj_matches_oracle_mix(seed):
     ref["dynprogindex"] = ores["reserved"]
     compare(res, pairs, npairs, ref, oflat, onp, "sj mix %d" % seed)
     assert np.sum(b.windows["length1"] > 64) > 100  # the 64-row stripe classes run too
+
+
+def test_gpu_sj_register_band_matches_rowlane(monkeypatch):
+    """The same splice-junction batch on the register band (k_fill's END = 2 fill
+    over the segment) and on k_rows' segment mode (GSNAPDP_ENDS_ROWLANE=1):
+    identical results, endpoints and pair lists."""
+    g = W.synthetic_genome(1_000_000, seed=53, n_rate=0.002)
+    b = W.sj_windows(g, 6000, seed=53)
+    out = []
+    for rowlane in ("0", "1"):
+        monkeypatch.setenv("GSNAPDP_ENDS_ROWLANE", rowlane)
+        ctx = Context(np.zeros(64, np.uint32))
+        res, ops, off = ctx.sj_run(b.windows, b.query, b.query_uc)
+        pairs, npairs = ctx.sj_all_pairs(b.windows, b.query, b.query_uc, res, ops, off)
+        out.append((res, pairs, npairs))
+    (r0, p0, n0), (r1, p1, n1) = out
+    for f in FIELDS + ("bestr", "bestc", "status", "reserved", "nops"):
+        bad = np.nonzero(r0[f] != r1[f])[0]
+        assert bad.size == 0, "%s differs at %s (band %s rowlane %s)" % (f, bad[:8], r0[f][bad[:8]], r1[f][bad[:8]])
+    assert np.array_equal(n0, n1) and all(np.array_equal(p0[f], p1[f]) for f in PAIR.names)
+    assert np.sum(r0["status"] == 0) > 5000

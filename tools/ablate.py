@@ -1,4 +1,4 @@
-"""Per-stage timing of the C2 bench workload for one library build (diagnostics)."""
+"""Per-stage timing of the C2 bench workload (C3 with ABLATE_C3=1) for one library build (diagnostics)."""
 import os, sys, json
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -8,9 +8,14 @@ from gsnapdp import Context, op_offsets
 from gsnapdp import workload as W
 from gsnapdp.records import RESULT
 
-genome = W.synthetic_genome(64_000_000, seed=1)
-blocks = W.pack_genome(genome)
-batch = W.c2_windows(genome, n=100_000, seed=2, indel_frac=float(os.environ.get("INDEL_FRAC", "0.3")))
+if os.environ.get("ABLATE_C3") == "1":  # the headline batch (bench.py's C3)
+    g3 = W.c3_genome(seed=3)
+    blocks = g3.blocks
+    batch = W.c3_windows(g3, n=1_000_000, seed=33)
+else:
+    genome = W.synthetic_genome(64_000_000, seed=1)
+    blocks = W.pack_genome(genome)
+    batch = W.c2_windows(genome, n=100_000, seed=2, indel_frac=float(os.environ.get("INDEL_FRAC", "0.3")))
 n = len(batch)
 off = op_offsets(batch.windows)
 ctx = Context(blocks, mode=0, device=0)
