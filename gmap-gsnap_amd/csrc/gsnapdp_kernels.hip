@@ -55,8 +55,10 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
                        int* __restrict__ big_count, int list_cap, int ends_on_band) {
   __shared__ int lh[NKEYS];  // block-local histogram: one global atomic per key per block
   __shared__ int lbig[RW_NCLS], lbase[RW_NCLS];  // block-local row-lane list appends
+  __shared__ int lend;                             // block-local END task kinds (bits 1, 2)
   for (int k = threadIdx.x; k < NKEYS; k += blockDim.x) lh[k] = 0;
   if (threadIdx.x < RW_NCLS) lbig[threadIdx.x] = 0;
+  if (threadIdx.x == 0) lend = 0;
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   int key = -1, big = -1;  // k_fill bucket key, or row-lane class
@@ -94,7 +96,7 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
       key = fill_key(L.d.W, L.d.lband, L.d.jl, 0);
     } else if (ends_on_band && (ek = end_kind(L.d)) != 0) {
       key = fill_key(L.d.W, L.d.lband, L.d.jl, ek);
-      atomicOr(big_count + RW_NCLS, 1 << ek);  // k_fill: this batch has END tasks of kind ek
+      atomicOr(&lend, 1 << ek);  // k_fill: this batch has END tasks of kind ek
     } else {
       big = rows_class(L.d.L1, L.d.L2, L.d.W);
       if (big < 0) {  // beyond the row-lane scratch: fail loudly
@@ -116,6 +118,7 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
   // k_rows writes each window's own result slot)
   if (threadIdx.x < RW_NCLS)
     lbase[threadIdx.x] = lbig[threadIdx.x] > 0 ? atomicAdd(big_count + threadIdx.x, lbig[threadIdx.x]) : 0;
+  if (threadIdx.x == 0 && lend != 0) atomicOr(big_count + RW_NCLS, lend);
   for (int k = threadIdx.x; k < NKEYS; k += blockDim.x)
     if (lh[k] > 0) atomicAdd(&hist[k], lh[k]);
   __syncthreads();
@@ -670,8 +673,8 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
   constexpr int B = LPW < TB_BATCH ? LPW : TB_BATCH;  // tasks per traceback sweep
   const int lane = threadIdx.x & 63;
   const int g = lane / LPW;
-  // the class's single-gap and end-gap tasks (bucket keys end in the END bit)
-  // run in two calls, END = 0 then 1, each over the tasks of its kind only
+  // the class's single-gap and end-gap tasks (bucket keys end in the END kind)
+  // run in one call per kind, END = 0, 1, 2, each over the tasks of its kind only
   auto kind_of = [&](int t) {
     const int m = derive(Wn[perm[(size_t)t * NG]]).mode;
     return __builtin_amdgcn_readfirstlane(m == 1 || m == 2 ? m : 0);
