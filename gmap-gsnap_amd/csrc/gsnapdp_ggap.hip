@@ -744,6 +744,9 @@ __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
                             gsnapdp_ggap_result* __restrict__ res,
                             gsnapdp_ggap_trace* __restrict__ trc, int* __restrict__ lists,
                             int* __restrict__ counts, int cap, int use_band) {
+  __shared__ int lcnt[GG_NLISTS], lbase[GG_NLISTS];  // block-local list appends
+  if (threadIdx.x < GG_NLISTS) lcnt[threadIdx.x] = 0;
+  __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   int cls = -1;
   if (i < n) {
@@ -795,12 +798,14 @@ __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
       trc[i] = X;
     }
   }
-  // one list append per class per wave
-#pragma unroll
-  for (int c = 0; c < GG_NLISTS; c++) {
-    const int pos = agg_atomic_inc(counts + c, cls == c ? 0 : -1);
-    if (cls == c) lists[(size_t)c * cap + pos] = i;
-  }
+  // one global reservation per non-empty list per block (list order is free:
+  // every window writes its own result slot)
+  const int slot = cls >= 0 ? atomicAdd(&lcnt[cls], 1) : 0;
+  __syncthreads();
+  if (threadIdx.x < GG_NLISTS)
+    lbase[threadIdx.x] = lcnt[threadIdx.x] > 0 ? atomicAdd(counts + threadIdx.x, lcnt[threadIdx.x]) : 0;
+  __syncthreads();
+  if (cls >= 0) lists[(size_t)cls * cap + lbase[cls] + slot] = i;
 }
 
 
