@@ -721,10 +721,24 @@ __global__ void k_sj_plan(const gsnapdp_sj_window* __restrict__ S, int n,
       const Derived d = derive(w);
       const int step = s.kind == GSNAPDP_END5_GAP ? -1 : 1;
       if (d.status != ST_OK) status = ST_UNSUPPORTED;
-      for (int k = 0; k < s.length2 && status == ST_OK; k++) {
-        const unsigned char a = (unsigned char)q[(int)s.spos + step * k];
-        if (seg_class(a) > 4 || (unsigned char)qu[(int)s.spos + step * k] != a) status = ST_UNSUPPORTED;
+      // the segment's bytes [lo, lo + length2) (either direction): A C G T N and
+      // the same in both buffers; a dword at a time where both are aligned
+      const int lo = step > 0 ? (int)s.spos : (int)s.spos - (s.length2 - 1);
+      const unsigned char* a = (const unsigned char*)q + lo;
+      const unsigned char* b = (const unsigned char*)qu + lo;
+      auto byte_ok = [](unsigned x, unsigned y) { return x == y && seg_class((unsigned char)x) <= 4; };
+      bool ok = d.status == ST_OK;
+      int k = 0;
+      for (; ok && k < s.length2 && ((uintptr_t)(a + k) & 3u); k++) ok = byte_ok(a[k], b[k]);
+      if (((uintptr_t)(b + k) & 3u) == 0) {
+        for (; ok && k + 4 <= s.length2; k += 4) {
+          const uint32_t x = *(const uint32_t*)(a + k), y = *(const uint32_t*)(b + k);
+          ok = x == y && seg_class(x & 255u) <= 4 && seg_class((x >> 8) & 255u) <= 4 &&
+               seg_class((x >> 16) & 255u) <= 4 && seg_class(x >> 24) <= 4;
+        }
       }
+      for (; ok && k < s.length2; k++) ok = byte_ok(a[k], b[k]);
+      if (!ok) status = ST_UNSUPPORTED;
     }
     if (status != ST_OK) {
       gsnapdp_result R = {};
