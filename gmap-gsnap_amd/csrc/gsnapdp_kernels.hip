@@ -140,7 +140,7 @@ __device__ inline int padded_bucket(int W, int h) {
 // allocation, so no per-batch memset is needed)
 __global__ void k_scan(int* __restrict__ hist, int* __restrict__ cursor,
                        int* __restrict__ class_start, int* __restrict__ perm) {
-  __shared__ int part[1024];
+  __shared__ int wtot[16];  // the 16 waves' totals
   constexpr int PER = (NKEYS + 1023) / 1024;
   const int tid = threadIdx.x;
   const int lo = tid * PER;
@@ -155,15 +155,23 @@ __global__ void k_scan(int* __restrict__ hist, int* __restrict__ cursor,
     p[i] = padded_bucket(W, h[i]);
     s += p[i];
   }
-  part[tid] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-    int v = tid >= off ? part[tid - off] : 0;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
+  // exclusive scan over the block: within each wave by shuffles, then the waves' totals
+  const int ln = tid & 63, wv = tid >> 6;
+  int x = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (ln >= o) x += y;
   }
-  int run = part[tid] - s;
+  if (ln == 63) wtot[wv] = x;
+  __syncthreads();
+  int wbase = 0, total = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    wbase += k < wv ? wtot[k] : 0;
+    total += wtot[k];
+  }
+  int run = wbase + x - s;
 #pragma unroll
   for (int i = 0; i < PER; i++) {
     const int k = lo + i;
@@ -179,10 +187,10 @@ __global__ void k_scan(int* __restrict__ hist, int* __restrict__ cursor,
     int wlo = 0;
     for (int c = 0; c < NCLASS; c++) {
       const int kfirst = first_key_of_w(wlo + 1);
-      class_start[c] = kfirst < NKEYS ? cursor[kfirst] : part[1023];
+      class_start[c] = kfirst < NKEYS ? cursor[kfirst] : total;
       wlo = CLASS_W[c];
     }
-    class_start[NCLASS] = part[1023];
+    class_start[NCLASS] = total;
   }
 }
 
