@@ -1,6 +1,6 @@
-"""GPU parity of Dynprog_end5/3_splicejunction (k_sj_plan + k_rows in segment
-mode, through the C-ABI) against the reference's golden vectors and the CPU
-restatement they pin."""
+"""GPU parity of Dynprog_end5/3_splicejunction (k_sj_plan, then k_fill's END = 2
+segment fills on the register band or k_rows in segment mode, through the
+C-ABI) against the reference's golden vectors and the CPU restatement they pin."""
 import os
 
 import numpy as np
