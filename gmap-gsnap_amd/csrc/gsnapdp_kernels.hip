@@ -723,7 +723,7 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
 // All register-band classes in one persistent launch: the wave-tasks of the
 // classes form one index space (class by class), so one class's tail overlaps
 // the next class's work and empty classes cost nothing.  Register budget:
-// 128 VGPRs (4 waves per SIMD); the few spills this forces sit in the task
+// 512 / GSNAPDP_FILL_WAVES VGPRs (168 at 3 waves per SIMD); any spills sit in the task
 // call's prologue/epilogue and loop preheaders, not in the column loops.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FILL_WAVES, 8))) void k_fill(
     const gsnapdp_window* __restrict__ Wn, const int* __restrict__ perm,
