@@ -212,7 +212,7 @@ constexpr int GB_L2MAX = 256;            // longest flank on the register band
 constexpr int GB_LIST0 = 3;
 constexpr int GG_NLISTS = GB_LIST0 + 2 * (NCLASS - 1);
 #ifndef GB_WAVES_PER_SIMD
-#define GB_WAVES_PER_SIMD 3
+#define GB_WAVES_PER_SIMD 2  // k_gband (256 VGPRs): C4 score 0.65 ms; 3 waves 0.70, 4 waves 0.95 (spills)
 #endif
 // per-wave scratch of k_gband in dwords (layout in gsnapdp_gband.hip)
 constexpr int GB_WAVE_DW = 2 * (GB_L2MAX + 4) * 80 + 2 * 32 * ((GB_L2MAX + 4) / 4 + 1) +
