@@ -46,7 +46,7 @@ static_assert(GB_LIST0 == GG_NCLS && GG_NLISTS <= 16, "genome-gap lists (the cou
 #define GG_SMALL_WORDS_CFG 1280
 #endif
 #ifndef GG_WAVES
-#define GG_WAVES 4
+#define GG_WAVES 4  // C4 prob k_ggap: 4 waves 1.62 ms; 2: 2.17, 3: 2.16, 5: 2.24, 6: 2.72
 #endif
 constexpr int GG_SMALL_WORDS = GG_SMALL_WORDS_CFG;  // LDS words per window, RL = 32 (2 per wave)
 constexpr int GG_SMALL_BLOCKS = 160 * 1024 / (8 * GG_SMALL_WORDS * 4);  // blocks per CU that fit in LDS
