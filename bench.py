@@ -51,12 +51,24 @@ C4_WINDOWS = 200_000          # intron windows per config-4 step
 C5_READS = 100_000            # reads per config-5 step (3 DP windows each)
 
 
-def window_bytes(w: np.ndarray, nops: np.ndarray) -> np.ndarray:
+def window_bytes(w: np.ndarray, nops: np.ndarray, uc_aliased: bool = False) -> np.ndarray:
     """Algorithmic HBM bytes of one window (DESIGN.md "Roofline"): query and
-    uppercase query (L1 each), the packed genome blocks its columns touch
+    uppercase query (L1 each; L1 once when the caller passes one buffer for
+    both, as this bench does), the packed genome blocks its columns touch
     (12 B per 32 nt), the 68 B descriptor, the 48 B result and 4 B per op."""
     span_blocks = (w["length2"].astype(np.int64) + 31) // 32 + 1
-    return (2 * w["length1"].astype(np.int64) + 12 * span_blocks + 68 + 48 + 4 * nops.astype(np.int64))
+    qb = (1 if uc_aliased else 2) * w["length1"].astype(np.int64)
+    return qb + 12 * span_blocks + 68 + 48 + 4 * nops.astype(np.int64)
+
+
+def profile_order(path: str):
+    """Sort key of a committed profile file: its round and version (r2v10 after
+    r2v9, r3v1 after both; r1_v1 / r2c3a style tags too), then the name."""
+    import re
+    m = re.match(r"r(\d+)_?[a-z]*?v?(\d*)", os.path.basename(path))
+    if not m:
+        return (-1, -1, os.path.basename(path))
+    return (int(m.group(1)), int(m.group(2) or 0), os.path.basename(path))
 
 
 def band_cells(w: np.ndarray) -> int:
@@ -77,10 +89,10 @@ def band_cells(w: np.ndarray) -> int:
 def pmc_traffic(kernel: str, workload: str):
     """HBM bytes per launch of `kernel` on `workload` from the committed
     rocprofv3 PMC passes (profiles/*_traffic.json, written by
-    tools/pmc_traffic.py), or None.  Last file by name wins."""
+    tools/pmc_traffic.py), or None.  The newest round/version wins (profile_order)."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), key=profile_order):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
@@ -98,7 +110,7 @@ def rocprof_kernel_ms(kernel: str, workload: str):
     import glob
     best = None
     pat = os.path.join(ROOT, "profiles", "*_%s_kernel_stats.csv" % workload.lower())
-    for f in sorted(glob.glob(pat)):
+    for f in sorted(glob.glob(pat), key=profile_order):
         try:
             for row in csv.DictReader(open(f)):
                 name = row.get("Name", "").replace("(anonymous namespace)::", "")
@@ -474,7 +486,8 @@ def main() -> None:
                           dtype=RESULT)
     Wd = (wl["extraband"].astype(np.int64) * 2 + 1 + np.abs(wl["length2"].astype(np.int64) - wl["length1"]))
     dom = (Wd <= 48) & (wl["length2"] <= 640)  # k_fill's windows (FAST_WMAX, FAST_L2MAX)
-    dom_bytes = float(window_bytes(wl[dom], res_l["nops"][dom]).sum())
+    # d_q is passed as both query and query_uc: its bytes count once
+    dom_bytes = float(window_bytes(wl[dom], res_l["nops"][dom], uc_aliased=True).sum())
     dom_ms = kernel_ms.get(DOMINANT, float("nan"))
     achieved_gbs = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms == dom_ms else None
     fill_ms = sum(v for k, v in kernel_ms.items() if k.startswith("k_fill"))
@@ -553,6 +566,9 @@ def main() -> None:
                          "traffic": traffic[0] if traffic else None,
                          "traffic_source": traffic[1] if traffic else None,
                          "algorithmic_bytes": round(dom_bytes), "kernel": DOMINANT,
+                         "bytes_note": "per window: L1 query bytes (query and query_uc are one buffer here, "
+                                       "counted once) + 12 B per genome block touched + 68 B descriptor + "
+                                       "48 B result + 4 B per op",
                          "kernel_ms": round(dom_ms, 4), "kernel_ms_rocprof": round(rp[0], 4) if rp else None,
                          "rocprof_source": rp[1] if rp else None, "windows_in_kernel": int(dom.sum())},
             "roofline_valu": {"bound": "valu-int32", "unit": "int32 ops/s",

@@ -962,6 +962,7 @@ gsnapdp_List_T Dynprog_genome_gap(
   if (t.status == gsnapdp::ST_UNSUPPORTED)
     fatal("genome-gap window outside the reference's domain (the reference aborts or reads past its matrices)");
   if (t.status == gsnapdp::ST_OPS_OVERFLOW) fatal("op stream overflow");
+  if (t.status == gsnapdp::ST_INTERNAL) fatal("genome-gap kernel invariant failed (bridge cell outside a flank)");
   // out-parameters exactly as the reference writes them on each path
   *nmatches = *nmismatches = *nopens = *nindels = 0;  // :4853-4854
   *left_prob = *right_prob = 0.0;

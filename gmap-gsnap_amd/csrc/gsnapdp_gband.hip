@@ -465,8 +465,13 @@ struct GCand {  // a bridge candidate: total score, scan order 2*rL + loop, the 
 
 // One wave-task of NG windows.  Not inlined (the same code for both tie
 // rules); the LDS pointers keep their address space through the call.
+#ifdef GB_INLINE
+#define GB_GROUP_ATTR __attribute__((always_inline)) inline  // diagnostic builds
+#else
+#define GB_GROUP_ATTR __noinline__
+#endif
 template <int S, int LPW, int JL>
-__device__ __noinline__ void gband_group(const gsnapdp_ggap_window* __restrict__ Wn, int wi,
+__device__ GB_GROUP_ATTR void gband_group(const gsnapdp_ggap_window* __restrict__ Wn, int wi,
                                          bool active, int lane, uint32_t* __restrict__ wpool,
                                          const char* __restrict__ q, const char* __restrict__ qu,
                                          const uint32_t* __restrict__ blocks, uint64_t nwords,
@@ -562,7 +567,7 @@ __device__ __noinline__ void gband_group(const gsnapdp_ggap_window* __restrict__
         const bool inner = r >= 1 && r < L1;
         const int cR = code[FL_RIGHT][i], cL = code[FL_LEFT][i];
         ri[FL_LEFT][GB_CHK(r, GB_RW, 6)] = inner ? (cR == 1 ? sL[1] : cR == 2 ? sL[2] : cR == 3 ? sL[3] : cR == 4 ? sL[4] : sL[0]) : 0u;
-        ri[FL_RIGHT][r] = inner ? (cL == 1 ? sR[1] : cL == 2 ? sR[2] : cL == 3 ? sR[3] : cL == 4 ? sR[4] : sR[0]) : 0u;
+        ri[FL_RIGHT][GB_CHK(r, GB_RW, 15)] = inner ? (cL == 1 ? sR[1] : cL == 2 ? sR[2] : cL == 3 ? sR[3] : cL == 4 ? sR[4] : sR[0]) : 0u;
       }
     }
   }
@@ -600,8 +605,8 @@ __device__ __noinline__ void gband_group(const gsnapdp_ggap_window* __restrict__
       const int rLc = rL < L1 ? rL : 1, rRc = max(0, L1 - rLc);
       kl[e] = rb[FL_LEFT][GB_CHK(rLc, GB_RW, 7)];
       kr[e] = rb[FL_RIGHT][GB_CHK(rRc, GB_RW, 8)];
-      hl[e] = (int)dg[FL_LEFT][rLc];
-      hr[e] = (int)dg[FL_RIGHT][rRc];
+      hl[e] = (int)dg[FL_LEFT][GB_CHK(rLc, GB_RW, 16)];
+      hr[e] = (int)dg[FL_RIGHT][GB_CHK(rRc, GB_RW, 17)];
       nl[e] = km != GSNAPDP_KNOWN_NONE ? krec[rLc] : 0;  // left_known[rL], right_known[rR]
       nr[e] = km != GSNAPDP_KNOWN_NONE ? krec[G.L2L + rRc] : 0;
     }
@@ -635,8 +640,17 @@ __device__ __noinline__ void gband_group(const gsnapdp_ggap_window* __restrict__
   memset(&X, 0, sizeof(X));
   int rc = 0;
   const bool lead = active && j == 0;
+  // The outcome re-reads the window record instead of keeping the fields it
+  // needs live across both fills (the laundered index defeats CSE with the
+  // first load).  Round 3: with gband_group inlined, a build kept offset2L
+  // live across the fills and traceback and stored a corrupted value for
+  // jump-late windows (DESIGN.md §4 k_gband); the short live range removes
+  // that exposure in every build.
+  int wo_i = wi;
+  asm volatile("" : "+v"(wo_i));
+  const gsnapdp_ggap_window wo = Wn[wo_i];
   if (lead) {
-    R.dynprogindex = w.dynprogindex;
+    R.dynprogindex = wo.dynprogindex;
     R.bridge_ok = 1;
     X.status = ST_OK;
     // the chosen columns' dinucleotides and known flags (:3331-3550)
@@ -646,14 +660,14 @@ __device__ __noinline__ void gband_group(const gsnapdp_ggap_window* __restrict__
     const bool kL = km != GSNAPDP_KNOWN_NONE && cL < G.L2L && krec[cL] != 0;
     const bool kR = km != GSNAPDP_KNOWN_NONE && cR < G.L2R && krec[G.L2L + cR] != 0;
     int it;
-    const int sI = intron_score(it, dl, dr, w.cdna_direction, G.canon, w.finalp);
-    const int finalscore = w.halfp ? best.score - sI / 2 : best.score;
+    const int sI = intron_score(it, dl, dr, wo.cdna_direction, G.canon, wo.finalp);
+    const int finalscore = wo.halfp ? best.score - sI / 2 : best.score;
     R.introntype = best.score > BRIDGE_INIT ? it : 0;
     rc = finalscore >= 0 ? 1 : 0;
     // novel splicing off with a site-level IIT: both chosen sites must be known (:4090-4096)
     if (rc == 1 && km == GSNAPDP_KNOWN_SITES)
       rc = kL && kR;
-    if (w.finalp && tables == nullptr) rc = -2;
+    if (wo.finalp && tables == nullptr) rc = -2;
     if (rc == -2) {
       X.status = ST_UNSUPPORTED;
       R.returned_null = 1;
@@ -662,14 +676,21 @@ __device__ __noinline__ void gband_group(const gsnapdp_ggap_window* __restrict__
       R.finalscore = finalscore;
       R.returned_null = rc == 0;
     }
+    // guard: the chosen cells lie inside both flanks (a violated invariant is
+    // reported, never traced: the sweep's loads are bounded by these columns)
+    if (rc == 1 && ((uint32_t)cL > (uint32_t)G.L2L || (uint32_t)cR > (uint32_t)G.L2R ||
+                    (uint32_t)rLb > (uint32_t)L1)) {
+      X.status = ST_INTERNAL;
+      rc = -3;
+    }
     if (rc == 1) {
-      if (w.finalp) {  // :4104-4108 (a known site has probability 1.0, :3215, :3255)
-        R.left_prob = kL ? 1.0 : left_site_prob(w, cL, blocks, nwords, tables);
-        R.right_prob = kR ? 1.0 : right_site_prob(w, cR, blocks, nwords, tables);
+      if (wo.finalp) {  // :4104-4108 (a known site has probability 1.0, :3215, :3255)
+        R.left_prob = kL ? 1.0 : left_site_prob(wo, cL, blocks, nwords, tables);
+        R.right_prob = kR ? 1.0 : right_site_prob(wo, cR, blocks, nwords, tables);
       }
-      R.new_leftgenomepos = w.offset2L + (best.cL - 1);
-      R.new_rightgenomepos = w.revoffset2R - (best.cR - 1);
-      R.exonhead = (w.offset1 + L1 - 1) - (rRb - 1);
+      R.new_leftgenomepos = wo.offset2L + (best.cL - 1);
+      R.new_rightgenomepos = wo.revoffset2R - (best.cR - 1);
+      R.exonhead = (wo.offset1 + L1 - 1) - (rRb - 1);
       X.brL = rLb;
       X.bcL = best.cL;
       X.brR = rRb;
@@ -726,7 +747,7 @@ __device__ __noinline__ void gband_group(const gsnapdp_ggap_window* __restrict__
       R.returned_null = 1;
       X.npairs = 0;
     }
-    R.dynprogindex = step_dpi(w.dynprogindex);
+    R.dynprogindex = step_dpi(wo.dynprogindex);
   }
   res[wi] = R;
   trc[wi] = X;

@@ -1244,6 +1244,8 @@ extern "C" int gsnapdp_sj_run_host(gsnapdp_ctx* ctx, const gsnapdp_sj_window* wi
                                    const int64_t* op_offsets) {
   if (!ctx) return -1;
   if (n <= 0) return 0;
+  // one host round trip at a time: the staging buffer is the context's
+  std::lock_guard<std::mutex> host_lock(ctx->host_mu);
   HIPCHK(hipSetDevice(ctx->device));
   const size_t nops = (size_t)op_offsets[n];
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -1457,6 +1459,8 @@ extern "C" int gsnapdp_cgap_run_host(gsnapdp_ctx* ctx, const gsnapdp_cgap_window
                                      const int64_t* op_offsets) {
   if (!ctx) return -1;
   if (n <= 0) return 0;
+  // one host round trip at a time: the staging buffer is the context's
+  std::lock_guard<std::mutex> host_lock(ctx->host_mu);
   HIPCHK(hipSetDevice(ctx->device));
   const size_t nops = (size_t)op_offsets[n];
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };

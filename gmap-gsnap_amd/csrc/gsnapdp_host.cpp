@@ -461,7 +461,7 @@ extern "C" int gsnapdp_ggap_expand(gsnapdp_ctx* ctx, const gsnapdp_ggap_window* 
                                    const uint32_t* ops, const char* query, const char* query_uc,
                                    gsnapdp_pair* pairs, int cap) {
   if (!ctx || !w || !res || !tr) return -1;
-  if (tr->status == ST_OPS_OVERFLOW) return -1;
+  if (tr->status == ST_OPS_OVERFLOW || tr->status == ST_INTERNAL) return -1;
   if (res->returned_null || tr->status != ST_OK) return 0;
   const uint32_t* prof = gsnapdp__host_prof(ctx);
   HostGenome G = {gsnapdp__host_blocks(ctx), gsnapdp__host_nwords(ctx), w->chroffset, w->chrhigh,

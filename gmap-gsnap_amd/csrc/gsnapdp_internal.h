@@ -59,7 +59,9 @@ GSNAPDP_HD_CONST inline int w_of_key(int k) {  // the W whose keys hold k
 enum { MT_HIGHQ = 0, MT_MEDQ = 1, MT_LOWQ = 2, MT_ENDQ = 3 };
 
 // Window status (gsnapdp_result.status)
-enum { ST_OK = 0, ST_EARLY = 1, ST_OPS_OVERFLOW = 2, ST_ZEROED = 3, ST_UNSUPPORTED = 4 };
+// ST_INTERNAL: a kernel invariant failed (k_gband's bridge cells outside the
+// flanks); the window is not traced and every host path reports an error
+enum { ST_OK = 0, ST_EARLY = 1, ST_OPS_OVERFLOW = 2, ST_ZEROED = 3, ST_UNSUPPORTED = 4, ST_INTERNAL = 6 };
 
 // Derived per-window parameters (device + host), restating the parameter
 // selection of Dynprog_single_gap (dynprog.c:4471-4519) and

@@ -346,6 +346,8 @@ extern "C" int gsnapdp_micro_run_host(gsnapdp_ctx* ctx, const gsnapdp_micro_wind
                                       gsnapdp_micro_result* results) {
   if (!ctx) return -1;
   if (n <= 0) return 0;
+  // one host round trip at a time: the staging buffer is the context's
+  std::lock_guard<std::mutex> host_lock(ctx->host_mu);
   HIPCHK(hipSetDevice(ctx->device));
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t szw = al((size_t)n * sizeof(gsnapdp_micro_window));

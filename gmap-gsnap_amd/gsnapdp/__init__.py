@@ -27,6 +27,7 @@ LIB_PATH = os.environ.get("GSNAPDP_LIB") or os.path.join(PKG, "lib", "libgsnapdp
 TABLES_PATH = os.path.join(PKG, "data", "maxent_hr_tables.bin")
 
 _lib = None
+ST_INTERNAL = 6  # a kernel invariant failed (gsnapdp_internal.h)
 
 
 class GsnapdpError(RuntimeError):
@@ -250,6 +251,9 @@ class Context:
                                          _p(ops), _p(off))
         if rc != 0:
             raise GsnapdpError("gsnapdp_ggap_run_host: %s" % lib().gsnapdp_last_error().decode())
+        bad = np.nonzero(trc["status"] == ST_INTERNAL)[0]
+        if bad.size:
+            raise GsnapdpError("genome-gap kernel invariant failed in windows %s" % bad[:8])
         return res, trc, ops, off
 
     def ggap_run_device(self, d_windows: int, n: int, d_query: int, d_query_uc: int, d_results: int,

@@ -1,0 +1,207 @@
+/*
+ * gsnapdp_oracle_abi.c -- TEST INFRASTRUCTURE ONLY (never shipped, never on a GPU box).
+ *
+ * The batched C-ABI of include/gsnapdp.h served on the CPU by the oracle's
+ * restatement (oracle/dp_oracle.c), for the subset the drop-in's known-site
+ * ends use: end gaps (gsnapdp_run_host / gsnapdp_expand), splice-junction ends
+ * (gsnapdp_sj_run_host / gsnapdp_sj_expand) and MaxEnt.  It exists so that the
+ * drop-in's host control flow (gmap-gsnap_amd/csrc/gsnapdp_dropin.cpp) can be
+ * linked, without a GPU, against the reference's own splicetrie.o / pairpool.o /
+ * list.o and run under AddressSanitizer (oracle/Makefile `asan`,
+ * tests/test_dropin_asan_cpu.py): the production configuration of
+ * Dynprog_end5/3_known (dynprog.c:6414-6943) with the host program's
+ * Splicetrie_solve_end5/3 (splicetrie.c:881, 952).
+ *
+ * The op stream between run and expand is this file's own: ops[0] of a window
+ * is an index into a table of pair lists that run_host filled.  Every other
+ * entry point aborts.
+ */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/gsnapdp.h"
+#include "../../oracle/dp_oracle.h"
+
+struct gsnapdp_ctx {
+  int mode;
+};
+
+typedef struct {
+  gsnapdp_pair *p;
+  int n;
+} stash_t;
+static stash_t *stash;
+static size_t nstash, capstash;
+static pthread_mutex_t stash_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static uint32_t put(const gsnapdp_pair *p, int n) {
+  uint32_t id;
+  pthread_mutex_lock(&stash_mu);
+  if (nstash == capstash) {
+    capstash = capstash ? 2 * capstash : 256;
+    stash = (stash_t *)realloc(stash, capstash * sizeof(stash_t));
+  }
+  stash[nstash].p = (gsnapdp_pair *)malloc((size_t)(n > 0 ? n : 1) * sizeof(gsnapdp_pair));
+  memcpy(stash[nstash].p, p, (size_t)n * sizeof(gsnapdp_pair));
+  stash[nstash].n = n;
+  id = (uint32_t)nstash++;
+  pthread_mutex_unlock(&stash_mu);
+  return id;
+}
+
+static int get(uint32_t id, gsnapdp_pair *out, int cap) {
+  int n;
+  pthread_mutex_lock(&stash_mu);
+  if (id >= nstash) {
+    pthread_mutex_unlock(&stash_mu);
+    fprintf(stderr, "oracle ABI: unknown op stream %u\n", id);
+    abort();
+  }
+  n = stash[id].n;
+  if (n > cap) n = -1;
+  else memcpy(out, stash[id].p, (size_t)n * sizeof(gsnapdp_pair));
+  pthread_mutex_unlock(&stash_mu);
+  return n;
+}
+
+static void unserved(const char *f) {
+  fprintf(stderr, "oracle ABI: %s is not served on the CPU\n", f);
+  abort();
+}
+
+gsnapdp_ctx *gsnapdp_create(int device, const uint32_t *blocks, size_t nblocks_u32, int mode) {
+  gsnapdp_ctx *c = (gsnapdp_ctx *)calloc(1, sizeof(gsnapdp_ctx));
+  (void)device;
+  (void)nblocks_u32;
+  c->mode = mode;
+  orc_init(mode);
+  orc_set_genome(blocks);
+  return c;
+}
+void gsnapdp_destroy(gsnapdp_ctx *ctx) { free(ctx); }
+const char *gsnapdp_last_error(void) { return "oracle ABI"; }
+void *gsnapdp_host_alloc(size_t bytes) { return malloc(bytes); }
+void gsnapdp_host_free(void *p) { free(p); }
+int gsnapdp_load_maxent_tables(gsnapdp_ctx *ctx, const double *tables, size_t ndoubles) {
+  (void)ctx;
+  return orc_maxent_load(tables, ndoubles);
+}
+int gsnapdp_maxent_host(gsnapdp_ctx *ctx, const uint8_t *model, const uint32_t *splice_pos,
+                        const uint32_t *chroffset, double *out, int n) {
+  int i;
+  (void)ctx;
+  for (i = 0; i < n; i++) {
+    switch (model[i]) {
+      case 0: out[i] = orc_maxent_donor(splice_pos[i], chroffset[i]); break;
+      case 1: out[i] = orc_maxent_acceptor(splice_pos[i], chroffset[i]); break;
+      case 2: out[i] = orc_maxent_antidonor(splice_pos[i], chroffset[i]); break;
+      default: out[i] = orc_maxent_antiacceptor(splice_pos[i], chroffset[i]); break;
+    }
+  }
+  return 0;
+}
+
+/* one window at a time through the oracle's batch drivers; the pairs go to the
+ * stash and ops[op_offsets[i]] names them */
+int gsnapdp_run_host(gsnapdp_ctx *ctx, const gsnapdp_window *windows, int n, const char *query,
+                     const char *query_uc, size_t query_bytes, gsnapdp_result *results,
+                     uint32_t *ops, const int64_t *op_offsets) {
+  int i;
+  (void)ctx;
+  (void)query_bytes;
+  for (i = 0; i < n; i++) {
+    const int64_t cap = 2 * (int64_t)(windows[i].length1 + windows[i].length2) + 16;
+    int64_t po[2] = {0, cap};
+    int32_t np = 0;
+    gsnapdp_pair *p = (gsnapdp_pair *)malloc((size_t)cap * sizeof(gsnapdp_pair));
+    orc_run_batch(&windows[i], 1, query, query_uc, &results[i], p, po, &np, 1);
+    results[i].status = 0;
+    ops[op_offsets[i]] = put(p, np);
+    free(p);
+  }
+  return 0;
+}
+
+int gsnapdp_expand(gsnapdp_ctx *ctx, const gsnapdp_window *w, const gsnapdp_result *res,
+                   const uint32_t *ops, const char *query, const char *query_uc,
+                   gsnapdp_pair *pairs, int cap, int *finalscore) {
+  (void)ctx;
+  (void)w;
+  (void)query;
+  (void)query_uc;
+  if (finalscore) *finalscore = res->finalscore;
+  return get(ops[0], pairs, cap);
+}
+
+int gsnapdp_sj_run_host(gsnapdp_ctx *ctx, const gsnapdp_sj_window *windows, int n,
+                        const char *query, const char *query_uc, size_t query_bytes,
+                        gsnapdp_result *results, uint32_t *ops, const int64_t *op_offsets) {
+  int i;
+  (void)ctx;
+  (void)query_bytes;
+  for (i = 0; i < n; i++) {
+    const int64_t cap = 2 * (int64_t)(windows[i].length1 + windows[i].length2) + 16;
+    int64_t po[2] = {0, cap};
+    int32_t np = 0;
+    gsnapdp_pair *p = (gsnapdp_pair *)malloc((size_t)cap * sizeof(gsnapdp_pair));
+    orc_run_sj_batch(&windows[i], 1, query, query_uc, &results[i], p, po, &np);
+    results[i].status = 0;
+    ops[op_offsets[i]] = put(p, np);
+    free(p);
+  }
+  return 0;
+}
+
+int gsnapdp_sj_expand(gsnapdp_ctx *ctx, const gsnapdp_sj_window *w, const gsnapdp_result *res,
+                      const uint32_t *ops, const char *query, const char *query_uc,
+                      gsnapdp_pair *pairs, int cap) {
+  (void)ctx;
+  (void)w;
+  (void)res;
+  (void)query;
+  (void)query_uc;
+  return get(ops[0], pairs, cap);
+}
+
+int gsnapdp_ggap_run_host(gsnapdp_ctx *c, const gsnapdp_ggap_window *w, int n, const char *q,
+                          const char *u, size_t b, gsnapdp_ggap_result *r, gsnapdp_ggap_trace *t,
+                          uint32_t *o, const int64_t *off) {
+  (void)c, (void)w, (void)n, (void)q, (void)u, (void)b, (void)r, (void)t, (void)o, (void)off;
+  unserved("gsnapdp_ggap_run_host");
+  return -1;
+}
+int gsnapdp_ggap_expand(gsnapdp_ctx *c, const gsnapdp_ggap_window *w, const gsnapdp_ggap_result *r,
+                        const gsnapdp_ggap_trace *t, const uint32_t *o, const char *q, const char *u,
+                        gsnapdp_pair *p, int cap) {
+  (void)c, (void)w, (void)r, (void)t, (void)o, (void)q, (void)u, (void)p, (void)cap;
+  unserved("gsnapdp_ggap_expand");
+  return -1;
+}
+int gsnapdp_cgap_run_host(gsnapdp_ctx *c, const gsnapdp_cgap_window *w, int n, const char *q,
+                          const char *u, size_t b, gsnapdp_cgap_result *r, uint32_t *o,
+                          const int64_t *off) {
+  (void)c, (void)w, (void)n, (void)q, (void)u, (void)b, (void)r, (void)o, (void)off;
+  unserved("gsnapdp_cgap_run_host");
+  return -1;
+}
+int gsnapdp_cgap_expand(gsnapdp_ctx *c, const gsnapdp_cgap_window *w, const gsnapdp_cgap_result *r,
+                        const uint32_t *o, const char *q, const char *u, const char *s2,
+                        gsnapdp_pair *p, int cap) {
+  (void)c, (void)w, (void)r, (void)o, (void)q, (void)u, (void)s2, (void)p, (void)cap;
+  unserved("gsnapdp_cgap_expand");
+  return -1;
+}
+int gsnapdp_micro_run_host(gsnapdp_ctx *c, const gsnapdp_micro_window *w, int n, const char *q,
+                           const char *u, size_t b, gsnapdp_micro_result *r) {
+  (void)c, (void)w, (void)n, (void)q, (void)u, (void)b, (void)r;
+  unserved("gsnapdp_micro_run_host");
+  return -1;
+}
+int gsnapdp_micro_expand(gsnapdp_ctx *c, const gsnapdp_micro_window *w, const gsnapdp_micro_result *r,
+                         const char *q, const char *u, gsnapdp_pair *p, int cap) {
+  (void)c, (void)w, (void)r, (void)q, (void)u, (void)p, (void)cap;
+  unserved("gsnapdp_micro_expand");
+  return -1;
+}

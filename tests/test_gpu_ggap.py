@@ -154,3 +154,26 @@ def test_gpu_ggap_ragged_batches_with_shadow_groups(n):
     ores, opairs, ooff, onp = O.run_ggap_batch(w, b.query, b.query_uc)
     oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
     compare(w, res, trc, pairs, npairs, ores, oflat, onp, "ragged %d" % n)
+
+
+@pytest.mark.parametrize("jl", ["mixed", "all"])
+def test_gpu_gband_jump_late_batches(jl):
+    """Round-3 regression for the k_gband fault of round 2 (DESIGN.md §4 k_gband):
+    register-band genome gaps with jump_late_p = 1 in every band class, in a
+    batch large enough to reuse every wave's scratch several times.  A build
+    that corrupted a long-lived window field produced wrong new_leftgenomepos
+    here; the kernel's invariant guard turns a bad bridge cell into an error."""
+    rng = np.random.default_rng(77)
+    g, b = W.c4_windows(W.synthetic_genome(16_000_000, seed=4), 100_000, seed=4)
+    w = b.windows.copy()
+    w["jump_late_p"] = rng.integers(0, 2, len(w)) if jl == "mixed" else 1
+    # wider bands too (the S = 8 classes): extraband_paired 10 on a third of the windows
+    w["extraband_paired"][::3] = 10
+    blocks = W.pack_genome(g)
+    ctx = Context(blocks)
+    res, trc, ops, off = ctx.ggap_run(w, b.query, b.query_uc)
+    pairs, npairs = ctx.ggap_all_pairs(w, b.query, b.query_uc, res, trc, ops, off)
+    O.setup(blocks)
+    ores, opairs, ooff, onp = O.run_ggap_batch(w, b.query, b.query_uc)
+    oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
+    compare(w, res, trc, pairs, npairs, ores, oflat, onp, "jump-late %s" % jl)

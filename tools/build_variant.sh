@@ -1,13 +1,13 @@
 #!/bin/bash
-# Diagnostics: build libgsnapdp.so with extra -D flags on one kernel source into exp/NAME/.
+# Diagnostics: build libgsnapdp.so with extra -D flags on one kernel source into gpuexp/NAME/ (git-ignored; it travels with gpurun: delete it after the experiment).
 # usage: [SRC=ggap|gband|kernels] bash tools/build_variant.sh NAME [-DFLAG ...]
-#        then GSNAPDP_LIB=exp/NAME/libgsnapdp.so python tools/ablate.py (or ablate_ggap.py)
+#        then GSNAPDP_LIB=gpuexp/NAME/libgsnapdp.so python tools/ablate.py (or ablate_ggap.py)
 set -e
 NAME=$1; shift
 SRC=${SRC:-kernels}
 cd "$(dirname "$0")/../gmap-gsnap_amd"
 make -s lib/gsnapdp_kernels.o lib/gsnapdp_ggap.o lib/gsnapdp_gband.o lib/gsnapdp_micro.o lib/gsnapdp_gather.o lib/gsnapdp_host.o
-O=../exp/$NAME; mkdir -p $O
+O=../gpuexp/$NAME; mkdir -p $O
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function "$@" \
   -c csrc/gsnapdp_$SRC.hip -o $O/gsnapdp_$SRC.o
 OBJS="lib/gsnapdp_micro.o lib/gsnapdp_gather.o lib/gsnapdp_host.o"
