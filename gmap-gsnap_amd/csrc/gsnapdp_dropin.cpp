@@ -728,13 +728,24 @@ SolveFn solver(bool end5) {
 
 extern "C" {
 
+static const int stats_order[6] = {F_GAP, F_SJ, F_GGAP, F_CGAP, F_MICRO, F_MAXENT};
+
+// the round-1 layout, kept for existing callers: windows per family, then the
+// gap family's batch count and largest batch
 int Gsnapdp_dropin_stats(unsigned long* out, int n) {
-  static const int order[6] = {F_GAP, F_SJ, F_GGAP, F_CGAP, F_MICRO, F_MAXENT};
+  std::lock_guard<std::mutex> lock(gb.m);
+  for (int i = 0; i < 6 && i < n; i++) out[i] = gb.windows[stats_order[i]];
+  if (n > 6) out[6] = gb.batches[F_GAP];
+  if (n > 7) out[7] = gb.maxbatch[F_GAP];
+  return 8;
+}
+
+int Gsnapdp_dropin_stats2(unsigned long* out, int n) {
   std::lock_guard<std::mutex> lock(gb.m);
   for (int i = 0; i < 6; i++) {
-    if (i < n) out[i] = gb.windows[order[i]];
-    if (6 + i < n) out[6 + i] = gb.batches[order[i]];
-    if (12 + i < n) out[12 + i] = gb.maxbatch[order[i]];
+    if (i < n) out[i] = gb.windows[stats_order[i]];
+    if (6 + i < n) out[6 + i] = gb.batches[stats_order[i]];
+    if (12 + i < n) out[12 + i] = gb.maxbatch[stats_order[i]];
   }
   return 18;
 }
@@ -984,7 +995,7 @@ gsnapdp_List_T Dynprog_genome_gap(
   // in the constrained known-intron mode (NONINTRON, :3695)
   if (w.known_mode == GSNAPDP_KNOWN_INTRONS) *introntype = 0;
   else if (!use_probabilities_p && r.finalscore != (halfp ? -50000 : -100000)) *introntype = r.introntype;
-  if (t.brL == 0) return nullptr;  // bridge rejected (:4084-4101)
+  if (!t.bridge_accepted) return nullptr;  // bridge rejected (:4084-4101)
   *new_leftgenomepos = r.new_leftgenomepos;
   *new_rightgenomepos = r.new_rightgenomepos;
   *exonhead = r.exonhead;

@@ -691,6 +691,7 @@ __device__ GB_GROUP_ATTR void gband_group(const gsnapdp_ggap_window* __restrict_
       R.new_leftgenomepos = wo.offset2L + (best.cL - 1);
       R.new_rightgenomepos = wo.revoffset2R - (best.cR - 1);
       R.exonhead = (wo.offset1 + L1 - 1) - (rRb - 1);
+      X.bridge_accepted = 1;
       X.brL = rLb;
       X.bcL = best.cL;
       X.brR = rRb;

@@ -509,6 +509,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
         R.new_leftgenomepos = w.offset2L + (best.cL - 1);
         R.new_rightgenomepos = w.revoffset2R - (best.cR - 1);
         R.exonhead = (w.offset1 + G.L1 - 1) - (best.rR - 1);
+        X.bridge_accepted = 1;
         X.brL = best.rL;
         X.bcL = best.cL;
         X.brR = best.rR;

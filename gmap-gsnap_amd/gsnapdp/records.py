@@ -48,8 +48,9 @@ assert GGAP_RESULT.itemsize == 64
 GGAP_TRACE = np.dtype([
     ("brL", "<i4"), ("bcL", "<i4"), ("brR", "<i4"), ("bcR", "<i4"),
     ("nops_right", "<i4"), ("nops_left", "<i4"), ("status", "<i4"), ("npairs", "<i4"),
+    ("bridge_accepted", "<i4"), ("reserved", "<i4"),
 ])
-assert GGAP_TRACE.itemsize == 32
+assert GGAP_TRACE.itemsize == 40
 
 CGAP_WINDOW = np.dtype([
     ("length1L", "<i4"), ("length1R", "<i4"), ("length2", "<i4"),

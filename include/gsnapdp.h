@@ -192,12 +192,17 @@ typedef struct gsnapdp_ggap_result {
  * left flank's (from (brL, bcL)); gsnapdp_ggap_expand replays them.
  * status: 0 ok, 1 early return, 2 op overflow, 4 unsupported (the reference
  * aborts or reads outside its matrices, or no MaxEnt tables were loaded for a
- * window that needs them).  npairs = length of the returned list (0 = NULL). */
+ * window that needs them, 6 kernel invariant failed).  npairs = length of the
+ * returned list (0 = NULL).  bridge_accepted = 1 when bridge_intron_gap took a
+ * candidate and accepted it (:4084-4101): the new intron ends, exonhead and
+ * probabilities are then the reference's out-parameters (0: rejected or early). */
 typedef struct gsnapdp_ggap_trace {
   int32_t brL, bcL, brR, bcR;
   int32_t nops_right, nops_left;
   int32_t status;
   int32_t npairs;
+  int32_t bridge_accepted;
+  int32_t reserved;
 } gsnapdp_ggap_trace;
 
 /* One cDNA-insertion window (Dynprog_cdna_gap, dynprog.c:4578-4793).  The

@@ -233,10 +233,16 @@ int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device)
 
 /* Counters of this process's GPU work, per entry-point family in the order
  * gap (single / end5 / end3), splice junction, genome gap, cDNA gap, microexon,
- * MaxEnt: out[0..5] = windows (or positions) run, out[6..11] = GPU batches,
- * out[12..17] = the largest batch (concurrent callers of any entry point are
- * combined into shared batches).  Writes min(n, 18) values; returns 18. */
+ * MaxEnt (concurrent callers of any entry point are combined into shared
+ * batches).
+ * Gsnapdp_dropin_stats (the round-1 layout): out[0..5] = windows (or
+ * positions) run, out[6] = gap batches, out[7] = the largest gap batch.
+ * Writes min(n, 8) values; returns 8.
+ * Gsnapdp_dropin_stats2: out[0..5] = windows, out[6..11] = GPU batches,
+ * out[12..17] = the largest batch, per family.  Writes min(n, 18) values;
+ * returns 18. */
 int Gsnapdp_dropin_stats(unsigned long* out, int n);
+int Gsnapdp_dropin_stats2(unsigned long* out, int n);
 
 /* ---- genome_hr subset (the reference's genome_hr.c is a missing blob;
  * gmap-gsnap_amd/csrc/genome_hr_sites.c): the setup calls gmap.c makes

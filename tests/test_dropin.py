@@ -704,7 +704,7 @@ def test_dropin_concurrent_callers_are_batched(golden_dir, tmp_path):
         L.Dynprog_free(ctypes.byref(ctypes.c_void_p(dp)))
 
     def run(nthreads):
-        L.Gsnapdp_dropin_stats(stats, 18)
+        L.Gsnapdp_dropin_stats2(stats, 18)
         b0 = stats[6]
         bad = []
         ts = [threading.Thread(target=worker, args=(range(t, len(W), nthreads), bad)) for t in range(nthreads)]
@@ -714,7 +714,7 @@ def test_dropin_concurrent_callers_are_batched(golden_dir, tmp_path):
         for t in ts:
             t.join()
         el = time.perf_counter() - t0
-        L.Gsnapdp_dropin_stats(stats, 18)
+        L.Gsnapdp_dropin_stats2(stats, 18)
         return el, stats[6] - b0, bad
 
     t1, b1, bad1 = run(1)
@@ -854,7 +854,7 @@ def test_dropin_mixed_families_concurrent_callers_are_batched(golden_dir, tmp_pa
             L.Dynprog_free(ctypes.byref(ctypes.c_void_p(d)))
 
     stats0 = (ctypes.c_ulong * 18)()
-    L.Gsnapdp_dropin_stats(stats0, 18)
+    L.Gsnapdp_dropin_stats2(stats0, 18)
     bad = []
     ts = [threading.Thread(target=worker, args=(range(t, len(tasks), 16), bad)) for t in range(16)]
     for t in ts:
@@ -862,7 +862,7 @@ def test_dropin_mixed_families_concurrent_callers_are_batched(golden_dir, tmp_pa
     for t in ts:
         t.join()
     stats = (ctypes.c_ulong * 18)()
-    L.Gsnapdp_dropin_stats(stats, 18)
+    L.Gsnapdp_dropin_stats2(stats, 18)
     d = [stats[k] - stats0[k] for k in range(12)]
     print("mixed families, 16 threads: windows gap %d ggap %d maxent %d; batches gap %d ggap %d maxent %d; "
           "largest gap %d ggap %d maxent %d" % (d[0], d[2], d[5], d[6], d[8], d[11], stats[12], stats[14],
