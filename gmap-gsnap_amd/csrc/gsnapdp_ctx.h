@@ -90,6 +90,9 @@ struct gsnapdp_ctx {
   // op-stream compaction (gsnapdp_gather.hip): per-block op counts
   int csum_cap = 0;
   int64_t* d_csum = nullptr;
+  // score_introns batches (gsnapdp_score_introns_host): device staging
+  size_t si_cap = 0;
+  char* d_si_stage = nullptr;
   // host round trips (gsnapdp_run_host): one at a time per context
   std::mutex host_mu;
   void* h_small = nullptr;          // pinned: the compaction header

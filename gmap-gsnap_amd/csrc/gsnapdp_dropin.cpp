@@ -8,6 +8,7 @@
 // There is no CPU fallback: without a gfx950 device the first call aborts,
 // as the reference aborts on its own fatal conditions.
 #include <dlfcn.h>
+#include <stddef.h>
 #include <malloc.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -112,7 +113,7 @@ void ensure_tables() {
 // the owners, which expand their own op streams into their own Pairpools.
 // No global lock is held across a GPU round trip; one thread alone sees
 // batches of one.
-enum Fam { F_GAP, F_GGAP, F_CGAP, F_SJ, F_MICRO, F_MAXENT, F_N };
+enum Fam { F_GAP, F_GGAP, F_CGAP, F_SJ, F_MICRO, F_MAXENT, F_INTRONS, F_N };
 
 struct Req {
   int fam;
@@ -154,6 +155,12 @@ struct MaxReq : Req {
   double out = 0.0;
   MaxReq() : Req(F_MAXENT) {}
 };
+struct IntronReq : Req {  // one score_introns path
+  gsnapdp_intron_path p;
+  std::vector<gsnapdp_intron> introns;
+  gsnapdp_intron_scores out;
+  IntronReq() : Req(F_INTRONS) {}
+};
 
 // Page-locked host arrays of the leader's batches (gsnapdp_host_alloc), grown
 // geometrically and kept for the life of the process.
@@ -191,7 +198,7 @@ struct StatsAtExit {
   ~StatsAtExit() {
     if (!getenv("GSNAPDP_DROPIN_STATS")) return;
     static const char* names[F_N] = {"gap", "genome_gap", "cdna_gap", "splicejunction", "microexon",
-                                     "maxent"};
+                                     "maxent", "score_introns"};
     fprintf(stderr, "gsnapdp_dropin:");
     for (int f = 0; f < F_N; f++)
       fprintf(stderr, " %s %lu in %lu batches (largest %lu, %.3f s);", names[f], gb.windows[f],
@@ -338,6 +345,25 @@ void run_family(gsnapdp_ctx* c, int fam, std::vector<Req*>& reqs) {
       }
       check(gsnapdp_maxent_host(c, M, P, P + n, O, (int)n), "maxent");
       for (size_t i = 0; i < n; i++) ((MaxReq*)reqs[i])->out = O[i];
+      break;
+    }
+    case F_INTRONS: {  // every queued path in one k_introns launch
+      std::vector<gsnapdp_intron_path> P(n);
+      std::vector<gsnapdp_intron> I;
+      for (size_t i = 0; i < n; i++) {
+        IntronReq* x = (IntronReq*)reqs[i];
+        P[i] = x->p;
+        P[i].first_intron = (int32_t)I.size();
+        P[i].nintrons = (int32_t)x->introns.size();
+        for (gsnapdp_intron t : x->introns) {
+          t.path = (int32_t)i;
+          I.push_back(t);
+        }
+      }
+      std::vector<gsnapdp_intron_scores> O(n);
+      check(gsnapdp_score_introns_host(c, P.data(), (int)n, I.data(), (int)I.size(), O.data()),
+            "gsnapdp_score_introns_host");
+      for (size_t i = 0; i < n; i++) ((IntronReq*)reqs[i])->out = O[i];
       break;
     }
   }
@@ -590,6 +616,16 @@ struct RefList {
   void* first;
   RefList* rest;
 };
+// ... through the fields score_introns reads (pairdef.h:9-32; flat, so the
+// chars and bools pack exactly as in Pair_T)
+struct RefPairGap {
+  int querypos;
+  unsigned genomepos;
+  int refquerypos, aapos, queryjump, genomejump, aaphase_g, aaphase_e, dynprogindex;
+  char cdna, comp, genome, aa_g, aa_e;
+  unsigned char gapp, knowngapp;  // bool (bool.h: unsigned char)
+};
+static_assert(offsetof(RefPairGap, gapp) == 41 && offsetof(RefPairGap, knowngapp) == 42, "Pair_T layout");
 
 // binary_search (dynprog.c:5068-5090)
 int binary_search(int lowi, int highi, const unsigned* positions, unsigned goal) {
@@ -1460,6 +1496,87 @@ void Maxent_hr_setup(unsigned int* ref_blocks) {  // maxent_hr.c:27195
   std::lock_guard<std::mutex> lock(g.mu);
   if (g.blocks && ref_blocks != g.blocks) fatal("Maxent_hr_setup blocks differ from the genome");
   if (!g.blocks) g.blocks = ref_blocks;  // sized in ctx() unless Dynprog_setup sizes it
+}
+
+// score_introns (stage3.c:7935-8162), the reference's static function with its
+// signature (non-WASTE build), for a stage3.c that calls it here: the path's
+// introns are picked on the host (gsnapdp_path_introns), the splicing IIT of
+// Dynprog_setup (= Stage3_setup's, gmap.c:3828-3835) is asked about each site
+// exactly where the reference asks, and the MaxEnt probabilities, sums and
+// averages run in one k_introns launch shared with concurrent callers.  The
+// returned list is the path's own cells in reverse order, which is what the
+// reference's pop / List_push_existing loop builds.
+gsnapdp_List_T Gsnapdp_score_introns(double* avg_donor_score, double* avg_acceptor_score, int* nbadintrons,
+                                     gsnapdp_List_T path, int cdna_direction, gsnapdp_bool watsonp, int chrnum,
+                                     gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh,
+                                     gsnapdp_Genomicpos_T chrpos, char* genomicuc_ptr, int genomiclength,
+                                     int nullgap, gsnapdp_bool use_genomicseg_p) {
+  (void)chrhigh;
+  (void)genomicuc_ptr;
+  if (use_genomicseg_p) fatal("score_introns on a genomic segment (maxent.c) is not served");
+  std::vector<gsnapdp_path_pair> pp;
+  for (const RefList* l = (const RefList*)path; l; l = l->rest) {
+    const RefPairGap* x = (const RefPairGap*)l->first;
+    gsnapdp_path_pair q;
+    q.genomepos = x->genomepos;
+    q.queryjump = x->queryjump;
+    q.genomejump = x->genomejump;
+    q.gapp = x->gapp;
+    q.knowngapp = x->knowngapp;
+    q.comp = (uint8_t)x->comp;
+    q.pad = 0;
+    pp.push_back(q);
+  }
+  IntronReq req;
+  const int n = gsnapdp_path_introns(pp.data(), (int)pp.size(), nullgap, 0, nullptr, 0);
+  if (n < 0) fatal("score_introns: an intron at the end of the path (the reference dereferences NULL)");
+  req.introns.resize((size_t)n);
+  gsnapdp_path_introns(pp.data(), (int)pp.size(), nullgap, 0, req.introns.data(), n);
+  if (g.iit) {  // known sites score 1.0 (:7997-8046, :8069-8116)
+    auto typed = [](auto f, const char* name) {
+      if (!f) f = (decltype(f))dlsym(RTLD_DEFAULT, name);
+      if (!f) fatal(std::string("a splicing IIT was given but the host program's ") + name + " is not linked");
+      return f;
+    };
+    const auto exists = typed(&IIT_exists_with_divno_typed_signed, "IIT_exists_with_divno_typed_signed");
+    const int divno = g.divint_crosstable[chrnum];
+    const unsigned gl1 = (unsigned)genomiclength - 1U;
+    for (gsnapdp_intron& t : req.introns) {
+      unsigned pd, pa;
+      int sign;
+      if (cdna_direction == +1) {
+        pd = watsonp ? chrpos + t.left_genomepos + 1U : chrpos + gl1 - t.left_genomepos;
+        pa = watsonp ? chrpos + t.right_genomepos : chrpos + gl1 - t.right_genomepos + 1U;
+        sign = watsonp ? +1 : -1;
+      } else if (cdna_direction == -1) {
+        pa = watsonp ? chrpos + t.left_genomepos + 1U : chrpos + gl1 - t.left_genomepos;
+        pd = watsonp ? chrpos + t.right_genomepos : chrpos + gl1 - t.right_genomepos + 1U;
+        sign = watsonp ? -1 : +1;
+      } else {
+        continue;
+      }
+      if (cdna_direction == +1) {  // the reference asks about the donor first
+        t.known_donor = exists(g.iit, divno, pd, pd + 1U, g.donor_typeint, sign) ? 1 : 0;
+        t.known_acceptor = exists(g.iit, divno, pa, pa + 1U, g.acceptor_typeint, sign) ? 1 : 0;
+      } else {
+        t.known_acceptor = exists(g.iit, divno, pa, pa + 1U, g.acceptor_typeint, sign) ? 1 : 0;
+        t.known_donor = exists(g.iit, divno, pd, pd + 1U, g.donor_typeint, sign) ? 1 : 0;
+      }
+    }
+  }
+  req.p.chroffset = chroffset;
+  req.p.chrpos = chrpos;
+  req.p.genomiclength = genomiclength;
+  req.p.cdna_direction = cdna_direction;
+  req.p.watsonp = watsonp ? 1 : 0;
+  req.p.first_intron = 0;
+  req.p.nintrons = n;
+  req.p.pad = 0;
+  submit(shared_ctx(true), &req);
+  *avg_donor_score = req.out.avg_donor_score;
+  *avg_acceptor_score = req.out.avg_acceptor_score;
+  *nbadintrons = req.out.nbadintrons;
+  return path ? List_reverse(path) : path;
 }
 
 double Maxent_hr_donor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomicpos_T chroffset) {

@@ -647,3 +647,36 @@ extern "C" int gsnapdp_cgap_expand(gsnapdp_ctx* ctx, const gsnapdp_cgap_window* 
     if (n < cap) pairs[n] = pl[i];
   return n;
 }
+
+// score_introns' walk over a path (stage3.c:7960-8146): a gap pair is an
+// intron when it is neither past nullgap (:7971) nor query-heavy
+// (queryjump > genomejump + EXTRAQUERYGAP, :7979) and its genome jump exceeds
+// the query jump by more than MININTRONLEN_FINAL (:7987); its leftpair is the
+// next pair of the list (path->first after the pop), its rightpair the
+// previous one (pairs->first).  The reference dereferences NULL for an intron
+// at either end of the list; that is -1 here.
+extern "C" int gsnapdp_path_introns(const gsnapdp_path_pair* pairs, int npairs, int nullgap, int path,
+                                    gsnapdp_intron* out, int cap) {
+  constexpr int EXTRAQUERYGAP = 10;        // stage3.h:29
+  constexpr int MININTRONLEN_FINAL = 50;   // stage3.c:52
+  if (npairs < 0 || (npairs > 0 && !pairs)) return -1;
+  int n = 0;
+  for (int i = 0; i < npairs; i++) {
+    const gsnapdp_path_pair& p = pairs[i];
+    if (!p.gapp || p.queryjump > nullgap || p.queryjump > p.genomejump + EXTRAQUERYGAP) continue;
+    if (p.genomejump > p.queryjump + MININTRONLEN_FINAL) {
+      if (i == 0 || i + 1 >= npairs) return -1;
+      if (n < cap && out) {
+        gsnapdp_intron& x = out[n];
+        x.left_genomepos = pairs[i + 1].genomepos;
+        x.right_genomepos = pairs[i - 1].genomepos;
+        x.path = path;
+        x.comp = p.comp;
+        x.knowngapp = p.knowngapp;
+        x.known_donor = x.known_acceptor = 0;
+      }
+      n++;
+    }
+  }
+  return n;
+}

@@ -792,6 +792,63 @@ __global__ void k_maxent(const uint8_t* __restrict__ model, const uint32_t* __re
   out[i] = maxent_prob(model[i], pos[i], chroff[i], blocks, nwords, T);
 }
 
+// --------------------------------------------------------------- k_introns
+// score_introns (stage3.c:7935-8162) for a batch of paths, one lane per path:
+// the lane walks its path's introns in list order, takes the two MaxEnt site
+// probabilities of each (the same maxent_prob as k_maxent; 1.0 for a site the
+// splicing IIT knows, :7997-8046 / :8069-8116), sums them in that order and
+// divides by the intron count, as the reference does in double precision.
+// Positions are the reference's unsigned Genomicpos_T arithmetic.
+__global__ void k_introns(const gsnapdp_intron_path* __restrict__ P, int npaths,
+                          const gsnapdp_intron* __restrict__ I, gsnapdp_intron_scores* __restrict__ out,
+                          const uint32_t* __restrict__ blocks, uint64_t nwords, const double* __restrict__ T) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npaths) return;
+  const gsnapdp_intron_path x = P[p];
+  const uint32_t gl1 = (uint32_t)x.genomiclength - 1u;
+  double sd = 0.0, sa = 0.0;
+  int nbad = 0, nin = 0;
+  for (int k = 0; k < x.nintrons; k++) {
+    const gsnapdp_intron t = I[x.first_intron + k];
+    int md, ma;        // models of the donor and acceptor sites
+    uint32_t pd, pa;   // their splicesitepos
+    if (x.cdna_direction == 1) {
+      if (x.watsonp) {
+        md = GSNAPDP_DONOR, pd = x.chrpos + t.left_genomepos + 1u;
+        ma = GSNAPDP_ACCEPTOR, pa = x.chrpos + t.right_genomepos;
+      } else {
+        md = GSNAPDP_ANTIDONOR, pd = x.chrpos + gl1 - t.left_genomepos;
+        ma = GSNAPDP_ANTIACCEPTOR, pa = x.chrpos + gl1 - t.right_genomepos + 1u;
+      }
+    } else if (x.cdna_direction == -1) {
+      if (x.watsonp) {
+        ma = GSNAPDP_ANTIACCEPTOR, pa = x.chrpos + t.left_genomepos + 1u;
+        md = GSNAPDP_ANTIDONOR, pd = x.chrpos + t.right_genomepos;
+      } else {
+        ma = GSNAPDP_ACCEPTOR, pa = x.chrpos + gl1 - t.left_genomepos;
+        md = GSNAPDP_DONOR, pd = x.chrpos + gl1 - t.right_genomepos + 1u;
+      }
+    } else {
+      continue;  // neither branch of the reference runs: the intron is not counted
+    }
+    const double d = t.known_donor ? 1.0 : maxent_prob(md, x.chroffset + pd, x.chroffset, blocks, nwords, T);
+    const double a = t.known_acceptor ? 1.0 : maxent_prob(ma, x.chroffset + pa, x.chroffset, blocks, nwords, T);
+    nin++;
+    if (!t.knowngapp && d < 0.9 && a < 0.9) {
+      if (x.cdna_direction == 1 && t.comp == '>') nbad = 1;        // FWD_CANONICAL_INTRON_COMP: set (:8048)
+      if (x.cdna_direction == -1 && t.comp == '<') nbad += 1;      // REV_CANONICAL_INTRON_COMP: counted (:8119)
+    }
+    sd = __dadd_rn(sd, d);
+    sa = __dadd_rn(sa, a);
+  }
+  gsnapdp_intron_scores r;
+  r.avg_donor_score = nin > 0 ? __ddiv_rn(sd, (double)nin) : sd;
+  r.avg_acceptor_score = nin > 0 ? __ddiv_rn(sa, (double)nin) : sa;
+  r.nbadintrons = nbad;
+  r.nintrons = nin;
+  out[p] = r;
+}
+
 }  // namespace
 
 // ======================================================================
@@ -887,6 +944,7 @@ extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   (void)hipFree(ctx->d_sj_win);
   (void)hipFree(ctx->d_stage);
   (void)hipFree(ctx->d_csum);
+  (void)hipFree(ctx->d_si_stage);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   if (ctx->h_in) (void)hipHostFree(ctx->h_in);
   if (ctx->h_mx) (void)hipHostFree(ctx->h_mx);
@@ -1205,3 +1263,60 @@ extern "C" int gsnapdp_maxent_host(gsnapdp_ctx* ctx, const uint8_t* model, const
 extern "C" const uint32_t* gsnapdp__host_blocks(gsnapdp_ctx* ctx) { return ctx->h_blocks; }
 extern "C" size_t gsnapdp__host_nwords(gsnapdp_ctx* ctx) { return ctx->nwords; }
 extern "C" const uint32_t* gsnapdp__host_prof(gsnapdp_ctx* ctx) { return ctx->h_prof; }
+
+extern "C" int gsnapdp_score_introns_device(gsnapdp_ctx* ctx, const gsnapdp_intron_path* d_paths, int npaths,
+                                            const gsnapdp_intron* d_introns, gsnapdp_intron_scores* d_out,
+                                            void* stream_v) {
+  if (!ctx || !ctx->d_tables) {
+    gsnapdp__set_err("maxent tables not loaded");
+    return -1;
+  }
+  if (npaths <= 0) return 0;
+  hipStream_t st = stream_v ? (hipStream_t)stream_v : ctx->stream;
+  hipLaunchKernelGGL(k_introns, dim3((npaths + 255) / 256), dim3(256), 0, st, d_paths, npaths, d_introns,
+                     d_out, ctx->d_blocks, (uint64_t)ctx->nwords, ctx->d_tables);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int gsnapdp_score_introns_host(gsnapdp_ctx* ctx, const gsnapdp_intron_path* paths, int npaths,
+                                          const gsnapdp_intron* introns, int nintrons,
+                                          gsnapdp_intron_scores* out) {
+  if (!ctx) return -1;
+  if (npaths <= 0) return 0;
+  for (int p = 0; p < npaths; p++)  // the kernel trusts the ranges: check them here
+    if (paths[p].nintrons < 0 || paths[p].first_intron < 0 ||
+        (int64_t)paths[p].first_intron + paths[p].nintrons > (int64_t)nintrons) {
+      gsnapdp__set_err("score_introns: a path's introns lie outside the intron array");
+      return -1;
+    }
+  HIPCHK(hipSetDevice(ctx->device));
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t szp = al((size_t)npaths * sizeof(gsnapdp_intron_path));
+  const size_t szi = al((size_t)(nintrons > 0 ? nintrons : 1) * sizeof(gsnapdp_intron));
+  const size_t szo = (size_t)npaths * sizeof(gsnapdp_intron_scores);
+  std::lock_guard<std::mutex> host_lock(ctx->host_mu);
+  {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (szp + szi + szo > ctx->si_cap) {
+      (void)hipFree(ctx->d_si_stage);
+      ctx->d_si_stage = nullptr;
+      const size_t cap = szp + szi + szo + (szp + szi + szo) / 2 + 4096;
+      HIPCHK(hipMalloc(&ctx->d_si_stage, cap));
+      ctx->si_cap = cap;
+    }
+  }
+  char* d = ctx->d_si_stage;
+  hipStream_t st = ctx->stream;
+  HIPCHK(hipMemcpyAsync(d, paths, (size_t)npaths * sizeof(gsnapdp_intron_path), hipMemcpyHostToDevice, st));
+  if (nintrons > 0)
+    HIPCHK(hipMemcpyAsync(d + szp, introns, (size_t)nintrons * sizeof(gsnapdp_intron), hipMemcpyHostToDevice, st));
+  int rc = gsnapdp_score_introns_device(ctx, (const gsnapdp_intron_path*)d, npaths,
+                                        (const gsnapdp_intron*)(d + szp),
+                                        (gsnapdp_intron_scores*)(d + szp + szi), st);
+  if (rc == 0) {
+    HIPCHK(hipMemcpyAsync(out, d + szp + szi, szo, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return rc;
+}

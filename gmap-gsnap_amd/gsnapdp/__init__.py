@@ -19,7 +19,8 @@ import os
 import numpy as np
 
 from .records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW,  # noqa: F401
-                      MAXENT_IN, MICRO_RESULT, MICRO_WINDOW, PAIR, RESULT, SJ_WINDOW, WINDOW)
+                      INTRON, INTRON_PATH, INTRON_SCORES, MAXENT_IN, MICRO_RESULT, MICRO_WINDOW, PAIR,
+                      PATH_PAIR, RESULT, SJ_WINDOW, WINDOW)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
@@ -99,12 +100,30 @@ def lib():
         L.gsnapdp_host_free.argtypes = [vp]
         L.gsnapdp_compact_ops_device.argtypes = [vp, vp, i32, vp, vp, vp, ctypes.c_int64, vp, vp]
         L.gsnapdp_compact_ops_device.restype = i32
+        L.gsnapdp_path_introns.argtypes = [vp, i32, i32, i32, vp, i32]
+        L.gsnapdp_path_introns.restype = i32
+        L.gsnapdp_score_introns_host.argtypes = [vp, vp, i32, vp, i32, vp]
+        L.gsnapdp_score_introns_host.restype = i32
+        L.gsnapdp_score_introns_device.argtypes = [vp, vp, i32, vp, vp, vp]
+        L.gsnapdp_score_introns_device.restype = i32
         _lib = L
     return _lib
 
 
 def _p(a):
     return ctypes.c_void_p(a.ctypes.data)
+
+
+def path_introns(pairs: np.ndarray, nullgap: int, path: int = 0) -> np.ndarray:
+    """score_introns' intron walk over one path's PATH_PAIR records
+    (gsnapdp_path_introns, host code, stage3.c:7960-8146)."""
+    pr = np.ascontiguousarray(pairs, dtype=PATH_PAIR)
+    n = lib().gsnapdp_path_introns(_p(pr), len(pr), nullgap, path, None, 0)
+    if n < 0:
+        raise GsnapdpError("gsnapdp_path_introns: an intron at the end of the path")
+    out = np.zeros(max(n, 1), dtype=INTRON)
+    lib().gsnapdp_path_introns(_p(pr), len(pr), nullgap, path, _p(out), n)
+    return out[:n]
 
 
 class _Pinned:
@@ -427,6 +446,17 @@ class Context:
     def sync(self):
         if lib().gsnapdp_sync(self.h) != 0:
             raise GsnapdpError(lib().gsnapdp_last_error().decode())
+
+    def score_introns(self, paths: np.ndarray, introns: np.ndarray) -> np.ndarray:
+        """score_introns (stage3.c:7935-8162) for every path in one k_introns launch."""
+        pa = np.ascontiguousarray(paths, dtype=INTRON_PATH)
+        it = np.ascontiguousarray(introns, dtype=INTRON)
+        out = np.zeros(len(pa), dtype=INTRON_SCORES)
+        rc = lib().gsnapdp_score_introns_host(self.h, _p(pa), len(pa), _p(it) if it.size else None, len(it),
+                                              _p(out))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_score_introns_host: %s" % lib().gsnapdp_last_error().decode())
+        return out
 
     def maxent(self, model: np.ndarray, pos: np.ndarray, chroffset: np.ndarray) -> np.ndarray:
         m = np.ascontiguousarray(model, dtype=np.uint8)

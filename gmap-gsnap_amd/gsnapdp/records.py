@@ -108,3 +108,18 @@ OP_DIAG, OP_HDASH, OP_HGAP, OP_VSKIP = 0, 1, 2, 3
 # Dynprog_new(600, 10, 11, 10, 8) as called by gmap.c:2270 -> 611 x 2000 (dynprog.c:831-852)
 MAXLENGTH1 = 611
 MAXLENGTH2 = 2000
+
+# score_introns batches (include/gsnapdp.h: gsnapdp_path_pair, _intron, _intron_path, _intron_scores)
+PATH_PAIR = np.dtype([("genomepos", "<u4"), ("queryjump", "<i4"), ("genomejump", "<i4"),
+                      ("gapp", "u1"), ("knowngapp", "u1"), ("comp", "u1"), ("pad", "u1")])
+assert PATH_PAIR.itemsize == 16
+INTRON = np.dtype([("left_genomepos", "<u4"), ("right_genomepos", "<u4"), ("path", "<i4"),
+                   ("comp", "u1"), ("knowngapp", "u1"), ("known_donor", "u1"), ("known_acceptor", "u1")])
+assert INTRON.itemsize == 16
+INTRON_PATH = np.dtype([("chroffset", "<u4"), ("chrpos", "<u4"), ("genomiclength", "<i4"),
+                        ("cdna_direction", "<i4"), ("watsonp", "<i4"), ("first_intron", "<i4"),
+                        ("nintrons", "<i4"), ("pad", "<i4")])
+assert INTRON_PATH.itemsize == 32
+INTRON_SCORES = np.dtype([("avg_donor_score", "<f8"), ("avg_acceptor_score", "<f8"),
+                          ("nbadintrons", "<i4"), ("nintrons", "<i4")])
+assert INTRON_SCORES.itemsize == 24

@@ -314,6 +314,50 @@ const char *gsnapdp_stage_name(int stage);
 enum { GSNAPDP_DONOR = 0, GSNAPDP_ACCEPTOR = 1, GSNAPDP_ANTIDONOR = 2, GSNAPDP_ANTIACCEPTOR = 3 };
 int gsnapdp_maxent_host(gsnapdp_ctx *ctx, const uint8_t *model, const uint32_t *splice_pos,
                         const uint32_t *chroffset, double *out, int n);
+
+/* ------------------------------------------------------- score_introns
+ * stage3.c:7935-8162 for many paths at once: each path's introns get their
+ * donor / acceptor MaxEnt probabilities (1.0 for a site the splicing IIT
+ * knows), summed in path order and averaged, and the path's bad-intron count
+ * (a canonical intron with both probabilities below 0.9; the reference SETS it
+ * to 1 for cdna_direction +1 and counts it for -1, :8048 / :8119).
+ *
+ * A path's pairs, as score_introns reads them (Pair_T, pairdef.h:9-49), in
+ * list order; gsnapdp_path_introns picks the introns out of them (the gaps
+ * with genomejump > queryjump + MININTRONLEN_FINAL that are neither past
+ * nullgap nor query-heavy, :7960-8146).  An intron's leftpair is the pair
+ * after its gap in the list, its rightpair the pair before it. */
+typedef struct gsnapdp_path_pair {
+  uint32_t genomepos;
+  int32_t queryjump, genomejump;
+  uint8_t gapp, knowngapp, comp, pad;
+} gsnapdp_path_pair;
+typedef struct gsnapdp_intron {
+  uint32_t left_genomepos, right_genomepos;  /* leftpair->genomepos, rightpair->genomepos */
+  int32_t path;                              /* owning path; a path's introns are consecutive, in list order */
+  uint8_t comp, knowngapp;                   /* the gap pair's comp and knowngapp */
+  uint8_t known_donor, known_acceptor;       /* the splicing IIT has the site (0 without an IIT) */
+} gsnapdp_intron;
+typedef struct gsnapdp_intron_path {
+  uint32_t chroffset, chrpos;
+  int32_t genomiclength, cdna_direction, watsonp;
+  int32_t first_intron, nintrons, pad;
+} gsnapdp_intron_path;
+typedef struct gsnapdp_intron_scores {
+  double avg_donor_score, avg_acceptor_score;
+  int32_t nbadintrons, nintrons;
+} gsnapdp_intron_scores;
+/* Host-only (no GPU): the introns of one path's pairs, tagged with `path`.
+ * Returns how many (at most cap are written), or -1. */
+int gsnapdp_path_introns(const gsnapdp_path_pair *pairs, int npairs, int nullgap, int path,
+                         gsnapdp_intron *out, int cap);
+/* One launch for every path (needs gsnapdp_load_maxent_tables).  The device
+ * form is asynchronous on `stream`. */
+int gsnapdp_score_introns_device(gsnapdp_ctx *ctx, const gsnapdp_intron_path *d_paths, int npaths,
+                                 const gsnapdp_intron *d_introns, gsnapdp_intron_scores *d_out,
+                                 void *stream);
+int gsnapdp_score_introns_host(gsnapdp_ctx *ctx, const gsnapdp_intron_path *paths, int npaths,
+                               const gsnapdp_intron *introns, int nintrons, gsnapdp_intron_scores *out);
 int gsnapdp_maxent_device(gsnapdp_ctx *ctx, const uint8_t *d_model, const uint32_t *d_splice_pos,
                           const uint32_t *d_chroffset, double *d_out, int n, void *stream);
 

@@ -222,6 +222,17 @@ double Maxent_hr_antidonor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomic
 double Maxent_hr_antiacceptor_prob(gsnapdp_Genomicpos_T splice_pos,
                                    gsnapdp_Genomicpos_T chroffset);
 
+/* score_introns (stage3.c:7935-8162, static there; non-WASTE signature): a
+ * stage3.c that calls Gsnapdp_score_introns at its two call sites
+ * (stage3.c:9892, 9935) gets the same outputs and the same
+ * returned list, with the path's MaxEnt probabilities run in one GPU launch
+ * (shared with concurrent callers) instead of four round trips per intron. */
+gsnapdp_List_T Gsnapdp_score_introns(double* avg_donor_score, double* avg_acceptor_score, int* nbadintrons,
+                                     gsnapdp_List_T path, int cdna_direction, gsnapdp_bool watsonp, int chrnum,
+                                     gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh,
+                                     gsnapdp_Genomicpos_T chrpos, char* genomicuc_ptr, int genomiclength,
+                                     int nullgap, gsnapdp_bool use_genomicseg_p);
+
 /* --- optional additions (not in the reference) ---
  * The shim finds the packed genome on its own: Dynprog_setup's Genome_T
  * (Genome_blocks / Genome_totallength, genome.c:96-107) for an index genome,

@@ -536,6 +536,15 @@ RECORDED = np.dtype([("finalscore", "<i4"), ("nmatches", "<i4"), ("nmismatches",
                      ("nindels", "<i4"), ("dynprogindex", "<i4"), ("npairs", "<i4"), ("pad", "<i4")])
 
 
+# oracle/gmap_trace.c's score_introns records (SiCall, SiPair)
+SI_CALL = np.dtype([("cdna_direction", "<i4"), ("watsonp", "<i4"), ("chrnum", "<i4"), ("genomiclength", "<i4"),
+                    ("nullgap", "<i4"), ("use_genomicseg_p", "<i4"), ("chroffset", "<u4"), ("chrhigh", "<u4"),
+                    ("chrpos", "<u4"), ("first_pair", "<i4"), ("npairs", "<i4"), ("nbadintrons", "<i4"),
+                    ("avg_donor_score", "<f8"), ("avg_acceptor_score", "<f8")])
+SI_PAIR = np.dtype([("querypos", "<i4"), ("genomepos", "<u4"), ("queryjump", "<i4"), ("genomejump", "<i4"),
+                    ("gapp", "u1"), ("knowngapp", "u1"), ("comp", "u1"), ("pad", "u1")])
+
+
 def gmap_trace_case(seed: int = 7) -> None:
     """The gap windows the reference's own gmap issues (oracle/gmap_trace.c) while
     aligning synthetic spliced cDNAs (workload.synthetic_transcripts) with
@@ -612,6 +621,15 @@ def trace_gmap_run(prefix: str, genome_fa: str, query_fa: str, d: str) -> bytes:
                         dropped_ub=np.int32((~keep).sum()))
     print("%s_ggap: %d windows (%d dropped: probability-mode UB; %d probability mode), %d pairs" %
           (prefix, len(w), int((~keep).sum()), int(w["use_probabilities_p"].sum()), pairs.size))
+
+    # every score_introns call gmap made (stage3.c:7935-8162): its path and its outputs
+    t = os.path.join(d, "trace", "si")
+    calls = np.fromfile(os.path.join(t, "paths.bin"), dtype=SI_CALL)
+    spairs = np.fromfile(os.path.join(t, "pairs.bin"), dtype=SI_PAIR)
+    assert calls.size > 0 and spairs.size == int(calls["npairs"].sum())
+    np.savez_compressed(os.path.join(OUT, prefix + "_introns.npz"), blocks=blocks, calls=calls, pairs=spairs)
+    print("%s_introns: %d score_introns calls, %d pairs, %d bad-intron flags" %
+          (prefix, calls.size, spairs.size, int((calls["nbadintrons"] > 0).sum())))
     return out
 
 

@@ -13,16 +13,26 @@
  * At exit, with $GMAP_TRACE_DIR set, writes
  *   $GMAP_TRACE_DIR/dp/{windows.bin,query.bin,query_uc.bin,genome.u32,gmap_results.bin}
  *   $GMAP_TRACE_DIR/ggap/{ggap_windows.bin,query.bin,query_uc.bin,genome.u32,gmap_results.bin}
+ *   $GMAP_TRACE_DIR/si/{paths.bin,pairs.bin}: every score_introns call (stage3.c:7935),
+ *     the path it was given (pair by pair, in list order) and its three outputs.
+ * score_introns is static, so it cannot be wrapped at link time: stage3_si.c
+ * hands its address over and the hook below is patched over its entry at start
+ * (x86-64 movabs/jmp); the hook restores the entry, runs the reference's
+ * function, records and re-patches (gmap is single-threaded here).
  */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include "bool.h"
 #include "dynprog.h"
 #include "list.h"
+#include "listdef.h"
+#include "pairdef.h"
 
 #include "../include/gsnapdp.h"
 
@@ -47,6 +57,7 @@ typedef struct {
 } Trace;
 
 static Trace dp, gg;
+static Buf si_paths, si_pairs;
 static const unsigned int *genome_blocks = NULL;
 static size_t genome_nwords = 0;
 
@@ -101,6 +112,79 @@ static void base_window(gsnapdp_window *w, int kind, Dynprog_T dynprog, int dpi,
   w->defect_rate = bin(defect_rate);
   w->watsonp = watsonp ? 1 : 0;
   w->jump_late_p = jump_late_p ? 1 : 0;
+}
+
+
+/* ---- score_introns (stage3.c:7935-8162), static: patched at start */
+typedef List_T (*si_fn_t)(double *, double *, int *, List_T, int, bool, int, Genomicpos_T, Genomicpos_T,
+                          Genomicpos_T, char *, int, int, bool);
+extern void *gmap_trace_score_introns_fn(void);
+static unsigned char si_saved[12], si_patch[12];
+static unsigned char *si_entry;
+
+typedef struct { /* one call: the arguments, the outputs, the path's extent in pairs.bin */
+  int32_t cdna_direction, watsonp, chrnum, genomiclength, nullgap, use_genomicseg_p;
+  uint32_t chroffset, chrhigh, chrpos;
+  int32_t first_pair, npairs, nbadintrons;
+  double avg_donor_score, avg_acceptor_score;
+} SiCall;
+typedef struct { /* the Pair_T fields score_introns reads */
+  int32_t querypos;
+  uint32_t genomepos;
+  int32_t queryjump, genomejump;
+  uint8_t gapp, knowngapp, comp, pad;
+} SiPair;
+
+static List_T si_hook(double *avg_donor_score, double *avg_acceptor_score, int *nbadintrons, List_T path,
+                      int cdna_direction, bool watsonp, int chrnum, Genomicpos_T chroffset,
+                      Genomicpos_T chrhigh, Genomicpos_T chrpos, char *genomicuc_ptr, int genomiclength,
+                      int nullgap, bool use_genomicseg_p) {
+  SiCall c;
+  List_T p, out;
+  memset(&c, 0, sizeof(c));
+  c.cdna_direction = cdna_direction;
+  c.watsonp = watsonp;
+  c.chrnum = chrnum;
+  c.genomiclength = genomiclength;
+  c.nullgap = nullgap;
+  c.use_genomicseg_p = use_genomicseg_p;
+  c.chroffset = chroffset;
+  c.chrhigh = chrhigh;
+  c.chrpos = chrpos;
+  c.first_pair = (int32_t)(si_pairs.n / sizeof(SiPair));
+  for (p = path; p != NULL; p = p->rest) {
+    const struct Pair_T *x = (const struct Pair_T *)p->first;
+    SiPair r = {x->querypos, x->genomepos, x->queryjump, x->genomejump, (uint8_t)x->gapp,
+                (uint8_t)x->knowngapp, (uint8_t)x->comp, 0};
+    put(&si_pairs, &r, sizeof(r));
+    c.npairs++;
+  }
+  memcpy(si_entry, si_saved, sizeof(si_saved));
+  out = ((si_fn_t)(void *)si_entry)(avg_donor_score, avg_acceptor_score, nbadintrons, path, cdna_direction,
+                                    watsonp, chrnum, chroffset, chrhigh, chrpos, genomicuc_ptr, genomiclength,
+                                    nullgap, use_genomicseg_p);
+  memcpy(si_entry, si_patch, sizeof(si_patch));
+  c.avg_donor_score = *avg_donor_score;
+  c.avg_acceptor_score = *avg_acceptor_score;
+  c.nbadintrons = *nbadintrons;
+  put(&si_paths, &c, sizeof(c));
+  return out;
+}
+
+__attribute__((constructor)) static void si_install(void) {
+  const long pg = sysconf(_SC_PAGESIZE);
+  const uint64_t target = (uint64_t)(void *)&si_hook;
+  uintptr_t lo;
+  si_entry = (unsigned char *)gmap_trace_score_introns_fn();
+  lo = (uintptr_t)si_entry & ~(uintptr_t)(pg - 1);
+  if (mprotect((void *)lo, (size_t)(2 * pg), PROT_READ | PROT_WRITE | PROT_EXEC) != 0) abort();
+  memcpy(si_saved, si_entry, sizeof(si_saved));
+  si_patch[0] = 0x48; /* movabs rax, imm64 */
+  si_patch[1] = 0xB8;
+  memcpy(si_patch + 2, &target, 8);
+  si_patch[10] = 0xFF; /* jmp rax */
+  si_patch[11] = 0xE0;
+  memcpy(si_entry, si_patch, sizeof(si_patch));
 }
 
 extern unsigned int *__real_Genome_create_blocks(char *genomicseg, unsigned int genomelength);
@@ -284,4 +368,12 @@ __attribute__((destructor)) static void write_trace(void) {
   mkdir(root, 0755);
   dump(root, "dp", "windows.bin", &dp);
   dump(root, "ggap", "ggap_windows.bin", &gg);
+  {
+    char dir[4096];
+    snprintf(dir, sizeof(dir), "%s/si", root);
+    mkdir(dir, 0755);
+    spit(dir, "paths.bin", si_paths.p, si_paths.n);
+    spit(dir, "pairs.bin", si_pairs.p, si_pairs.n);
+    spit(dir, "genome.u32", genome_blocks, genome_nwords * sizeof(unsigned int));
+  }
 }

@@ -118,3 +118,103 @@ void orc_maxent_batch(const uint8_t *model, const uint32_t *pos, const uint32_t 
     }
   }
 }
+
+/* ---- score_introns (stage3.c:7935-8162), TEST INFRASTRUCTURE ONLY.
+ * orc_path_introns restates the walk over a path (the pop loop of :7960-8146):
+ * a gap pair counts as an intron unless past nullgap (:7971) or query-heavy
+ * (:7979), when its genomejump exceeds queryjump + MININTRONLEN_FINAL (50,
+ * stage3.c:52, :7987); leftpair = path->first after the pop (the next list
+ * element), rightpair = pairs->first (the previous one).  Returns the count,
+ * or -1 where the reference would dereference NULL. */
+int orc_path_introns(const gsnapdp_path_pair *pairs, int npairs, int nullgap, int path,
+                     gsnapdp_intron *out, int cap) {
+  int i, n = 0;
+  for (i = 0; i < npairs; i++) {
+    const gsnapdp_path_pair *pair = &pairs[i];
+    if (pair->gapp == 0) continue;                               /* :7964 */
+    if (pair->queryjump > nullgap) continue;                     /* :7971 */
+    if (pair->queryjump > pair->genomejump + 10) continue;       /* :7979, EXTRAQUERYGAP stage3.h:29 */
+    if (pair->genomejump > pair->queryjump + 50) {               /* :7987 */
+      if (i == 0 || i == npairs - 1) return -1;                  /* pairs->first / path->first of NULL */
+      if (n < cap) {
+        out[n].left_genomepos = pairs[i + 1].genomepos;
+        out[n].right_genomepos = pairs[i - 1].genomepos;
+        out[n].path = path;
+        out[n].comp = pair->comp;
+        out[n].knowngapp = pair->knowngapp;
+        out[n].known_donor = out[n].known_acceptor = 0;
+      }
+      n++;
+    }
+  }
+  return n;
+}
+
+/* The probabilities and their averages, one path at a time in list order
+ * (:7992-8129, :8154-8157).  A known site (the splicing IIT) scores 1.0. */
+void orc_score_introns(const gsnapdp_intron_path *paths, int npaths, const gsnapdp_intron *introns,
+                       gsnapdp_intron_scores *out) {
+  int p, k;
+  for (p = 0; p < npaths; p++) {
+    const gsnapdp_intron_path *x = &paths[p];
+    double avg_donor_score = 0.0, avg_acceptor_score = 0.0, donor_score, acceptor_score;
+    int nbadintrons = 0, nintrons = 0;
+    uint32_t splicesitepos;
+    for (k = 0; k < x->nintrons; k++) {
+      const gsnapdp_intron *t = &introns[x->first_intron + k];
+      if (x->cdna_direction == +1) {
+        if (x->watsonp) {
+          splicesitepos = x->chrpos + t->left_genomepos + 1;                                   /* :7997 */
+          donor_score = t->known_donor ? 1.0 : orc_maxent_donor(x->chroffset + splicesitepos, x->chroffset);
+          splicesitepos = x->chrpos + t->right_genomepos;                                      /* :8007 */
+          acceptor_score = t->known_acceptor ? 1.0
+                                             : orc_maxent_acceptor(x->chroffset + splicesitepos, x->chroffset);
+        } else {
+          splicesitepos = x->chrpos + (uint32_t)(x->genomiclength - 1) - t->left_genomepos;    /* :8018 */
+          donor_score = t->known_donor ? 1.0 : orc_maxent_antidonor(x->chroffset + splicesitepos, x->chroffset);
+          splicesitepos = x->chrpos + (uint32_t)(x->genomiclength - 1) - t->right_genomepos + 1; /* :8028 */
+          acceptor_score = t->known_acceptor ? 1.0
+                                             : orc_maxent_antiacceptor(x->chroffset + splicesitepos, x->chroffset);
+        }
+        nintrons += 1;
+        if (t->knowngapp) {
+          /* skip */
+        } else if (t->comp == '>' && (donor_score < 0.9 && acceptor_score < 0.9)) {
+          nbadintrons = 1;                                                                     /* :8048 (sic) */
+        }
+        avg_donor_score += donor_score;
+        avg_acceptor_score += acceptor_score;
+      } else if (x->cdna_direction == -1) {
+        if (x->watsonp) {
+          splicesitepos = x->chrpos + t->left_genomepos + 1;                                   /* :8069 */
+          acceptor_score = t->known_acceptor ? 1.0
+                                             : orc_maxent_antiacceptor(x->chroffset + splicesitepos, x->chroffset);
+          splicesitepos = x->chrpos + t->right_genomepos;                                      /* :8080 */
+          donor_score = t->known_donor ? 1.0 : orc_maxent_antidonor(x->chroffset + splicesitepos, x->chroffset);
+        } else {
+          splicesitepos = x->chrpos + (uint32_t)(x->genomiclength - 1) - t->left_genomepos;    /* :8091 */
+          acceptor_score = t->known_acceptor ? 1.0
+                                             : orc_maxent_acceptor(x->chroffset + splicesitepos, x->chroffset);
+          splicesitepos = x->chrpos + (uint32_t)(x->genomiclength - 1) - t->right_genomepos + 1; /* :8101 */
+          donor_score = t->known_donor ? 1.0 : orc_maxent_donor(x->chroffset + splicesitepos, x->chroffset);
+        }
+        nintrons += 1;
+        if (t->knowngapp) {
+          /* skip */
+        } else if (t->comp == '<' && (donor_score < 0.9 && acceptor_score < 0.9)) {
+          nbadintrons += 1;                                                                    /* :8119 */
+        }
+        avg_donor_score += donor_score;
+        avg_acceptor_score += acceptor_score;
+      }
+    }
+    if (nintrons > 0) {
+      avg_donor_score /= (double)nintrons;
+      avg_acceptor_score /= (double)nintrons;
+    }
+    out[p].avg_donor_score = avg_donor_score;
+    out[p].avg_acceptor_score = avg_acceptor_score;
+    out[p].nbadintrons = nbadintrons;
+    out[p].nintrons = nintrons;
+  }
+}

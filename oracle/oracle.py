@@ -16,8 +16,9 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
-from gsnapdp.records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_WINDOW, MICRO_RESULT,  # noqa: E402
-                             MICRO_WINDOW, PAIR, RESULT, SJ_WINDOW, WINDOW)
+from gsnapdp.records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_WINDOW, INTRON,  # noqa: E402
+                             INTRON_PATH, INTRON_SCORES, MICRO_RESULT, MICRO_WINDOW, PAIR, PATH_PAIR,
+                             RESULT, SJ_WINDOW, WINDOW)
 
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 TABLES_PATH = os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin")
@@ -49,6 +50,9 @@ def lib():
         L.orc_run_sj_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
         L.orc_run_micro_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
         L.orc_maxent_batch.argtypes = [vp, vp, vp, vp, i32]
+        L.orc_path_introns.argtypes = [vp, i32, i32, i32, vp, i32]
+        L.orc_path_introns.restype = i32
+        L.orc_score_introns.argtypes = [vp, i32, vp, vp]
         L.orc_pairdistance.argtypes = [i32, i32, i32]
         L.orc_pairdistance.restype = i32
         L.orc_consistent.argtypes = [i32, i32]
@@ -178,6 +182,28 @@ def maxent(model: np.ndarray, pos: np.ndarray, chroffset: np.ndarray) -> np.ndar
     c = np.ascontiguousarray(chroffset, dtype=np.uint32)
     out = np.zeros(len(m), dtype=np.float64)
     L.orc_maxent_batch(_p(m), _p(p), _p(c), _p(out), len(m))
+    return out
+
+
+def path_introns(pairs: np.ndarray, nullgap: int, path: int = 0) -> np.ndarray:
+    """score_introns' intron walk over one path's PATH_PAIR records (stage3.c:7960-8146)."""
+    L = lib()
+    pr = np.ascontiguousarray(pairs, dtype=PATH_PAIR)
+    n = L.orc_path_introns(_p(pr), len(pr), nullgap, path, None, 0)
+    if n < 0:
+        raise ValueError("an intron at the end of the path (the reference dereferences NULL)")
+    out = np.zeros(max(n, 1), dtype=INTRON)
+    L.orc_path_introns(_p(pr), len(pr), nullgap, path, _p(out), n)
+    return out[:n]
+
+
+def score_introns(paths: np.ndarray, introns: np.ndarray) -> np.ndarray:
+    """score_introns' averages and bad-intron counts (stage3.c:7992-8157), per path."""
+    L = lib()
+    pa = np.ascontiguousarray(paths, dtype=INTRON_PATH)
+    it = np.ascontiguousarray(introns, dtype=INTRON)
+    out = np.zeros(len(pa), dtype=INTRON_SCORES)
+    L.orc_score_introns(_p(pa), len(pa), _p(it) if it.size else None, _p(out))
     return out
 
 

@@ -159,3 +159,29 @@ void dbl_list_free(List_T list) {
     list = next;
   }
 }
+
+/* A path for score_introns tests: records (the golden's SiPair layout:
+ * querypos, genomepos, queryjump, genomejump, gapp, knowngapp, comp, pad) ->
+ * a list whose head is recs[0]. */
+typedef struct PathRec {
+  int querypos;
+  unsigned int genomepos;
+  int queryjump, genomejump;
+  unsigned char gapp, knowngapp, comp, pad;
+} PathRec;
+List_T dbl_list_build(const PathRec* recs, int n) {
+  List_T list = NULL;
+  int i;
+  for (i = n - 1; i >= 0; i--) {
+    PairRec* r = (PairRec*)calloc(1, sizeof(PairRec));
+    r->querypos = recs[i].querypos;
+    r->genomepos = recs[i].genomepos;
+    r->queryjump = recs[i].queryjump;
+    r->genomejump = recs[i].genomejump;
+    r->gapp = recs[i].gapp;
+    r->knowngapp = recs[i].knowngapp;
+    r->comp = (char)recs[i].comp;
+    list = cons(list, r);
+  }
+  return list;
+}

@@ -25,7 +25,7 @@ assert REC.itemsize == PAIR.itemsize
 
 def declared_functions():
     text = open(HEADER).read()
-    names = re.findall(r"\b((?:Dynprog|Maxent_hr|Gsnapdp_dropin|Genome_hr|Genome_prev)_\w+)\s*\(", text)
+    names = re.findall(r"\b((?:Dynprog|Maxent_hr|Gsnapdp|Genome_hr|Genome_prev)_\w+)\s*\(", text)
     return sorted(set(names))
 
 

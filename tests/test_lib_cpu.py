@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 
 import gsnapdp
-from gsnapdp.records import GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW, PAIR, RESULT, WINDOW
+from gsnapdp.records import (GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW, INTRON, INTRON_PATH, INTRON_SCORES, PAIR,
+                             PATH_PAIR, RESULT, WINDOW)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -38,12 +39,15 @@ def test_record_layouts_match_c(tmp_path):
     src.write_text('#include <stdio.h>\n#include "%s/include/gsnapdp.h"\n'
                    'int main(){printf("%%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(gsnapdp_window), '
                    'sizeof(gsnapdp_result), sizeof(gsnapdp_pair), sizeof(gsnapdp_ggap_window), '
-                   'sizeof(gsnapdp_ggap_result), sizeof(gsnapdp_ggap_trace));return 0;}\n' % ROOT)
+                   'sizeof(gsnapdp_ggap_result), sizeof(gsnapdp_ggap_trace));'
+                   'printf("%%zu %%zu %%zu %%zu\\n", sizeof(gsnapdp_path_pair), sizeof(gsnapdp_intron), '
+                   'sizeof(gsnapdp_intron_path), sizeof(gsnapdp_intron_scores));return 0;}\n' % ROOT)
     exe = tmp_path / "sz"
     subprocess.check_call(["gcc", "-o", str(exe), str(src)])
     sizes = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     assert sizes == [WINDOW.itemsize, RESULT.itemsize, PAIR.itemsize, GGAP_WINDOW.itemsize,
-                     GGAP_RESULT.itemsize, GGAP_TRACE.itemsize]
+                     GGAP_RESULT.itemsize, GGAP_TRACE.itemsize, PATH_PAIR.itemsize, INTRON.itemsize,
+                     INTRON_PATH.itemsize, INTRON_SCORES.itemsize]
 
 
 def test_no_gpu_means_loud_failure():
@@ -53,3 +57,16 @@ def test_no_gpu_means_loud_failure():
         pytest.skip("GPU present")
     with pytest.raises(gsnapdp.GsnapdpError):
         gsnapdp.Context(np.zeros(64, np.uint32))
+
+
+@pytest.mark.parametrize("name", ["gmap_her2_introns", "gmap_synth_introns"])
+def test_path_introns_host_walk_matches_restatement(golden_dir, name):
+    """gsnapdp_path_introns (product host code, no GPU) picks the same introns,
+    with the same flanking pairs, as the restatement of score_introns' walk
+    (pinned to the reference by test_oracle_golden) on every recorded path."""
+    import oracle as O
+    from test_oracle_golden import golden_intron_paths
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    p1, i1 = golden_intron_paths(z, gsnapdp.path_introns)
+    p2, i2 = golden_intron_paths(z, O.path_introns)
+    assert p1.tobytes() == p2.tobytes() and i1.tobytes() == i2.tobytes() and i1.size > 0

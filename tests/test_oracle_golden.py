@@ -181,3 +181,38 @@ def test_splicetrie_double_matches_reference_splicetrie(golden_dir, tmp_path, am
     assert outs["ref"] == outs["dbl"]
     if amb_closest == int(z["amb_closest"]):
         assert outs["ref"][0] == z["results"].tobytes()
+
+
+def golden_intron_paths(z, path_introns):
+    """The golden score_introns calls (recorded in the reference's gmap by
+    oracle/gmap_trace.c) as batch records: each call's pairs -> its introns."""
+    from gsnapdp.records import INTRON, INTRON_PATH, PATH_PAIR
+    calls, sp = z["calls"], z["pairs"]
+    paths = np.zeros(len(calls), dtype=INTRON_PATH)
+    chunks = []
+    n = 0
+    for i, c in enumerate(calls):
+        pr = np.zeros(int(c["npairs"]), dtype=PATH_PAIR)
+        seg = sp[int(c["first_pair"]):int(c["first_pair"]) + int(c["npairs"])]
+        for f in ("genomepos", "queryjump", "genomejump", "gapp", "knowngapp", "comp"):
+            pr[f] = seg[f]
+        it = path_introns(pr, int(c["nullgap"]), i)
+        paths[i] = (c["chroffset"], c["chrpos"], c["genomiclength"], c["cdna_direction"], c["watsonp"], n, len(it), 0)
+        chunks.append(it)
+        n += len(it)
+    return paths, (np.concatenate(chunks) if chunks else np.zeros(0, INTRON))
+
+
+@pytest.mark.parametrize("name", ["gmap_her2_introns", "gmap_synth_introns"])
+def test_score_introns_oracle_matches_reference(golden_dir, name):
+    """score_introns (stage3.c:7935-8162): the restatement reproduces every
+    call the reference's gmap made, its averages bit for bit."""
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    O.setup(z["blocks"])
+    paths, introns = golden_intron_paths(z, O.path_introns)
+    out = O.score_introns(paths, introns)
+    c = z["calls"]
+    assert np.array_equal(out["nbadintrons"], c["nbadintrons"])
+    assert out["avg_donor_score"].tobytes() == c["avg_donor_score"].tobytes()
+    assert out["avg_acceptor_score"].tobytes() == c["avg_acceptor_score"].tobytes()
+    assert introns.size >= 20 and np.sum(out["nintrons"] > 0) >= 1
