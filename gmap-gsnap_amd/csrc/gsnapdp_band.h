@@ -206,6 +206,20 @@ struct SegCls {
   const unsigned char* seg;
   int g0;
 };
+#ifdef TB_PROF
+// diagnostic builds: sweep counters (0 sweeps, 1 groups, 2 groups some lane
+// could not bulk-step, 3 lane-columns stepped one by one, 4/5 fill / trace cycles)
+__device__ unsigned long long tb_prof[8];
+#define TB_COUNT(k, v)                                                      \
+  do {                                                                      \
+    if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63)) \
+      atomicAdd(&tb_prof[k], (unsigned long long)(v));                      \
+  } while (0)
+#else
+#define TB_COUNT(k, v) \
+  do {                 \
+  } while (0)
+#endif
 template <int S, int LPW>
 __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint8_t* __restrict__ M,
                                       int g, int r, int cstart, int maxC, int lband, int rband,
@@ -322,6 +336,7 @@ __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint
   };
   // wave-uniform sweep from the wave's longest window down to column -1
   int G = maxC >> 2;
+  TB_COUNT(0, 1);
   set_diag(r, cstart);
   // pre[0] is the group being visited, pre[1..TB_AHEAD] the next ones,
   // loaded TB_AHEAD groups ahead of their visit (global scratch latency)
@@ -365,7 +380,10 @@ __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint
     // lanes with nothing to do in this group: bulk-stepped, done, or still
     // waiting for their own start column
     const bool idle = fast4 || st == T_DONE || (st == T_WAIT && cstart < 4 * G);
+    TB_COUNT(1, 1);
     if (__builtin_amdgcn_ballot_w64(!idle) != 0) {
+      TB_COUNT(2, 1);
+      TB_COUNT(3, __builtin_popcountll(__builtin_amdgcn_ballot_w64(!idle)));
       for (int c = chi; c >= 4 * G; c--) {
         const int k = c & 3;
         if (!fast4 && st != T_DONE && (st != T_WAIT || c == cstart)) {

@@ -471,16 +471,29 @@ struct GCand {  // a bridge candidate: total score, scan order 2*rL + loop, the 
 #define GB_GROUP_ATTR __noinline__
 #endif
 template <int S, int LPW, int JL>
-__device__ GB_GROUP_ATTR void gband_group(const gsnapdp_ggap_window* __restrict__ Wn, int wi,
-                                         bool active, int lane, uint32_t* __restrict__ wpool,
-                                         const char* __restrict__ q, const char* __restrict__ qu,
-                                         const uint32_t* __restrict__ blocks, uint64_t nwords,
+__device__ GB_GROUP_ATTR void gband_group(const AS_GLOBAL gsnapdp_ggap_window* Wn1, int wi,
+                                         bool active, int lane, AS_GLOBAL uint32_t* wpool1,
+                                         const AS_GLOBAL char* q1, const AS_GLOBAL char* qu1,
+                                         const AS_GLOBAL uint32_t* blocks1, uint64_t nwords,
                                          const AS_LDS uint32_t* sprof, AS_LDS uint32_t* ring,
-                                         const double* __restrict__ tables,
-                                         gsnapdp_ggap_result* __restrict__ res,
-                                         gsnapdp_ggap_trace* __restrict__ trc,
-                                         uint32_t* __restrict__ ops,
-                                         const int64_t* __restrict__ op_off) {
+                                         const AS_GLOBAL double* tables1,
+                                         AS_GLOBAL gsnapdp_ggap_result* res1,
+                                         AS_GLOBAL gsnapdp_ggap_trace* trc1,
+                                         AS_GLOBAL uint32_t* ops1,
+                                         const AS_GLOBAL int64_t* op_off1) {
+  // address-space-qualified parameters: the tables, combine and tracebacks
+  // compile to global_* accesses (generic pointers made them flat_*, each use
+  // a full vmcnt(0) lgkmcnt(0) drain)
+  const gsnapdp_ggap_window* __restrict__ Wn = (const gsnapdp_ggap_window*)Wn1;
+  uint32_t* __restrict__ wpool = (uint32_t*)wpool1;
+  const char* __restrict__ q = (const char*)q1;
+  const char* __restrict__ qu = (const char*)qu1;
+  const uint32_t* __restrict__ blocks = (const uint32_t*)blocks1;
+  const double* __restrict__ tables = (const double*)tables1;
+  gsnapdp_ggap_result* __restrict__ res = (gsnapdp_ggap_result*)res1;
+  gsnapdp_ggap_trace* __restrict__ trc = (gsnapdp_ggap_trace*)trc1;
+  uint32_t* __restrict__ ops = (uint32_t*)ops1;
+  const int64_t* __restrict__ op_off = (const int64_t*)op_off1;
   constexpr int NG = 64 / LPW;
   static_assert(NG <= GB_NGMAX, "k_gband groups");
   const int j = lane % LPW, g = lane / LPW;
@@ -787,20 +800,12 @@ __device__ __noinline__ void gband_tasks(int cls, int t0, int t1, int stride, in
     GB_CHK(li, GG_NLISTS, 13);
     GB_CHK(wi, list_cap * 4, 14);
 #endif
-    const gsnapdp_ggap_window* Wn = (const gsnapdp_ggap_window*)Wn1;
-    uint32_t* wpool = (uint32_t*)wpool1;
     if (jl)
-      gband_group<S, LPW, 1>(Wn, wi, active, lane, wpool, (const char*)q1, (const char*)qu1,
-                                  (const uint32_t*)blocks1, nwords, sprof3, ring3,
-                                  (const double*)tables1, (gsnapdp_ggap_result*)res1,
-                                  (gsnapdp_ggap_trace*)trc1, (uint32_t*)ops1,
-                                  (const int64_t*)op_off1);
+      gband_group<S, LPW, 1>(Wn1, wi, active, lane, wpool1, q1, qu1, blocks1, nwords, sprof3, ring3,
+                             tables1, res1, trc1, ops1, op_off1);
     else
-      gband_group<S, LPW, 0>(Wn, wi, active, lane, wpool, (const char*)q1, (const char*)qu1,
-                                  (const uint32_t*)blocks1, nwords, sprof3, ring3,
-                                  (const double*)tables1, (gsnapdp_ggap_result*)res1,
-                                  (gsnapdp_ggap_trace*)trc1, (uint32_t*)ops1,
-                                  (const int64_t*)op_off1);
+      gband_group<S, LPW, 0>(Wn1, wi, active, lane, wpool1, q1, qu1, blocks1, nwords, sprof3, ring3,
+                             tables1, res1, trc1, ops1, op_off1);
   }
 }
 

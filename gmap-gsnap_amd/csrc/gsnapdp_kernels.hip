@@ -612,13 +612,25 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
 // task k (direction scratch region k).  A task's own sweep would run on lane 0
 // of each group only (NG of the 64 lanes); this sweep keeps up to
 // TB_BATCH * NG lanes busy.  wi < 0: no window on this lane.
+// The pointers carry the global address space (as fill_tasks' do), so that the
+// sweep's loads compile to global_load and the compiler can wait on the group
+// being visited (vmcnt) while the next group's prefetch stays in flight; with
+// generic pointers they were flat loads, each use a full vmcnt(0) lgkmcnt(0) drain.
 template <int S, int LPW>
-__device__ void trace_batch(int lane, int wi, const FillOut& fo, int jl,
-                            const gsnapdp_window* __restrict__ Wn, const uint32_t* __restrict__ D,
-                            const uint32_t* __restrict__ blocks, uint64_t nwords,
-                            gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
-                            const int64_t* __restrict__ op_off, const gsnapdp_sj_window* __restrict__ sjw,
-                            const char* __restrict__ q) {
+__device__ void trace_batch(int lane, int wi, FillOut fo, int jl,
+                            const AS_GLOBAL gsnapdp_window* Wn1, const AS_GLOBAL uint32_t* D1,
+                            const AS_GLOBAL uint32_t* blocks1, uint64_t nwords,
+                            AS_GLOBAL gsnapdp_result* res1, AS_GLOBAL uint32_t* ops1,
+                            const AS_GLOBAL int64_t* op_off1, const AS_GLOBAL gsnapdp_sj_window* sjw1,
+                            const AS_GLOBAL char* q1) {
+  const gsnapdp_window* __restrict__ Wn = (const gsnapdp_window*)Wn1;
+  const uint32_t* __restrict__ D = (const uint32_t*)D1;
+  const uint32_t* __restrict__ blocks = (const uint32_t*)blocks1;
+  gsnapdp_result* __restrict__ res = (gsnapdp_result*)res1;
+  uint32_t* __restrict__ ops = (uint32_t*)ops1;
+  const int64_t* __restrict__ op_off = (const int64_t*)op_off1;
+  const gsnapdp_sj_window* __restrict__ sjw = (const gsnapdp_sj_window*)sjw1;
+  const char* __restrict__ q = (const char*)q1;
   constexpr int NG = 64 / LPW;
   constexpr int WMAX = S * LPW;
   const int k = lane / NG, g = lane % NG;
@@ -673,9 +685,6 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
   const uint32_t* sprof = (const uint32_t*)sprof3;
   uint32_t* ring = (uint32_t*)ring3;
   uint32_t* __restrict__ D = (uint32_t*)D1;
-  gsnapdp_result* __restrict__ res = (gsnapdp_result*)res1;
-  uint32_t* __restrict__ ops = (uint32_t*)ops1;
-  const int64_t* __restrict__ op_off = (const int64_t*)op_off1;
   const gsnapdp_sj_window* __restrict__ sjw = (const gsnapdp_sj_window*)sjw1;
   constexpr int NG = 64 / LPW;
   constexpr int B = LPW < TB_BATCH ? LPW : TB_BATCH;  // tasks per traceback sweep
@@ -702,9 +711,15 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
       const int wi = active ? wi0 : w0;  // idle groups shadow group 0 (reads only)
       // the bucket's tie rule (an end5 gap's fill is reversed with !jump_late_p)
       const int jl = __builtin_amdgcn_readfirstlane(derive(Wn[w0]).jl);
+#ifdef TB_PROF
+      const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
       const FillOut fo =
           jl ? fill_group<S, LPW, LOW, 1, END>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords, sprof, ring, sjw)
              : fill_group<S, LPW, LOW, 0, END>(Wn, wi, active, lane, Dk, Mk, q, qu, blocks, nwords, sprof, ring, sjw);
+#ifdef TB_PROF
+      TB_COUNT(4, __builtin_amdgcn_s_memtime() - t0);
+#endif
       const int src = (lane % NG) * LPW;  // lane 0 of group lane % NG
       const int v_wi = __shfl(wi0, src);
       const FillOut v = {__shfl(fo.score, src), __shfl(fo.br, src), __shfl(fo.bc, src)};
@@ -716,7 +731,13 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
       do t += stride;
       while (t < t1 && kind_of(t) != END);
     }
-    trace_batch<S, LPW>(lane, my_wi, my, my_jl, Wn, D, blocks, nwords, res, ops, op_off, sjw, q);
+#ifdef TB_PROF
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+#endif
+    trace_batch<S, LPW>(lane, my_wi, my, my_jl, Wn1, D1, blocks1, nwords, res1, ops1, op_off1, sjw1, q1);
+#ifdef TB_PROF
+    TB_COUNT(5, __builtin_amdgcn_s_memtime() - t1);
+#endif
   }
 }
 
@@ -1019,6 +1040,17 @@ int gsnapdp__fill_pipeline(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_windo
                      d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_dirpool,
                      WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets, big_count + RW_NCLS, sjw);
   mark(2, 1);
+#ifdef TB_PROF
+  {
+    unsigned long long h[8];
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpyFromSymbol(h, HIP_SYMBOL(tb_prof), sizeof(h)));
+    fprintf(stderr, "tb_prof sweeps %llu groups %llu slow %llu lanecols %llu fill_cyc %llu trace_cyc %llu\n", h[0], h[1],
+            h[2], h[3], h[4], h[5]);
+    memset(h, 0, sizeof(h));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(tb_prof), h, sizeof(h)));
+  }
+#endif
   mark(3, 0);
   if (gsnapdp__rows_launch(ctx, st, d_windows, ctx->d_big_list, big_count, ctx->cap_n, d_query,
                            d_query_uc, d_results, d_ops, d_op_offsets, sjw))

@@ -36,6 +36,8 @@ Deterministic for a given seed (numpy PCG64).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from . import genome as _genome
@@ -1160,3 +1162,42 @@ def known_site_intervals(w, res, rng, site_level: bool) -> list:
                     p = lpos(x, cL)
                     out.append((p, p + 500, None) if rng.random() < 0.5 else (p + 500, p, None))
     return out
+
+
+def c3_cached(reads: int, local_rank: int, seed_genome: int = 3, seed_reads: int = 33, scale: float = 1.0,
+              cache_dir: str | None = None, timeout_s: float = 900.0):
+    """The C3 genome and read batch, generated ONCE per node: local rank 0 builds
+    them (c3_genome + c3_windows) into a cache directory (write, then rename, then
+    a completion marker) and every rank maps the files read-only, so N ranks of
+    one node share one copy in the page cache (1.16 GB of blocks + 0.4 GB of
+    batch at the C3 size) instead of N private copies and N start-ups.
+    Returns (PackedGenome, Batch)."""
+    import json
+    import tempfile
+    import time
+    d = cache_dir or os.path.join(tempfile.gettempdir(), "gsnapdp_c3_g%d_r%d_s%g_n%d" % (
+        seed_genome, seed_reads, scale, reads))
+    done = os.path.join(d, "complete.json")
+    names = ("blocks", "windows", "query", "query_uc")
+    if not os.path.exists(done):
+        if local_rank == 0:
+            g = c3_genome(seed=seed_genome, scale=scale)
+            b = c3_windows(g, n=reads, seed=seed_reads)
+            os.makedirs(d, exist_ok=True)
+            for k, a in zip(names, (g.blocks, b.windows, b.query, b.query_uc)):
+                tmp = os.path.join(d, k + ".tmp.npy")
+                np.save(tmp, a, allow_pickle=False)
+                os.replace(tmp, os.path.join(d, k + ".npy"))
+            with open(done + ".tmp", "w") as f:
+                json.dump({"names": g.names, "lengths": [int(x) for x in g.lengths]}, f)
+            os.replace(done + ".tmp", done)
+        else:
+            t0 = time.time()
+            while not os.path.exists(done):
+                if time.time() - t0 > timeout_s:
+                    raise RuntimeError("C3 cache %s not written by local rank 0 within %.0f s" % (d, timeout_s))
+                time.sleep(0.2)
+    meta = json.load(open(done))
+    a = {k: np.load(os.path.join(d, k + ".npy"), mmap_mode="r", allow_pickle=False) for k in names}
+    return PackedGenome(a["blocks"], meta["names"], np.array(meta["lengths"], np.int64)), \
+        Batch(a["windows"], a["query"], a["query_uc"])

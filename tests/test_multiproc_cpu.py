@@ -211,3 +211,63 @@ def test_two_ranks_gloo(tmp_path):
     el = res[0]["elapsed"][0]
     assert abs(res[0]["rate"] - 600 * 2 / el) < 1e-6 * res[0]["rate"]
     assert res[0]["score_sum"] != res[1]["score_sum"]
+
+
+def _bench_path_main(rank, world, port, outdir, cache):
+    """bench.py's own N>1 path on CPU: the node-level C3 cache (every rank maps
+    what local rank 0 wrote), bench.shard_slice, the payload layout with a
+    deliberately short op budget grown by bench.payload_budget (all-reduced),
+    the gather to rank 0 and gather.reassemble."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch
+    import bench
+    import oracle as O
+    from gsnapdp import gather as G
+    from gsnapdp import shard as S
+    from gsnapdp import workload as W
+
+    r = S.init_from_env("gloo")
+    g, batch = W.c3_cached(1603, r.local, scale=0.002, cache_dir=cache)
+    cells = bench.cells_per_window(batch.windows)
+    wl, ql, sizes, lo, hi = bench.shard_slice(batch, cells, world, r.rank)
+    O.setup(np.ascontiguousarray(g.blocks))
+    res, pairs, poff, npairs = O.run_batch(wl, ql, ql, nthreads=1)  # the GPU step's stand-in
+    rr, comp = _payload_of(res, pairs, poff, npairs)
+    lay = G.Layout(max(sizes), 64)  # far too small: 6 words per pair
+    mine = G.pack(lay, rr, comp)
+    grow = bench.payload_budget(r, mine[:G.HEADER], lay)
+    assert grow > 0
+    lay = G.Layout(max(sizes), grow)
+    mine = torch.from_numpy(G.pack(lay, rr, comp))
+    recv = [torch.zeros(lay.nbytes, dtype=torch.uint8) for _ in range(world)] if r.rank == 0 else None
+    S.gather_to_root(r, mine, recv)
+    if r.rank == 0:
+        allres, allops, alloff = G.reassemble(lay, [t.numpy() for t in recv], sizes)
+        np.save(os.path.join(outdir, "res.npy"), allres)
+        np.save(os.path.join(outdir, "ops.npy"), allops)
+        json.dump({"sizes": sizes, "budget": lay.budget}, open(os.path.join(outdir, "meta.json"), "w"))
+    S.finish(r)
+
+
+@pytest.mark.timeout(600)
+def test_bench_path_world8_equals_single_rank(tmp_path):
+    """World 8 (the scaling target's width) through bench.py's functions: one
+    batch, eight slices, one gather, byte-identical to one rank."""
+    world = 8
+    cache = str(tmp_path / "c3cache")
+    mp.spawn(_bench_path_main, args=(world, free_port(), str(tmp_path), cache), nprocs=world, join=True)
+    import oracle as O
+    from gsnapdp import workload as W
+    g, batch = W.c3_cached(1603, 0, scale=0.002, cache_dir=cache)
+    O.setup(np.ascontiguousarray(g.blocks))
+    res, pairs, poff, npairs = O.run_batch(batch.windows, batch.query, batch.query_uc, nthreads=4)
+    rr, comp = _payload_of(res, pairs, poff, npairs)
+    got_res = np.load(os.path.join(str(tmp_path), "res.npy"), allow_pickle=False)
+    got_ops = np.load(os.path.join(str(tmp_path), "ops.npy"), allow_pickle=False)
+    meta = json.load(open(os.path.join(str(tmp_path), "meta.json")))
+    assert len(meta["sizes"]) == 8 and sum(meta["sizes"]) == len(batch) and min(meta["sizes"]) > 0
+    assert got_res.tobytes() == rr.tobytes() and got_ops.tobytes() == comp.tobytes()

@@ -1,0 +1,7 @@
+#!/bin/bash
+# GPU check after a kernel change: parity tests, then the bench line (no CPU leg).
+# usage: bash tools/quick_round.sh TAG  -> gpurun_out/TAG/{pytest_gpu.txt,bench.json}
+O=gpurun_out/${1:?tag}; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 || { echo "tests failed"; tail -5 $O/pytest_gpu.txt; exit 1; }
+tail -1 $O/pytest_gpu.txt
+timeout -k 10 600 python bench.py --steps 20 --warmup 3 --no-cpu > $O/bench.json 2> $O/bench.err
