@@ -1,0 +1,1137 @@
+// gsnapdp_stage3.cpp -- the stage-3 intron pass (build_pairs_introns,
+// stage3.c:7735-7901) for many paths at once, over the batched gap families.
+//
+// Each path is the reference's list: the pass keeps the same cells and the
+// same list operations (Pairpool_pop / List_push_existing / Pairpool_transfer,
+// pairpool.c:471-519), so every peel, put-back and transfer leaves the lists
+// exactly as the reference leaves them.  What changes is the control flow
+// around the DP: a path runs until it needs a gap filled, parks its window,
+// and resumes when the round's batch for that gap family has run.  Rounds go
+// on until every path has reached the end of its list.
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/gsnapdp.h"
+#include "gsnapdp_internal.h"
+
+extern "C" const uint32_t* gsnapdp__host_blocks(gsnapdp_ctx* ctx);
+extern "C" size_t gsnapdp__host_nwords(gsnapdp_ctx* ctx);
+void gsnapdp__set_err(const std::string& s);  // gsnapdp_kernels.hip
+
+namespace {
+
+using gsnapdp::ST_EARLY;
+using gsnapdp::ST_INTERNAL;
+using gsnapdp::ST_OK;
+using gsnapdp::ST_OPS_OVERFLOW;
+using gsnapdp::ST_UNSUPPORTED;
+
+// stage3.c:50-70, dynprog.h:27-30, scores.h:7-8, intron.h:22-28
+constexpr int SINGLESLEN = 9, MININTRONLEN = 9, MININTRONLEN_FINAL = 50, EXTRAQUERYGAP = 10;
+constexpr int SUFFCONSECUTIVE = 5;
+constexpr int UNKNOWNJUMP = -1000000;
+constexpr int QOPEN = -5, QINDEL = -2;
+constexpr double DEFECT_HIGHQ = 0.003, DEFECT_MEDQ = 0.014;
+constexpr int NONINTRON = 0, GTAG_FWD = 0x20, GTAG_REV = 0x04;
+constexpr int BIG = 0x3fffffff;  // a workspace limit no window reaches
+
+enum Fam { F_GAP = 0, F_GGAP = 1, F_CGAP = 2, F_MICRO = 3, F_N = 4, F_NONE = -1 };
+
+float bin(double defect_rate) {  // dynprog.c:4471-4486: only the bin matters
+  return defect_rate < 0.003 ? 0.001f : (defect_rate < 0.014 ? 0.01f : 0.5f);
+}
+
+// UPPERCASE_U2T (complement.h:36) as peel_* compares pairs (stage3.c:4884)
+char upper_u2t(char c) {
+  if (c >= 'a' && c <= 'z') c = (char)(c - 'a' + 'A');
+  return c == 'U' ? 'T' : c;
+}
+bool unknown_base(char c) {  // pair.c
+  switch (c) {
+    case 'A': case 'C': case 'G': case 'T': case 'U':
+    case 'a': case 'c': case 'g': case 't': case 'u': return false;
+    default: return true;
+  }
+}
+
+// One path's pairs and list cells.  Cells are never freed; a cell's pair
+// index never changes (List_push_existing re-links the cell itself).
+struct Arena {
+  std::vector<gsnapdp_s3_pair> pr;
+  std::vector<int> cp, cn;
+  int cell(int pair, int next) {
+    cp.push_back(pair);
+    cn.push_back(next);
+    return (int)cp.size() - 1;
+  }
+  int pop(int list, int* pair) const {  // Pairpool_pop
+    *pair = cp[(size_t)list];
+    return cn[(size_t)list];
+  }
+  int push_existing(int list, int c) {  // List_push_existing
+    cn[(size_t)c] = list;
+    return c;
+  }
+  int transfer(int dest, int src) {  // Pairpool_transfer
+    for (int p = src, nx; p >= 0; p = nx) {
+      nx = cn[(size_t)p];
+      cn[(size_t)p] = dest;
+      dest = p;
+    }
+    return dest;
+  }
+  gsnapdp_s3_pair& at(int pair) { return pr[(size_t)pair]; }
+  gsnapdp_s3_pair& first(int list) { return pr[(size_t)cp[(size_t)list]]; }
+  int rest(int list) const { return cn[(size_t)list]; }
+  int push_pair(int list, const gsnapdp_s3_pair& x) {
+    pr.push_back(x);
+    return cell((int)pr.size() - 1, list);
+  }
+};
+bool gapp(const gsnapdp_s3_pair& p) { return (p.flags & GSNAPDP_S3_GAPP) != 0; }
+
+// The DP window a path is waiting for, in the batched C-ABI's records.
+struct Req {
+  int fam = F_NONE;
+  std::vector<char> q, qu;  // the window's query bytes; qpos fields are relative to them
+  int64_t cap = 0;
+  std::vector<uint32_t> ops;
+  gsnapdp_window w;
+  gsnapdp_result r;
+  gsnapdp_ggap_window gw;
+  gsnapdp_ggap_result gr;
+  gsnapdp_ggap_trace gt;
+  gsnapdp_cgap_window cw;
+  gsnapdp_cgap_result cr;
+  gsnapdp_micro_window mw;
+  gsnapdp_micro_result mr;
+};
+
+// where a path resumes when its window has run
+enum Stage {
+  S_SCAN,         // between gaps
+  S_SINGLE,       // traverse_single_gap's Dynprog_single_gap
+  S_CDNA_SINGLE,  // traverse_cdna_gap: "really a single gap"
+  S_CDNA,         // traverse_cdna_gap's Dynprog_cdna_gap
+  S_GG_SINGLE,    // traverse_genome_gap: "really a single gap"
+  S_GG_SCORE,     // traverse_genome_gap's score-mode Dynprog_genome_gap
+  S_GG_PROB,      // its probability-mode re-run
+  S_GG_MICRO,     // its Dynprog_microexon_int
+  S_DONE
+};
+
+struct Path {
+  gsnapdp_s3_call* c = nullptr;
+  const char* q = nullptr;   // queryseq_ptr
+  const char* qu = nullptr;  // queryuc_ptr
+  Arena A;
+  int path = -1, pairs = -1;
+  int stage = S_SCAN;
+  bool failed = false;
+  std::string why;
+  // build_pairs_introns' counters (its in/out arguments)
+  int minor = 0, major = 0, nintrons = 0, nnonintrons = 0, intronlen = 0, nonintronlen = 0;
+  bool shiftp = false, incompletep = false;
+  // the gap being traversed (pairptr, leftpair, rightpair) and its peels
+  int gapcell = -1, left = -1, right = -1;
+  int peeled_pairs = -1, peeled_path = -1;
+  int querydp5 = 0, genomedp5 = 0, querydp3 = 0, genomedp3 = 0, queryjump = 0, genomejump = 0;
+  // traverse_genome_gap's locals.  new_left/right and introntype keep their
+  // values across that function's calls, like the reference's stack slots do
+  // when a Dynprog_genome_gap early return leaves them unwritten.
+  int finalscore = 0, nmatches = 0, nmismatches = 0, nopens = 0, nindels = 0, exonhead = 0;
+  int new_left = 0, new_right = 0, introntype = 0;
+  double left_prob = 0.0, right_prob = 0.0;
+  int gappairs = -1;
+  Req req;
+};
+
+struct Pass {
+  gsnapdp_ctx* ctx;
+  const uint32_t* blocks;
+  size_t nwords;
+  gsnapdp_s3_stats st;
+};
+
+// ---- genome characters (stage3.c get_genomic_nt, with no genomic segment)
+char genomic_nt(const Pass& P, const Path& k, int gpos) {
+  const gsnapdp_s3_call& c = *k.c;
+  if (gpos < 0 || gpos >= c.genomiclength) return '*';
+  const uint32_t base = c.chroffset + c.chrpos;
+  if (base < c.chroffset || base >= c.chrhigh) return '*';
+  const uint32_t pos = c.watsonp ? base + (uint32_t)gpos : base + (uint32_t)(c.genomiclength - 1) - (uint32_t)gpos;
+  const size_t ptr = (size_t)(pos >> 5) * 3;
+  if (ptr + 2 >= P.nwords) return 'N';
+  const uint32_t bit = pos & 31u;
+  char ch = 'N';
+  if (!((P.blocks[ptr + 2] >> bit) & 1u))
+    ch = "ACGT"[((bit < 16 ? P.blocks[ptr + 1] : P.blocks[ptr]) >> ((bit & 15u) * 2u)) & 3u];
+  if (c.watsonp) return ch;
+  switch (ch) {  // complCode
+    case 'A': return 'T';
+    case 'C': return 'G';
+    case 'G': return 'C';
+    case 'T': return 'A';
+    default: return 'N';
+  }
+}
+int nt_class(char ch) {
+  switch (ch) {
+    case 'A': return 0;
+    case 'C': return 1;
+    case 'G': return 2;
+    case 'T': return 3;
+    case '*': return 5;
+    default: return 4;
+  }
+}
+
+// ---- Pair_fracidentity (pair.c:5426) and Dynprog_score (dynprog.c:381-394):
+// the score of a peeled stretch, for traverse_single_gap's accept test
+int peeled_score(Arena& A, int list, int cdna_direction, double defect_rate, std::string* err) {
+  (void)cdna_direction;  // only the canonical-intron counts depend on it
+  int matches = 0, mismatches = 0, qopens = 0, qindels = 0, topens = 0, tindels = 0;
+  int prev = -1;
+  for (int p = list; p >= 0; p = A.rest(p)) {
+    const gsnapdp_s3_pair& x = A.first(p);
+    if (!gapp(x)) {
+      if (x.comp == '-' || x.comp == '~') {
+        if (x.cdna == ' ') {
+          tindels++;
+          if (prev >= 0 && A.at(prev).cdna != ' ') topens++;
+        } else if (x.genome == ' ') {
+          qindels++;
+          if (prev >= 0 && A.at(prev).genome != ' ') qopens++;
+        } else {
+          *err = "Pair_fracidentity: cannot parse comp";  // the reference aborts
+          return 0;
+        }
+      } else if (unknown_base(x.cdna) || unknown_base(x.genome) || x.comp == ':') {
+        // unknowns
+      } else if (x.comp == '|' || x.comp == '*' || x.comp == ':') {
+        matches++;
+      } else if (x.comp == ' ') {
+        mismatches++;
+      } else {
+        *err = "Pair_fracidentity: cannot parse comp";
+        return 0;
+      }
+    }
+    prev = A.cp[(size_t)p];
+  }
+  const int mism = defect_rate < DEFECT_HIGHQ ? -3 : (defect_rate < DEFECT_MEDQ ? -2 : -1);
+  return 3 * matches + mism * mismatches - 10 * qopens - 3 * qindels - 10 * topens - 3 * tindels;
+}
+int dynprog_score(int qopens, int qindels, int topens, int tindels) {
+  return -10 * qopens - 3 * qindels - 10 * topens - 3 * tindels;  // every bin: open -10, extend -3
+}
+
+// ---- peel_rightward / peel_leftward (stage3.c:5126-5378, :4887-5122) without
+// end-gap pairs (every caller here passes endgappairs = NULL)
+int peel_rightward(Arena& A, bool* mismatchp, int* peeled_pairs, int pairs, int* querydp3,
+                   int* genomedp3, int maxpeelback, bool throughmismatchp) {
+  int peeled = -1, rest = -1, pair = -1, nextpair = -1, npeelback = 0, nconsecutive = 0;
+  *mismatchp = false;
+  if (pairs >= 0) {
+    if (gapp(A.first(pairs))) {  // throw away known gap
+      const int ptr = pairs;
+      pairs = A.pop(pairs, &pair);
+      peeled = A.push_existing(peeled, ptr);
+    }
+    rest = A.rest(pairs);
+    bool stopp = false;
+    while (rest >= 0 && !stopp) {
+      nextpair = A.cp[(size_t)rest];
+      const gsnapdp_s3_pair& nx = A.at(nextpair);
+      if (gapp(nx) || nx.cdna == ' ' || nx.genome == ' ') stopp = true;
+      const int ptr = pairs;
+      pairs = A.pop(pairs, &pair);
+      peeled = A.push_existing(peeled, ptr);
+      if (upper_u2t(A.at(pair).cdna) != upper_u2t(A.at(pair).genome)) *mismatchp = true;
+      if (++npeelback >= maxpeelback) stopp = true;
+      rest = A.rest(pairs);
+    }
+    if (throughmismatchp && rest >= 0 && !gapp(A.at(nextpair))) {
+      stopp = false;
+      while (rest >= 0 && !stopp) {
+        nextpair = A.cp[(size_t)rest];
+        if (gapp(A.at(nextpair))) stopp = true;
+        const int ptr = pairs;
+        pairs = A.pop(pairs, &pair);
+        peeled = A.push_existing(peeled, ptr);
+        const gsnapdp_s3_pair& x = A.at(pair);
+        if (upper_u2t(x.cdna) != upper_u2t(x.genome)) *mismatchp = true;
+        if (x.comp == '-' || x.comp == ' ') nconsecutive = 0;
+        else if (++nconsecutive >= SUFFCONSECUTIVE) stopp = true;
+        rest = A.rest(pairs);
+      }
+    }
+  }
+  if (peeled >= 0) {
+    const gsnapdp_s3_pair& lp = A.first(peeled);
+    if (gapp(lp)) {  // ran into a gap: undo the peel
+      pairs = A.transfer(pairs, peeled);
+      *peeled_pairs = -1;
+      return pairs;
+    }
+    *querydp3 = lp.cdna == ' ' ? lp.querypos - 1 : lp.querypos;
+    *genomedp3 = lp.genome == ' ' ? lp.genomepos - 1 : lp.genomepos;
+  }
+  *peeled_pairs = peeled;
+  return pairs;
+}
+
+int peel_leftward(Arena& A, bool* mismatchp, int* peeled_path, int path, int* querydp5, int* genomedp5,
+                  int maxpeelback, bool throughmismatchp) {
+  int peeled = -1, rest = -1, pair = -1, nextpair = -1, npeelback = 0, nconsecutive = 0;
+  *mismatchp = false;
+  if (path >= 0) {
+    if (gapp(A.first(path))) {
+      const int ptr = path;
+      path = A.pop(path, &pair);
+      peeled = A.push_existing(peeled, ptr);
+    }
+    rest = A.rest(path);
+    bool stopp = false;
+    while (rest >= 0 && !stopp) {
+      nextpair = A.cp[(size_t)rest];
+      const gsnapdp_s3_pair& nx = A.at(nextpair);
+      if (gapp(nx) || nx.cdna == ' ' || nx.genome == ' ') stopp = true;
+      const int ptr = path;
+      path = A.pop(path, &pair);
+      peeled = A.push_existing(peeled, ptr);
+      if (upper_u2t(A.at(pair).cdna) != upper_u2t(A.at(pair).genome)) *mismatchp = true;
+      if (++npeelback >= maxpeelback) stopp = true;
+      rest = A.rest(path);
+    }
+    if (throughmismatchp && rest >= 0 && !gapp(A.at(nextpair))) {
+      stopp = false;
+      while (rest >= 0 && !stopp) {
+        nextpair = A.cp[(size_t)rest];
+        if (gapp(A.at(nextpair))) stopp = true;
+        const int ptr = path;
+        path = A.pop(path, &pair);
+        peeled = A.push_existing(peeled, ptr);
+        const gsnapdp_s3_pair& x = A.at(pair);
+        if (upper_u2t(x.cdna) != upper_u2t(x.genome)) *mismatchp = true;
+        if (x.comp == '-' || x.comp == ' ') nconsecutive = 0;
+        else if (++nconsecutive >= SUFFCONSECUTIVE) stopp = true;
+        rest = A.rest(path);
+      }
+    }
+  }
+  if (peeled >= 0) {
+    const gsnapdp_s3_pair& rp = A.first(peeled);
+    if (gapp(rp)) {
+      path = A.transfer(path, peeled);
+      *peeled_path = -1;
+      return path;
+    }
+    *querydp5 = rp.querypos;
+    *genomedp5 = rp.genomepos;
+  }
+  *peeled_path = peeled;
+  return path;
+}
+
+// ---- the DP windows, built exactly as the drop-in's Dynprog_* entry points
+// build them (gsnapdp_dropin.cpp), from the arguments stage 3 passes
+
+// query bytes [from, from + n) of the path, zero past its end, dword padded
+void stage_query(const Path& k, Req& R, int from, int n, size_t extra = 0) {
+  const size_t sz = (((size_t)(n > 0 ? n : 0) + 8 + 3) & ~(size_t)3) + extra;
+  R.q.assign(sz, 0);
+  R.qu.assign(sz, 0);
+  for (int i = 0; i < n; i++) {
+    const int p = from + i;
+    if (p >= 0 && p < k.c->querylength) {
+      R.q[(size_t)i] = k.q[p];
+      R.qu[(size_t)i] = k.qu[p];
+    }
+  }
+}
+
+// Dynprog_single_gap (dynprog.c:4450-4572), widebandp = true, on dynprogM
+void req_single(Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  Req& R = k.req;
+  R.fam = F_GAP;
+  gsnapdp_window& w = R.w;
+  memset(&w, 0, sizeof(w));
+  w.kind = GSNAPDP_SINGLE_GAP;
+  w.length1 = k.queryjump;
+  w.length2 = k.genomejump;
+  w.offset1 = k.querydp5;
+  w.offset2 = k.genomedp5;
+  w.chroffset = c.chroffset;
+  w.chrhigh = c.chrhigh;
+  w.chrpos = c.chrpos;
+  w.genomiclength = (uint32_t)c.genomiclength;
+  w.cdna_direction = c.cdna_direction;
+  w.extraband = c.extraband_single;
+  w.dynprogindex = k.minor;
+  w.maxlength1 = c.maxlength1[1];
+  w.maxlength2 = c.maxlength2[1];
+  w.defect_rate = bin(c.defect_rate);
+  w.watsonp = c.watsonp ? 1 : 0;
+  w.jump_late_p = c.jump_late_p ? 1 : 0;
+  w.widebandp = 1;
+  stage_query(k, R, k.querydp5, k.queryjump);
+  w.qpos = 0;
+  R.cap = (int64_t)(k.queryjump > 0 ? k.queryjump : 0) + (k.genomejump > 0 ? k.genomejump : 0) + 2;
+}
+
+// Dynprog_genome_gap (dynprog.c:4798-5061), halfp = false, no splicing IIT
+void req_genome(Path& k, bool prob, int score_threshold) {
+  const gsnapdp_s3_call& c = *k.c;
+  Req& R = k.req;
+  R.fam = F_GGAP;
+  gsnapdp_ggap_window& w = R.gw;
+  memset(&w, 0, sizeof(w));
+  w.length1 = k.queryjump;
+  w.length2L = k.genomejump;
+  w.length2R = k.genomejump;
+  w.offset1 = k.querydp5;
+  w.offset2L = k.genomedp5;
+  w.revoffset2R = k.genomedp3;
+  w.chroffset = c.chroffset;
+  w.chrhigh = c.chrhigh;
+  w.chrpos = c.chrpos;
+  w.genomiclength = (uint32_t)c.genomiclength;
+  w.qpos = 0;
+  w.cdna_direction = c.cdna_direction;
+  w.extraband_paired = c.extraband_paired;
+  w.maxpeelback = c.maxpeelback;
+  w.score_threshold = score_threshold;
+  w.dynprogindex = k.major;
+  // the two workspaces' limits (:4898-4927), folded into one exact test
+  const bool too_long = k.queryjump > c.maxlength1[0] || k.genomejump > c.maxlength2[0] ||
+                        k.queryjump > c.maxlength1[2] || k.genomejump > c.maxlength2[2];
+  w.maxlength1 = too_long ? -1 : BIG;
+  w.maxlength2 = BIG;
+  w.defect_rate = bin(c.defect_rate);
+  w.watsonp = c.watsonp ? 1 : 0;
+  w.jump_late_p = c.jump_late_p ? 1 : 0;
+  w.halfp = 0;
+  w.finalp = (prob || c.finalp) ? 1 : 0;
+  w.use_probabilities_p = prob ? 1 : 0;
+  w.splicingp = c.splicingp ? 1 : 0;
+  w.known_mode = GSNAPDP_KNOWN_NONE;
+  stage_query(k, R, k.querydp5, k.queryjump);
+  const int L1 = k.queryjump > 0 ? k.queryjump : 0;
+  R.cap = 2 * (int64_t)L1 + 2 * (int64_t)(k.genomejump > 0 ? k.genomejump : 0) + 4;
+}
+
+// Dynprog_cdna_gap (dynprog.c:4578-4793): length1L = length1R = queryjump
+void req_cdna(Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  Req& R = k.req;
+  R.fam = F_CGAP;
+  gsnapdp_cgap_window& w = R.cw;
+  memset(&w, 0, sizeof(w));
+  const int length1 = k.queryjump, length2 = k.genomejump;
+  w.length1L = length1;
+  w.length1R = length1;
+  w.length2 = length2;
+  w.offset1L = k.querydp5;
+  w.revoffset1R = k.querydp3;
+  w.offset2 = k.genomedp5;
+  w.chroffset = c.chroffset;
+  w.chrhigh = c.chrhigh;
+  w.chrpos = c.chrpos;
+  w.genomiclength = (uint32_t)c.genomiclength;
+  w.cdna_direction = c.cdna_direction;
+  w.extraband_paired = c.extraband_paired;
+  w.dynprogindex = k.major;
+  const bool too_long = length2 > c.maxlength1[2] || length1 > c.maxlength2[2] || length2 > c.maxlength1[0] ||
+                        length1 > c.maxlength2[0];
+  w.maxlength1 = too_long ? -1 : BIG;
+  w.maxlength2 = BIG;
+  w.defect_rate = bin(c.defect_rate);
+  w.watsonp = c.watsonp ? 1 : 0;
+  w.jump_late_p = c.jump_late_p ? 1 : 0;
+  // sequence1L[0 .. span) forwards, then revsequence1R[-(nR-1) .. 0]
+  const int nL = length1 > 0 ? length1 : 0, nR = nL;
+  const int span = k.querydp3 - k.querydp5 + 1 > nL ? k.querydp3 - k.querydp5 + 1 : nL;
+  R.q.assign(((size_t)span + nR + 8 + 3) & ~(size_t)3, 0);
+  R.qu.assign(R.q.size(), 0);
+  if (length2 > 1) {
+    for (int i = 0; i < span; i++) {
+      const int p = k.querydp5 + i;
+      if (p >= 0 && p < c.querylength) {
+        R.q[(size_t)i] = k.q[p];
+        R.qu[(size_t)i] = k.qu[p];
+      }
+    }
+    for (int i = 0; i < nR; i++) {
+      const int p = k.querydp3 - (nR - 1) + i;
+      if (p >= 0 && p < c.querylength) {
+        R.q[(size_t)(span + i)] = k.q[p];
+        R.qu[(size_t)(span + i)] = k.qu[p];
+      }
+    }
+  }
+  w.qposL = 0;
+  w.qposR = (uint32_t)(span + nR - 1);
+  R.cap = (int64_t)nL + nR + 2 * (int64_t)(length2 > 0 ? length2 : 0) + 4;
+}
+
+// Dynprog_microexon_int (dynprog.c:7128-7432): sequence1 = &queryseq[offset1]
+void req_micro(Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  Req& R = k.req;
+  R.fam = F_MICRO;
+  const int L1 = k.queryjump > 0 ? k.queryjump : 0;
+  const size_t pbase = ((size_t)L1 + 8 + 3) & ~(size_t)3;
+  stage_query(k, R, k.querydp5, L1, pbase);
+  for (int i = 0; i < L1; i++) {
+    R.q[pbase + (size_t)i] = R.q[(size_t)i];
+    R.qu[pbase + (size_t)i] = R.qu[(size_t)i];
+  }
+  gsnapdp_micro_window& w = R.mw;
+  memset(&w, 0, sizeof(w));
+  w.length1 = k.queryjump;
+  w.offset1 = k.querydp5;
+  w.offset2L = k.genomedp5;
+  w.revoffset2R = k.genomedp3;
+  w.cdna_direction = c.cdna_direction;
+  w.dynprogindex = k.major;
+  w.chroffset = c.chroffset;
+  w.chrhigh = c.chrhigh;
+  w.chrpos = c.chrpos;
+  w.genomiclength = (uint32_t)c.genomiclength;
+  w.qpos = 0;
+  w.ppos = (uint32_t)pbase;
+  w.defect_rate = bin(c.defect_rate);
+  w.watsonp = c.watsonp ? 1 : 0;
+  R.cap = 0;
+}
+
+void fail(Path& k, const std::string& why) {
+  if (!k.failed) k.why = why;
+  k.failed = true;
+  k.stage = S_DONE;
+  k.req.fam = F_NONE;
+}
+
+// a gap family's expanded pairs as a list in the path's arena (push order as
+// the drop-in's push_pairs: the list's head is pairs[0])
+int list_of(Arena& A, const std::vector<gsnapdp_pair>& v, int n, bool micro) {
+  int list = -1;
+  for (int i = n - 1; i >= 0; i--) {
+    const gsnapdp_pair& p = v[(size_t)i];
+    gsnapdp_s3_pair x;
+    memset(&x, 0, sizeof(x));
+    x.src = -1;
+    if (p.gapp) {  // Pairpool_push_gapholder (pairpool.c:352-410)
+      x.querypos = -1;
+      x.genomepos = -1;
+      x.queryjump = p.queryjump;
+      x.genomejump = p.genomejump;
+      x.dynprogindex = 0;
+      x.cdna = ' ';
+      x.comp = micro ? p.comp : ' ';  // gappair->comp = gapchar (dynprog.c:6991)
+      x.genome = ' ';
+      x.flags = (uint8_t)(GSNAPDP_S3_GAPP | ((p.gapp & 2) ? GSNAPDP_S3_KNOWNGAPP : 0));
+    } else {  // Pairpool_push (pairpool.c:169-240)
+      x.querypos = p.querypos;
+      x.genomepos = p.genomepos;
+      x.dynprogindex = p.dynprogindex;
+      x.cdna = p.cdna;
+      x.comp = p.comp;
+      x.genome = p.genome;
+    }
+    list = A.push_pair(list, x);
+  }
+  return list;
+}
+
+// ---- results, read back exactly as the drop-in reads them
+bool done_single(Pass& P, Path& k, int* list) {
+  Req& R = k.req;
+  const gsnapdp_result& r = R.r;
+  if (r.status == ST_UNSUPPORTED) {
+    fail(k, "single-gap window outside the reference's domain (the reference aborts)");
+    return false;
+  }
+  if (r.status == ST_OPS_OVERFLOW) {
+    fail(k, "op stream overflow");
+    return false;
+  }
+  std::vector<gsnapdp_pair> v((size_t)R.cap + 8);
+  int fs = 0;
+  const int n = gsnapdp_expand(P.ctx, &R.w, &r, R.ops.data(), R.q.data(), R.qu.data(), v.data(), (int)v.size(), &fs);
+  if (n < 0 || n > (int)v.size()) {
+    fail(k, "gsnapdp_expand failed");
+    return false;
+  }
+  k.minor = r.reserved;
+  k.finalscore = r.finalscore;
+  k.nmatches = r.nmatches;
+  k.nmismatches = r.nmismatches;
+  k.nopens = r.nopens;
+  k.nindels = r.nindels;
+  *list = list_of(k.A, v, n, false);
+  return true;
+}
+
+// Dynprog_genome_gap's out-parameters into the traversal's variables
+// (finalscore, nmismatches, left/right probs: the score call's or the re-run's)
+bool done_genome(Pass& P, Path& k, int* finalscore, int* nmismatches, double* lp, double* rp, int* list) {
+  Req& R = k.req;
+  const gsnapdp_ggap_window& w = R.gw;
+  const gsnapdp_ggap_result& r = R.gr;
+  const gsnapdp_ggap_trace& t = R.gt;
+  *list = -1;
+  if (t.status == ST_UNSUPPORTED) {
+    fail(k, "genome-gap window outside the reference's domain");
+    return false;
+  }
+  if (t.status == ST_OPS_OVERFLOW || t.status == ST_INTERNAL) {
+    fail(k, t.status == ST_INTERNAL ? "genome-gap kernel invariant failed" : "op stream overflow");
+    return false;
+  }
+  k.nmatches = *nmismatches = k.nopens = k.nindels = 0;  // :4853-4854
+  *lp = *rp = 0.0;
+  *finalscore = r.finalscore;
+  k.major = r.dynprogindex;
+  if (t.status == ST_EARLY) {
+    if (w.maxlength1 == -1) {  // too long (:4898-4927)
+      k.new_left = r.new_leftgenomepos;
+      k.new_right = r.new_rightgenomepos;
+      k.exonhead = r.exonhead;
+    }
+    return true;
+  }
+  if (r.bridge_ok == 0) {
+    P.st.undefined++;
+    return true;
+  }
+  if (!w.use_probabilities_p && r.finalscore != -100000) k.introntype = r.introntype;
+  if (!t.bridge_accepted) return true;
+  k.new_left = r.new_leftgenomepos;
+  k.new_right = r.new_rightgenomepos;
+  k.exonhead = r.exonhead;
+  *lp = r.left_prob;
+  *rp = r.right_prob;
+  k.nmatches = r.nmatches;
+  *nmismatches = r.nmismatches;
+  k.nopens = r.nopens;
+  k.nindels = r.nindels;
+  if (r.returned_null) return true;
+  std::vector<gsnapdp_pair> v((size_t)R.cap + 8);
+  const int n = gsnapdp_ggap_expand(P.ctx, &w, &r, &t, R.ops.data(), R.q.data(), R.qu.data(), v.data(), (int)v.size());
+  if (n < 0 || n > (int)v.size()) {
+    fail(k, "gsnapdp_ggap_expand failed");
+    return false;
+  }
+  *list = list_of(k.A, v, n, false);
+  return true;
+}
+
+bool done_cdna(Pass& P, Path& k, int* list) {
+  Req& R = k.req;
+  const gsnapdp_cgap_result& r = R.cr;
+  *list = -1;
+  if (r.status == ST_UNSUPPORTED) {
+    fail(k, "cDNA-gap window outside the reference's domain (the reference aborts)");
+    return false;
+  }
+  if (r.status == ST_OPS_OVERFLOW) {
+    fail(k, "op stream overflow");
+    return false;
+  }
+  k.major = r.dynprogindex;
+  if (r.finalscore_set) k.finalscore = r.finalscore;
+  if (r.status != ST_OK) return true;
+  if (r.incompletep) k.incompletep = true;  // only ever set to true (:4756)
+  if (r.returned_null) return true;
+  std::vector<gsnapdp_pair> v((size_t)R.cap + 32);
+  const int n = gsnapdp_cgap_expand(P.ctx, &R.cw, &r, R.ops.data(), R.q.data(), R.qu.data(), nullptr, v.data(),
+                                    (int)v.size());
+  if (n < 0 || n > (int)v.size()) {
+    fail(k, "gsnapdp_cgap_expand failed");
+    return false;
+  }
+  *list = list_of(k.A, v, n, false);
+  return true;
+}
+
+bool done_micro(Pass& P, Path& k, double* prob2, double* prob3, int* microintrontype, int* list) {
+  Req& R = k.req;
+  const gsnapdp_micro_result& r = R.mr;
+  *list = -1;
+  if (r.status != 0) {
+    fail(k, "microexon window outside the reference's domain");
+    return false;
+  }
+  *prob2 = r.bestprob2;
+  *prob3 = r.bestprob3;
+  *microintrontype = r.microintrontype;
+  k.major = r.dynprogindex;
+  if (!r.found) return true;
+  const int L1 = R.mw.length1 > 0 ? R.mw.length1 : 0;
+  std::vector<gsnapdp_pair> v((size_t)L1 + 4);
+  const int n = gsnapdp_micro_expand(P.ctx, &R.mw, &r, R.q.data(), R.qu.data(), v.data(), (int)v.size());
+  if (n <= 0 || n > (int)v.size()) {
+    fail(k, "gsnapdp_micro_expand failed");
+    return false;
+  }
+  *list = list_of(k.A, v, n, true);
+  return true;
+}
+
+// ---- the traversals, split where they wait for a window
+
+// the dp5 / dp3 start of every traverse_* (stage3.c:5404-5409)
+void gap_bounds(Path& k) {
+  const gsnapdp_s3_pair& lp = k.A.at(k.left);
+  const gsnapdp_s3_pair& rp = k.A.at(k.right);
+  k.querydp5 = lp.querypos + 1;
+  k.genomedp5 = lp.genomepos + 1;
+  if (lp.cdna == ' ') k.querydp5--;
+  if (lp.genome == ' ') k.genomedp5--;
+  k.querydp3 = rp.querypos - 1;
+  k.genomedp3 = rp.genomepos - 1;
+}
+bool repeel_prior(Path& k) {  // "Re-peeling prior solution" (:5546, :5677)
+  const gsnapdp_s3_pair& lp = k.A.at(k.left);
+  const gsnapdp_s3_pair& rp = k.A.at(k.right);
+  return lp.dynprogindex < 0 && lp.dynprogindex == rp.dynprogindex;
+}
+void put_back(Path& k) {
+  k.pairs = k.A.transfer(k.pairs, k.peeled_pairs);
+  k.path = k.A.transfer(k.path, k.peeled_path);
+}
+void end_gap(Path& k, bool filledp) {  // build_pairs_introns after a traverse_*
+  if (!filledp) k.pairs = k.A.push_existing(k.pairs, k.gapcell);  // replace the gap
+  k.stage = S_SCAN;
+}
+
+// traverse_single_gap (:5381-5515), forcep = false.  Returns true when it waits.
+bool single_start(Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  bool mm = false;
+  gap_bounds(k);
+  k.pairs = peel_rightward(k.A, &mm, &k.peeled_pairs, k.pairs, &k.querydp3, &k.genomedp3, c.maxpeelback, false);
+  k.path = peel_leftward(k.A, &mm, &k.peeled_path, k.path, &k.querydp5, &k.genomedp5, c.maxpeelback, false);
+  k.queryjump = k.querydp3 - k.querydp5 + 1;
+  k.genomejump = k.genomedp3 - k.genomedp5 + 1;
+  if (k.queryjump <= 0 || k.genomejump <= 0) {
+    put_back(k);
+    end_gap(k, false);
+    return false;
+  }
+  req_single(k);
+  k.stage = S_SINGLE;
+  return true;
+}
+void single_done(Pass& P, Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  int gappairs = -1;
+  if (!done_single(P, k, &gappairs)) return;
+  std::string err;
+  int origscore = peeled_score(k.A, k.peeled_pairs, c.cdna_direction, c.defect_rate, &err);
+  origscore += peeled_score(k.A, k.peeled_path, c.cdna_direction, c.defect_rate, &err);
+  if (!err.empty()) return fail(k, err);
+  const gsnapdp_s3_pair& lp = k.A.at(k.left);
+  const gsnapdp_s3_pair& rp = k.A.at(k.right);
+  const int queryjump = rp.querypos - lp.querypos - 1;
+  if (queryjump > 0) origscore += dynprog_score(1, queryjump, 0, 0);
+  const int genomejump = (int)((uint32_t)rp.genomepos - (uint32_t)lp.genomepos - 1u);
+  if (genomejump > 0) origscore += dynprog_score(0, 0, 1, genomejump);
+  if (origscore > k.finalscore) {
+    put_back(k);
+    end_gap(k, false);
+  } else {
+    k.pairs = k.A.transfer(k.pairs, gappairs);
+    end_gap(k, true);
+  }
+}
+
+// traverse_cdna_gap (:5518-5627)
+bool cdna_start(Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  bool mm = false;
+  gap_bounds(k);
+  const bool through = !repeel_prior(k);
+  k.pairs = peel_rightward(k.A, &mm, &k.peeled_pairs, k.pairs, &k.querydp3, &k.genomedp3, c.maxpeelback, through);
+  k.path = peel_leftward(k.A, &mm, &k.peeled_path, k.path, &k.querydp5, &k.genomedp5, c.maxpeelback, through);
+  k.queryjump = k.querydp3 - k.querydp5 + 1;
+  k.genomejump = k.genomedp3 - k.genomedp5 + 1;
+  if (k.queryjump <= k.genomejump + MININTRONLEN) {  // really a single gap
+    req_single(k);
+    k.stage = S_CDNA_SINGLE;
+  } else {  // square matrices
+    k.queryjump = k.genomejump + c.extramaterial_paired;
+    req_cdna(k);
+    k.stage = S_CDNA;
+  }
+  return true;
+}
+void cdna_done(Pass& P, Path& k) {
+  int gappairs = -1;
+  if (k.stage == S_CDNA_SINGLE) {
+    if (!done_single(P, k, &gappairs)) return;
+    k.pairs = k.A.transfer(k.pairs, gappairs);
+    return end_gap(k, true);
+  }
+  if (!done_cdna(P, k, &gappairs)) return;
+  if (gappairs < 0) {
+    put_back(k);
+    gsnapdp_s3_pair g;
+    memset(&g, 0, sizeof(g));
+    g.querypos = -1;
+    g.genomepos = -1;
+    g.queryjump = UNKNOWNJUMP;
+    g.genomejump = UNKNOWNJUMP;
+    g.src = -1;
+    g.cdna = g.comp = g.genome = ' ';
+    g.flags = GSNAPDP_S3_GAPP;
+    k.pairs = k.A.push_pair(k.pairs, g);
+  } else {
+    k.pairs = k.A.transfer(k.pairs, gappairs);
+  }
+  end_gap(k, true);
+}
+
+// traverse_genome_gap (:5633-5976), SHORTCUT on (stage3.c:142)
+bool genome_start(Pass& P, Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  bool mr = false, ml = false;
+  gap_bounds(k);
+  const bool through = !repeel_prior(k);
+  if (k.querydp5 != k.querydp3 + 1) {
+    k.pairs = peel_rightward(k.A, &mr, &k.peeled_pairs, k.pairs, &k.querydp3, &k.genomedp3, c.maxpeelback, through);
+    k.path = peel_leftward(k.A, &ml, &k.peeled_path, k.path, &k.querydp5, &k.genomedp5, c.maxpeelback, through);
+  } else {
+    const int l1 = nt_class(genomic_nt(P, k, k.genomedp5)), l2 = nt_class(genomic_nt(P, k, k.genomedp5 + 1));
+    const int r2 = nt_class(genomic_nt(P, k, k.genomedp3 - 1)), r1 = nt_class(genomic_nt(P, k, k.genomedp3));
+    k.introntype = gsnapdp::intron_type_codes(l1, l2, r2, r1, c.cdna_direction);
+    k.pairs = peel_rightward(k.A, &mr, &k.peeled_pairs, k.pairs, &k.querydp3, &k.genomedp3, c.maxpeelback, through);
+    k.path = peel_leftward(k.A, &ml, &k.peeled_path, k.path, &k.querydp5, &k.genomedp5, c.maxpeelback, through);
+    if (c.novelsplicingp && !mr && !ml &&
+        ((c.cdna_direction > 0 && k.introntype == GTAG_FWD) || (c.cdna_direction < 0 && k.introntype == GTAG_REV))) {
+      put_back(k);  // already canonical
+      end_gap(k, false);
+      return false;
+    }
+  }
+  k.queryjump = k.querydp3 - k.querydp5 + 1;
+  k.genomejump = k.genomedp3 - k.genomedp5 + 1;
+  if (k.genomejump <= k.queryjump + MININTRONLEN) {  // really a single gap
+    req_single(k);
+    k.stage = S_GG_SINGLE;
+    return true;
+  }
+  k.genomejump = k.queryjump + c.extramaterial_paired;  // square matrices
+  req_genome(k, false, 0);
+  k.stage = S_GG_SCORE;
+  return true;
+}
+
+void genome_account(Path& k) {
+  if (k.introntype == NONINTRON) {
+    k.nnonintrons += 1;
+    k.nonintronlen += k.new_right - k.new_left - 1;
+  } else {
+    k.nintrons += 1;
+    k.intronlen += k.new_right - k.new_left - 1;
+  }
+}
+
+// after the score call and the optional probability re-run (:5858-5964)
+void genome_decide(Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  const int acceptable = c.defect_rate < DEFECT_HIGHQ ? 2 : (c.defect_rate < DEFECT_MEDQ ? 2 : 3);
+  if (k.gappairs < 0) {
+    for (int p = k.peeled_pairs; p >= 0; p = k.A.rest(p)) k.A.first(p).flags |= GSNAPDP_S3_DISALLOWED;
+    for (int p = k.peeled_path; p >= 0; p = k.A.rest(p)) k.A.first(p).flags |= GSNAPDP_S3_DISALLOWED;
+    put_back(k);
+    k.introntype = NONINTRON;
+    genome_account(k);
+    return end_gap(k, false);
+  }
+  if (!c.finalp && k.finalscore < 0) {
+    put_back(k);
+    k.introntype = NONINTRON;
+    genome_account(k);
+    return end_gap(k, false);
+  }
+  if (k.introntype != NONINTRON && k.nmismatches <= acceptable && k.nopens <= 1 && k.nindels <= 3) {
+    k.pairs = k.A.transfer(k.pairs, k.gappairs);
+    genome_account(k);
+    return end_gap(k, true);
+  }
+  if (c.cdna_direction == 0) return fail(k, "cdna_direction is 0 in Dynprog_microexon_int");  // :7203
+  if (k.genomedp3 - k.genomedp5 <= 0) return fail(k, "Dynprog_microexon_int: span <= 0");      // :7222
+  req_micro(k);
+  k.stage = S_GG_MICRO;
+}
+
+void genome_done(Pass& P, Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  int list = -1;
+  if (k.stage == S_GG_SINGLE) {
+    if (!done_single(P, k, &list)) return;
+    k.pairs = k.A.transfer(k.pairs, list);
+    return end_gap(k, true);
+  }
+  if (k.stage == S_GG_SCORE) {
+    if (!done_genome(P, k, &k.finalscore, &k.nmismatches, &k.left_prob, &k.right_prob, &list)) return;
+    k.gappairs = list;
+    if (list >= 0 && (k.new_left != k.A.at(k.left).genomepos || k.new_right != k.A.at(k.right).genomepos))
+      k.shiftp = true;
+    if (c.finalp && c.novelsplicingp && (k.left_prob < 0.90 || k.right_prob < 0.90)) {
+      req_genome(k, true, k.finalscore + QOPEN + 3 * QINDEL);
+      k.stage = S_GG_PROB;
+      return;
+    }
+    return genome_decide(k);
+  }
+  if (k.stage == S_GG_PROB) {
+    int finalscore_alt = 0, nmismatches_alt = 0;
+    double lp = 0.0, rp = 0.0;
+    if (!done_genome(P, k, &finalscore_alt, &nmismatches_alt, &lp, &rp, &list)) return;
+    if (list >= 0 && lp > k.left_prob && rp > k.right_prob) k.gappairs = list;
+    return genome_decide(k);
+  }
+  // S_GG_MICRO
+  double prob2 = 0.0, prob3 = 0.0;
+  int microintrontype = 0;
+  if (!done_micro(P, k, &prob2, &prob3, &microintrontype, &list)) return;
+  bool take = false;
+  if (list >= 0) {
+    if (k.nindels == 0 && k.nmismatches < 4) take = prob2 >= 0.95 && prob3 >= 0.95;  // a higher standard
+    else take = prob2 >= 0.90 || prob3 >= 0.90;
+  }
+  if (take) {
+    k.pairs = k.A.transfer(k.pairs, list);
+    k.introntype = microintrontype;
+    k.shiftp = true;
+  } else {
+    k.pairs = k.A.transfer(k.pairs, k.gappairs);
+  }
+  genome_account(k);
+  end_gap(k, true);
+}
+
+// build_pairs_introns' loop (:7763-7898) until the path waits or ends
+void scan(Pass& P, Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  const int minintronlen = c.finalp ? MININTRONLEN_FINAL : MININTRONLEN;
+  while (!k.failed && k.stage == S_SCAN) {
+    if (k.path < 0) {
+      k.stage = S_DONE;
+      return;
+    }
+    int pair = -1;
+    const int ptr = k.path;
+    k.path = k.A.pop(k.path, &pair);
+    const gsnapdp_s3_pair& g = k.A.at(pair);
+    int kind;  // 0 keep it, 1 cDNA gap, 2 genome gap, 3 single gap
+    if (!gapp(g)) kind = 0;
+    else if (g.queryjump > c.nullgap) kind = 0;  // a large gap
+    else if (g.queryjump > g.genomejump + EXTRAQUERYGAP) kind = 1;
+    else if (g.genomejump > g.queryjump + minintronlen) kind = 2;
+    else if (g.genomejump > g.queryjump + SINGLESLEN) kind = 0;  // a short intron
+    else kind = 3;
+    if (kind == 0) {
+      k.pairs = k.A.push_existing(k.pairs, ptr);
+      continue;
+    }
+    if (k.path < 0 || k.pairs < 0) return fail(k, "gap at the end of the path (the reference dereferences NULL)");
+    k.gapcell = ptr;
+    k.left = k.A.cp[(size_t)k.path];    // leftpair = path->first
+    k.right = k.A.cp[(size_t)k.pairs];  // rightpair = pairs->first
+    k.peeled_pairs = k.peeled_path = -1;
+    const bool waits = kind == 1 ? cdna_start(k) : (kind == 2 ? genome_start(P, k) : single_start(k));
+    if (waits) return;
+  }
+}
+
+void resume(Pass& P, Path& k) {
+  switch (k.stage) {
+    case S_SINGLE: single_done(P, k); break;
+    case S_CDNA_SINGLE:
+    case S_CDNA: cdna_done(P, k); break;
+    case S_GG_SINGLE:
+    case S_GG_SCORE:
+    case S_GG_PROB:
+    case S_GG_MICRO: genome_done(P, k); break;
+    default: break;
+  }
+  if (k.stage == S_SCAN) scan(P, k);
+}
+
+// ---- one round: every waiting path's window, one batch per family
+template <class T>
+std::vector<char> pack_query(const std::vector<Path*>& b, std::vector<size_t>* qo, std::vector<char>* QU,
+                             std::vector<int64_t>* off) {
+  std::vector<char> Q;
+  qo->resize(b.size());
+  off->assign(b.size() + 1, 0);
+  for (size_t i = 0; i < b.size(); i++) {
+    (*qo)[i] = Q.size();
+    Q.insert(Q.end(), b[i]->req.q.begin(), b[i]->req.q.end());
+    QU->insert(QU->end(), b[i]->req.qu.begin(), b[i]->req.qu.end());
+    (*off)[i + 1] = (*off)[i] + b[i]->req.cap;
+  }
+  Q.resize(Q.size() + 8, 0);
+  QU->resize(QU->size() + 8, 0);
+  return Q;
+}
+
+int run_round(Pass& P, std::vector<Path*> fam[F_N]) {
+  for (int f = 0; f < F_N; f++) {
+    std::vector<Path*>& b = fam[f];
+    if (b.empty()) continue;
+    const int n = (int)b.size();
+    std::vector<size_t> qo;
+    std::vector<char> QU;
+    std::vector<int64_t> off;
+    std::vector<char> Q = pack_query<char>(b, &qo, &QU, &off);
+    std::vector<uint32_t> ops((size_t)off[(size_t)n] + 1);
+    int rc = 0;
+    if (f == F_GAP) {
+      std::vector<gsnapdp_window> W((size_t)n);
+      std::vector<gsnapdp_result> R((size_t)n);
+      for (int i = 0; i < n; i++) {
+        W[(size_t)i] = b[(size_t)i]->req.w;
+        W[(size_t)i].qpos += (uint32_t)qo[(size_t)i];
+      }
+      rc = gsnapdp_run_host(P.ctx, W.data(), n, Q.data(), QU.data(), Q.size(), R.data(), ops.data(), off.data());
+      for (int i = 0; i < n; i++) b[(size_t)i]->req.r = R[(size_t)i];
+    } else if (f == F_GGAP) {
+      std::vector<gsnapdp_ggap_window> W((size_t)n);
+      std::vector<gsnapdp_ggap_result> R((size_t)n);
+      std::vector<gsnapdp_ggap_trace> T((size_t)n);
+      for (int i = 0; i < n; i++) {
+        W[(size_t)i] = b[(size_t)i]->req.gw;
+        W[(size_t)i].qpos += (uint32_t)qo[(size_t)i];
+      }
+      rc = gsnapdp_ggap_run_host(P.ctx, W.data(), n, Q.data(), QU.data(), Q.size(), R.data(), T.data(), ops.data(),
+                                 off.data());
+      for (int i = 0; i < n; i++) {
+        b[(size_t)i]->req.gr = R[(size_t)i];
+        b[(size_t)i]->req.gt = T[(size_t)i];
+      }
+    } else if (f == F_CGAP) {
+      std::vector<gsnapdp_cgap_window> W((size_t)n);
+      std::vector<gsnapdp_cgap_result> R((size_t)n);
+      for (int i = 0; i < n; i++) {
+        W[(size_t)i] = b[(size_t)i]->req.cw;
+        W[(size_t)i].qposL += (uint32_t)qo[(size_t)i];
+        W[(size_t)i].qposR += (uint32_t)qo[(size_t)i];
+      }
+      rc = gsnapdp_cgap_run_host(P.ctx, W.data(), n, Q.data(), QU.data(), Q.size(), R.data(), ops.data(), off.data());
+      for (int i = 0; i < n; i++) b[(size_t)i]->req.cr = R[(size_t)i];
+    } else {
+      std::vector<gsnapdp_micro_window> W((size_t)n);
+      std::vector<gsnapdp_micro_result> R((size_t)n);
+      for (int i = 0; i < n; i++) {
+        W[(size_t)i] = b[(size_t)i]->req.mw;
+        W[(size_t)i].qpos += (uint32_t)qo[(size_t)i];
+        W[(size_t)i].ppos += (uint32_t)qo[(size_t)i];
+      }
+      rc = gsnapdp_micro_run_host(P.ctx, W.data(), n, Q.data(), QU.data(), Q.size(), R.data());
+      for (int i = 0; i < n; i++) b[(size_t)i]->req.mr = R[(size_t)i];
+    }
+    if (rc) return -1;
+    for (int i = 0; i < n; i++) {
+      Req& R = b[(size_t)i]->req;
+      R.ops.assign(ops.begin() + off[(size_t)i], ops.begin() + off[(size_t)i + 1]);
+    }
+    P.st.windows[f] += n;
+    P.st.batches[f]++;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls,
+                                   const gsnapdp_s3_pair* pairs_in, const char* query, const char* query_uc,
+                                   gsnapdp_s3_pair* pairs_out, int64_t out_cap, gsnapdp_s3_stats* stats) {
+  if (!ctx || (ncalls > 0 && (!calls || !pairs_in || !query || !query_uc || !pairs_out)) || ncalls < 0) {
+    gsnapdp__set_err("gsnapdp_stage3_pass: bad arguments");
+    return -1;
+  }
+  Pass P;
+  P.ctx = ctx;
+  P.blocks = gsnapdp__host_blocks(ctx);
+  P.nwords = gsnapdp__host_nwords(ctx);
+  memset(&P.st, 0, sizeof(P.st));
+  std::vector<Path> paths((size_t)ncalls);
+  for (int i = 0; i < ncalls; i++) {
+    Path& k = paths[(size_t)i];
+    gsnapdp_s3_call& c = calls[i];
+    k.c = &c;
+    k.q = query + c.qpos;
+    k.qu = query_uc + c.qpos;
+    k.minor = c.in_minor;
+    k.major = c.in_major;
+    k.nintrons = c.in_nintrons;
+    k.nnonintrons = c.in_nnonintrons;
+    k.intronlen = c.in_intronlen;
+    k.nonintronlen = c.in_nonintronlen;
+    // the input list: path->first is pairs_in[first_pair]
+    k.A.pr.assign(pairs_in + c.first_pair, pairs_in + c.first_pair + c.npairs);
+    k.A.pr.reserve((size_t)c.npairs * 2 + 64);
+    for (int j = 0; j < c.npairs; j++) k.A.pr[(size_t)j].src = j;
+    for (int j = c.npairs - 1; j >= 0; j--) k.path = k.A.cell(j, k.path);
+    if (c.use_genomicseg_p) fail(k, "use_genomicseg_p passes are not served (the genome is the context's)");
+    else scan(P, k);
+  }
+  for (;;) {
+    std::vector<Path*> fam[F_N];
+    int waiting = 0;
+    for (Path& k : paths)
+      if (!k.failed && k.stage != S_DONE && k.req.fam != F_NONE) {
+        fam[k.req.fam].push_back(&k);
+        waiting++;
+      }
+    if (!waiting) break;
+    if (run_round(P, fam)) return -1;
+    P.st.rounds++;
+    for (int f = 0; f < F_N; f++)
+      for (Path* k : fam[f]) {
+        k->req.fam = F_NONE;
+        resume(P, *k);
+      }
+  }
+  int64_t at = 0;
+  for (int i = 0; i < ncalls; i++) {
+    Path& k = paths[(size_t)i];
+    gsnapdp_s3_call& c = calls[i];
+    c.status = k.failed ? -1 : 0;
+    c.first_out = (int32_t)at;
+    c.nout = 0;
+    if (k.failed) {
+      P.st.failed++;
+      continue;
+    }
+    for (int p = k.pairs; p >= 0; p = k.A.rest(p)) {
+      if (at >= out_cap) {
+        gsnapdp__set_err("gsnapdp_stage3_pass: pairs_out is too small");
+        return -1;
+      }
+      pairs_out[at++] = k.A.first(p);
+      c.nout++;
+    }
+    c.out_minor = k.minor;
+    c.out_major = k.major;
+    c.out_nintrons = k.nintrons;
+    c.out_nnonintrons = k.nnonintrons;
+    c.out_intronlen = k.intronlen;
+    c.out_nonintronlen = k.nonintronlen;
+    c.shiftp = k.shiftp ? 1 : 0;
+    c.incompletep = k.incompletep ? 1 : 0;
+  }
+  if (stats) *stats = P.st;
+  return 0;
+}

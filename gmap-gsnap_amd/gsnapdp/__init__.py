@@ -20,7 +20,7 @@ import numpy as np
 
 from .records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW,  # noqa: F401
                       INTRON, INTRON_PATH, INTRON_SCORES, MAXENT_IN, MICRO_RESULT, MICRO_WINDOW, PAIR,
-                      PATH_PAIR, RESULT, SJ_WINDOW, WINDOW)
+                      PATH_PAIR, RESULT, S3_CALL, S3_PAIR, S3_STATS, SJ_WINDOW, WINDOW)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
@@ -106,6 +106,8 @@ def lib():
         L.gsnapdp_score_introns_host.restype = i32
         L.gsnapdp_score_introns_device.argtypes = [vp, vp, i32, vp, vp, vp]
         L.gsnapdp_score_introns_device.restype = i32
+        L.gsnapdp_stage3_pass.argtypes = [vp, vp, i32, vp, vp, vp, vp, ctypes.c_int64, vp]
+        L.gsnapdp_stage3_pass.restype = i32
         _lib = L
     return _lib
 
@@ -457,6 +459,24 @@ class Context:
         if rc != 0:
             raise GsnapdpError("gsnapdp_score_introns_host: %s" % lib().gsnapdp_last_error().decode())
         return out
+
+    def stage3_pass(self, calls: np.ndarray, pairs_in: np.ndarray, query: np.ndarray, query_uc: np.ndarray):
+        """build_pairs_introns (stage3.c:7735-7901) over every call's path at once
+        (gsnapdp_stage3_pass).  Returns (calls with the out fields written, the
+        returned lists concatenated, S3_STATS)."""
+        c = np.array(calls, dtype=S3_CALL, copy=True)
+        pi = np.ascontiguousarray(pairs_in, dtype=S3_PAIR)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        cap = int((2 * (c["querylength"].astype(np.int64) + c["npairs"]) + 64).sum()) if len(c) else 1
+        out = np.zeros(max(cap, 1), dtype=S3_PAIR)
+        st = np.zeros(1, dtype=S3_STATS)
+        rc = lib().gsnapdp_stage3_pass(self.h, _p(c), len(c), _p(pi) if pi.size else _p(out), _p(q), _p(qu),
+                                       _p(out), cap, _p(st))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_stage3_pass: %s" % lib().gsnapdp_last_error().decode())
+        n = int(c["nout"].sum())
+        return c, out[:n], st[0]
 
     def maxent(self, model: np.ndarray, pos: np.ndarray, chroffset: np.ndarray) -> np.ndarray:
         m = np.ascontiguousarray(model, dtype=np.uint8)

@@ -123,3 +123,25 @@ assert INTRON_PATH.itemsize == 32
 INTRON_SCORES = np.dtype([("avg_donor_score", "<f8"), ("avg_acceptor_score", "<f8"),
                           ("nbadintrons", "<i4"), ("nintrons", "<i4")])
 assert INTRON_SCORES.itemsize == 24
+
+# the stage-3 intron pass (include/gsnapdp.h: gsnapdp_s3_pair, _s3_call, _s3_stats)
+S3_PAIR = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("queryjump", "<i4"), ("genomejump", "<i4"),
+                    ("dynprogindex", "<i4"), ("src", "<i4"), ("cdna", "u1"), ("comp", "u1"), ("genome", "u1"),
+                    ("flags", "u1")])
+assert S3_PAIR.itemsize == 28
+S3_GAPP, S3_KNOWNGAPP, S3_DISALLOWED = 1, 2, 4
+S3_CALL = np.dtype([(n, "<i4") for n in "first_pair npairs first_out nout qpos querylength".split()] +
+                   [(n, "<u4") for n in "chroffset chrhigh chrpos".split()] +
+                   [(n, "<i4") for n in ("chrnum genomiclength cdna_direction watsonp jump_late_p finalp "
+                                         "use_genomicseg_p maxpeelback nullgap extramaterial_paired "
+                                         "extraband_single extraband_paired close_indels_mode").split()] +
+                   [("defect_rate", "<f8"), ("maxlength1", "<i4", 3), ("maxlength2", "<i4", 3)] +
+                   [(n, "<i4") for n in ("in_minor in_major in_nintrons in_nnonintrons in_intronlen in_nonintronlen "
+                                         "out_minor out_major out_nintrons out_nnonintrons out_intronlen "
+                                         "out_nonintronlen shiftp incompletep novelsplicingp splicingp "
+                                         "status pad").split()] +
+                   [("ref_seconds", "<f8")])
+assert S3_CALL.itemsize == 200
+S3_STATS = np.dtype([("rounds", "<i4"), ("windows", "<i4", 4), ("batches", "<i4", 4), ("undefined", "<i4"),
+                     ("failed", "<i4")])
+assert S3_STATS.itemsize == 44

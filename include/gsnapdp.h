@@ -494,6 +494,74 @@ int gsnapdp_micro_expand(gsnapdp_ctx *ctx, const gsnapdp_micro_window *w,
                          const gsnapdp_micro_result *res, const char *query, const char *query_uc,
                          gsnapdp_pair *pairs, int cap);
 
+/* -------------------------------------------------- stage-3 intron pass
+ * build_pairs_introns (stage3.c:7735-7901) for many paths at once.  Each
+ * path's gaps are taken in list order, as the reference's loop takes them:
+ * classified (past nullgap, cDNA gap, genome gap, short intron, single gap),
+ * peeled (peel_leftward / peel_rightward, :4887-5378), filled by the gap
+ * families above -- traverse_single_gap (:5381) with its accept test,
+ * traverse_cdna_gap (:5518), traverse_genome_gap (:5633) with the SHORTCUT
+ * canonical-intron skip, the probability-mode re-run of a final pass (:5828)
+ * and the microexon fallback (:5915) -- and then kept, or put back.  All paths
+ * advance together: every round gathers the one pending DP window of each
+ * path and runs one batch per gap family (gsnapdp_*_run_host), so a pass over
+ * P paths with at most G sequential DP calls per path costs G rounds.
+ *
+ * A path is the reference's List_T of Pair_T in list order (path->first first,
+ * i.e. the alignment reversed, as insert_gapholders leaves it); each pair
+ * carries the fields the pass reads or writes.  The returned list is written
+ * in list order; `src` names the input pair (index within its path) that a
+ * returned cell holds, -1 for a pair the pass made.  Without a splicing IIT
+ * (known_mode NONE).  Genome characters come from the context genome.  Needs
+ * the MaxEnt tables when a call has finalp (probability re-runs, microexons). */
+typedef struct gsnapdp_s3_pair {
+  int32_t querypos, genomepos, queryjump, genomejump, dynprogindex;
+  int32_t src;
+  char cdna, comp, genome;
+  uint8_t flags;  /* GSNAPDP_S3_GAPP | GSNAPDP_S3_KNOWNGAPP | GSNAPDP_S3_DISALLOWED */
+} gsnapdp_s3_pair;
+enum { GSNAPDP_S3_GAPP = 1, GSNAPDP_S3_KNOWNGAPP = 2, GSNAPDP_S3_DISALLOWED = 4 };
+
+/* One build_pairs_introns call: its arguments (the query bytes at query[qpos],
+ * querylength of them; the three Dynprog_T workspaces' limits, L, M, R), its
+ * in/out counters, and (written by the pass) the returned list's extent in
+ * pairs_out, shiftp / incompletep and a status (0, or -1 when the reference
+ * would abort on the path: a window outside its domain). */
+typedef struct gsnapdp_s3_call {
+  int32_t first_pair, npairs;  /* the path in pairs_in */
+  int32_t first_out, nout;     /* written: the returned list in pairs_out */
+  int32_t qpos, querylength;
+  uint32_t chroffset, chrhigh, chrpos;
+  int32_t chrnum, genomiclength, cdna_direction;
+  int32_t watsonp, jump_late_p, finalp, use_genomicseg_p;
+  int32_t maxpeelback, nullgap, extramaterial_paired, extraband_single, extraband_paired, close_indels_mode;
+  double defect_rate;
+  int32_t maxlength1[3], maxlength2[3];  /* dynprogL, dynprogM, dynprogR */
+  int32_t in_minor, in_major, in_nintrons, in_nnonintrons, in_intronlen, in_nonintronlen;
+  int32_t out_minor, out_major, out_nintrons, out_nnonintrons, out_intronlen, out_nonintronlen;
+  int32_t shiftp, incompletep;
+  int32_t novelsplicingp, splicingp;  /* Stage3_setup's module flags (stage3.c:238-239) */
+  int32_t status, pad;                /* written: 0, or -1 (the path is left out, nout = 0) */
+  double ref_seconds;                 /* golden records: the reference's own call time (ignored) */
+} gsnapdp_s3_call;
+
+typedef struct gsnapdp_s3_stats {
+  int32_t rounds;
+  int32_t windows[4];   /* single gap, genome gap (score and probability), cDNA gap, microexon */
+  int32_t batches[4];
+  int32_t undefined;    /* probability re-runs with no qualifying candidate: the reference reads
+                         * uninitialised indices (dynprog.c:4055); taken as NULL here */
+  int32_t failed;       /* paths with status -1 */
+} gsnapdp_s3_stats;
+
+/* Runs the pass; pairs_out holds out_cap pairs (2 * (querylength + npairs) +
+ * 64 per call always suffices).  Returns 0, or -1 (gsnapdp_last_error) when a
+ * batch fails or pairs_out is too small; a path the reference would abort on
+ * gets status -1 and nout = 0, and the others still run. */
+int gsnapdp_stage3_pass(gsnapdp_ctx *ctx, gsnapdp_s3_call *calls, int ncalls,
+                        const gsnapdp_s3_pair *pairs_in, const char *query, const char *query_uc,
+                        gsnapdp_s3_pair *pairs_out, int64_t out_cap, gsnapdp_s3_stats *stats);
+
 /* Load the MaxEnt parameter tables (12 x 16384 + 4 x 16 doubles, order in
  * DESIGN.md) into the context.  Must be called before gsnapdp_maxent_*. */
 int gsnapdp_load_maxent_tables(gsnapdp_ctx *ctx, const double *tables, size_t ndoubles);

@@ -554,7 +554,7 @@ def gmap_trace_case(seed: int = 7) -> None:
     with tempfile.TemporaryDirectory() as d:
         W.write_fasta(os.path.join(d, "g.fa"), [("synthchr", g)])
         W.write_fasta(os.path.join(d, "q.fa"), q)
-        trace_gmap_run("gmap_synth", os.path.join(d, "g.fa"), os.path.join(d, "q.fa"), d)
+        trace_gmap_run("gmap_synth", os.path.join(d, "g.fa"), os.path.join(d, "q.fa"), d, stage3_every=4)
 
 
 def gmap_her2_case() -> None:
@@ -568,7 +568,49 @@ def gmap_her2_case() -> None:
             assert out == f.read(), "gmap_trace output differs from align.test.ok"
 
 
-def trace_gmap_run(prefix: str, genome_fa: str, query_fa: str, d: str) -> bytes:
+def stage3_golden(prefix: str, t: str, blocks: np.ndarray, every: int) -> None:
+    """Every `every`-th build_pairs_introns call gmap made (stage3.c:7735-7901):
+    its arguments, the path it was given and the list it returned, stored
+    compactly: a returned cell that is an input pair keeps only the input's
+    index (src) and its flags (disallowedp is the one field the pass may change
+    on an input pair, stage3.c:5873-5880); the pairs the call made are stored in
+    full (out_new, in list order)."""
+    sys.path.insert(0, os.path.join(HERE, "..", "gmap-gsnap_amd"))
+    from gsnapdp.records import S3_CALL, S3_PAIR
+    c = np.fromfile(os.path.join(t, "calls.bin"), dtype=S3_CALL)
+    pi = np.fromfile(os.path.join(t, "pairs_in.bin"), dtype=S3_PAIR)
+    po = np.fromfile(os.path.join(t, "pairs_out.bin"), dtype=S3_PAIR)
+    q = np.fromfile(os.path.join(t, "query.bin"), dtype=np.uint8)
+    qu = np.fromfile(os.path.join(t, "query_uc.bin"), dtype=np.uint8)
+    assert c.size > 0 and pi.size == int(c["npairs"].sum()) and po.size == int(c["nout"].sum())
+    sel = c[::every].copy()
+    PI, PO, Q, QU = [], [], [], []
+    a = b = e = 0
+    for i, x in enumerate(c[::every]):
+        inp = pi[x["first_pair"]:x["first_pair"] + x["npairs"]]
+        out = po[x["first_out"]:x["first_out"] + x["nout"]]
+        kept = out[out["src"] >= 0]
+        ref = inp[kept["src"]].copy()
+        ref["src"], ref["flags"] = kept["src"], kept["flags"]
+        assert ref.tobytes() == kept.tobytes(), "an input pair changed beyond its flags"
+        n = int(x["querylength"]) + 8 - (int(x["querylength"]) & 3)
+        PI.append(inp)
+        PO.append(out)
+        Q.append(q[x["qpos"]:x["qpos"] + n])
+        QU.append(qu[x["qpos"]:x["qpos"] + n])
+        sel[i]["first_pair"], sel[i]["first_out"], sel[i]["qpos"] = a, b, e
+        a, b, e = a + int(x["npairs"]), b + int(x["nout"]), e + n
+    PO = np.concatenate(PO)
+    np.savez_compressed(os.path.join(OUT, prefix + "_stage3.npz"), blocks=blocks, calls=sel,
+                        pairs_in=np.concatenate(PI), out_src=PO["src"], out_flags=PO["flags"],
+                        out_new=PO[PO["src"] < 0], query=np.concatenate(Q), query_uc=np.concatenate(QU),
+                        every=np.int32(every), ncalls_traced=np.int32(c.size))
+    print("%s_stage3: %d of %d build_pairs_introns calls (%d final), %d path pairs, %d new pairs, "
+          "reference %.3f s" % (prefix, sel.size, c.size, int(sel["finalp"].sum()), a, int((PO["src"] < 0).sum()),
+                                float(sel["ref_seconds"].sum())))
+
+
+def trace_gmap_run(prefix: str, genome_fa: str, query_fa: str, d: str, stage3_every: int = 1) -> bytes:
     """Run gmap_trace on (genome, queries), replay every recorded window through
     ref_driver, check it against what gmap got, write PREFIX_gap / PREFIX_ggap."""
     sys.path.insert(0, HERE)
@@ -630,6 +672,7 @@ def trace_gmap_run(prefix: str, genome_fa: str, query_fa: str, d: str) -> bytes:
     np.savez_compressed(os.path.join(OUT, prefix + "_introns.npz"), blocks=blocks, calls=calls, pairs=spairs)
     print("%s_introns: %d score_introns calls, %d pairs, %d bad-intron flags" %
           (prefix, calls.size, spairs.size, int((calls["nbadintrons"] > 0).sum())))
+    stage3_golden(prefix, os.path.join(d, "trace", "bpi"), blocks, stage3_every)
     return out
 
 

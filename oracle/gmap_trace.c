@@ -14,11 +14,14 @@
  *   $GMAP_TRACE_DIR/dp/{windows.bin,query.bin,query_uc.bin,genome.u32,gmap_results.bin}
  *   $GMAP_TRACE_DIR/ggap/{ggap_windows.bin,query.bin,query_uc.bin,genome.u32,gmap_results.bin}
  *   $GMAP_TRACE_DIR/si/{paths.bin,pairs.bin}: every score_introns call (stage3.c:7935),
- *     the path it was given (pair by pair, in list order) and its three outputs.
- * score_introns is static, so it cannot be wrapped at link time: stage3_si.c
- * hands its address over and the hook below is patched over its entry at start
- * (x86-64 movabs/jmp); the hook restores the entry, runs the reference's
- * function, records and re-patches (gmap is single-threaded here).
+ *     the path it was given (pair by pair, in list order) and its three outputs;
+ *   $GMAP_TRACE_DIR/bpi/{calls,pairs_in,pairs_out,query,query_uc}.bin: every
+ *     build_pairs_introns call (stage3.c:7735), one stage-3 intron pass over one path.
+ * score_introns and build_pairs_introns are static, so they cannot be wrapped
+ * at link time: stage3_si.c hands their addresses over and a hook is patched
+ * over each entry at start (x86-64 movabs/jmp); the hook restores the entry,
+ * runs the reference's function, records and re-patches (gmap is
+ * single-threaded here).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -26,6 +29,7 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "bool.h"
@@ -115,12 +119,34 @@ static void base_window(gsnapdp_window *w, int kind, Dynprog_T dynprog, int dpi,
 }
 
 
+/* the 12-byte entry patch of a static reference function: movabs rax, hook; jmp rax */
+typedef struct {
+  unsigned char saved[12], patch[12];
+  unsigned char *entry;
+} Patch;
+static void patch_install(Patch *p, void *fn, void *hook) {
+  const long pg = sysconf(_SC_PAGESIZE);
+  const uint64_t target = (uint64_t)hook;
+  uintptr_t lo;
+  p->entry = (unsigned char *)fn;
+  lo = (uintptr_t)p->entry & ~(uintptr_t)(pg - 1);
+  if (mprotect((void *)lo, (size_t)(2 * pg), PROT_READ | PROT_WRITE | PROT_EXEC) != 0) abort();
+  memcpy(p->saved, p->entry, sizeof(p->saved));
+  p->patch[0] = 0x48; /* movabs rax, imm64 */
+  p->patch[1] = 0xB8;
+  memcpy(p->patch + 2, &target, 8);
+  p->patch[10] = 0xFF; /* jmp rax */
+  p->patch[11] = 0xE0;
+  memcpy(p->entry, p->patch, sizeof(p->patch));
+}
+static void patch_off(Patch *p) { memcpy(p->entry, p->saved, sizeof(p->saved)); }
+static void patch_on(Patch *p) { memcpy(p->entry, p->patch, sizeof(p->patch)); }
+
 /* ---- score_introns (stage3.c:7935-8162), static: patched at start */
 typedef List_T (*si_fn_t)(double *, double *, int *, List_T, int, bool, int, Genomicpos_T, Genomicpos_T,
                           Genomicpos_T, char *, int, int, bool);
 extern void *gmap_trace_score_introns_fn(void);
-static unsigned char si_saved[12], si_patch[12];
-static unsigned char *si_entry;
+static Patch si_p;
 
 typedef struct { /* one call: the arguments, the outputs, the path's extent in pairs.bin */
   int32_t cdna_direction, watsonp, chrnum, genomiclength, nullgap, use_genomicseg_p;
@@ -159,11 +185,11 @@ static List_T si_hook(double *avg_donor_score, double *avg_acceptor_score, int *
     put(&si_pairs, &r, sizeof(r));
     c.npairs++;
   }
-  memcpy(si_entry, si_saved, sizeof(si_saved));
-  out = ((si_fn_t)(void *)si_entry)(avg_donor_score, avg_acceptor_score, nbadintrons, path, cdna_direction,
+  patch_off(&si_p);
+  out = ((si_fn_t)(void *)si_p.entry)(avg_donor_score, avg_acceptor_score, nbadintrons, path, cdna_direction,
                                     watsonp, chrnum, chroffset, chrhigh, chrpos, genomicuc_ptr, genomiclength,
                                     nullgap, use_genomicseg_p);
-  memcpy(si_entry, si_patch, sizeof(si_patch));
+  patch_on(&si_p);
   c.avg_donor_score = *avg_donor_score;
   c.avg_acceptor_score = *avg_acceptor_score;
   c.nbadintrons = *nbadintrons;
@@ -171,20 +197,166 @@ static List_T si_hook(double *avg_donor_score, double *avg_acceptor_score, int *
   return out;
 }
 
-__attribute__((constructor)) static void si_install(void) {
-  const long pg = sysconf(_SC_PAGESIZE);
-  const uint64_t target = (uint64_t)(void *)&si_hook;
-  uintptr_t lo;
-  si_entry = (unsigned char *)gmap_trace_score_introns_fn();
-  lo = (uintptr_t)si_entry & ~(uintptr_t)(pg - 1);
-  if (mprotect((void *)lo, (size_t)(2 * pg), PROT_READ | PROT_WRITE | PROT_EXEC) != 0) abort();
-  memcpy(si_saved, si_entry, sizeof(si_saved));
-  si_patch[0] = 0x48; /* movabs rax, imm64 */
-  si_patch[1] = 0xB8;
-  memcpy(si_patch + 2, &target, 8);
-  si_patch[10] = 0xFF; /* jmp rax */
-  si_patch[11] = 0xE0;
-  memcpy(si_entry, si_patch, sizeof(si_patch));
+/* ---- build_pairs_introns (stage3.c:7735-7901), static: patched at start.
+ * One record per call: the arguments, the path it was given (pair by pair, in
+ * list order), the list it returned (each pair with the index of the input pair
+ * it is, or -1 for a pair the call made), the in/out counters, and the wall time
+ * of the reference's own call (its DP included). */
+typedef List_T (*bpi_fn_t)(bool *, bool *, int *, int *, int *, int *, int *, int *, List_T, int, Genomicpos_T,
+                           Genomicpos_T, Genomicpos_T, void *, int, int, char *, char *, char *, char *, bool, int,
+                           bool, bool, int, int, int, int, int, double, int, Pairpool_T, Dynprog_T, Dynprog_T,
+                           Dynprog_T, bool);
+extern void *gmap_trace_build_pairs_introns_fn(void);
+extern int gmap_trace_novelsplicingp(void);
+extern int gmap_trace_splicingp(void);
+static Patch bpi_p;
+static Buf bpi_calls, bpi_in, bpi_out, bpi_q, bpi_qu;
+
+typedef struct { /* gsnapdp_s3_call (include/gsnapdp.h) */
+  int32_t first_pair, npairs, first_out, nout, qpos, querylength;
+  uint32_t chroffset, chrhigh, chrpos;
+  int32_t chrnum, genomiclength, cdna_direction;
+  int32_t watsonp, jump_late_p, finalp, use_genomicseg_p;
+  int32_t maxpeelback, nullgap, extramaterial_paired, extraband_single, extraband_paired, close_indels_mode;
+  double defect_rate;
+  int32_t maxlength1[3], maxlength2[3]; /* dynprogL, dynprogM, dynprogR */
+  int32_t in_minor, in_major, in_nintrons, in_nnonintrons, in_intronlen, in_nonintronlen;
+  int32_t out_minor, out_major, out_nintrons, out_nnonintrons, out_intronlen, out_nonintronlen;
+  int32_t shiftp, incompletep, novelsplicingp, splicingp;
+  int32_t status, pad;
+  double ref_seconds;
+} BpiCall;
+typedef struct { /* gsnapdp_s3_pair */
+  int32_t querypos, genomepos, queryjump, genomejump, dynprogindex, src;
+  char cdna, comp, genome;
+  uint8_t flags; /* 1 gapp, 2 knowngapp, 4 disallowedp */
+} BpiPair;
+
+static BpiPair bpi_pair(const struct Pair_T *x, int src) {
+  BpiPair r;
+  r.querypos = x->querypos;
+  r.genomepos = (int32_t)x->genomepos;
+  r.queryjump = x->queryjump;
+  r.genomejump = x->genomejump;
+  r.dynprogindex = x->dynprogindex;
+  r.src = src;
+  r.cdna = x->cdna;
+  r.comp = x->comp;
+  r.genome = x->genome;
+  r.flags = (uint8_t)((x->gapp ? 1 : 0) | (x->knowngapp ? 2 : 0) | (x->disallowedp ? 4 : 0));
+  return r;
+}
+typedef struct {
+  const void *p;
+  int i;
+} PtrIdx;
+static int cmp_ptr(const void *a, const void *b) {
+  const uintptr_t x = (uintptr_t)((const PtrIdx *)a)->p, y = (uintptr_t)((const PtrIdx *)b)->p;
+  return x < y ? -1 : (x > y ? 1 : 0);
+}
+
+static List_T bpi_hook(bool *shiftp, bool *incompletep, int *nintrons, int *nnonintrons, int *intronlen,
+                       int *nonintronlen, int *dynprogindex_minor, int *dynprogindex_major, List_T path, int chrnum,
+                       Genomicpos_T chroffset, Genomicpos_T chrhigh, Genomicpos_T chrpos, void *genome,
+                       int querylength, int genomiclength, char *queryseq_ptr, char *queryuc_ptr,
+                       char *genomicseg_ptr, char *genomicuc_ptr, bool use_genomicseg_p, int cdna_direction,
+                       bool watsonp, bool jump_late_p, int maxpeelback, int nullgap, int extramaterial_paired,
+                       int extraband_single, int extraband_paired, double defect_rate, int close_indels_mode,
+                       Pairpool_T pairpool, Dynprog_T dynprogL, Dynprog_T dynprogM, Dynprog_T dynprogR,
+                       bool finalp) {
+  BpiCall c;
+  List_T p, out;
+  PtrIdx *ix;
+  int n = 0, i;
+  struct timespec t0, t1;
+  static const char zero[8] = {0};
+  memset(&c, 0, sizeof(c));
+  c.first_pair = (int32_t)(bpi_in.n / sizeof(BpiPair));
+  c.qpos = (int32_t)bpi_q.n;
+  c.querylength = querylength;
+  put(&bpi_q, queryseq_ptr, (size_t)querylength);
+  put(&bpi_qu, queryuc_ptr, (size_t)querylength);
+  put(&bpi_q, zero, 8 - (size_t)(querylength & 3)); /* dword-padded, as the batch buffers */
+  put(&bpi_qu, zero, 8 - (size_t)(querylength & 3));
+  c.chroffset = chroffset;
+  c.chrhigh = chrhigh;
+  c.chrpos = chrpos;
+  c.chrnum = chrnum;
+  c.genomiclength = genomiclength;
+  c.cdna_direction = cdna_direction;
+  c.watsonp = watsonp;
+  c.jump_late_p = jump_late_p;
+  c.finalp = finalp;
+  c.use_genomicseg_p = use_genomicseg_p;
+  c.maxpeelback = maxpeelback;
+  c.nullgap = nullgap;
+  c.extramaterial_paired = extramaterial_paired;
+  c.extraband_single = extraband_single;
+  c.extraband_paired = extraband_paired;
+  c.close_indels_mode = close_indels_mode;
+  c.defect_rate = defect_rate;
+  c.maxlength1[0] = ((int *)dynprogL)[0];
+  c.maxlength2[0] = ((int *)dynprogL)[1];
+  c.maxlength1[1] = ((int *)dynprogM)[0];
+  c.maxlength2[1] = ((int *)dynprogM)[1];
+  c.maxlength1[2] = ((int *)dynprogR)[0];
+  c.maxlength2[2] = ((int *)dynprogR)[1];
+  c.in_minor = *dynprogindex_minor;
+  c.in_major = *dynprogindex_major;
+  c.in_nintrons = *nintrons;
+  c.in_nnonintrons = *nnonintrons;
+  c.in_intronlen = *intronlen;
+  c.in_nonintronlen = *nonintronlen;
+  c.novelsplicingp = gmap_trace_novelsplicingp();
+  c.splicingp = gmap_trace_splicingp();
+  for (p = path; p != NULL; p = p->rest) n++;
+  ix = (PtrIdx *)malloc((size_t)(n > 0 ? n : 1) * sizeof(PtrIdx));
+  for (p = path, i = 0; p != NULL; p = p->rest, i++) {
+    BpiPair r = bpi_pair((const struct Pair_T *)p->first, -1);
+    put(&bpi_in, &r, sizeof(r));
+    ix[i].p = p->first;
+    ix[i].i = i;
+  }
+  c.npairs = n;
+  qsort(ix, (size_t)n, sizeof(PtrIdx), cmp_ptr);
+  patch_off(&bpi_p);
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  out = ((bpi_fn_t)(void *)bpi_p.entry)(shiftp, incompletep, nintrons, nnonintrons, intronlen, nonintronlen,
+                                        dynprogindex_minor, dynprogindex_major, path, chrnum, chroffset, chrhigh,
+                                        chrpos, genome, querylength, genomiclength, queryseq_ptr, queryuc_ptr,
+                                        genomicseg_ptr, genomicuc_ptr, use_genomicseg_p, cdna_direction, watsonp,
+                                        jump_late_p, maxpeelback, nullgap, extramaterial_paired, extraband_single,
+                                        extraband_paired, defect_rate, close_indels_mode, pairpool, dynprogL,
+                                        dynprogM, dynprogR, finalp);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  patch_on(&bpi_p);
+  c.ref_seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+  c.first_out = (int32_t)(bpi_out.n / sizeof(BpiPair));
+  for (p = out; p != NULL; p = p->rest) {
+    PtrIdx key, *hit;
+    BpiPair r;
+    key.p = p->first;
+    hit = (PtrIdx *)bsearch(&key, ix, (size_t)n, sizeof(PtrIdx), cmp_ptr);
+    r = bpi_pair((const struct Pair_T *)p->first, hit ? hit->i : -1);
+    put(&bpi_out, &r, sizeof(r));
+    c.nout++;
+  }
+  free(ix);
+  c.out_minor = *dynprogindex_minor;
+  c.out_major = *dynprogindex_major;
+  c.out_nintrons = *nintrons;
+  c.out_nnonintrons = *nnonintrons;
+  c.out_intronlen = *intronlen;
+  c.out_nonintronlen = *nonintronlen;
+  c.shiftp = *shiftp;
+  c.incompletep = *incompletep;
+  put(&bpi_calls, &c, sizeof(c));
+  return out;
+}
+
+__attribute__((constructor)) static void install_hooks(void) {
+  patch_install(&si_p, gmap_trace_score_introns_fn(), (void *)&si_hook);
+  patch_install(&bpi_p, gmap_trace_build_pairs_introns_fn(), (void *)&bpi_hook);
 }
 
 extern unsigned int *__real_Genome_create_blocks(char *genomicseg, unsigned int genomelength);
@@ -375,5 +547,12 @@ __attribute__((destructor)) static void write_trace(void) {
     spit(dir, "paths.bin", si_paths.p, si_paths.n);
     spit(dir, "pairs.bin", si_pairs.p, si_pairs.n);
     spit(dir, "genome.u32", genome_blocks, genome_nwords * sizeof(unsigned int));
+    snprintf(dir, sizeof(dir), "%s/bpi", root);
+    mkdir(dir, 0755);
+    spit(dir, "calls.bin", bpi_calls.p, bpi_calls.n);
+    spit(dir, "pairs_in.bin", bpi_in.p, bpi_in.n);
+    spit(dir, "pairs_out.bin", bpi_out.p, bpi_out.n);
+    spit(dir, "query.bin", bpi_q.p, bpi_q.n);
+    spit(dir, "query_uc.bin", bpi_qu.p, bpi_qu.n);
   }
 }

@@ -3,8 +3,9 @@
  *
  * The batched C-ABI of include/gsnapdp.h served on the CPU by the oracle's
  * restatement (oracle/dp_oracle.c), for the subset the drop-in's known-site
- * ends use: end gaps (gsnapdp_run_host / gsnapdp_expand), splice-junction ends
- * (gsnapdp_sj_run_host / gsnapdp_sj_expand) and MaxEnt.  It exists so that the
+ * ends and the stage-3 intron pass use: end and single gaps (gsnapdp_run_host /
+ * gsnapdp_expand), splice-junction ends (gsnapdp_sj_*), genome gaps, cDNA gaps,
+ * microexons (expansion re-runs the window) and MaxEnt.  It exists so that the
  * drop-in's host control flow (gmap-gsnap_amd/csrc/gsnapdp_dropin.cpp) can be
  * linked, without a GPU, against the reference's own splicetrie.o / pairpool.o /
  * list.o and run under AddressSanitizer (oracle/Makefile `asan`,
@@ -12,9 +13,10 @@
  * Dynprog_end5/3_known (dynprog.c:6414-6943) with the host program's
  * Splicetrie_solve_end5/3 (splicetrie.c:881, 952).
  *
- * The op stream between run and expand is this file's own: ops[0] of a window
- * is an index into a table of pair lists that run_host filled.  Every other
- * entry point aborts.
+ * It also serves gsnapdp_stage3_pass (gmap-gsnap_amd/csrc/gsnapdp_stage3.cpp)
+ * for tests/test_stage3_cpu.py.  The op stream between run and expand is this
+ * file's own: ops[0] of a gap or splice-junction window is an index into a
+ * table of pair lists that run_host filled.
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -26,6 +28,8 @@
 
 struct gsnapdp_ctx {
   int mode;
+  const uint32_t *blocks;
+  size_t nwords;
 };
 
 typedef struct {
@@ -66,16 +70,12 @@ static int get(uint32_t id, gsnapdp_pair *out, int cap) {
   return n;
 }
 
-static void unserved(const char *f) {
-  fprintf(stderr, "oracle ABI: %s is not served on the CPU\n", f);
-  abort();
-}
-
 gsnapdp_ctx *gsnapdp_create(int device, const uint32_t *blocks, size_t nblocks_u32, int mode) {
   gsnapdp_ctx *c = (gsnapdp_ctx *)calloc(1, sizeof(gsnapdp_ctx));
   (void)device;
-  (void)nblocks_u32;
   c->mode = mode;
+  c->blocks = blocks;
+  c->nwords = nblocks_u32;
   orc_init(mode);
   orc_set_genome(blocks);
   return c;
@@ -165,43 +165,97 @@ int gsnapdp_sj_expand(gsnapdp_ctx *ctx, const gsnapdp_sj_window *w, const gsnapd
   return get(ops[0], pairs, cap);
 }
 
+/* genome gaps: the oracle's out-parameters, and the trace's status and
+ * bridge_accepted read off them (orc_genome_gap returns early for length1 <= 1
+ * or a too-long window, and leaves the intron ends unwritten, 0, when the
+ * bridge takes no candidate) */
+static void ggap_one(const gsnapdp_ggap_window *w, const char *q, const char *u, gsnapdp_ggap_result *r,
+                     gsnapdp_ggap_trace *t, gsnapdp_pair *pairs, int cap, int32_t *np) {
+  int64_t po[2] = {0, cap};
+  orc_run_ggap_batch(w, 1, q, u, r, pairs, pairs ? po : NULL, np);
+  if (t) {
+    memset(t, 0, sizeof(*t));
+    if (w->length1 <= 1 || w->maxlength1 < 0) {
+      t->status = 1;
+    } else if (r->bridge_ok) {
+      t->bridge_accepted = !(r->returned_null && r->new_leftgenomepos == 0 && r->new_rightgenomepos == 0 &&
+                             r->exonhead == 0);
+    }
+  }
+}
 int gsnapdp_ggap_run_host(gsnapdp_ctx *c, const gsnapdp_ggap_window *w, int n, const char *q,
                           const char *u, size_t b, gsnapdp_ggap_result *r, gsnapdp_ggap_trace *t,
                           uint32_t *o, const int64_t *off) {
-  (void)c, (void)w, (void)n, (void)q, (void)u, (void)b, (void)r, (void)t, (void)o, (void)off;
-  unserved("gsnapdp_ggap_run_host");
-  return -1;
+  int i;
+  (void)c, (void)b, (void)o, (void)off;
+  for (i = 0; i < n; i++) ggap_one(&w[i], q, u, &r[i], &t[i], NULL, 0, NULL);
+  return 0;
 }
+/* expansion re-runs the window (its query bytes are the caller's own) */
 int gsnapdp_ggap_expand(gsnapdp_ctx *c, const gsnapdp_ggap_window *w, const gsnapdp_ggap_result *r,
                         const gsnapdp_ggap_trace *t, const uint32_t *o, const char *q, const char *u,
                         gsnapdp_pair *p, int cap) {
-  (void)c, (void)w, (void)r, (void)t, (void)o, (void)q, (void)u, (void)p, (void)cap;
-  unserved("gsnapdp_ggap_expand");
-  return -1;
+  gsnapdp_ggap_result rr;
+  int32_t np = 0;
+  (void)c, (void)r, (void)t, (void)o;
+  ggap_one(w, q, u, &rr, NULL, p, cap, &np);
+  return np > cap ? -1 : np;
+}
+/* the reference's sequence2 of a cDNA gap: get_genomic_nt from offset2 on */
+static char *cgap_segment(const gsnapdp_cgap_window *w) {
+  int k, n = w->length2 > 0 ? w->length2 : 0;
+  char *s = (char *)calloc((size_t)n + 8, 1);
+  for (k = 0; k < n; k++)
+    s[k] = orc_get_genomic_nt(w->offset2 + k, w->chroffset, w->chrhigh, w->chrpos, (int)w->genomiclength,
+                              w->watsonp);
+  return s;
 }
 int gsnapdp_cgap_run_host(gsnapdp_ctx *c, const gsnapdp_cgap_window *w, int n, const char *q,
                           const char *u, size_t b, gsnapdp_cgap_result *r, uint32_t *o,
                           const int64_t *off) {
-  (void)c, (void)w, (void)n, (void)q, (void)u, (void)b, (void)r, (void)o, (void)off;
-  unserved("gsnapdp_cgap_run_host");
-  return -1;
+  int i;
+  int64_t zero = 0;
+  (void)c, (void)b, (void)o, (void)off;
+  for (i = 0; i < n; i++) {
+    char *s = cgap_segment(&w[i]);
+    orc_run_cgap_batch(&w[i], 1, q, u, s, &zero, &r[i], NULL, NULL, NULL);
+    free(s);
+  }
+  return 0;
 }
 int gsnapdp_cgap_expand(gsnapdp_ctx *c, const gsnapdp_cgap_window *w, const gsnapdp_cgap_result *r,
                         const uint32_t *o, const char *q, const char *u, const char *s2,
                         gsnapdp_pair *p, int cap) {
-  (void)c, (void)w, (void)r, (void)o, (void)q, (void)u, (void)s2, (void)p, (void)cap;
-  unserved("gsnapdp_cgap_expand");
-  return -1;
+  gsnapdp_cgap_result rr;
+  int64_t zero = 0, po[2] = {0, cap};
+  int32_t np = 0;
+  char *s = s2 ? NULL : cgap_segment(w);
+  (void)c, (void)r, (void)o;
+  orc_run_cgap_batch(w, 1, q, u, s2 ? s2 : s, &zero, &rr, p, po, &np);
+  free(s);
+  return np > cap ? -1 : np;
 }
 int gsnapdp_micro_run_host(gsnapdp_ctx *c, const gsnapdp_micro_window *w, int n, const char *q,
                            const char *u, size_t b, gsnapdp_micro_result *r) {
-  (void)c, (void)w, (void)n, (void)q, (void)u, (void)b, (void)r;
-  unserved("gsnapdp_micro_run_host");
-  return -1;
+  int i;
+  (void)c, (void)b;
+  for (i = 0; i < n; i++) {
+    int64_t po[2] = {0, 0};
+    int32_t np = 0;
+    orc_run_micro_batch(&w[i], 1, q, u, &r[i], NULL, po, &np);
+  }
+  return 0;
 }
 int gsnapdp_micro_expand(gsnapdp_ctx *c, const gsnapdp_micro_window *w, const gsnapdp_micro_result *r,
                          const char *q, const char *u, gsnapdp_pair *p, int cap) {
-  (void)c, (void)w, (void)r, (void)q, (void)u, (void)p, (void)cap;
-  unserved("gsnapdp_micro_expand");
-  return -1;
+  gsnapdp_micro_result rr;
+  int64_t po[2] = {0, cap};
+  int32_t np = 0;
+  (void)c, (void)r;
+  orc_run_micro_batch(w, 1, q, u, &rr, p, po, &np);
+  return np > cap ? -1 : np;
 }
+
+/* the product's internal accessors gsnapdp_stage3.cpp reads */
+const uint32_t *gsnapdp__host_blocks(gsnapdp_ctx *ctx) { return ctx->blocks; }
+size_t gsnapdp__host_nwords(gsnapdp_ctx *ctx) { return ctx->nwords; }

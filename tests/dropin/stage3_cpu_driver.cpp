@@ -1,0 +1,72 @@
+// stage3_cpu_driver.cpp -- TEST INFRASTRUCTURE ONLY (never shipped, never on a GPU box).
+//
+// Runs gsnapdp_stage3_pass (gmap-gsnap_amd/csrc/gsnapdp_stage3.cpp) on the CPU,
+// its gap families served by the oracle's restatement
+// (tests/dropin/gsnapdp_oracle_abi.c), under AddressSanitizer + UBSan
+// (oracle/Makefile `stage3_cpu`).  tests/test_stage3_cpu.py feeds it the
+// build_pairs_introns calls gmap_trace recorded and compares the lists.
+//
+//   stage3_cpu DIR    reads DIR/{calls,pairs_in,query,query_uc}.bin, DIR/genome.u32,
+//                     writes DIR/{pass_calls,pass_pairs,pass_stats}.bin
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/gsnapdp.h"
+
+static std::string g_err;
+void gsnapdp__set_err(const std::string& s) { g_err = s; }
+
+template <class T>
+static std::vector<T> slurp(const std::string& path) {
+  std::vector<T> v;
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) {
+    perror(path.c_str());
+    exit(2);
+  }
+  fseek(f, 0, SEEK_END);
+  const long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  v.resize((size_t)n / sizeof(T) + 1);
+  if (n && fread(v.data(), 1, (size_t)n, f) != (size_t)n) exit(2);
+  fclose(f);
+  v.resize((size_t)n / sizeof(T));
+  return v;
+}
+template <class T>
+static void spit(const std::string& path, const T* p, size_t n) {
+  FILE* f = fopen(path.c_str(), "wb");
+  if (!f || (n && fwrite(p, sizeof(T), n, f) != n)) exit(3);
+  fclose(f);
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) return 2;
+  const std::string d = argv[1];
+  std::vector<gsnapdp_s3_call> calls = slurp<gsnapdp_s3_call>(d + "/calls.bin");
+  std::vector<gsnapdp_s3_pair> in = slurp<gsnapdp_s3_pair>(d + "/pairs_in.bin");
+  std::vector<char> q = slurp<char>(d + "/query.bin"), qu = slurp<char>(d + "/query_uc.bin");
+  std::vector<uint32_t> blocks = slurp<uint32_t>(d + "/genome.u32");
+  std::vector<double> tables = slurp<double>(getenv("GSNAPDP_MAXENT_TABLES"));
+  gsnapdp_ctx* ctx = gsnapdp_create(0, blocks.data(), blocks.size(), 0);
+  if (!ctx || gsnapdp_load_maxent_tables(ctx, tables.data(), tables.size())) return 4;
+  int64_t cap = 0;
+  for (const gsnapdp_s3_call& c : calls) cap += 2 * ((int64_t)c.querylength + c.npairs) + 64;
+  std::vector<gsnapdp_s3_pair> out((size_t)cap);
+  gsnapdp_s3_stats st;
+  if (gsnapdp_stage3_pass(ctx, calls.data(), (int)calls.size(), in.data(), q.data(), qu.data(), out.data(), cap,
+                          &st)) {
+    fprintf(stderr, "gsnapdp_stage3_pass: %s\n", g_err.c_str());
+    return 5;
+  }
+  int64_t nout = 0;
+  for (const gsnapdp_s3_call& c : calls) nout += c.nout;
+  spit(d + "/pass_calls.bin", calls.data(), calls.size());
+  spit(d + "/pass_pairs.bin", out.data(), (size_t)nout);
+  spit(d + "/pass_stats.bin", &st, 1);
+  gsnapdp_destroy(ctx);
+  return 0;
+}

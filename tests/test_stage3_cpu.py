@@ -1,0 +1,97 @@
+"""The stage-3 intron pass (gsnapdp_stage3_pass, build_pairs_introns
+stage3.c:7735-7901 over many paths) on the CPU, against the reference.
+
+gmap_trace recorded every build_pairs_introns call the reference's gmap made
+(ss.her2 against ss.chr17test, and the synthetic spliced cDNAs): the path it was
+given, its arguments and counters, and the list it returned
+(tests/golden/gmap_*_stage3.npz, oracle/gen_golden.py stage3_golden).  Here the
+pass's host control flow (gmap-gsnap_amd/csrc/gsnapdp_stage3.cpp) runs with its
+gap families served by the oracle's restatement (tests/dropin/gsnapdp_oracle_abi.c),
+built under AddressSanitizer + UBSan (oracle/Makefile `stage3_cpu`), and must
+return the reference's lists cell for cell.  tests/test_gpu_stage3.py runs the
+same calls with the gap families on the GPU."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from gsnapdp.records import S3_CALL, S3_PAIR, S3_STATS
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NAMES = ["gmap_her2_stage3", "gmap_synth_stage3"]
+COUNTERS = ["out_minor", "out_major", "out_nintrons", "out_nnonintrons", "out_intronlen", "out_nonintronlen",
+            "shiftp", "incompletep", "nout"]
+
+
+def stage3_golden(z):
+    """(calls, pairs_in, query, query_uc, the expected returned lists concatenated)."""
+    calls = z["calls"].copy()
+    pin = z["pairs_in"]
+    src, flags, new = z["out_src"], z["out_flags"], z["out_new"]
+    out = np.zeros(src.size, dtype=S3_PAIR)
+    out[src < 0] = new
+    at = 0
+    for c in calls:
+        n = int(c["nout"])
+        s = src[at:at + n]
+        keep = np.nonzero(s >= 0)[0]
+        out[at + keep] = pin[int(c["first_pair"]) + s[keep]]
+        out["src"][at + keep] = s[keep]
+        out["flags"][at:at + n] = flags[at:at + n]
+        at += n
+    return calls, pin, z["query"], z["query_uc"], out
+
+
+def check_pass(calls, out, want_calls, want_out, what):
+    """the pass's counters and lists against the reference's, call by call"""
+    assert (calls["status"] == 0).all(), "%s: failed calls %s" % (what, np.nonzero(calls["status"])[0][:8])
+    for f in COUNTERS:
+        bad = np.nonzero(calls[f] != want_calls[f])[0]
+        assert bad.size == 0, "%s: %s differs at calls %s (got %s want %s)" % (
+            what, f, bad[:8], calls[f][bad[:8]], want_calls[f][bad[:8]])
+    for i, (c, w) in enumerate(zip(calls, want_calls)):
+        got = out[int(c["first_out"]):int(c["first_out"]) + int(c["nout"])]
+        exp = want_out[int(w["first_out"]):int(w["first_out"]) + int(w["nout"])]
+        if got.tobytes() != exp.tobytes():
+            k = int(np.nonzero(got != exp)[0][0])
+            raise AssertionError("%s: call %d, cell %d of %d: got %s want %s" % (what, i, k, len(exp), got[k], exp[k]))
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_stage3_pass_cpu_matches_reference(golden_dir, tmp_path, name):
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "stage3_cpu"])
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    calls, pin, q, qu, want = stage3_golden(z)
+    d = str(tmp_path)
+    calls.tofile(os.path.join(d, "calls.bin"))
+    pin.tofile(os.path.join(d, "pairs_in.bin"))
+    q.tofile(os.path.join(d, "query.bin"))
+    qu.tofile(os.path.join(d, "query_uc.bin"))
+    z["blocks"].astype("<u4").tofile(os.path.join(d, "genome.u32"))
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               GSNAPDP_MAXENT_TABLES=os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin"))
+    p = subprocess.run([os.path.join(ROOT, "oracle", "_build", "stage3_cpu"), d], env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert p.returncode == 0, "stage3_cpu failed (%d):\n%s" % (p.returncode, p.stderr[-6000:])
+    assert "runtime error" not in p.stderr, p.stderr[-6000:]
+    got_calls = np.fromfile(os.path.join(d, "pass_calls.bin"), dtype=S3_CALL)
+    got = np.fromfile(os.path.join(d, "pass_pairs.bin"), dtype=S3_PAIR)
+    st = np.fromfile(os.path.join(d, "pass_stats.bin"), dtype=S3_STATS)[0]
+    check_pass(got_calls, got, calls, want, name)
+    assert st["failed"] == 0 and st["undefined"] == 0
+    assert st["windows"][1] > 0 and st["windows"][3] > 0  # genome gaps and microexons were exercised
+
+
+def test_stage3_golden_covers_the_branches(golden_dir):
+    """what the recorded calls exercise: final and non-final passes, filled
+    genome gaps (new gapholders), shifted introns, both cDNA directions"""
+    z = np.load(os.path.join(golden_dir, "gmap_synth_stage3.npz"), allow_pickle=False)
+    c = z["calls"]
+    assert (c["finalp"] == 1).any() and (c["finalp"] == 0).any()
+    assert (c["shiftp"] == 1).any()
+    assert set(np.unique(c["cdna_direction"])) == {-1, 1}
+    new = z["out_new"]
+    assert ((new["flags"] & 1) == 1).any()  # gapholders made by the genome-gap fills
+    assert (c["out_nintrons"] > c["in_nintrons"]).any()
