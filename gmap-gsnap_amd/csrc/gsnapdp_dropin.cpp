@@ -626,6 +626,20 @@ struct RefPairGap {
   unsigned char gapp, knowngapp;  // bool (bool.h: unsigned char)
 };
 static_assert(offsetof(RefPairGap, gapp) == 41 && offsetof(RefPairGap, knowngapp) == 42, "Pair_T layout");
+// ... and the whole struct (pairdef.h:9-49), for build_pairs_introns' disallowedp
+struct RefPair {
+  int querypos;
+  unsigned genomepos;
+  int refquerypos, aapos, queryjump, genomejump, aaphase_g, aaphase_e, dynprogindex;
+  char cdna, comp, genome, aa_g, aa_e;
+  unsigned char gapp, knowngapp, extraexonp, shortexonp;
+  int state, vstate_good, vstate_bad;  // State_T
+  unsigned char protectedp, disallowedp;
+  double donor_prob, acceptor_prob;
+  unsigned char end_intron_p;
+};
+static_assert(offsetof(RefPair, disallowedp) == 61 && offsetof(RefPair, donor_prob) == 64 && sizeof(RefPair) == 88,
+              "Pair_T layout");
 
 // binary_search (dynprog.c:5068-5090)
 int binary_search(int lowi, int highi, const unsigned* positions, unsigned goal) {
@@ -1577,6 +1591,112 @@ gsnapdp_List_T Gsnapdp_score_introns(double* avg_donor_score, double* avg_accept
   *avg_acceptor_score = req.out.avg_acceptor_score;
   *nbadintrons = req.out.nbadintrons;
   return path ? List_reverse(path) : path;
+}
+
+// build_pairs_introns (stage3.c:7735-7901), the reference's static function with
+// its signature (non-PMAP, non-WASTE), for a stage3.c that calls it here
+// (:8766, :8865): the path goes through gsnapdp_stage3_pass (every gap filled
+// on the GPU, the peels and accept rules on the host) and comes back as the
+// reference's list: its own cells for the pairs it keeps (disallowedp set where
+// the reference sets it, :5873-5880) and the host's Pairpool for the pairs the
+// fills made.  The genome is the context's (genome / genomicseg_ptr unused).
+gsnapdp_List_T Gsnapdp_build_pairs_introns(
+    gsnapdp_bool* shiftp, gsnapdp_bool* incompletep, int* nintrons, int* nnonintrons, int* intronlen,
+    int* nonintronlen, int* dynprogindex_minor, int* dynprogindex_major, gsnapdp_List_T path, int chrnum,
+    gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genome_T /*genome*/, int querylength, int genomiclength, char* queryseq_ptr, char* queryuc_ptr,
+    char* /*genomicseg_ptr*/, char* /*genomicuc_ptr*/, gsnapdp_bool use_genomicseg_p, int cdna_direction,
+    gsnapdp_bool watsonp, gsnapdp_bool jump_late_p, int maxpeelback, int nullgap, int extramaterial_paired,
+    int extraband_single, int extraband_paired, double defect_rate, int close_indels_mode,
+    gsnapdp_Pairpool_T pairpool, gsnapdp_Dynprog_T dynprogL, gsnapdp_Dynprog_T dynprogM,
+    gsnapdp_Dynprog_T dynprogR, gsnapdp_bool finalp) {
+  if (g.splicing_iit) fatal("build_pairs_introns with a splicing IIT is not served by the batched pass");
+  if (use_genomicseg_p) fatal("build_pairs_introns on a genomic segment is not served by the batched pass");
+  gsnapdp_ctx* c = shared_ctx(true);
+  std::vector<RefList*> cells;
+  std::vector<gsnapdp_s3_pair> in;
+  for (RefList* l = (RefList*)path; l; l = l->rest) {
+    const RefPair* x = (const RefPair*)l->first;
+    gsnapdp_s3_pair p;
+    p.querypos = x->querypos;
+    p.genomepos = (int32_t)x->genomepos;
+    p.queryjump = x->queryjump;
+    p.genomejump = x->genomejump;
+    p.dynprogindex = x->dynprogindex;
+    p.src = (int32_t)cells.size();
+    p.cdna = x->cdna;
+    p.comp = x->comp;
+    p.genome = x->genome;
+    p.flags = (uint8_t)((x->gapp ? GSNAPDP_S3_GAPP : 0) | (x->knowngapp ? GSNAPDP_S3_KNOWNGAPP : 0) |
+                        (x->disallowedp ? GSNAPDP_S3_DISALLOWED : 0));
+    in.push_back(p);
+    cells.push_back(l);
+  }
+  gsnapdp_s3_call k;
+  memset(&k, 0, sizeof(k));
+  k.npairs = (int32_t)in.size();
+  k.querylength = querylength;
+  k.chroffset = chroffset;
+  k.chrhigh = chrhigh;
+  k.chrpos = chrpos;
+  k.chrnum = chrnum;
+  k.genomiclength = genomiclength;
+  k.cdna_direction = cdna_direction;
+  k.watsonp = watsonp ? 1 : 0;
+  k.jump_late_p = jump_late_p ? 1 : 0;
+  k.finalp = finalp ? 1 : 0;
+  k.maxpeelback = maxpeelback;
+  k.nullgap = nullgap;
+  k.extramaterial_paired = extramaterial_paired;
+  k.extraband_single = extraband_single;
+  k.extraband_paired = extraband_paired;
+  k.close_indels_mode = close_indels_mode;
+  k.defect_rate = defect_rate;
+  const Dynprog* dp[3] = {(const Dynprog*)dynprogL, (const Dynprog*)dynprogM, (const Dynprog*)dynprogR};
+  for (int i = 0; i < 3; i++) {
+    k.maxlength1[i] = dp[i]->maxlength1;
+    k.maxlength2[i] = dp[i]->maxlength2;
+  }
+  k.in_minor = *dynprogindex_minor;
+  k.in_major = *dynprogindex_major;
+  k.in_nintrons = *nintrons;
+  k.in_nnonintrons = *nnonintrons;
+  k.in_intronlen = *intronlen;
+  k.in_nonintronlen = *nonintronlen;
+  // Stage3_setup's flags as gmap derives them from Dynprog_setup's (gmap.c:3828-3849)
+  k.novelsplicingp = g.novelsplicingp ? 1 : 0;
+  k.splicingp = (g.novelsplicingp || g.splicing_iit) ? 1 : 0;
+  const int64_t cap = 2 * ((int64_t)querylength + k.npairs) + 64;
+  std::vector<gsnapdp_s3_pair> out((size_t)cap);
+  gsnapdp_s3_stats st;
+  if (gsnapdp_stage3_pass(c, &k, 1, in.data(), queryseq_ptr, queryuc_ptr, out.data(), cap, &st))
+    fatal(std::string("gsnapdp_stage3_pass: ") + gsnapdp_last_error());
+  if (k.status) fatal("build_pairs_introns: a window outside the reference's domain (the reference aborts)");
+  gsnapdp_List_T list = nullptr;
+  for (int i = k.nout - 1; i >= 0; i--) {
+    const gsnapdp_s3_pair& p = out[(size_t)i];
+    if (p.src >= 0) {  // the path's own cell (List_push_existing)
+      RefList* l = cells[(size_t)p.src];
+      ((RefPair*)l->first)->disallowedp = (p.flags & GSNAPDP_S3_DISALLOWED) ? 1 : 0;
+      l->rest = (RefList*)list;
+      list = (gsnapdp_List_T)l;
+    } else if (p.flags & GSNAPDP_S3_GAPP) {
+      list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump,
+                                     (p.flags & GSNAPDP_S3_KNOWNGAPP) ? 1 : 0);
+      ((RefPair*)((RefList*)list)->first)->comp = p.comp;  // a microexon's gapchar (dynprog.c:6991)
+    } else {
+      list = Pairpool_push(list, pairpool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome, p.dynprogindex);
+    }
+  }
+  *shiftp = k.shiftp ? 1 : 0;
+  *incompletep = k.incompletep ? 1 : 0;
+  *nintrons = k.out_nintrons;
+  *nnonintrons = k.out_nnonintrons;
+  *intronlen = k.out_intronlen;
+  *nonintronlen = k.out_nonintronlen;
+  *dynprogindex_minor = k.out_minor;
+  *dynprogindex_major = k.out_major;
+  return list;
 }
 
 double Maxent_hr_donor_prob(gsnapdp_Genomicpos_T splice_pos, gsnapdp_Genomicpos_T chroffset) {

@@ -233,6 +233,24 @@ gsnapdp_List_T Gsnapdp_score_introns(double* avg_donor_score, double* avg_accept
                                      gsnapdp_Genomicpos_T chrpos, char* genomicuc_ptr, int genomiclength,
                                      int nullgap, gsnapdp_bool use_genomicseg_p);
 
+/* build_pairs_introns (stage3.c:7735-7901, static there; non-PMAP, non-WASTE
+ * signature): a stage3.c that calls Gsnapdp_build_pairs_introns at its two
+ * call sites (stage3.c:8766, 8865) gets the same list, the
+ * same counters and flags, with every gap of the path filled by the GPU gap
+ * families (gsnapdp_stage3_pass over one path).  Without a splicing IIT; the
+ * genome is the context's.  A caller with many paths at hand calls
+ * gsnapdp_stage3_pass (gsnapdp.h) on all of them at once instead. */
+gsnapdp_List_T Gsnapdp_build_pairs_introns(
+    gsnapdp_bool* shiftp, gsnapdp_bool* incompletep, int* nintrons, int* nnonintrons, int* intronlen,
+    int* nonintronlen, int* dynprogindex_minor, int* dynprogindex_major, gsnapdp_List_T path, int chrnum,
+    gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genome_T genome, int querylength, int genomiclength, char* queryseq_ptr, char* queryuc_ptr,
+    char* genomicseg_ptr, char* genomicuc_ptr, gsnapdp_bool use_genomicseg_p, int cdna_direction,
+    gsnapdp_bool watsonp, gsnapdp_bool jump_late_p, int maxpeelback, int nullgap, int extramaterial_paired,
+    int extraband_single, int extraband_paired, double defect_rate, int close_indels_mode,
+    gsnapdp_Pairpool_T pairpool, gsnapdp_Dynprog_T dynprogL, gsnapdp_Dynprog_T dynprogM,
+    gsnapdp_Dynprog_T dynprogR, gsnapdp_bool finalp);
+
 /* --- optional additions (not in the reference) ---
  * The shim finds the packed genome on its own: Dynprog_setup's Genome_T
  * (Genome_blocks / Genome_totallength, genome.c:96-107) for an index genome,

@@ -185,3 +185,54 @@ List_T dbl_list_build(const PathRec* recs, int n) {
   }
   return list;
 }
+
+/* A stage-3 path (gsnapdp_s3_pair records, list order) -> a list whose head is
+ * recs[0]; refquerypos carries index + 1 so that dbl_s3_read can name the input
+ * pair a returned cell holds (0 for a pair the callee pushed). */
+typedef struct S3Rec {
+  int querypos, genomepos, queryjump, genomejump, dynprogindex, src;
+  char cdna, comp, genome;
+  unsigned char flags; /* 1 gapp, 2 knowngapp, 4 disallowedp */
+} S3Rec;
+List_T dbl_s3_build(const S3Rec* recs, int n) {
+  List_T list = NULL;
+  int i;
+  for (i = n - 1; i >= 0; i--) {
+    PairRec* r = (PairRec*)calloc(1, sizeof(PairRec));
+    r->querypos = recs[i].querypos;
+    r->genomepos = (unsigned int)recs[i].genomepos;
+    r->refquerypos = i + 1;
+    r->queryjump = recs[i].queryjump;
+    r->genomejump = recs[i].genomejump;
+    r->dynprogindex = recs[i].dynprogindex;
+    r->cdna = recs[i].cdna;
+    r->comp = recs[i].comp;
+    r->genome = recs[i].genome;
+    r->gapp = recs[i].flags & 1;
+    r->knowngapp = (recs[i].flags >> 1) & 1;
+    r->disallowedp = (recs[i].flags >> 2) & 1;
+    list = cons(list, r);
+  }
+  return list;
+}
+int dbl_s3_read(List_T list, S3Rec* out, int cap) {
+  int n = 0;
+  for (; list; list = list->rest, n++) {
+    const PairRec* p = (const PairRec*)list->first;
+    if (n < cap) {
+      S3Rec* o = &out[n];
+      memset(o, 0, sizeof(*o));
+      o->querypos = p->querypos;
+      o->genomepos = (int)p->genomepos;
+      o->queryjump = p->queryjump;
+      o->genomejump = p->genomejump;
+      o->dynprogindex = p->dynprogindex;
+      o->src = p->refquerypos - 1;
+      o->cdna = p->cdna;
+      o->comp = p->comp;
+      o->genome = p->genome;
+      o->flags = (unsigned char)((p->gapp ? 1 : 0) | (p->knowngapp ? 2 : 0) | (p->disallowedp ? 4 : 0));
+    }
+  }
+  return n;
+}
