@@ -10,9 +10,14 @@
 // on until every path has reached the end of its list.
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gsnapdp.h"
@@ -147,6 +152,7 @@ struct Path {
   int new_left = 0, new_right = 0, introntype = 0;
   double left_prob = 0.0, right_prob = 0.0;
   int gappairs = -1;
+  int undefined = 0;  // probability re-runs with no qualifying candidate
   Req req;
 };
 
@@ -608,7 +614,7 @@ bool done_genome(Pass& P, Path& k, int* finalscore, int* nmismatches, double* lp
     return true;
   }
   if (r.bridge_ok == 0) {
-    P.st.undefined++;
+    k.undefined++;
     return true;
   }
   if (!w.use_probabilities_p && r.finalscore != -100000) k.introntype = r.introntype;
@@ -968,6 +974,33 @@ void resume(Pass& P, Path& k) {
   if (k.stage == S_SCAN) scan(P, k);
 }
 
+// The paths' host work between rounds (peels, traversals, expansion) is
+// independent per path: `threads` workers take them in chunks.  The gap
+// families' expanders only read the context (genome, tables).
+template <class F>
+void for_paths(std::vector<Path*>& v, int threads, F fn) {
+  const int n = (int)v.size();
+  if (threads <= 1 || n < 64) {
+    for (Path* k : v) fn(*k);
+    return;
+  }
+  std::atomic<int> next(0);
+  auto work = [&]() {
+    for (int i; (i = next.fetch_add(16)) < n;)
+      for (int j = i; j < std::min(n, i + 16); j++) fn(*v[(size_t)j]);
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; t++) th.emplace_back(work);
+  work();
+  for (std::thread& x : th) x.join();
+}
+
+int pass_threads() {
+  if (const char* e = getenv("GSNAPDP_S3_THREADS")) return std::max(1, atoi(e));
+  const int hw = (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(16, hw));  // a GPU box's CPU share is 16 (nproc shows the whole machine)
+}
+
 // ---- one round: every waiting path's window, one batch per family
 template <class T>
 std::vector<char> pack_query(const std::vector<Path*>& b, std::vector<size_t>* qo, std::vector<char>* QU,
@@ -1066,7 +1099,12 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
   P.blocks = gsnapdp__host_blocks(ctx);
   P.nwords = gsnapdp__host_nwords(ctx);
   memset(&P.st, 0, sizeof(P.st));
+  using clock = std::chrono::steady_clock;
+  const auto t_start = clock::now();
+  double host_s = 0.0, gpu_s = 0.0;
+  const int threads = pass_threads();
   std::vector<Path> paths((size_t)ncalls);
+  std::vector<Path*> all;
   for (int i = 0; i < ncalls; i++) {
     Path& k = paths[(size_t)i];
     gsnapdp_s3_call& c = calls[i];
@@ -1079,30 +1117,39 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     k.nnonintrons = c.in_nnonintrons;
     k.intronlen = c.in_intronlen;
     k.nonintronlen = c.in_nonintronlen;
+    all.push_back(&k);
+  }
+  for_paths(all, threads, [&](Path& k) {
+    const gsnapdp_s3_call& c = *k.c;
     // the input list: path->first is pairs_in[first_pair]
-    k.A.pr.assign(pairs_in + c.first_pair, pairs_in + c.first_pair + c.npairs);
     k.A.pr.reserve((size_t)c.npairs * 2 + 64);
+    k.A.pr.assign(pairs_in + c.first_pair, pairs_in + c.first_pair + c.npairs);
     for (int j = 0; j < c.npairs; j++) k.A.pr[(size_t)j].src = j;
+    k.A.cp.reserve((size_t)c.npairs * 2 + 64);
+    k.A.cn.reserve((size_t)c.npairs * 2 + 64);
     for (int j = c.npairs - 1; j >= 0; j--) k.path = k.A.cell(j, k.path);
     if (c.use_genomicseg_p) fail(k, "use_genomicseg_p passes are not served (the genome is the context's)");
     else scan(P, k);
-  }
+  });
+  host_s += std::chrono::duration<double>(clock::now() - t_start).count();
   for (;;) {
-    std::vector<Path*> fam[F_N];
-    int waiting = 0;
+    std::vector<Path*> fam[F_N], waiting;
     for (Path& k : paths)
       if (!k.failed && k.stage != S_DONE && k.req.fam != F_NONE) {
         fam[k.req.fam].push_back(&k);
-        waiting++;
+        waiting.push_back(&k);
       }
-    if (!waiting) break;
+    if (waiting.empty()) break;
+    const auto t0 = clock::now();
     if (run_round(P, fam)) return -1;
+    const auto t1 = clock::now();
     P.st.rounds++;
-    for (int f = 0; f < F_N; f++)
-      for (Path* k : fam[f]) {
-        k->req.fam = F_NONE;
-        resume(P, *k);
-      }
+    for_paths(waiting, threads, [&](Path& k) {
+      k.req.fam = F_NONE;
+      resume(P, k);
+    });
+    gpu_s += std::chrono::duration<double>(t1 - t0).count();
+    host_s += std::chrono::duration<double>(clock::now() - t1).count();
   }
   int64_t at = 0;
   for (int i = 0; i < ncalls; i++) {
@@ -1111,6 +1158,7 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     c.status = k.failed ? -1 : 0;
     c.first_out = (int32_t)at;
     c.nout = 0;
+    P.st.undefined += k.undefined;
     if (k.failed) {
       P.st.failed++;
       continue;
@@ -1132,6 +1180,9 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     c.shiftp = k.shiftp ? 1 : 0;
     c.incompletep = k.incompletep ? 1 : 0;
   }
+  P.st.seconds[0] = host_s;
+  P.st.seconds[1] = gpu_s;
+  P.st.seconds[2] = std::chrono::duration<double>(clock::now() - t_start).count();
   if (stats) *stats = P.st;
   return 0;
 }

@@ -469,7 +469,7 @@ class Context:
         q = np.ascontiguousarray(query, dtype=np.uint8)
         qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
         cap = int((2 * (c["querylength"].astype(np.int64) + c["npairs"]) + 64).sum()) if len(c) else 1
-        out = np.zeros(max(cap, 1), dtype=S3_PAIR)
+        out = np.empty(max(cap, 1), dtype=S3_PAIR)  # only the lists written are touched
         st = np.zeros(1, dtype=S3_STATS)
         rc = lib().gsnapdp_stage3_pass(self.h, _p(c), len(c), _p(pi) if pi.size else _p(out), _p(q), _p(qu),
                                        _p(out), cap, _p(st))

@@ -143,5 +143,5 @@ S3_CALL = np.dtype([(n, "<i4") for n in "first_pair npairs first_out nout qpos q
                    [("ref_seconds", "<f8")])
 assert S3_CALL.itemsize == 200
 S3_STATS = np.dtype([("rounds", "<i4"), ("windows", "<i4", 4), ("batches", "<i4", 4), ("undefined", "<i4"),
-                     ("failed", "<i4")])
-assert S3_STATS.itemsize == 44
+                     ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3)])
+assert S3_STATS.itemsize == 72

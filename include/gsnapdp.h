@@ -552,6 +552,9 @@ typedef struct gsnapdp_s3_stats {
   int32_t undefined;    /* probability re-runs with no qualifying candidate: the reference reads
                          * uninitialised indices (dynprog.c:4055); taken as NULL here */
   int32_t failed;       /* paths with status -1 */
+  int32_t pad;
+  double seconds[3];    /* wall time: host list work (peels, traversals, expansion), batched
+                         * gap-family round trips (staging, kernels, copies), whole pass */
 } gsnapdp_s3_stats;
 
 /* Runs the pass; pairs_out holds out_cap pairs (2 * (querylength + npairs) +

@@ -55,10 +55,10 @@ def test_gpu_stage3_pass_at_scale(golden_dir):
     check_pass(got_calls, got, C, WANT, "replicated x%d" % copies)
     nwin = int(np.sum(st["windows"]))
     ref = float(calls["ref_seconds"].sum()) * copies
-    print("stage3 pass: %d paths in %.3f s (%d rounds; %d windows: %s; %d batches) = %.0f paths/s, %.0f windows/s; "
-          "reference build_pairs_introns (1 CPU thread) %.3f s = %.0f paths/s" %
-          (len(C), dt, st["rounds"], nwin, st["windows"], int(np.sum(st["batches"])), len(C) / dt, nwin / dt, ref,
-           len(C) / ref))
+    print("stage3 pass: %d paths in %.3f s (%d rounds; %d windows: %s; %d batches; host %.3f s, batches %.3f s) "
+          "= %.0f paths/s, %.0f windows/s; reference build_pairs_introns (1 CPU thread) %.3f s = %.0f paths/s" %
+          (len(C), dt, st["rounds"], nwin, st["windows"], int(np.sum(st["batches"])), st["seconds"][0],
+           st["seconds"][1], len(C) / dt, nwin / dt, ref, len(C) / ref))
     ctx.close()
 
 
