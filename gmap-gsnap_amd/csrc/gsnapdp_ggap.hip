@@ -268,7 +268,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
         clsL[c] = (uint8_t)((c >= 1 && c <= G.L2L) ? gclass(blocks, nwords, LL, w.offset2L + c - 1) : 5);
       for (int c = rho; c <= G.L2R + 1; c += RL)
         clsR[c] = (uint8_t)((c >= 1 && c <= G.L2R) ? gclass(blocks, nwords, LR, w.revoffset2R + 1 - c) : 5);
+#ifdef GG_EXP_NOPROB  // timing experiment only: no MaxEnt evaluation (wrong probabilities)
+      if (probmode) {
+        for (int c = rho; c < G.L2L; c += RL) lp[c] = 0.01 * (double)(c & 63);
+        for (int c = rho; c < G.L2R; c += RL) rp[c] = 0.01 * (double)(c & 31);
+      }
+      if (false) {
+#else
       if (probmode) {  // :3856-3903 (a known site has probability 1.0)
+#endif
         for (int c = rho; c < G.L2L; c += RL)
           lp[c] = c < G.L2L - 1 ? (kflag(krec, km, c) ? 1.0 : left_site_prob(w, c, blocks, nwords, tables)) : 0.0;
         for (int c = rho; c < G.L2R; c += RL)

@@ -360,7 +360,11 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
   // row's bits come in at bit S-1 of each byte (from the LDS lookup table).
   const uint64_t* mlut = (const uint64_t*)(sprof + MLUT);
   constexpr uint64_t MB_KEEP = 0x0101010101ull * ((1u << (S - 1)) - 1u);
+#ifdef EXP_NOMLUT  // timing experiment only: no LDS lookup (wrong match bits)
+  auto row_spread = [&](uint32_t pw) -> uint64_t { return ((uint64_t)(pw & 0x1F000000u) << 8) >> (8 - S); };
+#else
   auto row_spread = [&](uint32_t pw) -> uint64_t { return mlut[(pw >> 24) & 31u] >> (8 - S); };
+#endif
   uint64_t MB = 0;
   // column 0 (dynprog.c:1460-1488) in offset coordinates
 #pragma unroll

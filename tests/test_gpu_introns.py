@@ -97,6 +97,7 @@ def test_dropin_score_introns_matches_reference_golden(golden_dir, tmp_path):
     # one genome per process in the drop-in: the synthetic cDNA set (the larger one)
     zz = z["gmap_synth_introns"]
     blocks = np.ascontiguousarray(zz["blocks"])
+    L.Dynprog_term()  # a context an earlier test left holds another genome
     L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
     from test_dropin import REC
     calls, sp = zz["calls"], np.ascontiguousarray(zz["pairs"])
@@ -116,3 +117,4 @@ def test_dropin_score_introns_matches_reference_golden(golden_dir, tmp_path):
         k = dbl.dbl_list_read(out, back.ctypes.data, back.size)
         assert k == npairs and np.array_equal(back["querypos"][:k], recs["querypos"][::-1]), i
         dbl.dbl_list_free(out)
+    L.Dynprog_term()  # releases the device context (the genome array dies with this test)

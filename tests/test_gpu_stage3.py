@@ -93,6 +93,7 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path):
     calls, pin, q, qu, want = stage3_golden(z)
     assert (calls["maxlength1"] == 611).all() and (calls["maxlength2"] == 2000).all()
     blocks = np.ascontiguousarray(z["blocks"])
+    L.Dynprog_term()  # a context an earlier test left holds another genome
     L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
     dp = L.Dynprog_new(600, 10, 11, 10, 8)  # gmap.c's dynprogL / M / R: 611 x 2000
     qb = np.ascontiguousarray(q)
@@ -121,3 +122,4 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path):
         assert (shift.value, inc.value) == (int(c["shiftp"]), int(c["incompletep"])), i
         assert [x.value for x in ctr] == [int(c[f]) for f in ("out_nintrons", "out_nnonintrons", "out_intronlen",
                                                               "out_nonintronlen", "out_minor", "out_major")], i
+    L.Dynprog_term()  # releases the device context (the genome array dies with this test)
