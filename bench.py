@@ -336,6 +336,45 @@ def measure_micro(genome, n, steps, warmup, dev, with_cpu):
     return out
 
 
+def measure_stage3(copies=64, reps=3):
+    """Side line: the stage-3 intron pass (gsnapdp_stage3_pass, build_pairs_introns
+    over many paths) on the recorded calls of the reference's gmap
+    (tests/golden/gmap_synth_stage3.npz) replicated `copies` times into one pass;
+    every copy is checked against the reference's lists.  `reference_s` is the
+    reference's own time for the same calls (its build_pairs_introns wall time,
+    DP included, one thread; recorded by oracle/gmap_trace in the dev container,
+    not on this host)."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "gmap_synth_stage3.npz"), allow_pickle=False)
+    calls, pin, q, qu, want = W.stage3_calls(z, copies)
+    ctx = Context(z["blocks"])
+    ctx.stage3_pass(calls[:64], pin, q, qu)  # warm-up
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        c, got, st = ctx.stage3_pass(calls, pin, q, qu)
+        dt = time.perf_counter() - t0
+        if best is None or dt < best[0]:
+            best = (dt, c, got, st)
+    dt, c, got, st = best
+    ok = bool((c["status"] == 0).all()) and got.tobytes() == want.tobytes()
+    for f in ("out_minor", "out_major", "out_nintrons", "out_nnonintrons", "out_intronlen", "out_nonintronlen",
+              "shiftp", "incompletep", "nout"):
+        ok = ok and bool(np.array_equal(c[f], calls[f]))
+    nwin = int(np.sum(st["windows"]))
+    ref = float(z["calls"]["ref_seconds"].sum()) * copies
+    ctx.close()
+    return {"metric": "stage-3 intron pass (build_pairs_introns), paths/s", "value": round(len(calls) / dt, 1),
+            "unit": "paths/s", "paths": int(len(calls)), "seconds": round(dt, 4), "rounds": int(st["rounds"]),
+            "windows": nwin, "windows_per_s": round(nwin / dt, 1),
+            "windows_by_family": {"single": int(st["windows"][0]), "genome_gap": int(st["windows"][1]),
+                                  "cdna_gap": int(st["windows"][2]), "microexon": int(st["windows"][3])},
+            "host_s": round(float(st["seconds"][0]), 4), "batches_s": round(float(st["seconds"][1]), 4),
+            "bit_exact_vs_reference": ok,
+            "reference": {"value": round(len(calls) / ref, 1), "unit": "paths/s", "seconds": round(ref, 4),
+                          "cores": 1, "kind": "reference",
+                          "note": "the reference's build_pairs_introns on the same calls, recorded by gmap_trace"}}
+
+
 def measure_c2(genome, n, steps, warmup, dev):
     """Side line, BASELINE config 2 (round-1 headline): 100k reads on the 64 Mbp
     genome, one GPU, device-resident; per-kernel event times."""
@@ -644,6 +683,7 @@ def main() -> None:
             if not args.no_extra:
                 out["splicejunction"] = measure_sj(genome, 100_000, 20, args.warmup, dev, not args.no_cpu)
                 out["microexon"] = measure_micro(genome, 20_000, 20, args.warmup, dev, not args.no_cpu)
+                out["stage3_pass"] = measure_stage3()
         print(json.dumps(out), flush=True)
     shard.finish(ranks)
     ctx.close()

@@ -1201,3 +1201,36 @@ def c3_cached(reads: int, local_rank: int, seed_genome: int = 3, seed_reads: int
     a = {k: np.load(os.path.join(d, k + ".npy"), mmap_mode="r", allow_pickle=False) for k in names}
     return PackedGenome(a["blocks"], meta["names"], np.array(meta["lengths"], np.int64)), \
         Batch(a["windows"], a["query"], a["query_uc"])
+
+
+def stage3_calls(z, copies: int = 1):
+    """Unpack a recorded stage-3 pass (tests/golden/gmap_*_stage3.npz,
+    oracle/gen_golden.py stage3_golden) into the inputs of
+    Context.stage3_pass -- (calls, pairs_in, query, query_uc) -- and the lists
+    the reference returned (concatenated, call by call), `copies` times over
+    (every copy its own paths and query bytes)."""
+    from .records import S3_PAIR
+    calls = z["calls"].copy()
+    pin = z["pairs_in"]
+    src, flags, new = z["out_src"], z["out_flags"], z["out_new"]
+    want = np.zeros(src.size, dtype=S3_PAIR)
+    want[src < 0] = new
+    at = 0
+    for c in calls:
+        n = int(c["nout"])
+        s = src[at:at + n]
+        keep = np.nonzero(s >= 0)[0]
+        want[at + keep] = pin[int(c["first_pair"]) + s[keep]]
+        want["src"][at + keep] = s[keep]
+        want["flags"][at:at + n] = flags[at:at + n]
+        at += n
+    q, qu = z["query"], z["query_uc"]
+    if copies > 1:
+        n = len(calls)
+        k = np.repeat(np.arange(copies), n)
+        calls = np.tile(calls, copies)
+        calls["first_pair"] += (k * pin.size).astype(np.int32)
+        calls["qpos"] += (k * q.size).astype(np.int32)
+        calls["first_out"] += (k * want.size).astype(np.int32)
+        pin, q, qu, want = np.tile(pin, copies), np.tile(q, copies), np.tile(qu, copies), np.tile(want, copies)
+    return calls, pin, q, qu, want

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from gsnapdp import Context
+from gsnapdp import workload as W
 from test_stage3_cpu import NAMES, check_pass, stage3_golden
 
 pytestmark = pytest.mark.gpu
@@ -31,24 +32,13 @@ def test_gpu_stage3_pass_matches_reference(golden_dir, name):
     ctx.close()
 
 
-def replicate(calls, pin, q, qu, want, copies):
-    """`copies` copies of every call, in one set of buffers"""
-    n = len(calls)
-    C = np.tile(calls, copies)
-    k = np.repeat(np.arange(copies), n)
-    C["first_pair"] += (k * pin.size).astype(np.int32)
-    C["qpos"] += (k * q.size).astype(np.int32)
-    C["first_out"] += (k * want.size).astype(np.int32)
-    return C, np.tile(pin, copies), np.tile(q, copies), np.tile(qu, copies), np.tile(want, copies)
-
-
 def test_gpu_stage3_pass_at_scale(golden_dir):
     z = np.load(os.path.join(golden_dir, "gmap_synth_stage3.npz"), allow_pickle=False)
     calls, pin, q, qu, want = stage3_golden(z)
     ctx = Context(z["blocks"])
     ctx.stage3_pass(calls[:8], pin, q, qu)  # warm-up (first launches, staging)
     copies = 64
-    C, PI, Q, QU, WANT = replicate(calls, pin, q, qu, want, copies)
+    C, PI, Q, QU, WANT = W.stage3_calls(z, copies)
     t0 = time.perf_counter()
     got_calls, got, st = ctx.stage3_pass(C, PI, Q, QU)
     dt = time.perf_counter() - t0

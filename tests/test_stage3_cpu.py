@@ -16,6 +16,7 @@ import subprocess
 import numpy as np
 import pytest
 
+from gsnapdp import workload as W
 from gsnapdp.records import S3_CALL, S3_PAIR, S3_STATS
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -26,21 +27,7 @@ COUNTERS = ["out_minor", "out_major", "out_nintrons", "out_nnonintrons", "out_in
 
 def stage3_golden(z):
     """(calls, pairs_in, query, query_uc, the expected returned lists concatenated)."""
-    calls = z["calls"].copy()
-    pin = z["pairs_in"]
-    src, flags, new = z["out_src"], z["out_flags"], z["out_new"]
-    out = np.zeros(src.size, dtype=S3_PAIR)
-    out[src < 0] = new
-    at = 0
-    for c in calls:
-        n = int(c["nout"])
-        s = src[at:at + n]
-        keep = np.nonzero(s >= 0)[0]
-        out[at + keep] = pin[int(c["first_pair"]) + s[keep]]
-        out["src"][at + keep] = s[keep]
-        out["flags"][at:at + n] = flags[at:at + n]
-        at += n
-    return calls, pin, z["query"], z["query_uc"], out
+    return W.stage3_calls(z)
 
 
 def check_pass(calls, out, want_calls, want_out, what):
