@@ -98,6 +98,16 @@ struct Tally {
   int npush;  // pairs the reference pushes (gapholders included)
 };
 
+// The match mask of a query row: bit g set when a diagonal step against genome
+// class g (A C G T N) counts as a match -- the uppercase bytes are equal or
+// consistent_array holds (dynprog.c:2650-2656).  prof rows as build_profile_table.
+__device__ inline uint32_t row_match_mask(const uint32_t* __restrict__ prof, int mt, unsigned char c1,
+                                          unsigned char u1) {
+  const uint32_t a = prof[mt * 128 + (c1 & 127u)];
+  const uint32_t b = u1 < 128 ? prof[4 * 128 + u1] : 0u;
+  return ((a | b) >> 24) & 31u;
+}
+
 // Direction nibble: bit0 gap1==HORIZ, bit1 gap2==VERT, bit2 nogap HORIZ, bit3 nogap VERT.
 // `dirs(r, c)` returns the nibble of an in-band cell with r >= 1, c >= 1.
 //
@@ -106,11 +116,13 @@ struct Tally {
 // (dynprog.c:1460-1488).
 //
 // `colcls(c)` is the genome class (0..5 = A C G T N *) of column c in 1..L2;
-// `qrow(r)` is row r's query byte | uppercase query byte << 8.
-template <class Dirs, class Col, class QRow>
-__device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c, const QRow& qrow,
-                                 const Col& colcls, const uint32_t* __restrict__ prof, Tally& t,
-                                 OpWriter& ow) {
+// `qmask(r)` is row r's match mask (row_match_mask).  Runs of diagonal steps
+// are taken four cells at a time: the cells (r-k, c-k), k = 0..3, share the
+// diagonal, so they are in the band when r, c >= 4, and their eight loads are
+// independent.
+template <class Dirs, class Col, class QMask>
+__device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c, const QMask& qmask,
+                                 const Col& colcls, Tally& t, OpWriter& ow) {
   const int lband = L.d.lband, rband = L.d.rband;
   auto inband = [&](int rr, int cc) {
     const int d = rr - cc + rband;
@@ -126,20 +138,34 @@ __device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c, 
     if (!inband(rr, cc)) return false;
     return (dirs(rr, cc) >> 1) & 1u;
   };
-  const uint32_t* ptab = prof + L.d.mt * 128;
-  while (inband(r, c)) {
-    const uint32_t nib = dirs(r, c);
-    // the nogap cell (r,c) itself: one pair unless the genome is '*'
-    const int g = colcls(c);
+  auto count = [&](int rr, int cc) {  // the nogap cell (rr, cc): one pair unless the genome is '*'
+    const int g = colcls(cc);
     if (g != 5) {
-      const uint32_t qq = qrow(r);
-      const unsigned char c1 = (unsigned char)(qq & 127u);
-      const unsigned char u1 = (unsigned char)(qq >> 8);
-      const unsigned char gch = (unsigned char)("ACGTN"[g]);
-      if (u1 == gch || ((ptab[c1] >> (24 + g)) & 1u)) t.nmatches++;
-      else t.nmismatches++;
+      const int m = (int)((qmask(rr) >> g) & 1u);
+      t.nmatches += m;
+      t.nmismatches += 1 - m;
       t.npush++;
     }
+  };
+  while (inband(r, c)) {
+    uint32_t nib;
+    if (r >= 4 && c >= 4) {
+      const uint32_t n0 = dirs(r, c), n1 = dirs(r - 1, c - 1), n2 = dirs(r - 2, c - 2), n3 = dirs(r - 3, c - 3);
+      if (((n0 | n1 | n2 | n3) & 12u) == 0u) {
+        count(r, c);
+        count(r - 1, c - 1);
+        count(r - 2, c - 2);
+        count(r - 3, c - 3);
+        ow.run += 4;
+        r -= 4;
+        c -= 4;
+        continue;
+      }
+      nib = n0;
+    } else {
+      nib = dirs(r, c);
+    }
+    count(r, c);
     ow.run++;
     if (nib & 8u) {  // VERT: query skip (add_queryskip, dynprog.c:2372)
       int dist = 1;

@@ -290,8 +290,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
     const PH itab = (PH)(region + G.oItab);
     const PH qb = (PH)(region + G.oQ);
     if (act) {
-      for (int i = rho; i < G.L1; i += RL)
-        qb[i] = (uint16_t)((unsigned char)q[w.qpos + i] | ((unsigned)(unsigned char)qu[w.qpos + i] << 8));
+      for (int i = rho; i < G.L1; i += RL)  // the traceback's per-row match masks
+        qb[i] = (uint16_t)row_match_mask(prof, G.mt, (unsigned char)q[w.qpos + i], (unsigned char)qu[w.qpos + i]);
       for (int t = rho; t < 64; t += RL) {  // intron_score by leftdi & rightdi (:3148-3192)
         int it;
         const int sI = intron_score(it, t, 0x3F, w.cdna_direction, G.canon, w.finalp);
@@ -531,14 +531,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
         const int L1 = G.L1;
         traceback(CellDirs<P>{HR, G.WR, G.lbR}, LR, best.rR, best.cR,
                   [&](int r) -> uint32_t { return qb[L1 - r]; }, [&](int c) -> int { return clsR[c]; },
-                  prof, t, owR);
+                  t, owR);
 #endif
         const int nR = owR.n < cap ? owR.n : cap;
         OpWriter owL = {ops + o0 + nR, cap - nR, 0, 0};
 #ifndef GG_EXP_NOTRACE
         traceback(CellDirs<P>{HL, G.WL, G.lbL}, LL, best.rL, best.cL,
                   [&](int r) -> uint32_t { return qb[r - 1]; }, [&](int c) -> int { return clsL[c]; },
-                  prof, t, owL);
+                  t, owL);
 #endif
         X.nops_right = nR;
         X.nops_left = owL.n < owL.cap ? owL.n : owL.cap;
@@ -619,7 +619,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
       }
       for (int i = rho; i < L1; i += RL) {
         const int qi = L.qbase + L.qstep * i;
-        qb[i] = (uint16_t)((unsigned char)q[qi] | ((unsigned)(unsigned char)qu[qi] << 8));
+        qb[i] = (uint16_t)row_match_mask(prof, d.mt, (unsigned char)q[qi], (unsigned char)qu[qi]);
       }
     }
     if constexpr (GMEM) wave_fence();
@@ -683,7 +683,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
       OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
       traceback(CellDirs<P>{H, W, d.lband}, L, br, bc,
                 [&](int r) -> uint32_t { return qb[r - 1]; }, [&](int c) -> int { return cls[c]; },
-                prof, t, ow);
+                t, ow);
       if constexpr (SEG)
         score = t.nmatches * 3 - 5 * t.nmismatches + t.nopens * d.open + t.nindels * d.ext;
       write_result(&res[wi], w, L, score, br, bc, t, ow);

@@ -1151,26 +1151,30 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     gpu_s += std::chrono::duration<double>(t1 - t0).count();
     host_s += std::chrono::duration<double>(clock::now() - t1).count();
   }
-  int64_t at = 0;
+  // the returned lists, each path's at its running offset (lengths first,
+  // then the copies by the workers)
+  const auto t_out = clock::now();
+  std::vector<int64_t> first((size_t)ncalls + 1, 0);
   for (int i = 0; i < ncalls; i++) {
     Path& k = paths[(size_t)i];
-    gsnapdp_s3_call& c = calls[i];
+    int n = 0;
+    if (!k.failed)
+      for (int p = k.pairs; p >= 0; p = k.A.rest(p)) n++;
+    first[(size_t)i + 1] = first[(size_t)i] + n;
+  }
+  if (first[(size_t)ncalls] > out_cap) {
+    gsnapdp__set_err("gsnapdp_stage3_pass: pairs_out is too small");
+    return -1;
+  }
+  for_paths(all, threads, [&](Path& k) {
+    gsnapdp_s3_call& c = *k.c;
+    const size_t i = (size_t)(&k - paths.data());
     c.status = k.failed ? -1 : 0;
-    c.first_out = (int32_t)at;
-    c.nout = 0;
-    P.st.undefined += k.undefined;
-    if (k.failed) {
-      P.st.failed++;
-      continue;
-    }
-    for (int p = k.pairs; p >= 0; p = k.A.rest(p)) {
-      if (at >= out_cap) {
-        gsnapdp__set_err("gsnapdp_stage3_pass: pairs_out is too small");
-        return -1;
-      }
-      pairs_out[at++] = k.A.first(p);
-      c.nout++;
-    }
+    c.first_out = (int32_t)first[i];
+    c.nout = (int32_t)(first[i + 1] - first[i]);
+    if (k.failed) return;
+    int64_t at = first[i];
+    for (int p = k.pairs; p >= 0; p = k.A.rest(p)) pairs_out[at++] = k.A.first(p);
     c.out_minor = k.minor;
     c.out_major = k.major;
     c.out_nintrons = k.nintrons;
@@ -1179,7 +1183,12 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     c.out_nonintronlen = k.nonintronlen;
     c.shiftp = k.shiftp ? 1 : 0;
     c.incompletep = k.incompletep ? 1 : 0;
+  });
+  for (Path& k : paths) {
+    P.st.undefined += k.undefined;
+    if (k.failed) P.st.failed++;
   }
+  host_s += std::chrono::duration<double>(clock::now() - t_out).count();
   P.st.seconds[0] = host_s;
   P.st.seconds[1] = gpu_s;
   P.st.seconds[2] = std::chrono::duration<double>(clock::now() - t_start).count();

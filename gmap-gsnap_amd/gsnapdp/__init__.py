@@ -460,16 +460,24 @@ class Context:
             raise GsnapdpError("gsnapdp_score_introns_host: %s" % lib().gsnapdp_last_error().decode())
         return out
 
-    def stage3_pass(self, calls: np.ndarray, pairs_in: np.ndarray, query: np.ndarray, query_uc: np.ndarray):
+    @staticmethod
+    def stage3_capacity(calls: np.ndarray) -> int:
+        """pairs_out capacity that always suffices for these calls"""
+        return int((2 * (calls["querylength"].astype(np.int64) + calls["npairs"]) + 64).sum()) if len(calls) else 1
+
+    def stage3_pass(self, calls: np.ndarray, pairs_in: np.ndarray, query: np.ndarray, query_uc: np.ndarray,
+                    out: np.ndarray = None):
         """build_pairs_introns (stage3.c:7735-7901) over every call's path at once
         (gsnapdp_stage3_pass).  Returns (calls with the out fields written, the
-        returned lists concatenated, S3_STATS)."""
+        returned lists concatenated, S3_STATS).  `out`: a reusable S3_PAIR buffer
+        of stage3_capacity(calls) pairs."""
         c = np.array(calls, dtype=S3_CALL, copy=True)
         pi = np.ascontiguousarray(pairs_in, dtype=S3_PAIR)
         q = np.ascontiguousarray(query, dtype=np.uint8)
         qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
-        cap = int((2 * (c["querylength"].astype(np.int64) + c["npairs"]) + 64).sum()) if len(c) else 1
-        out = np.empty(max(cap, 1), dtype=S3_PAIR)  # only the lists written are touched
+        cap = self.stage3_capacity(c)
+        if out is None or out.dtype != S3_PAIR or out.size < cap:
+            out = np.empty(max(cap, 1), dtype=S3_PAIR)  # only the lists written are touched
         st = np.zeros(1, dtype=S3_STATS)
         rc = lib().gsnapdp_stage3_pass(self.h, _p(c), len(c), _p(pi) if pi.size else _p(out), _p(q), _p(qu),
                                        _p(out), cap, _p(st))
