@@ -220,7 +220,10 @@ __device__ unsigned long long tb_prof[8];
   do {                 \
   } while (0)
 #endif
-template <int S, int LPW>
+// MATCH = false (k_fill): no match bytes; every diagonal step inside the
+// window's genome is counted in nmismatches, and k_count splits the total into
+// matches and mismatches afterwards from the op stream.
+template <int S, int LPW, bool MATCH = true>
 __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint8_t* __restrict__ M,
                                       int g, int r, int cstart, int maxC, int lband, int rband,
                                       int stop, int cvlo, int cvhi, int JL, const Lane& L,
@@ -253,7 +256,7 @@ __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint
     for (int k = 0; k < 4; k++) {
       const int cc = 4 * G + k;
       x.w[k] = ldw(cc, jw);
-      x.m[k] = ldm(cc, jw);
+      if constexpr (MATCH) x.m[k] = ldm(cc, jw);
     }
     x.jw = jw;
   };
@@ -318,9 +321,13 @@ __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint
       } else {
         const uint32_t x = ((jj == jw) ? wk : ldw(c, jj)) >> pb;
         if (c >= cvlo && c <= cvhi) {  // not a '*' column (dynprog.c:2644)
-          const uint32_t mb = (((jj == jw) ? mk : ldm(c, jj)) >> (S - 1 - pb)) & 1u;
-          tal.nmatches += (int)mb;
-          tal.nmismatches += 1 - (int)mb;
+          if constexpr (MATCH) {
+            const uint32_t mb = (((jj == jw) ? mk : ldm(c, jj)) >> (S - 1 - pb)) & 1u;
+            tal.nmatches += (int)mb;
+            tal.nmismatches += 1 - (int)mb;
+          } else {
+            tal.nmismatches++;
+          }
         }
         ow.run++;
         if (((x >> (3 * S)) & 1u) ^ jlbit) {  // v1: VERT
@@ -365,7 +372,9 @@ __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint
         const uint32_t vh = (1u << (2 * S)) | (1u << (3 * S));  // h1 and v1 of this slot
         fast4 = ((x0 | x1 | x2 | x3) & vh) == 0u && (inside || outside);
         if (fast4) {
-          if (inside) {
+          if (!MATCH && inside) {
+            tal.nmismatches += 4;
+          } else if (inside) {
             const int mb = S - 1 - pb;  // match bit of the diagonal's slot
             const int mcount = (int)(((ga.m[0] >> mb) & 1u) + ((ga.m[1] >> mb) & 1u) +
                                      ((ga.m[2] >> mb) & 1u) + ((ga.m[3] >> mb) & 1u));
@@ -388,7 +397,7 @@ __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint
         const int k = c & 3;
         if (!fast4 && st != T_DONE && (st != T_WAIT || c == cstart)) {
           const uint32_t wk = k == 0 ? ga.w[0] : k == 1 ? ga.w[1] : k == 2 ? ga.w[2] : ga.w[3];
-          const uint32_t mk = k == 0 ? ga.m[0] : k == 1 ? ga.m[1] : k == 2 ? ga.m[2] : ga.m[3];
+          const uint32_t mk = !MATCH ? 0u : k == 0 ? ga.m[0] : k == 1 ? ga.m[1] : k == 2 ? ga.m[2] : ga.m[3];
           column(c, wk, mk, ga.jw);
         }
       }

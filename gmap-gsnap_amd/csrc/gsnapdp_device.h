@@ -240,7 +240,7 @@ __device__ inline int agg_atomic_inc(int* counter, int key) {
 // Final bookkeeping shared by all paths.
 __device__ inline void write_result(gsnapdp_result* res, const gsnapdp_window& w, const Lane& L,
                                     int score, int bestr, int bestc, const Tally& t,
-                                    const OpWriter& ow) {
+                                    const OpWriter& ow, bool post = true) {
   gsnapdp_result R;
   R.finalscore = score;
   R.nmatches = t.nmatches;
@@ -254,8 +254,10 @@ __device__ inline void write_result(gsnapdp_result* res, const gsnapdp_window& w
   R.length1 = L.d.L1;
   R.length2 = L.d.L2;
   R.reserved = step_dpi(w.dynprogindex);
+  // (post = false: k_fill's tracebacks; k_count applies the rules below once it
+  // has split the diagonal steps into matches and mismatches)
   // end gaps, QUERYEND_GAP / BEST_LOCAL: dynprog.c:5259-5262 / 5715-5718
-  if (L.d.mode == 1 && t.nmatches + 1 < t.nmismatches) {
+  if (post && L.d.mode == 1 && t.nmatches + 1 < t.nmismatches) {
     R.finalscore = 0;
     if (R.status == ST_OK) R.status = ST_ZEROED;
   }

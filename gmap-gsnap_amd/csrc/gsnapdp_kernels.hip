@@ -34,6 +34,17 @@ namespace {
 // (the rank of a band cell must fit END_RANK_BITS), 2 the last row's scan of
 // find_best_endpoint_to_queryend_indels; 0 not on the register band.
 constexpr int END_RANK_BITS = 14;
+// k_fill's match bits: 1 (default) -- the fill tracks a match byte per
+// lane-column in the scratch beside the direction words and the traceback
+// reads it; 0 -- the fill keeps no match bits, its tracebacks count diagonal
+// steps only and k_count splits them afterwards from the op streams.  Both are
+// bit-exact (all GPU tests); 0 makes k_fill 7.7 % faster on C3 (3.50 -> 3.23 ms)
+// but k_count costs 0.62 ms per 1M windows (latency-bound: a chain of five
+// dependent loads per window), so 1 stays the product (k_fill).
+#ifndef GSNAPDP_FILL_MATCH
+#define GSNAPDP_FILL_MATCH 1
+#endif
+constexpr bool FILL_MATCH = GSNAPDP_FILL_MATCH != 0;
 constexpr int END_RANK_MAX = (1 << END_RANK_BITS) - 1;
 __device__ inline int end_kind(const Derived& d) {
 #ifdef GSNAPDP_FILL32
@@ -374,7 +385,7 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
     E[s] = NEGV;
     F[s] = (r >= 1) ? FV_BIAS + open : NEGV;  // open + r*ext - r*ext
     P[s] = row_word(r);
-    MB = ((MB >> 1) & MB_KEEP) | row_spread(P[s]);
+    if constexpr (FILL_MATCH) MB = ((MB >> 1) & MB_KEEP) | row_spread(P[s]);
   }
   // Rings: lane j of a window stages the rows / columns congruent to j mod
   // LPW.  Lane j's bottom slot holds row t + j*(S-1) + rbase at step t, its
@@ -539,9 +550,11 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
       } else {
         P[ROT] = pnext;
       }
-      MB = ((MB >> 1) & MB_KEEP) | row_spread(pnext);
       gsh = 4u * (uint32_t)gnext;
-      macc = (uint32_t)(MB >> (8u * (uint32_t)gnext));
+      if constexpr (FILL_MATCH) {
+        MB = ((MB >> 1) & MB_KEEP) | row_spread(pnext);
+        macc = (uint32_t)(MB >> (8u * (uint32_t)gnext));
+      }
       cell(0, H[1], E[1]);
     }
     FV hb = NEGV, eb = NEGV;  // old (nogap, gap1) just below the lowest local slot
@@ -562,7 +575,7 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
 #ifndef EXP_NOSTORE
       D[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = acc;
 #ifndef EXP_NOMATCH
-      M[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = (uint8_t)macc;
+      if constexpr (FILL_MATCH) M[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = (uint8_t)macc;
 #endif
 #else
       if (acc == 0x12345678u && macc == 77u) D[0] = 1u;
@@ -655,12 +668,14 @@ __device__ void trace_batch(int lane, int wi, FillOut fo, int jl,
   OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
   // a segment window's genome classes (the long-gap intron test) come from its segment
   const SegCls sc = {sjw ? (const unsigned char*)q + sjw[wi].spos : nullptr, L.g0};
-  band_traceback<S, LPW>(Dk, Mk, g, fo.br, fo.bc, maxC, L.d.lband, L.d.rband, WMAX - L.d.W,
+  band_traceback<S, LPW, FILL_MATCH>(Dk, Mk, g, fo.br, fo.bc, maxC, L.d.lband, L.d.rband, WMAX - L.d.W,
                          sjw ? 1 : cs.cvlo, sjw ? L.d.L2 : cs.cvhi, jl, L, blocks, nwords, tal, ow, sc);
   // Dynprog_end5/3_splicejunction score the alignment from its counts (:5541 / :6045)
-  const int score = sjw ? tal.nmatches * 3 - 5 * tal.nmismatches + tal.nopens * L.d.open + tal.nindels * L.d.ext
+  // (without the fill's match bits k_count does both once it has the counts)
+  const int score = sjw && FILL_MATCH
+                        ? tal.nmatches * 3 - 5 * tal.nmismatches + tal.nopens * L.d.open + tal.nindels * L.d.ext
                         : fo.score;
-  write_result(res + wi, w, L, score, fo.br, fo.bc, tal, ow);
+  write_result(res + wi, w, L, score, fo.br, fo.bc, tal, ow, FILL_MATCH);
 }
 
 // This wave's wave-tasks of class (S, LPW, LOW), in batches of B (<= TB_BATCH)
@@ -807,6 +822,123 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
 #undef FILL_CLASS
 }
 
+// --------------------------------------------------------------- k_count
+// The match / mismatch split of k_fill's tracebacks (k_fill counts every
+// diagonal step inside the window's genome in nmismatches, FILL_MATCH = 0).
+// One lane per window replays the op stream from the traceback's start cell
+// as the host expansion does (gsnapdp_host.cpp replay: DIAG r--, c--; HDASH /
+// HGAP c -= n; VSKIP r -= n) and tests each diagonal cell as dynprog.c:2644-2656
+// does: '*' columns are skipped, a match is uppercase equality or
+// consistent_array.  Then the post-rules of write_result that need the split
+// (the end-gap zeroing, dynprog.c:5259-5262 / 5715-5718) and the
+// splice-junction ends' score from the counts (:5541 / :6045).
+constexpr int COUNT_LANES = 16;                        // k_count: lanes per window
+constexpr int COUNT_ROWS = FAST_L2MAX + FAST_WMAX + 16;  // > any k_fill window's length1 (<= L2 + lband)
+constexpr int COUNT_COLS = FAST_L2MAX + 16;
+__global__ __launch_bounds__(256) void k_count(const gsnapdp_window* __restrict__ Wn, const int* __restrict__ perm,
+                                               const int* __restrict__ class_start, const char* __restrict__ q,
+                                               const char* __restrict__ qu, const uint32_t* __restrict__ blocks,
+                                               uint64_t nwords, const uint32_t* __restrict__ prof,
+                                               gsnapdp_result* __restrict__ res, const uint32_t* __restrict__ ops,
+                                               const int64_t* __restrict__ op_off,
+                                               const gsnapdp_sj_window* __restrict__ sjw) {
+  // match bits (bit g: class g of A C G T N) of consistent_array per matrix
+  // type and query character, then of uppercase equality per query_uc byte
+  __shared__ uint8_t mbits[5 * 128];
+  // per window of the block: each row's match bits against the five classes,
+  // and each column's genome class
+  __shared__ uint8_t mrow[256 / COUNT_LANES][COUNT_ROWS];
+  __shared__ uint8_t gcol[256 / COUNT_LANES][COUNT_COLS];
+  for (int x = threadIdx.x; x < 5 * 128; x += blockDim.x) mbits[x] = (uint8_t)((prof[x] >> 24) & 31u);
+  __syncthreads();
+  const int u0 = threadIdx.x % COUNT_LANES;
+  const int slot = threadIdx.x / COUNT_LANES;
+  const int i = (blockIdx.x * blockDim.x + threadIdx.x) / COUNT_LANES;
+  if (i >= class_start[NCLASS]) return;
+  const int wi = perm[i];
+  if (wi < 0) return;  // (the whole lane group leaves together; no block barrier below)
+  gsnapdp_result R = res[wi];
+  if (R.status == ST_OPS_OVERFLOW || R.status == ST_INTERNAL) return;
+  const gsnapdp_window w = Wn[wi];
+  const Lane L = make_lane(w);
+  const int L1 = L.d.L1, L2 = L.d.L2;
+  if (L1 >= COUNT_ROWS || L2 >= COUNT_COLS) {  // (k_plan never buckets such a window for k_fill)
+    if (u0 == 0) res[wi].status = ST_INTERNAL;
+    return;
+  }
+  const uint8_t* mt = mbits + L.d.mt * 128;
+  uint8_t* mr = mrow[slot];
+  uint8_t* gc = gcol[slot];
+  // rows 1..L1: the group's lanes read adjacent query bytes
+  // (four rows per lane at a time: their loads are issued together)
+  for (int r0 = 1 + u0; r0 <= L1; r0 += 4 * COUNT_LANES) {
+    unsigned char qc[4], uc[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int r = min(r0 + e * COUNT_LANES, L1);
+      const int qi = L.qbase + L.qstep * (r - 1);
+      qc[e] = qchar(q, qi);
+      uc[e] = (unsigned char)qu[qi];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int r = r0 + e * COUNT_LANES;
+      if (r <= L1) mr[r] = mt[qc[e]] | (uc[e] < 128 ? mbits[4 * 128 + uc[e]] : (uint8_t)0);
+    }
+  }
+  // columns 1..L2: adjacent genome positions (or segment bytes)
+  if (sjw) {
+    const int sp = (int)sjw[wi].spos - L.gstep;  // column c is q[sp + gstep * c] (every column inside)
+    for (int c = 1 + u0; c <= L2; c += COUNT_LANES) gc[c] = (uint8_t)seg_class((unsigned char)q[sp + L.gstep * c]);
+  } else {
+    ColStream cs;
+    cs.init(L);
+    for (int c0 = 1 + u0; c0 <= L2; c0 += 4 * COUNT_LANES) {
+      int g[4];
+#pragma unroll
+      for (int e = 0; e < 4; e++) g[e] = cs.cls(blocks, nwords, min(c0 + e * COUNT_LANES, L2));
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if (c0 + e * COUNT_LANES <= L2) gc[c0 + e * COUNT_LANES] = (uint8_t)g[e];
+    }
+  }
+  // the other lanes of the group read what these lanes wrote (same wave, LDS in order)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int total = R.nmismatches;
+  const uint32_t* o = ops + op_off[wi];
+  int r = R.bestr, c = R.bestc, m = 0;
+  for (int k = 0; k < R.nops; k++) {
+    const uint32_t op = o[k];
+    const int cnt = (int)GSNAPDP_OP_COUNT(op);
+    const uint32_t ty = GSNAPDP_OP_TYPE(op);
+    if (ty == GSNAPDP_OP_DIAG) {
+      for (int x = u0; x < cnt; x += COUNT_LANES) {
+        const int g = gc[c - x];
+        if (g < 5) m += (int)((mr[r - x] >> g) & 1u);  // '*' columns skipped (dynprog.c:2644)
+      }
+      r -= cnt;
+      c -= cnt;
+    } else if (ty == GSNAPDP_OP_VSKIP) {
+      r -= cnt;
+    } else {
+      c -= cnt;
+    }
+  }
+#pragma unroll
+  for (int x = COUNT_LANES / 2; x > 0; x >>= 1) m += __shfl_xor(m, x, COUNT_LANES);
+  if (u0 != 0) return;
+  R.nmatches = m;
+  R.nmismatches = total - m;
+  if (sjw) R.finalscore = m * 3 - 5 * R.nmismatches + R.nopens * L.d.open + R.nindels * L.d.ext;
+  if (L.d.mode == 1 && R.nmatches + 1 < R.nmismatches) {
+    R.finalscore = 0;
+    if (R.status == ST_OK) R.status = ST_ZEROED;
+  }
+  res[wi] = R;
+}
+
 // --------------------------------------------------------------- k_maxent
 __global__ void k_maxent(const uint8_t* __restrict__ model, const uint32_t* __restrict__ pos,
                          const uint32_t* __restrict__ chroff, double* __restrict__ out, int n,
@@ -883,6 +1015,7 @@ __global__ void k_introns(const gsnapdp_intron_path* __restrict__ P, int npaths,
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1044,6 +1177,15 @@ int gsnapdp__fill_pipeline(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_windo
                      d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_dirpool,
                      WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets, big_count + RW_NCLS, sjw);
   mark(2, 1);
+  if constexpr (!FILL_MATCH) {
+    mark(7, 0);
+    // perm holds at most 64 entries per window (a bucket pads to whole waves)
+    const size_t nperm = std::min(ctx->perm_cap, (size_t)n * 64);
+    const size_t per_block = 256 / COUNT_LANES;
+    hipLaunchKernelGGL(k_count, dim3((unsigned)((nperm + per_block - 1) / per_block)), dim3(256), 0, st, d_windows, ctx->d_perm, class_start, d_query,
+                       d_query_uc, ctx->d_blocks, nw, ctx->d_prof, d_results, d_ops, d_op_offsets, sjw);
+    mark(7, 1);
+  }
 #ifdef TB_PROF
   {
     unsigned long long h[8];
@@ -1196,7 +1338,7 @@ void gsnapdp__mark(gsnapdp_ctx* ctx, hipStream_t st, int stage, int end) {
 }
 
 static const char* const kStageNames[] = {"k_plan", "k_scan+k_scatter", "k_fill", "k_rows",
-                                          "k_ggap_plan", "k_ggap", "k_gband"};
+                                          "k_ggap_plan", "k_ggap", "k_gband", "k_count"};
 static const int kNStages = (int)(sizeof(kStageNames) / sizeof(kStageNames[0]));
 
 extern "C" const char* gsnapdp_stage_name(int stage) {
