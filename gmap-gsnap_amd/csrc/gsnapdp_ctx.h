@@ -103,5 +103,10 @@ struct gsnapdp_ctx {
   void* h_mx = nullptr;             // pinned: its packed inputs / outputs
   size_t h_mx_cap = 0;
   std::vector<uint32_t> h_comp;     // compacted ops on their way to op_offsets
+  // stage-3 pass executors (gsnapdp_stage3_exec.cpp): staging of idle ones
+  std::mutex s3_mu;
+  std::vector<void*> s3_pool;
 };
+// frees the context's idle stage-3 executors (gsnapdp_destroy)
+void gsnapdp__s3_pool_free(gsnapdp_ctx* ctx);
 

@@ -24,6 +24,7 @@
 #include "../../include/gsnapdp.h"
 #include "../../include/gsnapdp_dropin.h"
 #include "gsnapdp_internal.h"
+#include "gsnapdp_pairlayout.h"
 
 namespace {
 
@@ -625,7 +626,9 @@ struct RefPairGap {
   char cdna, comp, genome, aa_g, aa_e;
   unsigned char gapp, knowngapp;  // bool (bool.h: unsigned char)
 };
-static_assert(offsetof(RefPairGap, gapp) == 41 && offsetof(RefPairGap, knowngapp) == 42, "Pair_T layout");
+static_assert(offsetof(RefPairGap, gapp) == GSNAPDP_PAIR_OFF_GAPP &&
+                  offsetof(RefPairGap, knowngapp) == GSNAPDP_PAIR_OFF_KNOWNGAPP,
+              "Pair_T layout");
 // ... and the whole struct (pairdef.h:9-49), for build_pairs_introns' disallowedp
 struct RefPair {
   int querypos;
@@ -638,8 +641,26 @@ struct RefPair {
   double donor_prob, acceptor_prob;
   unsigned char end_intron_p;
 };
-static_assert(offsetof(RefPair, disallowedp) == 61 && offsetof(RefPair, donor_prob) == 64 && sizeof(RefPair) == 88,
+// every field the shim touches, against the constants oracle/pairdef_check.c
+// asserts against the reference's pairdef.h / listdef.h (gsnapdp_pairlayout.h)
+static_assert(offsetof(RefPair, querypos) == GSNAPDP_PAIR_OFF_QUERYPOS &&
+                  offsetof(RefPair, genomepos) == GSNAPDP_PAIR_OFF_GENOMEPOS &&
+                  offsetof(RefPair, queryjump) == GSNAPDP_PAIR_OFF_QUERYJUMP &&
+                  offsetof(RefPair, genomejump) == GSNAPDP_PAIR_OFF_GENOMEJUMP &&
+                  offsetof(RefPair, dynprogindex) == GSNAPDP_PAIR_OFF_DYNPROGINDEX &&
+                  offsetof(RefPair, cdna) == GSNAPDP_PAIR_OFF_CDNA && offsetof(RefPair, comp) == GSNAPDP_PAIR_OFF_COMP &&
+                  offsetof(RefPair, genome) == GSNAPDP_PAIR_OFF_GENOME &&
+                  offsetof(RefPair, gapp) == GSNAPDP_PAIR_OFF_GAPP &&
+                  offsetof(RefPair, knowngapp) == GSNAPDP_PAIR_OFF_KNOWNGAPP &&
+                  offsetof(RefPair, disallowedp) == GSNAPDP_PAIR_OFF_DISALLOWEDP &&
+                  offsetof(RefPair, donor_prob) == GSNAPDP_PAIR_OFF_DONOR_PROB && sizeof(RefPair) == GSNAPDP_PAIR_SIZE,
               "Pair_T layout");
+static_assert(offsetof(RefPairHead, querypos) == GSNAPDP_PAIR_OFF_QUERYPOS &&
+                  offsetof(RefPairHead, comp) == GSNAPDP_PAIR_OFF_COMP,
+              "Pair_T layout");
+static_assert(offsetof(RefList, first) == GSNAPDP_LIST_OFF_FIRST && offsetof(RefList, rest) == GSNAPDP_LIST_OFF_REST &&
+                  sizeof(RefList) == GSNAPDP_LIST_SIZE,
+              "List_T layout");
 
 // binary_search (dynprog.c:5068-5090)
 int binary_search(int lowi, int highi, const unsigned* positions, unsigned goal) {
@@ -685,84 +706,59 @@ extern "C" __attribute__((weak)) gsnapdp_bool IIT_high_exists_signed_p(gsnapdp_I
 extern "C" __attribute__((weak)) gsnapdp_bool IIT_exists_with_divno_signed(
     gsnapdp_IIT_T, int divno, unsigned int x, unsigned int y, int sign);
 
+// The host program's splicing IIT as the batched ABI asks it (gsnapdp_iit):
+// each query goes to the host's own iit-read function with the division and
+// type ints Dynprog_setup was given (dynprog.c:350-376), so the known-site
+// records (gsnapdp_known_site_record) and score_introns' verdicts
+// (gsnapdp_introns_known) see exactly what the reference's queries see.
+template <class F>
+F resolve_host(F f, const char* name) {  // weak reference, else a lookup in the process
+  if (!f) f = (F)dlsym(RTLD_DEFAULT, name);
+  if (!f) fatal(std::string("a splicing IIT was given but the host program's ") + name + " is not linked");
+  return f;
+}
+int host_typed(void*, int chrnum, uint32_t x, uint32_t y, int type, int sign) {
+  static const auto f = resolve_host(&IIT_exists_with_divno_typed_signed, "IIT_exists_with_divno_typed_signed");
+  return f(g.iit, g.divint_crosstable[chrnum], x, y, type == GSNAPDP_DONOR ? g.donor_typeint : g.acceptor_typeint,
+           sign) ? 1 : 0;
+}
+int host_low(void*, int chrnum, uint32_t x, int sign) {
+  static const auto f = resolve_host(&IIT_low_exists_signed_p, "IIT_low_exists_signed_p");
+  return f(g.iit, g.divint_crosstable[chrnum], x, sign) ? 1 : 0;
+}
+int host_high(void*, int chrnum, uint32_t x, int sign) {
+  static const auto f = resolve_host(&IIT_high_exists_signed_p, "IIT_high_exists_signed_p");
+  return f(g.iit, g.divint_crosstable[chrnum], x, sign) ? 1 : 0;
+}
+int host_exact(void*, int chrnum, uint32_t x, uint32_t y, int sign) {
+  static const auto f = resolve_host(&IIT_exists_with_divno_signed, "IIT_exists_with_divno_signed");
+  return f(g.iit, g.divint_crosstable[chrnum], x, y, sign) ? 1 : 0;
+}
+const gsnapdp_iit* host_iit() {
+  static gsnapdp_iit h;
+  h.user = nullptr;
+  h.site_level = g.donor_typeint >= 0 && g.acceptor_typeint >= 0 ? 1 : 0;
+  h.pad = 0;
+  h.typed = host_typed;
+  h.low = host_low;
+  h.high = host_high;
+  h.exact = host_exact;
+  return &h;
+}
+
 // Appends one window's known-site record (left_known[L2L], right_known[L2R],
-// the KNOWN_INTRONS pair list) to `q` and returns its known_mode.
+// the KNOWN_INTRONS pair list) to `q` at `at` and returns its known_mode.
 int known_site_record(std::vector<char>& q, size_t at, int chrnum, unsigned chrpos,
                       unsigned genomiclength, int leftoffset, int rightoffset, int L2L, int L2R,
                       int cdna_direction, bool watsonp) {
-  // weak references bound at link time, else looked up in the process (a host
-  // that dlopens the shim before its iit-read code)
-  auto resolve = [](auto f, const char* name) {
-    if (!f) f = (decltype(f))dlsym(RTLD_DEFAULT, name);
-    if (!f) fatal(std::string("a splicing IIT was given but the host program's ") + name + " is not linked");
-    return f;
-  };
-  const auto typed = resolve(&IIT_exists_with_divno_typed_signed, "IIT_exists_with_divno_typed_signed");
-  const auto lowp = resolve(&IIT_low_exists_signed_p, "IIT_low_exists_signed_p");
-  const auto highp = resolve(&IIT_high_exists_signed_p, "IIT_high_exists_signed_p");
-  const auto exact = resolve(&IIT_exists_with_divno_signed, "IIT_exists_with_divno_signed");
-  const int divno = g.divint_crosstable[chrnum];
-  const bool sites = g.donor_typeint >= 0 && g.acceptor_typeint >= 0;
-  const bool fwd = cdna_direction > 0;
-  const unsigned gl1 = genomiclength - 1U;
-  q.resize(at + (size_t)L2L + (size_t)L2R + 2, 0);
-  char* left = q.data() + at;
-  char* right = left + L2L;
-  for (int cL = 0; cL < L2L - 1; cL++) {  // :3379-3530, left half of each case
-    const unsigned pos = watsonp ? chrpos + leftoffset + cL : chrpos + gl1 - leftoffset - cL + 1U;
-    bool k;
-    if (sites)
-      k = typed(g.iit, divno, pos, pos + 1U, fwd ? g.donor_typeint : g.acceptor_typeint,
-                watsonp ? (fwd ? +1 : -1) : (fwd ? -1 : +1));
-    else if (watsonp)
-      k = lowp(g.iit, divno, pos, fwd ? +1 : -1);
-    else
-      k = highp(g.iit, divno, pos + 1U, fwd ? -1 : +1);
-    left[cL] = k ? 1 : 0;
-  }
-  for (int cR = 0; cR < L2R - 1; cR++) {  // right half of each case
-    const unsigned pos = watsonp ? chrpos + rightoffset - cR + 1U : chrpos + gl1 - rightoffset + cR;
-    bool k;
-    if (sites)
-      k = typed(g.iit, divno, pos, pos + 1U, fwd ? g.acceptor_typeint : g.donor_typeint,
-                watsonp ? (fwd ? +1 : -1) : (fwd ? -1 : +1));
-    else if (watsonp)
-      k = highp(g.iit, divno, pos + 1U, fwd ? +1 : -1);
-    else
-      k = lowp(g.iit, divno, pos, fwd ? -1 : +1);
-    right[cR] = k ? 1 : 0;
-  }
-  int mode;
-  if (g.novelsplicingp) mode = GSNAPDP_KNOWN_REWARD;
-  else if (sites) mode = GSNAPDP_KNOWN_SITES;
-  else mode = GSNAPDP_KNOWN_INTRONS;
-  if (mode == GSNAPDP_KNOWN_INTRONS) {  // the introns the constrained bridge may take (:3598-3612)
-    std::vector<std::pair<int, int>> pairs;
-    for (int cL = 0; cL < L2L - 1; cL++) {
-      if (!q[at + cL]) continue;
-      for (int cR = 0; cR < L2R - 1; cR++) {
-        if (!q[at + L2L + cR]) continue;
-        bool ok;
-        if (watsonp)
-          ok = exact(g.iit, divno, chrpos + leftoffset + cL,
-                                            chrpos + rightoffset - cR + 1U + 1U, cdna_direction);
-        else
-          ok = exact(g.iit, divno, chrpos + gl1 - rightoffset + cR,
-                                            chrpos + gl1 - leftoffset - cL + 1U + 1U, -cdna_direction);
-        if (ok) pairs.emplace_back(cL, cR);
-      }
-    }
-    if (pairs.size() > 0xffff) fatal("more than 65535 known introns in one genome-gap window");
-    const size_t p0 = at + (size_t)L2L + (size_t)L2R;
-    q[p0] = (char)(pairs.size() & 255);
-    q[p0 + 1] = (char)(pairs.size() >> 8);
-    for (const auto& pr : pairs) {
-      const unsigned char e[4] = {(unsigned char)(pr.first & 255), (unsigned char)(pr.first >> 8),
-                                  (unsigned char)(pr.second & 255), (unsigned char)(pr.second >> 8)};
-      q.insert(q.end(), (const char*)e, (const char*)e + 4);
-    }
-  }
-  q.resize(q.size() + 8, 0);
+  const int cap = L2L + L2R + 2 + 4 * L2L * L2R;
+  q.resize(at + (size_t)cap);
+  int len = 0;
+  const int mode = gsnapdp_known_site_record(host_iit(), g.novelsplicingp ? 1 : 0, chrnum, chrpos, genomiclength,
+                                             leftoffset, rightoffset, L2L, L2R, cdna_direction, watsonp ? 1 : 0,
+                                             q.data() + at, cap, &len);
+  if (mode < 0) fatal(std::string("known-site record: ") + gsnapdp_last_error());
+  q.resize(at + (size_t)len + 8, 0);
   return mode;
 }
 
@@ -1546,38 +1542,9 @@ gsnapdp_List_T Gsnapdp_score_introns(double* avg_donor_score, double* avg_accept
   if (n < 0) fatal("score_introns: an intron at the end of the path (the reference dereferences NULL)");
   req.introns.resize((size_t)n);
   gsnapdp_path_introns(pp.data(), (int)pp.size(), nullgap, 0, req.introns.data(), n);
-  if (g.iit) {  // known sites score 1.0 (:7997-8046, :8069-8116)
-    auto typed = [](auto f, const char* name) {
-      if (!f) f = (decltype(f))dlsym(RTLD_DEFAULT, name);
-      if (!f) fatal(std::string("a splicing IIT was given but the host program's ") + name + " is not linked");
-      return f;
-    };
-    const auto exists = typed(&IIT_exists_with_divno_typed_signed, "IIT_exists_with_divno_typed_signed");
-    const int divno = g.divint_crosstable[chrnum];
-    const unsigned gl1 = (unsigned)genomiclength - 1U;
-    for (gsnapdp_intron& t : req.introns) {
-      unsigned pd, pa;
-      int sign;
-      if (cdna_direction == +1) {
-        pd = watsonp ? chrpos + t.left_genomepos + 1U : chrpos + gl1 - t.left_genomepos;
-        pa = watsonp ? chrpos + t.right_genomepos : chrpos + gl1 - t.right_genomepos + 1U;
-        sign = watsonp ? +1 : -1;
-      } else if (cdna_direction == -1) {
-        pa = watsonp ? chrpos + t.left_genomepos + 1U : chrpos + gl1 - t.left_genomepos;
-        pd = watsonp ? chrpos + t.right_genomepos : chrpos + gl1 - t.right_genomepos + 1U;
-        sign = watsonp ? -1 : +1;
-      } else {
-        continue;
-      }
-      if (cdna_direction == +1) {  // the reference asks about the donor first
-        t.known_donor = exists(g.iit, divno, pd, pd + 1U, g.donor_typeint, sign) ? 1 : 0;
-        t.known_acceptor = exists(g.iit, divno, pa, pa + 1U, g.acceptor_typeint, sign) ? 1 : 0;
-      } else {
-        t.known_acceptor = exists(g.iit, divno, pa, pa + 1U, g.acceptor_typeint, sign) ? 1 : 0;
-        t.known_donor = exists(g.iit, divno, pd, pd + 1U, g.donor_typeint, sign) ? 1 : 0;
-      }
-    }
-  }
+  if (g.iit && gsnapdp_introns_known(host_iit(), chrnum, chrpos, genomiclength, cdna_direction, watsonp ? 1 : 0,
+                                     req.introns.data(), n))  // known sites score 1.0 (:7997-8046, :8069-8116)
+    fatal(std::string("score_introns: ") + gsnapdp_last_error());
   req.p.chroffset = chroffset;
   req.p.chrpos = chrpos;
   req.p.genomiclength = genomiclength;
@@ -1610,7 +1577,6 @@ gsnapdp_List_T Gsnapdp_build_pairs_introns(
     int extraband_single, int extraband_paired, double defect_rate, int close_indels_mode,
     gsnapdp_Pairpool_T pairpool, gsnapdp_Dynprog_T dynprogL, gsnapdp_Dynprog_T dynprogM,
     gsnapdp_Dynprog_T dynprogR, gsnapdp_bool finalp) {
-  if (g.splicing_iit) fatal("build_pairs_introns with a splicing IIT is not served by the batched pass");
   if (use_genomicseg_p) fatal("build_pairs_introns on a genomic segment is not served by the batched pass");
   gsnapdp_ctx* c = shared_ctx(true);
   std::vector<RefList*> cells;
@@ -1669,7 +1635,10 @@ gsnapdp_List_T Gsnapdp_build_pairs_introns(
   const int64_t cap = 2 * ((int64_t)querylength + k.npairs) + 64;
   std::vector<gsnapdp_s3_pair> out((size_t)cap);
   gsnapdp_s3_stats st;
-  if (gsnapdp_stage3_pass(c, &k, 1, in.data(), queryseq_ptr, queryuc_ptr, out.data(), cap, &st))
+  // the splicing IIT of Dynprog_setup, asked through the host's own iit-read
+  // functions (every genome-gap window's known-site record)
+  if (gsnapdp_stage3_pass(c, &k, 1, in.data(), (int64_t)in.size(), queryseq_ptr, queryuc_ptr, (size_t)querylength,
+                          g.iit ? host_iit() : nullptr, out.data(), cap, &st))
     fatal(std::string("gsnapdp_stage3_pass: ") + gsnapdp_last_error());
   if (k.status) fatal("build_pairs_introns: a window outside the reference's domain (the reference aborts)");
   gsnapdp_List_T list = nullptr;
@@ -1680,12 +1649,18 @@ gsnapdp_List_T Gsnapdp_build_pairs_introns(
       ((RefPair*)l->first)->disallowedp = (p.flags & GSNAPDP_S3_DISALLOWED) ? 1 : 0;
       l->rest = (RefList*)list;
       list = (gsnapdp_List_T)l;
-    } else if (p.flags & GSNAPDP_S3_GAPP) {
-      list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump,
-                                     (p.flags & GSNAPDP_S3_KNOWNGAPP) ? 1 : 0);
-      ((RefPair*)((RefList*)list)->first)->comp = p.comp;  // a microexon's gapchar (dynprog.c:6991)
     } else {
-      list = Pairpool_push(list, pairpool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome, p.dynprogindex);
+      if (p.flags & GSNAPDP_S3_GAPP) {
+        list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump,
+                                       (p.flags & GSNAPDP_S3_KNOWNGAPP) ? 1 : 0);
+        ((RefPair*)((RefList*)list)->first)->comp = p.comp;  // a microexon's gapchar (dynprog.c:6991)
+      } else {
+        list = Pairpool_push(list, pairpool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome, p.dynprogindex);
+      }
+      // a pair an earlier fill of this call made and a later genome gap peeled
+      // and put back keeps disallowedp = true (stage3.c:5873-5880); both pushes
+      // start it false (pairpool.c:212, :400)
+      ((RefPair*)((RefList*)list)->first)->disallowedp = (p.flags & GSNAPDP_S3_DISALLOWED) ? 1 : 0;
     }
   }
   *shiftp = k.shiftp ? 1 : 0;

@@ -1084,6 +1084,7 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
 extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  gsnapdp__s3_pool_free(ctx);
   (void)hipFree(ctx->d_blocks);
   (void)hipFree(ctx->d_prof);
   (void)hipFree(ctx->d_tables);

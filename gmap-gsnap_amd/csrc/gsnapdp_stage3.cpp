@@ -6,8 +6,10 @@
 // pairpool.c:471-519), so every peel, put-back and transfer leaves the lists
 // exactly as the reference leaves them.  What changes is the control flow
 // around the DP: a path runs until it needs a gap filled, parks its window,
-// and resumes when the round's batch for that gap family has run.  Rounds go
-// on until every path has reached the end of its list.
+// and resumes when its round's batch has run.  The paths are split into two
+// cohorts with one round each in flight (gsnapdp_stage3.h): while the GPU runs
+// one cohort's windows, a persistent pool of host threads resumes the other's
+// paths, so the host work hides behind the batches instead of adding to them.
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -16,12 +18,16 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/gsnapdp.h"
 #include "gsnapdp_internal.h"
+#include "gsnapdp_stage3.h"
 
 extern "C" const uint32_t* gsnapdp__host_blocks(gsnapdp_ctx* ctx);
 extern "C" size_t gsnapdp__host_nwords(gsnapdp_ctx* ctx);
@@ -104,7 +110,7 @@ struct Req {
   int fam = F_NONE;
   std::vector<char> q, qu;  // the window's query bytes; qpos fields are relative to them
   int64_t cap = 0;
-  std::vector<uint32_t> ops;
+  const uint32_t* ops = nullptr;  // the window's op stream in its round's output staging
   gsnapdp_window w;
   gsnapdp_result r;
   gsnapdp_ggap_window gw;
@@ -160,6 +166,7 @@ struct Pass {
   gsnapdp_ctx* ctx;
   const uint32_t* blocks;
   size_t nwords;
+  const gsnapdp_iit* iit;  // Dynprog_setup's splicing IIT, or nullptr
   gsnapdp_s3_stats st;
 };
 
@@ -391,8 +398,10 @@ void req_single(Path& k) {
   R.cap = (int64_t)(k.queryjump > 0 ? k.queryjump : 0) + (k.genomejump > 0 ? k.genomejump : 0) + 2;
 }
 
-// Dynprog_genome_gap (dynprog.c:4798-5061), halfp = false, no splicing IIT
-void req_genome(Path& k, bool prob, int score_threshold) {
+// Dynprog_genome_gap (dynprog.c:4798-5061), halfp = false; with a splicing IIT
+// the window's known-site record follows its query rows, as the drop-in's
+// Dynprog_genome_gap places it
+bool req_genome(const Pass& P, Path& k, bool prob, int score_threshold) {
   const gsnapdp_s3_call& c = *k.c;
   Req& R = k.req;
   R.fam = F_GGAP;
@@ -430,6 +439,20 @@ void req_genome(Path& k, bool prob, int score_threshold) {
   stage_query(k, R, k.querydp5, k.queryjump);
   const int L1 = k.queryjump > 0 ? k.queryjump : 0;
   R.cap = 2 * (int64_t)L1 + 2 * (int64_t)(k.genomejump > 0 ? k.genomejump : 0) + 4;
+  if (P.iit && L1 > 1 && k.genomejump > 0 && !too_long) {
+    const int rcap = 2 * k.genomejump + 2 + 4 * k.genomejump * k.genomejump;
+    R.q.resize((size_t)L1 + (size_t)rcap);
+    int len = 0;
+    const int mode = gsnapdp_known_site_record(P.iit, c.novelsplicingp, c.chrnum, c.chrpos,
+                                               (uint32_t)c.genomiclength, k.genomedp5, k.genomedp3, k.genomejump,
+                                               k.genomejump, c.cdna_direction, c.watsonp, R.q.data() + L1, rcap,
+                                               &len);
+    if (mode < 0) return false;
+    w.known_mode = (uint8_t)mode;
+    R.q.resize((((size_t)L1 + (size_t)len + 8) + 3) & ~(size_t)3, 0);
+    R.qu.resize(R.q.size(), 0);
+  }
+  return true;
 }
 
 // Dynprog_cdna_gap (dynprog.c:4578-4793): length1L = length1R = queryjump
@@ -524,6 +547,13 @@ void fail(Path& k, const std::string& why) {
   k.req.fam = F_NONE;
 }
 
+// the pairs a family's op stream expands into (one buffer per host thread)
+std::vector<gsnapdp_pair>& expand_buf(size_t n) {
+  thread_local std::vector<gsnapdp_pair> v;
+  if (v.size() < n) v.resize(n);
+  return v;
+}
+
 // a gap family's expanded pairs as a list in the path's arena (push order as
 // the drop-in's push_pairs: the list's head is pairs[0])
 int list_of(Arena& A, const std::vector<gsnapdp_pair>& v, int n, bool micro) {
@@ -568,9 +598,9 @@ bool done_single(Pass& P, Path& k, int* list) {
     fail(k, "op stream overflow");
     return false;
   }
-  std::vector<gsnapdp_pair> v((size_t)R.cap + 8);
+  std::vector<gsnapdp_pair>& v = expand_buf((size_t)R.cap + 8);
   int fs = 0;
-  const int n = gsnapdp_expand(P.ctx, &R.w, &r, R.ops.data(), R.q.data(), R.qu.data(), v.data(), (int)v.size(), &fs);
+  const int n = gsnapdp_expand(P.ctx, &R.w, &r, R.ops, R.q.data(), R.qu.data(), v.data(), (int)v.size(), &fs);
   if (n < 0 || n > (int)v.size()) {
     fail(k, "gsnapdp_expand failed");
     return false;
@@ -617,7 +647,10 @@ bool done_genome(Pass& P, Path& k, int* finalscore, int* nmismatches, double* lp
     k.undefined++;
     return true;
   }
-  if (!w.use_probabilities_p && r.finalscore != -100000) k.introntype = r.introntype;
+  // *introntype: always NONINTRON in the constrained known-intron mode (:3695),
+  // else written only when a score-mode candidate was taken
+  if (w.known_mode == GSNAPDP_KNOWN_INTRONS) k.introntype = NONINTRON;
+  else if (!w.use_probabilities_p && r.finalscore != -100000) k.introntype = r.introntype;
   if (!t.bridge_accepted) return true;
   k.new_left = r.new_leftgenomepos;
   k.new_right = r.new_rightgenomepos;
@@ -629,8 +662,8 @@ bool done_genome(Pass& P, Path& k, int* finalscore, int* nmismatches, double* lp
   k.nopens = r.nopens;
   k.nindels = r.nindels;
   if (r.returned_null) return true;
-  std::vector<gsnapdp_pair> v((size_t)R.cap + 8);
-  const int n = gsnapdp_ggap_expand(P.ctx, &w, &r, &t, R.ops.data(), R.q.data(), R.qu.data(), v.data(), (int)v.size());
+  std::vector<gsnapdp_pair>& v = expand_buf((size_t)R.cap + 8);
+  const int n = gsnapdp_ggap_expand(P.ctx, &w, &r, &t, R.ops, R.q.data(), R.qu.data(), v.data(), (int)v.size());
   if (n < 0 || n > (int)v.size()) {
     fail(k, "gsnapdp_ggap_expand failed");
     return false;
@@ -656,8 +689,8 @@ bool done_cdna(Pass& P, Path& k, int* list) {
   if (r.status != ST_OK) return true;
   if (r.incompletep) k.incompletep = true;  // only ever set to true (:4756)
   if (r.returned_null) return true;
-  std::vector<gsnapdp_pair> v((size_t)R.cap + 32);
-  const int n = gsnapdp_cgap_expand(P.ctx, &R.cw, &r, R.ops.data(), R.q.data(), R.qu.data(), nullptr, v.data(),
+  std::vector<gsnapdp_pair>& v = expand_buf((size_t)R.cap + 32);
+  const int n = gsnapdp_cgap_expand(P.ctx, &R.cw, &r, R.ops, R.q.data(), R.qu.data(), nullptr, v.data(),
                                     (int)v.size());
   if (n < 0 || n > (int)v.size()) {
     fail(k, "gsnapdp_cgap_expand failed");
@@ -681,7 +714,7 @@ bool done_micro(Pass& P, Path& k, double* prob2, double* prob3, int* microintron
   k.major = r.dynprogindex;
   if (!r.found) return true;
   const int L1 = R.mw.length1 > 0 ? R.mw.length1 : 0;
-  std::vector<gsnapdp_pair> v((size_t)L1 + 4);
+  std::vector<gsnapdp_pair>& v = expand_buf((size_t)L1 + 4);
   const int n = gsnapdp_micro_expand(P.ctx, &R.mw, &r, R.q.data(), R.qu.data(), v.data(), (int)v.size());
   if (n <= 0 || n > (int)v.size()) {
     fail(k, "gsnapdp_micro_expand failed");
@@ -835,7 +868,10 @@ bool genome_start(Pass& P, Path& k) {
     return true;
   }
   k.genomejump = k.queryjump + c.extramaterial_paired;  // square matrices
-  req_genome(k, false, 0);
+  if (!req_genome(P, k, false, 0)) {
+    fail(k, "known-site record");
+    return false;
+  }
   k.stage = S_GG_SCORE;
   return true;
 }
@@ -893,7 +929,7 @@ void genome_done(Pass& P, Path& k) {
     if (list >= 0 && (k.new_left != k.A.at(k.left).genomepos || k.new_right != k.A.at(k.right).genomepos))
       k.shiftp = true;
     if (c.finalp && c.novelsplicingp && (k.left_prob < 0.90 || k.right_prob < 0.90)) {
-      req_genome(k, true, k.finalscore + QOPEN + 3 * QINDEL);
+      if (!req_genome(P, k, true, k.finalscore + QOPEN + 3 * QINDEL)) return fail(k, "known-site record");
       k.stage = S_GG_PROB;
       return;
     }
@@ -974,137 +1010,265 @@ void resume(Pass& P, Path& k) {
   if (k.stage == S_SCAN) scan(P, k);
 }
 
-// The paths' host work between rounds (peels, traversals, expansion) is
-// independent per path: `threads` workers take them in chunks.  The gap
-// families' expanders only read the context (genome, tables).
-template <class F>
-void for_paths(std::vector<Path*>& v, int threads, F fn) {
-  const int n = (int)v.size();
-  if (threads <= 1 || n < 64) {
-    for (Path* k : v) fn(*k);
-    return;
-  }
-  std::atomic<int> next(0);
-  auto work = [&]() {
-    for (int i; (i = next.fetch_add(16)) < n;)
-      for (int j = i; j < std::min(n, i + 16); j++) fn(*v[(size_t)j]);
-  };
-  std::vector<std::thread> th;
-  for (int t = 1; t < threads; t++) th.emplace_back(work);
-  work();
-  for (std::thread& x : th) x.join();
-}
 
+// ---- host threads: one persistent pool per process.  A round's host work is
+// a few hundred microseconds, so the workers spin briefly for the next job
+// before they sleep, and nothing is spawned per round.
 int pass_threads() {
   if (const char* e = getenv("GSNAPDP_S3_THREADS")) return std::max(1, atoi(e));
   const int hw = (int)std::thread::hardware_concurrency();
   return std::max(1, std::min(16, hw));  // a GPU box's CPU share is 16 (nproc shows the whole machine)
 }
 
-// ---- one round: every waiting path's window, one batch per family
-template <class T>
-std::vector<char> pack_query(const std::vector<Path*>& b, std::vector<size_t>* qo, std::vector<char>* QU,
-                             std::vector<int64_t>* off) {
-  std::vector<char> Q;
-  qo->resize(b.size());
-  off->assign(b.size() + 1, 0);
-  for (size_t i = 0; i < b.size(); i++) {
-    (*qo)[i] = Q.size();
-    Q.insert(Q.end(), b[i]->req.q.begin(), b[i]->req.q.end());
-    QU->insert(QU->end(), b[i]->req.qu.begin(), b[i]->req.qu.end());
-    (*off)[i + 1] = (*off)[i] + b[i]->req.cap;
+class Workers {
+ public:
+  static Workers& get() {
+    static Workers* w = new Workers(pass_threads());  // never joined: the workers outlive every pass
+    return *w;
   }
-  Q.resize(Q.size() + 8, 0);
-  QU->resize(QU->size() + 8, 0);
-  return Q;
+  // fn(i) for every i in [0, n), `grain` indices at a time, on the pool and the caller
+  void run(int n, int grain, const std::function<void(int)>& fn) {
+    if (n <= 0) return;
+    if (nthreads_ <= 1 || n <= grain) {
+      for (int i = 0; i < n; i++) fn(i);
+      return;
+    }
+    std::lock_guard<std::mutex> one(run_m_);  // concurrent passes take turns
+    {
+      std::lock_guard<std::mutex> l(m_);
+      fn_ = &fn;
+      n_ = n;
+      grain_ = grain;
+      next_.store(0);
+      active_.store(nthreads_ - 1);
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> l(m_);
+    done_.wait(l, [&] { return active_.load() == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  explicit Workers(int n) : nthreads_(n) {
+    for (int t = 1; t < n; t++) std::thread([this] { loop(); }).detach();
+  }
+  void work() {
+    for (int i; (i = next_.fetch_add(grain_)) < n_;)
+      for (int j = i; j < std::min(n_, i + grain_); j++) (*fn_)(j);
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (gen_.load(std::memory_order_acquire) == seen) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+          std::unique_lock<std::mutex> l(m_);
+          cv_.wait(l, [&] { return gen_.load() != seen; });
+          break;
+        }
+      }
+      seen = gen_.load(std::memory_order_acquire);
+      work();
+      if (active_.fetch_sub(1) == 1) {
+        std::lock_guard<std::mutex> l(m_);
+        done_.notify_all();
+      }
+    }
+  }
+  const int nthreads_;
+  std::mutex m_, run_m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* fn_ = nullptr;
+  std::atomic<int> next_{0}, active_{0};
+  std::atomic<uint64_t> gen_{0};
+  int n_ = 0, grain_ = 1;
+};
+
+// ---- a cohort of paths and its round in flight
+constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Cohort {
+  std::vector<Path*> paths;
+  std::vector<Path*> fam[F_N];  // the round's waiting paths, in batch order
+  std::vector<Path*> all;       // the same, concatenated
+  std::vector<size_t> qoff;     // each waiting path's query bytes in the packed round (all's order)
+  gsnapdp::S3Layout L;
+  int slot = 0;
+  bool inflight = false;
+};
+
+// Packs the cohort's waiting windows into its slot's input staging and
+// submits them.  Returns 1 when a round was submitted, 0 when no path waits,
+// -1 on an error.
+int pack_submit(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
+  size_t nwait = 0;
+  for (int f = 0; f < F_N; f++) C.fam[f].clear();
+  for (Path* k : C.paths)
+    if (!k->failed && k->stage != S_DONE && k->req.fam != F_NONE) C.fam[k->req.fam].push_back(k), nwait++;
+  if (!nwait) return 0;
+  gsnapdp::S3Layout& L = C.L;
+  L = gsnapdp::S3Layout();
+  C.all.clear();
+  C.qoff.clear();
+  size_t q = 0;
+  int64_t ncap[F_N] = {0, 0, 0, 0};
+  for (int f = 0; f < F_N; f++) {
+    L.n[f] = (int)C.fam[f].size();
+    for (Path* k : C.fam[f]) {
+      C.all.push_back(k);
+      C.qoff.push_back(q);
+      q += (k->req.q.size() + 3) & ~(size_t)3;
+      ncap[f] += k->req.cap;
+    }
+  }
+  L.q = 0;
+  L.qbytes = q + 8;
+  L.qu = al256(L.qbytes);
+  size_t at = L.qu + al256(L.qbytes);
+  const size_t wsz[F_N] = {sizeof(gsnapdp_window), sizeof(gsnapdp_ggap_window), sizeof(gsnapdp_cgap_window),
+                           sizeof(gsnapdp_micro_window)};
+  const size_t rsz[F_N] = {sizeof(gsnapdp_result), sizeof(gsnapdp_ggap_result), sizeof(gsnapdp_cgap_result),
+                           sizeof(gsnapdp_micro_result)};
+  for (int f = 0; f < F_N; f++) {
+    L.w[f] = at;
+    at += al256((size_t)L.n[f] * wsz[f]);
+    if (f != F_MICRO) {
+      L.off[f] = at;
+      at += al256((size_t)(L.n[f] + 1) * 8);
+    }
+  }
+  L.in_bytes = at;
+  at = 0;
+  for (int f = 0; f < F_N; f++) {
+    L.r[f] = at;
+    at += al256((size_t)L.n[f] * rsz[f]);
+    if (f == F_GGAP) {
+      L.t = at;
+      at += al256((size_t)L.n[f] * sizeof(gsnapdp_ggap_trace));
+    }
+    if (f != F_MICRO) {
+      L.ops[f] = at;
+      at += al256((size_t)ncap[f] * 4 + 4);
+    }
+  }
+  L.out_bytes = at;
+  char* in = X.in_buf(C.slot, L.in_bytes);
+  if (!in || !X.out_buf(C.slot, L.out_bytes)) return -1;
+  for (int f = 0; f < F_N; f++) {  // op offsets: each family's capacity layout
+    if (f == F_MICRO) continue;
+    int64_t* off = (int64_t*)(in + L.off[f]);
+    off[0] = 0;
+    for (int i = 0; i < L.n[f]; i++) off[i + 1] = off[i] + C.fam[f][(size_t)i]->req.cap;
+  }
+  memset(in + L.q + q, 0, 8);
+  memset(in + L.qu + q, 0, 8);
+  int base[F_N + 1] = {0};
+  for (int f = 0; f < F_N; f++) base[f + 1] = base[f] + L.n[f];
+  Workers::get().run((int)C.all.size(), 64, [&](int j) {
+    Path& k = *C.all[(size_t)j];
+    const Req& R = k.req;
+    const size_t qo = C.qoff[(size_t)j];
+    const size_t qn = R.q.size();
+    memcpy(in + L.q + qo, R.q.data(), qn);
+    memcpy(in + L.qu + qo, R.qu.data(), qn);
+    const size_t pad = ((qn + 3) & ~(size_t)3) - qn;
+    if (pad) memset(in + L.q + qo + qn, 0, pad), memset(in + L.qu + qo + qn, 0, pad);
+    const int f = R.fam, i = j - base[f];
+    const uint32_t o = (uint32_t)qo;
+    if (f == F_GAP) {
+      gsnapdp_window w = R.w;
+      w.qpos += o;
+      memcpy(in + L.w[f] + (size_t)i * sizeof(w), &w, sizeof(w));
+    } else if (f == F_GGAP) {
+      gsnapdp_ggap_window w = R.gw;
+      w.qpos += o;
+      memcpy(in + L.w[f] + (size_t)i * sizeof(w), &w, sizeof(w));
+    } else if (f == F_CGAP) {
+      gsnapdp_cgap_window w = R.cw;
+      w.qposL += o;
+      w.qposR += o;
+      memcpy(in + L.w[f] + (size_t)i * sizeof(w), &w, sizeof(w));
+    } else {
+      gsnapdp_micro_window w = R.mw;
+      w.qpos += o;
+      w.ppos += o;
+      memcpy(in + L.w[f] + (size_t)i * sizeof(w), &w, sizeof(w));
+    }
+  });
+  if (X.submit(C.slot, L)) return -1;
+  for (int f = 0; f < F_N; f++)
+    if (L.n[f]) {
+      P.st.windows[f] += L.n[f];
+      P.st.batches[f]++;
+    }
+  P.st.rounds++;
+  return 1;
 }
 
-int run_round(Pass& P, std::vector<Path*> fam[F_N]) {
-  for (int f = 0; f < F_N; f++) {
-    std::vector<Path*>& b = fam[f];
-    if (b.empty()) continue;
-    const int n = (int)b.size();
-    std::vector<size_t> qo;
-    std::vector<char> QU;
-    std::vector<int64_t> off;
-    std::vector<char> Q = pack_query<char>(b, &qo, &QU, &off);
-    std::vector<uint32_t> ops((size_t)off[(size_t)n] + 1);
-    int rc = 0;
+// Hands the round's results to its paths and resumes them (the slot's staging
+// stays untouched until the cohort packs its next round).
+void unpack_resume(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
+  const gsnapdp::S3Layout& L = C.L;
+  const char* in = X.in_buf(C.slot, 0);
+  const char* out = X.out_buf(C.slot, 0);
+  int base[F_N + 1] = {0};
+  for (int f = 0; f < F_N; f++) base[f + 1] = base[f] + L.n[f];
+  Workers::get().run((int)C.all.size(), 16, [&](int j) {
+    Path& k = *C.all[(size_t)j];
+    Req& R = k.req;
+    const int f = R.fam, i = j - base[f];
+    const int64_t* off = f == F_MICRO ? nullptr : (const int64_t*)(in + L.off[f]);
     if (f == F_GAP) {
-      std::vector<gsnapdp_window> W((size_t)n);
-      std::vector<gsnapdp_result> R((size_t)n);
-      for (int i = 0; i < n; i++) {
-        W[(size_t)i] = b[(size_t)i]->req.w;
-        W[(size_t)i].qpos += (uint32_t)qo[(size_t)i];
-      }
-      rc = gsnapdp_run_host(P.ctx, W.data(), n, Q.data(), QU.data(), Q.size(), R.data(), ops.data(), off.data());
-      for (int i = 0; i < n; i++) b[(size_t)i]->req.r = R[(size_t)i];
+      memcpy(&R.r, out + L.r[f] + (size_t)i * sizeof(R.r), sizeof(R.r));
     } else if (f == F_GGAP) {
-      std::vector<gsnapdp_ggap_window> W((size_t)n);
-      std::vector<gsnapdp_ggap_result> R((size_t)n);
-      std::vector<gsnapdp_ggap_trace> T((size_t)n);
-      for (int i = 0; i < n; i++) {
-        W[(size_t)i] = b[(size_t)i]->req.gw;
-        W[(size_t)i].qpos += (uint32_t)qo[(size_t)i];
-      }
-      rc = gsnapdp_ggap_run_host(P.ctx, W.data(), n, Q.data(), QU.data(), Q.size(), R.data(), T.data(), ops.data(),
-                                 off.data());
-      for (int i = 0; i < n; i++) {
-        b[(size_t)i]->req.gr = R[(size_t)i];
-        b[(size_t)i]->req.gt = T[(size_t)i];
-      }
+      memcpy(&R.gr, out + L.r[f] + (size_t)i * sizeof(R.gr), sizeof(R.gr));
+      memcpy(&R.gt, out + L.t + (size_t)i * sizeof(R.gt), sizeof(R.gt));
     } else if (f == F_CGAP) {
-      std::vector<gsnapdp_cgap_window> W((size_t)n);
-      std::vector<gsnapdp_cgap_result> R((size_t)n);
-      for (int i = 0; i < n; i++) {
-        W[(size_t)i] = b[(size_t)i]->req.cw;
-        W[(size_t)i].qposL += (uint32_t)qo[(size_t)i];
-        W[(size_t)i].qposR += (uint32_t)qo[(size_t)i];
-      }
-      rc = gsnapdp_cgap_run_host(P.ctx, W.data(), n, Q.data(), QU.data(), Q.size(), R.data(), ops.data(), off.data());
-      for (int i = 0; i < n; i++) b[(size_t)i]->req.cr = R[(size_t)i];
+      memcpy(&R.cr, out + L.r[f] + (size_t)i * sizeof(R.cr), sizeof(R.cr));
     } else {
-      std::vector<gsnapdp_micro_window> W((size_t)n);
-      std::vector<gsnapdp_micro_result> R((size_t)n);
-      for (int i = 0; i < n; i++) {
-        W[(size_t)i] = b[(size_t)i]->req.mw;
-        W[(size_t)i].qpos += (uint32_t)qo[(size_t)i];
-        W[(size_t)i].ppos += (uint32_t)qo[(size_t)i];
-      }
-      rc = gsnapdp_micro_run_host(P.ctx, W.data(), n, Q.data(), QU.data(), Q.size(), R.data());
-      for (int i = 0; i < n; i++) b[(size_t)i]->req.mr = R[(size_t)i];
+      memcpy(&R.mr, out + L.r[f] + (size_t)i * sizeof(R.mr), sizeof(R.mr));
     }
-    if (rc) return -1;
-    for (int i = 0; i < n; i++) {
-      Req& R = b[(size_t)i]->req;
-      R.ops.assign(ops.begin() + off[(size_t)i], ops.begin() + off[(size_t)i + 1]);
-    }
-    P.st.windows[f] += n;
-    P.st.batches[f]++;
-  }
-  return 0;
+    R.ops = off ? (const uint32_t*)(out + L.ops[f]) + off[i] : nullptr;
+    R.fam = F_NONE;
+    resume(P, k);
+  });
+}
+
+bool call_in_range(const gsnapdp_s3_call& c, int64_t npairs_in, size_t query_bytes) {
+  return c.first_pair >= 0 && c.npairs >= 0 && (int64_t)c.first_pair + c.npairs <= npairs_in && c.qpos >= 0 &&
+         c.querylength >= 0 && (uint64_t)c.qpos + (uint64_t)c.querylength <= (uint64_t)query_bytes;
 }
 
 }  // namespace
 
 extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls,
-                                   const gsnapdp_s3_pair* pairs_in, const char* query, const char* query_uc,
+                                   const gsnapdp_s3_pair* pairs_in, int64_t npairs_in, const char* query,
+                                   const char* query_uc, size_t query_bytes, const gsnapdp_iit* iit,
                                    gsnapdp_s3_pair* pairs_out, int64_t out_cap, gsnapdp_s3_stats* stats) {
-  if (!ctx || (ncalls > 0 && (!calls || !pairs_in || !query || !query_uc || !pairs_out)) || ncalls < 0) {
+  if (!ctx || ncalls < 0 || npairs_in < 0 ||
+      (ncalls > 0 && (!calls || (npairs_in > 0 && !pairs_in) || !query || !query_uc || !pairs_out))) {
     gsnapdp__set_err("gsnapdp_stage3_pass: bad arguments");
     return -1;
   }
+  for (int i = 0; i < ncalls; i++)
+    if (!call_in_range(calls[i], npairs_in, query_bytes)) {
+      gsnapdp__set_err("gsnapdp_stage3_pass: call " + std::to_string(i) +
+                       " names pairs or query bytes outside the buffers");
+      return -1;
+    }
   Pass P;
   P.ctx = ctx;
   P.blocks = gsnapdp__host_blocks(ctx);
   P.nwords = gsnapdp__host_nwords(ctx);
+  P.iit = iit;
   memset(&P.st, 0, sizeof(P.st));
   using clock = std::chrono::steady_clock;
   const auto t_start = clock::now();
-  double host_s = 0.0, gpu_s = 0.0;
-  const int threads = pass_threads();
+  double wait_s = 0.0;
+  Workers& pool = Workers::get();
   std::vector<Path> paths((size_t)ncalls);
-  std::vector<Path*> all;
   for (int i = 0; i < ncalls; i++) {
     Path& k = paths[(size_t)i];
     gsnapdp_s3_call& c = calls[i];
@@ -1117,9 +1281,9 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     k.nnonintrons = c.in_nnonintrons;
     k.intronlen = c.in_intronlen;
     k.nonintronlen = c.in_nonintronlen;
-    all.push_back(&k);
   }
-  for_paths(all, threads, [&](Path& k) {
+  pool.run(ncalls, 16, [&](int i) {
+    Path& k = paths[(size_t)i];
     const gsnapdp_s3_call& c = *k.c;
     // the input list: path->first is pairs_in[first_pair]
     k.A.pr.reserve((size_t)c.npairs * 2 + 64);
@@ -1131,29 +1295,44 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     if (c.use_genomicseg_p) fail(k, "use_genomicseg_p passes are not served (the genome is the context's)");
     else scan(P, k);
   });
-  host_s += std::chrono::duration<double>(clock::now() - t_start).count();
-  for (;;) {
-    std::vector<Path*> fam[F_N], waiting;
-    for (Path& k : paths)
-      if (!k.failed && k.stage != S_DONE && k.req.fam != F_NONE) {
-        fam[k.req.fam].push_back(&k);
-        waiting.push_back(&k);
-      }
-    if (waiting.empty()) break;
-    const auto t0 = clock::now();
-    if (run_round(P, fam)) return -1;
-    const auto t1 = clock::now();
-    P.st.rounds++;
-    for_paths(waiting, threads, [&](Path& k) {
-      k.req.fam = F_NONE;
-      resume(P, k);
-    });
-    gpu_s += std::chrono::duration<double>(t1 - t0).count();
-    host_s += std::chrono::duration<double>(clock::now() - t1).count();
+  // two cohorts (alternate paths, so both get a similar mix) when there are
+  // enough paths for each round to be worth a batch of its own
+  const int ncoh = ncalls >= 256 ? 2 : 1;
+  Cohort coh[2];
+  for (int i = 0; i < ncalls; i++) coh[i % ncoh].paths.push_back(&paths[(size_t)i]);
+  gsnapdp::S3Exec* X = gsnapdp::s3_exec_acquire(ctx);
+  int rc = 0;
+  for (int h = 0; h < ncoh && !rc; h++) {
+    coh[h].slot = h;
+    const int s = pack_submit(P, *X, coh[h]);
+    if (s < 0) rc = -1;
+    coh[h].inflight = s == 1;
   }
+  while (!rc && (coh[0].inflight || coh[1].inflight)) {
+    for (int h = 0; h < ncoh && !rc; h++) {
+      Cohort& C = coh[h];
+      if (!C.inflight) continue;
+      const auto t0 = clock::now();
+      if (X->wait(C.slot)) {
+        rc = -1;
+        break;
+      }
+      wait_s += std::chrono::duration<double>(clock::now() - t0).count();
+      unpack_resume(P, *X, C);
+      const int s = pack_submit(P, *X, C);
+      if (s < 0) rc = -1;
+      C.inflight = s == 1;
+    }
+  }
+  if (rc) {
+    for (int h = 0; h < ncoh; h++)
+      if (coh[h].inflight) (void)X->wait(coh[h].slot);  // drain before the staging is reused
+    gsnapdp::s3_exec_release(ctx, X);
+    return -1;
+  }
+  gsnapdp::s3_exec_release(ctx, X);
   // the returned lists, each path's at its running offset (lengths first,
   // then the copies by the workers)
-  const auto t_out = clock::now();
   std::vector<int64_t> first((size_t)ncalls + 1, 0);
   for (int i = 0; i < ncalls; i++) {
     Path& k = paths[(size_t)i];
@@ -1166,14 +1345,14 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     gsnapdp__set_err("gsnapdp_stage3_pass: pairs_out is too small");
     return -1;
   }
-  for_paths(all, threads, [&](Path& k) {
+  pool.run(ncalls, 16, [&](int i) {
+    Path& k = paths[(size_t)i];
     gsnapdp_s3_call& c = *k.c;
-    const size_t i = (size_t)(&k - paths.data());
     c.status = k.failed ? -1 : 0;
-    c.first_out = (int32_t)first[i];
-    c.nout = (int32_t)(first[i + 1] - first[i]);
+    c.first_out = (int32_t)first[(size_t)i];
+    c.nout = (int32_t)(first[(size_t)i + 1] - first[(size_t)i]);
     if (k.failed) return;
-    int64_t at = first[i];
+    int64_t at = first[(size_t)i];
     for (int p = k.pairs; p >= 0; p = k.A.rest(p)) pairs_out[at++] = k.A.first(p);
     c.out_minor = k.minor;
     c.out_major = k.major;
@@ -1188,10 +1367,77 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     P.st.undefined += k.undefined;
     if (k.failed) P.st.failed++;
   }
-  host_s += std::chrono::duration<double>(clock::now() - t_out).count();
-  P.st.seconds[0] = host_s;
-  P.st.seconds[1] = gpu_s;
-  P.st.seconds[2] = std::chrono::duration<double>(clock::now() - t_start).count();
+  const double total = std::chrono::duration<double>(clock::now() - t_start).count();
+  P.st.seconds[0] = total - wait_s;
+  P.st.seconds[1] = wait_s;
+  P.st.seconds[2] = total;
   if (stats) *stats = P.st;
+  return 0;
+}
+
+// score_introns on the lists a pass returned (include/gsnapdp.h)
+extern "C" int gsnapdp_stage3_score_introns(gsnapdp_ctx* ctx, const gsnapdp_s3_call* calls, int ncalls,
+                                            const gsnapdp_s3_pair* pairs_out, const gsnapdp_iit* iit,
+                                            gsnapdp_intron_scores* scores) {
+  if (!ctx || ncalls < 0 || (ncalls > 0 && (!calls || !scores))) {
+    gsnapdp__set_err("gsnapdp_stage3_score_introns: bad arguments");
+    return -1;
+  }
+  std::vector<std::vector<gsnapdp_intron>> per((size_t)ncalls);
+  std::atomic<int> bad(0);
+  Workers::get().run(ncalls, 16, [&](int i) {
+    const gsnapdp_s3_call& c = calls[i];
+    if (c.status != 0 || c.nout <= 0) return;
+    thread_local std::vector<gsnapdp_path_pair> pp;
+    pp.resize((size_t)c.nout);
+    for (int j = 0; j < c.nout; j++) {  // List_reverse(pairs): path order
+      const gsnapdp_s3_pair& x = pairs_out[(size_t)c.first_out + (size_t)(c.nout - 1 - j)];
+      gsnapdp_path_pair& y = pp[(size_t)j];
+      y.genomepos = (uint32_t)x.genomepos;
+      y.queryjump = x.queryjump;
+      y.genomejump = x.genomejump;
+      y.gapp = (x.flags & GSNAPDP_S3_GAPP) ? 1 : 0;
+      y.knowngapp = (x.flags & GSNAPDP_S3_KNOWNGAPP) ? 1 : 0;
+      y.comp = (uint8_t)x.comp;
+      y.pad = 0;
+    }
+    const int n = gsnapdp_path_introns(pp.data(), c.nout, c.nullgap, i, nullptr, 0);
+    if (n < 0) {
+      bad.store(i + 1);
+      return;
+    }
+    std::vector<gsnapdp_intron>& v = per[(size_t)i];
+    v.resize((size_t)n);
+    gsnapdp_path_introns(pp.data(), c.nout, c.nullgap, i, v.data(), n);
+    if (iit && gsnapdp_introns_known(iit, c.chrnum, c.chrpos, c.genomiclength, c.cdna_direction, c.watsonp,
+                                     v.data(), n))
+      bad.store(i + 1);
+  });
+  if (bad.load()) {
+    gsnapdp__set_err("gsnapdp_stage3_score_introns: call " + std::to_string(bad.load() - 1) +
+                     " has an intron at the end of its path (the reference dereferences NULL)");
+    return -1;
+  }
+  std::vector<gsnapdp_intron_path> ip((size_t)ncalls);
+  std::vector<gsnapdp_intron> all;
+  for (int i = 0; i < ncalls; i++) {
+    const gsnapdp_s3_call& c = calls[i];
+    gsnapdp_intron_path& p = ip[(size_t)i];
+    p.chroffset = c.chroffset;
+    p.chrpos = c.chrpos;
+    p.genomiclength = c.genomiclength;
+    p.cdna_direction = c.cdna_direction;
+    p.watsonp = c.watsonp;
+    p.first_intron = (int32_t)all.size();
+    p.nintrons = (int32_t)per[(size_t)i].size();
+    p.pad = 0;
+    all.insert(all.end(), per[(size_t)i].begin(), per[(size_t)i].end());
+  }
+  if (ncalls == 0) return 0;
+  if (gsnapdp_score_introns_host(ctx, ip.data(), ncalls, all.empty() ? nullptr : all.data(), (int)all.size(),
+                                 scores))
+    return -1;
+  for (int i = 0; i < ncalls; i++)
+    if (calls[i].status != 0) memset(&scores[i], 0, sizeof(scores[i]));
   return 0;
 }

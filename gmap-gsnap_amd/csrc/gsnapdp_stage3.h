@@ -1,0 +1,57 @@
+// gsnapdp_stage3.h -- the stage-3 passes' batch executor (internal).
+//
+// A pass (gsnapdp_stage3.cpp) advances many paths at once: every round it packs
+// the one pending DP window of each waiting path -- single gaps, genome gaps,
+// cDNA gaps and microexons -- into ONE input buffer (query bytes, then each
+// family's window records and op offsets), and the executor runs the four
+// families on it and brings their results back into ONE output buffer.  A pass
+// keeps two such rounds in flight (two cohorts of paths, one slot each), so
+// the host work of one cohort overlaps the other cohort's batch.
+//
+// The product executor (gsnapdp_stage3_exec.cpp) stages each slot through
+// page-locked memory: one H2D copy, the families' device pipelines back to
+// back on the context stream, one D2H copy and an event; the CPU test build
+// (tests/dropin/stage3_exec_host.cpp) serves the same layout with the host
+// entry points.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/gsnapdp.h"
+
+namespace gsnapdp {
+
+enum S3Fam { S3F_GAP = 0, S3F_GGAP = 1, S3F_CGAP = 2, S3F_MICRO = 3, S3F_N = 4 };
+
+// Byte offsets of one round's regions (each 256-byte aligned).
+struct S3Layout {
+  int n[S3F_N] = {0, 0, 0, 0};
+  size_t q = 0, qu = 0, qbytes = 0;           // in: query, query_uc (qbytes each)
+  size_t w[S3F_N] = {0, 0, 0, 0};             // in: window records
+  size_t off[S3F_N] = {0, 0, 0, 0};           // in: int64 op offsets, n + 1 each (not for microexons)
+  size_t in_bytes = 0;
+  size_t r[S3F_N] = {0, 0, 0, 0};             // out: results
+  size_t t = 0;                               // out: genome-gap traces
+  size_t ops[S3F_N] = {0, 0, 0, 0};           // out: op streams, capacity layout (op offsets)
+  size_t out_bytes = 0;
+};
+
+class S3Exec {
+ public:
+  virtual ~S3Exec() {}
+  // the slot's input / output staging, at least `bytes` long (contents are not kept)
+  virtual char* in_buf(int slot, size_t bytes) = 0;
+  virtual char* out_buf(int slot, size_t bytes) = 0;
+  // run every family of the slot's packed round; the results are in out_buf(slot)
+  // once wait(slot) returns 0.  Returns 0 or -1 (gsnapdp_last_error).
+  virtual int submit(int slot, const S3Layout& L) = 0;
+  virtual int wait(int slot) = 0;
+};
+
+// An executor for one pass over `ctx` (2 slots), taken from the context's pool
+// (created on first use; concurrent passes each get their own staging) and
+// handed back with s3_exec_release.
+S3Exec* s3_exec_acquire(gsnapdp_ctx* ctx);
+void s3_exec_release(gsnapdp_ctx* ctx, S3Exec* e);
+
+}  // namespace gsnapdp

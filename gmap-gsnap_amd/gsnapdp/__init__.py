@@ -19,7 +19,7 @@ import os
 import numpy as np
 
 from .records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW,  # noqa: F401
-                      INTRON, INTRON_PATH, INTRON_SCORES, MAXENT_IN, MICRO_RESULT, MICRO_WINDOW, PAIR,
+                      IIT_INTERVAL, INTRON, INTRON_PATH, INTRON_SCORES, MAXENT_IN, MICRO_RESULT, MICRO_WINDOW, PAIR,
                       PATH_PAIR, RESULT, S3_CALL, S3_PAIR, S3_STATS, SJ_WINDOW, WINDOW)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -106,8 +106,16 @@ def lib():
         L.gsnapdp_score_introns_host.restype = i32
         L.gsnapdp_score_introns_device.argtypes = [vp, vp, i32, vp, vp, vp]
         L.gsnapdp_score_introns_device.restype = i32
-        L.gsnapdp_stage3_pass.argtypes = [vp, vp, i32, vp, vp, vp, vp, ctypes.c_int64, vp]
+        L.gsnapdp_stage3_pass.argtypes = [vp, vp, i32, vp, ctypes.c_int64, vp, vp, sz, vp, vp, ctypes.c_int64, vp]
         L.gsnapdp_stage3_pass.restype = i32
+        L.gsnapdp_stage3_score_introns.argtypes = [vp, vp, i32, vp, vp, vp]
+        L.gsnapdp_stage3_score_introns.restype = i32
+        L.gsnapdp_iit_from_intervals.argtypes = [vp, i32]
+        L.gsnapdp_iit_from_intervals.restype = vp
+        L.gsnapdp_iit_free.argtypes = [vp]
+        L.gsnapdp_known_site_record.argtypes = [vp, i32, i32, ctypes.c_uint32, ctypes.c_uint32] + [i32] * 6 + \
+            [vp, i32, vp]
+        L.gsnapdp_known_site_record.restype = i32
         _lib = L
     return _lib
 
@@ -183,6 +191,29 @@ def cgap_op_offsets(windows: np.ndarray) -> np.ndarray:
     off = np.zeros(len(windows) + 1, dtype=np.int64)
     np.cumsum(cap, out=off[1:])
     return off
+
+
+class SplicingIIT:
+    """A splicing IIT for the batched ABI (gsnapdp_iit_from_intervals): intervals
+    as iit_store writes them (IIT_INTERVAL records: start > end is the minus
+    sign; type -1 none, 0 donor, 1 acceptor)."""
+
+    def __init__(self, intervals: np.ndarray):
+        self.iv = np.ascontiguousarray(intervals, dtype=IIT_INTERVAL)
+        self.h = lib().gsnapdp_iit_from_intervals(_p(self.iv) if self.iv.size else None, self.iv.size)
+        if not self.h:
+            raise GsnapdpError("gsnapdp_iit_from_intervals: %s" % lib().gsnapdp_last_error().decode())
+
+    def close(self):
+        if self.h:
+            lib().gsnapdp_iit_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Context:
@@ -466,11 +497,11 @@ class Context:
         return int((2 * (calls["querylength"].astype(np.int64) + calls["npairs"]) + 64).sum()) if len(calls) else 1
 
     def stage3_pass(self, calls: np.ndarray, pairs_in: np.ndarray, query: np.ndarray, query_uc: np.ndarray,
-                    out: np.ndarray = None):
+                    out: np.ndarray = None, iit: "SplicingIIT" = None):
         """build_pairs_introns (stage3.c:7735-7901) over every call's path at once
         (gsnapdp_stage3_pass).  Returns (calls with the out fields written, the
         returned lists concatenated, S3_STATS).  `out`: a reusable S3_PAIR buffer
-        of stage3_capacity(calls) pairs."""
+        of stage3_capacity(calls) pairs; `iit`: the splicing IIT (SplicingIIT) or None."""
         c = np.array(calls, dtype=S3_CALL, copy=True)
         pi = np.ascontiguousarray(pairs_in, dtype=S3_PAIR)
         q = np.ascontiguousarray(query, dtype=np.uint8)
@@ -479,12 +510,25 @@ class Context:
         if out is None or out.dtype != S3_PAIR or out.size < cap:
             out = np.empty(max(cap, 1), dtype=S3_PAIR)  # only the lists written are touched
         st = np.zeros(1, dtype=S3_STATS)
-        rc = lib().gsnapdp_stage3_pass(self.h, _p(c), len(c), _p(pi) if pi.size else _p(out), _p(q), _p(qu),
-                                       _p(out), cap, _p(st))
+        rc = lib().gsnapdp_stage3_pass(self.h, _p(c), len(c), _p(pi) if pi.size else _p(out), pi.size, _p(q),
+                                       _p(qu), min(q.size, qu.size), iit.h if iit is not None else None, _p(out),
+                                       cap, _p(st))
         if rc != 0:
             raise GsnapdpError("gsnapdp_stage3_pass: %s" % lib().gsnapdp_last_error().decode())
         n = int(c["nout"].sum())
         return c, out[:n], st[0]
+
+    def stage3_score_introns(self, calls: np.ndarray, pairs_out: np.ndarray, iit: "SplicingIIT" = None):
+        """score_introns (stage3.c:7935-8162) on the lists stage3_pass returned
+        (gsnapdp_stage3_score_introns): one INTRON_SCORES per call."""
+        c = np.ascontiguousarray(calls, dtype=S3_CALL)
+        po = np.ascontiguousarray(pairs_out, dtype=S3_PAIR)
+        out = np.zeros(len(c), dtype=INTRON_SCORES)
+        rc = lib().gsnapdp_stage3_score_introns(self.h, _p(c), len(c), _p(po) if po.size else None,
+                                                iit.h if iit is not None else None, _p(out))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_stage3_score_introns: %s" % lib().gsnapdp_last_error().decode())
+        return out
 
     def maxent(self, model: np.ndarray, pos: np.ndarray, chroffset: np.ndarray) -> np.ndarray:
         m = np.ascontiguousarray(model, dtype=np.uint8)

@@ -145,3 +145,8 @@ assert S3_CALL.itemsize == 200
 S3_STATS = np.dtype([("rounds", "<i4"), ("windows", "<i4", 4), ("batches", "<i4", 4), ("undefined", "<i4"),
                      ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3)])
 assert S3_STATS.itemsize == 72
+
+# a splicing IIT's intervals (include/gsnapdp.h: gsnapdp_iit_interval); start > end is the minus sign,
+# type -1 none (an intron), 0 donor, 1 acceptor
+IIT_INTERVAL = np.dtype([("chrnum", "<i4"), ("start", "<u4"), ("end", "<u4"), ("type", "<i4")])
+assert IIT_INTERVAL.itemsize == 16

@@ -765,7 +765,7 @@ def pack_genome(gseq: np.ndarray) -> np.ndarray:
     return _genome.pack(gseq)
 
 
-def synthetic_transcripts(seed: int = 7, ngenes: int = 16, genome_len: int = 160_000):
+def synthetic_transcripts(seed: int = 7, ngenes: int = 16, genome_len: int = 160_000, cins: float = 0.0):
     """End-to-end gmap inputs (tests/test_gmap_e2e.py): a genomic segment
     carrying ``ngenes`` spliced genes and one cDNA per gene.
 
@@ -820,6 +820,16 @@ def synthetic_transcripts(seed: int = 7, ngenes: int = 16, genome_len: int = 160
         exons = [gene[s0:s0 + L].copy() for s0, L in spans]
         minus = rng.random() < 1 / 3
         g[pos:pos + span] = revcomp(gene) if minus else gene
+        if cins > 0:
+            # query-side insertions of 11-60 nt (beyond EXTRAQUERYGAP, stage3.c:7783):
+            # inside an exon or at an exon boundary, so that stage 2 leaves a gap
+            # with queryjump > genomejump + 10 for traverse_cdna_gap (:5518)
+            for e in range(nex):
+                if rng.random() < cins:
+                    n = int(rng.integers(11, 61))
+                    at = int(rng.integers(0, exons[e].size + 1)) if rng.random() < 0.6 else \
+                        (exons[e].size if rng.random() < 0.5 else 0)
+                    exons[e] = np.concatenate([exons[e][:at], ACGT[rng.integers(0, 4, size=n)], exons[e][at:]])
         cdna = np.concatenate(exons)
         cdna = _mutate(rng, cdna, 0.01, 0.001)
         if rng.random() < 1 / 3:

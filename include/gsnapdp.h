@@ -162,7 +162,7 @@ typedef struct gsnapdp_pair {
  *   uint16 npairs (little endian)  KNOWN_INTRONS: the (cL, cR) pairs, both
  *   uint16 cL, cR  x npairs        flagged, for which the reference's
  *                                  IIT_exists_with_divno_signed holds
- * (gsnapdp_dropin.cpp builds it from the host program's IIT queries.) */
+ * (gsnapdp_known_site_record builds it from a gsnapdp_iit, below.) */
 enum { GSNAPDP_KNOWN_NONE = 0, GSNAPDP_KNOWN_REWARD = 1, GSNAPDP_KNOWN_SITES = 2,
        GSNAPDP_KNOWN_INTRONS = 3 };
 typedef struct gsnapdp_ggap_window {
@@ -494,6 +494,50 @@ int gsnapdp_micro_expand(gsnapdp_ctx *ctx, const gsnapdp_micro_window *w,
                          const gsnapdp_micro_result *res, const char *query, const char *query_uc,
                          gsnapdp_pair *pairs, int cap);
 
+/* -------------------------------------------------------- splicing IIT
+ * The splicing IIT gmap / gsnap hand to Dynprog_setup and Stage3_setup
+ * (gmap.c:3281-3318, 3721-3837) as the four queries the DP path makes of it:
+ *   typed  IIT_exists_with_divno_typed_signed (iit-read.c:4011): an interval
+ *          with low == x, high == y, the type (GSNAPDP_DONOR / GSNAPDP_ACCEPTOR:
+ *          the IIT's "donor" / "acceptor" type ints) and the sign;
+ *   low    IIT_low_exists_signed_p (:3770): an interval whose low end is x;
+ *   high   IIT_high_exists_signed_p (:3808): an interval whose high end is x;
+ *   exact  IIT_exists_with_divno_signed (:3973): low == x, high == y, sign.
+ * chrnum is the caller's chromosome number (the reference maps it to the IIT's
+ * division through its divint crosstable).  site_level: the IIT has donor and
+ * acceptor types (a splice-sites file, gmap.c:3730), else it holds introns.
+ * The callbacks may be called from several threads at once.
+ * gsnapdp_iit_from_intervals builds one over intervals as iit_store writes them
+ * (start..end; start > end is the minus sign, interval.c:22-40). */
+typedef struct gsnapdp_iit {
+  void *user;
+  int32_t site_level, pad;
+  int (*typed)(void *user, int chrnum, uint32_t x, uint32_t y, int type, int sign);
+  int (*low)(void *user, int chrnum, uint32_t x, int sign);
+  int (*high)(void *user, int chrnum, uint32_t x, int sign);
+  int (*exact)(void *user, int chrnum, uint32_t x, uint32_t y, int sign);
+} gsnapdp_iit;
+typedef struct gsnapdp_iit_interval {
+  int32_t chrnum;
+  uint32_t start, end;
+  int32_t type; /* -1 none (an intron), GSNAPDP_DONOR, GSNAPDP_ACCEPTOR */
+} gsnapdp_iit_interval;
+gsnapdp_iit *gsnapdp_iit_from_intervals(const gsnapdp_iit_interval *intervals, int n);
+void gsnapdp_iit_free(gsnapdp_iit *iit);
+/* Host-only: one genome-gap window's known-site record (gsnapdp_ggap_window
+ * above), asked of `iit` exactly where bridge_intron_gap asks
+ * (dynprog.c:3375-3550, 3598-3612).  Writes *len bytes (at most cap; length2L
+ * + length2R + 2 + 4 * known introns) and returns the window's known_mode
+ * (REWARD with novelsplicingp, else SITES or INTRONS), or -1 if cap is short. */
+int gsnapdp_known_site_record(const gsnapdp_iit *iit, int novelsplicingp, int chrnum, uint32_t chrpos,
+                              uint32_t genomiclength, int offset2L, int revoffset2R, int length2L, int length2R,
+                              int cdna_direction, int watsonp, char *rec, int cap, int *len);
+/* Host-only: score_introns' known-site verdicts for `n` introns of paths on
+ * chromosome chrnum (stage3.c:7995-8116): intron[i].known_donor /
+ * known_acceptor from the IIT, asked in the reference's order. */
+int gsnapdp_introns_known(const gsnapdp_iit *iit, int chrnum, uint32_t chrpos, int genomiclength,
+                          int cdna_direction, int watsonp, gsnapdp_intron *introns, int n);
+
 /* -------------------------------------------------- stage-3 intron pass
  * build_pairs_introns (stage3.c:7735-7901) for many paths at once.  Each
  * path's gaps are taken in list order, as the reference's loop takes them:
@@ -511,9 +555,11 @@ int gsnapdp_micro_expand(gsnapdp_ctx *ctx, const gsnapdp_micro_window *w,
  * i.e. the alignment reversed, as insert_gapholders leaves it); each pair
  * carries the fields the pass reads or writes.  The returned list is written
  * in list order; `src` names the input pair (index within its path) that a
- * returned cell holds, -1 for a pair the pass made.  Without a splicing IIT
- * (known_mode NONE).  Genome characters come from the context genome.  Needs
- * the MaxEnt tables when a call has finalp (probability re-runs, microexons). */
+ * returned cell holds, -1 for a pair the pass made.  With a splicing IIT
+ * (`iit`, as Dynprog_setup / Stage3_setup got it) every genome-gap window
+ * carries its known-site record; NULL for none.  Genome characters come from
+ * the context genome.  Needs the MaxEnt tables when a call has finalp
+ * (probability re-runs, microexons). */
 typedef struct gsnapdp_s3_pair {
   int32_t querypos, genomepos, queryjump, genomejump, dynprogindex;
   int32_t src;
@@ -557,13 +603,30 @@ typedef struct gsnapdp_s3_stats {
                          * gap-family round trips (staging, kernels, copies), whole pass */
 } gsnapdp_s3_stats;
 
-/* Runs the pass; pairs_out holds out_cap pairs (2 * (querylength + npairs) +
- * 64 per call always suffices).  Returns 0, or -1 (gsnapdp_last_error) when a
- * batch fails or pairs_out is too small; a path the reference would abort on
- * gets status -1 and nout = 0, and the others still run. */
+/* Runs the pass; pairs_in holds npairs_in pairs and query / query_uc
+ * query_bytes bytes each (every call's path and query must lie inside them);
+ * pairs_out holds out_cap pairs (2 * (querylength + npairs) + 64 per call
+ * always suffices).  Returns 0, or -1 (gsnapdp_last_error) on bad arguments,
+ * when a batch fails or when pairs_out is too small; a path the reference would
+ * abort on gets status -1 and nout = 0, and the others still run.
+ *
+ * The pass keeps two rounds in flight (two cohorts of paths): while one
+ * cohort's windows run on the GPU, the host peels and expands the other's.
+ * The host work runs on a persistent pool of GSNAPDP_S3_THREADS threads
+ * (default min(16, hardware threads)). */
 int gsnapdp_stage3_pass(gsnapdp_ctx *ctx, gsnapdp_s3_call *calls, int ncalls,
-                        const gsnapdp_s3_pair *pairs_in, const char *query, const char *query_uc,
+                        const gsnapdp_s3_pair *pairs_in, int64_t npairs_in, const char *query,
+                        const char *query_uc, size_t query_bytes, const gsnapdp_iit *iit,
                         gsnapdp_s3_pair *pairs_out, int64_t out_cap, gsnapdp_s3_stats *stats);
+
+/* score_introns (stage3.c:7935-8162) on the lists a pass returned: for every
+ * call with status 0, its list reversed into path order (as stage3_compute
+ * reverses path_compute's pairs, :9890-9941), the introns picked on the host
+ * (gsnapdp_path_introns), the IIT's verdicts (NULL for none) and one k_introns
+ * launch for all of them.  scores[i] is call i's (zeros for a failed call). */
+int gsnapdp_stage3_score_introns(gsnapdp_ctx *ctx, const gsnapdp_s3_call *calls, int ncalls,
+                                 const gsnapdp_s3_pair *pairs_out, const gsnapdp_iit *iit,
+                                 gsnapdp_intron_scores *scores);
 
 /* Load the MaxEnt parameter tables (12 x 16384 + 4 x 16 doubles, order in
  * DESIGN.md) into the context.  Must be called before gsnapdp_maxent_*. */

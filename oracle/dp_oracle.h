@@ -133,6 +133,11 @@ double orc_maxent_donor(uint32_t splice_pos, uint32_t chroffset);
 double orc_maxent_acceptor(uint32_t splice_pos, uint32_t chroffset);
 double orc_maxent_antidonor(uint32_t splice_pos, uint32_t chroffset);
 double orc_maxent_antiacceptor(uint32_t splice_pos, uint32_t chroffset);
+/* score_introns (stage3.c:7935-8162): the intron walk and the sums (maxent_oracle.c) */
+int orc_path_introns(const gsnapdp_path_pair *pairs, int npairs, int nullgap, int path, gsnapdp_intron *out,
+                     int cap);
+void orc_score_introns(const gsnapdp_intron_path *paths, int npaths, const gsnapdp_intron *introns,
+                       gsnapdp_intron_scores *out);
 
 /* Batch driver over gsnapdp_window records (same input format as the
  * product ABI).  Writes results[i] (finalscore, counts, status) and the

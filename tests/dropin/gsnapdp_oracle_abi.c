@@ -259,3 +259,15 @@ int gsnapdp_micro_expand(gsnapdp_ctx *c, const gsnapdp_micro_window *w, const gs
 /* the product's internal accessors gsnapdp_stage3.cpp reads */
 const uint32_t *gsnapdp__host_blocks(gsnapdp_ctx *ctx) { return ctx->blocks; }
 size_t gsnapdp__host_nwords(gsnapdp_ctx *ctx) { return ctx->nwords; }
+
+/* score_introns for gsnapdp_stage3_score_introns: the oracle's walk and sums */
+int gsnapdp_path_introns(const gsnapdp_path_pair *pairs, int npairs, int nullgap, int path, gsnapdp_intron *out,
+                         int cap) {
+  return orc_path_introns(pairs, npairs, nullgap, path, out, cap);
+}
+int gsnapdp_score_introns_host(gsnapdp_ctx *ctx, const gsnapdp_intron_path *paths, int npaths,
+                               const gsnapdp_intron *introns, int nintrons, gsnapdp_intron_scores *out) {
+  (void)ctx, (void)nintrons;
+  orc_score_introns(paths, npaths, introns, out);
+  return 0;
+}

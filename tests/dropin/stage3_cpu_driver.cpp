@@ -6,17 +6,21 @@
 // (oracle/Makefile `stage3_cpu`).  tests/test_stage3_cpu.py feeds it the
 // build_pairs_introns calls gmap_trace recorded and compares the lists.
 //
-//   stage3_cpu DIR    reads DIR/{calls,pairs_in,query,query_uc}.bin, DIR/genome.u32,
-//                     writes DIR/{pass_calls,pass_pairs,pass_stats}.bin
+//   stage3_cpu DIR    reads DIR/{calls,pairs_in,query,query_uc}.bin, DIR/genome.u32 and, when
+//                     present, DIR/intervals.bin (gsnapdp_iit_interval: a splicing IIT);
+//                     writes DIR/{pass_calls,pass_pairs,pass_stats}.bin, and with
+//                     --introns DIR/pass_scores.bin (score_introns on the returned lists)
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
 #include "../../include/gsnapdp.h"
 
 static std::string g_err;
+extern double g_s3_exec_seconds;  // stage3_exec_host.cpp
 void gsnapdp__set_err(const std::string& s) { g_err = s; }
 
 template <class T>
@@ -46,6 +50,7 @@ static void spit(const std::string& path, const T* p, size_t n) {
 int main(int argc, char** argv) {
   if (argc < 2) return 2;
   const std::string d = argv[1];
+  const bool introns = argc > 2 && std::string(argv[2]) == "--introns";
   std::vector<gsnapdp_s3_call> calls = slurp<gsnapdp_s3_call>(d + "/calls.bin");
   std::vector<gsnapdp_s3_pair> in = slurp<gsnapdp_s3_pair>(d + "/pairs_in.bin");
   std::vector<char> q = slurp<char>(d + "/query.bin"), qu = slurp<char>(d + "/query_uc.bin");
@@ -57,11 +62,28 @@ int main(int argc, char** argv) {
   for (const gsnapdp_s3_call& c : calls) cap += 2 * ((int64_t)c.querylength + c.npairs) + 64;
   std::vector<gsnapdp_s3_pair> out((size_t)cap);
   gsnapdp_s3_stats st;
-  if (gsnapdp_stage3_pass(ctx, calls.data(), (int)calls.size(), in.data(), q.data(), qu.data(), out.data(), cap,
-                          &st)) {
+  gsnapdp_iit* iit = nullptr;
+  if (FILE* f = fopen((d + "/intervals.bin").c_str(), "rb")) {
+    fclose(f);
+    std::vector<gsnapdp_iit_interval> iv = slurp<gsnapdp_iit_interval>(d + "/intervals.bin");
+    if (!(iit = gsnapdp_iit_from_intervals(iv.data(), (int)iv.size()))) return 4;
+  }
+  if (gsnapdp_stage3_pass(ctx, calls.data(), (int)calls.size(), in.data(), (int64_t)in.size(), q.data(),
+                          qu.data(), std::min(q.size(), qu.size()), iit, out.data(), cap, &st)) {
     fprintf(stderr, "gsnapdp_stage3_pass: %s\n", g_err.c_str());
     return 5;
   }
+  if (introns) {
+    std::vector<gsnapdp_intron_scores> sc(calls.size());
+    if (gsnapdp_stage3_score_introns(ctx, calls.data(), (int)calls.size(), out.data(), iit, sc.data())) {
+      fprintf(stderr, "gsnapdp_stage3_score_introns: %s\n", g_err.c_str());
+      return 6;
+    }
+    spit(d + "/pass_scores.bin", sc.data(), sc.size());
+  }
+  gsnapdp_iit_free(iit);
+  fprintf(stderr, "pass %.4f s (host %.4f, waits %.4f), batches served by the oracle %.4f s, %d rounds\n",
+          st.seconds[2], st.seconds[0], st.seconds[1], g_s3_exec_seconds, st.rounds);
   int64_t nout = 0;
   for (const gsnapdp_s3_call& c : calls) nout += c.nout;
   spit(d + "/pass_calls.bin", calls.data(), calls.size());

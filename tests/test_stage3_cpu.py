@@ -45,6 +45,42 @@ def check_pass(calls, out, want_calls, want_out, what):
             raise AssertionError("%s: call %d, cell %d of %d: got %s want %s" % (what, i, k, len(exp), got[k], exp[k]))
 
 
+def run_stage3_cpu(d, z, calls, pin, q, qu, intervals=None, introns=False):
+    """stage3_cpu (ASan + UBSan) on the calls; returns (calls, lists, stats[, scores])"""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "stage3_cpu"])
+    calls.tofile(os.path.join(d, "calls.bin"))
+    pin.tofile(os.path.join(d, "pairs_in.bin"))
+    q.tofile(os.path.join(d, "query.bin"))
+    qu.tofile(os.path.join(d, "query_uc.bin"))
+    z["blocks"].astype("<u4").tofile(os.path.join(d, "genome.u32"))
+    if intervals is not None:
+        intervals.tofile(os.path.join(d, "intervals.bin"))
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               GSNAPDP_MAXENT_TABLES=os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin"))
+    p = subprocess.run([os.path.join(ROOT, "oracle", "_build", "stage3_cpu"), d] + (["--introns"] if introns else []),
+                       env=env, capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, "stage3_cpu failed (%d):\n%s" % (p.returncode, p.stderr[-6000:])
+    assert "runtime error" not in p.stderr, p.stderr[-6000:]
+    got_calls = np.fromfile(os.path.join(d, "pass_calls.bin"), dtype=S3_CALL)
+    got = np.fromfile(os.path.join(d, "pass_pairs.bin"), dtype=S3_PAIR)
+    st = np.fromfile(os.path.join(d, "pass_stats.bin"), dtype=S3_STATS)[0]
+    if introns:
+        from gsnapdp.records import INTRON_SCORES
+        return got_calls, got, st, np.fromfile(os.path.join(d, "pass_scores.bin"), dtype=INTRON_SCORES)
+    return got_calls, got, st
+
+
+def test_stage3_pass_cpu_two_cohorts(golden_dir, tmp_path):
+    """enough paths (the synthetic calls x3) for the pass's two cohorts in flight"""
+    z = np.load(os.path.join(golden_dir, "gmap_synth_stage3.npz"), allow_pickle=False)
+    calls, pin, q, qu, want = W.stage3_calls(z, 3)
+    assert len(calls) >= 256
+    got_calls, got, st = run_stage3_cpu(str(tmp_path), z, calls, pin, q, qu)
+    check_pass(got_calls, got, calls, want, "x3")
+    assert st["failed"] == 0 and st["undefined"] == 0
+
+
 @pytest.mark.parametrize("name", NAMES)
 def test_stage3_pass_cpu_matches_reference(golden_dir, tmp_path, name):
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "stage3_cpu"])
