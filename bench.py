@@ -336,7 +336,7 @@ def measure_micro(genome, n, steps, warmup, dev, with_cpu):
     return out
 
 
-def measure_stage3(copies=64, reps=3):
+def measure_stage3(paths=7424, reps=3):
     """Side line: the stage-3 intron pass (gsnapdp_stage3_pass, build_pairs_introns
     over many paths) on the recorded calls of the reference's gmap
     (tests/golden/gmap_synth_stage3.npz) replicated `copies` times into one pass;
@@ -345,6 +345,7 @@ def measure_stage3(copies=64, reps=3):
     DP included, one thread; recorded by oracle/gmap_trace in the dev container,
     not on this host)."""
     z = np.load(os.path.join(ROOT, "tests", "golden", "gmap_synth_stage3.npz"), allow_pickle=False)
+    copies = max(1, paths // len(z["calls"]))
     calls, pin, q, qu, want = W.stage3_calls(z, copies)
     ctx = Context(z["blocks"])
     ctx.stage3_pass(calls[:64], pin, q, qu)  # warm-up

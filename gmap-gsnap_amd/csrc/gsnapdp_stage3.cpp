@@ -156,6 +156,8 @@ struct Path {
   // when a Dynprog_genome_gap early return leaves them unwritten.
   int finalscore = 0, nmatches = 0, nmismatches = 0, nopens = 0, nindels = 0, exonhead = 0;
   int new_left = 0, new_right = 0, introntype = 0;
+  bool newpos_set = false;  // new_left / new_right written in this traverse_genome_gap call
+  bool ub = false;          // the counters took the reference's uninitialised locals
   double left_prob = 0.0, right_prob = 0.0;
   int gappairs = -1;
   int undefined = 0;  // probability re-runs with no qualifying candidate
@@ -547,6 +549,29 @@ void fail(Path& k, const std::string& why) {
   k.req.fam = F_NONE;
 }
 
+// GSNAPDP_S3_PROFILE=1: where a pass's host time goes (stderr at the end of the pass)
+struct Prof {
+  bool on = getenv("GSNAPDP_S3_PROFILE") != nullptr;
+  std::atomic<int64_t> expand_ns[F_N] = {{0}, {0}, {0}, {0}}, resume_ns{0};
+  double init = 0, pack = 0, copy = 0, submit = 0, wait = 0, resume = 0, output = 0;
+};
+Prof& prof() {
+  static Prof p;
+  return p;
+}
+struct Tic {  // adds its lifetime to an atomic nanosecond counter when profiling
+  std::atomic<int64_t>* acc;
+  std::chrono::steady_clock::time_point t0;
+  explicit Tic(std::atomic<int64_t>& a) : acc(prof().on ? &a : nullptr) {
+    if (acc) t0 = std::chrono::steady_clock::now();
+  }
+  ~Tic() {
+    if (acc)
+      acc->fetch_add(
+          std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+  }
+};
+
 // the pairs a family's op stream expands into (one buffer per host thread)
 std::vector<gsnapdp_pair>& expand_buf(size_t n) {
   thread_local std::vector<gsnapdp_pair> v;
@@ -600,6 +625,7 @@ bool done_single(Pass& P, Path& k, int* list) {
   }
   std::vector<gsnapdp_pair>& v = expand_buf((size_t)R.cap + 8);
   int fs = 0;
+  Tic tic(prof().expand_ns[F_GAP]);
   const int n = gsnapdp_expand(P.ctx, &R.w, &r, R.ops, R.q.data(), R.qu.data(), v.data(), (int)v.size(), &fs);
   if (n < 0 || n > (int)v.size()) {
     fail(k, "gsnapdp_expand failed");
@@ -639,6 +665,7 @@ bool done_genome(Pass& P, Path& k, int* finalscore, int* nmismatches, double* lp
     if (w.maxlength1 == -1) {  // too long (:4898-4927)
       k.new_left = r.new_leftgenomepos;
       k.new_right = r.new_rightgenomepos;
+      k.newpos_set = true;
       k.exonhead = r.exonhead;
     }
     return true;
@@ -654,6 +681,7 @@ bool done_genome(Pass& P, Path& k, int* finalscore, int* nmismatches, double* lp
   if (!t.bridge_accepted) return true;
   k.new_left = r.new_leftgenomepos;
   k.new_right = r.new_rightgenomepos;
+  k.newpos_set = true;
   k.exonhead = r.exonhead;
   *lp = r.left_prob;
   *rp = r.right_prob;
@@ -663,6 +691,7 @@ bool done_genome(Pass& P, Path& k, int* finalscore, int* nmismatches, double* lp
   k.nindels = r.nindels;
   if (r.returned_null) return true;
   std::vector<gsnapdp_pair>& v = expand_buf((size_t)R.cap + 8);
+  Tic tic(prof().expand_ns[F_GGAP]);
   const int n = gsnapdp_ggap_expand(P.ctx, &w, &r, &t, R.ops, R.q.data(), R.qu.data(), v.data(), (int)v.size());
   if (n < 0 || n > (int)v.size()) {
     fail(k, "gsnapdp_ggap_expand failed");
@@ -690,6 +719,7 @@ bool done_cdna(Pass& P, Path& k, int* list) {
   if (r.incompletep) k.incompletep = true;  // only ever set to true (:4756)
   if (r.returned_null) return true;
   std::vector<gsnapdp_pair>& v = expand_buf((size_t)R.cap + 32);
+  Tic tic(prof().expand_ns[F_CGAP]);
   const int n = gsnapdp_cgap_expand(P.ctx, &R.cw, &r, R.ops, R.q.data(), R.qu.data(), nullptr, v.data(),
                                     (int)v.size());
   if (n < 0 || n > (int)v.size()) {
@@ -715,6 +745,7 @@ bool done_micro(Pass& P, Path& k, double* prob2, double* prob3, int* microintron
   if (!r.found) return true;
   const int L1 = R.mw.length1 > 0 ? R.mw.length1 : 0;
   std::vector<gsnapdp_pair>& v = expand_buf((size_t)L1 + 4);
+  Tic tic(prof().expand_ns[F_MICRO]);
   const int n = gsnapdp_micro_expand(P.ctx, &R.mw, &r, R.q.data(), R.qu.data(), v.data(), (int)v.size());
   if (n <= 0 || n > (int)v.size()) {
     fail(k, "gsnapdp_micro_expand failed");
@@ -842,6 +873,7 @@ void cdna_done(Pass& P, Path& k) {
 bool genome_start(Pass& P, Path& k) {
   const gsnapdp_s3_call& c = *k.c;
   bool mr = false, ml = false;
+  k.newpos_set = false;  // a new traverse_genome_gap frame
   gap_bounds(k);
   const bool through = !repeel_prior(k);
   if (k.querydp5 != k.querydp3 + 1) {
@@ -877,6 +909,12 @@ bool genome_start(Pass& P, Path& k) {
 }
 
 void genome_account(Path& k) {
+  // traverse_genome_gap's new_left/rightgenomepos are plain locals: when no
+  // Dynprog_genome_gap of this traverse_genome_gap call has written them, the
+  // reference adds whatever its stack slots hold (a previous call's value, or
+  // garbage that differs between runs of the same input); the pass keeps the
+  // path's previous values there and reports the counters as undefined
+  if (!k.newpos_set) k.ub = true;
   if (k.introntype == NONINTRON) {
     k.nnonintrons += 1;
     k.nonintronlen += k.new_right - k.new_left - 1;
@@ -1103,6 +1141,8 @@ struct Cohort {
 // submits them.  Returns 1 when a round was submitted, 0 when no path waits,
 // -1 on an error.
 int pack_submit(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
   size_t nwait = 0;
   for (int f = 0; f < F_N; f++) C.fam[f].clear();
   for (Path* k : C.paths)
@@ -1166,6 +1206,7 @@ int pack_submit(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
   memset(in + L.qu + q, 0, 8);
   int base[F_N + 1] = {0};
   for (int f = 0; f < F_N; f++) base[f + 1] = base[f] + L.n[f];
+  const auto t1 = clock::now();
   Workers::get().run((int)C.all.size(), 64, [&](int j) {
     Path& k = *C.all[(size_t)j];
     const Req& R = k.req;
@@ -1197,7 +1238,14 @@ int pack_submit(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
       memcpy(in + L.w[f] + (size_t)i * sizeof(w), &w, sizeof(w));
     }
   });
+  const auto t2 = clock::now();
   if (X.submit(C.slot, L)) return -1;
+  if (prof().on) {
+    const auto t3 = clock::now();
+    prof().pack += std::chrono::duration<double>(t1 - t0).count();
+    prof().copy += std::chrono::duration<double>(t2 - t1).count();
+    prof().submit += std::chrono::duration<double>(t3 - t2).count();
+  }
   for (int f = 0; f < F_N; f++)
     if (L.n[f]) {
       P.st.windows[f] += L.n[f];
@@ -1232,6 +1280,7 @@ void unpack_resume(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
     }
     R.ops = off ? (const uint32_t*)(out + L.ops[f]) + off[i] : nullptr;
     R.fam = F_NONE;
+    Tic tic(prof().resume_ns);
     resume(P, k);
   });
 }
@@ -1282,6 +1331,12 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     k.intronlen = c.in_intronlen;
     k.nonintronlen = c.in_nonintronlen;
   }
+  Prof& pf = prof();
+  if (pf.on) {
+    for (int f = 0; f < F_N; f++) pf.expand_ns[f] = 0;
+    pf.resume_ns = 0;
+    pf.init = pf.pack = pf.copy = pf.submit = pf.wait = pf.resume = pf.output = 0;
+  }
   pool.run(ncalls, 16, [&](int i) {
     Path& k = paths[(size_t)i];
     const gsnapdp_s3_call& c = *k.c;
@@ -1297,6 +1352,8 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
   });
   // two cohorts (alternate paths, so both get a similar mix) when there are
   // enough paths for each round to be worth a batch of its own
+  const auto t_init = clock::now();
+  pf.init = std::chrono::duration<double>(t_init - t_start).count();
   const int ncoh = ncalls >= 256 ? 2 : 1;
   Cohort coh[2];
   for (int i = 0; i < ncalls; i++) coh[i % ncoh].paths.push_back(&paths[(size_t)i]);
@@ -1317,8 +1374,10 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
         rc = -1;
         break;
       }
-      wait_s += std::chrono::duration<double>(clock::now() - t0).count();
+      const auto t1 = clock::now();
+      wait_s += std::chrono::duration<double>(t1 - t0).count();
       unpack_resume(P, *X, C);
+      pf.resume += std::chrono::duration<double>(clock::now() - t1).count();
       const int s = pack_submit(P, *X, C);
       if (s < 0) rc = -1;
       C.inflight = s == 1;
@@ -1331,6 +1390,7 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     return -1;
   }
   gsnapdp::s3_exec_release(ctx, X);
+  const auto t_out = clock::now();
   // the returned lists, each path's at its running offset (lengths first,
   // then the copies by the workers)
   std::vector<int64_t> first((size_t)ncalls + 1, 0);
@@ -1362,12 +1422,23 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     c.out_nonintronlen = k.nonintronlen;
     c.shiftp = k.shiftp ? 1 : 0;
     c.incompletep = k.incompletep ? 1 : 0;
+    c.ub = k.ub ? GSNAPDP_S3_UB_INTRONLEN : 0;
   });
   for (Path& k : paths) {
     P.st.undefined += k.undefined;
     if (k.failed) P.st.failed++;
   }
   const double total = std::chrono::duration<double>(clock::now() - t_start).count();
+  if (pf.on) {
+    pf.output = std::chrono::duration<double>(clock::now() - t_out).count();
+    fprintf(stderr,
+            "gsnapdp_stage3_pass profile: %d paths, %d rounds, total %.4f s: init %.4f, pack %.4f, copy %.4f, "
+            "submit %.4f, wait %.4f, resume %.4f (thread-s: resume %.4f; expand gap %.4f ggap %.4f cgap %.4f "
+            "micro %.4f), output %.4f\n",
+            ncalls, P.st.rounds, total, pf.init, pf.pack, pf.copy, pf.submit, wait_s, pf.resume, pf.resume_ns * 1e-9,
+            pf.expand_ns[0] * 1e-9, pf.expand_ns[1] * 1e-9, pf.expand_ns[2] * 1e-9, pf.expand_ns[3] * 1e-9,
+            pf.output);
+  }
   P.st.seconds[0] = total - wait_s;
   P.st.seconds[1] = wait_s;
   P.st.seconds[2] = total;

@@ -130,6 +130,7 @@ S3_PAIR = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("queryjump", "<i
                     ("flags", "u1")])
 assert S3_PAIR.itemsize == 28
 S3_GAPP, S3_KNOWNGAPP, S3_DISALLOWED = 1, 2, 4
+S3_UB_INTRONLEN = 1  # gsnapdp_s3_call.ub: intronlen / nonintronlen took the reference's uninitialised locals
 S3_CALL = np.dtype([(n, "<i4") for n in "first_pair npairs first_out nout qpos querylength".split()] +
                    [(n, "<u4") for n in "chroffset chrhigh chrpos".split()] +
                    [(n, "<i4") for n in ("chrnum genomiclength cdna_direction watsonp jump_late_p finalp "
@@ -139,7 +140,7 @@ S3_CALL = np.dtype([(n, "<i4") for n in "first_pair npairs first_out nout qpos q
                    [(n, "<i4") for n in ("in_minor in_major in_nintrons in_nnonintrons in_intronlen in_nonintronlen "
                                          "out_minor out_major out_nintrons out_nnonintrons out_intronlen "
                                          "out_nonintronlen shiftp incompletep novelsplicingp splicingp "
-                                         "status pad").split()] +
+                                         "status ub").split()] +
                    [("ref_seconds", "<f8")])
 assert S3_CALL.itemsize == 200
 S3_STATS = np.dtype([("rounds", "<i4"), ("windows", "<i4", 4), ("batches", "<i4", 4), ("undefined", "<i4"),

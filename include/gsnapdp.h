@@ -567,6 +567,7 @@ typedef struct gsnapdp_s3_pair {
   uint8_t flags;  /* GSNAPDP_S3_GAPP | GSNAPDP_S3_KNOWNGAPP | GSNAPDP_S3_DISALLOWED */
 } gsnapdp_s3_pair;
 enum { GSNAPDP_S3_GAPP = 1, GSNAPDP_S3_KNOWNGAPP = 2, GSNAPDP_S3_DISALLOWED = 4 };
+enum { GSNAPDP_S3_UB_INTRONLEN = 1 };
 
 /* One build_pairs_introns call: its arguments (the query bytes at query[qpos],
  * querylength of them; the three Dynprog_T workspaces' limits, L, M, R), its
@@ -587,7 +588,12 @@ typedef struct gsnapdp_s3_call {
   int32_t out_minor, out_major, out_nintrons, out_nnonintrons, out_intronlen, out_nonintronlen;
   int32_t shiftp, incompletep;
   int32_t novelsplicingp, splicingp;  /* Stage3_setup's module flags (stage3.c:238-239) */
-  int32_t status, pad;                /* written: 0, or -1 (the path is left out, nout = 0) */
+  int32_t status;                     /* written: 0, or -1 (the path is left out, nout = 0) */
+  int32_t ub;                         /* written: GSNAPDP_S3_UB_INTRONLEN when out_intronlen /
+                                       * out_nonintronlen took traverse_genome_gap's uninitialised
+                                       * new_left/rightgenomepos (stage3.c:5651; an early-returning
+                                       * Dynprog_genome_gap leaves them unwritten): the reference's own
+                                       * value is stack garbage there, and differs between runs */
   double ref_seconds;                 /* golden records: the reference's own call time (ignored) */
 } gsnapdp_s3_call;
 

@@ -554,7 +554,148 @@ def gmap_trace_case(seed: int = 7) -> None:
     with tempfile.TemporaryDirectory() as d:
         W.write_fasta(os.path.join(d, "g.fa"), [("synthchr", g)])
         W.write_fasta(os.path.join(d, "q.fa"), q)
-        trace_gmap_run("gmap_synth", os.path.join(d, "g.fa"), os.path.join(d, "q.fa"), d, stage3_every=4)
+        trace_gmap_run("gmap_synth", os.path.join(d, "g.fa"), os.path.join(d, "q.fa"), d, stage3_every=1)
+
+
+def site_intervals(sic, sip, rng, site_level: bool) -> np.ndarray:
+    """A splicing IIT around the introns of final alignments (every score_introns
+    call gmap made): their donor / acceptor sites (site_level) or the introns
+    themselves, at the coordinates the reference queries them (score_introns
+    stage3.c:7995-8116; bridge_intron_gap dynprog.c:3375-3612), with about a
+    fifth left out and decoys added -- shifted by 1-4 nt, of the wrong type or
+    of the wrong sign -- so that the known-site paths change results.
+    IIT_INTERVAL records (chrnum, start, end, type)."""
+    from gsnapdp import path_introns
+    from gsnapdp.records import IIT_INTERVAL, PATH_PAIR
+    seen, out = set(), []
+    for c in sic:
+        d = int(c["cdna_direction"])
+        if d not in (1, -1):
+            continue
+        assert c["watsonp"] == 1, "gmap -g aligns on the plus strand only"
+        x = sip[int(c["first_pair"]):int(c["first_pair"]) + int(c["npairs"])]
+        pp = np.zeros(x.size, PATH_PAIR)
+        for f in ("genomepos", "queryjump", "genomejump", "gapp", "knowngapp", "comp"):
+            pp[f] = x[f]
+        for t in path_introns(pp, int(c["nullgap"])):
+            key = (int(c["chrnum"]), int(c["chrpos"]), d, int(t["left_genomepos"]), int(t["right_genomepos"]))
+            if key not in seen:
+                seen.add(key)
+    for chrnum, chrpos, d, left, right in sorted(seen):
+        lpos, rpos = chrpos + left + 1, chrpos + right
+        if site_level:
+            sign = d  # watsonp: +1 for a sense cDNA, -1 for an antisense one
+            sites = [(lpos, 0 if d > 0 else 1), (rpos, 1 if d > 0 else 0)]  # (pos, donor 0 / acceptor 1)
+            for p, typ in sites:
+                if rng.random() < 0.8:
+                    out.append((chrnum, p, p + 1, typ) if sign > 0 else (chrnum, p + 1, p, typ))
+                if rng.random() < 0.3:
+                    q = p + int(rng.choice([-4, -3, -2, -1, 1, 2, 3, 4]))
+                    out.append((chrnum, q, q + 1, typ) if sign > 0 else (chrnum, q + 1, q, typ))
+                if rng.random() < 0.1:
+                    out.append((chrnum, p, p + 1, 1 - typ) if sign > 0 else (chrnum, p + 1, p, 1 - typ))
+                if rng.random() < 0.1:
+                    out.append((chrnum, p + 1, p, typ) if sign > 0 else (chrnum, p, p + 1, typ))
+        else:
+            lo, hi = lpos, rpos + 1
+            variants = []
+            if rng.random() < 0.8:
+                variants.append((lo, hi, d))
+            if rng.random() < 0.3:
+                variants.append((lo + int(rng.choice([-3, -2, -1, 1, 2, 3])), hi, d))
+            if rng.random() < 0.3:
+                variants.append((lo, hi + int(rng.choice([-3, -2, -1, 1, 2, 3])), d))
+            if rng.random() < 0.1:
+                variants.append((lo, hi, -d))
+            for a, b, sg in variants:
+                out.append((chrnum, a, b, -1) if sg > 0 else (chrnum, b, a, -1))
+    return np.array(out, dtype=IIT_INTERVAL)
+
+
+def iit_text(iv: np.ndarray, div: str) -> str:
+    """iit_store FASTA input (">label div:start..end [type]") for IIT_INTERVAL records"""
+    names = {-1: "", 0: " donor", 1: " acceptor"}
+    return "".join(">s%d %s:%d..%d%s\n" % (i, div, int(x["start"]), int(x["end"]), names[int(x["type"])])
+                   for i, x in enumerate(iv))
+
+
+def gmap_cins_case(seed: int = 21, ngenes: int = 60, genome_len: int = 500_000) -> None:
+    """build_pairs_introns calls whose paths hold cDNA gaps, and the same calls
+    under a splicing IIT.
+
+    gmap_trace on synthetic spliced cDNAs with 11-60 nt query-side insertions
+    (workload.synthetic_transcripts(cins=...)), so that stage 2 leaves gaps with
+    queryjump > genomejump + EXTRAQUERYGAP and the pass takes traverse_cdna_gap
+    (stage3.c:5518-5627).  First the reference's own build_pairs_introns is
+    replayed over every recorded call (oracle/s3_replay.c) and must give gmap's
+    lists byte for byte; then
+    * gmap_cins_stage3: the recorded calls whose paths hold a cDNA gap, the
+      smallest first, until ~300 such gaps are in;
+    * gmap_cins_iit_{sites_novel,sites,introns}: those calls replayed through the
+      reference with a splicing IIT (s3_replay --iit: Dynprog_setup and
+      Stage3_setup get it as gmap.c:3283-3302, 3721-3837 hand it over; `gmap -s`
+      itself reads an IIT only for a genome database, which is out of scope),
+      site-level with novel splicing (known-site rewards), site-level without
+      (both chosen sites must be known) and intron-level without (the
+      constrained known-intron bridge), plus score_introns on every returned
+      list (s3_replay --si)."""
+    g, qs = W.synthetic_transcripts(seed=seed, ngenes=ngenes, genome_len=genome_len, cins=0.35)
+    rng = np.random.default_rng(seed + 100)
+    with tempfile.TemporaryDirectory() as d:
+        W.write_fasta(os.path.join(d, "g.fa"), [("synthchr", g)])
+        W.write_fasta(os.path.join(d, "q.fa"), qs)
+        env = dict(os.environ, GMAP_TRACE_DIR=os.path.join(d, "trace"))
+        subprocess.run([GMAP_TRACE, "-A", "-g", os.path.join(d, "g.fa"), os.path.join(d, "q.fa")], env=env,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True)
+        blocks = np.fromfile(os.path.join(d, "trace", "dp", "genome.u32"), dtype="<u4")
+        c, pi, po, q, qu = stage3_trace(os.path.join(d, "trace", "bpi"))
+        sic = np.fromfile(os.path.join(d, "trace", "si", "paths.bin"), dtype=SI_CALL)
+        sip = np.fromfile(os.path.join(d, "trace", "si", "pairs.bin"), dtype=SI_PAIR)
+    rc, rp = s3_replay(blocks, c, pi, q, qu)
+    for f in ("first_out", "nout", "out_minor", "out_major", "out_nintrons", "out_nnonintrons", "shiftp",
+              "incompletep"):
+        assert np.array_equal(rc[f], c[f]), f
+    assert rp.tobytes() == po.tobytes(), "s3_replay differs from the lists gmap recorded"
+    # intronlen / nonintronlen may take traverse_genome_gap's uninitialised locals
+    # (stage3.c:5651): where gmap's and the replay's values differ, the
+    # reference's own value is stack garbage (gsnapdp_s3_call.ub)
+    ub_ref = ((rc["out_intronlen"] != c["out_intronlen"]) |
+              (rc["out_nonintronlen"] != c["out_nonintronlen"])).astype(np.int32)
+    gp = (pi["flags"] & 1) != 0
+    cd = gp & (pi["queryjump"] > pi["genomejump"] + 10) & (pi["queryjump"] <= 600)
+    owner = np.repeat(np.arange(c.size), c["npairs"])
+    per = np.bincount(owner[cd], minlength=c.size)
+    order = [int(i) for i in np.argsort(c["npairs"], kind="stable") if per[i] > 0]
+    pick, ncd = [], 0
+    for i in order:
+        pick.append(i)
+        ncd += int(per[i])
+        if ncd >= 300:
+            break
+    pick = np.array(sorted(pick))
+    sel = c[pick]
+    dd = stage3_pack(sel, pi, po, q, qu)
+    np.savez_compressed(os.path.join(OUT, "gmap_cins_stage3.npz"), blocks=blocks, ncalls_traced=np.int32(c.size),
+                        cdna_gaps=np.int32(ncd), ub_ref=ub_ref[pick], **dd)
+    print("gmap_cins_stage3: %d of %d calls, %d cDNA gaps in their paths, %d path pairs, %d new pairs; "
+          "%d calls (%d picked) whose intron-length counters are stack garbage in the reference" %
+          (sel.size, c.size, ncd, dd["pairs_in"].size, dd["out_new"].size, int(ub_ref.sum()), int(ub_ref[pick].sum())))
+    for name, site_level, novel in (("sites_novel", True, 1), ("sites", True, 0), ("introns", False, 0)):
+        iv = site_intervals(sic, sip, rng, site_level)
+        cc, ppi, qq, qqu = dd["calls"], dd["pairs_in"], dd["query"], dd["query_uc"]
+        r_c, r_p, s_c, s_p = s3_replay(blocks, cc, ppi, qq, qqu, iit_text(iv, "synthchr"), "synthchr", novel, si=True)
+        kd = stage3_pack(r_c, ppi, r_p, qq, qqu)
+        flags = kd["out_flags"]
+        np.savez_compressed(os.path.join(OUT, "gmap_cins_iit_%s.npz" % name), blocks=blocks, intervals=iv,
+                            novelsplicingp=np.int32(novel), si_calls=s_c, si_pairs=s_p, **kd)
+        print("gmap_cins_iit_%s: %d calls, %d intervals, %d new pairs, %d disallowed cells (%d new), "
+              "lists differing from the no-IIT run: %d" %
+              (name, r_c.size, iv.size, kd["out_new"].size, int(((flags & 4) != 0).sum()),
+               int(((flags & 4) != 0)[kd["out_src"] < 0].sum()),
+               sum(1 for a, b in zip(np.split(r_p, np.cumsum(r_c["nout"])[:-1]),
+                                     np.split(po[np.concatenate([np.arange(x["first_out"], x["first_out"] + x["nout"])
+                                                                 for x in sel])],
+                                              np.cumsum(sel["nout"])[:-1])) if a.tobytes() != b.tobytes())))
 
 
 def gmap_her2_case() -> None:
@@ -568,25 +709,17 @@ def gmap_her2_case() -> None:
             assert out == f.read(), "gmap_trace output differs from align.test.ok"
 
 
-def stage3_golden(prefix: str, t: str, blocks: np.ndarray, every: int) -> None:
-    """Every `every`-th build_pairs_introns call gmap made (stage3.c:7735-7901):
-    its arguments, the path it was given and the list it returned, stored
-    compactly: a returned cell that is an input pair keeps only the input's
-    index (src) and its flags (disallowedp is the one field the pass may change
-    on an input pair, stage3.c:5873-5880); the pairs the call made are stored in
-    full (out_new, in list order)."""
-    sys.path.insert(0, os.path.join(HERE, "..", "gmap-gsnap_amd"))
-    from gsnapdp.records import S3_CALL, S3_PAIR
-    c = np.fromfile(os.path.join(t, "calls.bin"), dtype=S3_CALL)
-    pi = np.fromfile(os.path.join(t, "pairs_in.bin"), dtype=S3_PAIR)
-    po = np.fromfile(os.path.join(t, "pairs_out.bin"), dtype=S3_PAIR)
-    q = np.fromfile(os.path.join(t, "query.bin"), dtype=np.uint8)
-    qu = np.fromfile(os.path.join(t, "query_uc.bin"), dtype=np.uint8)
-    assert c.size > 0 and pi.size == int(c["npairs"].sum()) and po.size == int(c["nout"].sum())
-    sel = c[::every].copy()
+def stage3_pack(c, pi, po, q, qu) -> dict:
+    """Compact storage of build_pairs_introns calls (stage3.c:7735-7901): their
+    arguments, the path each was given and the list it returned.  A returned
+    cell that is an input pair keeps only the input's index (src) and its flags
+    (disallowedp is the one field the pass may change on an input pair,
+    stage3.c:5873-5880); the pairs the call made are stored in full (out_new,
+    in list order).  Calls, paths and query bytes are renumbered compactly."""
+    sel = c.copy()
     PI, PO, Q, QU = [], [], [], []
     a = b = e = 0
-    for i, x in enumerate(c[::every]):
+    for i, x in enumerate(c):
         inp = pi[x["first_pair"]:x["first_pair"] + x["npairs"]]
         out = po[x["first_out"]:x["first_out"] + x["nout"]]
         kept = out[out["src"] >= 0]
@@ -601,13 +734,65 @@ def stage3_golden(prefix: str, t: str, blocks: np.ndarray, every: int) -> None:
         sel[i]["first_pair"], sel[i]["first_out"], sel[i]["qpos"] = a, b, e
         a, b, e = a + int(x["npairs"]), b + int(x["nout"]), e + n
     PO = np.concatenate(PO)
-    np.savez_compressed(os.path.join(OUT, prefix + "_stage3.npz"), blocks=blocks, calls=sel,
-                        pairs_in=np.concatenate(PI), out_src=PO["src"], out_flags=PO["flags"],
-                        out_new=PO[PO["src"] < 0], query=np.concatenate(Q), query_uc=np.concatenate(QU),
-                        every=np.int32(every), ncalls_traced=np.int32(c.size))
+    return dict(calls=sel, pairs_in=np.concatenate(PI), out_src=PO["src"], out_flags=PO["flags"],
+                out_new=PO[PO["src"] < 0], query=np.concatenate(Q), query_uc=np.concatenate(QU))
+
+
+def stage3_trace(t: str):
+    """(calls, pairs_in, pairs_out, query, query_uc) of a gmap_trace bpi directory"""
+    from gsnapdp.records import S3_CALL, S3_PAIR
+    c = np.fromfile(os.path.join(t, "calls.bin"), dtype=S3_CALL)
+    pi = np.fromfile(os.path.join(t, "pairs_in.bin"), dtype=S3_PAIR)
+    po = np.fromfile(os.path.join(t, "pairs_out.bin"), dtype=S3_PAIR)
+    q = np.fromfile(os.path.join(t, "query.bin"), dtype=np.uint8)
+    qu = np.fromfile(os.path.join(t, "query_uc.bin"), dtype=np.uint8)
+    assert c.size > 0 and pi.size == int(c["npairs"].sum()) and po.size == int(c["nout"].sum())
+    return c, pi, po, q, qu
+
+
+def stage3_golden(prefix: str, t: str, blocks: np.ndarray, every: int) -> None:
+    """Every `every`-th build_pairs_introns call gmap made (stage3_pack)."""
+    c, pi, po, q, qu = stage3_trace(t)
+    d = stage3_pack(c[::every], pi, po, q, qu)
+    np.savez_compressed(os.path.join(OUT, prefix + "_stage3.npz"), blocks=blocks, every=np.int32(every),
+                        ncalls_traced=np.int32(c.size), **d)
+    sel = d["calls"]
     print("%s_stage3: %d of %d build_pairs_introns calls (%d final), %d path pairs, %d new pairs, "
-          "reference %.3f s" % (prefix, sel.size, c.size, int(sel["finalp"].sum()), a, int((PO["src"] < 0).sum()),
-                                float(sel["ref_seconds"].sum())))
+          "reference %.3f s" % (prefix, sel.size, c.size, int(sel["finalp"].sum()), d["pairs_in"].size,
+                                d["out_new"].size, float(sel["ref_seconds"].sum())))
+
+
+S3R = os.path.join(HERE, "_ref", "s3_replay")
+
+
+def s3_replay(blocks, c, pi, q, qu, iit_text=None, div="synthchr", novel=1, si=False):
+    """The reference's build_pairs_introns (and with `si` its score_introns on
+    each returned list) over the calls, through oracle/_ref/s3_replay; with
+    `iit_text` (iit_store input) a splicing IIT set up as gmap sets it.
+    Returns (calls, pairs_out[, si_calls, si_pairs])."""
+    from gsnapdp.records import S3_CALL, S3_PAIR
+    with tempfile.TemporaryDirectory() as d:
+        blocks.astype("<u4").tofile(os.path.join(d, "genome.u32"))
+        c.tofile(os.path.join(d, "calls.bin"))
+        pi.tofile(os.path.join(d, "pairs_in.bin"))
+        q.tofile(os.path.join(d, "query.bin"))
+        qu.tofile(os.path.join(d, "query_uc.bin"))
+        args = [S3R, d]
+        if iit_text is not None:
+            with open(os.path.join(d, "sites.txt"), "w") as f:
+                f.write(iit_text)
+            subprocess.check_call([os.path.join(HERE, "_ref", "iit_store"), "-o", os.path.join(d, "sites"),
+                                   os.path.join(d, "sites.txt")], stdout=subprocess.DEVNULL)
+            args += ["--iit", os.path.join(d, "sites.iit"), div, str(int(novel))]
+        if si:
+            args.append("--si")
+        subprocess.check_call(args)
+        rc = np.fromfile(os.path.join(d, "replay_calls.bin"), dtype=S3_CALL)
+        rp = np.fromfile(os.path.join(d, "replay_pairs.bin"), dtype=S3_PAIR)
+        if not si:
+            return rc, rp
+        return (rc, rp, np.fromfile(os.path.join(d, "si_paths.bin"), dtype=SI_CALL),
+                np.fromfile(os.path.join(d, "si_pairs.bin"), dtype=SI_PAIR))
 
 
 def trace_gmap_run(prefix: str, genome_fa: str, query_fa: str, d: str, stage3_every: int = 1) -> bytes:
@@ -713,6 +898,7 @@ def main() -> None:
         ("maxent_synth", lambda: maxent_case("maxent_synth", bsyn, synth.size, 6000, seed=302)),
         ("gmap_trace", lambda: gmap_trace_case()),
         ("gmap_her2", lambda: gmap_her2_case()),
+        ("gmap_cins", lambda: gmap_cins_case()),
     ]
     for name, fn in cases:
         if not only or name in only:

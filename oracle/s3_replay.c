@@ -23,7 +23,14 @@
  * Replaying gmap_trace's own calls without an IIT reproduces gmap's recorded
  * lists byte for byte (gen_golden.py checks this before it trusts a replay).
  *
- * Usage: s3_replay <dir> [--iit FILE DIV NOVEL] [--si]
+ * traverse_genome_gap reads its locals new_leftgenomepos / new_rightgenomepos
+ * uninitialised when a Dynprog_genome_gap returns early without writing them
+ * (stage3.c:5633-5976; dynprog.c:4855-4858), and adds their difference to
+ * *nonintronlen: that counter then depends on stack garbage.  --poison B fills
+ * the stack below the call with byte B first, so that two runs with different
+ * bytes show which outputs depend on it (gen_golden.py excludes those fields).
+ *
+ * Usage: s3_replay <dir> [--iit FILE DIV NOVEL] [--si] [--poison B]
  *   in:  <dir>/{genome.u32,calls.bin,pairs_in.bin,query.bin,query_uc.bin}
  *   out: <dir>/{replay_calls.bin,replay_pairs.bin}  (+ --si: si_paths.bin, si_pairs.bin)
  */
@@ -125,6 +132,13 @@ static int cmp_ptr(const void *a, const void *b) {
   return x < y ? -1 : (x > y ? 1 : 0);
 }
 
+/* the stack the next call's frames will use, filled with one byte */
+__attribute__((noinline)) static void poison_stack(int b) {
+  volatile unsigned char buf[1 << 17];
+  memset((void *)buf, b, sizeof(buf));
+  __asm__ volatile("" : : "r"(buf) : "memory");
+}
+
 static S3Pair rec(const struct Pair_T *x, int src) {
   S3Pair r;
   r.querypos = x->querypos;
@@ -142,7 +156,7 @@ static S3Pair rec(const struct Pair_T *x, int src) {
 
 int main(int argc, char **argv) {
   const char *dir, *iitfile = NULL, *div = NULL;
-  int novel = 1, do_si = 0, a;
+  int novel = 1, do_si = 0, poison = -1, a;
   size_t ng, nc, np, nq, nqu, i;
   unsigned int *g;
   S3Call *calls;
@@ -172,6 +186,8 @@ int main(int argc, char **argv) {
       a += 3;
     } else if (!strcmp(argv[a], "--si")) {
       do_si = 1;
+    } else if (!strcmp(argv[a], "--poison") && a + 1 < argc) {
+      poison = (int)strtol(argv[++a], NULL, 0);
     } else {
       fprintf(stderr, "s3_replay: unknown argument %s\n", argv[a]);
       return 1;
@@ -248,6 +264,7 @@ int main(int argc, char **argv) {
       inptr[j].i = j;
     }
     qsort(inptr, (size_t)c->npairs, sizeof(PtrIdx), cmp_ptr);
+    if (poison >= 0) poison_stack(poison);
     clock_gettime(CLOCK_MONOTONIC, &t0);
     out = bpi(&shiftp, &incompletep, &nintrons, &nnonintrons, &intronlen, &nonintronlen, &minor, &major, path,
               c->chrnum, c->chroffset, c->chrhigh, c->chrpos, NULL, c->querylength, c->genomiclength, q + c->qpos,

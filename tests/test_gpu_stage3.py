@@ -12,9 +12,9 @@ import time
 import numpy as np
 import pytest
 
-from gsnapdp import Context
+from gsnapdp import Context, SplicingIIT
 from gsnapdp import workload as W
-from test_stage3_cpu import NAMES, check_pass, stage3_golden
+from test_stage3_cpu import IIT_NAMES, NAMES, check_pass, check_scores, iit_intervals, stage3_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -25,10 +25,31 @@ def test_gpu_stage3_pass_matches_reference(golden_dir, name):
     calls, pin, q, qu, want = stage3_golden(z)
     ctx = Context(z["blocks"])
     got_calls, got, st = ctx.stage3_pass(calls, pin, q, qu)
+    check_pass(got_calls, got, calls, want, name, z["ub_ref"] if "ub_ref" in z else None)
+    assert st["failed"] == 0 and st["undefined"] == 0
+    if name == "gmap_cins_stage3":
+        assert st["windows"][2] >= 200  # traverse_cdna_gap's Dynprog_cdna_gap windows
+    print("%s: %d calls, %d rounds, windows %s in batches %s, %d calls with undefined intron lengths" % (
+        name, len(calls), st["rounds"], st["windows"], st["batches"], int((got_calls["ub"] & 1).sum())))
+    ctx.close()
+
+
+@pytest.mark.parametrize("name", IIT_NAMES)
+def test_gpu_stage3_pass_with_splicing_iit(golden_dir, name):
+    """known-site records on every genome-gap window (site-level and intron-level
+    IITs, novel splicing on and off) and score_introns with the IIT's verdicts,
+    against the reference run with the same IIT"""
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    calls, pin, q, qu, want = stage3_golden(z)
+    ctx = Context(z["blocks"])
+    iit = SplicingIIT(iit_intervals(z))
+    got_calls, got, st = ctx.stage3_pass(calls, pin, q, qu, iit=iit)
     check_pass(got_calls, got, calls, want, name)
     assert st["failed"] == 0 and st["undefined"] == 0
-    print("%s: %d calls, %d rounds, windows %s in batches %s" % (name, len(calls), st["rounds"], st["windows"],
-                                                                st["batches"]))
+    check_scores(ctx.stage3_score_introns(got_calls, got, iit=iit), got_calls, z["si_calls"], name)
+    print("%s: %d calls, windows %s, %d disallowed cells" % (name, len(calls), st["windows"],
+                                                            int(((got["flags"] & 4) != 0).sum())))
+    iit.close()
     ctx.close()
 
 
@@ -37,7 +58,7 @@ def test_gpu_stage3_pass_at_scale(golden_dir):
     calls, pin, q, qu, want = stage3_golden(z)
     ctx = Context(z["blocks"])
     ctx.stage3_pass(calls[:8], pin, q, qu)  # warm-up (first launches, staging)
-    copies = 64
+    copies = 16  # 7,424 paths
     C, PI, Q, QU, WANT = W.stage3_calls(z, copies)
     t0 = time.perf_counter()
     got_calls, got, st = ctx.stage3_pass(C, PI, Q, QU)
@@ -52,14 +73,18 @@ def test_gpu_stage3_pass_at_scale(golden_dir):
     ctx.close()
 
 
-def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path):
+@pytest.mark.parametrize("name", ["gmap_synth_stage3", "gmap_cins_stage3"] + IIT_NAMES)
+def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name):
     """Gsnapdp_build_pairs_introns as stage3.c would call it (the reference's
     signature): the path as a List_T of the host's Pair_T cells, the counters
-    as in/out arguments, the returned list (kept cells and pushed pairs)."""
+    as in/out arguments, the returned list (kept cells and pushed pairs, with
+    disallowedp).  The IIT sets give Dynprog_setup a splicing IIT (the IIT test
+    double over the golden's intervals, as test_dropin's genome-gap test does)."""
     import ctypes
     import subprocess
 
     from gsnapdp.records import S3_PAIR
+    from test_dropin import SETUP_ARGS, load_iit_double
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     so = os.path.join(str(tmp_path), "libpairpool_double.so")
@@ -79,15 +104,32 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path):
     L.Gsnapdp_build_pairs_introns.argtypes = (
         [vp] * 8 + [vp, i32, u32, u32, u32, vp, i32, i32, vp, vp, vp, vp, u8, i32, u8, u8] + [i32] * 5 +
         [ctypes.c_double, i32, vp, vp, vp, vp, u8])
-    z = np.load(os.path.join(golden_dir, "gmap_synth_stage3.npz"), allow_pickle=False)
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
     calls, pin, q, qu, want = stage3_golden(z)
     assert (calls["maxlength1"] == 611).all() and (calls["maxlength2"] == 2000).all()
     blocks = np.ascontiguousarray(z["blocks"])
     L.Dynprog_term()  # a context an earlier test left holds another genome
+    L.Dynprog_setup.argtypes = SETUP_ARGS
+    iit = None
+    if "intervals" in z:
+        iv = iit_intervals(z)  # as the ggap_known_* sets store them: start, end, 0 none / 1 donor / 2 acceptor
+        dz = {"intervals": np.stack([iv["start"].astype(np.int64), iv["end"].astype(np.int64),
+                                     iv["type"].astype(np.int64) + 1], axis=1)}
+        iitlib, iit, (dtype, atype) = load_iit_double(tmp_path, dz)
+        crosstable = (ctypes.c_int * 2)(0, 0)  # the calls' chrnum 0 -> the IIT's one division
+        L.Dynprog_setup(int(z["novelsplicingp"]), iit, ctypes.addressof(crosstable), dtype, atype,
+                        None, None, None, 0, None, None, None, None, None)
+    else:
+        L.Dynprog_setup(1, None, None, -1, -1, None, None, None, 0, None, None, None, None, None)
     L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
     dp = L.Dynprog_new(600, 10, 11, 10, 8)  # gmap.c's dynprogL / M / R: 611 x 2000
     qb = np.ascontiguousarray(q)
     qub = np.ascontiguousarray(qu)
+    # which calls' intron lengths the reference took from uninitialised locals: the pass says
+    ctx = Context(z["blocks"])
+    siit = SplicingIIT(iit_intervals(z)) if iit is not None else None
+    ub = (ctx.stage3_pass(calls, pin, q, qu, iit=siit)[0]["ub"] & 1) != 0
+    ctx.close()
     for i, c in enumerate(calls):
         f0, n = int(c["first_pair"]), int(c["npairs"])
         recs = np.ascontiguousarray(pin[f0:f0 + n])
@@ -110,6 +152,10 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path):
         assert k == len(exp), (i, k, len(exp))
         assert got[:k].tobytes() == exp.tobytes(), i
         assert (shift.value, inc.value) == (int(c["shiftp"]), int(c["incompletep"])), i
-        assert [x.value for x in ctr] == [int(c[f]) for f in ("out_nintrons", "out_nnonintrons", "out_intronlen",
-                                                              "out_nonintronlen", "out_minor", "out_major")], i
+        fields = ("out_nintrons", "out_nnonintrons", "out_intronlen", "out_nonintronlen", "out_minor", "out_major")
+        skip = ub[i] if ub is not None else False  # the reference's own intron lengths are garbage there
+        assert [x.value for j, x in enumerate(ctr) if not (skip and j in (2, 3))] == [
+            int(c[f]) for j, f in enumerate(fields) if not (skip and j in (2, 3))], i
+    if iit is not None:  # back to no IIT for the other tests of this process
+        L.Dynprog_setup(1, None, None, -1, -1, None, None, None, 0, None, None, None, None, None)
     L.Dynprog_term()  # releases the device context (the genome array dies with this test)

@@ -20,7 +20,12 @@ from gsnapdp import workload as W
 from gsnapdp.records import S3_CALL, S3_PAIR, S3_STATS
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-NAMES = ["gmap_her2_stage3", "gmap_synth_stage3"]
+NAMES = ["gmap_her2_stage3", "gmap_synth_stage3", "gmap_cins_stage3"]
+# the cDNA-insertion calls replayed through the reference with a splicing IIT
+# (oracle/gen_golden.py gmap_cins_case): site-level with and without novel
+# splicing, intron-level without
+IIT_NAMES = ["gmap_cins_iit_sites_novel", "gmap_cins_iit_sites", "gmap_cins_iit_introns"]
+UB_COUNTERS = ("out_intronlen", "out_nonintronlen")
 COUNTERS = ["out_minor", "out_major", "out_nintrons", "out_nnonintrons", "out_intronlen", "out_nonintronlen",
             "shiftp", "incompletep", "nout"]
 
@@ -30,11 +35,19 @@ def stage3_golden(z):
     return W.stage3_calls(z)
 
 
-def check_pass(calls, out, want_calls, want_out, what):
-    """the pass's counters and lists against the reference's, call by call"""
+def check_pass(calls, out, want_calls, want_out, what, ub_ref=None):
+    """the pass's counters and lists against the reference's, call by call.
+    The intron-length counters are skipped where the pass reports that the
+    reference read traverse_genome_gap's uninitialised locals (calls["ub"]);
+    `ub_ref` marks the calls where two runs of the reference itself disagree
+    there, and the pass must report every one of them."""
     assert (calls["status"] == 0).all(), "%s: failed calls %s" % (what, np.nonzero(calls["status"])[0][:8])
+    ub = (calls["ub"] & 1) != 0
+    if ub_ref is not None:
+        miss = np.nonzero((np.asarray(ub_ref) != 0) & ~ub)[0]
+        assert miss.size == 0, "%s: reference garbage not flagged at calls %s" % (what, miss[:8])
     for f in COUNTERS:
-        bad = np.nonzero(calls[f] != want_calls[f])[0]
+        bad = np.nonzero((calls[f] != want_calls[f]) & ~(ub if f in UB_COUNTERS else False))[0]
         assert bad.size == 0, "%s: %s differs at calls %s (got %s want %s)" % (
             what, f, bad[:8], calls[f][bad[:8]], want_calls[f][bad[:8]])
     for i, (c, w) in enumerate(zip(calls, want_calls)):
@@ -102,9 +115,11 @@ def test_stage3_pass_cpu_matches_reference(golden_dir, tmp_path, name):
     got_calls = np.fromfile(os.path.join(d, "pass_calls.bin"), dtype=S3_CALL)
     got = np.fromfile(os.path.join(d, "pass_pairs.bin"), dtype=S3_PAIR)
     st = np.fromfile(os.path.join(d, "pass_stats.bin"), dtype=S3_STATS)[0]
-    check_pass(got_calls, got, calls, want, name)
+    check_pass(got_calls, got, calls, want, name, z["ub_ref"] if "ub_ref" in z else None)
     assert st["failed"] == 0 and st["undefined"] == 0
     assert st["windows"][1] > 0 and st["windows"][3] > 0  # genome gaps and microexons were exercised
+    if name == "gmap_cins_stage3":
+        assert st["windows"][2] >= 200  # traverse_cdna_gap's Dynprog_cdna_gap windows
 
 
 def test_stage3_golden_covers_the_branches(golden_dir):
@@ -118,3 +133,32 @@ def test_stage3_golden_covers_the_branches(golden_dir):
     new = z["out_new"]
     assert ((new["flags"] & 1) == 1).any()  # gapholders made by the genome-gap fills
     assert (c["out_nintrons"] > c["in_nintrons"]).any()
+
+
+def iit_intervals(z):
+    from gsnapdp.records import IIT_INTERVAL
+    return np.ascontiguousarray(z["intervals"], dtype=IIT_INTERVAL)
+
+
+def check_scores(scores, calls, si_calls, what):
+    """score_introns on every returned list against the reference's (s3_replay --si)"""
+    assert len(scores) == len(si_calls)
+    for f in ("avg_donor_score", "avg_acceptor_score"):
+        bad = np.nonzero(scores[f].view(np.uint64) != si_calls[f].astype(np.float64).view(np.uint64))[0]
+        assert bad.size == 0, "%s: %s differs at calls %s" % (what, f, bad[:8])
+    bad = np.nonzero(scores["nbadintrons"] != si_calls["nbadintrons"])[0]
+    assert bad.size == 0, "%s: nbadintrons differs at calls %s" % (what, bad[:8])
+
+
+@pytest.mark.parametrize("name", IIT_NAMES)
+def test_stage3_pass_cpu_with_splicing_iit(golden_dir, tmp_path, name):
+    """the pass with a splicing IIT (every genome-gap window's known-site record,
+    gsnapdp_known_site_record) and score_introns on its lists with the IIT's
+    verdicts, against the reference's build_pairs_introns / score_introns run
+    with the same IIT (oracle/s3_replay.c)"""
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    calls, pin, q, qu, want = stage3_golden(z)
+    got_calls, got, st, scores = run_stage3_cpu(str(tmp_path), z, calls, pin, q, qu, iit_intervals(z), introns=True)
+    check_pass(got_calls, got, calls, want, name)
+    assert st["failed"] == 0 and st["undefined"] == 0
+    check_scores(scores, got_calls, z["si_calls"], name)

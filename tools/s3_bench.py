@@ -1,5 +1,5 @@
 """The stage-3 pass side line of bench.py alone (bench.measure_stage3), for
-quick GPU iterations: python tools/s3_bench.py [COPIES] [REPS]"""
+quick GPU iterations: python tools/s3_bench.py [PATHS] [REPS]"""
 import json
 import os
 import sys
@@ -9,6 +9,6 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 if __name__ == "__main__":
-    copies = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    paths = int(sys.argv[1]) if len(sys.argv) > 1 else 7424
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    print(json.dumps(bench.measure_stage3(copies=copies, reps=reps)), flush=True)
+    print(json.dumps(bench.measure_stage3(paths=paths, reps=reps)), flush=True)
