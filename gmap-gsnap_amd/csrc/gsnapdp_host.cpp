@@ -228,8 +228,8 @@ extern "C" int gsnapdp_expand(gsnapdp_ctx* ctx, const gsnapdp_window* w, const g
   const char* qu = query_uc + w->qpos;
   const int qoff = w->offset1, goff = w->offset2, dpi = w->dynprogindex;
   int r = res->bestr, c = res->bestc;
-  std::vector<gsnapdp_pair> p;  // push order
-  p.reserve(256);
+  thread_local std::vector<gsnapdp_pair> p;  // push order (a buffer per host thread)
+  p.clear();
   replay(ops, res->nops, r, c, q, qu, qoff, goff, rev, G, prof, dpi, p);
   // final list orientation (dynprog.c:4571, 5264-5283, 5721-5740)
   const int m = (int)p.size();
@@ -374,8 +374,8 @@ extern "C" int gsnapdp_sj_expand(gsnapdp_ctx* ctx, const gsnapdp_sj_window* w,
   if (res->status == ST_OPS_OVERFLOW) return -1;
   const bool rev = w->kind == GSNAPDP_END5_GAP;
   const int jump = rev ? w->offset2_anchor - w->offset2_far : w->offset2_far - w->offset2_anchor;
-  std::vector<gsnapdp_pair> p;
-  p.reserve(256);
+  thread_local std::vector<gsnapdp_pair> p;
+  p.clear();
   replay_local(ops, res->nops, res->bestr, res->bestc, w->contlength, query + w->qpos,
                query_uc + w->qpos, query + w->spos, w->offset1, w->offset2_far,
                w->offset2_anchor, jump, rev, gsnapdp__host_prof(ctx), w->dynprogindex, p);
@@ -411,8 +411,8 @@ extern "C" int gsnapdp_micro_expand(gsnapdp_ctx* ctx, const gsnapdp_micro_window
   const int offs1[3] = {0, res->bestcL, res->bestcL + res->middlelength};
   const int offs2[3] = {w->offset2L, res->offset2M, w->revoffset2R - res->bestcR + 1};
   const int lens[3] = {res->bestcL, res->middlelength, res->bestcR};
-  std::vector<gsnapdp_pair> p;
-  p.reserve((size_t)w->length1 + 2);
+  thread_local std::vector<gsnapdp_pair> p;
+  p.clear();
   for (int seg = 0; seg < 3; seg++) {
     for (int k = 0; k < lens[seg]; k++) {
       const int qi = offs1[seg] + k;
@@ -467,9 +467,9 @@ extern "C" int gsnapdp_ggap_expand(gsnapdp_ctx* ctx, const gsnapdp_ggap_window* 
   HostGenome G = {gsnapdp__host_blocks(ctx), gsnapdp__host_nwords(ctx), w->chroffset, w->chrhigh,
                   w->chrpos, (int)w->genomiclength, w->watsonp ? 1 : 0};
   const int L1 = w->length1, dpi = w->dynprogindex;
-  std::vector<gsnapdp_pair> pr, pl;
-  pr.reserve(128);
-  pl.reserve(128);
+  thread_local std::vector<gsnapdp_pair> pr, pl;  // buffers per host thread
+  pr.clear();
+  pl.clear();
   replay(ops, tr->nops_right, tr->brR, tr->bcR, query + w->qpos + L1 - 1,
          query_uc + w->qpos + L1 - 1, w->offset1 + L1 - 1, w->revoffset2R, true, G, prof, dpi, pr);
   replay(ops + tr->nops_right, tr->nops_left, tr->brL, tr->bcL, query + w->qpos,
@@ -597,7 +597,10 @@ extern "C" int gsnapdp_cgap_expand(gsnapdp_ctx* ctx, const gsnapdp_cgap_window* 
   HostGenome G = {gsnapdp__host_blocks(ctx), gsnapdp__host_nwords(ctx), w->chroffset, w->chrhigh,
                   w->chrpos, (int)w->genomiclength, w->watsonp ? 1 : 0};
   const int dpi = w->dynprogindex, revoffset2 = w->offset2 + w->length2 - 1;
-  std::vector<gsnapdp_pair> pr, pl, pi;
+  thread_local std::vector<gsnapdp_pair> pr, pl, pi;
+  pr.clear();
+  pl.clear();
+  pi.clear();
   replay_cdna(ops, res->nops_right, res->brR, res->bcR, query + w->qposR, query_uc + w->qposR,
               w->revoffset1R, revoffset2, true, G, dpi, pr);
   replay_cdna(ops + res->nops_right, res->nops_left, res->brL, res->bcL, query + w->qposL,

@@ -69,18 +69,48 @@ bool unknown_base(char c) {  // pair.c
   }
 }
 
-// One path's pairs and list cells.  Cells are never freed; a cell's pair
-// index never changes (List_push_existing re-links the cell itself).
+// One path's pairs and list cells.  The caller's pairs are read in place:
+// pair j < nin is pairs_in[j] (only its DISALLOWED flag can change, kept in
+// `flags`), cell j < nin starts as the input list's j-th cell (pair j, next
+// j + 1), and the pairs and cells the pass makes are appended after them.
+// Cells are never freed; a cell's pair never changes (List_push_existing
+// re-links the cell itself).
+// a pair record that a resize leaves uninitialised (list_of writes every field)
+struct RawPair {
+  gsnapdp_s3_pair p;
+  RawPair() {}
+};
+
 struct Arena {
-  std::vector<gsnapdp_s3_pair> pr;
-  std::vector<int> cp, cn;
+  const gsnapdp_s3_pair* in = nullptr;
+  int nin = 0;
+  std::vector<uint8_t> flags;          // the input pairs' flags
+  std::vector<RawPair> extra;  // pair nin + i
+  std::vector<int> cp;                 // pair of cell nin + i
+  std::vector<int> cn;                 // next cell of every cell
+  void init(const gsnapdp_s3_pair* pairs, int n) {
+    in = pairs;
+    nin = n;
+    flags.resize((size_t)n);
+    cn.resize((size_t)n);
+    for (int j = 0; j < n; j++) {
+      flags[(size_t)j] = pairs[j].flags;
+      cn[(size_t)j] = j + 1 < n ? j + 1 : -1;
+    }
+    extra.clear();
+    cp.clear();
+    extra.reserve(256);
+    cp.reserve(256);
+    cn.reserve((size_t)n + 256);
+  }
+  int pairof(int cell) const { return cell < nin ? cell : cp[(size_t)(cell - nin)]; }
   int cell(int pair, int next) {
     cp.push_back(pair);
     cn.push_back(next);
-    return (int)cp.size() - 1;
+    return nin + (int)cp.size() - 1;
   }
   int pop(int list, int* pair) const {  // Pairpool_pop
-    *pair = cp[(size_t)list];
+    *pair = pairof(list);
     return cn[(size_t)list];
   }
   int push_existing(int list, int c) {  // List_push_existing
@@ -95,12 +125,30 @@ struct Arena {
     }
     return dest;
   }
-  gsnapdp_s3_pair& at(int pair) { return pr[(size_t)pair]; }
-  gsnapdp_s3_pair& first(int list) { return pr[(size_t)cp[(size_t)list]]; }
+  const gsnapdp_s3_pair& at(int pair) const { return pair < nin ? in[pair] : extra[(size_t)(pair - nin)].p; }
+  // a pair's flags without touching the pair record (the scan's hot loop)
+  uint8_t flag(int pair) const { return pair < nin ? flags[(size_t)pair] : extra[(size_t)(pair - nin)].p.flags; }
+  const gsnapdp_s3_pair& first(int list) const { return at(pairof(list)); }
+  void disallow(int list) {  // pair->disallowedp = true (stage3.c:5873-5880)
+    const int p = pairof(list);
+    if (p < nin) flags[(size_t)p] |= GSNAPDP_S3_DISALLOWED;
+    else extra[(size_t)(p - nin)].p.flags |= GSNAPDP_S3_DISALLOWED;
+  }
   int rest(int list) const { return cn[(size_t)list]; }
   int push_pair(int list, const gsnapdp_s3_pair& x) {
-    pr.push_back(x);
-    return cell((int)pr.size() - 1, list);
+    extra.emplace_back();
+    extra.back().p = x;
+    return cell(nin + (int)extra.size() - 1, list);
+  }
+  // the returned cell as the ABI reports it: an input pair with its flags and
+  // src = its index, or a pair the pass made (src -1)
+  gsnapdp_s3_pair out(int list) const {
+    const int p = pairof(list);
+    if (p >= nin) return extra[(size_t)(p - nin)].p;
+    gsnapdp_s3_pair x = in[p];
+    x.src = p;
+    x.flags = flags[(size_t)p];
+    return x;
   }
 };
 bool gapp(const gsnapdp_s3_pair& p) { return (p.flags & GSNAPDP_S3_GAPP) != 0; }
@@ -163,6 +211,38 @@ struct Path {
   int undefined = 0;  // probability re-runs with no qualifying candidate
   Req req;
 };
+
+// Paths are kept between passes (their vectors keep their capacity), so a
+// pass does not fault fresh pages in for every arena; concurrent passes each
+// take their own set.
+struct PathStore {
+  std::vector<Path> paths;
+};
+std::mutex g_store_mu;
+std::vector<PathStore*> g_store;
+PathStore* store_acquire() {
+  std::lock_guard<std::mutex> l(g_store_mu);
+  if (g_store.empty()) return new PathStore;
+  PathStore* s = g_store.back();
+  g_store.pop_back();
+  return s;
+}
+void store_release(PathStore* s) {
+  std::lock_guard<std::mutex> l(g_store_mu);
+  g_store.push_back(s);
+}
+// a path as a fresh Path, keeping its vectors' storage
+void reset(Path& k) {
+  Arena A = std::move(k.A);
+  Req R = std::move(k.req);
+  std::string why = std::move(k.why);
+  k = Path();
+  k.A = std::move(A);
+  k.req = std::move(R);
+  k.req.fam = F_NONE;
+  k.why = std::move(why);
+  k.why.clear();
+}
 
 struct Pass {
   gsnapdp_ctx* ctx;
@@ -236,7 +316,7 @@ int peeled_score(Arena& A, int list, int cdna_direction, double defect_rate, std
         return 0;
       }
     }
-    prev = A.cp[(size_t)p];
+    prev = A.pairof(p);
   }
   const int mism = defect_rate < DEFECT_HIGHQ ? -3 : (defect_rate < DEFECT_MEDQ ? -2 : -1);
   return 3 * matches + mism * mismatches - 10 * qopens - 3 * qindels - 10 * topens - 3 * tindels;
@@ -260,7 +340,7 @@ int peel_rightward(Arena& A, bool* mismatchp, int* peeled_pairs, int pairs, int*
     rest = A.rest(pairs);
     bool stopp = false;
     while (rest >= 0 && !stopp) {
-      nextpair = A.cp[(size_t)rest];
+      nextpair = A.pairof(rest);
       const gsnapdp_s3_pair& nx = A.at(nextpair);
       if (gapp(nx) || nx.cdna == ' ' || nx.genome == ' ') stopp = true;
       const int ptr = pairs;
@@ -273,7 +353,7 @@ int peel_rightward(Arena& A, bool* mismatchp, int* peeled_pairs, int pairs, int*
     if (throughmismatchp && rest >= 0 && !gapp(A.at(nextpair))) {
       stopp = false;
       while (rest >= 0 && !stopp) {
-        nextpair = A.cp[(size_t)rest];
+        nextpair = A.pairof(rest);
         if (gapp(A.at(nextpair))) stopp = true;
         const int ptr = pairs;
         pairs = A.pop(pairs, &pair);
@@ -313,7 +393,7 @@ int peel_leftward(Arena& A, bool* mismatchp, int* peeled_path, int path, int* qu
     rest = A.rest(path);
     bool stopp = false;
     while (rest >= 0 && !stopp) {
-      nextpair = A.cp[(size_t)rest];
+      nextpair = A.pairof(rest);
       const gsnapdp_s3_pair& nx = A.at(nextpair);
       if (gapp(nx) || nx.cdna == ' ' || nx.genome == ' ') stopp = true;
       const int ptr = path;
@@ -326,7 +406,7 @@ int peel_leftward(Arena& A, bool* mismatchp, int* peeled_path, int path, int* qu
     if (throughmismatchp && rest >= 0 && !gapp(A.at(nextpair))) {
       stopp = false;
       while (rest >= 0 && !stopp) {
-        nextpair = A.cp[(size_t)rest];
+        nextpair = A.pairof(rest);
         if (gapp(A.at(nextpair))) stopp = true;
         const int ptr = path;
         path = A.pop(path, &pair);
@@ -582,12 +662,19 @@ std::vector<gsnapdp_pair>& expand_buf(size_t n) {
 // a gap family's expanded pairs as a list in the path's arena (push order as
 // the drop-in's push_pairs: the list's head is pairs[0])
 int list_of(Arena& A, const std::vector<gsnapdp_pair>& v, int n, bool micro) {
-  int list = -1;
-  for (int i = n - 1; i >= 0; i--) {
+  if (n <= 0) return -1;
+  // pairs nin + e0 .. e0 + n - 1 in cells c0 .. c0 + n - 1: the list's head is
+  // v[0]'s cell, and each cell links to the next (push order from v[n - 1])
+  const size_t e0 = A.extra.size(), k0 = A.cp.size(), c0 = A.cn.size();
+  A.extra.resize(e0 + (size_t)n);
+  A.cp.resize(k0 + (size_t)n);
+  A.cn.resize(c0 + (size_t)n);
+  for (int i = 0; i < n; i++) {
     const gsnapdp_pair& p = v[(size_t)i];
-    gsnapdp_s3_pair x;
-    memset(&x, 0, sizeof(x));
+    gsnapdp_s3_pair& x = A.extra[e0 + (size_t)i].p;
+    x.queryjump = x.genomejump = 0;
     x.src = -1;
+    x.flags = 0;
     if (p.gapp) {  // Pairpool_push_gapholder (pairpool.c:352-410)
       x.querypos = -1;
       x.genomepos = -1;
@@ -606,9 +693,10 @@ int list_of(Arena& A, const std::vector<gsnapdp_pair>& v, int n, bool micro) {
       x.comp = p.comp;
       x.genome = p.genome;
     }
-    list = A.push_pair(list, x);
+    A.cp[k0 + (size_t)i] = A.nin + (int)(e0 + (size_t)i);
+    A.cn[c0 + (size_t)i] = i + 1 < n ? (int)(c0 + (size_t)i + 1) : -1;
   }
-  return list;
+  return (int)c0;
 }
 
 // ---- results, read back exactly as the drop-in reads them
@@ -929,8 +1017,8 @@ void genome_decide(Path& k) {
   const gsnapdp_s3_call& c = *k.c;
   const int acceptable = c.defect_rate < DEFECT_HIGHQ ? 2 : (c.defect_rate < DEFECT_MEDQ ? 2 : 3);
   if (k.gappairs < 0) {
-    for (int p = k.peeled_pairs; p >= 0; p = k.A.rest(p)) k.A.first(p).flags |= GSNAPDP_S3_DISALLOWED;
-    for (int p = k.peeled_path; p >= 0; p = k.A.rest(p)) k.A.first(p).flags |= GSNAPDP_S3_DISALLOWED;
+    for (int p = k.peeled_pairs; p >= 0; p = k.A.rest(p)) k.A.disallow(p);
+    for (int p = k.peeled_path; p >= 0; p = k.A.rest(p)) k.A.disallow(p);
     put_back(k);
     k.introntype = NONINTRON;
     genome_account(k);
@@ -1012,10 +1100,13 @@ void scan(Pass& P, Path& k) {
     int pair = -1;
     const int ptr = k.path;
     k.path = k.A.pop(k.path, &pair);
+    if (!(k.A.flag(pair) & GSNAPDP_S3_GAPP)) {  // not a gap: keep it
+      k.pairs = k.A.push_existing(k.pairs, ptr);
+      continue;
+    }
     const gsnapdp_s3_pair& g = k.A.at(pair);
     int kind;  // 0 keep it, 1 cDNA gap, 2 genome gap, 3 single gap
-    if (!gapp(g)) kind = 0;
-    else if (g.queryjump > c.nullgap) kind = 0;  // a large gap
+    if (g.queryjump > c.nullgap) kind = 0;  // a large gap
     else if (g.queryjump > g.genomejump + EXTRAQUERYGAP) kind = 1;
     else if (g.genomejump > g.queryjump + minintronlen) kind = 2;
     else if (g.genomejump > g.queryjump + SINGLESLEN) kind = 0;  // a short intron
@@ -1026,8 +1117,8 @@ void scan(Pass& P, Path& k) {
     }
     if (k.path < 0 || k.pairs < 0) return fail(k, "gap at the end of the path (the reference dereferences NULL)");
     k.gapcell = ptr;
-    k.left = k.A.cp[(size_t)k.path];    // leftpair = path->first
-    k.right = k.A.cp[(size_t)k.pairs];  // rightpair = pairs->first
+    k.left = k.A.pairof(k.path);    // leftpair = path->first
+    k.right = k.A.pairof(k.pairs);  // rightpair = pairs->first
     k.peeled_pairs = k.peeled_path = -1;
     const bool waits = kind == 1 ? cdna_start(k) : (kind == 2 ? genome_start(P, k) : single_start(k));
     if (waits) return;
@@ -1083,8 +1174,10 @@ class Workers {
     }
     cv_.notify_all();
     work();
-    std::unique_lock<std::mutex> l(m_);
-    done_.wait(l, [&] { return active_.load() == 0; });
+    // the workers are spinning or waking; a run is a few hundred microseconds,
+    // so the caller spins for them too rather than sleeping on a condition
+    while (active_.load(std::memory_order_acquire) != 0) {
+    }
     fn_ = nullptr;
   }
 
@@ -1109,15 +1202,12 @@ class Workers {
       }
       seen = gen_.load(std::memory_order_acquire);
       work();
-      if (active_.fetch_sub(1) == 1) {
-        std::lock_guard<std::mutex> l(m_);
-        done_.notify_all();
-      }
+      active_.fetch_sub(1, std::memory_order_acq_rel);
     }
   }
   const int nthreads_;
   std::mutex m_, run_m_;
-  std::condition_variable cv_, done_;
+  std::condition_variable cv_;
   const std::function<void(int)>* fn_ = nullptr;
   std::atomic<int> next_{0}, active_{0};
   std::atomic<uint64_t> gen_{0};
@@ -1128,7 +1218,9 @@ class Workers {
 constexpr size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct Cohort {
-  std::vector<Path*> paths;
+  std::vector<Path*> paths;     // the paths that may still wait: a path waits in a round only if
+                                // it was resumed in the previous one, so after each round this
+                                // is that round's `all`
   std::vector<Path*> fam[F_N];  // the round's waiting paths, in batch order
   std::vector<Path*> all;       // the same, concatenated
   std::vector<size_t> qoff;     // each waiting path's query bytes in the packed round (all's order)
@@ -1147,7 +1239,9 @@ int pack_submit(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
   for (int f = 0; f < F_N; f++) C.fam[f].clear();
   for (Path* k : C.paths)
     if (!k->failed && k->stage != S_DONE && k->req.fam != F_NONE) C.fam[k->req.fam].push_back(k), nwait++;
+  C.paths.clear();
   if (!nwait) return 0;
+  for (int f = 0; f < F_N; f++) std::sort(C.fam[f].begin(), C.fam[f].end());  // batches in path order
   gsnapdp::S3Layout& L = C.L;
   L = gsnapdp::S3Layout();
   C.all.clear();
@@ -1283,6 +1377,7 @@ void unpack_resume(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
     Tic tic(prof().resume_ns);
     resume(P, k);
   });
+  C.paths.swap(C.all);  // the candidates for the next round
 }
 
 bool call_in_range(const gsnapdp_s3_call& c, int64_t npairs_in, size_t query_bytes) {
@@ -1291,6 +1386,8 @@ bool call_in_range(const gsnapdp_s3_call& c, int64_t npairs_in, size_t query_byt
 }
 
 }  // namespace
+
+void gsnapdp::s3_parallel_for(int n, int grain, const std::function<void(int)>& fn) { Workers::get().run(n, grain, fn); }
 
 extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls,
                                    const gsnapdp_s3_pair* pairs_in, int64_t npairs_in, const char* query,
@@ -1317,10 +1414,13 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
   const auto t_start = clock::now();
   double wait_s = 0.0;
   Workers& pool = Workers::get();
-  std::vector<Path> paths((size_t)ncalls);
+  PathStore* store = store_acquire();
+  if (store->paths.size() < (size_t)ncalls) store->paths.resize((size_t)ncalls);
+  Path* paths = store->paths.data();
   for (int i = 0; i < ncalls; i++) {
     Path& k = paths[(size_t)i];
     gsnapdp_s3_call& c = calls[i];
+    reset(k);
     k.c = &c;
     k.q = query + c.qpos;
     k.qu = query_uc + c.qpos;
@@ -1340,13 +1440,9 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
   pool.run(ncalls, 16, [&](int i) {
     Path& k = paths[(size_t)i];
     const gsnapdp_s3_call& c = *k.c;
-    // the input list: path->first is pairs_in[first_pair]
-    k.A.pr.reserve((size_t)c.npairs * 2 + 64);
-    k.A.pr.assign(pairs_in + c.first_pair, pairs_in + c.first_pair + c.npairs);
-    for (int j = 0; j < c.npairs; j++) k.A.pr[(size_t)j].src = j;
-    k.A.cp.reserve((size_t)c.npairs * 2 + 64);
-    k.A.cn.reserve((size_t)c.npairs * 2 + 64);
-    for (int j = c.npairs - 1; j >= 0; j--) k.path = k.A.cell(j, k.path);
+    // the input list: path->first is pairs_in[first_pair] (cell 0)
+    k.A.init(pairs_in + c.first_pair, c.npairs);
+    k.path = c.npairs > 0 ? 0 : -1;
     if (c.use_genomicseg_p) fail(k, "use_genomicseg_p passes are not served (the genome is the context's)");
     else scan(P, k);
   });
@@ -1387,22 +1483,25 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     for (int h = 0; h < ncoh; h++)
       if (coh[h].inflight) (void)X->wait(coh[h].slot);  // drain before the staging is reused
     gsnapdp::s3_exec_release(ctx, X);
+    store_release(store);
     return -1;
   }
   gsnapdp::s3_exec_release(ctx, X);
   const auto t_out = clock::now();
-  // the returned lists, each path's at its running offset (lengths first,
-  // then the copies by the workers)
+  // the returned lists, each path's at its running offset (lengths by the
+  // workers, offsets, then the copies by the workers)
   std::vector<int64_t> first((size_t)ncalls + 1, 0);
-  for (int i = 0; i < ncalls; i++) {
+  pool.run(ncalls, 16, [&](int i) {
     Path& k = paths[(size_t)i];
     int n = 0;
     if (!k.failed)
       for (int p = k.pairs; p >= 0; p = k.A.rest(p)) n++;
-    first[(size_t)i + 1] = first[(size_t)i] + n;
-  }
+    first[(size_t)i + 1] = n;
+  });
+  for (int i = 0; i < ncalls; i++) first[(size_t)i + 1] += first[(size_t)i];
   if (first[(size_t)ncalls] > out_cap) {
     gsnapdp__set_err("gsnapdp_stage3_pass: pairs_out is too small");
+    store_release(store);
     return -1;
   }
   pool.run(ncalls, 16, [&](int i) {
@@ -1413,7 +1512,7 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     c.nout = (int32_t)(first[(size_t)i + 1] - first[(size_t)i]);
     if (k.failed) return;
     int64_t at = first[(size_t)i];
-    for (int p = k.pairs; p >= 0; p = k.A.rest(p)) pairs_out[at++] = k.A.first(p);
+    for (int p = k.pairs; p >= 0; p = k.A.rest(p)) pairs_out[at++] = k.A.out(p);
     c.out_minor = k.minor;
     c.out_major = k.major;
     c.out_nintrons = k.nintrons;
@@ -1424,10 +1523,11 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     c.incompletep = k.incompletep ? 1 : 0;
     c.ub = k.ub ? GSNAPDP_S3_UB_INTRONLEN : 0;
   });
-  for (Path& k : paths) {
-    P.st.undefined += k.undefined;
-    if (k.failed) P.st.failed++;
+  for (int i = 0; i < ncalls; i++) {
+    P.st.undefined += paths[(size_t)i].undefined;
+    if (paths[(size_t)i].failed) P.st.failed++;
   }
+  store_release(store);
   const double total = std::chrono::duration<double>(clock::now() - t_start).count();
   if (pf.on) {
     pf.output = std::chrono::duration<double>(clock::now() - t_out).count();

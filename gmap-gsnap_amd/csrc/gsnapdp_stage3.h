@@ -17,6 +17,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <functional>
+
 #include "../../include/gsnapdp.h"
 
 namespace gsnapdp {
@@ -47,6 +49,10 @@ class S3Exec {
   virtual int submit(int slot, const S3Layout& L) = 0;
   virtual int wait(int slot) = 0;
 };
+
+// fn(i) for every i in [0, n) on the passes' persistent host threads (the
+// calling thread included); not reentrant (a pass calls it between rounds).
+void s3_parallel_for(int n, int grain, const std::function<void(int)>& fn);
 
 // An executor for one pass over `ctx` (2 slots), taken from the context's pool
 // (created on first use; concurrent passes each get their own staging) and

@@ -10,7 +10,11 @@
 // every slot of every executor uses the one context stream (FIFO), which is
 // also what makes concurrent passes on one context safe.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <atomic>
 
 #include <string>
 #include <vector>
@@ -21,6 +25,15 @@
 namespace gsnapdp {
 namespace {
 
+// GSNAPDP_S3_RECORD=DIR: every round's layout and output staging, in order
+// (DIR/round_NNNNNN.bin), so that the pass's host work can be replayed and
+// profiled on a machine without a GPU (tests/dropin/stage3_exec_replay.cpp)
+const char* record_dir() {
+  static const char* d = getenv("GSNAPDP_S3_RECORD");
+  return d;
+}
+std::atomic<int> g_round{0};
+
 struct Slot {
   char* h_in = nullptr;
   char* h_out = nullptr;
@@ -29,6 +42,7 @@ struct Slot {
   size_t in_cap = 0, out_cap = 0;
   hipEvent_t ev = nullptr;
   bool pending = false;
+  S3Layout L;  // the round in flight (for recording)
 };
 
 class GpuExec final : public S3Exec {
@@ -111,6 +125,7 @@ class GpuExec final : public S3Exec {
     HIPCHK(hipMemcpyAsync(s.h_out, s.d_out, L.out_bytes, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(s.ev, st));
     s.pending = true;
+    s.L = L;
     return 0;
   }
   int wait(int k) override {
@@ -118,6 +133,15 @@ class GpuExec final : public S3Exec {
     if (!s.pending) return 0;
     s.pending = false;
     HIPCHK(hipEventSynchronize(s.ev));
+    if (record_dir()) {
+      char path[4096];
+      snprintf(path, sizeof(path), "%s/round_%06d.bin", record_dir(), g_round.fetch_add(1));
+      if (FILE* f = fopen(path, "wb")) {
+        fwrite(&s.L, sizeof(s.L), 1, f);
+        fwrite(s.h_out, 1, s.L.out_bytes, f);
+        fclose(f);
+      }
+    }
     return 0;
   }
 

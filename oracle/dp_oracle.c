@@ -255,16 +255,33 @@ static inline char gnt(const gpar *g, int pos) {
 
 /* --------------------------------------------------------------- workspace */
 
+/* Each thread keeps its last few workspaces: a batch driver makes one per call,
+ * and every fill clears the rectangle it uses (:352-357, as Matrix3_alloc's
+ * callers do), so a reused allocation behaves as a fresh one; allocating and
+ * unmapping ~18 MB per call serialised the threads of a multi-threaded caller. */
+#define ORC_DP_CACHE 4
+static __thread orc_dp *dp_cache[ORC_DP_CACHE];
+
 orc_dp *orc_dp_new(int maxlookback, int extraquerygap, int maxpeelback, int extramaterial_end,
                    int extramaterial_paired) {
   /* compute_maxlengths + Dynprog_new (dynprog.c:831-873) */
-  orc_dp *dp = (orc_dp *)calloc(1, sizeof(orc_dp));
+  orc_dp *dp;
   size_t cells;
-  dp->maxlength1 = maxlookback + maxpeelback;
-  if (dp->maxlength1 < 500) dp->maxlength1 = 500;
-  dp->maxlength2 = dp->maxlength1 + extraquerygap +
-                   (extramaterial_end > extramaterial_paired ? extramaterial_end : extramaterial_paired);
-  if (dp->maxlength2 < 2000) dp->maxlength2 = 2000;
+  int m1 = maxlookback + maxpeelback, m2, i;
+  if (m1 < 500) m1 = 500;
+  m2 = m1 + extraquerygap + (extramaterial_end > extramaterial_paired ? extramaterial_end : extramaterial_paired);
+  if (m2 < 2000) m2 = 2000;
+  for (i = 0; i < ORC_DP_CACHE; i++)
+    if (dp_cache[i] && dp_cache[i]->alloc1 == m1 && dp_cache[i]->alloc2 == m2) {
+      dp = dp_cache[i];
+      dp_cache[i] = NULL;
+      dp->maxlength1 = m1;
+      dp->maxlength2 = m2;
+      return dp;
+    }
+  dp = (orc_dp *)calloc(1, sizeof(orc_dp));
+  dp->maxlength1 = dp->alloc1 = m1;
+  dp->maxlength2 = dp->alloc2 = m2;
   cells = (size_t)(dp->maxlength1 + 1) * (size_t)(dp->maxlength2 + 1);
   dp->nogap = (int32_t *)calloc(cells, 4);
   dp->gap1 = (int32_t *)calloc(cells, 4);
@@ -276,7 +293,13 @@ orc_dp *orc_dp_new(int maxlookback, int extraquerygap, int maxpeelback, int extr
 }
 
 void orc_dp_free(orc_dp *dp) {
+  int i;
   if (!dp) return;
+  for (i = 0; i < ORC_DP_CACHE; i++)
+    if (!dp_cache[i]) {
+      dp_cache[i] = dp;
+      return;
+    }
   free(dp->nogap);
   free(dp->gap1);
   free(dp->gap2);

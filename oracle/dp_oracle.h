@@ -39,6 +39,7 @@ typedef struct orc_dp {
   int maxlength1, maxlength2;
   int32_t *nogap, *gap1, *gap2;     /* (maxlength1+1) x (maxlength2+1) */
   uint8_t *dnogap, *dgap1, *dgap2;
+  int alloc1, alloc2;               /* the allocation's maxlengths (a reused workspace) */
 } orc_dp;
 
 /* Dynprog_init (dynprog.c:1339): builds the substitution tables. */

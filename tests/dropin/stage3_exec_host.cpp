@@ -5,6 +5,8 @@
 // packed round layout the GPU executor stages through page-locked memory,
 // served synchronously by the host entry points, which the oracle's
 // restatement provides there (tests/dropin/gsnapdp_oracle_abi.c).
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <vector>
 
@@ -36,32 +38,44 @@ class HostExec final : public S3Exec {
   int wait(int) override { return 0; }
 
  private:
+  // every family's windows in chunks on the pass's host threads (the oracle's
+  // batch drivers are reentrant: one workspace per call)
   int serve(int k, const S3Layout& L) {
     char* in = in_[k].data();
     char* out = out_[k].data();
     const char* q = in + L.q;
     const char* qu = in + L.qu;
     auto off = [&](int f) { return (const int64_t*)(in + L.off[f]); };
-    if (L.n[S3F_GAP] && gsnapdp_run_host(ctx_, (const gsnapdp_window*)(in + L.w[S3F_GAP]), L.n[S3F_GAP], q, qu,
-                                         L.qbytes, (gsnapdp_result*)(out + L.r[S3F_GAP]),
-                                         (uint32_t*)(out + L.ops[S3F_GAP]), off(S3F_GAP)))
-      return -1;
-    if (L.n[S3F_GGAP] &&
-        gsnapdp_ggap_run_host(ctx_, (const gsnapdp_ggap_window*)(in + L.w[S3F_GGAP]), L.n[S3F_GGAP], q, qu,
-                              L.qbytes, (gsnapdp_ggap_result*)(out + L.r[S3F_GGAP]),
-                              (gsnapdp_ggap_trace*)(out + L.t), (uint32_t*)(out + L.ops[S3F_GGAP]), off(S3F_GGAP)))
-      return -1;
-    if (L.n[S3F_CGAP] &&
-        gsnapdp_cgap_run_host(ctx_, (const gsnapdp_cgap_window*)(in + L.w[S3F_CGAP]), L.n[S3F_CGAP], q, qu,
-                              L.qbytes, (gsnapdp_cgap_result*)(out + L.r[S3F_CGAP]),
-                              (uint32_t*)(out + L.ops[S3F_CGAP]), off(S3F_CGAP)))
-      return -1;
-    if (L.n[S3F_MICRO] &&
-        gsnapdp_micro_run_host(ctx_, (const gsnapdp_micro_window*)(in + L.w[S3F_MICRO]), L.n[S3F_MICRO], q, qu,
-                               L.qbytes, (gsnapdp_micro_result*)(out + L.r[S3F_MICRO])))
-      return -1;
-    return 0;
+    std::vector<int> jf, jlo, jhi;
+    for (int f = 0; f < S3F_N; f++)
+      for (int lo = 0; lo < L.n[f]; lo += kChunk) {
+        jf.push_back(f);
+        jlo.push_back(lo);
+        jhi.push_back(std::min(L.n[f], lo + kChunk));
+      }
+    std::atomic<int> bad(0);
+    s3_parallel_for((int)jf.size(), 1, [&](int j) {
+      const int f = jf[(size_t)j], lo = jlo[(size_t)j], n = jhi[(size_t)j] - lo;
+      int rc = 0;
+      if (f == S3F_GAP)
+        rc = gsnapdp_run_host(ctx_, (const gsnapdp_window*)(in + L.w[f]) + lo, n, q, qu, L.qbytes,
+                              (gsnapdp_result*)(out + L.r[f]) + lo, (uint32_t*)(out + L.ops[f]), off(f) + lo);
+      else if (f == S3F_GGAP)
+        rc = gsnapdp_ggap_run_host(ctx_, (const gsnapdp_ggap_window*)(in + L.w[f]) + lo, n, q, qu, L.qbytes,
+                                   (gsnapdp_ggap_result*)(out + L.r[f]) + lo, (gsnapdp_ggap_trace*)(out + L.t) + lo,
+                                   (uint32_t*)(out + L.ops[f]), off(f) + lo);
+      else if (f == S3F_CGAP)
+        rc = gsnapdp_cgap_run_host(ctx_, (const gsnapdp_cgap_window*)(in + L.w[f]) + lo, n, q, qu, L.qbytes,
+                                   (gsnapdp_cgap_result*)(out + L.r[f]) + lo, (uint32_t*)(out + L.ops[f]),
+                                   off(f) + lo);
+      else
+        rc = gsnapdp_micro_run_host(ctx_, (const gsnapdp_micro_window*)(in + L.w[f]) + lo, n, q, qu, L.qbytes,
+                                    (gsnapdp_micro_result*)(out + L.r[f]) + lo);
+      if (rc) bad.store(1);
+    });
+    return bad.load() ? -1 : 0;
   }
+  static constexpr int kChunk = 64;
   gsnapdp_ctx* ctx_;
   std::vector<char> in_[2], out_[2];
 };
