@@ -48,6 +48,7 @@ GENOME_NT = 64_000_000        # side-line genome (C2, C4, C5, ...)
 MIN_STEADY_S = 1.0            # steady-state figure: at least this many seconds of steps
 DOMINANT = "k_fill"           # every C2 window is a register-band (k_fill) window
 C4_WINDOWS = 200_000          # intron windows per config-4 step
+C4_TRANSCRIPTS = 50_000       # config 4 as stated: transcripts through the final intron pass
 C5_READS = 100_000            # reads per config-5 step (3 DP windows each)
 
 
@@ -365,6 +366,7 @@ def measure_stage3(paths=7424, reps=3):
     nwin = int(np.sum(st["windows"]))
     ref = float(z["calls"]["ref_seconds"].sum()) * copies
     ctx.close()
+    cpu = stage3_cpu_baseline(z["blocks"], calls, pin, q, qu, got)
     return {"metric": "stage-3 intron pass (build_pairs_introns), paths/s", "value": round(len(calls) / dt, 1),
             "unit": "paths/s", "paths": int(len(calls)), "seconds": round(dt, 4), "rounds": int(st["rounds"]),
             "windows": nwin, "windows_per_s": round(nwin / dt, 1),
@@ -372,9 +374,111 @@ def measure_stage3(paths=7424, reps=3):
                                   "cdna_gap": int(st["windows"][2]), "microexon": int(st["windows"][3])},
             "host_s": round(float(st["seconds"][0]), 4), "batches_s": round(float(st["seconds"][1]), 4),
             "bit_exact_vs_reference": ok,
-            "reference": {"value": round(len(calls) / ref, 1), "unit": "paths/s", "seconds": round(ref, 4),
-                          "cores": 1, "kind": "reference",
-                          "note": "the reference's build_pairs_introns on the same calls, recorded by gmap_trace"}}
+            "cpu_baseline": cpu,
+            "reference_cross_machine": {
+                "value": round(len(calls) / ref, 1), "unit": "paths/s", "seconds": round(ref, 4), "cores": 1,
+                "kind": "reference",
+                "note": "the reference's own build_pairs_introns on the same calls, timed by gmap_trace in the "
+                        "development container (a different machine), DP included"}}
+
+
+def stage3_cpu_baseline(blocks, calls, pin, q, qu, want=None, compact=False):
+    """The same pass on this host's CPU: the pass's host code with every DP
+    window served by the oracle/ restatement on the pass's 16 threads
+    (oracle/_build/libstage3_cpu.so) -- best of two runs after a warm-up on a
+    slice.  Its lists are compared with the GPU pass's (`want`)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # CPU baseline leg
+    S = O.Stage3Cpu(blocks)
+    S.run_compact(calls[:min(len(calls), 256)], pin, q, qu)
+    best = None
+    for _ in range(2):
+        t0 = time.perf_counter()
+        res = S.run_compact(calls, pin, q, qu) if compact else S.run(calls, pin, q, qu)
+        dt = time.perf_counter() - t0
+        if best is None or dt < best[0]:
+            best = (dt, res)
+    S.close()
+    dt, res = best
+    out = {"value": round(len(calls) / dt, 1), "unit": "paths/s", "seconds": round(dt, 4),
+           "cores": int(os.environ.get("GSNAPDP_S3_THREADS", min(16, os.cpu_count() or 1))), "kind": "port",
+           "sample": "the same %d paths, oracle/ restatement of every DP window under the pass's host code "
+                     "(oracle/_build/libstage3_cpu.so)" % len(calls)}
+    if want is not None and not compact:
+        out["lists_equal_gpu"] = bool(res[1].tobytes() == want.tobytes())
+    return out if not compact else (out, res)
+
+
+def measure_c4_transcripts(n=C4_TRANSCRIPTS, cpu=True, pinned=2000):
+    """Side line, BASELINE config 4 as stated: `n` synthetic 5 kbp transcripts
+    (workload.c4_transcripts: 8-12 exons, GT-AG introns of 80-5000 nt, 1 % subs,
+    30 % of the boundaries stage 2 misplaces by 1-6 nt) through GMAP's final
+    intron pass (gsnapdp_stage3_pass_compact: build_pairs_introns with finalp,
+    stage3.c:8860-8875) and score_introns on every returned list
+    (gsnapdp_stage3_score_introns: one k_introns launch, :9890-9941).  The timed
+    region is one pass plus score_introns over all paths, inputs in host memory
+    (the pass is host-driven).  Parity: the first `pinned` paths against the
+    reference's own results (tests/golden/c4_pinned.npz), all paths against the
+    CPU restatement run in the same process."""
+    import hashlib
+    from gsnapdp import expand_compact
+    t0 = time.perf_counter()
+    w = W.c4_transcripts(n)
+    gen_s = time.perf_counter() - t0
+    ctx = Context(w.blocks)
+    ctx.stage3_pass_compact(w.calls[:256], w.pairs_in, w.query, w.query_uc)  # launches, staging
+    bufs = None
+    best = None
+    for _ in range(3):  # the first run also faults the output buffers in
+        t0 = time.perf_counter()
+        c, cells, new, st = ctx.stage3_pass_compact(w.calls, w.pairs_in, w.query, w.query_uc, bufs=bufs)
+        t1 = time.perf_counter()
+        if bufs is None:
+            bufs = (cells.base, new.base)
+        if best is None or t1 - t0 < best[0]:
+            best = (t1 - t0, c, cells.copy(), new.copy(), st)
+    dt, c, cells, new, st = best
+    lists = expand_compact(c, w.pairs_in, cells, new)
+    t0 = time.perf_counter()
+    sc = ctx.stage3_score_introns(c, lists)
+    si_s = time.perf_counter() - t0
+    introns = int(sc["nintrons"].sum())
+    ctx.close()
+    z = np.load(os.path.join(ROOT, "tests", "golden", "c4_pinned.npz"), allow_pickle=False)
+    m = min(pinned, n, int(z["n"]))
+    ok_ref = all(hashlib.sha256(lists[int(c["first_out"][i]):int(c["first_out"][i]) + int(c["nout"][i])].tobytes())
+                 .digest() == z["digests"][i].tobytes() for i in range(m))
+    for f in ("out_minor", "out_major", "out_nintrons", "out_nnonintrons", "shiftp", "incompletep", "nout"):
+        ok_ref = ok_ref and bool(np.array_equal(c[f][:m], z["ref_" + f][:m]))
+    ok_ref = ok_ref and bool(np.array_equal(sc["avg_donor_score"][:m].view(np.uint64),
+                                            z["si_calls"]["avg_donor_score"][:m].astype(np.float64).view(np.uint64)))
+    nwin = int(np.sum(st["windows"]))
+    total = dt + si_s
+    out = {"workload": "C4 as stated: %d synthetic transcripts of 4.5-5.5 kbp (8-12 exons, GT-AG introns of "
+                       "80-5000 nt, 1%% substitutions), each GMAP's final intron pass (build_pairs_introns, "
+                       "finalp) + score_introns; %d path pairs, %d introns; generated in %.1f s"
+                       % (n, w.pairs_in.size, w.nintrons, gen_s),
+           "metric": "C4 transcripts (final intron pass + score_introns), paths/s",
+           "value": round(n / total, 1), "unit": "paths/s", "seconds": round(total, 4),
+           "pass_s": round(dt, 4), "score_introns_s": round(si_s, 4),
+           "windows": nwin, "windows_per_s": round(nwin / dt, 1),
+           "windows_by_family": {"single": int(st["windows"][0]), "genome_gap": int(st["windows"][1]),
+                                 "cdna_gap": int(st["windows"][2]), "microexon": int(st["windows"][3])},
+           "introns_scored": introns, "introns_per_s": round(introns / si_s, 1),
+           "rounds": int(st["rounds"]), "host_s": round(float(st["seconds"][0]), 4),
+           "wait_s": round(float(st["seconds"][1]), 4),
+           "bit_exact_vs_reference": {"paths": m, "ok": bool(ok_ref)}}
+    if cpu:
+        cb, (rc, rcells, rnew, rst) = stage3_cpu_baseline(w.blocks, w.calls, w.pairs_in, w.query, w.query_uc,
+                                                          compact=True)
+        same = bool(np.array_equal(rcells, cells) and rnew.tobytes() == new.tobytes())
+        for f in ("out_minor", "out_major", "out_nintrons", "out_nnonintrons", "out_intronlen", "out_nonintronlen",
+                  "shiftp", "incompletep", "nout"):
+            same = same and bool(np.array_equal(rc[f], c[f]))
+        cb["note"] = "the pass alone (no score_introns)"
+        out["cpu_baseline"] = cb
+        out["bit_exact_vs_cpu_restatement"] = {"paths": n, "ok": same}
+    return out
 
 
 def measure_c2(genome, n, steps, warmup, dev):
@@ -462,6 +566,9 @@ def main() -> None:
     ap.add_argument("--no-c5", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the splice-junction / microexon side lines")
     ap.add_argument("--c4-windows", type=int, default=C4_WINDOWS)
+    ap.add_argument("--c4-transcripts", type=int, default=C4_TRANSCRIPTS,
+                    help="transcripts in the C4 final-pass line (BASELINE: 50k)")
+    ap.add_argument("--no-c4t", action="store_true", help="skip the C4 transcript line")
     ap.add_argument("--no-steady", action="store_true", help="skip the >= 1 s steady-state figure (profiling runs)")
     args = ap.parse_args()
     relaunch_if_needed(args)
@@ -686,6 +793,8 @@ def main() -> None:
                 out["splicejunction"] = measure_sj(genome, 100_000, 20, args.warmup, dev, not args.no_cpu)
                 out["microexon"] = measure_micro(genome, 20_000, 20, args.warmup, dev, not args.no_cpu)
                 out["stage3_pass"] = measure_stage3()
+            if not args.no_c4t:
+                out["c4_transcripts"] = measure_c4_transcripts(args.c4_transcripts, not args.no_cpu)
         print(json.dumps(out), flush=True)
     shard.finish(ranks)
     ctx.close()

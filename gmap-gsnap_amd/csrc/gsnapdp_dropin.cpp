@@ -1579,7 +1579,7 @@ gsnapdp_List_T Gsnapdp_build_pairs_introns(
     gsnapdp_Dynprog_T dynprogR, gsnapdp_bool finalp) {
   if (use_genomicseg_p) fatal("build_pairs_introns on a genomic segment is not served by the batched pass");
   gsnapdp_ctx* c = shared_ctx(true);
-  std::vector<RefList*> cells;
+  std::vector<RefList*> incells;
   std::vector<gsnapdp_s3_pair> in;
   for (RefList* l = (RefList*)path; l; l = l->rest) {
     const RefPair* x = (const RefPair*)l->first;
@@ -1589,14 +1589,14 @@ gsnapdp_List_T Gsnapdp_build_pairs_introns(
     p.queryjump = x->queryjump;
     p.genomejump = x->genomejump;
     p.dynprogindex = x->dynprogindex;
-    p.src = (int32_t)cells.size();
+    p.src = (int32_t)incells.size();
     p.cdna = x->cdna;
     p.comp = x->comp;
     p.genome = x->genome;
     p.flags = (uint8_t)((x->gapp ? GSNAPDP_S3_GAPP : 0) | (x->knowngapp ? GSNAPDP_S3_KNOWNGAPP : 0) |
                         (x->disallowedp ? GSNAPDP_S3_DISALLOWED : 0));
     in.push_back(p);
-    cells.push_back(l);
+    incells.push_back(l);
   }
   gsnapdp_s3_call k;
   memset(&k, 0, sizeof(k));
@@ -1633,23 +1633,28 @@ gsnapdp_List_T Gsnapdp_build_pairs_introns(
   k.novelsplicingp = g.novelsplicingp ? 1 : 0;
   k.splicingp = (g.novelsplicingp || g.splicing_iit) ? 1 : 0;
   const int64_t cap = 2 * ((int64_t)querylength + k.npairs) + 64;
-  std::vector<gsnapdp_s3_pair> out((size_t)cap);
+  thread_local std::vector<int32_t> cells;  // the returned list, compactly (per gmap worker thread)
+  thread_local std::vector<gsnapdp_s3_pair> news;
+  cells.resize((size_t)cap);
+  news.resize((size_t)(2 * (int64_t)querylength + 256));
   gsnapdp_s3_stats st;
   // the splicing IIT of Dynprog_setup, asked through the host's own iit-read
   // functions (every genome-gap window's known-site record)
-  if (gsnapdp_stage3_pass(c, &k, 1, in.data(), (int64_t)in.size(), queryseq_ptr, queryuc_ptr, (size_t)querylength,
-                          g.iit ? host_iit() : nullptr, out.data(), cap, &st))
-    fatal(std::string("gsnapdp_stage3_pass: ") + gsnapdp_last_error());
+  if (gsnapdp_stage3_pass_compact(c, &k, 1, in.data(), (int64_t)in.size(), queryseq_ptr, queryuc_ptr,
+                                  (size_t)querylength, g.iit ? host_iit() : nullptr, cells.data(), cap, news.data(),
+                                  (int64_t)news.size(), &st))
+    fatal(std::string("gsnapdp_stage3_pass_compact: ") + gsnapdp_last_error());
   if (k.status) fatal("build_pairs_introns: a window outside the reference's domain (the reference aborts)");
   gsnapdp_List_T list = nullptr;
   for (int i = k.nout - 1; i >= 0; i--) {
-    const gsnapdp_s3_pair& p = out[(size_t)i];
-    if (p.src >= 0) {  // the path's own cell (List_push_existing)
-      RefList* l = cells[(size_t)p.src];
-      ((RefPair*)l->first)->disallowedp = (p.flags & GSNAPDP_S3_DISALLOWED) ? 1 : 0;
+    const int32_t cell = cells[(size_t)i];
+    if (cell >= 0) {  // the path's own cell (List_push_existing)
+      RefList* l = incells[(size_t)(cell & (GSNAPDP_S3_CELL_DISALLOWED - 1))];
+      ((RefPair*)l->first)->disallowedp = (cell & GSNAPDP_S3_CELL_DISALLOWED) ? 1 : 0;
       l->rest = (RefList*)list;
       list = (gsnapdp_List_T)l;
     } else {
+      const gsnapdp_s3_pair& p = news[(size_t)(-1 - cell)];
       if (p.flags & GSNAPDP_S3_GAPP) {
         list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump,
                                        (p.flags & GSNAPDP_S3_KNOWNGAPP) ? 1 : 0);

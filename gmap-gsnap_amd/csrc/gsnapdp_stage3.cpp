@@ -1389,12 +1389,25 @@ bool call_in_range(const gsnapdp_s3_call& c, int64_t npairs_in, size_t query_byt
 
 void gsnapdp::s3_parallel_for(int n, int grain, const std::function<void(int)>& fn) { Workers::get().run(n, grain, fn); }
 
-extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls,
-                                   const gsnapdp_s3_pair* pairs_in, int64_t npairs_in, const char* query,
-                                   const char* query_uc, size_t query_bytes, const gsnapdp_iit* iit,
-                                   gsnapdp_s3_pair* pairs_out, int64_t out_cap, gsnapdp_s3_stats* stats) {
+namespace {
+
+// Where a pass writes the returned lists: every cell as a full pair record
+// (pairs_out), or compactly (cells_out: the input pair's index, or a new pair
+// in new_out; include/gsnapdp.h gsnapdp_stage3_pass_compact).
+struct Out {
+  gsnapdp_s3_pair* pairs = nullptr;
+  int64_t cap = 0;
+  int32_t* cells = nullptr;
+  gsnapdp_s3_pair* news = nullptr;
+  int64_t new_cap = 0;
+};
+
+int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp_s3_pair* pairs_in,
+             int64_t npairs_in, const char* query, const char* query_uc, size_t query_bytes, const gsnapdp_iit* iit,
+             const Out& out, gsnapdp_s3_stats* stats) {
   if (!ctx || ncalls < 0 || npairs_in < 0 ||
-      (ncalls > 0 && (!calls || (npairs_in > 0 && !pairs_in) || !query || !query_uc || !pairs_out))) {
+      (ncalls > 0 && (!calls || (npairs_in > 0 && !pairs_in) || !query || !query_uc ||
+                      !(out.pairs || (out.cells && out.news))))) {
     gsnapdp__set_err("gsnapdp_stage3_pass: bad arguments");
     return -1;
   }
@@ -1488,19 +1501,27 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
   }
   gsnapdp::s3_exec_release(ctx, X);
   const auto t_out = clock::now();
-  // the returned lists, each path's at its running offset (lengths by the
-  // workers, offsets, then the copies by the workers)
-  std::vector<int64_t> first((size_t)ncalls + 1, 0);
+  // the returned lists, each path's at its running offset (lengths -- and
+  // the new pairs among them -- by the workers, offsets, then the copies)
+  std::vector<int64_t> first((size_t)ncalls + 1, 0), nfirst((size_t)ncalls + 1, 0);
   pool.run(ncalls, 16, [&](int i) {
     Path& k = paths[(size_t)i];
-    int n = 0;
+    int n = 0, nn = 0;
     if (!k.failed)
-      for (int p = k.pairs; p >= 0; p = k.A.rest(p)) n++;
+      for (int p = k.pairs; p >= 0; p = k.A.rest(p)) n++, nn += k.A.pairof(p) >= k.A.nin;
     first[(size_t)i + 1] = n;
+    nfirst[(size_t)i + 1] = nn;
   });
-  for (int i = 0; i < ncalls; i++) first[(size_t)i + 1] += first[(size_t)i];
-  if (first[(size_t)ncalls] > out_cap) {
-    gsnapdp__set_err("gsnapdp_stage3_pass: pairs_out is too small");
+  for (int i = 0; i < ncalls; i++) {
+    first[(size_t)i + 1] += first[(size_t)i];
+    nfirst[(size_t)i + 1] += nfirst[(size_t)i];
+  }
+  P.st.new_pairs = nfirst[(size_t)ncalls];
+  if (first[(size_t)ncalls] > out.cap || (!out.pairs && nfirst[(size_t)ncalls] > out.new_cap)) {
+    gsnapdp__set_err(std::string("gsnapdp_stage3_pass: ") + (first[(size_t)ncalls] > out.cap ? "the cell" : "the new-pair") +
+                     " output is too small (" + std::to_string(first[(size_t)ncalls]) + " cells, " +
+                     std::to_string(nfirst[(size_t)ncalls]) + " new pairs)");
+    if (stats) *stats = P.st;
     store_release(store);
     return -1;
   }
@@ -1512,7 +1533,20 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
     c.nout = (int32_t)(first[(size_t)i + 1] - first[(size_t)i]);
     if (k.failed) return;
     int64_t at = first[(size_t)i];
-    for (int p = k.pairs; p >= 0; p = k.A.rest(p)) pairs_out[at++] = k.A.out(p);
+    if (out.pairs) {
+      for (int p = k.pairs; p >= 0; p = k.A.rest(p)) out.pairs[at++] = k.A.out(p);
+    } else {
+      int64_t nat = nfirst[(size_t)i];
+      for (int p = k.pairs; p >= 0; p = k.A.rest(p)) {
+        const int pr = k.A.pairof(p);
+        if (pr < k.A.nin) {
+          out.cells[at++] = pr | ((k.A.flags[(size_t)pr] & GSNAPDP_S3_DISALLOWED) ? GSNAPDP_S3_CELL_DISALLOWED : 0);
+        } else {
+          out.news[nat] = k.A.extra[(size_t)(pr - k.A.nin)].p;
+          out.cells[at++] = (int32_t)(-1 - nat++);
+        }
+      }
+    }
     c.out_minor = k.minor;
     c.out_major = k.major;
     c.out_nintrons = k.nintrons;
@@ -1544,6 +1578,31 @@ extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int
   P.st.seconds[2] = total;
   if (stats) *stats = P.st;
   return 0;
+}
+
+}  // namespace
+
+extern "C" int gsnapdp_stage3_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls,
+                                   const gsnapdp_s3_pair* pairs_in, int64_t npairs_in, const char* query,
+                                   const char* query_uc, size_t query_bytes, const gsnapdp_iit* iit,
+                                   gsnapdp_s3_pair* pairs_out, int64_t out_cap, gsnapdp_s3_stats* stats) {
+  Out o;
+  o.pairs = pairs_out;
+  o.cap = out_cap;
+  return run_pass(ctx, calls, ncalls, pairs_in, npairs_in, query, query_uc, query_bytes, iit, o, stats);
+}
+
+extern "C" int gsnapdp_stage3_pass_compact(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls,
+                                           const gsnapdp_s3_pair* pairs_in, int64_t npairs_in, const char* query,
+                                           const char* query_uc, size_t query_bytes, const gsnapdp_iit* iit,
+                                           int32_t* cells_out, int64_t cells_cap, gsnapdp_s3_pair* new_out,
+                                           int64_t new_cap, gsnapdp_s3_stats* stats) {
+  Out o;
+  o.cells = cells_out;
+  o.cap = cells_cap;
+  o.news = new_out;
+  o.new_cap = new_cap;
+  return run_pass(ctx, calls, ncalls, pairs_in, npairs_in, query, query_uc, query_bytes, iit, o, stats);
 }
 
 // score_introns on the lists a pass returned (include/gsnapdp.h)

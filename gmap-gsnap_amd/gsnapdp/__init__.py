@@ -18,6 +18,7 @@ import os
 
 import numpy as np
 
+from .records import S3_DISALLOWED  # noqa: E402
 from .records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW,  # noqa: F401
                       IIT_INTERVAL, INTRON, INTRON_PATH, INTRON_SCORES, MAXENT_IN, MICRO_RESULT, MICRO_WINDOW, PAIR,
                       PATH_PAIR, RESULT, S3_CALL, S3_PAIR, S3_STATS, SJ_WINDOW, WINDOW)
@@ -108,6 +109,9 @@ def lib():
         L.gsnapdp_score_introns_device.restype = i32
         L.gsnapdp_stage3_pass.argtypes = [vp, vp, i32, vp, ctypes.c_int64, vp, vp, sz, vp, vp, ctypes.c_int64, vp]
         L.gsnapdp_stage3_pass.restype = i32
+        L.gsnapdp_stage3_pass_compact.argtypes = [vp, vp, i32, vp, ctypes.c_int64, vp, vp, sz, vp, vp,
+                                                  ctypes.c_int64, vp, ctypes.c_int64, vp]
+        L.gsnapdp_stage3_pass_compact.restype = i32
         L.gsnapdp_stage3_score_introns.argtypes = [vp, vp, i32, vp, vp, vp]
         L.gsnapdp_stage3_score_introns.restype = i32
         L.gsnapdp_iit_from_intervals.argtypes = [vp, i32]
@@ -518,6 +522,28 @@ class Context:
         n = int(c["nout"].sum())
         return c, out[:n], st[0]
 
+    def stage3_pass_compact(self, calls: np.ndarray, pairs_in: np.ndarray, query: np.ndarray,
+                            query_uc: np.ndarray, iit: "SplicingIIT" = None, bufs=None):
+        """gsnapdp_stage3_pass_compact: (calls, cells, new pairs, S3_STATS); a cell is
+        the input pair's index (| S3_CELL_DISALLOWED) or -1 - k for new[k]
+        (expand_compact rebuilds the lists).  `bufs`: reusable (cells, new) arrays."""
+        c = np.array(calls, dtype=S3_CALL, copy=True)
+        pi = np.ascontiguousarray(pairs_in, dtype=S3_PAIR)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        cap = self.stage3_capacity(c)
+        ncap = int((2 * c["querylength"].astype(np.int64) + 256).sum()) if len(c) else 1
+        if bufs is None or bufs[0].size < cap or bufs[1].size < ncap:
+            bufs = (np.empty(max(cap, 1), dtype=np.int32), np.empty(max(ncap, 1), dtype=S3_PAIR))
+        st = np.zeros(1, dtype=S3_STATS)
+        rc = lib().gsnapdp_stage3_pass_compact(self.h, _p(c), len(c), _p(pi) if pi.size else _p(bufs[1]), pi.size,
+                                               _p(q), _p(qu), min(q.size, qu.size),
+                                               iit.h if iit is not None else None, _p(bufs[0]), bufs[0].size,
+                                               _p(bufs[1]), bufs[1].size, _p(st))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_stage3_pass_compact: %s" % lib().gsnapdp_last_error().decode())
+        return c, bufs[0][:int(c["nout"].sum())], bufs[1][:int(st[0]["new_pairs"])], st[0]
+
     def stage3_score_introns(self, calls: np.ndarray, pairs_out: np.ndarray, iit: "SplicingIIT" = None):
         """score_introns (stage3.c:7935-8162) on the lists stage3_pass returned
         (gsnapdp_stage3_score_introns): one INTRON_SCORES per call."""
@@ -545,3 +571,20 @@ class Context:
                                          ctypes.c_void_p(stream) if stream else None)
         if rc != 0:
             raise GsnapdpError("maxent_device: %s" % lib().gsnapdp_last_error().decode())
+
+
+def expand_compact(calls: np.ndarray, pairs_in: np.ndarray, cells: np.ndarray, new: np.ndarray) -> np.ndarray:
+    """The full returned lists (as Context.stage3_pass writes them) from a compact
+    pass's cells: input pairs with src set (and DISALLOWED where the cell says),
+    new pairs as made."""
+    from .records import S3_CELL_DISALLOWED
+    out = np.empty(cells.size, dtype=S3_PAIR)
+    owner = np.repeat(np.arange(len(calls)), calls["nout"])
+    kept = cells >= 0
+    src = (cells & (S3_CELL_DISALLOWED - 1))[kept]
+    x = pairs_in[calls["first_pair"][owner[kept]] + src].copy()
+    x["src"] = src
+    x["flags"] |= np.where((cells[kept] & S3_CELL_DISALLOWED) != 0, S3_DISALLOWED, 0).astype(np.uint8)
+    out[kept] = x
+    out[~kept] = new[-1 - cells[~kept]]
+    return out

@@ -144,8 +144,9 @@ S3_CALL = np.dtype([(n, "<i4") for n in "first_pair npairs first_out nout qpos q
                    [("ref_seconds", "<f8")])
 assert S3_CALL.itemsize == 200
 S3_STATS = np.dtype([("rounds", "<i4"), ("windows", "<i4", 4), ("batches", "<i4", 4), ("undefined", "<i4"),
-                     ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3)])
-assert S3_STATS.itemsize == 72
+                     ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3), ("new_pairs", "<i8")])
+assert S3_STATS.itemsize == 80
+S3_CELL_DISALLOWED = 1 << 30  # gsnapdp_stage3_pass_compact: an input pair whose disallowedp the pass set
 
 # a splicing IIT's intervals (include/gsnapdp.h: gsnapdp_iit_interval); start > end is the minus sign,
 # type -1 none (an intron), 0 donor, 1 acceptor

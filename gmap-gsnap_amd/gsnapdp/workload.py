@@ -1244,3 +1244,238 @@ def stage3_calls(z, copies: int = 1):
         calls["first_out"] += (k * want.size).astype(np.int32)
         pin, q, qu, want = np.tile(pin, copies), np.tile(q, copies), np.tile(qu, copies), np.tile(want, copies)
     return calls, pin, q, qu, want
+
+
+# ---------------------------------------------------------------------------
+# BASELINE config 4 as stated: 50k synthetic 5 kbp transcripts through GMAP's
+# final intron pass (build_pairs_introns with finalp, stage3.c:8860-8875) and
+# score_introns (:9890-9941).  No gmapindex database or stage 2 exists here,
+# so the generator builds what stage 2 + passes 1-5 hand to pass 6 directly:
+# each transcript's path as insert_gapholders leaves it (stage3.c:817-900).
+
+# donor and acceptor consensus in the transcript's (sense) coordinates:
+# (anchor, offset, base); anchor 0 = the intron's first base, 1 = the base
+# after its last one.  exon ..AG | GTAAGT ... (14 nt pyrimidine tract) CAG | G exon
+_C4_DONOR = [(0, -2, "A"), (0, -1, "G"), (0, 0, "G"), (0, 1, "T"), (0, 2, "A"), (0, 3, "A"), (0, 4, "G"),
+             (0, 5, "T")]
+_C4_ACCEPTOR = [(1, -17 + i, b) for i, b in enumerate("TTTTCCCTTTCTTT")] + [(1, -3, "C"), (1, -2, "A"),
+                                                                          (1, -1, "G"), (1, 0, "G")]
+_CODE = {"A": 0, "C": 1, "G": 2, "T": 3}
+
+
+class C4Workload:
+    """One pass-6 call per transcript (gsnapdp_s3_call records), the paths
+    (gsnapdp_s3_pair, list order), the cDNAs, and the packed genome."""
+
+    def __init__(self, blocks, calls, pairs_in, query, query_uc, nintrons, genome_nt):
+        self.blocks, self.calls, self.pairs_in = blocks, calls, pairs_in
+        self.query, self.query_uc = query, query_uc
+        self.nintrons, self.genome_nt = nintrons, genome_nt
+
+
+def c4_transcripts(n: int = 50_000, seed: int = 4, shift_frac: float = 0.3, weak_frac: float = 0.2,
+                   sub_rate: float = 0.01, near: int = 15, chunk_genes: int = 2048) -> C4Workload:
+    """BASELINE config 4: `n` synthetic transcripts of 4.5-5.5 kbp,
+    8-12 exons, GT-AG introns of 80-5,000 nt, 1 % substitutions, a third of
+    them antisense (the cDNA aligns to the plus strand with cdna_direction -1,
+    CT-AC on the plus strand), on one genome of their gene regions.
+
+    The path of each is what pass 6 (stage3.c:8860-8875) receives: one pair per
+    aligned cDNA base in reversed alignment order (path->first is the last query
+    base) and one gapholder per intron (queryjump 0, genomejump the intron span
+    as insert_gapholders computes it, :868-871).  Stage 2 places ~30 % of the
+    boundaries 1-6 nt off the true site (the cDNA bases there then sit in the
+    intron), which pass 6 repairs; pairs within `near` of a boundary carry the
+    negative dynprogindex and '*' comp an earlier intron pass leaves there, the
+    rest '|' (or ' ' for a mismatch) and 0.  The donor / acceptor consensus is
+    planted at every intron (weakened at `weak_frac` of them).
+
+    Every parameter stream is its own generator ([seed, k]) drawn once per
+    gene or base in order, so the first m transcripts of c4_transcripts(n) are
+    c4_transcripts(m) for any n >= m (the reference pins a prefix)."""
+    from .records import MAXLENGTH1, MAXLENGTH2, S3_CALL, S3_PAIR
+
+    def S(k):
+        return np.random.default_rng([seed, k])
+
+    nex = S(1).integers(8, 13, size=n)
+    T = S(2).integers(4500, 5501, size=n).astype(np.int64)
+    ne, ni = int(nex.sum()), int(nex.sum()) - n
+    gene_of_ex = np.repeat(np.arange(n), nex)
+    first_ex = np.concatenate([[0], np.cumsum(nex)[:-1]])
+    w = S(3).random(ne) * 1.4 + 0.3
+    wsum = np.add.reduceat(w, first_ex)
+    exl = np.maximum(30, np.floor(T[gene_of_ex] * w / wsum[gene_of_ex])).astype(np.int64)
+    last = first_ex + nex - 1
+    exl[last] += T - np.add.reduceat(exl, first_ex)
+    assert exl.min() >= 30
+    first_in = first_ex - np.arange(n)  # introns of gene i: first_in[i] .. + nex[i] - 1
+    inl = S(4).integers(80, 5001, size=ni).astype(np.int64)
+    anti = S(5).random(n) < 1 / 3
+    u = S(6).random(ni)
+    shift = np.where(u < shift_frac, S(7).integers(1, 7, size=ni) * np.where(S(8).random(ni) < 0.5, 1, -1), 0)
+    weak = S(9).random(ni) < weak_frac
+    # plus-strand layout: 600 nt, exon 0, intron 0, ..., exon m, 600 nt
+    span = 1200 + np.add.reduceat(exl, first_ex) + np.add.reduceat(inl, first_in) * (nex > 1)
+    gene_start = np.concatenate([[0], np.cumsum(span)[:-1]]).astype(np.int64)
+    total = int(span.sum())
+    exon_local = np.arange(ne) - first_ex[gene_of_ex]
+    gene_of_in = np.repeat(np.arange(n), nex - 1)
+    intron_local = np.arange(ni) - first_in[gene_of_in]
+    # element lengths interleaved exon/intron per gene; exclusive sums within a gene
+    el = np.zeros(ne + ni, dtype=np.int64)
+    first_el = first_ex + first_in
+    el[first_el[gene_of_ex] + 2 * exon_local] = exl
+    el[first_el[gene_of_in] + 2 * intron_local + 1] = inl
+    cs = np.cumsum(el) - el
+    within = cs - cs[first_el][np.repeat(np.arange(n), 2 * nex - 1)]
+    ex_start = gene_start[gene_of_ex] + 600 + within[first_el[gene_of_ex] + 2 * exon_local]
+    in_start = gene_start[gene_of_in] + 600 + within[first_el[gene_of_in] + 2 * intron_local + 1]
+    in_end = in_start + inl
+    # the genome: random packed words (interleaved high / low), flags 0, X past the end
+    nblocks = (total + 31) // 32
+    hl = S(10).integers(0, 1 << 32, size=2 * nblocks, dtype=np.uint32)
+    blocks = np.empty(3 * nblocks + 4, dtype=np.uint32)
+    blocks[0:3 * nblocks:3] = hl[0::2]
+    blocks[1:3 * nblocks:3] = hl[1::2]
+    blocks[2:3 * nblocks:3] = 0
+    blocks[3 * nblocks:] = 0xFFFFFFFF
+    del hl
+    tail = nblocks * 32 - total
+    for b in range(32 - tail, 32):
+        blocks[3 * (nblocks - 1) + 2] |= np.uint32(1) << np.uint32(b)
+        word = 3 * (nblocks - 1) + (1 if b < 16 else 0)
+        blocks[word] |= np.uint32(3) << np.uint32(2 * (b & 15))
+
+    def plant(pos, code):  # one base per intron at a time: distinct words
+        pos = np.asarray(pos, dtype=np.int64)
+        bit = (pos & 31).astype(np.uint32)
+        word = (pos >> 5) * 3 + np.where(bit < 16, 1, 0)
+        sh = (2 * (bit & 15)).astype(np.uint32)
+        blocks[word] = (blocks[word] & ~(np.uint32(3) << sh)) | (np.asarray(code, np.uint32) << sh)
+
+    comp = {"A": "T", "C": "G", "G": "C", "T": "A"}
+    keep_weak_tract = np.arange(14) % 2 == 0
+    for motif in (_C4_DONOR, _C4_ACCEPTOR):
+        for j, (anchor, off, base) in enumerate(motif):
+            sel = np.ones(ni, bool)
+            if motif is _C4_DONOR and off >= 2:
+                sel = ~weak  # weak donors keep random +3..+5 (and +2)
+            if motif is _C4_ACCEPTOR and j < 14:
+                sel = ~weak | keep_weak_tract[j]
+            a = in_start[sel]
+            b = in_end[sel]
+            an = anti[gene_of_in[sel]]
+            site = np.where(anchor == 0, a, b)
+            other = np.where(anchor == 0, b, a)
+            # antisense: sense offset `off` from the sense anchor, mirrored on the plus strand
+            pos = np.where(an, other - 1 - off, site + off)
+            code = np.where(an, _CODE[comp[base]], _CODE[base])
+            plant(pos, code)
+    # pass-6 calls
+    calls = np.zeros(n, dtype=S3_CALL)
+    npairs = T + (nex - 1)
+    calls["npairs"] = npairs
+    calls["first_pair"] = np.concatenate([[0], np.cumsum(npairs)[:-1]])
+    qlen_pad = T + 8 - (T & 3)
+    calls["qpos"] = np.concatenate([[0], np.cumsum(qlen_pad)[:-1]])
+    calls["querylength"] = T
+    calls["chroffset"] = 0
+    calls["chrhigh"] = total
+    calls["chrpos"] = gene_start
+    calls["chrnum"] = 1
+    calls["genomiclength"] = span
+    calls["cdna_direction"] = np.where(anti, -1, 1)
+    calls["watsonp"] = 1
+    calls["finalp"] = 1
+    for f, v in (("maxpeelback", 11), ("nullgap", 600), ("extramaterial_paired", 8), ("extraband_single", 3),
+                 ("extraband_paired", 7), ("close_indels_mode", 1), ("novelsplicingp", 1), ("splicingp", 1)):
+        calls[f] = v
+    calls["defect_rate"] = sub_rate
+    calls["maxlength1"] = MAXLENGTH1
+    calls["maxlength2"] = MAXLENGTH2
+    calls["in_minor"] = 1
+    calls["in_major"] = -nex
+    if total >= 1 << 31:
+        raise ValueError("C4 genome of %d nt does not fit Genomicpos_T arithmetic on int32 paths" % total)
+    pairs = np.zeros(int(npairs.sum()), dtype=S3_PAIR)
+    query = np.zeros(int(qlen_pad.sum()), dtype=np.uint8)
+    rs, rk = S(11), S(12)  # substitutions: one draw per cDNA base, in order
+    qstart_ex = np.concatenate([[0], np.cumsum(exl)[:-1]]) - np.repeat(np.concatenate([[0], np.cumsum(T)[:-1]]), nex)
+    for g0 in range(0, n, chunk_genes):
+        g1 = min(n, g0 + chunk_genes)
+        e0, e1 = int(first_ex[g0]), int(first_ex[g1 - 1] + nex[g1 - 1])
+        i0, i1 = int(first_in[g0]), int(first_in[g1 - 1] + nex[g1 - 1] - 1)
+        # every cDNA base of the chunk: its gene, query position and true genome position
+        L = exl[e0:e1]
+        gq = np.repeat(gene_of_ex[e0:e1], L)
+        q = np.repeat(qstart_ex[e0:e1], L) + (np.arange(int(L.sum())) - np.repeat(np.cumsum(L) - L, L))
+        gpos = np.repeat(ex_start[e0:e1], L) + (np.arange(int(L.sum())) - np.repeat(np.cumsum(L) - L, L))
+        base = decode_blocks(blocks, gpos)
+        m = rs.random(base.size) < sub_rate
+        k = rk.integers(1, 4, size=base.size)
+        cd = np.where(m, ACGT[(np.searchsorted(ACGT, base) + k) % 4], base).astype(np.uint8)
+        # stage 2's boundary placement: the path's genome position of every cDNA base
+        qb_true = (qstart_ex[e0:e1] + exl[e0:e1])[np.setdiff1d(np.arange(e1 - e0), last[g0:g1] - e0)]
+        ig = np.arange(i0, i1)
+        s = shift[ig]
+        pg = gpos.copy()
+        qofs = np.concatenate([[0], np.cumsum(T[g0:g1])[:-1]])  # chunk-local offset of each gene's bases
+        gl = gene_of_in[ig] - g0
+        for d in range(1, 7):
+            pos_ = s >= d  # exon e continues d-1 bases into the intron
+            idx = qofs[gl[pos_]] + qb_true[pos_] + (d - 1)
+            pg[idx] = in_start[ig[pos_]] + (d - 1)
+            neg = -s >= d  # exon e+1 starts d bases early, at the intron's end
+            idx = qofs[gl[neg]] + qb_true[neg] - d
+            pg[idx] = in_end[ig[neg]] - d
+        qb = qb_true + s  # the path's boundary: first query base after the gap
+        gch = decode_blocks(blocks, pg)
+        # distance to the gene's nearest boundary, for dynprogindex / comp
+        near_mask = np.zeros(base.size, bool)
+        dpi = np.zeros(base.size, np.int32)
+        for d in range(-near, near):
+            idx = qofs[gl] + qb + d
+            ok = (qb + d >= 0) & (qb + d < T[g0:g1][gl])
+            near_mask[idx[ok]] = True
+            dpi[idx[ok]] = -(intron_local[ig][ok] + 1)
+        match = cd == gch
+        # list order: path->first is the last query base; gap k of a gene sits after
+        # the pair of its boundary qb_k (ascending k): before pair q lie the
+        # T-1-q later pairs and the gaps whose boundary is > q
+        nb_after = np.zeros(base.size, np.int64)  # gaps with qb > q, per base
+        gap_rank = (nex[gene_of_in[ig]] - 2) - intron_local[ig]  # = #(qb' > qb_k) within the gene
+        np.add.at(nb_after, qofs[gl] + qb - 1, 1)
+        # suffix counts within each gene: gaps with boundary > q  = sum over q' >= q of marks at qb-1
+        rev_cum = np.cumsum(nb_after[::-1])[::-1]
+        gstart_chunk = np.repeat(qofs, T[g0:g1])
+        gend_total = np.repeat(np.append(rev_cum[qofs[1:]], 0) if g1 - g0 > 1 else np.array([0]), T[g0:g1])
+        after = rev_cum - gend_total  # marks at q' >= q within the gene = gaps with qb > q
+        fp = calls["first_pair"][gq]
+        lpos = fp + (T[gq] - 1 - q) + after
+        rec = pairs[lpos] if False else None  # (written field by field below)
+        pairs["querypos"][lpos] = q
+        pairs["genomepos"][lpos] = pg - gene_start[gq]
+        pairs["dynprogindex"][lpos] = np.where(near_mask, dpi, 0)
+        pairs["cdna"][lpos] = cd
+        pairs["genome"][lpos] = gch
+        pairs["comp"][lpos] = np.where(match, np.where(near_mask, ord("*"), ord("|")), ord(" "))
+        pairs["src"][lpos] = 0
+        # gapholders: after the pair of qb (list order), between qb - 1 and qb
+        gg = gene_of_in[ig]
+        gpos_hi = pg[qofs[gl] + qb]
+        gpos_lo = pg[qofs[gl] + qb - 1]
+        gl_pos = calls["first_pair"][gg] + (T[gg] - qb) + gap_rank
+        pairs["querypos"][gl_pos] = -1
+        pairs["genomepos"][gl_pos] = -1
+        pairs["queryjump"][gl_pos] = 0
+        pairs["genomejump"][gl_pos] = gpos_hi - gpos_lo - 1
+        pairs["cdna"][gl_pos] = ord(" ")
+        pairs["comp"][gl_pos] = ord(" ")
+        pairs["genome"][gl_pos] = ord(" ")
+        pairs["flags"][gl_pos] = 1  # GSNAPDP_S3_GAPP
+        # the cDNA bytes
+        qp = calls["qpos"][gq] + q
+        query[qp] = cd
+    calls["first_pair"] = calls["first_pair"]  # (records are final)
+    return C4Workload(blocks, calls, pairs, query, query.copy(), int(ni), total)

@@ -605,8 +605,10 @@ typedef struct gsnapdp_s3_stats {
                          * uninitialised indices (dynprog.c:4055); taken as NULL here */
   int32_t failed;       /* paths with status -1 */
   int32_t pad;
-  double seconds[3];    /* wall time: host list work (peels, traversals, expansion), batched
-                         * gap-family round trips (staging, kernels, copies), whole pass */
+  double seconds[3];    /* wall time: the host's (packing, launches, peels, traversals,
+                         * expansion), the time it waited for a batch, the whole pass */
+  int64_t new_pairs;    /* pairs the pass made among the returned lists (the new_out a compact
+                         * pass needs; written also when new_out was too small) */
 } gsnapdp_s3_stats;
 
 /* Runs the pass; pairs_in holds npairs_in pairs and query / query_uc
@@ -624,6 +626,23 @@ int gsnapdp_stage3_pass(gsnapdp_ctx *ctx, gsnapdp_s3_call *calls, int ncalls,
                         const gsnapdp_s3_pair *pairs_in, int64_t npairs_in, const char *query,
                         const char *query_uc, size_t query_bytes, const gsnapdp_iit *iit,
                         gsnapdp_s3_pair *pairs_out, int64_t out_cap, gsnapdp_s3_stats *stats);
+
+/* The same pass with the returned lists written compactly: the pairs a path
+ * keeps are named, not copied.  cells_out[first_out + j] for the j-th cell of
+ * call i's list is
+ *   s (| GSNAPDP_S3_CELL_DISALLOWED)  input pair s of the call's path (the pass
+ *                                     set its disallowedp, stage3.c:5873-5880)
+ *   -1 - k                            new_out[k], a pair the pass made
+ * (a call's new pairs are consecutive in new_out, in list order).  cells_cap
+ * as out_cap above; new_cap too small fails the pass with stats->new_pairs
+ * set to the size needed.  This is what a caller that owns its Pair_T cells
+ * needs (the drop-in relinks them), at 4 bytes per kept pair instead of 28. */
+enum { GSNAPDP_S3_CELL_DISALLOWED = 1 << 30 };
+int gsnapdp_stage3_pass_compact(gsnapdp_ctx *ctx, gsnapdp_s3_call *calls, int ncalls,
+                                const gsnapdp_s3_pair *pairs_in, int64_t npairs_in, const char *query,
+                                const char *query_uc, size_t query_bytes, const gsnapdp_iit *iit,
+                                int32_t *cells_out, int64_t cells_cap, gsnapdp_s3_pair *new_out, int64_t new_cap,
+                                gsnapdp_s3_stats *stats);
 
 /* score_introns (stage3.c:7935-8162) on the lists a pass returned: for every
  * call with status 0, its list reversed into path order (as stage3_compute

@@ -698,6 +698,40 @@ def gmap_cins_case(seed: int = 21, ngenes: int = 60, genome_len: int = 500_000) 
                                               np.cumsum(sel["nout"])[:-1])) if a.tobytes() != b.tobytes())))
 
 
+def s3_digests(calls, pairs) -> np.ndarray:
+    """sha256 of each call's returned list (S3_PAIR records, list order)"""
+    import hashlib
+    out = np.zeros((len(calls), 32), np.uint8)
+    for i, c in enumerate(calls):
+        b = pairs[int(c["first_out"]):int(c["first_out"]) + int(c["nout"])].tobytes()
+        out[i] = np.frombuffer(hashlib.sha256(b).digest(), np.uint8)
+    return out
+
+
+def c4_pinned_case(n: int = 2000, seed: int = 4, full: int = 50) -> None:
+    """BASELINE config 4's transcripts (workload.c4_transcripts), the first `n`
+    of the 50k, through the reference's own build_pairs_introns (final pass)
+    and score_introns on its lists (oracle/s3_replay.c --si).  The inputs are
+    regenerated from the seed by the tests (the generator is prefix-stable), so
+    the fixture holds the reference's outputs: every call's counters and
+    score_introns results, a sha256 of every returned list, and the first
+    `full` lists in full."""
+    from gsnapdp.records import S3_CALL
+    w = W.c4_transcripts(n, seed=seed)
+    rc, rp, sic, sip = s3_replay(w.blocks, w.calls, w.pairs_in, w.query, w.query_uc, si=True)
+    assert (rc["status"] == 0).all()
+    keep = [f for f in S3_CALL.names if f.startswith("out_")] + ["nout", "shiftp", "incompletep", "ref_seconds"]
+    res = {f: rc[f] for f in keep}
+    nfull = int(rc["nout"][:full].sum())
+    np.savez_compressed(os.path.join(OUT, "c4_pinned.npz"), n=np.int32(n), seed=np.int32(seed),
+                        digests=s3_digests(rc, rp), lists_head=rp[:nfull], si_calls=sic,
+                        **{"ref_" + k: v for k, v in res.items()})
+    print("c4_pinned: %d transcripts, %d introns, %d path pairs, %d returned pairs, reference %.3f s "
+          "(%.0f paths/s, 1 thread); shifted %d, bad-intron flags %d" %
+          (n, w.nintrons, w.pairs_in.size, rp.size, float(rc["ref_seconds"].sum()),
+           n / float(rc["ref_seconds"].sum()), int(rc["shiftp"].sum()), int((sic["nbadintrons"] > 0).sum())))
+
+
 def gmap_her2_case() -> None:
     """BASELINE config 1: the gap windows of `gmap -A -g ss.chr17test ss.her2`
     (the reference's own align.test, tests/align.test.in:9-10), whose output
@@ -899,6 +933,7 @@ def main() -> None:
         ("gmap_trace", lambda: gmap_trace_case()),
         ("gmap_her2", lambda: gmap_her2_case()),
         ("gmap_cins", lambda: gmap_cins_case()),
+        ("c4_pinned", lambda: c4_pinned_case()),
     ]
     for name, fn in cases:
         if not only or name in only:

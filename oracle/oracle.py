@@ -209,3 +209,113 @@ def score_introns(paths: np.ndarray, introns: np.ndarray) -> np.ndarray:
 
 def pairs_of(pairs: np.ndarray, off: np.ndarray, npairs: np.ndarray, i: int) -> np.ndarray:
     return pairs[off[i]:off[i] + npairs[i]]
+
+
+# ---- the stage-3 pass on the CPU (oracle/_build/libstage3_cpu.so): the pass's host
+# code with its DP batches served by this restatement, on GSNAPDP_S3_THREADS threads.
+# bench.py's same-box baseline for the pass, and the checker of the full C4 set.
+S3LIB_PATH = os.path.join(HERE, "_build", "libstage3_cpu.so")
+_s3lib = None
+
+
+def s3lib():
+    global _s3lib
+    if _s3lib is None:
+        if not os.path.exists(S3LIB_PATH):
+            build()
+        L = ctypes.CDLL(S3LIB_PATH)
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+        L.gsnapdp_create.argtypes = [i32, vp, ctypes.c_size_t, i32]
+        L.gsnapdp_create.restype = vp
+        L.gsnapdp_destroy.argtypes = [vp]
+        L.gsnapdp_load_maxent_tables.argtypes = [vp, vp, ctypes.c_size_t]
+        L.gsnapdp_load_maxent_tables.restype = i32
+        L.gsnapdp_stage3_pass.argtypes = [vp, vp, i32, vp, i64, vp, vp, ctypes.c_size_t, vp, vp, i64, vp]
+        L.gsnapdp_stage3_pass.restype = i32
+        L.gsnapdp_stage3_pass_compact.argtypes = [vp, vp, i32, vp, i64, vp, vp, ctypes.c_size_t, vp, vp, i64, vp,
+                                                  i64, vp]
+        L.gsnapdp_stage3_pass_compact.restype = i32
+        L.gsnapdp_stage3_score_introns.argtypes = [vp, vp, i32, vp, vp, vp]
+        L.gsnapdp_stage3_score_introns.restype = i32
+        L.gsnapdp_iit_from_intervals.argtypes = [vp, i32]
+        L.gsnapdp_iit_from_intervals.restype = vp
+        L.gsnapdp_iit_free.argtypes = [vp]
+        L.gsnapdp_oracle_stash_reset.argtypes = []
+        L.s3cpu_last_error.restype = ctypes.c_char_p
+        _s3lib = L
+    return _s3lib
+
+
+class Stage3Cpu:
+    """gsnapdp_stage3_pass / gsnapdp_stage3_score_introns with the batches served
+    by the restatement (test / baseline infrastructure)."""
+
+    def __init__(self, blocks: np.ndarray):
+        from gsnapdp.records import S3_CALL, S3_PAIR, S3_STATS, IIT_INTERVAL  # noqa: F401
+        L = s3lib()
+        self.blocks = np.ascontiguousarray(blocks, dtype=np.uint32)
+        self.h = L.gsnapdp_create(0, self.blocks.ctypes.data, self.blocks.size, 0)
+        tables = np.fromfile(TABLES_PATH, dtype=np.float64)
+        if not self.h or L.gsnapdp_load_maxent_tables(self.h, tables.ctypes.data, tables.size):
+            raise RuntimeError("libstage3_cpu: context")
+
+    def run_compact(self, calls, pairs_in, query, query_uc):
+        """gsnapdp_stage3_pass_compact: (calls, cells, new pairs, S3_STATS)"""
+        from gsnapdp.records import S3_CALL, S3_PAIR, S3_STATS
+        L = s3lib()
+        c = np.array(calls, dtype=S3_CALL, copy=True)
+        pi = np.ascontiguousarray(pairs_in, dtype=S3_PAIR)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        cap = int((2 * (c["querylength"].astype(np.int64) + c["npairs"]) + 64).sum()) if len(c) else 1
+        ncap = int((2 * c["querylength"].astype(np.int64) + 256).sum()) if len(c) else 1
+        cells = np.empty(max(cap, 1), dtype=np.int32)
+        new = np.empty(max(ncap, 1), dtype=S3_PAIR)
+        st = np.zeros(1, dtype=S3_STATS)
+        try:
+            if L.gsnapdp_stage3_pass_compact(self.h, c.ctypes.data, len(c), pi.ctypes.data, pi.size, q.ctypes.data,
+                                             qu.ctypes.data, min(q.size, qu.size), None, cells.ctypes.data, cap,
+                                             new.ctypes.data, ncap, st.ctypes.data):
+                raise RuntimeError("libstage3_cpu pass: %s" % L.s3cpu_last_error().decode())
+        finally:
+            L.gsnapdp_oracle_stash_reset()
+        return c, cells[:int(c["nout"].sum())], new[:int(st[0]["new_pairs"])], st[0]
+
+    def run(self, calls, pairs_in, query, query_uc, intervals=None, introns=False):
+        """(calls with out fields, the returned lists, S3_STATS[, INTRON_SCORES])"""
+        from gsnapdp.records import IIT_INTERVAL, S3_CALL, S3_PAIR, S3_STATS
+        L = s3lib()
+        c = np.array(calls, dtype=S3_CALL, copy=True)
+        pi = np.ascontiguousarray(pairs_in, dtype=S3_PAIR)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        cap = int((2 * (c["querylength"].astype(np.int64) + c["npairs"]) + 64).sum()) if len(c) else 1
+        out = np.empty(max(cap, 1), dtype=S3_PAIR)
+        st = np.zeros(1, dtype=S3_STATS)
+        iit = None
+        if intervals is not None:
+            iv = np.ascontiguousarray(intervals, dtype=IIT_INTERVAL)
+            iit = L.gsnapdp_iit_from_intervals(iv.ctypes.data if iv.size else None, iv.size)
+        try:
+            if L.gsnapdp_stage3_pass(self.h, c.ctypes.data, len(c), pi.ctypes.data, pi.size, q.ctypes.data,
+                                     qu.ctypes.data, min(q.size, qu.size), iit, out.ctypes.data, cap,
+                                     st.ctypes.data):
+                raise RuntimeError("libstage3_cpu pass: %s" % L.s3cpu_last_error().decode())
+            n = int(c["nout"].sum())
+            res = (c, out[:n], st[0])
+            if introns:
+                sc = np.zeros(len(c), dtype=INTRON_SCORES)
+                if L.gsnapdp_stage3_score_introns(self.h, c.ctypes.data, len(c), out.ctypes.data, iit,
+                                                  sc.ctypes.data):
+                    raise RuntimeError("libstage3_cpu score_introns: %s" % L.s3cpu_last_error().decode())
+                res = res + (sc,)
+        finally:
+            if iit:
+                L.gsnapdp_iit_free(iit)
+            L.gsnapdp_oracle_stash_reset()
+        return res
+
+    def close(self):
+        if self.h:
+            s3lib().gsnapdp_destroy(self.h)
+            self.h = None
