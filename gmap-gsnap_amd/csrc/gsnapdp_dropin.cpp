@@ -1560,27 +1560,21 @@ gsnapdp_List_T Gsnapdp_score_introns(double* avg_donor_score, double* avg_accept
   return path ? List_reverse(path) : path;
 }
 
-// build_pairs_introns (stage3.c:7735-7901), the reference's static function with
-// its signature (non-PMAP, non-WASTE), for a stage3.c that calls it here
-// (:8766, :8865): the path goes through gsnapdp_stage3_pass (every gap filled
-// on the GPU, the peels and accept rules on the host) and comes back as the
-// reference's list: its own cells for the pairs it keeps (disallowedp set where
-// the reference sets it, :5873-5880) and the host's Pairpool for the pairs the
-// fills made.  The genome is the context's (genome / genomicseg_ptr unused).
-gsnapdp_List_T Gsnapdp_build_pairs_introns(
-    gsnapdp_bool* shiftp, gsnapdp_bool* incompletep, int* nintrons, int* nnonintrons, int* intronlen,
-    int* nonintronlen, int* dynprogindex_minor, int* dynprogindex_major, gsnapdp_List_T path, int chrnum,
-    gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
-    gsnapdp_Genome_T /*genome*/, int querylength, int genomiclength, char* queryseq_ptr, char* queryuc_ptr,
-    char* /*genomicseg_ptr*/, char* /*genomicuc_ptr*/, gsnapdp_bool use_genomicseg_p, int cdna_direction,
-    gsnapdp_bool watsonp, gsnapdp_bool jump_late_p, int maxpeelback, int nullgap, int extramaterial_paired,
-    int extraband_single, int extraband_paired, double defect_rate, int close_indels_mode,
-    gsnapdp_Pairpool_T pairpool, gsnapdp_Dynprog_T dynprogL, gsnapdp_Dynprog_T dynprogM,
-    gsnapdp_Dynprog_T dynprogR, gsnapdp_bool finalp) {
-  if (use_genomicseg_p) fatal("build_pairs_introns on a genomic segment is not served by the batched pass");
+}  // extern "C"
+
+namespace {
+
+// One path through gsnapdp_stage3_pass_compact (k holds the call's arguments and
+// in-counters) and back as the reference's list: its own cells for the pairs it
+// keeps (disallowedp set where the reference sets it, stage3.c:5873-5880) and the
+// host's Pairpool for the pairs the fills made.
+gsnapdp_List_T pass_one(gsnapdp_s3_call& k, gsnapdp_List_T path, char* queryseq_ptr, char* queryuc_ptr,
+                        gsnapdp_Pairpool_T pairpool, const gsnapdp_iit* iit, const char* what) {
   gsnapdp_ctx* c = shared_ctx(true);
-  std::vector<RefList*> incells;
-  std::vector<gsnapdp_s3_pair> in;
+  thread_local std::vector<RefList*> incells;  // per gmap worker thread
+  thread_local std::vector<gsnapdp_s3_pair> in;
+  incells.clear();
+  in.clear();
   for (RefList* l = (RefList*)path; l; l = l->rest) {
     const RefPair* x = (const RefPair*)l->first;
     gsnapdp_s3_pair p;
@@ -1598,9 +1592,67 @@ gsnapdp_List_T Gsnapdp_build_pairs_introns(
     in.push_back(p);
     incells.push_back(l);
   }
+  k.npairs = (int32_t)in.size();
+  const int64_t cap = 2 * ((int64_t)k.querylength + k.npairs) + 64;
+  thread_local std::vector<int32_t> cells;  // the returned list, compactly
+  thread_local std::vector<gsnapdp_s3_pair> news;
+  cells.resize((size_t)cap);
+  news.resize((size_t)(2 * (int64_t)k.querylength + 256));
+  gsnapdp_s3_stats st;
+  if (gsnapdp_stage3_pass_compact(c, &k, 1, in.data(), (int64_t)in.size(), queryseq_ptr, queryuc_ptr,
+                                  (size_t)k.querylength, iit, cells.data(), cap, news.data(), (int64_t)news.size(),
+                                  &st))
+    fatal(std::string("gsnapdp_stage3_pass_compact: ") + gsnapdp_last_error());
+  if (k.status) fatal(std::string(what) + ": a window outside the reference's domain (the reference aborts)");
+  gsnapdp_List_T list = nullptr;
+  for (int i = k.nout - 1; i >= 0; i--) {
+    const int32_t cell = cells[(size_t)i];
+    if (cell >= 0) {  // the path's own cell (List_push_existing)
+      RefList* l = incells[(size_t)(cell & (GSNAPDP_S3_CELL_DISALLOWED - 1))];
+      ((RefPair*)l->first)->disallowedp = (cell & GSNAPDP_S3_CELL_DISALLOWED) ? 1 : 0;
+      l->rest = (RefList*)list;
+      list = (gsnapdp_List_T)l;
+    } else {
+      const gsnapdp_s3_pair& p = news[(size_t)(-1 - cell)];
+      if (p.flags & GSNAPDP_S3_GAPP) {
+        list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump,
+                                       (p.flags & GSNAPDP_S3_KNOWNGAPP) ? 1 : 0);
+        ((RefPair*)((RefList*)list)->first)->comp = p.comp;  // a microexon's gapchar (dynprog.c:6991)
+      } else {
+        list = Pairpool_push(list, pairpool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome, p.dynprogindex);
+      }
+      // a pair an earlier fill of this call made and a later genome gap peeled
+      // and put back keeps disallowedp = true (stage3.c:5873-5880); both pushes
+      // start it false (pairpool.c:212, :400)
+      ((RefPair*)((RefList*)list)->first)->disallowedp = (p.flags & GSNAPDP_S3_DISALLOWED) ? 1 : 0;
+    }
+  }
+  return list;
+}
+
+}  // namespace
+
+extern "C" {
+
+// build_pairs_introns (stage3.c:7735-7901), the reference's static function with
+// its signature (non-PMAP, non-WASTE), for a stage3.c that calls it here
+// (:8766, :8865): the path goes through gsnapdp_stage3_pass (every gap filled
+// on the GPU, the peels and accept rules on the host).  The genome is the
+// context's (genome / genomicseg_ptr unused).
+gsnapdp_List_T Gsnapdp_build_pairs_introns(
+    gsnapdp_bool* shiftp, gsnapdp_bool* incompletep, int* nintrons, int* nnonintrons, int* intronlen,
+    int* nonintronlen, int* dynprogindex_minor, int* dynprogindex_major, gsnapdp_List_T path, int chrnum,
+    gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+    gsnapdp_Genome_T /*genome*/, int querylength, int genomiclength, char* queryseq_ptr, char* queryuc_ptr,
+    char* /*genomicseg_ptr*/, char* /*genomicuc_ptr*/, gsnapdp_bool use_genomicseg_p, int cdna_direction,
+    gsnapdp_bool watsonp, gsnapdp_bool jump_late_p, int maxpeelback, int nullgap, int extramaterial_paired,
+    int extraband_single, int extraband_paired, double defect_rate, int close_indels_mode,
+    gsnapdp_Pairpool_T pairpool, gsnapdp_Dynprog_T dynprogL, gsnapdp_Dynprog_T dynprogM,
+    gsnapdp_Dynprog_T dynprogR, gsnapdp_bool finalp) {
+  if (use_genomicseg_p) fatal("build_pairs_introns on a genomic segment is not served by the batched pass");
   gsnapdp_s3_call k;
   memset(&k, 0, sizeof(k));
-  k.npairs = (int32_t)in.size();
+  k.pass = GSNAPDP_S3_INTRONS;
   k.querylength = querylength;
   k.chroffset = chroffset;
   k.chrhigh = chrhigh;
@@ -1632,42 +1684,10 @@ gsnapdp_List_T Gsnapdp_build_pairs_introns(
   // Stage3_setup's flags as gmap derives them from Dynprog_setup's (gmap.c:3828-3849)
   k.novelsplicingp = g.novelsplicingp ? 1 : 0;
   k.splicingp = (g.novelsplicingp || g.splicing_iit) ? 1 : 0;
-  const int64_t cap = 2 * ((int64_t)querylength + k.npairs) + 64;
-  thread_local std::vector<int32_t> cells;  // the returned list, compactly (per gmap worker thread)
-  thread_local std::vector<gsnapdp_s3_pair> news;
-  cells.resize((size_t)cap);
-  news.resize((size_t)(2 * (int64_t)querylength + 256));
-  gsnapdp_s3_stats st;
   // the splicing IIT of Dynprog_setup, asked through the host's own iit-read
   // functions (every genome-gap window's known-site record)
-  if (gsnapdp_stage3_pass_compact(c, &k, 1, in.data(), (int64_t)in.size(), queryseq_ptr, queryuc_ptr,
-                                  (size_t)querylength, g.iit ? host_iit() : nullptr, cells.data(), cap, news.data(),
-                                  (int64_t)news.size(), &st))
-    fatal(std::string("gsnapdp_stage3_pass_compact: ") + gsnapdp_last_error());
-  if (k.status) fatal("build_pairs_introns: a window outside the reference's domain (the reference aborts)");
-  gsnapdp_List_T list = nullptr;
-  for (int i = k.nout - 1; i >= 0; i--) {
-    const int32_t cell = cells[(size_t)i];
-    if (cell >= 0) {  // the path's own cell (List_push_existing)
-      RefList* l = incells[(size_t)(cell & (GSNAPDP_S3_CELL_DISALLOWED - 1))];
-      ((RefPair*)l->first)->disallowedp = (cell & GSNAPDP_S3_CELL_DISALLOWED) ? 1 : 0;
-      l->rest = (RefList*)list;
-      list = (gsnapdp_List_T)l;
-    } else {
-      const gsnapdp_s3_pair& p = news[(size_t)(-1 - cell)];
-      if (p.flags & GSNAPDP_S3_GAPP) {
-        list = Pairpool_push_gapholder(list, pairpool, p.queryjump, p.genomejump,
-                                       (p.flags & GSNAPDP_S3_KNOWNGAPP) ? 1 : 0);
-        ((RefPair*)((RefList*)list)->first)->comp = p.comp;  // a microexon's gapchar (dynprog.c:6991)
-      } else {
-        list = Pairpool_push(list, pairpool, p.querypos, p.genomepos, p.cdna, p.comp, p.genome, p.dynprogindex);
-      }
-      // a pair an earlier fill of this call made and a later genome gap peeled
-      // and put back keeps disallowedp = true (stage3.c:5873-5880); both pushes
-      // start it false (pairpool.c:212, :400)
-      ((RefPair*)((RefList*)list)->first)->disallowedp = (p.flags & GSNAPDP_S3_DISALLOWED) ? 1 : 0;
-    }
-  }
+  gsnapdp_List_T list = pass_one(k, path, queryseq_ptr, queryuc_ptr, pairpool, g.iit ? host_iit() : nullptr,
+                                 "build_pairs_introns");
   *shiftp = k.shiftp ? 1 : 0;
   *incompletep = k.incompletep ? 1 : 0;
   *nintrons = k.out_nintrons;
@@ -1676,6 +1696,46 @@ gsnapdp_List_T Gsnapdp_build_pairs_introns(
   *nonintronlen = k.out_nonintronlen;
   *dynprogindex_minor = k.out_minor;
   *dynprogindex_major = k.out_major;
+  return list;
+}
+
+// build_pairs_singles (stage3.c:7454-7583), passes 2A / 2C / 7C of path_compute
+// (:8671, :8700, :8938), with the reference's signature (non-PMAP, non-WASTE):
+// every single gap (queryjump <= nullgap, neither a cDNA insertion nor an
+// intron) is filled by traverse_single_gap (forcep false) in the batched pass;
+// the query is the whole NUL-terminated query (Sequence_fullpointer).
+gsnapdp_List_T Gsnapdp_build_pairs_singles(int* dynprogindex, gsnapdp_List_T path, gsnapdp_Genomicpos_T chroffset,
+                                           gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+                                           gsnapdp_Genomicpos_T genomiclength, char* queryseq_ptr,
+                                           char* queryuc_ptr, char* /*genomicseg_ptr*/, char* /*genomicuc_ptr*/,
+                                           int cdna_direction, gsnapdp_bool watsonp, gsnapdp_bool jump_late_p,
+                                           int maxpeelback, int nullgap, int extraband_single, double defect_rate,
+                                           int close_indels_mode, gsnapdp_Pairpool_T pairpool,
+                                           gsnapdp_Dynprog_T dynprogM) {
+  gsnapdp_s3_call k;
+  memset(&k, 0, sizeof(k));
+  k.pass = GSNAPDP_S3_SINGLES;
+  k.querylength = (int32_t)strlen(queryseq_ptr);
+  k.chroffset = chroffset;
+  k.chrhigh = chrhigh;
+  k.chrpos = chrpos;
+  k.genomiclength = (int32_t)genomiclength;
+  k.cdna_direction = cdna_direction;
+  k.watsonp = watsonp ? 1 : 0;
+  k.jump_late_p = jump_late_p ? 1 : 0;
+  k.maxpeelback = maxpeelback;
+  k.nullgap = nullgap;
+  k.extraband_single = extraband_single;
+  k.close_indels_mode = close_indels_mode;
+  k.defect_rate = defect_rate;
+  for (int i = 0; i < 3; i++) {
+    k.maxlength1[i] = ((const Dynprog*)dynprogM)->maxlength1;
+    k.maxlength2[i] = ((const Dynprog*)dynprogM)->maxlength2;
+  }
+  k.in_minor = *dynprogindex;
+  gsnapdp_List_T list =
+      pass_one(k, path, queryseq_ptr, queryuc_ptr, pairpool, nullptr, "build_pairs_singles");
+  *dynprogindex = k.out_minor;
   return list;
 }
 

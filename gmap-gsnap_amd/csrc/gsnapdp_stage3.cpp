@@ -1106,7 +1106,10 @@ void scan(Pass& P, Path& k) {
     }
     const gsnapdp_s3_pair& g = k.A.at(pair);
     int kind;  // 0 keep it, 1 cDNA gap, 2 genome gap, 3 single gap
-    if (g.queryjump > c.nullgap) kind = 0;  // a large gap
+    if (c.pass == GSNAPDP_S3_SINGLES) {  // build_pairs_singles (stage3.c:7469-7583)
+      kind = (g.queryjump > c.nullgap || g.queryjump > g.genomejump + EXTRAQUERYGAP ||
+              g.genomejump > g.queryjump + SINGLESLEN) ? 0 : 3;
+    } else if (g.queryjump > c.nullgap) kind = 0;  // a large gap
     else if (g.queryjump > g.genomejump + EXTRAQUERYGAP) kind = 1;
     else if (g.genomejump > g.queryjump + minintronlen) kind = 2;
     else if (g.genomejump > g.queryjump + SINGLESLEN) kind = 0;  // a short intron
@@ -1115,7 +1118,8 @@ void scan(Pass& P, Path& k) {
       k.pairs = k.A.push_existing(k.pairs, ptr);
       continue;
     }
-    if (k.path < 0 || k.pairs < 0) return fail(k, "gap at the end of the path (the reference dereferences NULL)");
+    if (k.path < 0 || k.pairs < 0)  // build_pairs_introns dereferences NULL; build_pairs_singles aborts (:7543)
+      return fail(k, "gap at the end of the path (the reference dereferences NULL or aborts)");
     k.gapcell = ptr;
     k.left = k.A.pairof(k.path);    // leftpair = path->first
     k.right = k.A.pairof(k.pairs);  // rightpair = pairs->first
@@ -1381,7 +1385,7 @@ void unpack_resume(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
 }
 
 bool call_in_range(const gsnapdp_s3_call& c, int64_t npairs_in, size_t query_bytes) {
-  return c.first_pair >= 0 && c.npairs >= 0 && (int64_t)c.first_pair + c.npairs <= npairs_in && c.qpos >= 0 &&
+  return (c.pass == GSNAPDP_S3_INTRONS || c.pass == GSNAPDP_S3_SINGLES) && c.first_pair >= 0 && c.npairs >= 0 && (int64_t)c.first_pair + c.npairs <= npairs_in && c.qpos >= 0 &&
          c.querylength >= 0 && (uint64_t)c.qpos + (uint64_t)c.querylength <= (uint64_t)query_bytes;
 }
 

@@ -140,9 +140,10 @@ S3_CALL = np.dtype([(n, "<i4") for n in "first_pair npairs first_out nout qpos q
                    [(n, "<i4") for n in ("in_minor in_major in_nintrons in_nnonintrons in_intronlen in_nonintronlen "
                                          "out_minor out_major out_nintrons out_nnonintrons out_intronlen "
                                          "out_nonintronlen shiftp incompletep novelsplicingp splicingp "
-                                         "status ub").split()] +
+                                         "status ub pass pad").split()] +
                    [("ref_seconds", "<f8")])
-assert S3_CALL.itemsize == 200
+assert S3_CALL.itemsize == 208
+S3_INTRONS, S3_SINGLES = 0, 1  # gsnapdp_s3_call.pass
 S3_STATS = np.dtype([("rounds", "<i4"), ("windows", "<i4", 4), ("batches", "<i4", 4), ("undefined", "<i4"),
                      ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3), ("new_pairs", "<i8")])
 assert S3_STATS.itemsize == 80

@@ -568,6 +568,7 @@ typedef struct gsnapdp_s3_pair {
 } gsnapdp_s3_pair;
 enum { GSNAPDP_S3_GAPP = 1, GSNAPDP_S3_KNOWNGAPP = 2, GSNAPDP_S3_DISALLOWED = 4 };
 enum { GSNAPDP_S3_UB_INTRONLEN = 1 };
+enum { GSNAPDP_S3_INTRONS = 0, GSNAPDP_S3_SINGLES = 1 };
 
 /* One build_pairs_introns call: its arguments (the query bytes at query[qpos],
  * querylength of them; the three Dynprog_T workspaces' limits, L, M, R), its
@@ -594,6 +595,11 @@ typedef struct gsnapdp_s3_call {
                                        * new_left/rightgenomepos (stage3.c:5651; an early-returning
                                        * Dynprog_genome_gap leaves them unwritten): the reference's own
                                        * value is stack garbage there, and differs between runs */
+  int32_t pass;                       /* GSNAPDP_S3_INTRONS: build_pairs_introns (stage3.c:7735);
+                                       * GSNAPDP_S3_SINGLES: build_pairs_singles (:7454; passes 2A, 2C
+                                       * and 7C of path_compute), whose dynprogindex is in_minor /
+                                       * out_minor and which reads neither finalp nor the intron counters */
+  int32_t pad;
   double ref_seconds;                 /* golden records: the reference's own call time (ignored) */
 } gsnapdp_s3_call;
 

@@ -237,7 +237,8 @@ gsnapdp_List_T Gsnapdp_score_introns(double* avg_donor_score, double* avg_accept
  * signature): a stage3.c that calls Gsnapdp_build_pairs_introns at its two
  * call sites (stage3.c:8766, 8865) gets the same list, the
  * same counters and flags, with every gap of the path filled by the GPU gap
- * families (gsnapdp_stage3_pass over one path).  Without a splicing IIT; the
+ * families (gsnapdp_stage3_pass over one path).  The splicing IIT is
+ * Dynprog_setup's, asked through the host's own iit-read functions; the
  * genome is the context's.  A caller with many paths at hand calls
  * gsnapdp_stage3_pass (gsnapdp.h) on all of them at once instead. */
 gsnapdp_List_T Gsnapdp_build_pairs_introns(
@@ -250,6 +251,20 @@ gsnapdp_List_T Gsnapdp_build_pairs_introns(
     int extraband_single, int extraband_paired, double defect_rate, int close_indels_mode,
     gsnapdp_Pairpool_T pairpool, gsnapdp_Dynprog_T dynprogL, gsnapdp_Dynprog_T dynprogM,
     gsnapdp_Dynprog_T dynprogR, gsnapdp_bool finalp);
+
+/* build_pairs_singles (stage3.c:7454-7583, static there; non-PMAP, non-WASTE
+ * signature): passes 2A / 2C / 7C of path_compute (call sites stage3.c:8671,
+ * 8700, 8938).  Same list and dynprogindex as the reference,
+ * every single gap filled by traverse_single_gap's GPU family
+ * (gsnapdp_stage3_pass, pass GSNAPDP_S3_SINGLES, over one path). */
+gsnapdp_List_T Gsnapdp_build_pairs_singles(int* dynprogindex, gsnapdp_List_T path, gsnapdp_Genomicpos_T chroffset,
+                                           gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos,
+                                           gsnapdp_Genomicpos_T genomiclength, char* queryseq_ptr,
+                                           char* queryuc_ptr, char* genomicseg_ptr, char* genomicuc_ptr,
+                                           int cdna_direction, gsnapdp_bool watsonp, gsnapdp_bool jump_late_p,
+                                           int maxpeelback, int nullgap, int extraband_single, double defect_rate,
+                                           int close_indels_mode, gsnapdp_Pairpool_T pairpool,
+                                           gsnapdp_Dynprog_T dynprogM);
 
 /* --- optional additions (not in the reference) ---
  * The shim finds the packed genome on its own: Dynprog_setup's Genome_T

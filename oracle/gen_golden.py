@@ -665,7 +665,8 @@ def gmap_cins_case(seed: int = 21, ngenes: int = 60, genome_len: int = 500_000) 
     cd = gp & (pi["queryjump"] > pi["genomejump"] + 10) & (pi["queryjump"] <= 600)
     owner = np.repeat(np.arange(c.size), c["npairs"])
     per = np.bincount(owner[cd], minlength=c.size)
-    order = [int(i) for i in np.argsort(c["npairs"], kind="stable") if per[i] > 0]
+    # build_pairs_introns calls only: build_pairs_singles keeps cDNA gaps as they are
+    order = [int(i) for i in np.argsort(c["npairs"], kind="stable") if per[i] > 0 and c["pass"][i] == 0]
     pick, ncd = [], 0
     for i in order:
         pick.append(i)

@@ -223,7 +223,7 @@ typedef struct { /* gsnapdp_s3_call (include/gsnapdp.h) */
   int32_t in_minor, in_major, in_nintrons, in_nnonintrons, in_intronlen, in_nonintronlen;
   int32_t out_minor, out_major, out_nintrons, out_nnonintrons, out_intronlen, out_nonintronlen;
   int32_t shiftp, incompletep, novelsplicingp, splicingp;
-  int32_t status, pad;
+  int32_t status, ub, pass, pad;
   double ref_seconds;
 } BpiCall;
 typedef struct { /* gsnapdp_s3_pair */
@@ -255,6 +255,63 @@ static int cmp_ptr(const void *a, const void *b) {
   return x < y ? -1 : (x > y ? 1 : 0);
 }
 
+/* the call's query, its path (pair by pair, list order), the in-counters */
+static PtrIdx *bpi_begin(BpiCall *c, List_T path, const char *queryseq_ptr, const char *queryuc_ptr,
+                         int querylength, int *n) {
+  List_T p;
+  PtrIdx *ix;
+  int i;
+  static const char zero[8] = {0};
+  c->first_pair = (int32_t)(bpi_in.n / sizeof(BpiPair));
+  c->qpos = (int32_t)bpi_q.n;
+  c->querylength = querylength;
+  put(&bpi_q, queryseq_ptr, (size_t)querylength);
+  put(&bpi_qu, queryuc_ptr, (size_t)querylength);
+  put(&bpi_q, zero, 8 - (size_t)(querylength & 3)); /* dword-padded, as the batch buffers */
+  put(&bpi_qu, zero, 8 - (size_t)(querylength & 3));
+  c->novelsplicingp = gmap_trace_novelsplicingp();
+  c->splicingp = gmap_trace_splicingp();
+  *n = 0;
+  for (p = path; p != NULL; p = p->rest) (*n)++;
+  ix = (PtrIdx *)malloc((size_t)(*n > 0 ? *n : 1) * sizeof(PtrIdx));
+  for (p = path, i = 0; p != NULL; p = p->rest, i++) {
+    BpiPair r = bpi_pair((const struct Pair_T *)p->first, -1);
+    put(&bpi_in, &r, sizeof(r));
+    ix[i].p = p->first;
+    ix[i].i = i;
+  }
+  c->npairs = *n;
+  qsort(ix, (size_t)*n, sizeof(PtrIdx), cmp_ptr);
+  return ix;
+}
+/* the list the call returned (each cell's input index, or -1) and the call */
+static void bpi_end(BpiCall *c, List_T out, PtrIdx *ix, int n, const struct timespec *t0) {
+  List_T p;
+  struct timespec t1;
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  c->ref_seconds = (double)(t1.tv_sec - t0->tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0->tv_nsec);
+  c->first_out = (int32_t)(bpi_out.n / sizeof(BpiPair));
+  for (p = out; p != NULL; p = p->rest) {
+    PtrIdx key, *hit;
+    BpiPair r;
+    key.p = p->first;
+    hit = (PtrIdx *)bsearch(&key, ix, (size_t)n, sizeof(PtrIdx), cmp_ptr);
+    r = bpi_pair((const struct Pair_T *)p->first, hit ? hit->i : -1);
+    put(&bpi_out, &r, sizeof(r));
+    c->nout++;
+  }
+  free(ix);
+  put(&bpi_calls, c, sizeof(*c));
+}
+static void bpi_dynprogs(BpiCall *c, Dynprog_T dynprogL, Dynprog_T dynprogM, Dynprog_T dynprogR) {
+  c->maxlength1[0] = ((int *)dynprogL)[0];
+  c->maxlength2[0] = ((int *)dynprogL)[1];
+  c->maxlength1[1] = ((int *)dynprogM)[0];
+  c->maxlength2[1] = ((int *)dynprogM)[1];
+  c->maxlength1[2] = ((int *)dynprogR)[0];
+  c->maxlength2[2] = ((int *)dynprogR)[1];
+}
+
 static List_T bpi_hook(bool *shiftp, bool *incompletep, int *nintrons, int *nnonintrons, int *intronlen,
                        int *nonintronlen, int *dynprogindex_minor, int *dynprogindex_major, List_T path, int chrnum,
                        Genomicpos_T chroffset, Genomicpos_T chrhigh, Genomicpos_T chrpos, void *genome,
@@ -265,19 +322,12 @@ static List_T bpi_hook(bool *shiftp, bool *incompletep, int *nintrons, int *nnon
                        Pairpool_T pairpool, Dynprog_T dynprogL, Dynprog_T dynprogM, Dynprog_T dynprogR,
                        bool finalp) {
   BpiCall c;
-  List_T p, out;
+  List_T out;
   PtrIdx *ix;
-  int n = 0, i;
-  struct timespec t0, t1;
-  static const char zero[8] = {0};
+  int n = 0;
+  struct timespec t0;
   memset(&c, 0, sizeof(c));
-  c.first_pair = (int32_t)(bpi_in.n / sizeof(BpiPair));
-  c.qpos = (int32_t)bpi_q.n;
-  c.querylength = querylength;
-  put(&bpi_q, queryseq_ptr, (size_t)querylength);
-  put(&bpi_qu, queryuc_ptr, (size_t)querylength);
-  put(&bpi_q, zero, 8 - (size_t)(querylength & 3)); /* dword-padded, as the batch buffers */
-  put(&bpi_qu, zero, 8 - (size_t)(querylength & 3));
+  c.pass = GSNAPDP_S3_INTRONS;
   c.chroffset = chroffset;
   c.chrhigh = chrhigh;
   c.chrpos = chrpos;
@@ -295,30 +345,14 @@ static List_T bpi_hook(bool *shiftp, bool *incompletep, int *nintrons, int *nnon
   c.extraband_paired = extraband_paired;
   c.close_indels_mode = close_indels_mode;
   c.defect_rate = defect_rate;
-  c.maxlength1[0] = ((int *)dynprogL)[0];
-  c.maxlength2[0] = ((int *)dynprogL)[1];
-  c.maxlength1[1] = ((int *)dynprogM)[0];
-  c.maxlength2[1] = ((int *)dynprogM)[1];
-  c.maxlength1[2] = ((int *)dynprogR)[0];
-  c.maxlength2[2] = ((int *)dynprogR)[1];
+  bpi_dynprogs(&c, dynprogL, dynprogM, dynprogR);
   c.in_minor = *dynprogindex_minor;
   c.in_major = *dynprogindex_major;
   c.in_nintrons = *nintrons;
   c.in_nnonintrons = *nnonintrons;
   c.in_intronlen = *intronlen;
   c.in_nonintronlen = *nonintronlen;
-  c.novelsplicingp = gmap_trace_novelsplicingp();
-  c.splicingp = gmap_trace_splicingp();
-  for (p = path; p != NULL; p = p->rest) n++;
-  ix = (PtrIdx *)malloc((size_t)(n > 0 ? n : 1) * sizeof(PtrIdx));
-  for (p = path, i = 0; p != NULL; p = p->rest, i++) {
-    BpiPair r = bpi_pair((const struct Pair_T *)p->first, -1);
-    put(&bpi_in, &r, sizeof(r));
-    ix[i].p = p->first;
-    ix[i].i = i;
-  }
-  c.npairs = n;
-  qsort(ix, (size_t)n, sizeof(PtrIdx), cmp_ptr);
+  ix = bpi_begin(&c, path, queryseq_ptr, queryuc_ptr, querylength, &n);
   patch_off(&bpi_p);
   clock_gettime(CLOCK_MONOTONIC, &t0);
   out = ((bpi_fn_t)(void *)bpi_p.entry)(shiftp, incompletep, nintrons, nnonintrons, intronlen, nonintronlen,
@@ -328,20 +362,7 @@ static List_T bpi_hook(bool *shiftp, bool *incompletep, int *nintrons, int *nnon
                                         jump_late_p, maxpeelback, nullgap, extramaterial_paired, extraband_single,
                                         extraband_paired, defect_rate, close_indels_mode, pairpool, dynprogL,
                                         dynprogM, dynprogR, finalp);
-  clock_gettime(CLOCK_MONOTONIC, &t1);
   patch_on(&bpi_p);
-  c.ref_seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
-  c.first_out = (int32_t)(bpi_out.n / sizeof(BpiPair));
-  for (p = out; p != NULL; p = p->rest) {
-    PtrIdx key, *hit;
-    BpiPair r;
-    key.p = p->first;
-    hit = (PtrIdx *)bsearch(&key, ix, (size_t)n, sizeof(PtrIdx), cmp_ptr);
-    r = bpi_pair((const struct Pair_T *)p->first, hit ? hit->i : -1);
-    put(&bpi_out, &r, sizeof(r));
-    c.nout++;
-  }
-  free(ix);
   c.out_minor = *dynprogindex_minor;
   c.out_major = *dynprogindex_major;
   c.out_nintrons = *nintrons;
@@ -350,13 +371,60 @@ static List_T bpi_hook(bool *shiftp, bool *incompletep, int *nintrons, int *nnon
   c.out_nonintronlen = *nonintronlen;
   c.shiftp = *shiftp;
   c.incompletep = *incompletep;
-  put(&bpi_calls, &c, sizeof(c));
+  bpi_end(&c, out, ix, n, &t0);
+  return out;
+}
+
+/* ---- build_pairs_singles (stage3.c:7454-7583), passes 2A / 2C / 7C: the same
+ * records, pass GSNAPDP_S3_SINGLES, dynprogindex_minor in in_minor / out_minor */
+typedef List_T (*bps_fn_t)(int *, List_T, Genomicpos_T, Genomicpos_T, Genomicpos_T, Genomicpos_T, char *, char *,
+                           char *, char *, int, bool, bool, int, int, int, double, int, Pairpool_T, Dynprog_T);
+extern void *gmap_trace_build_pairs_singles_fn(void);
+static Patch bps_p;
+static List_T bps_hook(int *dynprogindex, List_T path, Genomicpos_T chroffset, Genomicpos_T chrhigh,
+                       Genomicpos_T chrpos, Genomicpos_T genomiclength, char *queryseq_ptr, char *queryuc_ptr,
+                       char *genomicseg_ptr, char *genomicuc_ptr, int cdna_direction, bool watsonp,
+                       bool jump_late_p, int maxpeelback, int nullgap, int extraband_single, double defect_rate,
+                       int close_indels_mode, Pairpool_T pairpool, Dynprog_T dynprogM) {
+  BpiCall c;
+  List_T out;
+  PtrIdx *ix;
+  int n = 0;
+  struct timespec t0;
+  memset(&c, 0, sizeof(c));
+  c.pass = GSNAPDP_S3_SINGLES;
+  c.chroffset = chroffset;
+  c.chrhigh = chrhigh;
+  c.chrpos = chrpos;
+  c.genomiclength = (int32_t)genomiclength;
+  c.cdna_direction = cdna_direction;
+  c.watsonp = watsonp;
+  c.jump_late_p = jump_late_p;
+  c.maxpeelback = maxpeelback;
+  c.nullgap = nullgap;
+  c.extraband_single = extraband_single;
+  c.close_indels_mode = close_indels_mode;
+  c.defect_rate = defect_rate;
+  bpi_dynprogs(&c, dynprogM, dynprogM, dynprogM);
+  c.in_minor = *dynprogindex;
+  /* the query is gmap's whole query (Sequence_fullpointer, NUL-terminated) */
+  ix = bpi_begin(&c, path, queryseq_ptr, queryuc_ptr, (int)strlen(queryseq_ptr), &n);
+  patch_off(&bps_p);
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  out = ((bps_fn_t)(void *)bps_p.entry)(dynprogindex, path, chroffset, chrhigh, chrpos, genomiclength,
+                                        queryseq_ptr, queryuc_ptr, genomicseg_ptr, genomicuc_ptr, cdna_direction,
+                                        watsonp, jump_late_p, maxpeelback, nullgap, extraband_single, defect_rate,
+                                        close_indels_mode, pairpool, dynprogM);
+  patch_on(&bps_p);
+  c.out_minor = *dynprogindex;
+  bpi_end(&c, out, ix, n, &t0);
   return out;
 }
 
 __attribute__((constructor)) static void install_hooks(void) {
   patch_install(&si_p, gmap_trace_score_introns_fn(), (void *)&si_hook);
   patch_install(&bpi_p, gmap_trace_build_pairs_introns_fn(), (void *)&bpi_hook);
+  patch_install(&bps_p, gmap_trace_build_pairs_singles_fn(), (void *)&bps_hook);
 }
 
 extern unsigned int *__real_Genome_create_blocks(char *genomicseg, unsigned int genomelength);

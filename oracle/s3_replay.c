@@ -62,7 +62,7 @@ typedef struct { /* gsnapdp_s3_call (include/gsnapdp.h) */
   int32_t in_minor, in_major, in_nintrons, in_nnonintrons, in_intronlen, in_nonintronlen;
   int32_t out_minor, out_major, out_nintrons, out_nnonintrons, out_intronlen, out_nonintronlen;
   int32_t shiftp, incompletep, novelsplicingp, splicingp;
-  int32_t status, pad;
+  int32_t status, ub, pass, pad;
   double ref_seconds;
 } S3Call;
 typedef struct { /* gsnapdp_s3_pair */
@@ -90,6 +90,9 @@ typedef List_T (*bpi_fn_t)(bool *, bool *, int *, int *, int *, int *, int *, in
 typedef List_T (*si_fn_t)(double *, double *, int *, List_T, int, bool, int, Genomicpos_T, Genomicpos_T,
                           Genomicpos_T, char *, int, int, bool);
 extern void *gmap_trace_build_pairs_introns_fn(void);
+extern void *gmap_trace_build_pairs_singles_fn(void);
+typedef List_T (*bps_fn_t)(int *, List_T, Genomicpos_T, Genomicpos_T, Genomicpos_T, Genomicpos_T, char *, char *,
+                           char *, char *, int, bool, bool, int, int, int, double, int, Pairpool_T, Dynprog_T);
 extern void *gmap_trace_score_introns_fn(void);
 
 static void *slurp(const char *dir, const char *name, size_t *n) {
@@ -171,6 +174,7 @@ int main(int argc, char **argv) {
   Pairpool_T pool;
   Dynprog_T dynprogL, dynprogM, dynprogR;
   bpi_fn_t bpi = (bpi_fn_t)gmap_trace_build_pairs_introns_fn();
+  bps_fn_t bps = (bps_fn_t)gmap_trace_build_pairs_singles_fn();
   si_fn_t si = (si_fn_t)gmap_trace_score_introns_fn();
 
   if (argc < 2) {
@@ -266,12 +270,18 @@ int main(int argc, char **argv) {
     qsort(inptr, (size_t)c->npairs, sizeof(PtrIdx), cmp_ptr);
     if (poison >= 0) poison_stack(poison);
     clock_gettime(CLOCK_MONOTONIC, &t0);
-    out = bpi(&shiftp, &incompletep, &nintrons, &nnonintrons, &intronlen, &nonintronlen, &minor, &major, path,
-              c->chrnum, c->chroffset, c->chrhigh, c->chrpos, NULL, c->querylength, c->genomiclength, q + c->qpos,
-              qu + c->qpos, NULL, NULL, c->use_genomicseg_p ? true : false, c->cdna_direction,
-              c->watsonp ? true : false, c->jump_late_p ? true : false, c->maxpeelback, c->nullgap,
-              c->extramaterial_paired, c->extraband_single, c->extraband_paired, c->defect_rate,
-              c->close_indels_mode, pool, dynprogL, dynprogM, dynprogR, c->finalp ? true : false);
+    if (c->pass == 1) /* GSNAPDP_S3_SINGLES: build_pairs_singles (stage3.c:7454) */
+      out = bps(&minor, path, c->chroffset, c->chrhigh, c->chrpos, (Genomicpos_T)c->genomiclength, q + c->qpos,
+                qu + c->qpos, NULL, NULL, c->cdna_direction, c->watsonp ? true : false,
+                c->jump_late_p ? true : false, c->maxpeelback, c->nullgap, c->extraband_single, c->defect_rate,
+                c->close_indels_mode, pool, dynprogM);
+    else
+      out = bpi(&shiftp, &incompletep, &nintrons, &nnonintrons, &intronlen, &nonintronlen, &minor, &major, path,
+                c->chrnum, c->chroffset, c->chrhigh, c->chrpos, NULL, c->querylength, c->genomiclength, q + c->qpos,
+                qu + c->qpos, NULL, NULL, c->use_genomicseg_p ? true : false, c->cdna_direction,
+                c->watsonp ? true : false, c->jump_late_p ? true : false, c->maxpeelback, c->nullgap,
+                c->extramaterial_paired, c->extraband_single, c->extraband_paired, c->defect_rate,
+                c->close_indels_mode, pool, dynprogL, dynprogM, dynprogR, c->finalp ? true : false);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     c->ref_seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
     c->first_out = (int32_t)nout;

@@ -1,6 +1,7 @@
-"""The stage-3 intron pass on the GPU (gsnapdp_stage3_pass: build_pairs_introns,
-stage3.c:7735-7901, for many paths at once, every round one batch per gap
-family) against every recorded build_pairs_introns call of the reference's gmap
+"""The stage-3 passes on the GPU (gsnapdp_stage3_pass: build_pairs_introns,
+stage3.c:7735-7901, and build_pairs_singles, :7454-7583, for many paths at once,
+every round one batch per gap family) against every recorded call of the
+reference's gmap
 (tests/golden/gmap_*_stage3.npz; see test_stage3_cpu.py), and at scale: the
 synthetic calls replicated into one pass of thousands of paths, each copy
 checked against the reference, with the pass's throughput printed beside the
@@ -75,7 +76,7 @@ def test_gpu_stage3_pass_at_scale(golden_dir):
 
 @pytest.mark.parametrize("name", ["gmap_synth_stage3", "gmap_cins_stage3"] + IIT_NAMES)
 def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name):
-    """Gsnapdp_build_pairs_introns as stage3.c would call it (the reference's
+    """Gsnapdp_build_pairs_introns and Gsnapdp_build_pairs_singles as stage3.c would call them (the reference's
     signature): the path as a List_T of the host's Pair_T cells, the counters
     as in/out arguments, the returned list (kept cells and pushed pairs, with
     disallowedp).  The IIT sets give Dynprog_setup a splicing IIT (the IIT test
@@ -83,7 +84,7 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     import ctypes
     import subprocess
 
-    from gsnapdp.records import S3_PAIR
+    from gsnapdp.records import S3_PAIR, S3_SINGLES
     from test_dropin import SETUP_ARGS, load_iit_double
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -100,6 +101,9 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     L.Gsnapdp_dropin_genome.argtypes = [vp, ctypes.c_size_t, i32]
     L.Dynprog_new.restype = vp
     L.Dynprog_new.argtypes = [i32] * 5
+    L.Gsnapdp_build_pairs_singles.restype = vp
+    L.Gsnapdp_build_pairs_singles.argtypes = [vp, vp, u32, u32, u32, u32, vp, vp, vp, vp, i32, u8, u8, i32, i32,
+                                              i32, ctypes.c_double, i32, vp, vp]
     L.Gsnapdp_build_pairs_introns.restype = vp
     L.Gsnapdp_build_pairs_introns.argtypes = (
         [vp] * 8 + [vp, i32, u32, u32, u32, vp, i32, i32, vp, vp, vp, vp, u8, i32, u8, u8] + [i32] * 5 +
@@ -130,6 +134,7 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     siit = SplicingIIT(iit_intervals(z)) if iit is not None else None
     ub = (ctx.stage3_pass(calls, pin, q, qu, iit=siit)[0]["ub"] & 1) != 0
     ctx.close()
+    nsingles = 0
     for i, c in enumerate(calls):
         f0, n = int(c["first_pair"]), int(c["npairs"])
         recs = np.ascontiguousarray(pin[f0:f0 + n])
@@ -139,6 +144,20 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
                                                  "in_nonintronlen", "in_minor", "in_major")]
         qp = qb.ctypes.data + int(c["qpos"])
         qup = qub.ctypes.data + int(c["qpos"])
+        exp = want[int(c["first_out"]):int(c["first_out"]) + int(c["nout"])]
+        got = np.zeros(len(exp) + 1, S3_PAIR)
+        if c["pass"] == S3_SINGLES:  # the golden's query is NUL-padded, as Sequence_fullpointer's
+            ctr[4] = ctypes.c_int(int(c["in_minor"]))
+            out = L.Gsnapdp_build_pairs_singles(
+                ctypes.byref(ctr[4]), lst, int(c["chroffset"]), int(c["chrhigh"]), int(c["chrpos"]),
+                int(c["genomiclength"]), qp, qup, None, None, int(c["cdna_direction"]), int(c["watsonp"]),
+                int(c["jump_late_p"]), int(c["maxpeelback"]), int(c["nullgap"]), int(c["extraband_single"]),
+                float(c["defect_rate"]), int(c["close_indels_mode"]), None, dp)
+            k = dbl.dbl_s3_read(out, got.ctypes.data, got.size)
+            assert k == len(exp) and got[:k].tobytes() == exp.tobytes(), i
+            assert ctr[4].value == int(c["out_minor"]), i
+            nsingles += 1
+            continue
         out = L.Gsnapdp_build_pairs_introns(
             ctypes.byref(shift), ctypes.byref(inc), *[ctypes.byref(x) for x in ctr], lst, int(c["chrnum"]),
             int(c["chroffset"]), int(c["chrhigh"]), int(c["chrpos"]), None, int(c["querylength"]),
@@ -146,8 +165,6 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
             int(c["jump_late_p"]), int(c["maxpeelback"]), int(c["nullgap"]), int(c["extramaterial_paired"]),
             int(c["extraband_single"]), int(c["extraband_paired"]), float(c["defect_rate"]),
             int(c["close_indels_mode"]), None, dp, dp, dp, int(c["finalp"]))
-        exp = want[int(c["first_out"]):int(c["first_out"]) + int(c["nout"])]
-        got = np.zeros(len(exp) + 1, S3_PAIR)
         k = dbl.dbl_s3_read(out, got.ctypes.data, got.size)
         assert k == len(exp), (i, k, len(exp))
         assert got[:k].tobytes() == exp.tobytes(), i
@@ -156,6 +173,7 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
         skip = ub[i] if ub is not None else False  # the reference's own intron lengths are garbage there
         assert [x.value for j, x in enumerate(ctr) if not (skip and j in (2, 3))] == [
             int(c[f]) for j, f in enumerate(fields) if not (skip and j in (2, 3))], i
+    assert nsingles == int((calls["pass"] == S3_SINGLES).sum())
     if iit is not None:  # back to no IIT for the other tests of this process
         L.Dynprog_setup(1, None, None, -1, -1, None, None, None, 0, None, None, None, None, None)
     L.Dynprog_term()  # releases the device context (the genome array dies with this test)

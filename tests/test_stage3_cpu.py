@@ -1,7 +1,9 @@
-"""The stage-3 intron pass (gsnapdp_stage3_pass, build_pairs_introns
-stage3.c:7735-7901 over many paths) on the CPU, against the reference.
+"""The stage-3 passes (gsnapdp_stage3_pass: build_pairs_introns
+stage3.c:7735-7901 and build_pairs_singles :7454-7583 over many paths) on the
+CPU, against the reference.
 
-gmap_trace recorded every build_pairs_introns call the reference's gmap made
+gmap_trace recorded every build_pairs_introns and build_pairs_singles call the
+reference's gmap made
 (ss.her2 against ss.chr17test, and the synthetic spliced cDNAs): the path it was
 given, its arguments and counters, and the list it returned
 (tests/golden/gmap_*_stage3.npz, oracle/gen_golden.py stage3_golden).  Here the
@@ -17,7 +19,7 @@ import numpy as np
 import pytest
 
 from gsnapdp import workload as W
-from gsnapdp.records import S3_CALL, S3_PAIR, S3_STATS
+from gsnapdp.records import S3_CALL, S3_PAIR, S3_SINGLES, S3_STATS
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NAMES = ["gmap_her2_stage3", "gmap_synth_stage3", "gmap_cins_stage3"]
@@ -133,6 +135,10 @@ def test_stage3_golden_covers_the_branches(golden_dir):
     new = z["out_new"]
     assert ((new["flags"] & 1) == 1).any()  # gapholders made by the genome-gap fills
     assert (c["out_nintrons"] > c["in_nintrons"]).any()
+    # build_pairs_singles calls (passes 2A / 2C / 7C of path_compute) among them,
+    # some of whose single gaps were filled by traverse_single_gap
+    singles = c["pass"] == S3_SINGLES
+    assert singles.sum() >= 100 and (c["out_minor"][singles] > c["in_minor"][singles]).any()
 
 
 def iit_intervals(z):
