@@ -338,10 +338,11 @@ def measure_micro(genome, n, steps, warmup, dev, with_cpu):
 
 
 def measure_stage3(paths=7424, reps=3):
-    """Side line: the stage-3 passes (gsnapdp_stage3_pass: build_pairs_introns and
-    build_pairs_singles over many paths, mixed in one pass) on the recorded calls
-    of the reference's gmap (tests/golden/gmap_synth_stage3.npz: 464
-    build_pairs_introns + 336 build_pairs_singles calls) replicated `copies`
+    """Side line: the stage-3 passes (gsnapdp_stage3_pass: path_compute's
+    build_pairs_introns, build_pairs_singles, build_pairs_end5 / build_path_end3
+    and build_pairs_dualintrons, mixed in one pass) on the recorded calls of the
+    reference's gmap (tests/golden/gmap_synth_stage3.npz: 464 introns, 336
+    singles, 160 end5, 152 end3 and 96 dual-intron calls) replicated `copies`
     times into one pass;
     every copy is checked against the reference's lists.  `reference_s` is the
     reference's own time for the same calls (its build_pairs_introns wall time,
@@ -369,9 +370,10 @@ def measure_stage3(paths=7424, reps=3):
     ref = float(z["calls"]["ref_seconds"].sum()) * copies
     ctx.close()
     cpu = stage3_cpu_baseline(z["blocks"], calls, pin, q, qu, got)
-    return {"metric": "stage-3 passes (build_pairs_introns + build_pairs_singles), paths/s",
+    return {"metric": "stage-3 passes (path_compute's DP passes), paths/s",
             "value": round(len(calls) / dt, 1), "unit": "paths/s", "paths": int(len(calls)),
-            "paths_by_pass": {"introns": int((calls["pass"] == 0).sum()), "singles": int((calls["pass"] == 1).sum())},
+            "paths_by_pass": {n: int((calls["pass"] == i).sum())
+                              for i, n in enumerate(("introns", "singles", "end5", "end3", "dualintrons"))},
             "seconds": round(dt, 4), "rounds": int(st["rounds"]),
             "windows": nwin, "windows_per_s": round(nwin / dt, 1),
             "windows_by_family": {"single": int(st["windows"][0]), "genome_gap": int(st["windows"][1]),
@@ -382,8 +384,7 @@ def measure_stage3(paths=7424, reps=3):
             "reference_cross_machine": {
                 "value": round(len(calls) / ref, 1), "unit": "paths/s", "seconds": round(ref, 4), "cores": 1,
                 "kind": "reference",
-                "note": "the reference's own build_pairs_introns / build_pairs_singles on the same calls, timed by "
-                        "gmap_trace in the "
+                "note": "the reference's own pass functions on the same calls, timed by gmap_trace in the "
                         "development container (a different machine), DP included"}}
 
 

@@ -653,7 +653,9 @@ static_assert(offsetof(RefPair, querypos) == GSNAPDP_PAIR_OFF_QUERYPOS &&
                   offsetof(RefPair, gapp) == GSNAPDP_PAIR_OFF_GAPP &&
                   offsetof(RefPair, knowngapp) == GSNAPDP_PAIR_OFF_KNOWNGAPP &&
                   offsetof(RefPair, disallowedp) == GSNAPDP_PAIR_OFF_DISALLOWEDP &&
-                  offsetof(RefPair, donor_prob) == GSNAPDP_PAIR_OFF_DONOR_PROB && sizeof(RefPair) == GSNAPDP_PAIR_SIZE,
+                  offsetof(RefPair, donor_prob) == GSNAPDP_PAIR_OFF_DONOR_PROB &&
+                  offsetof(RefPair, shortexonp) == GSNAPDP_PAIR_OFF_SHORTEXONP &&
+                  offsetof(RefPair, end_intron_p) == GSNAPDP_PAIR_OFF_END_INTRON_P && sizeof(RefPair) == GSNAPDP_PAIR_SIZE,
               "Pair_T layout");
 static_assert(offsetof(RefPairHead, querypos) == GSNAPDP_PAIR_OFF_QUERYPOS &&
                   offsetof(RefPairHead, comp) == GSNAPDP_PAIR_OFF_COMP,
@@ -1588,7 +1590,8 @@ gsnapdp_List_T pass_one(gsnapdp_s3_call& k, gsnapdp_List_T path, char* queryseq_
     p.comp = x->comp;
     p.genome = x->genome;
     p.flags = (uint8_t)((x->gapp ? GSNAPDP_S3_GAPP : 0) | (x->knowngapp ? GSNAPDP_S3_KNOWNGAPP : 0) |
-                        (x->disallowedp ? GSNAPDP_S3_DISALLOWED : 0));
+                        (x->disallowedp ? GSNAPDP_S3_DISALLOWED : 0) | (x->shortexonp ? GSNAPDP_S3_SHORTEXON : 0) |
+                        (x->end_intron_p ? GSNAPDP_S3_END_INTRON : 0));
     in.push_back(p);
     incells.push_back(l);
   }
@@ -1736,6 +1739,145 @@ gsnapdp_List_T Gsnapdp_build_pairs_singles(int* dynprogindex, gsnapdp_List_T pat
   gsnapdp_List_T list =
       pass_one(k, path, queryseq_ptr, queryuc_ptr, pairpool, nullptr, "build_pairs_singles");
   *dynprogindex = k.out_minor;
+  return list;
+}
+
+}  // extern "C"
+
+namespace {
+
+// the arguments build_pairs_end5 / build_path_end3 share (extendp; extend_ending5
+// / extend_ending3, stage3.c:6587-6719 / :6906-7041)
+void end_call(gsnapdp_s3_call& k, int pass, gsnapdp_Genomicpos_T chroffset, gsnapdp_Genomicpos_T chrhigh,
+              gsnapdp_Genomicpos_T chrpos, int querylength, int genomiclength, int cdna_direction,
+              gsnapdp_bool watsonp, gsnapdp_bool jump_late_p, int maxpeelback, int nullgap, int extramaterial_end,
+              int extraband_end, double defect_rate, gsnapdp_Dynprog_T dynprog, gsnapdp_Endalign_T endalign,
+              int minor) {
+  memset(&k, 0, sizeof(k));
+  k.pass = pass;
+  k.querylength = querylength;
+  k.chroffset = chroffset;
+  k.chrhigh = chrhigh;
+  k.chrpos = chrpos;
+  k.genomiclength = genomiclength;
+  k.cdna_direction = cdna_direction;
+  k.watsonp = watsonp ? 1 : 0;
+  k.jump_late_p = jump_late_p ? 1 : 0;
+  k.maxpeelback = maxpeelback;
+  k.nullgap = nullgap;
+  k.extramaterial_end = extramaterial_end;
+  k.extraband_end = extraband_end;
+  k.defect_rate = defect_rate;
+  k.endalign = (int32_t)endalign;
+  for (int i = 0; i < 3; i++) {
+    k.maxlength1[i] = ((const Dynprog*)dynprog)->maxlength1;
+    k.maxlength2[i] = ((const Dynprog*)dynprog)->maxlength2;
+  }
+  k.in_minor = minor;
+}
+
+}  // namespace
+
+extern "C" {
+
+// build_pairs_end5 (stage3.c:7351-7450), passes 8, 9a and 10 of path_compute
+// (:8966, :9036, :9167; path_trim :9660, :9722), with the reference's signature
+// (non-GSNAP, non-PMAP):
+// the 5' extension's Dynprog_end5_gap in the batched pass.  extendp only (the
+// distalmedial branch is unused, :7420); without splice sites (Dynprog_end5_known
+// is the splice-site branch of QUERYEND_GAP, :6651).
+gsnapdp_List_T Gsnapdp_build_pairs_end5(
+    gsnapdp_bool* knownsplicep, int* ambig_end_length_5, gsnapdp_Splicetype_T* /*ambig_splicetype_5*/,
+    gsnapdp_bool* chop_exon_p, int* dynprogindex_minor, gsnapdp_List_T pairs, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos, int genomiclength,
+    gsnapdp_Genomicpos_T /*knownsplice_limit_low*/, gsnapdp_Genomicpos_T /*knownsplice_limit_high*/,
+    char* queryseq_ptr, char* queryuc_ptr, char* /*genomicseg_ptr*/, char* /*genomicuc_ptr*/, int cdna_direction,
+    gsnapdp_bool watsonp, gsnapdp_bool jump_late_p, int maxpeelback, int /*maxpeelback_distalmedial*/, int nullgap,
+    int extramaterial_end, int extraband_end, double defect_rate, gsnapdp_Pairpool_T pairpool,
+    gsnapdp_Dynprog_T dynprogR, gsnapdp_bool extendp, gsnapdp_Endalign_T endalign) {
+  if (!extendp) fatal("build_pairs_end5: distalmedial_ending5 (extendp false) is not served");
+  if (g.splicesites && endalign == GSNAPDP_QUERYEND_GAP)
+    fatal("build_pairs_end5: Dynprog_end5_known (splice sites) is not served by the batched pass");
+  *ambig_end_length_5 = 0;
+  if (!pairs || ((const RefPair*)((RefList*)pairs)->first)->querypos < 0) return nullptr;  // :7372-7390
+  gsnapdp_s3_call k;
+  end_call(k, GSNAPDP_S3_END5, chroffset, chrhigh, chrpos, (int)strlen(queryseq_ptr), genomiclength, cdna_direction,
+           watsonp, jump_late_p, maxpeelback, nullgap, extramaterial_end, extraband_end, defect_rate, dynprogR,
+           endalign, *dynprogindex_minor);
+  gsnapdp_List_T list = pass_one(k, pairs, queryseq_ptr, queryuc_ptr, pairpool, nullptr, "build_pairs_end5");
+  *chop_exon_p = 0;
+  *knownsplicep = 0;
+  *dynprogindex_minor = k.out_minor;
+  return list;
+}
+
+// build_path_end3 (stage3.c:7236-7347), the 3' counterpart (:8990, :9088, :9190,
+// :9683, :9744)
+gsnapdp_List_T Gsnapdp_build_path_end3(
+    gsnapdp_bool* knownsplicep, int* ambig_end_length_3, gsnapdp_Splicetype_T* /*ambig_splicetype_3*/,
+    gsnapdp_bool* chop_exon_p, int* dynprogindex_minor, gsnapdp_List_T path, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos, int querylength, int genomiclength,
+    gsnapdp_Genomicpos_T /*knownsplice_limit_low*/, gsnapdp_Genomicpos_T /*knownsplice_limit_high*/,
+    char* queryseq_ptr, char* queryuc_ptr, char* /*genomicseg_ptr*/, char* /*genomicuc_ptr*/, int cdna_direction,
+    gsnapdp_bool watsonp, gsnapdp_bool jump_late_p, int maxpeelback, int /*maxpeelback_distalmedial*/, int nullgap,
+    int extramaterial_end, int extraband_end, double defect_rate, gsnapdp_Pairpool_T pairpool,
+    gsnapdp_Dynprog_T dynprogL, gsnapdp_bool extendp, gsnapdp_Endalign_T endalign) {
+  if (!extendp) fatal("build_path_end3: distalmedial_ending3 (extendp false) is not served");
+  if (g.splicesites && endalign == GSNAPDP_QUERYEND_GAP)
+    fatal("build_path_end3: Dynprog_end3_known (splice sites) is not served by the batched pass");
+  *ambig_end_length_3 = 0;
+  if (!path || ((const RefPair*)((RefList*)path)->first)->querypos < 0) return nullptr;  // :7257-7274
+  gsnapdp_s3_call k;
+  end_call(k, GSNAPDP_S3_END3, chroffset, chrhigh, chrpos, querylength, genomiclength, cdna_direction, watsonp,
+           jump_late_p, maxpeelback, nullgap, extramaterial_end, extraband_end, defect_rate, dynprogL, endalign,
+           *dynprogindex_minor);
+  gsnapdp_List_T list = pass_one(k, path, queryseq_ptr, queryuc_ptr, pairpool, nullptr, "build_path_end3");
+  *chop_exon_p = 0;
+  *knownsplicep = 0;
+  *dynprogindex_minor = k.out_minor;
+  return list;
+}
+
+// build_pairs_dualintrons (stage3.c:7592-7733), pass 3b of path_compute
+// (:8746): every short exon Smooth_pairs_by_size marked between two introns is
+// weighed by traverse_dual_genome_gap (:5980-6364) -- one intron, two, or one
+// of them -- with its Dynprog_genome_gap windows in the batched pass.
+gsnapdp_List_T Gsnapdp_build_pairs_dualintrons(
+    int* dynprogindex, gsnapdp_List_T path, int chrnum, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos, int genomiclength, char* queryseq_ptr,
+    char* queryuc_ptr, char* /*genomicseg_ptr*/, char* /*genomicuc_ptr*/, gsnapdp_bool use_genomicseg_p,
+    int cdna_direction, gsnapdp_bool watsonp, gsnapdp_bool jump_late_p, int maxpeelback, int nullgap,
+    int extramaterial_paired, int extraband_paired, double defect_rate, gsnapdp_Pairpool_T pairpool,
+    gsnapdp_Dynprog_T dynprogL, gsnapdp_Dynprog_T dynprogR) {
+  if (use_genomicseg_p) fatal("build_pairs_dualintrons on a genomic segment is not served by the batched pass");
+  gsnapdp_s3_call k;
+  memset(&k, 0, sizeof(k));
+  k.pass = GSNAPDP_S3_DUALINTRONS;
+  k.querylength = (int32_t)strlen(queryseq_ptr);
+  k.chroffset = chroffset;
+  k.chrhigh = chrhigh;
+  k.chrpos = chrpos;
+  k.chrnum = chrnum;
+  k.genomiclength = genomiclength;
+  k.cdna_direction = cdna_direction;
+  k.watsonp = watsonp ? 1 : 0;
+  k.jump_late_p = jump_late_p ? 1 : 0;
+  k.maxpeelback = maxpeelback;
+  k.nullgap = nullgap;
+  k.extramaterial_paired = extramaterial_paired;
+  k.extraband_paired = extraband_paired;
+  k.defect_rate = defect_rate;
+  const Dynprog* dp[3] = {(const Dynprog*)dynprogL, (const Dynprog*)dynprogL, (const Dynprog*)dynprogR};
+  for (int i = 0; i < 3; i++) {
+    k.maxlength1[i] = dp[i]->maxlength1;
+    k.maxlength2[i] = dp[i]->maxlength2;
+  }
+  k.in_major = *dynprogindex;
+  k.novelsplicingp = g.novelsplicingp ? 1 : 0;  // Stage3_setup's flags (gmap.c:3828-3849)
+  k.splicingp = (g.novelsplicingp || g.splicing_iit) ? 1 : 0;
+  gsnapdp_List_T list = pass_one(k, path, queryseq_ptr, queryuc_ptr, pairpool, g.iit ? host_iit() : nullptr,
+                                 "build_pairs_dualintrons");
+  *dynprogindex = k.out_major;
   return list;
 }
 

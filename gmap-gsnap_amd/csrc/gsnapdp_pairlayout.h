@@ -20,8 +20,10 @@
 #define GSNAPDP_PAIR_OFF_GENOME 38
 #define GSNAPDP_PAIR_OFF_GAPP 41
 #define GSNAPDP_PAIR_OFF_KNOWNGAPP 42
+#define GSNAPDP_PAIR_OFF_SHORTEXONP 44
 #define GSNAPDP_PAIR_OFF_DISALLOWEDP 61
 #define GSNAPDP_PAIR_OFF_DONOR_PROB 64
+#define GSNAPDP_PAIR_OFF_END_INTRON_P 80
 #define GSNAPDP_PAIR_SIZE 88
 #define GSNAPDP_LIST_OFF_FIRST 0
 #define GSNAPDP_LIST_OFF_REST 8

@@ -1,5 +1,7 @@
-// gsnapdp_stage3.cpp -- the stage-3 intron pass (build_pairs_introns,
-// stage3.c:7735-7901) for many paths at once, over the batched gap families.
+// gsnapdp_stage3.cpp -- the stage-3 DP passes of path_compute for many paths
+// at once, over the batched gap families: build_pairs_introns (stage3.c:7735),
+// build_pairs_singles (:7454), build_pairs_dualintrons (:7592) and the end
+// extensions build_pairs_end5 / build_path_end3 (:7351 / :7236).
 //
 // Each path is the reference's list: the pass keeps the same cells and the
 // same list operations (Pairpool_pop / List_push_existing / Pairpool_transfer,
@@ -10,6 +12,7 @@
 // cohorts with one round each in flight (gsnapdp_stage3.h): while the GPU runs
 // one cohort's windows, a persistent pool of host threads resumes the other's
 // paths, so the host work hides behind the batches instead of adding to them.
+#include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -45,7 +48,7 @@ using gsnapdp::ST_UNSUPPORTED;
 constexpr int SINGLESLEN = 9, MININTRONLEN = 9, MININTRONLEN_FINAL = 50, EXTRAQUERYGAP = 10;
 constexpr int SUFFCONSECUTIVE = 5;
 constexpr int UNKNOWNJUMP = -1000000;
-constexpr int QOPEN = -5, QINDEL = -2;
+constexpr int QOPEN = -5, QINDEL = -2, MISMATCH = -3, DUAL_HALFCANONICAL_POINTS = 4;  // scores.h:6-13
 constexpr double DEFECT_HIGHQ = 0.003, DEFECT_MEDQ = 0.014;
 constexpr int NONINTRON = 0, GTAG_FWD = 0x20, GTAG_REV = 0x04;
 constexpr int BIG = 0x3fffffff;  // a workspace limit no window reaches
@@ -125,6 +128,7 @@ struct Arena {
     }
     return dest;
   }
+  int reverse(int list) { return transfer(-1, list); }  // List_reverse (the same cells)
   const gsnapdp_s3_pair& at(int pair) const { return pair < nin ? in[pair] : extra[(size_t)(pair - nin)].p; }
   // a pair's flags without touching the pair record (the scan's hot loop)
   uint8_t flag(int pair) const { return pair < nin ? flags[(size_t)pair] : extra[(size_t)(pair - nin)].p.flags; }
@@ -180,6 +184,12 @@ enum Stage {
   S_GG_SCORE,     // traverse_genome_gap's score-mode Dynprog_genome_gap
   S_GG_PROB,      // its probability-mode re-run
   S_GG_MICRO,     // its Dynprog_microexon_int
+  S_END,          // extend_ending5 / extend_ending3's Dynprog_end5_gap / Dynprog_end3_gap
+  S_DUAL_SINGLE,  // traverse_dual_genome_gap: the single-intron Dynprog_genome_gap
+  S_DUAL_2,       // its right-of-short-exon window (halfp)
+  S_DUAL_1,       // its left-of-short-exon window (halfp)
+  S_DUAL_RIGHT,   // single wins, right_end_intron_p: keep the left intron only
+  S_DUAL_LEFT,    // single wins, left_end_intron_p: keep the right intron only
   S_DONE
 };
 
@@ -205,10 +215,25 @@ struct Path {
   int finalscore = 0, nmatches = 0, nmismatches = 0, nopens = 0, nindels = 0, exonhead = 0;
   int new_left = 0, new_right = 0, introntype = 0;
   bool newpos_set = false;  // new_left / new_right written in this traverse_genome_gap call
-  bool ub = false;          // the counters took the reference's uninitialised locals
+  bool ub = false;          // the outputs took the reference's uninitialised locals
+  int ub_bits = 0;          // which (GSNAPDP_S3_UB_*)
   double left_prob = 0.0, right_prob = 0.0;
   int gappairs = -1;
   int undefined = 0;  // probability re-runs with no qualifying candidate
+  // build_pairs_dualintrons' midexon_pairs (a function-scope local that keeps
+  // its value from one short exon to the next) and traverse_dual_genome_gap's
+  // state between its windows
+  int midexon = -1;
+  struct Dual {
+    bool left_end = false, right_end = false;
+    int midq = 0, midg = 0;
+    int q5 = 0, g5 = 0, q3 = 0, g3 = 0;  // the peeled bounds
+    int single = -1, dual2 = -1, dual1 = -1;
+    int single_goodness = 0, dual_goodness = 0;
+    bool single_typed = false;  // single_introntype written by its Dynprog_genome_gap
+    int single_introntype = 0, introntype2 = 0, introntype1 = 0;
+    int right_exonhead = 0, left_exonhead = 0;
+  } d;
   Req req;
 };
 
@@ -480,10 +505,10 @@ void req_single(Path& k) {
   R.cap = (int64_t)(k.queryjump > 0 ? k.queryjump : 0) + (k.genomejump > 0 ? k.genomejump : 0) + 2;
 }
 
-// Dynprog_genome_gap (dynprog.c:4798-5061), halfp = false; with a splicing IIT
+// Dynprog_genome_gap (dynprog.c:4798-5061); with a splicing IIT
 // the window's known-site record follows its query rows, as the drop-in's
 // Dynprog_genome_gap places it
-bool req_genome(const Pass& P, Path& k, bool prob, int score_threshold) {
+bool req_genome(const Pass& P, Path& k, bool prob, int score_threshold, bool halfp = false, int finalp = -1) {
   const gsnapdp_s3_call& c = *k.c;
   Req& R = k.req;
   R.fam = F_GGAP;
@@ -513,8 +538,8 @@ bool req_genome(const Pass& P, Path& k, bool prob, int score_threshold) {
   w.defect_rate = bin(c.defect_rate);
   w.watsonp = c.watsonp ? 1 : 0;
   w.jump_late_p = c.jump_late_p ? 1 : 0;
-  w.halfp = 0;
-  w.finalp = (prob || c.finalp) ? 1 : 0;
+  w.halfp = halfp ? 1 : 0;
+  w.finalp = (prob || (finalp < 0 ? c.finalp != 0 : finalp != 0)) ? 1 : 0;
   w.use_probabilities_p = prob ? 1 : 0;
   w.splicingp = c.splicingp ? 1 : 0;
   w.known_mode = GSNAPDP_KNOWN_NONE;
@@ -620,6 +645,41 @@ void req_micro(Path& k) {
   w.defect_rate = bin(c.defect_rate);
   w.watsonp = c.watsonp ? 1 : 0;
   R.cap = 0;
+}
+
+// Dynprog_end5_gap / Dynprog_end3_gap (dynprog.c:5094-5284 / 5290-5406), as
+// extend_ending5 / extend_ending3 call them (stage3.c:6665-6676, :6983-6994):
+// dynprogR at the 5' end, dynprogL at the 3' end, widebandp
+void req_end(Path& k, bool end5) {
+  const gsnapdp_s3_call& c = *k.c;
+  Req& R = k.req;
+  R.fam = F_GAP;
+  gsnapdp_window& w = R.w;
+  memset(&w, 0, sizeof(w));
+  w.kind = end5 ? GSNAPDP_END5_GAP : GSNAPDP_END3_GAP;
+  w.length1 = k.queryjump;
+  w.length2 = k.genomejump;
+  w.offset1 = end5 ? k.querydp3 : k.querydp5;  // revoffset1 / offset1
+  w.offset2 = end5 ? k.genomedp3 : k.genomedp5;
+  w.chroffset = c.chroffset;
+  w.chrhigh = c.chrhigh;
+  w.chrpos = c.chrpos;
+  w.genomiclength = (uint32_t)c.genomiclength;
+  w.cdna_direction = c.cdna_direction;
+  w.extraband = c.extraband_end;
+  w.dynprogindex = k.minor;
+  w.maxlength1 = c.maxlength1[end5 ? 2 : 0];
+  w.maxlength2 = c.maxlength2[end5 ? 2 : 0];
+  w.defect_rate = bin(c.defect_rate);
+  w.watsonp = c.watsonp ? 1 : 0;
+  w.jump_late_p = c.jump_late_p ? 1 : 0;
+  w.widebandp = 1;
+  w.endalign = (uint8_t)c.endalign;
+  const int L1 = k.queryjump > 0 ? k.queryjump : 0;
+  // revsequence1[-(L1 - 1) .. 0] ends at querydp3; sequence1 starts at querydp5
+  stage_query(k, R, end5 ? k.querydp3 - (L1 - 1) : k.querydp5, L1);
+  w.qpos = end5 ? (uint32_t)(L1 > 0 ? L1 - 1 : 0) : 0u;
+  R.cap = (int64_t)L1 + (k.genomejump > 0 ? k.genomejump : 0) + 2;
 }
 
 void fail(Path& k, const std::string& why) {
@@ -765,7 +825,7 @@ bool done_genome(Pass& P, Path& k, int* finalscore, int* nmismatches, double* lp
   // *introntype: always NONINTRON in the constrained known-intron mode (:3695),
   // else written only when a score-mode candidate was taken
   if (w.known_mode == GSNAPDP_KNOWN_INTRONS) k.introntype = NONINTRON;
-  else if (!w.use_probabilities_p && r.finalscore != -100000) k.introntype = r.introntype;
+  else if (!w.use_probabilities_p && r.finalscore != (w.halfp ? -50000 : -100000)) k.introntype = r.introntype;
   if (!t.bridge_accepted) return true;
   k.new_left = r.new_leftgenomepos;
   k.new_right = r.new_rightgenomepos;
@@ -1002,7 +1062,7 @@ void genome_account(Path& k) {
   // reference adds whatever its stack slots hold (a previous call's value, or
   // garbage that differs between runs of the same input); the pass keeps the
   // path's previous values there and reports the counters as undefined
-  if (!k.newpos_set) k.ub = true;
+  if (!k.newpos_set) k.ub = true, k.ub_bits |= GSNAPDP_S3_UB_INTRONLEN;
   if (k.introntype == NONINTRON) {
     k.nnonintrons += 1;
     k.nonintronlen += k.new_right - k.new_left - 1;
@@ -1088,6 +1148,267 @@ void genome_done(Pass& P, Path& k) {
   end_gap(k, true);
 }
 
+// ---- build_pairs_end5 (:7351-7450) / build_path_end3 (:7236-7347) with
+// extendp: extend_ending5 / extend_ending3 (:6587-6719 / :6906-7041) without
+// splice sites.  The list is `pairs` (END5) or `path` (END3); the peeled
+// stretch is dropped whatever the window returns, as the reference drops it.
+void end_start(Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  const bool end5 = c.pass == GSNAPDP_S3_END5;
+  const bool peel = c.endalign != GSNAPDP_QUERYEND_NOGAPS && c.maxpeelback != 0;
+  bool mm = false;
+  k.stage = S_DONE;
+  if (end5) {
+    if (k.pairs < 0) return;  // NULL in, NULL out
+    const gsnapdp_s3_pair& rp = k.A.first(k.pairs);
+    if (rp.querypos < 0) {  // :7386-7390: the whole list is dropped
+      k.pairs = -1;
+      return;
+    }
+    const int leftquerypos = rp.querypos > c.nullgap ? rp.querypos - c.nullgap - 1 : -1;
+    k.querydp5 = leftquerypos + 1;
+    k.querydp3 = rp.querypos - 1;
+    k.genomedp3 = rp.genomepos - 1;
+    if (peel)
+      k.pairs = peel_rightward(k.A, &mm, &k.peeled_pairs, k.pairs, &k.querydp3, &k.genomedp3, c.maxpeelback, true);
+    k.queryjump = k.querydp3 - k.querydp5 + 1;
+    k.genomejump = k.queryjump + c.extramaterial_end;
+    k.genomedp5 = k.genomedp3 - k.genomejump + 1;
+  } else {
+    if (k.path < 0) return;
+    const gsnapdp_s3_pair& lp = k.A.first(k.path);
+    if (lp.querypos < 0) {  // :7270-7274
+      k.path = -1;
+      return;
+    }
+    int queryjump = c.querylength - lp.querypos - 1;
+    if (lp.cdna == ' ') queryjump++;
+    const int rightquerypos = queryjump + 1 > c.nullgap ? lp.querypos + c.nullgap + 1 : c.querylength;
+    k.querydp5 = lp.cdna == ' ' ? lp.querypos : lp.querypos + 1;
+    k.genomedp5 = lp.genome == ' ' ? lp.genomepos : lp.genomepos + 1;
+    k.querydp3 = rightquerypos - 1;
+    k.genomedp3 = c.genomiclength - 1;
+    if (peel)
+      k.path = peel_leftward(k.A, &mm, &k.peeled_path, k.path, &k.querydp5, &k.genomedp5, c.maxpeelback, true);
+    k.queryjump = k.querydp3 - k.querydp5 + 1;
+    k.genomejump = k.queryjump + c.extramaterial_end;
+    k.genomedp3 = k.genomedp5 + k.genomejump - 1;
+  }
+  req_end(k, end5);
+  k.stage = S_END;
+}
+void end_done(Pass& P, Path& k) {
+  const bool end5 = k.c->pass == GSNAPDP_S3_END5;
+  int list = -1;
+  if (!done_single(P, k, &list)) return;
+  if (!end5) list = k.A.reverse(list);
+  // an indel between the extension and the rest of the read (:6707, :7029)
+  if (list >= 0 && k.A.first(list).querypos != (end5 ? k.querydp3 : k.querydp5)) list = -1;
+  if (end5) k.pairs = k.A.transfer(k.pairs, list);
+  else k.path = k.A.transfer(k.path, list);
+  k.stage = S_DONE;
+}
+
+// ---- traverse_dual_genome_gap (:5980-6364): one intron or two around a short
+// exon.  Its windows run one per round, in the reference's order (the
+// dynprogindex each takes is the reference's).
+int dual_goodness(const Path& k, int nmismatches) {
+  return k.nmatches + MISMATCH * nmismatches + QOPEN * k.nopens + QINDEL * k.nindels;
+}
+// a Dynprog_genome_gap of the traversal over [q5, q3] x [g5, g3], square
+// (genomejump = queryjump + extramaterial_paired), score mode, not final
+bool dual_window(Pass& P, Path& k, int q5, int g5, int q3, int g3, bool halfp, int stage) {
+  const gsnapdp_s3_call& c = *k.c;
+  k.querydp5 = q5;
+  k.genomedp5 = g5;
+  k.querydp3 = q3;
+  k.genomedp3 = g3;
+  k.queryjump = q3 - q5 + 1;
+  k.genomejump = k.queryjump + c.extramaterial_paired;
+  if (!req_genome(P, k, false, 0, halfp, 0)) {
+    fail(k, "known-site record");
+    return false;
+  }
+  k.stage = stage;
+  return true;
+}
+// whether [q5, q3] fits the genome stretch: the "bounds don't make sense"
+// tests of the half windows (:6128, :6166, :6279, :6325)
+bool dual_fits(const Path& k, int q5, int g5, int q3, int g3) {
+  return g5 + (q3 - q5 + 1 + k.c->extramaterial_paired) - 1 < g3;
+}
+void dual_unknown_gap(Path& k) {  // put back, Pairpool_push_gapholder(UNKNOWNJUMP) (:6066-6072)
+  put_back(k);
+  gsnapdp_s3_pair g;
+  memset(&g, 0, sizeof(g));
+  g.querypos = -1;
+  g.genomepos = -1;
+  g.queryjump = UNKNOWNJUMP;
+  g.genomejump = UNKNOWNJUMP;
+  g.src = -1;
+  g.cdna = g.comp = g.genome = ' ';
+  g.flags = GSNAPDP_S3_GAPP;
+  k.pairs = k.A.push_pair(k.pairs, g);
+  k.stage = S_SCAN;
+}
+bool dual_start(Pass& P, Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  bool mr = false, ml = false;
+  gap_bounds(k);
+  k.pairs = peel_rightward(k.A, &mr, &k.peeled_pairs, k.pairs, &k.querydp3, &k.genomedp3, c.maxpeelback, true);
+  k.path = peel_leftward(k.A, &ml, &k.peeled_path, k.path, &k.querydp5, &k.genomedp5, c.maxpeelback, true);
+  Path::Dual& d = k.d;
+  d.q5 = k.querydp5, d.g5 = k.genomedp5, d.q3 = k.querydp3, d.g3 = k.genomedp3;
+  const int queryjump = d.q3 - d.q5 + 1, genomejump = queryjump + c.extramaterial_paired;
+  if (queryjump > c.nullgap || d.g5 + genomejump - 1 >= d.g3 - genomejump + 1) {
+    dual_unknown_gap(k);
+    return false;
+  }
+  d.single = d.dual2 = d.dual1 = -1;
+  return dual_window(P, k, d.q5, d.g5, d.q3, d.g3, false, S_DUAL_SINGLE);
+}
+// the single result (or a better one-intron alternative) wins (:6264-6360)
+void dual_single_wins(Pass& P, Path& k, int from) {
+  Path::Dual& d = k.d;
+  if (from < S_DUAL_RIGHT && d.right_end && dual_fits(k, d.q5, d.g5, d.midq, d.midg)) {
+    dual_window(P, k, d.q5, d.g5, d.midq, d.midg, false, S_DUAL_RIGHT);
+    return;
+  }
+  if (from < S_DUAL_LEFT && d.left_end && dual_fits(k, d.midq, d.midg, d.q3, d.g3)) {
+    dual_window(P, k, d.midq, d.midg, d.q3, d.g3, false, S_DUAL_LEFT);
+    return;
+  }
+  k.pairs = k.A.transfer(k.pairs, d.single);
+  k.stage = S_SCAN;
+}
+void dual_decide(Pass& P, Path& k) {  // :6195-6262
+  const gsnapdp_s3_call& c = *k.c;
+  Path::Dual& d = k.d;
+  if (d.dual2 < 0 || d.dual1 < 0) return dual_single_wins(P, k, S_DUAL_1);
+  const int canonical = c.cdna_direction > 0 ? GTAG_FWD : GTAG_REV;
+  const bool dual_canonical = d.introntype1 == canonical && d.introntype2 == canonical;
+  int middle_exonlength = d.right_exonhead - d.left_exonhead;
+  double middle_exonprob;
+  if (middle_exonlength <= 0) {
+    middle_exonprob = 0.0;
+  } else {
+    const int interexon_region = k.new_right - k.new_left;
+    if (d.introntype2 == canonical) middle_exonlength += DUAL_HALFCANONICAL_POINTS;
+    if (d.introntype1 == canonical) middle_exonlength += DUAL_HALFCANONICAL_POINTS;
+    middle_exonprob = 1.0 - pow(1.0 - pow(4.0, -(double)middle_exonlength), (double)interexon_region);
+  }
+  if (dual_canonical && middle_exonprob < 0.001 && d.single_goodness > d.dual_goodness && !d.single_typed)
+    k.ub = true, k.ub_bits |= GSNAPDP_S3_UB_DUAL;  // single_canonical_p read an uninitialised introntype
+  const bool single_canonical = d.single_typed && d.single_introntype == canonical;
+  if (dual_canonical && middle_exonprob < 0.001 && (!single_canonical || d.single_goodness <= d.dual_goodness)) {
+    k.pairs = k.A.transfer(k.pairs, d.dual2);
+    k.pairs = k.A.transfer(k.pairs, d.dual1);
+    k.stage = S_SCAN;
+    return;
+  }
+  dual_single_wins(P, k, S_DUAL_1);
+}
+void dual_done(Pass& P, Path& k) {
+  Path::Dual& d = k.d;
+  int fs = 0, nmm = 0, list = -1;
+  double lp = 0.0, rp = 0.0;
+  const int stage = k.stage;
+  const int before = k.introntype;
+  k.introntype = INT32_MIN;  // written or not, by this window
+  if (!done_genome(P, k, &fs, &nmm, &lp, &rp, &list)) return;
+  const bool typed = k.introntype != INT32_MIN;
+  const int introntype = k.introntype;
+  k.introntype = before;
+  switch (stage) {
+    case S_DUAL_SINGLE:
+      d.single = list;
+      d.single_goodness = k.nopens <= 1 ? (k.nmatches + k.nindels) + MISMATCH * nmm
+                                        : k.nmatches + MISMATCH * nmm + QOPEN * (k.nopens - 1) + QINDEL * k.nindels;
+      d.single_typed = typed;
+      d.single_introntype = introntype;
+      if (!dual_fits(k, d.midq, d.midg, d.q3, d.g3)) return dual_single_wins(P, k, S_DUAL_1);
+      dual_window(P, k, d.midq, d.midg, d.q3, d.g3, true, S_DUAL_2);
+      return;
+    case S_DUAL_2:
+      d.dual2 = list;
+      d.dual_goodness = dual_goodness(k, nmm);
+      d.right_exonhead = k.exonhead;
+      d.introntype2 = typed ? introntype : INT32_MIN;
+      if (!dual_fits(k, d.q5, d.g5, d.midq - 1, d.midg - 1)) return dual_single_wins(P, k, S_DUAL_1);
+      dual_window(P, k, d.q5, d.g5, d.midq - 1, d.midg - 1, true, S_DUAL_1);
+      return;
+    case S_DUAL_1:
+      d.dual1 = list;
+      d.dual_goodness += dual_goodness(k, nmm);
+      d.left_exonhead = k.exonhead;
+      d.introntype1 = typed ? introntype : INT32_MIN;
+      return dual_decide(P, k);
+    default: {  // S_DUAL_RIGHT / S_DUAL_LEFT
+      const int goodness = dual_goodness(k, nmm);
+      if (goodness > d.single_goodness) {
+        d.single = list;
+        d.single_goodness = goodness;
+      }
+      return dual_single_wins(P, k, stage);
+    }
+  }
+}
+
+// build_pairs_dualintrons past a gap it may take (:7645-7726): cross the short
+// exon after it and run traverse_dual_genome_gap.  Returns true when it waits.
+bool dual_gap(Pass& P, Path& k, int gapcell, int gap) {
+  Arena& A = k.A;
+  Path::Dual& d = k.d;
+  d.right_end = (A.flag(gap) & GSNAPDP_S3_END_INTRON) != 0;
+  const int midrightpair = A.pairof(k.path);
+  // List_transfer_one: the cell moves to midexon_pairs, whose first tail is
+  // the local's uninitialised value (see below)
+  auto transfer_one = [&]() {
+    const int cell = k.path;
+    k.path = A.rest(cell);
+    A.cn[(size_t)cell] = k.midexon;
+    k.midexon = cell;
+  };
+  transfer_one();
+  bool exonp = true;
+  while (k.path >= 0 && exonp) {
+    const int mp = A.pairof(k.path);
+    if (A.flag(mp) & GSNAPDP_S3_GAPP) {
+      d.left_end = (A.flag(mp) & GSNAPDP_S3_END_INTRON) != 0;
+      exonp = false;
+      k.path = A.rest(k.path);
+    } else {
+      transfer_one();
+    }
+  }
+  if (k.path < 0) {
+    // "Short exon is the first one": Pairpool_push_existing (a new cell) and
+    // List_reverse(midexon_pairs), whose last cell links to the value
+    // midexon_pairs held before the first short exon of the call: garbage in
+    // the reference, taken as NULL here and reported
+    k.ub = true, k.ub_bits |= GSNAPDP_S3_UB_DUAL;
+    k.pairs = A.cell(gap, k.pairs);
+    k.pairs = A.transfer(k.pairs, A.reverse(k.midexon));
+    k.midexon = -1;
+    return false;
+  }
+  (void)gapcell;
+  const gsnapdp_s3_pair& ml = A.first(k.midexon);
+  const gsnapdp_s3_pair& mr = A.at(midrightpair);
+  const uint32_t midgenomepos = ((uint32_t)ml.genomepos + (uint32_t)mr.genomepos) / 2u;  // Genomicpos_T
+  d.midg = (int)midgenomepos;
+  d.midq = mr.querypos - (int)((uint32_t)mr.genomepos - midgenomepos);
+  if (k.pairs < 0) {
+    fail(k, "dual intron at the end of the path (the reference dereferences NULL)");
+    return false;
+  }
+  k.left = A.pairof(k.path);
+  k.right = A.pairof(k.pairs);
+  if (d.midq <= A.at(k.left).querypos || d.midq >= A.at(k.right).querypos) return false;  // skip
+  k.peeled_pairs = k.peeled_path = -1;
+  return dual_start(P, k);
+}
+
 // build_pairs_introns' loop (:7763-7898) until the path waits or ends
 void scan(Pass& P, Path& k) {
   const gsnapdp_s3_call& c = *k.c;
@@ -1105,6 +1426,20 @@ void scan(Pass& P, Path& k) {
       continue;
     }
     const gsnapdp_s3_pair& g = k.A.at(pair);
+    if (c.pass == GSNAPDP_S3_DUALINTRONS) {  // build_pairs_dualintrons (:7613-7730)
+      if (g.queryjump > c.nullgap || g.queryjump > g.genomejump + EXTRAQUERYGAP ||
+          g.genomejump <= g.queryjump + MININTRONLEN) {
+        k.pairs = k.A.push_existing(k.pairs, ptr);
+        continue;
+      }
+      if (k.path < 0) return fail(k, "dual-intron gap at the end of the path (the reference dereferences NULL)");
+      if (!(k.A.flag(k.A.pairof(k.path)) & GSNAPDP_S3_SHORTEXON)) {  // a long exon
+        k.pairs = k.A.push_existing(k.pairs, ptr);
+        continue;
+      }
+      if (dual_gap(P, k, ptr, pair)) return;
+      continue;
+    }
     int kind;  // 0 keep it, 1 cDNA gap, 2 genome gap, 3 single gap
     if (c.pass == GSNAPDP_S3_SINGLES) {  // build_pairs_singles (stage3.c:7469-7583)
       kind = (g.queryjump > c.nullgap || g.queryjump > g.genomejump + EXTRAQUERYGAP ||
@@ -1138,6 +1473,12 @@ void resume(Pass& P, Path& k) {
     case S_GG_SCORE:
     case S_GG_PROB:
     case S_GG_MICRO: genome_done(P, k); break;
+    case S_END: end_done(P, k); break;
+    case S_DUAL_SINGLE:
+    case S_DUAL_2:
+    case S_DUAL_1:
+    case S_DUAL_RIGHT:
+    case S_DUAL_LEFT: dual_done(P, k); break;
     default: break;
   }
   if (k.stage == S_SCAN) scan(P, k);
@@ -1385,7 +1726,7 @@ void unpack_resume(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
 }
 
 bool call_in_range(const gsnapdp_s3_call& c, int64_t npairs_in, size_t query_bytes) {
-  return (c.pass == GSNAPDP_S3_INTRONS || c.pass == GSNAPDP_S3_SINGLES) && c.first_pair >= 0 && c.npairs >= 0 && (int64_t)c.first_pair + c.npairs <= npairs_in && c.qpos >= 0 &&
+  return c.pass >= GSNAPDP_S3_INTRONS && c.pass <= GSNAPDP_S3_DUALINTRONS && c.first_pair >= 0 && c.npairs >= 0 && (int64_t)c.first_pair + c.npairs <= npairs_in && c.qpos >= 0 &&
          c.querylength >= 0 && (uint64_t)c.qpos + (uint64_t)c.querylength <= (uint64_t)query_bytes;
 }
 
@@ -1459,9 +1800,18 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
     const gsnapdp_s3_call& c = *k.c;
     // the input list: path->first is pairs_in[first_pair] (cell 0)
     k.A.init(pairs_in + c.first_pair, c.npairs);
-    k.path = c.npairs > 0 ? 0 : -1;
-    if (c.use_genomicseg_p) fail(k, "use_genomicseg_p passes are not served (the genome is the context's)");
-    else scan(P, k);
+    const int list = c.npairs > 0 ? 0 : -1;
+    if (c.use_genomicseg_p) {
+      fail(k, "use_genomicseg_p passes are not served (the genome is the context's)");
+    } else if (c.pass == GSNAPDP_S3_END5 || c.pass == GSNAPDP_S3_END3) {
+      if (c.splicesitesp && c.endalign == GSNAPDP_QUERYEND_GAP)
+        fail(k, "an end extension with splice sites (Dynprog_end5/3_known) is not served");
+      else if (c.pass == GSNAPDP_S3_END5) k.pairs = list, end_start(k);
+      else k.path = list, end_start(k);
+    } else {
+      k.path = list;
+      scan(P, k);
+    }
   });
   // two cohorts (alternate paths, so both get a similar mix) when there are
   // enough paths for each round to be worth a batch of its own
@@ -1510,6 +1860,7 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
   std::vector<int64_t> first((size_t)ncalls + 1, 0), nfirst((size_t)ncalls + 1, 0);
   pool.run(ncalls, 16, [&](int i) {
     Path& k = paths[(size_t)i];
+    if (k.c->pass == GSNAPDP_S3_END3) k.pairs = k.path;  // build_path_end3 returns its path
     int n = 0, nn = 0;
     if (!k.failed)
       for (int p = k.pairs; p >= 0; p = k.A.rest(p)) n++, nn += k.A.pairof(p) >= k.A.nin;
@@ -1559,7 +1910,7 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
     c.out_nonintronlen = k.nonintronlen;
     c.shiftp = k.shiftp ? 1 : 0;
     c.incompletep = k.incompletep ? 1 : 0;
-    c.ub = k.ub ? GSNAPDP_S3_UB_INTRONLEN : 0;
+    c.ub = k.ub_bits;
   });
   for (int i = 0; i < ncalls; i++) {
     P.st.undefined += paths[(size_t)i].undefined;

@@ -129,8 +129,9 @@ S3_PAIR = np.dtype([("querypos", "<i4"), ("genomepos", "<i4"), ("queryjump", "<i
                     ("dynprogindex", "<i4"), ("src", "<i4"), ("cdna", "u1"), ("comp", "u1"), ("genome", "u1"),
                     ("flags", "u1")])
 assert S3_PAIR.itemsize == 28
-S3_GAPP, S3_KNOWNGAPP, S3_DISALLOWED = 1, 2, 4
+S3_GAPP, S3_KNOWNGAPP, S3_DISALLOWED, S3_SHORTEXON, S3_END_INTRON = 1, 2, 4, 8, 16
 S3_UB_INTRONLEN = 1  # gsnapdp_s3_call.ub: intronlen / nonintronlen took the reference's uninitialised locals
+S3_UB_DUAL = 2  # a dual-intron decision read one of traverse_dual_genome_gap's uninitialised locals
 S3_CALL = np.dtype([(n, "<i4") for n in "first_pair npairs first_out nout qpos querylength".split()] +
                    [(n, "<u4") for n in "chroffset chrhigh chrpos".split()] +
                    [(n, "<i4") for n in ("chrnum genomiclength cdna_direction watsonp jump_late_p finalp "
@@ -140,10 +141,13 @@ S3_CALL = np.dtype([(n, "<i4") for n in "first_pair npairs first_out nout qpos q
                    [(n, "<i4") for n in ("in_minor in_major in_nintrons in_nnonintrons in_intronlen in_nonintronlen "
                                          "out_minor out_major out_nintrons out_nnonintrons out_intronlen "
                                          "out_nonintronlen shiftp incompletep novelsplicingp splicingp "
-                                         "status ub pass pad").split()] +
+                                         "status ub pass endalign extramaterial_end extraband_end splicesitesp "
+                                         "pad").split()] +
                    [("ref_seconds", "<f8")])
-assert S3_CALL.itemsize == 208
-S3_INTRONS, S3_SINGLES = 0, 1  # gsnapdp_s3_call.pass
+assert S3_CALL.itemsize == 224
+# gsnapdp_s3_call.pass: build_pairs_introns, build_pairs_singles, build_pairs_end5, build_path_end3,
+# build_pairs_dualintrons
+S3_INTRONS, S3_SINGLES, S3_END5, S3_END3, S3_DUALINTRONS = 0, 1, 2, 3, 4
 S3_STATS = np.dtype([("rounds", "<i4"), ("windows", "<i4", 4), ("batches", "<i4", 4), ("undefined", "<i4"),
                      ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3), ("new_pairs", "<i8")])
 assert S3_STATS.itemsize == 80

@@ -765,12 +765,14 @@ def pack_genome(gseq: np.ndarray) -> np.ndarray:
     return _genome.pack(gseq)
 
 
-def synthetic_transcripts(seed: int = 7, ngenes: int = 16, genome_len: int = 160_000, cins: float = 0.0):
+def synthetic_transcripts(seed: int = 7, ngenes: int = 16, genome_len: int = 160_000, cins: float = 0.0,
+                          small_frac: float = 0.12, small_len=(12, 30), intron_len=(70, 1501)):
     """End-to-end gmap inputs (tests/test_gmap_e2e.py): a genomic segment
     carrying ``ngenes`` spliced genes and one cDNA per gene.
 
-    Each gene has 2-12 exons of 12-260 nt (a few microexon-sized ones) and
-    introns of 70-1500 nt.  Intron ends are GT-AG (80 %), GC-AG (8 %), AT-AC
+    Each gene has 2-12 exons of 12-260 nt (a few microexon-sized ones:
+    `small_frac` of them, `small_len` nt) and introns of 70-1500 nt
+    (`intron_len`).  Intron ends are GT-AG (80 %), GC-AG (8 %), AT-AC
     (5 %) or random (7 %); the canonical ones sit in splice-site context
     (exon ..AG | GTRAGT donor, a pyrimidine tract and YAG | G acceptor) so that
     GMAP's MaxEnt-guided stage 3 accepts them.  A third of the genes lie on
@@ -789,11 +791,11 @@ def synthetic_transcripts(seed: int = 7, ngenes: int = 16, genome_len: int = 160
     for k in range(ngenes):
         nex = int(rng.integers(2, 13))
         exl = rng.integers(40, 261, size=nex)
-        small = rng.random(nex) < 0.12
-        exl[small] = rng.integers(12, 30, size=int(small.sum()))
+        small = rng.random(nex) < small_frac
+        exl[small] = rng.integers(small_len[0], small_len[1], size=int(small.sum()))
         exl[0] = max(exl[0], 60)
         exl[-1] = max(exl[-1], 60)
-        inl = rng.integers(70, 1501, size=nex - 1)
+        inl = rng.integers(intron_len[0], intron_len[1], size=nex - 1)
         span = int(exl.sum() + inl.sum())
         if pos + span + 2000 > genome_len:
             break

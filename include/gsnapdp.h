@@ -564,11 +564,29 @@ typedef struct gsnapdp_s3_pair {
   int32_t querypos, genomepos, queryjump, genomejump, dynprogindex;
   int32_t src;
   char cdna, comp, genome;
-  uint8_t flags;  /* GSNAPDP_S3_GAPP | GSNAPDP_S3_KNOWNGAPP | GSNAPDP_S3_DISALLOWED */
+  uint8_t flags;  /* GSNAPDP_S3_GAPP | GSNAPDP_S3_KNOWNGAPP | GSNAPDP_S3_DISALLOWED |
+                   * GSNAPDP_S3_SHORTEXON | GSNAPDP_S3_END_INTRON */
 } gsnapdp_s3_pair;
-enum { GSNAPDP_S3_GAPP = 1, GSNAPDP_S3_KNOWNGAPP = 2, GSNAPDP_S3_DISALLOWED = 4 };
-enum { GSNAPDP_S3_UB_INTRONLEN = 1 };
-enum { GSNAPDP_S3_INTRONS = 0, GSNAPDP_S3_SINGLES = 1 };
+/* Pair_T's gapp, knowngapp, disallowedp, shortexonp (set by Smooth_pairs_by_size,
+ * read by build_pairs_dualintrons) and end_intron_p (set by insert_gapholders on
+ * the first and last gap, stage3.c:902-916) */
+enum {
+  GSNAPDP_S3_GAPP = 1,
+  GSNAPDP_S3_KNOWNGAPP = 2,
+  GSNAPDP_S3_DISALLOWED = 4,
+  GSNAPDP_S3_SHORTEXON = 8,
+  GSNAPDP_S3_END_INTRON = 16
+};
+/* gsnapdp_s3_call.ub bits */
+enum { GSNAPDP_S3_UB_INTRONLEN = 1, GSNAPDP_S3_UB_DUAL = 2 };
+/* gsnapdp_s3_call.pass: which of path_compute's DP passes the call is */
+enum {
+  GSNAPDP_S3_INTRONS = 0,     /* build_pairs_introns (stage3.c:7735), passes 3c / 6 */
+  GSNAPDP_S3_SINGLES = 1,     /* build_pairs_singles (:7454), passes 2A / 2C / 7C */
+  GSNAPDP_S3_END5 = 2,        /* build_pairs_end5 (:7351) with extendp, passes 8 / 9a / 10 */
+  GSNAPDP_S3_END3 = 3,        /* build_path_end3 (:7236) with extendp, passes 8 / 9b / 10 */
+  GSNAPDP_S3_DUALINTRONS = 4  /* build_pairs_dualintrons (:7592), pass 3b */
+};
 
 /* One build_pairs_introns call: its arguments (the query bytes at query[qpos],
  * querylength of them; the three Dynprog_T workspaces' limits, L, M, R), its
@@ -595,10 +613,15 @@ typedef struct gsnapdp_s3_call {
                                        * new_left/rightgenomepos (stage3.c:5651; an early-returning
                                        * Dynprog_genome_gap leaves them unwritten): the reference's own
                                        * value is stack garbage there, and differs between runs */
-  int32_t pass;                       /* GSNAPDP_S3_INTRONS: build_pairs_introns (stage3.c:7735);
-                                       * GSNAPDP_S3_SINGLES: build_pairs_singles (:7454; passes 2A, 2C
-                                       * and 7C of path_compute), whose dynprogindex is in_minor /
-                                       * out_minor and which reads neither finalp nor the intron counters */
+  int32_t pass;                       /* GSNAPDP_S3_*: which pass.  SINGLES, END5 and END3 step
+                                       * dynprogindex_minor (in_minor / out_minor), DUALINTRONS
+                                       * dynprogindex_major (in_major / out_major); they read neither
+                                       * finalp nor the intron counters (passed through).  END5 gets the
+                                       * alignment as `pairs` (ascending querypos), END3 as `path`. */
+  int32_t endalign;                   /* END5 / END3: GSNAPDP_QUERYEND_GAP, _NOGAPS or BEST_LOCAL */
+  int32_t extramaterial_end, extraband_end;  /* END5 / END3 */
+  int32_t splicesitesp;               /* END5 / END3: Stage3_setup got splice sites (the
+                                       * Dynprog_end5/3_known branch, not served: status -1) */
   int32_t pad;
   double ref_seconds;                 /* golden records: the reference's own call time (ignored) */
 } gsnapdp_s3_call;

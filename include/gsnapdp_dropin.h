@@ -266,6 +266,47 @@ gsnapdp_List_T Gsnapdp_build_pairs_singles(int* dynprogindex, gsnapdp_List_T pat
                                            int close_indels_mode, gsnapdp_Pairpool_T pairpool,
                                            gsnapdp_Dynprog_T dynprogM);
 
+/* build_pairs_end5 (stage3.c:7351-7450) and build_path_end3 (:7236-7347),
+ * static there (non-GSNAP, non-PMAP signatures): passes 8, 9a / 9b and 10 of
+ * path_compute and path_trim (call sites :8966, :9036, :9167, :9660, :9722 and
+ * :8990, :9088, :9190, :9683, :9744;
+ * INTEGRATION.md 5) with extendp -- the extension's Dynprog_end5_gap /
+ * Dynprog_end3_gap in the batched pass.  Same list, dynprogindex_minor,
+ * knownsplicep, ambig_end_length and chop_exon_p as the reference without splice
+ * sites; distalmedial (extendp false) and the splice-site branch
+ * (Dynprog_end5/3_known) are refused with a message. */
+gsnapdp_List_T Gsnapdp_build_pairs_end5(
+    gsnapdp_bool* knownsplicep, int* ambig_end_length_5, gsnapdp_Splicetype_T* ambig_splicetype_5,
+    gsnapdp_bool* chop_exon_p, int* dynprogindex_minor, gsnapdp_List_T pairs, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos, int genomiclength,
+    gsnapdp_Genomicpos_T knownsplice_limit_low, gsnapdp_Genomicpos_T knownsplice_limit_high, char* queryseq_ptr,
+    char* queryuc_ptr, char* genomicseg_ptr, char* genomicuc_ptr, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, int maxpeelback, int maxpeelback_distalmedial, int nullgap, int extramaterial_end,
+    int extraband_end, double defect_rate, gsnapdp_Pairpool_T pairpool, gsnapdp_Dynprog_T dynprogR,
+    gsnapdp_bool extendp, gsnapdp_Endalign_T endalign);
+gsnapdp_List_T Gsnapdp_build_path_end3(
+    gsnapdp_bool* knownsplicep, int* ambig_end_length_3, gsnapdp_Splicetype_T* ambig_splicetype_3,
+    gsnapdp_bool* chop_exon_p, int* dynprogindex_minor, gsnapdp_List_T path, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos, int querylength, int genomiclength,
+    gsnapdp_Genomicpos_T knownsplice_limit_low, gsnapdp_Genomicpos_T knownsplice_limit_high, char* queryseq_ptr,
+    char* queryuc_ptr, char* genomicseg_ptr, char* genomicuc_ptr, int cdna_direction, gsnapdp_bool watsonp,
+    gsnapdp_bool jump_late_p, int maxpeelback, int maxpeelback_distalmedial, int nullgap, int extramaterial_end,
+    int extraband_end, double defect_rate, gsnapdp_Pairpool_T pairpool, gsnapdp_Dynprog_T dynprogL,
+    gsnapdp_bool extendp, gsnapdp_Endalign_T endalign);
+
+/* build_pairs_dualintrons (stage3.c:7592-7733, static there; non-PMAP
+ * signature; Chrnum_T is an int): pass 3b of path_compute (call site :8746).
+ * Same list and dynprogindex_major as the reference; each short exon's
+ * traverse_dual_genome_gap (:5980-6364) windows run in the batched pass, with
+ * Dynprog_setup's splicing IIT as Gsnapdp_build_pairs_introns takes it. */
+gsnapdp_List_T Gsnapdp_build_pairs_dualintrons(
+    int* dynprogindex, gsnapdp_List_T path, int chrnum, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos, int genomiclength, char* queryseq_ptr,
+    char* queryuc_ptr, char* genomicseg_ptr, char* genomicuc_ptr, gsnapdp_bool use_genomicseg_p,
+    int cdna_direction, gsnapdp_bool watsonp, gsnapdp_bool jump_late_p, int maxpeelback, int nullgap,
+    int extramaterial_paired, int extraband_paired, double defect_rate, gsnapdp_Pairpool_T pairpool,
+    gsnapdp_Dynprog_T dynprogL, gsnapdp_Dynprog_T dynprogR);
+
 /* --- optional additions (not in the reference) ---
  * The shim finds the packed genome on its own: Dynprog_setup's Genome_T
  * (Genome_blocks / Genome_totallength, genome.c:96-107) for an index genome,

@@ -554,7 +554,40 @@ def gmap_trace_case(seed: int = 7) -> None:
     with tempfile.TemporaryDirectory() as d:
         W.write_fasta(os.path.join(d, "g.fa"), [("synthchr", g)])
         W.write_fasta(os.path.join(d, "q.fa"), q)
-        trace_gmap_run("gmap_synth", os.path.join(d, "g.fa"), os.path.join(d, "q.fa"), d, stage3_every=1)
+        trace_gmap_run("gmap_synth", os.path.join(d, "g.fa"), os.path.join(d, "q.fa"), d, stage3_every=1,
+                       end_every=4)
+
+
+def gmap_dual_case(seed: int = 31, ngenes: int = 70, genome_len: int = 900_000) -> None:
+    """build_pairs_dualintrons calls (stage3.c:7592-7733, pass 3b) that cross a
+    short exon: synthetic spliced cDNAs with many 9-16 nt internal exons between
+    long introns, so that Smooth_pairs_by_size marks them (smooth.c:295-323:
+    1e-7 < P(random match) <= 0.1) and traverse_dual_genome_gap (:5980-6364)
+    weighs one intron against two.  Every dual-intron call gmap made is kept
+    (gmap_dual_stage3), replayed first through the reference (s3_replay) to
+    check the recording."""
+    g, qs = W.synthetic_transcripts(seed=seed, ngenes=ngenes, genome_len=genome_len, small_frac=0.35,
+                                    small_len=(9, 17), intron_len=(600, 4001))
+    from gsnapdp.records import S3_DUALINTRONS
+    with tempfile.TemporaryDirectory() as d:
+        W.write_fasta(os.path.join(d, "g.fa"), [("synthchr", g)])
+        W.write_fasta(os.path.join(d, "q.fa"), qs)
+        env = dict(os.environ, GMAP_TRACE_DIR=os.path.join(d, "trace"))
+        subprocess.run([GMAP_TRACE, "-A", "-g", os.path.join(d, "g.fa"), os.path.join(d, "q.fa")], env=env,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True)
+        blocks = np.fromfile(os.path.join(d, "trace", "dp", "genome.u32"), dtype="<u4")
+        c, pi, po, q, qu = stage3_trace(os.path.join(d, "trace", "bpi"))
+    sel = c[c["pass"] == S3_DUALINTRONS]
+    dd = stage3_pack(sel, pi, po, q, qu)
+    rc, rp = s3_replay(blocks, dd["calls"], dd["pairs_in"], dd["query"], dd["query_uc"])
+    for f in ("nout", "out_major"):
+        assert np.array_equal(rc[f], dd["calls"][f]), f
+    np.savez_compressed(os.path.join(OUT, "gmap_dual_stage3.npz"), blocks=blocks, ncalls_traced=np.int32(c.size), **dd)
+    ran = sel["out_major"] != sel["in_major"]
+    print("gmap_dual_stage3: %d dual-intron calls of %d pass calls; %d ran traverse_dual_genome_gap (%d DP windows), "
+          "%d changed their list, %d path pairs" %
+          (sel.size, c.size, int(ran.sum()), int((sel["in_major"] - sel["out_major"]).sum()),
+           int((sel["nout"] != sel["npairs"]).sum()), dd["pairs_in"].size))
 
 
 def site_intervals(sic, sip, rng, site_level: bool) -> np.ndarray:
@@ -785,16 +818,25 @@ def stage3_trace(t: str):
     return c, pi, po, q, qu
 
 
-def stage3_golden(prefix: str, t: str, blocks: np.ndarray, every: int) -> None:
-    """Every `every`-th build_pairs_introns call gmap made (stage3_pack)."""
+def stage3_golden(prefix: str, t: str, blocks: np.ndarray, every: int, end_every: int = 1) -> None:
+    """Every `every`-th stage-3 pass call gmap made (stage3_pack): build_pairs_introns,
+    build_pairs_singles, build_pairs_dualintrons, and of build_pairs_end5 /
+    build_path_end3 (one window each, their paths the bulk of the bytes) every
+    `end_every`-th."""
+    from gsnapdp.records import S3_END3, S3_END5
     c, pi, po, q, qu = stage3_trace(t)
-    d = stage3_pack(c[::every], pi, po, q, qu)
+    assert (c["status"] == 0).all(), "an end pass left knownsplicep / ambig_end_length / chop_exon_p set"
+    idx = np.arange(c.size)
+    end = (c["pass"] == S3_END5) | (c["pass"] == S3_END3)
+    keep = (idx % every == 0) & (~end | (np.cumsum(end) % end_every == 1 % end_every))
+    d = stage3_pack(c[keep], pi, po, q, qu)
     np.savez_compressed(os.path.join(OUT, prefix + "_stage3.npz"), blocks=blocks, every=np.int32(every),
-                        ncalls_traced=np.int32(c.size), **d)
+                        end_every=np.int32(end_every), ncalls_traced=np.int32(c.size), **d)
     sel = d["calls"]
-    print("%s_stage3: %d of %d build_pairs_introns calls (%d final), %d path pairs, %d new pairs, "
-          "reference %.3f s" % (prefix, sel.size, c.size, int(sel["finalp"].sum()), d["pairs_in"].size,
-                                d["out_new"].size, float(sel["ref_seconds"].sum())))
+    print("%s_stage3: %d of %d pass calls (by pass %s; %d final introns), %d path pairs, %d new pairs, "
+          "reference %.3f s" % (prefix, sel.size, c.size, np.bincount(sel["pass"], minlength=5).tolist(),
+                                int(sel["finalp"].sum()), d["pairs_in"].size, d["out_new"].size,
+                                float(sel["ref_seconds"].sum())))
 
 
 S3R = os.path.join(HERE, "_ref", "s3_replay")
@@ -830,7 +872,8 @@ def s3_replay(blocks, c, pi, q, qu, iit_text=None, div="synthchr", novel=1, si=F
                 np.fromfile(os.path.join(d, "si_pairs.bin"), dtype=SI_PAIR))
 
 
-def trace_gmap_run(prefix: str, genome_fa: str, query_fa: str, d: str, stage3_every: int = 1) -> bytes:
+def trace_gmap_run(prefix: str, genome_fa: str, query_fa: str, d: str, stage3_every: int = 1,
+                   end_every: int = 1) -> bytes:
     """Run gmap_trace on (genome, queries), replay every recorded window through
     ref_driver, check it against what gmap got, write PREFIX_gap / PREFIX_ggap."""
     sys.path.insert(0, HERE)
@@ -892,7 +935,7 @@ def trace_gmap_run(prefix: str, genome_fa: str, query_fa: str, d: str, stage3_ev
     np.savez_compressed(os.path.join(OUT, prefix + "_introns.npz"), blocks=blocks, calls=calls, pairs=spairs)
     print("%s_introns: %d score_introns calls, %d pairs, %d bad-intron flags" %
           (prefix, calls.size, spairs.size, int((calls["nbadintrons"] > 0).sum())))
-    stage3_golden(prefix, os.path.join(d, "trace", "bpi"), blocks, stage3_every)
+    stage3_golden(prefix, os.path.join(d, "trace", "bpi"), blocks, stage3_every, end_every)
     return out
 
 
@@ -934,6 +977,7 @@ def main() -> None:
         ("gmap_trace", lambda: gmap_trace_case()),
         ("gmap_her2", lambda: gmap_her2_case()),
         ("gmap_cins", lambda: gmap_cins_case()),
+        ("gmap_dual", lambda: gmap_dual_case()),
         ("c4_pinned", lambda: c4_pinned_case()),
     ]
     for name, fn in cases:

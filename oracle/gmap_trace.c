@@ -33,6 +33,7 @@
 #include <unistd.h>
 
 #include "bool.h"
+#include "chrnum.h"
 #include "dynprog.h"
 #include "list.h"
 #include "listdef.h"
@@ -223,13 +224,14 @@ typedef struct { /* gsnapdp_s3_call (include/gsnapdp.h) */
   int32_t in_minor, in_major, in_nintrons, in_nnonintrons, in_intronlen, in_nonintronlen;
   int32_t out_minor, out_major, out_nintrons, out_nnonintrons, out_intronlen, out_nonintronlen;
   int32_t shiftp, incompletep, novelsplicingp, splicingp;
-  int32_t status, ub, pass, pad;
+  int32_t status, ub, pass, endalign, extramaterial_end, extraband_end, splicesitesp, pad;
   double ref_seconds;
 } BpiCall;
+_Static_assert(sizeof(BpiCall) == sizeof(gsnapdp_s3_call), "BpiCall is gsnapdp_s3_call");
 typedef struct { /* gsnapdp_s3_pair */
   int32_t querypos, genomepos, queryjump, genomejump, dynprogindex, src;
   char cdna, comp, genome;
-  uint8_t flags; /* 1 gapp, 2 knowngapp, 4 disallowedp */
+  uint8_t flags; /* 1 gapp, 2 knowngapp, 4 disallowedp, 8 shortexonp, 16 end_intron_p */
 } BpiPair;
 
 static BpiPair bpi_pair(const struct Pair_T *x, int src) {
@@ -243,7 +245,8 @@ static BpiPair bpi_pair(const struct Pair_T *x, int src) {
   r.cdna = x->cdna;
   r.comp = x->comp;
   r.genome = x->genome;
-  r.flags = (uint8_t)((x->gapp ? 1 : 0) | (x->knowngapp ? 2 : 0) | (x->disallowedp ? 4 : 0));
+  r.flags = (uint8_t)((x->gapp ? 1 : 0) | (x->knowngapp ? 2 : 0) | (x->disallowedp ? 4 : 0) |
+                      (x->shortexonp ? 8 : 0) | (x->end_intron_p ? 16 : 0));
   return r;
 }
 typedef struct {
@@ -421,10 +424,166 @@ static List_T bps_hook(int *dynprogindex, List_T path, Genomicpos_T chroffset, G
   return out;
 }
 
+/* ---- build_pairs_end5 (stage3.c:7351-7450) and build_path_end3 (:7236-7347),
+ * passes 8, 9a / 9b and 10: pass GSNAPDP_S3_END5 / END3, dynprogindex_minor in
+ * in_minor / out_minor, the Dynprog_T's limits in all three slots.  Their other
+ * outputs are what extend_ending5/3 leave without splice sites (knownsplicep
+ * false, ambig_end_length 0, chop_exon_p false): status 1 marks a call where
+ * they are not (none is expected). */
+typedef List_T (*bpe5_fn_t)(bool *, int *, int *, bool *, int *, List_T, Genomicpos_T, Genomicpos_T, Genomicpos_T,
+                            int, Genomicpos_T, Genomicpos_T, char *, char *, char *, char *, int, bool, bool, int,
+                            int, int, int, int, double, Pairpool_T, Dynprog_T, bool, int);
+typedef List_T (*bpe3_fn_t)(bool *, int *, int *, bool *, int *, List_T, Genomicpos_T, Genomicpos_T, Genomicpos_T,
+                            int, int, Genomicpos_T, Genomicpos_T, char *, char *, char *, char *, int, bool, bool,
+                            int, int, int, int, int, double, Pairpool_T, Dynprog_T, bool, int);
+extern void *gmap_trace_build_pairs_end5_fn(void);
+extern void *gmap_trace_build_path_end3_fn(void);
+extern int gmap_trace_splicesitesp(void);
+static Patch bpe5_p, bpe3_p;
+static void bpe_args(BpiCall *c, int pass, Genomicpos_T chroffset, Genomicpos_T chrhigh, Genomicpos_T chrpos,
+                     int genomiclength, int cdna_direction, bool watsonp, bool jump_late_p, int maxpeelback,
+                     int nullgap, int extramaterial_end, int extraband_end, double defect_rate, Dynprog_T dynprog,
+                     int endalign, int minor) {
+  memset(c, 0, sizeof(*c));
+  c->pass = pass;
+  c->chroffset = chroffset;
+  c->chrhigh = chrhigh;
+  c->chrpos = chrpos;
+  c->genomiclength = genomiclength;
+  c->cdna_direction = cdna_direction;
+  c->watsonp = watsonp;
+  c->jump_late_p = jump_late_p;
+  c->maxpeelback = maxpeelback;
+  c->nullgap = nullgap;
+  c->extramaterial_end = extramaterial_end;
+  c->extraband_end = extraband_end;
+  c->defect_rate = defect_rate;
+  c->endalign = endalign;
+  c->splicesitesp = gmap_trace_splicesitesp();
+  bpi_dynprogs(c, dynprog, dynprog, dynprog);
+  c->in_minor = minor;
+}
+static List_T bpe5_hook(bool *knownsplicep, int *ambig_end_length_5, int *ambig_splicetype_5, bool *chop_exon_p,
+                        int *dynprogindex_minor, List_T pairs, Genomicpos_T chroffset, Genomicpos_T chrhigh,
+                        Genomicpos_T chrpos, int genomiclength, Genomicpos_T knownsplice_limit_low,
+                        Genomicpos_T knownsplice_limit_high, char *queryseq_ptr, char *queryuc_ptr,
+                        char *genomicseg_ptr, char *genomicuc_ptr, int cdna_direction, bool watsonp,
+                        bool jump_late_p, int maxpeelback, int maxpeelback_distalmedial, int nullgap,
+                        int extramaterial_end, int extraband_end, double defect_rate, Pairpool_T pairpool,
+                        Dynprog_T dynprogR, bool extendp, int endalign) {
+  BpiCall c;
+  List_T out;
+  PtrIdx *ix;
+  int n = 0;
+  struct timespec t0;
+  bpe_args(&c, GSNAPDP_S3_END5, chroffset, chrhigh, chrpos, genomiclength, cdna_direction, watsonp, jump_late_p,
+           maxpeelback, nullgap, extramaterial_end, extraband_end, defect_rate, dynprogR, endalign,
+           *dynprogindex_minor);
+  ix = bpi_begin(&c, pairs, queryseq_ptr, queryuc_ptr, (int)strlen(queryseq_ptr), &n);
+  patch_off(&bpe5_p);
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  out = ((bpe5_fn_t)(void *)bpe5_p.entry)(knownsplicep, ambig_end_length_5, ambig_splicetype_5, chop_exon_p,
+                                          dynprogindex_minor, pairs, chroffset, chrhigh, chrpos, genomiclength,
+                                          knownsplice_limit_low, knownsplice_limit_high, queryseq_ptr, queryuc_ptr,
+                                          genomicseg_ptr, genomicuc_ptr, cdna_direction, watsonp, jump_late_p,
+                                          maxpeelback, maxpeelback_distalmedial, nullgap, extramaterial_end,
+                                          extraband_end, defect_rate, pairpool, dynprogR, extendp, endalign);
+  patch_on(&bpe5_p);
+  c.out_minor = *dynprogindex_minor;
+  c.status = (!extendp || *knownsplicep || *ambig_end_length_5 != 0 || *chop_exon_p) ? 1 : 0;
+  bpi_end(&c, out, ix, n, &t0);
+  return out;
+}
+static List_T bpe3_hook(bool *knownsplicep, int *ambig_end_length_3, int *ambig_splicetype_3, bool *chop_exon_p,
+                        int *dynprogindex_minor, List_T path, Genomicpos_T chroffset, Genomicpos_T chrhigh,
+                        Genomicpos_T chrpos, int querylength, int genomiclength, Genomicpos_T knownsplice_limit_low,
+                        Genomicpos_T knownsplice_limit_high, char *queryseq_ptr, char *queryuc_ptr,
+                        char *genomicseg_ptr, char *genomicuc_ptr, int cdna_direction, bool watsonp,
+                        bool jump_late_p, int maxpeelback, int maxpeelback_distalmedial, int nullgap,
+                        int extramaterial_end, int extraband_end, double defect_rate, Pairpool_T pairpool,
+                        Dynprog_T dynprogL, bool extendp, int endalign) {
+  BpiCall c;
+  List_T out;
+  PtrIdx *ix;
+  int n = 0;
+  struct timespec t0;
+  bpe_args(&c, GSNAPDP_S3_END3, chroffset, chrhigh, chrpos, genomiclength, cdna_direction, watsonp, jump_late_p,
+           maxpeelback, nullgap, extramaterial_end, extraband_end, defect_rate, dynprogL, endalign,
+           *dynprogindex_minor);
+  ix = bpi_begin(&c, path, queryseq_ptr, queryuc_ptr, querylength, &n);
+  patch_off(&bpe3_p);
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  out = ((bpe3_fn_t)(void *)bpe3_p.entry)(knownsplicep, ambig_end_length_3, ambig_splicetype_3, chop_exon_p,
+                                          dynprogindex_minor, path, chroffset, chrhigh, chrpos, querylength,
+                                          genomiclength, knownsplice_limit_low, knownsplice_limit_high, queryseq_ptr,
+                                          queryuc_ptr, genomicseg_ptr, genomicuc_ptr, cdna_direction, watsonp,
+                                          jump_late_p, maxpeelback, maxpeelback_distalmedial, nullgap,
+                                          extramaterial_end, extraband_end, defect_rate, pairpool, dynprogL, extendp,
+                                          endalign);
+  patch_on(&bpe3_p);
+  c.out_minor = *dynprogindex_minor;
+  c.status = (!extendp || *knownsplicep || *ambig_end_length_3 != 0 || *chop_exon_p) ? 1 : 0;
+  bpi_end(&c, out, ix, n, &t0);
+  return out;
+}
+
+/* ---- build_pairs_dualintrons (stage3.c:7592-7733), pass 3b: pass
+ * GSNAPDP_S3_DUALINTRONS, dynprogindex_major in in_major / out_major */
+typedef List_T (*bpd_fn_t)(int *, List_T, Chrnum_T, Genomicpos_T, Genomicpos_T, Genomicpos_T, int, char *, char *,
+                           char *, char *, bool, int, bool, bool, int, int, int, int, double, Pairpool_T, Dynprog_T,
+                           Dynprog_T);
+extern void *gmap_trace_build_pairs_dualintrons_fn(void);
+static Patch bpd_p;
+static List_T bpd_hook(int *dynprogindex, List_T path, Chrnum_T chrnum, Genomicpos_T chroffset, Genomicpos_T chrhigh,
+                       Genomicpos_T chrpos, int genomiclength, char *queryseq_ptr, char *queryuc_ptr,
+                       char *genomicseg_ptr, char *genomicuc_ptr, bool use_genomicseg_p, int cdna_direction,
+                       bool watsonp, bool jump_late_p, int maxpeelback, int nullgap, int extramaterial_paired,
+                       int extraband_paired, double defect_rate, Pairpool_T pairpool, Dynprog_T dynprogL,
+                       Dynprog_T dynprogR) {
+  BpiCall c;
+  List_T out;
+  PtrIdx *ix;
+  int n = 0;
+  struct timespec t0;
+  memset(&c, 0, sizeof(c));
+  c.pass = GSNAPDP_S3_DUALINTRONS;
+  c.chroffset = chroffset;
+  c.chrhigh = chrhigh;
+  c.chrpos = chrpos;
+  c.chrnum = (int32_t)chrnum;
+  c.genomiclength = genomiclength;
+  c.cdna_direction = cdna_direction;
+  c.watsonp = watsonp;
+  c.jump_late_p = jump_late_p;
+  c.use_genomicseg_p = use_genomicseg_p;
+  c.maxpeelback = maxpeelback;
+  c.nullgap = nullgap;
+  c.extramaterial_paired = extramaterial_paired;
+  c.extraband_paired = extraband_paired;
+  c.defect_rate = defect_rate;
+  bpi_dynprogs(&c, dynprogL, dynprogL, dynprogR);
+  c.in_major = *dynprogindex;
+  ix = bpi_begin(&c, path, queryseq_ptr, queryuc_ptr, (int)strlen(queryseq_ptr), &n);
+  patch_off(&bpd_p);
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  out = ((bpd_fn_t)(void *)bpd_p.entry)(dynprogindex, path, chrnum, chroffset, chrhigh, chrpos, genomiclength,
+                                        queryseq_ptr, queryuc_ptr, genomicseg_ptr, genomicuc_ptr, use_genomicseg_p,
+                                        cdna_direction, watsonp, jump_late_p, maxpeelback, nullgap,
+                                        extramaterial_paired, extraband_paired, defect_rate, pairpool, dynprogL,
+                                        dynprogR);
+  patch_on(&bpd_p);
+  c.out_major = *dynprogindex;
+  bpi_end(&c, out, ix, n, &t0);
+  return out;
+}
+
 __attribute__((constructor)) static void install_hooks(void) {
   patch_install(&si_p, gmap_trace_score_introns_fn(), (void *)&si_hook);
   patch_install(&bpi_p, gmap_trace_build_pairs_introns_fn(), (void *)&bpi_hook);
   patch_install(&bps_p, gmap_trace_build_pairs_singles_fn(), (void *)&bps_hook);
+  patch_install(&bpe5_p, gmap_trace_build_pairs_end5_fn(), (void *)&bpe5_hook);
+  patch_install(&bpe3_p, gmap_trace_build_path_end3_fn(), (void *)&bpe3_hook);
+  patch_install(&bpd_p, gmap_trace_build_pairs_dualintrons_fn(), (void *)&bpd_hook);
 }
 
 extern unsigned int *__real_Genome_create_blocks(char *genomicseg, unsigned int genomelength);

@@ -31,6 +31,8 @@ AT(gapp, GAPP);
 AT(knowngapp, KNOWNGAPP);
 AT(disallowedp, DISALLOWEDP);
 AT(donor_prob, DONOR_PROB);
+AT(shortexonp, SHORTEXONP);
+AT(end_intron_p, END_INTRON_P);
 _Static_assert(sizeof(struct Pair_T) == GSNAPDP_PAIR_SIZE, "sizeof(Pair_T)");
 _Static_assert(sizeof(bool) == 1, "bool");
 _Static_assert(offsetof(struct List_T, first) == GSNAPDP_LIST_OFF_FIRST, "List_T.first");

@@ -41,6 +41,7 @@
 #include <time.h>
 
 #include "bool.h"
+#include "chrnum.h"
 #include "dynprog.h"
 #include "genome.h"
 #include "iit-read.h"
@@ -62,13 +63,13 @@ typedef struct { /* gsnapdp_s3_call (include/gsnapdp.h) */
   int32_t in_minor, in_major, in_nintrons, in_nnonintrons, in_intronlen, in_nonintronlen;
   int32_t out_minor, out_major, out_nintrons, out_nnonintrons, out_intronlen, out_nonintronlen;
   int32_t shiftp, incompletep, novelsplicingp, splicingp;
-  int32_t status, ub, pass, pad;
+  int32_t status, ub, pass, endalign, extramaterial_end, extraband_end, splicesitesp, pad;
   double ref_seconds;
 } S3Call;
 typedef struct { /* gsnapdp_s3_pair */
   int32_t querypos, genomepos, queryjump, genomejump, dynprogindex, src;
   char cdna, comp, genome;
-  uint8_t flags; /* 1 gapp, 2 knowngapp, 4 disallowedp */
+  uint8_t flags; /* 1 gapp, 2 knowngapp, 4 disallowedp, 8 shortexonp, 16 end_intron_p */
 } S3Pair;
 typedef struct { /* gmap_trace.c SiCall */
   int32_t cdna_direction, watsonp, chrnum, genomiclength, nullgap, use_genomicseg_p;
@@ -94,6 +95,18 @@ extern void *gmap_trace_build_pairs_singles_fn(void);
 typedef List_T (*bps_fn_t)(int *, List_T, Genomicpos_T, Genomicpos_T, Genomicpos_T, Genomicpos_T, char *, char *,
                            char *, char *, int, bool, bool, int, int, int, double, int, Pairpool_T, Dynprog_T);
 extern void *gmap_trace_score_introns_fn(void);
+typedef List_T (*bpe5_fn_t)(bool *, int *, int *, bool *, int *, List_T, Genomicpos_T, Genomicpos_T, Genomicpos_T,
+                            int, Genomicpos_T, Genomicpos_T, char *, char *, char *, char *, int, bool, bool, int,
+                            int, int, int, int, double, Pairpool_T, Dynprog_T, bool, int);
+typedef List_T (*bpe3_fn_t)(bool *, int *, int *, bool *, int *, List_T, Genomicpos_T, Genomicpos_T, Genomicpos_T,
+                            int, int, Genomicpos_T, Genomicpos_T, char *, char *, char *, char *, int, bool, bool,
+                            int, int, int, int, int, double, Pairpool_T, Dynprog_T, bool, int);
+typedef List_T (*bpd_fn_t)(int *, List_T, Chrnum_T, Genomicpos_T, Genomicpos_T, Genomicpos_T, int, char *, char *,
+                           char *, char *, bool, int, bool, bool, int, int, int, int, double, Pairpool_T, Dynprog_T,
+                           Dynprog_T);
+extern void *gmap_trace_build_pairs_end5_fn(void);
+extern void *gmap_trace_build_path_end3_fn(void);
+extern void *gmap_trace_build_pairs_dualintrons_fn(void);
 
 static void *slurp(const char *dir, const char *name, size_t *n) {
   char path[4096];
@@ -153,7 +166,8 @@ static S3Pair rec(const struct Pair_T *x, int src) {
   r.cdna = x->cdna;
   r.comp = x->comp;
   r.genome = x->genome;
-  r.flags = (uint8_t)((x->gapp ? 1 : 0) | (x->knowngapp ? 2 : 0) | (x->disallowedp ? 4 : 0));
+  r.flags = (uint8_t)((x->gapp ? 1 : 0) | (x->knowngapp ? 2 : 0) | (x->disallowedp ? 4 : 0) |
+                      (x->shortexonp ? 8 : 0) | (x->end_intron_p ? 16 : 0));
   return r;
 }
 
@@ -175,6 +189,9 @@ int main(int argc, char **argv) {
   Dynprog_T dynprogL, dynprogM, dynprogR;
   bpi_fn_t bpi = (bpi_fn_t)gmap_trace_build_pairs_introns_fn();
   bps_fn_t bps = (bps_fn_t)gmap_trace_build_pairs_singles_fn();
+  bpe5_fn_t bpe5 = (bpe5_fn_t)gmap_trace_build_pairs_end5_fn();
+  bpe3_fn_t bpe3 = (bpe3_fn_t)gmap_trace_build_path_end3_fn();
+  bpd_fn_t bpd = (bpd_fn_t)gmap_trace_build_pairs_dualintrons_fn();
   si_fn_t si = (si_fn_t)gmap_trace_score_introns_fn();
 
   if (argc < 2) {
@@ -264,13 +281,36 @@ int main(int argc, char **argv) {
       y->gapp = (x->flags & 1) ? true : false;
       y->knowngapp = (x->flags & 2) ? true : false;
       y->disallowedp = (x->flags & 4) ? true : false;
+      y->shortexonp = (x->flags & 8) ? true : false;
+      y->end_intron_p = (x->flags & 16) ? true : false;
       inptr[j].p = y;
       inptr[j].i = j;
     }
     qsort(inptr, (size_t)c->npairs, sizeof(PtrIdx), cmp_ptr);
     if (poison >= 0) poison_stack(poison);
     clock_gettime(CLOCK_MONOTONIC, &t0);
-    if (c->pass == 1) /* GSNAPDP_S3_SINGLES: build_pairs_singles (stage3.c:7454) */
+    if (c->pass == 2 || c->pass == 3) { /* GSNAPDP_S3_END5 / END3 (stage3.c:7351 / 7236), extendp */
+      bool knownsplicep = false, chop_exon_p = false;
+      int ambig_end_length = 0, ambig_splicetype = 0;
+      if (c->pass == 2)
+        out = bpe5(&knownsplicep, &ambig_end_length, &ambig_splicetype, &chop_exon_p, &minor, path, c->chroffset,
+                   c->chrhigh, c->chrpos, c->genomiclength, 0, 0, q + c->qpos, qu + c->qpos, NULL, NULL,
+                   c->cdna_direction, c->watsonp ? true : false, c->jump_late_p ? true : false, c->maxpeelback,
+                   c->maxpeelback, c->nullgap, c->extramaterial_end, c->extraband_end, c->defect_rate, pool,
+                   dynprogR, true, c->endalign);
+      else
+        out = bpe3(&knownsplicep, &ambig_end_length, &ambig_splicetype, &chop_exon_p, &minor, path, c->chroffset,
+                   c->chrhigh, c->chrpos, c->querylength, c->genomiclength, 0, 0, q + c->qpos, qu + c->qpos, NULL,
+                   NULL, c->cdna_direction, c->watsonp ? true : false, c->jump_late_p ? true : false,
+                   c->maxpeelback, c->maxpeelback, c->nullgap, c->extramaterial_end, c->extraband_end,
+                   c->defect_rate, pool, dynprogL, true, c->endalign);
+      c->status = (knownsplicep || ambig_end_length != 0 || chop_exon_p) ? 1 : 0;
+    } else if (c->pass == 4) /* GSNAPDP_S3_DUALINTRONS (stage3.c:7592) */
+      out = bpd(&major, path, (Chrnum_T)c->chrnum, c->chroffset, c->chrhigh, c->chrpos, c->genomiclength,
+                q + c->qpos, qu + c->qpos, NULL, NULL, c->use_genomicseg_p ? true : false, c->cdna_direction,
+                c->watsonp ? true : false, c->jump_late_p ? true : false, c->maxpeelback, c->nullgap,
+                c->extramaterial_paired, c->extraband_paired, c->defect_rate, pool, dynprogL, dynprogR);
+    else if (c->pass == 1) /* GSNAPDP_S3_SINGLES: build_pairs_singles (stage3.c:7454) */
       out = bps(&minor, path, c->chroffset, c->chrhigh, c->chrpos, (Genomicpos_T)c->genomiclength, q + c->qpos,
                 qu + c->qpos, NULL, NULL, c->cdna_direction, c->watsonp ? true : false,
                 c->jump_late_p ? true : false, c->maxpeelback, c->nullgap, c->extraband_single, c->defect_rate,
@@ -308,7 +348,7 @@ int main(int argc, char **argv) {
     c->out_nonintronlen = nonintronlen;
     c->shiftp = shiftp;
     c->incompletep = incompletep;
-    c->status = 0;
+    if (c->pass != 2 && c->pass != 3) c->status = 0;
     if (do_si) { /* stage3_compute after path_compute (:9890-9941): score_introns(List_reverse(pairs)) */
       SiCall *s = &sic[i];
       double d = 0.0, acc = 0.0;

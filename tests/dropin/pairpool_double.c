@@ -192,7 +192,7 @@ List_T dbl_list_build(const PathRec* recs, int n) {
 typedef struct S3Rec {
   int querypos, genomepos, queryjump, genomejump, dynprogindex, src;
   char cdna, comp, genome;
-  unsigned char flags; /* 1 gapp, 2 knowngapp, 4 disallowedp */
+  unsigned char flags; /* 1 gapp, 2 knowngapp, 4 disallowedp, 8 shortexonp, 16 end_intron_p */
 } S3Rec;
 List_T dbl_s3_build(const S3Rec* recs, int n) {
   List_T list = NULL;
@@ -211,6 +211,8 @@ List_T dbl_s3_build(const S3Rec* recs, int n) {
     r->gapp = recs[i].flags & 1;
     r->knowngapp = (recs[i].flags >> 1) & 1;
     r->disallowedp = (recs[i].flags >> 2) & 1;
+    r->shortexonp = (recs[i].flags >> 3) & 1;
+    r->end_intron_p = (recs[i].flags >> 4) & 1;
     list = cons(list, r);
   }
   return list;
@@ -231,7 +233,8 @@ int dbl_s3_read(List_T list, S3Rec* out, int cap) {
       o->cdna = p->cdna;
       o->comp = p->comp;
       o->genome = p->genome;
-      o->flags = (unsigned char)((p->gapp ? 1 : 0) | (p->knowngapp ? 2 : 0) | (p->disallowedp ? 4 : 0));
+      o->flags = (unsigned char)((p->gapp ? 1 : 0) | (p->knowngapp ? 2 : 0) | (p->disallowedp ? 4 : 0) |
+                                 (p->shortexonp ? 8 : 0) | (p->end_intron_p ? 16 : 0));
     }
   }
   return n;

@@ -74,9 +74,10 @@ def test_gpu_stage3_pass_at_scale(golden_dir):
     ctx.close()
 
 
-@pytest.mark.parametrize("name", ["gmap_synth_stage3", "gmap_cins_stage3"] + IIT_NAMES)
+@pytest.mark.parametrize("name", ["gmap_synth_stage3", "gmap_cins_stage3", "gmap_dual_stage3"] + IIT_NAMES)
 def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name):
-    """Gsnapdp_build_pairs_introns and Gsnapdp_build_pairs_singles as stage3.c would call them (the reference's
+    """Gsnapdp_build_pairs_introns, _singles, _end5, _dualintrons and
+    Gsnapdp_build_path_end3 as stage3.c would call them (the reference's
     signature): the path as a List_T of the host's Pair_T cells, the counters
     as in/out arguments, the returned list (kept cells and pushed pairs, with
     disallowedp).  The IIT sets give Dynprog_setup a splicing IIT (the IIT test
@@ -84,7 +85,7 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     import ctypes
     import subprocess
 
-    from gsnapdp.records import S3_PAIR, S3_SINGLES
+    from gsnapdp.records import S3_DUALINTRONS, S3_END3, S3_END5, S3_PAIR, S3_SINGLES
     from test_dropin import SETUP_ARGS, load_iit_double
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -104,6 +105,16 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     L.Gsnapdp_build_pairs_singles.restype = vp
     L.Gsnapdp_build_pairs_singles.argtypes = [vp, vp, u32, u32, u32, u32, vp, vp, vp, vp, i32, u8, u8, i32, i32,
                                               i32, ctypes.c_double, i32, vp, vp]
+    dbl_ = ctypes.c_double
+    L.Gsnapdp_build_pairs_end5.restype = vp
+    L.Gsnapdp_build_pairs_end5.argtypes = ([vp] * 5 + [vp, u32, u32, u32, i32, u32, u32, vp, vp, vp, vp, i32, u8, u8] +
+                                           [i32] * 5 + [dbl_, vp, vp, u8, i32])
+    L.Gsnapdp_build_path_end3.restype = vp
+    L.Gsnapdp_build_path_end3.argtypes = ([vp] * 5 + [vp, u32, u32, u32, i32, i32, u32, u32, vp, vp, vp, vp, i32, u8,
+                                                      u8] + [i32] * 5 + [dbl_, vp, vp, u8, i32])
+    L.Gsnapdp_build_pairs_dualintrons.restype = vp
+    L.Gsnapdp_build_pairs_dualintrons.argtypes = ([vp, vp, i32, u32, u32, u32, i32, vp, vp, vp, vp, u8, i32, u8, u8] +
+                                                  [i32] * 4 + [dbl_, vp, vp, vp])
     L.Gsnapdp_build_pairs_introns.restype = vp
     L.Gsnapdp_build_pairs_introns.argtypes = (
         [vp] * 8 + [vp, i32, u32, u32, u32, vp, i32, i32, vp, vp, vp, vp, u8, i32, u8, u8] + [i32] * 5 +
@@ -134,7 +145,7 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     siit = SplicingIIT(iit_intervals(z)) if iit is not None else None
     ub = (ctx.stage3_pass(calls, pin, q, qu, iit=siit)[0]["ub"] & 1) != 0
     ctx.close()
-    nsingles = 0
+    nsingles = nother = 0
     for i, c in enumerate(calls):
         f0, n = int(c["first_pair"]), int(c["npairs"])
         recs = np.ascontiguousarray(pin[f0:f0 + n])
@@ -158,6 +169,39 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
             assert ctr[4].value == int(c["out_minor"]), i
             nsingles += 1
             continue
+        if c["pass"] in (S3_END5, S3_END3):
+            ks, ch = ctypes.c_ubyte(7), ctypes.c_ubyte(7)
+            amb, ambt = ctypes.c_int(7), ctypes.c_int(0)
+            minor = ctypes.c_int(int(c["in_minor"]))
+            common = (int(c["cdna_direction"]), int(c["watsonp"]), int(c["jump_late_p"]), int(c["maxpeelback"]),
+                      int(c["maxpeelback"]), int(c["nullgap"]), int(c["extramaterial_end"]), int(c["extraband_end"]),
+                      float(c["defect_rate"]), None, dp, 1, int(c["endalign"]))
+            head = (ctypes.byref(ks), ctypes.byref(amb), ctypes.byref(ambt), ctypes.byref(ch), ctypes.byref(minor), lst,
+                    int(c["chroffset"]), int(c["chrhigh"]), int(c["chrpos"]))
+            if c["pass"] == S3_END5:
+                out = L.Gsnapdp_build_pairs_end5(*head, int(c["genomiclength"]), 0, 0, qp, qup, None, None, *common)
+            else:
+                out = L.Gsnapdp_build_path_end3(*head, int(c["querylength"]), int(c["genomiclength"]), 0, 0, qp, qup,
+                                                None, None, *common)
+            k = dbl.dbl_s3_read(out, got.ctypes.data, got.size)
+            assert k == len(exp) and got[:k].tobytes() == exp.tobytes(), i
+            assert minor.value == int(c["out_minor"]) and amb.value == 0, i
+            if len(exp):  # extend_ending ran: no known splice, no chopped exon
+                assert (ks.value, ch.value) == (0, 0), i
+            nother += 1
+            continue
+        if c["pass"] == S3_DUALINTRONS:
+            major = ctypes.c_int(int(c["in_major"]))
+            out = L.Gsnapdp_build_pairs_dualintrons(
+                ctypes.byref(major), lst, int(c["chrnum"]), int(c["chroffset"]), int(c["chrhigh"]), int(c["chrpos"]),
+                int(c["genomiclength"]), qp, qup, None, None, 0, int(c["cdna_direction"]), int(c["watsonp"]),
+                int(c["jump_late_p"]), int(c["maxpeelback"]), int(c["nullgap"]), int(c["extramaterial_paired"]),
+                int(c["extraband_paired"]), float(c["defect_rate"]), None, dp, dp)
+            k = dbl.dbl_s3_read(out, got.ctypes.data, got.size)
+            assert k == len(exp) and got[:k].tobytes() == exp.tobytes(), i
+            assert major.value == int(c["out_major"]), i
+            nother += 1
+            continue
         out = L.Gsnapdp_build_pairs_introns(
             ctypes.byref(shift), ctypes.byref(inc), *[ctypes.byref(x) for x in ctr], lst, int(c["chrnum"]),
             int(c["chroffset"]), int(c["chrhigh"]), int(c["chrpos"]), None, int(c["querylength"]),
@@ -174,6 +218,7 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
         assert [x.value for j, x in enumerate(ctr) if not (skip and j in (2, 3))] == [
             int(c[f]) for j, f in enumerate(fields) if not (skip and j in (2, 3))], i
     assert nsingles == int((calls["pass"] == S3_SINGLES).sum())
+    assert nother == int(np.isin(calls["pass"], (S3_END5, S3_END3, S3_DUALINTRONS)).sum())
     if iit is not None:  # back to no IIT for the other tests of this process
         L.Dynprog_setup(1, None, None, -1, -1, None, None, None, 0, None, None, None, None, None)
     L.Dynprog_term()  # releases the device context (the genome array dies with this test)

@@ -22,7 +22,7 @@ from gsnapdp import workload as W
 from gsnapdp.records import S3_CALL, S3_PAIR, S3_SINGLES, S3_STATS
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-NAMES = ["gmap_her2_stage3", "gmap_synth_stage3", "gmap_cins_stage3"]
+NAMES = ["gmap_her2_stage3", "gmap_synth_stage3", "gmap_cins_stage3", "gmap_dual_stage3"]
 # the cDNA-insertion calls replayed through the reference with a splicing IIT
 # (oracle/gen_golden.py gmap_cins_case): site-level with and without novel
 # splicing, intron-level without
@@ -119,7 +119,11 @@ def test_stage3_pass_cpu_matches_reference(golden_dir, tmp_path, name):
     st = np.fromfile(os.path.join(d, "pass_stats.bin"), dtype=S3_STATS)[0]
     check_pass(got_calls, got, calls, want, name, z["ub_ref"] if "ub_ref" in z else None)
     assert st["failed"] == 0 and st["undefined"] == 0
-    assert st["windows"][1] > 0 and st["windows"][3] > 0  # genome gaps and microexons were exercised
+    assert st["windows"][1] > 0  # genome gaps were exercised
+    if name != "gmap_dual_stage3":
+        assert st["windows"][3] > 0  # and microexons
+    else:  # traverse_dual_genome_gap's windows, the reference's dynprogindex_major steps
+        assert st["windows"][1] == int((calls["in_major"] - calls["out_major"]).sum()) >= 300
     if name == "gmap_cins_stage3":
         assert st["windows"][2] >= 200  # traverse_cdna_gap's Dynprog_cdna_gap windows
 
