@@ -798,6 +798,18 @@ int Gsnapdp_dropin_stats2(unsigned long* out, int n) {
   return 18;
 }
 
+// every family, score_introns' k_introns launches included (7 x 3 values)
+int Gsnapdp_dropin_stats3(unsigned long* out, int n) {
+  static const int order[7] = {F_GAP, F_SJ, F_GGAP, F_CGAP, F_MICRO, F_MAXENT, F_INTRONS};
+  std::lock_guard<std::mutex> lock(gb.m);
+  for (int i = 0; i < 7; i++) {
+    if (i < n) out[i] = gb.windows[order[i]];
+    if (7 + i < n) out[7 + i] = gb.batches[order[i]];
+    if (14 + i < n) out[14 + i] = gb.maxbatch[order[i]];
+  }
+  return 21;
+}
+
 int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device) {
   std::lock_guard<std::mutex> lock(g.mu);
   if (g.ctx && (blocks != g.blocks || nwords != g.nwords)) fatal("genome changed after first use");

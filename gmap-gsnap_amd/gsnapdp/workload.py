@@ -1184,32 +1184,48 @@ def c3_cached(reads: int, local_rank: int, seed_genome: int = 3, seed_reads: int
     one node share one copy in the page cache (1.16 GB of blocks + 0.4 GB of
     batch at the C3 size) instead of N private copies and N start-ups.
     Returns (PackedGenome, Batch)."""
+    import hashlib
     import json
     import tempfile
     import time
-    d = cache_dir or os.path.join(tempfile.gettempdir(), "gsnapdp_c3_g%d_r%d_s%g_n%d" % (
-        seed_genome, seed_reads, scale, reads))
+    # the generator's own source names the cache, so an edit to c3_genome /
+    # c3_windows (or anything else in this module) never reuses a stale copy
+    with open(os.path.abspath(__file__), "rb") as f:
+        gen = hashlib.sha1(f.read()).hexdigest()[:12]
+    d = cache_dir or os.path.join(tempfile.gettempdir(), "gsnapdp_c3_g%d_r%d_s%g_n%d_%s" % (
+        seed_genome, seed_reads, scale, reads, gen))
     done = os.path.join(d, "complete.json")
+    failed = os.path.join(d, "error.json")
     names = ("blocks", "windows", "query", "query_uc")
     if not os.path.exists(done):
         if local_rank == 0:
-            g = c3_genome(seed=seed_genome, scale=scale)
-            b = c3_windows(g, n=reads, seed=seed_reads)
             os.makedirs(d, exist_ok=True)
-            for k, a in zip(names, (g.blocks, b.windows, b.query, b.query_uc)):
-                tmp = os.path.join(d, k + ".tmp.npy")
-                np.save(tmp, a, allow_pickle=False)
-                os.replace(tmp, os.path.join(d, k + ".npy"))
+            try:
+                g = c3_genome(seed=seed_genome, scale=scale)
+                b = c3_windows(g, n=reads, seed=seed_reads)
+                for k, a in zip(names, (g.blocks, b.windows, b.query, b.query_uc)):
+                    tmp = os.path.join(d, k + ".tmp.npy")
+                    np.save(tmp, a, allow_pickle=False)
+                    os.replace(tmp, os.path.join(d, k + ".npy"))
+            except BaseException as e:  # tell the waiting ranks instead of letting them time out
+                with open(failed, "w") as f:
+                    json.dump({"error": repr(e)}, f)
+                raise
             with open(done + ".tmp", "w") as f:
-                json.dump({"names": g.names, "lengths": [int(x) for x in g.lengths]}, f)
+                json.dump({"names": g.names, "lengths": [int(x) for x in g.lengths], "generator": gen}, f)
             os.replace(done + ".tmp", done)
         else:
             t0 = time.time()
             while not os.path.exists(done):
+                if os.path.exists(failed):
+                    raise RuntimeError("C3 cache %s: local rank 0 failed: %s" % (d, open(failed).read()))
                 if time.time() - t0 > timeout_s:
                     raise RuntimeError("C3 cache %s not written by local rank 0 within %.0f s" % (d, timeout_s))
                 time.sleep(0.2)
     meta = json.load(open(done))
+    if meta.get("generator") != gen:
+        raise RuntimeError("C3 cache %s was written by another generator (%s, this is %s)" % (
+            d, meta.get("generator"), gen))
     a = {k: np.load(os.path.join(d, k + ".npy"), mmap_mode="r", allow_pickle=False) for k in names}
     return PackedGenome(a["blocks"], meta["names"], np.array(meta["lengths"], np.int64)), \
         Batch(a["windows"], a["query"], a["query_uc"])

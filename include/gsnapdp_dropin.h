@@ -325,9 +325,16 @@ int Gsnapdp_dropin_genome(const unsigned int* blocks, size_t nwords, int device)
  * Writes min(n, 8) values; returns 8.
  * Gsnapdp_dropin_stats2: out[0..5] = windows, out[6..11] = GPU batches,
  * out[12..17] = the largest batch, per family.  Writes min(n, 18) values;
- * returns 18. */
+ * returns 18.
+ * Gsnapdp_dropin_stats3: the same for seven families -- the six above, then
+ * score_introns' paths (Gsnapdp_score_introns, one k_introns launch per batch):
+ * out[0..6] = windows (paths for score_introns), out[7..13] = batches,
+ * out[14..20] = the largest batch.  Writes min(n, 21) values; returns 21.
+ * Each symbol keeps its layout; a caller that wants the newer counters calls the
+ * newer symbol. */
 int Gsnapdp_dropin_stats(unsigned long* out, int n);
 int Gsnapdp_dropin_stats2(unsigned long* out, int n);
+int Gsnapdp_dropin_stats3(unsigned long* out, int n);
 
 /* ---- genome_hr subset (the reference's genome_hr.c is a missing blob;
  * gmap-gsnap_amd/csrc/genome_hr_sites.c): the setup calls gmap.c makes

@@ -101,6 +101,8 @@ def test_dropin_score_introns_matches_reference_golden(golden_dir, tmp_path):
     L.Gsnapdp_dropin_genome(blocks.ctypes.data, blocks.size, 0)
     from test_dropin import REC
     calls, sp = zz["calls"], np.ascontiguousarray(zz["pairs"])
+    st0 = (ctypes.c_ulong * 21)()
+    assert L.Gsnapdp_dropin_stats3(st0, 21) == 21
     for i, c in enumerate(calls):
         f0, npairs = int(c["first_pair"]), int(c["npairs"])
         recs = np.ascontiguousarray(sp[f0:f0 + npairs])
@@ -117,4 +119,7 @@ def test_dropin_score_introns_matches_reference_golden(golden_dir, tmp_path):
         k = dbl.dbl_list_read(out, back.ctypes.data, back.size)
         assert k == npairs and np.array_equal(back["querypos"][:k], recs["querypos"][::-1]), i
         dbl.dbl_list_free(out)
+    st1 = (ctypes.c_ulong * 21)()
+    L.Gsnapdp_dropin_stats3(st1, 21)
+    assert st1[6] - st0[6] == len(calls) and st1[13] > st0[13]  # score_introns' paths and k_introns batches
     L.Dynprog_term()  # releases the device context (the genome array dies with this test)
