@@ -106,6 +106,9 @@ struct gsnapdp_ctx {
   // stage-3 pass executors (gsnapdp_stage3_exec.cpp): staging of idle ones
   std::mutex s3_mu;
   std::vector<void*> s3_pool;
+  // traverse_dual_break's stage-2 realignment, served by the caller
+  // (gsnapdp_stage3_set_stage2)
+  gsnapdp_s3_stage2 s3_stage2 = {nullptr, nullptr};
 };
 // frees the context's idle stage-3 executors (gsnapdp_destroy)
 void gsnapdp__s3_pool_free(gsnapdp_ctx* ctx);

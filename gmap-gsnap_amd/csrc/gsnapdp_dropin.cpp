@@ -19,6 +19,7 @@
 #include <utility>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/gsnapdp.h"
@@ -694,6 +695,18 @@ extern "C" __attribute__((weak)) gsnapdp_List_T Splicetrie_solve_end3(
 using SolveFn = decltype(&Splicetrie_solve_end5);
 
 // The host program's genome accessors (genome.c:96-107), for Dynprog_setup.
+// The host program's stage 2 (stage2.c:4260), which traverse_dual_break calls
+// (stage3.c:7104-7117) for a dual break no single gap can solve
+extern "C" __attribute__((weak)) gsnapdp_List_T Stage2_compute_one(
+    int* stage2_source, int* stage2_indexsize, char* queryseq_ptr, char* queryuc_ptr, int querylength,
+    int query_offset, char* genomicseg_ptr, char* genomicuc_ptr, gsnapdp_Genomicpos_T genomicstart,
+    gsnapdp_Genomicpos_T genomicend, gsnapdp_Genomicpos_T mappingstart, gsnapdp_Genomicpos_T mappingend,
+    gsnapdp_bool plusp, int genestrand, int genomiclength, void* oligoindices, int noligoindices,
+    double proceed_pctcoverage, gsnapdp_Pairpool_T pairpool, void* diagpool, int sufflookback, int nsufflookback,
+    int maxintronlen, gsnapdp_bool localp, gsnapdp_bool skip_repetitive_p, gsnapdp_bool use_shifted_canonical_p,
+    gsnapdp_bool favor_right_p, gsnapdp_bool debug_graphic_p, gsnapdp_bool diagnosticp, void* stopwatch,
+    gsnapdp_bool diag_debug);
+
 extern "C" __attribute__((weak)) unsigned int* Genome_blocks(gsnapdp_Genome_T);
 extern "C" __attribute__((weak)) gsnapdp_Genomicpos_T Genome_totallength(gsnapdp_Genome_T);
 
@@ -716,7 +729,7 @@ extern "C" __attribute__((weak)) gsnapdp_bool IIT_exists_with_divno_signed(
 template <class F>
 F resolve_host(F f, const char* name) {  // weak reference, else a lookup in the process
   if (!f) f = (F)dlsym(RTLD_DEFAULT, name);
-  if (!f) fatal(std::string("a splicing IIT was given but the host program's ") + name + " is not linked");
+  if (!f) fatal(std::string("the host program's ") + name + " is needed here and is not linked");
   return f;
 }
 int host_typed(void*, int chrnum, uint32_t x, uint32_t y, int type, int sign) {
@@ -1578,6 +1591,71 @@ gsnapdp_List_T Gsnapdp_score_introns(double* avg_donor_score, double* avg_accept
 
 namespace {
 
+// ---- traverse_dual_break's stage 2, served by the host program (the pass's
+// stage-2 callback).  Each Gsnapdp_build_dual_breaks call registers its
+// Stage2_compute_one arguments under a tag the pass hands back (`invocation`).
+struct Stage2Args {
+  char *queryseq_ptr, *queryuc_ptr, *genomicseg_ptr, *genomicuc_ptr;
+  int genestrand, watsonp;
+  void* oligoindices;
+  int noligoindices;
+  gsnapdp_Pairpool_T pairpool;
+  void* diagpool;
+  int sufflookback, nsufflookback, maxintronlen;
+};
+std::mutex g_s2_mu;
+std::unordered_map<int, Stage2Args*> g_s2_calls;
+int g_s2_next = 0;
+int stage2_register(Stage2Args* a) {
+  std::lock_guard<std::mutex> l(g_s2_mu);
+  const int id = g_s2_next++ & 0x3fffffff;
+  g_s2_calls[id] = a;
+  return id;
+}
+void stage2_unregister(int id) {
+  std::lock_guard<std::mutex> l(g_s2_mu);
+  g_s2_calls.erase(id);
+}
+int host_stage2(void*, const gsnapdp_s3_call* c, int querydp5, int querydp3, int, int, uint32_t mappingstart,
+                uint32_t mappingend, gsnapdp_s3_pair* out, int cap) {
+  Stage2Args* a;
+  {
+    std::lock_guard<std::mutex> l(g_s2_mu);
+    auto it = g_s2_calls.find(c->invocation);
+    if (it == g_s2_calls.end()) return -1;
+    a = it->second;
+  }
+  static const auto f = resolve_host(&Stage2_compute_one, "Stage2_compute_one");
+  const uint32_t genomicstart = c->chroffset + c->chrpos, genomicend = genomicstart + (uint32_t)c->genomiclength;
+  int source = 0, indexsize = 0;
+  // :7104-7117, as traverse_dual_break calls it
+  gsnapdp_List_T l = f(&source, &indexsize, a->queryseq_ptr + querydp5, a->queryuc_ptr + querydp5,
+                       querydp3 - querydp5 + 1, querydp5, a->genomicseg_ptr, a->genomicuc_ptr, genomicstart,
+                       genomicend, mappingstart, mappingend, a->watsonp, a->genestrand, c->genomiclength,
+                       a->oligoindices, a->noligoindices, 0.80, a->pairpool, a->diagpool, a->sufflookback,
+                       a->nsufflookback, a->maxintronlen, /*localp*/ 1, /*skip_repetitive_p*/ 0,
+                       /*use_shifted_canonical_p*/ 1, /*favor_right_p*/ 0, 0, 0, nullptr, 0);
+  int n = 0;
+  for (const RefList* p = (const RefList*)l; p; p = p->rest, n++) {
+    if (n >= cap) continue;
+    const RefPair* x = (const RefPair*)p->first;
+    gsnapdp_s3_pair& o = out[n];
+    o.querypos = x->querypos;
+    o.genomepos = (int32_t)x->genomepos;
+    o.queryjump = x->queryjump;
+    o.genomejump = x->genomejump;
+    o.dynprogindex = x->dynprogindex;
+    o.src = -1;
+    o.cdna = x->cdna;
+    o.comp = x->comp;
+    o.genome = x->genome;
+    o.flags = (uint8_t)((x->gapp ? GSNAPDP_S3_GAPP : 0) | (x->knowngapp ? GSNAPDP_S3_KNOWNGAPP : 0) |
+                        (x->disallowedp ? GSNAPDP_S3_DISALLOWED : 0) | (x->shortexonp ? GSNAPDP_S3_SHORTEXON : 0) |
+                        (x->end_intron_p ? GSNAPDP_S3_END_INTRON : 0));
+  }
+  return n;
+}
+
 // One path through gsnapdp_stage3_pass_compact (k holds the call's arguments and
 // in-counters) and back as the reference's list: its own cells for the pairs it
 // keeps (disallowedp set where the reference sets it, stage3.c:5873-5880) and the
@@ -1585,6 +1663,10 @@ namespace {
 gsnapdp_List_T pass_one(gsnapdp_s3_call& k, gsnapdp_List_T path, char* queryseq_ptr, char* queryuc_ptr,
                         gsnapdp_Pairpool_T pairpool, const gsnapdp_iit* iit, const char* what) {
   gsnapdp_ctx* c = shared_ctx(true);
+  if (k.pass == GSNAPDP_S3_DUALBREAKS) {  // the host's stage 2 for traverse_dual_break (a context may be new)
+    const gsnapdp_s3_stage2 s2 = {nullptr, host_stage2};
+    gsnapdp_stage3_set_stage2(c, &s2);
+  }
   thread_local std::vector<RefList*> incells;  // per gmap worker thread
   thread_local std::vector<gsnapdp_s3_pair> in;
   incells.clear();
@@ -1846,6 +1928,49 @@ gsnapdp_List_T Gsnapdp_build_path_end3(
   gsnapdp_List_T list = pass_one(k, path, queryseq_ptr, queryuc_ptr, pairpool, nullptr, "build_path_end3");
   *chop_exon_p = 0;
   *knownsplicep = 0;
+  *dynprogindex_minor = k.out_minor;
+  return list;
+}
+
+// build_dual_breaks (stage3.c:7149-7232), pass 5 of path_compute (:8831): a
+// dual break solvable as a single gap runs traverse_single_gap (forcep) in the
+// batched pass; one that is not calls the host program's own stage 2 through
+// the pass's stage-2 callback, with this call's oligoindices and pools.
+gsnapdp_List_T Gsnapdp_build_dual_breaks(
+    gsnapdp_bool* dual_break_p, int* dynprogindex_minor, gsnapdp_List_T path, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos, gsnapdp_Genomicpos_T genomiclength,
+    char* queryseq_ptr, char* queryuc_ptr, char* genomicseg_ptr, char* genomicuc_ptr, int cdna_direction,
+    gsnapdp_bool watsonp, int genestrand, gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool,
+    gsnapdp_Dynprog_T dynprogM, int maxpeelback, void* oligoindices_minor, int noligoindices_minor, void* diagpool,
+    int sufflookback, int nsufflookback, int maxintronlen_bound, int extraband_single, double defect_rate,
+    int close_indels_mode) {
+  gsnapdp_s3_call k;
+  memset(&k, 0, sizeof(k));
+  k.pass = GSNAPDP_S3_DUALBREAKS;
+  k.querylength = (int32_t)strlen(queryseq_ptr);
+  k.chroffset = chroffset;
+  k.chrhigh = chrhigh;
+  k.chrpos = chrpos;
+  k.genomiclength = (int32_t)genomiclength;
+  k.cdna_direction = cdna_direction;
+  k.watsonp = watsonp ? 1 : 0;
+  k.jump_late_p = jump_late_p ? 1 : 0;
+  k.maxpeelback = maxpeelback;
+  k.extraband_single = extraband_single;
+  k.close_indels_mode = close_indels_mode;
+  k.defect_rate = defect_rate;
+  for (int i = 0; i < 3; i++) {
+    k.maxlength1[i] = ((const Dynprog*)dynprogM)->maxlength1;
+    k.maxlength2[i] = ((const Dynprog*)dynprogM)->maxlength2;
+  }
+  k.in_minor = *dynprogindex_minor;
+  Stage2Args a = {queryseq_ptr, queryuc_ptr, genomicseg_ptr, genomicuc_ptr, genestrand, watsonp ? 1 : 0,
+                  oligoindices_minor, noligoindices_minor, pairpool, diagpool, sufflookback, nsufflookback,
+                  maxintronlen_bound};
+  k.invocation = stage2_register(&a);
+  gsnapdp_List_T list = pass_one(k, path, queryseq_ptr, queryuc_ptr, pairpool, nullptr, "build_dual_breaks");
+  stage2_unregister(k.invocation);
+  *dual_break_p = k.shiftp ? 1 : 0;
   *dynprogindex_minor = k.out_minor;
   return list;
 }

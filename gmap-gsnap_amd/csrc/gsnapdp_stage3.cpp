@@ -926,11 +926,13 @@ void put_back(Path& k) {
   k.path = k.A.transfer(k.path, k.peeled_path);
 }
 void end_gap(Path& k, bool filledp) {  // build_pairs_introns after a traverse_*
-  if (!filledp) k.pairs = k.A.push_existing(k.pairs, k.gapcell);  // replace the gap
+  // replace the gap; build_dual_breaks never does (:7196-7224)
+  if (!filledp && k.c->pass != GSNAPDP_S3_DUALBREAKS) k.pairs = k.A.push_existing(k.pairs, k.gapcell);
   k.stage = S_SCAN;
 }
 
-// traverse_single_gap (:5381-5515), forcep = false.  Returns true when it waits.
+// traverse_single_gap (:5381-5515): forcep = false, or true in build_dual_breaks.
+// Returns true when it waits.
 bool single_start(Path& k) {
   const gsnapdp_s3_call& c = *k.c;
   bool mm = false;
@@ -952,6 +954,10 @@ void single_done(Pass& P, Path& k) {
   const gsnapdp_s3_call& c = *k.c;
   int gappairs = -1;
   if (!done_single(P, k, &gappairs)) return;
+  if (c.pass == GSNAPDP_S3_DUALBREAKS) {  // forcep: "Intended for build_dual_breaks" (:5475-5479)
+    k.pairs = k.A.transfer(k.pairs, gappairs);
+    return end_gap(k, true);
+  }
   std::string err;
   int origscore = peeled_score(k.A, k.peeled_pairs, c.cdna_direction, c.defect_rate, &err);
   origscore += peeled_score(k.A, k.peeled_path, c.cdna_direction, c.defect_rate, &err);
@@ -1409,6 +1415,46 @@ bool dual_gap(Pass& P, Path& k, int gapcell, int gap) {
   return dual_start(P, k);
 }
 
+// traverse_dual_break (:7044-7142): peel one pair each side, ask the caller's
+// stage 2 for the stretch, keep its list if it bridges the whole stretch,
+// otherwise put the peels back under an unknown gap
+void dual_break(Pass& P, Path& k) {
+  const gsnapdp_s3_call& c = *k.c;
+  const gsnapdp_s3_stage2 s2 = gsnapdp::s3_stage2(P.ctx);
+  if (!s2.compute_one) return fail(k, "a dual break needs stage 2 (Stage2_compute_one) and no stage-2 callback is set");
+  bool mm = false;
+  gap_bounds(k);
+  k.pairs = peel_rightward(k.A, &mm, &k.peeled_pairs, k.pairs, &k.querydp3, &k.genomedp3, 1, true);
+  k.path = peel_leftward(k.A, &mm, &k.peeled_path, k.path, &k.querydp5, &k.genomedp5, 1, true);
+  const uint32_t genomicstart = c.chroffset + c.chrpos, genomicend = genomicstart + (uint32_t)c.genomiclength;
+  const uint32_t mappingstart = c.watsonp ? genomicstart + (uint32_t)k.genomedp5 : genomicend - (uint32_t)k.genomedp3;
+  const uint32_t mappingend = c.watsonp ? genomicstart + (uint32_t)k.genomedp3 : genomicend - (uint32_t)k.genomedp5;
+  thread_local std::vector<gsnapdp_s3_pair> v;
+  int cap = 2 * ((k.querydp3 - k.querydp5 + 1) + (k.genomedp3 - k.genomedp5 + 1)) + 64, n;
+  for (;;) {
+    if (cap < 64) cap = 64;
+    v.resize((size_t)cap);
+    n = s2.compute_one(s2.user, &c, k.querydp5, k.querydp3, k.genomedp5, k.genomedp3, mappingstart, mappingend,
+                       v.data(), cap);
+    if (n <= cap) break;
+    cap = n;
+  }
+  if (n < 0) return fail(k, "the stage-2 callback failed");
+  int list = -1;
+  for (int i = n - 1; i >= 0; i--) {  // the caller's list, head first
+    gsnapdp_s3_pair x = v[(size_t)i];
+    x.src = -1;
+    list = k.A.push_pair(list, x);
+  }
+  // lastpair = gappairs->first, firstpair = its last cell (:7121-7122)
+  if (n > 0 && v[(size_t)n - 1].querypos == k.querydp5 && v[0].querypos == k.querydp3) {
+    k.pairs = k.A.transfer(k.pairs, list);
+  } else {
+    dual_unknown_gap(k);
+  }
+  k.stage = S_SCAN;
+}
+
 // build_pairs_introns' loop (:7763-7898) until the path waits or ends
 void scan(Pass& P, Path& k) {
   const gsnapdp_s3_call& c = *k.c;
@@ -1426,6 +1472,27 @@ void scan(Pass& P, Path& k) {
       continue;
     }
     const gsnapdp_s3_pair& g = k.A.at(pair);
+    if (c.pass == GSNAPDP_S3_DUALBREAKS) {  // build_dual_breaks (:7168-7226)
+      if (g.comp != '#') {  // not DUALBREAK_COMP
+        k.pairs = k.A.push_existing(k.pairs, ptr);
+        continue;
+      }
+      // a dual break at an end of the alignment: the gap is dropped (:7179-7187)
+      if (k.path < 0 || k.pairs < 0) continue;
+      k.left = k.A.pairof(k.path);
+      k.right = k.A.pairof(k.pairs);
+      if (k.A.at(k.left).querypos < 0 || k.A.at(k.right).querypos < 0) continue;
+      k.gapcell = ptr;
+      k.peeled_pairs = k.peeled_path = -1;
+      if (g.queryjump != 1 && g.genomejump != 1 && g.genomejump - g.queryjump < SINGLESLEN &&
+          g.queryjump - g.genomejump < SINGLESLEN) {
+        if (single_start(k)) return;  // solved as a single gap, forcep
+        continue;
+      }
+      k.shiftp = true;  // *dual_break_p
+      dual_break(P, k);
+      continue;
+    }
     if (c.pass == GSNAPDP_S3_DUALINTRONS) {  // build_pairs_dualintrons (:7613-7730)
       if (g.queryjump > c.nullgap || g.queryjump > g.genomejump + EXTRAQUERYGAP ||
           g.genomejump <= g.queryjump + MININTRONLEN) {
@@ -1726,13 +1793,22 @@ void unpack_resume(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
 }
 
 bool call_in_range(const gsnapdp_s3_call& c, int64_t npairs_in, size_t query_bytes) {
-  return c.pass >= GSNAPDP_S3_INTRONS && c.pass <= GSNAPDP_S3_DUALINTRONS && c.first_pair >= 0 && c.npairs >= 0 && (int64_t)c.first_pair + c.npairs <= npairs_in && c.qpos >= 0 &&
+  return c.pass >= GSNAPDP_S3_INTRONS && c.pass <= GSNAPDP_S3_DUALBREAKS && c.first_pair >= 0 && c.npairs >= 0 && (int64_t)c.first_pair + c.npairs <= npairs_in && c.qpos >= 0 &&
          c.querylength >= 0 && (uint64_t)c.qpos + (uint64_t)c.querylength <= (uint64_t)query_bytes;
 }
 
 }  // namespace
 
 void gsnapdp::s3_parallel_for(int n, int grain, const std::function<void(int)>& fn) { Workers::get().run(n, grain, fn); }
+
+extern "C" int gsnapdp_stage3_set_stage2(gsnapdp_ctx* ctx, const gsnapdp_s3_stage2* stage2) {
+  if (!ctx) {
+    gsnapdp__set_err("gsnapdp_stage3_set_stage2: no context");
+    return -1;
+  }
+  gsnapdp::s3_set_stage2(ctx, stage2 ? *stage2 : gsnapdp_s3_stage2{nullptr, nullptr});
+  return 0;
+}
 
 namespace {
 

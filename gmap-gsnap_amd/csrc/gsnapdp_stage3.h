@@ -60,4 +60,8 @@ void s3_parallel_for(int n, int grain, const std::function<void(int)>& fn);
 S3Exec* s3_exec_acquire(gsnapdp_ctx* ctx);
 void s3_exec_release(gsnapdp_ctx* ctx, S3Exec* e);
 
+// the context's stage-2 callback for traverse_dual_break (gsnapdp_stage3_set_stage2)
+gsnapdp_s3_stage2 s3_stage2(gsnapdp_ctx* ctx);
+void s3_set_stage2(gsnapdp_ctx* ctx, const gsnapdp_s3_stage2& s2);
+
 }  // namespace gsnapdp

@@ -167,6 +167,15 @@ S3Exec* s3_exec_acquire(gsnapdp_ctx* ctx) {
   return new GpuExec(ctx);
 }
 
+gsnapdp_s3_stage2 s3_stage2(gsnapdp_ctx* ctx) {
+  std::lock_guard<std::mutex> lock(ctx->s3_mu);
+  return ctx->s3_stage2;
+}
+void s3_set_stage2(gsnapdp_ctx* ctx, const gsnapdp_s3_stage2& s2) {
+  std::lock_guard<std::mutex> lock(ctx->s3_mu);
+  ctx->s3_stage2 = s2;
+}
+
 void s3_exec_release(gsnapdp_ctx* ctx, S3Exec* e) {
   if (!e) return;
   std::lock_guard<std::mutex> lock(ctx->s3_mu);

@@ -112,6 +112,8 @@ def lib():
         L.gsnapdp_stage3_pass_compact.argtypes = [vp, vp, i32, vp, ctypes.c_int64, vp, vp, sz, vp, vp,
                                                   ctypes.c_int64, vp, ctypes.c_int64, vp]
         L.gsnapdp_stage3_pass_compact.restype = i32
+        L.gsnapdp_stage3_set_stage2.argtypes = [vp, vp]
+        L.gsnapdp_stage3_set_stage2.restype = i32
         L.gsnapdp_stage3_score_introns.argtypes = [vp, vp, i32, vp, vp, vp]
         L.gsnapdp_stage3_score_introns.restype = i32
         L.gsnapdp_iit_from_intervals.argtypes = [vp, i32]
@@ -543,6 +545,14 @@ class Context:
         if rc != 0:
             raise GsnapdpError("gsnapdp_stage3_pass_compact: %s" % lib().gsnapdp_last_error().decode())
         return c, bufs[0][:int(c["nout"].sum())], bufs[1][:int(st[0]["new_pairs"])], st[0]
+
+    def set_stage2(self, compute_one: int, user: int):
+        """traverse_dual_break's stage-2 realignment (gsnapdp_stage3_set_stage2):
+        `compute_one` the address of a C callback with gsnapdp_s3_stage2's
+        signature, `user` its first argument; 0, 0 clears it."""
+        self._stage2 = (ctypes.c_void_p * 2)(user or None, compute_one or None)
+        if lib().gsnapdp_stage3_set_stage2(self.h, ctypes.addressof(self._stage2)) != 0:
+            raise GsnapdpError("gsnapdp_stage3_set_stage2: %s" % lib().gsnapdp_last_error().decode())
 
     def stage3_score_introns(self, calls: np.ndarray, pairs_out: np.ndarray, iit: "SplicingIIT" = None):
         """score_introns (stage3.c:7935-8162) on the lists stage3_pass returned

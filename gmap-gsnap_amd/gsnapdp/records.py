@@ -142,12 +142,21 @@ S3_CALL = np.dtype([(n, "<i4") for n in "first_pair npairs first_out nout qpos q
                                          "out_minor out_major out_nintrons out_nnonintrons out_intronlen "
                                          "out_nonintronlen shiftp incompletep novelsplicingp splicingp "
                                          "status ub pass endalign extramaterial_end extraband_end splicesitesp "
-                                         "pad").split()] +
+                                         "invocation").split()] +
                    [("ref_seconds", "<f8")])
 assert S3_CALL.itemsize == 224
 # gsnapdp_s3_call.pass: build_pairs_introns, build_pairs_singles, build_pairs_end5, build_path_end3,
-# build_pairs_dualintrons
-S3_INTRONS, S3_SINGLES, S3_END5, S3_END3, S3_DUALINTRONS = 0, 1, 2, 3, 4
+# build_pairs_dualintrons, build_dual_breaks
+S3_INTRONS, S3_SINGLES, S3_END5, S3_END3, S3_DUALINTRONS, S3_DUALBREAKS = 0, 1, 2, 3, 4, 5
+# golden records of gmap_trace (oracle/gmap_trace.c): one Stage2_compute_one call that
+# traverse_dual_break made (its pairs in S3_PAIR records), and one path_compute call
+S2_CALL = np.dtype([(n, "<i4") for n in "invocation query_offset querylength genomiclength".split()] +
+                   [(n, "<u4") for n in "genomicstart genomicend mappingstart mappingend".split()] +
+                   [(n, "<i4") for n in "plusp first_pair npairs pad".split()])
+assert S2_CALL.itemsize == 48
+PC_CALL = np.dtype([(n, "<i4") for n in ("invocation do_final_p stage3debug cdna_direction querylength "
+                                         "genomiclength watsonp pad").split()] + [("defect_rate", "<f8")])
+assert PC_CALL.itemsize == 40
 S3_STATS = np.dtype([("rounds", "<i4"), ("windows", "<i4", 4), ("batches", "<i4", 4), ("undefined", "<i4"),
                      ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3), ("new_pairs", "<i8")])
 assert S3_STATS.itemsize == 80

@@ -585,7 +585,10 @@ enum {
   GSNAPDP_S3_SINGLES = 1,     /* build_pairs_singles (:7454), passes 2A / 2C / 7C */
   GSNAPDP_S3_END5 = 2,        /* build_pairs_end5 (:7351) with extendp, passes 8 / 9a / 10 */
   GSNAPDP_S3_END3 = 3,        /* build_path_end3 (:7236) with extendp, passes 8 / 9b / 10 */
-  GSNAPDP_S3_DUALINTRONS = 4  /* build_pairs_dualintrons (:7592), pass 3b */
+  GSNAPDP_S3_DUALINTRONS = 4, /* build_pairs_dualintrons (:7592), pass 3b */
+  GSNAPDP_S3_DUALBREAKS = 5   /* build_dual_breaks (:7149), pass 5: the gaps solvable as single gaps
+                               * (traverse_single_gap with forcep); a dual break that needs
+                               * traverse_dual_break's stage-2 realignment gives status -1 */
 };
 
 /* One build_pairs_introns call: its arguments (the query bytes at query[qpos],
@@ -605,7 +608,7 @@ typedef struct gsnapdp_s3_call {
   int32_t maxlength1[3], maxlength2[3];  /* dynprogL, dynprogM, dynprogR */
   int32_t in_minor, in_major, in_nintrons, in_nnonintrons, in_intronlen, in_nonintronlen;
   int32_t out_minor, out_major, out_nintrons, out_nnonintrons, out_intronlen, out_nonintronlen;
-  int32_t shiftp, incompletep;
+  int32_t shiftp, incompletep;       /* written (INTRONS); DUALBREAKS: shiftp = *dual_break_p */
   int32_t novelsplicingp, splicingp;  /* Stage3_setup's module flags (stage3.c:238-239) */
   int32_t status;                     /* written: 0, or -1 (the path is left out, nout = 0) */
   int32_t ub;                         /* written: GSNAPDP_S3_UB_INTRONLEN when out_intronlen /
@@ -622,7 +625,8 @@ typedef struct gsnapdp_s3_call {
   int32_t extramaterial_end, extraband_end;  /* END5 / END3 */
   int32_t splicesitesp;               /* END5 / END3: Stage3_setup got splice sites (the
                                        * Dynprog_end5/3_known branch, not served: status -1) */
-  int32_t pad;
+  int32_t invocation;                 /* the caller's tag, passed through (golden records: which
+                                       * path_compute call of gmap the pass call belongs to) */
   double ref_seconds;                 /* golden records: the reference's own call time (ignored) */
 } gsnapdp_s3_call;
 
@@ -672,6 +676,24 @@ int gsnapdp_stage3_pass_compact(gsnapdp_ctx *ctx, gsnapdp_s3_call *calls, int nc
                                 const char *query_uc, size_t query_bytes, const gsnapdp_iit *iit,
                                 int32_t *cells_out, int64_t cells_cap, gsnapdp_s3_pair *new_out, int64_t new_cap,
                                 gsnapdp_s3_stats *stats);
+
+/* traverse_dual_break's stage-2 realignment (stage3.c:7044-7142): build_dual_breaks
+ * runs Stage2_compute_one (stage2.c:4260) on the query bytes [querydp5, querydp3]
+ * of a call's query against genomic [mappingstart, mappingend] (the peeled
+ * gap's bounds in the call's genomic coordinates, genomedp5 / genomedp3), and
+ * stage 2 is the caller's (out of scope here).  The caller writes the list
+ * Stage2_compute_one returns, head first (its last pair first), into out[0 ..
+ * cap) and returns its length (which may exceed cap: the pass then asks again
+ * with room for it), 0 for NULL, or -1 on an error (the path fails).  It is
+ * called from the pass's host threads and must be thread-safe; `call` is the
+ * pass call (its `invocation` is the caller's own tag).  Without one, a dual
+ * break that needs stage 2 fails its path (status -1). */
+typedef struct gsnapdp_s3_stage2 {
+  void *user;
+  int (*compute_one)(void *user, const gsnapdp_s3_call *call, int querydp5, int querydp3, int genomedp5,
+                     int genomedp3, uint32_t mappingstart, uint32_t mappingend, gsnapdp_s3_pair *out, int cap);
+} gsnapdp_s3_stage2;
+int gsnapdp_stage3_set_stage2(gsnapdp_ctx *ctx, const gsnapdp_s3_stage2 *stage2);
 
 /* score_introns (stage3.c:7935-8162) on the lists a pass returned: for every
  * call with status 0, its list reversed into path order (as stage3_compute

@@ -294,6 +294,22 @@ gsnapdp_List_T Gsnapdp_build_path_end3(
     int extraband_end, double defect_rate, gsnapdp_Pairpool_T pairpool, gsnapdp_Dynprog_T dynprogL,
     gsnapdp_bool extendp, gsnapdp_Endalign_T endalign);
 
+/* build_dual_breaks (stage3.c:7149-7232, static there; non-PMAP signature, the
+ * Oligoindex_T * / Diagpool_T arguments as void *): pass 5 of path_compute
+ * (call site :8831).  Same list, dynprogindex_minor and dual_break_p as the
+ * reference: the gaps solvable as single gaps run traverse_single_gap (forcep)
+ * in the batched pass; the others run traverse_dual_break with the host
+ * program's own Stage2_compute_one (stage2.c:4260; looked up in the process)
+ * on this call's oligoindices and pools. */
+gsnapdp_List_T Gsnapdp_build_dual_breaks(
+    gsnapdp_bool* dual_break_p, int* dynprogindex_minor, gsnapdp_List_T path, gsnapdp_Genomicpos_T chroffset,
+    gsnapdp_Genomicpos_T chrhigh, gsnapdp_Genomicpos_T chrpos, gsnapdp_Genomicpos_T genomiclength,
+    char* queryseq_ptr, char* queryuc_ptr, char* genomicseg_ptr, char* genomicuc_ptr, int cdna_direction,
+    gsnapdp_bool watsonp, int genestrand, gsnapdp_bool jump_late_p, gsnapdp_Pairpool_T pairpool,
+    gsnapdp_Dynprog_T dynprogM, int maxpeelback, void* oligoindices_minor, int noligoindices_minor, void* diagpool,
+    int sufflookback, int nsufflookback, int maxintronlen_bound, int extraband_single, double defect_rate,
+    int close_indels_mode);
+
 /* build_pairs_dualintrons (stage3.c:7592-7733, static there; non-PMAP
  * signature; Chrnum_T is an int): pass 3b of path_compute (call site :8746).
  * Same list and dynprogindex_major as the reference; each short exon's

@@ -823,20 +823,26 @@ def stage3_golden(prefix: str, t: str, blocks: np.ndarray, every: int, end_every
     build_pairs_singles, build_pairs_dualintrons, and of build_pairs_end5 /
     build_path_end3 (one window each, their paths the bulk of the bytes) every
     `end_every`-th."""
-    from gsnapdp.records import S3_END3, S3_END5
+    from gsnapdp.records import S3_END3, S3_END5, S3_PAIR
     c, pi, po, q, qu = stage3_trace(t)
     assert (c["status"] == 0).all(), "an end pass left knownsplicep / ambig_end_length / chop_exon_p set"
     idx = np.arange(c.size)
     end = (c["pass"] == S3_END5) | (c["pass"] == S3_END3)
     keep = (idx % every == 0) & (~end | (np.cumsum(end) % end_every == 1 % end_every))
+    from gsnapdp.records import PC_CALL, S2_CALL
     d = stage3_pack(c[keep], pi, po, q, qu)
+    # traverse_dual_break's stage-2 calls and every path_compute call (the pipeline tests)
+    s2c = np.fromfile(os.path.join(t, "stage2_calls.bin"), dtype=S2_CALL)
+    s2p = np.fromfile(os.path.join(t, "stage2_pairs.bin"), dtype=S3_PAIR)
+    pcc = np.fromfile(os.path.join(t, "path_compute.bin"), dtype=PC_CALL)
     np.savez_compressed(os.path.join(OUT, prefix + "_stage3.npz"), blocks=blocks, every=np.int32(every),
-                        end_every=np.int32(end_every), ncalls_traced=np.int32(c.size), **d)
+                        end_every=np.int32(end_every), ncalls_traced=np.int32(c.size), s2_calls=s2c, s2_pairs=s2p,
+                        pc_calls=pcc, **d)
     sel = d["calls"]
     print("%s_stage3: %d of %d pass calls (by pass %s; %d final introns), %d path pairs, %d new pairs, "
-          "reference %.3f s" % (prefix, sel.size, c.size, np.bincount(sel["pass"], minlength=5).tolist(),
-                                int(sel["finalp"].sum()), d["pairs_in"].size, d["out_new"].size,
-                                float(sel["ref_seconds"].sum())))
+          "reference %.3f s; %d path_compute calls, %d stage-2 calls of traverse_dual_break" %
+          (prefix, sel.size, c.size, np.bincount(sel["pass"], minlength=6).tolist(), int(sel["finalp"].sum()),
+           d["pairs_in"].size, d["out_new"].size, float(sel["ref_seconds"].sum()), pcc.size, s2c.size))
 
 
 S3R = os.path.join(HERE, "_ref", "s3_replay")

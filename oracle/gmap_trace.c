@@ -224,7 +224,7 @@ typedef struct { /* gsnapdp_s3_call (include/gsnapdp.h) */
   int32_t in_minor, in_major, in_nintrons, in_nnonintrons, in_intronlen, in_nonintronlen;
   int32_t out_minor, out_major, out_nintrons, out_nnonintrons, out_intronlen, out_nonintronlen;
   int32_t shiftp, incompletep, novelsplicingp, splicingp;
-  int32_t status, ub, pass, endalign, extramaterial_end, extraband_end, splicesitesp, pad;
+  int32_t status, ub, pass, endalign, extramaterial_end, extraband_end, splicesitesp, invocation;
   double ref_seconds;
 } BpiCall;
 _Static_assert(sizeof(BpiCall) == sizeof(gsnapdp_s3_call), "BpiCall is gsnapdp_s3_call");
@@ -315,6 +315,15 @@ static void bpi_dynprogs(BpiCall *c, Dynprog_T dynprogL, Dynprog_T dynprogM, Dyn
   c->maxlength2[2] = ((int *)dynprogR)[1];
 }
 
+/* path_compute (stage3.c:8586), static: patched so that every pass call below
+ * carries the number of the path_compute call it belongs to (`invocation`) */
+static int32_t pc_invocation = -1;
+static Buf pc_calls;
+typedef struct { /* one path_compute call */
+  int32_t invocation, do_final_p, stage3debug, cdna_direction, querylength, genomiclength, watsonp, pad;
+  double defect_rate; /* its output */
+} PcCall;
+
 static List_T bpi_hook(bool *shiftp, bool *incompletep, int *nintrons, int *nnonintrons, int *intronlen,
                        int *nonintronlen, int *dynprogindex_minor, int *dynprogindex_major, List_T path, int chrnum,
                        Genomicpos_T chroffset, Genomicpos_T chrhigh, Genomicpos_T chrpos, void *genome,
@@ -331,6 +340,7 @@ static List_T bpi_hook(bool *shiftp, bool *incompletep, int *nintrons, int *nnon
   struct timespec t0;
   memset(&c, 0, sizeof(c));
   c.pass = GSNAPDP_S3_INTRONS;
+  c.invocation = pc_invocation;
   c.chroffset = chroffset;
   c.chrhigh = chrhigh;
   c.chrpos = chrpos;
@@ -396,6 +406,7 @@ static List_T bps_hook(int *dynprogindex, List_T path, Genomicpos_T chroffset, G
   struct timespec t0;
   memset(&c, 0, sizeof(c));
   c.pass = GSNAPDP_S3_SINGLES;
+  c.invocation = pc_invocation;
   c.chroffset = chroffset;
   c.chrhigh = chrhigh;
   c.chrpos = chrpos;
@@ -446,6 +457,7 @@ static void bpe_args(BpiCall *c, int pass, Genomicpos_T chroffset, Genomicpos_T 
                      int endalign, int minor) {
   memset(c, 0, sizeof(*c));
   c->pass = pass;
+  c->invocation = pc_invocation;
   c->chroffset = chroffset;
   c->chrhigh = chrhigh;
   c->chrpos = chrpos;
@@ -547,6 +559,7 @@ static List_T bpd_hook(int *dynprogindex, List_T path, Chrnum_T chrnum, Genomicp
   struct timespec t0;
   memset(&c, 0, sizeof(c));
   c.pass = GSNAPDP_S3_DUALINTRONS;
+  c.invocation = pc_invocation;
   c.chroffset = chroffset;
   c.chrhigh = chrhigh;
   c.chrpos = chrpos;
@@ -577,6 +590,153 @@ static List_T bpd_hook(int *dynprogindex, List_T path, Chrnum_T chrnum, Genomicp
   return out;
 }
 
+/* ---- build_dual_breaks (stage3.c:7149-7232), pass 5: pass GSNAPDP_S3_DUALBREAKS,
+ * dynprogindex_minor in in_minor / out_minor, *dual_break_p in shiftp */
+typedef List_T (*bdb_fn_t)(bool *, int *, List_T, Genomicpos_T, Genomicpos_T, Genomicpos_T, Genomicpos_T, char *,
+                           char *, char *, char *, int, bool, int, bool, Pairpool_T, Dynprog_T, int, void *, int,
+                           void *, int, int, int, int, double, int);
+extern void *gmap_trace_build_dual_breaks_fn(void);
+static Patch bdb_p;
+static List_T bdb_hook(bool *dual_break_p, int *dynprogindex_minor, List_T path, Genomicpos_T chroffset,
+                       Genomicpos_T chrhigh, Genomicpos_T chrpos, Genomicpos_T genomiclength, char *queryseq_ptr,
+                       char *queryuc_ptr, char *genomicseg_ptr, char *genomicuc_ptr, int cdna_direction,
+                       bool watsonp, int genestrand, bool jump_late_p, Pairpool_T pairpool, Dynprog_T dynprogM,
+                       int maxpeelback, void *oligoindices_minor, int noligoindices_minor, void *diagpool,
+                       int sufflookback, int nsufflookback, int maxintronlen_bound, int extraband_single,
+                       double defect_rate, int close_indels_mode) {
+  BpiCall c;
+  List_T out;
+  PtrIdx *ix;
+  int n = 0;
+  struct timespec t0;
+  memset(&c, 0, sizeof(c));
+  c.pass = GSNAPDP_S3_DUALBREAKS;
+  c.invocation = pc_invocation;
+  c.chroffset = chroffset;
+  c.chrhigh = chrhigh;
+  c.chrpos = chrpos;
+  c.genomiclength = (int32_t)genomiclength;
+  c.cdna_direction = cdna_direction;
+  c.watsonp = watsonp;
+  c.jump_late_p = jump_late_p;
+  c.maxpeelback = maxpeelback;
+  c.extraband_single = extraband_single;
+  c.close_indels_mode = close_indels_mode;
+  c.defect_rate = defect_rate;
+  bpi_dynprogs(&c, dynprogM, dynprogM, dynprogM);
+  c.in_minor = *dynprogindex_minor;
+  ix = bpi_begin(&c, path, queryseq_ptr, queryuc_ptr, (int)strlen(queryseq_ptr), &n);
+  patch_off(&bdb_p);
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  out = ((bdb_fn_t)(void *)bdb_p.entry)(dual_break_p, dynprogindex_minor, path, chroffset, chrhigh, chrpos,
+                                        genomiclength, queryseq_ptr, queryuc_ptr, genomicseg_ptr, genomicuc_ptr,
+                                        cdna_direction, watsonp, genestrand, jump_late_p, pairpool, dynprogM,
+                                        maxpeelback, oligoindices_minor, noligoindices_minor, diagpool, sufflookback,
+                                        nsufflookback, maxintronlen_bound, extraband_single, defect_rate,
+                                        close_indels_mode);
+  patch_on(&bdb_p);
+  c.out_minor = *dynprogindex_minor;
+  c.shiftp = *dual_break_p;
+  bpi_end(&c, out, ix, n, &t0);
+  return out;
+}
+
+/* Stage2_compute_one (stage2.c:4260), which only traverse_dual_break calls
+ * (stage3.c:7104): every call's stretch and the list it returned, so that the
+ * pass's stage-2 callback can be served from the recording (stage 2 itself is
+ * out of scope).  S2Call per call, its pairs (BpiPair, list order, src -1) in
+ * stage2_pairs.bin. */
+typedef struct {
+  int32_t invocation, query_offset, querylength, genomiclength;
+  uint32_t genomicstart, genomicend, mappingstart, mappingend;
+  int32_t plusp, first_pair, npairs, pad;
+} S2Call;
+static Buf s2_calls, s2_pairs;
+extern List_T __real_Stage2_compute_one(int *, int *, char *, char *, int, int, char *, char *, Genomicpos_T,
+                                        Genomicpos_T, Genomicpos_T, Genomicpos_T, bool, int, int, void *, int, double,
+                                        Pairpool_T, void *, int, int, int, bool, bool, bool, bool, bool, bool, void *,
+                                        bool);
+List_T __wrap_Stage2_compute_one(int *stage2_source, int *stage2_indexsize, char *queryseq_ptr, char *queryuc_ptr,
+                                 int querylength, int query_offset, char *genomicseg_ptr, char *genomicuc_ptr,
+                                 Genomicpos_T genomicstart, Genomicpos_T genomicend, Genomicpos_T mappingstart,
+                                 Genomicpos_T mappingend, bool plusp, int genestrand, int genomiclength,
+                                 void *oligoindices, int noligoindices, double proceed_pctcoverage,
+                                 Pairpool_T pairpool, void *diagpool, int sufflookback, int nsufflookback,
+                                 int maxintronlen, bool localp, bool skip_repetitive_p, bool use_shifted_canonical_p,
+                                 bool favor_right_p, bool debug_graphic_p, bool diagnosticp, void *stopwatch,
+                                 bool diag_debug) {
+  List_T out, p;
+  S2Call r;
+  out = __real_Stage2_compute_one(stage2_source, stage2_indexsize, queryseq_ptr, queryuc_ptr, querylength,
+                                  query_offset, genomicseg_ptr, genomicuc_ptr, genomicstart, genomicend, mappingstart,
+                                  mappingend, plusp, genestrand, genomiclength, oligoindices, noligoindices,
+                                  proceed_pctcoverage, pairpool, diagpool, sufflookback, nsufflookback, maxintronlen,
+                                  localp, skip_repetitive_p, use_shifted_canonical_p, favor_right_p, debug_graphic_p,
+                                  diagnosticp, stopwatch, diag_debug);
+  memset(&r, 0, sizeof(r));
+  r.invocation = pc_invocation;
+  r.query_offset = query_offset;
+  r.querylength = querylength;
+  r.genomiclength = genomiclength;
+  r.genomicstart = genomicstart;
+  r.genomicend = genomicend;
+  r.mappingstart = mappingstart;
+  r.mappingend = mappingend;
+  r.plusp = plusp;
+  r.first_pair = (int32_t)(s2_pairs.n / sizeof(BpiPair));
+  for (p = out; p != NULL; p = p->rest) {
+    BpiPair x = bpi_pair((const struct Pair_T *)p->first, -1);
+    put(&s2_pairs, &x, sizeof(x));
+    r.npairs++;
+  }
+  put(&s2_calls, &r, sizeof(r));
+  return out;
+}
+
+/* path_compute with the reference's non-GSNAP, non-PMAP prototype */
+typedef List_T (*pc_fn_t)(double *, int *, int *, List_T, int, bool, int, bool, int, int, char *, char *, char *,
+                          char *, bool, Chrnum_T, Genomicpos_T, Genomicpos_T, Genomicpos_T, Genomicpos_T,
+                          Genomicpos_T, void *, int, int, int, int, int, int, int, int, Pairpool_T, Dynprog_T,
+                          Dynprog_T, Dynprog_T, int, bool, void *, int, void *, int, int, int, int, int, int);
+extern void *gmap_trace_path_compute_fn(void);
+static Patch pc_p;
+static List_T pc_hook(double *defect_rate, int *intronlen, int *nonintronlen, List_T path, int cdna_direction,
+                      bool watsonp, int genestrand, bool jump_late_p, int querylength, int genomiclength,
+                      char *queryseq_ptr, char *queryuc_ptr, char *genomicseg_ptr, char *genomicuc_ptr,
+                      bool use_genomicseg_p, Chrnum_T chrnum, Genomicpos_T chroffset, Genomicpos_T chrhigh,
+                      Genomicpos_T chrpos, Genomicpos_T knownsplice_limit_low, Genomicpos_T knownsplice_limit_high,
+                      void *genome, int maxpeelback, int maxpeelback_distalmedial, int nullgap, int extramaterial_end,
+                      int extraband_end, int extramaterial_paired, int extraband_single, int extraband_paired,
+                      Pairpool_T pairpool, Dynprog_T dynprogL, Dynprog_T dynprogM, Dynprog_T dynprogR,
+                      int stage3debug, bool do_final_p, void *oligoindices_minor, int noligoindices_minor,
+                      void *diagpool, int sufflookback, int nsufflookback, int maxintronlen_bound,
+                      int close_indels_mode, int paired_favor_mode, int zero_offset) {
+  PcCall r;
+  List_T out;
+  memset(&r, 0, sizeof(r));
+  r.invocation = ++pc_invocation;
+  r.do_final_p = do_final_p;
+  r.stage3debug = stage3debug;
+  r.cdna_direction = cdna_direction;
+  r.querylength = querylength;
+  r.genomiclength = genomiclength;
+  r.watsonp = watsonp;
+  patch_off(&pc_p);
+  out = ((pc_fn_t)(void *)pc_p.entry)(defect_rate, intronlen, nonintronlen, path, cdna_direction, watsonp, genestrand,
+                                      jump_late_p, querylength, genomiclength, queryseq_ptr, queryuc_ptr,
+                                      genomicseg_ptr, genomicuc_ptr, use_genomicseg_p, chrnum, chroffset, chrhigh,
+                                      chrpos, knownsplice_limit_low, knownsplice_limit_high, genome, maxpeelback,
+                                      maxpeelback_distalmedial, nullgap, extramaterial_end, extraband_end,
+                                      extramaterial_paired, extraband_single, extraband_paired, pairpool, dynprogL,
+                                      dynprogM, dynprogR, stage3debug, do_final_p, oligoindices_minor,
+                                      noligoindices_minor, diagpool, sufflookback, nsufflookback, maxintronlen_bound,
+                                      close_indels_mode, paired_favor_mode, zero_offset);
+  patch_on(&pc_p);
+  r.defect_rate = *defect_rate;
+  put(&pc_calls, &r, sizeof(r));
+  return out;
+}
+
 __attribute__((constructor)) static void install_hooks(void) {
   patch_install(&si_p, gmap_trace_score_introns_fn(), (void *)&si_hook);
   patch_install(&bpi_p, gmap_trace_build_pairs_introns_fn(), (void *)&bpi_hook);
@@ -584,6 +744,8 @@ __attribute__((constructor)) static void install_hooks(void) {
   patch_install(&bpe5_p, gmap_trace_build_pairs_end5_fn(), (void *)&bpe5_hook);
   patch_install(&bpe3_p, gmap_trace_build_path_end3_fn(), (void *)&bpe3_hook);
   patch_install(&bpd_p, gmap_trace_build_pairs_dualintrons_fn(), (void *)&bpd_hook);
+  patch_install(&bdb_p, gmap_trace_build_dual_breaks_fn(), (void *)&bdb_hook);
+  patch_install(&pc_p, gmap_trace_path_compute_fn(), (void *)&pc_hook);
 }
 
 extern unsigned int *__real_Genome_create_blocks(char *genomicseg, unsigned int genomelength);
@@ -781,5 +943,8 @@ __attribute__((destructor)) static void write_trace(void) {
     spit(dir, "pairs_out.bin", bpi_out.p, bpi_out.n);
     spit(dir, "query.bin", bpi_q.p, bpi_q.n);
     spit(dir, "query_uc.bin", bpi_qu.p, bpi_qu.n);
+    spit(dir, "path_compute.bin", pc_calls.p, pc_calls.n);
+    spit(dir, "stage2_calls.bin", s2_calls.p, s2_calls.n);
+    spit(dir, "stage2_pairs.bin", s2_pairs.p, s2_pairs.n);
   }
 }

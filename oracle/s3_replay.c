@@ -63,7 +63,7 @@ typedef struct { /* gsnapdp_s3_call (include/gsnapdp.h) */
   int32_t in_minor, in_major, in_nintrons, in_nnonintrons, in_intronlen, in_nonintronlen;
   int32_t out_minor, out_major, out_nintrons, out_nnonintrons, out_intronlen, out_nonintronlen;
   int32_t shiftp, incompletep, novelsplicingp, splicingp;
-  int32_t status, ub, pass, endalign, extramaterial_end, extraband_end, splicesitesp, pad;
+  int32_t status, ub, pass, endalign, extramaterial_end, extraband_end, splicesitesp, invocation;
   double ref_seconds;
 } S3Call;
 typedef struct { /* gsnapdp_s3_pair */
@@ -289,6 +289,10 @@ int main(int argc, char **argv) {
     qsort(inptr, (size_t)c->npairs, sizeof(PtrIdx), cmp_ptr);
     if (poison >= 0) poison_stack(poison);
     clock_gettime(CLOCK_MONOTONIC, &t0);
+    if (c->pass < 0 || c->pass > 4) { /* build_dual_breaks needs stage 2's oligoindices: not replayed */
+      fprintf(stderr, "s3_replay: call %zu: pass %d is not replayed\n", i, c->pass);
+      return 6;
+    }
     if (c->pass == 2 || c->pass == 3) { /* GSNAPDP_S3_END5 / END3 (stage3.c:7351 / 7236), extendp */
       bool knownsplicep = false, chop_exon_p = false;
       int ambig_end_length = 0, ambig_splicetype = 0;

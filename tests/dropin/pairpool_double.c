@@ -9,6 +9,7 @@
 #include <signal.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdio.h>
 #include <unistd.h>
 
 /* a crash inside the shim or the host-side code prints its C frames */
@@ -238,4 +239,72 @@ int dbl_s3_read(List_T list, S3Rec* out, int cap) {
     }
   }
   return n;
+}
+
+/* Stage2_compute_one (stage2.c:4260) for the drop-in's traverse_dual_break:
+ * answers from the stage-2 calls gmap_trace recorded (records.S2_CALL and their
+ * lists in S3Rec), matched on the query stretch and the mapping bounds, with a
+ * fresh list of fresh PairRec cells (refquerypos 0: pairs the callee made).
+ * A request the recording does not hold aborts. */
+typedef struct S2Rec {
+  int invocation, query_offset, querylength, genomiclength;
+  unsigned int genomicstart, genomicend, mappingstart, mappingend;
+  int plusp, first_pair, npairs, pad;
+} S2Rec;
+static const S2Rec* s2_calls;
+static const S3Rec* s2_pairs;
+static int s2_ncalls, s2_served;
+void dbl_stage2_load(const S2Rec* calls, int ncalls, const S3Rec* pairs) {
+  s2_calls = calls;
+  s2_ncalls = ncalls;
+  s2_pairs = pairs;
+  s2_served = 0;
+}
+int dbl_stage2_served(void) { return s2_served; }
+List_T Stage2_compute_one(int* stage2_source, int* stage2_indexsize, char* queryseq_ptr, char* queryuc_ptr,
+                          int querylength, int query_offset, char* genomicseg_ptr, char* genomicuc_ptr,
+                          unsigned int genomicstart, unsigned int genomicend, unsigned int mappingstart,
+                          unsigned int mappingend, unsigned char plusp, int genestrand, int genomiclength,
+                          void* oligoindices, int noligoindices, double proceed_pctcoverage, void* pairpool,
+                          void* diagpool, int sufflookback, int nsufflookback, int maxintronlen, unsigned char localp,
+                          unsigned char skip_repetitive_p, unsigned char use_shifted_canonical_p,
+                          unsigned char favor_right_p, unsigned char debug_graphic_p, unsigned char diagnosticp,
+                          void* stopwatch, unsigned char diag_debug) {
+  int i, j;
+  (void)stage2_source, (void)stage2_indexsize, (void)queryseq_ptr, (void)queryuc_ptr, (void)genomicseg_ptr;
+  (void)genomicuc_ptr, (void)plusp, (void)genestrand, (void)oligoindices, (void)noligoindices;
+  (void)proceed_pctcoverage, (void)pairpool, (void)diagpool, (void)sufflookback, (void)nsufflookback;
+  (void)maxintronlen, (void)localp, (void)skip_repetitive_p, (void)use_shifted_canonical_p, (void)favor_right_p;
+  (void)debug_graphic_p, (void)diagnosticp, (void)stopwatch, (void)diag_debug;
+  for (i = 0; i < s2_ncalls; i++) {
+    const S2Rec* r = &s2_calls[i];
+    if (r->query_offset == query_offset && r->querylength == querylength && r->genomicstart == genomicstart &&
+        r->genomicend == genomicend && r->mappingstart == mappingstart && r->mappingend == mappingend &&
+        r->genomiclength == genomiclength) {
+      List_T list = NULL;
+      for (j = r->npairs - 1; j >= 0; j--) {
+        const S3Rec* x = &s2_pairs[r->first_pair + j];
+        PairRec* p = (PairRec*)calloc(1, sizeof(PairRec));
+        p->querypos = x->querypos;
+        p->genomepos = (unsigned int)x->genomepos;
+        p->queryjump = x->queryjump;
+        p->genomejump = x->genomejump;
+        p->dynprogindex = x->dynprogindex;
+        p->cdna = x->cdna;
+        p->comp = x->comp;
+        p->genome = x->genome;
+        p->gapp = x->flags & 1;
+        p->knowngapp = (x->flags >> 1) & 1;
+        p->disallowedp = (x->flags >> 2) & 1;
+        p->shortexonp = (x->flags >> 3) & 1;
+        p->end_intron_p = (x->flags >> 4) & 1;
+        list = cons(list, p);
+      }
+      s2_served++;
+      return list;
+    }
+  }
+  fprintf(stderr, "Stage2_compute_one double: no recorded call for query %d+%d, mapping %u..%u\n", query_offset,
+          querylength, mappingstart, mappingend);
+  abort();
 }

@@ -7,7 +7,8 @@
 // build_pairs_introns calls gmap_trace recorded and compares the lists.
 //
 //   stage3_cpu DIR    reads DIR/{calls,pairs_in,query,query_uc}.bin, DIR/genome.u32 and, when
-//                     present, DIR/intervals.bin (gsnapdp_iit_interval: a splicing IIT);
+//                     present, DIR/intervals.bin (gsnapdp_iit_interval: a splicing IIT) and
+//                     DIR/stage2_{calls,pairs}.bin (traverse_dual_break's recorded stage-2 lists);
 //                     writes DIR/{pass_calls,pass_pairs,pass_stats}.bin, and with
 //                     --introns DIR/pass_scores.bin (score_introns on the returned lists)
 #include <stdio.h>
@@ -18,6 +19,12 @@
 #include <vector>
 
 #include "../../include/gsnapdp.h"
+
+extern "C" {
+void* s2dbl_new(const void* calls, int ncalls, const gsnapdp_s3_pair* pairs, int npairs);
+int s2dbl_compute_one(void* u, const gsnapdp_s3_call* call, int querydp5, int querydp3, int genomedp5,
+                      int genomedp3, uint32_t mappingstart, uint32_t mappingend, gsnapdp_s3_pair* out, int cap);
+}
 
 static std::string g_err;
 extern double g_s3_exec_seconds;  // stage3_exec_host.cpp
@@ -67,6 +74,15 @@ int main(int argc, char** argv) {
     fclose(f);
     std::vector<gsnapdp_iit_interval> iv = slurp<gsnapdp_iit_interval>(d + "/intervals.bin");
     if (!(iit = gsnapdp_iit_from_intervals(iv.data(), (int)iv.size()))) return 4;
+  }
+  void* s2 = nullptr;  // traverse_dual_break's stage-2 lists, from the recording (stage2_double.c)
+  if (FILE* f = fopen((d + "/stage2_calls.bin").c_str(), "rb")) {
+    fclose(f);
+    std::vector<char> sc = slurp<char>(d + "/stage2_calls.bin");
+    std::vector<gsnapdp_s3_pair> sp = slurp<gsnapdp_s3_pair>(d + "/stage2_pairs.bin");
+    s2 = s2dbl_new(sc.data(), (int)(sc.size() / 48), sp.data(), (int)sp.size());
+    gsnapdp_s3_stage2 cb = {s2, s2dbl_compute_one};
+    gsnapdp_stage3_set_stage2(ctx, &cb);
   }
   if (gsnapdp_stage3_pass(ctx, calls.data(), (int)calls.size(), in.data(), (int64_t)in.size(), q.data(),
                           qu.data(), std::min(q.size(), qu.size()), iit, out.data(), cap, &st)) {

@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "../../gmap-gsnap_amd/csrc/gsnapdp_stage3.h"
@@ -62,5 +63,17 @@ S3Exec* s3_exec_acquire(gsnapdp_ctx*) {
   return new ReplayExec();
 }
 void s3_exec_release(gsnapdp_ctx*, S3Exec* e) { delete e; }
+
+// the stage-2 callback (one per process in the test builds)
+static std::mutex g_s2_mu;
+static gsnapdp_s3_stage2 g_s2 = {nullptr, nullptr};
+gsnapdp_s3_stage2 s3_stage2(gsnapdp_ctx*) {
+  std::lock_guard<std::mutex> l(g_s2_mu);
+  return g_s2;
+}
+void s3_set_stage2(gsnapdp_ctx*, const gsnapdp_s3_stage2& s2) {
+  std::lock_guard<std::mutex> l(g_s2_mu);
+  g_s2 = s2;
+}
 
 }  // namespace gsnapdp

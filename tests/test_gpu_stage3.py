@@ -18,13 +18,35 @@ from gsnapdp import workload as W
 from test_stage3_cpu import IIT_NAMES, NAMES, check_pass, check_scores, iit_intervals, stage3_golden
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def stage2_double(ctx, z, tmp):
+    """traverse_dual_break's stage-2 lists served from the golden's recording
+    (tests/dropin/stage2_double.c, built here with gcc) as the context's
+    stage-2 callback.  Returns (the library, its handle) or None."""
+    import ctypes
+    import subprocess
+    if "s2_calls" not in z:
+        return None
+    so = os.path.join(str(tmp), "libstage2_double.so")
+    subprocess.check_call(["gcc", "-O1", "-shared", "-fPIC", "-o", so,
+                           os.path.join(ROOT, "tests", "dropin", "stage2_double.c")])
+    d = ctypes.CDLL(so)
+    d.s2dbl_new.restype = ctypes.c_void_p
+    d.s2dbl_new.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    sc, sp = np.ascontiguousarray(z["s2_calls"]), np.ascontiguousarray(z["s2_pairs"])
+    h = d.s2dbl_new(sc.ctypes.data, sc.size, sp.ctypes.data, sp.size)
+    ctx.set_stage2(ctypes.cast(d.s2dbl_compute_one, ctypes.c_void_p).value, h)
+    return d, h
 
 
 @pytest.mark.parametrize("name", NAMES)
-def test_gpu_stage3_pass_matches_reference(golden_dir, name):
+def test_gpu_stage3_pass_matches_reference(golden_dir, tmp_path, name):
     z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
     calls, pin, q, qu, want = stage3_golden(z)
     ctx = Context(z["blocks"])
+    s2 = stage2_double(ctx, z, tmp_path)
     got_calls, got, st = ctx.stage3_pass(calls, pin, q, qu)
     check_pass(got_calls, got, calls, want, name, z["ub_ref"] if "ub_ref" in z else None)
     assert st["failed"] == 0 and st["undefined"] == 0
@@ -54,10 +76,11 @@ def test_gpu_stage3_pass_with_splicing_iit(golden_dir, name):
     ctx.close()
 
 
-def test_gpu_stage3_pass_at_scale(golden_dir):
+def test_gpu_stage3_pass_at_scale(golden_dir, tmp_path):
     z = np.load(os.path.join(golden_dir, "gmap_synth_stage3.npz"), allow_pickle=False)
     calls, pin, q, qu, want = stage3_golden(z)
     ctx = Context(z["blocks"])
+    s2 = stage2_double(ctx, z, tmp_path)
     ctx.stage3_pass(calls[:8], pin, q, qu)  # warm-up (first launches, staging)
     copies = 16  # 7,424 paths
     C, PI, Q, QU, WANT = W.stage3_calls(z, copies)
@@ -85,7 +108,7 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     import ctypes
     import subprocess
 
-    from gsnapdp.records import S3_DUALINTRONS, S3_END3, S3_END5, S3_PAIR, S3_SINGLES
+    from gsnapdp.records import S3_DUALBREAKS, S3_DUALINTRONS, S3_END3, S3_END5, S3_PAIR, S3_SINGLES
     from test_dropin import SETUP_ARGS, load_iit_double
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -98,6 +121,7 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     dbl.dbl_s3_build.argtypes = [vp, i32]
     dbl.dbl_s3_read.restype = i32
     dbl.dbl_s3_read.argtypes = [vp, vp, i32]
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
     L = ctypes.CDLL(os.path.join(root, "gmap-gsnap_amd", "lib", "libgsnapdp_dropin.so"))
     L.Gsnapdp_dropin_genome.argtypes = [vp, ctypes.c_size_t, i32]
     L.Dynprog_new.restype = vp
@@ -115,11 +139,16 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     L.Gsnapdp_build_pairs_dualintrons.restype = vp
     L.Gsnapdp_build_pairs_dualintrons.argtypes = ([vp, vp, i32, u32, u32, u32, i32, vp, vp, vp, vp, u8, i32, u8, u8] +
                                                   [i32] * 4 + [dbl_, vp, vp, vp])
+    L.Gsnapdp_build_dual_breaks.restype = vp
+    L.Gsnapdp_build_dual_breaks.argtypes = ([vp, vp, vp, u32, u32, u32, u32, vp, vp, vp, vp, i32, u8, i32, u8, vp, vp,
+                                             i32, vp, i32, vp, i32, i32, i32, i32, dbl_, i32])
+    if "s2_calls" in z:  # traverse_dual_break's stage 2: the host's Stage2_compute_one, served by the double
+        s2c, s2p = np.ascontiguousarray(z["s2_calls"]), np.ascontiguousarray(z["s2_pairs"])
+        dbl.dbl_stage2_load(ctypes.c_void_p(s2c.ctypes.data), s2c.size, ctypes.c_void_p(s2p.ctypes.data))
     L.Gsnapdp_build_pairs_introns.restype = vp
     L.Gsnapdp_build_pairs_introns.argtypes = (
         [vp] * 8 + [vp, i32, u32, u32, u32, vp, i32, i32, vp, vp, vp, vp, u8, i32, u8, u8] + [i32] * 5 +
         [ctypes.c_double, i32, vp, vp, vp, vp, u8])
-    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
     calls, pin, q, qu, want = stage3_golden(z)
     assert (calls["maxlength1"] == 611).all() and (calls["maxlength2"] == 2000).all()
     blocks = np.ascontiguousarray(z["blocks"])
@@ -143,6 +172,7 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     # which calls' intron lengths the reference took from uninitialised locals: the pass says
     ctx = Context(z["blocks"])
     siit = SplicingIIT(iit_intervals(z)) if iit is not None else None
+    s2 = stage2_double(ctx, z, tmp_path)
     ub = (ctx.stage3_pass(calls, pin, q, qu, iit=siit)[0]["ub"] & 1) != 0
     ctx.close()
     nsingles = nother = 0
@@ -190,6 +220,18 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
                 assert (ks.value, ch.value) == (0, 0), i
             nother += 1
             continue
+        if c["pass"] == S3_DUALBREAKS:
+            minor, dbp = ctypes.c_int(int(c["in_minor"])), ctypes.c_ubyte(7)
+            out = L.Gsnapdp_build_dual_breaks(
+                ctypes.byref(dbp), ctypes.byref(minor), lst, int(c["chroffset"]), int(c["chrhigh"]), int(c["chrpos"]),
+                int(c["genomiclength"]), qp, qup, None, None, int(c["cdna_direction"]), int(c["watsonp"]), 0,
+                int(c["jump_late_p"]), None, dp, int(c["maxpeelback"]), None, 0, None, 0, 0, 0,
+                int(c["extraband_single"]), float(c["defect_rate"]), int(c["close_indels_mode"]))
+            k = dbl.dbl_s3_read(out, got.ctypes.data, got.size)
+            assert k == len(exp) and got[:k].tobytes() == exp.tobytes(), i
+            assert minor.value == int(c["out_minor"]) and dbp.value == int(c["shiftp"]), i
+            nother += 1
+            continue
         if c["pass"] == S3_DUALINTRONS:
             major = ctypes.c_int(int(c["in_major"]))
             out = L.Gsnapdp_build_pairs_dualintrons(
@@ -218,7 +260,7 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
         assert [x.value for j, x in enumerate(ctr) if not (skip and j in (2, 3))] == [
             int(c[f]) for j, f in enumerate(fields) if not (skip and j in (2, 3))], i
     assert nsingles == int((calls["pass"] == S3_SINGLES).sum())
-    assert nother == int(np.isin(calls["pass"], (S3_END5, S3_END3, S3_DUALINTRONS)).sum())
+    assert nother == int(np.isin(calls["pass"], (S3_END5, S3_END3, S3_DUALINTRONS, S3_DUALBREAKS)).sum())
     if iit is not None:  # back to no IIT for the other tests of this process
         L.Dynprog_setup(1, None, None, -1, -1, None, None, None, 0, None, None, None, None, None)
     L.Dynprog_term()  # releases the device context (the genome array dies with this test)

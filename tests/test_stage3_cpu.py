@@ -60,6 +60,13 @@ def check_pass(calls, out, want_calls, want_out, what, ub_ref=None):
             raise AssertionError("%s: call %d, cell %d of %d: got %s want %s" % (what, i, k, len(exp), got[k], exp[k]))
 
 
+def write_stage2(d, z):
+    """traverse_dual_break's recorded stage-2 lists, for the driver's stage-2 callback"""
+    if "s2_calls" in z:
+        z["s2_calls"].tofile(os.path.join(d, "stage2_calls.bin"))
+        z["s2_pairs"].tofile(os.path.join(d, "stage2_pairs.bin"))
+
+
 def run_stage3_cpu(d, z, calls, pin, q, qu, intervals=None, introns=False):
     """stage3_cpu (ASan + UBSan) on the calls; returns (calls, lists, stats[, scores])"""
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "stage3_cpu"])
@@ -68,6 +75,7 @@ def run_stage3_cpu(d, z, calls, pin, q, qu, intervals=None, introns=False):
     q.tofile(os.path.join(d, "query.bin"))
     qu.tofile(os.path.join(d, "query_uc.bin"))
     z["blocks"].astype("<u4").tofile(os.path.join(d, "genome.u32"))
+    write_stage2(d, z)
     if intervals is not None:
         intervals.tofile(os.path.join(d, "intervals.bin"))
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:halt_on_error=1",
@@ -107,6 +115,7 @@ def test_stage3_pass_cpu_matches_reference(golden_dir, tmp_path, name):
     q.tofile(os.path.join(d, "query.bin"))
     qu.tofile(os.path.join(d, "query_uc.bin"))
     z["blocks"].astype("<u4").tofile(os.path.join(d, "genome.u32"))
+    write_stage2(d, z)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:halt_on_error=1",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
                GSNAPDP_MAXENT_TABLES=os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin"))
