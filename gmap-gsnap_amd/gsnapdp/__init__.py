@@ -112,6 +112,9 @@ def lib():
         L.gsnapdp_stage3_pass_compact.argtypes = [vp, vp, i32, vp, ctypes.c_int64, vp, vp, sz, vp, vp,
                                                   ctypes.c_int64, vp, ctypes.c_int64, vp]
         L.gsnapdp_stage3_pass_compact.restype = i32
+        L.gsnapdp_stage3_compute.argtypes = [vp, vp, i32, vp, ctypes.c_int64, vp, vp, sz, vp, i32, vp,
+                                             ctypes.c_int64, vp]
+        L.gsnapdp_stage3_compute.restype = i32
         L.gsnapdp_stage3_set_stage2.argtypes = [vp, vp]
         L.gsnapdp_stage3_set_stage2.restype = i32
         L.gsnapdp_stage3_score_introns.argtypes = [vp, vp, i32, vp, vp, vp]
@@ -545,6 +548,27 @@ class Context:
         if rc != 0:
             raise GsnapdpError("gsnapdp_stage3_pass_compact: %s" % lib().gsnapdp_last_error().decode())
         return c, bufs[0][:int(c["nout"].sum())], bufs[1][:int(st[0]["new_pairs"])], st[0]
+
+    def stage3_compute(self, queries: np.ndarray, paths_in: np.ndarray, query: np.ndarray, query_uc: np.ndarray,
+                       iit: "SplicingIIT" = None, min_intronlength: int = 9, out: np.ndarray = None):
+        """Passes 2A-6 of path_compute (stage3.c:8639-8876) for every query
+        (gsnapdp_stage3_compute).  Returns (queries with the out fields written,
+        the lists after pass 6 concatenated, S3_COMPUTE_STATS)."""
+        from .records import S3_COMPUTE_STATS
+        c = np.array(queries, dtype=S3_CALL, copy=True)
+        pi = np.ascontiguousarray(paths_in, dtype=S3_PAIR)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        cap = 2 * self.stage3_capacity(c) + 1024
+        if out is None or out.dtype != S3_PAIR or out.size < cap:
+            out = np.empty(cap, dtype=S3_PAIR)
+        st = np.zeros(1, dtype=S3_COMPUTE_STATS)
+        rc = lib().gsnapdp_stage3_compute(self.h, _p(c), len(c), _p(pi) if pi.size else _p(out), pi.size, _p(q),
+                                          _p(qu), min(q.size, qu.size), iit.h if iit is not None else None,
+                                          int(min_intronlength), _p(out), out.size, _p(st))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_stage3_compute: %s" % lib().gsnapdp_last_error().decode())
+        return c, out[:int(c["nout"].sum())], st[0]
 
     def set_stage2(self, compute_one: int, user: int):
         """traverse_dual_break's stage-2 realignment (gsnapdp_stage3_set_stage2):

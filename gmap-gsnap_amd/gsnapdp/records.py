@@ -157,6 +157,9 @@ assert S2_CALL.itemsize == 48
 PC_CALL = np.dtype([(n, "<i4") for n in ("invocation do_final_p stage3debug cdna_direction querylength "
                                          "genomiclength watsonp pad").split()] + [("defect_rate", "<f8")])
 assert PC_CALL.itemsize == 40
+S3_COMPUTE_STATS = np.dtype([("passes", "<i4"), ("rounds", "<i4"), ("windows", "<i4", 4), ("pass_calls", "<i4", 6),
+                             ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3)])
+assert S3_COMPUTE_STATS.itemsize == 80
 S3_STATS = np.dtype([("rounds", "<i4"), ("windows", "<i4", 4), ("batches", "<i4", 4), ("undefined", "<i4"),
                      ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3), ("new_pairs", "<i8")])
 assert S3_STATS.itemsize == 80

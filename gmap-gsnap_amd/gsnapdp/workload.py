@@ -1231,6 +1231,62 @@ def c3_cached(reads: int, local_rank: int, seed_genome: int = 3, seed_reads: int
         Batch(a["windows"], a["query"], a["query_uc"])
 
 
+def stage3_pipeline(z, copies: int = 1):
+    """The path_compute calls of a recorded gmap run (tests/golden/gmap_*_stage3.npz,
+    whose pass calls carry their path_compute `invocation`) as queries for
+    gsnapdp_stage3_compute (passes 2A-6): each query is the invocation's first
+    build_pairs_singles call (pass 2A: its path, query and arguments) with the
+    final build_pairs_introns call's arguments and counters (pass 6).  Returns
+    (queries, paths_in, query, query_uc, the lists pass 6 returned concatenated,
+    the pass-6 calls, the pass counts per query before pass 6), `copies` times
+    over; invocations without a final pass in the recording are left out."""
+    from .records import S3_DUALBREAKS, S3_DUALINTRONS, S3_INTRONS, S3_SINGLES
+    calls, pin, q, qu, want = stage3_calls(z)
+    inv = calls["invocation"]
+    order = np.argsort(inv, kind="stable")
+    Q, P, W, F, counts = [], [], [], [], []
+    at = 0
+    for v in np.unique(inv):
+        idx = order[inv[order] == v]
+        cs = calls[idx]
+        fin = np.nonzero((cs["pass"] == S3_INTRONS) & (cs["finalp"] == 1))[0]
+        sg = np.nonzero(cs["pass"] == S3_SINGLES)[0]
+        if fin.size != 1 or sg.size == 0 or sg[0] > fin[0]:
+            continue
+        first, last = cs[sg[0]], cs[fin[0]]
+        before = cs[:fin[0] + 1]
+        maj = before[np.isin(before["pass"], (S3_DUALINTRONS, S3_INTRONS))]
+        k = last.copy()
+        k["first_pair"], k["npairs"] = first["first_pair"], first["npairs"]
+        k["qpos"], k["querylength"] = first["qpos"], first["querylength"]
+        k["in_minor"], k["in_major"] = first["in_minor"], maj[0]["in_major"]
+        ins = before[before["pass"] == S3_INTRONS][0]
+        for f in ("in_nintrons", "in_nnonintrons", "in_intronlen", "in_nonintronlen"):
+            k[f] = ins[f]
+        k["finalp"] = 1
+        Q.append(k)
+        F.append(last)
+        W.append(want[int(last["first_out"]):int(last["first_out"]) + int(last["nout"])])
+        counts.append(np.bincount(before["pass"], minlength=6))
+        at += 1
+    queries = np.array(Q, dtype=calls.dtype)
+    final = np.array(F, dtype=calls.dtype)
+    wl = np.concatenate(W) if W else np.zeros(0, dtype=want.dtype)
+    final["first_out"] = np.concatenate([[0], np.cumsum(final["nout"])[:-1]]).astype(np.int32)
+    counts = np.array(counts)
+    if copies > 1:
+        n = len(queries)
+        kk = np.repeat(np.arange(copies), n)
+        queries = np.tile(queries, copies)
+        queries["first_pair"] += (kk * pin.size).astype(np.int32)
+        queries["qpos"] += (kk * q.size).astype(np.int32)
+        final = np.tile(final, copies)
+        final["first_out"] += (kk * wl.size).astype(np.int32)
+        pin, q, qu, wl = np.tile(pin, copies), np.tile(q, copies), np.tile(qu, copies), np.tile(wl, copies)
+        counts = np.tile(counts, (copies, 1))
+    return queries, pin, q, qu, wl, final, counts
+
+
 def stage3_calls(z, copies: int = 1):
     """Unpack a recorded stage-3 pass (tests/golden/gmap_*_stage3.npz,
     oracle/gen_golden.py stage3_golden) into the inputs of

@@ -695,6 +695,38 @@ typedef struct gsnapdp_s3_stage2 {
 } gsnapdp_s3_stage2;
 int gsnapdp_stage3_set_stage2(gsnapdp_ctx *ctx, const gsnapdp_s3_stage2 *stage2);
 
+/* Passes 2A to 6 of path_compute (stage3.c:8639-8876) for many queries:
+ * build_pairs_singles (2A), fix_adjacent_indels + build_pairs_singles (2B, 2C),
+ * the defect rate, Smooth_pairs_by_size + build_pairs_dualintrons +
+ * build_pairs_introns iterations (3a-3c), chop_ends_by_changepoint, the two HMM
+ * filters (4), remove_indel_gaps + build_dual_breaks (5) and the final
+ * build_pairs_introns (6, when finalp).  The host steps run on each query's
+ * list; every round of DP passes is ONE gsnapdp_stage3_pass over all the
+ * queries waiting on one, whichever pass each is at.
+ *
+ * A query is a gsnapdp_s3_call record: first_pair / npairs = the path pass 2A
+ * gets (as path_compute's pass 1 leaves it), finalp = do_final_p, the pass
+ * arguments as for gsnapdp_stage3_pass (pass and defect_rate are set by the
+ * pipeline), in_minor / in_major / in_* = the counters at pass 2A.  Written:
+ * first_out / nout (the list after pass 6, list order, src -1), the out_*
+ * counters, shiftp / incompletep of the last build_pairs_introns, defect_rate
+ * (pass 4's), ub (OR of the passes'), status (-1 when a pass or a host step
+ * would make the reference abort, or a stage-2 dual break has no callback).
+ * min_intronlength is gmap's (-j, default 9; remove_indel_gaps). */
+typedef struct gsnapdp_s3_compute_stats {
+  int32_t passes;         /* gsnapdp_stage3_pass calls */
+  int32_t rounds;         /* their rounds */
+  int32_t windows[4];     /* as gsnapdp_s3_stats */
+  int32_t pass_calls[6];  /* the pass calls, by GSNAPDP_S3_* */
+  int32_t failed;
+  int32_t pad;
+  double seconds[3];      /* wall time: host steps between the passes, the passes, the whole call */
+} gsnapdp_s3_compute_stats;
+int gsnapdp_stage3_compute(gsnapdp_ctx *ctx, gsnapdp_s3_call *queries, int nqueries,
+                           const gsnapdp_s3_pair *paths_in, int64_t npairs_in, const char *query,
+                           const char *query_uc, size_t query_bytes, const gsnapdp_iit *iit, int min_intronlength,
+                           gsnapdp_s3_pair *out, int64_t out_cap, gsnapdp_s3_compute_stats *stats);
+
 /* score_introns (stage3.c:7935-8162) on the lists a pass returned: for every
  * call with status 0, its list reversed into path order (as stage3_compute
  * reverses path_compute's pairs, :9890-9941), the introns picked on the host

@@ -10,7 +10,9 @@
 //                     present, DIR/intervals.bin (gsnapdp_iit_interval: a splicing IIT) and
 //                     DIR/stage2_{calls,pairs}.bin (traverse_dual_break's recorded stage-2 lists);
 //                     writes DIR/{pass_calls,pass_pairs,pass_stats}.bin, and with
-//                     --introns DIR/pass_scores.bin (score_introns on the returned lists)
+//                     --introns DIR/pass_scores.bin (score_introns on the returned lists);
+//   stage3_cpu DIR --compute MINLEN   passes 2A-6 (gsnapdp_stage3_compute) over the queries in
+//                     calls.bin: DIR/{pass_calls,pass_pairs,compute_stats}.bin
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -58,6 +60,8 @@ int main(int argc, char** argv) {
   if (argc < 2) return 2;
   const std::string d = argv[1];
   const bool introns = argc > 2 && std::string(argv[2]) == "--introns";
+  // --compute MINLEN: gsnapdp_stage3_compute with min_intronlength MINLEN
+  const int compute = argc > 3 && std::string(argv[2]) == "--compute" ? atoi(argv[3]) : -1;
   std::vector<gsnapdp_s3_call> calls = slurp<gsnapdp_s3_call>(d + "/calls.bin");
   std::vector<gsnapdp_s3_pair> in = slurp<gsnapdp_s3_pair>(d + "/pairs_in.bin");
   std::vector<char> q = slurp<char>(d + "/query.bin"), qu = slurp<char>(d + "/query_uc.bin");
@@ -83,6 +87,25 @@ int main(int argc, char** argv) {
     s2 = s2dbl_new(sc.data(), (int)(sc.size() / 48), sp.data(), (int)sp.size());
     gsnapdp_s3_stage2 cb = {s2, s2dbl_compute_one};
     gsnapdp_stage3_set_stage2(ctx, &cb);
+  }
+  if (compute >= 0) {  // passes 2A-6 (gsnapdp_stage3_compute): calls.bin holds the queries
+    gsnapdp_s3_compute_stats cs;
+    std::vector<gsnapdp_s3_pair> big((size_t)cap * 2 + 1024);
+    if (gsnapdp_stage3_compute(ctx, calls.data(), (int)calls.size(), in.data(), (int64_t)in.size(), q.data(),
+                               qu.data(), std::min(q.size(), qu.size()), iit, compute, big.data(),
+                               (int64_t)big.size(), &cs)) {
+      fprintf(stderr, "gsnapdp_stage3_compute: %s\n", g_err.c_str());
+      return 5;
+    }
+    fprintf(stderr, "compute %.4f s (host steps %.4f, passes %.4f), %d passes, %d rounds, %d failed\n",
+            cs.seconds[2], cs.seconds[0], cs.seconds[1], cs.passes, cs.rounds, cs.failed);
+    int64_t nout = 0;
+    for (const gsnapdp_s3_call& c : calls) nout += c.nout;
+    spit(d + "/pass_calls.bin", calls.data(), calls.size());
+    spit(d + "/pass_pairs.bin", big.data(), (size_t)nout);
+    spit(d + "/compute_stats.bin", &cs, 1);
+    gsnapdp_destroy(ctx);
+    return 0;
   }
   if (gsnapdp_stage3_pass(ctx, calls.data(), (int)calls.size(), in.data(), (int64_t)in.size(), q.data(),
                           qu.data(), std::min(q.size(), qu.size()), iit, out.data(), cap, &st)) {

@@ -15,7 +15,8 @@ import pytest
 
 from gsnapdp import Context, SplicingIIT
 from gsnapdp import workload as W
-from test_stage3_cpu import IIT_NAMES, NAMES, check_pass, check_scores, iit_intervals, stage3_golden
+from test_stage3_cpu import (IIT_NAMES, NAMES, PIPE_NAMES, check_compute, check_pass, check_scores, iit_intervals,
+                             stage3_golden)
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -73,6 +74,32 @@ def test_gpu_stage3_pass_with_splicing_iit(golden_dir, name):
     print("%s: %d calls, windows %s, %d disallowed cells" % (name, len(calls), st["windows"],
                                                             int(((got["flags"] & 4) != 0).sum())))
     iit.close()
+    ctx.close()
+
+
+@pytest.mark.parametrize("name", PIPE_NAMES)
+def test_gpu_stage3_compute_matches_reference(golden_dir, tmp_path, name):
+    """passes 2A-6 of path_compute for every recorded invocation at once
+    (gsnapdp_stage3_compute), the DP passes on the GPU: the lists pass 6
+    returned in gmap, bit for bit, and the same pass calls; then the
+    synthetic set x8 in one call, each copy checked, timed"""
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    queries, pin, q, qu, want, final, counts = W.stage3_pipeline(z)
+    ctx = Context(z["blocks"])
+    s2 = stage2_double(ctx, z, tmp_path)
+    got_calls, got, st = ctx.stage3_compute(queries, pin, q, qu)
+    check_compute(got_calls, got, final, want, name)
+    assert list(st["pass_calls"]) == list(counts.sum(axis=0))
+    if name == "gmap_synth_stage3":
+        copies = 8
+        Q, PI, QQ, QU, WANT, FINAL, _ = W.stage3_pipeline(z, copies)
+        t0 = time.perf_counter()
+        got_calls, got, st = ctx.stage3_compute(Q, PI, QQ, QU)
+        dt = time.perf_counter() - t0
+        check_compute(got_calls, got, FINAL, WANT, "x%d" % copies)
+        print("stage3 compute (passes 2A-6): %d queries in %.3f s = %.0f queries/s (%d passes, %d rounds, windows %s; "
+              "host steps %.3f s, passes %.3f s)" % (len(Q), dt, len(Q) / dt, st["passes"], st["rounds"],
+                                                    st["windows"], st["seconds"][0], st["seconds"][1]))
     ctx.close()
 
 

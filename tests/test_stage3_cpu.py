@@ -181,3 +181,62 @@ def test_stage3_pass_cpu_with_splicing_iit(golden_dir, tmp_path, name):
     check_pass(got_calls, got, calls, want, name)
     assert st["failed"] == 0 and st["undefined"] == 0
     check_scores(scores, got_calls, z["si_calls"], name)
+
+
+PIPE_NAMES = ["gmap_her2_stage3", "gmap_synth_stage3"]
+
+
+def check_compute(got_calls, got, final, want, what):
+    """gsnapdp_stage3_compute's lists and counters against the pass-6 calls gmap made"""
+    assert (got_calls["status"] == 0).all(), "%s: failed queries %s" % (what, np.nonzero(got_calls["status"])[0][:8])
+    ub = (got_calls["ub"] & 1) != 0
+    for f in COUNTERS:
+        bad = np.nonzero((got_calls[f] != final[f]) & ~(ub if f in UB_COUNTERS else False))[0]
+        assert bad.size == 0, "%s: %s differs at queries %s (got %s want %s)" % (
+            what, f, bad[:8], got_calls[f][bad[:8]], final[f][bad[:8]])
+    bad = np.nonzero(got_calls["defect_rate"].view(np.uint64) != final["defect_rate"].view(np.uint64))[0]
+    assert bad.size == 0, "%s: defect_rate differs at queries %s" % (what, bad[:8])
+    for i, (c, w) in enumerate(zip(got_calls, final)):
+        g = got[int(c["first_out"]):int(c["first_out"]) + int(c["nout"])].copy()
+        e = want[int(w["first_out"]):int(w["first_out"]) + int(w["nout"])].copy()
+        g["src"] = e["src"] = -1  # the pipeline's cells are its own
+        if g.tobytes() != e.tobytes():
+            k = int(np.nonzero(g != e)[0][0]) if len(g) == len(e) else min(len(g), len(e))
+            raise AssertionError("%s: query %d (invocation %d): %d cells, want %d; first difference at %d: "
+                                 "got %s want %s" % (what, i, int(c["invocation"]), len(g), len(e), k,
+                                                     g[k] if k < len(g) else None, e[k] if k < len(e) else None))
+
+
+@pytest.mark.parametrize("name", PIPE_NAMES)
+def test_stage3_compute_cpu_matches_reference(golden_dir, tmp_path, name):
+    """passes 2A-6 of path_compute (gsnapdp_stage3_compute: the host steps
+    restated, the DP passes batched across queries) from each recorded
+    invocation's pass-2A path to the list its pass 6 returned, bit for bit, with
+    the DP families served by the oracle and traverse_dual_break's stage 2 by
+    the recording"""
+    from gsnapdp.records import S3_CALL, S3_PAIR
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    queries, pin, q, qu, want, final, counts = W.stage3_pipeline(z)
+    assert len(queries) >= (2 if name == "gmap_her2_stage3" else 150)
+    d = str(tmp_path)
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "stage3_cpu"])
+    queries.tofile(os.path.join(d, "calls.bin"))
+    pin.tofile(os.path.join(d, "pairs_in.bin"))
+    q.tofile(os.path.join(d, "query.bin"))
+    qu.tofile(os.path.join(d, "query_uc.bin"))
+    z["blocks"].astype("<u4").tofile(os.path.join(d, "genome.u32"))
+    write_stage2(d, z)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               GSNAPDP_MAXENT_TABLES=os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin"))
+    p = subprocess.run([os.path.join(ROOT, "oracle", "_build", "stage3_cpu"), d, "--compute", "9"], env=env,
+                       capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, "stage3_cpu --compute failed (%d):\n%s" % (p.returncode, p.stderr[-6000:])
+    assert "runtime error" not in p.stderr, p.stderr[-6000:]
+    got_calls = np.fromfile(os.path.join(d, "pass_calls.bin"), dtype=S3_CALL)
+    got = np.fromfile(os.path.join(d, "pass_pairs.bin"), dtype=S3_PAIR)
+    check_compute(got_calls, got, final, want, name)
+    from gsnapdp.records import S3_COMPUTE_STATS
+    cs = np.fromfile(os.path.join(d, "compute_stats.bin"), dtype=S3_COMPUTE_STATS)[0]
+    # the same pass calls as gmap made up to pass 6: 2A / 2C singles, dual introns, introns, dual breaks
+    assert list(cs["pass_calls"]) == list(counts.sum(axis=0)), (cs["pass_calls"], counts.sum(axis=0))
