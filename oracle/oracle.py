@@ -241,6 +241,11 @@ def s3lib():
         L.gsnapdp_iit_from_intervals.restype = vp
         L.gsnapdp_iit_free.argtypes = [vp]
         L.gsnapdp_oracle_stash_reset.argtypes = []
+        L.gsnapdp_stage3_compute.argtypes = [vp, vp, i32, vp, i64, vp, vp, ctypes.c_size_t, vp, i32, vp, i64, vp]
+        L.gsnapdp_stage3_compute.restype = i32
+        L.gsnapdp_stage3_set_stage2.argtypes = [vp, vp]
+        L.s2dbl_new.argtypes = [vp, i32, vp, i32]
+        L.s2dbl_new.restype = vp
         L.s3cpu_last_error.restype = ctypes.c_char_p
         _s3lib = L
     return _s3lib
@@ -258,6 +263,34 @@ class Stage3Cpu:
         tables = np.fromfile(TABLES_PATH, dtype=np.float64)
         if not self.h or L.gsnapdp_load_maxent_tables(self.h, tables.ctypes.data, tables.size):
             raise RuntimeError("libstage3_cpu: context")
+
+    def set_stage2_recording(self, s2_calls, s2_pairs):
+        """traverse_dual_break's stage 2 served from a gmap_trace recording (tests/dropin/stage2_double.c)"""
+        L = s3lib()
+        self._s2 = (np.ascontiguousarray(s2_calls), np.ascontiguousarray(s2_pairs))
+        h = L.s2dbl_new(self._s2[0].ctypes.data, self._s2[0].size, self._s2[1].ctypes.data, self._s2[1].size)
+        self._s2cb = (ctypes.c_void_p * 2)(h, ctypes.cast(L.s2dbl_compute_one, ctypes.c_void_p).value)
+        L.gsnapdp_stage3_set_stage2(self.h, ctypes.addressof(self._s2cb))
+
+    def compute(self, queries, paths_in, query, query_uc, min_intronlength=9):
+        """gsnapdp_stage3_compute (passes 2A-6): (queries with out fields, lists, S3_COMPUTE_STATS)"""
+        from gsnapdp.records import S3_CALL, S3_COMPUTE_STATS, S3_PAIR
+        L = s3lib()
+        c = np.array(queries, dtype=S3_CALL, copy=True)
+        pi = np.ascontiguousarray(paths_in, dtype=S3_PAIR)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        cap = 2 * int((2 * (c["querylength"].astype(np.int64) + c["npairs"]) + 64).sum()) + 1024
+        out = np.empty(cap, dtype=S3_PAIR)
+        st = np.zeros(1, dtype=S3_COMPUTE_STATS)
+        try:
+            if L.gsnapdp_stage3_compute(self.h, c.ctypes.data, len(c), pi.ctypes.data, pi.size, q.ctypes.data,
+                                        qu.ctypes.data, min(q.size, qu.size), None, int(min_intronlength),
+                                        out.ctypes.data, cap, st.ctypes.data):
+                raise RuntimeError("libstage3_cpu compute: %s" % L.s3cpu_last_error().decode())
+        finally:
+            L.gsnapdp_oracle_stash_reset()
+        return c, out[:int(c["nout"].sum())], st[0]
 
     def run_compact(self, calls, pairs_in, query, query_uc):
         """gsnapdp_stage3_pass_compact: (calls, cells, new pairs, S3_STATS)"""
