@@ -1988,9 +1988,15 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
     c.incompletep = k.incompletep ? 1 : 0;
     c.ub = k.ub_bits;
   });
+  static const bool debug = getenv("GSNAPDP_S3_DEBUG") != nullptr;
   for (int i = 0; i < ncalls; i++) {
     P.st.undefined += paths[(size_t)i].undefined;
-    if (paths[(size_t)i].failed) P.st.failed++;
+    if (paths[(size_t)i].failed) {
+      P.st.failed++;
+      if (debug)
+        fprintf(stderr, "gsnapdp_stage3_pass: call %d (pass %d, tag %d) failed: %s\n", i, calls[i].pass,
+                calls[i].invocation, paths[(size_t)i].why.c_str());
+    }
   }
   store_release(store);
   const double total = std::chrono::duration<double>(clock::now() - t_start).count();

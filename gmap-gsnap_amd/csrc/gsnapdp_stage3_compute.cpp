@@ -786,6 +786,8 @@ extern "C" int gsnapdp_stage3_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries
     c.nout = q.failed ? 0 : (int32_t)q.list.size();
     if (q.failed) {
       st.failed++;
+      if (getenv("GSNAPDP_S3_DEBUG"))
+        fprintf(stderr, "gsnapdp_stage3_compute: query %d (tag %d) failed: %s\n", i, c.invocation, q.why.c_str());
       continue;
     }
     if (at + c.nout > out_cap) {

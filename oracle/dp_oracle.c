@@ -1970,7 +1970,13 @@ int orc_microexon_int(orc_list *out, orc_micro_out *o, int dynprogindex, const c
   int min_len, span, leftbound, rightbound, nmm, i, cL, cR;
   char intron1, intron2, intron3, intron4, gapchar;
   double pvalue, bestprob = 0.0;
-  static int hits[1 << 16];
+  /* the Boyer-Moore hit buffer: one per thread (the batch runs on many) */
+  static __thread int *hits;
+  enum { NHITS = 1 << 16 };
+  if (!hits && !(hits = (int *)malloc(sizeof(int) * NHITS))) {
+    o->unsupported = 1;
+    return 0;
+  }
   orc_list_clear(out);
   memset(o, 0, sizeof(*o));
   o->dynprogindex = dynprogindex;
@@ -2026,7 +2032,7 @@ int orc_microexon_int(orc_list *out, orc_micro_out *o, int dynprogindex, const c
           int middlelength = length1 - cL - cR;
           int textleft = offset2L + cL + MICROINTRON_LENGTH;
           int textright = revoffset2R - cR - MICROINTRON_LENGTH;
-          int nh = bm_hits(hits, (int)(sizeof(hits) / sizeof(hits[0])), &sequenceuc1[cL],
+          int nh = bm_hits(hits, NHITS, &sequenceuc1[cL],
                            middlelength, textleft, textright - textleft, &g), h;
           for (h = 0; h < nh; h++) {
             candidate = textleft + hits[h];
