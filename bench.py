@@ -337,6 +337,28 @@ def measure_micro(genome, n, steps, warmup, dev, with_cpu):
     return out
 
 
+_S2 = []  # the stage-2 doubles the contexts use (kept alive)
+
+
+def stage2_double(ctx, z):
+    """traverse_dual_break's stage 2 served from the golden's recording
+    (tests/dropin/stage2_double.c, built here with gcc) as ctx's stage-2 callback"""
+    import ctypes
+    import subprocess
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="gsnapdp_s2_")
+    so = os.path.join(tmp, "libstage2_double.so")
+    subprocess.check_call(["gcc", "-O2", "-shared", "-fPIC", "-o", so,
+                           os.path.join(ROOT, "tests", "dropin", "stage2_double.c")])
+    d = ctypes.CDLL(so)
+    d.s2dbl_new.restype = ctypes.c_void_p
+    d.s2dbl_new.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    sc, sp = np.ascontiguousarray(z["s2_calls"]), np.ascontiguousarray(z["s2_pairs"])
+    h = d.s2dbl_new(sc.ctypes.data, sc.size, sp.ctypes.data, sp.size)
+    _S2.append((d, sc, sp))
+    ctx.set_stage2(ctypes.cast(d.s2dbl_compute_one, ctypes.c_void_p).value, h)
+
+
 def measure_stage3(paths=7424, reps=3):
     """Side line: the stage-3 passes (gsnapdp_stage3_pass: path_compute's
     build_pairs_introns, build_pairs_singles, build_pairs_end5 / build_path_end3
@@ -352,6 +374,7 @@ def measure_stage3(paths=7424, reps=3):
     copies = max(1, paths // len(z["calls"]))
     calls, pin, q, qu, want = W.stage3_calls(z, copies)
     ctx = Context(z["blocks"])
+    stage2_double(ctx, z)  # build_dual_breaks' stage-2 dual breaks, from the recording
     ctx.stage3_pass(calls[:64], pin, q, qu)  # warm-up
     buf = np.empty(ctx.stage3_capacity(calls), dtype=want.dtype)
     best = None
@@ -369,7 +392,7 @@ def measure_stage3(paths=7424, reps=3):
     nwin = int(np.sum(st["windows"]))
     ref = float(z["calls"]["ref_seconds"].sum()) * copies
     ctx.close()
-    cpu = stage3_cpu_baseline(z["blocks"], calls, pin, q, qu, got)
+    cpu = stage3_cpu_baseline(z["blocks"], calls, pin, q, qu, got, z=z)
     return {"metric": "stage-3 passes (path_compute's DP passes), paths/s",
             "value": round(len(calls) / dt, 1), "unit": "paths/s", "paths": int(len(calls)),
             "paths_by_pass": {n: int((calls["pass"] == i).sum())
@@ -388,7 +411,7 @@ def measure_stage3(paths=7424, reps=3):
                         "development container (a different machine), DP included"}}
 
 
-def stage3_cpu_baseline(blocks, calls, pin, q, qu, want=None, compact=False):
+def stage3_cpu_baseline(blocks, calls, pin, q, qu, want=None, compact=False, z=None):
     """The same pass on this host's CPU: the pass's host code with every DP
     window served by the oracle/ restatement on the pass's 16 threads
     (oracle/_build/libstage3_cpu.so) -- best of two runs after a warm-up on a
@@ -396,6 +419,8 @@ def stage3_cpu_baseline(blocks, calls, pin, q, qu, want=None, compact=False):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # CPU baseline leg
     S = O.Stage3Cpu(blocks)
+    if z is not None and "s2_calls" in z:
+        S.set_stage2_recording(z["s2_calls"], z["s2_pairs"])
     S.run_compact(calls[:min(len(calls), 256)], pin, q, qu)
     best = None
     for _ in range(2):
@@ -413,6 +438,61 @@ def stage3_cpu_baseline(blocks, calls, pin, q, qu, want=None, compact=False):
     if want is not None and not compact:
         out["lists_equal_gpu"] = bool(res[1].tobytes() == want.tobytes())
     return out if not compact else (out, res)
+
+
+def measure_stage3_compute(copies=8, reps=3, cpu=True):
+    """Side line: passes 2A-6 of path_compute (gsnapdp_stage3_compute: the host
+    steps restated, every round of DP passes one gsnapdp_stage3_pass across the
+    queries) for every path_compute call the reference's gmap made on the
+    synthetic cDNAs (tests/golden/gmap_synth_stage3.npz, 168 calls) x `copies`,
+    each copy checked against the list the reference's pass 6 returned.
+    traverse_dual_break's stage 2 is served from the recording
+    (tests/dropin/stage2_double.c, built here).  The CPU leg runs the same host
+    code with every DP window served by the oracle/ restatement, 16 threads."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_stage3_cpu import check_compute  # list-by-list comparison with the recording
+    z = np.load(os.path.join(ROOT, "tests", "golden", "gmap_synth_stage3.npz"), allow_pickle=False)
+    Q, PI, QQ, QU, WANT, FINAL, counts = W.stage3_pipeline(z, copies)
+    out = {"metric": "stage-3 passes 2A-6 of path_compute, queries/s", "unit": "queries/s", "queries": int(len(Q))}
+    ctx = Context(z["blocks"])
+    stage2_double(ctx, z)
+    ctx.stage3_compute(Q[:8], PI, QQ, QU)  # warm-up
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        res = ctx.stage3_compute(Q, PI, QQ, QU)
+        dt = time.perf_counter() - t0
+        if best is None or dt < best[0]:
+            best = (dt, res)
+    dt, (c, got, st) = best
+    check_compute(c, got, FINAL, WANT, "stage3 compute")
+    ctx.close()
+    out.update({"value": round(len(Q) / dt, 1), "seconds": round(dt, 4), "bit_exact_vs_reference": True,
+                "passes": int(st["passes"]), "rounds": int(st["rounds"]),
+                "pass_calls": [int(x) for x in st["pass_calls"]], "windows": [int(x) for x in st["windows"]],
+                "host_steps_s": round(float(st["seconds"][0]), 4), "passes_s": round(float(st["seconds"][1]), 4)})
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # CPU baseline leg
+        S = O.Stage3Cpu(z["blocks"])
+        S.set_stage2_recording(z["s2_calls"], z["s2_pairs"])
+        S.compute(Q[:8], PI, QQ, QU)
+        best = None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            res = S.compute(Q, PI, QQ, QU)
+            dt = time.perf_counter() - t0
+            if best is None or dt < best[0]:
+                best = (dt, res)
+        dt, (c, got, st) = best
+        check_compute(c, got, FINAL, WANT, "stage3 compute, CPU")
+        S.close()
+        out["cpu_baseline"] = {"value": round(len(Q) / dt, 1), "unit": "queries/s", "seconds": round(dt, 4),
+                               "cores": int(os.environ.get("GSNAPDP_S3_THREADS", min(16, os.cpu_count() or 1))),
+                               "kind": "port",
+                               "sample": "the same %d queries, the host steps and passes with every DP window served "
+                                         "by the oracle/ restatement (oracle/_build/libstage3_cpu.so)" % len(Q)}
+    return out
 
 
 def measure_c4_transcripts(n=C4_TRANSCRIPTS, cpu=True, pinned=2000):
@@ -799,6 +879,7 @@ def main() -> None:
                 out["splicejunction"] = measure_sj(genome, 100_000, 20, args.warmup, dev, not args.no_cpu)
                 out["microexon"] = measure_micro(genome, 20_000, 20, args.warmup, dev, not args.no_cpu)
                 out["stage3_pass"] = measure_stage3()
+                out["stage3_compute"] = measure_stage3_compute(cpu=not args.no_cpu)
             if not args.no_c4t:
                 out["c4_transcripts"] = measure_c4_transcripts(args.c4_transcripts, not args.no_cpu)
         print(json.dumps(out), flush=True)

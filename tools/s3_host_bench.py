@@ -30,6 +30,9 @@ def main():
         q.tofile(os.path.join(d, "query.bin"))
         qu.tofile(os.path.join(d, "query_uc.bin"))
         z["blocks"].astype("<u4").tofile(os.path.join(d, "genome.u32"))
+        if "s2_calls" in z:  # build_dual_breaks' stage 2, from the recording
+            z["s2_calls"].tofile(os.path.join(d, "stage2_calls.bin"))
+            z["s2_pairs"].tofile(os.path.join(d, "stage2_pairs.bin"))
         env = dict(os.environ, GSNAPDP_S3_THREADS=threads,
                    GSNAPDP_MAXENT_TABLES=os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin"))
         p = subprocess.run([os.path.join(ROOT, "oracle", "_build", "stage3_cpu_fast"), d], env=env,

@@ -32,6 +32,9 @@ def main():
     os.environ["GSNAPDP_S3_RECORD"] = d  # read once, when the first pass runs
     from gsnapdp import Context
     ctx = Context(z["blocks"])
+    sys.path.insert(0, ROOT)
+    import bench
+    bench.stage2_double(ctx, z)  # build_dual_breaks' stage 2, from the recording
     c, got, st = ctx.stage3_pass(calls, pin, q, qu)
     assert got.tobytes() == want.tobytes()
     print("recorded %d paths, %d rounds into %s" % (len(calls), st["rounds"], d))
