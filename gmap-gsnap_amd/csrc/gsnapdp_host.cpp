@@ -683,3 +683,4 @@ extern "C" int gsnapdp_path_introns(const gsnapdp_path_pair* pairs, int npairs, 
   }
   return n;
 }
+

@@ -116,6 +116,8 @@ def lib():
                                              ctypes.c_int64, vp]
         L.gsnapdp_stage3_compute.restype = i32
         L.gsnapdp_stage3_set_stage2.argtypes = [vp, vp]
+        L.gsnapdp_scan_site_probs.argtypes = [vp, vp, i32, vp]
+        L.gsnapdp_scan_site_probs.restype = i32
         L.gsnapdp_stage3_set_stage2.restype = i32
         L.gsnapdp_stage3_score_introns.argtypes = [vp, vp, i32, vp, vp, vp]
         L.gsnapdp_stage3_score_introns.restype = i32
@@ -569,6 +571,17 @@ class Context:
         if rc != 0:
             raise GsnapdpError("gsnapdp_stage3_compute: %s" % lib().gsnapdp_last_error().decode())
         return c, out[:int(c["nout"].sum())], st[0]
+
+    def scan_site_probs(self, sites: np.ndarray) -> np.ndarray:
+        """GSNAP's splice-site scan candidates (SCAN_SITE records) in one batch
+        (gsnapdp_scan_site_probs): 1.0 for a known site, else the MaxEnt
+        probability at segment_left + splice_pos."""
+        from .records import SCAN_SITE
+        s = np.ascontiguousarray(sites, dtype=SCAN_SITE)
+        out = np.zeros(s.size, dtype=np.float64)
+        if lib().gsnapdp_scan_site_probs(self.h, _p(s) if s.size else None, s.size, _p(out)) != 0:
+            raise GsnapdpError("gsnapdp_scan_site_probs: %s" % lib().gsnapdp_last_error().decode())
+        return out
 
     def set_stage2(self, compute_one: int, user: int):
         """traverse_dual_break's stage-2 realignment (gsnapdp_stage3_set_stage2):

@@ -157,6 +157,10 @@ assert S2_CALL.itemsize == 48
 PC_CALL = np.dtype([(n, "<i4") for n in ("invocation do_final_p stage3debug cdna_direction querylength "
                                          "genomiclength watsonp pad").split()] + [("defect_rate", "<f8")])
 assert PC_CALL.itemsize == 40
+# GSNAP's splice-site scan candidates (include/gsnapdp.h gsnapdp_scan_site)
+SCAN_SITE = np.dtype([("segment_left", "<u4"), ("splice_pos", "<i4"), ("chroffset", "<u4"), ("knowni", "<i4"),
+                      ("model", "<i4")])
+assert SCAN_SITE.itemsize == 20
 S3_COMPUTE_STATS = np.dtype([("passes", "<i4"), ("rounds", "<i4"), ("windows", "<i4", 4), ("pass_calls", "<i4", 6),
                              ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3)])
 assert S3_COMPUTE_STATS.itemsize == 80

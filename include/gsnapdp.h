@@ -315,6 +315,21 @@ enum { GSNAPDP_DONOR = 0, GSNAPDP_ACCEPTOR = 1, GSNAPDP_ANTIDONOR = 2, GSNAPDP_A
 int gsnapdp_maxent_host(gsnapdp_ctx *ctx, const uint8_t *model, const uint32_t *splice_pos,
                         const uint32_t *chroffset, double *out, int n);
 
+/* GSNAP's splice-site scans (stage1hr.c:6300-7046, 8703-8976): every candidate
+ * splice position of a read's segment pair asks Maxent_hr_* at
+ * segment_left + splice_pos (Genomicpos_T arithmetic) unless the site is known
+ * (knowni >= 0: probability 1.0, no model run).  Many reads' candidates in one
+ * call: the unknown sites go to one k_maxent launch.  The scans' threshold logic
+ * (the mismatch counts and sufficient_splice_prob_local) stays the caller's. */
+typedef struct gsnapdp_scan_site {
+  uint32_t segment_left;  /* segmenti_left / segmentj_left */
+  int32_t splice_pos;
+  uint32_t chroffset;
+  int32_t knowni;         /* donori_knowni[i] etc.: >= 0 for a known site */
+  int32_t model;          /* GSNAPDP_DONOR / _ACCEPTOR / _ANTIDONOR / _ANTIACCEPTOR */
+} gsnapdp_scan_site;
+int gsnapdp_scan_site_probs(gsnapdp_ctx *ctx, const gsnapdp_scan_site *sites, int n, double *probs);
+
 /* ------------------------------------------------------- score_introns
  * stage3.c:7935-8162 for many paths at once: each path's introns get their
  * donor / acceptor MaxEnt probabilities (1.0 for a site the splicing IIT
