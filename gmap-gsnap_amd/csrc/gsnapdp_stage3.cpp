@@ -87,24 +87,27 @@ struct RawPair {
 struct Arena {
   const gsnapdp_s3_pair* in = nullptr;
   int nin = 0;
-  std::vector<uint8_t> flags;          // the input pairs' flags
+  std::vector<uint8_t> dis;    // the input pairs the pass disallowed (allocated at the first one)
   std::vector<RawPair> extra;  // pair nin + i
-  std::vector<int> cp;                 // pair of cell nin + i
-  std::vector<int> cn;                 // next cell of every cell
+  std::vector<int> cp;         // pair of cell nin + i
+  std::vector<int> cn;         // next cell of every cell
   void init(const gsnapdp_s3_pair* pairs, int n) {
     in = pairs;
     nin = n;
-    flags.resize((size_t)n);
+    dis.clear();
     cn.resize((size_t)n);
-    for (int j = 0; j < n; j++) {
-      flags[(size_t)j] = pairs[j].flags;
-      cn[(size_t)j] = j + 1 < n ? j + 1 : -1;
-    }
+    int* c = cn.data();
+    for (int j = 0; j < n; j++) c[j] = j + 1;  // (vectorised)
+    if (n) c[n - 1] = -1;
     extra.clear();
     cp.clear();
     extra.reserve(256);
     cp.reserve(256);
     cn.reserve((size_t)n + 256);
+  }
+  // the flags of input pair p as the pass left them
+  uint8_t in_flags(int p) const {
+    return (uint8_t)(in[p].flags | (!dis.empty() && dis[(size_t)p] ? GSNAPDP_S3_DISALLOWED : 0));
   }
   int pairof(int cell) const { return cell < nin ? cell : cp[(size_t)(cell - nin)]; }
   int cell(int pair, int next) {
@@ -130,13 +133,16 @@ struct Arena {
   }
   int reverse(int list) { return transfer(-1, list); }  // List_reverse (the same cells)
   const gsnapdp_s3_pair& at(int pair) const { return pair < nin ? in[pair] : extra[(size_t)(pair - nin)].p; }
-  // a pair's flags without touching the pair record (the scan's hot loop)
-  uint8_t flag(int pair) const { return pair < nin ? flags[(size_t)pair] : extra[(size_t)(pair - nin)].p.flags; }
+  uint8_t flag(int pair) const { return pair < nin ? in_flags(pair) : extra[(size_t)(pair - nin)].p.flags; }
   const gsnapdp_s3_pair& first(int list) const { return at(pairof(list)); }
   void disallow(int list) {  // pair->disallowedp = true (stage3.c:5873-5880)
     const int p = pairof(list);
-    if (p < nin) flags[(size_t)p] |= GSNAPDP_S3_DISALLOWED;
-    else extra[(size_t)(p - nin)].p.flags |= GSNAPDP_S3_DISALLOWED;
+    if (p < nin) {
+      if (dis.empty()) dis.assign((size_t)nin, 0);
+      dis[(size_t)p] = 1;
+    } else {
+      extra[(size_t)(p - nin)].p.flags |= GSNAPDP_S3_DISALLOWED;
+    }
   }
   int rest(int list) const { return cn[(size_t)list]; }
   int push_pair(int list, const gsnapdp_s3_pair& x) {
@@ -151,8 +157,17 @@ struct Arena {
     if (p >= nin) return extra[(size_t)(p - nin)].p;
     gsnapdp_s3_pair x = in[p];
     x.src = p;
-    x.flags = flags[(size_t)p];
+    x.flags = in_flags(p);
     return x;
+  }
+  // the run of input cells from `cell` down: cell, cell - 1, ..., returned as
+  // its lowest cell (the scan's reversal of an untouched stretch of the path)
+  int run_end(int cell) const {
+    if (cell >= nin) return cell;
+    const int* c = cn.data();
+    int q = cell;
+    while (q > 0 && c[q] == q - 1) q--;
+    return q;
   }
 };
 bool gapp(const gsnapdp_s3_pair& p) { return (p.flags & GSNAPDP_S3_GAPP) != 0; }
@@ -1460,6 +1475,22 @@ void scan(Pass& P, Path& k) {
   const gsnapdp_s3_call& c = *k.c;
   const int minintronlen = c.finalp ? MININTRONLEN_FINAL : MININTRONLEN;
   while (!k.failed && k.stage == S_SCAN) {
+    // the non-gap input cells at the head of the path, each pushed onto pairs
+    // (Pairpool_pop + List_push_existing, the loop below) in one tight loop
+    if (k.path >= 0 && k.path < k.A.nin) {
+      int* cn = k.A.cn.data();
+      const gsnapdp_s3_pair* in = k.A.in;
+      const int nin = k.A.nin;
+      int x = k.path, head = k.pairs;
+      while (x >= 0 && x < nin && !(in[x].flags & GSNAPDP_S3_GAPP)) {
+        const int nx = cn[x];
+        cn[x] = head;
+        head = x;
+        x = nx;
+      }
+      k.path = x;
+      k.pairs = head;
+    }
     if (k.path < 0) {
       k.stage = S_DONE;
       return;
@@ -1939,7 +1970,16 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
     if (k.c->pass == GSNAPDP_S3_END3) k.pairs = k.path;  // build_path_end3 returns its path
     int n = 0, nn = 0;
     if (!k.failed)
-      for (int p = k.pairs; p >= 0; p = k.A.rest(p)) n++, nn += k.A.pairof(p) >= k.A.nin;
+      for (int p = k.pairs; p >= 0;) {
+        const int q = k.A.run_end(p);
+        if (q != p || p < k.A.nin) {
+          n += p - q + 1;  // input cells p .. q
+          p = k.A.rest(q);
+        } else {
+          n++, nn += k.A.pairof(p) >= k.A.nin;
+          p = k.A.rest(p);
+        }
+      }
     first[(size_t)i + 1] = n;
     nfirst[(size_t)i + 1] = nn;
   });
@@ -1964,18 +2004,45 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
     c.nout = (int32_t)(first[(size_t)i + 1] - first[(size_t)i]);
     if (k.failed) return;
     int64_t at = first[(size_t)i];
+    const Arena& A = k.A;
+    const bool dis = !A.dis.empty();
     if (out.pairs) {
-      for (int p = k.pairs; p >= 0; p = k.A.rest(p)) out.pairs[at++] = k.A.out(p);
+      for (int p = k.pairs; p >= 0;) {
+        if (p < A.nin) {  // a run of input cells p, p - 1, .., q: a reversed block copy
+          const int q = A.run_end(p);
+          gsnapdp_s3_pair* o = out.pairs + at;
+          for (int x = p; x >= q; x--, o++) {
+            *o = A.in[x];
+            o->src = x;
+            if (dis && A.dis[(size_t)x]) o->flags |= GSNAPDP_S3_DISALLOWED;
+          }
+          at += p - q + 1;
+          p = A.rest(q);
+        } else {
+          out.pairs[at++] = A.out(p);
+          p = A.rest(p);
+        }
+      }
     } else {
       int64_t nat = nfirst[(size_t)i];
-      for (int p = k.pairs; p >= 0; p = k.A.rest(p)) {
-        const int pr = k.A.pairof(p);
-        if (pr < k.A.nin) {
-          out.cells[at++] = pr | ((k.A.flags[(size_t)pr] & GSNAPDP_S3_DISALLOWED) ? GSNAPDP_S3_CELL_DISALLOWED : 0);
+      for (int p = k.pairs; p >= 0;) {
+        if (p < A.nin) {
+          const int q = A.run_end(p);
+          int32_t* o = out.cells + at;
+          for (int x = p; x >= q; x--, o++)
+            *o = x | ((dis && A.dis[(size_t)x]) ? GSNAPDP_S3_CELL_DISALLOWED : 0);
+          at += p - q + 1;
+          p = A.rest(q);
+          continue;
+        }
+        const int pr = A.pairof(p);
+        if (pr < A.nin) {
+          out.cells[at++] = pr | ((dis && A.dis[(size_t)pr]) ? GSNAPDP_S3_CELL_DISALLOWED : 0);
         } else {
-          out.news[nat] = k.A.extra[(size_t)(pr - k.A.nin)].p;
+          out.news[nat] = A.extra[(size_t)(pr - A.nin)].p;
           out.cells[at++] = (int32_t)(-1 - nat++);
         }
+        p = A.rest(p);
       }
     }
     c.out_minor = k.minor;
