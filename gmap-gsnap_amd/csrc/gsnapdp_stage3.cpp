@@ -209,6 +209,7 @@ enum Stage {
 };
 
 struct Path {
+  int idx = -1;  // the path's index in the pass (kept by reset)
   gsnapdp_s3_call* c = nullptr;
   const char* q = nullptr;   // queryseq_ptr
   const char* qu = nullptr;  // queryuc_ptr
@@ -276,7 +277,9 @@ void reset(Path& k) {
   Arena A = std::move(k.A);
   Req R = std::move(k.req);
   std::string why = std::move(k.why);
+  const int idx = k.idx;
   k = Path();
+  k.idx = idx;
   k.A = std::move(A);
   k.req = std::move(R);
   k.req.fam = F_NONE;
@@ -290,6 +293,9 @@ struct Pass {
   size_t nwords;
   const gsnapdp_iit* iit;  // Dynprog_setup's splicing IIT, or nullptr
   gsnapdp_s3_stats st;
+  const char* query = nullptr;
+  const char* query_uc = nullptr;
+  gsnapdp::S3Driver* driver = nullptr;  // driven passes: a path's next pass when one ends
 };
 
 // ---- genome characters (stage3.c get_genomic_nt, with no genomic segment)
@@ -1583,6 +1589,72 @@ void resume(Pass& P, Path& k) {
 }
 
 
+// a path at the start of its pass: call c over the list pairs[0 .. npairs)
+void start_path(Pass& P, Path& k, gsnapdp_s3_call* cp, const gsnapdp_s3_pair* pairs, int npairs) {
+  reset(k);
+  gsnapdp_s3_call& c = *cp;
+  k.c = cp;
+  k.q = P.query + c.qpos;
+  k.qu = P.query_uc + c.qpos;
+  k.minor = c.in_minor;
+  k.major = c.in_major;
+  k.nintrons = c.in_nintrons;
+  k.nnonintrons = c.in_nnonintrons;
+  k.intronlen = c.in_intronlen;
+  k.nonintronlen = c.in_nonintronlen;
+  k.A.init(pairs, npairs);  // path->first is pairs[0] (cell 0)
+  const int list = npairs > 0 ? 0 : -1;
+  if (c.use_genomicseg_p) {
+    fail(k, "use_genomicseg_p passes are not served (the genome is the context's)");
+  } else if (c.pass == GSNAPDP_S3_END5 || c.pass == GSNAPDP_S3_END3) {
+    if (c.splicesitesp && c.endalign == GSNAPDP_QUERYEND_GAP)
+      fail(k, "an end extension with splice sites (Dynprog_end5/3_known) is not served");
+    else if (c.pass == GSNAPDP_S3_END5) k.pairs = list, end_start(k);
+    else k.path = list, end_start(k);
+  } else {
+    k.path = list;
+    scan(P, k);
+  }
+}
+
+// a finished path's counters into its call record
+void write_call(const Path& k, gsnapdp_s3_call& c) {
+  c.status = k.failed ? -1 : 0;
+  c.out_minor = k.minor;
+  c.out_major = k.major;
+  c.out_nintrons = k.nintrons;
+  c.out_nnonintrons = k.nnonintrons;
+  c.out_intronlen = k.intronlen;
+  c.out_nonintronlen = k.nonintronlen;
+  c.shiftp = k.shiftp ? 1 : 0;
+  c.incompletep = k.incompletep ? 1 : 0;
+  c.ub = k.ub_bits;
+}
+
+// driven passes: when a path's pass ends, its list goes to the driver, which
+// names the path's next pass (started at once, in this round) or ends it
+void finish_path(Pass& P, Path& k) {
+  thread_local std::vector<gsnapdp_s3_pair> list;
+  while (k.stage == S_DONE || k.failed) {
+    list.clear();
+    if (!k.failed) {
+      if (k.c->pass == GSNAPDP_S3_END3) k.pairs = k.path;  // build_path_end3 returns its path
+      for (int p = k.pairs; p >= 0; p = k.A.rest(p)) list.push_back(k.A.out(p));
+    }
+    write_call(k, *k.c);
+    const gsnapdp_s3_pair* pairs = nullptr;
+    int n = 0;
+    gsnapdp_s3_call* next = P.driver->next(k.idx, k.c, list, &pairs, &n);
+    if (!next) {
+      k.stage = S_DONE;
+      k.failed = false;  // reported through the call; the path is out of the pass
+      k.c = nullptr;
+      return;
+    }
+    start_path(P, k, next, pairs, n);
+  }
+}
+
 // ---- host threads: one persistent pool per process.  A round's host work is
 // a few hundred microseconds, so the workers spin briefly for the next job
 // before they sleep, and nothing is spawned per round.
@@ -1819,6 +1891,7 @@ void unpack_resume(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
     R.fam = F_NONE;
     Tic tic(prof().resume_ns);
     resume(P, k);
+    if (P.driver && (k.stage == S_DONE || k.failed)) finish_path(P, k);
   });
   C.paths.swap(C.all);  // the candidates for the next round
 }
@@ -1856,10 +1929,10 @@ struct Out {
 
 int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp_s3_pair* pairs_in,
              int64_t npairs_in, const char* query, const char* query_uc, size_t query_bytes, const gsnapdp_iit* iit,
-             const Out& out, gsnapdp_s3_stats* stats) {
+             const Out& out, gsnapdp_s3_stats* stats, gsnapdp::S3Driver* driver = nullptr) {
   if (!ctx || ncalls < 0 || npairs_in < 0 ||
       (ncalls > 0 && (!calls || (npairs_in > 0 && !pairs_in) || !query || !query_uc ||
-                      !(out.pairs || (out.cells && out.news))))) {
+                      !(driver || out.pairs || (out.cells && out.news))))) {
     gsnapdp__set_err("gsnapdp_stage3_pass: bad arguments");
     return -1;
   }
@@ -1874,6 +1947,9 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
   P.blocks = gsnapdp__host_blocks(ctx);
   P.nwords = gsnapdp__host_nwords(ctx);
   P.iit = iit;
+  P.query = query;
+  P.query_uc = query_uc;
+  P.driver = driver;
   memset(&P.st, 0, sizeof(P.st));
   using clock = std::chrono::steady_clock;
   const auto t_start = clock::now();
@@ -1882,20 +1958,7 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
   PathStore* store = store_acquire();
   if (store->paths.size() < (size_t)ncalls) store->paths.resize((size_t)ncalls);
   Path* paths = store->paths.data();
-  for (int i = 0; i < ncalls; i++) {
-    Path& k = paths[(size_t)i];
-    gsnapdp_s3_call& c = calls[i];
-    reset(k);
-    k.c = &c;
-    k.q = query + c.qpos;
-    k.qu = query_uc + c.qpos;
-    k.minor = c.in_minor;
-    k.major = c.in_major;
-    k.nintrons = c.in_nintrons;
-    k.nnonintrons = c.in_nnonintrons;
-    k.intronlen = c.in_intronlen;
-    k.nonintronlen = c.in_nonintronlen;
-  }
+  for (int i = 0; i < ncalls; i++) paths[(size_t)i].idx = i;
   Prof& pf = prof();
   if (pf.on) {
     for (int f = 0; f < F_N; f++) pf.expand_ns[f] = 0;
@@ -1904,21 +1967,9 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
   }
   pool.run(ncalls, 16, [&](int i) {
     Path& k = paths[(size_t)i];
-    const gsnapdp_s3_call& c = *k.c;
-    // the input list: path->first is pairs_in[first_pair] (cell 0)
-    k.A.init(pairs_in + c.first_pair, c.npairs);
-    const int list = c.npairs > 0 ? 0 : -1;
-    if (c.use_genomicseg_p) {
-      fail(k, "use_genomicseg_p passes are not served (the genome is the context's)");
-    } else if (c.pass == GSNAPDP_S3_END5 || c.pass == GSNAPDP_S3_END3) {
-      if (c.splicesitesp && c.endalign == GSNAPDP_QUERYEND_GAP)
-        fail(k, "an end extension with splice sites (Dynprog_end5/3_known) is not served");
-      else if (c.pass == GSNAPDP_S3_END5) k.pairs = list, end_start(k);
-      else k.path = list, end_start(k);
-    } else {
-      k.path = list;
-      scan(P, k);
-    }
+    gsnapdp_s3_call& c = calls[i];
+    start_path(P, k, &c, pairs_in + c.first_pair, c.npairs);
+    if (driver && (k.stage == S_DONE || k.failed)) finish_path(P, k);
   });
   // two cohorts (alternate paths, so both get a similar mix) when there are
   // enough paths for each round to be worth a batch of its own
@@ -1961,6 +2012,14 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
     return -1;
   }
   gsnapdp::s3_exec_release(ctx, X);
+  if (driver) {  // the driver holds every path's lists and calls
+    store_release(store);
+    P.st.seconds[1] = wait_s;
+    P.st.seconds[2] = std::chrono::duration<double>(clock::now() - t_start).count();
+    P.st.seconds[0] = P.st.seconds[2] - wait_s;
+    if (stats) *stats = P.st;
+    return 0;
+  }
   const auto t_out = clock::now();
   // the returned lists, each path's at its running offset (lengths -- and
   // the new pairs among them -- by the workers, offsets, then the copies)
@@ -2045,15 +2104,7 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
         p = A.rest(p);
       }
     }
-    c.out_minor = k.minor;
-    c.out_major = k.major;
-    c.out_nintrons = k.nintrons;
-    c.out_nnonintrons = k.nnonintrons;
-    c.out_intronlen = k.intronlen;
-    c.out_nonintronlen = k.nonintronlen;
-    c.shiftp = k.shiftp ? 1 : 0;
-    c.incompletep = k.incompletep ? 1 : 0;
-    c.ub = k.ub_bits;
+    write_call(k, c);
   });
   static const bool debug = getenv("GSNAPDP_S3_DEBUG") != nullptr;
   for (int i = 0; i < ncalls; i++) {
@@ -2174,4 +2225,10 @@ extern "C" int gsnapdp_stage3_score_introns(gsnapdp_ctx* ctx, const gsnapdp_s3_c
   for (int i = 0; i < ncalls; i++)
     if (calls[i].status != 0) memset(&scores[i], 0, sizeof(scores[i]));
   return 0;
+}
+
+int gsnapdp::s3_run_driven(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp_s3_pair* pairs_in,
+                           int64_t npairs_in, const char* query, const char* query_uc, size_t query_bytes,
+                           const gsnapdp_iit* iit, S3Driver* driver, gsnapdp_s3_stats* stats) {
+  return run_pass(ctx, calls, ncalls, pairs_in, npairs_in, query, query_uc, query_bytes, iit, Out(), stats, driver);
 }

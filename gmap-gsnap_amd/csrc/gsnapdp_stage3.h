@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include <functional>
+#include <vector>
 
 #include "../../include/gsnapdp.h"
 
@@ -59,6 +60,25 @@ void s3_parallel_for(int n, int grain, const std::function<void(int)>& fn);
 // handed back with s3_exec_release.
 S3Exec* s3_exec_acquire(gsnapdp_ctx* ctx);
 void s3_exec_release(gsnapdp_ctx* ctx, S3Exec* e);
+
+// Driven passes (gsnapdp_stage3_compute): when path i's pass ends, next() gets
+// its call (out fields written, status -1 for a failed path) and its list (list
+// order, full records), and returns the path's next pass -- its call, and its
+// list in *pairs / *n, which must stay valid until that pass ends -- or nullptr
+// when the path is finished.  The next pass starts in the same round, so paths
+// at different passes share every round's batches.  Called on the pass's host
+// threads, each path from one thread at a time.
+class S3Driver {
+ public:
+  virtual ~S3Driver() {}
+  virtual gsnapdp_s3_call* next(int i, gsnapdp_s3_call* ended, std::vector<gsnapdp_s3_pair>& list,
+                                const gsnapdp_s3_pair** pairs, int* n) = 0;
+};
+// the pass over the calls' first passes, every path continued by the driver;
+// no lists are written (the driver has them)
+int s3_run_driven(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp_s3_pair* pairs_in,
+                  int64_t npairs_in, const char* query, const char* query_uc, size_t query_bytes,
+                  const gsnapdp_iit* iit, S3Driver* driver, gsnapdp_s3_stats* stats);
 
 // the context's stage-2 callback for traverse_dual_break (gsnapdp_stage3_set_stage2)
 gsnapdp_s3_stage2 s3_stage2(gsnapdp_ctx* ctx);

@@ -575,6 +575,7 @@ struct Query {
   int minor = 0, major = 0, nintrons = 0, nnonintrons = 0, intronlen = 0, nonintronlen = 0;
   int ub = 0;
   int passes[6] = {0, 0, 0, 0, 0, 0};
+  gsnapdp_s3_call k;  // the pending pass's call (its pairs are list)
 };
 void fail(Query& q, const std::string& why) {
   if (!q.failed) q.why = why;
@@ -673,6 +674,65 @@ int pass_of(int step) {
   }
 }
 
+// the pipeline as the pass's driver: a query's next pass starts as soon as its
+// last one has ended, in the same round, so queries at different passes share
+// every round's batches
+class Pipeline final : public gsnapdp::S3Driver {
+ public:
+  Pipeline(std::vector<Query>& qs, int min_intronlength) : qs_(qs), min_intronlength_(min_intronlength) {}
+  // the query's next pass call (q.list is its input), or nullptr when it is done
+  gsnapdp_s3_call* call_for(Query& q) {
+    if (q.failed || q.step == Q_DONE) return nullptr;
+    gsnapdp_s3_call& k = q.k;
+    k = *q.c;
+    k.pass = pass_of(q.step);
+    k.first_pair = 0;
+    k.npairs = (int32_t)q.list.size();
+    k.finalp = q.step == Q_6 ? 1 : 0;
+    // 2A / 2C run with defect_rate 0.0 (:8676, :8705); the rest with the running rate
+    k.defect_rate = (q.step == Q_2A || q.step == Q_2C) ? 0.0 : q.defect;
+    k.in_minor = q.minor;
+    k.in_major = q.major;
+    k.in_nintrons = q.nintrons;
+    k.in_nnonintrons = q.nnonintrons;
+    k.in_intronlen = q.intronlen;
+    k.in_nonintronlen = q.nonintronlen;
+    q.passes[k.pass]++;
+    return &k;
+  }
+  gsnapdp_s3_call* next(int i, gsnapdp_s3_call* k, std::vector<gsnapdp_s3_pair>& list,
+                        const gsnapdp_s3_pair** pairs, int* n) override {
+    Query& q = qs_[(size_t)i];
+    if (k->status) {
+      fail(q, "a DP pass failed on the path (status -1)");
+      return nullptr;
+    }
+    q.list.assign(list.begin(), list.end());
+    q.minor = k->out_minor;
+    q.major = k->out_major;
+    q.ub |= k->ub;
+    if (k->pass == GSNAPDP_S3_INTRONS) {
+      q.nintrons = k->out_nintrons;
+      q.nnonintrons = k->out_nnonintrons;
+      q.intronlen = k->out_intronlen;
+      q.nonintronlen = k->out_nonintronlen;
+      q.shiftp = k->shiftp != 0;
+      q.incompletep = k->incompletep != 0;
+    }
+    advance(q, min_intronlength_);
+    gsnapdp_s3_call* c = call_for(q);
+    if (c) {
+      *pairs = q.list.data();
+      *n = (int)q.list.size();
+    }
+    return c;
+  }
+
+ private:
+  std::vector<Query>& qs_;
+  int min_intronlength_;
+};
+
 }  // namespace
 
 extern "C" int gsnapdp_stage3_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries,
@@ -689,6 +749,8 @@ extern "C" int gsnapdp_stage3_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries
   gsnapdp_s3_compute_stats st;
   memset(&st, 0, sizeof(st));
   std::vector<Query> qs((size_t)nqueries);
+  std::vector<gsnapdp_s3_call> first((size_t)nqueries);
+  Pipeline pipe(qs, min_intronlength);
   for (int i = 0; i < nqueries; i++) {
     gsnapdp_s3_call& c = queries[i];
     if (c.first_pair < 0 || c.npairs < 0 || (int64_t)c.first_pair + c.npairs > npairs_in || c.qpos < 0 ||
@@ -705,81 +767,26 @@ extern "C" int gsnapdp_stage3_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries
     q.nnonintrons = c.in_nnonintrons;
     q.intronlen = c.in_intronlen;
     q.nonintronlen = c.in_nonintronlen;
+    first[(size_t)i] = *pipe.call_for(q);  // pass 2A; its list is paths_in[first_pair ..]
+    first[(size_t)i].first_pair = c.first_pair;
   }
-  std::vector<gsnapdp_s3_call> calls;
-  std::vector<int> owner;
-  std::vector<gsnapdp_s3_pair> pin, pout;
-  double pass_s = 0.0;
-  for (;;) {
-    // every query waiting on a DP pass, in one gsnapdp_stage3_pass
-    calls.clear();
-    owner.clear();
-    pin.clear();
-    for (int i = 0; i < nqueries; i++) {
-      Query& q = qs[(size_t)i];
-      if (q.failed || q.step == Q_DONE) continue;
-      gsnapdp_s3_call k = *q.c;
-      k.pass = pass_of(q.step);
-      k.first_pair = (int32_t)pin.size();
-      k.npairs = (int32_t)q.list.size();
-      k.finalp = q.step == Q_6 ? 1 : 0;
-      // 2A / 2C run with defect_rate 0.0 (:8676, :8705); the rest with the running rate
-      k.defect_rate = (q.step == Q_2A || q.step == Q_2C) ? 0.0 : q.defect;
-      k.in_minor = q.minor;
-      k.in_major = q.major;
-      k.in_nintrons = q.nintrons;
-      k.in_nnonintrons = q.nnonintrons;
-      k.in_intronlen = q.intronlen;
-      k.in_nonintronlen = q.nonintronlen;
-      pin.insert(pin.end(), q.list.begin(), q.list.end());
-      calls.push_back(k);
-      owner.push_back(i);
-      q.passes[k.pass]++;
-      st.pass_calls[k.pass]++;
-    }
-    if (calls.empty()) break;
-    if (const char* dump = getenv("GSNAPDP_S3_COMPUTE_DUMP")) {  // debugging: every pass's calls and paths
-      char path[4096];
-      snprintf(path, sizeof(path), "%s/pass_%03d_calls.bin", dump, st.passes);
-      if (FILE* f = fopen(path, "wb")) fwrite(calls.data(), sizeof(calls[0]), calls.size(), f), fclose(f);
-      snprintf(path, sizeof(path), "%s/pass_%03d_pairs.bin", dump, st.passes);
-      if (FILE* f = fopen(path, "wb")) fwrite(pin.data(), sizeof(pin[0]), pin.size(), f), fclose(f);
-    }
-    int64_t cap = 0;
-    for (const gsnapdp_s3_call& k : calls) cap += 2 * ((int64_t)k.querylength + k.npairs) + 64;
-    pout.resize((size_t)cap);
-    gsnapdp_s3_stats ps;
-    const auto tp = clock::now();
-    if (gsnapdp_stage3_pass(ctx, calls.data(), (int)calls.size(), pin.data(), (int64_t)pin.size(), query, query_uc,
-                            query_bytes, iit, pout.data(), cap, &ps))
-      return -1;
-    pass_s += std::chrono::duration<double>(clock::now() - tp).count();
-    st.passes++;
-    st.rounds += ps.rounds;
-    for (int f = 0; f < 4; f++) st.windows[f] += ps.windows[f];
-    gsnapdp::s3_parallel_for((int)calls.size(), 8, [&](int j) {
-      const gsnapdp_s3_call& k = calls[(size_t)j];
-      Query& q = qs[(size_t)owner[(size_t)j]];
-      if (k.status) return fail(q, "a DP pass failed on the path (status -1)");
-      q.list.assign(pout.begin() + k.first_out, pout.begin() + k.first_out + k.nout);
-      q.minor = k.out_minor;
-      q.major = k.out_major;
-      q.ub |= k.ub;
-      if (k.pass == GSNAPDP_S3_INTRONS) {
-        q.nintrons = k.out_nintrons;
-        q.nnonintrons = k.out_nnonintrons;
-        q.intronlen = k.out_intronlen;
-        q.nonintronlen = k.out_nonintronlen;
-        q.shiftp = k.shiftp != 0;
-        q.incompletep = k.incompletep != 0;
-      }
-      advance(q, min_intronlength);
-    });
+  if (getenv("GSNAPDP_S3_COMPUTE_DUMP")) {  // debugging: the first pass's calls
+    char path[4096];
+    snprintf(path, sizeof(path), "%s/pass_000_calls.bin", getenv("GSNAPDP_S3_COMPUTE_DUMP"));
+    if (FILE* f = fopen(path, "wb")) fwrite(first.data(), sizeof(first[0]), first.size(), f), fclose(f);
   }
+  gsnapdp_s3_stats ps;
+  if (gsnapdp::s3_run_driven(ctx, first.data(), nqueries, paths_in, npairs_in, query, query_uc, query_bytes, iit,
+                             &pipe, &ps))
+    return -1;
+  st.passes = 1;
+  st.rounds = ps.rounds;
+  for (int f = 0; f < 4; f++) st.windows[f] = ps.windows[f];
   // the lists after pass 6, in the caller's buffer
   int64_t at = 0;
   for (int i = 0; i < nqueries; i++) {
     Query& q = qs[(size_t)i];
+    for (int p = 0; p < 6; p++) st.pass_calls[p] += q.passes[p];
     gsnapdp_s3_call& c = *q.c;
     c.status = q.failed ? -1 : 0;
     c.first_out = (int32_t)at;
@@ -811,9 +818,9 @@ extern "C" int gsnapdp_stage3_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries
     c.defect_rate = q.defect;
     c.ub = q.ub;
   }
-  st.seconds[0] = std::chrono::duration<double>(clock::now() - t0).count() - pass_s;
-  st.seconds[1] = pass_s;
+  st.seconds[1] = ps.seconds[1];  // the time the host waited for the GPU
   st.seconds[2] = std::chrono::duration<double>(clock::now() - t0).count();
+  st.seconds[0] = st.seconds[2] - st.seconds[1];
   if (stats) *stats = st;
   return 0;
 }
