@@ -366,4 +366,92 @@ __device__ inline double maxent_prob(int m, uint32_t sp, uint32_t co,
 }
 
 
+// maxent_prob for N sites of one model at once, for latency: every site's
+// genome words are loaded before any table index is formed, and every table
+// load before the products (the same operations in the same order per site,
+// so the values are bit-identical).  ok[i] false: out[i] = 0.0.
+__device__ inline uint32_t kmer_sel(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int bit) {
+  const int i = bit >> 5;  // kmer_at without a register array (no indexed private access)
+  const uint32_t lo = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
+  const uint32_t hi = i == 0 ? w1 : i == 1 ? w2 : i == 2 ? w3 : 0u;
+  return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)(bit & 31));
+}
+template <int N>
+__device__ inline void maxent_probs(int m, const uint32_t (&sp)[N], const bool (&ok)[N], uint32_t co,
+                                    const uint32_t* __restrict__ blocks, uint64_t nwords,
+                                    const double* __restrict__ T, double (&out)[N]) {
+  const uint32_t margin = (m == 0) ? 3u : (m == 1) ? 20u : (m == 2) ? 6u : 3u;
+  uint32_t w0[N], w1[N], w2[N], w3[N];
+  int b0[N];
+  bool v[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const uint32_t start = sp[i] - margin;
+    const uint64_t ptr = (uint64_t)(start >> 5) * 3u;
+    v[i] = ok[i] && sp[i] >= co + margin && ptr + 4 < nwords;
+    const uint64_t p = v[i] ? ptr : 0;
+    w1[i] = blocks[p];  // high
+    w0[i] = blocks[p + 1];  // low
+    w3[i] = blocks[p + 3];  // nexthigh
+    w2[i] = blocks[p + 4];  // nextlow
+    b0[i] = 2 * (int)(start & 31u);
+  }
+  auto seq = [&](int i, int off) { return kmer_sel(w0[i], w1[i], w2[i], w3[i], b0[i] + 2 * off); };
+  const double* donor_p = T;
+  const double* donor_di_p = donor_p + 16384;
+  const double* acc1_p = donor_di_p + 16;
+  const double* acc2_p = acc1_p + 16384;
+  const double* acc3_p = acc2_p + 16384;
+  const double* accdi_p = acc3_p + 16384;
+  const double* acc467_p = accdi_p + 16;
+  const double* acc589_p = acc467_p + 16384;
+  const double* donor_m = acc589_p + 16384;
+  const double* donor_di_m = donor_m + 16384;
+  const double* acc1_m = donor_di_m + 16;
+  const double* acc2_m = acc1_m + 16384;
+  const double* acc3_m = acc2_m + 16384;
+  const double* accdi_m = acc3_m + 16384;
+  const double* acc467_m = accdi_m + 16;
+  const double* acc589_m = acc467_m + 16384;
+  double odds[N];
+  if (m == 0 || m == 2) {
+    double a[N], b[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const uint32_t s = seq(i, 0);
+      a[i] = m == 0 ? donor_p[(s & 0x3Fu) | ((s >> 4) & 0x3FC0u)] : donor_m[(s & 0xFFu) | ((s >> 4) & 0x3F00u)];
+      b[i] = m == 0 ? donor_di_p[(s >> 6) & 0xFu] : donor_di_m[(s >> 8) & 0xFu];
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) odds[i] = a[i] * b[i];
+  } else {
+    double a[N], b[N], c[N], d[N], e[N], f[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      if (m == 1) {
+        const uint32_t s = seq(i, 14);
+        a[i] = acc1_p[seq(i, 0) & 0x3FFFu];
+        b[i] = acc2_p[seq(i, 7) & 0x3FFFu];
+        c[i] = acc3_p[(s & 0xFFu) | ((s >> 4) & 0x3F00u)];
+        d[i] = accdi_p[(s >> 8) & 0xFu];
+        e[i] = acc467_p[seq(i, 4) & 0x3FFFu];
+        f[i] = acc589_p[seq(i, 11) & 0x3FFFu];
+      } else {
+        const uint32_t s = seq(i, 0);
+        a[i] = acc1_m[seq(i, 16) & 0x3FFFu];
+        b[i] = acc2_m[seq(i, 9) & 0x3FFFu];
+        c[i] = acc3_m[(s & 0x3Fu) | ((s >> 4) & 0x3FC0u)];
+        d[i] = accdi_m[(s >> 6) & 0xFu];
+        e[i] = acc467_m[seq(i, 12) & 0x3FFFu];
+        f[i] = acc589_m[seq(i, 5) & 0x3FFFu];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++)
+      odds[i] = __dmul_rn(__dmul_rn(__dmul_rn(__dmul_rn(__dmul_rn(a[i], b[i]), c[i]), d[i]), e[i]), f[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) out[i] = v[i] ? __ddiv_rn(odds[i], __dadd_rn(1.0, odds[i])) : 0.0;
+}
+
 }  // namespace gsnapdp

@@ -56,6 +56,7 @@ static_assert(FV_BIAS + 2 * PAIRED_OPEN > FV_NEG + 9u * (GB_L2MAX + 48) + 20 + 4
               "reachable and NEG-like values stay apart with the paired open");
 constexpr int GB_KEY_NONE = -(1 << 30);
 constexpr int GB_PB = 8;  // rows per lane per batch of the combine
+constexpr int GB_SD = 4;  // steps of look-ahead of the probability-mode bridge sweep
 constexpr int GB_COLKEY = 1023;  // column part of a key: 1023 - c (c <= GB_L2MAX)
 
 // per-wave scratch (dwords): the two flanks' direction words and match bytes,
@@ -70,7 +71,19 @@ constexpr int GB_OCI = 2 * GB_FLANK;
 constexpr int GB_ORI = GB_OCI + 2 * GB_NGMAX * GB_CW;
 constexpr int GB_ORB = GB_ORI + 2 * GB_NGMAX * GB_RW;
 constexpr int GB_ODG = GB_ORB + 2 * GB_NGMAX * GB_RW;
-static_assert(GB_ODG + 2 * GB_NGMAX * GB_RW == GB_WAVE_DW, "k_gband scratch layout");
+// probability mode: each flank's cell values H - pen (16 bits, the fill's
+// offset form), 8 per lane and column in the fill's lane order, then the site
+// probabilities of each window's columns (doubles)
+constexpr int GB_OCV = GB_ODG + 2 * GB_NGMAX * GB_RW;
+constexpr int GB_CVF = GB_COLS * 256;
+constexpr int GB_OPR = GB_OCV + 2 * GB_CVF;
+// probability mode's row records, per window and flank row r: {threshold T(r),
+// intron word, the partner row's site probability (a double)} for the bridge
+// sweep, which overwrites each with the row's loop result {column, 0, sum}
+constexpr int GB_OREC = GB_OPR + 2 * GB_NGMAX * GB_COLS * 2;
+static_assert(GB_OREC + 2 * GB_NGMAX * GB_RW * 4 == GB_WAVE_DW && GB_OPR % 2 == 0 && GB_WAVE_DW % 4 == 0,
+              "k_gband scratch layout");
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 enum { FL_RIGHT = 0, FL_LEFT = 1 };
 #ifdef GB_CHECK
 // diagnostic builds: bounds checks that record the first bad access instead of faulting
@@ -203,7 +216,7 @@ __device__ inline T& at_b(T* base, uint32_t boff) {
   return *(T*)((char*)base + boff);
 }
 
-template <int S, int LPW, int JL, int FL>
+template <int S, int LPW, int JL, int FL, bool PM>
 __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, int open, int mtoff,
                                         int qbase, int qstep, AS_GLOBAL uint32_t* wpool1,
                                         const AS_GLOBAL char* q1, const AS_GLOBAL char* qu1,
@@ -222,6 +235,7 @@ __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, in
   uint32_t* ring = (uint32_t*)ring3;
   uint32_t* __restrict__ D = (uint32_t*)wpool + (uint32_t)(FL * GB_FLANK);
   uint8_t* __restrict__ M = (uint8_t*)(D + GB_COLS * 64);
+  u32x4* __restrict__ CV = (u32x4*)((uint32_t*)wpool + GB_OCV + FL * GB_CVF);
   // this group's tables and outputs: byte offsets from the wave's scratch
   const uint8_t* __restrict__ wb = (const uint8_t*)wpool;
   const uint32_t ci_b = 4u * (uint32_t)(GB_OCI + (FL * GB_NGMAX + g) * GB_CW);
@@ -276,7 +290,8 @@ __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, in
     E[s] = FV_NEG;
     F[s] = (r >= 1) ? FV_BIAS + open : FV_NEG;
     P[s] = row_word(r);
-    RI[s] = (r >= 1 && r <= L1) ? at_b(wpool, ri_b + 4u * (uint32_t)r) : 0u;
+    if constexpr (!PM) RI[s] = (r >= 1 && r <= L1) ? at_b(wpool, ri_b + 4u * (uint32_t)r) : 0u;
+    else RI[s] = 0u;
     A[s] = GB_KEY_NONE;
     MB = ((MB >> 1) & MB_KEEP) | row_spread(P[s]);
   }
@@ -296,7 +311,7 @@ __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, in
       const uint32_t qi = (uint32_t)(qbase + qstep * (rc - 1));
       qb[e] = q[qi];
       ub[e] = qu[qi];
-      iw[e] = at_b(wpool, ri_b + 4u * (uint32_t)((r >= 0 && r <= L1) ? r : 0));
+      if constexpr (!PM) iw[e] = at_b(wpool, ri_b + 4u * (uint32_t)((r >= 0 && r <= L1) ? r : 0));
     }
 #pragma unroll
     for (int e = 0; e < EC; e++) {
@@ -310,7 +325,7 @@ __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, in
       const uint32_t w = sprof[mtoff + (ok ? (qb[e] & 127u) : 0u)] | sprof[UTAB + (ok ? ub[e] : 255u)];
       if (e * LPW + j < NR) {
         rr[r & (RG::RR - 1)] = w;
-        rri[r & (RG::RR - 1)] = ok ? iw[e] : 0u;
+        if constexpr (!PM) rri[r & (RG::RR - 1)] = ok ? iw[e] : 0u;
       }
     }
 #pragma unroll
@@ -322,7 +337,7 @@ __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, in
   };
   stage(std::integral_constant<int, RG::K + RG::SPAN>(), 1 + rbase, 1);
   uint32_t pnext = rr[(1 + j * (S - 1) + rbase) & (RG::RR - 1)];
-  uint32_t inext = rri[(1 + j * (S - 1) + rbase) & (RG::RR - 1)];
+  uint32_t inext = PM ? 0u : rri[(1 + j * (S - 1) + rbase) & (RG::RR - 1)];
   uint32_t gnext = cr[(1 - j) & (RG::CR - 1)];
   const uint32_t lane_off = (uint32_t)((LPW - 1 - j) * 64 + j * NG + g);
   // column part of a key: ((c * ext + known * 20) << 10) + 1023 - c, with
@@ -351,6 +366,7 @@ __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, in
     }
     uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u, gsh = 0u, csh = 0u;
     int ck = GB_KEY_NONE;
+    uint32_t cv[S];  // probability mode: the cells' H - pen
     auto cell = [&](int s, FV Hr, FV Er, int Ar) {
       const FV Hd = H[s], Ed = E[s], Fd = F[s];
       const uint32_t pw = pslot(s);
@@ -367,12 +383,18 @@ __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, in
       ah = push_sign(ah, dh);
       af = push_sign(af, df);
       ae = push_sign(ae, de);
-      // this cell as a bridge candidate: H - pen + intron score (+ column terms in
-      // ck); pen = the nogap came from gap1 or gap2 (dynprog.c:3723)
-      const int npen = JL ? (int)((uint32_t)(dv & dh) >> 31) : ((dv | dh) >> 31);
-      const int sI = (int)__builtin_amdgcn_ubfe(islot(s), csh, 6);
-      const int key = (((int)hn + sI + npen) << 10) + ck;
-      A[s] = max(Ar, key);
+      if constexpr (PM) {
+        // H - pen for the bridge scan; pen = the nogap came from gap1 or gap2 (dynprog.c:3723)
+        const int npen = JL ? (int)((uint32_t)(dv & dh) >> 31) - 1 : ((dv | dh) >> 31);
+        cv[s] = (uint32_t)((int)hn + npen);
+      } else {
+        // this cell as a bridge candidate: H - pen + intron score (+ column terms in
+        // ck; a jump-late flank's -1 rides there)
+        const int npen = JL ? (int)((uint32_t)(dv & dh) >> 31) : ((dv | dh) >> 31);
+        const int sI = (int)__builtin_amdgcn_ubfe(islot(s), csh, 6);
+        const int key = (((int)hn + sI + npen) << 10) + ck;
+        A[s] = max(Ar, key);
+      }
       E[s] = fv_max(a, Er);
       const FV f = fv_max(b, fp);
       F[s] = f;
@@ -398,21 +420,23 @@ __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, in
       const uint32_t gc = gnext & 7u;
       gsh = 4u * gc;
       macc = (uint32_t)(MB >> (8u * gc));
-      csh = __builtin_amdgcn_ubfe(gnext, 3, 3) * 6u;
-      // column L2 is not a bridge column (:3704, :3753)
-      const int ckc = (int)((gnext & 64u) * 320u) + ck0 - __mul24(c, 3 * 1024 + 1);
-      ck = t < t_ck ? ckc : GB_KEY_NONE;
-      // the row leaving the band through lane 0's slot 0 (above the band for
-      // `stop` columns already) is complete: slot 1's row overwrites it now
-      const int r0 = t - xr;
-      if ((uint32_t)(r0 - 1) < nrx) at_b(wout, rb_b + 4u * GB_CHK(r0, GB_RW, 2)) = (uint32_t)A[0];
+      if constexpr (!PM) {
+        csh = __builtin_amdgcn_ubfe(gnext, 3, 3) * 6u;
+        // column L2 is not a bridge column (:3704, :3753)
+        const int ckc = (int)((gnext & 64u) * 320u) + ck0 - __mul24(c, 3 * 1024 + 1);
+        ck = t < t_ck ? ckc : GB_KEY_NONE;
+        // the row leaving the band through lane 0's slot 0 (above the band for
+        // `stop` columns already) is complete: slot 1's row overwrites it now
+        const int r0 = t - xr;
+        if ((uint32_t)(r0 - 1) < nrx) at_b(wout, rb_b + 4u * GB_CHK(r0, GB_RW, 2)) = (uint32_t)A[0];
+      }
       cell(0, H[1], E[1], A[1]);
     }
     FV hb = FV_NEG, eb = FV_NEG;
     int ab = GB_KEY_NONE;
     if (LPW > 1) {
       const FV h = (FV)from_lane_below((int)H[0]), e = (FV)from_lane_below((int)E[0]);
-      const int x = from_lane_below(A[0]);
+      const int x = PM ? GB_KEY_NONE : from_lane_below(A[0]);
       if (j != LPW - 1) {
         hb = h;
         eb = e;
@@ -427,6 +451,18 @@ __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, in
       const uint32_t o = GB_CHK((uint32_t)(t - (LPW - 1)) * 64u + lane_off, GB_COLS * 64, 1);
       at_b(D, 4u * o) = acc;
       at_b(M, o) = (uint8_t)macc;
+#ifdef GB_EXP_NOCV
+      if constexpr (false) {  // ablation: no cell values (wrong results, timing only)
+#else
+      if constexpr (PM) {
+#endif
+        static_assert(S <= 8, "8 cell values per lane and column");
+        uint32_t pk[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int s = 0; s < S; s++) pk[s >> 1] |= cv[s] << (16 * (s & 1));
+        u32x4 x = {pk[0], pk[1], pk[2], pk[3]};
+        at_b(CV, 16u * o) = x;
+      }
       // the diagonal cell H(c, c) of this column, for the other flank's bridge loop
       uint32_t dv = H[0];
 #pragma unroll
@@ -435,7 +471,7 @@ __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, in
     }
     if (MAYSTAGE && t % RG::K == 0) stage(std::integral_constant<int, RG::K>(), t + 1 + rbase + RG::SPAN, t + 1);
     pnext = rr[(t + 1 + j * (S - 1) + rbase) & (RG::RR - 1)];
-    inext = rri[(t + 1 + j * (S - 1) + rbase) & (RG::RR - 1)];
+    if constexpr (!PM) inext = rri[(t + 1 + j * (S - 1) + rbase) & (RG::RR - 1)];
     gnext = cr[(t + 1 - j) & (RG::CR - 1)];
   };
   using Masked = std::integral_constant<bool, true>;
@@ -450,13 +486,132 @@ __device__ __noinline__ void gband_fill(int L1, int L2, int lband, int rband, in
   for (; t <= minL2; t++) step(Full(), Shift(), t);
   for (; t < maxL2 + LPW; t++) step(Masked(), Shift(), t);
   // the rows still in the band at column L2
-  if (L1 > 0) {
+  if (!PM && L1 > 0) {
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const int r = L2 - rband + j * S + s - stop;
       if (r >= 1 && r < L1) at_b(wout, rb_b + 4u * GB_CHK(r, GB_RW, 4)) = (uint32_t)A[s];
     }
   }
+}
+
+
+// Probability mode's bridge loops over one flank (bridge_intron_gap
+// :3905-4041), after both fills: for every flank row r, the first column c of
+// its band (c ascending, the reference's order) with the largest
+// probC(c) + probOther(r) among the cells whose score reaches score_threshold,
+//   H(r, c) - pen + known(c) + intronscore + D_other(L1 - r) >= threshold,
+// i.e. v + c * ext + known(c) * 20 + sI(code(c), word(r)) >= T(r) on the fill's
+// 16-bit cell values v.  The sweep visits the columns in order with the fill's
+// lane layout: a lane reads back its own cell values of column c (one coalesced
+// 16-byte load per lane), slot s holds row row0 + s + c, and each row's best so
+// far moves down one slot per column and from lane j + 1 to lane j, like the
+// fill's gap values.  A row's result replaces its record when it leaves the
+// band (lane 0, slot 0) or at the end.
+template <int S, int LPW, int FL>
+__device__ __noinline__ void gband_sweep(int L1, int L2, int lband, int rband, AS_GLOBAL uint32_t* wpool1) {
+  constexpr int WMAX = S * LPW;
+  constexpr int NG = 64 / LPW;
+  const int lane = threadIdx.x & 63;
+  const int j = lane % LPW;
+  const int g = lane / LPW;
+  uint32_t* __restrict__ wpool = wave_uniform((uint32_t*)wpool1);
+  const u32x4* __restrict__ CV = (const u32x4*)(wpool + GB_OCV + FL * GB_CVF);
+  u32x4* __restrict__ rec = (u32x4*)(wpool + GB_OREC + 4 * (FL * GB_NGMAX + g) * GB_RW);
+  const double* __restrict__ prc = (const double*)(wpool + GB_OPR + 2 * (FL * GB_NGMAX + g) * GB_COLS);
+  const uint8_t* __restrict__ cib = (const uint8_t*)(wpool + GB_OCI + (FL * GB_NGMAX + g) * GB_CW);
+  const int stop = WMAX - (lband + rband + 1);
+  const int row0 = j * S - stop - rband;
+  const int cend = __builtin_amdgcn_readfirstlane(wave_max(L1 > 0 ? L2 : 0)) - 1;  // bridge columns 1 .. L2 - 1
+  int T[S], bc[S];
+  uint32_t Wd[S];
+  double pO[S], bs[S];
+  bool inb[S];
+  auto load_row = [&](int r, int& t, uint32_t& w, double& po) {
+    const bool ok = r >= 1 && r < L1;
+    const u32x4 x = rec[GB_CHK(ok ? r : 0, GB_RW, 22)];
+    t = ok ? (int)x.x : 0x7fffffff;
+    w = x.y;
+    po = __hiloint2double((int)x.w, (int)x.z);
+  };
+  auto put_row = [&](int r, int c, double sum) {
+    if (r >= 1 && r < L1) {
+      u32x4 x = {(uint32_t)c, 0u, (uint32_t)__double2loint(sum), (uint32_t)__double2hiint(sum)};
+      rec[GB_CHK(r, GB_RW, 23)] = x;
+    }
+  };
+  // the loads of step c (the lane's cell values of column c, the record of the
+  // row entering slot S - 1, the column's probability and byte), issued
+  // GB_SD steps ahead of their use
+  struct Pre {
+    u32x4 e, r;
+    double pc;
+    uint32_t cb;
+  };
+  auto issue = [&](int c, Pre& q) {
+    const int cl = c <= cend ? c : cend;
+    q.e = CV[GB_CHK(cl * 64 + j * NG + g, GB_COLS * 64, 24)];
+    const int r = row0 + S - 1 + c;
+    q.r = rec[GB_CHK(r >= 1 && r < L1 ? r : 0, GB_RW, 22)];
+    const int cc = c <= L2 - 1 ? c : 0;
+    q.pc = c <= L2 - 1 ? prc[cc] : -2.0;  // past the window's bridge columns: never a candidate
+    q.cb = cib[cc];
+  };
+  auto step = [&](int c, const Pre& q) {
+    if (c > 1) {
+      // the row in slot 0 moves to lane j - 1 (lane 0: it leaves the band, complete)
+      if (j == 0) put_row(row0 + c - 1, bc[0], bs[0]);
+      const int ilo = from_lane_below(__double2loint(bs[0])), ihi = from_lane_below(__double2hiint(bs[0]));
+      const int icc = from_lane_below(bc[0]);
+#pragma unroll
+      for (int s = 0; s < S - 1; s++) {
+        bs[s] = bs[s + 1];
+        bc[s] = bc[s + 1];
+        T[s] = T[s + 1];
+        Wd[s] = Wd[s + 1];
+        pO[s] = pO[s + 1];
+      }
+      const bool top = j == LPW - 1;
+      bs[S - 1] = top ? 0.0 : __hiloint2double(ihi, ilo);
+      bc[S - 1] = top ? -1 : icc;
+      const int r = row0 + S - 1 + c;
+      T[S - 1] = r >= 1 && r < L1 ? (int)q.r.x : 0x7fffffff;
+      Wd[S - 1] = q.r.y;
+      pO[S - 1] = __hiloint2double((int)q.r.w, (int)q.r.z);
+    }
+    const int colt = c * GB_EXT + (int)((q.cb >> 6) & 1u) * KNOWN_REWARD;
+    const uint32_t csh = ((q.cb >> 3) & 7u) * 6u;
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const uint32_t word = s < 2 ? q.e.x : s < 4 ? q.e.y : s < 6 ? q.e.z : q.e.w;
+      const int v = (int)((word >> (16 * (s & 1))) & 0xffffu);
+      const int sI = (int)__builtin_amdgcn_ubfe(Wd[s], csh, 6);
+      const double sum = q.pc + pO[s];
+      const bool take = inb[s] && v + colt + sI >= T[s] && sum > bs[s];
+      bs[s] = take ? sum : bs[s];
+      bc[s] = take ? c : bc[s];
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    inb[s] = j * S + s >= stop;
+    load_row(row0 + s + 1, T[s], Wd[s], pO[s]);
+    bs[s] = 0.0;  // bestprob starts at 0.0 (:3905): a row's sum must exceed it
+    bc[s] = -1;
+  }
+  Pre pq[GB_SD];
+#pragma unroll
+  for (int d = 0; d < GB_SD; d++) issue(1 + d, pq[d]);
+  for (int c = 1; c <= cend; c += GB_SD) {
+#pragma unroll
+    for (int d = 0; d < GB_SD; d++) {
+      if (c + d <= cend) step(c + d, pq[d]);
+      issue(c + d + GB_SD, pq[d]);
+    }
+  }
+  // the rows still in the band after the last column
+#pragma unroll
+  for (int s = 0; s < S; s++) put_row(row0 + s + max(cend, 1), bc[s], bs[s]);
 }
 
 struct GCand {  // a bridge candidate: total score, scan order 2*rL + loop, the two cells' columns
@@ -470,7 +625,7 @@ struct GCand {  // a bridge candidate: total score, scan order 2*rL + loop, the 
 #else
 #define GB_GROUP_ATTR __noinline__
 #endif
-template <int S, int LPW, int JL>
+template <int S, int LPW, int JL, bool PM>
 __device__ GB_GROUP_ATTR void gband_group(const AS_GLOBAL gsnapdp_ggap_window* Wn1, int wi,
                                          bool active, int lane, AS_GLOBAL uint32_t* wpool1,
                                          const AS_GLOBAL char* q1, const AS_GLOBAL char* qu1,
@@ -515,8 +670,10 @@ __device__ GB_GROUP_ATTR void gband_group(const AS_GLOBAL gsnapdp_ggap_window* W
   uint32_t* ri[2];
   int* rb[2];
   uint32_t* dg[2];
+  double* pr[2];  // probability mode: the site probabilities of the window's columns
 #pragma unroll
   for (int f = 0; f < 2; f++) {
+    pr[f] = (double*)(wpool + GB_OPR + 2 * (f * GB_NGMAX + g) * GB_COLS);
     ci[f] = (uint8_t*)(wpool + GB_OCI + (f * GB_NGMAX + g) * GB_CW);
     ri[f] = wpool + GB_ORI + (f * GB_NGMAX + g) * GB_RW;
     rb[f] = (int*)(wpool + GB_ORB + (f * GB_NGMAX + g) * GB_RW);
@@ -572,6 +729,30 @@ __device__ GB_GROUP_ATTR void gband_group(const AS_GLOBAL gsnapdp_ggap_window* W
         packed |= (uint64_t)(k[i] | cd << 3 | known << 6) << (8 * i);
       }
       if (cb <= L2 + 1) *(uint64_t*)(ci[f] + GB_CHK(cb, GB_CW * 4 - 7, 5)) = packed;  // bytes past L2 + 1 are never read
+      if constexpr (PM) {
+        // :3856-3903: a known site has probability 1.0, column L2 - 1 none (calloc)
+        if (tables != nullptr && cb < L2) {
+          int m, step;
+          uint32_t sp0;
+          site_line(w, f == FL_RIGHT, m, sp0, step);
+          uint32_t sp[GB_RUN];
+          bool ok[GB_RUN], kn[GB_RUN];
+          double pv[GB_RUN];
+#pragma unroll
+          for (int i = 0; i < GB_RUN; i++) {
+            const int c = cb + i;
+            kn[i] = c < L2 - 1 && km != GSNAPDP_KNOWN_NONE && kf[c] != 0;
+            ok[i] = c < L2 - 1 && !kn[i];
+            sp[i] = sp0 + (uint32_t)(step * c);
+          }
+          maxent_probs<GB_RUN>(m, sp, ok, w.chroffset, blocks, nwords, tables, pv);
+#pragma unroll
+          for (int i = 0; i < GB_RUN; i++) {
+            const int c = cb + i;
+            if (c < L2) pr[f][GB_CHK(c, GB_COLS, 18)] = kn[i] ? 1.0 : pv[i];  // column L2 - 1: 0.0
+          }
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < GB_RUN; i++) {
@@ -594,11 +775,11 @@ __device__ GB_GROUP_ATTR void gband_group(const AS_GLOBAL gsnapdp_ggap_window* W
   uint8_t* Ml = (uint8_t*)(Dl + GB_COLS * 64);
 #ifndef GB_EXP_NOFILL
   if (GB_PH(1)) {
-  gband_fill<S, LPW, 1 - JL, FL_RIGHT>(L1, G.L2R, G.lbR, G.rbR, G.open, G.mt * 128, LR.qbase, LR.qstep,
+  gband_fill<S, LPW, 1 - JL, FL_RIGHT, PM>(L1, G.L2R, G.lbR, G.rbR, G.open, G.mt * 128, LR.qbase, LR.qstep,
                                        (AS_GLOBAL uint32_t*)wpool, (const AS_GLOBAL char*)q,
                                        (const AS_GLOBAL char*)qu, sprof, ring);
   GB_TICK(1);
-  gband_fill<S, LPW, JL, FL_LEFT>(L1, G.L2L, G.lbL, G.rbL, G.open, G.mt * 128, LL.qbase, LL.qstep,
+  gband_fill<S, LPW, JL, FL_LEFT, PM>(L1, G.L2L, G.lbL, G.rbL, G.open, G.mt * 128, LL.qbase, LL.qstep,
                                   (AS_GLOBAL uint32_t*)wpool, (const AS_GLOBAL char*)q,
                                   (const AS_GLOBAL char*)qu, sprof, ring);
   }
@@ -610,7 +791,76 @@ __device__ GB_GROUP_ATTR void gband_group(const AS_GLOBAL gsnapdp_ggap_window* W
   // the left loop's best plus DR, then DL plus the right loop's best
   GCand best = {BRIDGE_INIT, 0x7fffffff, 0, 0};
   const int bias = (int)FV_BIAS;
-  for (int r0 = 1; r0 < (GB_PH(2) ? rmaxw : 0); r0 += GB_PB * LPW) {
+  // probability mode: a flank cell's H - pen (dynprog.c:3723) from the fill's
+  // cell values (lane jj = G / S, slot G % S of column c, G = r - c + WMAX - 1 - lband)
+  auto cellv = [&](int f, int r, int c) -> int {
+    const int lb = f == FL_LEFT ? G.lbL : G.lbR;
+    const int gs = r - c + S * LPW - 1 - lb;
+    const int jj = gs / S, sl = gs - jj * S;
+    const uint32_t wd = wpool[GB_OCV + f * GB_CVF + GB_CHK(4 * (c * 64 + jj * NG + g) + (sl >> 1), GB_CVF, 19)];
+    return (int)((wd >> (16 * (sl & 1))) & 0xffffu) - bias + (r + c) * GB_EXT;
+  };
+  double pbest = 0.0;  // probability mode: bestprob (:3905)
+  if constexpr (PM) {
+    // bridge_intron_gap's probability mode (:3905-4041): the row records, the
+    // two flank sweeps (gband_sweep), then the ordered argmax over (rL, loop)
+    int thr_i = wi;
+    asm volatile("" : "+v"(thr_i));
+    const int thr = Wn[thr_i].score_threshold;
+    for (int r = 1 + j; r < (GB_PH(2) ? rmaxw : 0); r += LPW) {
+      if (r >= L1) continue;
+      const int rp = L1 - r;  // the partner row of the other flank
+      const int npl = km != GSNAPDP_KNOWN_NONE ? krec[rp] : 0, npr = km != GSNAPDP_KNOWN_NONE ? krec[G.L2L + rp] : 0;
+      // D_other of the partner: H(rp, rp) + known(rp) (:3727, :3767)
+      const int DRp = ((int)dg[FL_RIGHT][GB_CHK(rp, GB_RW, 20)] - bias) + 2 * rp * GB_EXT + (npr != 0 ? KNOWN_REWARD : 0);
+      const int DLp = ((int)dg[FL_LEFT][GB_CHK(rp, GB_RW, 21)] - bias) + 2 * rp * GB_EXT + (npl != 0 ? KNOWN_REWARD : 0);
+      const double pRp = rp < G.L2R - 1 ? pr[FL_RIGHT][rp] : 0.0;
+      const double pLp = rp < G.L2L - 1 ? pr[FL_LEFT][rp] : 0.0;
+      u32x4 xl = {(uint32_t)(thr - DRp + bias - r * GB_EXT), ri[FL_LEFT][r], (uint32_t)__double2loint(pRp),
+                  (uint32_t)__double2hiint(pRp)};
+      u32x4 xr = {(uint32_t)(thr - DLp + bias - r * GB_EXT), ri[FL_RIGHT][r], (uint32_t)__double2loint(pLp),
+                  (uint32_t)__double2hiint(pLp)};
+      *(u32x4*)(wpool + GB_OREC + 4 * ((FL_LEFT * GB_NGMAX + g) * GB_RW + r)) = xl;
+      *(u32x4*)(wpool + GB_OREC + 4 * ((FL_RIGHT * GB_NGMAX + g) * GB_RW + r)) = xr;
+    }
+    wave_fence();
+    if (GB_PH(2)) {
+      gband_sweep<S, LPW, FL_LEFT>(L1, G.L2L, G.lbL, G.rbL, (AS_GLOBAL uint32_t*)wpool);
+      gband_sweep<S, LPW, FL_RIGHT>(L1, G.L2R, G.lbR, G.rbR, (AS_GLOBAL uint32_t*)wpool);
+    }
+    wave_fence();
+    for (int rL = 1 + j; rL < (GB_PH(2) ? rmaxw : 0); rL += LPW) {
+      if (rL >= L1) continue;
+      const int rR = L1 - rL;
+      const u32x4 xl = *(const u32x4*)(wpool + GB_OREC + 4 * ((FL_LEFT * GB_NGMAX + g) * GB_RW + rL));
+      const u32x4 xr = *(const u32x4*)(wpool + GB_OREC + 4 * ((FL_RIGHT * GB_NGMAX + g) * GB_RW + rR));
+      const double sl = __hiloint2double((int)xl.w, (int)xl.z), sr = __hiloint2double((int)xr.w, (int)xr.z);
+      if (sl > pbest) {  // left loop of row rL (cR = rR)
+        pbest = sl;
+        best.key = 2 * rL;
+        best.cL = (int)xl.x;
+        best.cR = rR;
+      }
+      if (sr > pbest) {  // right loop (cL = rL)
+        pbest = sr;
+        best.key = 2 * rL + 1;
+        best.cL = rL;
+        best.cR = (int)xr.x;
+      }
+    }
+#pragma unroll
+    for (int o = LPW / 2; o > 0; o >>= 1) {
+      const double xp = __shfl_xor(pbest, o);
+      const int xk = __shfl_xor(best.key, o), xl = __shfl_xor(best.cL, o), xr = __shfl_xor(best.cR, o);
+      if (xp > pbest || (xp == pbest && xk < best.key)) {
+        pbest = xp;
+        best.key = xk;
+        best.cL = xl;
+        best.cR = xr;
+      }
+    }
+  }
+  for (int r0 = 1; r0 < (!PM && GB_PH(2) ? rmaxw : 0); r0 += GB_PB * LPW) {
     int kl[GB_PB], kr[GB_PB], hl[GB_PB], hr[GB_PB], nl[GB_PB], nr[GB_PB];
 #pragma unroll
     for (int e = 0; e < GB_PB; e++) {
@@ -636,7 +886,7 @@ __device__ GB_GROUP_ATTR void gband_group(const AS_GLOBAL gsnapdp_ggap_window* W
     }
   }
 #pragma unroll
-  for (int o = LPW / 2; o > 0; o >>= 1) {
+  for (int o = PM ? 0 : LPW / 2; o > 0; o >>= 1) {
     GCand x;
     x.score = __shfl_xor(best.score, o);
     x.key = __shfl_xor(best.key, o);
@@ -674,15 +924,32 @@ __device__ GB_GROUP_ATTR void gband_group(const AS_GLOBAL gsnapdp_ggap_window* W
     const bool kR = km != GSNAPDP_KNOWN_NONE && cR < G.L2R && krec[G.L2L + cR] != 0;
     int it;
     const int sI = intron_score(it, dl, dr, wo.cdna_direction, G.canon, wo.finalp);
-    const int finalscore = wo.halfp ? best.score - sI / 2 : best.score;
-    R.introntype = best.score > BRIDGE_INIT ? it : 0;
-    rc = finalscore >= 0 ? 1 : 0;
+    int finalscore = 0;
+    if constexpr (PM) {
+      // :4043-4068: the chosen cells' scores, both with their pen
+      if (!(pbest > 0.0)) {
+        rc = -1;  // no candidate: the reference reads uninitialised indices (:4055)
+      } else {
+        const int sL = cellv(FL_LEFT, rLb, cL) + (kL ? KNOWN_REWARD : 0);
+        const int sR = cellv(FL_RIGHT, rRb, cR) + (kR ? KNOWN_REWARD : 0);
+        finalscore = wo.halfp ? sL + sI + sR - sI / 2 : sL + sI + sR;
+        rc = finalscore >= 0 ? 1 : 0;
+      }
+    } else {
+      finalscore = wo.halfp ? best.score - sI / 2 : best.score;
+      R.introntype = best.score > BRIDGE_INIT ? it : 0;
+      rc = finalscore >= 0 ? 1 : 0;
+    }
     // novel splicing off with a site-level IIT: both chosen sites must be known (:4090-4096)
     if (rc == 1 && km == GSNAPDP_KNOWN_SITES)
       rc = kL && kR;
-    if (wo.finalp && tables == nullptr) rc = -2;
+    if ((PM || wo.finalp) && tables == nullptr) rc = -2;
     if (rc == -2) {
       X.status = ST_UNSUPPORTED;
+      R.returned_null = 1;
+      R.finalscore = NEG;
+    } else if (rc == -1) {
+      R.bridge_ok = 0;
       R.returned_null = 1;
       R.finalscore = NEG;
     } else {
@@ -770,7 +1037,7 @@ __device__ GB_GROUP_ATTR void gband_group(const AS_GLOBAL gsnapdp_ggap_window* W
 
 // This wave's wave-tasks of one band class (both tie-rule lists; __noinline__
 // for its own register allocation, as k_fill's fill_tasks).
-template <int S, int LPW>
+template <int S, int LPW, bool PM>
 __device__ __noinline__ void gband_tasks(int cls, int t0, int t1, int stride, int ntask0,
                                          const AS_GLOBAL gsnapdp_ggap_window* Wn1,
                                          const AS_GLOBAL int* lists1, const AS_GLOBAL int* counts1,
@@ -790,7 +1057,7 @@ __device__ __noinline__ void gband_tasks(int cls, int t0, int t1, int stride, in
   for (int t = t0; t < t1; t += stride) {
     const int jl = t >= ntask0 ? 1 : 0;
     const int lt = t - (jl ? ntask0 : 0);
-    const int li = GB_LIST0 + 2 * cls + jl;
+    const int li = (PM ? GP_LIST0 : GB_LIST0) + 2 * cls + jl;
     const int* list = (const int*)lists1 + (size_t)li * list_cap;
     const int n = ((const int*)counts1)[li];
     const int k = lt * NG + g;
@@ -801,10 +1068,10 @@ __device__ __noinline__ void gband_tasks(int cls, int t0, int t1, int stride, in
     GB_CHK(wi, list_cap * 4, 14);
 #endif
     if (jl)
-      gband_group<S, LPW, 1>(Wn1, wi, active, lane, wpool1, q1, qu1, blocks1, nwords, sprof3, ring3,
+      gband_group<S, LPW, 1, PM>(Wn1, wi, active, lane, wpool1, q1, qu1, blocks1, nwords, sprof3, ring3,
                              tables1, res1, trc1, ops1, op_off1);
     else
-      gband_group<S, LPW, 0>(Wn1, wi, active, lane, wpool1, q1, qu1, blocks1, nwords, sprof3, ring3,
+      gband_group<S, LPW, 0, PM>(Wn1, wi, active, lane, wpool1, q1, qu1, blocks1, nwords, sprof3, ring3,
                              tables1, res1, trc1, ops1, op_off1);
   }
 }
@@ -832,23 +1099,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GB_WAVES_PE
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nw = (gridDim.x * blockDim.x) >> 6;
   uint32_t* wpool = pool + (size_t)gw * GB_WAVE_DW;
-  // tasks of class k (classes 1..NCLASS-1 of k_fill's table): both tie-rule lists
-  int tfirst[NCLASS], ntask0[NCLASS];
+  // tasks of list pair k: score mode for k < NCLASS - 1, then probability mode
+  // (band class k % (NCLASS - 1) + 1 of k_fill's table), both tie-rule lists
+  static_assert(GP_LIST0 == GB_LIST0 + 2 * (NCLASS - 1), "k_gband's list pairs");
+  constexpr int NK = 2 * (NCLASS - 1);
+  int tfirst[NK + 1], ntask0[NK];
   tfirst[0] = 0;
 #pragma unroll
-  for (int k = 0; k < NCLASS - 1; k++) {
-    const int ng = 64 / CLASS_LPW[k + 1];
+  for (int k = 0; k < NK; k++) {
+    const int ng = 64 / CLASS_LPW[k % (NCLASS - 1) + 1];
     const int n0 = counts[GB_LIST0 + 2 * k], n1 = counts[GB_LIST0 + 2 * k + 1];
     ntask0[k] = (n0 + ng - 1) / ng;
     tfirst[k + 1] = tfirst[k] + ntask0[k] + (n1 + ng - 1) / ng;
   }
-#define GBAND_CLASS(K)                                                                           \
+#define GBAND_CLASS(K, PM)                                                                       \
   {                                                                                              \
-    const int lo = tfirst[K], hi = tfirst[K + 1];                                                \
+    constexpr int KK = K + (PM ? NCLASS - 1 : 0);                                                \
+    const int lo = tfirst[KK], hi = tfirst[KK + 1];                                              \
     const int tau0 = gw >= lo ? gw : gw + (lo - gw + nw - 1) / nw * nw;                          \
     if (tau0 < hi)                                                                               \
-      gband_tasks<CLASS_S[K + 1], CLASS_LPW[K + 1]>(                                            \
-          K, tau0 - lo, hi - lo, nw, ntask0[K], (const AS_GLOBAL gsnapdp_ggap_window*)Wn,         \
+      gband_tasks<CLASS_S[K + 1], CLASS_LPW[K + 1], PM>(                                        \
+          K, tau0 - lo, hi - lo, nw, ntask0[KK], (const AS_GLOBAL gsnapdp_ggap_window*)Wn,        \
           (const AS_GLOBAL int*)lists, (const AS_GLOBAL int*)counts, list_cap,                    \
           (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu, (const AS_GLOBAL uint32_t*)blocks, \
           nwords, (const AS_LDS uint32_t*)sprof, (AS_LDS uint32_t*)ring,                         \
@@ -858,7 +1129,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GB_WAVES_PE
           (const AS_GLOBAL int64_t*)op_off);                                                     \
   }
   static_assert(NCLASS == 7, "k_gband dispatches classes 1..6");
-  GBAND_CLASS(0) GBAND_CLASS(1) GBAND_CLASS(2) GBAND_CLASS(3) GBAND_CLASS(4) GBAND_CLASS(5)
+  GBAND_CLASS(0, false) GBAND_CLASS(1, false) GBAND_CLASS(2, false)
+  GBAND_CLASS(3, false) GBAND_CLASS(4, false) GBAND_CLASS(5, false)
+  GBAND_CLASS(0, true) GBAND_CLASS(1, true) GBAND_CLASS(2, true)
+  GBAND_CLASS(3, true) GBAND_CLASS(4, true) GBAND_CLASS(5, true)
 #undef GBAND_CLASS
 }
 

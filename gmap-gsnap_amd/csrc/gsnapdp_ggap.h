@@ -171,6 +171,35 @@ __device__ inline double right_site_prob(const gsnapdp_ggap_window& w, int cR,
                      w.chroffset, blocks, nwords, T);
 }
 
+// The model and position line of one flank's splice columns: column c's site
+// is sp0 + step * c with model m, as left_site_prob / right_site_prob compute
+// them (uint32 arithmetic, the same wrap-around).
+__device__ inline void site_line(const gsnapdp_ggap_window& w, int right, int& m, uint32_t& sp0, int& step) {
+  const int cdir = w.cdna_direction;
+  const uint32_t last = (uint32_t)(w.genomiclength - 1);
+  if (!right) {
+    if (w.watsonp) {
+      m = cdir > 0 ? GSNAPDP_DONOR : GSNAPDP_ANTIACCEPTOR;
+      sp0 = w.chroffset + (w.chrpos + (uint32_t)w.offset2L);
+      step = 1;
+    } else {
+      m = cdir > 0 ? GSNAPDP_ANTIDONOR : GSNAPDP_ACCEPTOR;
+      sp0 = w.chroffset + (w.chrpos + last - (uint32_t)w.offset2L + 1u);
+      step = -1;
+    }
+  } else {
+    if (w.watsonp) {
+      m = cdir > 0 ? GSNAPDP_ACCEPTOR : GSNAPDP_ANTIDONOR;
+      sp0 = w.chroffset + (w.chrpos + (uint32_t)w.revoffset2R + 1u);
+      step = -1;
+    } else {
+      m = cdir > 0 ? GSNAPDP_ANTIACCEPTOR : GSNAPDP_DONOR;
+      sp0 = w.chroffset + (w.chrpos + last - (uint32_t)w.revoffset2R);
+      step = 1;
+    }
+  }
+}
+
 // The per-side view the shared traceback template expects (gsnapdp_device.h).
 __device__ inline Lane side_lane(const gsnapdp_ggap_window& w, const GGeo& G, int right) {
   Lane L;
@@ -205,33 +234,43 @@ __device__ inline Lane side_lane(const gsnapdp_ggap_window& w, const GGeo& G, in
 }
 
 
-// ---- k_gband (gsnapdp_gband.hip): the register-band path of score-mode windows.
-// Lists of a genome-gap batch: 0..2 the row-lane classes of k_ggap, then
-// GB_LIST0 + 2*k + jump_late_p for k_fill's band classes k + 1 = 1..6.
+// ---- k_gband (gsnapdp_gband.hip): the register-band path of score- and
+// probability-mode windows.  Lists of a genome-gap batch: 0..2 the row-lane
+// classes of k_ggap, then GB_LIST0 + 2*k + jump_late_p (score mode) and
+// GP_LIST0 + 2*k + jump_late_p (probability mode) for k_fill's band classes
+// k + 1 = 1..6.
 constexpr int GB_L2MAX = 256;            // longest flank on the register band
 constexpr int GB_LIST0 = 3;
-constexpr int GG_NLISTS = GB_LIST0 + 2 * (NCLASS - 1);
+constexpr int GP_LIST0 = GB_LIST0 + 2 * (NCLASS - 1);
+constexpr int GG_NLISTS = GP_LIST0 + 2 * (NCLASS - 1);
 #ifndef GB_WAVES_PER_SIMD
 #define GB_WAVES_PER_SIMD 2  // k_gband (256 VGPRs): C4 score 0.65 ms; 3 waves 0.70, 4 waves 0.95 (spills)
 #endif
-// per-wave scratch of k_gband in dwords (layout in gsnapdp_gband.hip)
+// per-wave scratch of k_gband in dwords (layout in gsnapdp_gband.hip): the
+// score-mode part, then probability mode's cell values (4 dwords per lane and
+// column, both flanks), site probabilities (doubles per window and column) and
+// row records (4 dwords per window and row)
 constexpr int GB_WAVE_DW = 2 * (GB_L2MAX + 4) * 80 + 2 * 32 * ((GB_L2MAX + 4) / 4 + 1) +
-                           3 * 2 * 32 * (GB_L2MAX + 4);
+                           3 * 2 * 32 * (GB_L2MAX + 4) + 2 * (GB_L2MAX + 4) * 256 + 2 * 32 * (GB_L2MAX + 4) * 2 +
+                           2 * 32 * (GB_L2MAX + 4) * 4;
+// use_band bits of k_ggap_plan
+enum { GB_USE_SCORE = 1, GB_USE_PROB = 2 };
 
 // The register-band list of a window that reached the fills, or -1 for k_ggap:
-// score mode without the constrained known-intron bridge, both flanks at
-// least length1 long (so the bridge's band is the fill band, :3716-3760) and
-// at most GB_L2MAX, band width <= FAST_WMAX, and an intron span that never
-// cuts the bridge's columns (cL < span - rR, cR < span - rL; :3720, :3760).
-__device__ inline int gband_list(const gsnapdp_ggap_window& w, const GGeo& G) {
-  if (w.use_probabilities_p || w.known_mode == GSNAPDP_KNOWN_INTRONS) return -1;
+// no constrained known-intron bridge, both flanks at least length1 long (so the
+// bridge's band is the fill band, :3716-3760) and at most GB_L2MAX, band width
+// <= FAST_WMAX, and an intron span that never cuts the bridge's columns
+// (cL < span - rR, cR < span - rL; :3720, :3760).
+__device__ inline int gband_list(const gsnapdp_ggap_window& w, const GGeo& G, int use_band) {
+  if (w.known_mode == GSNAPDP_KNOWN_INTRONS) return -1;
+  if (!(use_band & (w.use_probabilities_p ? GB_USE_PROB : GB_USE_SCORE))) return -1;
   if (G.L2L < G.L1 || G.L2R < G.L1 || G.L2L > GB_L2MAX || G.L2R > GB_L2MAX) return -1;
   const int W = G.WL > G.WR ? G.WL : G.WR;
   if (W > FAST_WMAX) return -1;
   const int span = w.revoffset2R - w.offset2L;
   if (span - G.L1 - 1 < (G.rbL > G.rbR ? G.rbL : G.rbR)) return -1;
   const int k = class_of_w(W);
-  return GB_LIST0 + 2 * (k > 0 ? k - 1 : 0) + (w.jump_late_p ? 1 : 0);
+  return (w.use_probabilities_p ? GP_LIST0 : GB_LIST0) + 2 * (k > 0 ? k - 1 : 0) + (w.jump_late_p ? 1 : 0);
 }
 
 }  // namespace gsnapdp

@@ -41,7 +41,7 @@ namespace {
 
 // window classes of the batch
 enum { GG_SMALL = 0, GG_MID = 1, GG_BIG = 2, GG_NCLS = 3 };
-static_assert(GB_LIST0 == GG_NCLS && GG_NLISTS <= 16, "genome-gap lists (the counts buffer holds 16)");
+static_assert(GB_LIST0 == GG_NCLS && GG_NLISTS <= 32, "genome-gap lists (the counts buffer holds 32)");
 #ifndef GG_SMALL_WORDS_CFG
 #define GG_SMALL_WORDS_CFG 1280
 #endif
@@ -803,7 +803,7 @@ __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
       X.status = ST_UNSUPPORTED;
     } else {
       done = false;
-      cls = use_band ? gband_list(w, G) : -1;  // the register band (k_gband) when it can
+      cls = gband_list(w, G, use_band);  // the register band (k_gband) when it can
       const int bndw = G.L1 + 1 > 64 ? 3 * (max(G.L2L, G.L2R) + 2) : 0;  // stripe boundary row
       if (cls >= 0) {
       } else if (G.L1 + 1 <= 32 && G.words <= GG_SMALL_WORDS) cls = GG_SMALL;
@@ -1305,7 +1305,7 @@ static int ggap_capacity(gsnapdp_ctx* ctx, int n) {
     HIPCHK(hipMalloc(&ctx->d_ggap_lists, (size_t)GG_NLISTS * cap * 4));
     ctx->ggap_cap = cap;
   }
-  if (!ctx->d_ggap_counts) HIPCHK(hipMalloc(&ctx->d_ggap_counts, 64));
+  if (!ctx->d_ggap_counts) HIPCHK(hipMalloc(&ctx->d_ggap_counts, 128));
   return 0;
 }
 
@@ -1328,7 +1328,7 @@ extern "C" int gsnapdp_ggap_run_device(gsnapdp_ctx* ctx, const gsnapdp_ggap_wind
   HIPCHK(hipMemsetAsync(counts, 0, 4 * GG_NLISTS, st));
   gsnapdp__mark(ctx, st, 4, 0);
   hipLaunchKernelGGL(k_ggap_plan, dim3((n + 255) / 256), dim3(256), 0, st, d_windows, n,
-                     d_results, d_traces, lists, counts, cap, ctx->ggap_rowlane_only ? 0 : 1);
+                     d_results, d_traces, lists, counts, cap, ctx->ggap_use_band);
   gsnapdp__mark(ctx, st, 4, 1);
   gsnapdp__mark(ctx, st, 6, 0);
   if (!ctx->ggap_rowlane_only &&

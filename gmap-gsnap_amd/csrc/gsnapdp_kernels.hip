@@ -1057,6 +1057,10 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
   {
     const char* e = getenv("GSNAPDP_GGAP_ROWLANE");
     ctx->ggap_rowlane_only = (e && e[0] == '1') ? 1 : 0;
+    // GSNAPDP_GBAND_PROB=1: probability-mode windows on k_gband too (A/B tests;
+    // off by default until it beats k_ggap, DESIGN.md §4 k_gband)
+    const char* p = getenv("GSNAPDP_GBAND_PROB");
+    ctx->ggap_use_band = ctx->ggap_rowlane_only ? 0 : (1 | ((p && p[0] == '1') ? 2 : 0));  // GB_USE_SCORE | GB_USE_PROB
     const char* f = getenv("GSNAPDP_ENDS_ROWLANE");
     ctx->ends_rowlane = (f && f[0] == '1') ? 1 : 0;
   }

@@ -177,3 +177,38 @@ def test_gpu_gband_jump_late_batches(jl):
     ores, opairs, ooff, onp = O.run_ggap_batch(w, b.query, b.query_uc)
     oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
     compare(w, res, trc, pairs, npairs, ores, oflat, onp, "jump-late %s" % jl)
+
+
+@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap", "gmap_her2_ggap", "ggap_known_sites",
+                                  "ggap_known_sites_novel"])
+def test_gpu_gband_probability_mode_matches_reference_golden(golden_dir, name, monkeypatch):
+    """Probability-mode windows on the register band (GSNAPDP_GBAND_PROB=1:
+    the fills' cell values and the bridge sweeps of gsnapdp_gband.hip) against
+    the reference's goldens."""
+    monkeypatch.setenv("GSNAPDP_GBAND_PROB", "1")
+    z = load(golden_dir, name)
+    ctx = Context(z["blocks"])
+    w = z["windows"]
+    res, trc, ops, off = ctx.ggap_run(w, z["query"], z["query_uc"])
+    pairs, npairs = ctx.ggap_all_pairs(w, z["query"], z["query_uc"], res, trc, ops, off)
+    compare(w, res, trc, pairs, npairs, z["results"], z["pairs"], z["npairs"], name + " (band prob)")
+
+
+@pytest.mark.parametrize("jl", ["none", "mixed"])
+def test_gpu_gband_probability_mode_matches_oracle(jl, monkeypatch):
+    """C4-shape probability-mode windows on the register band, jump-late mixed,
+    a third with extraband 10 (the S = 8 classes), against the oracle."""
+    monkeypatch.setenv("GSNAPDP_GBAND_PROB", "1")
+    rng = np.random.default_rng(78)
+    g, b = W.c4_windows(W.synthetic_genome(8_000_000, seed=5), 20_000, seed=5, use_probabilities=True)
+    w = b.windows.copy()
+    if jl == "mixed":
+        w["jump_late_p"] = rng.integers(0, 2, len(w))
+        w["extraband_paired"][::3] = 10
+    blocks = W.pack_genome(g)
+    res, trc, pairs, npairs = run_gpu(blocks, W.Batch(w, b.query, b.query_uc))
+    O.setup(blocks)
+    ores, opairs, ooff, onp = O.run_ggap_batch(w, b.query, b.query_uc)
+    oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
+    compare(w, res, trc, pairs, npairs, ores, oflat, onp, "band prob %s" % jl)
+    assert np.mean(ores["returned_null"] == 0) > 0.5

@@ -22,6 +22,7 @@ genome = W.synthetic_genome(64_000_000, seed=1)
 
 def run(blocks, b, rowlane, steps=10):
     os.environ["GSNAPDP_GGAP_ROWLANE"] = "1" if rowlane else "0"
+    os.environ["GSNAPDP_GBAND_PROB"] = "1"  # probability mode on the band too
     ctx = Context(blocks, mode=0, device=0)
     m = len(b.windows)
     off = ggap_op_offsets(b.windows)
