@@ -56,7 +56,6 @@ static_assert(FV_BIAS + 2 * PAIRED_OPEN > FV_NEG + 9u * (GB_L2MAX + 48) + 20 + 4
               "reachable and NEG-like values stay apart with the paired open");
 constexpr int GB_KEY_NONE = -(1 << 30);
 constexpr int GB_PB = 8;  // rows per lane per batch of the combine
-constexpr int GB_SD = 4;  // steps of look-ahead of the probability-mode bridge sweep
 constexpr int GB_COLKEY = 1023;  // column part of a key: 1023 - c (c <= GB_L2MAX)
 
 // per-wave scratch (dwords): the two flanks' direction words and match bytes,
@@ -540,9 +539,13 @@ __device__ __noinline__ void gband_sweep(int L1, int L2, int lband, int rband, A
       rec[GB_CHK(r, GB_RW, 23)] = x;
     }
   };
-  // the loads of step c (the lane's cell values of column c, the record of the
-  // row entering slot S - 1, the column's probability and byte), issued
-  // GB_SD steps ahead of their use
+  // The loads of step c (the lane's cell values of column c, the record of the
+  // row entering slot S - 1, the column's probability and byte) are issued S
+  // steps ahead of their use.  No register moves with the rows: logical slot s
+  // at column c lives in register (s + c) % S, so the loop runs S columns per
+  // iteration with every index a constant (column c = 1 + kS + u: slot s in
+  // register (s + 1 + u) % S; the row leaving slot 0 and the one entering slot
+  // S - 1 share register u).
   struct Pre {
     u32x4 e, r;
     double pc;
@@ -557,61 +560,61 @@ __device__ __noinline__ void gband_sweep(int L1, int L2, int lband, int rband, A
     q.pc = c <= L2 - 1 ? prc[cc] : -2.0;  // past the window's bridge columns: never a candidate
     q.cb = cib[cc];
   };
-  auto step = [&](int c, const Pre& q) {
+  auto step = [&](auto ut, int c, const Pre& q) {
+    constexpr int U = decltype(ut)::value;
     if (c > 1) {
       // the row in slot 0 moves to lane j - 1 (lane 0: it leaves the band, complete)
-      if (j == 0) put_row(row0 + c - 1, bc[0], bs[0]);
-      const int ilo = from_lane_below(__double2loint(bs[0])), ihi = from_lane_below(__double2hiint(bs[0]));
-      const int icc = from_lane_below(bc[0]);
-#pragma unroll
-      for (int s = 0; s < S - 1; s++) {
-        bs[s] = bs[s + 1];
-        bc[s] = bc[s + 1];
-        T[s] = T[s + 1];
-        Wd[s] = Wd[s + 1];
-        pO[s] = pO[s + 1];
-      }
+      if (j == 0) put_row(row0 + c - 1, bc[U], bs[U]);
+      const int ilo = from_lane_below(__double2loint(bs[U])), ihi = from_lane_below(__double2hiint(bs[U]));
+      const int icc = from_lane_below(bc[U]);
       const bool top = j == LPW - 1;
-      bs[S - 1] = top ? 0.0 : __hiloint2double(ihi, ilo);
-      bc[S - 1] = top ? -1 : icc;
+      bs[U] = top ? 0.0 : __hiloint2double(ihi, ilo);
+      bc[U] = top ? -1 : icc;
       const int r = row0 + S - 1 + c;
-      T[S - 1] = r >= 1 && r < L1 ? (int)q.r.x : 0x7fffffff;
-      Wd[S - 1] = q.r.y;
-      pO[S - 1] = __hiloint2double((int)q.r.w, (int)q.r.z);
+      T[U] = r >= 1 && r < L1 ? (int)q.r.x : 0x7fffffff;
+      Wd[U] = q.r.y;
+      pO[U] = __hiloint2double((int)q.r.w, (int)q.r.z);
     }
     const int colt = c * GB_EXT + (int)((q.cb >> 6) & 1u) * KNOWN_REWARD;
     const uint32_t csh = ((q.cb >> 3) & 7u) * 6u;
 #pragma unroll
     for (int s = 0; s < S; s++) {
+      const int p = (s + 1 + U) % S;
       const uint32_t word = s < 2 ? q.e.x : s < 4 ? q.e.y : s < 6 ? q.e.z : q.e.w;
       const int v = (int)((word >> (16 * (s & 1))) & 0xffffu);
-      const int sI = (int)__builtin_amdgcn_ubfe(Wd[s], csh, 6);
-      const double sum = q.pc + pO[s];
-      const bool take = inb[s] && v + colt + sI >= T[s] && sum > bs[s];
-      bs[s] = take ? sum : bs[s];
-      bc[s] = take ? c : bc[s];
+      const int sI = (int)__builtin_amdgcn_ubfe(Wd[p], csh, 6);
+      const double sum = q.pc + pO[p];
+      const bool take = inb[s] && v + colt + sI >= T[p] && sum > bs[p];
+      bs[p] = take ? sum : bs[p];
+      bc[p] = take ? c : bc[p];
     }
   };
 #pragma unroll
   for (int s = 0; s < S; s++) {
+    const int p = (s + 1) % S;
     inb[s] = j * S + s >= stop;
-    load_row(row0 + s + 1, T[s], Wd[s], pO[s]);
-    bs[s] = 0.0;  // bestprob starts at 0.0 (:3905): a row's sum must exceed it
-    bc[s] = -1;
+    load_row(row0 + s + 1, T[p], Wd[p], pO[p]);
+    bs[p] = 0.0;  // bestprob starts at 0.0 (:3905): a row's sum must exceed it
+    bc[p] = -1;
   }
-  Pre pq[GB_SD];
+  Pre pq[S];
 #pragma unroll
-  for (int d = 0; d < GB_SD; d++) issue(1 + d, pq[d]);
-  for (int c = 1; c <= cend; c += GB_SD) {
-#pragma unroll
-    for (int d = 0; d < GB_SD; d++) {
-      if (c + d <= cend) step(c + d, pq[d]);
-      issue(c + d + GB_SD, pq[d]);
-    }
+  for (int d = 0; d < S; d++) issue(1 + d, pq[d]);
+  for (int c = 1; c <= cend; c += S) {
+    unroll_seq(std::make_integer_sequence<int, S>(), [&](auto ut) {
+      constexpr int U = decltype(ut)::value;
+      if (c + U <= cend) step(ut, c + U, pq[U]);
+      issue(c + U + S, pq[U]);
+    });
   }
-  // the rows still in the band after the last column
+  // the rows still in the band after the last column cl: register p holds
+  // logical slot (p - cl) mod S
+  const int cl = max(cend, 1);
 #pragma unroll
-  for (int s = 0; s < S; s++) put_row(row0 + s + max(cend, 1), bc[s], bs[s]);
+  for (int p = 0; p < S; p++) {
+    const int sl = ((p - cl) % S + S) % S;
+    put_row(row0 + sl + cl, bc[p], bs[p]);
+  }
 }
 
 struct GCand {  // a bridge candidate: total score, scan order 2*rL + loop, the two cells' columns
