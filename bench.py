@@ -375,25 +375,43 @@ def measure_stage3(paths=7424, reps=3):
     calls, pin, q, qu, want = W.stage3_calls(z, copies)
     ctx = Context(z["blocks"])
     stage2_double(ctx, z)  # build_dual_breaks' stage-2 dual breaks, from the recording
+    from gsnapdp import expand_compact
     ctx.stage3_pass(calls[:64], pin, q, qu)  # warm-up
+    # the full-pair output (every returned cell as a whole pair record) ...
     buf = np.empty(ctx.stage3_capacity(calls), dtype=want.dtype)
-    best = None
+    full_s = None
     for _ in range(reps + 1):  # the first run also faults the output buffer in
         t0 = time.perf_counter()
         c, got, st = ctx.stage3_pass(calls, pin, q, qu, out=buf)
         dt = time.perf_counter() - t0
+        full_s = dt if full_s is None else min(full_s, dt)
+    ok_full = bool((c["status"] == 0).all()) and got.tobytes() == want.tobytes()
+    # ... and the timed form, the compact output a caller that owns the input
+    # cells takes (gsnapdp_stage3_pass_compact: each returned cell as the index
+    # of its input pair, new pairs apart; what the drop-in relinks)
+    bufs = None
+    best = None
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        c, cells, new, st = ctx.stage3_pass_compact(calls, pin, q, qu, bufs=bufs)
+        dt = time.perf_counter() - t0
+        if bufs is None:
+            bufs = (cells.base, new.base)
         if best is None or dt < best[0]:
-            best = (dt, c, got.copy(), st)
-    dt, c, got, st = best
-    ok = bool((c["status"] == 0).all()) and got.tobytes() == want.tobytes()
+            best = (dt, c, cells.copy(), new.copy(), st)
+    dt, c, cells, new, st = best
+    got = expand_compact(c, pin, cells, new)
+    ok = ok_full and bool((c["status"] == 0).all()) and got.tobytes() == want.tobytes()
     for f in ("out_minor", "out_major", "out_nintrons", "out_nnonintrons", "out_intronlen", "out_nonintronlen",
               "shiftp", "incompletep", "nout"):
         ok = ok and bool(np.array_equal(c[f], calls[f]))
     nwin = int(np.sum(st["windows"]))
     ref = float(z["calls"]["ref_seconds"].sum()) * copies
     ctx.close()
-    cpu = stage3_cpu_baseline(z["blocks"], calls, pin, q, qu, got, z=z)
+    cpu, (_, rcells, rnew, _) = stage3_cpu_baseline(z["blocks"], calls, pin, q, qu, z=z, compact=True)
+    cpu["cells_equal_gpu"] = bool(np.array_equal(rcells, cells) and rnew.tobytes() == new.tobytes())
     return {"metric": "stage-3 passes (path_compute's DP passes), paths/s",
+            "output": "compact (gsnapdp_stage3_pass_compact); full-pair output %.4f s" % full_s,
             "value": round(len(calls) / dt, 1), "unit": "paths/s", "paths": int(len(calls)),
             "paths_by_pass": {n: int((calls["pass"] == i).sum())
                               for i, n in enumerate(("introns", "singles", "end5", "end3", "dualintrons"))},
