@@ -87,9 +87,8 @@ def test_dropin_host_helpers_match_reference(tmp_path):
 
 
 def load_double(tmp_path):
-    so = os.path.join(str(tmp_path), "libpairpool_double.so")
-    subprocess.check_call(["gcc", "-O1", "-shared", "-fPIC", "-o", so, DOUBLE_SRC])
-    lib = ctypes.CDLL(so, mode=ctypes.RTLD_GLOBAL)  # resolves the shim's Pairpool_push*
+    from doubles import pairpool_double
+    lib = pairpool_double()  # resolves the shim's Pairpool_push* (one copy per process)
     lib.dbl_list_read.restype = ctypes.c_int
     lib.dbl_list_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     lib.dbl_list_free.argtypes = [ctypes.c_void_p]

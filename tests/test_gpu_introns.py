@@ -5,7 +5,6 @@ against every call the reference's gmap made (gmap_trace goldens: ss.her2 and
 the synthetic spliced cDNAs), and against the restatement on random paths."""
 import ctypes
 import os
-import subprocess
 
 import numpy as np
 import pytest
@@ -79,9 +78,8 @@ def test_dropin_score_introns_matches_reference_golden(golden_dir, tmp_path):
     """Gsnapdp_score_introns as stage3.c would call it: the path as a List_T of
     the host's Pair_T cells, the three out-parameters, and the returned list
     (the path's cells, reversed)."""
-    so = os.path.join(str(tmp_path), "libpairpool_double.so")
-    subprocess.check_call(["gcc", "-O1", "-shared", "-fPIC", "-o", so, DOUBLE_SRC])
-    dbl = ctypes.CDLL(so, mode=ctypes.RTLD_GLOBAL)
+    from doubles import pairpool_double
+    dbl = pairpool_double()  # one copy per process (tests/doubles.py)
     dbl.dbl_list_build.restype = ctypes.c_void_p
     dbl.dbl_list_build.argtypes = [ctypes.c_void_p, ctypes.c_int]
     dbl.dbl_list_read.restype = ctypes.c_int

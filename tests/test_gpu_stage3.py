@@ -133,16 +133,13 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     disallowedp).  The IIT sets give Dynprog_setup a splicing IIT (the IIT test
     double over the golden's intervals, as test_dropin's genome-gap test does)."""
     import ctypes
-    import subprocess
 
     from gsnapdp.records import S3_DUALBREAKS, S3_DUALINTRONS, S3_END3, S3_END5, S3_PAIR, S3_SINGLES
     from test_dropin import SETUP_ARGS, load_iit_double
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    so = os.path.join(str(tmp_path), "libpairpool_double.so")
-    subprocess.check_call(["gcc", "-O1", "-shared", "-fPIC", "-o", so,
-                           os.path.join(root, "tests", "dropin", "pairpool_double.c")])
-    dbl = ctypes.CDLL(so, mode=ctypes.RTLD_GLOBAL)
+    from doubles import pairpool_double
+    dbl = pairpool_double()  # one copy per process: the drop-in binds Stage2_compute_one from the first one
     vp, i32, u8, u32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_ubyte, ctypes.c_uint
     dbl.dbl_s3_build.restype = vp
     dbl.dbl_s3_build.argtypes = [vp, i32]
