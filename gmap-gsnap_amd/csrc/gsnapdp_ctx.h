@@ -82,6 +82,7 @@ struct gsnapdp_ctx {
   uint32_t* d_gband_pool = nullptr; // per-wave scratch of the register-band path (k_gband)
   int ggap_rowlane_only = 0;        // GSNAPDP_GGAP_ROWLANE=1: every window on k_ggap (A/B tests)
   int ggap_use_band = 1;            // k_ggap_plan's GB_USE_* bits (GSNAPDP_GBAND_PROB=1 sets the prob bit)
+  int gband_min = 16384;            // smallest genome-gap batch on the register band (GSNAPDP_GBAND_MIN)
   int ends_rowlane = 0;             // GSNAPDP_ENDS_ROWLANE=1: every end gap on k_rows (A/B tests)
   size_t ggap_stage_cap = 0;
   void* d_ggap_stage = nullptr;

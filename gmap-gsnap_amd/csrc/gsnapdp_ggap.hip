@@ -1327,13 +1327,13 @@ extern "C" int gsnapdp_ggap_run_device(gsnapdp_ctx* ctx, const gsnapdp_ggap_wind
   const int cap = ctx->ggap_cap;
   HIPCHK(hipMemsetAsync(counts, 0, 4 * GG_NLISTS, st));
   gsnapdp__mark(ctx, st, 4, 0);
+  const int use_band = n >= ctx->gband_min ? ctx->ggap_use_band : 0;
   hipLaunchKernelGGL(k_ggap_plan, dim3((n + 255) / 256), dim3(256), 0, st, d_windows, n,
-                     d_results, d_traces, lists, counts, cap, ctx->ggap_use_band);
+                     d_results, d_traces, lists, counts, cap, use_band);
   gsnapdp__mark(ctx, st, 4, 1);
   gsnapdp__mark(ctx, st, 6, 0);
-  if (!ctx->ggap_rowlane_only &&
-      gsnapdp__gband_launch(ctx, st, d_windows, lists, counts, cap, d_query, d_query_uc, d_results,
-                            d_traces, d_ops, d_op_offsets))
+  if (use_band && gsnapdp__gband_launch(ctx, st, d_windows, lists, counts, cap, d_query, d_query_uc, d_results,
+                                        d_traces, d_ops, d_op_offsets))
     return -1;
   gsnapdp__mark(ctx, st, 6, 1);
   gsnapdp__mark(ctx, st, 5, 0);

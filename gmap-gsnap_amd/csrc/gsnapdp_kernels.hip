@@ -1061,6 +1061,12 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
     // off by default until it beats k_ggap, DESIGN.md §4 k_gband)
     const char* p = getenv("GSNAPDP_GBAND_PROB");
     ctx->ggap_use_band = ctx->ggap_rowlane_only ? 0 : (1 | ((p && p[0] == '1') ? 2 : 0));  // GB_USE_SCORE | GB_USE_PROB
+    // a register-band wave-task (16 windows) takes ~80 us and a row-lane one (2
+    // windows) ~37 us, so the band pays only once a batch fills the row-lane
+    // waves several times over: smaller batches (the stage-3 pass's rounds) stay
+    // on k_ggap (DESIGN.md §4 k_gband)
+    const char* m = getenv("GSNAPDP_GBAND_MIN");
+    if (m) ctx->gband_min = atoi(m);
     const char* f = getenv("GSNAPDP_ENDS_ROWLANE");
     ctx->ends_rowlane = (f && f[0] == '1') ? 1 : 0;
   }

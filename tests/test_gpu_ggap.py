@@ -84,6 +84,19 @@ def test_gpu_ggap_matches_reference_golden(golden_dir, name):
     assert np.sum(z["results"]["returned_null"] == 0) > len(w) // 2 and z["pairs"].size > 1000
 
 
+@pytest.mark.parametrize("name", GOLDEN)
+def test_gpu_gband_matches_reference_golden(golden_dir, name, monkeypatch):
+    """The goldens with every qualifying score-mode window on the register band
+    (GSNAPDP_GBAND_MIN=0; by default batches under 16384 windows run on k_ggap)."""
+    monkeypatch.setenv("GSNAPDP_GBAND_MIN", "0")
+    z = load(golden_dir, name)
+    ctx = Context(z["blocks"])
+    w = z["windows"]
+    res, trc, ops, off = ctx.ggap_run(w, z["query"], z["query_uc"])
+    pairs, npairs = ctx.ggap_all_pairs(w, z["query"], z["query_uc"], res, trc, ops, off)
+    compare(w, res, trc, pairs, npairs, z["results"], z["pairs"], z["npairs"], name + " (band)")
+
+
 @pytest.mark.parametrize("seed", [11, 12, 13])
 def test_gpu_ggap_matches_oracle_mix(seed):
     """Every class (rows <= 31, <= 63, striped), both modes, odd shapes, early returns."""
@@ -139,10 +152,12 @@ def test_gpu_c4_parity(prob):
 
 
 @pytest.mark.parametrize("n", [1, 5, 17, 33])
-def test_gpu_ggap_ragged_batches_with_shadow_groups(n):
+def test_gpu_ggap_ragged_batches_with_shadow_groups(n, monkeypatch):
     """Batches that leave window groups of a register-band wave empty: the
     shadow groups replay the task's first window (here at query offset 0)
-    without touching memory outside the batch."""
+    without touching memory outside the batch (GSNAPDP_GBAND_MIN=0: batches
+    this small run on the register band too)."""
+    monkeypatch.setenv("GSNAPDP_GBAND_MIN", "0")
     g, b = W.c4_windows(W.synthetic_genome(2_000_000, seed=9), 64, seed=9, use_probabilities=False)
     w = b.windows[:n].copy()
     assert w["qpos"][0] == 0
@@ -186,6 +201,7 @@ def test_gpu_gband_probability_mode_matches_reference_golden(golden_dir, name, m
     the fills' cell values and the bridge sweeps of gsnapdp_gband.hip) against
     the reference's goldens."""
     monkeypatch.setenv("GSNAPDP_GBAND_PROB", "1")
+    monkeypatch.setenv("GSNAPDP_GBAND_MIN", "0")
     z = load(golden_dir, name)
     ctx = Context(z["blocks"])
     w = z["windows"]
@@ -199,6 +215,7 @@ def test_gpu_gband_probability_mode_matches_oracle(jl, monkeypatch):
     """C4-shape probability-mode windows on the register band, jump-late mixed,
     a third with extraband 10 (the S = 8 classes), against the oracle."""
     monkeypatch.setenv("GSNAPDP_GBAND_PROB", "1")
+    monkeypatch.setenv("GSNAPDP_GBAND_MIN", "0")
     rng = np.random.default_rng(78)
     g, b = W.c4_windows(W.synthetic_genome(8_000_000, seed=5), 20_000, seed=5, use_probabilities=True)
     w = b.windows.copy()
