@@ -713,7 +713,7 @@ void fail(Path& k, const std::string& why) {
 // GSNAPDP_S3_PROFILE=1: where a pass's host time goes (stderr at the end of the pass)
 struct Prof {
   bool on = getenv("GSNAPDP_S3_PROFILE") != nullptr;
-  std::atomic<int64_t> expand_ns[F_N] = {{0}, {0}, {0}, {0}}, resume_ns{0};
+  std::atomic<int64_t> expand_ns[F_N] = {{0}, {0}, {0}, {0}}, resume_ns{0}, driver_ns{0};
   double init = 0, pack = 0, copy = 0, submit = 0, wait = 0, resume = 0, output = 0;
 };
 Prof& prof() {
@@ -1644,7 +1644,11 @@ void finish_path(Pass& P, Path& k) {
     write_call(k, *k.c);
     const gsnapdp_s3_pair* pairs = nullptr;
     int n = 0;
-    gsnapdp_s3_call* next = P.driver->next(k.idx, k.c, list, &pairs, &n);
+    gsnapdp_s3_call* next;
+    {
+      Tic tic(prof().driver_ns);
+      next = P.driver->next(k.idx, k.c, list, &pairs, &n);
+    }
     if (!next) {
       k.stage = S_DONE;
       k.failed = false;  // reported through the call; the path is out of the pass
@@ -1963,6 +1967,7 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
   if (pf.on) {
     for (int f = 0; f < F_N; f++) pf.expand_ns[f] = 0;
     pf.resume_ns = 0;
+    pf.driver_ns = 0;
     pf.init = pf.pack = pf.copy = pf.submit = pf.wait = pf.resume = pf.output = 0;
   }
   pool.run(ncalls, 16, [&](int i) {
@@ -2016,6 +2021,13 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
     store_release(store);
     P.st.seconds[1] = wait_s;
     P.st.seconds[2] = std::chrono::duration<double>(clock::now() - t_start).count();
+    if (pf.on)
+      fprintf(stderr,
+              "gsnapdp_stage3_pass profile (driven): %d paths, %d rounds, total %.4f s: init %.4f, pack %.4f, "
+              "copy %.4f, submit %.4f, wait %.4f, resume %.4f (thread-s: resume %.4f, of which the driver's host "
+              "steps %.4f; expand gap %.4f ggap %.4f)\n",
+              ncalls, P.st.rounds, P.st.seconds[2], pf.init, pf.pack, pf.copy, pf.submit, wait_s, pf.resume,
+              pf.resume_ns * 1e-9, pf.driver_ns * 1e-9, pf.expand_ns[0] * 1e-9, pf.expand_ns[1] * 1e-9);
     P.st.seconds[0] = P.st.seconds[2] - wait_s;
     if (stats) *stats = P.st;
     return 0;

@@ -487,25 +487,34 @@ List viterbi_filter(const List& pairs, bool goodness, double defect) {
   if (goodness && defect == 0.0) defect = 0.001;
   const size_t n = pairs.size();
   std::vector<uint8_t> vgood(n), vbad(n);  // the previous state each state came from (1 GOOD)
-  double pg = 0.0, pb = 0.0;
-  for (size_t i = 0; i < n; i++) {
-    const gsnapdp_s3_pair& p = pairs[i];
+  // A pair's emissions take one of two values (match / mismatch, or indel / not),
+  // so its four log sums are tabulated once per call: the same operands in the
+  // same order as per pair, so the same doubles.
+  double GG[2], BG[2], GBd[2], BBd[2];
+  for (int m = 0; m < 2; m++) {  // m = 1: a match (goodness) or an indel
     double eg, eb, tgg, tbg, tgb, tbb;
     if (goodness) {
-      const bool match = p.comp == '|' || p.comp == '*' || p.comp == ':';
-      eg = match ? 1.0 - defect : defect;
-      eb = match ? 0.25 : 0.75;
+      eg = m ? 1.0 - defect : defect;
+      eb = m ? 0.25 : 0.75;
       tgg = 0.99, tbg = 0.10, tgb = 0.01, tbb = 0.90;
     } else {
-      const bool indel = p.comp == '-';
-      eg = indel ? 0.0001 : 0.9999;
+      eg = m ? 0.0001 : 0.9999;
       eb = 0.5;
       tgg = 0.9999, tbg = 0.25, tgb = 0.0001, tbb = 0.75;
     }
-    double gi = log(eg) + log(tgg), bi = log(eg) + log(tbg), vg, vb;
+    GG[m] = log(eg) + log(tgg);
+    BG[m] = log(eg) + log(tbg);
+    GBd[m] = log(eb) + log(tgb);
+    BBd[m] = log(eb) + log(tbb);
+  }
+  double pg = 0.0, pb = 0.0;
+  for (size_t i = 0; i < n; i++) {
+    const gsnapdp_s3_pair& p = pairs[i];
+    const int m = goodness ? (p.comp == '|' || p.comp == '*' || p.comp == ':') : (p.comp == '-');
+    double gi = GG[m], bi = BG[m], vg, vb;
     if (pg + gi > pb + bi) vg = pg + gi, vgood[i] = 1;
     else vg = pb + bi, vgood[i] = 0;
-    gi = log(eb) + log(tgb), bi = log(eb) + log(tbb);
+    gi = GBd[m], bi = BBd[m];
     if (pg + gi > pb + bi) vb = pg + gi, vbad[i] = 1;
     else vb = pb + bi, vbad[i] = 0;
     pg = vg, pb = vb;
@@ -707,7 +716,7 @@ class Pipeline final : public gsnapdp::S3Driver {
       fail(q, "a DP pass failed on the path (status -1)");
       return nullptr;
     }
-    q.list.assign(list.begin(), list.end());
+    q.list.swap(list);  // (the pass's buffer takes the old list's storage for its next use)
     q.minor = k->out_minor;
     q.major = k->out_major;
     q.ub |= k->ub;
