@@ -1639,7 +1639,25 @@ void finish_path(Pass& P, Path& k) {
     list.clear();
     if (!k.failed) {
       if (k.c->pass == GSNAPDP_S3_END3) k.pairs = k.path;  // build_path_end3 returns its path
-      for (int p = k.pairs; p >= 0; p = k.A.rest(p)) list.push_back(k.A.out(p));
+      const Arena& A = k.A;
+      const bool dis = !A.dis.empty();
+      for (int p = k.pairs; p >= 0;) {
+        if (p < A.nin) {  // a run of input cells p, p - 1, .., q: a reversed block copy (A.out of each)
+          const int q = A.run_end(p);
+          const size_t at = list.size();
+          list.resize(at + (size_t)(p - q + 1));
+          gsnapdp_s3_pair* o = list.data() + at;
+          for (int x = p; x >= q; x--, o++) {
+            *o = A.in[x];
+            o->src = x;
+            if (dis && A.dis[(size_t)x]) o->flags |= GSNAPDP_S3_DISALLOWED;
+          }
+          p = A.rest(q);
+        } else {
+          list.push_back(A.out(p));
+          p = A.rest(p);
+        }
+      }
     }
     write_call(k, *k.c);
     const gsnapdp_s3_pair* pairs = nullptr;

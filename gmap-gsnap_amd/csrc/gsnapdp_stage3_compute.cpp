@@ -65,25 +65,24 @@ gsnapdp_s3_pair gapholder(int queryjump, int genomejump) {
 // insert_gapholders (stage3.c:817-925): pairs -> path (the reversed list, with
 // the unknown gaps dropped and one gapholder per jump; the first and the last
 // gapholder made are end introns)
-List insert_gapholders(const List& pairs) {
-  List kept;
-  kept.reserve(pairs.size());
-  for (const gsnapdp_s3_pair& p : pairs)
-    if (knowngapp(p) || !gapp(p)) kept.push_back(p);
+List insert_gapholders(const List& pairs, bool reversed = true) {
   List st;  // the path as a stack: back() is its head
-  st.reserve(kept.size() + kept.size() / 8 + 4);
-  if (kept.empty()) return st;
-  st.push_back(kept[0]);
-  gsnapdp_s3_pair left = kept[0];
+  st.reserve(pairs.size() + pairs.size() / 8 + 4);
+  const gsnapdp_s3_pair* left = nullptr;  // the last pair kept
   int gappair = -1;  // the last gapholder made (its index in st)
   bool firstp = true;
-  for (size_t i = 1; i < kept.size(); i++) {
-    const gsnapdp_s3_pair& pair = kept[i];
-    int queryjump = pair.querypos - left.querypos - 1;
-    int genomejump = (int)((uint32_t)pair.genomepos - (uint32_t)left.genomepos - 1u);  // Genomicpos_T
-    if (left.cdna == ' ') queryjump++;
-    if (left.genome == ' ') genomejump++;
-    if (knowngapp(pair) || knowngapp(left) || (queryjump <= 0 && genomejump <= 0)) {
+  for (const gsnapdp_s3_pair& pair : pairs) {
+    if (!(knowngapp(pair) || !gapp(pair))) continue;  // old gapholders are dropped
+    if (!left) {
+      st.push_back(pair);
+      left = &pair;
+      continue;
+    }
+    int queryjump = pair.querypos - left->querypos - 1;
+    int genomejump = (int)((uint32_t)pair.genomepos - (uint32_t)left->genomepos - 1u);  // Genomicpos_T
+    if (left->cdna == ' ') queryjump++;
+    if (left->genome == ' ') genomejump++;
+    if (knowngapp(pair) || knowngapp(*left) || (queryjump <= 0 && genomejump <= 0)) {
       st.push_back(pair);
     } else {
       st.push_back(gapholder(queryjump, genomejump));
@@ -94,10 +93,10 @@ List insert_gapholders(const List& pairs) {
       }
       st.push_back(pair);
     }
-    left = pair;
+    left = &pair;
   }
   if (gappair >= 0) st[(size_t)gappair].flags |= GSNAPDP_S3_END_INTRON;
-  reverse(st);
+  if (reversed) reverse(st);  // (reversed false: the caller's List_reverse of the result, done)
   return st;
 }
 
@@ -619,8 +618,8 @@ void advance(Query& q, int min_intronlength) {
       q.iter2++;
       break;
     case Q_5: {
-      List path = insert_gapholders(pairs);  // the path that ends iteration 0 (:8848)
-      reverse(path);                         // pass 6: pairs = List_reverse(path)
+      List path = insert_gapholders(pairs, false);  // the path that ends iteration 0 (:8848), and pass 6's
+                                                    // pairs = List_reverse(path)
       if (q.c->finalp) {
         q.list = insert_gapholders(path);
         q.step = Q_6;
@@ -648,8 +647,7 @@ void advance(Query& q, int min_intronlength) {
     }
     if (!(q.shortp && q.iter1 < MAXITER_SMOOTH_BY_SIZE)) break;
     {  // 3a: smoothing by size
-      List path = insert_gapholders(pairs);
-      reverse(path);
+      List path = insert_gapholders(pairs, false);  // List_reverse(insert_gapholders(..))
       pairs = smooth_by_size(&q.shortp, &q.deletep, std::move(path));
     }
     if (q.shortp || q.deletep) {  // 3b: dual introns
