@@ -1641,16 +1641,15 @@ void finish_path(Pass& P, Path& k) {
       if (k.c->pass == GSNAPDP_S3_END3) k.pairs = k.path;  // build_path_end3 returns its path
       const Arena& A = k.A;
       const bool dis = !A.dis.empty();
+      list.reserve((size_t)A.nin + A.extra.size());  // every cell at most once
       for (int p = k.pairs; p >= 0;) {
         if (p < A.nin) {  // a run of input cells p, p - 1, .., q: a reversed block copy (A.out of each)
           const int q = A.run_end(p);
-          const size_t at = list.size();
-          list.resize(at + (size_t)(p - q + 1));
-          gsnapdp_s3_pair* o = list.data() + at;
-          for (int x = p; x >= q; x--, o++) {
-            *o = A.in[x];
-            o->src = x;
-            if (dis && A.dis[(size_t)x]) o->flags |= GSNAPDP_S3_DISALLOWED;
+          for (int x = p; x >= q; x--) {
+            list.push_back(A.in[x]);
+            gsnapdp_s3_pair& o = list.back();
+            o.src = x;
+            if (dis && A.dis[(size_t)x]) o.flags |= GSNAPDP_S3_DISALLOWED;
           }
           p = A.rest(q);
         } else {
