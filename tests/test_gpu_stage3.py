@@ -288,3 +288,41 @@ def test_dropin_build_pairs_introns_matches_reference(golden_dir, tmp_path, name
     if iit is not None:  # back to no IIT for the other tests of this process
         L.Dynprog_setup(1, None, None, -1, -1, None, None, None, 0, None, None, None, None, None)
     L.Dynprog_term()  # releases the device context (the genome array dies with this test)
+
+
+def test_gpu_stage3_concurrent_passes_on_one_context(golden_dir, tmp_path):
+    """Three host threads running whole passes (and a 2A-6 pipeline) on ONE
+    context at once: each pass takes its own executor (staging, launcher
+    thread) from the context's pool, the rounds of all passes share the context
+    stream in submission order, and every result equals the serial run's."""
+    import threading
+    z = np.load(os.path.join(golden_dir, "gmap_synth_stage3.npz"), allow_pickle=False)
+    calls, pin, q, qu, want = stage3_golden(z)
+    Q, PI, QQ, QU, WANT, FINAL, counts = W.stage3_pipeline(z)
+    ctx = Context(z["blocks"])
+    s2 = stage2_double(ctx, z, tmp_path)
+    c0, g0, _ = ctx.stage3_pass(calls, pin, q, qu)
+    check_pass(c0, g0, calls, want, "serial", z["ub_ref"] if "ub_ref" in z else None)
+    k0, l0, _ = ctx.stage3_compute(Q, PI, QQ, QU)
+    out, errs = {}, []
+
+    def worker(t):
+        try:
+            for r in range(3):
+                if t == 2:
+                    k, l, _ = ctx.stage3_compute(Q, PI, QQ, QU)
+                    out[(t, r)] = (k.tobytes() == k0.tobytes(), l.tobytes() == l0.tobytes())
+                else:
+                    c, g, _ = ctx.stage3_pass(calls, pin, q, qu)
+                    out[(t, r)] = (c.tobytes() == c0.tobytes(), g.tobytes() == g0.tobytes())
+        except Exception as e:  # reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(3)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not errs, errs
+    assert len(out) == 9 and all(a and b for a, b in out.values()), out
+    ctx.close()
