@@ -9,3 +9,4 @@ cp $O/trace/run_domain_stats.csv profiles/${TAG}_c3_domain_stats.csv 2>/dev/null
 cp $O/traffic.json profiles/${TAG}_traffic.json
 cp $O/bench.json profiles/${TAG}_bench.json
 cp $O/pytest_gpu.txt profiles/${TAG}_pytest_gpu.txt
+cp $O/pmc_ggap_modes.json profiles/${TAG}_pmc_ggap_modes.json 2>/dev/null || true

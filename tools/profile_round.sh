@@ -17,3 +17,6 @@ B="--steps 3 --warmup 1 --no-cpu --no-side --no-steady"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 bench.py $B > /dev/null 2> $O/pmc1.err
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 bench.py $B > /dev/null 2> $O/pmc2.err
 python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write k_fill $O/traffic.json C3
+# genome-gap kernels per mode (k_gband score / probability, k_ggap probability): SQ counters and rocprof summaries
+bash tools/pmc_ggap_modes.sh $TAG/ggap_modes
+python3 tools/pmc_summary.py $O/ggap_modes/*_pmc1 $O/ggap_modes/*_pmc2 > $O/pmc_ggap_modes.json
