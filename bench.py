@@ -359,7 +359,7 @@ def stage2_double(ctx, z):
     ctx.set_stage2(ctypes.cast(d.s2dbl_compute_one, ctypes.c_void_p).value, h)
 
 
-def measure_stage3(paths=7424, reps=3):
+def measure_stage3(paths=7424, reps=6):
     """Side line: the stage-3 passes (gsnapdp_stage3_pass: path_compute's
     build_pairs_introns, build_pairs_singles, build_pairs_end5 / build_path_end3
     and build_pairs_dualintrons, mixed in one pass) on the recorded calls of the
@@ -458,7 +458,7 @@ def stage3_cpu_baseline(blocks, calls, pin, q, qu, want=None, compact=False, z=N
     return out if not compact else (out, res)
 
 
-def measure_stage3_compute(copies=8, reps=3, cpu=True):
+def measure_stage3_compute(copies=8, reps=5, cpu=True):
     """Side line: passes 2A-6 of path_compute (gsnapdp_stage3_compute: the host
     steps restated, every round of DP passes one gsnapdp_stage3_pass across the
     queries) for every path_compute call the reference's gmap made on the
