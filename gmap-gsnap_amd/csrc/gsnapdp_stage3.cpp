@@ -1893,7 +1893,8 @@ void unpack_resume(Pass& P, gsnapdp::S3Exec& X, Cohort& C) {
   const char* out = X.out_buf(C.slot, 0);
   int base[F_N + 1] = {0};
   for (int f = 0; f < F_N; f++) base[f + 1] = base[f] + L.n[f];
-  Workers::get().run((int)C.all.size(), 16, [&](int j) {
+  // small grains when driven: a path's resume can then run a whole host step of its query
+  Workers::get().run((int)C.all.size(), P.driver ? 4 : 16, [&](int j) {
     Path& k = *C.all[(size_t)j];
     Req& R = k.req;
     const int f = R.fam, i = j - base[f];
