@@ -298,19 +298,20 @@ struct Pass {
   gsnapdp::S3Driver* driver = nullptr;  // driven passes: a path's next pass when one ends
 };
 
+}  // namespace
+
 // ---- genome characters (stage3.c get_genomic_nt, with no genomic segment)
-char genomic_nt(const Pass& P, const Path& k, int gpos) {
-  const gsnapdp_s3_call& c = *k.c;
+char gsnapdp::s3_genomic_nt(const uint32_t* blocks, size_t nwords, const gsnapdp_s3_call& c, int gpos) {
   if (gpos < 0 || gpos >= c.genomiclength) return '*';
   const uint32_t base = c.chroffset + c.chrpos;
   if (base < c.chroffset || base >= c.chrhigh) return '*';
   const uint32_t pos = c.watsonp ? base + (uint32_t)gpos : base + (uint32_t)(c.genomiclength - 1) - (uint32_t)gpos;
   const size_t ptr = (size_t)(pos >> 5) * 3;
-  if (ptr + 2 >= P.nwords) return 'N';
+  if (ptr + 2 >= nwords) return 'N';
   const uint32_t bit = pos & 31u;
   char ch = 'N';
-  if (!((P.blocks[ptr + 2] >> bit) & 1u))
-    ch = "ACGT"[((bit < 16 ? P.blocks[ptr + 1] : P.blocks[ptr]) >> ((bit & 15u) * 2u)) & 3u];
+  if (!((blocks[ptr + 2] >> bit) & 1u))
+    ch = "ACGT"[((bit < 16 ? blocks[ptr + 1] : blocks[ptr]) >> ((bit & 15u) * 2u)) & 3u];
   if (c.watsonp) return ch;
   switch (ch) {  // complCode
     case 'A': return 'T';
@@ -319,6 +320,12 @@ char genomic_nt(const Pass& P, const Path& k, int gpos) {
     case 'T': return 'A';
     default: return 'N';
   }
+}
+
+namespace {
+
+char genomic_nt(const Pass& P, const Path& k, int gpos) {
+  return gsnapdp::s3_genomic_nt(P.blocks, P.nwords, *k.c, gpos);
 }
 int nt_class(char ch) {
   switch (ch) {

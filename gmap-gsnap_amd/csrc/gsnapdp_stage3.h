@@ -80,6 +80,10 @@ int s3_run_driven(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gs
                   int64_t npairs_in, const char* query, const char* query_uc, size_t query_bytes,
                   const gsnapdp_iit* iit, S3Driver* driver, gsnapdp_s3_stats* stats);
 
+// get_genomic_nt (stage3.c) on the packed genome, with no genomic segment: the
+// character at position gpos of the call's genomic stretch, '*' outside it
+char s3_genomic_nt(const uint32_t* blocks, size_t nwords, const gsnapdp_s3_call& c, int gpos);
+
 // the context's stage-2 callback for traverse_dual_break (gsnapdp_stage3_set_stage2)
 gsnapdp_s3_stage2 s3_stage2(gsnapdp_ctx* ctx);
 void s3_set_stage2(gsnapdp_ctx* ctx, const gsnapdp_s3_stage2& s2);

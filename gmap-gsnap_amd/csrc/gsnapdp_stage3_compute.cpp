@@ -1,12 +1,16 @@
-// gsnapdp_stage3_compute.cpp -- passes 2A to 6 of path_compute (stage3.c:8639-8876)
-// for many queries at once.
+// gsnapdp_stage3_compute.cpp -- path_compute (stage3.c:8586-9220) from pass 2A
+// for many queries at once: passes 2A-6 (gsnapdp_stage3_compute) and 2A-10
+// (gsnapdp_stage3_path_compute).
 //
 // Every query runs the reference's sequence: build_pairs_singles (2A), the
 // adjacent-indel fix, build_pairs_singles again (2C), the defect rate,
 // Smooth_pairs_by_size with build_pairs_dualintrons and the build_pairs_introns
 // iterations (3a-3c), the end chop by changepoint, the two HMM filters (4),
 // remove_indel_gaps and build_dual_breaks (5), and the final build_pairs_introns
-// (6).  The host steps between the DP passes are restated here on each query's
+// (6); then the dual breaks at the ends (7), the adjacent indels (7b, 7C), the
+// end extensions (8), assign_gap_types and the BEST_LOCAL extensions (9) and
+// the noncanonical end-exon trims (10).  The host steps between the DP passes
+// are restated here on each query's
 // list (a vector of gsnapdp_s3_pair in list order); the DP passes of all the
 // queries that have reached one run as ONE gsnapdp_stage3_pass, whatever pass
 // each query is at, so the GPU sees every query's windows of a round together.
@@ -22,8 +26,11 @@
 #include <vector>
 
 #include "../../include/gsnapdp.h"
+#include "gsnapdp_internal.h"
 #include "gsnapdp_stage3.h"
 
+extern "C" const uint32_t* gsnapdp__host_blocks(gsnapdp_ctx* ctx);
+extern "C" size_t gsnapdp__host_nwords(gsnapdp_ctx* ctx);
 void gsnapdp__set_err(const std::string& s);  // gsnapdp_kernels.hip
 
 namespace {
@@ -561,6 +568,188 @@ List remove_indel_gaps(const List& path, int min_intronlength) {
   return st;
 }
 
+// ---- passes 7-10 (stage3.c:8885-9212)
+
+// A pair's donor_prob / acceptor_prob: assign_gap_types writes them on the
+// intron gaps (stage3.c:1131-1244); every other pair keeps what
+// Pairpool_push / Pairpool_push_gapholder gave it (pairpool.c:213-214,
+// 385-391: 2.0 for a known gap, else 0.0).  The pipeline's lists carry a
+// pair's row in the query's table in `src` (-1: none).
+struct Probs {
+  double d = 0.0, a = 0.0;
+};
+
+bool match_comp(char c) { return c == '|' || c == '*' || c == ':'; }  // MATCH, DYNPROG_MATCH, AMBIGUOUS
+
+// dualbreak_p (stage3.c:2586-2598)
+bool dualbreak_p(const List& l) {
+  for (const gsnapdp_s3_pair& p : l)
+    if (gapp(p) && p.queryjump > 0 && p.genomejump > 0) return true;
+  return false;
+}
+// dualbreak_distance_from_end (:2601-2640): the pairs up to and including the
+// first dual break, and its query jump weighed against the matches before it
+int dualbreak_distance(int* npairs, int* totaljump, const List& l) {
+  *totaljump = 0;
+  if (l.empty()) return 0;
+  int nmatches = 0, nmismatches = 0;
+  size_t i = 0;
+  const gsnapdp_s3_pair* pair = &l[0];
+  *npairs = 0;
+  while (i < l.size() && (!gapp(*pair) || pair->queryjump == 0 || pair->genomejump == 0)) {
+    if (gapp(*pair)) {
+    } else if (pair->comp == ' ' || pair->comp == '-') {
+      nmismatches++;
+    } else {
+      nmatches++;
+    }
+    if (++i < l.size()) pair = &l[i];
+    (*npairs)++;
+  }
+  if (gapp(*pair) && pair->queryjump > 0 && pair->genomejump > 0) {
+    (*npairs)++;
+    *totaljump = 10 * pair->queryjump;  // DUALBREAK_QUERYJUMP_FACTOR
+  }
+  return nmatches - nmismatches;
+}
+List reversed(const List& l) { return List(l.rbegin(), l.rend()); }
+
+// pass 7 (:8885-8925): remove the dual breaks nearer an end than their query
+// jump is worth.  pairs (pass 6's) -> pairs.
+bool remove_end_dual_breaks(const List& pairs6, List* out, std::string* err) {
+  List path = insert_gapholders(pairs6);
+  List pairs;
+  if (path.empty()) {
+    if (!pairs6.empty())  // every pair an unknown gap: the reference keeps a list insert_gapholders re-linked
+      return *err = "pass 7: a path of gaps only (the reference returns a stale list)", false;
+    out->clear();
+    return true;
+  }
+  for (;;) {
+    if (path.empty()) break;  // (pairs as the last trim left it)
+    if (!dualbreak_p(path)) {
+      pairs = reversed(path);
+      break;
+    }
+    int n3 = 0, t3, n5 = 0, t5;
+    const int d3 = dualbreak_distance(&n3, &t3, path);
+    pairs = reversed(path);
+    const int d5 = dualbreak_distance(&n5, &t5, pairs);
+    bool trim5;
+    if (t5 < d5 && t3 < d3) break;  // keep the dual breaks
+    if (t5 > d5 && t3 > d3) trim5 = d5 < d3;
+    else trim5 = t5 > d5;
+    if (trim5) {  // trim_npairs(pairs, npairs5)
+      pairs.erase(pairs.begin(), pairs.begin() + n5);
+      path = reversed(pairs);
+    } else {  // path = List_reverse(pairs); trim_npairs(path, npairs3)
+      const gsnapdp_s3_pair head = pairs[0];
+      path = reversed(pairs);
+      path.erase(path.begin(), path.begin() + n3);
+      // the reversal left pairs' old head cell last in path, its rest NULL:
+      // if the trim took all of path, `pairs` is that one cell
+      if (path.empty()) pairs.assign(1, head);
+    }
+  }
+  *out = std::move(pairs);
+  return true;
+}
+
+// remove_adjacent_ins_del (:1889-1971): an insertion run directly followed by
+// a deletion run (or the reverse) is dropped, both sides.  pairs -> pairs (the
+// reference's path, List_reverse'd by path_compute).
+bool remove_adjacent_ins_del(bool* foundp, const List& pairs, List* out, std::string* err) {
+  auto indel = [](const gsnapdp_s3_pair& p) { return p.comp == '-' || p.comp == '~'; };  // INDEL, SHORTGAP
+  enum { NORMAL = 0, INSERTION = 1, DELETION = -1 };
+  List st;  // path as a stack
+  st.reserve(pairs.size());
+  int state = NORMAL;
+  *foundp = false;
+  size_t i = 0;
+  while (i < pairs.size()) {
+    const gsnapdp_s3_pair& t = pairs[i++];
+    if (!indel(t)) {
+      st.push_back(t);
+      state = NORMAL;
+    } else if (t.genome == ' ') {
+      if (state != DELETION) {
+        st.push_back(t);
+        state = INSERTION;
+      } else {
+        while (!st.empty() && indel(st.back()) && st.back().cdna == ' ') st.pop_back();
+        while (i < pairs.size() && indel(pairs[i]) && pairs[i].genome == ' ') i++;
+        *foundp = true;
+        state = NORMAL;
+      }
+    } else if (t.cdna == ' ') {
+      if (state != INSERTION) {
+        st.push_back(t);
+        state = DELETION;
+      } else {
+        while (!st.empty() && indel(st.back()) && st.back().genome == ' ') st.pop_back();
+        while (i < pairs.size() && indel(pairs[i]) && pairs[i].cdna == ' ') i++;
+        *foundp = true;
+        state = NORMAL;
+      }
+    } else {
+      return *err = "remove_adjacent_ins_del: an indel with neither side blank (the reference aborts)", false;
+    }
+  }
+  *out = std::move(st);  // List_reverse(path): the stack bottom first
+  return true;
+}
+
+// clean_pairs_end5_gap_indels / clean_path_end3_gap_indels (:2056-2126): pop
+// gaps and indels off the list's head
+void clean_end_gap_indels(List& l) {
+  size_t n = 0;
+  while (n < l.size() && (gapp(l[n]) || l[n].comp == '-')) n++;
+  l.erase(l.begin(), l.begin() + (ptrdiff_t)n);
+}
+
+// enough_matches (:2655-2692), canonicalp (:2695-2720), sufficient_splice_prob_local (:2724-2744)
+bool enough_matches(int matches, int genomejump) {
+  if (genomejump > 100000) return matches >= 10;
+  if (genomejump > 32000) return matches >= 9;
+  if (genomejump > 8000) return matches >= 8;
+  if (genomejump > 2000) return matches >= 7;
+  return matches >= 6;
+}
+bool canonicalp(bool known, char comp, int cdna_direction) {
+  const bool fwd = comp == '>' || comp == ')' || comp == ']';
+  const bool rev = comp == '<' || comp == '(' || comp == '[';
+  if (known) return true;
+  if (cdna_direction > 0) return fwd;
+  if (cdna_direction < 0) return rev;
+  return fwd || rev;
+}
+bool sufficient_splice_prob_local(int support, int nmismatches, double distal) {
+  support -= 2 * nmismatches;
+  if (support < 0) return false;
+  if (support < 7) return distal > 0.95;
+  if (support < 11) return distal > 0.90;
+  if (support < 15) return distal > 0.85;
+  if (support < 19) return distal > 0.50;
+  return true;
+}
+
+// the options and tables the host steps of passes 7-10 read
+struct Env {
+  gsnapdp_s3_path_opts o;
+  const uint32_t* blocks = nullptr;
+  size_t nwords = 0;
+  const gsnapdp_iit* iit = nullptr;
+  const char* query = nullptr;
+  bool full = false;  // passes 7-10 too (gsnapdp_stage3_path_compute)
+};
+
+// one site probability assign_gap_types needs
+struct Site {
+  int row, acceptor;  // the query's table row, donor (0) or acceptor (1)
+  uint8_t model;
+  uint32_t pos, chroffset;
+};
+
 // ---- one query through the passes
 enum Step {
   Q_2A,       // waiting for build_pairs_singles (2A)
@@ -569,6 +758,15 @@ enum Step {
   Q_3C,       // build_pairs_introns, not final
   Q_5,        // build_dual_breaks
   Q_6,        // build_pairs_introns, final
+  Q_7C,       // build_pairs_singles (7C)
+  Q_8_5,      // build_pairs_end5, QUERYEND_GAP (8)
+  Q_8_3,      // build_path_end3, QUERYEND_GAP (8)
+  Q_GT_9,     // parked: assign_gap_types before 9a, its MaxEnt sites pending
+  Q_9A,       // build_pairs_end5, BEST_LOCAL, maxpeelback 0 (9a)
+  Q_9B,       // build_path_end3 (9b)
+  Q_GT_10,    // parked: assign_gap_types before pass 10
+  Q_10_5,     // build_pairs_end5, QUERYEND_NOGAPS (10)
+  Q_10_3,     // build_path_end3, QUERYEND_NOGAPS (10)
   Q_DONE
 };
 struct Query {
@@ -583,17 +781,208 @@ struct Query {
   int minor = 0, major = 0, nintrons = 0, nnonintrons = 0, intronlen = 0, nonintronlen = 0;
   int ub = 0;
   int passes[6] = {0, 0, 0, 0, 0, 0};
-  gsnapdp_s3_call k;  // the pending pass's call (its pairs are list)
+  gsnapdp_s3_call k;        // the pending pass's call (its pairs are list)
+  std::vector<int> insrc;   // the pending pass's input pairs' src (the pass renumbers them)
+  std::vector<Probs> probs; // assign_gap_types' rows
+  std::vector<Site> sites;  // parked: the rows' MaxEnt sites
+  int iter10 = 0;           // pass 10's iterations
+  bool trim5p = true, trim3p = true;
 };
 void fail(Query& q, const std::string& why) {
   if (!q.failed) q.why = why;
   q.failed = true;
   q.step = Q_DONE;
 }
+Probs probs_of(const Query& q, const gsnapdp_s3_pair& p) {
+  if (p.src >= 0) return q.probs[(size_t)p.src];
+  Probs r;
+  if (gapp(p) && knowngapp(p)) r.d = r.a = 2.0;
+  return r;
+}
 
-// the loops of path_compute between DP passes (:8711-8876), from the list the
-// last pass returned (q.list) to the next pass's input, or to the end
-void advance(Query& q, int min_intronlength) {
+// Pairpool_push (pairpool.c:169-230) of a pair assign_gap_types makes
+gsnapdp_s3_pair new_pair(int querypos, int genomepos, char cdna, char comp, char genome) {
+  gsnapdp_s3_pair p;
+  memset(&p, 0, sizeof(p));
+  p.querypos = querypos;
+  p.genomepos = genomepos;
+  p.cdna = cdna;
+  p.comp = comp;
+  p.genome = genome;
+  p.src = -1;
+  return p;
+}
+
+// assign_gap_types (stage3.c:1015-1260) with no genomic segment: path -> pairs.
+// The intron gaps get their type and a table row whose MaxEnt probabilities
+// are queued in q.sites (1.0 at once for a site the splicing IIT knows).
+bool assign_gap_types(Query& q, const Env& E, const List& path, List* out, std::string* err) {
+  const gsnapdp_s3_call& c = *q.c;
+  auto nt = [&](int gpos) { return gsnapdp::s3_genomic_nt(E.blocks, E.nwords, c, gpos); };
+  auto cls = [](char ch) { return ch == 'A' ? 0 : ch == 'C' ? 1 : ch == 'G' ? 2 : ch == 'T' ? 3 : 4; };
+  List st;  // pairs as a stack
+  st.reserve(path.size() + 16);
+  for (size_t i = 0; i < path.size(); i++) {
+    gsnapdp_s3_pair pair = path[i];
+    if (!gapp(pair)) {
+      st.push_back(pair);
+      continue;
+    }
+    if (st.empty() || i + 1 == path.size()) continue;  // the initial / terminal gap is discarded
+    const int queryjump = pair.queryjump, genomejump = pair.genomejump;
+    if (queryjump == 0 && genomejump == 0) continue;
+    const gsnapdp_s3_pair& left = path[i + 1];  // path->first
+    const gsnapdp_s3_pair right = st.back();    // pairs->first
+    int leftquerypos = left.querypos, leftgenomepos = left.genomepos;
+    if (left.cdna == ' ') leftquerypos--;
+    if (genomejump == 0) {  // a cDNA insertion: its query bytes as indel pairs
+      for (int cur = right.querypos - 1; cur > leftquerypos; --cur) {
+        if (cur < 0 || cur >= c.querylength) return *err = "assign_gap_types: an insertion outside the query", false;
+        st.push_back(new_pair(cur, right.genomepos, E.query[(size_t)c.qpos + (size_t)cur], '-', ' '));
+      }
+      continue;
+    }
+    if (queryjump > 0) {  // a dual break
+      pair.comp = '#';
+      st.push_back(pair);
+      continue;
+    }
+    if (left.genome == ' ') leftgenomepos--;
+    const int rightquerypos = right.querypos, rightgenomepos = right.genomepos;
+    const int introntype = gsnapdp::intron_type_codes(cls(nt(leftgenomepos + 1)), cls(nt(leftgenomepos + 2)),
+                                                      cls(nt(rightgenomepos - 2)), cls(nt(rightgenomepos - 1)),
+                                                      c.cdna_direction);
+    const int intronlength = rightgenomepos - leftgenomepos - 1;
+    if (intronlength < E.o.min_intronlength) {  // too short for an intron: the genome as gap pairs
+      for (int gpos = rightgenomepos - 1; gpos > leftgenomepos; --gpos)
+        st.push_back(new_pair(rightquerypos, gpos, ' ', '~', nt(gpos)));
+      continue;
+    }
+    const bool fwd = c.cdna_direction >= 0;
+    switch (introntype) {
+      case 0x20: pair.comp = fwd ? '>' : 0; break;  // GTAG_FWD
+      case 0x10: pair.comp = fwd ? ')' : 0; break;  // GCAG_FWD
+      case 0x08: pair.comp = fwd ? ']' : 0; break;  // ATAC_FWD
+      case 0x01: pair.comp = fwd ? 0 : '['; break;  // ATAC_REV
+      case 0x02: pair.comp = fwd ? 0 : '('; break;  // GCAG_REV
+      case 0x04: pair.comp = fwd ? 0 : '<'; break;  // GTAG_REV
+      default: pair.comp = '='; break;              // NONINTRON
+    }
+    if (!pair.comp) return *err = "assign_gap_types: unexpected intron type (the reference exits)", false;
+    // the site probabilities (:1135-1244): donor at the left for fwd, at the right for rev
+    const uint32_t gl1 = (uint32_t)c.genomiclength - 1U;
+    const uint32_t lpos = c.watsonp ? c.chrpos + (uint32_t)leftgenomepos + 1U : c.chrpos + gl1 - (uint32_t)leftgenomepos;
+    const uint32_t rpos = c.watsonp ? c.chrpos + (uint32_t)rightgenomepos
+                                    : c.chrpos + gl1 - (uint32_t)rightgenomepos + 1U;
+    gsnapdp_intron kn;
+    memset(&kn, 0, sizeof(kn));
+    kn.left_genomepos = (uint32_t)leftgenomepos;
+    kn.right_genomepos = (uint32_t)rightgenomepos;
+    if (E.iit && (c.cdna_direction == 1 || c.cdna_direction == -1) &&
+        gsnapdp_introns_known(E.iit, c.chrnum, c.chrpos, c.genomiclength, c.cdna_direction, c.watsonp, &kn, 1))
+      return *err = "assign_gap_types: the splicing IIT query failed", false;
+    const int row = (int)q.probs.size();
+    q.probs.emplace_back();
+    pair.src = row;
+    uint8_t dmodel, amodel;
+    uint32_t dpos, apos;
+    if (fwd) {
+      dmodel = c.watsonp ? GSNAPDP_DONOR : GSNAPDP_ANTIDONOR, dpos = lpos;
+      amodel = c.watsonp ? GSNAPDP_ACCEPTOR : GSNAPDP_ANTIACCEPTOR, apos = rpos;
+    } else {
+      amodel = c.watsonp ? GSNAPDP_ANTIACCEPTOR : GSNAPDP_ACCEPTOR, apos = lpos;
+      dmodel = c.watsonp ? GSNAPDP_ANTIDONOR : GSNAPDP_DONOR, dpos = rpos;
+    }
+    if (kn.known_donor) q.probs.back().d = 1.0;
+    else q.sites.push_back(Site{row, 0, dmodel, c.chroffset + dpos, c.chroffset});
+    if (kn.known_acceptor) q.probs.back().a = 1.0;
+    else q.sites.push_back(Site{row, 1, amodel, c.chroffset + apos, c.chroffset});
+    st.push_back(pair);
+  }
+  *out = reversed(st);
+  return true;
+}
+
+// trim_noncanonical_end5_exons (:2793-3014) on pairs / trim_noncanonical_end3_exons
+// (:3021-3243) on path: the end exon up to and including the first gap, kept or
+// trimmed by its matches against the gap's type, length and site probabilities.
+// Returns the rest of the list reversed, after the kept exon (pairs -> path,
+// path -> pairs).
+bool trim_noncanonical_end(bool end5, bool* trimp, const List& l, const Query& q, const Env& E, List* out,
+                           std::string* err) {
+  const gsnapdp_s3_call& c = *q.c;
+  out->clear();
+  if (l.empty()) {
+    *trimp = false;
+    return true;
+  }
+  const gsnapdp_s3_pair* pair = &l[0];
+  bool bingop = false;
+  if (end5 ? E.o.paired_favor_mode < 0 : E.o.paired_favor_mode > 0) {
+    const int insertlength = end5 ? pair->genomepos + c.querylength - E.o.zero_offset
+                                  : (c.genomiclength - pair->genomepos) + c.querylength - E.o.zero_offset;
+    if (insertlength > E.o.expected_pairlength - E.o.pairlength_deviation &&
+        insertlength < E.o.expected_pairlength + E.o.pairlength_deviation)
+      bingop = true;
+  }
+  size_t i = 0;  // the exon is l[0, i): up to and including the first gap
+  int nmatches = 0, nmismatches = -1;  // -1 because of the gap
+  while (i < l.size() && !gapp(*pair)) {
+    pair = &l[i++];
+    if (match_comp(pair->comp)) nmatches++;
+    else nmismatches++;
+  }
+  bool nearindelp = false;
+  for (size_t j = i, n = 0; j < l.size() && n < 6; j++, n++)  // NEARBY_INDEL medial to the gap
+    if (!match_comp(l[j].comp) && l[j].comp == '-') nearindelp = true;
+  for (ptrdiff_t j = (ptrdiff_t)i - 2, n = 0; j >= 0 && n < 6; j--, n++)  // distal, after the gap itself
+    if (!match_comp(l[(size_t)j].comp) && l[(size_t)j].comp == '-') nearindelp = true;
+  const Probs pr = probs_of(q, *pair);
+  if (nearindelp) {
+    nmismatches += pr.d >= 0.90 ? 0 : (pr.d >= 0.80 ? 1 : 3);
+    nmismatches += pr.a >= 0.90 ? 0 : (pr.a >= 0.80 ? 1 : 3);
+  }
+  const bool is_canonical = canonicalp(knowngapp(*pair), pair->comp, c.cdna_direction);
+  if (!is_canonical) nmismatches += 2;
+  const int nrest = (int)(l.size() - i);
+  bool keep;
+  if (nrest == 0) {
+    keep = true;
+  } else if (knowngapp(*pair) && nmismatches == 0) {
+    keep = true;
+  } else if (i == 0) {  // the list starts with a gap: exon->rest dereferences NULL
+    return *err = "trim_noncanonical_end_exons: the list starts with a gap (the reference crashes)", false;
+  } else if (i >= 2 && (l[i - 2].flags & GSNAPDP_S3_DISALLOWED)) {
+    keep = false;
+  } else if ((int)i - 1 > nrest) {  // more than halfway across
+    keep = true;
+  } else if (pair->genomejump > E.o.maxintronlen_bound) {
+    keep = false;
+  } else if (bingop && is_canonical && nmismatches <= 1) {
+    keep = true;
+  } else if (nearindelp && nmatches < 12) {  // INDEL_SPLICE_ENDLENGTH
+    keep = false;
+  } else if (!enough_matches(nmatches - nmismatches, pair->genomejump)) {
+    keep = false;
+  } else if (sufficient_splice_prob_local((int)i, nmismatches,
+                                          (c.cdna_direction >= 0) == end5 ? pr.d : pr.a)) {
+    keep = E.o.gsnap ? true : (pr.d >= 0.9 || pr.a >= 0.9);  // :2968-2983
+  } else {
+    keep = false;
+  }
+  *trimp = nrest != 0 && !keep;
+  // Pairpool_transfer(exon or NULL, the rest): the rest reversed onto the kept exon
+  out->reserve(l.size());
+  for (size_t j = l.size(); j-- > i;) out->push_back(l[j]);
+  if (keep)
+    for (size_t j = i; j-- > 0;) out->push_back(l[j]);
+  return true;
+}
+
+// the loops of path_compute between DP passes (:8711-9212), from the list the
+// last pass returned (q.list) to the next pass's input, a parked
+// assign_gap_types, or the end
+void advance(Query& q, const Env& E) {
   std::string err;
   List pairs = std::move(q.list);
   switch (q.step) {
@@ -623,17 +1012,104 @@ void advance(Query& q, int min_intronlength) {
       if (q.c->finalp) {
         q.list = insert_gapholders(path);
         q.step = Q_6;
-      } else {
+        return;
+      }
+      if (!E.full) {
         q.list = std::move(path);
         q.step = Q_DONE;
+        return;
       }
+      pairs = std::move(path);  // pass 7 on pass 6's pairs
+    }
+      [[fallthrough]];
+    case Q_6: {
+      if (!E.full) {
+        q.list = std::move(pairs);
+        q.step = Q_DONE;
+        return;
+      }
+      List p7;  // 7: dual breaks at the ends; 7b: adjacent insertions / deletions
+      bool adjacent;
+      if (!remove_end_dual_breaks(pairs, &p7, &err) || !remove_adjacent_ins_del(&adjacent, p7, &pairs, &err))
+        return fail(q, err);
+      if (adjacent) {  // 7C
+        q.list = insert_gapholders(pairs);
+        q.step = Q_7C;
+        return;
+      }
+    }
+      [[fallthrough]];
+    case Q_7C: {  // remove_indel_gaps; 8: extend to the 5' end
+      pairs = remove_indel_gaps(insert_gapholders(pairs), E.o.min_intronlength);
+      clean_end_gap_indels(pairs);
+      q.list = std::move(pairs);
+      q.step = Q_8_5;
       return;
     }
-    case Q_6:
-      q.list = std::move(pairs);
-      q.step = Q_DONE;
+    case Q_8_5: {  // 8: extend to the 3' end
+      List path = reversed(pairs);
+      clean_end_gap_indels(path);
+      q.list = std::move(path);
+      q.step = Q_8_3;
       return;
+    }
+    case Q_8_3:  // 9: gapholders, then assign_gap_types (parked for its sites)
+    case Q_9B: {
+      List path = insert_gapholders(reversed(pairs));
+      const int next = q.step == Q_8_3 ? Q_GT_9 : Q_GT_10;
+      q.sites.clear();
+      if (!assign_gap_types(q, E, path, &q.list, &err)) return fail(q, err);
+      q.step = next;
+      return;
+    }
+    case Q_GT_9:  // 9a (knownsplice5p is false: every end pass here ran Dynprog_end5_gap)
+      q.list = std::move(pairs);
+      q.step = Q_9A;
+      return;
+    case Q_9A:  // 9b
+      q.list = reversed(pairs);
+      q.step = Q_9B;
+      return;
+    case Q_GT_10:  // pass 10
+      q.iter10 = 0;
+      q.trim5p = q.trim3p = true;
+      break;
+    case Q_10_5:
+      if (q.trim3p) {
+        q.list = reversed(pairs);
+        q.step = Q_10_3;
+        return;
+      }
+      q.iter10++;
+      break;
+    case Q_10_3:
+      pairs = reversed(pairs);
+      q.iter10++;
+      break;
     default: return;
+  }
+  if (q.step >= Q_GT_10) {  // pass 10's loop (:9139-9212)
+    while (q.iter10 < 5 && (q.trim5p || q.trim3p)) {
+      List path;
+      if (!q.trim5p) path = reversed(pairs);
+      else if (!trim_noncanonical_end(true, &q.trim5p, pairs, q, E, &path, &err)) return fail(q, err);
+      if (!q.trim3p) pairs = reversed(path);
+      else if (!trim_noncanonical_end(false, &q.trim3p, path, q, E, &pairs, &err)) return fail(q, err);
+      if (q.trim5p) {
+        q.list = std::move(pairs);
+        q.step = Q_10_5;
+        return;
+      }
+      if (q.trim3p) {
+        q.list = reversed(pairs);
+        q.step = Q_10_3;
+        return;
+      }
+      q.iter10++;
+    }
+    q.list = std::move(pairs);
+    q.step = Q_DONE;
+    return;
   }
   // pass 3: while (shortp && iter1 < MAXITER_SMOOTH_BY_SIZE) { 3a, 3b, 3c }
   for (;;) {
@@ -665,7 +1141,7 @@ void advance(Query& q, int min_intronlength) {
   pairs = viterbi_filter(pairs, true, q.defect);
   pairs = viterbi_filter(pairs, false, 0.0);
   // 5: remove_indel_gaps, then build_dual_breaks on the reversed list
-  List gaps = remove_indel_gaps(insert_gapholders(pairs), min_intronlength);
+  List gaps = remove_indel_gaps(insert_gapholders(pairs), E.o.min_intronlength);
   reverse(gaps);
   q.list = std::move(gaps);
   q.step = Q_5;
@@ -674,30 +1150,47 @@ void advance(Query& q, int min_intronlength) {
 int pass_of(int step) {
   switch (step) {
     case Q_2A:
-    case Q_2C: return GSNAPDP_S3_SINGLES;
+    case Q_2C:
+    case Q_7C: return GSNAPDP_S3_SINGLES;
     case Q_3B: return GSNAPDP_S3_DUALINTRONS;
     case Q_5: return GSNAPDP_S3_DUALBREAKS;
+    case Q_8_5:
+    case Q_9A:
+    case Q_10_5: return GSNAPDP_S3_END5;
+    case Q_8_3:
+    case Q_9B:
+    case Q_10_3: return GSNAPDP_S3_END3;
     default: return GSNAPDP_S3_INTRONS;
   }
 }
 
 // the pipeline as the pass's driver: a query's next pass starts as soon as its
 // last one has ended, in the same round, so queries at different passes share
-// every round's batches
+// every round's batches.  A query that reaches assign_gap_types parks (its
+// MaxEnt sites go to the next batch of all parked queries' sites).
 class Pipeline final : public gsnapdp::S3Driver {
  public:
-  Pipeline(std::vector<Query>& qs, int min_intronlength) : qs_(qs), min_intronlength_(min_intronlength) {}
-  // the query's next pass call (q.list is its input), or nullptr when it is done
+  Pipeline(std::vector<Query>& qs, const Env& env) : qs_(qs), env_(env) {}
+  void set_map(const std::vector<int>* map) { map_ = map; }
+  // the query's next pass call (q.list is its input), or nullptr when it is done or parked
   gsnapdp_s3_call* call_for(Query& q) {
-    if (q.failed || q.step == Q_DONE) return nullptr;
+    if (q.failed || q.step == Q_DONE || q.step == Q_GT_9 || q.step == Q_GT_10) return nullptr;
     gsnapdp_s3_call& k = q.k;
     k = *q.c;
     k.pass = pass_of(q.step);
     k.first_pair = 0;
     k.npairs = (int32_t)q.list.size();
     k.finalp = q.step == Q_6 ? 1 : 0;
-    // 2A / 2C run with defect_rate 0.0 (:8676, :8705); the rest with the running rate
-    k.defect_rate = (q.step == Q_2A || q.step == Q_2C) ? 0.0 : q.defect;
+    // 2A / 2C / 7C run with defect_rate 0.0 (:8676, :8705, :8944); the rest with the running rate
+    k.defect_rate = (q.step == Q_2A || q.step == Q_2C || q.step == Q_7C) ? 0.0 : q.defect;
+    if (k.pass == GSNAPDP_S3_END5 || k.pass == GSNAPDP_S3_END3) {
+      // 8: QUERYEND_GAP; 9a / 9b: maxpeelback 0 and BEST_LOCAL (GSNAP: QUERYEND_NOGAPS); 10: QUERYEND_NOGAPS
+      const bool nine = q.step == Q_9A || q.step == Q_9B;
+      k.endalign = (q.step == Q_8_5 || q.step == Q_8_3)
+                       ? GSNAPDP_QUERYEND_GAP
+                       : (nine && !env_.o.gsnap ? GSNAPDP_BEST_LOCAL : GSNAPDP_QUERYEND_NOGAPS);
+      if (nine) k.maxpeelback = 0;
+    }
     k.in_minor = q.minor;
     k.in_major = q.major;
     k.in_nintrons = q.nintrons;
@@ -705,16 +1198,20 @@ class Pipeline final : public gsnapdp::S3Driver {
     k.in_intronlen = q.intronlen;
     k.in_nonintronlen = q.nonintronlen;
     q.passes[k.pass]++;
+    q.insrc.resize(q.list.size());
+    for (size_t j = 0; j < q.list.size(); j++) q.insrc[j] = q.list[j].src;
     return &k;
   }
   gsnapdp_s3_call* next(int i, gsnapdp_s3_call* k, std::vector<gsnapdp_s3_pair>& list,
                         const gsnapdp_s3_pair** pairs, int* n) override {
-    Query& q = qs_[(size_t)i];
+    Query& q = qs_[(size_t)(map_ ? (*map_)[(size_t)i] : i)];
     if (k->status) {
       fail(q, "a DP pass failed on the path (status -1)");
       return nullptr;
     }
     q.list.swap(list);  // (the pass's buffer takes the old list's storage for its next use)
+    for (gsnapdp_s3_pair& p : q.list)  // the pass's src is the input position: back to table rows
+      p.src = p.src >= 0 ? q.insrc[(size_t)p.src] : -1;
     q.minor = k->out_minor;
     q.major = k->out_major;
     q.ub |= k->ub;
@@ -726,7 +1223,7 @@ class Pipeline final : public gsnapdp::S3Driver {
       q.shiftp = k->shiftp != 0;
       q.incompletep = k->incompletep != 0;
     }
-    advance(q, min_intronlength_);
+    advance(q, env_);
     gsnapdp_s3_call* c = call_for(q);
     if (c) {
       *pairs = q.list.data();
@@ -737,37 +1234,37 @@ class Pipeline final : public gsnapdp::S3Driver {
 
  private:
   std::vector<Query>& qs_;
-  int min_intronlength_;
+  const Env& env_;
+  const std::vector<int>* map_ = nullptr;
 };
 
-}  // namespace
-
-extern "C" int gsnapdp_stage3_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries,
-                                      const gsnapdp_s3_pair* paths_in, int64_t npairs_in, const char* query,
-                                      const char* query_uc, size_t query_bytes, const gsnapdp_iit* iit,
-                                      int min_intronlength, gsnapdp_s3_pair* out, int64_t out_cap,
-                                      gsnapdp_s3_compute_stats* stats) {
+int compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries, const gsnapdp_s3_pair* paths_in,
+            int64_t npairs_in, const char* query, const char* query_uc, size_t query_bytes, const gsnapdp_iit* iit,
+            const Env& env, gsnapdp_s3_pair* out, int64_t out_cap, double* probs_out,
+            gsnapdp_s3_compute_stats* stats) {
   using clock = std::chrono::steady_clock;
   const auto t0 = clock::now();
+  const char* fn = env.full ? "gsnapdp_stage3_path_compute" : "gsnapdp_stage3_compute";
   if (!ctx || nqueries < 0 || npairs_in < 0 || (nqueries > 0 && (!queries || !query || !query_uc || !out))) {
-    gsnapdp__set_err("gsnapdp_stage3_compute: bad arguments");
+    gsnapdp__set_err(std::string(fn) + ": bad arguments");
     return -1;
   }
   gsnapdp_s3_compute_stats st;
   memset(&st, 0, sizeof(st));
   std::vector<Query> qs((size_t)nqueries);
   std::vector<gsnapdp_s3_call> first((size_t)nqueries);
-  Pipeline pipe(qs, min_intronlength);
+  Pipeline pipe(qs, env);
   for (int i = 0; i < nqueries; i++) {
     gsnapdp_s3_call& c = queries[i];
     if (c.first_pair < 0 || c.npairs < 0 || (int64_t)c.first_pair + c.npairs > npairs_in || c.qpos < 0 ||
         c.querylength < 0 || (uint64_t)c.qpos + (uint64_t)c.querylength > (uint64_t)query_bytes) {
-      gsnapdp__set_err("gsnapdp_stage3_compute: query " + std::to_string(i) + " outside the buffers");
+      gsnapdp__set_err(std::string(fn) + ": query " + std::to_string(i) + " outside the buffers");
       return -1;
     }
     Query& q = qs[(size_t)i];
     q.c = &c;
     q.list.assign(paths_in + c.first_pair, paths_in + c.first_pair + c.npairs);
+    for (gsnapdp_s3_pair& p : q.list) p.src = -1;
     q.minor = c.in_minor;
     q.major = c.in_major;
     q.nintrons = c.in_nintrons;
@@ -786,10 +1283,67 @@ extern "C" int gsnapdp_stage3_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries
   if (gsnapdp::s3_run_driven(ctx, first.data(), nqueries, paths_in, npairs_in, query, query_uc, query_bytes, iit,
                              &pipe, &ps))
     return -1;
-  st.passes = 1;
-  st.rounds = ps.rounds;
-  for (int f = 0; f < 4; f++) st.windows[f] = ps.windows[f];
-  // the lists after pass 6, in the caller's buffer
+  double gpu_s = ps.seconds[1];
+  auto add = [&](const gsnapdp_s3_stats& s) {
+    st.passes++;
+    st.rounds += s.rounds;
+    for (int f = 0; f < 4; f++) st.windows[f] += s.windows[f];
+  };
+  add(ps);
+  // the parked queries' assign_gap_types: one MaxEnt batch for all their sites,
+  // then their next passes in one more driven pass, until none parks
+  std::vector<int> map;
+  std::vector<gsnapdp_s3_pair> phase_in;
+  std::vector<uint8_t> model;
+  std::vector<uint32_t> pos, chroff;
+  std::vector<double> prob;
+  for (;;) {
+    map.clear();
+    model.clear(), pos.clear(), chroff.clear();
+    for (int i = 0; i < nqueries; i++) {
+      Query& q = qs[(size_t)i];
+      if (q.failed || (q.step != Q_GT_9 && q.step != Q_GT_10)) continue;
+      map.push_back(i);
+      for (const Site& s : q.sites) model.push_back(s.model), pos.push_back(s.pos), chroff.push_back(s.chroffset);
+    }
+    if (map.empty()) break;
+    prob.resize(model.size());
+    if (!model.empty()) {
+      const auto t1 = clock::now();
+      if (gsnapdp_maxent_host(ctx, model.data(), pos.data(), chroff.data(), prob.data(), (int)model.size()))
+        return -1;
+      gpu_s += std::chrono::duration<double>(clock::now() - t1).count();
+      st.sites += (int32_t)model.size();
+    }
+    size_t at = 0;
+    std::vector<gsnapdp_s3_call> calls;
+    std::vector<int> cmap;
+    phase_in.clear();
+    for (int i : map) {
+      Query& q = qs[(size_t)i];
+      for (const Site& s : q.sites) {
+        Probs& p = q.probs[(size_t)s.row];
+        (s.acceptor ? p.a : p.d) = prob[at++];
+      }
+      q.sites.clear();
+      advance(q, env);
+      gsnapdp_s3_call* c = pipe.call_for(q);
+      if (!c) continue;
+      calls.push_back(*c);
+      calls.back().first_pair = (int32_t)phase_in.size();
+      phase_in.insert(phase_in.end(), q.list.begin(), q.list.end());
+      cmap.push_back(i);
+    }
+    if (calls.empty()) continue;
+    pipe.set_map(&cmap);
+    const int rc = gsnapdp::s3_run_driven(ctx, calls.data(), (int)calls.size(), phase_in.data(),
+                                          (int64_t)phase_in.size(), query, query_uc, query_bytes, iit, &pipe, &ps);
+    pipe.set_map(nullptr);
+    if (rc) return -1;
+    gpu_s += ps.seconds[1];
+    add(ps);
+  }
+  // the returned lists, in the caller's buffer
   int64_t at = 0;
   for (int i = 0; i < nqueries; i++) {
     Query& q = qs[(size_t)i];
@@ -801,15 +1355,20 @@ extern "C" int gsnapdp_stage3_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries
     if (q.failed) {
       st.failed++;
       if (getenv("GSNAPDP_S3_DEBUG"))
-        fprintf(stderr, "gsnapdp_stage3_compute: query %d (tag %d) failed: %s\n", i, c.invocation, q.why.c_str());
+        fprintf(stderr, "%s: query %d (tag %d) failed: %s\n", fn, i, c.invocation, q.why.c_str());
       continue;
     }
     if (at + c.nout > out_cap) {
-      gsnapdp__set_err("gsnapdp_stage3_compute: the output is too small");
+      gsnapdp__set_err(std::string(fn) + ": the output is too small");
       return -1;
     }
     for (int64_t j = 0; j < c.nout; j++) {
       gsnapdp_s3_pair p = q.list[(size_t)j];
+      if (probs_out) {
+        const Probs r = probs_of(q, p);
+        probs_out[2 * (at + j)] = r.d;
+        probs_out[2 * (at + j) + 1] = r.a;
+      }
       p.src = -1;
       out[at + j] = p;
     }
@@ -825,9 +1384,43 @@ extern "C" int gsnapdp_stage3_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries
     c.defect_rate = q.defect;
     c.ub = q.ub;
   }
-  st.seconds[1] = ps.seconds[1];  // the time the host waited for the GPU
+  st.seconds[1] = gpu_s;  // the time the host waited for the GPU
   st.seconds[2] = std::chrono::duration<double>(clock::now() - t0).count();
   st.seconds[0] = st.seconds[2] - st.seconds[1];
   if (stats) *stats = st;
   return 0;
+}
+
+}  // namespace
+
+extern "C" int gsnapdp_stage3_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries,
+                                      const gsnapdp_s3_pair* paths_in, int64_t npairs_in, const char* query,
+                                      const char* query_uc, size_t query_bytes, const gsnapdp_iit* iit,
+                                      int min_intronlength, gsnapdp_s3_pair* out, int64_t out_cap,
+                                      gsnapdp_s3_compute_stats* stats) {
+  Env env;
+  memset(&env.o, 0, sizeof(env.o));
+  env.o.min_intronlength = min_intronlength;
+  return compute(ctx, queries, nqueries, paths_in, npairs_in, query, query_uc, query_bytes, iit, env, out, out_cap,
+                 nullptr, stats);
+}
+
+extern "C" int gsnapdp_stage3_path_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries,
+                                           const gsnapdp_s3_pair* paths_in, int64_t npairs_in, const char* query,
+                                           const char* query_uc, size_t query_bytes, const gsnapdp_iit* iit,
+                                           const gsnapdp_s3_path_opts* opts, gsnapdp_s3_pair* out, int64_t out_cap,
+                                           double* probs_out, gsnapdp_s3_compute_stats* stats) {
+  if (!opts || (nqueries > 0 && !query)) {
+    gsnapdp__set_err("gsnapdp_stage3_path_compute: bad arguments");
+    return -1;
+  }
+  Env env;
+  env.o = *opts;
+  env.full = true;
+  env.blocks = gsnapdp__host_blocks(ctx);
+  env.nwords = gsnapdp__host_nwords(ctx);
+  env.iit = iit;
+  env.query = query;
+  return compute(ctx, queries, nqueries, paths_in, npairs_in, query, query_uc, query_bytes, iit, env, out, out_cap,
+                 probs_out, stats);
 }

@@ -115,6 +115,9 @@ def lib():
         L.gsnapdp_stage3_compute.argtypes = [vp, vp, i32, vp, ctypes.c_int64, vp, vp, sz, vp, i32, vp,
                                              ctypes.c_int64, vp]
         L.gsnapdp_stage3_compute.restype = i32
+        L.gsnapdp_stage3_path_compute.argtypes = [vp, vp, i32, vp, ctypes.c_int64, vp, vp, sz, vp, vp, vp,
+                                                  ctypes.c_int64, vp, vp]
+        L.gsnapdp_stage3_path_compute.restype = i32
         L.gsnapdp_stage3_set_stage2.argtypes = [vp, vp]
         L.gsnapdp_scan_site_probs.argtypes = [vp, vp, i32, vp]
         L.gsnapdp_scan_site_probs.restype = i32
@@ -571,6 +574,36 @@ class Context:
         if rc != 0:
             raise GsnapdpError("gsnapdp_stage3_compute: %s" % lib().gsnapdp_last_error().decode())
         return c, out[:int(c["nout"].sum())], st[0]
+
+    def stage3_path_compute(self, queries: np.ndarray, paths_in: np.ndarray, query: np.ndarray,
+                            query_uc: np.ndarray, iit: "SplicingIIT" = None, min_intronlength: int = 9,
+                            maxintronlen_bound: int = 1000000, gsnap: bool = False, out: np.ndarray = None):
+        """path_compute (stage3.c:8586-9220) from pass 2A to its return value
+        for every query (gsnapdp_stage3_path_compute; GMAP's paired_favor_mode 0).
+        Returns (queries with the out fields written, the returned lists
+        concatenated, their pairs' (donor_prob, acceptor_prob) as an (n, 2)
+        array, S3_COMPUTE_STATS)."""
+        from .records import S3_COMPUTE_STATS, S3_PATH_OPTS
+        c = np.array(queries, dtype=S3_CALL, copy=True)
+        pi = np.ascontiguousarray(paths_in, dtype=S3_PAIR)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        cap = 2 * self.stage3_capacity(c) + 1024
+        if out is None or out.dtype != S3_PAIR or out.size < cap:
+            out = np.empty(cap, dtype=S3_PAIR)
+        probs = np.empty((out.size, 2), dtype=np.float64)
+        o = np.zeros(1, dtype=S3_PATH_OPTS)
+        o["min_intronlength"], o["maxintronlen_bound"] = min_intronlength, maxintronlen_bound
+        o["gsnap"] = 1 if gsnap else 0
+        st = np.zeros(1, dtype=S3_COMPUTE_STATS)
+        rc = lib().gsnapdp_stage3_path_compute(self.h, _p(c), len(c), _p(pi) if pi.size else _p(out), pi.size,
+                                               _p(q), _p(qu), min(q.size, qu.size),
+                                               iit.h if iit is not None else None, _p(o), _p(out), out.size,
+                                               _p(probs), _p(st))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_stage3_path_compute: %s" % lib().gsnapdp_last_error().decode())
+        n = int(c["nout"].sum())
+        return c, out[:n], probs[:n], st[0]
 
     def scan_site_probs(self, sites: np.ndarray) -> np.ndarray:
         """GSNAP's splice-site scan candidates (SCAN_SITE records) in one batch

@@ -155,15 +155,21 @@ S2_CALL = np.dtype([(n, "<i4") for n in "invocation query_offset querylength gen
                    [(n, "<i4") for n in "plusp first_pair npairs pad".split()])
 assert S2_CALL.itemsize == 48
 PC_CALL = np.dtype([(n, "<i4") for n in ("invocation do_final_p stage3debug cdna_direction querylength "
-                                         "genomiclength watsonp pad").split()] + [("defect_rate", "<f8")])
-assert PC_CALL.itemsize == 40
+                                         "genomiclength watsonp pad").split()] + [("defect_rate", "<f8")] +
+                   [(n, "<i4") for n in ("first_out nout intronlen nonintronlen maxpeelback nullgap "
+                                         "extramaterial_end extraband_end maxintronlen_bound paired_favor_mode "
+                                         "zero_offset jump_late_p").split()] + [("passes", "<i4", 6)])
+assert PC_CALL.itemsize == 112
 # GSNAP's splice-site scan candidates (include/gsnapdp.h gsnapdp_scan_site)
 SCAN_SITE = np.dtype([("segment_left", "<u4"), ("splice_pos", "<i4"), ("chroffset", "<u4"), ("knowni", "<i4"),
                       ("model", "<i4")])
 assert SCAN_SITE.itemsize == 20
 S3_COMPUTE_STATS = np.dtype([("passes", "<i4"), ("rounds", "<i4"), ("windows", "<i4", 4), ("pass_calls", "<i4", 6),
-                             ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3)])
+                             ("failed", "<i4"), ("sites", "<i4"), ("seconds", "<f8", 3)])
 assert S3_COMPUTE_STATS.itemsize == 80
+S3_PATH_OPTS = np.dtype([(n, "<i4") for n in ("min_intronlength maxintronlen_bound paired_favor_mode zero_offset "
+                                             "expected_pairlength pairlength_deviation gsnap pad").split()])
+assert S3_PATH_OPTS.itemsize == 32
 S3_STATS = np.dtype([("rounds", "<i4"), ("windows", "<i4", 4), ("batches", "<i4", 4), ("undefined", "<i4"),
                      ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3), ("new_pairs", "<i8")])
 assert S3_STATS.itemsize == 80

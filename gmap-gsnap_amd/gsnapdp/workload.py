@@ -1287,6 +1287,66 @@ def stage3_pipeline(z, copies: int = 1):
     return queries, pin, q, qu, wl, final, counts
 
 
+def stage3_path_pipeline(z, copies: int = 1):
+    """The path_compute calls of a recorded gmap run (tests/golden/gmap_*_stage3.npz
+    with its pc_calls / pc_pairs / pc_probs) as queries for
+    gsnapdp_stage3_path_compute (pass 2A to path_compute's return value): each
+    query is the invocation's first build_pairs_singles call (its path, query
+    and arguments) with the last build_pairs_introns call's arguments, the
+    counters at their first use, and path_compute's own arguments for passes
+    7-10 (maxpeelback, extramaterial_end, extraband_end, do_final_p).  Returns
+    (queries, paths_in, query, query_uc, the lists path_compute returned
+    concatenated, their (donor_prob, acceptor_prob) rows, the PC_CALL records
+    in query order), `copies` times over."""
+    from .records import S3_DUALINTRONS, S3_INTRONS, S3_SINGLES
+    calls, pin, q, qu, _ = stage3_calls(z)
+    pc, pcp, pcr = z["pc_calls"], z["pc_pairs"], z["pc_probs"]
+    inv = calls["invocation"]
+    order = np.argsort(inv, kind="stable")
+    Q, W_, R, F = [], [], [], []
+    for rec in pc:
+        v = int(rec["invocation"])
+        idx = order[inv[order] == v]
+        cs = calls[idx]
+        sg = np.nonzero(cs["pass"] == S3_SINGLES)[0]
+        intr = np.nonzero(cs["pass"] == S3_INTRONS)[0]
+        if rec["stage3debug"] != 0 or sg.size == 0 or intr.size == 0 or sg[0] > intr[0]:
+            continue
+        first, last = cs[sg[0]], cs[intr[-1]]
+        before = cs[:intr[-1] + 1]
+        maj = before[np.isin(before["pass"], (S3_DUALINTRONS, S3_INTRONS))]
+        k = last.copy()
+        k["first_pair"], k["npairs"] = first["first_pair"], first["npairs"]
+        k["qpos"], k["querylength"] = first["qpos"], first["querylength"]
+        k["in_minor"], k["in_major"] = first["in_minor"], maj[0]["in_major"]
+        ins = cs[intr[0]]
+        for f in ("in_nintrons", "in_nnonintrons", "in_intronlen", "in_nonintronlen"):
+            k[f] = ins[f]
+        k["finalp"] = rec["do_final_p"]
+        k["maxpeelback"], k["extramaterial_end"], k["extraband_end"] = (
+            rec["maxpeelback"], rec["extramaterial_end"], rec["extraband_end"])
+        Q.append(k)
+        F.append(rec)
+        W_.append(pcp[int(rec["first_out"]):int(rec["first_out"]) + int(rec["nout"])])
+        R.append(pcr[int(rec["first_out"]):int(rec["first_out"]) + int(rec["nout"])])
+    queries = np.array(Q, dtype=calls.dtype)
+    final = np.array(F, dtype=pc.dtype)
+    wl = np.concatenate(W_) if W_ else np.zeros(0, dtype=pcp.dtype)
+    wr = np.concatenate(R) if R else np.zeros((0, 2), dtype=np.float64)
+    final["first_out"] = np.concatenate([[0], np.cumsum(final["nout"])[:-1]]).astype(np.int32)
+    if copies > 1:
+        n = len(queries)
+        kk = np.repeat(np.arange(copies), n)
+        queries = np.tile(queries, copies)
+        queries["first_pair"] += (kk * pin.size).astype(np.int32)
+        queries["qpos"] += (kk * q.size).astype(np.int32)
+        final = np.tile(final, copies)
+        final["first_out"] += (kk * wl.size).astype(np.int32)
+        pin, q, qu = np.tile(pin, copies), np.tile(q, copies), np.tile(qu, copies)
+        wl, wr = np.tile(wl, copies), np.tile(wr, (copies, 1))
+    return queries, pin, q, qu, wl, wr, final
+
+
 def stage3_calls(z, copies: int = 1):
     """Unpack a recorded stage-3 pass (tests/golden/gmap_*_stage3.npz,
     oracle/gen_golden.py stage3_golden) into the inputs of

@@ -734,13 +734,54 @@ typedef struct gsnapdp_s3_compute_stats {
   int32_t windows[4];     /* as gsnapdp_s3_stats */
   int32_t pass_calls[6];  /* the pass calls, by GSNAPDP_S3_* */
   int32_t failed;
-  int32_t pad;
-  double seconds[3];      /* wall time: host steps between the passes, the passes, the whole call */
+  int32_t sites;          /* MaxEnt site probabilities evaluated for assign_gap_types (path_compute) */
+  double seconds[3];      /* wall time: host steps between the passes, the GPU work (passes and MaxEnt
+                           * batches), the whole call */
 } gsnapdp_s3_compute_stats;
 int gsnapdp_stage3_compute(gsnapdp_ctx *ctx, gsnapdp_s3_call *queries, int nqueries,
                            const gsnapdp_s3_pair *paths_in, int64_t npairs_in, const char *query,
                            const char *query_uc, size_t query_bytes, const gsnapdp_iit *iit, int min_intronlength,
                            gsnapdp_s3_pair *out, int64_t out_cap, gsnapdp_s3_compute_stats *stats);
+
+/* path_compute (stage3.c:8586-9220) from pass 2A to its return value, for many
+ * queries: passes 2A-6 as gsnapdp_stage3_compute, then
+ *   7   the dual breaks at the ends (:8885-8925: dualbreak_distance_from_end,
+ *       trim_npairs),
+ *   7b  remove_adjacent_ins_del (:1889) and, when it removed any, 7C
+ *       build_pairs_singles; remove_indel_gaps,
+ *   8   clean_pairs_end5_gap_indels / clean_path_end3_gap_indels (:2056-2126),
+ *       build_pairs_end5 / build_path_end3 with QUERYEND_GAP,
+ *   9   assign_gap_types (:1015: intron types, cDNA-insertion and short-gap
+ *       pairs, the MaxEnt donor / acceptor probabilities of every intron) and
+ *       build_pairs_end5 / build_path_end3 with BEST_LOCAL and maxpeelback 0,
+ *       then assign_gap_types again,
+ *   10  trim_noncanonical_end5_exons / _end3_exons (:2793, :3021) with their
+ *       QUERYEND_NOGAPS re-extensions, at most 5 iterations.
+ * Every DP pass of every query runs in driven gsnapdp_stage3_pass rounds; the
+ * MaxEnt probabilities of each assign_gap_types are one k_maxent batch over all
+ * queries that reached it (1.0 for a site the splicing IIT knows, as the
+ * reference asks it).  Queries as for gsnapdp_stage3_compute, plus their
+ * maxpeelback, extramaterial_end, extraband_end and finalp (= do_final_p).
+ * Written: the returned list (list order, src -1) at first_out / nout, and in
+ * probs_out (2 doubles per returned pair, NULL to skip) each pair's donor_prob
+ * and acceptor_prob; out_minor / out_major, out_intronlen / out_nonintronlen
+ * (path_compute's *intronlen / *nonintronlen), defect_rate, ub, status.  Needs
+ * the MaxEnt tables. */
+typedef struct gsnapdp_s3_path_opts {
+  int32_t min_intronlength;    /* Stage3_setup's (gmap -j, default 9): remove_indel_gaps, assign_gap_types */
+  int32_t maxintronlen_bound;  /* path_compute's maxintronlen (gmap: maxintronlen_bound, default 1000000) */
+  int32_t paired_favor_mode;   /* 0 in GMAP; GSNAP's GMAP-in-GSNAP passes its own */
+  int32_t zero_offset;
+  int32_t expected_pairlength, pairlength_deviation;  /* Stage3_setup's (read when paired_favor_mode != 0) */
+  int32_t gsnap;               /* 1: stage3.c as GSNAP builds it (-DGSNAP: passes 9a / 9b with QUERYEND_NOGAPS,
+                                * a sufficiently supported end exon always kept); 0: GMAP */
+  int32_t pad;
+} gsnapdp_s3_path_opts;
+int gsnapdp_stage3_path_compute(gsnapdp_ctx *ctx, gsnapdp_s3_call *queries, int nqueries,
+                                const gsnapdp_s3_pair *paths_in, int64_t npairs_in, const char *query,
+                                const char *query_uc, size_t query_bytes, const gsnapdp_iit *iit,
+                                const gsnapdp_s3_path_opts *opts, gsnapdp_s3_pair *out, int64_t out_cap,
+                                double *probs_out, gsnapdp_s3_compute_stats *stats);
 
 /* score_introns (stage3.c:7935-8162) on the lists a pass returned: for every
  * call with status 0, its list reversed into path order (as stage3_compute

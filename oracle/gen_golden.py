@@ -818,6 +818,18 @@ def stage3_trace(t: str):
     return c, pi, po, q, qu
 
 
+def path_compute_trace(t: str):
+    """every path_compute call of a gmap_trace bpi directory: (PC_CALL records, the
+    lists they returned (S3_PAIR, list order, src -1), the pairs' (donor_prob,
+    acceptor_prob))"""
+    from gsnapdp.records import PC_CALL, S3_PAIR
+    pcc = np.fromfile(os.path.join(t, "path_compute.bin"), dtype=PC_CALL)
+    pcp = np.fromfile(os.path.join(t, "pc_pairs.bin"), dtype=S3_PAIR)
+    pcr = np.fromfile(os.path.join(t, "pc_probs.bin"), dtype="<f8").reshape(-1, 2)
+    assert pcp.size == int(pcc["nout"].sum()) == pcr.shape[0]
+    return pcc, pcp, pcr
+
+
 def stage3_golden(prefix: str, t: str, blocks: np.ndarray, every: int, end_every: int = 1) -> None:
     """Every `every`-th stage-3 pass call gmap made (stage3_pack): build_pairs_introns,
     build_pairs_singles, build_pairs_dualintrons, and of build_pairs_end5 /
@@ -834,10 +846,10 @@ def stage3_golden(prefix: str, t: str, blocks: np.ndarray, every: int, end_every
     # traverse_dual_break's stage-2 calls and every path_compute call (the pipeline tests)
     s2c = np.fromfile(os.path.join(t, "stage2_calls.bin"), dtype=S2_CALL)
     s2p = np.fromfile(os.path.join(t, "stage2_pairs.bin"), dtype=S3_PAIR)
-    pcc = np.fromfile(os.path.join(t, "path_compute.bin"), dtype=PC_CALL)
+    pcc, pcp, pcr = path_compute_trace(t)
     np.savez_compressed(os.path.join(OUT, prefix + "_stage3.npz"), blocks=blocks, every=np.int32(every),
                         end_every=np.int32(end_every), ncalls_traced=np.int32(c.size), s2_calls=s2c, s2_pairs=s2p,
-                        pc_calls=pcc, **d)
+                        pc_calls=pcc, pc_pairs=pcp, pc_probs=pcr, **d)
     sel = d["calls"]
     print("%s_stage3: %d of %d pass calls (by pass %s; %d final introns), %d path pairs, %d new pairs, "
           "reference %.3f s; %d path_compute calls, %d stage-2 calls of traverse_dual_break" %

@@ -212,6 +212,7 @@ extern int gmap_trace_novelsplicingp(void);
 extern int gmap_trace_splicingp(void);
 static Patch bpi_p;
 static Buf bpi_calls, bpi_in, bpi_out, bpi_q, bpi_qu;
+static int32_t pc_passes[6]; /* the pass calls of the path_compute call in progress, by GSNAPDP_S3_* */
 
 typedef struct { /* gsnapdp_s3_call (include/gsnapdp.h) */
   int32_t first_pair, npairs, first_out, nout, qpos, querylength;
@@ -305,6 +306,7 @@ static void bpi_end(BpiCall *c, List_T out, PtrIdx *ix, int n, const struct time
   }
   free(ix);
   put(&bpi_calls, c, sizeof(*c));
+  if (c->pass >= 0 && c->pass < 6) pc_passes[c->pass]++;
 }
 static void bpi_dynprogs(BpiCall *c, Dynprog_T dynprogL, Dynprog_T dynprogM, Dynprog_T dynprogR) {
   c->maxlength1[0] = ((int *)dynprogL)[0];
@@ -318,10 +320,16 @@ static void bpi_dynprogs(BpiCall *c, Dynprog_T dynprogL, Dynprog_T dynprogM, Dyn
 /* path_compute (stage3.c:8586), static: patched so that every pass call below
  * carries the number of the path_compute call it belongs to (`invocation`) */
 static int32_t pc_invocation = -1;
-static Buf pc_calls;
-typedef struct { /* one path_compute call */
+static Buf pc_calls, pc_pairs, pc_probs;
+typedef struct { /* one path_compute call (gsnapdp/records.py PC_CALL) */
   int32_t invocation, do_final_p, stage3debug, cdna_direction, querylength, genomiclength, watsonp, pad;
-  double defect_rate; /* its output */
+  double defect_rate;              /* its output */
+  int32_t first_out, nout;         /* the list it returned: pc_pairs.bin (BpiPair, list order, src -1) and
+                                    * pc_probs.bin (donor_prob, acceptor_prob per pair) */
+  int32_t intronlen, nonintronlen; /* its outputs */
+  int32_t maxpeelback, nullgap, extramaterial_end, extraband_end; /* what passes 7-10 read (stage3.c:8885-9212) */
+  int32_t maxintronlen_bound, paired_favor_mode, zero_offset, jump_late_p;
+  int32_t passes[6];               /* the pass calls it made */
 } PcCall;
 
 static List_T bpi_hook(bool *shiftp, bool *incompletep, int *nintrons, int *nnonintrons, int *intronlen,
@@ -712,8 +720,9 @@ static List_T pc_hook(double *defect_rate, int *intronlen, int *nonintronlen, Li
                       void *diagpool, int sufflookback, int nsufflookback, int maxintronlen_bound,
                       int close_indels_mode, int paired_favor_mode, int zero_offset) {
   PcCall r;
-  List_T out;
+  List_T out, p;
   memset(&r, 0, sizeof(r));
+  memset(pc_passes, 0, sizeof(pc_passes));
   r.invocation = ++pc_invocation;
   r.do_final_p = do_final_p;
   r.stage3debug = stage3debug;
@@ -733,6 +742,28 @@ static List_T pc_hook(double *defect_rate, int *intronlen, int *nonintronlen, Li
                                       close_indels_mode, paired_favor_mode, zero_offset);
   patch_on(&pc_p);
   r.defect_rate = *defect_rate;
+  r.intronlen = *intronlen;
+  r.nonintronlen = *nonintronlen;
+  r.maxpeelback = maxpeelback;
+  r.nullgap = nullgap;
+  r.extramaterial_end = extramaterial_end;
+  r.extraband_end = extraband_end;
+  r.maxintronlen_bound = maxintronlen_bound;
+  r.paired_favor_mode = paired_favor_mode;
+  r.zero_offset = zero_offset;
+  r.jump_late_p = jump_late_p;
+  memcpy(r.passes, pc_passes, sizeof(pc_passes));
+  r.first_out = (int32_t)(pc_pairs.n / sizeof(BpiPair));
+  for (p = out; p != NULL; p = p->rest) {
+    const struct Pair_T *x = (const struct Pair_T *)p->first;
+    BpiPair b = bpi_pair(x, -1);
+    double pr[2];
+    pr[0] = x->donor_prob;
+    pr[1] = x->acceptor_prob;
+    put(&pc_pairs, &b, sizeof(b));
+    put(&pc_probs, pr, sizeof(pr));
+    r.nout++;
+  }
   put(&pc_calls, &r, sizeof(r));
   return out;
 }
@@ -944,6 +975,8 @@ __attribute__((destructor)) static void write_trace(void) {
     spit(dir, "query.bin", bpi_q.p, bpi_q.n);
     spit(dir, "query_uc.bin", bpi_qu.p, bpi_qu.n);
     spit(dir, "path_compute.bin", pc_calls.p, pc_calls.n);
+    spit(dir, "pc_pairs.bin", pc_pairs.p, pc_pairs.n);
+    spit(dir, "pc_probs.bin", pc_probs.p, pc_probs.n);
     spit(dir, "stage2_calls.bin", s2_calls.p, s2_calls.n);
     spit(dir, "stage2_pairs.bin", s2_pairs.p, s2_pairs.n);
   }

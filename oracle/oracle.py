@@ -243,6 +243,9 @@ def s3lib():
         L.gsnapdp_oracle_stash_reset.argtypes = []
         L.gsnapdp_stage3_compute.argtypes = [vp, vp, i32, vp, i64, vp, vp, ctypes.c_size_t, vp, i32, vp, i64, vp]
         L.gsnapdp_stage3_compute.restype = i32
+        L.gsnapdp_stage3_path_compute.argtypes = [vp, vp, i32, vp, i64, vp, vp, ctypes.c_size_t, vp, vp, vp, i64,
+                                                  vp, vp]
+        L.gsnapdp_stage3_path_compute.restype = i32
         L.gsnapdp_stage3_set_stage2.argtypes = [vp, vp]
         L.s2dbl_new.argtypes = [vp, i32, vp, i32]
         L.s2dbl_new.restype = vp
@@ -291,6 +294,31 @@ class Stage3Cpu:
         finally:
             L.gsnapdp_oracle_stash_reset()
         return c, out[:int(c["nout"].sum())], st[0]
+
+    def path_compute(self, queries, paths_in, query, query_uc, min_intronlength=9, maxintronlen_bound=1000000):
+        """gsnapdp_stage3_path_compute (pass 2A to path_compute's return value):
+        (queries with out fields, lists, their (donor_prob, acceptor_prob), S3_COMPUTE_STATS)"""
+        from gsnapdp.records import S3_CALL, S3_COMPUTE_STATS, S3_PAIR, S3_PATH_OPTS
+        L = s3lib()
+        c = np.array(queries, dtype=S3_CALL, copy=True)
+        pi = np.ascontiguousarray(paths_in, dtype=S3_PAIR)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        cap = 2 * int((2 * (c["querylength"].astype(np.int64) + c["npairs"]) + 64).sum()) + 1024
+        out = np.empty(cap, dtype=S3_PAIR)
+        probs = np.empty((cap, 2), dtype=np.float64)
+        o = np.zeros(1, dtype=S3_PATH_OPTS)
+        o["min_intronlength"], o["maxintronlen_bound"] = min_intronlength, maxintronlen_bound
+        st = np.zeros(1, dtype=S3_COMPUTE_STATS)
+        try:
+            if L.gsnapdp_stage3_path_compute(self.h, c.ctypes.data, len(c), pi.ctypes.data, pi.size, q.ctypes.data,
+                                             qu.ctypes.data, min(q.size, qu.size), None, o.ctypes.data,
+                                             out.ctypes.data, cap, probs.ctypes.data, st.ctypes.data):
+                raise RuntimeError("libstage3_cpu path_compute: %s" % L.s3cpu_last_error().decode())
+        finally:
+            L.gsnapdp_oracle_stash_reset()
+        n = int(c["nout"].sum())
+        return c, out[:n], probs[:n], st[0]
 
     def run_compact(self, calls, pairs_in, query, query_uc):
         """gsnapdp_stage3_pass_compact: (calls, cells, new pairs, S3_STATS)"""

@@ -13,6 +13,8 @@
 //                     --introns DIR/pass_scores.bin (score_introns on the returned lists);
 //   stage3_cpu DIR --compute MINLEN   passes 2A-6 (gsnapdp_stage3_compute) over the queries in
 //                     calls.bin: DIR/{pass_calls,pass_pairs,compute_stats}.bin
+//   stage3_cpu DIR --path-compute MINLEN MAXINTRONLEN   path_compute from pass 2A to its return
+//                     value (gsnapdp_stage3_path_compute): the same files and DIR/pass_probs.bin
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -62,6 +64,8 @@ int main(int argc, char** argv) {
   const bool introns = argc > 2 && std::string(argv[2]) == "--introns";
   // --compute MINLEN: gsnapdp_stage3_compute with min_intronlength MINLEN
   const int compute = argc > 3 && std::string(argv[2]) == "--compute" ? atoi(argv[3]) : -1;
+  // --path-compute MINLEN MAXINTRONLEN: gsnapdp_stage3_path_compute
+  const bool path_compute = argc > 4 && std::string(argv[2]) == "--path-compute";
   std::vector<gsnapdp_s3_call> calls = slurp<gsnapdp_s3_call>(d + "/calls.bin");
   std::vector<gsnapdp_s3_pair> in = slurp<gsnapdp_s3_pair>(d + "/pairs_in.bin");
   std::vector<char> q = slurp<char>(d + "/query.bin"), qu = slurp<char>(d + "/query_uc.bin");
@@ -87,6 +91,30 @@ int main(int argc, char** argv) {
     s2 = s2dbl_new(sc.data(), (int)(sc.size() / 48), sp.data(), (int)sp.size());
     gsnapdp_s3_stage2 cb = {s2, s2dbl_compute_one};
     gsnapdp_stage3_set_stage2(ctx, &cb);
+  }
+  if (path_compute) {  // pass 2A to path_compute's return value: calls.bin holds the queries
+    gsnapdp_s3_compute_stats cs;
+    gsnapdp_s3_path_opts o = {};
+    o.min_intronlength = atoi(argv[3]);
+    o.maxintronlen_bound = atoi(argv[4]);
+    std::vector<gsnapdp_s3_pair> big((size_t)cap * 2 + 1024);
+    std::vector<double> probs(big.size() * 2);
+    if (gsnapdp_stage3_path_compute(ctx, calls.data(), (int)calls.size(), in.data(), (int64_t)in.size(), q.data(),
+                                    qu.data(), std::min(q.size(), qu.size()), iit, &o, big.data(),
+                                    (int64_t)big.size(), probs.data(), &cs)) {
+      fprintf(stderr, "gsnapdp_stage3_path_compute: %s\n", g_err.c_str());
+      return 5;
+    }
+    fprintf(stderr, "path_compute %.4f s (host steps %.4f, passes %.4f), %d passes, %d rounds, %d sites, %d failed\n",
+            cs.seconds[2], cs.seconds[0], cs.seconds[1], cs.passes, cs.rounds, cs.sites, cs.failed);
+    int64_t nout = 0;
+    for (const gsnapdp_s3_call& c : calls) nout += c.nout;
+    spit(d + "/pass_calls.bin", calls.data(), calls.size());
+    spit(d + "/pass_pairs.bin", big.data(), (size_t)nout);
+    spit(d + "/pass_probs.bin", probs.data(), (size_t)nout * 2);
+    spit(d + "/compute_stats.bin", &cs, 1);
+    gsnapdp_destroy(ctx);
+    return 0;
   }
   if (compute >= 0) {  // passes 2A-6 (gsnapdp_stage3_compute): calls.bin holds the queries
     gsnapdp_s3_compute_stats cs;

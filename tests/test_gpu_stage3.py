@@ -15,8 +15,8 @@ import pytest
 
 from gsnapdp import Context, SplicingIIT
 from gsnapdp import workload as W
-from test_stage3_cpu import (IIT_NAMES, NAMES, PIPE_NAMES, check_compute, check_pass, check_scores, iit_intervals,
-                             stage3_golden)
+from test_stage3_cpu import (IIT_NAMES, NAMES, PIPE_NAMES, check_compute, check_pass, check_path_compute,
+                             check_scores, iit_intervals, stage3_golden)
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -100,6 +100,37 @@ def test_gpu_stage3_compute_matches_reference(golden_dir, tmp_path, name):
         print("stage3 compute (passes 2A-6): %d queries in %.3f s = %.0f queries/s (%d passes, %d rounds, windows %s; "
               "host steps %.3f s, passes %.3f s)" % (len(Q), dt, len(Q) / dt, st["passes"], st["rounds"],
                                                     st["windows"], st["seconds"][0], st["seconds"][1]))
+    ctx.close()
+
+
+@pytest.mark.parametrize("name", PIPE_NAMES)
+def test_gpu_stage3_path_compute_matches_reference(golden_dir, tmp_path, name):
+    """path_compute from pass 2A to its return value for every recorded
+    invocation at once (gsnapdp_stage3_path_compute: passes 2A-10, the DP
+    passes and assign_gap_types' MaxEnt sites on the GPU): the lists, the
+    pairs' donor / acceptor probabilities, *intronlen / *nonintronlen /
+    *defect_rate and the pass calls gmap made, bit for bit; then the synthetic
+    set x8 in one call, each copy checked, timed"""
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    queries, pin, q, qu, want, wprobs, final = W.stage3_path_pipeline(z)
+    ctx = Context(z["blocks"])
+    s2 = stage2_double(ctx, z, tmp_path)
+    maxintron = int(final["maxintronlen_bound"][0])
+    got_calls, got, probs, st = ctx.stage3_path_compute(queries, pin, q, qu, maxintronlen_bound=maxintron)
+    check_path_compute(got_calls, got, probs, want, wprobs, final, name)
+    assert list(st["pass_calls"]) == list(final["passes"].sum(axis=0))
+    assert st["sites"] > 0
+    if name == "gmap_synth_stage3":
+        copies = 8
+        Q, PI, QQ, QU, WANT, WP, FINAL = W.stage3_path_pipeline(z, copies)
+        t0 = time.perf_counter()
+        got_calls, got, probs, st = ctx.stage3_path_compute(Q, PI, QQ, QU, maxintronlen_bound=maxintron)
+        dt = time.perf_counter() - t0
+        check_path_compute(got_calls, got, probs, WANT, WP, FINAL, "x%d" % copies)
+        print("stage3 path_compute (passes 2A-10): %d queries in %.3f s = %.0f queries/s (%d passes, %d rounds, "
+              "windows %s, %d MaxEnt sites; host steps %.3f s, GPU %.3f s)" % (
+                  len(Q), dt, len(Q) / dt, st["passes"], st["rounds"], st["windows"], st["sites"],
+                  st["seconds"][0], st["seconds"][1]))
     ctx.close()
 
 

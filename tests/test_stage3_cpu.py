@@ -240,3 +240,68 @@ def test_stage3_compute_cpu_matches_reference(golden_dir, tmp_path, name):
     cs = np.fromfile(os.path.join(d, "compute_stats.bin"), dtype=S3_COMPUTE_STATS)[0]
     # the same pass calls as gmap made up to pass 6: 2A / 2C singles, dual introns, introns, dual breaks
     assert list(cs["pass_calls"]) == list(counts.sum(axis=0)), (cs["pass_calls"], counts.sum(axis=0))
+
+
+def check_path_compute(got_calls, got, probs, want, want_probs, final, what):
+    """gsnapdp_stage3_path_compute's lists, pair probabilities and outputs
+    against what path_compute returned in gmap (tests/golden pc_*)"""
+    assert (got_calls["status"] == 0).all(), "%s: failed queries %s" % (what, np.nonzero(got_calls["status"])[0][:8])
+    ub = (got_calls["ub"] & 1) != 0
+    for f, g in (("intronlen", "out_intronlen"), ("nonintronlen", "out_nonintronlen")):
+        bad = np.nonzero((got_calls[g] != final[f]) & ~ub)[0]
+        assert bad.size == 0, "%s: %s differs at queries %s" % (what, f, bad[:8])
+    bad = np.nonzero(got_calls["defect_rate"].view(np.uint64) != final["defect_rate"].view(np.uint64))[0]
+    assert bad.size == 0, "%s: defect_rate differs at queries %s" % (what, bad[:8])
+    for i, (c, w) in enumerate(zip(got_calls, final)):
+        a, n = int(c["first_out"]), int(c["nout"])
+        b, m = int(w["first_out"]), int(w["nout"])
+        g, e = got[a:a + n].copy(), want[b:b + m].copy()
+        g["src"] = e["src"] = -1
+        if g.tobytes() != e.tobytes():
+            k = int(np.nonzero(g != e)[0][0]) if n == m else min(n, m)
+            raise AssertionError("%s: query %d (invocation %d): %d cells, want %d; first difference at %d: "
+                                 "got %s want %s" % (what, i, int(c["invocation"]), n, m, k,
+                                                     g[k] if k < n else None, e[k] if k < m else None))
+        gp, ep = probs[a:a + n], want_probs[b:b + m]
+        if gp.tobytes() != ep.tobytes():
+            k = int(np.nonzero((gp != ep).any(axis=1))[0][0])
+            raise AssertionError("%s: query %d pair %d: probabilities %s, want %s" % (what, i, k, gp[k], ep[k]))
+
+
+@pytest.mark.parametrize("name", PIPE_NAMES)
+def test_stage3_path_compute_cpu_matches_reference(golden_dir, tmp_path, name):
+    """path_compute from pass 2A to its return value (passes 2A-10: the dual
+    breaks at the ends, the adjacent indels, the end extensions,
+    assign_gap_types with its MaxEnt probabilities and the noncanonical
+    end-exon trims; gsnapdp_stage3_path_compute) for every recorded
+    invocation, bit for bit: the returned list, every pair's
+    donor_prob / acceptor_prob, *intronlen, *nonintronlen, *defect_rate and
+    the pass calls made, with the DP families and MaxEnt served by the oracle
+    under ASan + UBSan"""
+    from gsnapdp.records import S3_COMPUTE_STATS, S3_CALL, S3_PAIR
+    z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    queries, pin, q, qu, want, want_probs, final = W.stage3_path_pipeline(z)
+    assert len(queries) == len(z["pc_calls"])
+    d = str(tmp_path)
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "stage3_cpu"])
+    queries.tofile(os.path.join(d, "calls.bin"))
+    pin.tofile(os.path.join(d, "pairs_in.bin"))
+    q.tofile(os.path.join(d, "query.bin"))
+    qu.tofile(os.path.join(d, "query_uc.bin"))
+    z["blocks"].astype("<u4").tofile(os.path.join(d, "genome.u32"))
+    write_stage2(d, z)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               GSNAPDP_MAXENT_TABLES=os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin"))
+    maxintron = int(final["maxintronlen_bound"][0])
+    p = subprocess.run([os.path.join(ROOT, "oracle", "_build", "stage3_cpu"), d, "--path-compute", "9",
+                        str(maxintron)], env=env, capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, "stage3_cpu --path-compute failed (%d):\n%s" % (p.returncode, p.stderr[-6000:])
+    assert "runtime error" not in p.stderr, p.stderr[-6000:]
+    got_calls = np.fromfile(os.path.join(d, "pass_calls.bin"), dtype=S3_CALL)
+    got = np.fromfile(os.path.join(d, "pass_pairs.bin"), dtype=S3_PAIR)
+    probs = np.fromfile(os.path.join(d, "pass_probs.bin"), dtype=np.float64).reshape(-1, 2)
+    check_path_compute(got_calls, got, probs, want, want_probs, final, name)
+    cs = np.fromfile(os.path.join(d, "compute_stats.bin"), dtype=S3_COMPUTE_STATS)[0]
+    assert list(cs["pass_calls"]) == list(final["passes"].sum(axis=0)), (cs["pass_calls"], final["passes"].sum(0))
+    assert cs["sites"] > 0

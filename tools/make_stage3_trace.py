@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.join(ROOT, "gmap-gsnap_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import gen_golden as G  # noqa: E402
 from gsnapdp import workload as W  # noqa: E402
-from gsnapdp.records import PC_CALL, S2_CALL, S3_PAIR  # noqa: E402
+from gsnapdp.records import S2_CALL, S3_PAIR  # noqa: E402
 
 
 def main():
@@ -41,7 +41,7 @@ def main():
         np.savez_compressed(out, blocks=blocks, ncalls_traced=np.int32(c.size),
                             s2_calls=np.fromfile(os.path.join(t, "stage2_calls.bin"), dtype=S2_CALL),
                             s2_pairs=np.fromfile(os.path.join(t, "stage2_pairs.bin"), dtype=S3_PAIR),
-                            pc_calls=np.fromfile(os.path.join(t, "path_compute.bin"), dtype=PC_CALL), **dd)
+                            **dict(zip(("pc_calls", "pc_pairs", "pc_probs"), G.path_compute_trace(t))), **dd)
     print("%s: %d cDNAs, %d pass calls (by pass %s), %d path pairs, reference %.3f s" %
           (out, len(qs), c.size, np.bincount(c["pass"], minlength=6).tolist(), dd["pairs_in"].size,
            float(c["ref_seconds"].sum())))
