@@ -429,28 +429,174 @@ int changepoint_right(int* nmatches_right, int* ntotal_right, const std::vector<
   }
   return edge;
 }
-// Pbinom (pbinom.c:1680, GSL's binomial CDF P(X <= k)): only compared with
-// TRIM_END_PVALUE here, so it is computed as an exact sum of the terms in
-// long double (log-space), not with GSL's incomplete-beta continued fraction
-double pbinom(int k, int n, double theta) {
-  if (k >= n) return 1.0;
-  if (k < 0) return 0.0;
-  const long double lt = logl((long double)theta), l1t = log1pl(-(long double)theta);
-  long double mx = -INFINITY, sum = 0.0L;
-  std::vector<long double> terms((size_t)k + 1);
-  for (int i = 0; i <= k; i++) {
-    const long double t = lgammal((long double)n + 1) - lgammal((long double)i + 1) - lgammal((long double)(n - i) + 1) +
-                          (theta > 0 ? (long double)i * lt : (i ? -INFINITY : 0.0L)) +
-                          (theta < 1 ? (long double)(n - i) * l1t : (n - i ? -INFINITY : 0.0L));
-    terms[(size_t)i] = t;
-    if (t > mx) mx = t;
+// ---- Pbinom (pbinom.c:1680): GSL 1.8's binomial CDF P(X <= k) as the
+// reference carries it (gsl_cdf_binomial_P :1634 -> gsl_cdf_beta_Q :1617 ->
+// beta_inc_AXPY :1563, beta_cont_frac :1465, gsl_sf_lnbeta :1419), restated for
+// the arguments chop_ends_by_changepoint passes: a = k + 1 and b = n - k are
+// integers >= 1 and 0.1 <= theta < 1, so lngamma is the Lanczos sum (or exactly 0
+// at 1 and 2, :1146-1160) and gammastar its Chebyshev / Stirling branches for
+// x >= 1 (:1315-1350).  The operations are the reference's, in its order, so the
+// doubles are its doubles; tests/test_pbinom.py compares them bit for bit with
+// the reference's own pbinom.c.
+constexpr double PB_EPS = 2.2204460492503131e-16, PB_DBL_MIN = 2.2250738585072014e-308;
+constexpr double PB_ROOT4_EPS = 1.2207031250000000e-04, PB_ROOT6_EPS = 2.4607833005759251e-03;
+constexpr double PB_E = 2.71828182845904523536028747135, PB_SQRT2 = 1.41421356237309504880168872421;
+constexpr double PB_SQRTPI = 1.77245385090551602729816748334, PB_LOGROOT2PI = 0.9189385332046727418;
+
+// the Chebyshev series (coefficients c[0..order], interval [-1, 1]) by Clenshaw's recurrence (:146-168)
+double pb_cheb(const double* c, int order, double x) {
+  double d = 0.0, dd = 0.0;
+  const double y = (2.0 * x - -1.0 - 1.0) / (1.0 - -1.0), y2 = 2.0 * y;
+  for (int j = order; j >= 1; j--) {
+    const double t = d;
+    d = y2 * d - dd + c[j];
+    dd = t;
   }
-  if (mx == -INFINITY) return 0.0;
-  for (long double t : terms) sum += expl(t - mx);
-  return (double)(expl(mx) * sum);
+  return y * d - dd + 0.5 * c[0];
 }
-List chop_ends_by_changepoint(List pairs) {
-  if (pairs.empty()) return pairs;
+// Lanczos coefficients, gamma = 7, kmax = 8 (:650-659)
+const double PB_LANCZOS[9] = {0.99999999999980993227684700473478,  676.520368121885098567009190444019,
+                              -1259.13921672240287047156078755283, 771.3234287776530788486528258894,
+                              -176.61502916214059906584551354,     12.507343278686904814458936853,
+                              -0.13857109526572011689554707,       9.984369578019570859563e-6,
+                              1.50563273514931155834e-7};
+double pb_lngamma(double x) {  // x >= 1 (:1146-1160, :661-678)
+  if (fabs(x - 1.0) < 0.01 || fabs(x - 2.0) < 0.01) return 0.0 * x;  // the Pade forms at eps = 0: exactly 0
+  x -= 1.0;
+  double ag = PB_LANCZOS[0];
+  for (int k = 1; k <= 8; k++) ag += PB_LANCZOS[k] / (x + k);
+  const double t1 = (x + 0.5) * log((x + 7.5) / PB_E);
+  const double t2 = PB_LOGROOT2PI + log(ag);
+  return t1 + (t2 - 7.0);
+}
+// Gamma*(x) Chebyshev data for [0.5, 2) and [2, 10) (:1187-1260)
+const double PB_GSTAR_A[30] = {
+    2.16786447866463034423060819465,     -0.05533249018745584258035832802,    0.01800392431460719960888319748,
+    -0.00580919269468937714480019814,    0.00186523689488400339978881560,     -0.00059746524113955531852595159,
+    0.00019125169907783353925426722,     -0.00006124996546944685735909697,    0.00001963889633130842586440945,
+    -6.3067741254637180272515795142e-06, 2.0288698405861392526872789863e-06,  -6.5384896660838465981983750582e-07,
+    2.1108698058908865476480734911e-07,  -6.8260714912274941677892994580e-08, 2.2108560875880560555583978510e-08,
+    -7.1710331930255456643627187187e-09, 2.3290892983985406754602564745e-09,  -7.5740371598505586754890405359e-10,
+    2.4658267222594334398525312084e-10,  -8.0362243171659883803428749516e-11, 2.6215616826341594653521346229e-11,
+    -8.5596155025948750540420068109e-12, 2.7970831499487963614315315444e-12,  -9.1471771211886202805502562414e-13,
+    2.9934720198063397094916415927e-13,  -9.8026575909753445931073620469e-14, 3.2116773667767153777571410671e-14,
+    -1.0518035333878147029650507254e-14, 3.4144405720185253938994854173e-15,  -1.0115153943081187052322643819e-15};
+const double PB_GSTAR_B[30] = {
+    0.0057502277273114339831606096782,   0.0004496689534965685038254147807,   -0.0001672763153188717308905047405,
+    0.0000615137014913154794776670946,   -0.0000223726551711525016380862195,  8.0507405356647954540694800545e-06,
+    -2.8671077107583395569766746448e-06, 1.0106727053742747568362254106e-06,  -3.5265558477595061262310873482e-07,
+    1.2179216046419401193247254591e-07,  -4.1619640180795366971160162267e-08, 1.4066283500795206892487241294e-08,
+    -4.6982570380537099016106141654e-09, 1.5491248664620612686423108936e-09,  -5.0340936319394885789686867772e-10,
+    1.6084448673736032249959475006e-10,  -5.0349733196835456497619787559e-11, 1.5357154939762136997591808461e-11,
+    -4.5233809655775649997667176224e-12, 1.2664429179254447281068538964e-12,  -3.2648287937449326771785041692e-13,
+    7.1528272726086133795579071407e-14,  -9.4831735252566034505739531258e-15, -2.3124001991413207293120906691e-15,
+    2.8406613277170391482590129474e-15,  -1.7245370321618816421281770927e-15, 8.6507923128671112154695006592e-16,
+    -3.9506563665427555895391869919e-16, 1.6779342132074761078792361165e-16,  -6.0483153034414765129837716260e-17};
+double pb_gammastar(double x) {  // x >= 1 (:1315-1350; the x < 0.5 branch is not reached)
+  if (x < 2.0) return pb_cheb(PB_GSTAR_A, 29, 4.0 / 3.0 * (x - 0.5) - 1.0);
+  if (x < 10.0) return pb_cheb(PB_GSTAR_B, 29, 0.25 * (x - 2.0) - 1.0) / (x * x) + 1.0 + 1.0 / (12.0 * x);
+  if (x < 1.0 / PB_ROOT4_EPS) {  // the Stirling series of the log correction (:1295-1311)
+    const double y = 1.0 / (x * x);
+    const double c0 = 1.0 / 12.0, c1 = -1.0 / 360.0, c2 = 1.0 / 1260.0, c3 = -1.0 / 1680.0, c4 = 1.0 / 1188.0,
+                 c5 = -691.0 / 360360.0, c6 = 1.0 / 156.0, c7 = -3617.0 / 122400.0;
+    const double ser = c0 + y * (c1 + y * (c2 + y * (c3 + y * (c4 + y * (c5 + y * (c6 + y * c7))))));
+    return exp(ser / x);
+  }
+  if (x < 1.0 / PB_EPS) {
+    const double xi = 1.0 / x;
+    return 1.0 + xi / 12.0 * (1.0 + xi / 24.0 * (1.0 - xi * (139.0 / 180.0 + 571.0 / 8640.0 * xi)));
+  }
+  return 1.0;
+}
+// log(1 + x)/x Chebyshev data (:1363-1386)
+const double PB_LOPX[21] = {
+    2.16647910664395270521272590407,     -0.28565398551049742084877469679,    0.01517767255690553732382488171,
+    -0.00200215904941415466274422081,    0.00019211375164056698287947962,     -0.00002553258886105542567601400,
+    2.9004512660400621301999384544e-06,  -3.8873813517057343800270917900e-07, 4.7743678729400456026672697926e-08,
+    -6.4501969776090319441714445454e-09, 8.2751976628812389601561347296e-10,  -1.1260499376492049411710290413e-10,
+    1.4844576692270934446023686322e-11,  -2.0328515972462118942821556033e-12, 2.7291231220549214896095654769e-13,
+    -3.7581977830387938294437434651e-14, 5.1107345870861673561462339876e-15,  -7.0722150011433276578323272272e-16,
+    9.7089758328248469219003866867e-17,  -1.3492637457521938883731579510e-17, 1.8657327910677296608121390705e-18};
+double pb_log1plusx(double x) {  // 0 < x < 0.2 here (:1389-1414)
+  if (fabs(x) < PB_ROOT6_EPS) {
+    const double c1 = -0.5, c2 = 1.0 / 3.0, c3 = -1.0 / 4.0, c4 = 1.0 / 5.0, c5 = -1.0 / 6.0, c6 = 1.0 / 7.0,
+                 c7 = -1.0 / 8.0, c8 = 1.0 / 9.0, c9 = -1.0 / 10.0;
+    const double t = c5 + x * (c6 + x * (c7 + x * (c8 + x * c9)));
+    return x * (1.0 + x * (c1 + x * (c2 + x * (c3 + x * (c4 + x * t)))));
+  }
+  if (fabs(x) < 0.5) return x * pb_cheb(PB_LOPX, 20, 0.5 * (8.0 * x + 1.0) / (x + 2.0));
+  return log(1.0 + x);
+}
+double pb_lnbeta(double x, double y) {  // x, y >= 1 (:1419-1458)
+  const double max = x > y ? x : y, min = x < y ? x : y, rat = min / max;
+  if (rat < 0.2) {  // min << max: through Gamma*
+    const double gsx = pb_gammastar(x), gsy = pb_gammastar(y), gsxy = pb_gammastar(x + y);
+    const double lnopr = pb_log1plusx(rat);
+    const double lnpre = log(gsx * gsy / gsxy * PB_SQRT2 * PB_SQRTPI);
+    const double t1 = min * log(rat), t2 = 0.5 * log(min), t3 = (x + y - 0.5) * lnopr;
+    return lnpre + (t1 - t2 - t3);
+  }
+  return pb_lngamma(x) + pb_lngamma(y) - pb_lngamma(x + y);
+}
+// the continued fraction of the incomplete beta function (:1465-1557); false
+// where the reference aborts
+bool pb_cont_frac(double a, double b, double x, double epsabs, double* cf_out) {
+  const double cutoff = 2.0 * PB_DBL_MIN;
+  double num = 1.0, den = 1.0 - (a + b) * x / (a + 1.0);
+  if (fabs(den) < cutoff) return false;
+  den = 1.0 / den;
+  double cf = den;
+  unsigned iter = 0;
+  for (; iter < 512; iter++) {
+    const int k = (int)iter + 1;
+    double coeff = k * (b - k) * x / (((a - 1.0) + 2 * k) * (a + 2 * k));
+    den = 1.0 + coeff * den;
+    num = 1.0 + coeff / num;
+    if (fabs(den) < cutoff || fabs(num) < cutoff) return false;
+    den = 1.0 / den;
+    double delta = den * num;
+    cf *= delta;
+    coeff = -(a + k) * (a + b + k) * x / ((a + 2 * k) * (a + 2 * k + 1.0));
+    den = 1.0 + coeff * den;
+    num = 1.0 + coeff / num;
+    if (fabs(den) < cutoff || fabs(num) < cutoff) return false;
+    den = 1.0 / den;
+    delta = den * num;
+    cf *= delta;
+    if (fabs(delta - 1.0) < 2.0 * PB_EPS) break;
+    if (cf * fabs(delta - 1.0) < epsabs) break;
+  }
+  if (iter >= 512) return false;
+  *cf_out = cf;
+  return true;
+}
+// Pbinom(k, n, theta) = gsl_cdf_binomial_P(k, theta, n) (k and n as the
+// reference's unsigned ints) = gsl_cdf_beta_Q(theta, k + 1, n - k) =
+// beta_inc_AXPY(-1, 1, a, b, theta); false where the reference aborts
+bool pbinom(int k, int n, double theta, double* p) {
+  if (theta > 1.0 || theta < 0.0) return false;
+  if ((unsigned)k >= (unsigned)n) return *p = 1.0, true;
+  const double a = (double)(unsigned)k + 1.0, b = (double)(unsigned)n - (unsigned)k, x = theta;
+  if (x >= 1.0) return *p = 0.0, true;
+  if (x <= 0.0) return *p = 1.0, true;
+  if (a < 1.0 || b < 1.0) return false;  // (not reached: unsigned k < n)
+  const double A = -1.0, Y = 1.0;
+  const double ln_pre = -pb_lnbeta(a, b) + a * log(x) + b * log1p(-x);
+  const double prefactor = exp(ln_pre);
+  double cf;
+  if (x < (a + 1.0) / (a + b + 2.0)) {
+    const double epsabs = fabs(Y / (A * prefactor / a)) * PB_EPS;
+    if (!pb_cont_frac(a, b, x, epsabs, &cf)) return false;
+    *p = A * (prefactor * cf / a) + Y;
+  } else {
+    const double epsabs = fabs((A + Y) / (A * prefactor / b)) * PB_EPS;
+    if (!pb_cont_frac(b, a, 1.0 - x, epsabs, &cf)) return false;
+    *p = -A * (prefactor * cf / b);  // A == -Y
+  }
+  return true;
+}
+bool chop_ends_by_changepoint(List& pairs, std::string* err) {
+  if (pairs.empty()) return true;
   // Pair_matchscores_list (pair.c:5785-5818)
   std::vector<int> ms;
   ms.reserve(pairs.size());
@@ -476,15 +622,22 @@ List chop_ends_by_changepoint(List pairs) {
     else side = ntl < ntr ? -1 : +1;  // the shorter side
     if (side == -1) chop_left(pairs);
     else chop_right(pairs);
-    return pairs;
+    return true;
   }
   auto theta_of = [&](int m, int t) {
     double theta = (double)(nmatches - m) / (double)(ntotal - t) - THETA_SLACK;
     return theta < 0.10 ? 0.10 : theta;
   };
-  if (!(ntl == 0 || ntotal - ntl <= 0) && !(pbinom(nml, ntl, theta_of(nml, ntl)) > TRIM_END_PVALUE)) chop_left(pairs);
-  if (!(ntr == 0 || ntotal - ntr <= 0) && !(pbinom(nmr, ntr, theta_of(nmr, ntr)) > TRIM_END_PVALUE)) chop_right(pairs);
-  return pairs;
+  double p;
+  if (!(ntl == 0 || ntotal - ntl <= 0)) {
+    if (!pbinom(nml, ntl, theta_of(nml, ntl), &p)) return *err = "Pbinom: the reference aborts", false;
+    if (!(p > TRIM_END_PVALUE)) chop_left(pairs);
+  }
+  if (!(ntr == 0 || ntotal - ntr <= 0)) {
+    if (!pbinom(nmr, ntr, theta_of(nmr, ntr), &p)) return *err = "Pbinom: the reference aborts", false;
+    if (!(p > TRIM_END_PVALUE)) chop_right(pairs);
+  }
+  return true;
 }
 
 // ---- filter_goodness_hmm / filter_indels_hmm (stage3.c:8166-8339): the
@@ -1136,7 +1289,7 @@ void advance(Query& q, const Env& E) {
     q.step = Q_3B;  // (as if 3b had run: 3c's loop next)
   }
   // 3b': chop_ends_by_changepoint; 4: the HMM filters on a fresh defect rate
-  pairs = chop_ends_by_changepoint(std::move(pairs));
+  if (!chop_ends_by_changepoint(pairs, &err)) return fail(q, err);
   if (!defect_rate(pairs, &q.defect, &err)) return fail(q, err);
   pairs = viterbi_filter(pairs, true, q.defect);
   pairs = viterbi_filter(pairs, false, 0.0);
@@ -1424,3 +1577,6 @@ extern "C" int gsnapdp_stage3_path_compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* qu
   return compute(ctx, queries, nqueries, paths_in, npairs_in, query, query_uc, query_bytes, iit, env, out, out_cap,
                  probs_out, stats);
 }
+
+// Pbinom as chop_ends_by_changepoint computes it (host; tests/test_pbinom.py)
+extern "C" int gsnapdp_pbinom(int k, int n, double theta, double* p) { return pbinom(k, n, theta, p) ? 0 : -1; }

@@ -783,6 +783,12 @@ int gsnapdp_stage3_path_compute(gsnapdp_ctx *ctx, gsnapdp_s3_call *queries, int 
                                 const gsnapdp_s3_path_opts *opts, gsnapdp_s3_pair *out, int64_t out_cap,
                                 double *probs_out, gsnapdp_s3_compute_stats *stats);
 
+/* Host-only: Pbinom (pbinom.c:1680, GSL 1.8's binomial CDF through the
+ * incomplete beta function) as chop_ends_by_changepoint calls it (stage3.c:2130:
+ * k <= n, theta in [0.1, 1)), bit for bit the reference's double.  Returns 0, or
+ * -1 where the reference aborts. */
+int gsnapdp_pbinom(int k, int n, double theta, double *p);
+
 /* score_introns (stage3.c:7935-8162) on the lists a pass returned: for every
  * call with status 0, its list reversed into path order (as stage3_compute
  * reverses path_compute's pairs, :9890-9941), the introns picked on the host
