@@ -30,7 +30,8 @@ int gsnapdp__rows_pools(gsnapdp_ctx* ctx);
 int gsnapdp__gband_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_ggap_window* d_windows,
                           const int* lists, const int* counts, int list_cap, const char* d_query,
                           const char* d_query_uc, gsnapdp_ggap_result* d_results,
-                          gsnapdp_ggap_trace* d_traces, uint32_t* d_ops, const int64_t* d_op_offsets);
+                          gsnapdp_ggap_trace* d_traces, uint32_t* d_ops, const int64_t* d_op_offsets,
+                          int use_band);
 
 #define HIPCHK(x)                                                                        \
   do {                                                                                   \
@@ -79,7 +80,8 @@ struct gsnapdp_ctx {
   int* d_ggap_lists = nullptr;     // per-class window lists, GG_NLISTS x ggap_cap
   int* d_ggap_counts = nullptr;    // per-class counts
   uint32_t* d_ggap_pool = nullptr; // global scratch of the large-window path
-  uint32_t* d_gband_pool = nullptr; // per-wave scratch of the register-band path (k_gband)
+  uint32_t* d_gband_pool = nullptr; // per-wave scratch of the register-band path (k_gband), score mode
+  uint32_t* d_gband_pool_prob = nullptr;  // the same with probability mode's part (first use)
   int ggap_rowlane_only = 0;        // GSNAPDP_GGAP_ROWLANE=1: every window on k_ggap (A/B tests)
   int ggap_use_band = 1;            // k_ggap_plan's GB_USE_* bits (GSNAPDP_GBAND_PROB=1 sets the prob bit)
   int gband_min = 16384;            // smallest genome-gap batch on the register band (GSNAPDP_GBAND_MIN)

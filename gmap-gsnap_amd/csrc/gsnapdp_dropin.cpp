@@ -749,29 +749,37 @@ int host_exact(void*, int chrnum, uint32_t x, uint32_t y, int sign) {
   static const auto f = resolve_host(&IIT_exists_with_divno_signed, "IIT_exists_with_divno_signed");
   return f(g.iit, g.divint_crosstable[chrnum], x, y, sign) ? 1 : 0;
 }
-const gsnapdp_iit* host_iit() {
-  static gsnapdp_iit h;
-  h.user = nullptr;
-  h.site_level = g.donor_typeint >= 0 && g.acceptor_typeint >= 0 ? 1 : 0;
-  h.pad = 0;
-  h.typed = host_typed;
-  h.low = host_low;
-  h.high = host_high;
-  h.exact = host_exact;
-  return &h;
+// The host's IIT as the batched ABI asks it: written by Dynprog_setup (before
+// any aligner thread runs), only read by gmap's worker threads.
+gsnapdp_iit g_host_iit;
+void host_iit_setup() {
+  gsnapdp_iit& x = g_host_iit;
+  x.user = nullptr;
+  x.site_level = g.donor_typeint >= 0 && g.acceptor_typeint >= 0 ? 1 : 0;
+  x.pad = 0;
+  x.typed = host_typed;
+  x.low = host_low;
+  x.high = host_high;
+  x.exact = host_exact;
 }
+const gsnapdp_iit* host_iit() { return &g_host_iit; }
 
 // Appends one window's known-site record (left_known[L2L], right_known[L2R],
 // the KNOWN_INTRONS pair list) to `q` at `at` and returns its known_mode.
 int known_site_record(std::vector<char>& q, size_t at, int chrnum, unsigned chrpos,
                       unsigned genomiclength, int leftoffset, int rightoffset, int L2L, int L2R,
                       int cdna_direction, bool watsonp) {
-  const int cap = L2L + L2R + 2 + 4 * L2L * L2R;
-  q.resize(at + (size_t)cap);
-  int len = 0;
-  const int mode = gsnapdp_known_site_record(host_iit(), g.novelsplicingp ? 1 : 0, chrnum, chrpos, genomiclength,
-                                             leftoffset, rightoffset, L2L, L2R, cdna_direction, watsonp ? 1 : 0,
-                                             q.data() + at, cap, &len);
+  // the two site arrays and room for a few known introns; a longer intron list
+  // (KNOWN_INTRONS mode) asks again with the length the first call reported
+  int cap = (int)std::min<size_t>((size_t)L2L + (size_t)L2R + 2 + 4 * 64, 0x7fffffff);
+  int len = 0, mode = -1;
+  for (int tries = 0; tries < 2 && mode < 0; tries++) {
+    q.resize(at + (size_t)cap);
+    mode = gsnapdp_known_site_record(host_iit(), g.novelsplicingp ? 1 : 0, chrnum, chrpos, genomiclength, leftoffset,
+                                     rightoffset, L2L, L2R, cdna_direction, watsonp ? 1 : 0, q.data() + at, cap, &len);
+    if (mode < 0 && len > cap) cap = len;
+    else break;
+  }
   if (mode < 0) fatal(std::string("known-site record: ") + gsnapdp_last_error());
   q.resize(at + (size_t)len + 8, 0);
   return mode;
@@ -875,6 +883,7 @@ void Dynprog_setup(gsnapdp_bool novelsplicingp, gsnapdp_IIT_T splicing_iit,
   g.triecontents_obs = triecontents_obs;
   g.trieoffsets_max = trieoffsets_max;
   g.triecontents_max = triecontents_max;
+  host_iit_setup();
 }
 
 int Dynprog_score(int matches, int mismatches, int qopens, int qindels, int topens, int tindels,
@@ -1694,12 +1703,20 @@ gsnapdp_List_T pass_one(gsnapdp_s3_call& k, gsnapdp_List_T path, char* queryseq_
   thread_local std::vector<int32_t> cells;  // the returned list, compactly
   thread_local std::vector<gsnapdp_s3_pair> news;
   cells.resize((size_t)cap);
-  news.resize((size_t)(2 * (int64_t)k.querylength + 256));
+  news.resize((size_t)cap);  // every new pair is one returned cell
   gsnapdp_s3_stats st;
-  if (gsnapdp_stage3_pass_compact(c, &k, 1, in.data(), (int64_t)in.size(), queryseq_ptr, queryuc_ptr,
-                                  (size_t)k.querylength, iit, cells.data(), cap, news.data(), (int64_t)news.size(),
-                                  &st))
-    fatal(std::string("gsnapdp_stage3_pass_compact: ") + gsnapdp_last_error());
+  const gsnapdp_s3_call k0 = k;
+  int rc = gsnapdp_stage3_pass_compact(c, &k, 1, in.data(), (int64_t)in.size(), queryseq_ptr, queryuc_ptr,
+                                       (size_t)k.querylength, iit, cells.data(), cap, news.data(),
+                                       (int64_t)news.size(), &st);
+  if (rc && st.new_pairs > (int64_t)news.size()) {  // the pass reported what it needs: once more with room
+    k = k0;
+    news.resize((size_t)st.new_pairs);
+    rc = gsnapdp_stage3_pass_compact(c, &k, 1, in.data(), (int64_t)in.size(), queryseq_ptr, queryuc_ptr,
+                                     (size_t)k.querylength, iit, cells.data(), cap, news.data(),
+                                     (int64_t)news.size(), &st);
+  }
+  if (rc) fatal(std::string("gsnapdp_stage3_pass_compact: ") + gsnapdp_last_error());
   if (k.status) fatal(std::string(what) + ": a window outside the reference's domain (the reference aborts)");
   gsnapdp_List_T list = nullptr;
   for (int i = k.nout - 1; i >= 0; i--) {

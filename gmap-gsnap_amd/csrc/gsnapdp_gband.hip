@@ -1086,7 +1086,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GB_WAVES_PE
     const int* __restrict__ counts, int list_cap, const char* __restrict__ q,
     const char* __restrict__ qu, const uint32_t* __restrict__ blocks, uint64_t nwords,
     const uint32_t* __restrict__ prof, const double* __restrict__ tables, uint32_t* __restrict__ pool,
-    gsnapdp_ggap_result* __restrict__ res, gsnapdp_ggap_trace* __restrict__ trc,
+    uint32_t wave_dw, gsnapdp_ggap_result* __restrict__ res, gsnapdp_ggap_trace* __restrict__ trc,
     uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
   __shared__ alignas(8) uint32_t sprof[SPROF_WORDS];
   __shared__ uint32_t rings[4][GB_RING_WORDS];
@@ -1101,7 +1101,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GB_WAVES_PE
   uint32_t* ring = rings[threadIdx.x >> 6];
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nw = (gridDim.x * blockDim.x) >> 6;
-  uint32_t* wpool = pool + (size_t)gw * GB_WAVE_DW;
+  uint32_t* wpool = pool + (size_t)gw * wave_dw;  // GB_OCV dwords, or GB_WAVE_DW with probability-mode lists
   // tasks of list pair k: score mode for k < NCLASS - 1, then probability mode
   // (band class k % (NCLASS - 1) + 1 of k_fill's table), both tie-rule lists
   static_assert(GP_LIST0 == GB_LIST0 + 2 * (NCLASS - 1), "k_gband's list pairs");
@@ -1146,9 +1146,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GB_WAVES_PE
 int gsnapdp__gband_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_ggap_window* d_windows,
                           const int* lists, const int* counts, int list_cap, const char* d_query,
                           const char* d_query_uc, gsnapdp_ggap_result* d_results,
-                          gsnapdp_ggap_trace* d_traces, uint32_t* d_ops, const int64_t* d_op_offsets) {
+                          gsnapdp_ggap_trace* d_traces, uint32_t* d_ops, const int64_t* d_op_offsets,
+                          int use_band) {
   const int waves = ctx->num_cus * 4 * GB_WAVES_PER_SIMD;
-  if (!ctx->d_gband_pool) HIPCHK(hipMalloc(&ctx->d_gband_pool, (size_t)waves * GB_WAVE_DW * 4));
+  // score mode needs the scratch up to GB_OCV only; probability-mode lists
+  // (use_band & GB_USE_PROB) the whole layout, in a pool of their own made on
+  // first use (1.3 MB per wave against 0.4 MB)
+  const bool prob = (use_band & gsnapdp::GB_USE_PROB) != 0;
+  const uint32_t wave_dw = prob ? (uint32_t)GB_WAVE_DW : (uint32_t)GB_OCV;
+  uint32_t** poolp = prob ? &ctx->d_gband_pool_prob : &ctx->d_gband_pool;
+  if (!*poolp) HIPCHK(hipMalloc(poolp, (size_t)waves * wave_dw * 4));
 #ifdef GB_PHASES
   {
     const char* e = getenv("GSNAPDP_GB_PHASES");
@@ -1158,7 +1165,7 @@ int gsnapdp__gband_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_ggap_w
 #endif
   hipLaunchKernelGGL(k_gband, dim3(waves / 4), dim3(256), 0, st, d_windows, lists, counts, list_cap,
                      d_query, d_query_uc, ctx->d_blocks, (uint64_t)ctx->nwords, ctx->d_prof,
-                     ctx->d_tables, ctx->d_gband_pool, d_results, d_traces, d_ops, d_op_offsets);
+                     ctx->d_tables, *poolp, wave_dw, d_results, d_traces, d_ops, d_op_offsets);
   HIPCHK(hipGetLastError());
 #ifdef GB_CHECK
   {

@@ -1333,7 +1333,7 @@ extern "C" int gsnapdp_ggap_run_device(gsnapdp_ctx* ctx, const gsnapdp_ggap_wind
   gsnapdp__mark(ctx, st, 4, 1);
   gsnapdp__mark(ctx, st, 6, 0);
   if (use_band && gsnapdp__gband_launch(ctx, st, d_windows, lists, counts, cap, d_query, d_query_uc, d_results,
-                                        d_traces, d_ops, d_op_offsets))
+                                        d_traces, d_ops, d_op_offsets, use_band))
     return -1;
   gsnapdp__mark(ctx, st, 6, 1);
   gsnapdp__mark(ctx, st, 5, 0);

@@ -102,8 +102,10 @@ extern "C" int gsnapdp_known_site_record(const gsnapdp_iit* iit, int novelsplici
   const bool sites = iit->site_level != 0;
   const bool fwd = cdna_direction > 0;
   const unsigned gl1 = genomiclength - 1U;
-  int n = L2L + L2R + 2;
-  if (n > cap) return -1;
+  const size_t base = (size_t)L2L + (size_t)L2R + 2;
+  *len = (int)std::min(base, (size_t)0x7fffffff);
+  if (base > (size_t)cap) return -1;
+  int n = (int)base;
   memset(rec, 0, (size_t)n);
   char* left = rec;
   char* right = rec + L2L;
@@ -143,13 +145,16 @@ extern "C" int gsnapdp_known_site_record(const gsnapdp_iit* iit, int novelsplici
                                : iit->exact(iit->user, chrnum, chrpos + gl1 - rightoffset + cR,
                                             chrpos + gl1 - leftoffset - cL + 1U + 1U, -cdna_direction);
         if (!ok) continue;
-        if (npairs == 0xffff || n + 4 > cap) {
+        if (npairs == 0xffff) {
           gsnapdp__set_err("gsnapdp_known_site_record: too many known introns for the record");
+          *len = -1;
           return -1;
         }
-        unsigned char* e = (unsigned char*)rec + n;
-        e[0] = (unsigned char)(cL & 255), e[1] = (unsigned char)(cL >> 8);
-        e[2] = (unsigned char)(cR & 255), e[3] = (unsigned char)(cR >> 8);
+        if (n + 4 <= cap) {  // past cap the pairs are only counted: *len says what the record needs
+          unsigned char* e = (unsigned char*)rec + n;
+          e[0] = (unsigned char)(cL & 255), e[1] = (unsigned char)(cL >> 8);
+          e[2] = (unsigned char)(cR & 255), e[3] = (unsigned char)(cR >> 8);
+        }
         n += 4;
         npairs++;
       }
@@ -158,6 +163,10 @@ extern "C" int gsnapdp_known_site_record(const gsnapdp_iit* iit, int novelsplici
   rec[L2L + L2R] = (char)(npairs & 255);
   rec[L2L + L2R + 1] = (char)(npairs >> 8);
   *len = n;
+  if (n > cap) {
+    gsnapdp__set_err("gsnapdp_known_site_record: the record needs " + std::to_string(n) + " bytes");
+    return -1;
+  }
   return mode;
 }
 

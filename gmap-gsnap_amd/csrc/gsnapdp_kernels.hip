@@ -1109,6 +1109,7 @@ extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   (void)hipFree(ctx->d_ggap_counts);
   (void)hipFree(ctx->d_ggap_pool);
   (void)hipFree(ctx->d_gband_pool);
+  (void)hipFree(ctx->d_gband_pool_prob);
   (void)hipFree(ctx->d_ggap_stage);
   (void)hipFree(ctx->d_sj_win);
   (void)hipFree(ctx->d_stage);

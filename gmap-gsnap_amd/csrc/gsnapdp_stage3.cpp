@@ -575,13 +575,18 @@ bool req_genome(const Pass& P, Path& k, bool prob, int score_threshold, bool hal
   const int L1 = k.queryjump > 0 ? k.queryjump : 0;
   R.cap = 2 * (int64_t)L1 + 2 * (int64_t)(k.genomejump > 0 ? k.genomejump : 0) + 4;
   if (P.iit && L1 > 1 && k.genomejump > 0 && !too_long) {
-    const int rcap = 2 * k.genomejump + 2 + 4 * k.genomejump * k.genomejump;
-    R.q.resize((size_t)L1 + (size_t)rcap);
-    int len = 0;
-    const int mode = gsnapdp_known_site_record(P.iit, c.novelsplicingp, c.chrnum, c.chrpos,
-                                               (uint32_t)c.genomiclength, k.genomedp5, k.genomedp3, k.genomejump,
-                                               k.genomejump, c.cdna_direction, c.watsonp, R.q.data() + L1, rcap,
-                                               &len);
+    // the two site arrays and room for a few known introns; a longer intron list
+    // (KNOWN_INTRONS mode) asks again with the length the first call reported
+    int rcap = (int)std::min<size_t>(2 * (size_t)k.genomejump + 2 + 4 * 64, 0x7fffffff);
+    int len = 0, mode = -1;
+    for (int tries = 0; tries < 2 && mode < 0; tries++) {
+      R.q.resize((size_t)L1 + (size_t)rcap);
+      mode = gsnapdp_known_site_record(P.iit, c.novelsplicingp, c.chrnum, c.chrpos, (uint32_t)c.genomiclength,
+                                       k.genomedp5, k.genomedp3, k.genomejump, k.genomejump, c.cdna_direction,
+                                       c.watsonp, R.q.data() + L1, rcap, &len);
+      if (mode < 0 && len > rcap) rcap = len;
+      else break;
+    }
     if (mode < 0) return false;
     w.known_mode = (uint8_t)mode;
     R.q.resize((((size_t)L1 + (size_t)len + 8) + 3) & ~(size_t)3, 0);

@@ -541,9 +541,10 @@ gsnapdp_iit *gsnapdp_iit_from_intervals(const gsnapdp_iit_interval *intervals, i
 void gsnapdp_iit_free(gsnapdp_iit *iit);
 /* Host-only: one genome-gap window's known-site record (gsnapdp_ggap_window
  * above), asked of `iit` exactly where bridge_intron_gap asks
- * (dynprog.c:3375-3550, 3598-3612).  Writes *len bytes (at most cap; length2L
- * + length2R + 2 + 4 * known introns) and returns the window's known_mode
- * (REWARD with novelsplicingp, else SITES or INTRONS), or -1 if cap is short. */
+ * (dynprog.c:3375-3550, 3598-3612).  Writes *len bytes (length2L + length2R
+ * + 2 + 4 * known introns) and returns the window's known_mode (REWARD with
+ * novelsplicingp, else SITES or INTRONS); or -1 when cap is short, with *len
+ * the bytes the record needs (-1 for an error). */
 int gsnapdp_known_site_record(const gsnapdp_iit *iit, int novelsplicingp, int chrnum, uint32_t chrpos,
                               uint32_t genomiclength, int offset2L, int revoffset2R, int length2L, int length2R,
                               int cdna_direction, int watsonp, char *rec, int cap, int *len);
