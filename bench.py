@@ -42,6 +42,7 @@ HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # SIMD (fp32 FMA issues at 2 cycles): 256 CU x 4 SIMD x 16 lanes x 2.4 GHz
 VALU_INT32_PEAK = 256 * 4 * 16 * 2.4e9
 OPS_PER_CELL = 14             # gap1 4 + gap2 4 + nogap 6 int32 ops
+XGMI_LINK_GBS = 153.0         # one xGMI link per peer (7 links x ~153 GB/s per GPU, nominal)
 C3_READS = 1_000_000          # BASELINE config 3: one fixed batch, split across the GPUs
 C2_READS = 100_000            # side line: BASELINE config 2
 GENOME_NT = 64_000_000        # side-line genome (C2, C4, C5, ...)
@@ -643,6 +644,63 @@ def payload_budget(ranks, payload_header: np.ndarray, layout) -> int:
     return 0 if need <= layout.budget else int(need * 1.25) + 1024
 
 
+def measure_slices(ctx, batch, cells, dev, sp, t1_ms, steps=20, warmup=3, xgmi_gbs=XGMI_LINK_GBS):
+    """The N = 2, 4, 8 step of the fixed batch, projected from one GPU: every
+    rank's slice (shard.balanced_ranges, as bench.py --gpus N cuts it) run
+    through the per-rank step itself -- k_plan / k_scan / k_scatter, k_fill,
+    k_rows, and the op-stream compaction into the payload -- timed like the
+    bench's step (K steps between two synchronisations), k_fill by HIP events.  A step of N ranks takes its slowest slice;
+    the RCCL gather of the N - 1 remote payloads into rank 0 (bytes measured
+    here) is asynchronous in the step and overlaps the next one, and is
+    bounded below at one xGMI link per peer.  projected = T(1) / T(N)."""
+    out = {"method": "per-rank step on each slice of the fixed batch, one GPU, K steps between synchronisations; "
+                     "gather overlapped (payload bytes and their one-link time reported beside)",
+           "t1_ms": round(t1_ms, 4), "slices": {}}
+    for N in (2, 4, 8):
+        worst, fill_worst, pay_bytes = 0.0, 0.0, 0
+        per = []
+        for r in range(N):
+            wl, ql, sizes, lo, hi = shard_slice(batch, cells, N, r)
+            n = hi - lo
+            off = op_offsets(wl)
+            d_w = torch.from_numpy(wl.view(np.uint8).copy()).to(dev)
+            d_q = torch.from_numpy(ql.copy()).to(dev)
+            d_off = torch.from_numpy(off.copy()).to(dev)
+            d_ops = torch.zeros(int(off[-1]) + 1, dtype=torch.int32, device=dev)
+            lay = gather.Layout(max(sizes), gather.op_budget(max(sizes)))
+            payb = torch.zeros(lay.nbytes, dtype=torch.uint8, device=dev)
+            base = payb.data_ptr()
+
+            def step():
+                ctx.run_device(d_w.data_ptr(), n, d_q.data_ptr(), d_q.data_ptr(), base + lay.res_off,
+                               d_ops.data_ptr(), d_off.data_ptr(), stream=sp)
+                ctx.compact_ops_device(base + lay.res_off, n, d_ops.data_ptr(), d_off.data_ptr(),
+                                       base + lay.ops_off, lay.budget, base, stream=sp)
+            ms = 1000.0 * timed(step, ctx.sync, steps, warmup) / steps
+            names = ctx.profile(True)
+            acc = np.zeros(len(names))
+            for _ in range(steps):
+                step()
+                ctx.profile_read(acc)
+            ctx.profile(False)
+            fill = float(sum(acc[i] for i, nm in enumerate(names) if nm.startswith("k_fill"))) / steps
+            nops = int(payb[:gather.HEADER].cpu().numpy().view(np.int64)[0])
+            pay_bytes = max(pay_bytes, gather.HEADER + n * RESULT.itemsize + 4 * nops)
+            per.append(round(ms, 4))
+            if ms > worst:
+                worst, fill_worst = ms, fill
+        gather_ms = pay_bytes / (xgmi_gbs * 1e9) * 1e3
+        out["slices"][str(N)] = {"reads_per_rank": int(len(batch) // N), "slice_ms": per,
+                                 "step_ms": round(worst, 4), "k_fill_ms": round(fill_worst, 4),
+                                 "fixed_ms": round(worst - fill_worst, 4),
+                                 "fixed_frac": round((worst - fill_worst) / worst, 4),
+                                 "payload_bytes_per_rank": pay_bytes,
+                                 "gather_one_link_ms": round(gather_ms, 4),
+                                 "projected_scaling": round(t1_ms / worst, 3),
+                                 "projected_scaling_gather_unoverlapped": round(t1_ms / (worst + gather_ms), 3)}
+    return out
+
+
 def relaunch_if_needed(args) -> None:
     """--gpus N > 1 without a launcher: run this script under
     torch.distributed.run as a child (before anything touches the GPU) and
@@ -679,6 +737,7 @@ def main() -> None:
                     help="transcripts in the C4 final-pass line (BASELINE: 50k)")
     ap.add_argument("--no-c4t", action="store_true", help="skip the C4 transcript line")
     ap.add_argument("--no-steady", action="store_true", help="skip the >= 1 s steady-state figure (profiling runs)")
+    ap.add_argument("--no-slices", action="store_true", help="skip the N = 2/4/8 slice projection")
     args = ap.parse_args()
     relaunch_if_needed(args)
 
@@ -873,6 +932,8 @@ def main() -> None:
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        if world == 1 and not args.no_slices and not args.no_side:
+            out["projected_scaling"] = measure_slices(ctx, batch, cells, dev, sp, ms_per_step)
         if world == 1 and not args.no_side:
             genome = W.synthetic_genome(GENOME_NT, seed=1)
             out["c2"] = measure_c2(genome, C2_READS, 20, args.warmup, dev)

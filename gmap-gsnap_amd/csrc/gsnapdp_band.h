@@ -223,7 +223,9 @@ __device__ unsigned long long tb_prof[8];
 // MATCH = false (k_fill): no match bytes; every diagonal step inside the
 // window's genome is counted in nmismatches, and k_count splits the total into
 // matches and mismatches afterwards from the op stream.
-template <int S, int LPW, bool MATCH = true>
+// PL: the bit stride of the direction planes in a lane's word (S: packed, the
+// k_gband fills; 8: one byte per plane, k_fill's v_perm_b32 assembly)
+template <int S, int LPW, bool MATCH = true, int PL = S>
 __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint8_t* __restrict__ M,
                                       int g, int r, int cstart, int maxC, int lband, int rband,
                                       int stop, int cvlo, int cvhi, int JL, const Lane& L,
@@ -269,7 +271,7 @@ __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint
       const int sg = stop + rr - c + rband;
       const int jr = sg / S, sl = sg - jr * S;
       const uint32_t x = (jr == jw) ? wk : ldw(c, jr);
-      return ((x >> (plane * S + S - 1 - sl)) & 1u) ^ jlbit;
+      return ((x >> (plane * PL + S - 1 - sl)) & 1u) ^ jlbit;
     };
     if (st == T_WAIT && c == cstart) {
       st = T_DIAG;
@@ -330,10 +332,10 @@ __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint
           }
         }
         ow.run++;
-        if (((x >> (3 * S)) & 1u) ^ jlbit) {  // v1: VERT
+        if (((x >> (3 * PL)) & 1u) ^ jlbit) {  // v1: VERT
           st = T_VERT;
           dist = 1;
-        } else if (((x >> (2 * S)) & 1u) ^ jlbit) {  // h1: HORIZ
+        } else if (((x >> (2 * PL)) & 1u) ^ jlbit) {  // h1: HORIZ
           st = T_HORIZ;
           dist = 1;
         }
@@ -369,7 +371,7 @@ __device__ inline void band_traceback(const uint32_t* __restrict__ D, const uint
         const uint32_t x2 = (ga.w[2] ^ invall) >> pb, x3 = (ga.w[3] ^ invall) >> pb;
         const bool inside = c - 3 >= cvlo && c <= cvhi;
         const bool outside = c < cvlo || c - 3 > cvhi;
-        const uint32_t vh = (1u << (2 * S)) | (1u << (3 * S));  // h1 and v1 of this slot
+        const uint32_t vh = (1u << (2 * PL)) | (1u << (3 * PL));  // h1 and v1 of this slot
         fast4 = ((x0 | x1 | x2 | x3) & vh) == 0u && (inside || outside);
         if (fast4) {
           if (!MATCH && inside) {

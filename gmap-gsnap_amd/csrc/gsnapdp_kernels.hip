@@ -263,6 +263,13 @@ __global__ void k_scatter(const int* __restrict__ keys, int n, int* __restrict__
 #define GSNAPDP_TB_BATCH 4
 #endif
 constexpr int TB_BATCH = GSNAPDP_TB_BATCH;
+// GSNAPDP_PERMBITS: the direction bits by v_perm_b32 (one byte per plane) instead
+// of four alignbit pushes per cell
+#ifndef GSNAPDP_PERMBITS
+#define GSNAPDP_PERMBITS 0
+#endif
+constexpr int FILL_PL = GSNAPDP_PERMBITS ? 8 : 0;  // the plane stride (0: S)
+[[maybe_unused]] constexpr uint32_t PERM_SIGNS = 0x0B0A0908u;  // result bytes 0..3 = signs of bytes 1, 3, 5, 7
 constexpr size_t FILL_COLS_DEV = (size_t)FAST_L2MAX + 4;
 constexpr size_t FILL_REGION_DW = FILL_COLS_DEV * 64 + FILL_COLS_DEV * 16;
 
@@ -511,6 +518,7 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
     }
     // four bit planes (v1, h1, dF, dE), each a short independent chain
     uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u, gsh = 0u;
+    [[maybe_unused]] uint32_t bits = 0u;  // GSNAPDP_PERMBITS: the four planes, one byte each
     int bstep = END == 2 ? 0 : -(1 << 30);  // END: this column's best scan key (END 2: value), less R(c)
     auto cell = [&](int s, FV Hr, FV Er) {
       const FV Hd = H[s], Ed = E[s], Fd = F[s];
@@ -530,10 +538,36 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
       const int dh = JL ? (int)(Ed - Hd) : (int)(Hd - Ed);  // h1: nogap from gap1
       const int df = JL ? (int)(fp - b) : (int)(b - fp);    // dF: gap2 extends
       const int de = JL ? (int)(Er - a) : (int)(a - Er);    // dE: gap1 extends
+#if GSNAPDP_PERMBITS
+      // the cell's four signs in one dword: (dh, dv) and (de, df) as the low and
+      // high halves of two 16-bit difference pairs (|difference| < 2^15, so bit
+      // 15 of each half is its sign), v_perm_b32 selectors 8-11 spread the four
+      // sign bits over the four bytes (plane p in byte p), and one and-or keeps
+      // bit S-1-s of each byte: the layout the four pushes built, at byte stride
+      {
+        uint32_t p01, p23, sg;
+        asm("v_sub_u16 %0, %1, %2" : "=v"(p01) : "v"(JL ? Ed : Hd), "v"(JL ? Hd : Ed));
+        asm("v_sub_u16_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
+            : "+v"(p01)
+            : "v"(JL ? Fd : m1), "v"(JL ? m1 : Fd));
+        asm("v_sub_u16 %0, %1, %2" : "=v"(p23) : "v"(JL ? Er : a), "v"(JL ? a : Er));
+        asm("v_sub_u16_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
+            : "+v"(p23)
+            : "v"(JL ? fp : b), "v"(JL ? b : fp));
+        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(sg) : "v"(p01), "v"(p23), "s"(PERM_SIGNS));
+        bits = s == 0 ? (sg & (0x01010101u << (S - 1))) : ((sg & (0x01010101u << (S - 1 - s))) | bits);
+      }
+      (void)dv, (void)dh, (void)df, (void)de;
+#elif defined(EXP_NODIFF)  // timing experiments only (wrong direction bits)
+      (void)dv, (void)dh, (void)df, (void)de;
+#elif defined(EXP_ADDPUSH)
+      av += (uint32_t)dv, ah += (uint32_t)dh, af += (uint32_t)df, ae += (uint32_t)de;
+#else
       av = push_sign(av, dv);  // (the first push shifts in zeros: one op, not a compare)
       ah = push_sign(ah, dh);
       af = push_sign(af, df);
       ae = push_sign(ae, de);
+#endif
       E[s] = fv_max(a, Er);
       const FV f = fv_max(b, fp);
       F[s] = f;
@@ -571,7 +605,11 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
       cell(S - 1, hb, eb);
       if constexpr (END == 1) Bt = max(Bt, bstep + Rc);
       if constexpr (END == 2) Bt = max(Bt, (bstep << END_RANK_BITS) + Rc);
+#if GSNAPDP_PERMBITS
+      const uint32_t acc = bits;
+#else
       const uint32_t acc = (((((av << S) | ah) << S) | af) << S) | ae;
+#endif
 #ifndef EXP_NOSTORE
       D[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = acc;
 #ifndef EXP_NOMATCH
@@ -584,8 +622,13 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
     if constexpr (END) Rc += dR;
     // next column's inputs from the rings (every lane, every step)
     if (t % RING_K == 0) stage(std::integral_constant<int, RING_K>(), t + 1 + rbase + RG::SPAN, t + 1);
+#ifdef EXP_NORINGREAD  // timing experiment only: no per-step LDS reads (wrong inputs)
+    pnext = pnext * 3u + (uint32_t)t;
+    gnext = (gnext + 1) & 3;
+#else
     pnext = rr[(t + 1 + j * (S - 1) + rbase) & (RG::RR - 1)];
     gnext = cr[(t + 1 - j) & (RG::CR - 1)];
+#endif
   };
   using Masked = std::integral_constant<bool, true>;
   using Full = std::integral_constant<bool, false>;
@@ -668,7 +711,7 @@ __device__ void trace_batch(int lane, int wi, FillOut fo, int jl,
   OpWriter ow = {ops + op_off[wi], (int)(op_off[wi + 1] - op_off[wi]), 0, 0};
   // a segment window's genome classes (the long-gap intron test) come from its segment
   const SegCls sc = {sjw ? (const unsigned char*)q + sjw[wi].spos : nullptr, L.g0};
-  band_traceback<S, LPW, FILL_MATCH>(Dk, Mk, g, fo.br, fo.bc, maxC, L.d.lband, L.d.rband, WMAX - L.d.W,
+  band_traceback<S, LPW, FILL_MATCH, FILL_PL ? FILL_PL : S>(Dk, Mk, g, fo.br, fo.bc, maxC, L.d.lband, L.d.rband, WMAX - L.d.W,
                          sjw ? 1 : cs.cvlo, sjw ? L.d.L2 : cs.cvhi, jl, L, blocks, nwords, tal, ow, sc);
   // Dynprog_end5/3_splicejunction score the alignment from its counts (:5541 / :6045)
   // (without the fill's match bits k_count does both once it has the counts)

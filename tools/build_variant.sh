@@ -15,4 +15,4 @@ OBJS="$REST"
 for s in kernels ggap gband; do
   if [ $s = $SRC ]; then OBJS="$OBJS $O/gsnapdp_$s.o"; else OBJS="$OBJS lib/gsnapdp_$s.o"; fi
 done
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $O/libgsnapdp.so $OBJS
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -Wl,-Bsymbolic -o $O/libgsnapdp.so $OBJS
