@@ -523,70 +523,90 @@ def measure_c4_transcripts(n=C4_TRANSCRIPTS, cpu=True, pinned=2000):
     """Side line, BASELINE config 4 as stated: `n` synthetic 5 kbp transcripts
     (workload.c4_transcripts: 8-12 exons, GT-AG introns of 80-5000 nt, 1 % subs,
     30 % of the boundaries stage 2 misplaces by 1-6 nt) through GMAP's final
-    intron pass (gsnapdp_stage3_pass_compact: build_pairs_introns with finalp,
-    stage3.c:8860-8875) and score_introns on every returned list
-    (gsnapdp_stage3_score_introns: one k_introns launch, :9890-9941).  The timed
-    region is one pass plus score_introns over all paths, inputs in host memory
-    (the pass is host-driven).  Parity: the first `pinned` paths against the
-    reference's own results (tests/golden/c4_pinned.npz), all paths against the
-    CPU restatement run in the same process."""
+    intron pass (gsnapdp_stage3_pass_runs: build_pairs_introns with finalp,
+    stage3.c:8860-8875, each path's gap pairs named by the caller as
+    insert_gapholders placed them, the lists returned as runs) and score_introns
+    on every returned list (gsnapdp_stage3_score_introns_runs: one k_introns
+    launch, :9890-9941).  The timed region is the pass plus score_introns over
+    all paths, inputs in host memory (the pass is host-driven).  Parity: the
+    lists expanded from the runs -- the first `pinned` against the reference's
+    own results (tests/golden/c4_pinned.npz), all against the CPU restatement
+    run in the same process, which times the same two calls."""
     import hashlib
-    from gsnapdp import expand_compact
+    from gsnapdp import expand_runs, gap_lists
     t0 = time.perf_counter()
     w = W.c4_transcripts(n)
     gen_s = time.perf_counter() - t0
+    gaps, gap_off = gap_lists(w.calls, w.pairs_in)  # the caller's own bookkeeping (insert_gapholders)
     ctx = Context(w.blocks)
     ctx.stage3_pass_compact(w.calls[:256], w.pairs_in, w.query, w.query_uc)  # launches, staging
     bufs = None
     best = None
     for _ in range(3):  # the first run also faults the output buffers in
         t0 = time.perf_counter()
-        c, cells, new, st = ctx.stage3_pass_compact(w.calls, w.pairs_in, w.query, w.query_uc, bufs=bufs)
+        c, runs, new, st, bufs = ctx.stage3_pass_runs(w.calls, w.pairs_in, w.query, w.query_uc, gaps, gap_off,
+                                                      bufs=bufs)
         t1 = time.perf_counter()
-        if bufs is None:
-            bufs = (cells.base, new.base)
-        if best is None or t1 - t0 < best[0]:
-            best = (t1 - t0, c, cells.copy(), new.copy(), st)
-    dt, c, cells, new, st = best
-    lists = expand_compact(c, w.pairs_in, cells, new)
-    t0 = time.perf_counter()
-    sc = ctx.stage3_score_introns(c, lists)
-    si_s = time.perf_counter() - t0
+        sc = ctx.stage3_score_introns_runs(c, w.pairs_in, runs, new, gaps, gap_off)
+        t2 = time.perf_counter()
+        if best is None or t2 - t0 < best[0]:
+            best = (t2 - t0, t1 - t0, t2 - t1, c, runs.copy(), new.copy(), st, sc)
+    total, dt, si_s, c, runs, new, st, sc = best
+    c_full, lists = expand_runs(c, w.pairs_in, runs, new)
     introns = int(sc["nintrons"].sum())
     ctx.close()
     z = np.load(os.path.join(ROOT, "tests", "golden", "c4_pinned.npz"), allow_pickle=False)
     m = min(pinned, n, int(z["n"]))
-    ok_ref = all(hashlib.sha256(lists[int(c["first_out"][i]):int(c["first_out"][i]) + int(c["nout"][i])].tobytes())
-                 .digest() == z["digests"][i].tobytes() for i in range(m))
-    for f in ("out_minor", "out_major", "out_nintrons", "out_nnonintrons", "shiftp", "incompletep", "nout"):
+    fo, no = c_full["first_out"], c_full["nout"]
+    ok_ref = all(hashlib.sha256(lists[int(fo[i]):int(fo[i]) + int(no[i])].tobytes()).digest() ==
+                 z["digests"][i].tobytes() for i in range(m))
+    for f in ("out_minor", "out_major", "out_nintrons", "out_nnonintrons", "shiftp", "incompletep"):
         ok_ref = ok_ref and bool(np.array_equal(c[f][:m], z["ref_" + f][:m]))
+    ok_ref = ok_ref and bool(np.array_equal(no[:m], z["ref_nout"][:m]))
     ok_ref = ok_ref and bool(np.array_equal(sc["avg_donor_score"][:m].view(np.uint64),
                                             z["si_calls"]["avg_donor_score"][:m].astype(np.float64).view(np.uint64)))
     nwin = int(np.sum(st["windows"]))
-    total = dt + si_s
     out = {"workload": "C4 as stated: %d synthetic transcripts of 4.5-5.5 kbp (8-12 exons, GT-AG introns of "
                        "80-5000 nt, 1%% substitutions), each GMAP's final intron pass (build_pairs_introns, "
-                       "finalp) + score_introns; %d path pairs, %d introns; generated in %.1f s"
-                       % (n, w.pairs_in.size, w.nintrons, gen_s),
+                       "finalp) + score_introns; %d path pairs, %d gap pairs, %d introns; generated in %.1f s"
+                       % (n, w.pairs_in.size, gaps.size, w.nintrons, gen_s),
            "metric": "C4 transcripts (final intron pass + score_introns), paths/s",
            "value": round(n / total, 1), "unit": "paths/s", "seconds": round(total, 4),
            "pass_s": round(dt, 4), "score_introns_s": round(si_s, 4),
+           "output": "runs (gsnapdp_stage3_pass_runs: %d runs for %d returned pairs)" % (runs.size, lists.size),
            "windows": nwin, "windows_per_s": round(nwin / dt, 1),
            "windows_by_family": {"single": int(st["windows"][0]), "genome_gap": int(st["windows"][1]),
                                  "cdna_gap": int(st["windows"][2]), "microexon": int(st["windows"][3])},
            "introns_scored": introns, "introns_per_s": round(introns / si_s, 1),
            "rounds": int(st["rounds"]), "host_s": round(float(st["seconds"][0]), 4),
            "wait_s": round(float(st["seconds"][1]), 4),
+           "host_frac": round((float(st["seconds"][0]) + si_s) / total, 3),
            "bit_exact_vs_reference": {"paths": m, "ok": bool(ok_ref)}}
     if cpu:
-        cb, (rc, rcells, rnew, rst) = stage3_cpu_baseline(w.blocks, w.calls, w.pairs_in, w.query, w.query_uc,
-                                                          compact=True)
-        same = bool(np.array_equal(rcells, cells) and rnew.tobytes() == new.tobytes())
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # CPU baseline leg
+        S = O.Stage3Cpu(w.blocks)
+        S.run_compact(w.calls[:256], w.pairs_in, w.query, w.query_uc)
+        cb = None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            rc, rruns, rnew, rst, rsc = S.run_runs(w.calls, w.pairs_in, w.query, w.query_uc, gaps, gap_off,
+                                                   introns=True)
+            dt_c = time.perf_counter() - t0
+            if cb is None or dt_c < cb[0]:
+                cb = (dt_c, rc, rruns, rnew, rsc)
+        S.close()
+        dt_c, rc, rruns, rnew, rsc = cb
+        same = bool(np.array_equal(rruns, runs) and rnew.tobytes() == new.tobytes() and
+                    rsc.tobytes() == sc.tobytes())
         for f in ("out_minor", "out_major", "out_nintrons", "out_nnonintrons", "out_intronlen", "out_nonintronlen",
                   "shiftp", "incompletep", "nout"):
             same = same and bool(np.array_equal(rc[f], c[f]))
-        cb["note"] = "the pass alone (no score_introns)"
-        out["cpu_baseline"] = cb
+        out["cpu_baseline"] = {
+            "value": round(n / dt_c, 1), "unit": "paths/s", "seconds": round(dt_c, 4),
+            "cores": int(os.environ.get("GSNAPDP_S3_THREADS", min(16, os.cpu_count() or 1))), "kind": "port",
+            "sample": "the same %d paths: the pass's host code with every DP window served by the oracle/ "
+                      "restatement, then score_introns on the same runs (oracle/_build/libstage3_cpu.so)" % n}
         out["bit_exact_vs_cpu_restatement"] = {"paths": n, "ok": same}
     return out
 

@@ -266,7 +266,7 @@ constexpr int TB_BATCH = GSNAPDP_TB_BATCH;
 // GSNAPDP_PERMBITS: the direction bits by v_perm_b32 (one byte per plane) instead
 // of four alignbit pushes per cell
 #ifndef GSNAPDP_PERMBITS
-#define GSNAPDP_PERMBITS 0
+#define GSNAPDP_PERMBITS 1
 #endif
 constexpr int FILL_PL = GSNAPDP_PERMBITS ? 8 : 0;  // the plane stride (0: S)
 [[maybe_unused]] constexpr uint32_t PERM_SIGNS = 0x0B0A0908u;  // result bytes 0..3 = signs of bytes 1, 3, 5, 7
@@ -517,7 +517,8 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
       }
     }
     // four bit planes (v1, h1, dF, dE), each a short independent chain
-    uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u, gsh = 0u;
+    [[maybe_unused]] uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u;
+    uint32_t gsh = 0u;
     [[maybe_unused]] uint32_t bits = 0u;  // GSNAPDP_PERMBITS: the four planes, one byte each
     int bstep = END == 2 ? 0 : -(1 << 30);  // END: this column's best scan key (END 2: value), less R(c)
     auto cell = [&](int s, FV Hr, FV Er) {

@@ -74,59 +74,144 @@ bool unknown_base(char c) {  // pair.c
 
 // One path's pairs and list cells.  The caller's pairs are read in place:
 // pair j < nin is pairs_in[j] (only its DISALLOWED flag can change, kept in
-// `flags`), cell j < nin starts as the input list's j-th cell (pair j, next
+// `dis`), cell j < nin starts as the input list's j-th cell (pair j, next
 // j + 1), and the pairs and cells the pass makes are appended after them.
 // Cells are never freed; a cell's pair never changes (List_push_existing
 // re-links the cell itself).
+//
+// The input cells' links are stored sparsely, so a path costs its gaps, not
+// its pairs: a cell whose link was written is in `links` (sorted by cell); a
+// cell inside a reversed stretch (`rev`, [a, b): the scan's move of an
+// untouched run a .. b - 1 onto `pairs`) links to cell - 1; any other still
+// links to cell + 1, as the input list does (-1 after the last).  The gap
+// pairs among the input pairs are `gaps` (ascending), the caller's or derived
+// from the flags.
 // a pair record that a resize leaves uninitialised (list_of writes every field)
 struct RawPair {
   gsnapdp_s3_pair p;
   RawPair() {}
 };
 
+struct Link {
+  int cell, next;
+};
+
 struct Arena {
   const gsnapdp_s3_pair* in = nullptr;
   int nin = 0;
-  std::vector<uint8_t> dis;    // the input pairs the pass disallowed (allocated at the first one)
-  std::vector<RawPair> extra;  // pair nin + i
-  std::vector<int> cp;         // pair of cell nin + i
-  std::vector<int> cn;         // next cell of every cell
-  void init(const gsnapdp_s3_pair* pairs, int n) {
+  const int32_t* gaps = nullptr;  // the input pairs with GAPP, ascending
+  int ngaps = 0;
+  std::vector<int32_t> own_gaps;       // gaps derived from the flags (no caller list)
+  std::vector<Link> links;             // written links of input cells, by cell
+  std::vector<std::pair<int, int>> rev;  // reversed stretches [a, b), ascending, disjoint
+  std::vector<int> dis;                // the input pairs the pass disallowed, ascending
+  std::vector<RawPair> extra;          // pair nin + i
+  std::vector<int> cp;                 // pair of cell nin + i
+  std::vector<int> cnx;                // next cell of cell nin + i
+  void init(const gsnapdp_s3_pair* pairs, int n, const int32_t* g, int ng) {
     in = pairs;
     nin = n;
+    if (g) {
+      gaps = g;
+      ngaps = ng;
+    } else {  // the gap pairs from the flags (one pass over the path)
+      own_gaps.clear();
+      for (int j = 0; j < n; j++)
+        if (pairs[j].flags & GSNAPDP_S3_GAPP) own_gaps.push_back(j);
+      gaps = own_gaps.data();
+      ngaps = (int)own_gaps.size();
+    }
+    links.clear();
+    rev.clear();
     dis.clear();
-    cn.resize((size_t)n);
-    int* c = cn.data();
-    for (int j = 0; j < n; j++) c[j] = j + 1;  // (vectorised)
-    if (n) c[n - 1] = -1;
     extra.clear();
     cp.clear();
-    extra.reserve(256);
-    cp.reserve(256);
-    cn.reserve((size_t)n + 256);
+    cnx.clear();
   }
+  // the first gap pair at or after input pair x (nin when none)
+  int next_gap(int x) const {
+    const int32_t* g = std::lower_bound(gaps, gaps + ngaps, x);
+    return g == gaps + ngaps ? nin : *g;
+  }
+  bool is_dis(int p) const { return !dis.empty() && std::binary_search(dis.begin(), dis.end(), p); }
   // the flags of input pair p as the pass left them
-  uint8_t in_flags(int p) const {
-    return (uint8_t)(in[p].flags | (!dis.empty() && dis[(size_t)p] ? GSNAPDP_S3_DISALLOWED : 0));
+  uint8_t in_flags(int p) const { return (uint8_t)(in[p].flags | (is_dis(p) ? GSNAPDP_S3_DISALLOWED : 0)); }
+  // the reversed stretch holding c strictly inside (a < c < b), or nullptr
+  const std::pair<int, int>* rev_of(int c) const {
+    auto it = std::upper_bound(rev.begin(), rev.end(), c,
+                               [](int x, const std::pair<int, int>& r) { return x < r.first; });
+    if (it == rev.begin()) return nullptr;
+    --it;
+    return c > it->first && c < it->second ? &*it : nullptr;
+  }
+  std::vector<Link>::const_iterator link_at(int c) const {
+    return std::lower_bound(links.begin(), links.end(), c, [](const Link& l, int x) { return l.cell < x; });
+  }
+  int next(int c) const {
+    if (c >= nin) return cnx[(size_t)(c - nin)];
+    const auto it = link_at(c);
+    if (it != links.end() && it->cell == c) return it->next;
+    if (rev_of(c)) return c - 1;
+    return c + 1 < nin ? c + 1 : -1;
+  }
+  void set_next(int c, int v) {
+    if (c >= nin) {
+      cnx[(size_t)(c - nin)] = v;
+      return;
+    }
+    auto it = std::lower_bound(links.begin(), links.end(), c, [](const Link& l, int x) { return l.cell < x; });
+    if (it != links.end() && it->cell == c) it->next = v;
+    else links.insert(it, Link{c, v});
+  }
+  bool linked_in(int lo, int hi) const {  // a written link among cells lo .. hi
+    const auto it = link_at(lo);
+    return it != links.end() && it->cell <= hi;
+  }
+  // the scan's moves of the non-gap input cells at the head of `path` onto
+  // `pairs` (Pairpool_pop + List_push_existing each): an untouched run a .. g - 1
+  // up to the next gap moves at once (a link for a, the stretch for the rest)
+  void move_run(int* path, int* pairs) {
+    int x = *path, head = *pairs;
+    while (x >= 0 && x < nin) {
+      const int g = next_gap(x);
+      if (g == x) break;  // a gap pair
+      const std::pair<int, int>* r = rev_of(x);
+      auto ov = std::upper_bound(rev.begin(), rev.end(), g - 1,
+                                 [](int v, const std::pair<int, int>& s) { return v < s.first; });
+      const bool rev_clear = ov == rev.begin() || std::prev(ov)->second <= x;
+      if (!r && rev_clear && !linked_in(x, g - 1)) {
+        set_next(x, head);
+        if (g - 1 > x) rev.insert(ov, std::make_pair(x, g));
+        head = g - 1;
+        x = g < nin ? g : -1;
+        continue;
+      }
+      const int nx = next(x);
+      set_next(x, head);
+      head = x;
+      x = nx;
+    }
+    *path = x;
+    *pairs = head;
   }
   int pairof(int cell) const { return cell < nin ? cell : cp[(size_t)(cell - nin)]; }
-  int cell(int pair, int next) {
+  int cell(int pair, int nx) {
     cp.push_back(pair);
-    cn.push_back(next);
+    cnx.push_back(nx);
     return nin + (int)cp.size() - 1;
   }
   int pop(int list, int* pair) const {  // Pairpool_pop
     *pair = pairof(list);
-    return cn[(size_t)list];
+    return next(list);
   }
   int push_existing(int list, int c) {  // List_push_existing
-    cn[(size_t)c] = list;
+    set_next(c, list);
     return c;
   }
   int transfer(int dest, int src) {  // Pairpool_transfer
     for (int p = src, nx; p >= 0; p = nx) {
-      nx = cn[(size_t)p];
-      cn[(size_t)p] = dest;
+      nx = next(p);
+      set_next(p, dest);
       dest = p;
     }
     return dest;
@@ -138,13 +223,13 @@ struct Arena {
   void disallow(int list) {  // pair->disallowedp = true (stage3.c:5873-5880)
     const int p = pairof(list);
     if (p < nin) {
-      if (dis.empty()) dis.assign((size_t)nin, 0);
-      dis[(size_t)p] = 1;
+      auto it = std::lower_bound(dis.begin(), dis.end(), p);
+      if (it == dis.end() || *it != p) dis.insert(it, p);
     } else {
       extra[(size_t)(p - nin)].p.flags |= GSNAPDP_S3_DISALLOWED;
     }
   }
-  int rest(int list) const { return cn[(size_t)list]; }
+  int rest(int list) const { return next(list); }
   int push_pair(int list, const gsnapdp_s3_pair& x) {
     extra.emplace_back();
     extra.back().p = x;
@@ -161,16 +246,58 @@ struct Arena {
     return x;
   }
   // the run of input cells from `cell` down: cell, cell - 1, ..., returned as
-  // its lowest cell (the scan's reversal of an untouched stretch of the path)
+  // its lowest cell (the scan's reversal of an untouched stretch of the path),
+  // in steps of whole stretches between written links
   int run_end(int cell) const {
     if (cell >= nin) return cell;
-    const int* c = cn.data();
     int q = cell;
-    while (q > 0 && c[q] == q - 1) q--;
+    while (q > 0) {
+      const auto it = link_at(q);
+      if (it != links.end() && it->cell == q) {
+        if (it->next != q - 1) break;
+        q--;
+        continue;
+      }
+      const std::pair<int, int>* r = rev_of(q);
+      if (!r) break;  // an input link: q + 1
+      // cells r->first + 1 .. q link downwards unless written: down to the
+      // highest written link below q, or to the stretch's first cell
+      const int below = it == links.begin() ? -1 : std::prev(it)->cell;
+      q = std::max(r->first, below);
+    }
     return q;
   }
 };
 bool gapp(const gsnapdp_s3_pair& p) { return (p.flags & GSNAPDP_S3_GAPP) != 0; }
+
+// A returned list as segments, in list order: in_run(hi, lo, d) for input
+// pairs hi, hi - 1, .., lo (a disallowed pair is a run of its own with d set),
+// new_pair(e) for the pass's pair nin + e.  Costs the list's runs, not its pairs.
+template <class In, class New>
+void walk_list(const Arena& A, int list, In&& in_run, New&& new_pair) {
+  for (int p = list; p >= 0;) {
+    if (p < A.nin) {
+      const int lo = A.run_end(p);
+      int hi = p;
+      if (!A.dis.empty()) {
+        auto it = std::upper_bound(A.dis.begin(), A.dis.end(), hi);
+        while (it != A.dis.begin() && *std::prev(it) >= lo) {
+          const int d = *--it;
+          if (d < hi) in_run(hi, d + 1, false);
+          in_run(d, d, true);
+          hi = d - 1;
+        }
+      }
+      if (hi >= lo) in_run(hi, lo, false);
+      p = A.rest(lo);
+    } else {
+      const int pr = A.pairof(p);
+      if (pr < A.nin) in_run(pr, pr, A.is_dis(pr));
+      else new_pair(pr - A.nin);
+      p = A.rest(p);
+    }
+  }
+}
 
 // The DP window a path is waiting for, in the batched C-ABI's records.
 struct Req {
@@ -296,6 +423,8 @@ struct Pass {
   const char* query = nullptr;
   const char* query_uc = nullptr;
   gsnapdp::S3Driver* driver = nullptr;  // driven passes: a path's next pass when one ends
+  const int32_t* gaps = nullptr;        // the callers' gap-pair lists (gsnapdp_stage3_pass_runs), or nullptr
+  const int64_t* gap_off = nullptr;
 };
 
 }  // namespace
@@ -758,10 +887,11 @@ int list_of(Arena& A, const std::vector<gsnapdp_pair>& v, int n, bool micro) {
   if (n <= 0) return -1;
   // pairs nin + e0 .. e0 + n - 1 in cells c0 .. c0 + n - 1: the list's head is
   // v[0]'s cell, and each cell links to the next (push order from v[n - 1])
-  const size_t e0 = A.extra.size(), k0 = A.cp.size(), c0 = A.cn.size();
+  const size_t e0 = A.extra.size(), k0 = A.cp.size();
   A.extra.resize(e0 + (size_t)n);
   A.cp.resize(k0 + (size_t)n);
-  A.cn.resize(c0 + (size_t)n);
+  A.cnx.resize(k0 + (size_t)n);
+  const size_t c0 = (size_t)A.nin + k0;
   for (int i = 0; i < n; i++) {
     const gsnapdp_pair& p = v[(size_t)i];
     gsnapdp_s3_pair& x = A.extra[e0 + (size_t)i].p;
@@ -787,7 +917,7 @@ int list_of(Arena& A, const std::vector<gsnapdp_pair>& v, int n, bool micro) {
       x.genome = p.genome;
     }
     A.cp[k0 + (size_t)i] = A.nin + (int)(e0 + (size_t)i);
-    A.cn[c0 + (size_t)i] = i + 1 < n ? (int)(c0 + (size_t)i + 1) : -1;
+    A.cnx[k0 + (size_t)i] = i + 1 < n ? (int)(c0 + (size_t)i + 1) : -1;
   }
   return (int)c0;
 }
@@ -1405,7 +1535,7 @@ bool dual_gap(Pass& P, Path& k, int gapcell, int gap) {
   auto transfer_one = [&]() {
     const int cell = k.path;
     k.path = A.rest(cell);
-    A.cn[(size_t)cell] = k.midexon;
+    A.set_next(cell, k.midexon);
     k.midexon = cell;
   };
   transfer_one();
@@ -1494,21 +1624,8 @@ void scan(Pass& P, Path& k) {
   const int minintronlen = c.finalp ? MININTRONLEN_FINAL : MININTRONLEN;
   while (!k.failed && k.stage == S_SCAN) {
     // the non-gap input cells at the head of the path, each pushed onto pairs
-    // (Pairpool_pop + List_push_existing, the loop below) in one tight loop
-    if (k.path >= 0 && k.path < k.A.nin) {
-      int* cn = k.A.cn.data();
-      const gsnapdp_s3_pair* in = k.A.in;
-      const int nin = k.A.nin;
-      int x = k.path, head = k.pairs;
-      while (x >= 0 && x < nin && !(in[x].flags & GSNAPDP_S3_GAPP)) {
-        const int nx = cn[x];
-        cn[x] = head;
-        head = x;
-        x = nx;
-      }
-      k.path = x;
-      k.pairs = head;
-    }
+    // (Pairpool_pop + List_push_existing, the loop below), a run at a time
+    if (k.path >= 0 && k.path < k.A.nin) k.A.move_run(&k.path, &k.pairs);
     if (k.path < 0) {
       k.stage = S_DONE;
       return;
@@ -1602,7 +1719,9 @@ void resume(Pass& P, Path& k) {
 
 
 // a path at the start of its pass: call c over the list pairs[0 .. npairs)
-void start_path(Pass& P, Path& k, gsnapdp_s3_call* cp, const gsnapdp_s3_pair* pairs, int npairs) {
+// (gaps: its gap pairs, ascending, or nullptr to find them from the flags)
+void start_path(Pass& P, Path& k, gsnapdp_s3_call* cp, const gsnapdp_s3_pair* pairs, int npairs,
+                const int32_t* gaps = nullptr, int ngaps = 0) {
   reset(k);
   gsnapdp_s3_call& c = *cp;
   k.c = cp;
@@ -1614,7 +1733,7 @@ void start_path(Pass& P, Path& k, gsnapdp_s3_call* cp, const gsnapdp_s3_pair* pa
   k.nnonintrons = c.in_nnonintrons;
   k.intronlen = c.in_intronlen;
   k.nonintronlen = c.in_nonintronlen;
-  k.A.init(pairs, npairs);  // path->first is pairs[0] (cell 0)
+  k.A.init(pairs, npairs, gaps, ngaps);  // path->first is pairs[0] (cell 0)
   const int list = npairs > 0 ? 0 : -1;
   if (c.use_genomicseg_p) {
     fail(k, "use_genomicseg_p passes are not served (the genome is the context's)");
@@ -1652,23 +1771,18 @@ void finish_path(Pass& P, Path& k) {
     if (!k.failed) {
       if (k.c->pass == GSNAPDP_S3_END3) k.pairs = k.path;  // build_path_end3 returns its path
       const Arena& A = k.A;
-      const bool dis = !A.dis.empty();
       list.reserve((size_t)A.nin + A.extra.size());  // every cell at most once
-      for (int p = k.pairs; p >= 0;) {
-        if (p < A.nin) {  // a run of input cells p, p - 1, .., q: a reversed block copy (A.out of each)
-          const int q = A.run_end(p);
-          for (int x = p; x >= q; x--) {
-            list.push_back(A.in[x]);
-            gsnapdp_s3_pair& o = list.back();
-            o.src = x;
-            if (dis && A.dis[(size_t)x]) o.flags |= GSNAPDP_S3_DISALLOWED;
-          }
-          p = A.rest(q);
-        } else {
-          list.push_back(A.out(p));
-          p = A.rest(p);
-        }
-      }
+      walk_list(
+          A, k.pairs,
+          [&](int hi, int lo, bool d) {  // a reversed block copy (A.out of each)
+            for (int x = hi; x >= lo; x--) {
+              list.push_back(A.in[x]);
+              gsnapdp_s3_pair& o = list.back();
+              o.src = x;
+              if (d) o.flags |= GSNAPDP_S3_DISALLOWED;
+            }
+          },
+          [&](int e) { list.push_back(A.extra[(size_t)e].p); });
     }
     write_call(k, *k.c);
     const gsnapdp_s3_pair* pairs = nullptr;
@@ -1955,18 +2069,56 @@ namespace {
 // in new_out; include/gsnapdp.h gsnapdp_stage3_pass_compact).
 struct Out {
   gsnapdp_s3_pair* pairs = nullptr;
-  int64_t cap = 0;
+  int64_t cap = 0;  // pairs, cells or runs
   int32_t* cells = nullptr;
+  gsnapdp_s3_run* runs = nullptr;
   gsnapdp_s3_pair* news = nullptr;
   int64_t new_cap = 0;
 };
 
+// a returned list's segments as gsnapdp_s3_run records: a run of input pairs
+// continued by the next segment's (one below it), and consecutive new pairs,
+// merge; o = nullptr counts them
+struct RunWriter {
+  gsnapdp_s3_run* o = nullptr;
+  int64_t n = 0;
+  gsnapdp_s3_run cur{0, 0};
+  bool open = false;
+  void flush() {
+    if (open) {
+      if (o) o[n] = cur;
+      n++;
+      open = false;
+    }
+  }
+  void in(int hi, int lo, bool d) {
+    const int cnt = hi - lo + 1;
+    if (!d && open && cur.start >= 0 && !(cur.count & GSNAPDP_S3_CELL_DISALLOWED) && cur.start - cur.count == hi) {
+      cur.count += cnt;
+      return;
+    }
+    flush();
+    cur = gsnapdp_s3_run{hi, cnt | (d ? (int32_t)GSNAPDP_S3_CELL_DISALLOWED : 0)};
+    open = true;
+  }
+  void nw(int64_t e) {  // new_out[e]
+    if (open && cur.start < 0 && (int64_t)(-1 - cur.start) + cur.count == e) {
+      cur.count++;
+      return;
+    }
+    flush();
+    cur = gsnapdp_s3_run{(int32_t)(-1 - e), 1};
+    open = true;
+  }
+};
+
 int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp_s3_pair* pairs_in,
              int64_t npairs_in, const char* query, const char* query_uc, size_t query_bytes, const gsnapdp_iit* iit,
-             const Out& out, gsnapdp_s3_stats* stats, gsnapdp::S3Driver* driver = nullptr) {
+             const Out& out, gsnapdp_s3_stats* stats, gsnapdp::S3Driver* driver = nullptr,
+             const int32_t* gaps = nullptr, const int64_t* gap_off = nullptr) {
   if (!ctx || ncalls < 0 || npairs_in < 0 ||
       (ncalls > 0 && (!calls || (npairs_in > 0 && !pairs_in) || !query || !query_uc ||
-                      !(driver || out.pairs || (out.cells && out.news))))) {
+                      !(driver || out.pairs || ((out.cells || out.runs) && out.news))))) {
     gsnapdp__set_err("gsnapdp_stage3_pass: bad arguments");
     return -1;
   }
@@ -1976,6 +2128,20 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
                        " names pairs or query bytes outside the buffers");
       return -1;
     }
+  if ((gaps != nullptr) != (gap_off != nullptr) || (gap_off && ncalls > 0 && gap_off[0] < 0)) {
+    gsnapdp__set_err("gsnapdp_stage3_pass_runs: gaps and gap_off go together");
+    return -1;
+  }
+  for (int i = 0; gaps && i < ncalls; i++) {  // ascending pair indices inside each path
+    bool ok = gap_off[i + 1] >= gap_off[i];
+    for (int64_t j = gap_off[i]; ok && j < gap_off[i + 1]; j++)
+      ok = gaps[j] >= 0 && gaps[j] < calls[i].npairs && (j == gap_off[i] || gaps[j] > gaps[j - 1]);
+    if (!ok) {
+      gsnapdp__set_err("gsnapdp_stage3_pass_runs: call " + std::to_string(i) +
+                       "'s gap list is not ascending pair indices of its path");
+      return -1;
+    }
+  }
   Pass P;
   P.ctx = ctx;
   P.blocks = gsnapdp__host_blocks(ctx);
@@ -1984,6 +2150,8 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
   P.query = query;
   P.query_uc = query_uc;
   P.driver = driver;
+  P.gaps = gaps;
+  P.gap_off = gap_off;
   memset(&P.st, 0, sizeof(P.st));
   using clock = std::chrono::steady_clock;
   const auto t_start = clock::now();
@@ -2003,7 +2171,12 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
   pool.run(ncalls, 16, [&](int i) {
     Path& k = paths[(size_t)i];
     gsnapdp_s3_call& c = calls[i];
-    start_path(P, k, &c, pairs_in + c.first_pair, c.npairs);
+    if (P.gaps) {
+      const int64_t g0 = P.gap_off[i], g1 = P.gap_off[i + 1];
+      start_path(P, k, &c, pairs_in + c.first_pair, c.npairs, P.gaps + g0, (int)(g1 - g0));
+    } else {
+      start_path(P, k, &c, pairs_in + c.first_pair, c.npairs);
+    }
     if (driver && (k.stage == S_DONE || k.failed)) finish_path(P, k);
   });
   // two cohorts (alternate paths, so both get a similar mix) when there are
@@ -2069,18 +2242,17 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
   pool.run(ncalls, 16, [&](int i) {
     Path& k = paths[(size_t)i];
     if (k.c->pass == GSNAPDP_S3_END3) k.pairs = k.path;  // build_path_end3 returns its path
-    int n = 0, nn = 0;
-    if (!k.failed)
-      for (int p = k.pairs; p >= 0;) {
-        const int q = k.A.run_end(p);
-        if (q != p || p < k.A.nin) {
-          n += p - q + 1;  // input cells p .. q
-          p = k.A.rest(q);
-        } else {
-          n++, nn += k.A.pairof(p) >= k.A.nin;
-          p = k.A.rest(p);
-        }
+    int64_t n = 0, nn = 0;
+    if (!k.failed) {
+      if (out.runs) {
+        RunWriter w;
+        walk_list(k.A, k.pairs, [&](int hi, int lo, bool d) { w.in(hi, lo, d); }, [&](int) { w.nw(nn++); });
+        w.flush();
+        n = w.n;
+      } else {
+        walk_list(k.A, k.pairs, [&](int hi, int lo, bool) { n += hi - lo + 1; }, [&](int) { n++, nn++; });
       }
+    }
     first[(size_t)i + 1] = n;
     nfirst[(size_t)i + 1] = nn;
   });
@@ -2089,10 +2261,12 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
     nfirst[(size_t)i + 1] += nfirst[(size_t)i];
   }
   P.st.new_pairs = nfirst[(size_t)ncalls];
+  P.st.out_needed = first[(size_t)ncalls];
   if (first[(size_t)ncalls] > out.cap || (!out.pairs && nfirst[(size_t)ncalls] > out.new_cap)) {
-    gsnapdp__set_err(std::string("gsnapdp_stage3_pass: ") + (first[(size_t)ncalls] > out.cap ? "the cell" : "the new-pair") +
-                     " output is too small (" + std::to_string(first[(size_t)ncalls]) + " cells, " +
-                     std::to_string(nfirst[(size_t)ncalls]) + " new pairs)");
+    gsnapdp__set_err(std::string("gsnapdp_stage3_pass: ") +
+                     (first[(size_t)ncalls] > out.cap ? (out.runs ? "the run" : "the cell") : "the new-pair") +
+                     " output is too small (" + std::to_string(first[(size_t)ncalls]) +
+                     (out.runs ? " runs, " : " cells, ") + std::to_string(nfirst[(size_t)ncalls]) + " new pairs)");
     if (stats) *stats = P.st;
     store_release(store);
     return -1;
@@ -2104,47 +2278,44 @@ int run_pass(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp
     c.first_out = (int32_t)first[(size_t)i];
     c.nout = (int32_t)(first[(size_t)i + 1] - first[(size_t)i]);
     if (k.failed) return;
-    int64_t at = first[(size_t)i];
+    int64_t at = first[(size_t)i], nat = nfirst[(size_t)i];
     const Arena& A = k.A;
-    const bool dis = !A.dis.empty();
     if (out.pairs) {
-      for (int p = k.pairs; p >= 0;) {
-        if (p < A.nin) {  // a run of input cells p, p - 1, .., q: a reversed block copy
-          const int q = A.run_end(p);
-          gsnapdp_s3_pair* o = out.pairs + at;
-          for (int x = p; x >= q; x--, o++) {
-            *o = A.in[x];
-            o->src = x;
-            if (dis && A.dis[(size_t)x]) o->flags |= GSNAPDP_S3_DISALLOWED;
-          }
-          at += p - q + 1;
-          p = A.rest(q);
-        } else {
-          out.pairs[at++] = A.out(p);
-          p = A.rest(p);
-        }
-      }
+      walk_list(
+          A, k.pairs,
+          [&](int hi, int lo, bool d) {  // a reversed block copy
+            gsnapdp_s3_pair* o = out.pairs + at;
+            for (int x = hi; x >= lo; x--, o++) {
+              *o = A.in[x];
+              o->src = x;
+              if (d) o->flags |= GSNAPDP_S3_DISALLOWED;
+            }
+            at += hi - lo + 1;
+          },
+          [&](int e) { out.pairs[at++] = A.extra[(size_t)e].p; });
+    } else if (out.runs) {
+      RunWriter w;
+      w.o = out.runs + at;
+      walk_list(
+          A, k.pairs, [&](int hi, int lo, bool d) { w.in(hi, lo, d); },
+          [&](int e) {
+            out.news[nat] = A.extra[(size_t)e].p;
+            w.nw(nat++);
+          });
+      w.flush();
     } else {
-      int64_t nat = nfirst[(size_t)i];
-      for (int p = k.pairs; p >= 0;) {
-        if (p < A.nin) {
-          const int q = A.run_end(p);
-          int32_t* o = out.cells + at;
-          for (int x = p; x >= q; x--, o++)
-            *o = x | ((dis && A.dis[(size_t)x]) ? GSNAPDP_S3_CELL_DISALLOWED : 0);
-          at += p - q + 1;
-          p = A.rest(q);
-          continue;
-        }
-        const int pr = A.pairof(p);
-        if (pr < A.nin) {
-          out.cells[at++] = pr | ((dis && A.dis[(size_t)pr]) ? GSNAPDP_S3_CELL_DISALLOWED : 0);
-        } else {
-          out.news[nat] = A.extra[(size_t)(pr - A.nin)].p;
-          out.cells[at++] = (int32_t)(-1 - nat++);
-        }
-        p = A.rest(p);
-      }
+      walk_list(
+          A, k.pairs,
+          [&](int hi, int lo, bool d) {
+            int32_t* o = out.cells + at;
+            const int32_t f = d ? GSNAPDP_S3_CELL_DISALLOWED : 0;
+            for (int x = hi; x >= lo; x--) *o++ = x | f;
+            at += hi - lo + 1;
+          },
+          [&](int e) {
+            out.news[nat] = A.extra[(size_t)e].p;
+            out.cells[at++] = (int32_t)(-1 - nat++);
+          });
     }
     write_call(k, c);
   });
@@ -2202,6 +2373,84 @@ extern "C" int gsnapdp_stage3_pass_compact(gsnapdp_ctx* ctx, gsnapdp_s3_call* ca
   return run_pass(ctx, calls, ncalls, pairs_in, npairs_in, query, query_uc, query_bytes, iit, o, stats);
 }
 
+extern "C" int gsnapdp_stage3_pass_runs(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls,
+                                        const gsnapdp_s3_pair* pairs_in, int64_t npairs_in, const int32_t* gaps,
+                                        const int64_t* gap_off, const char* query, const char* query_uc,
+                                        size_t query_bytes, const gsnapdp_iit* iit, gsnapdp_s3_run* runs_out,
+                                        int64_t runs_cap, gsnapdp_s3_pair* new_out, int64_t new_cap,
+                                        gsnapdp_s3_stats* stats) {
+  Out o;
+  o.runs = runs_out;
+  o.cap = runs_cap;
+  o.news = new_out;
+  o.new_cap = new_cap;
+  return run_pass(ctx, calls, ncalls, pairs_in, npairs_in, query, query_uc, query_bytes, iit, o, stats, nullptr, gaps,
+                  gap_off);
+}
+
+namespace {
+
+constexpr int SI_EXTRAQUERYGAP = 10;       // stage3.h:29
+constexpr int SI_MININTRONLEN_FINAL = 50;  // stage3.c:52
+
+// score_introns' test of a gap pair (stage3.c:7971-7987, as gsnapdp_path_introns)
+bool si_intron(const gsnapdp_s3_pair& p, int nullgap) {
+  return (p.flags & GSNAPDP_S3_GAPP) && p.queryjump <= nullgap && p.queryjump <= p.genomejump + SI_EXTRAQUERYGAP &&
+         p.genomejump > p.queryjump + SI_MININTRONLEN_FINAL;
+}
+
+// the introns each call's list holds (per[i], path order) -> IIT verdicts and
+// one k_introns launch
+int score_core(gsnapdp_ctx* ctx, const gsnapdp_s3_call* calls, int ncalls, const gsnapdp_iit* iit,
+               std::vector<std::vector<gsnapdp_intron>>& per, std::atomic<int>& bad, const char* who,
+               gsnapdp_intron_scores* scores) {
+  if (bad.load()) {
+    gsnapdp__set_err(std::string(who) + ": call " + std::to_string(bad.load() - 1) +
+                     " has an intron at the end of its path (the reference dereferences NULL)");
+    return -1;
+  }
+  if (iit) {
+    Workers::get().run(ncalls, 16, [&](int i) {
+      const gsnapdp_s3_call& c = calls[i];
+      std::vector<gsnapdp_intron>& v = per[(size_t)i];
+      if (!v.empty() && gsnapdp_introns_known(iit, c.chrnum, c.chrpos, c.genomiclength, c.cdna_direction,
+                                              c.watsonp, v.data(), (int)v.size()))
+        bad.store(i + 1);
+    });
+    if (bad.load()) {
+      gsnapdp__set_err(std::string(who) + ": call " + std::to_string(bad.load() - 1) + ": " + gsnapdp_last_error());
+      return -1;
+    }
+  }
+  std::vector<gsnapdp_intron_path> ip((size_t)ncalls);
+  size_t total = 0;
+  for (int i = 0; i < ncalls; i++) total += per[(size_t)i].size();
+  std::vector<gsnapdp_intron> all;
+  all.reserve(total);
+  for (int i = 0; i < ncalls; i++) {
+    const gsnapdp_s3_call& c = calls[i];
+    gsnapdp_intron_path& p = ip[(size_t)i];
+    p.chroffset = c.chroffset;
+    p.chrpos = c.chrpos;
+    p.genomiclength = c.genomiclength;
+    p.cdna_direction = c.cdna_direction;
+    p.watsonp = c.watsonp;
+    p.first_intron = (int32_t)all.size();
+    p.nintrons = (int32_t)per[(size_t)i].size();
+    p.pad = 0;
+    all.insert(all.end(), per[(size_t)i].begin(), per[(size_t)i].end());
+  }
+  if (ncalls == 0) return 0;
+  if (gsnapdp_score_introns_host(ctx, ip.data(), ncalls, all.empty() ? nullptr : all.data(), (int)all.size(),
+                                 scores))
+    return -1;
+  for (int i = 0; i < ncalls; i++)
+    if (calls[i].status != 0) memset(&scores[i], 0, sizeof(scores[i]));
+  return 0;
+}
+
+}  // namespace
+
 // score_introns on the lists a pass returned (include/gsnapdp.h)
 extern "C" int gsnapdp_stage3_score_introns(gsnapdp_ctx* ctx, const gsnapdp_s3_call* calls, int ncalls,
                                             const gsnapdp_s3_pair* pairs_out, const gsnapdp_iit* iit,
@@ -2236,37 +2485,86 @@ extern "C" int gsnapdp_stage3_score_introns(gsnapdp_ctx* ctx, const gsnapdp_s3_c
     std::vector<gsnapdp_intron>& v = per[(size_t)i];
     v.resize((size_t)n);
     gsnapdp_path_introns(pp.data(), c.nout, c.nullgap, i, v.data(), n);
-    if (iit && gsnapdp_introns_known(iit, c.chrnum, c.chrpos, c.genomiclength, c.cdna_direction, c.watsonp,
-                                     v.data(), n))
-      bad.store(i + 1);
   });
-  if (bad.load()) {
-    gsnapdp__set_err("gsnapdp_stage3_score_introns: call " + std::to_string(bad.load() - 1) +
-                     " has an intron at the end of its path (the reference dereferences NULL)");
+  return score_core(ctx, calls, ncalls, iit, per, bad, "gsnapdp_stage3_score_introns", scores);
+}
+
+// The same on gsnapdp_stage3_pass_runs' output: only the gap pairs of each
+// list are visited (an input run's through the gap lists, a new pair run's
+// one by one), with their list neighbours for the intron's ends.
+extern "C" int gsnapdp_stage3_score_introns_runs(gsnapdp_ctx* ctx, const gsnapdp_s3_call* calls, int ncalls,
+                                                 const gsnapdp_s3_pair* pairs_in, const int32_t* gaps,
+                                                 const int64_t* gap_off, const gsnapdp_s3_run* runs,
+                                                 const gsnapdp_s3_pair* new_pairs, const gsnapdp_iit* iit,
+                                                 gsnapdp_intron_scores* scores) {
+  if (!ctx || ncalls < 0 || (ncalls > 0 && (!calls || !scores || !pairs_in || !runs)) ||
+      (gaps != nullptr) != (gap_off != nullptr)) {
+    gsnapdp__set_err("gsnapdp_stage3_score_introns_runs: bad arguments");
     return -1;
   }
-  std::vector<gsnapdp_intron_path> ip((size_t)ncalls);
-  std::vector<gsnapdp_intron> all;
-  for (int i = 0; i < ncalls; i++) {
+  std::vector<std::vector<gsnapdp_intron>> per((size_t)ncalls);
+  std::atomic<int> bad(0);
+  Workers::get().run(ncalls, 16, [&](int i) {
     const gsnapdp_s3_call& c = calls[i];
-    gsnapdp_intron_path& p = ip[(size_t)i];
-    p.chroffset = c.chroffset;
-    p.chrpos = c.chrpos;
-    p.genomiclength = c.genomiclength;
-    p.cdna_direction = c.cdna_direction;
-    p.watsonp = c.watsonp;
-    p.first_intron = (int32_t)all.size();
-    p.nintrons = (int32_t)per[(size_t)i].size();
-    p.pad = 0;
-    all.insert(all.end(), per[(size_t)i].begin(), per[(size_t)i].end());
-  }
-  if (ncalls == 0) return 0;
-  if (gsnapdp_score_introns_host(ctx, ip.data(), ncalls, all.empty() ? nullptr : all.data(), (int)all.size(),
-                                 scores))
-    return -1;
-  for (int i = 0; i < ncalls; i++)
-    if (calls[i].status != 0) memset(&scores[i], 0, sizeof(scores[i]));
-  return 0;
+    if (c.status != 0 || c.nout <= 0) return;
+    const gsnapdp_s3_pair* in = pairs_in + c.first_pair;
+    const gsnapdp_s3_run* R = runs + c.first_out;
+    const int nr = c.nout;
+    auto count = [&](int r) { return (int)(R[r].count & ~GSNAPDP_S3_CELL_DISALLOWED); };
+    auto elem = [&](int r, int off) -> const gsnapdp_s3_pair& {
+      return R[r].start >= 0 ? in[R[r].start - off] : new_pairs[(int64_t)(-1 - R[r].start) + off];
+    };
+    thread_local std::vector<int32_t> own;
+    const int32_t *g0 = nullptr, *g1 = nullptr;
+    if (gaps) {
+      g0 = gaps + gap_off[i];
+      g1 = gaps + gap_off[i + 1];
+    } else {
+      own.clear();
+      for (int j = 0; j < c.npairs; j++)
+        if (in[j].flags & GSNAPDP_S3_GAPP) own.push_back(j);
+      g0 = own.data();
+      g1 = own.data() + own.size();
+    }
+    std::vector<gsnapdp_intron>& v = per[(size_t)i];
+    v.clear();
+    // an intron at (run r, offset off): leftpair is the list's previous pair,
+    // rightpair its next (path order reversed, gsnapdp_path_introns)
+    auto take = [&](int r, int off) {
+      const gsnapdp_s3_pair& p = elem(r, off);
+      if (!si_intron(p, c.nullgap)) return;
+      const gsnapdp_s3_pair* prev = off > 0 ? &elem(r, off - 1) : (r > 0 ? &elem(r - 1, count(r - 1) - 1) : nullptr);
+      const gsnapdp_s3_pair* next = off + 1 < count(r) ? &elem(r, off + 1) : (r + 1 < nr ? &elem(r + 1, 0) : nullptr);
+      if (!prev || !next) {
+        bad.store(i + 1);
+        return;
+      }
+      gsnapdp_intron x;
+      x.left_genomepos = (uint32_t)prev->genomepos;
+      x.right_genomepos = (uint32_t)next->genomepos;
+      x.path = i;
+      x.comp = (uint8_t)p.comp;
+      x.knowngapp = (p.flags & GSNAPDP_S3_KNOWNGAPP) ? 1 : 0;
+      x.known_donor = x.known_acceptor = 0;
+      v.push_back(x);
+    };
+    for (int r = 0; r < nr; r++) {
+      const int n = count(r);
+      if (R[r].start >= 0) {  // input pairs start .. start - n + 1: their gaps, descending
+        const int hi = R[r].start, lo = hi - n + 1;
+        const int32_t* g = std::upper_bound(g0, g1, hi);
+        while (g != g0 && *(g - 1) >= lo) {
+          --g;
+          take(r, hi - *g);
+        }
+      } else {
+        for (int off = 0; off < n; off++)
+          if (elem(r, off).flags & GSNAPDP_S3_GAPP) take(r, off);
+      }
+    }
+    std::reverse(v.begin(), v.end());  // path order
+  });
+  return score_core(ctx, calls, ncalls, iit, per, bad, "gsnapdp_stage3_score_introns_runs", scores);
 }
 
 int gsnapdp::s3_run_driven(gsnapdp_ctx* ctx, gsnapdp_s3_call* calls, int ncalls, const gsnapdp_s3_pair* pairs_in,

@@ -18,7 +18,7 @@ import os
 
 import numpy as np
 
-from .records import S3_DISALLOWED  # noqa: E402
+from .records import S3_DISALLOWED, S3_GAPP  # noqa: E402
 from .records import (CGAP_RESULT, CGAP_WINDOW, GGAP_RESULT, GGAP_TRACE, GGAP_WINDOW,  # noqa: F401
                       IIT_INTERVAL, INTRON, INTRON_PATH, INTRON_SCORES, MAXENT_IN, MICRO_RESULT, MICRO_WINDOW, PAIR,
                       PATH_PAIR, RESULT, S3_CALL, S3_PAIR, S3_STATS, SJ_WINDOW, WINDOW)
@@ -124,6 +124,11 @@ def lib():
         L.gsnapdp_stage3_set_stage2.restype = i32
         L.gsnapdp_stage3_score_introns.argtypes = [vp, vp, i32, vp, vp, vp]
         L.gsnapdp_stage3_score_introns.restype = i32
+        L.gsnapdp_stage3_pass_runs.argtypes = [vp, vp, i32, vp, ctypes.c_int64, vp, vp, vp, vp, sz, vp, vp,
+                                               ctypes.c_int64, vp, ctypes.c_int64, vp]
+        L.gsnapdp_stage3_pass_runs.restype = i32
+        L.gsnapdp_stage3_score_introns_runs.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]
+        L.gsnapdp_stage3_score_introns_runs.restype = i32
         L.gsnapdp_iit_from_intervals.argtypes = [vp, i32]
         L.gsnapdp_iit_from_intervals.restype = vp
         L.gsnapdp_iit_free.argtypes = [vp]
@@ -554,6 +559,65 @@ class Context:
             raise GsnapdpError("gsnapdp_stage3_pass_compact: %s" % lib().gsnapdp_last_error().decode())
         return c, bufs[0][:int(c["nout"].sum())], bufs[1][:int(st[0]["new_pairs"])], st[0]
 
+    def stage3_pass_runs(self, calls: np.ndarray, pairs_in: np.ndarray, query: np.ndarray, query_uc: np.ndarray,
+                         gaps: np.ndarray = None, gap_off: np.ndarray = None, iit: "SplicingIIT" = None, bufs=None):
+        """gsnapdp_stage3_pass_runs: (calls, runs, new pairs, S3_STATS, bufs); call
+        i's list is runs[first_out : first_out + nout] (S3_RUN: input pairs start,
+        start - 1, .. or new[-1 - start ..]; expand_runs rebuilds the lists).
+        `gaps` / `gap_off` as gap_lists makes them (None: the pass finds them).
+        `bufs`: reusable (runs, new) arrays; the returned bufs may be larger."""
+        from .records import S3_RUN
+        c = np.array(calls, dtype=S3_CALL, copy=True)
+        pi = np.ascontiguousarray(pairs_in, dtype=S3_PAIR)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        g = go = None
+        if gaps is not None:
+            g = np.ascontiguousarray(gaps, dtype=np.int32)
+            go = np.ascontiguousarray(gap_off, dtype=np.int64)
+        cap = 8 * (len(g) if g is not None else 0) + 16 * len(c) + 1024
+        ncap = int((2 * c["querylength"].astype(np.int64) + 256).sum()) if len(c) else 1
+        if bufs is None or bufs[0].size < cap or bufs[1].size < ncap:
+            bufs = (np.empty(max(cap, 1 if bufs is None else bufs[0].size), dtype=S3_RUN),
+                    np.empty(max(ncap, 1), dtype=S3_PAIR))
+        for attempt in range(2):
+            c = np.array(calls, dtype=S3_CALL, copy=True)
+            st = np.zeros(1, dtype=S3_STATS)
+            rc = lib().gsnapdp_stage3_pass_runs(self.h, _p(c), len(c), _p(pi) if pi.size else _p(bufs[1]), pi.size,
+                                                _p(g) if g is not None and g.size else (_p(go) if g is not None else None),
+                                                _p(go) if go is not None else None, _p(q), _p(qu),
+                                                min(q.size, qu.size), iit.h if iit is not None else None,
+                                                _p(bufs[0]), bufs[0].size, _p(bufs[1]), bufs[1].size, _p(st))
+            need = int(st[0]["out_needed"])
+            if rc != 0 and attempt == 0 and need > bufs[0].size:  # the runs output was too small: once more
+                bufs = (np.empty(need + 1024, dtype=S3_RUN), bufs[1])
+                continue
+            break
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_stage3_pass_runs: %s" % lib().gsnapdp_last_error().decode())
+        return c, bufs[0][:int(c["nout"].sum())], bufs[1][:int(st[0]["new_pairs"])], st[0], bufs
+
+    def stage3_score_introns_runs(self, calls: np.ndarray, pairs_in: np.ndarray, runs: np.ndarray, new: np.ndarray,
+                                  gaps: np.ndarray = None, gap_off: np.ndarray = None, iit: "SplicingIIT" = None):
+        """score_introns on stage3_pass_runs' output (gsnapdp_stage3_score_introns_runs)"""
+        from .records import S3_RUN
+        c = np.ascontiguousarray(calls, dtype=S3_CALL)
+        pi = np.ascontiguousarray(pairs_in, dtype=S3_PAIR)
+        r = np.ascontiguousarray(runs, dtype=S3_RUN)
+        nw = np.ascontiguousarray(new, dtype=S3_PAIR)
+        g = go = None
+        if gaps is not None:
+            g = np.ascontiguousarray(gaps, dtype=np.int32)
+            go = np.ascontiguousarray(gap_off, dtype=np.int64)
+        out = np.zeros(len(c), dtype=INTRON_SCORES)
+        rc = lib().gsnapdp_stage3_score_introns_runs(
+            self.h, _p(c), len(c), _p(pi) if pi.size else None,
+            (_p(g) if g.size else _p(go)) if g is not None else None, _p(go) if go is not None else None,
+            _p(r) if r.size else _p(out), _p(nw) if nw.size else None, iit.h if iit is not None else None, _p(out))
+        if rc != 0:
+            raise GsnapdpError("gsnapdp_stage3_score_introns_runs: %s" % lib().gsnapdp_last_error().decode())
+        return out
+
     def stage3_compute(self, queries: np.ndarray, paths_in: np.ndarray, query: np.ndarray, query_uc: np.ndarray,
                        iit: "SplicingIIT" = None, min_intronlength: int = 9, out: np.ndarray = None):
         """Passes 2A-6 of path_compute (stage3.c:8639-8876) for every query
@@ -668,3 +732,44 @@ def expand_compact(calls: np.ndarray, pairs_in: np.ndarray, cells: np.ndarray, n
     out[kept] = x
     out[~kept] = new[-1 - cells[~kept]]
     return out
+
+
+def gap_lists(calls: np.ndarray, pairs_in: np.ndarray):
+    """(gaps, gap_off) for gsnapdp_stage3_pass_runs: each call's GAPP pairs, as
+    indices within its path, ascending."""
+    gp = np.flatnonzero((pairs_in["flags"] & S3_GAPP) != 0)
+    first = calls["first_pair"].astype(np.int64)
+    lo = np.searchsorted(gp, first)
+    hi = np.searchsorted(gp, first + calls["npairs"])
+    cnt = hi - lo
+    gap_off = np.zeros(len(calls) + 1, dtype=np.int64)
+    np.cumsum(cnt, out=gap_off[1:])
+    owner = np.repeat(np.arange(len(calls)), cnt)
+    idx = np.repeat(lo - gap_off[:-1], cnt) + np.arange(int(gap_off[-1]))
+    gaps = (gp[idx] - first[owner]).astype(np.int32)
+    return gaps, gap_off
+
+
+def expand_runs(calls: np.ndarray, pairs_in: np.ndarray, runs: np.ndarray, new: np.ndarray):
+    """The full returned lists (as Context.stage3_pass writes them) from
+    stage3_pass_runs' runs, and the calls with first_out / nout in pairs."""
+    from .records import S3_CELL_DISALLOWED
+    cnt = (runs["count"] & (S3_CELL_DISALLOWED - 1)).astype(np.int64)
+    owner = np.repeat(np.arange(len(calls)), calls["nout"])
+    k = np.repeat(np.arange(runs.size), cnt)  # the run of each pair
+    off = np.arange(k.size) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    st = runs["start"].astype(np.int64)[k]
+    out = np.empty(k.size, dtype=S3_PAIR)
+    inp = st >= 0
+    src = (st - off)[inp]
+    x = pairs_in[calls["first_pair"].astype(np.int64)[owner[k[inp]]] + src].copy()
+    x["src"] = src
+    x["flags"] |= np.where((runs["count"][k[inp]] & S3_CELL_DISALLOWED) != 0, S3_DISALLOWED, 0).astype(np.uint8)
+    out[inp] = x
+    out[~inp] = new[(-1 - st + off)[~inp]]
+    c = np.array(calls, copy=True)
+    per = np.bincount(owner, weights=cnt, minlength=len(calls)).astype(np.int64) if runs.size else \
+        np.zeros(len(calls), np.int64)
+    c["nout"] = per
+    c["first_out"] = np.concatenate([[0], np.cumsum(per)[:-1]]) if len(calls) else per
+    return c, out

@@ -171,8 +171,10 @@ S3_PATH_OPTS = np.dtype([(n, "<i4") for n in ("min_intronlength maxintronlen_bou
                                              "expected_pairlength pairlength_deviation gsnap pad").split()])
 assert S3_PATH_OPTS.itemsize == 32
 S3_STATS = np.dtype([("rounds", "<i4"), ("windows", "<i4", 4), ("batches", "<i4", 4), ("undefined", "<i4"),
-                     ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3), ("new_pairs", "<i8")])
-assert S3_STATS.itemsize == 80
+                     ("failed", "<i4"), ("pad", "<i4"), ("seconds", "<f8", 3), ("new_pairs", "<i8"),
+                     ("out_needed", "<i8")])
+assert S3_STATS.itemsize == 88
+S3_RUN = np.dtype([("start", "<i4"), ("count", "<i4")])  # gsnapdp_s3_run (gsnapdp_stage3_pass_runs)
 S3_CELL_DISALLOWED = 1 << 30  # gsnapdp_stage3_pass_compact: an input pair whose disallowedp the pass set
 
 # a splicing IIT's intervals (include/gsnapdp.h: gsnapdp_iit_interval); start > end is the minus sign,

@@ -658,6 +658,8 @@ typedef struct gsnapdp_s3_stats {
                          * expansion), the time it waited for a batch, the whole pass */
   int64_t new_pairs;    /* pairs the pass made among the returned lists (the new_out a compact
                          * pass needs; written also when new_out was too small) */
+  int64_t out_needed;   /* the pairs, cells or runs the returned lists took (written also when the
+                         * output was too small) */
 } gsnapdp_s3_stats;
 
 /* Runs the pass; pairs_in holds npairs_in pairs and query / query_uc
@@ -692,6 +694,30 @@ int gsnapdp_stage3_pass_compact(gsnapdp_ctx *ctx, gsnapdp_s3_call *calls, int nc
                                 const char *query_uc, size_t query_bytes, const gsnapdp_iit *iit,
                                 int32_t *cells_out, int64_t cells_cap, gsnapdp_s3_pair *new_out, int64_t new_cap,
                                 gsnapdp_s3_stats *stats);
+
+/* The same pass with the returned lists as runs, and the gap pairs named by
+ * the caller, so that a path costs its gaps, not its pairs (a 5 kbp transcript
+ * holds ~5,000 pairs around ~10 gaps).  gaps[gap_off[i] .. gap_off[i + 1]) are
+ * the indices (within call i's path, ascending) of exactly the pairs whose
+ * flags have GSNAPDP_S3_GAPP -- what insert_gapholders knows as it inserts
+ * them (stage3.c:902-916); gaps = gap_off = NULL finds them from the flags (one
+ * read of every pair).  runs_out[first_out .. first_out + nout) is call i's
+ * list in list order (first_out / nout count runs here), each run
+ *   start >= 0: input pairs start, start - 1, .., start - n + 1 of the call's
+ *               path (n = count & ~GSNAPDP_S3_CELL_DISALLOWED; with the bit set,
+ *               the pass set their disallowedp, stage3.c:5873-5880)
+ *   start <  0: new_out[-1 - start .. -1 - start + count), pairs the pass made
+ * runs_cap too small fails with stats->out_needed set (2 * (querylength +
+ * npairs) + 64 per call always suffices; ~4 per gap is typical), new_cap as
+ * gsnapdp_stage3_pass_compact. */
+typedef struct gsnapdp_s3_run {
+  int32_t start, count;
+} gsnapdp_s3_run;
+int gsnapdp_stage3_pass_runs(gsnapdp_ctx *ctx, gsnapdp_s3_call *calls, int ncalls,
+                             const gsnapdp_s3_pair *pairs_in, int64_t npairs_in, const int32_t *gaps,
+                             const int64_t *gap_off, const char *query, const char *query_uc, size_t query_bytes,
+                             const gsnapdp_iit *iit, gsnapdp_s3_run *runs_out, int64_t runs_cap,
+                             gsnapdp_s3_pair *new_out, int64_t new_cap, gsnapdp_s3_stats *stats);
 
 /* traverse_dual_break's stage-2 realignment (stage3.c:7044-7142): build_dual_breaks
  * runs Stage2_compute_one (stage2.c:4260) on the query bytes [querydp5, querydp3]
@@ -798,6 +824,13 @@ int gsnapdp_pbinom(int k, int n, double theta, double *p);
 int gsnapdp_stage3_score_introns(gsnapdp_ctx *ctx, const gsnapdp_s3_call *calls, int ncalls,
                                  const gsnapdp_s3_pair *pairs_out, const gsnapdp_iit *iit,
                                  gsnapdp_intron_scores *scores);
+/* The same on gsnapdp_stage3_pass_runs' output (calls as it left them, its
+ * pairs_in, gaps / gap_off (or NULL) and new_out): only each list's gap pairs
+ * and their neighbours are read. */
+int gsnapdp_stage3_score_introns_runs(gsnapdp_ctx *ctx, const gsnapdp_s3_call *calls, int ncalls,
+                                      const gsnapdp_s3_pair *pairs_in, const int32_t *gaps, const int64_t *gap_off,
+                                      const gsnapdp_s3_run *runs, const gsnapdp_s3_pair *new_pairs,
+                                      const gsnapdp_iit *iit, gsnapdp_intron_scores *scores);
 
 /* Load the MaxEnt parameter tables (12 x 16384 + 4 x 16 doubles, order in
  * DESIGN.md) into the context.  Must be called before gsnapdp_maxent_*. */

@@ -237,6 +237,11 @@ def s3lib():
         L.gsnapdp_stage3_pass_compact.restype = i32
         L.gsnapdp_stage3_score_introns.argtypes = [vp, vp, i32, vp, vp, vp]
         L.gsnapdp_stage3_score_introns.restype = i32
+        L.gsnapdp_stage3_pass_runs.argtypes = [vp, vp, i32, vp, i64, vp, vp, vp, vp, ctypes.c_size_t, vp, vp, i64,
+                                               vp, i64, vp]
+        L.gsnapdp_stage3_pass_runs.restype = i32
+        L.gsnapdp_stage3_score_introns_runs.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]
+        L.gsnapdp_stage3_score_introns_runs.restype = i32
         L.gsnapdp_iit_from_intervals.argtypes = [vp, i32]
         L.gsnapdp_iit_from_intervals.restype = vp
         L.gsnapdp_iit_free.argtypes = [vp]
@@ -341,6 +346,42 @@ class Stage3Cpu:
         finally:
             L.gsnapdp_oracle_stash_reset()
         return c, cells[:int(c["nout"].sum())], new[:int(st[0]["new_pairs"])], st[0]
+
+    def run_runs(self, calls, pairs_in, query, query_uc, gaps=None, gap_off=None, introns=False):
+        """gsnapdp_stage3_pass_runs (+ gsnapdp_stage3_score_introns_runs):
+        (calls, runs, new pairs, S3_STATS[, INTRON_SCORES])"""
+        from gsnapdp.records import INTRON_SCORES, S3_CALL, S3_PAIR, S3_RUN, S3_STATS
+        L = s3lib()
+        c = np.array(calls, dtype=S3_CALL, copy=True)
+        pi = np.ascontiguousarray(pairs_in, dtype=S3_PAIR)
+        q = np.ascontiguousarray(query, dtype=np.uint8)
+        qu = np.ascontiguousarray(query_uc, dtype=np.uint8)
+        g = go = None
+        if gaps is not None:
+            g = np.ascontiguousarray(gaps, dtype=np.int32)
+            go = np.ascontiguousarray(gap_off, dtype=np.int64)
+        gp = (g.ctypes.data if g.size else go.ctypes.data) if g is not None else None
+        gop = go.ctypes.data if go is not None else None
+        cap = int((2 * (c["querylength"].astype(np.int64) + c["npairs"]) + 64).sum()) if len(c) else 1
+        ncap = int((2 * c["querylength"].astype(np.int64) + 256).sum()) if len(c) else 1
+        runs = np.empty(max(cap, 1), dtype=S3_RUN)
+        new = np.empty(max(ncap, 1), dtype=S3_PAIR)
+        st = np.zeros(1, dtype=S3_STATS)
+        try:
+            if L.gsnapdp_stage3_pass_runs(self.h, c.ctypes.data, len(c), pi.ctypes.data, pi.size, gp, gop,
+                                          q.ctypes.data, qu.ctypes.data, min(q.size, qu.size), None,
+                                          runs.ctypes.data, runs.size, new.ctypes.data, new.size, st.ctypes.data):
+                raise RuntimeError("libstage3_cpu pass_runs: %s" % L.s3cpu_last_error().decode())
+            res = (c, runs[:int(c["nout"].sum())], new[:int(st[0]["new_pairs"])], st[0])
+            if introns:
+                sc = np.zeros(len(c), dtype=INTRON_SCORES)
+                if L.gsnapdp_stage3_score_introns_runs(self.h, c.ctypes.data, len(c), pi.ctypes.data, gp, gop,
+                                                       runs.ctypes.data, new.ctypes.data, None, sc.ctypes.data):
+                    raise RuntimeError("libstage3_cpu score_introns_runs: %s" % L.s3cpu_last_error().decode())
+                res = res + (sc,)
+        finally:
+            L.gsnapdp_oracle_stash_reset()
+        return res
 
     def run(self, calls, pairs_in, query, query_uc, intervals=None, introns=False):
         """(calls with out fields, the returned lists, S3_STATS[, INTRON_SCORES])"""

@@ -73,3 +73,27 @@ def test_c4_pass_cpu_matches_reference_prefix(golden_dir, tmp_path):
                                               w.query_uc, introns=True)
     check_c4(z, calls, lists, "c4 prefix", scores)
     assert st["windows"][1] > 0
+
+
+def test_c4_runs_cpu_matches_reference_prefix(golden_dir):
+    """the runs output (gsnapdp_stage3_pass_runs, the caller's gap lists) and
+    score_introns on the runs, the DP served by the restatement
+    (oracle/_build/libstage3_cpu.so): the same lists and scores as the reference's"""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import oracle as O  # checker
+    from gsnapdp import expand_runs, gap_lists
+    z = np.load(os.path.join(golden_dir, "c4_pinned.npz"), allow_pickle=False)
+    w = W.c4_transcripts(300, seed=int(z["seed"]))
+    gaps, gap_off = gap_lists(w.calls, w.pairs_in)
+    S = O.Stage3Cpu(w.blocks)
+    try:
+        for g, go in ((gaps, gap_off), (None, None)):
+            c, runs, new, st, sc = S.run_runs(w.calls, w.pairs_in, w.query, w.query_uc, g, go, introns=True)
+            cf, lists = expand_runs(c, w.pairs_in, runs, new)
+            for f in ("first_out", "nout"):
+                c[f] = cf[f]
+            check_c4(z, c, lists, "c4 runs", sc)
+            assert runs.size < lists.size // 50
+    finally:
+        S.close()

@@ -5,7 +5,8 @@ build_pairs_introns with finalp, stage3.c:8860-8875) and score_introns
 
 * the first 2000 transcripts against the reference's own build_pairs_introns /
   score_introns (tests/golden/c4_pinned.npz: counters, scores, list digests),
-  through both output forms of the pass;
+  through the three output forms of the pass (pairs, cells, runs with and
+  without the caller's gap lists) and both score_introns entries;
 * 10k transcripts against the CPU restatement of the pass (the same host code
   with the DP served by oracle/, oracle/_build/libstage3_cpu.so).  bench.py's
   c4_transcripts line checks all 50k the same way."""
@@ -15,7 +16,7 @@ import sys
 import numpy as np
 import pytest
 
-from gsnapdp import Context, expand_compact
+from gsnapdp import Context, expand_compact, expand_runs, gap_lists
 from gsnapdp import workload as W
 from test_c4_cpu import check_c4
 
@@ -33,6 +34,15 @@ def test_gpu_c4_pinned_matches_reference(golden_dir):
     check_c4(z, c, lists, "gpu c4 (compact)", scores)
     c2, full, st2 = ctx.stage3_pass(w.calls, w.pairs_in, w.query, w.query_uc)
     assert full.tobytes() == lists.tobytes() and np.array_equal(c2["nout"], c["nout"])
+    # the runs form, with the caller's gap lists and without (the pass finds them)
+    gaps, gap_off = gap_lists(w.calls, w.pairs_in)
+    for g, go in ((gaps, gap_off), (None, None)):
+        c3, runs, new3, st3, _ = ctx.stage3_pass_runs(w.calls, w.pairs_in, w.query, w.query_uc, g, go)
+        c3f, lists3 = expand_runs(c3, w.pairs_in, runs, new3)
+        assert lists3.tobytes() == lists.tobytes() and np.array_equal(c3f["nout"], c["nout"])
+        assert runs.size < lists.size // 50, (runs.size, lists.size)
+        sc3 = ctx.stage3_score_introns_runs(c3, w.pairs_in, runs, new3, g, go)
+        assert sc3.tobytes() == scores.tobytes()
     print("c4 pinned: %d transcripts, windows %s, %d new pairs, %d rounds" % (len(c), st["windows"],
                                                                              st["new_pairs"], st["rounds"]))
     ctx.close()
@@ -52,4 +62,8 @@ def test_gpu_c4_matches_cpu_restatement():
         assert np.array_equal(c[f], rc[f]), f
     assert np.array_equal(cells, rcells) and new.tobytes() == rnew.tobytes()
     assert list(st["windows"]) == list(rst["windows"])
+    gaps, gap_off = gap_lists(w.calls, w.pairs_in)
+    c3, runs, new3, st3, _ = ctx.stage3_pass_runs(w.calls, w.pairs_in, w.query, w.query_uc, gaps, gap_off)
+    c3f, lists3 = expand_runs(c3, w.pairs_in, runs, new3)
+    assert lists3.tobytes() == expand_compact(c, w.pairs_in, cells, new).tobytes()
     ctx.close()
