@@ -459,42 +459,53 @@ def stage3_cpu_baseline(blocks, calls, pin, q, qu, want=None, compact=False, z=N
     return out if not compact else (out, res)
 
 
-def measure_stage3_compute(copies=8, reps=5, cpu=True):
+def measure_stage3_compute(copies=64, reps=5, cpu=True, small=8):
     """Side line: path_compute from pass 2A to its return value
     (gsnapdp_stage3_path_compute: passes 2A-10, the host steps restated, every
     round of DP passes one gsnapdp_stage3_pass across the queries, each
     assign_gap_types' MaxEnt sites one k_maxent batch) for every path_compute
     call the reference's gmap made on the synthetic cDNAs
-    (tests/golden/gmap_synth_stage3.npz, 168 calls) x `copies`, each copy checked
-    against the list path_compute returned in gmap (pairs and their donor /
-    acceptor probabilities).  traverse_dual_break's stage 2 is served from the
-    recording (tests/dropin/stage2_double.c, built here).  The CPU leg runs the
-    same host code with every DP window and MaxEnt site served by the oracle/
-    restatement, 16 threads."""
+    (tests/golden/gmap_synth_stage3.npz, 168 calls) x `copies` in one batch,
+    each copy checked against the list path_compute returned in gmap (pairs and
+    their donor / acceptor probabilities); `by_batch` gives the same at `small`
+    copies.  traverse_dual_break's stage 2 is served from the recording
+    (tests/dropin/stage2_double.c, built here).  The CPU leg runs the same host
+    code with every DP window and MaxEnt site served by the oracle/ restatement,
+    16 threads."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from test_stage3_cpu import check_path_compute  # list-by-list comparison with the recording
     z = np.load(os.path.join(ROOT, "tests", "golden", "gmap_synth_stage3.npz"), allow_pickle=False)
-    Q, PI, QQ, QU, WANT, WP, FINAL = W.stage3_path_pipeline(z, copies)
-    maxintron = int(FINAL["maxintronlen_bound"][0])
-    out = {"metric": "stage-3 path_compute (passes 2A-10), queries/s", "unit": "queries/s", "queries": int(len(Q))}
     ctx = Context(z["blocks"])
     stage2_double(ctx, z)
-    ctx.stage3_path_compute(Q[:8], PI, QQ, QU, maxintronlen_bound=maxintron)  # warm-up
-    best = None
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        res = ctx.stage3_path_compute(Q, PI, QQ, QU, maxintronlen_bound=maxintron)
-        dt = time.perf_counter() - t0
-        if best is None or dt < best[0]:
-            best = (dt, res)
-    dt, (c, got, probs, st) = best
-    check_path_compute(c, got, probs, WANT, WP, FINAL, "stage3 path_compute")
+
+    def gpu(k):
+        Q, PI, QQ, QU, WANT, WP, FINAL = W.stage3_path_pipeline(z, k)
+        maxintron = int(FINAL["maxintronlen_bound"][0])
+        ctx.stage3_path_compute(Q[:8], PI, QQ, QU, maxintronlen_bound=maxintron)  # warm-up
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            res = ctx.stage3_path_compute(Q, PI, QQ, QU, maxintronlen_bound=maxintron)
+            dt = time.perf_counter() - t0
+            if best is None or dt < best[0]:
+                best = (dt, res)
+        dt, (c, got, probs, st) = best
+        check_path_compute(c, got, probs, WANT, WP, FINAL, "stage3 path_compute x%d" % k)
+        r = {"queries": int(len(Q)), "value": round(len(Q) / dt, 1), "seconds": round(dt, 4),
+             "bit_exact_vs_reference": True, "passes": int(st["passes"]), "rounds": int(st["rounds"]),
+             "maxent_sites": int(st["sites"]), "pass_calls": [int(x) for x in st["pass_calls"]],
+             "windows": [int(x) for x in st["windows"]], "host_steps_s": round(float(st["seconds"][0]), 4),
+             "gpu_wait_s": round(float(st["seconds"][1]), 4),
+             "host_frac": round(float(st["seconds"][0]) / dt, 3)}
+        return r, (Q, PI, QQ, QU, WANT, WP, FINAL, maxintron)
+
+    out = {"metric": "stage-3 path_compute (passes 2A-10), queries/s", "unit": "queries/s"}
+    r, data = gpu(copies)
+    out.update(r)
+    out["by_batch"] = {str(small): gpu(small)[0]}
     ctx.close()
-    out.update({"value": round(len(Q) / dt, 1), "seconds": round(dt, 4), "bit_exact_vs_reference": True,
-                "passes": int(st["passes"]), "rounds": int(st["rounds"]), "maxent_sites": int(st["sites"]),
-                "pass_calls": [int(x) for x in st["pass_calls"]], "windows": [int(x) for x in st["windows"]],
-                "host_steps_s": round(float(st["seconds"][0]), 4), "gpu_wait_s": round(float(st["seconds"][1]), 4)})
     if cpu:
+        Q, PI, QQ, QU, WANT, WP, FINAL, maxintron = data
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # CPU baseline leg
         S = O.Stage3Cpu(z["blocks"])

@@ -1414,6 +1414,9 @@ int compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries, const gsna
       gsnapdp__set_err(std::string(fn) + ": query " + std::to_string(i) + " outside the buffers");
       return -1;
     }
+  }
+  gsnapdp::s3_parallel_for(nqueries, 16, [&](int i) {
+    gsnapdp_s3_call& c = queries[i];
     Query& q = qs[(size_t)i];
     q.c = &c;
     q.list.assign(paths_in + c.first_pair, paths_in + c.first_pair + c.npairs);
@@ -1426,7 +1429,7 @@ int compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries, const gsna
     q.nonintronlen = c.in_nonintronlen;
     first[(size_t)i] = *pipe.call_for(q);  // pass 2A; its list is paths_in[first_pair ..]
     first[(size_t)i].first_pair = c.first_pair;
-  }
+  });
   if (getenv("GSNAPDP_S3_COMPUTE_DUMP")) {  // debugging: the first pass's calls
     char path[4096];
     snprintf(path, sizeof(path), "%s/pass_000_calls.bin", getenv("GSNAPDP_S3_COMPUTE_DUMP"));
@@ -1450,44 +1453,62 @@ int compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries, const gsna
   std::vector<uint8_t> model;
   std::vector<uint32_t> pos, chroff;
   std::vector<double> prob;
+  std::vector<int64_t> soff, loff;
+  std::vector<gsnapdp_s3_call*> next;
   for (;;) {
     map.clear();
-    model.clear(), pos.clear(), chroff.clear();
     for (int i = 0; i < nqueries; i++) {
-      Query& q = qs[(size_t)i];
-      if (q.failed || (q.step != Q_GT_9 && q.step != Q_GT_10)) continue;
-      map.push_back(i);
-      for (const Site& s : q.sites) model.push_back(s.model), pos.push_back(s.pos), chroff.push_back(s.chroffset);
+      const Query& q = qs[(size_t)i];
+      if (!q.failed && (q.step == Q_GT_9 || q.step == Q_GT_10)) map.push_back(i);
     }
     if (map.empty()) break;
-    prob.resize(model.size());
-    if (!model.empty()) {
+    const int nm = (int)map.size();
+    soff.assign((size_t)nm + 1, 0);
+    for (int j = 0; j < nm; j++) soff[(size_t)j + 1] = soff[(size_t)j] + (int64_t)qs[(size_t)map[(size_t)j]].sites.size();
+    const size_t nsites = (size_t)soff[(size_t)nm];
+    model.resize(nsites), pos.resize(nsites), chroff.resize(nsites), prob.resize(nsites);
+    gsnapdp::s3_parallel_for(nm, 64, [&](int j) {
+      size_t at = (size_t)soff[(size_t)j];
+      for (const Site& s : qs[(size_t)map[(size_t)j]].sites)
+        model[at] = s.model, pos[at] = s.pos, chroff[at] = s.chroffset, at++;
+    });
+    if (nsites) {
       const auto t1 = clock::now();
-      if (gsnapdp_maxent_host(ctx, model.data(), pos.data(), chroff.data(), prob.data(), (int)model.size()))
-        return -1;
+      if (gsnapdp_maxent_host(ctx, model.data(), pos.data(), chroff.data(), prob.data(), (int)nsites)) return -1;
       gpu_s += std::chrono::duration<double>(clock::now() - t1).count();
-      st.sites += (int32_t)model.size();
+      st.sites += (int32_t)nsites;
     }
-    size_t at = 0;
-    std::vector<gsnapdp_s3_call> calls;
-    std::vector<int> cmap;
-    phase_in.clear();
-    for (int i : map) {
-      Query& q = qs[(size_t)i];
+    // each parked query's probabilities, its host steps up to its next pass
+    next.assign((size_t)nm, nullptr);
+    gsnapdp::s3_parallel_for(nm, 4, [&](int j) {
+      Query& q = qs[(size_t)map[(size_t)j]];
+      size_t at = (size_t)soff[(size_t)j];
       for (const Site& s : q.sites) {
         Probs& p = q.probs[(size_t)s.row];
         (s.acceptor ? p.a : p.d) = prob[at++];
       }
       q.sites.clear();
       advance(q, env);
-      gsnapdp_s3_call* c = pipe.call_for(q);
-      if (!c) continue;
-      calls.push_back(*c);
-      calls.back().first_pair = (int32_t)phase_in.size();
-      phase_in.insert(phase_in.end(), q.list.begin(), q.list.end());
-      cmap.push_back(i);
+      next[(size_t)j] = pipe.call_for(q);
+    });
+    std::vector<gsnapdp_s3_call> calls;
+    std::vector<int> cmap;
+    loff.clear();
+    int64_t tot = 0;
+    for (int j = 0; j < nm; j++) {
+      if (!next[(size_t)j]) continue;
+      calls.push_back(*next[(size_t)j]);
+      calls.back().first_pair = (int32_t)tot;
+      loff.push_back(tot);
+      tot += (int64_t)qs[(size_t)map[(size_t)j]].list.size();
+      cmap.push_back(map[(size_t)j]);
     }
     if (calls.empty()) continue;
+    phase_in.resize((size_t)tot);
+    gsnapdp::s3_parallel_for((int)cmap.size(), 16, [&](int j) {
+      const List& l = qs[(size_t)cmap[(size_t)j]].list;
+      std::copy(l.begin(), l.end(), phase_in.begin() + loff[(size_t)j]);
+    });
     pipe.set_map(&cmap);
     const int rc = gsnapdp::s3_run_driven(ctx, calls.data(), (int)calls.size(), phase_in.data(),
                                           (int64_t)phase_in.size(), query, query_uc, query_bytes, iit, &pipe, &ps);
@@ -1496,25 +1517,30 @@ int compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries, const gsna
     gpu_s += ps.seconds[1];
     add(ps);
   }
-  // the returned lists, in the caller's buffer
-  int64_t at = 0;
+  // the returned lists, in the caller's buffer (offsets, then the copies)
+  std::vector<int64_t> ooff((size_t)nqueries + 1, 0);
   for (int i = 0; i < nqueries; i++) {
-    Query& q = qs[(size_t)i];
+    const Query& q = qs[(size_t)i];
     for (int p = 0; p < 6; p++) st.pass_calls[p] += q.passes[p];
-    gsnapdp_s3_call& c = *q.c;
-    c.status = q.failed ? -1 : 0;
-    c.first_out = (int32_t)at;
-    c.nout = q.failed ? 0 : (int32_t)q.list.size();
+    ooff[(size_t)i + 1] = ooff[(size_t)i] + (q.failed ? 0 : (int64_t)q.list.size());
     if (q.failed) {
       st.failed++;
       if (getenv("GSNAPDP_S3_DEBUG"))
-        fprintf(stderr, "%s: query %d (tag %d) failed: %s\n", fn, i, c.invocation, q.why.c_str());
-      continue;
+        fprintf(stderr, "%s: query %d (tag %d) failed: %s\n", fn, i, q.c->invocation, q.why.c_str());
     }
-    if (at + c.nout > out_cap) {
-      gsnapdp__set_err(std::string(fn) + ": the output is too small");
-      return -1;
-    }
+  }
+  if (ooff[(size_t)nqueries] > out_cap) {
+    gsnapdp__set_err(std::string(fn) + ": the output is too small");
+    return -1;
+  }
+  gsnapdp::s3_parallel_for(nqueries, 16, [&](int i) {
+    Query& q = qs[(size_t)i];
+    gsnapdp_s3_call& c = *q.c;
+    const int64_t at = ooff[(size_t)i];
+    c.status = q.failed ? -1 : 0;
+    c.first_out = (int32_t)at;
+    c.nout = (int32_t)(ooff[(size_t)i + 1] - at);
+    if (q.failed) return;
     for (int64_t j = 0; j < c.nout; j++) {
       gsnapdp_s3_pair p = q.list[(size_t)j];
       if (probs_out) {
@@ -1525,7 +1551,6 @@ int compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries, const gsna
       p.src = -1;
       out[at + j] = p;
     }
-    at += c.nout;
     c.out_minor = q.minor;
     c.out_major = q.major;
     c.out_nintrons = q.nintrons;
@@ -1536,7 +1561,7 @@ int compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries, const gsna
     c.incompletep = q.incompletep ? 1 : 0;
     c.defect_rate = q.defect;
     c.ub = q.ub;
-  }
+  });
   st.seconds[1] = gpu_s;  // the time the host waited for the GPU
   st.seconds[2] = std::chrono::duration<double>(clock::now() - t0).count();
   st.seconds[0] = st.seconds[2] - st.seconds[1];
