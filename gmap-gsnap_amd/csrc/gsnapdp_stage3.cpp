@@ -1772,15 +1772,13 @@ void finish_path(Pass& P, Path& k) {
       if (k.c->pass == GSNAPDP_S3_END3) k.pairs = k.path;  // build_path_end3 returns its path
       const Arena& A = k.A;
       list.reserve((size_t)A.nin + A.extra.size());  // every cell at most once
+      // a reversed block copy of each input run; src stays the input pair's own
+      // (the driver's numbering, not the pass's position)
       walk_list(
           A, k.pairs,
-          [&](int hi, int lo, bool d) {  // a reversed block copy (A.out of each)
-            for (int x = hi; x >= lo; x--) {
-              list.push_back(A.in[x]);
-              gsnapdp_s3_pair& o = list.back();
-              o.src = x;
-              if (d) o.flags |= GSNAPDP_S3_DISALLOWED;
-            }
+          [&](int hi, int lo, bool d) {
+            list.insert(list.end(), std::make_reverse_iterator(A.in + hi + 1), std::make_reverse_iterator(A.in + lo));
+            if (d) list.back().flags |= GSNAPDP_S3_DISALLOWED;  // (a disallowed pair is a run of its own)
           },
           [&](int e) { list.push_back(A.extra[(size_t)e].p); });
     }

@@ -63,7 +63,9 @@ void s3_exec_release(gsnapdp_ctx* ctx, S3Exec* e);
 
 // Driven passes (gsnapdp_stage3_compute): when path i's pass ends, next() gets
 // its call (out fields written, status -1 for a failed path) and its list (list
-// order, full records; the driver may take the vector's storage), and returns the path's next pass -- its call, and its
+// order, full records, an input pair with the src the driver gave it, a new
+// pair with src -1; the driver may take the vector's storage), and returns the
+// path's next pass -- its call, and its
 // list in *pairs / *n, which must stay valid until that pass ends -- or nullptr
 // when the path is finished.  The next pass starts in the same round, so paths
 // at different passes share every round's batches.  Called on the pass's host

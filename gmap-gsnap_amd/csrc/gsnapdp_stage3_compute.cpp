@@ -935,7 +935,6 @@ struct Query {
   int ub = 0;
   int passes[6] = {0, 0, 0, 0, 0, 0};
   gsnapdp_s3_call k;        // the pending pass's call (its pairs are list)
-  std::vector<int> insrc;   // the pending pass's input pairs' src (the pass renumbers them)
   std::vector<Probs> probs; // assign_gap_types' rows
   std::vector<Site> sites;  // parked: the rows' MaxEnt sites
   int iter10 = 0;           // pass 10's iterations
@@ -1351,8 +1350,6 @@ class Pipeline final : public gsnapdp::S3Driver {
     k.in_intronlen = q.intronlen;
     k.in_nonintronlen = q.nonintronlen;
     q.passes[k.pass]++;
-    q.insrc.resize(q.list.size());
-    for (size_t j = 0; j < q.list.size(); j++) q.insrc[j] = q.list[j].src;
     return &k;
   }
   gsnapdp_s3_call* next(int i, gsnapdp_s3_call* k, std::vector<gsnapdp_s3_pair>& list,
@@ -1362,9 +1359,8 @@ class Pipeline final : public gsnapdp::S3Driver {
       fail(q, "a DP pass failed on the path (status -1)");
       return nullptr;
     }
-    q.list.swap(list);  // (the pass's buffer takes the old list's storage for its next use)
-    for (gsnapdp_s3_pair& p : q.list)  // the pass's src is the input position: back to table rows
-      p.src = p.src >= 0 ? q.insrc[(size_t)p.src] : -1;
+    q.list.swap(list);  // (the pass's buffer takes the old list's storage for its next use; a
+                        // driven pass returns each input pair with its own src: the table row)
     q.minor = k->out_minor;
     q.major = k->out_major;
     q.ub |= k->ub;
