@@ -188,19 +188,20 @@ __global__ void k_scan(int* __restrict__ hist, int* __restrict__ cursor,
     const int k = lo + i;
     if (k >= NKEYS) break;
     cursor[k] = run;
+    // class c covers W in (CLASS_W[c-1], CLASS_W[c]] and keys are W-major: the
+    // thread holding a class's first key writes its start (no serial re-read
+    // of the cursors after a barrier)
+#pragma unroll
+    for (int c = 0; c < NCLASS; c++)
+      if (k == first_key_of_w(class_low(c))) class_start[c] = run;
     for (int e = run + h[i]; e < run + p[i]; e++) perm[e] = -1;
     run += p[i];
     hist[k] = 0;
   }
-  __syncthreads();
   if (tid == 0) {
-    // class c covers W in (CLASS_W[c-1], CLASS_W[c]]; keys are W-major
-    int wlo = 0;
-    for (int c = 0; c < NCLASS; c++) {
-      const int kfirst = first_key_of_w(wlo + 1);
-      class_start[c] = kfirst < NKEYS ? cursor[kfirst] : total;
-      wlo = CLASS_W[c];
-    }
+#pragma unroll
+    for (int c = 0; c < NCLASS; c++)
+      if (first_key_of_w(class_low(c)) >= NKEYS) class_start[c] = total;
     class_start[NCLASS] = total;
   }
 }
@@ -815,7 +816,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
     const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
     uint32_t* __restrict__ dirpool, size_t wave_stride, gsnapdp_result* __restrict__ res,
     uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off, const int* __restrict__ end_flag,
-    const gsnapdp_sj_window* __restrict__ sjw) {
+    const gsnapdp_sj_window* __restrict__ sjw, int min_tasks) {
   __shared__ alignas(8) uint32_t sprof[SPROF_WORDS];
   __shared__ uint32_t rings[4][RING_WORDS_MAX];  // one per wave of the block
   for (int i = threadIdx.x; i < MLUT; i += blockDim.x)
@@ -828,9 +829,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
   }
   __syncthreads();
   uint32_t* ring = rings[threadIdx.x >> 6];
-  const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nw = (gridDim.x * blockDim.x) >> 6;
-  uint32_t* D = dirpool + (size_t)gw * wave_stride;
+  uint32_t* D = dirpool + (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * wave_stride;
   // the kinds of task in the batch (bit e: END = e; k_plan sets bits 1, 2; a
   // segment batch has end gaps only): each kind's bodies are called only when present
   const int ends = (sjw ? 0 : 1) | *end_flag;
@@ -839,6 +838,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
 #pragma unroll
   for (int c = 0; c < NCLASS; c++)
     tfirst[c + 1] = tfirst[c] + (class_start[c + 1] - class_start[c]) / (64 / CLASS_LPW[c]);
+  // Small batches: a wave's traceback sweep serves up to TB_BATCH tasks and
+  // costs about the same with one task as with four, so a batch with fewer
+  // than min_tasks tasks per wave runs on kw < GSNAPDP_FILL_WAVES waves per
+  // SIMD.  The grid is GSNAPDP_FILL_WAVES blocks per CU; block b is active when
+  // b % GSNAPDP_FILL_WAVES < kw, which leaves every CU kw of its blocks
+  // whether the dispatcher places blocks across the CUs first or per CU.
+  int kw = GSNAPDP_FILL_WAVES;
+  if (min_tasks > 0) {
+    const int simds = (int)((gridDim.x * blockDim.x) >> 6) / GSNAPDP_FILL_WAVES;
+    kw = (tfirst[NCLASS] + min_tasks * simds - 1) / (min_tasks * simds);
+    kw = kw < 1 ? 1 : (kw > GSNAPDP_FILL_WAVES ? GSNAPDP_FILL_WAVES : kw);
+  }
+  if ((int)(blockIdx.x % GSNAPDP_FILL_WAVES) >= kw) return;  // (no block barrier follows)
+  const int gw = ((((int)blockIdx.x / GSNAPDP_FILL_WAVES) * kw + (int)blockIdx.x % GSNAPDP_FILL_WAVES) *
+                      (int)blockDim.x + (int)threadIdx.x) >> 6;
+  const int nw = ((int)gridDim.x / GSNAPDP_FILL_WAVES * kw * (int)blockDim.x) >> 6;
   // the wave takes global task indices tau = gw, gw + nw, ...; those of class c
   // are its tasks t = base_c + (tau - tfirst[c]), visited class by class
   static_assert(NCLASS <= 8, "k_fill dispatches at most 8 classes");
@@ -1111,6 +1126,10 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
     // on k_ggap (DESIGN.md §4 k_gband)
     const char* m = getenv("GSNAPDP_GBAND_MIN");
     if (m) ctx->gband_min = atoi(m);
+    // k_fill on fewer waves per SIMD when a batch gives each wave fewer than
+    // this many tasks (0: always GSNAPDP_FILL_WAVES)
+    const char* mt = getenv("GSNAPDP_FILL_MIN_TASKS");
+    if (mt) ctx->fill_min_tasks = atoi(mt);
     const char* f = getenv("GSNAPDP_ENDS_ROWLANE");
     ctx->ends_rowlane = (f && f[0] == '1') ? 1 : 0;
   }
@@ -1231,7 +1250,8 @@ int gsnapdp__fill_pipeline(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_windo
   mark(2, 0);
   hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, st, d_windows, ctx->d_perm, class_start,
                      d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_dirpool,
-                     WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets, big_count + RW_NCLS, sjw);
+                     WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets, big_count + RW_NCLS, sjw,
+                     ctx->fill_min_tasks);
   mark(2, 1);
   if constexpr (!FILL_MATCH) {
     mark(7, 0);

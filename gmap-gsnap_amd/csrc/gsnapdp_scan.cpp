@@ -1,6 +1,9 @@
-// gsnapdp_scan.cpp -- GSNAP's splice-site scans batched (stage1hr.c:6300-7046,
-// 8703-8976): the MaxEnt probability of every candidate site of many reads in
-// one k_maxent launch (include/gsnapdp.h gsnapdp_scan_site_probs).  Host code.
+// gsnapdp_scan.cpp -- the MaxEnt half of GSNAP's splice-site scans
+// (stage1hr.c:6300-7046, 8703-8976): the probability of every caller-supplied
+// candidate site of many reads in one k_maxent launch (include/gsnapdp.h
+// gsnapdp_scan_site_probs).  The candidate generation (Genome_donor_positions
+// and the like) is defined in genome_hr.c, a missing blob of the reference, so
+// it is not restated here (parity unpinned).  Host code.
 #include <stdint.h>
 
 #include <string>

@@ -1836,8 +1836,7 @@ class Workers {
     work();
     // the workers are spinning or waking; a run is a few hundred microseconds,
     // so the caller spins for them too rather than sleeping on a condition
-    while (active_.load(std::memory_order_acquire) != 0) {
-    }
+    while (active_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
     fn_ = nullptr;
   }
 
@@ -1854,6 +1853,7 @@ class Workers {
     for (;;) {
       const auto t0 = std::chrono::steady_clock::now();
       while (gen_.load(std::memory_order_acquire) == seen) {
+        __builtin_ia32_pause();
         if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
           std::unique_lock<std::mutex> l(m_);
           cv_.wait(l, [&] { return gen_.load() != seen; });

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <chrono>
 #include <string>
+#include <memory>
 #include <vector>
 
 #include "../../include/gsnapdp.h"
@@ -1445,7 +1446,10 @@ int compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries, const gsna
   // the parked queries' assign_gap_types: one MaxEnt batch for all their sites,
   // then their next passes in one more driven pass, until none parks
   std::vector<int> map;
-  std::vector<gsnapdp_s3_pair> phase_in;
+  // the parked queries' lists for their next driven pass: a buffer that is
+  // copied into, never value-initialised (a resize would zero ~30 B per pair)
+  std::unique_ptr<gsnapdp_s3_pair[]> phase_in;
+  size_t phase_cap = 0;
   std::vector<uint8_t> model;
   std::vector<uint32_t> pos, chroff;
   std::vector<double> prob;
@@ -1500,14 +1504,17 @@ int compute(gsnapdp_ctx* ctx, gsnapdp_s3_call* queries, int nqueries, const gsna
       cmap.push_back(map[(size_t)j]);
     }
     if (calls.empty()) continue;
-    phase_in.resize((size_t)tot);
+    if ((size_t)tot > phase_cap) {
+      phase_cap = (size_t)tot + (size_t)tot / 8;
+      phase_in.reset(new gsnapdp_s3_pair[phase_cap]);  // (default-initialised: no zeroing)
+    }
     gsnapdp::s3_parallel_for((int)cmap.size(), 16, [&](int j) {
       const List& l = qs[(size_t)cmap[(size_t)j]].list;
-      std::copy(l.begin(), l.end(), phase_in.begin() + loff[(size_t)j]);
+      std::copy(l.begin(), l.end(), phase_in.get() + loff[(size_t)j]);
     });
     pipe.set_map(&cmap);
-    const int rc = gsnapdp::s3_run_driven(ctx, calls.data(), (int)calls.size(), phase_in.data(),
-                                          (int64_t)phase_in.size(), query, query_uc, query_bytes, iit, &pipe, &ps);
+    const int rc = gsnapdp::s3_run_driven(ctx, calls.data(), (int)calls.size(), phase_in.get(), tot, query,
+                                          query_uc, query_bytes, iit, &pipe, &ps);
     pipe.set_map(nullptr);
     if (rc) return -1;
     gpu_s += ps.seconds[1];

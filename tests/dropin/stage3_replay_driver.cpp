@@ -9,6 +9,8 @@
 //   stage3_host_replay DIR [REPS]   DIR holds the recorded pass: calls.bin pairs_in.bin
 //                                   query.bin query_uc.bin genome.u32 round_*.bin;
 //                                   checks every rep's lists against DIR/pairs_out.bin
+//                                   (with DIR/gaps.bin + gap_off.bin: the runs-mode pass,
+//                                   checked against DIR/runs_out.bin + new_out.bin)
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -72,6 +74,40 @@ int main(int argc, char** argv) {
   ctx.blocks = blocks.data();
   ctx.nwords = blocks.size();
   gsnapdp::build_profile_table(0, ctx.prof);
+  // runs mode (gsnapdp_stage3_pass_runs) when the recording holds the caller's gap lists
+  FILE* gf = fopen((d + "/gaps.bin").c_str(), "rb");
+  if (gf) {
+    fclose(gf);
+    std::vector<int32_t> gaps = slurp<int32_t>(d + "/gaps.bin");
+    std::vector<int64_t> gap_off = slurp<int64_t>(d + "/gap_off.bin");
+    std::vector<gsnapdp_s3_run> want_runs = slurp<gsnapdp_s3_run>(d + "/runs_out.bin");
+    std::vector<gsnapdp_s3_pair> want_new = slurp<gsnapdp_s3_pair>(d + "/new_out.bin");
+    std::vector<gsnapdp_s3_run> runs(want_runs.size() + 1024);
+    int64_t ncap = 0;
+    for (const gsnapdp_s3_call& c : calls0) ncap += 2 * (int64_t)c.querylength + 256;
+    std::vector<gsnapdp_s3_pair> news((size_t)ncap);
+    for (int r = 0; r < reps; r++) {
+      std::vector<gsnapdp_s3_call> calls = calls0;
+      gsnapdp_s3_stats st;
+      const auto t0 = std::chrono::steady_clock::now();
+      if (gsnapdp_stage3_pass_runs(&ctx, calls.data(), (int)calls.size(), in.data(), (int64_t)in.size(), gaps.data(),
+                                   gap_off.data(), q.data(), qu.data(), std::min(q.size(), qu.size()), nullptr,
+                                   runs.data(), (int64_t)runs.size(), news.data(), ncap, &st)) {
+        fprintf(stderr, "gsnapdp_stage3_pass_runs: %s\n", g_err.c_str());
+        return 5;
+      }
+      const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      int64_t nout = 0;
+      for (const gsnapdp_s3_call& c : calls) nout += c.nout;
+      const bool same = (size_t)nout == want_runs.size() && (size_t)st.new_pairs == want_new.size() &&
+                        !memcmp(runs.data(), want_runs.data(), want_runs.size() * sizeof(want_runs[0])) &&
+                        !memcmp(news.data(), want_new.data(), want_new.size() * sizeof(want_new[0]));
+      printf("rep %d: %zu paths in %.4f s = %.0f paths/s, %d rounds, runs %s\n", r, calls.size(), dt,
+             calls.size() / dt, st.rounds, same ? "identical to the GPU run's" : "DIFFER");
+      if (!same) return 6;
+    }
+    return 0;
+  }
   int64_t cap = 0;
   for (const gsnapdp_s3_call& c : calls0) cap += 2 * ((int64_t)c.querylength + c.npairs) + 64;
   std::vector<gsnapdp_s3_pair> out((size_t)cap);

@@ -40,6 +40,12 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
                                  : "+v"(v[i]) : "v"(w[i]));
       if (OP == 12) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(v[i]) : "v"(w[i]));
       if (OP == 13) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(v[i]) : "v"(w[i]));
+      if (OP == 14) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(v[i]) : "v"(w[i]));
+      if (OP == 15) asm volatile("v_pk_sub_u16 %0, %0, %1" : "+v"(v[i]) : "v"(w[i]));
+      if (OP == 16)  // three simple 32-bit-encoded ops per chain step (counted as 3 instructions)
+        asm volatile("v_max_u16 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_sub_u16 %0, %0, %1" : "+v"(v[i]) : "v"(w[i]));
+      if (OP == 17)  // their packed forms
+        asm volatile("v_pk_max_u16 %0, %0, %1\n v_pk_add_u16 %0, %0, %1\n v_pk_sub_u16 %0, %0, %1" : "+v"(v[i]) : "v"(w[i]));
     }
   }
   uint32_t acc = 0;
@@ -48,7 +54,8 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
 }
 static const char* NAMES[] = {"v_add_u32", "v_max_u16", "v_sub_u16", "v_sub_u16_sdwa(hi,pres)", "v_perm_b32",
                               "v_and_or_b32", "v_alignbit_b32", "v_sub_u32", "v_lshrrev_b64", "v_lshl_or_b32",
-                              "v_bfe_u32", "v_mov_b32_dpp", "v_pk_max_u16", "v_cndmask_b32_e32"};
+                              "v_bfe_u32", "v_mov_b32_dpp", "v_pk_max_u16", "v_cndmask_b32_e32",
+                              "v_pk_add_u16", "v_pk_sub_u16", "max/add/sub (per op)", "pk max/add/sub (per op)"};
 template <int OP, int CHAINS>
 static double cyc(int cus, int wps, uint32_t* out) {
   hipEvent_t a, b;
@@ -63,7 +70,7 @@ static double cyc(int cus, int wps, uint32_t* out) {
   float ms;
   (void)hipEventElapsedTime(&ms, a, b);
   // SIMD cycles / (wave-instructions per SIMD)
-  return ms * 1e-3 * 2.4e9 / ((double)wps * N_ITERS * CHAINS);
+  return ms * 1e-3 * 2.4e9 / ((double)wps * N_ITERS * CHAINS * (OP >= 16 ? 3 : 1));
 }
 template <int OP>
 static void row(int cus, uint32_t* out) {
@@ -84,5 +91,6 @@ int main() {
   row<0>(cus, out); row<1>(cus, out); row<2>(cus, out); row<3>(cus, out); row<4>(cus, out);
   row<5>(cus, out); row<6>(cus, out); row<7>(cus, out); row<8>(cus, out); row<9>(cus, out);
   row<10>(cus, out); row<11>(cus, out); row<12>(cus, out); row<13>(cus, out);
+  row<14>(cus, out); row<15>(cus, out); row<16>(cus, out); row<17>(cus, out);
   return 0;
 }
