@@ -70,6 +70,7 @@ struct gsnapdp_ctx {
   std::string arch;
   std::mutex mu;
   int fill_waves = 0;  // waves launched per k_fill class kernel
+  int fill_stagger = 0;  // k_fill: first traceback batch k * this short in the k-th block of a CU (GSNAPDP_FILL_STAGGER)
   int fill_min_tasks = 0;  // k_fill: fewer waves per SIMD below this many tasks per wave (GSNAPDP_FILL_MIN_TASKS)
   int num_cus = 0;
   // per-stage event timing (gsnapdp_profile)

@@ -740,7 +740,7 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
                                         AS_LDS uint32_t* ring3,
                                         AS_GLOBAL uint32_t* D1, AS_GLOBAL gsnapdp_result* res1,
                                         AS_GLOBAL uint32_t* ops1, const AS_GLOBAL int64_t* op_off1,
-                                        const AS_GLOBAL gsnapdp_sj_window* sjw1) {
+                                        const AS_GLOBAL gsnapdp_sj_window* sjw1, int lag) {
   const gsnapdp_window* __restrict__ Wn = (const gsnapdp_window*)Wn1;
   const int* __restrict__ perm = (const int*)perm1;
   const char* __restrict__ q = (const char*)q1;
@@ -762,11 +762,17 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
   };
   int t = t0;
   while (t < t1 && kind_of(t) != END) t += stride;
+  // lag > 0: the wave's first batch is lag tasks short, so that the waves
+  // sharing a SIMD reach their (latency-bound) traceback sweeps at different
+  // times instead of together
+  int bsz = lag > 0 ? (B - lag > 1 ? B - lag : 1) : B;
   while (t < t1) {
     // this lane's window in the batch's sweep: group (lane % NG) of task lane / NG
     int my_wi = -1, my_jl = 0;
     FillOut my = {0, 0, 0};
-    for (int k = 0; k < B && t < t1; k++) {
+    const int bk = bsz;
+    bsz = B;
+    for (int k = 0; k < bk && t < t1; k++) {
       uint32_t* Dk = D + (size_t)k * FILL_REGION_DW;
       uint8_t* Mk = (uint8_t*)(Dk + FILL_COLS_DEV * 64);
       const int wi0 = perm[(size_t)t * NG + g];
@@ -816,7 +822,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
     const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
     uint32_t* __restrict__ dirpool, size_t wave_stride, gsnapdp_result* __restrict__ res,
     uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off, const int* __restrict__ end_flag,
-    const gsnapdp_sj_window* __restrict__ sjw, int min_tasks) {
+    const gsnapdp_sj_window* __restrict__ sjw, int min_tasks, int stagger) {
   __shared__ alignas(8) uint32_t sprof[SPROF_WORDS];
   __shared__ uint32_t rings[4][RING_WORDS_MAX];  // one per wave of the block
   for (int i = threadIdx.x; i < MLUT; i += blockDim.x)
@@ -833,6 +839,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
   // the kinds of task in the batch (bit e: END = e; k_plan sets bits 1, 2; a
   // segment batch has end gaps only): each kind's bodies are called only when present
   const int ends = (sjw ? 0 : 1) | *end_flag;
+  const int lag = (int)(blockIdx.x % GSNAPDP_FILL_WAVES) * stagger;  // fill_tasks: the first batch's shortfall
   int tfirst[NCLASS + 1];  // first task index of each class, then the total
   tfirst[0] = 0;
 #pragma unroll
@@ -863,7 +870,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
       (const AS_GLOBAL char*)q, (const AS_GLOBAL char*)qu, (const AS_GLOBAL uint32_t*)blocks,      \
       nwords, (const AS_LDS uint32_t*)sprof, (AS_LDS uint32_t*)ring, (AS_GLOBAL uint32_t*)D,       \
       (AS_GLOBAL gsnapdp_result*)res, (AS_GLOBAL uint32_t*)ops, (const AS_GLOBAL int64_t*)op_off,  \
-      (const AS_GLOBAL gsnapdp_sj_window*)sjw);
+      (const AS_GLOBAL gsnapdp_sj_window*)sjw, lag);
 #define FILL_CLASS(C)                                                                            \
   if constexpr (C < NCLASS) {                                                                    \
     const int lo = tfirst[C], hi = tfirst[C + 1];                                                \
@@ -1130,6 +1137,9 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
     // this many tasks (0: always GSNAPDP_FILL_WAVES)
     const char* mt = getenv("GSNAPDP_FILL_MIN_TASKS");
     if (mt) ctx->fill_min_tasks = atoi(mt);
+    // the first traceback batch of the k-th block of a CU is k * this many tasks short
+    const char* sg = getenv("GSNAPDP_FILL_STAGGER");
+    if (sg) ctx->fill_stagger = atoi(sg);
     const char* f = getenv("GSNAPDP_ENDS_ROWLANE");
     ctx->ends_rowlane = (f && f[0] == '1') ? 1 : 0;
   }
@@ -1251,7 +1261,7 @@ int gsnapdp__fill_pipeline(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_windo
   hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, st, d_windows, ctx->d_perm, class_start,
                      d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_dirpool,
                      WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets, big_count + RW_NCLS, sjw,
-                     ctx->fill_min_tasks);
+                     ctx->fill_min_tasks, ctx->fill_stagger);
   mark(2, 1);
   if constexpr (!FILL_MATCH) {
     mark(7, 0);

@@ -8,10 +8,9 @@ from gsnapdp import Context, op_offsets
 from gsnapdp import workload as W
 from gsnapdp.records import RESULT
 
-if os.environ.get("ABLATE_C3") == "1":  # the headline batch (bench.py's C3)
-    g3 = W.c3_genome(seed=3)
+if os.environ.get("ABLATE_C3") == "1":  # the headline batch (bench.py's C3, node-cached)
+    g3, batch = W.c3_cached(int(os.environ.get("ABLATE_READS", "1000000")), 0)
     blocks = g3.blocks
-    batch = W.c3_windows(g3, n=1_000_000, seed=33)
 else:
     genome = W.synthetic_genome(64_000_000, seed=1)
     blocks = W.pack_genome(genome)

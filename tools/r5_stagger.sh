@@ -1,0 +1,11 @@
+# traceback-batch stagger (GSNAPDP_FILL_STAGGER): GPU suite on the product, then C3 and 125k k_fill per setting, alternating
+O=gpurun_out/${1:-r5s1}; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+tail -1 $O/pytest.txt
+for i in 1 2; do
+  for sg in 0 1 2; do
+    GSNAPDP_FILL_STAGGER=$sg ABLATE_C3=1 ABLATE_STEPS=20 timeout -k 10 300 python3 tools/ablate.py > $O/s${sg}_$i.json 2>&1 || exit 1
+    GSNAPDP_FILL_STAGGER=$sg ABLATE_READS=125000 ABLATE_C3=1 ABLATE_STEPS=20 timeout -k 10 300 python3 tools/ablate.py > $O/s${sg}125_$i.json 2>&1 || exit 1
+  done
+done
+for f in $O/s*.json; do echo "$f $(tail -n1 $f)"; done
