@@ -968,8 +968,11 @@ __device__ GB_GROUP_ATTR void gband_group(const AS_GLOBAL gsnapdp_ggap_window* W
     }
     if (rc == 1) {
       if (wo.finalp) {  // :4104-4108 (a known site has probability 1.0, :3215, :3255)
-        R.left_prob = kL ? 1.0 : left_site_prob(wo, cL, blocks, nwords, tables);
-        R.right_prob = kR ? 1.0 : right_site_prob(wo, cR, blocks, nwords, tables);
+        // probability mode's tables hold these sites already (the same model at the
+        // same position, columns below L2 - 1)
+        R.left_prob = kL ? 1.0 : (PM && cL < G.L2L - 1) ? pr[FL_LEFT][cL] : left_site_prob(wo, cL, blocks, nwords, tables);
+        R.right_prob =
+            kR ? 1.0 : (PM && cR < G.L2R - 1) ? pr[FL_RIGHT][cR] : right_site_prob(wo, cR, blocks, nwords, tables);
       }
       R.new_leftgenomepos = wo.offset2L + (best.cL - 1);
       R.new_rightgenomepos = wo.revoffset2R - (best.cR - 1);

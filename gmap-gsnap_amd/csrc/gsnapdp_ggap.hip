@@ -511,8 +511,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
       } else {
         R.finalscore = finalscore;
         if (w.finalp) {  // :4104-4108 (get_splicesite_probs: a known site is 1.0, :3215, :3255)
-          R.left_prob = (diL[best.cL] & KNOWN_BIT) ? 1.0 : left_site_prob(w, best.cL, blocks, nwords, tables);
-          R.right_prob = (diR[best.cR] & KNOWN_BIT) ? 1.0 : right_site_prob(w, best.cR, blocks, nwords, tables);
+          // probability mode evaluated these sites already (lp / rp: the same model at the
+          // same position, columns below L2 - 1); the leader re-evaluates only the others
+          R.left_prob = (diL[best.cL] & KNOWN_BIT)              ? 1.0
+                        : (probmode && best.cL < G.L2L - 1) ? (double)lp[best.cL]
+                                                            : left_site_prob(w, best.cL, blocks, nwords, tables);
+          R.right_prob = (diR[best.cR] & KNOWN_BIT)              ? 1.0
+                         : (probmode && best.cR < G.L2R - 1) ? (double)rp[best.cR]
+                                                             : right_site_prob(w, best.cR, blocks, nwords, tables);
         }
         R.new_leftgenomepos = w.offset2L + (best.cL - 1);
         R.new_rightgenomepos = w.revoffset2R - (best.cR - 1);

@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <chrono>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -85,14 +86,14 @@ int main(int argc, char** argv) {
     std::vector<gsnapdp_s3_run> runs(want_runs.size() + 1024);
     int64_t ncap = 0;
     for (const gsnapdp_s3_call& c : calls0) ncap += 2 * (int64_t)c.querylength + 256;
-    std::vector<gsnapdp_s3_pair> news((size_t)ncap);
+    std::unique_ptr<gsnapdp_s3_pair[]> news(new gsnapdp_s3_pair[(size_t)ncap]);  // (not zero-filled)
     for (int r = 0; r < reps; r++) {
       std::vector<gsnapdp_s3_call> calls = calls0;
       gsnapdp_s3_stats st;
       const auto t0 = std::chrono::steady_clock::now();
       if (gsnapdp_stage3_pass_runs(&ctx, calls.data(), (int)calls.size(), in.data(), (int64_t)in.size(), gaps.data(),
                                    gap_off.data(), q.data(), qu.data(), std::min(q.size(), qu.size()), nullptr,
-                                   runs.data(), (int64_t)runs.size(), news.data(), ncap, &st)) {
+                                   runs.data(), (int64_t)runs.size(), news.get(), ncap, &st)) {
         fprintf(stderr, "gsnapdp_stage3_pass_runs: %s\n", g_err.c_str());
         return 5;
       }
@@ -101,7 +102,7 @@ int main(int argc, char** argv) {
       for (const gsnapdp_s3_call& c : calls) nout += c.nout;
       const bool same = (size_t)nout == want_runs.size() && (size_t)st.new_pairs == want_new.size() &&
                         !memcmp(runs.data(), want_runs.data(), want_runs.size() * sizeof(want_runs[0])) &&
-                        !memcmp(news.data(), want_new.data(), want_new.size() * sizeof(want_new[0]));
+                        !memcmp(news.get(), want_new.data(), want_new.size() * sizeof(want_new[0]));
       printf("rep %d: %zu paths in %.4f s = %.0f paths/s, %d rounds, runs %s\n", r, calls.size(), dt,
              calls.size() / dt, st.rounds, same ? "identical to the GPU run's" : "DIFFER");
       if (!same) return 6;
