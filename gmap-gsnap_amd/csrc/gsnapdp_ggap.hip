@@ -460,7 +460,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
     }
     best = group_best<RL>(best, probmode);
 
-    // ---- outcome, probabilities and tracebacks (group leader)
+    // ---- outcome and probabilities (group leader), then the two tracebacks
+    int do_tr = 0;
     if (act && rho == 0) {
       gsnapdp_ggap_result R;
       gsnapdp_ggap_trace X;
@@ -528,27 +529,81 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
         X.bcL = best.cL;
         X.brR = best.rR;
         X.bcR = best.cR;
-        // right flank (reversed), the gapholder, then the left flank (:5000-5040)
-        const int64_t o0 = op_off[wi];
-        const int cap = (int)(op_off[wi + 1] - o0);
-        Tally t = {0, 0, 0, 0, 0};
+        do_tr = 1;  // the counts and op totals follow from the tracebacks below
+      }
+      res[wi] = R;
+      trc[wi] = X;
+    }
+    // The right flank (reversed), the gapholder, then the left flank (:5000-5040).
+    // Lanes 0 and 1 of the group trace the two flanks at once (one traceback
+    // each, same code, lane-selected flank): the right flank's ops at the
+    // window's op offset, the left flank's at L1 + L2R + 2 (past the most a
+    // right traceback emits), then lane 0 moves them down behind the right
+    // flank's.  An op capacity below 2*L1 + L2L + L2R + 4 traces both flanks on
+    // lane 0, one after the other.
+    do_tr = __shfl(do_tr, lane - rho);
+    if (act && do_tr && rho < 2) {
+      const int64_t o0 = op_off[wi];
+      const int cap = (int)(op_off[wi + 1] - o0);
+      const int offL = G.L1 + G.L2R + 2;
+      const bool split = cap >= 2 * G.L1 + G.L2L + G.L2R + 4;  // (wave-uniform per group)
+      const int L1 = G.L1;
+      Tally t = {0, 0, 0, 0, 0};
+      int nR = 0, nL = 0;
+      bool over = false;
+      if (split) {
+        const bool right = rho == 0;
+        OpWriter ow = {ops + o0 + (right ? 0 : offL), right ? offL : cap - offL, 0, 0};
+#ifndef GG_EXP_NOTRACE
+        const P Hs = right ? HR : HL;
+        const PB cls = right ? clsR : clsL;
+        const int qa = right ? L1 : -1, qs = right ? -1 : 1;
+        traceback(CellDirs<P>{Hs, right ? G.WR : G.WL, right ? G.lbR : G.lbL}, right ? LR : LL,
+                  right ? best.rR : best.rL, right ? best.cR : best.cL,
+                  [&](int r) -> uint32_t { return qb[qa + qs * r]; }, [&](int c) -> int { return cls[c]; }, t, ow);
+#endif
+        // lane 1 moves its own ops behind lane 0's (a lane reads back only its own
+        // stores; nR <= offL, so the forward move never overwrites an unread op)
+        const int n0 = __shfl(ow.n, lane - rho), c0 = __shfl(ow.cap, lane - rho);
+        const int n1 = __shfl(ow.n, lane - rho + 1), c1 = __shfl(ow.cap, lane - rho + 1);
+        nR = n0 < c0 ? n0 : c0;
+        nL = n1 < c1 ? n1 : c1;
+        if (!right)
+          for (int i = 0; i < nL; i++) ops[o0 + nR + i] = ops[o0 + offL + i];
+        const Tally t1 = {__shfl(t.nmatches, lane - rho + 1), __shfl(t.nmismatches, lane - rho + 1),
+                          __shfl(t.nopens, lane - rho + 1), __shfl(t.nindels, lane - rho + 1),
+                          __shfl(t.npush, lane - rho + 1)};
+        if (right) {
+          over = n0 > c0 || n1 > c1;
+          t.nmatches += t1.nmatches;
+          t.nmismatches += t1.nmismatches;
+          t.nopens += t1.nopens;
+          t.nindels += t1.nindels;
+          t.npush += t1.npush;
+        }
+      } else if (rho == 0) {
         OpWriter owR = {ops + o0, cap, 0, 0};
 #ifndef GG_EXP_NOTRACE
-        const int L1 = G.L1;
         traceback(CellDirs<P>{HR, G.WR, G.lbR}, LR, best.rR, best.cR,
                   [&](int r) -> uint32_t { return qb[L1 - r]; }, [&](int c) -> int { return clsR[c]; },
                   t, owR);
 #endif
-        const int nR = owR.n < cap ? owR.n : cap;
+        nR = owR.n < cap ? owR.n : cap;
         OpWriter owL = {ops + o0 + nR, cap - nR, 0, 0};
 #ifndef GG_EXP_NOTRACE
         traceback(CellDirs<P>{HL, G.WL, G.lbL}, LL, best.rL, best.cL,
                   [&](int r) -> uint32_t { return qb[r - 1]; }, [&](int c) -> int { return clsL[c]; },
                   t, owL);
 #endif
+        nL = owL.n < owL.cap ? owL.n : owL.cap;
+        over = owR.n > cap || owL.n > owL.cap;
+      }
+      if (rho == 0) {
+        gsnapdp_ggap_result R = res[wi];
+        gsnapdp_ggap_trace X = trc[wi];
         X.nops_right = nR;
-        X.nops_left = owL.n < owL.cap ? owL.n : owL.cap;
-        if (owR.n > cap || owL.n > owL.cap) X.status = ST_OPS_OVERFLOW;
+        X.nops_left = nL;
+        if (over) X.status = ST_OPS_OVERFLOW;
         R.nmatches = t.nmatches;
         R.nmismatches = t.nmismatches;
         R.nopens = t.nopens;
@@ -559,9 +614,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
           X.npairs = 0;
         }
         R.dynprogindex = step_dpi(w.dynprogindex);
+        res[wi] = R;
+        trc[wi] = X;
       }
-      res[wi] = R;
-      trc[wi] = X;
     }
   }
 }
