@@ -634,27 +634,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
 // derived (endalign QUERYEND_INDELS), the genome of column c is the caller's
 // segment byte at sjw[wi].spos (use_genomicseg_p, :1535 / :1690), and the
 // final score is recomputed from the counts (:5541 / :6045).
+//
+// One class's share of the windows for wave gw of nw (wave wv of its block
+// for the LDS regions).
 template <int RL, bool GMEM, bool SEG>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8))) void k_rows(
+__device__ __forceinline__ void rows_class(
     const gsnapdp_window* __restrict__ Wn, const int* __restrict__ list,
     const int* __restrict__ count, const char* __restrict__ q, const char* __restrict__ qu,
     const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
     uint32_t* __restrict__ pool, size_t stride, gsnapdp_result* __restrict__ res,
     uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off,
-    const gsnapdp_sj_window* __restrict__ sjw) {
+    const gsnapdp_sj_window* __restrict__ sjw, int gw, int nw, int wv) {
   extern __shared__ uint32_t smem[];
   using P = typename std::conditional<GMEM, AS_GLOBAL uint32_t*, AS_LDS uint32_t*>::type;
   using PB = typename std::conditional<GMEM, AS_GLOBAL uint8_t*, AS_LDS uint8_t*>::type;
   using PH = typename std::conditional<GMEM, AS_GLOBAL uint16_t*, AS_LDS uint16_t*>::type;
   constexpr int NGW = 64 / RL;
   const int lane = threadIdx.x & 63, grp = lane / RL, rho = lane % RL;
-  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  const int nw = (int)((gridDim.x * blockDim.x) >> 6);
   P region;
   if constexpr (GMEM) {
     region = (P)(pool + (size_t)gw * stride);
   } else {
-    region = (P)(smem + ((threadIdx.x >> 6) * NGW + grp) * stride);
+    region = (P)(smem + (wv * NGW + grp) * stride);
   }
   const int n = *count;
   for (int base = gw * NGW; base < n; base += nw * NGW) {
@@ -750,6 +751,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8
       write_result(&res[wi], w, L, score, br, bc, t, ow);
     }
   }
+}
+
+// All five row-lane classes in one launch of one 16-wave block per CU (the
+// whole 160 KB of LDS): the LDS classes in turn, a block barrier between two
+// of them since their regions overlap, then the global-scratch classes.  A
+// batch with no row-lane windows (most single-gap batches) pays for one
+// launch instead of five.
+template <bool SEG>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8))) void k_rows(
+    const gsnapdp_window* __restrict__ Wn, const int* __restrict__ lists, int list_cap,
+    const int* __restrict__ counts, const char* __restrict__ q, const char* __restrict__ qu,
+    const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
+    uint32_t* __restrict__ largepool, uint32_t* __restrict__ bigpool,
+    gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
+    const int64_t* __restrict__ op_off, const gsnapdp_sj_window* __restrict__ sjw) {
+  const int wv = (int)(threadIdx.x >> 6), nb = (int)gridDim.x;
+  const int gw = (int)blockIdx.x * 16 + wv, nw = nb * 16;
+  rows_class<16, false, SEG>(Wn, lists + (size_t)RW_TINY * list_cap, counts + RW_TINY, q, qu,
+                             blocks, nwords, prof, nullptr, RW_TINY_WORDS, res, ops, op_off, sjw,
+                             gw, nw, wv);
+  __syncthreads();
+  rows_class<32, false, SEG>(Wn, lists + (size_t)RW_SMALL * list_cap, counts + RW_SMALL, q, qu,
+                             blocks, nwords, prof, nullptr, RW_SMALL_WORDS, res, ops, op_off, sjw,
+                             gw, nw, wv);
+  __syncthreads();
+  if (wv < 8)  // 8 regions of RW_MID_WORDS
+    rows_class<64, false, SEG>(Wn, lists + (size_t)RW_MID * list_cap, counts + RW_MID, q, qu,
+                               blocks, nwords, prof, nullptr, RW_MID_WORDS, res, ops, op_off, sjw,
+                               (int)blockIdx.x * 8 + wv, nb * 8, wv);
+  rows_class<64, true, SEG>(Wn, lists + (size_t)RW_LARGE * list_cap, counts + RW_LARGE, q, qu,
+                            blocks, nwords, prof, largepool, RW_LARGE_WORDS, res, ops, op_off, sjw,
+                            gw, nw, wv);
+  if (gw < RW_BIG_WAVES)
+    rows_class<64, true, SEG>(Wn, lists + (size_t)RW_BIG * list_cap, counts + RW_BIG, q, qu,
+                              blocks, nwords, prof, bigpool, RW_BIG_WORDS, res, ops, op_off, sjw,
+                              gw, RW_BIG_WAVES, wv);
 }
 
 // Dynprog_end5/3_splicejunction windows -> the end-gap records k_rows runs
@@ -1242,28 +1279,16 @@ static int rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d
                        gsnapdp_result* d_results, uint32_t* d_ops, const int64_t* d_op_offsets,
                        const gsnapdp_sj_window* sjw) {
   const uint64_t nw = (uint64_t)ctx->nwords;
-  constexpr int tiny_blocks = 160 * 1024 / (16 * RW_TINY_WORDS * 4);
-  hipLaunchKernelGGL((k_rows<16, false, SEG>), dim3(ctx->num_cus * tiny_blocks), dim3(256),
-                     (size_t)16 * RW_TINY_WORDS * 4, st, dw, lists + (size_t)RW_TINY * list_cap,
-                     counts + RW_TINY, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
-                     (uint32_t*)nullptr, (size_t)RW_TINY_WORDS, d_results, d_ops, d_op_offsets, sjw);
-  constexpr int small_blocks = 160 * 1024 / (8 * RW_SMALL_WORDS * 4);
-  hipLaunchKernelGGL((k_rows<32, false, SEG>), dim3(ctx->num_cus * small_blocks), dim3(256),
-                     (size_t)8 * RW_SMALL_WORDS * 4, st, dw, lists, counts + RW_SMALL, d_query,
-                     d_query_uc, ctx->d_blocks, nw, ctx->d_prof, (uint32_t*)nullptr,
-                     (size_t)RW_SMALL_WORDS, d_results, d_ops, d_op_offsets, sjw);
-  hipLaunchKernelGGL((k_rows<64, false, SEG>), dim3(ctx->num_cus * 2), dim3(256),
-                     (size_t)4 * RW_MID_WORDS * 4, st, dw, lists + (size_t)RW_MID * list_cap,
-                     counts + RW_MID, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
-                     (uint32_t*)nullptr, (size_t)RW_MID_WORDS, d_results, d_ops, d_op_offsets, sjw);
-  hipLaunchKernelGGL((k_rows<64, true, SEG>), dim3(ctx->num_cus * RW_LARGE_WAVES_PER_CU / 4),
-                     dim3(256), 0, st, dw, lists + (size_t)RW_LARGE * list_cap, counts + RW_LARGE,
-                     d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_largepool,
-                     (size_t)RW_LARGE_WORDS, d_results, d_ops, d_op_offsets, sjw);
-  hipLaunchKernelGGL((k_rows<64, true, SEG>), dim3(RW_BIG_WAVES), dim3(64), 0, st, dw,
-                     lists + (size_t)RW_BIG * list_cap, counts + RW_BIG, d_query, d_query_uc,
-                     ctx->d_blocks, nw, ctx->d_prof, ctx->d_bigpool, RW_BIG_WORDS, d_results,
-                     d_ops, d_op_offsets, sjw);
+  // k_rows: one 16-wave block per CU, every class in turn (the LDS classes at
+  // their old occupancy: tiny 64 windows, small 32, mid 8 per CU)
+  static_assert(64 * RW_TINY_WORDS * 4 <= 160 * 1024 && 32 * RW_SMALL_WORDS * 4 <= 160 * 1024 &&
+                    8 * RW_MID_WORDS * 4 <= 160 * 1024 && RW_LARGE_WAVES_PER_CU == 16 &&
+                    RW_BIG_WAVES % 16 == 0,
+                "k_rows regions");
+  if (ctx->num_cus * 16 < RW_BIG_WAVES) return -1;  // the big class's waves
+  hipLaunchKernelGGL((k_rows<SEG>), dim3(ctx->num_cus), dim3(1024), (size_t)160 * 1024, st, dw, lists,
+                     list_cap, counts, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
+                     ctx->d_largepool, ctx->d_bigpool, d_results, d_ops, d_op_offsets, sjw);
   HIPCHK(hipGetLastError());
   return 0;
 }
