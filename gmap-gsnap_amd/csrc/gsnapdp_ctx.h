@@ -16,7 +16,7 @@ struct gsnapdp_ctx;
 void gsnapdp__mark(gsnapdp_ctx* ctx, hipStream_t st, int stage, int end);
 // k_rows over the RW_NCLS row-lane class lists (gsnapdp_ggap.hip)
 int gsnapdp__rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d_windows,
-                         const int* lists, const int* counts, int list_cap, const char* d_query,
+                         const int* lists, int* counts, int list_cap, const char* d_query,
                          const char* d_query_uc, gsnapdp_result* d_results, uint32_t* d_ops,
                          const int64_t* d_op_offsets, const gsnapdp_sj_window* sjw);
 // plan + bucketing + k_fill + k_rows over device windows (caller holds ctx->mu);
@@ -95,7 +95,8 @@ struct gsnapdp_ctx {
   gsnapdp_window* d_sj_win = nullptr;  // the end-gap records k_sj_plan derives
   // op-stream compaction (gsnapdp_gather.hip): per-block op counts
   int csum_cap = 0;
-  int64_t* d_csum = nullptr;
+  int64_t* d_csum = nullptr;    // k_compact: per-block status words (epoch-tagged)
+  uint32_t compact_epoch = 0;
   // score_introns batches (gsnapdp_score_introns_host): device staging
   size_t si_cap = 0;
   char* d_si_stage = nullptr;

@@ -278,6 +278,9 @@ constexpr int RW_LARGE_WORDS = 16384;            // global words per wave (64 KB
 constexpr int RW_LARGE_WAVES_PER_CU = 16;        // enough waves to cover the latency of global scratch
 constexpr size_t RW_BIG_WORDS = (size_t)2 << 20; // global words per wave
 constexpr int RW_BIG_WAVES = 128;
+// after the row-lane class counts and k_fill's END flags (RW_NCLS + 1 words):
+// k_plan's and k_rows' last-block tickets (the context's small area, zeroed once)
+constexpr int PLAN_TICKET = RW_NCLS + 2, ROWS_TICKET = RW_NCLS + 3;
 
 // storage of one window: band cells, column classes (bytes), query (u16 per
 // row) and, for more than one 64-row stripe, the boundary row (3 words per column)

@@ -761,7 +761,7 @@ __device__ __forceinline__ void rows_class(
 template <bool SEG>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 8))) void k_rows(
     const gsnapdp_window* __restrict__ Wn, const int* __restrict__ lists, int list_cap,
-    const int* __restrict__ counts, const char* __restrict__ q, const char* __restrict__ qu,
+    int* __restrict__ counts, const char* __restrict__ q, const char* __restrict__ qu,
     const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
     uint32_t* __restrict__ largepool, uint32_t* __restrict__ bigpool,
     gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
@@ -787,6 +787,19 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(GG_WAVES, 
     rows_class<64, true, SEG>(Wn, lists + (size_t)RW_BIG * list_cap, counts + RW_BIG, q, qu,
                               blocks, nwords, prof, bigpool, RW_BIG_WORDS, res, ops, op_off, sjw,
                               gw, RW_BIG_WAVES, wv);
+  // the last block out clears the class counts and END flags for the next batch
+  // (every wave read its counts before its block's ticket; wave 0 takes the
+  // ticket and clears -- no static LDS beside the 160 KB of regions)
+  __syncthreads();
+  if (wv == 0) {
+    int t = 0;
+    if (threadIdx.x == 0)
+      t = __hip_atomic_fetch_add(counts + ROWS_TICKET, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__shfl(t, 0) == (int)gridDim.x - 1) {
+      if (threadIdx.x <= RW_NCLS) counts[threadIdx.x] = 0;
+      if (threadIdx.x == 0) counts[ROWS_TICKET] = 0;
+    }
+  }
 }
 
 // Dynprog_end5/3_splicejunction windows -> the end-gap records k_rows runs
@@ -1275,7 +1288,7 @@ int gsnapdp__rows_pools(gsnapdp_ctx* ctx) {
 // the row-lane classes, one launch each (lists[c * list_cap ...], counts[c])
 template <bool SEG>
 static int rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* dw, const int* lists,
-                       const int* counts, int list_cap, const char* d_query, const char* d_query_uc,
+                       int* counts, int list_cap, const char* d_query, const char* d_query_uc,
                        gsnapdp_result* d_results, uint32_t* d_ops, const int64_t* d_op_offsets,
                        const gsnapdp_sj_window* sjw) {
   const uint64_t nw = (uint64_t)ctx->nwords;
@@ -1294,7 +1307,7 @@ static int rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d
 }
 
 int gsnapdp__rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d_windows,
-                         const int* lists, const int* counts, int list_cap, const char* d_query,
+                         const int* lists, int* counts, int list_cap, const char* d_query,
                          const char* d_query_uc, gsnapdp_result* d_results, uint32_t* d_ops,
                          const int64_t* d_op_offsets, const gsnapdp_sj_window* sjw) {
   if (sjw)

@@ -10,7 +10,7 @@
 //     per column every slot does gap1 (from slot+1), gap2 (chained from slot-1)
 //     and nogap (same slot) with the sequential tie rule;
 //   * waves are made uniform in (band, tie rule, endpoint mode) by an on-device
-//     counting sort (k_plan / k_scan / k_scatter), so band edges are scalar;
+//     counting sort (k_plan, whose last block scans, / k_scatter), so band edges are scalar;
 //   * 4-bit direction nibbles stream to HBM scratch; each lane then walks its
 //     own traceback and emits a compact op stream (include/gsnapdp.h).
 //   End gaps in find_best_endpoint mode run here too (the END fills); the
@@ -55,6 +55,102 @@ __device__ inline int end_kind(const Derived& d) {
   return d.mode == 2 ? 2 : 0;
 }
 
+// Exclusive scan of bucket sizes, each padded to whole waves of its class
+// (64 / CLASS_LPW windows).  cursor[k] = first perm entry of bucket k;
+// class_start[c] = first perm entry of class c (a multiple of its wave size,
+// since wave sizes shrink as W grows and are powers of two).
+// The wave size (64 / CLASS_LPW) of key k's class, branch-free: W from the
+// key's triangle index t = k / (2 NEND) (W (W - 1) / 2 <= t < W (W + 1) / 2).
+__device__ inline int key_wave(int k) {
+  const int t = k / (2 * NEND);
+  int W = (int)((1.0f + __builtin_sqrtf((float)(8 * t + 1))) * 0.5f);
+  W += key_tri(W + 1) <= t ? 1 : 0;
+  W -= key_tri(W) > t ? 1 : 0;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < NCLASS - 1; j++) c += W > CLASS_W[j] ? 1 : 0;
+  int lpw = CLASS_LPW[0];
+#pragma unroll
+  for (int j = 1; j < NCLASS; j++) lpw = c == j ? CLASS_LPW[j] : lpw;
+  return 64 >> __builtin_ctz(lpw);
+}
+
+// Run by the last k_plan block to finish (1024 threads; stage: its NKEYS-word
+// LDS histogram, free by then).  Also writes -1 into every bucket's padding
+// entries of perm, so perm needs no clearing, and zeroes the global histogram
+// for the next batch (the context clears it once at allocation).  Keys are
+// read and written coalesced (key tid + 1024 i); the scan runs over each
+// thread's contiguous PER keys in LDS.
+constexpr int SCAN_PAD_SHIFT = 26;  // stage word: count | padding << 26
+__device__ void scan_buckets(int* __restrict__ hist, int* __restrict__ cursor,
+                             int* __restrict__ class_start, int* __restrict__ perm, int* stage) {
+  __shared__ int wtot[16];  // the 16 waves' totals
+  constexpr int PER = (NKEYS + 1023) / 1024;
+  const int tid = threadIdx.x;
+  {
+    // the other blocks' histogram atomics, read (and cleared) by atomics where
+    // they were performed, all of this thread's in flight at once
+    int v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; i++) v[i] = tid + i * 1024 < NKEYS ? atomicExch(hist + tid + i * 1024, 0) : 0;
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+      const int k = tid + i * 1024;
+      if (k < NKEYS) {
+        const int ng = key_wave(k);
+        stage[k] = v[i] | ((((v[i] + ng - 1) & -ng) - v[i]) << SCAN_PAD_SHIFT);
+      }
+    }
+  }
+  __syncthreads();
+  // exclusive scan of the padded sizes: this thread's PER keys, then the
+  // wave by shuffles, then the waves' totals
+  const int lo = tid * PER;
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    if (lo + i < NKEYS) {
+      const int x = stage[lo + i];
+      s += (x & ((1 << SCAN_PAD_SHIFT) - 1)) + (int)((unsigned)x >> SCAN_PAD_SHIFT);
+    }
+  }
+  const int ln = tid & 63, wv = tid >> 6;
+  int x = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (ln >= o) x += y;
+  }
+  if (ln == 63) wtot[wv] = x;
+  __syncthreads();
+  int run = x - s, total = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    run += k < wv ? wtot[k] : 0;
+    total += wtot[k];
+  }
+  // this thread's own entries become cursors; its buckets' padding entries
+  // of perm (at most 63 each, after the bucket's count) get -1
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    if (lo + i < NKEYS) {
+      const int w = stage[lo + i];
+      const int h = w & ((1 << SCAN_PAD_SHIFT) - 1), pad = (int)((unsigned)w >> SCAN_PAD_SHIFT);
+      stage[lo + i] = run;
+      for (int e = run + h; e < run + h + pad; e++) perm[e] = -1;
+      run += h + pad;
+    }
+  }
+  __syncthreads();
+  for (int k = tid; k < NKEYS; k += 1024) cursor[k] = stage[k];  // coalesced
+  if (tid < NCLASS) {
+    // class c covers W in (CLASS_W[c-1], CLASS_W[c]] and keys are W-major
+    const int k = first_key_of_w(class_low(tid));
+    class_start[tid] = k < NKEYS ? stage[k] : total;
+  }
+  if (tid == 0) class_start[NCLASS] = total;
+}
+
 // ------------------------------------------------------------------ k_plan
 // Early returns, QUERYEND_NOGAPS windows (no fill at all) and bucketing.
 __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* __restrict__ q,
@@ -63,10 +159,13 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
                        gsnapdp_result* __restrict__ res, uint32_t* __restrict__ ops,
                        const int64_t* __restrict__ op_off, int* __restrict__ keys,
                        int* __restrict__ hist, int* __restrict__ big_list,
-                       int* __restrict__ big_count, int list_cap, int ends_on_band) {
+                       int* __restrict__ big_count, int list_cap, int ends_on_band,
+                       int* __restrict__ cursor, int* __restrict__ class_start,
+                       int* __restrict__ perm, int* __restrict__ ticket) {
   __shared__ int lh[NKEYS];  // block-local histogram: one global atomic per key per block
   __shared__ int lbig[RW_NCLS], lbase[RW_NCLS];  // block-local row-lane list appends
   __shared__ int lend;                             // block-local END task kinds (bits 1, 2)
+  __shared__ int last;                             // this block finished last
   for (int k = threadIdx.x; k < NKEYS; k += blockDim.x) lh[k] = 0;
   if (threadIdx.x < RW_NCLS) lbig[threadIdx.x] = 0;
   if (threadIdx.x == 0) lend = 0;
@@ -134,76 +233,20 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
     if (lh[k] > 0) atomicAdd(&hist[k], lh[k]);
   __syncthreads();
   if (big >= 0) big_list[(size_t)big * list_cap + lbase[big] + lslot] = i;
-}
-
-// Exclusive scan of bucket sizes, each padded to whole waves of its class
-// (64 / CLASS_LPW windows).  cursor[k] = first perm entry of bucket k;
-// class_start[c] = first perm entry of class c (a multiple of its wave size,
-// since wave sizes shrink as W grows and are powers of two).
-__device__ inline int padded_bucket(int W, int h) {
-  const int ng = 64 / CLASS_LPW[class_of_w(W)];
-  return (h + ng - 1) / ng * ng;
-}
-
-// Also writes -1 into every bucket's padding entries of perm, so perm needs
-// no clearing.
-// (also zeroes the histogram for the next batch: the context clears it once at
-// allocation, so no per-batch memset is needed)
-__global__ void k_scan(int* __restrict__ hist, int* __restrict__ cursor,
-                       int* __restrict__ class_start, int* __restrict__ perm) {
-  __shared__ int wtot[16];  // the 16 waves' totals
-  constexpr int PER = (NKEYS + 1023) / 1024;
-  const int tid = threadIdx.x;
-  const int lo = tid * PER;
-  // this thread's keys: counts and padded sizes (W steps along the keys)
-  int h[PER], p[PER];
-  int s = 0, W = w_of_key(lo);
-#pragma unroll
-  for (int i = 0; i < PER; i++) {
-    const int k = lo + i;
-    while (W < FAST_WMAX && first_key_of_w(W + 1) <= k) W++;
-    h[i] = k < NKEYS ? hist[k] : 0;
-    p[i] = padded_bucket(W, h[i]);
-    s += p[i];
-  }
-  // exclusive scan over the block: within each wave by shuffles, then the waves' totals
-  const int ln = tid & 63, wv = tid >> 6;
-  int x = s;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o);
-    if (ln >= o) x += y;
-  }
-  if (ln == 63) wtot[wv] = x;
+  // The last block to finish scans the histogram (no separate k_scan launch).
+  // Every thread waits for its histogram atomics to be performed before the
+  // block takes its ticket; the scan reads them back by atomics.  (No
+  // agent-scope fence: each one writes back the XCD's L2, 0.28 ms per batch.)
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  int wbase = 0, total = 0;
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    wbase += k < wv ? wtot[k] : 0;
-    total += wtot[k];
-  }
-  int run = wbase + x - s;
-#pragma unroll
-  for (int i = 0; i < PER; i++) {
-    const int k = lo + i;
-    if (k >= NKEYS) break;
-    cursor[k] = run;
-    // class c covers W in (CLASS_W[c-1], CLASS_W[c]] and keys are W-major: the
-    // thread holding a class's first key writes its start (no serial re-read
-    // of the cursors after a barrier)
-#pragma unroll
-    for (int c = 0; c < NCLASS; c++)
-      if (k == first_key_of_w(class_low(c))) class_start[c] = run;
-    for (int e = run + h[i]; e < run + p[i]; e++) perm[e] = -1;
-    run += p[i];
-    hist[k] = 0;
-  }
-  if (tid == 0) {
-#pragma unroll
-    for (int c = 0; c < NCLASS; c++)
-      if (first_key_of_w(class_low(c)) >= NKEYS) class_start[c] = total;
-    class_start[NCLASS] = total;
-  }
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (int)gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  scan_buckets(hist, cursor, class_start, perm, lh);
+  if (threadIdx.x == 0) *ticket = 0;  // for the next batch
 }
 
 // Block-local ranks (LDS atomics), one global reservation per key per block.
@@ -1234,23 +1277,31 @@ static int ensure_capacity(gsnapdp_ctx* ctx, int n) {
 int gsnapdp__fill_pipeline(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d_windows, int n,
                            const char* d_query, const char* d_query_uc, gsnapdp_result* d_results,
                            uint32_t* d_ops, const int64_t* d_op_offsets, const gsnapdp_sj_window* sjw) {
+  if (n >= (1 << SCAN_PAD_SHIFT)) {  // a bucket count must fit scan_buckets' stage word
+    g_err = "batch of " + std::to_string(n) + " windows: at most 2^26 - 1 per call";
+    return -1;
+  }
   if (ensure_capacity(ctx, n)) return -1;
   int* hist = ctx->d_small;
   int* cursor = hist + NKEYS;
   int* class_start = cursor + NKEYS;
   int* big_count = class_start + NCLASS + 1;  // RW_NCLS row-lane class counts
-  HIPCHK(hipMemsetAsync(big_count, 0, 4 * (RW_NCLS + 1), st));  // + k_fill's END flags
+  // (the class counts and END flags start at zero: the context clears them once
+  // and k_rows' last block after every batch)
+  static_assert(ROWS_TICKET < 64, "tickets inside the context's small area");
   if (gsnapdp__rows_pools(ctx)) return -1;
-  const int tb = 1024, nb = (n + tb - 1) / tb;
+  constexpr int tb = 1024;
+  const int nb = (n + tb - 1) / tb;
   auto mark = [&](int stage, int end) { gsnapdp__mark(ctx, st, stage, end); };
   mark(0, 0);
+  static_assert(tb == 1024, "k_plan's last block runs scan_buckets with 1024 threads");
   hipLaunchKernelGGL(k_plan, dim3(nb), dim3(tb), 0, st, d_windows, n, d_query, d_query_uc,
                      ctx->d_blocks, (uint64_t)ctx->nwords, ctx->d_prof, d_results, d_ops,
                      d_op_offsets, ctx->d_keys, hist, ctx->d_big_list, big_count,
-                     ctx->cap_n, ctx->ends_rowlane ? 0 : 1);
+                     ctx->cap_n, ctx->ends_rowlane ? 0 : 1, cursor, class_start, ctx->d_perm,
+                     big_count + PLAN_TICKET);
   mark(0, 1);
   mark(1, 0);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, hist, cursor, class_start, ctx->d_perm);
   hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(tb), 0, st, ctx->d_keys, n, cursor, ctx->d_perm);
   mark(1, 1);
   const int blocks = (int)(ctx->dirpool_waves / 4);
