@@ -43,7 +43,7 @@ def test_gpu_compact_ops_matches_host_mirror():
     dev = torch.device("cuda", 0)
     ctx = Context(np.zeros(64, np.uint32), device=0)
     rng = np.random.default_rng(3)
-    for n in (1, 1023, 1024, 1025, 70_000):
+    for n in (1, 1023, 1024, 1025, 70_000, 2_500_000):  # (the last: more blocks than are resident at once)
         res = np.zeros(n, dtype=RESULT)
         cap = rng.integers(1, 40, size=n)
         off = np.zeros(n + 1, dtype=np.int64)

@@ -160,3 +160,33 @@ def test_gpu_end_gaps_on_register_band(seed, monkeypatch):
     for f in ("bestr", "bestc", "status"):
         assert np.array_equal(res[f], res2[f]), f
     assert np.sum(res["bestc"] == 0) > 0 and np.sum(res["bestr"] > 0) > 5000
+
+
+def test_gpu_consecutive_batches_on_one_context():
+    """One context, batches in turn whose row-lane lists are full, empty and
+    full again (end gaps of every row class, then single gaps only, then wide and
+    long windows): k_plan's last block resets its ticket and the histogram,
+    k_rows' last block clears the class counts and END flags, so no batch sees
+    another's lists.  Every batch bit-exact against the restatement."""
+    g = W.synthetic_genome(2_000_000, seed=77, n_rate=0.002)
+    blocks = W.pack_genome(g)
+    ends = W.concat_batches([W.random_windows(g, 800, seed=700 + k, kinds=(END5_GAP, END3_GAP), max_len1=m1,
+                                              max_len2=m1 + 20, max_band=b)
+                             for k, (m1, b) in enumerate(((30, 6), (250, 5), (600, 12)))])
+    singles = W.random_windows(g, 3000, seed=71, max_len1=120, max_len2=140, max_band=20)
+    wide = W.random_windows(g, 300, seed=72, max_len1=700, max_len2=900, max_band=60)
+    O.setup(blocks)
+    refs = []
+    for b in (ends, singles, wide):
+        ores, opairs, ooff, onp = O.run_batch(b.windows, b.query, b.query_uc, nthreads=16)
+        oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
+        ref = {f: ores[f] for f in ("finalscore", "nmatches", "nmismatches", "nopens", "nindels")}
+        ref["dynprogindex"] = ores["reserved"]
+        refs.append((ref, oflat, onp))
+    ctx = Context(blocks)
+    for k in (0, 1, 0, 2, 1, 2, 0):
+        b = (ends, singles, wide)[k]
+        res, ops, off = ctx.run(b.windows, b.query, b.query_uc)
+        pairs, npairs = ctx.all_pairs(b.windows, b.query, b.query_uc, res, ops, off)
+        compare(res, pairs, npairs, *refs[k], "batch kind %d on a shared context" % k)
+    ctx.close()
