@@ -868,6 +868,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
     const gsnapdp_sj_window* __restrict__ sjw, int min_tasks, int stagger) {
   __shared__ alignas(8) uint32_t sprof[SPROF_WORDS];
   __shared__ uint32_t rings[4][RING_WORDS_MAX];  // one per wave of the block
+#ifdef TB_PROF
+  const uint64_t kt0 = __builtin_amdgcn_s_memtime();
+#endif
   for (int i = threadIdx.x; i < MLUT; i += blockDim.x)
     sprof[i] = i < UTAB ? fill_profile_word(prof[i], i >= MT_ENDQ * 128 ? END_SC_BIAS : FILL_SC_BIAS)
                         : (i - UTAB < 128 ? prof[i] : 0u);
@@ -929,6 +932,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
   FILL_CLASS(4) FILL_CLASS(5) FILL_CLASS(6) FILL_CLASS(7)
 #undef FILL_BODY
 #undef FILL_CLASS
+#ifdef TB_PROF
+  TB_COUNT(6, __builtin_amdgcn_s_memtime() - kt0);  // the wave's whole time
+  TB_COUNT(7, 1);
+#endif
 }
 
 // --------------------------------------------------------------- k_count
@@ -1328,8 +1335,8 @@ int gsnapdp__fill_pipeline(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_windo
     unsigned long long h[8];
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipMemcpyFromSymbol(h, HIP_SYMBOL(tb_prof), sizeof(h)));
-    fprintf(stderr, "tb_prof sweeps %llu groups %llu slow %llu lanecols %llu fill_cyc %llu trace_cyc %llu\n", h[0], h[1],
-            h[2], h[3], h[4], h[5]);
+    fprintf(stderr, "tb_prof sweeps %llu groups %llu slow %llu lanecols %llu fill_cyc %llu trace_cyc %llu wave_cyc %llu waves %llu\n",
+            h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
     memset(h, 0, sizeof(h));
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(tb_prof), h, sizeof(h)));
   }
