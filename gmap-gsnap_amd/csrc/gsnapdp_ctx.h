@@ -72,6 +72,8 @@ struct gsnapdp_ctx {
   int fill_waves = 0;  // waves launched per k_fill class kernel
   int fill_stagger = 0;  // k_fill: first traceback batch k * this short in the k-th block of a CU (GSNAPDP_FILL_STAGGER)
   int fill_min_tasks = 0;  // k_fill: fewer waves per SIMD below this many tasks per wave (GSNAPDP_FILL_MIN_TASKS)
+  int fill_split = -1;   // k_fill: waves split among the band classes: -1 small batches, 0 never, 1 always (GSNAPDP_FILL_SPLIT)
+  int fill_split_w = 5;  // k_fill: a class's per-task weight S + this (GSNAPDP_FILL_SPLIT_W)
   int num_cus = 0;
   // per-stage event timing (gsnapdp_profile)
   int prof_on = 0;

@@ -865,7 +865,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
     const uint32_t* __restrict__ blocks, uint64_t nwords, const uint32_t* __restrict__ prof,
     uint32_t* __restrict__ dirpool, size_t wave_stride, gsnapdp_result* __restrict__ res,
     uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off, const int* __restrict__ end_flag,
-    const gsnapdp_sj_window* __restrict__ sjw, int min_tasks, int stagger) {
+    const gsnapdp_sj_window* __restrict__ sjw, int min_tasks, int stagger, int split_mode, int split_w) {
   __shared__ alignas(8) uint32_t sprof[SPROF_WORDS];
   __shared__ uint32_t rings[4][RING_WORDS_MAX];  // one per wave of the block
 #ifdef TB_PROF
@@ -912,17 +912,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSNAPDP_FIL
   // t = first_c + (tau - tfirst[c]), visited class by class, so every wave gets
   // the same mix of classes.  Small batches: the waves are split among the
   // classes in proportion to their task counts weighted by a task's rough cost
-  // (2 S + 3: S cell updates and the per-column work of a step) and a wave
+  // (S + split_w: S cell updates and the per-column work of a step) and a wave
   // strides over its own class only, so it runs one traceback sweep instead of
   // one per class (at 125k reads two sweeps for three tasks; the split measured
-  // 2.4 % faster there and 9 % slower at 1M, where the weights' error decides
-  // the balance).  A class too small for a wave of its own is spread one task
-  // per wave.
-  const bool split = tfirst[NCLASS] <= TB_BATCH * nw;
+  // 3 % faster there, and 6-9 % slower at 1M with either weight, so large
+  // batches keep the mix; GSNAPDP_FILL_SPLIT / _W override for experiments).
+  // A class too small for a wave of its own is spread one task per wave.
+  const bool split = split_mode < 0 ? tfirst[NCLASS] <= TB_BATCH * nw : split_mode != 0;
   int64_t wcum[NCLASS + 1];
   wcum[0] = 0;
 #pragma unroll
-  for (int c = 0; c < NCLASS; c++) wcum[c + 1] = wcum[c] + (int64_t)(tfirst[c + 1] - tfirst[c]) * (2 * CLASS_S[c] + 3);
+  for (int c = 0; c < NCLASS; c++) wcum[c + 1] = wcum[c] + (int64_t)(tfirst[c + 1] - tfirst[c]) * (CLASS_S[c] + split_w);
   static_assert(NCLASS <= 8, "k_fill dispatches at most 8 classes");
 #define FILL_BODY(C, E)                                                                          \
   fill_tasks<CLASS_S[C % NCLASS], CLASS_LPW[C % NCLASS], class_low(C % NCLASS), E>(               \
@@ -1224,6 +1224,11 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
     // the first traceback batch of the k-th block of a CU is k * this many tasks short
     const char* sg = getenv("GSNAPDP_FILL_STAGGER");
     if (sg) ctx->fill_stagger = atoi(sg);
+    // k_fill's class split: -1 small batches only, 0 never, 1 always; the per-task weight S + w
+    const char* sm = getenv("GSNAPDP_FILL_SPLIT");
+    if (sm) ctx->fill_split = atoi(sm);
+    const char* sw = getenv("GSNAPDP_FILL_SPLIT_W");
+    if (sw) ctx->fill_split_w = atoi(sw);
     const char* f = getenv("GSNAPDP_ENDS_ROWLANE");
     ctx->ends_rowlane = (f && f[0] == '1') ? 1 : 0;
   }
@@ -1353,7 +1358,7 @@ int gsnapdp__fill_pipeline(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_windo
   hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, st, d_windows, ctx->d_perm, class_start,
                      d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof, ctx->d_dirpool,
                      WAVE_STRIDE_DW, d_results, d_ops, d_op_offsets, big_count + RW_NCLS, sjw,
-                     ctx->fill_min_tasks, ctx->fill_stagger);
+                     ctx->fill_min_tasks, ctx->fill_stagger, ctx->fill_split, ctx->fill_split_w);
   mark(2, 1);
   if constexpr (!FILL_MATCH) {
     mark(7, 0);
