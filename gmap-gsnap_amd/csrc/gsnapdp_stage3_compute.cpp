@@ -40,7 +40,9 @@ using List = std::vector<gsnapdp_s3_pair>;  // list order: [0] is the head
 
 // stage3.c:42-44, smooth.c:20-36, stage3.c:74-75, changepoint.c:11-12
 constexpr int MAXITER_SMOOTH_BY_SIZE = 2, MAXITER_INTRONS = 2;
-constexpr double DELETE_THRESHOLD = 0.1, MARK_THRESHOLD = 1e-7, SHORTEXONPROB_END = 0.05;
+constexpr double DELETE_THRESHOLD = 0.1, MARK_THRESHOLD = 1e-7;
+// smooth.c:30-35: GSNAP "allows more intron predictions in ends of short reads"
+constexpr double SHORTEXONPROB_END_GMAP = 0.05, SHORTEXONPROB_END_GSNAP = 0.10;
 constexpr int SHORTEXONLEN_END = 10, STAGE2_INDEXSIZE = 6;
 constexpr double THETA_SLACK = 0.10, TRIM_END_PVALUE = 1e-4, NPSEUDO = 12.0, CP_SLACK = 0.10;
 enum { KEEP = 0, DELETE = 1, MARK = 2 };
@@ -307,7 +309,8 @@ List delete_and_mark(const List& pairs, const std::vector<int>& status, bool mar
   reverse(fwd);  // list order
   return fwd;
 }
-List smooth_by_size(bool* shortp, bool* deletep, List pairs) {
+List smooth_by_size(bool* shortp, bool* deletep, List pairs, bool gsnap) {
+  const double SHORTEXONPROB_END = gsnap ? SHORTEXONPROB_END_GSNAP : SHORTEXONPROB_END_GMAP;
   *shortp = *deletep = false;
   for (gsnapdp_s3_pair& p : pairs) p.flags &= (uint8_t)~GSNAPDP_S3_SHORTEXON;  // smooth_reset
   std::vector<int> em, il, status;
@@ -1277,7 +1280,7 @@ void advance(Query& q, const Env& E) {
     if (!(q.shortp && q.iter1 < MAXITER_SMOOTH_BY_SIZE)) break;
     {  // 3a: smoothing by size
       List path = insert_gapholders(pairs, false);  // List_reverse(insert_gapholders(..))
-      pairs = smooth_by_size(&q.shortp, &q.deletep, std::move(path));
+      pairs = smooth_by_size(&q.shortp, &q.deletep, std::move(path), E.o.gsnap != 0);
     }
     if (q.shortp || q.deletep) {  // 3b: dual introns
       q.list = insert_gapholders(pairs);

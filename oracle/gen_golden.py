@@ -957,6 +957,80 @@ def trace_gmap_run(prefix: str, genome_fa: str, query_fa: str, d: str, stage3_ev
     return out
 
 
+def pc_replay(z) -> tuple:
+    """The reference's own path_compute (oracle/pc_replay.c) over the path_compute
+    invocations of a gmap_trace recording z (a gmap_*_stage3 set), from each one's
+    pass-2A path, in gmap's build and in gsnap's (-DGSNAP).  gmap's build must
+    reproduce every recorded return value, list, probability and pass count bit
+    for bit (that validates the harness).  Returns (the pipeline queries, paths,
+    query bytes as workload.stage3_path_pipeline gives them, gmap's recorded
+    (lists, probabilities, PC_CALL records), gsnap's (PC_CALL records, lists,
+    probabilities), the number of invocations whose GSNAP outputs differ)."""
+    import tempfile
+    subprocess.check_call(["make", "-s", "-C", HERE, "pc_replay"])
+    queries, pin, q, qu, want, want_probs, final = W.stage3_path_pipeline(z)
+    outs = {}
+    with tempfile.TemporaryDirectory() as d:
+        queries.tofile(os.path.join(d, "calls.bin"))
+        final.tofile(os.path.join(d, "pc.bin"))
+        pin.tofile(os.path.join(d, "pairs_in.bin"))
+        q.tofile(os.path.join(d, "query.bin"))
+        qu.tofile(os.path.join(d, "query_uc.bin"))
+        z["blocks"].astype("<u4").tofile(os.path.join(d, "genome.u32"))
+        z["s2_calls"].tofile(os.path.join(d, "stage2_calls.bin"))
+        z["s2_pairs"].tofile(os.path.join(d, "stage2_pairs.bin"))
+        for flavour in ("gmap", "gsnap"):
+            subprocess.check_call([os.path.join(HERE, "_ref", "pc_replay_" + flavour), d])
+            pc = np.fromfile(os.path.join(d, "out_pc.bin"), dtype=final.dtype)
+            pp = np.fromfile(os.path.join(d, "out_pairs.bin"), dtype=want.dtype)
+            pr = np.fromfile(os.path.join(d, "out_probs.bin"), dtype=np.float64).reshape(-1, 2)
+            outs[flavour] = (pc, pp, pr)
+    pc, pp, pr = outs["gmap"]
+    assert (pc["pad"] == 0).all(), "gmap build: stage-2 request missing from the recording"
+    for f in ("intronlen", "nonintronlen", "passes", "nout"):
+        assert np.array_equal(pc[f], final[f]), "gmap build: %s differs from the recording" % f
+    assert pc["defect_rate"].tobytes() == final["defect_rate"].tobytes()
+    assert pp.tobytes() == want.tobytes() and pr.tobytes() == want_probs.tobytes(), "gmap build: lists differ"
+    pc, pp, pr = outs["gsnap"]
+    differ = 0
+    for i in range(len(pc)):
+        a, n = int(pc["first_out"][i]), int(pc["nout"][i])
+        b, m = int(final["first_out"][i]), int(final["nout"][i])
+        if (n != m or pp[a:a + n].tobytes() != want[b:b + m].tobytes() or pr[a:a + n].tobytes() !=
+                want_probs[b:b + m].tobytes() or pc["defect_rate"][i] != final["defect_rate"][i] or
+                not np.array_equal(pc["passes"][i], final["passes"][i])):
+            differ += 1
+    return (queries, pin, q, qu), (want, want_probs, final), (pc, pp, pr), differ
+
+
+def gsnap_pc_case(prefix: str) -> None:
+    """path_compute as GSNAP builds it (stage3.c with -DGSNAP: SCORE_SIGDIFF :87-91,
+    smooth.c's SHORTEXONPROB_END :30-35, passes 9a / 9b with QUERYEND_NOGAPS
+    :9054-9058 / :9106-9110, the end-exon trims that keep a supported exon
+    :2968-2983 / :3198-3213) over the path_compute invocations of PREFIX_stage3
+    (gmap's recording), from each one's pass-2A path (pc_replay above).  Writes
+    PREFIX_stage3_gsnap: PREFIX_stage3's arrays with pc_calls / pc_pairs / pc_probs
+    replaced by GSNAP's (only the invocations whose stage-2 requests the recording
+    serves; pc_calls.pad = 0 for all of them)."""
+    z = np.load(os.path.join(OUT, prefix + "_stage3.npz"), allow_pickle=False)
+    _, (_, _, final), (pc, pp, pr), differ = pc_replay(z)
+    keep = pc["pad"] == 0
+    sel = np.nonzero(keep)[0]
+    lists = [pp[int(pc["first_out"][i]):int(pc["first_out"][i]) + int(pc["nout"][i])] for i in sel]
+    probs = [pr[int(pc["first_out"][i]):int(pc["first_out"][i]) + int(pc["nout"][i])] for i in sel]
+    gpc = pc[sel].copy()
+    gpc["first_out"] = np.concatenate([[0], np.cumsum(gpc["nout"])[:-1]]).astype(np.int32)
+    arrays = {k: z[k] for k in z.files}
+    arrays["pc_calls"] = gpc
+    arrays["pc_pairs"] = np.concatenate(lists) if lists else pp[:0]
+    arrays["pc_probs"] = np.concatenate(probs) if probs else pr[:0]
+    arrays["gsnap"] = np.int32(1)
+    np.savez_compressed(os.path.join(OUT, prefix + "_stage3_gsnap.npz"), **arrays)
+    print("%s_stage3_gsnap: gmap build reproduces all %d recorded path_compute calls; gsnap build: %d of them "
+          "kept (%d with a stage-2 request the recording lacks), %d differ from gmap's, %d pairs" % (
+              prefix, len(final), len(sel), int((~keep).sum()), differ, arrays["pc_pairs"].size))
+
+
 def main() -> None:
     only = set(sys.argv[1:])  # optional: names of the fixtures to (re)generate
     os.makedirs(OUT, exist_ok=True)
@@ -997,6 +1071,8 @@ def main() -> None:
         ("gmap_cins", lambda: gmap_cins_case()),
         ("gmap_dual", lambda: gmap_dual_case()),
         ("c4_pinned", lambda: c4_pinned_case()),
+        ("gmap_her2_gsnap", lambda: gsnap_pc_case("gmap_her2")),
+        ("gmap_synth_gsnap", lambda: gsnap_pc_case("gmap_synth")),
     ]
     for name, fn in cases:
         if not only or name in only:

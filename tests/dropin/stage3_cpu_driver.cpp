@@ -13,7 +13,7 @@
 //                     --introns DIR/pass_scores.bin (score_introns on the returned lists);
 //   stage3_cpu DIR --compute MINLEN   passes 2A-6 (gsnapdp_stage3_compute) over the queries in
 //                     calls.bin: DIR/{pass_calls,pass_pairs,compute_stats}.bin
-//   stage3_cpu DIR --path-compute MINLEN MAXINTRONLEN   path_compute from pass 2A to its return
+//   stage3_cpu DIR --path-compute MINLEN MAXINTRONLEN [GSNAP]   path_compute from pass 2A to its return
 //                     value (gsnapdp_stage3_path_compute): the same files and DIR/pass_probs.bin
 #include <stdio.h>
 #include <stdlib.h>
@@ -97,6 +97,7 @@ int main(int argc, char** argv) {
     gsnapdp_s3_path_opts o = {};
     o.min_intronlength = atoi(argv[3]);
     o.maxintronlen_bound = atoi(argv[4]);
+    o.gsnap = argc > 5 ? atoi(argv[5]) : 0;  // 1: stage3.c as GSNAP builds it
     std::vector<gsnapdp_s3_pair> big((size_t)cap * 2 + 1024);
     std::vector<double> probs(big.size() * 2);
     if (gsnapdp_stage3_path_compute(ctx, calls.data(), (int)calls.size(), in.data(), (int64_t)in.size(), q.data(),

@@ -15,7 +15,7 @@ import pytest
 
 from gsnapdp import Context, SplicingIIT
 from gsnapdp import workload as W
-from test_stage3_cpu import (IIT_NAMES, NAMES, PIPE_NAMES, check_compute, check_pass, check_path_compute,
+from test_stage3_cpu import (GSNAP_PIPE_NAMES, IIT_NAMES, NAMES, PIPE_NAMES, check_compute, check_pass, check_path_compute,
                              check_scores, iit_intervals, stage3_golden)
 
 pytestmark = pytest.mark.gpu
@@ -103,20 +103,23 @@ def test_gpu_stage3_compute_matches_reference(golden_dir, tmp_path, name):
     ctx.close()
 
 
-@pytest.mark.parametrize("name", PIPE_NAMES)
+@pytest.mark.parametrize("name", PIPE_NAMES + GSNAP_PIPE_NAMES)
 def test_gpu_stage3_path_compute_matches_reference(golden_dir, tmp_path, name):
     """path_compute from pass 2A to its return value for every recorded
     invocation at once (gsnapdp_stage3_path_compute: passes 2A-10, the DP
     passes and assign_gap_types' MaxEnt sites on the GPU): the lists, the
     pairs' donor / acceptor probabilities, *intronlen / *nonintronlen /
     *defect_rate and the pass calls gmap made, bit for bit; then the synthetic
-    set x8 in one call, each copy checked, timed"""
+    set x8 in one call, each copy checked, timed.  The *_gsnap sets run with
+    gsnap = 1 against path_compute as GSNAP builds it (oracle/pc_replay.c)"""
     z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    gsnap = bool(int(z["gsnap"])) if "gsnap" in z else False
     queries, pin, q, qu, want, wprobs, final = W.stage3_path_pipeline(z)
     ctx = Context(z["blocks"])
     s2 = stage2_double(ctx, z, tmp_path)
     maxintron = int(final["maxintronlen_bound"][0])
-    got_calls, got, probs, st = ctx.stage3_path_compute(queries, pin, q, qu, maxintronlen_bound=maxintron)
+    got_calls, got, probs, st = ctx.stage3_path_compute(queries, pin, q, qu, maxintronlen_bound=maxintron,
+                                                        gsnap=gsnap)
     check_path_compute(got_calls, got, probs, want, wprobs, final, name)
     assert list(st["pass_calls"]) == list(final["passes"].sum(axis=0))
     assert st["sites"] > 0

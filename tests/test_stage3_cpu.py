@@ -184,6 +184,8 @@ def test_stage3_pass_cpu_with_splicing_iit(golden_dir, tmp_path, name):
 
 
 PIPE_NAMES = ["gmap_her2_stage3", "gmap_synth_stage3"]
+# the same invocations through path_compute as GSNAP builds it (-DGSNAP; oracle/pc_replay.c)
+GSNAP_PIPE_NAMES = ["gmap_her2_stage3_gsnap", "gmap_synth_stage3_gsnap"]
 
 
 def check_compute(got_calls, got, final, want, what):
@@ -268,7 +270,7 @@ def check_path_compute(got_calls, got, probs, want, want_probs, final, what):
             raise AssertionError("%s: query %d pair %d: probabilities %s, want %s" % (what, i, k, gp[k], ep[k]))
 
 
-@pytest.mark.parametrize("name", PIPE_NAMES)
+@pytest.mark.parametrize("name", PIPE_NAMES + GSNAP_PIPE_NAMES)
 def test_stage3_path_compute_cpu_matches_reference(golden_dir, tmp_path, name):
     """path_compute from pass 2A to its return value (passes 2A-10: the dual
     breaks at the ends, the adjacent indels, the end extensions,
@@ -277,9 +279,12 @@ def test_stage3_path_compute_cpu_matches_reference(golden_dir, tmp_path, name):
     invocation, bit for bit: the returned list, every pair's
     donor_prob / acceptor_prob, *intronlen, *nonintronlen, *defect_rate and
     the pass calls made, with the DP families and MaxEnt served by the oracle
-    under ASan + UBSan"""
+    under ASan + UBSan.  The *_gsnap sets hold what the reference's path_compute
+    returns when built as GSNAP builds it (-DGSNAP, oracle/pc_replay.c) on the
+    same invocations, and run with gsnap = 1"""
     from gsnapdp.records import S3_COMPUTE_STATS, S3_CALL, S3_PAIR
     z = np.load(os.path.join(golden_dir, name + ".npz"), allow_pickle=False)
+    gsnap = int(z["gsnap"]) if "gsnap" in z else 0
     queries, pin, q, qu, want, want_probs, final = W.stage3_path_pipeline(z)
     assert len(queries) == len(z["pc_calls"])
     d = str(tmp_path)
@@ -295,7 +300,7 @@ def test_stage3_path_compute_cpu_matches_reference(golden_dir, tmp_path, name):
                GSNAPDP_MAXENT_TABLES=os.path.join(ROOT, "gmap-gsnap_amd", "data", "maxent_hr_tables.bin"))
     maxintron = int(final["maxintronlen_bound"][0])
     p = subprocess.run([os.path.join(ROOT, "oracle", "_build", "stage3_cpu"), d, "--path-compute", "9",
-                        str(maxintron)], env=env, capture_output=True, text=True, timeout=900)
+                        str(maxintron), str(gsnap)], env=env, capture_output=True, text=True, timeout=900)
     assert p.returncode == 0, "stage3_cpu --path-compute failed (%d):\n%s" % (p.returncode, p.stderr[-6000:])
     assert "runtime error" not in p.stderr, p.stderr[-6000:]
     got_calls = np.fromfile(os.path.join(d, "pass_calls.bin"), dtype=S3_CALL)
