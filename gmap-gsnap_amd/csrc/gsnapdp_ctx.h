@@ -26,6 +26,15 @@ int gsnapdp__fill_pipeline(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_windo
                            uint32_t* d_ops, const int64_t* d_op_offsets, const gsnapdp_sj_window* sjw);
 // allocate the row-lane classes' global scratch on first use
 int gsnapdp__rows_pools(gsnapdp_ctx* ctx);
+// LDS guard, run once by gsnapdp_create: a kernel's static LDS (hipFuncGetAttributes)
+// plus the dynamic LDS it is launched with must fit one workgroup's LDS (max_lds), or
+// the launch aborts the queue (HSA_STATUS_ERROR_INVALID_ALLOCATION) instead of
+// failing with a message.  Returns -1 with gsnapdp_last_error naming the kernel.
+int gsnapdp__lds_fits(const void* fn, size_t dyn, size_t max_lds, const char* name);
+int gsnapdp__ggap_lds_check(size_t max_lds);   // gsnapdp_ggap.hip's kernels
+int gsnapdp__gband_lds_check(size_t max_lds);  // k_gband
+int gsnapdp__micro_lds_check(size_t max_lds);  // k_micro
+int gsnapdp__gather_lds_check(size_t max_lds); // k_compact
 // k_gband over the register-band lists of a genome-gap batch (gsnapdp_gband.hip)
 int gsnapdp__gband_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_ggap_window* d_windows,
                           const int* lists, const int* counts, int list_cap, const char* d_query,
@@ -99,6 +108,7 @@ struct gsnapdp_ctx {
   int csum_cap = 0;
   int64_t* d_csum = nullptr;    // k_compact: per-block status words (epoch-tagged)
   uint32_t compact_epoch = 0;
+  hipEvent_t compact_done = nullptr;  // the last compaction's launch (the next one waits for it)
   // score_introns batches (gsnapdp_score_introns_host): device staging
   size_t si_cap = 0;
   char* d_si_stage = nullptr;

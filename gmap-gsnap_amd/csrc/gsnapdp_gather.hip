@@ -136,6 +136,12 @@ extern "C" int gsnapdp_compact_ops_device(gsnapdp_ctx* ctx, const gsnapdp_result
     ctx->csum_cap = cap;
     ctx->compact_epoch = 0;
   }
+  // The status words are the context's, so two compactions must not overlap on
+  // the GPU (one call's epoch would hide the words the other's look-back waits
+  // for, and it would spin forever): each launch waits for the previous one,
+  // whatever stream either was issued on.
+  if (!ctx->compact_done) HIPCHK(hipEventCreateWithFlags(&ctx->compact_done, hipEventDisableTiming));
+  else HIPCHK(hipStreamWaitEvent(st, ctx->compact_done, 0));
   // a fresh epoch per call, so no status word of an earlier call matches;
   // the words are cleared once per 2^24 calls (and on allocation)
   ctx->compact_epoch = (ctx->compact_epoch + 1) & 0xFFFFFFu;
@@ -145,5 +151,8 @@ extern "C" int gsnapdp_compact_ops_device(gsnapdp_ctx* ctx, const gsnapdp_result
   hipLaunchKernelGGL(k_compact, dim3(nb), dim3(CT), 0, st, d_results, n, d_ops, d_op_offsets,
                      (uint64_t*)ctx->d_csum, (uint64_t)ctx->compact_epoch, d_out, out_cap, d_header);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ctx->compact_done, st));
   return 0;
 }
+
+int gsnapdp__gather_lds_check(size_t max_lds) { return gsnapdp__lds_fits((const void*)&k_compact, 0, max_lds, "k_compact"); }

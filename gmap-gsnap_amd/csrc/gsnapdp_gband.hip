@@ -1191,3 +1191,5 @@ int gsnapdp__gband_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_ggap_w
 #endif
   return 0;
 }
+
+int gsnapdp__gband_lds_check(size_t max_lds) { return gsnapdp__lds_fits((const void*)&k_gband, 0, max_lds, "k_gband"); }

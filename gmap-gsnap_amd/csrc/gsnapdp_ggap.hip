@@ -1285,6 +1285,28 @@ int gsnapdp__rows_pools(gsnapdp_ctx* ctx) {
   return 0;
 }
 
+// k_rows takes every byte of a CU's LDS as dynamic LDS, so it must declare no
+// static __shared__ of its own (round 5: a 4-byte static ticket beside the
+// 160 KB made group_seg_size 163844 and aborted the queue)
+constexpr size_t RW_DYN_LDS = (size_t)160 * 1024;
+
+int gsnapdp__ggap_lds_check(size_t max_lds) {
+  const size_t small = (size_t)8 * GG_SMALL_WORDS * 4, mid = (size_t)4 * GG_MID_WORDS * 4;
+  if (gsnapdp__lds_fits((const void*)&k_rows<false>, RW_DYN_LDS, max_lds, "k_rows") ||
+      gsnapdp__lds_fits((const void*)&k_rows<true>, RW_DYN_LDS, max_lds, "k_rows<SEG>") ||
+      gsnapdp__lds_fits((const void*)&k_sj_plan, 0, max_lds, "k_sj_plan") ||
+      gsnapdp__lds_fits((const void*)&k_ggap_plan, 0, max_lds, "k_ggap_plan") ||
+      gsnapdp__lds_fits((const void*)&k_ggap<32, false>, small, max_lds, "k_ggap<32>") ||
+      gsnapdp__lds_fits((const void*)&k_ggap<64, false>, mid, max_lds, "k_ggap<64>") ||
+      gsnapdp__lds_fits((const void*)&k_ggap<64, true>, 0, max_lds, "k_ggap<64, striped>") ||
+      gsnapdp__lds_fits((const void*)&k_cgap_plan, 0, max_lds, "k_cgap_plan") ||
+      gsnapdp__lds_fits((const void*)&k_cgap<32, false>, small, max_lds, "k_cgap<32>") ||
+      gsnapdp__lds_fits((const void*)&k_cgap<64, false>, mid, max_lds, "k_cgap<64>") ||
+      gsnapdp__lds_fits((const void*)&k_cgap<64, true>, 0, max_lds, "k_cgap<64, striped>"))
+    return -1;
+  return 0;
+}
+
 // the row-lane classes, one launch each (lists[c * list_cap ...], counts[c])
 template <bool SEG>
 static int rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* dw, const int* lists,
@@ -1298,8 +1320,8 @@ static int rows_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_window* d
                     8 * RW_MID_WORDS * 4 <= 160 * 1024 && RW_LARGE_WAVES_PER_CU == 16 &&
                     RW_BIG_WAVES % 16 == 0,
                 "k_rows regions");
-  if (ctx->num_cus * 16 < RW_BIG_WAVES) return -1;  // the big class's waves
-  hipLaunchKernelGGL((k_rows<SEG>), dim3(ctx->num_cus), dim3(1024), (size_t)160 * 1024, st, dw, lists,
+  // (gsnapdp_create checked num_cus * 16 >= RW_BIG_WAVES and the static + dynamic LDS)
+  hipLaunchKernelGGL((k_rows<SEG>), dim3(ctx->num_cus), dim3(1024), RW_DYN_LDS, st, dw, lists,
                      list_cap, counts, d_query, d_query_uc, ctx->d_blocks, nw, ctx->d_prof,
                      ctx->d_largepool, ctx->d_bigpool, d_results, d_ops, d_op_offsets, sjw);
   HIPCHK(hipGetLastError());

@@ -229,15 +229,28 @@ __global__ void k_plan(const gsnapdp_window* __restrict__ W, int n, const char* 
   if (threadIdx.x < RW_NCLS)
     lbase[threadIdx.x] = lbig[threadIdx.x] > 0 ? atomicAdd(big_count + threadIdx.x, lbig[threadIdx.x]) : 0;
   if (threadIdx.x == 0 && lend != 0) atomicOr(big_count + RW_NCLS, lend);
+  // returning atomics, their results consumed below: each thread holds the
+  // values its histogram atomics returned before the block takes its ticket
+  int seen = 0;
   for (int k = threadIdx.x; k < NKEYS; k += blockDim.x)
-    if (lh[k] > 0) atomicAdd(&hist[k], lh[k]);
+    if (lh[k] > 0) seen |= __hip_atomic_fetch_add(&hist[k], lh[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (seen < 0) lend = -1;  // counts are never negative: keeps the returned values live
   __syncthreads();
   if (big >= 0) big_list[(size_t)big * list_cap + lbase[big] + lslot] = i;
   // The last block to finish scans the histogram (no separate k_scan launch).
-  // Every thread waits for its histogram atomics to be performed before the
-  // block takes its ticket; the scan reads them back by atomics.  (No
-  // agent-scope fence: each one writes back the XCD's L2, 0.28 ms per batch.)
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  // Ordering, and the hardware property it rests on (measured, not an
+  // architectural guarantee: MI355X_MICROARCH.md's inter-workgroup hand-off
+  // table, the "last adder told by its returned value" row): the histogram
+  // words and the ticket are only ever accessed by agent-scope atomics, which
+  // gfx950 performs at the memory side, past the non-coherent per-XCD L2s, so
+  // every atomic on a word reads the latest value in its modification order.  A block takes its ticket only
+  // after every thread has the RESULTS of its histogram atomics back (returned
+  // value = performed there); the ticket's own atomic order then puts every
+  // block's histogram adds before the last block's atomicExch reads in
+  // scan_buckets.  No release/acquire pair is used because an agent-scope
+  // release on gfx950 writes back the XCD's L2 (buffer_wbl2): 0.28 ms per 1M
+  // batch when tried.  tests/test_gpu_parity.py::test_gpu_bucket_scan_stress
+  // checks the buckets over many batches of varying size.
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0)
@@ -1175,10 +1188,39 @@ __global__ void k_introns(const gsnapdp_intron_path* __restrict__ P, int npaths,
 static thread_local std::string g_err;
 void gsnapdp__set_err(const std::string& s) { g_err = s; }
 
+// the context's small area: histogram, cursors, class starts, row-lane class
+// counts, END flags and tickets (zero between batches)
+static constexpr size_t SMALL_WORDS = (size_t)2 * NKEYS + NCLASS + 1 + 1 + 64;
+
 // per-wave k_fill scratch: TB_BATCH regions (see FILL_REGION_DW)
 static const size_t WAVE_STRIDE_DW = (size_t)TB_BATCH * FILL_REGION_DW;
 
 extern "C" const char* gsnapdp_last_error(void) { return g_err.c_str(); }
+
+int gsnapdp__lds_fits(const void* fn, size_t dyn, size_t max_lds, const char* name) {
+  hipFuncAttributes a;
+  HIPCHK(hipFuncGetAttributes(&a, fn));
+  if (a.sharedSizeBytes + dyn > max_lds) {
+    g_err = std::string(name) + ": " + std::to_string(a.sharedSizeBytes) + " B of static LDS + " +
+            std::to_string(dyn) + " B dynamic exceed the " + std::to_string(max_lds) +
+            " B a workgroup can hold (the launch would abort the queue)";
+    return -1;
+  }
+  return 0;
+}
+
+// this file's kernels (none takes dynamic LDS)
+static int kernels_lds_check(size_t max_lds) {
+  if (gsnapdp__lds_fits((const void*)&k_plan, 0, max_lds, "k_plan") ||
+      gsnapdp__lds_fits((const void*)&k_scatter, 0, max_lds, "k_scatter") ||
+      gsnapdp__lds_fits((const void*)&k_fill, 0, max_lds, "k_fill") ||
+      gsnapdp__lds_fits((const void*)&k_maxent, 0, max_lds, "k_maxent") ||
+      gsnapdp__lds_fits((const void*)&k_introns, 0, max_lds, "k_introns"))
+    return -1;
+  if constexpr (!FILL_MATCH)
+    if (gsnapdp__lds_fits((const void*)&k_count, 0, max_lds, "k_count")) return -1;
+  return 0;
+}
 
 extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_t nwords,
                                         int mode) {
@@ -1204,6 +1246,23 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
   }
   ctx->fill_waves = prop.multiProcessorCount * 4 * GSNAPDP_FILL_WAVES;  // k_fill's occupancy
   ctx->num_cus = prop.multiProcessorCount;
+  if (ctx->num_cus * 16 < RW_BIG_WAVES) {  // k_rows' big class runs on 16 waves per CU
+    gsnapdp__set_err("gsnapdp needs at least " + std::to_string(RW_BIG_WAVES / 16) + " CUs; device has " +
+                     std::to_string(ctx->num_cus));
+    delete ctx;
+    return nullptr;
+  }
+  {  // static + dynamic LDS of every kernel against one workgroup's LDS
+    int max_lds = 0;
+    if ((e = hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device)) != hipSuccess)
+      return fail("max LDS", e);
+    if (kernels_lds_check((size_t)max_lds) || gsnapdp__ggap_lds_check((size_t)max_lds) ||
+        gsnapdp__gband_lds_check((size_t)max_lds) || gsnapdp__micro_lds_check((size_t)max_lds) ||
+        gsnapdp__gather_lds_check((size_t)max_lds)) {
+      delete ctx;
+      return nullptr;
+    }
+  }
   {
     const char* e = getenv("GSNAPDP_GGAP_ROWLANE");
     ctx->ggap_rowlane_only = (e && e[0] == '1') ? 1 : 0;
@@ -1243,9 +1302,8 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
   if ((e = hipMemcpy(ctx->d_prof, ctx->h_prof, sizeof(ctx->h_prof), hipMemcpyHostToDevice)) !=
       hipSuccess)
     return fail("copy prof", e);
-  const size_t small = (size_t)2 * NKEYS + NCLASS + 1 + 1 + 64;
-  if ((e = hipMalloc(&ctx->d_small, small * 4)) != hipSuccess) return fail("malloc small", e);
-  if ((e = hipMemset(ctx->d_small, 0, small * 4)) != hipSuccess) return fail("memset small", e);
+  if ((e = hipMalloc(&ctx->d_small, SMALL_WORDS * 4)) != hipSuccess) return fail("malloc small", e);
+  if ((e = hipMemset(ctx->d_small, 0, SMALL_WORDS * 4)) != hipSuccess) return fail("memset small", e);
 
   ctx->dirpool_waves = (size_t)ctx->fill_waves;
   if ((e = hipMalloc(&ctx->d_dirpool, ctx->dirpool_waves * WAVE_STRIDE_DW * 4)) != hipSuccess)
@@ -1281,11 +1339,37 @@ extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   if (ctx->h_in) (void)hipHostFree(ctx->h_in);
   if (ctx->h_mx) (void)hipHostFree(ctx->h_mx);
   (void)hipFree(ctx->d_mx_stage);
+  if (ctx->compact_done) (void)hipEventDestroy(ctx->compact_done);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
 
 extern "C" const char* gsnapdp_device_arch(gsnapdp_ctx* ctx) { return ctx ? ctx->arch.c_str() : ""; }
+
+extern "C" int64_t gsnapdp_debug_buckets(gsnapdp_ctx* ctx, int n, int32_t* keys, int32_t* perm,
+                                         int64_t perm_cap, int32_t* class_start, int32_t* class_wave,
+                                         int ncls) {
+  if (!ctx) return -1;
+  if (!keys && !perm && !class_start && !class_wave) return NCLASS;
+  if (ncls != NCLASS || n < 0 || n > ctx->cap_n) {
+    g_err = "gsnapdp_debug_buckets: ncls must be " + std::to_string(NCLASS) + " and n at most the last batch";
+    return -1;
+  }
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  int32_t cs[NCLASS + 1];
+  const int* class_start_d = ctx->d_small + 2 * NKEYS;  // after hist and cursor (gsnapdp__fill_pipeline)
+  HIPCHK(hipMemcpy(cs, class_start_d, sizeof(cs), hipMemcpyDeviceToHost));
+  const int64_t nperm = cs[NCLASS];
+  if (class_start) memcpy(class_start, cs, sizeof(cs));
+  if (class_wave)
+    for (int c = 0; c < NCLASS; c++) class_wave[c] = 64 / CLASS_LPW[c];
+  if (keys && n) HIPCHK(hipMemcpy(keys, ctx->d_keys, (size_t)n * 4, hipMemcpyDeviceToHost));
+  if (perm && nperm > 0)
+    HIPCHK(hipMemcpy(perm, ctx->d_perm, (size_t)std::min(nperm, perm_cap) * 4, hipMemcpyDeviceToHost));
+  return nperm;
+}
 
 extern "C" int gsnapdp_sync(gsnapdp_ctx* ctx) {
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1381,11 +1465,23 @@ int gsnapdp__fill_pipeline(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_windo
   }
 #endif
   mark(3, 0);
+  // A batch that stops between k_plan and the end of k_rows would leave the
+  // histogram, row-lane counts, END flags or tickets set (only the last blocks
+  // of k_plan / k_rows clear them): put the whole small area back to its
+  // allocation state so the next batch starts clean.
+  auto recover = [&]() {
+    (void)hipGetLastError();
+    (void)hipMemsetAsync(ctx->d_small, 0, SMALL_WORDS * 4, st);
+    return -1;
+  };
   if (gsnapdp__rows_launch(ctx, st, d_windows, ctx->d_big_list, big_count, ctx->cap_n, d_query,
                            d_query_uc, d_results, d_ops, d_op_offsets, sjw))
-    return -1;
+    return recover();
   mark(3, 1);
-  HIPCHK(hipGetLastError());
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) {
+    g_err = std::string("single/end-gap pipeline launch: ") + hipGetErrorString(e);
+    return recover();
+  }
   return 0;
 }
 

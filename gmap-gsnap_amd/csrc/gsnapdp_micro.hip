@@ -379,3 +379,5 @@ extern "C" int gsnapdp_micro_run_host(gsnapdp_ctx* ctx, const gsnapdp_micro_wind
   HIPCHK(hipStreamSynchronize(st));
   return 0;
 }
+
+int gsnapdp__micro_lds_check(size_t max_lds) { return gsnapdp__lds_fits((const void*)&k_micro, 0, max_lds, "k_micro"); }

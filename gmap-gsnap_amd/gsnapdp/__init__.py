@@ -71,6 +71,8 @@ def lib():
         L.gsnapdp_profile_read.argtypes = [vp, vp, i32]
         L.gsnapdp_profile_read.restype = i32
         L.gsnapdp_stage_name.argtypes = [i32]
+        L.gsnapdp_debug_buckets.argtypes = [vp, i32, vp, vp, ctypes.c_int64, vp, vp, i32]
+        L.gsnapdp_debug_buckets.restype = ctypes.c_int64
         L.gsnapdp_stage_name.restype = ctypes.c_char_p
         L.gsnapdp_ggap_run_host.argtypes = [vp, vp, i32, vp, vp, sz, vp, vp, vp, vp]
         L.gsnapdp_ggap_run_host.restype = i32
@@ -285,6 +287,21 @@ class Context:
         if rc != 0:
             raise GsnapdpError("gsnapdp_run_host: %s" % lib().gsnapdp_last_error().decode())
         return res, ops, off
+
+    def debug_buckets(self, n: int):
+        """Test hook: the last single/end-gap batch's bucketing (gsnapdp_debug_buckets):
+        (keys[n], perm[nperm], class_start[ncls + 1], class_wave[ncls])."""
+        ncls = int(lib().gsnapdp_debug_buckets(self.h, 0, None, None, 0, None, None, 0))
+        keys = np.zeros(max(n, 1), dtype=np.int32)
+        cs = np.zeros(ncls + 1, dtype=np.int32)
+        cw = np.zeros(ncls, dtype=np.int32)
+        nperm = int(lib().gsnapdp_debug_buckets(self.h, n, _p(keys), None, 0, _p(cs), _p(cw), ncls))
+        if nperm < 0:
+            raise GsnapdpError("gsnapdp_debug_buckets: %s" % lib().gsnapdp_last_error().decode())
+        perm = np.zeros(max(nperm, 1), dtype=np.int32)
+        if lib().gsnapdp_debug_buckets(self.h, n, None, _p(perm), nperm, None, None, ncls) != nperm:
+            raise GsnapdpError("gsnapdp_debug_buckets: %s" % lib().gsnapdp_last_error().decode())
+        return keys[:n], perm[:nperm], cs, cw
 
     def pairs(self, windows, query, query_uc, results, ops, off, i: int) -> tuple[np.ndarray, int]:
         """The pair list window i's reference call returns (gsnapdp_expand)."""
@@ -588,9 +605,11 @@ class Context:
                                                 _p(go) if go is not None else None, _p(q), _p(qu),
                                                 min(q.size, qu.size), iit.h if iit is not None else None,
                                                 _p(bufs[0]), bufs[0].size, _p(bufs[1]), bufs[1].size, _p(st))
-            need = int(st[0]["out_needed"])
-            if rc != 0 and attempt == 0 and need > bufs[0].size:  # the runs output was too small: once more
-                bufs = (np.empty(need + 1024, dtype=S3_RUN), bufs[1])
+            need, nnew = int(st[0]["out_needed"]), int(st[0]["new_pairs"])
+            if rc != 0 and attempt == 0 and (need > bufs[0].size or nnew > bufs[1].size):
+                # the runs or the new-pair output was too small: once more, both grown to what was asked
+                bufs = (bufs[0] if need <= bufs[0].size else np.empty(need + 1024, dtype=S3_RUN),
+                        bufs[1] if nnew <= bufs[1].size else np.empty(nnew + 1024, dtype=S3_PAIR))
                 continue
             break
         if rc != 0:

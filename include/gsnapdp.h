@@ -284,7 +284,12 @@ size_t gsnapdp_scratch_bytes(gsnapdp_ctx *ctx, int n, int max_length1, int max_l
  * rebuilds every window's offset from the nops column (exclusive prefix sum).
  * d_header (2 x int64, device) receives {total ops, overflow}: overflow = 1
  * when total > out_cap, in which case only the windows that fit entirely
- * were written.  Asynchronous on `stream` (NULL = context stream). */
+ * were written.  Asynchronous on `stream` (NULL = context stream); calls on
+ * one context run one after another on the GPU whatever streams they are
+ * issued on (each waits for the previous call's launch: they share the
+ * context's look-back status words).  The other device entry points of one
+ * context share its scratch too: issue them on one stream, or order the
+ * streams yourself. */
 int gsnapdp_compact_ops_device(gsnapdp_ctx *ctx, const gsnapdp_result *d_results, int n,
                                const uint32_t *d_ops, const int64_t *d_op_offsets, uint32_t *d_out,
                                int64_t out_cap, int64_t *d_header, void *stream);
@@ -306,6 +311,18 @@ int gsnapdp_sync(gsnapdp_ctx *ctx);
 int gsnapdp_profile(gsnapdp_ctx *ctx, int enable);
 int gsnapdp_profile_read(gsnapdp_ctx *ctx, double *ms, int nstages);
 const char *gsnapdp_stage_name(int stage);
+
+/* Test hook (no reference counterpart): the register-band bucketing of the last
+ * single/end-gap batch on this context (k_plan + its last-block scan +
+ * k_scatter).  Synchronises the context stream, then copies keys[0..n) (each
+ * window's bucket key, -1 for a window not on k_fill), the first min(nperm,
+ * perm_cap) entries of perm (a window index, or -1 for a bucket's padding),
+ * class_start[0..ncls] and the class wave sizes (windows per wave-task) into
+ * class_wave[0..ncls).  Returns nperm (= class_start[ncls]), or -1; ncls must
+ * be the number of band classes, gsnapdp_debug_buckets(ctx, 0, ...) with all
+ * pointers NULL returns it. */
+int64_t gsnapdp_debug_buckets(gsnapdp_ctx *ctx, int n, int32_t *keys, int32_t *perm, int64_t perm_cap,
+                              int32_t *class_start, int32_t *class_wave, int ncls);
 
 /* ------------------------------------------------------------ maxent_hr
  * Batched Maxent_hr_{donor,acceptor,antidonor,antiacceptor}_prob

@@ -190,3 +190,58 @@ def test_gpu_consecutive_batches_on_one_context():
         pairs, npairs = ctx.all_pairs(b.windows, b.query, b.query_uc, res, ops, off)
         compare(res, pairs, npairs, *refs[k], "batch kind %d on a shared context" % k)
     ctx.close()
+
+
+def check_buckets(keys, perm, cs, cw, what):
+    """k_plan's last-block scan + k_scatter: every k_fill window (key >= 0) in perm
+    exactly once; each class range a whole number of wave-tasks; each wave-task
+    one key, its padding (-1) at its end; each key's windows contiguous."""
+    n = keys.size
+    live = perm[perm >= 0]
+    assert np.array_equal(np.sort(live), np.nonzero(keys >= 0)[0]), "%s: perm is not the k_fill windows" % what
+    assert cs[0] == 0 and np.all(np.diff(cs) >= 0) and cs[-1] == perm.size, what
+    pk = np.where(perm >= 0, keys[np.clip(perm, 0, max(n - 1, 0))], -1)
+    for c in range(cw.size):
+        a, b, g = int(cs[c]), int(cs[c + 1]), int(cw[c])
+        assert (b - a) % g == 0, "%s: class %d range %d not a multiple of %d" % (what, c, b - a, g)
+        chunks = pk[a:b].reshape(-1, g)
+        if chunks.size == 0:
+            continue
+        first = chunks[:, 0]
+        assert np.all(first >= 0), "%s: class %d has an empty wave-task" % (what, c)
+        ok = (chunks == first[:, None]) | (chunks == -1)
+        assert ok.all(), "%s: class %d: a wave-task mixes keys" % (what, c)
+        pad = chunks == -1
+        assert np.all(np.diff(pad.astype(np.int8), axis=1) >= 0), "%s: class %d: padding inside a task" % (what, c)
+    # a key's wave-tasks are contiguous: keys appear as one run each in task order
+    tk = pk[pk >= 0]
+    runs = tk[np.r_[True, tk[1:] != tk[:-1]]]
+    assert runs.size == np.unique(tk).size, "%s: a key's windows are split" % what
+
+
+def test_gpu_bucket_scan_stress():
+    """The bucketing (k_plan's histogram atomics read back by its last block's
+    scan, then k_scatter) over 48 batches of 1 to 120k windows on one context,
+    each batch's buckets checked against the host (check_buckets) and its
+    results bit-exact against the restatement's over the same windows."""
+    g = W.synthetic_genome(4_000_000, seed=91, n_rate=0.002)
+    blocks = W.pack_genome(g)
+    pool = W.concat_batches([W.random_windows(g, 20_000, seed=910 + k, max_len1=m1, max_len2=m1 + 20,
+                                              max_band=b)
+                             for k, (m1, b) in enumerate(((40, 3), (120, 10), (160, 20), (200, 40)))])
+    O.setup(blocks)
+    ores, _, _, _ = O.run_batch(pool.windows, pool.query, pool.query_uc, nthreads=16)
+    rng = np.random.default_rng(92)
+    ctx = Context(blocks)
+    sizes = [1, 2, 63, 64, 65, 1000, 120_000 if len(pool) >= 120_000 else len(pool)]
+    sizes += [int(x) for x in rng.integers(1, len(pool), 41)]
+    for t, m in enumerate(sizes):
+        idx = rng.choice(len(pool), size=m, replace=False)
+        w = pool.windows[idx]
+        res, _, _ = ctx.run(w, pool.query, pool.query_uc)
+        keys, perm, cs, cw = ctx.debug_buckets(m)
+        check_buckets(keys, perm, cs, cw, "batch %d (%d windows)" % (t, m))
+        for f in ("finalscore", "nmatches", "nmismatches", "nopens", "nindels", "reserved"):
+            bad = np.nonzero(res[f] != ores[f][idx])[0]
+            assert bad.size == 0, "batch %d (%d windows): %s differs at %s" % (t, m, f, bad[:8])
+    ctx.close()

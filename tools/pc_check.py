@@ -29,6 +29,10 @@ def prep(trace, out):
     import gen_golden as G
     z = np.load(trace, allow_pickle=False)
     (queries, pin, q, qu), (want, wprobs, final), (gpc, gpp, gpr), differ = G.pc_replay(z)
+    # keep only the pass-2A paths and query bytes the queries use
+    pin = np.concatenate([pin[int(c["first_pair"]):int(c["first_pair"]) + int(c["npairs"])] for c in queries])
+    queries = queries.copy()
+    queries["first_pair"] = np.concatenate([[0], np.cumsum(queries["npairs"])[:-1]]).astype(np.int32)
     np.savez_compressed(out, blocks=z["blocks"], queries=queries, pin=pin, q=q, qu=qu, want=want, wprobs=wprobs,
                         final=final, gsnap_final=gpc, gsnap_want=gpp, gsnap_wprobs=gpr, s2_calls=z["s2_calls"],
                         s2_pairs=z["s2_pairs"])
