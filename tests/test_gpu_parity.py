@@ -215,6 +215,8 @@ def check_buckets(keys, perm, cs, cw, what):
         assert np.all(np.diff(pad.astype(np.int8), axis=1) >= 0), "%s: class %d: padding inside a task" % (what, c)
     # a key's wave-tasks are contiguous: keys appear as one run each in task order
     tk = pk[pk >= 0]
+    if tk.size == 0:
+        return
     runs = tk[np.r_[True, tk[1:] != tk[:-1]]]
     assert runs.size == np.unique(tk).size, "%s: a key's windows are split" % what
 
