@@ -164,6 +164,26 @@ __device__ inline int from_lane_above(int v) {
 __device__ inline int from_lane_below(int v) {
   return __builtin_amdgcn_mov_dpp(v, 0x101, 0xF, 0xF, true);  // row_shl:1
 }
+// (a, b) = min((x, y) of lane-1, cap) as 16-bit values, one v_min_u16_dpp each
+// where a DPP move and a select were two.  A lane without a source in its
+// 16-lane row is not written (bound_ctrl off): a and b are loop-carried, so
+// those lanes keep what they held (the caller starts them at a NEG-like
+// value).  The s_nop covers the DPP read-after-VALU-write hazard (2 wait
+// states), which the compiler does not see through inline asm.
+__device__ inline void min2_from_lane_above(uint32_t& a, uint32_t& b, uint32_t x, uint32_t y, uint32_t cap) {
+  asm("s_nop 1\n\t"
+      "v_min_u16_dpp %0, %2, %4 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_min_u16_dpp %1, %3, %4 row_shr:1 row_mask:0xf bank_mask:0xf"
+      : "+v"(a), "+v"(b)
+      : "v"(x), "v"(y), "v"(cap));
+}
+__device__ inline void min2_from_lane_below(uint32_t& a, uint32_t& b, uint32_t x, uint32_t y, uint32_t cap) {
+  asm("s_nop 1\n\t"
+      "v_min_u16_dpp %0, %2, %4 row_shl:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_min_u16_dpp %1, %3, %4 row_shl:1 row_mask:0xf bank_mask:0xf"
+      : "+v"(a), "+v"(b)
+      : "v"(x), "v"(y), "v"(cap));
+}
 
 // Per-wave LDS rings of k_fill (sizes per band class): for each window of the
 // wave, the profile words of the rows its lanes' bottom slots will need and the

@@ -326,6 +326,15 @@ constexpr int TB_BATCH = GSNAPDP_TB_BATCH;
 #define GSNAPDP_PERMBITS 1
 #endif
 constexpr int FILL_PL = GSNAPDP_PERMBITS ? 8 : 0;  // the plane stride (0: S)
+// GSNAPDP_DPP_MIN: the lane shifts as v_min_u16_dpp against a per-lane cap
+// instead of a DPP move and a select
+#ifndef GSNAPDP_DPP_MIN
+#define GSNAPDP_DPP_MIN 1
+#endif
+// GSNAPDP_ANDOR: each cell's direction bits joined by one v_and_or_b32
+#ifndef GSNAPDP_ANDOR
+#define GSNAPDP_ANDOR 1
+#endif
 [[maybe_unused]] constexpr uint32_t PERM_SIGNS = 0x0B0A0908u;  // result bytes 0..3 = signs of bytes 1, 3, 5, 7
 constexpr size_t FILL_COLS_DEV = (size_t)FAST_L2MAX + 4;
 constexpr size_t FILL_REGION_DW = FILL_COLS_DEV * 64 + FILL_COLS_DEV * 16;
@@ -550,6 +559,11 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
   // (j, g) stores column c = t - j at the wave-uniform row t-(LPW-1) plus a
   // non-negative lane offset.
   const int lane_off = (LPW - 1 - j) * 64 + j * NG + g;
+  // the lane shifts' caps: NEGV on the group's first (above) / last (below) lane
+  [[maybe_unused]] const FV capA = j == 0 ? NEGV : (FV)0xFFFFu, capB = j == LPW - 1 ? NEGV : (FV)0xFFFFu;
+  // their loop-carried results (the first lane of each 16-lane row never writes
+  // its above pair, the last never its below pair: they stay NEGV)
+  [[maybe_unused]] FV hpA = NEGV, fpA = NEGV, hbB = NEGV, ebB = NEGV;
 
   // One skewed step.  MASKED steps (the first and last LPW-1) leave lanes
   // whose column is outside 1..maxL2 untouched.
@@ -566,6 +580,16 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
     // a window stops at its own last column, so its registers end on column L2
     const bool act = !MASKED || (c >= 1 && c <= L2);
     FV hp = NEGV, fp = NEGV;  // new (nogap, gap2) just above local slot 0
+#if GSNAPDP_DPP_MIN
+    // lane j = 0 takes min(the lane above's value, NEGV): a NEG-like value (every
+    // value of the fill is >= the NEG-like floor, so the min is either NEGV or a
+    // NEG-like value itself; DESIGN.md "Band edges"), in one v_min_u16_dpp each
+    if (LPW > 1) {
+      min2_from_lane_above(hpA, fpA, H[S - 1], F[S - 1], capA);
+      hp = hpA;
+      fp = fpA;
+    }
+#else
     if (LPW > 1) {
       const FV h = (FV)from_lane_above((int)H[S - 1]), f = (FV)from_lane_above((int)F[S - 1]);
       if (j != 0) {
@@ -573,6 +597,7 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
         fp = f;
       }
     }
+#endif
     // four bit planes (v1, h1, dF, dE), each a short independent chain
     [[maybe_unused]] uint32_t av = 0u, ah = 0u, af = 0u, ae = 0u;
     uint32_t gsh = 0u;
@@ -613,7 +638,16 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
             : "+v"(p23)
             : "v"(JL ? fp : b), "v"(JL ? b : fp));
         asm("v_perm_b32 %0, %1, %2, %3" : "=v"(sg) : "v"(p01), "v"(p23), "s"(PERM_SIGNS));
+#if GSNAPDP_ANDOR
+        // one v_and_or_b32 per cell (the compiler's and + or3 tree issues twice as many)
+        if (s == 0) {
+          bits = sg & (0x01010101u << (S - 1));
+        } else {
+          asm("v_and_or_b32 %0, %1, %2, %0" : "+v"(bits) : "v"(sg), "s"(0x01010101u << (S - 1 - s)));
+        }
+#else
         bits = s == 0 ? (sg & (0x01010101u << (S - 1))) : ((sg & (0x01010101u << (S - 1 - s))) | bits);
+#endif
       }
       (void)dv, (void)dh, (void)df, (void)de;
 #elif defined(EXP_NODIFF)  // timing experiments only (wrong direction bits)
@@ -650,6 +684,13 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
       cell(0, H[1], E[1]);
     }
     FV hb = NEGV, eb = NEGV;  // old (nogap, gap1) just below the lowest local slot
+#if GSNAPDP_DPP_MIN
+    if (LPW > 1) {
+      min2_from_lane_below(hbB, ebB, H[0], E[0], capB);
+      hb = hbB;
+      eb = ebB;
+    }
+#else
     if (LPW > 1) {
       const FV h = (FV)from_lane_below((int)H[0]), e = (FV)from_lane_below((int)E[0]);
       if (j != LPW - 1) {
@@ -657,6 +698,7 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
         eb = e;
       }
     }
+#endif
     if (act) {
 #pragma unroll
       for (int s = 1; s < S - 1; s++) cell(s, H[s + 1], E[s + 1]);
