@@ -331,6 +331,10 @@ constexpr int FILL_PL = GSNAPDP_PERMBITS ? 8 : 0;  // the plane stride (0: S)
 #ifndef GSNAPDP_DPP_MIN
 #define GSNAPDP_DPP_MIN 1
 #endif
+// GSNAPDP_BUFSTAGE: the ring staging's loads as buffer loads with 32-bit offsets
+#ifndef GSNAPDP_BUFSTAGE
+#define GSNAPDP_BUFSTAGE 1
+#endif
 // GSNAPDP_ANDOR: each cell's direction bits joined by one v_and_or_b32
 #ifndef GSNAPDP_ANDOR
 #define GSNAPDP_ANDOR 1
@@ -414,7 +418,9 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
     qbase = L.qbase;
     qstep = L.qstep;
   }
-  const bool segw = sjw != nullptr;  // wave-uniform (a kernel argument)
+  // wave-uniform (a kernel argument; made so for the compiler, which sees a
+  // non-inlined function argument in VGPRs and would branch per lane)
+  const bool segw = __builtin_amdgcn_readfirstlane(sjw != nullptr ? 1 : 0) != 0;
   maxL2 = __builtin_amdgcn_readfirstlane(wave_max(L2));
   // the nogap step's constant -2*extend (= +6: k_fill serves single gaps, extend -3)
   // is folded into the LDS profile nibbles (FILL_SC_BIAS); the nogap value of a
@@ -468,11 +474,57 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
   uint32_t* rr = ring + g * RG::RR;
   uint8_t* cr = (uint8_t*)(ring + NG * RG::RR) + g * RG::CR;
   const int rbase = S - 1 - stop - rband;
+#if GSNAPDP_BUFSTAGE
+  // the staging's buffer resources (raw, byte offsets < 2^31; the genome's
+  // ends at its last word, so a block past it reads as 0)
+  // (the pointers arrive as arguments of a non-inlined function, in VGPRs: made
+  // wave-uniform first, so the resources live in SGPRs and no load needs a
+  // waterfall loop)
+  auto uniform = [](const void* p) -> void* {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return (void*)(((uint64_t)hi << 32) | lo);
+  };
+  const int nbytes = __builtin_amdgcn_readfirstlane((int)(nwords * 4 < 0x7FFFFFFFull ? nwords * 4 : 0x7FFFFFFFull));
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(uniform(q), 0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rqu = __builtin_amdgcn_make_buffer_rsrc(uniform(qu), 0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rgb = __builtin_amdgcn_make_buffer_rsrc(uniform(blocks), 0, nbytes, 0x00020000);
+  const int L1c = L1 > 0 ? L1 : 1, L2c = L2 > 0 ? L2 : 1, qb1 = qbase - qstep;
+  const uint32_t gmax32 = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(gmax < 0xFFFFFFFFull ? gmax : 0xFFFFFFFFull));
+#endif
   auto stage = [&](auto nrows_tag, int rlo, int clo) {
     constexpr int NR = decltype(nrows_tag)::value;
     constexpr int ER = (NR + LPW - 1) / LPW, EC = (RING_K + LPW - 1) / LPW;
     // all loads first (clamped addresses, no branches), then the words
     uint32_t qb[ER], ub[ER], gw[EC], gf[EC];
+#if GSNAPDP_BUFSTAGE
+    // buffer loads with 32-bit offsets (buffer resources rq / rqu / rgb below):
+    // a clamp and a 24-bit multiply-add per row, no 64-bit address arithmetic
+#pragma unroll
+    for (int e = 0; e < ER; e++) {
+      const int r = rlo + e * LPW + j;
+      const int qi = __mul24(qstep, min(max(r, 1), L1c)) + qb1;
+      qb[e] = __builtin_amdgcn_raw_buffer_load_b8(rq, qi, 0, 0);
+      ub[e] = __builtin_amdgcn_raw_buffer_load_b8(rqu, qi, 0, 0);
+    }
+#pragma unroll
+    for (int e = 0; e < EC; e++) {
+      const int c = clo + e * LPW + j;
+      if (segw) {  // the segment byte of column c (clamped into 1..L2; a shadow group's L2 is 0)
+        const int cc = min(max(c, 1), L2c);
+        gw[e] = __builtin_amdgcn_raw_buffer_load_b8(rq, (int)gp0 + __mul24(gps, cc), 0, 0);
+        gf[e] = 0u;
+      } else {
+        // block b of position pos at byte 12 b (a block past the genome reads 0: the
+        // resource ends at the genome's last word; such columns are N anyway)
+        const uint32_t pos = gp0 + (uint32_t)__mul24(gps, c);
+        const uint32_t b = pos >> 5;
+        const uint32_t ob = (b << 3) + (b << 2);
+        gw[e] = __builtin_amdgcn_raw_buffer_load_b32(rgb, (int)(ob + ((pos & 16u) ? 0u : 4u)), 0, 0);
+        gf[e] = __builtin_amdgcn_raw_buffer_load_b32(rgb, (int)(ob + 8u), 0, 0);
+      }
+    }
+#else
 #pragma unroll
     for (int e = 0; e < ER; e++) {
       const int r = rlo + e * LPW + j;
@@ -496,6 +548,7 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
         gf[e] = blocks[ptr + 2];
       }
     }
+#endif
 #pragma unroll
     for (int e = 0; e < ER; e++) {
       const int r = rlo + e * LPW + j;
@@ -508,9 +561,14 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
 #pragma unroll
     for (int e = 0; e < EC; e++) {
       const int c = clo + e * LPW + j;
+#if GSNAPDP_BUFSTAGE
+      const uint32_t pos = gp0 + (uint32_t)__mul24(gps, c);
+      const bool ing = (pos >> 5) <= gmax32;  // outside the genome: N
+#else
       const uint32_t pos = gp0 + (uint32_t)(gps * c);
-      const uint32_t bit = pos & 31u;
       const bool ing = (uint64_t)(pos >> 5) <= gmax;  // outside the genome: N
+#endif
+      const uint32_t bit = pos & 31u;
       const int code = (int)((gw[e] >> ((bit & 15u) * 2u)) & 3u) ^ xorc;
       const bool inr = c >= cvlo && c <= cvhi;
       int k = !inr ? 5 : ((!ing || ((gf[e] >> bit) & 1u)) ? 4 : code);
