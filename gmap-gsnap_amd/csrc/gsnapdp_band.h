@@ -185,6 +185,18 @@ __device__ inline void min2_from_lane_below(uint32_t& a, uint32_t& b, uint32_t x
       : "v"(x), "v"(y), "v"(cap));
 }
 
+// A pointer every lane holds the same value of (a kernel argument passed down
+// into a non-inlined function, which receives it in VGPRs): rebuilt from SGPRs,
+// so that its loads and stores address it as a scalar base (global_* saddr,
+// buffer resources) instead of per-lane 64-bit arithmetic.
+template <class T>
+__device__ inline T* wave_uniform(T* p) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return (T*)(((uint64_t)hi << 32) | lo);
+}
+
 // Per-wave LDS rings of k_fill (sizes per band class): for each window of the
 // wave, the profile words of the rows its lanes' bottom slots will need and the
 // genome classes of the columns they will need, staged RING_K columns at a time.

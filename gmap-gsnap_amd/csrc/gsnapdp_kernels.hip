@@ -490,6 +490,12 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
   const __amdgpu_buffer_rsrc_t rqu = __builtin_amdgcn_make_buffer_rsrc(uniform(qu), 0, 0x7FFFFFFF, 0x00020000);
   const __amdgpu_buffer_rsrc_t rgb = __builtin_amdgcn_make_buffer_rsrc(uniform(blocks), 0, nbytes, 0x00020000);
   const int L1c = L1 > 0 ? L1 : 1, L2c = L2 > 0 ? L2 : 1, qb1 = qbase - qstep;
+  // the direction / match scratch of this task, based LPW - 1 rows (of 64 lanes)
+  // early: a step's row offset t * 256 (t * 64) is then non-negative
+  const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(
+      uniform((const void*)((const char*)D - (LPW - 1) * 256)), 0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rM = __builtin_amdgcn_make_buffer_rsrc(
+      uniform((const void*)((const char*)M - (LPW - 1) * 64)), 0, 0x7FFFFFFF, 0x00020000);
   const uint32_t gmax32 = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(gmax < 0xFFFFFFFFull ? gmax : 0xFFFFFFFFull));
 #endif
   auto stage = [&](auto nrows_tag, int rlo, int clo) {
@@ -769,9 +775,19 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
       const uint32_t acc = (((((av << S) | ah) << S) | af) << S) | ae;
 #endif
 #ifndef EXP_NOSTORE
+#if GSNAPDP_BUFSTAGE
+      // buffer stores: the lane's constant offset in a VGPR, the step's row in an
+      // SGPR (t * 256 / t * 64 from resources based LPW - 1 rows below D / M),
+      // so a step's two stores need no address arithmetic
+      __builtin_amdgcn_raw_buffer_store_b32(acc, rD, lane_off * 4, t * 256, 0);
+#ifndef EXP_NOMATCH
+      if constexpr (FILL_MATCH) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)macc, rM, lane_off, t * 64, 0);
+#endif
+#else
       D[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = acc;
 #ifndef EXP_NOMATCH
       if constexpr (FILL_MATCH) M[(ptrdiff_t)(t - (LPW - 1)) * 64 + lane_off] = (uint8_t)macc;
+#endif
 #endif
 #else
       if (acc == 0x12345678u && macc == 77u) D[0] = 1u;
@@ -841,14 +857,14 @@ __device__ void trace_batch(int lane, int wi, FillOut fo, int jl,
                             AS_GLOBAL gsnapdp_result* res1, AS_GLOBAL uint32_t* ops1,
                             const AS_GLOBAL int64_t* op_off1, const AS_GLOBAL gsnapdp_sj_window* sjw1,
                             const AS_GLOBAL char* q1) {
-  const gsnapdp_window* __restrict__ Wn = (const gsnapdp_window*)Wn1;
-  const uint32_t* __restrict__ D = (const uint32_t*)D1;
-  const uint32_t* __restrict__ blocks = (const uint32_t*)blocks1;
-  gsnapdp_result* __restrict__ res = (gsnapdp_result*)res1;
-  uint32_t* __restrict__ ops = (uint32_t*)ops1;
-  const int64_t* __restrict__ op_off = (const int64_t*)op_off1;
-  const gsnapdp_sj_window* __restrict__ sjw = (const gsnapdp_sj_window*)sjw1;
-  const char* __restrict__ q = (const char*)q1;
+  const gsnapdp_window* __restrict__ Wn = wave_uniform((const gsnapdp_window*)Wn1);
+  const uint32_t* __restrict__ D = wave_uniform((const uint32_t*)D1);
+  const uint32_t* __restrict__ blocks = wave_uniform((const uint32_t*)blocks1);
+  gsnapdp_result* __restrict__ res = wave_uniform((gsnapdp_result*)res1);
+  uint32_t* __restrict__ ops = wave_uniform((uint32_t*)ops1);
+  const int64_t* __restrict__ op_off = wave_uniform((const int64_t*)op_off1);
+  const gsnapdp_sj_window* __restrict__ sjw = wave_uniform((const gsnapdp_sj_window*)sjw1);
+  const char* __restrict__ q = wave_uniform((const char*)q1);
   constexpr int NG = 64 / LPW;
   constexpr int WMAX = S * LPW;
   const int k = lane / NG, g = lane % NG;
@@ -897,15 +913,15 @@ __device__ __noinline__ void fill_tasks(int t0, int t1, int stride, const AS_GLO
                                         AS_GLOBAL uint32_t* D1, AS_GLOBAL gsnapdp_result* res1,
                                         AS_GLOBAL uint32_t* ops1, const AS_GLOBAL int64_t* op_off1,
                                         const AS_GLOBAL gsnapdp_sj_window* sjw1, int lag) {
-  const gsnapdp_window* __restrict__ Wn = (const gsnapdp_window*)Wn1;
-  const int* __restrict__ perm = (const int*)perm1;
-  const char* __restrict__ q = (const char*)q1;
-  const char* __restrict__ qu = (const char*)qu1;
-  const uint32_t* __restrict__ blocks = (const uint32_t*)blocks1;
+  const gsnapdp_window* __restrict__ Wn = wave_uniform((const gsnapdp_window*)Wn1);
+  const int* __restrict__ perm = wave_uniform((const int*)perm1);
+  const char* __restrict__ q = wave_uniform((const char*)q1);
+  const char* __restrict__ qu = wave_uniform((const char*)qu1);
+  const uint32_t* __restrict__ blocks = wave_uniform((const uint32_t*)blocks1);
   const uint32_t* sprof = (const uint32_t*)sprof3;
   uint32_t* ring = (uint32_t*)ring3;
-  uint32_t* __restrict__ D = (uint32_t*)D1;
-  const gsnapdp_sj_window* __restrict__ sjw = (const gsnapdp_sj_window*)sjw1;
+  uint32_t* __restrict__ D = wave_uniform((uint32_t*)D1);
+  const gsnapdp_sj_window* __restrict__ sjw = wave_uniform((const gsnapdp_sj_window*)sjw1);
   constexpr int NG = 64 / LPW;
   constexpr int B = LPW < TB_BATCH ? LPW : TB_BATCH;  // tasks per traceback sweep
   const int lane = threadIdx.x & 63;
