@@ -317,7 +317,7 @@ __global__ void k_scatter(const int* __restrict__ keys, int n, int* __restrict__
 // bytes, one 64-lane row per column 0 .. FAST_L2MAX + 3 (the traceback reads
 // whole 4-column groups)
 #ifndef GSNAPDP_TB_BATCH
-#define GSNAPDP_TB_BATCH 4
+#define GSNAPDP_TB_BATCH 8  // regions per wave; a class sweeps min(LPW, this) tasks at once (64 lanes)
 #endif
 constexpr int TB_BATCH = GSNAPDP_TB_BATCH;
 // GSNAPDP_PERMBITS: the direction bits by v_perm_b32 (one byte per plane) instead
