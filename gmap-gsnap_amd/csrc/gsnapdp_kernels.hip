@@ -339,6 +339,13 @@ constexpr int FILL_PL = GSNAPDP_PERMBITS ? 8 : 0;  // the plane stride (0: S)
 #ifndef GSNAPDP_ANDOR
 #define GSNAPDP_ANDOR 1
 #endif
+// GSNAPDP_GOPEN: each cell's H + open computed once (G) and read twice, as the
+// gap2 opening of the slot below (this step) and the gap1 opening of the slot
+// above (next step), instead of two adds per cell
+#ifndef GSNAPDP_GOPEN
+#define GSNAPDP_GOPEN 1
+#endif
+constexpr bool GOPEN = GSNAPDP_GOPEN != 0;
 [[maybe_unused]] constexpr uint32_t PERM_SIGNS = 0x0B0A0908u;  // result bytes 0..3 = signs of bytes 1, 3, 5, 7
 constexpr size_t FILL_COLS_DEV = (size_t)FAST_L2MAX + 4;
 constexpr size_t FILL_REGION_DW = FILL_COLS_DEV * 64 + FILL_COLS_DEV * 16;
@@ -442,6 +449,8 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
   const uint64_t gmax = nwords >= 3 ? (nwords - 3) / 3 : 0;  // last whole genome block
 
   FV H[S], E[S], F[S];
+  // GOPEN: G[s] = H[s] + open (the gap openings from slot s); otherwise unused
+  [[maybe_unused]] FV G[S];
   uint32_t P[S];
   // Match bits of the lane's S rows against each genome class: byte k of MB
   // holds, in bits 0..S-1, whether slot s's query row matches class k
@@ -464,6 +473,7 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
     E[s] = NEGV;
     F[s] = (r >= 1) ? FV_BIAS + open : NEGV;  // open + r*ext - r*ext
     P[s] = row_word(r);
+    if constexpr (GOPEN) G[s] = H[s] + open;
     if constexpr (FILL_MATCH) MB = ((MB >> 1) & MB_KEEP) | row_spread(P[s]);
   }
   // Rings: lane j of a window stages the rows / columns congruent to j mod
@@ -643,19 +653,22 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
     const int c = t - j;
     // a window stops at its own last column, so its registers end on column L2
     const bool act = !MASKED || (c >= 1 && c <= L2);
-    FV hp = NEGV, fp = NEGV;  // new (nogap, gap2) just above local slot 0
+    // new (nogap, gap2) just above local slot 0 (GOPEN: nogap + open)
+    FV hp = NEGV, fp = NEGV;
 #if GSNAPDP_DPP_MIN
     // lane j = 0 takes min(the lane above's value, NEGV): a NEG-like value (every
     // value of the fill is >= the NEG-like floor, so the min is either NEGV or a
     // NEG-like value itself; DESIGN.md "Band edges"), in one v_min_u16_dpp each
     if (LPW > 1) {
-      min2_from_lane_above(hpA, fpA, H[S - 1], F[S - 1], capA);
+      // (GOPEN: G instead of H; min(G, NEGV) is NEG-like exactly when
+      // min(H, NEGV) + open is, so the cap stays NEGV)
+      min2_from_lane_above(hpA, fpA, GOPEN ? G[S - 1] : H[S - 1], F[S - 1], capA);
       hp = hpA;
       fp = fpA;
     }
 #else
     if (LPW > 1) {
-      const FV h = (FV)from_lane_above((int)H[S - 1]), f = (FV)from_lane_above((int)F[S - 1]);
+      const FV h = (FV)from_lane_above((int)(GOPEN ? G[S - 1] : H[S - 1])), f = (FV)from_lane_above((int)F[S - 1]);
       if (j != 0) {
         hp = h;
         fp = f;
@@ -667,11 +680,11 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
     uint32_t gsh = 0u;
     [[maybe_unused]] uint32_t bits = 0u;  // GSNAPDP_PERMBITS: the four planes, one byte each
     int bstep = END == 2 ? 0 : -(1 << 30);  // END: this column's best scan key (END 2: value), less R(c)
-    auto cell = [&](int s, FV Hr, FV Er) {
+    auto cell = [&](int s, FV Hr, FV Er) {  // (GOPEN: Hr is the slot below's G)
       const FV Hd = H[s], Ed = E[s], Fd = F[s];
       const uint32_t pw = pslot(s);
-      const FV a = Hr + open;
-      const FV b = hp + open;
+      const FV a = GOPEN ? Hr : Hr + open;
+      const FV b = GOPEN ? hp : hp + open;
       const FV m1 = fv_max(Hd, Ed);
       // pairdistance - 2*extend
       const FV sc = END ? (FV)__builtin_amdgcn_sbfe((int)pw, (int)gsh, 4) : (FV)__builtin_amdgcn_ubfe(pw, gsh, 4);
@@ -728,7 +741,12 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
       const FV f = fv_max(b, fp);
       F[s] = f;
       H[s] = hn;
-      hp = hn;
+      if constexpr (GOPEN) {
+        G[s] = hn + open;
+        hp = G[s];
+      } else {
+        hp = hn;
+      }
       fp = f;
     };
     uint32_t macc = 0u;  // this column's match bits, bit s = slot s
@@ -745,18 +763,18 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
         MB = ((MB >> 1) & MB_KEEP) | row_spread(pnext);
         macc = (uint32_t)(MB >> (8u * (uint32_t)gnext));
       }
-      cell(0, H[1], E[1]);
+      cell(0, GOPEN ? G[1] : H[1], E[1]);
     }
     FV hb = NEGV, eb = NEGV;  // old (nogap, gap1) just below the lowest local slot
 #if GSNAPDP_DPP_MIN
     if (LPW > 1) {
-      min2_from_lane_below(hbB, ebB, H[0], E[0], capB);
+      min2_from_lane_below(hbB, ebB, GOPEN ? G[0] : H[0], E[0], capB);
       hb = hbB;
       eb = ebB;
     }
 #else
     if (LPW > 1) {
-      const FV h = (FV)from_lane_below((int)H[0]), e = (FV)from_lane_below((int)E[0]);
+      const FV h = (FV)from_lane_below((int)(GOPEN ? G[0] : H[0])), e = (FV)from_lane_below((int)E[0]);
       if (j != LPW - 1) {
         hb = h;
         eb = e;
@@ -765,7 +783,7 @@ __device__ __forceinline__ FillOut fill_group(const gsnapdp_window* __restrict__
 #endif
     if (act) {
 #pragma unroll
-      for (int s = 1; s < S - 1; s++) cell(s, H[s + 1], E[s + 1]);
+      for (int s = 1; s < S - 1; s++) cell(s, GOPEN ? G[s + 1] : H[s + 1], E[s + 1]);
       cell(S - 1, hb, eb);
       if constexpr (END == 1) Bt = max(Bt, bstep + Rc);
       if constexpr (END == 2) Bt = max(Bt, (bstep << END_RANK_BITS) + Rc);
