@@ -35,12 +35,18 @@ int gsnapdp__ggap_lds_check(size_t max_lds);   // gsnapdp_ggap.hip's kernels
 int gsnapdp__gband_lds_check(size_t max_lds);  // k_gband
 int gsnapdp__micro_lds_check(size_t max_lds);  // k_micro
 int gsnapdp__gather_lds_check(size_t max_lds); // k_compact
+int gsnapdp__gwin_lds_check(size_t max_lds);   // k_gwin
 // k_gband over the register-band lists of a genome-gap batch (gsnapdp_gband.hip)
 int gsnapdp__gband_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_ggap_window* d_windows,
                           const int* lists, const int* counts, int list_cap, const char* d_query,
                           const char* d_query_uc, gsnapdp_ggap_result* d_results,
                           gsnapdp_ggap_trace* d_traces, uint32_t* d_ops, const int64_t* d_op_offsets,
                           int use_band);
+// k_gwin over the window-per-lane list of a genome-gap batch (gsnapdp_gwin.hip)
+int gsnapdp__gwin_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_ggap_window* d_windows,
+                         const int* lists, const int* counts, int list_cap, const char* d_query,
+                         const char* d_query_uc, gsnapdp_ggap_result* d_results, gsnapdp_ggap_trace* d_traces,
+                         uint32_t* d_ops, const int64_t* d_op_offsets);
 
 #define HIPCHK(x)                                                                        \
   do {                                                                                   \
@@ -95,6 +101,10 @@ struct gsnapdp_ctx {
   uint32_t* d_ggap_pool = nullptr; // global scratch of the large-window path
   uint32_t* d_gband_pool = nullptr; // per-wave scratch of the register-band path (k_gband), score mode
   uint32_t* d_gband_pool_prob = nullptr;  // the same with probability mode's part (first use)
+  uint32_t* d_gwin_pool = nullptr;  // per-wave scratch of k_gwin (first use)
+  double* d_gwin_probs = nullptr;   // k_gwin_probs' site probabilities, 64 per list window
+  size_t gwin_probs_cap = 0;
+  int gwin_on = 1;                  // probability-mode windows on k_gwin (GSNAPDP_GWIN=0: off)
   int ggap_rowlane_only = 0;        // GSNAPDP_GGAP_ROWLANE=1: every window on k_ggap (A/B tests)
   int ggap_use_band = 1;            // k_ggap_plan's GB_USE_* bits (GSNAPDP_GBAND_PROB=1 sets the prob bit)
   int gband_min = 16384;            // smallest genome-gap batch on the register band (GSNAPDP_GBAND_MIN)

@@ -120,9 +120,16 @@ __device__ inline uint32_t row_match_mask(const uint32_t* __restrict__ prof, int
 // are taken four cells at a time: the cells (r-k, c-k), k = 0..3, share the
 // diagonal, so they are in the band when r, c >= 4, and their eight loads are
 // independent.
-template <class Dirs, class Col, class QMask>
+// `score` (optional) is told every step of the path: diag(r, c) for a nogap
+// cell and gap(dist) for a gap of dist cells, so a caller can total the path's
+// score (the DP value of the start cell: every path ends at (0, 0) with 0).
+struct NoScore {
+  __device__ inline void diag(int, int) const {}
+  __device__ inline void gap(int) const {}
+};
+template <class Dirs, class Col, class QMask, class Score = NoScore>
 __device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c, const QMask& qmask,
-                                 const Col& colcls, Tally& t, OpWriter& ow) {
+                                 const Col& colcls, Tally& t, OpWriter& ow, Score&& score = Score()) {
   const int lband = L.d.lband, rband = L.d.rband;
   auto inband = [&](int rr, int cc) {
     const int d = rr - cc + rband;
@@ -139,6 +146,7 @@ __device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c, 
     return (dirs(rr, cc) >> 1) & 1u;
   };
   auto count = [&](int rr, int cc) {  // the nogap cell (rr, cc): one pair unless the genome is '*'
+    score.diag(rr, cc);
     const int g = colcls(cc);
     if (g != 5) {
       const int m = (int)((qmask(rr) >> g) & 1u);
@@ -176,6 +184,7 @@ __device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c, 
         r--;
       }
       r--;
+      score.gap(dist);
       ow.flush();
       ow.put(GSNAPDP_OP(GSNAPDP_OP_VSKIP, dist));
       t.npush += dist;
@@ -202,6 +211,7 @@ __device__ inline void traceback(const Dirs& dirs, const Lane& L, int r, int c, 
         const int r2 = colcls(rv ? cl + 1 : cr - 1), r1 = colcls(rv ? cl : cr);
         dashes = intron_type_codes(l1, l2, r2, r1, L.cdna_direction) == 0;
       }
+      score.gap(dist);
       ow.flush();
       ow.put(GSNAPDP_OP(dashes ? GSNAPDP_OP_HDASH : GSNAPDP_OP_HGAP, dist));
       t.npush += dashes ? dist : 1;

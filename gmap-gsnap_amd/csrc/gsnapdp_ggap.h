@@ -242,7 +242,15 @@ __device__ inline Lane side_lane(const gsnapdp_ggap_window& w, const GGeo& G, in
 constexpr int GB_L2MAX = 256;            // longest flank on the register band
 constexpr int GB_LIST0 = 3;
 constexpr int GP_LIST0 = GB_LIST0 + 2 * (NCLASS - 1);
-constexpr int GG_NLISTS = GP_LIST0 + 2 * (NCLASS - 1);
+// k_gwin (gsnapdp_gwin.hip): probability-mode windows with one window per lane
+constexpr int GW_LIST = GP_LIST0 + 2 * (NCLASS - 1);
+constexpr int GG_NLISTS = GW_LIST + 1;
+constexpr int GW_WMAX = 24;   // widest band of either flank
+// the band shapes k_gwin is built for: width 2 * extraband + 9 with extraband
+// 7 and 3 (GMAP's length2 = length1 + 8, stage3.c:5793); both flanks alike
+constexpr int GW_CLASSES = 2, GW_W0 = 23, GW_LB0 = 7, GW_W1 = 15, GW_LB1 = 3;
+constexpr int GW_L1MAX = 24;  // rows
+constexpr int GW_L2MAX = 32;  // columns of a flank (their probability ranks fit bits 0..30)
 #ifndef GB_WAVES_PER_SIMD
 #define GB_WAVES_PER_SIMD 2  // k_gband (256 VGPRs): C4 score 0.65 ms; 3 waves 0.70, 4 waves 0.95 (spills)
 #endif
@@ -253,8 +261,8 @@ constexpr int GG_NLISTS = GP_LIST0 + 2 * (NCLASS - 1);
 constexpr int GB_WAVE_DW = 2 * (GB_L2MAX + 4) * 80 + 2 * 32 * ((GB_L2MAX + 4) / 4 + 1) +
                            3 * 2 * 32 * (GB_L2MAX + 4) + 2 * (GB_L2MAX + 4) * 256 + 2 * 32 * (GB_L2MAX + 4) * 2 +
                            2 * 32 * (GB_L2MAX + 4) * 4;
-// use_band bits of k_ggap_plan
-enum { GB_USE_SCORE = 1, GB_USE_PROB = 2 };
+// use_band bits of k_ggap_plan (GW_USE: probability-mode windows on k_gwin)
+enum { GB_USE_SCORE = 1, GB_USE_PROB = 2, GW_USE = 4 };
 
 // The register-band list of a window that reached the fills, or -1 for k_ggap:
 // no constrained known-intron bridge, both flanks at least length1 long (so the
@@ -271,6 +279,21 @@ __device__ inline int gband_list(const gsnapdp_ggap_window& w, const GGeo& G, in
   if (span - G.L1 - 1 < (G.rbL > G.rbR ? G.rbL : G.rbR)) return -1;
   const int k = class_of_w(W);
   return (w.use_probabilities_p ? GP_LIST0 : GB_LIST0) + 2 * (k > 0 ? k - 1 : 0) + (w.jump_late_p ? 1 : 0);
+}
+
+// A window k_gwin takes (its fills and bridge assume all of this): probability
+// mode without a splicing IIT, both flanks at least length1 long (the bridge's
+// band is then the fill band, :3716-3760) and at most GW_L2MAX, band widths
+// <= GW_WMAX, length1 <= GW_L1MAX, and an intron span that never cuts the
+// bridge's columns (cL < span - rR, cR < span - rL; :3720, :3760).
+__device__ inline bool gwin_ok(const gsnapdp_ggap_window& w, const GGeo& G) {
+  if (!w.use_probabilities_p || w.known_mode != GSNAPDP_KNOWN_NONE) return false;
+  if (G.L1 < 2 || G.L1 > GW_L1MAX) return false;
+  if (G.L2L < G.L1 || G.L2R < G.L1 || G.L2L > GW_L2MAX || G.L2R > GW_L2MAX) return false;
+  if (G.WL != G.WR || G.lbL != G.lbR) return false;
+  if (!((G.WL == GW_W0 && G.lbL == GW_LB0) || (G.WL == GW_W1 && G.lbL == GW_LB1))) return false;
+  const int span = w.revoffset2R - w.offset2L;
+  return span - G.L1 - 1 >= (G.rbL > G.rbR ? G.rbL : G.rbR);
 }
 
 }  // namespace gsnapdp

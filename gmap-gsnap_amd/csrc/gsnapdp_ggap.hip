@@ -914,7 +914,7 @@ __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
       X.status = ST_UNSUPPORTED;
     } else {
       done = false;
-      cls = gband_list(w, G, use_band);  // the register band (k_gband) when it can
+      cls = (use_band & GW_USE) && gwin_ok(w, G) ? GW_LIST : gband_list(w, G, use_band);  // k_gwin / k_gband when they can
       const int bndw = G.L1 + 1 > 64 ? 3 * (max(G.L2L, G.L2R) + 2) : 0;  // stripe boundary row
       if (cls >= 0) {
       } else if (G.L1 + 1 <= 32 && G.words <= GG_SMALL_WORDS) cls = GG_SMALL;
@@ -1448,14 +1448,23 @@ extern "C" int gsnapdp_ggap_run_device(gsnapdp_ctx* ctx, const gsnapdp_ggap_wind
   const int cap = ctx->ggap_cap;
   HIPCHK(hipMemsetAsync(counts, 0, 4 * GG_NLISTS, st));
   gsnapdp__mark(ctx, st, 4, 0);
-  const int use_band = n >= ctx->gband_min ? ctx->ggap_use_band : 0;
+  // k_gwin takes probability-mode windows whenever the MaxEnt tables are loaded
+  // (GSNAPDP_GWIN=0: k_ggap / k_gband as before, for A/B tests)
+  const int use_gwin = ctx->gwin_on && ctx->d_tables && !ctx->ggap_rowlane_only ? GW_USE : 0;
+  const int use_band = (n >= ctx->gband_min ? ctx->ggap_use_band : 0) | use_gwin;
   hipLaunchKernelGGL(k_ggap_plan, dim3((n + 255) / 256), dim3(256), 0, st, d_windows, n,
                      d_results, d_traces, lists, counts, cap, use_band);
   gsnapdp__mark(ctx, st, 4, 1);
   gsnapdp__mark(ctx, st, 6, 0);
-  if (use_band && gsnapdp__gband_launch(ctx, st, d_windows, lists, counts, cap, d_query, d_query_uc, d_results,
-                                        d_traces, d_ops, d_op_offsets, use_band))
+  if ((use_band & (GB_USE_SCORE | GB_USE_PROB)) &&
+      gsnapdp__gband_launch(ctx, st, d_windows, lists, counts, cap, d_query, d_query_uc, d_results, d_traces,
+                            d_ops, d_op_offsets, use_band))
     return -1;
+  gsnapdp__mark(ctx, st, 8, 0);
+  if (use_gwin && gsnapdp__gwin_launch(ctx, st, d_windows, lists, counts, cap, d_query, d_query_uc, d_results,
+                                       d_traces, d_ops, d_op_offsets))
+    return -1;
+  gsnapdp__mark(ctx, st, 8, 1);
   gsnapdp__mark(ctx, st, 6, 1);
   gsnapdp__mark(ctx, st, 5, 0);
   // small windows: 4 waves x 2 windows per block, as many blocks per CU as LDS holds

@@ -1392,7 +1392,7 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
       return fail("max LDS", e);
     if (kernels_lds_check((size_t)max_lds) || gsnapdp__ggap_lds_check((size_t)max_lds) ||
         gsnapdp__gband_lds_check((size_t)max_lds) || gsnapdp__micro_lds_check((size_t)max_lds) ||
-        gsnapdp__gather_lds_check((size_t)max_lds)) {
+        gsnapdp__gather_lds_check((size_t)max_lds) || gsnapdp__gwin_lds_check((size_t)max_lds)) {
       delete ctx;
       return nullptr;
     }
@@ -1400,6 +1400,8 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
   {
     const char* e = getenv("GSNAPDP_GGAP_ROWLANE");
     ctx->ggap_rowlane_only = (e && e[0] == '1') ? 1 : 0;
+    const char* gwe = getenv("GSNAPDP_GWIN");  // 0: probability-mode windows off k_gwin (A/B tests)
+    ctx->gwin_on = (gwe && gwe[0] == '0') ? 0 : 1;
     // GSNAPDP_GBAND_PROB=1: probability-mode windows on k_gband too (A/B tests;
     // off by default until it beats k_ggap, DESIGN.md §4 k_gband)
     const char* p = getenv("GSNAPDP_GBAND_PROB");
@@ -1464,6 +1466,8 @@ extern "C" void gsnapdp_destroy(gsnapdp_ctx* ctx) {
   (void)hipFree(ctx->d_ggap_pool);
   (void)hipFree(ctx->d_gband_pool);
   (void)hipFree(ctx->d_gband_pool_prob);
+  (void)hipFree(ctx->d_gwin_pool);
+  (void)hipFree(ctx->d_gwin_probs);
   (void)hipFree(ctx->d_ggap_stage);
   (void)hipFree(ctx->d_sj_win);
   (void)hipFree(ctx->d_stage);
@@ -1751,7 +1755,7 @@ void gsnapdp__mark(gsnapdp_ctx* ctx, hipStream_t st, int stage, int end) {
 }
 
 static const char* const kStageNames[] = {"k_plan", "k_scan+k_scatter", "k_fill", "k_rows",
-                                          "k_ggap_plan", "k_ggap", "k_gband", "k_count"};
+                                          "k_ggap_plan", "k_ggap", "k_gband", "k_count", "k_gwin"};
 static const int kNStages = (int)(sizeof(kStageNames) / sizeof(kStageNames[0]));
 
 extern "C" const char* gsnapdp_stage_name(int stage) {

@@ -6,7 +6,7 @@ set -e
 NAME=$1; shift
 SRC=${SRC:-kernels}
 cd "$(dirname "$0")/../gmap-gsnap_amd"
-REST="lib/gsnapdp_micro.o lib/gsnapdp_gather.o lib/gsnapdp_host.o lib/gsnapdp_stage3.o lib/gsnapdp_stage3_exec.o lib/gsnapdp_stage3_compute.o lib/gsnapdp_iit.o lib/gsnapdp_scan.o"
+REST="lib/gsnapdp_micro.o lib/gsnapdp_gather.o lib/gsnapdp_gwin.o lib/gsnapdp_host.o lib/gsnapdp_stage3.o lib/gsnapdp_stage3_exec.o lib/gsnapdp_stage3_compute.o lib/gsnapdp_iit.o lib/gsnapdp_scan.o"
 O=../gpuexp/$NAME; mkdir -p $O
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function "$@" \
   -c csrc/gsnapdp_$SRC.hip -o $O/gsnapdp_$SRC.o
