@@ -389,6 +389,9 @@ __device__ inline uint32_t kmer_sel(uint32_t w0, uint32_t w1, uint32_t w2, uint3
   const uint32_t hi = i == 0 ? w1 : i == 1 ? w2 : i == 2 ? w3 : 0u;
   return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)(bit & 31));
 }
+template <int N, class Seq>
+__device__ inline void maxent_probs_of(int m, Seq&& seq, const bool (&v)[N], const double* __restrict__ T,
+                                       double (&out)[N]);
 template <int N>
 __device__ inline void maxent_probs(int m, const uint32_t (&sp)[N], const bool (&ok)[N], uint32_t co,
                                     const uint32_t* __restrict__ blocks, uint64_t nwords,
@@ -410,6 +413,14 @@ __device__ inline void maxent_probs(int m, const uint32_t (&sp)[N], const bool (
     b0[i] = 2 * (int)(start & 31u);
   }
   auto seq = [&](int i, int off) { return kmer_sel(w0[i], w1[i], w2[i], w3[i], b0[i] + 2 * off); };
+  maxent_probs_of<N>(m, seq, v, T, out);
+}
+
+// the table part of maxent_probs: seq(i, off) = the 16-mer `off` nt past site
+// i's start (startpos - margin); v[i] false: out[i] = 0.0
+template <int N, class Seq>
+__device__ inline void maxent_probs_of(int m, Seq&& seq, const bool (&v)[N], const double* __restrict__ T,
+                                       double (&out)[N]) {
   const double* donor_p = T;
   const double* donor_di_p = donor_p + 16384;
   const double* acc1_p = donor_di_p + 16;

@@ -90,9 +90,7 @@ enum {
   GS_INVR = GS_INVL + 32,             // right
   GS_PL = GS_INVR + 32,               // direction planes, left: 3 dwords per row
   GS_PR = GS_PL + 3 * (GW_L1MAX + 1), // right
-  GS_PROBL = GS_PR + 3 * (GW_L1MAX + 1),  // site probabilities (double), left, c = 0..31
-  GS_PROBR = GS_PROBL + 2 * 32,
-  GS_SPL = GS_PROBR + 2 * 32,         // the same by rank (double), left
+  GS_SPL = GS_PR + 3 * (GW_L1MAX + 1),  // site probabilities by rank (double), left
   GS_SPR = GS_SPL + 2 * 32,
   GS_SL = GS_SPR + 2 * 32,            // a row's best candidate: probL + probR (double), left loop by rL
   GS_SR = GS_SL + 2 * (GW_L1MAX + 1), // right loop by rR
@@ -164,7 +162,7 @@ struct Scr {  // the wave's scratch: [index][lane] dwords / doubles
 };
 
 template <int W, int LB, int JL, int MODE>
-__device__ __forceinline__ void gw_fill(int L1max, int L1, int L2, int open, int thr, const Scr& sc_,
+__device__ __forceinline__ void gw_fill(int L1max, int L1, int L2, int open, int thr, const Scr& sc_, const Scr& po_,
                                         const AS_LDS uint8_t* lw, const FillIO& io, const uint32_t (&rwd)[5]) {
   const AS_LDS uint8_t* lA = lw + io.A;
   const AS_LDS uint8_t* lB = lw + io.B;
@@ -196,7 +194,7 @@ __device__ __forceinline__ void gw_fill(int L1max, int L1, int L2, int open, int
   if constexpr (MODE == 1) {
     Dn = (int)sc_.u(io.Din, other(1));
     cn = lCo[(size_t)(other(1) + lband) * 64];
-    pOn = sc_.d(io.PO, other(1));
+    pOn = po_.d(io.PO, other(1));
   }
   // the previous row's best candidate, finished a row later (its loads in flight meanwhile)
   int rp = 0, ip = 31, jp = 31;
@@ -222,7 +220,7 @@ __device__ __forceinline__ void gw_fill(int L1max, int L1, int L2, int open, int
       pOc = pOn;
       Dn = (int)sc_.u(io.Din, other(r + 1));
       cn = lCo[(size_t)(other(r + 1) + lband) * 64];
-      pOn = sc_.d(io.PO, other(r + 1));
+      pOn = po_.d(io.PO, other(r + 1));
     }
     const AS_LDS uint8_t* a = lA + (size_t)r * 64;
     const AS_LDS uint8_t* b = lB + (size_t)r * 64;
@@ -410,35 +408,48 @@ __device__ __forceinline__ void gw_traceback(const AS_GLOBAL uint32_t* planes, i
 // gstep * (c - 1); the flank's positions are consecutive, so two packed blocks
 // hold them all (one load batch instead of a chain per column).  Column 0 and
 // the columns past L2 are '*'.
-__device__ inline void flank_classes(const uint32_t* __restrict__ blocks, uint64_t nwords, const Lane& L, int g0,
-                                     int gstep, int L2, int (&cls)[GW_L2MAX + 3]) {
-  auto posof = [&](int gp) -> uint32_t {
-    return L.watson ? (L.base + (uint32_t)gp) : (L.base + (uint32_t)(L.glen - 1) - (uint32_t)gp);
-  };
-  const uint32_t pa = posof(g0), pb = posof(g0 + gstep * (L2 - 1));
+struct FlankBlk {
+  uint32_t h0, l0, f0, h1, l1, f1;
+  uint32_t b0;
+  bool ok0, ok1, wrap;
+};
+__device__ inline uint32_t flank_pos(const Lane& L, int gp) {
+  return L.watson ? (L.base + (uint32_t)gp) : (L.base + (uint32_t)(L.glen - 1) - (uint32_t)gp);
+}
+__device__ inline FlankBlk flank_load(const uint32_t* __restrict__ blocks, uint64_t nwords, const Lane& L, int g0,
+                                      int gstep, int L2) {
+  FlankBlk f;
+  const uint32_t pa = flank_pos(L, g0), pb = flank_pos(L, g0 + gstep * (L2 - 1));
   const uint32_t lo = pa < pb ? pa : pb, hi = pa < pb ? pb : pa;
-  if (hi - lo != (uint32_t)(L2 - 1)) {  // (positions wrap around 2^32: column by column)
+  f.wrap = hi - lo != (uint32_t)(L2 - 1);  // (positions wrap around 2^32: column by column)
+  const uint64_t b0 = lo >> 5;
+  f.b0 = (uint32_t)b0;
+  f.ok0 = b0 * 3u + 2u < nwords;
+  f.ok1 = (b0 + 1u) * 3u + 2u < nwords;
+  const uint64_t p0 = f.ok0 ? b0 * 3u : 0u, p1 = f.ok1 ? (b0 + 1u) * 3u : 0u;
+  f.h0 = blocks[p0], f.l0 = blocks[p0 + 1], f.f0 = blocks[p0 + 2];
+  f.h1 = blocks[p1], f.l1 = blocks[p1 + 1], f.f1 = blocks[p1 + 2];
+  return f;
+}
+__device__ inline void flank_classes(const FlankBlk& f, const uint32_t* __restrict__ blocks, uint64_t nwords,
+                                     const Lane& L, int g0, int gstep, int L2, int (&cls)[GW_L2MAX + 3]) {
+  if (f.wrap) {
 #pragma unroll
     for (int c = 0; c < GW_L2MAX + 3; c++) cls[c] = (c >= 1 && c <= L2) ? gclass(blocks, nwords, L, g0 + gstep * (c - 1)) : 5;
     return;
   }
-  const uint64_t b0 = lo >> 5;
-  const bool ok0 = b0 * 3u + 2u < nwords, ok1 = (b0 + 1u) * 3u + 2u < nwords;
-  const uint64_t p0 = ok0 ? b0 * 3u : 0u, p1 = ok1 ? (b0 + 1u) * 3u : 0u;
-  const uint32_t h0 = blocks[p0], l0 = blocks[p0 + 1], f0 = blocks[p0 + 2];
-  const uint32_t h1 = blocks[p1], l1 = blocks[p1 + 1], f1 = blocks[p1 + 2];
   cls[0] = 5;
 #pragma unroll
   for (int c = 1; c < GW_L2MAX + 3; c++) {
     const int gp = g0 + gstep * (c - 1);
-    const uint32_t pos = posof(gp);
-    const bool second = (pos >> 5) != (uint32_t)b0;
+    const uint32_t pos = flank_pos(L, gp);
+    const bool second = (pos >> 5) != f.b0;
     const uint32_t bit = pos & 31u;
-    const uint32_t fl = second ? f1 : f0;
-    const uint32_t word = bit < 16 ? (second ? l1 : l0) : (second ? h1 : h0);
+    const uint32_t fl = second ? f.f1 : f.f0;
+    const uint32_t word = bit < 16 ? (second ? f.l1 : f.l0) : (second ? f.h1 : f.h0);
     const int code = (int)((word >> ((bit & 15u) * 2u)) & 3u);
     int k = L.watson ? code : 3 - code;
-    if (!(second ? ok1 : ok0) || ((fl >> bit) & 1u)) k = 4;  // outside the genome / N
+    if (!(second ? f.ok1 : f.ok0) || ((fl >> bit) & 1u)) k = 4;  // outside the genome / N
     if (gp < 0 || gp >= L.glen || L.allstar) k = 5;
     cls[c] = c <= L2 ? k : 5;
   }
@@ -468,6 +479,51 @@ __global__ __launch_bounds__(256) void k_gwin_probs(const gsnapdp_ggap_window* _
     int m, step;
     uint32_t sp0;
     site_line(w, side, m, sp0, step);
+    const uint32_t margin = (m == 0) ? 3u : (m == 1) ? 20u : (m == 2) ? 6u : 3u;
+    const uint32_t spmin = step > 0 ? sp0 : sp0 - (uint32_t)(GW_L2MAX - 1);
+    if (step > 0 ? sp0 <= 0xFFFFFFFFu - (GW_L2MAX - 1) && sp0 >= margin : sp0 >= (GW_L2MAX - 1) + margin) {
+      // the columns' sites are consecutive genome positions (no uint32 wrap):
+      // the three blocks under all of them are loaded once, and each site's
+      // 16-mers are constant funnel shifts of that span (site c starts c, or
+      // 31 - c for a descending line, nt past the lowest start s0)
+      const uint32_t s0 = spmin - margin;
+      const uint64_t blk = (uint64_t)(s0 >> 5) * 3u;
+      uint32_t wv[6];
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        wv[2 * j] = blk + 3 * j + 1 < nwords ? blocks[blk + 3 * j + 1] : 0u;  // low
+        wv[2 * j + 1] = blk + 3 * j < nwords ? blocks[blk + 3 * j] : 0u;      // high
+      }
+      const uint32_t sh = (s0 & 31u) * 2u, b = sh & 31u;
+      const bool i0 = sh >= 32u;
+      uint32_t x[5];
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        x[j] = __builtin_amdgcn_alignbit(i0 ? wv[j + 2] : wv[j + 1], i0 ? wv[j + 1] : wv[j], b);
+      x[4] = 0u;
+      const bool up = step > 0;
+#pragma unroll
+      for (int c0 = 0; c0 < GW_L2MAX; c0 += 8) {
+        bool v[8];
+        double o[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const uint32_t sp = sp0 + (uint32_t)(step * (c0 + j));
+          const uint64_t ptr = (uint64_t)((sp - margin) >> 5) * 3u;
+          v[j] = c0 + j < L2 - 1 && sp >= w.chroffset + margin && ptr + 4 < nwords;
+        }
+        auto seq = [&](int j, int off) -> uint32_t {
+          const int bf = 2 * (c0 + j + off), br = 2 * (GW_L2MAX - 1 - (c0 + j) + off);
+          const uint32_t kf = __builtin_amdgcn_alignbit(x[(bf >> 5) + 1], x[bf >> 5], (uint32_t)(bf & 31));
+          const uint32_t kr = __builtin_amdgcn_alignbit(x[(br >> 5) + 1], x[br >> 5], (uint32_t)(br & 31));
+          return up ? kf : kr;
+        };
+        maxent_probs_of<8>(m, seq, v, tables, o);
+#pragma unroll
+        for (int j = 0; j < 8; j++) out[(c0 + j) * 64] = o[j];
+      }
+      continue;
+    }
 #pragma unroll
     for (int c0 = 0; c0 < GW_L2MAX; c0 += 8) {
       uint32_t sp[8];
@@ -506,14 +562,14 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
   // the wave's scratch from a wave-uniform base (SGPRs) and the lane
   const Scr SC = {(AS_GLOBAL uint32_t*)pool + (size_t)__builtin_amdgcn_readfirstlane(gw) * GW_WAVE_DW, lane};
   auto S32 = [&](int region, int i) -> AS_GLOBAL uint32_t* { return &SC.u(region, i); };
-  auto PL = [&](int c) -> double { return SC.d(GS_PROBL, c); };
-  auto PR = [&](int c) -> double { return SC.d(GS_PROBR, c); };
   const int n = *count;
 #ifdef GW_PROF
   uint64_t gw_acc[16] = {};
 #endif
   for (int base = gw * 64; base < n; base += nw * 64) {
     const int k0 = base + lane;
+    // the chunk's site probabilities (k_gwin_probs): [side][column][lane] doubles
+    AS_GLOBAL uint32_t* const PB_base = (AS_GLOBAL uint32_t*)(probs + (size_t)(base >> 6) * 4096);
     const bool valid = k0 < n;
     const int wi = list[valid ? k0 : base];
     int key, L1v;
@@ -543,62 +599,96 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
       // stay live through the fills; the outcome re-reads the window record)
       int ws = wi;
       asm volatile("" : "+v"(ws));
+      // (the setup's scratch addresses from a laundered lane: invariant across
+      // tasks, they would otherwise be hoisted out of the task loop and spilled)
+      int lane1 = lane;
+      asm volatile("" : "+v"(lane1));
+      const Scr SC1 = {SC.b, lane1};
       const gsnapdp_ggap_window w = Wn[ws];
       const GGeo G = gg_geo(w);
       const int L1 = G.L1, L2L = G.L2L, L2R = G.L2R, open = G.open, thr = w.score_threshold;
       uint32_t rwL[5], rwR[5];
       {
       const Lane LL = side_lane(w, G, 0), LR = side_lane(w, G, 1);
-      const uint32_t* ptab = prof + G.mt * 128;
+      // every load the record alone addresses goes out at once, with no branch
+      // between them (a dependent global round trip under load is thousands of
+      // cycles): the query rows, both flanks' genome blocks, the left flank's
+      // site probabilities; then the rows' profile words
+      uint32_t qc[GW_L1MAX], uc[GW_L1MAX];
 #pragma unroll
-      for (int r = 1; r <= GW_L1MAX; r++) {  // (unrolled: every row's loads in flight at once)
-        const int qi = (int)w.qpos + min(r, L1) - 1;
-        const uint32_t rk = ptab[(unsigned char)q[qi] & 127u];
-        const uint32_t qm = row_match_mask(prof, G.mt, (unsigned char)q[qi], (unsigned char)qu[qi]);
-        if (r <= L1) {
-          *S32(GS_RW, r) = rk;
-          *S32(GS_QB, r - 1) = qm;
+      for (int i = 0; i < GW_L1MAX; i++) {
+        const int qi = (int)w.qpos + min(i + 1, L1) - 1;
+        qc[i] = (unsigned char)q[qi];
+        uc[i] = (unsigned char)qu[qi];
+      }
+      const FlankBlk fbL = flank_load(blocks, nwords, LL, w.offset2L, 1, L2L);
+      const FlankBlk fbR = flank_load(blocks, nwords, LR, w.revoffset2R, -1, L2R);
+      const Scr PB = {PB_base, lane1};
+      {
+        const uint32_t* ptab = prof + G.mt * 128;
+        uint32_t rk[GW_L1MAX], ub[GW_L1MAX];
+#pragma unroll
+        for (int i = 0; i < GW_L1MAX; i++) {
+          rk[i] = ptab[qc[i] & 127u];
+          ub[i] = prof[4 * 128 + (uc[i] & 127u)];
+        }
+        // rows past L1 get row L1's words (never read)
+#pragma unroll
+        for (int i = 0; i < GW_L1MAX; i++) {
+          SC1.u(GS_RW, i + 1) = rk[i];
+          SC1.u(GS_QB, i) = ((rk[i] | (uc[i] < 128u ? ub[i] : 0u)) >> 24) & 31u;  // row_match_mask
         }
       }
+#pragma unroll
       for (int side = 0; side < 2; side++) {
         const int L2 = side ? G.L2R : G.L2L;
-        const Lane& LF = side ? LR : LL;
         AS_LDS uint8_t* lA = side ? lAR : lAL;
         AS_LDS uint8_t* lB = side ? lBR : lBL;
         AS_LDS uint8_t* lC = side ? lCR : lCL;
-        const int PRG = side ? GS_PROBR : GS_PROBL;
         // classes of columns 0 .. 33 (0 and past L2: '*', never read as such)
         int cls[GW_L2MAX + 3];
-        flank_classes(blocks, nwords, LF, side ? w.revoffset2R : w.offset2L, side ? -1 : 1, L2, cls);
+        const Lane& LF = side ? LR : LL;
+        FlankBlk fb;
+        fb.h0 = side ? fbR.h0 : fbL.h0;
+        fb.l0 = side ? fbR.l0 : fbL.l0;
+        fb.f0 = side ? fbR.f0 : fbL.f0;
+        fb.h1 = side ? fbR.h1 : fbL.h1;
+        fb.l1 = side ? fbR.l1 : fbL.l1;
+        fb.f1 = side ? fbR.f1 : fbL.f1;
+        fb.b0 = side ? fbR.b0 : fbL.b0;
+        fb.ok0 = side ? fbR.ok0 : fbL.ok0;
+        fb.ok1 = side ? fbR.ok1 : fbL.ok1;
+        fb.wrap = side ? fbR.wrap : fbL.wrap;
+        flank_classes(fb, blocks, nwords, LF, side ? w.revoffset2R : w.offset2L, side ? -1 : 1, L2, cls);
         GW_T(14, tp);
         // A[c + eb] = 4 x class ('*' outside 1..L2); B, C: no candidate, no term
-        for (int i = 0; i < GW_NC; i++) {
+        for (int i = 0; i <= eb; i++) {
           lA[i * 64] = (uint8_t)(4 * 5);
           lB[i * 64] = (uint8_t)GW_RANK_NONE;
           lC[i * 64] = 0;
         }
-#pragma unroll
-        for (int c = 1; c <= GW_L2MAX; c++) lA[(c + eb) * 64] = (uint8_t)(4 * cls[c]);
-        // leftdi / rightdi (:3331-3373) as 6 x their index, 0 from column L2 - 1 on
-        // (straight to LDS: the classes die here, before the MaxEnt batches)
+        for (int i = eb + GW_L2MAX; i < GW_NC; i++) {
+          lA[i * 64] = (uint8_t)(4 * 5);
+          lB[i * 64] = (uint8_t)GW_RANK_NONE;
+          lC[i * 64] = 0;
+        }
+        lA[(eb + GW_L2MAX) * 64] = (uint8_t)(4 * cls[GW_L2MAX]);
 #pragma unroll
         for (int c = 1; c < GW_L2MAX; c++) {
+          lA[(c + eb) * 64] = (uint8_t)(4 * cls[c]);
+          // leftdi / rightdi (:3331-3373) as 6 x their index, 0 from column L2 - 1 on
           const int d = c < L2 - 1 ? (side ? right_di(cls[c + 2], cls[c + 1]) : left_di(cls[c + 1], cls[c + 2])) : 0;
           lC[(c + eb) * 64] = (uint8_t)(6 * (side ? right_idx(d) : left_idx(d)));
         }
-        // site probabilities of columns 0 .. L2 - 2 (:3856-3903), 0 at L2 - 1:
-        // k_gwin_probs wrote them, [chunk][side][column][lane] (coalesced)
-        GW_T(13, tp);
         double p[GW_L2MAX];
 #pragma unroll
-        for (int c = 0; c < GW_L2MAX; c++) p[c] = probs[(size_t)(base >> 6) * 4096 + side * 2048 + c * 64 + lane];
-#pragma unroll
-        for (int c = 0; c < GW_L2MAX; c++) SC.d(PRG, c) = p[c];
-        GW_T(12, tp);
+        for (int c = 0; c < GW_L2MAX; c++) p[c] = PB.d(side * 64, c);
+        GW_T(13, tp);
         // ranks of the candidate columns 1 .. L2 - 1 by probability (larger
         // first, then the smaller column); RANK_NONE elsewhere.  Every pair is
         // compared once: c < c2 puts c first unless p[c2] > p[c] (the others
-        // carry -1, below every probability, so they rank last).
+        // carry -1, below every probability, so they rank last, ranks L2 .. 30,
+        // whose slots no mask bit reaches).
         const int INVG = side ? GS_INVR : GS_INVL, SPG = side ? GS_SPR : GS_SPL;
         int rank[GW_L2MAX];
 #pragma unroll
@@ -617,13 +707,11 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
           }
 #pragma unroll
         for (int c = 1; c < GW_L2MAX; c++) {
-          const bool cand = c < L2;
-          if (cand) {
-            SC.u(INVG, rank[c]) = (uint32_t)c;
-            SC.d(SPG, rank[c]) = p[c];
-          }
-          lB[(c + eb) * 64] = (uint8_t)(cand ? rank[c] : GW_RANK_NONE);
+          SC1.u(INVG, rank[c]) = (uint32_t)c;
+          SC1.d(SPG, rank[c]) = p[c];
+          lB[(c + eb) * 64] = (uint8_t)(c < L2 ? rank[c] : GW_RANK_NONE);
         }
+        GW_T(12, tp);
       }
       // intron terms (:3148-3192) by dinucleotide index: rwL[ri] for the left
       // loop (keyed by rightdi[rR]), fields by leftdi index; rwR[li] likewise
@@ -643,7 +731,9 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
           rwR[li] |= s << (6 * ri);
         }
       }
+#ifdef GW_PROF
       __builtin_amdgcn_s_waitcnt(0);
+#endif
       GW_T(0, tp);
       // ---- the three fills: right (diagonal only), left, right; the band
       // shape (W, lband) of the wave's windows as template arguments
@@ -651,27 +741,27 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
       // (byte offsets of the LDS arrays from lw: A_L, A_R, B_L, B_R, C_L, C_R)
       const FillIO ioR1 = {GS_RW, GS_DR, 0, 0, 0, 0, 0, 0, 0, 0, 1 * GW_NC * 64, 3 * GW_NC * 64, 5 * GW_NC * 64,
                            4 * GW_NC * 64, 1};
-      const FillIO ioL = {GS_RW, GS_DL, GS_DR, GS_PL, GS_ML, GS_SPL, GS_INVL, GS_PROBR, GS_SL, GS_CL,
+      const FillIO ioL = {GS_RW, GS_DL, GS_DR, GS_PL, GS_ML, GS_SPL, GS_INVL, 64, GS_SL, GS_CL,
                           0, 2 * GW_NC * 64, 4 * GW_NC * 64, 5 * GW_NC * 64, 0};
-      const FillIO ioR2 = {GS_RW, GS_DR, GS_DL, GS_PR, GS_MR, GS_SPR, GS_INVR, GS_PROBL, GS_SR, GS_CR,
+      const FillIO ioR2 = {GS_RW, GS_DR, GS_DL, GS_PR, GS_MR, GS_SPR, GS_INVR, 0, GS_SR, GS_CR,
                            1 * GW_NC * 64, 3 * GW_NC * 64, 5 * GW_NC * 64, 4 * GW_NC * 64, 1};
       auto fills = [&](auto wt, auto lt) {
         constexpr int W = decltype(wt)::value, LB = decltype(lt)::value;
         int lane3 = lane;
         asm volatile("" : "+v"(lane3));
-        const Scr SC = {SO_base, lane3};
+        const Scr SC = {SO_base, lane3}, PO = {PB_base, lane3};
         if (JLL) {
-          gw_fill<W, LB, 0, 0>(L1max, L1, L2R, open, thr, SC, lw, ioR1, rwR);
+          gw_fill<W, LB, 0, 0>(L1max, L1, L2R, open, thr, SC, PO, lw, ioR1, rwR);
           GW_T(4, tp);
-          gw_fill<W, LB, 1, 1>(L1max, L1, L2L, open, thr, SC, lw, ioL, rwL);
+          gw_fill<W, LB, 1, 1>(L1max, L1, L2L, open, thr, SC, PO, lw, ioL, rwL);
           GW_T(5, tp);
-          gw_fill<W, LB, 0, 1>(L1max, L1, L2R, open, thr, SC, lw, ioR2, rwR);
+          gw_fill<W, LB, 0, 1>(L1max, L1, L2R, open, thr, SC, PO, lw, ioR2, rwR);
         } else {
-          gw_fill<W, LB, 1, 0>(L1max, L1, L2R, open, thr, SC, lw, ioR1, rwR);
+          gw_fill<W, LB, 1, 0>(L1max, L1, L2R, open, thr, SC, PO, lw, ioR1, rwR);
           GW_T(4, tp);
-          gw_fill<W, LB, 0, 1>(L1max, L1, L2L, open, thr, SC, lw, ioL, rwL);
+          gw_fill<W, LB, 0, 1>(L1max, L1, L2L, open, thr, SC, PO, lw, ioL, rwL);
           GW_T(5, tp);
-          gw_fill<W, LB, 1, 1>(L1max, L1, L2R, open, thr, SC, lw, ioR2, rwR);
+          gw_fill<W, LB, 1, 1>(L1max, L1, L2R, open, thr, SC, PO, lw, ioR2, rwR);
         }
       };
       static_assert(GW_CLASSES == 2, "k_gwin's band shapes");
@@ -682,6 +772,9 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
       // loop before the right), strict `>` on probL + probR; each row's best of a
       // loop was found by its fill (a row whose next candidate has an equal sum
       // scans its mask here for the smallest such column)
+      const Scr PB = {PB_base, lane};
+      auto PL = [&](int c) -> double { return PB.d(0, c); };
+      auto PR = [&](int c) -> double { return PB.d(64, c); };
       double bestp = 0.0;
       int brL = 0, bcL = 0, bcR = 0;
       auto tie_scan = [&](uint32_t m, int INVG, int SPG, double pO, double S) -> int {

@@ -1,6 +1,7 @@
 """Diagnostics: one C4 genome-gap batch (score or probability mode) through
-the register band (k_gband) or the row-lane kernel (k_ggap), for counter runs.
-usage: python tools/ggap_one.py score|prob band|rowlane [n] [steps]"""
+the register band (k_gband), the row-lane kernel (k_ggap) or, probability
+mode only, the window-per-lane kernel (k_gwin, the default), for counter runs.
+usage: python tools/ggap_one.py score|prob band|rowlane|gwin [n] [steps]"""
 import os
 import sys
 
@@ -12,6 +13,7 @@ mode, path = sys.argv[1], sys.argv[2]
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 200_000
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 3
 os.environ["GSNAPDP_GGAP_ROWLANE"] = "1" if path == "rowlane" else "0"
+os.environ["GSNAPDP_GWIN"] = "1" if path == "gwin" else "0"
 os.environ["GSNAPDP_GBAND_PROB"] = "1"  # probability mode on the band too (band runs)
 from gsnapdp import Context  # noqa: E402
 from gsnapdp import workload as W  # noqa: E402

@@ -11,7 +11,7 @@ import sys
 
 
 def kernel_key(name):
-    for k in ("k_gband", "k_ggap_plan", "k_ggap<32", "k_ggap<64, false", "k_ggap<64, true"):
+    for k in ("k_gwin_probs", "k_gwin", "k_gband", "k_ggap_plan", "k_ggap<32", "k_ggap<64, false", "k_ggap<64, true"):
         if k in name:
             return k
     return None
