@@ -73,9 +73,12 @@ constexpr int GW_EXT = -3;  // SINGLE_EXTEND = PAIRED_EXTEND (dynprog.c:142-293)
 static_assert(SINGLE_EXTEND == GW_EXT && PAIRED_EXTEND == GW_EXT, "one extend penalty");
 constexpr int GW_NC = GW_L1MAX + GW_WMAX;  // column slots per flank in LDS: index c + lband
 constexpr int GW_RANK_NONE = 31;           // rank byte of a column that is never a candidate
-// LDS per wave: [array][index][lane] bytes, arrays A (4 x genome class), B
-// (probability rank), C (6 x dinucleotide index) of the left and right flanks
+// LDS per wave: each flank's columns [index][lane] as u16 words packing A (4 x
+// genome class, bits 0-4), C (6 x dinucleotide index, bits 5-9) and B
+// (probability rank, bits 10-14); then the traceback rows [i][lane] u32
+constexpr int GW_LDS_PL = 0, GW_LDS_PR = 2 * GW_NC * 64, GW_LDS_T = 4 * GW_NC * 64;
 constexpr int GW_LDS_WAVE = 6 * GW_NC * 64;
+constexpr uint32_t GW_COL_NONE = 4 * 5 | (uint32_t)GW_RANK_NONE << 10;  // '*', no term, no candidate
 constexpr int GW_BLOCK = 256;
 constexpr int GW_WAVES_PER_SIMD = 2;
 // global scratch per wave, [index][lane] dwords (uint4 / double as 4 / 2 dwords)
@@ -143,11 +146,11 @@ __device__ inline int right_code(int i) {
 //   RW: row words; Dout / Din: this / the other flank's diagonal values; P, M:
 //   direction planes and pass masks; SP, INV: this flank's probabilities and
 //   columns by rank; PO: the other flank's probabilities by column; S, C: the
-//   row's best candidate; A, B, Cc: this flank's column arrays, CO: the other
-//   flank's dinucleotide indices; rev: rows read the query backwards.
+//   row's best candidate; COL / COLO: this / the other flank's column words
+//   (LDS); rev: rows read the query backwards.
 struct FillIO {
   int RW, Dout, Din, P, M, SP, INV, PO, S, C;
-  int A, B, Cc, CO;
+  int COL, COLO;  // LDS byte offsets of this / the other flank's column words
   int rev;
 };
 struct Scr {  // the wave's scratch: [index][lane] dwords / doubles
@@ -163,11 +166,9 @@ struct Scr {  // the wave's scratch: [index][lane] dwords / doubles
 
 template <int W, int LB, int JL, int MODE>
 __device__ __forceinline__ void gw_fill(int L1max, int L1, int L2, int open, int thr, const Scr& sc_, const Scr& po_,
-                                        const AS_LDS uint8_t* lw, const FillIO& io, const uint32_t (&rwd)[5]) {
-  const AS_LDS uint8_t* lA = lw + io.A;
-  const AS_LDS uint8_t* lB = lw + io.B;
-  const AS_LDS uint8_t* lC = lw + io.Cc;
-  const AS_LDS uint8_t* lCo = lw + io.CO;
+                                        const AS_LDS uint8_t* lwb, const FillIO& io, const uint32_t (&rwd)[5]) {
+  const AS_LDS uint16_t* lP = (const AS_LDS uint16_t*)(lwb + io.COL) + sc_.lane;
+  const AS_LDS uint16_t* lPo = (const AS_LDS uint16_t*)(lwb + io.COLO) + sc_.lane;
   const int rev = io.rev;
   static_assert(W <= GW_WMAX && LB < W, "band shape");
   constexpr int lband = LB;
@@ -193,9 +194,15 @@ __device__ __forceinline__ void gw_fill(int L1max, int L1, int L2, int open, int
   double pOn = 0.0;
   if constexpr (MODE == 1) {
     Dn = (int)sc_.u(io.Din, other(1));
-    cn = lCo[(size_t)(other(1) + lband) * 64];
+    cn = ((uint32_t)lPo[(size_t)(other(1) + lband) * 64] >> 5) & 31u;
     pOn = po_.d(io.PO, other(1));
   }
+  // slot k of row r is column r - lband + k, index r + k: the slots' column
+  // words shift down one slot per row, one new word entering at the top (read
+  // a row ahead: no LDS wait inside the row)
+  uint32_t cv[W];
+#pragma unroll
+  for (int k = 0; k < W; k++) cv[k] = lP[(size_t)(1 + k) * 64];
   // the previous row's best candidate, finished a row later (its loads in flight meanwhile)
   int rp = 0, ip = 31, jp = 31;
   uint32_t cp = 0;
@@ -219,12 +226,10 @@ __device__ __forceinline__ void gw_fill(int L1max, int L1, int L2, int open, int
       rwc = cn == 6 ? rwd[1] : cn == 12 ? rwd[2] : cn == 18 ? rwd[3] : cn == 24 ? rwd[4] : rwd[0];
       pOc = pOn;
       Dn = (int)sc_.u(io.Din, other(r + 1));
-      cn = lCo[(size_t)(other(r + 1) + lband) * 64];
+      cn = ((uint32_t)lPo[(size_t)(other(r + 1) + lband) * 64] >> 5) & 31u;
       pOn = po_.d(io.PO, other(r + 1));
     }
-    const AS_LDS uint8_t* a = lA + (size_t)r * 64;
-    const AS_LDS uint8_t* b = lB + (size_t)r * 64;
-    const AS_LDS uint8_t* cc = lC + (size_t)r * 64;
+    const uint32_t cnext = lP[(size_t)(r + W) * 64];
     int Hl = NEG, El = NEG;  // (r, c-1) of slot 0: outside the band
     uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0, pm = 0;
     int dg = NEG;
@@ -237,7 +242,7 @@ __device__ __forceinline__ void gw_fill(int L1max, int L1, int L2, int open, int
       const int En = max(El, av) + GW_EXT;
       const int Fn = max(Fa, bv) + GW_EXT;
       const int m1 = max(Hd, Ed);
-      const int sc = __builtin_amdgcn_sbfe((int)rkc, (int)a[k * 64], 4);
+      const int sc = __builtin_amdgcn_sbfe((int)rkc, (int)cv[k], 4);  // (offset: bits 0-4, A)
       const int Hn = max(m1, Fd) + sc;
       if constexpr (MODE == 1) {
         // direction signs (recurrences :1519-1561, "x wins ties iff jump_late")
@@ -251,10 +256,10 @@ __device__ __forceinline__ void gw_fill(int L1max, int L1, int L2, int open, int
         p3 = __builtin_amdgcn_alignbit(p3, (uint32_t)dv, 31u);
         // the bridge's test on this cell: H - pen + intron term >= threshold - D
         const uint32_t penraw = JL ? ((uint32_t)(dh & dv) >> 31) : ((uint32_t)(dh | dv) >> 31);
-        const int term = (int)__builtin_amdgcn_ubfe(rwc, (uint32_t)cc[k * 64], 6);
+        const int term = (int)__builtin_amdgcn_ubfe(rwc, cv[k] >> 5, 6);
         const int x = JL ? Hn + term + (int)penraw : Hn + term - (int)penraw;
         const uint32_t ok = (uint32_t)(Tm1 - x) >> 31;
-        pm |= ok << (uint32_t)b[k * 64];
+        pm |= ok << (cv[k] >> 10);
       }
       if (k == lband) dg = Hn;  // the diagonal cell (r, r)
       H[k] = Hn;
@@ -263,6 +268,9 @@ __device__ __forceinline__ void gw_fill(int L1max, int L1, int L2, int open, int
       Hl = Hn;
       El = En;
     }
+#pragma unroll
+    for (int k = 0; k + 1 < W; k++) cv[k] = cv[k + 1];
+    cv[W - 1] = cnext;
     if (r <= L1) {
       sc_.u(io.Dout, r) = (uint32_t)dg;
       if constexpr (MODE == 1) {
@@ -552,13 +560,9 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
   const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int nw = (int)((gridDim.x * blockDim.x) >> 6);
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  AS_LDS uint8_t* lw = (AS_LDS uint8_t*)(gw_lds + (size_t)wv * GW_LDS_WAVE) + lane;
-  AS_LDS uint8_t* lAL = lw;
-  AS_LDS uint8_t* lAR = lw + 1 * GW_NC * 64;
-  AS_LDS uint8_t* lBL = lw + 2 * GW_NC * 64;
-  AS_LDS uint8_t* lBR = lw + 3 * GW_NC * 64;
-  AS_LDS uint8_t* lCL = lw + 4 * GW_NC * 64;
-  AS_LDS uint8_t* lCR = lw + 5 * GW_NC * 64;
+  AS_LDS uint8_t* lwb = (AS_LDS uint8_t*)(gw_lds + (size_t)wv * GW_LDS_WAVE);  // (wave-uniform)
+  AS_LDS uint16_t* lPL = (AS_LDS uint16_t*)(lwb + GW_LDS_PL) + lane;
+  AS_LDS uint16_t* lPR = (AS_LDS uint16_t*)(lwb + GW_LDS_PR) + lane;
   // the wave's scratch from a wave-uniform base (SGPRs) and the lane
   const Scr SC = {(AS_GLOBAL uint32_t*)pool + (size_t)__builtin_amdgcn_readfirstlane(gw) * GW_WAVE_DW, lane};
   auto S32 = [&](int region, int i) -> AS_GLOBAL uint32_t* { return &SC.u(region, i); };
@@ -642,9 +646,7 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
 #pragma unroll
       for (int side = 0; side < 2; side++) {
         const int L2 = side ? G.L2R : G.L2L;
-        AS_LDS uint8_t* lA = side ? lAR : lAL;
-        AS_LDS uint8_t* lB = side ? lBR : lBL;
-        AS_LDS uint8_t* lC = side ? lCR : lCL;
+        AS_LDS uint16_t* lP = side ? lPR : lPL;
         // classes of columns 0 .. 33 (0 and past L2: '*', never read as such)
         int cls[GW_L2MAX + 3];
         const Lane& LF = side ? LR : LL;
@@ -661,24 +663,16 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
         fb.wrap = side ? fbR.wrap : fbL.wrap;
         flank_classes(fb, blocks, nwords, LF, side ? w.revoffset2R : w.offset2L, side ? -1 : 1, L2, cls);
         GW_T(14, tp);
-        // A[c + eb] = 4 x class ('*' outside 1..L2); B, C: no candidate, no term
-        for (int i = 0; i <= eb; i++) {
-          lA[i * 64] = (uint8_t)(4 * 5);
-          lB[i * 64] = (uint8_t)GW_RANK_NONE;
-          lC[i * 64] = 0;
-        }
-        for (int i = eb + GW_L2MAX; i < GW_NC; i++) {
-          lA[i * 64] = (uint8_t)(4 * 5);
-          lB[i * 64] = (uint8_t)GW_RANK_NONE;
-          lC[i * 64] = 0;
-        }
-        lA[(eb + GW_L2MAX) * 64] = (uint8_t)(4 * cls[GW_L2MAX]);
+        // column words at index c + eb: A = 4 x class ('*' outside 1..L2), C =
+        // 6 x the leftdi / rightdi index (:3331-3373; 0 from column L2 - 1 on),
+        // B (below) = the rank; outside columns 1..32 no term, no candidate
+        for (int i = 0; i <= eb; i++) lP[i * 64] = (uint16_t)GW_COL_NONE;
+        for (int i = eb + GW_L2MAX + 1; i < GW_NC; i++) lP[i * 64] = (uint16_t)GW_COL_NONE;
+        uint32_t pk[GW_L2MAX + 1];
 #pragma unroll
-        for (int c = 1; c < GW_L2MAX; c++) {
-          lA[(c + eb) * 64] = (uint8_t)(4 * cls[c]);
-          // leftdi / rightdi (:3331-3373) as 6 x their index, 0 from column L2 - 1 on
+        for (int c = 1; c <= GW_L2MAX; c++) {
           const int d = c < L2 - 1 ? (side ? right_di(cls[c + 2], cls[c + 1]) : left_di(cls[c + 1], cls[c + 2])) : 0;
-          lC[(c + eb) * 64] = (uint8_t)(6 * (side ? right_idx(d) : left_idx(d)));
+          pk[c] = (uint32_t)(4 * cls[c]) | (uint32_t)(6 * (side ? right_idx(d) : left_idx(d))) << 5;
         }
         double p[GW_L2MAX];
 #pragma unroll
@@ -709,8 +703,9 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
         for (int c = 1; c < GW_L2MAX; c++) {
           SC1.u(INVG, rank[c]) = (uint32_t)c;
           SC1.d(SPG, rank[c]) = p[c];
-          lB[(c + eb) * 64] = (uint8_t)(c < L2 ? rank[c] : GW_RANK_NONE);
+          lP[(c + eb) * 64] = (uint16_t)(pk[c] | (uint32_t)(c < L2 ? rank[c] : GW_RANK_NONE) << 10);
         }
+        lP[(GW_L2MAX + eb) * 64] = (uint16_t)(pk[GW_L2MAX] | (uint32_t)GW_RANK_NONE << 10);
         GW_T(12, tp);
       }
       // intron terms (:3148-3192) by dinucleotide index: rwL[ri] for the left
@@ -739,29 +734,28 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
       // shape (W, lband) of the wave's windows as template arguments
       AS_GLOBAL uint32_t* const SO_base = SC.b;
       // (byte offsets of the LDS arrays from lw: A_L, A_R, B_L, B_R, C_L, C_R)
-      const FillIO ioR1 = {GS_RW, GS_DR, 0, 0, 0, 0, 0, 0, 0, 0, 1 * GW_NC * 64, 3 * GW_NC * 64, 5 * GW_NC * 64,
-                           4 * GW_NC * 64, 1};
+      const FillIO ioR1 = {GS_RW, GS_DR, 0, 0, 0, 0, 0, 0, 0, 0, GW_LDS_PR, GW_LDS_PL, 1};
       const FillIO ioL = {GS_RW, GS_DL, GS_DR, GS_PL, GS_ML, GS_SPL, GS_INVL, 64, GS_SL, GS_CL,
-                          0, 2 * GW_NC * 64, 4 * GW_NC * 64, 5 * GW_NC * 64, 0};
+                          GW_LDS_PL, GW_LDS_PR, 0};
       const FillIO ioR2 = {GS_RW, GS_DR, GS_DL, GS_PR, GS_MR, GS_SPR, GS_INVR, 0, GS_SR, GS_CR,
-                           1 * GW_NC * 64, 3 * GW_NC * 64, 5 * GW_NC * 64, 4 * GW_NC * 64, 1};
+                           GW_LDS_PR, GW_LDS_PL, 1};
       auto fills = [&](auto wt, auto lt) {
         constexpr int W = decltype(wt)::value, LB = decltype(lt)::value;
         int lane3 = lane;
         asm volatile("" : "+v"(lane3));
         const Scr SC = {SO_base, lane3}, PO = {PB_base, lane3};
         if (JLL) {
-          gw_fill<W, LB, 0, 0>(L1max, L1, L2R, open, thr, SC, PO, lw, ioR1, rwR);
+          gw_fill<W, LB, 0, 0>(L1max, L1, L2R, open, thr, SC, PO, lwb, ioR1, rwR);
           GW_T(4, tp);
-          gw_fill<W, LB, 1, 1>(L1max, L1, L2L, open, thr, SC, PO, lw, ioL, rwL);
+          gw_fill<W, LB, 1, 1>(L1max, L1, L2L, open, thr, SC, PO, lwb, ioL, rwL);
           GW_T(5, tp);
-          gw_fill<W, LB, 0, 1>(L1max, L1, L2R, open, thr, SC, PO, lw, ioR2, rwR);
+          gw_fill<W, LB, 0, 1>(L1max, L1, L2R, open, thr, SC, PO, lwb, ioR2, rwR);
         } else {
-          gw_fill<W, LB, 1, 0>(L1max, L1, L2R, open, thr, SC, PO, lw, ioR1, rwR);
+          gw_fill<W, LB, 1, 0>(L1max, L1, L2R, open, thr, SC, PO, lwb, ioR1, rwR);
           GW_T(4, tp);
-          gw_fill<W, LB, 0, 1>(L1max, L1, L2L, open, thr, SC, PO, lw, ioL, rwL);
+          gw_fill<W, LB, 0, 1>(L1max, L1, L2L, open, thr, SC, PO, lwb, ioL, rwL);
           GW_T(5, tp);
-          gw_fill<W, LB, 1, 1>(L1max, L1, L2R, open, thr, SC, PO, lw, ioR2, rwR);
+          gw_fill<W, LB, 1, 1>(L1max, L1, L2R, open, thr, SC, PO, lwb, ioR2, rwR);
         }
       };
       static_assert(GW_CLASSES == 2, "k_gwin's band shapes");
@@ -829,8 +823,8 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
       // per query index i, for the tracebacks: the row's score nibbles (bits
       // 0..23, as the fill's profile word) and its match mask (bits 24..28), in
       // LDS over the rank arrays (dead after the fills)
-      AS_LDS uint32_t* lT = (AS_LDS uint32_t*)(lw - lane + 2 * GW_NC * 64) + lane;
-      static_assert(GW_L1MAX * 256 <= 2 * GW_NC * 64, "the traceback rows fit the rank arrays");
+      AS_LDS uint32_t* lT = (AS_LDS uint32_t*)(lwb + GW_LDS_T) + lane;
+      static_assert(GW_LDS_T + GW_L1MAX * 256 <= GW_LDS_WAVE, "the traceback rows fit");
       // (scratch addresses from a laundered lane: recomputed here, not kept live
       // or spilled from the setup's identical ones; all rows' loads at once)
       int lane2 = lane;
@@ -866,7 +860,7 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
       struct PathScore {  // the traceback path's score = the start cell's H
         int s;
         const AS_LDS uint32_t* rw;  // lT: query index i
-        const AS_LDS uint8_t* la;
+        const AS_LDS uint16_t* la;  // the flank's column words (A: bits 0-4)
         int L1, eb, rev, open;
         __device__ inline void diag(int r, int c) {
           const uint32_t rk = rw[(size_t)(rev ? L1 - r : r - 1) * 64];
@@ -889,14 +883,15 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
         // by the compiler through pointers to their writers, kept in scratch)
         for (int f = 0; f < 2; f++) {
           const bool right = f == 0;
-          PathScore ps = {0, lT, right ? lAR : lAL, L1, eb, right ? 1 : 0, wopen};
+          PathScore ps = {0, lT, right ? lPR : lPL, L1, eb, right ? 1 : 0, wopen};
           int pen = 0;
           OpWriter ow = {ops + o0 + (right ? 0 : nR), right ? cap : cap - nR, 0, 0};
           // (the sweep starts at L1max, wave-uniform: the lanes' start rows are below)
           gw_traceback(S32(right ? GS_PR : GS_PL, 0), right ? WR : WL, eb, (right ? !JLL : JLL) ? 0xF : 0, L1,
                        right ? L2R : L2L, right ? 1 : 0, cdir, right ? brR : brL, right ? bcR : bcL, L1max,
                        [&](int r) -> uint32_t { return lT[(size_t)(right ? L1 - r : r - 1) * 64] >> 24; },
-                       [&](int c) -> int { return (right ? lAR : lAL)[(size_t)(c + eb) * 64] >> 2; }, t, ow, ps, pen);
+                       [&](int c) -> int { return ((right ? lPR : lPL)[(size_t)(c + eb) * 64] & 31) >> 2; }, t, ow,
+                       ps, pen);
           const int nn = ow.n < ow.cap ? ow.n : ow.cap;
           over = over || ow.n > ow.cap;
           if (right) {
@@ -910,8 +905,8 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
           }
         }
         GW_T(10, tp);
-        const int dl = bcL < L2L - 1 ? left_code((int)lCL[(size_t)(bcL + eb) * 64] / 6) : 0;
-        const int dr = bcR < L2R - 1 ? right_code((int)lCR[(size_t)(bcR + eb) * 64] / 6) : 0;
+        const int dl = bcL < L2L - 1 ? left_code((((int)lPL[(size_t)(bcL + eb) * 64] >> 5) & 31) / 6) : 0;
+        const int dr = bcR < L2R - 1 ? right_code((((int)lPR[(size_t)(bcR + eb) * 64] >> 5) & 31) / 6) : 0;
         int it;
         const int sI = intron_score(it, dl, dr, cdir, canon, finalp);
         sL -= penL;
