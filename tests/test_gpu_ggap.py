@@ -229,3 +229,30 @@ def test_gpu_gband_probability_mode_matches_oracle(jl, monkeypatch):
     oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
     compare(w, res, trc, pairs, npairs, ores, oflat, onp, "band prob %s" % jl)
     assert np.mean(ores["returned_null"] == 0) > 0.5
+
+
+@pytest.mark.parametrize("jl", ["none", "mixed"])
+def test_gpu_gwin_probability_mode_matches_oracle(jl):
+    """Probability-mode windows on k_gwin (one window per lane, the default for
+    them): both of its band shapes (extraband_paired 7 and 3), jump-late mixed,
+    against the oracle; the k_gwin stage must have run."""
+    rng = np.random.default_rng(79)
+    g, b = W.c4_windows(W.synthetic_genome(8_000_000, seed=6), 20_000, seed=6, use_probabilities=True)
+    w = b.windows.copy()
+    w["extraband_paired"][1::3] = 3
+    if jl == "mixed":
+        w["jump_late_p"] = rng.integers(0, 2, len(w))
+    blocks = W.pack_genome(g)
+    ctx = Context(blocks)
+    names = ctx.profile(True)
+    res, trc, ops, off = ctx.ggap_run(w, b.query, b.query_uc)
+    acc = np.zeros(len(names))
+    ctx.profile_read(acc)
+    ctx.profile(False)
+    assert acc[names.index("k_gwin")] > 0, "k_gwin did not run"
+    pairs, npairs = ctx.ggap_all_pairs(w, b.query, b.query_uc, res, trc, ops, off)
+    O.setup(blocks)
+    ores, opairs, ooff, onp = O.run_ggap_batch(w, b.query, b.query_uc)
+    oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
+    compare(w, res, trc, pairs, npairs, ores, oflat, onp, "gwin prob %s" % jl)
+    assert np.mean(ores["returned_null"] == 0) > 0.5
