@@ -105,6 +105,7 @@ struct gsnapdp_ctx {
   double* d_gwin_probs = nullptr;   // k_gwin_probs' site probabilities, 64 per list window
   size_t gwin_probs_cap = 0;
   int gwin_on = 1;                  // probability-mode windows on k_gwin (GSNAPDP_GWIN=0: off)
+  int gwin_min = 16384;             // smallest genome-gap batch on k_gwin (GSNAPDP_GWIN_MIN)
   int ggap_rowlane_only = 0;        // GSNAPDP_GGAP_ROWLANE=1: every window on k_ggap (A/B tests)
   int ggap_use_band = 1;            // k_ggap_plan's GB_USE_* bits (GSNAPDP_GBAND_PROB=1 sets the prob bit)
   int gband_min = 16384;            // smallest genome-gap batch on the register band (GSNAPDP_GBAND_MIN)

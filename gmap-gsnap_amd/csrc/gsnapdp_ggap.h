@@ -242,9 +242,12 @@ __device__ inline Lane side_lane(const gsnapdp_ggap_window& w, const GGeo& G, in
 constexpr int GB_L2MAX = 256;            // longest flank on the register band
 constexpr int GB_LIST0 = 3;
 constexpr int GP_LIST0 = GB_LIST0 + 2 * (NCLASS - 1);
-// k_gwin (gsnapdp_gwin.hip): probability-mode windows with one window per lane
+// k_gwin (gsnapdp_gwin.hip): probability-mode windows with one window per
+// lane, lists GW_LIST + 2 * shape + jump_late_p (a wave's 64 windows share the
+// band shape and the tie rule)
 constexpr int GW_LIST = GP_LIST0 + 2 * (NCLASS - 1);
-constexpr int GG_NLISTS = GW_LIST + 1;
+constexpr int GW_NSUB = 4;
+constexpr int GG_NLISTS = GW_LIST + GW_NSUB;
 constexpr int GW_WMAX = 24;   // widest band of either flank
 // the band shapes k_gwin is built for: width 2 * extraband + 9 with extraband
 // 7 and 3 (GMAP's length2 = length1 + 8, stage3.c:5793); both flanks alike
@@ -294,6 +297,10 @@ __device__ inline bool gwin_ok(const gsnapdp_ggap_window& w, const GGeo& G) {
   if (!((G.WL == GW_W0 && G.lbL == GW_LB0) || (G.WL == GW_W1 && G.lbL == GW_LB1))) return false;
   const int span = w.revoffset2R - w.offset2L;
   return span - G.L1 - 1 >= (G.rbL > G.rbR ? G.rbL : G.rbR);
+}
+// the k_gwin list of a window gwin_ok takes: its band shape and tie rule
+__device__ inline int gwin_list(const gsnapdp_ggap_window& w, const GGeo& G) {
+  return GW_LIST + (G.WL == GW_W0 ? 0 : 2) + (w.jump_late_p ? 1 : 0);
 }
 
 }  // namespace gsnapdp

@@ -914,7 +914,7 @@ __global__ void k_ggap_plan(const gsnapdp_ggap_window* __restrict__ Wn, int n,
       X.status = ST_UNSUPPORTED;
     } else {
       done = false;
-      cls = (use_band & GW_USE) && gwin_ok(w, G) ? GW_LIST : gband_list(w, G, use_band);  // k_gwin / k_gband when they can
+      cls = (use_band & GW_USE) && gwin_ok(w, G) ? gwin_list(w, G) : gband_list(w, G, use_band);  // k_gwin / k_gband when they can
       const int bndw = G.L1 + 1 > 64 ? 3 * (max(G.L2L, G.L2R) + 2) : 0;  // stripe boundary row
       if (cls >= 0) {
       } else if (G.L1 + 1 <= 32 && G.words <= GG_SMALL_WORDS) cls = GG_SMALL;
@@ -1448,9 +1448,11 @@ extern "C" int gsnapdp_ggap_run_device(gsnapdp_ctx* ctx, const gsnapdp_ggap_wind
   const int cap = ctx->ggap_cap;
   HIPCHK(hipMemsetAsync(counts, 0, 4 * GG_NLISTS, st));
   gsnapdp__mark(ctx, st, 4, 0);
-  // k_gwin takes probability-mode windows whenever the MaxEnt tables are loaded
-  // (GSNAPDP_GWIN=0: k_ggap / k_gband as before, for A/B tests)
-  const int use_gwin = ctx->gwin_on && ctx->d_tables && !ctx->ggap_rowlane_only ? GW_USE : 0;
+  // k_gwin takes probability-mode windows of batches of at least gwin_min
+  // windows when the MaxEnt tables are loaded (GSNAPDP_GWIN=0: k_ggap / k_gband
+  // as before, for A/B tests)
+  const int use_gwin =
+      ctx->gwin_on && ctx->d_tables && !ctx->ggap_rowlane_only && n >= ctx->gwin_min ? GW_USE : 0;
   const int use_band = (n >= ctx->gband_min ? ctx->ggap_use_band : 0) | use_gwin;
   hipLaunchKernelGGL(k_ggap_plan, dim3((n + 255) / 256), dim3(256), 0, st, d_windows, n,
                      d_results, d_traces, lists, counts, cap, use_band);

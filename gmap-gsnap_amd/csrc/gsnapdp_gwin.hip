@@ -464,94 +464,218 @@ __device__ inline void flank_classes(const FlankBlk& f, const uint32_t* __restri
 }
 
 // The MaxEnt site probabilities of every list window's candidate columns
-// (:3856-3903; a window here has no known sites), ahead of k_gwin and at high
-// occupancy (their table loads are latency): thread (chunk, side, lane) takes
-// list entry chunk * 64 + lane, one flank, columns 0..GW_L2MAX-1 (0 from L2 - 1
-// on), and writes them [chunk][side][column][lane] as k_gwin reads them.
-__global__ __launch_bounds__(256) void k_gwin_probs(const gsnapdp_ggap_window* __restrict__ Wn,
-                                                    const int* __restrict__ list, const int* __restrict__ count,
-                                                    const uint32_t* __restrict__ blocks, uint64_t nwords,
-                                                    const double* __restrict__ tables, double* __restrict__ probs) {
-  const int n = *count;
-  const int nthreads = ((n + 63) >> 6) * 128;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nthreads; t += gridDim.x * blockDim.x) {
-    const int chunk = t >> 7, side = (t >> 6) & 1, ln = t & 63;
-    const int k = chunk * 64 + ln;
-    double* out = probs + (size_t)chunk * 4096 + side * 2048 + ln;
-    if (k >= n) {
-      for (int c = 0; c < GW_L2MAX; c++) out[c * 64] = 0.0;
-      continue;
-    }
-    const gsnapdp_ggap_window w = Wn[list[k]];
-    const int L2 = side ? w.length2R : w.length2L;
-    int m, step;
-    uint32_t sp0;
-    site_line(w, side, m, sp0, step);
-    const uint32_t margin = (m == 0) ? 3u : (m == 1) ? 20u : (m == 2) ? 6u : 3u;
-    const uint32_t spmin = step > 0 ? sp0 : sp0 - (uint32_t)(GW_L2MAX - 1);
-    if (step > 0 ? sp0 <= 0xFFFFFFFFu - (GW_L2MAX - 1) && sp0 >= margin : sp0 >= (GW_L2MAX - 1) + margin) {
-      // the columns' sites are consecutive genome positions (no uint32 wrap):
-      // the three blocks under all of them are loaded once, and each site's
-      // 16-mers are constant funnel shifts of that span (site c starts c, or
-      // 31 - c for a descending line, nt past the lowest start s0)
-      const uint32_t s0 = spmin - margin;
-      const uint64_t blk = (uint64_t)(s0 >> 5) * 3u;
-      uint32_t wv[6];
+// (:3856-3903; a window here has no known sites), ahead of k_gwin: item (chunk,
+// side, lane) takes list entry chunk * 64 + lane, one flank, columns
+// 0..GW_L2MAX-1 (0 from L2 - 1 on), and writes them [chunk][side][column][lane]
+// as k_gwin reads them.
+//
+// The tables' gathers are the work (about four per site, all over 1.5 MB), so
+// the tables come through LDS: a block of GP_THREADS items streams the twelve
+// 16384-entry tables through one 128 KB LDS buffer in their order in the
+// product (maxent_hr.c's acceptor odds a*b*c*d*e*f, donor a*b), and each item
+// multiplies its 32 sites' running odds by the current table's entries; the
+// 16-entry dinucleotide tables stay in global memory (cached).  A flank's
+// candidate sites are consecutive genome positions, so the three packed blocks
+// under all of them are loaded once and each site's 16-mers are constant
+// funnel shifts of that span (a line that would wrap 2^32 is computed site by
+// site from global tables before the table phases).
+// the k_gwin lists' 64-window chunks, numbered across the lists in order
+struct GwChunks {
+  int cnt[GW_NSUB], cum[GW_NSUB + 1];
+};
+__device__ inline GwChunks gw_chunks(const int* __restrict__ counts) {
+  GwChunks q;
+  q.cum[0] = 0;
 #pragma unroll
-      for (int j = 0; j < 3; j++) {
-        wv[2 * j] = blk + 3 * j + 1 < nwords ? blocks[blk + 3 * j + 1] : 0u;  // low
-        wv[2 * j + 1] = blk + 3 * j < nwords ? blocks[blk + 3 * j] : 0u;      // high
-      }
-      const uint32_t sh = (s0 & 31u) * 2u, b = sh & 31u;
-      const bool i0 = sh >= 32u;
-      uint32_t x[5];
+  for (int l = 0; l < GW_NSUB; l++) {
+    q.cnt[l] = counts[l];
+    q.cum[l + 1] = q.cum[l] + (q.cnt[l] + 63) / 64;
+  }
+  return q;
+}
+__device__ inline int gw_sub(const GwChunks& q, int chunk) {
+  return (chunk >= q.cum[1] ? 1 : 0) + (chunk >= q.cum[2] ? 1 : 0) + (chunk >= q.cum[3] ? 1 : 0);
+}
+// (selects, not a dynamically indexed private array)
+__device__ inline int gw_cnt(const GwChunks& q, int l) {
+  return l == 0 ? q.cnt[0] : l == 1 ? q.cnt[1] : l == 2 ? q.cnt[2] : q.cnt[3];
+}
+__device__ inline int gw_cum(const GwChunks& q, int l) {
+  return l == 0 ? q.cum[0] : l == 1 ? q.cum[1] : l == 2 ? q.cum[2] : q.cum[3];
+}
+static_assert(GW_NSUB == 4, "gw_sub");
+
+constexpr int GP_THREADS = 1024;
+constexpr int GP_TABLE = 16384;  // entries of a big table
+constexpr size_t GP_LDS = (size_t)GP_TABLE * sizeof(double);
+// the big tables' offsets in the table buffer (gsnapdp_load_maxent_tables'
+// order: donor_p, donor_di_p, acc1..3_p, accdi_p, acc467_p, acc589_p, then
+// the same for the minus models), the phase's model, and the di tables
+__device__ constexpr int gp_off(int t) {
+  return t == 0 ? 0 : t == 1 ? 16400 : t == 2 ? 32784 : t == 3 ? 49168 : t == 4 ? 65568 : t == 5 ? 81952
+       : t == 6 ? 98336 : t == 7 ? 114736 : t == 8 ? 131120 : t == 9 ? 147504 : t == 10 ? 163904 : 180288;
+}
+__device__ constexpr int gp_model(int t) { return t == 0 ? 0 : t <= 5 ? 1 : t == 6 ? 2 : 3; }
+
+template <int T>
+__device__ __forceinline__ void gp_phase(const uint32_t (&x_)[5], bool up, const AS_LDS double* tab,
+                                         const double* __restrict__ tables, double (&odds)[GW_L2MAX]) {
+  // (the span laundered per phase: the k-mers are recomputed here, not kept
+  // live from another phase's identical ones)
+  uint32_t x[5];
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        x[j] = __builtin_amdgcn_alignbit(i0 ? wv[j + 2] : wv[j + 1], i0 ? wv[j + 1] : wv[j], b);
-      x[4] = 0u;
-      const bool up = step > 0;
+  for (int j = 0; j < 5; j++) {
+    x[j] = x_[j];
+    asm volatile("" : "+v"(x[j]));
+  }
+  // the 16-mer `off` nt past site c's start
+  auto seq = [&](int c, int off) -> uint32_t {
+    const int bf = 2 * (c + off), br = 2 * (GW_L2MAX - 1 - c + off);
+    const uint32_t kf = __builtin_amdgcn_alignbit(x[(bf >> 5) + 1], x[bf >> 5], (uint32_t)(bf & 31));
+    const uint32_t kr = __builtin_amdgcn_alignbit(x[(br >> 5) + 1], x[br >> 5], (uint32_t)(br & 31));
+    return up ? kf : kr;
+  };
 #pragma unroll
-      for (int c0 = 0; c0 < GW_L2MAX; c0 += 8) {
-        bool v[8];
-        double o[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const uint32_t sp = sp0 + (uint32_t)(step * (c0 + j));
-          const uint64_t ptr = (uint64_t)((sp - margin) >> 5) * 3u;
-          v[j] = c0 + j < L2 - 1 && sp >= w.chroffset + margin && ptr + 4 < nwords;
-        }
-        auto seq = [&](int j, int off) -> uint32_t {
-          const int bf = 2 * (c0 + j + off), br = 2 * (GW_L2MAX - 1 - (c0 + j) + off);
-          const uint32_t kf = __builtin_amdgcn_alignbit(x[(bf >> 5) + 1], x[bf >> 5], (uint32_t)(bf & 31));
-          const uint32_t kr = __builtin_amdgcn_alignbit(x[(br >> 5) + 1], x[br >> 5], (uint32_t)(br & 31));
-          return up ? kf : kr;
-        };
-        maxent_probs_of<8>(m, seq, v, tables, o);
-#pragma unroll
-        for (int j = 0; j < 8; j++) out[(c0 + j) * 64] = o[j];
-      }
-      continue;
-    }
-#pragma unroll
-    for (int c0 = 0; c0 < GW_L2MAX; c0 += 8) {
-      uint32_t sp[8];
-      bool ok[8];
-      double o[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        sp[j] = sp0 + (uint32_t)(step * (c0 + j));
-        ok[j] = c0 + j < L2 - 1;
-      }
-      maxent_probs<8>(m, sp, ok, w.chroffset, blocks, nwords, tables, o);
-#pragma unroll
-      for (int j = 0; j < 8; j++) out[(c0 + j) * 64] = o[j];
+  for (int c = 0; c < GW_L2MAX; c++) {
+    if constexpr (T == 0) {  // donor: donor_p * donor_di_p
+      const uint32_t s = seq(c, 0);
+      odds[c] = tab[(s & 0x3Fu) | ((s >> 4) & 0x3FC0u)] * tables[16384 + ((s >> 6) & 0xFu)];
+    } else if constexpr (T == 6) {  // antidonor
+      const uint32_t s = seq(c, 0);
+      odds[c] = tab[(s & 0xFFu) | ((s >> 4) & 0x3F00u)] * tables[114720 + ((s >> 8) & 0xFu)];
+    } else if constexpr (T == 1) {
+      odds[c] = tab[seq(c, 0) & 0x3FFFu];
+    } else if constexpr (T == 2) {
+      odds[c] = __dmul_rn(odds[c], tab[seq(c, 7) & 0x3FFFu]);
+    } else if constexpr (T == 3) {  // acc3_p, then accdi_p
+      const uint32_t s = seq(c, 14);
+      odds[c] = __dmul_rn(__dmul_rn(odds[c], tab[(s & 0xFFu) | ((s >> 4) & 0x3F00u)]), tables[65552 + ((s >> 8) & 0xFu)]);
+    } else if constexpr (T == 4) {
+      odds[c] = __dmul_rn(odds[c], tab[seq(c, 4) & 0x3FFFu]);
+    } else if constexpr (T == 5) {
+      odds[c] = __dmul_rn(odds[c], tab[seq(c, 11) & 0x3FFFu]);
+    } else if constexpr (T == 7) {
+      odds[c] = tab[seq(c, 16) & 0x3FFFu];
+    } else if constexpr (T == 8) {
+      odds[c] = __dmul_rn(odds[c], tab[seq(c, 9) & 0x3FFFu]);
+    } else if constexpr (T == 9) {  // acc3_m, then accdi_m
+      const uint32_t s = seq(c, 0);
+      odds[c] = __dmul_rn(__dmul_rn(odds[c], tab[(s & 0x3Fu) | ((s >> 4) & 0x3FC0u)]), tables[163888 + ((s >> 6) & 0xFu)]);
+    } else if constexpr (T == 10) {
+      odds[c] = __dmul_rn(odds[c], tab[seq(c, 12) & 0x3FFFu]);
+    } else {
+      odds[c] = __dmul_rn(odds[c], tab[seq(c, 5) & 0x3FFFu]);
     }
   }
 }
 
+__global__ __launch_bounds__(GP_THREADS) void k_gwin_probs(const gsnapdp_ggap_window* __restrict__ Wn,
+                                                           const int* __restrict__ lists, int list_cap,
+                                                           const int* __restrict__ counts,
+                                                           const uint32_t* __restrict__ blocks, uint64_t nwords,
+                                                           const double* __restrict__ tables, double* __restrict__ probs) {
+  extern __shared__ double gp_tab[];
+  const AS_LDS double* tab = (const AS_LDS double*)gp_tab;
+  const GwChunks q = gw_chunks(counts);
+  const int nitems = q.cum[GW_NSUB] * 128;
+  for (int base = blockIdx.x * GP_THREADS; base < nitems; base += gridDim.x * GP_THREADS) {  // (block-uniform)
+    const int t = base + (int)threadIdx.x;
+    const int chunk = t >> 7, side = (t >> 6) & 1, ln = t & 63;
+    const int l = gw_sub(q, chunk);
+    const int k = (chunk - gw_cum(q, l)) * 64 + ln;
+    double* out = probs + (size_t)chunk * 4096 + side * 2048 + ln;
+    bool act = t < nitems && k < gw_cnt(q, l);
+    if (t < nitems && !act)
+      for (int c = 0; c < GW_L2MAX; c++) out[c * 64] = 0.0;
+    int m = 0;
+    bool up = true;
+    uint32_t vmask = 0, x[5] = {0u, 0u, 0u, 0u, 0u};
+    if (act) {
+      const gsnapdp_ggap_window w = Wn[lists[(size_t)(GW_LIST + l) * list_cap + k]];
+      const int L2 = side ? w.length2R : w.length2L;
+      int step;
+      uint32_t sp0;
+      site_line(w, side, m, sp0, step);
+      const uint32_t margin = (m == 0) ? 3u : (m == 1) ? 20u : (m == 2) ? 6u : 3u;
+      up = step > 0;
+      if (up ? sp0 <= 0xFFFFFFFFu - (GW_L2MAX - 1) && sp0 >= margin : sp0 >= (GW_L2MAX - 1) + margin) {
+        // no uint32 wrap: site c starts c (or 31 - c) nt past the lowest start s0
+        const uint32_t s0 = (up ? sp0 : sp0 - (uint32_t)(GW_L2MAX - 1)) - margin;
+        const uint64_t blk = (uint64_t)(s0 >> 5) * 3u;
+        uint32_t wv[6];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          wv[2 * j] = blk + 3 * j + 1 < nwords ? blocks[blk + 3 * j + 1] : 0u;  // low
+          wv[2 * j + 1] = blk + 3 * j < nwords ? blocks[blk + 3 * j] : 0u;      // high
+        }
+        const uint32_t sh = (s0 & 31u) * 2u, b = sh & 31u;
+        const bool i0 = sh >= 32u;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          x[j] = __builtin_amdgcn_alignbit(i0 ? wv[j + 2] : wv[j + 1], i0 ? wv[j + 1] : wv[j], b);
+#pragma unroll
+        for (int c = 0; c < GW_L2MAX; c++) {
+          const uint32_t sp = sp0 + (uint32_t)(step * c);
+          const uint64_t ptr = (uint64_t)((sp - margin) >> 5) * 3u;
+          const bool v = c < L2 - 1 && sp >= w.chroffset + margin && ptr + 4 < nwords;
+          vmask |= (v ? 1u : 0u) << c;
+        }
+      } else {
+        // (a line that wraps: site by site, from the global tables)
+#pragma clang loop unroll(disable)
+        for (int c = 0; c < GW_L2MAX; c++)
+          out[c * 64] = c < L2 - 1 ? maxent_prob(m, sp0 + (uint32_t)(step * c), w.chroffset, blocks, nwords, tables)
+                                   : 0.0;
+        act = false;
+      }
+    }
+    // the models some item of the block needs (a phase nobody needs is skipped)
+    const int mm = act ? 1 << m : 0;
+    const bool need0 = __syncthreads_or(mm & 1), need1 = __syncthreads_or(mm & 2);
+    const bool need2 = __syncthreads_or(mm & 4), need3 = __syncthreads_or(mm & 8);
+    double odds[GW_L2MAX];
+#pragma unroll
+    for (int c = 0; c < GW_L2MAX; c++) odds[c] = 0.0;
+    auto phase = [&](auto tc) {
+      constexpr int T = decltype(tc)::value;
+      constexpr int M = gp_model(T);
+      if (!(M == 0 ? need0 : M == 1 ? need1 : M == 2 ? need2 : need3)) return;
+      __syncthreads();  // the previous table's readers are done
+      // (from a laundered thread index: the addresses are invariant across
+      // rounds and would be hoisted and spilled)
+      int tid = (int)threadIdx.x;
+      asm volatile("" : "+v"(tid));
+      const double2* src = (const double2*)(tables + gp_off(T)) + tid;
+      double2* dst = (double2*)gp_tab + tid;
+#pragma unroll
+      for (int i = 0; i < GP_TABLE / 2 / GP_THREADS; i++) dst[i * GP_THREADS] = src[i * GP_THREADS];
+      __syncthreads();
+      if (act && m == M) gp_phase<T>(x, up, tab, tables, odds);
+    };
+    phase(std::integral_constant<int, 0>());
+    phase(std::integral_constant<int, 1>());
+    phase(std::integral_constant<int, 2>());
+    phase(std::integral_constant<int, 3>());
+    phase(std::integral_constant<int, 4>());
+    phase(std::integral_constant<int, 5>());
+    phase(std::integral_constant<int, 6>());
+    phase(std::integral_constant<int, 7>());
+    phase(std::integral_constant<int, 8>());
+    phase(std::integral_constant<int, 9>());
+    phase(std::integral_constant<int, 10>());
+    phase(std::integral_constant<int, 11>());
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < GW_L2MAX; c++)
+        out[c * 64] = (vmask >> c) & 1u ? __ddiv_rn(odds[c], __dadd_rn(1.0, odds[c])) : 0.0;
+    }
+    __syncthreads();  // (the next round's first table overwrites the buffer)
+  }
+}
+
 __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAVES_PER_SIMD, 8))) void k_gwin(
-    const gsnapdp_ggap_window* __restrict__ Wn, const int* __restrict__ list, const int* __restrict__ count,
-    const char* __restrict__ q, const char* __restrict__ qu, const uint32_t* __restrict__ blocks,
+    const gsnapdp_ggap_window* __restrict__ Wn, const int* __restrict__ lists, int list_cap,
+    const int* __restrict__ counts, const char* __restrict__ q, const char* __restrict__ qu, const uint32_t* __restrict__ blocks,
     uint64_t nwords, const uint32_t* __restrict__ prof, const double* __restrict__ tables,
     uint32_t* __restrict__ pool, const double* __restrict__ probs, gsnapdp_ggap_result* __restrict__ res,
     gsnapdp_ggap_trace* __restrict__ trc, uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
@@ -566,15 +690,18 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
   // the wave's scratch from a wave-uniform base (SGPRs) and the lane
   const Scr SC = {(AS_GLOBAL uint32_t*)pool + (size_t)__builtin_amdgcn_readfirstlane(gw) * GW_WAVE_DW, lane};
   auto S32 = [&](int region, int i) -> AS_GLOBAL uint32_t* { return &SC.u(region, i); };
-  const int n = *count;
+  const GwChunks qc = gw_chunks(counts);
 #ifdef GW_PROF
   uint64_t gw_acc[16] = {};
 #endif
-  for (int base = gw * 64; base < n; base += nw * 64) {
+  for (int chunk = gw; chunk < qc.cum[GW_NSUB]; chunk += nw) {  // (wave-uniform)
+    const int l = gw_sub(qc, chunk);
+    const int base = (chunk - gw_cum(qc, l)) * 64;
     const int k0 = base + lane;
     // the chunk's site probabilities (k_gwin_probs): [side][column][lane] doubles
-    AS_GLOBAL uint32_t* const PB_base = (AS_GLOBAL uint32_t*)(probs + (size_t)(base >> 6) * 4096);
-    const bool valid = k0 < n;
+    AS_GLOBAL uint32_t* const PB_base = (AS_GLOBAL uint32_t*)(probs + (size_t)chunk * 4096);
+    const bool valid = k0 < gw_cnt(qc, l);
+    const int* list = lists + (size_t)(GW_LIST + l) * list_cap;
     const int wi = list[valid ? k0 : base];
     int key, L1v;
     {  // (only the key and length1 stay live across the groups; each reads the record again)
@@ -643,7 +770,6 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
           SC1.u(GS_QB, i) = ((rk[i] | (uc[i] < 128u ? ub[i] : 0u)) >> 24) & 31u;  // row_match_mask
         }
       }
-#pragma unroll
       for (int side = 0; side < 2; side++) {
         const int L2 = side ? G.L2R : G.L2L;
         AS_LDS uint16_t* lP = side ? lPR : lPL;
@@ -978,8 +1104,8 @@ __global__ __launch_bounds__(GW_BLOCK) __attribute__((amdgpu_waves_per_eu(GW_WAV
 
 }  // namespace
 
-// Launch k_gwin over list GW_LIST of a genome-gap batch (k_ggap_plan fills it
-// only when the MaxEnt tables are loaded).
+// Launch k_gwin over lists GW_LIST .. + GW_NSUB - 1 of a genome-gap batch
+// (k_ggap_plan fills them only when the MaxEnt tables are loaded).
 int gsnapdp__gwin_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_ggap_window* d_windows,
                          const int* lists, const int* counts, int list_cap, const char* d_query,
                          const char* d_query_uc, gsnapdp_ggap_result* d_results, gsnapdp_ggap_trace* d_traces,
@@ -988,18 +1114,18 @@ int gsnapdp__gwin_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_ggap_wi
   const int waves = blocks * (GW_BLOCK / 64);
   if (!ctx->d_gwin_pool) HIPCHK(hipMalloc(&ctx->d_gwin_pool, (size_t)waves * GW_WAVE_DW * 4));
   // the site probabilities of up to list_cap windows (64 doubles each, by chunk)
-  const size_t pcap = ((size_t)list_cap + 63) / 64 * 4096;
+  const size_t pcap = (((size_t)list_cap + 63) / 64 + GW_NSUB) * 4096;
   if (pcap > ctx->gwin_probs_cap) {
     (void)hipFree(ctx->d_gwin_probs);
     ctx->d_gwin_probs = nullptr;
     HIPCHK(hipMalloc(&ctx->d_gwin_probs, pcap * sizeof(double)));
     ctx->gwin_probs_cap = pcap;
   }
-  const int* list = lists + (size_t)GW_LIST * list_cap;
-  hipLaunchKernelGGL(k_gwin_probs, dim3(ctx->num_cus * 8), dim3(256), 0, st, d_windows, list, counts + GW_LIST,
+  hipLaunchKernelGGL(k_gwin_probs, dim3(ctx->num_cus), dim3(GP_THREADS), GP_LDS, st, d_windows, lists, list_cap,
+                     counts + GW_LIST,
                      ctx->d_blocks, (uint64_t)ctx->nwords, ctx->d_tables, ctx->d_gwin_probs);
   hipLaunchKernelGGL(k_gwin, dim3(blocks), dim3(GW_BLOCK), (size_t)(GW_BLOCK / 64) * GW_LDS_WAVE, st, d_windows,
-                     list, counts + GW_LIST, d_query, d_query_uc, ctx->d_blocks, (uint64_t)ctx->nwords,
+                     lists, list_cap, counts + GW_LIST, d_query, d_query_uc, ctx->d_blocks, (uint64_t)ctx->nwords,
                      ctx->d_prof, ctx->d_tables, ctx->d_gwin_pool, ctx->d_gwin_probs, d_results, d_traces, d_ops,
                      d_op_offsets);
   HIPCHK(hipGetLastError());
@@ -1022,5 +1148,5 @@ int gsnapdp__gwin_launch(gsnapdp_ctx* ctx, hipStream_t st, const gsnapdp_ggap_wi
 
 int gsnapdp__gwin_lds_check(size_t max_lds) {
   return gsnapdp__lds_fits((const void*)&k_gwin, (size_t)(GW_BLOCK / 64) * GW_LDS_WAVE, max_lds, "k_gwin") ||
-         gsnapdp__lds_fits((const void*)&k_gwin_probs, 0, max_lds, "k_gwin_probs");
+         gsnapdp__lds_fits((const void*)&k_gwin_probs, GP_LDS, max_lds, "k_gwin_probs");
 }

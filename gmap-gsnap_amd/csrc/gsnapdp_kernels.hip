@@ -1412,6 +1412,11 @@ extern "C" gsnapdp_ctx* gsnapdp_create(int device, const uint32_t* blocks, size_
     // on k_ggap (DESIGN.md §4 k_gband)
     const char* m = getenv("GSNAPDP_GBAND_MIN");
     if (m) ctx->gband_min = atoi(m);
+    // k_gwin runs a wave-task (64 windows) in ~0.4 ms of latency-bound steps:
+    // only batches that fill its waves go there (the stage-3 pass's rounds stay
+    // on k_ggap; DESIGN.md §4 k_gwin)
+    const char* gm = getenv("GSNAPDP_GWIN_MIN");
+    if (gm) ctx->gwin_min = atoi(gm);
     // k_fill on fewer waves per SIMD when a batch gives each wave fewer than
     // this many tasks (0: always GSNAPDP_FILL_WAVES)
     const char* mt = getenv("GSNAPDP_FILL_MIN_TASKS");

@@ -256,3 +256,29 @@ def test_gpu_gwin_probability_mode_matches_oracle(jl):
     oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
     compare(w, res, trc, pairs, npairs, ores, oflat, onp, "gwin prob %s" % jl)
     assert np.mean(ores["returned_null"] == 0) > 0.5
+
+
+@pytest.mark.parametrize("name", ["ggap_chr17", "gmap_synth_ggap", "gmap_her2_ggap"])
+def test_gpu_gwin_matches_reference_golden(golden_dir, name, monkeypatch):
+    """The goldens with every qualifying probability-mode window on k_gwin
+    (GSNAPDP_GWIN_MIN=0; by default batches under 16384 windows run on k_ggap)."""
+    monkeypatch.setenv("GSNAPDP_GWIN_MIN", "0")
+    z = load(golden_dir, name)
+    ctx = Context(z["blocks"])
+    w = z["windows"]
+    res, trc, ops, off = ctx.ggap_run(w, z["query"], z["query_uc"])
+    pairs, npairs = ctx.ggap_all_pairs(w, z["query"], z["query_uc"], res, trc, ops, off)
+    compare(w, res, trc, pairs, npairs, z["results"], z["pairs"], z["npairs"], name + " (gwin)")
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_gpu_gwin_matches_oracle_mix(seed, monkeypatch):
+    """The mixed sets (every shape, both modes) with k_gwin taking what qualifies."""
+    monkeypatch.setenv("GSNAPDP_GWIN_MIN", "0")
+    g, b = W.ggap_windows(W.synthetic_genome(2_000_000, seed=seed, n_rate=0.002), 3000, seed=seed)
+    blocks = W.pack_genome(g)
+    res, trc, pairs, npairs = run_gpu(blocks, b)
+    O.setup(blocks)
+    ores, opairs, ooff, onp = O.run_ggap_batch(b.windows, b.query, b.query_uc)
+    oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
+    compare(b.windows, res, trc, pairs, npairs, ores, oflat, onp, "gwin mix seed %d" % seed)

@@ -15,6 +15,7 @@ from gsnapdp import Context, ggap_op_offsets  # noqa: E402
 from gsnapdp import workload as W  # noqa: E402
 from gsnapdp.records import GGAP_RESULT, GGAP_TRACE  # noqa: E402
 
+os.environ["GSNAPDP_GWIN_MIN"] = "0"  # every batch size on k_gwin (the mixed sets are 3000 windows)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 200_000
 out_path = sys.argv[2] if len(sys.argv) > 2 else None
 dev = torch.device("cuda", 0)
