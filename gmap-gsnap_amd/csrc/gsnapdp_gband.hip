@@ -1093,6 +1093,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GB_WAVES_PE
     uint32_t* __restrict__ ops, const int64_t* __restrict__ op_off) {
   __shared__ alignas(8) uint32_t sprof[SPROF_WORDS];
   __shared__ uint32_t rings[4][GB_RING_WORDS];
+  {  // no register-band window in the batch (a probability-mode batch on k_gwin): no table staging
+    int any = 0;
+#pragma unroll
+    for (int k = GB_LIST0; k < GB_LIST0 + 4 * (NCLASS - 1); k++) any |= counts[k];
+    if (any == 0) return;  // (block-uniform)
+  }
   for (int i = threadIdx.x; i < MLUT; i += blockDim.x)
     sprof[i] = i < UTAB ? fill_profile_word(prof[i]) : (i - UTAB < 128 ? prof[i] : 0u);
   for (int i = threadIdx.x; i < 32; i += blockDim.x) {
