@@ -282,3 +282,31 @@ def test_gpu_gwin_matches_oracle_mix(seed, monkeypatch):
     ores, opairs, ooff, onp = O.run_ggap_batch(b.windows, b.query, b.query_uc)
     oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))])
     compare(b.windows, res, trc, pairs, npairs, ores, oflat, onp, "gwin mix seed %d" % seed)
+
+
+@pytest.mark.parametrize("length1,eb", [(2, 7), (5, 3), (13, 7), (24, 7), (24, 3), (16, 3)])
+def test_gpu_gwin_shapes_match_oracle(length1, eb, monkeypatch):
+    """k_gwin at the edges of its window shapes: length1 2 .. 24 (flanks of
+    length1 + 8), both band shapes, jump-late mixed, a tenth of the windows at
+    the genome's start (site positions below the MaxEnt margins: the per-site
+    path of k_gwin_probs), against the oracle (GSNAPDP_GWIN_MIN=0)."""
+    monkeypatch.setenv("GSNAPDP_GWIN_MIN", "0")
+    rng = np.random.default_rng(length1 * 100 + eb)
+    g, b = W.c4_windows(W.synthetic_genome(4_000_000, seed=length1), 3000, seed=length1,
+                        use_probabilities=True, length1=length1, extraband=eb)
+    w = b.windows.copy()
+    w["jump_late_p"] = rng.integers(0, 2, len(w))
+    w["chrpos"][::10] = rng.integers(0, 12, len(w[::10]))
+    blocks = W.pack_genome(g)
+    ctx = Context(blocks)
+    names = ctx.profile(True)
+    res, trc, ops, off = ctx.ggap_run(w, b.query, b.query_uc)
+    acc = np.zeros(len(names))
+    ctx.profile_read(acc)
+    ctx.profile(False)
+    assert acc[names.index("k_gwin")] > 0, "k_gwin did not run"
+    pairs, npairs = ctx.ggap_all_pairs(w, b.query, b.query_uc, res, trc, ops, off)
+    O.setup(blocks)
+    ores, opairs, ooff, onp = O.run_ggap_batch(w, b.query, b.query_uc)
+    oflat = np.concatenate([opairs[ooff[i]:ooff[i] + onp[i]] for i in range(len(onp))] + [np.zeros(0, PAIR)])
+    compare(w, res, trc, pairs, npairs, ores, oflat, onp, "gwin L1 %d eb %d" % (length1, eb))
