@@ -1462,12 +1462,13 @@ extern "C" int gsnapdp_ggap_run_device(gsnapdp_ctx* ctx, const gsnapdp_ggap_wind
       gsnapdp__gband_launch(ctx, st, d_windows, lists, counts, cap, d_query, d_query_uc, d_results, d_traces,
                             d_ops, d_op_offsets, use_band))
     return -1;
+  gsnapdp__mark(ctx, st, 6, 1);
+  // (k_gwin timed as a stage of its own, not inside k_gband's)
   gsnapdp__mark(ctx, st, 8, 0);
   if (use_gwin && gsnapdp__gwin_launch(ctx, st, d_windows, lists, counts, cap, d_query, d_query_uc, d_results,
                                        d_traces, d_ops, d_op_offsets))
     return -1;
   gsnapdp__mark(ctx, st, 8, 1);
-  gsnapdp__mark(ctx, st, 6, 1);
   gsnapdp__mark(ctx, st, 5, 0);
   // small windows: 4 waves x 2 windows per block, as many blocks per CU as LDS holds
   hipLaunchKernelGGL((k_ggap<32, false>), dim3(ctx->num_cus * GG_SMALL_BLOCKS), dim3(256),
